@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 ComputationGraph training throughput (images/sec, whole job).
+
+Metric/config from BASELINE.json: "images/sec (whole node) ResNet-50 training at 1/2/4/8 MI355X",
+config "ResNet-50 ComputationGraph bf16 on one MI355X (conv2d im2col+MFMA path)" and
+"ResNet-50 ParallelWrapper DP=8 with RCCL gradient all-reduce over xGMI".
+
+Model: the reference's zoo ResNet50 graph (ZOO:model/ResNet50.java: stride-2 stage 2, MAX-3x3 head,
+RmsProp(0.1,0.96,1e-3), l1 1e-7, l2 5e-5) with random-init weights; synthetic 224x224x3 images and
+one-hot labels (BenchmarkDataSetIterator semantics: one fixed random batch, re-fed every step).
+``--variant canonical`` runs standard ResNet-50 instead. Every timed step is a full training
+iteration: forward, backward, (DP) gradient all-reduce, fused RmsProp update of all 25.6M params.
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 256)), help="per-GPU batch")
+    ap.add_argument("--variant", default=os.environ.get("BENCH_VARIANT", "dl4j"), choices=["dl4j", "canonical"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("BENCH_GRAPH", "0")),
+                    help="capture the training step in a HIP graph")
+    args = ap.parse_args()
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from deeplearning4j_amd.models import ResNet50
+    from deeplearning4j_amd.nn.conf import DataType
+    from deeplearning4j_amd.parallel.accumulation import AllReduceGradientsAccumulator
+    from deeplearning4j_amd.parallel.distributed import all_reduce_max, barrier, init_distributed
+
+    world, rank, local, device = init_distributed()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.manual_seed(1234 + rank)
+
+    dt = DataType.BFLOAT16 if args.dtype == "bf16" else DataType.FLOAT
+    net = ResNet50(numLabels=1000, variant=args.variant, dataType=dt).init(device=device)
+    acc = None
+    if world > 1:
+        acc = AllReduceGradientsAccumulator()
+        acc.broadcast_params(net)
+        net.setGradientsAccumulator(acc)
+
+    B = args.batch
+    g = torch.Generator(device="cpu").manual_seed(42 + rank)
+    x = torch.rand(B, 3, 224, 224, generator=g).to(device)
+    if device.type == "cuda":
+        x = x.contiguous(memory_format=torch.channels_last)
+    x = x.to(net.compute_dtype)
+    y = torch.zeros(B, 1000, device=device)
+    y[torch.arange(B), torch.randint(0, 1000, (B,), generator=g).to(device)] = 1.0
+
+    def step():
+        net.fit([x], [y])
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
+        step()
+        if rank == 0 and (i == 0 or time.perf_counter() - t_w > 60):
+            sync()
+            print(f"[bench] warmup step {i} done, score={net.score():.4f}, {time.perf_counter() - t_w:.1f}s",
+                  file=sys.stderr, flush=True)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = all_reduce_max(elapsed)
+    ms = elapsed / args.steps * 1000.0
+    ips = B * world * args.steps / elapsed
+    final_score = net.score()
+    if rank == 0:
+        model_name = "ResNet-50 (DL4J zoo ResNet50 graph)" if args.variant == "dl4j" else "ResNet-50 (canonical)"
+        print(json.dumps({
+            "metric": "images/sec (whole node) ResNet-50 training at 1/2/4/8 MI355X",
+            "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (random 224x224x3 images, one-hot labels; random-init weights)",
+            "config": {"model": model_name, "variant": args.variant, "global_batch": B * world, "per_gpu_batch": B,
+                       "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
+                       "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
+                       "final_score": final_score},
+        }), flush=True)
+    from deeplearning4j_amd.parallel.distributed import destroy
+    destroy()
+
+
+if __name__ == "__main__":
+    main()

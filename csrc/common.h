@@ -1,0 +1,85 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of deeplearning4j_amd.
+// Wave size is 64 on CDNA; everything here is written for that.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DL4J_API extern "C" __attribute__((visibility("default")))
+
+typedef __hip_bfloat16 bf16;
+typedef unsigned short u16;
+
+// 8 x bf16 = 16 bytes: the coalescing sweet spot (one dwordx4 per lane).
+struct __attribute__((aligned(16))) bf16x8 { u16 v[8]; };
+struct __attribute__((aligned(16))) f32x4 { float v[4]; };
+
+__device__ __forceinline__ float bf2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) {
+  bf16 b = __float2bfloat16(f);           // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return *reinterpret_cast<u16*>(&b);
+}
+
+// Load / store 8 consecutive elements as float, for bf16 or fp32 storage.
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float* o) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = bf2f(v.v[i]);
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* o) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v.v[i] = f2bf(o[i]);
+    *reinterpret_cast<bf16x8*>(p) = v;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* o) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a.v[i]; o[i + 4] = b.v[i]; }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* o) {
+    f32x4 a, b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a.v[i] = o[i]; b.v[i] = o[i + 4]; }
+    *reinterpret_cast<f32x4*>(p) = a;
+    *reinterpret_cast<f32x4*>(p + 4) = b;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld1<bf16>(const bf16* p) { return bf2f(*reinterpret_cast<const u16*>(p)); }
+template <typename T> __device__ __forceinline__ void st1(T* p, float v);
+template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st1<bf16>(bf16* p, float v) { *reinterpret_cast<u16*>(p) = f2bf(v); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide reduction for blockDim.x <= 1024 (multiple of 64). `red` needs blockDim/64 floats.
+template <bool MAX>
+__device__ __forceinline__ float block_reduce(float v, float* red) {
+  v = MAX ? wave_max(v) : wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = MAX ? -INFINITY : 0.f;
+  for (int i = 0; i < nw; ++i) r = MAX ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+#define HIP_LAUNCH_CHECK() (hipGetLastError())

@@ -1,0 +1,108 @@
+// Fused multi-tensor updater: ONE launch updates every parameter segment of a network's flat vector.
+//
+// Per element (reference order: BaseMultiLayerUpdater.java:223-309, UpdaterBlock.java:142-193):
+//   u = updater(g, state)            Sgd/Nesterovs/Adam/AdaMax/Nadam/AdaGrad/AdaDelta/RmsProp/NoOp
+//   u += l2*p + l1*sign(p)            (post-apply regularisation)
+//   u *= 1/minibatch                  (BaseMultiLayerUpdater divi(batchSize))
+//   p -= u                            (NegativeGradientStepFunction)
+//   shadow = bf16(p)                  (reduced-precision compute copy, optional)
+//   g = u                             (DL4J leaves the update in the gradient view, optional)
+// Memory-bound: each param is touched once (~22-26 B/param). grid.y = segment, grid.x strides the segment.
+#include "common.h"
+
+struct SegDesc {
+  long long p_off, n, st_off, in_block, block_n;
+  int op, pad;
+  float h0, h1, h2, h3, l1, l2;
+};
+
+enum { OP_NOOP = 0, OP_SGD = 1, OP_NESTEROVS = 2, OP_ADAM = 3, OP_ADAMAX = 4, OP_NADAM = 5, OP_ADAGRAD = 6,
+       OP_ADADELTA = 7, OP_RMSPROP = 8 };
+
+template <typename TS>
+__global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __restrict__ segs, float* __restrict__ p,
+                                                           float* __restrict__ g, float* __restrict__ st,
+                                                           TS* __restrict__ shadow, float inv_div, int write_update) {
+  const SegDesc s = segs[blockIdx.y];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  float* s1 = st + s.st_off + s.in_block;
+  float* s2 = st + s.st_off + s.block_n + s.in_block;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < s.n; i += stride) {
+    const long long pi = s.p_off + i;
+    const float gi = g[pi];
+    float pv = p[pi];
+    float u;
+    switch (s.op) {
+      case OP_SGD: u = s.h0 * gi; break;
+      case OP_NESTEROVS: {  // v = mu*v - lr*g ; u = mu*v_prev - (1+mu)*v
+        const float vp = s1[i];
+        const float v = s.h1 * vp - s.h0 * gi;
+        s1[i] = v;
+        u = s.h1 * vp - (1.f + s.h1) * v;
+      } break;
+      case OP_ADAM: {       // h0 = alpha_t, h1 = b1, h2 = b2, h3 = eps
+        const float m = s.h1 * s1[i] + (1.f - s.h1) * gi;
+        const float v = s.h2 * s2[i] + (1.f - s.h2) * gi * gi;
+        s1[i] = m; s2[i] = v;
+        u = s.h0 * m / (sqrtf(v) + s.h3);
+      } break;
+      case OP_ADAMAX: {     // h0 = lr/(1-b1^t)
+        const float m = s.h1 * s1[i] + (1.f - s.h1) * gi;
+        const float uu = fmaxf(s.h2 * s2[i], fabsf(gi));
+        s1[i] = m; s2[i] = uu;
+        u = s.h0 * m / (uu + s.h3);
+      } break;
+      case OP_NADAM: {      // h0 = lr/(1-b1^t)
+        const float omg = (1.f - s.h1) * gi;
+        const float m = s.h1 * s1[i] + omg;
+        const float v = s.h2 * s2[i] + (1.f - s.h2) * gi * gi;
+        s1[i] = m; s2[i] = v;
+        u = (m * s.h1 + omg) * s.h0 / (sqrtf(v) + s.h3);
+      } break;
+      case OP_ADAGRAD: {    // h0 = lr, h1 = eps
+        const float h = s1[i] + gi * gi;
+        s1[i] = h;
+        u = s.h0 * gi / sqrtf(h + s.h1);
+      } break;
+      case OP_ADADELTA: {   // h0 = rho, h1 = eps
+        const float msg = s.h0 * s1[i] + (1.f - s.h0) * gi * gi;
+        const float dx = sqrtf(s2[i] + s.h1) / sqrtf(msg + s.h1) * gi;
+        s1[i] = msg;
+        s2[i] = s.h0 * s2[i] + (1.f - s.h0) * dx * dx;
+        u = dx;
+      } break;
+      case OP_RMSPROP: {    // h0 = lr, h1 = decay, h2 = eps
+        const float c = s.h1 * s1[i] + (1.f - s.h1) * gi * gi;
+        s1[i] = c;
+        u = s.h0 * gi / sqrtf(c + s.h2);
+      } break;
+      default: u = gi;    // OP_NOOP: ND4J NoOpUpdater leaves the gradient unchanged
+    }
+    if (s.l2 > 0.f) u += s.l2 * pv;
+    if (s.l1 > 0.f) u += s.l1 * ((pv > 0.f) - (pv < 0.f));
+    u *= inv_div;
+    pv -= u;
+    p[pi] = pv;
+    if (shadow) st1<TS>(shadow + pi, pv);
+    if (write_update) g[pi] = u;
+  }
+}
+
+// segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (treated as bf16 layout not supported -> none)
+DL4J_API int dl4j_fused_update(const void* segs, int nseg, long long max_n, float* p, float* g, float* st,
+                               void* shadow, int shadow_kind, float inv_div, int write_update, hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  long long bx = (max_n + 256 * 4 - 1) / (256 * 4);
+  if (bx < 1) bx = 1;
+  if (bx > 512) bx = 512;
+  dim3 grid((unsigned)bx, (unsigned)nseg);
+  if (shadow_kind == 1)
+    hipLaunchKernelGGL(fused_update_kernel<bf16>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
+                       (bf16*)shadow, inv_div, write_update);
+  else
+    hipLaunchKernelGGL(fused_update_kernel<float>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
+                       (float*)nullptr, inv_div, write_update);
+  return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_segdesc_size() { return (int)sizeof(SegDesc); }

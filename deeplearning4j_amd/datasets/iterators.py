@@ -1,0 +1,307 @@
+"""Utility iterators (reference deeplearning4j-data/deeplearning4j-utility-iterators):
+BenchmarkDataSetIterator (synthetic, BenchmarkDataSetIterator.java:26-47), AsyncDataSetIterator
+(background prefetch, ITER:AsyncDataSetIterator.java:29-108,383-397), MultipleEpochsIterator,
+EarlyTerminationDataSetIterator, SamplingDataSetIterator, KFoldIterator, ... .
+
+AsyncDataSetIterator on a GPU stages each batch into pinned host memory and copies it to the device
+on a dedicated HIP copy stream from the prefetch thread, recording an event the consumer waits on,
+so H2D overlaps the previous step's compute.
+"""
+import queue
+import threading
+
+import torch
+
+from .dataset import DataSet, DataSetIterator, MultiDataSet
+
+
+class BenchmarkDataSetIterator(DataSetIterator):
+    """Returns the same random [mb, ...] features and one-hot labels ``totalIterations`` times."""
+
+    def __init__(self, featuresShape, numLabels, totalIterations, gridWidth=-1, gridHeight=-1, device=None,
+                 dtype=torch.float32, seed=12345):
+        g = torch.Generator().manual_seed(seed)
+        mb = featuresShape[0]
+        f = torch.rand(*featuresShape, generator=g, dtype=torch.float32)
+        if gridWidth > 0 and gridHeight > 0:
+            lab = torch.zeros(mb, numLabels, gridHeight, gridWidth)
+            cls = torch.randint(0, numLabels, (mb, gridHeight, gridWidth), generator=g)
+            lab.scatter_(1, cls.unsqueeze(1), 1.0)
+        else:
+            lab = torch.zeros(mb, numLabels)
+            lab[torch.arange(mb), torch.randint(0, numLabels, (mb,), generator=g)] = 1.0
+        if device is not None:
+            f, lab = f.to(device), lab.to(device)
+            if f.dim() == 4 and f.is_cuda:
+                f = f.contiguous(memory_format=torch.channels_last)
+        self.ds = DataSet(f.to(dtype), lab)
+        self.total = totalIterations
+        self.i = 0
+
+    def hasNext(self):
+        return self.total < 0 or self.i < self.total
+
+    def next(self, num=None):
+        self.i += 1
+        return self.ds
+
+    def reset(self):
+        self.i = 0
+
+    def batch(self):
+        return self.ds.features.shape[0]
+
+    def inputColumns(self):
+        return self.ds.features[0].numel()
+
+    def totalOutcomes(self):
+        return self.ds.labels.shape[1]
+
+
+class BenchmarkMultiDataSetIterator(BenchmarkDataSetIterator):
+    def next(self, num=None):
+        self.i += 1
+        return MultiDataSet.fromDataSet(self.ds)
+
+
+_END = object()
+
+
+class AsyncDataSetIterator(DataSetIterator):
+    def __init__(self, base, queueSize=2, device=None, useWorkspace=True):
+        self.base = base
+        self.qsize = max(1, queueSize)
+        self.device = device
+        self._thread = None
+        self._q = None
+        self._next = None
+        self._err = None
+        self._stop = threading.Event()
+
+    def _worker(self):
+        stream = torch.cuda.Stream(device=self.device) if (self.device is not None and
+                                                           torch.device(self.device).type == "cuda") else None
+        try:
+            while not self._stop.is_set() and self.base.hasNext():
+                ds = self.base.next()
+                ev = None
+                if stream is not None:
+                    with torch.cuda.stream(stream):
+                        ds = _to_device(ds, self.device, pin=True)
+                        ev = torch.cuda.Event()
+                        ev.record(stream)
+                while not self._stop.is_set():
+                    try:
+                        self._q.put((ds, ev), timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+        except BaseException as e:  # propagate to consumer
+            self._err = e
+        finally:
+            while True:
+                try:
+                    self._q.put((_END, None), timeout=0.1)
+                    break
+                except queue.Full:
+                    if self._stop.is_set():
+                        break
+
+    def _start(self):
+        self._stop.clear()
+        self._q = queue.Queue(self.qsize)
+        self._next = None
+        self._thread = threading.Thread(target=self._worker, name="ADSI prefetch thread", daemon=True)
+        self._thread.start()
+
+    def _peek(self):
+        if self._thread is None:
+            self._start()
+        if self._next is None:
+            self._next = self._q.get()
+            if self._err is not None:
+                raise self._err
+        return self._next
+
+    def hasNext(self):
+        return self._peek()[0] is not _END
+
+    def next(self, num=None):
+        ds, ev = self._peek()
+        if ds is _END:
+            raise StopIteration
+        self._next = None
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        return ds
+
+    def shutdown(self):
+        if self._thread is not None:
+            self._stop.set()
+            try:
+                while True:
+                    self._q.get_nowait()
+            except queue.Empty:
+                pass
+            self._thread.join(timeout=5)
+            self._thread = None
+
+    def reset(self):
+        self.shutdown()
+        self.base.reset()
+
+    def batch(self):
+        return self.base.batch()
+
+    def inputColumns(self):
+        return self.base.inputColumns()
+
+    def totalOutcomes(self):
+        return self.base.totalOutcomes()
+
+    def __del__(self):
+        try:
+            self.shutdown()
+        except Exception:
+            pass
+
+
+AsyncMultiDataSetIterator = AsyncDataSetIterator
+
+
+def _to_device(ds, device, pin=False):
+    def mv(t):
+        if t is None:
+            return None
+        if pin and not t.is_cuda and not t.is_pinned():
+            t = t.pin_memory()
+        return t.to(device, non_blocking=True)
+    if isinstance(ds, MultiDataSet):
+        m = lambda xs: None if xs is None else [mv(x) for x in xs]  # noqa: E731
+        return MultiDataSet(m(ds.features), m(ds.labels), m(ds.featuresMasks), m(ds.labelsMasks))
+    return DataSet(mv(ds.features), mv(ds.labels), mv(ds.featuresMask), mv(ds.labelsMask))
+
+
+class MultipleEpochsIterator(DataSetIterator):
+    def __init__(self, numEpochs, base):
+        self.n = numEpochs
+        self.base = base
+        self.epoch = 0
+
+    def hasNext(self):
+        if self.base.hasNext():
+            return True
+        if self.epoch + 1 < self.n:
+            self.epoch += 1
+            self.base.reset()
+            return self.base.hasNext()
+        return False
+
+    def next(self, num=None):
+        return self.base.next()
+
+    def reset(self):
+        self.epoch = 0
+        self.base.reset()
+
+    def batch(self):
+        return self.base.batch()
+
+
+class EarlyTerminationDataSetIterator(DataSetIterator):
+    def __init__(self, base, terminationPoint):
+        self.base = base
+        self.limit = terminationPoint
+        self.i = 0
+
+    def hasNext(self):
+        return self.i < self.limit and self.base.hasNext()
+
+    def next(self, num=None):
+        self.i += 1
+        return self.base.next()
+
+    def reset(self):
+        self.i = 0
+        self.base.reset()
+
+    def batch(self):
+        return self.base.batch()
+
+
+class SamplingDataSetIterator(DataSetIterator):
+    def __init__(self, sampleFrom, batchSize, totalNumberSamples, seed=None):
+        self.ds = sampleFrom
+        self.bs = batchSize
+        self.total = totalNumberSamples
+        self.n = 0
+        self.g = torch.Generator().manual_seed(seed if seed is not None else 12345)
+
+    def hasNext(self):
+        return self.n < self.total
+
+    def next(self, num=None):
+        idx = torch.randint(0, self.ds.numExamples(), (self.bs,), generator=self.g)
+        self.n += self.bs
+        return self.ds._sub(idx)
+
+    def reset(self):
+        self.n = 0
+
+    def batch(self):
+        return self.bs
+
+
+class KFoldIterator(DataSetIterator):
+    def __init__(self, k, ds):
+        self.k = k
+        self.ds = ds
+        self.i = 0
+        n = ds.numExamples()
+        self.bounds = [(j * n // k, (j + 1) * n // k) for j in range(k)]
+
+    def hasNext(self):
+        return self.i < self.k
+
+    def next(self, num=None):
+        a, b = self.bounds[self.i]
+        n = self.ds.numExamples()
+        idx = torch.cat([torch.arange(0, a), torch.arange(b, n)])
+        self._test = self.ds._sub(torch.arange(a, b))
+        self.i += 1
+        return self.ds._sub(idx)
+
+    def testFold(self):
+        return self._test
+
+    def reset(self):
+        self.i = 0
+
+
+class DoublesDataSetIterator(DataSetIterator):
+    """Iterates (features, labels) pairs of python lists/arrays in minibatches."""
+
+    def __init__(self, pairs, batchSize):
+        self.pairs = list(pairs)
+        self.bs = batchSize
+        self.i = 0
+
+    def hasNext(self):
+        return self.i < len(self.pairs)
+
+    def next(self, num=None):
+        chunk = self.pairs[self.i:self.i + self.bs]
+        self.i += self.bs
+        f = torch.tensor([list(p[0]) for p in chunk], dtype=torch.float32)
+        l = torch.tensor([list(p[1]) for p in chunk], dtype=torch.float32)
+        return DataSet(f, l)
+
+    def reset(self):
+        self.i = 0
+
+    def batch(self):
+        return self.bs
+
+
+class INDArrayDataSetIterator(DoublesDataSetIterator):
+    pass

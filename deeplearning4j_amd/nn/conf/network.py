@@ -1,0 +1,523 @@
+"""Network-level configuration: NeuralNetConfiguration.Builder -> MultiLayerConfiguration /
+ComputationGraphConfiguration (reference nn/conf/NeuralNetConfiguration.java:584-1262,
+MultiLayerConfiguration.java:57-83,349-470, ComputationGraphConfiguration.java:59 (GraphBuilder)).
+
+Global builder properties are inherited by every layer whose own value is unset. The JSON form
+(``toJson``/``fromJson``) carries everything needed to rebuild the net, including iteration/epoch
+counts so learning-rate schedules resume (MultiLayerConfiguration.java:80-83).
+"""
+import copy
+import json
+
+from .base import Config, _decode
+from .enums import BackpropType, CacheMode, ConvolutionMode, DataType, OptimizationAlgorithm, WorkspaceMode
+from .graph import GraphVertex, LayerVertex
+from .inputs import InputType
+from .layers import Layer
+from .regularization import to_dropout
+from .updaters import to_updater
+from .weights import to_weight_init
+
+
+_GLOBAL_DEFAULTS = {
+    "seed": 12345, "optimizationAlgo": OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT, "miniBatch": True,
+    "maxNumLineSearchIterations": 5, "minimize": True, "stepFunction": None,
+    "trainingWorkspaceMode": WorkspaceMode.ENABLED, "inferenceWorkspaceMode": WorkspaceMode.ENABLED,
+    "cacheMode": CacheMode.NONE, "dataType": DataType.FLOAT,
+    # inheritable layer properties
+    "activation": None, "weightInit": None, "biasInit": None, "dist": None, "l1": None, "l2": None,
+    "l1Bias": None, "l2Bias": None, "updater": None, "biasUpdater": None, "weightNoise": None,
+    "gradientNormalization": None, "gradientNormalizationThreshold": None, "idropout": None,
+    "convolutionMode": None, "cudnnAlgoMode": None, "constraints": None,
+}
+
+
+class NeuralNetConfiguration:
+    """Namespace holding the global ``Builder`` (reference class of the same name)."""
+
+    class Builder:
+        def __init__(self):
+            self._g = dict(_GLOBAL_DEFAULTS)
+
+        def _set(self, k, v):
+            self._g[k] = v
+            return self
+
+        # hyperparameters ------------------------------------------------------------------
+        def seed(self, s):
+            return self._set("seed", int(s))
+
+        def activation(self, a):
+            from .activations import to_activation
+            return self._set("activation", to_activation(a))
+
+        def weightInit(self, w):
+            from .weights import Distribution
+            if isinstance(w, Distribution):
+                self._set("dist", w)
+                from .weights import WeightInit
+                return self._set("weightInit", WeightInit.DISTRIBUTION)
+            return self._set("weightInit", to_weight_init(w))
+
+        def dist(self, d):
+            return self._set("dist", d)
+
+        def biasInit(self, b):
+            return self._set("biasInit", float(b))
+
+        def l1(self, v):
+            return self._set("l1", float(v))
+
+        def l2(self, v):
+            return self._set("l2", float(v))
+
+        def l1Bias(self, v):
+            return self._set("l1Bias", float(v))
+
+        def l2Bias(self, v):
+            return self._set("l2Bias", float(v))
+
+        def updater(self, u):
+            return self._set("updater", to_updater(u))
+
+        def biasUpdater(self, u):
+            return self._set("biasUpdater", to_updater(u))
+
+        def dropOut(self, d):
+            return self._set("idropout", to_dropout(d))
+
+        def weightNoise(self, w):
+            return self._set("weightNoise", w)
+
+        def gradientNormalization(self, g):
+            from .enums import GradientNormalization
+            return self._set("gradientNormalization", GradientNormalization.of(g))
+
+        def gradientNormalizationThreshold(self, t):
+            return self._set("gradientNormalizationThreshold", float(t))
+
+        def convolutionMode(self, m):
+            return self._set("convolutionMode", ConvolutionMode.of(m))
+
+        def cudnnAlgoMode(self, m):
+            from .enums import AlgoMode
+            return self._set("cudnnAlgoMode", AlgoMode.of(m))
+
+        def constrainWeights(self, *cs):
+            out = []
+            for c in cs:
+                c = c.clone()
+                c.params = ["W"]
+                out.append(c)
+            return self._set("constraints", (self._g.get("constraints") or []) + out)
+
+        def constrainBias(self, *cs):
+            out = []
+            for c in cs:
+                c = c.clone()
+                c.params = ["b"]
+                out.append(c)
+            return self._set("constraints", (self._g.get("constraints") or []) + out)
+
+        def constrainAllParameters(self, *cs):
+            out = []
+            for c in cs:
+                c = c.clone()
+                c.params = ["*"]
+                out.append(c)
+            return self._set("constraints", (self._g.get("constraints") or []) + out)
+
+        def optimizationAlgo(self, a):
+            return self._set("optimizationAlgo", OptimizationAlgorithm.of(a))
+
+        def miniBatch(self, b):
+            return self._set("miniBatch", bool(b))
+
+        def maxNumLineSearchIterations(self, n):
+            return self._set("maxNumLineSearchIterations", int(n))
+
+        def minimize(self, b):
+            return self._set("minimize", bool(b))
+
+        def stepFunction(self, s):
+            return self._set("stepFunction", s)
+
+        def trainingWorkspaceMode(self, m):
+            return self._set("trainingWorkspaceMode", WorkspaceMode.of(m))
+
+        def inferenceWorkspaceMode(self, m):
+            return self._set("inferenceWorkspaceMode", WorkspaceMode.of(m))
+
+        def cacheMode(self, m):
+            return self._set("cacheMode", CacheMode.of(m))
+
+        def dataType(self, d):
+            """Compute dtype policy (extension: FLOAT / BFLOAT16 / HALF / DOUBLE)."""
+            return self._set("dataType", DataType.of(d))
+
+        # deprecated reference knobs accepted for source compatibility
+        def learningRate(self, lr):
+            u = self._g.get("updater")
+            if u is not None and hasattr(u, "learningRate"):
+                u.learningRate = lr
+            else:
+                from .updaters import Sgd
+                self._g["updater"] = Sgd(lr)
+            return self
+
+        def iterations(self, n):
+            return self
+
+        def regularization(self, b):
+            return self
+
+        def list(self, *layers):
+            lb = ListBuilder(self._g)
+            for i, l in enumerate(layers):
+                lb.layer(i, l)
+            return lb
+
+        def graphBuilder(self):
+            return GraphBuilder(self._g)
+
+        def build(self):
+            return dict(self._g)
+
+
+class ListBuilder:
+    def __init__(self, g):
+        self._g = g
+        self._layers = {}
+        self._pp = {}
+        self._inputType = None
+        self._backprop = True
+        self._pretrain = False
+        self._bpType = BackpropType.Standard
+        self._fwd = 20
+        self._back = 20
+
+    def layer(self, idx, layer=None):
+        if layer is None:
+            layer, idx = idx, len(self._layers)
+        if hasattr(layer, "build") and not isinstance(layer, Layer):
+            layer = layer.build()
+        self._layers[int(idx)] = layer
+        return self
+
+    def inputPreProcessor(self, idx, pp):
+        self._pp[int(idx)] = pp
+        return self
+
+    def setInputType(self, t):
+        self._inputType = t
+        return self
+
+    def backprop(self, b):
+        self._backprop = bool(b)
+        return self
+
+    def pretrain(self, b):
+        self._pretrain = bool(b)
+        return self
+
+    def backpropType(self, t):
+        self._bpType = BackpropType.of(t)
+        return self
+
+    def tBPTTLength(self, n):
+        self._fwd = self._back = int(n)
+        return self
+
+    def tBPTTForwardLength(self, n):
+        self._fwd = int(n)
+        return self
+
+    def tBPTTBackwardLength(self, n):
+        self._back = int(n)
+        return self
+
+    def trainingWorkspaceMode(self, m):
+        self._g["trainingWorkspaceMode"] = WorkspaceMode.of(m)
+        return self
+
+    def inferenceWorkspaceMode(self, m):
+        self._g["inferenceWorkspaceMode"] = WorkspaceMode.of(m)
+        return self
+
+    def cacheMode(self, m):
+        self._g["cacheMode"] = CacheMode.of(m)
+        return self
+
+    def build(self):
+        n = len(self._layers)
+        if sorted(self._layers) != list(range(n)):
+            raise ValueError(f"Layer indices must be contiguous from 0: got {sorted(self._layers)}")
+        confs = [copy.deepcopy(self._layers[i]) for i in range(n)]
+        g = self._g
+        for c in confs:
+            c.applyGlobal(g)
+        pps = dict(self._pp)
+        if self._inputType is not None:
+            t = self._inputType
+            for i, c in enumerate(confs):
+                if i not in pps:
+                    pp = c.getPreProcessorForInputType(t)
+                    if pp is not None:
+                        pps[i] = pp
+                if i in pps:
+                    t = pps[i].getOutputType(t)
+                c.setNIn(t, False)
+                t = c.getOutputType(i, t)
+        for i, c in enumerate(confs):
+            if hasattr(c, "finalize_defaults"):
+                c.finalize_defaults()
+            if c.layerName is None:
+                c.layerName = f"layer{i}"
+        return MultiLayerConfiguration(
+            confs=confs, inputPreProcessors=pps, backprop=self._backprop, pretrain=self._pretrain,
+            backpropType=self._bpType, tbpttFwdLength=self._fwd, tbpttBackLength=self._back,
+            globalConf={k: v for k, v in g.items() if k in _NET_KEYS}, inputType=self._inputType)
+
+
+_NET_KEYS = ("seed", "optimizationAlgo", "miniBatch", "maxNumLineSearchIterations", "minimize", "stepFunction",
+             "trainingWorkspaceMode", "inferenceWorkspaceMode", "cacheMode", "dataType")
+
+
+class MultiLayerConfiguration(Config):
+    FIELDS = {"confs": [], "inputPreProcessors": {}, "backprop": True, "pretrain": False,
+              "backpropType": BackpropType.Standard, "tbpttFwdLength": 20, "tbpttBackLength": 20,
+              "globalConf": {}, "iterationCount": 0, "epochCount": 0, "inputType": None}
+
+    def getConf(self, i):
+        return self.confs[i]
+
+    def getInputPreProcess(self, i):
+        return self.inputPreProcessors.get(i)
+
+    def getInputPreProcessors(self):
+        return self.inputPreProcessors
+
+    @property
+    def seed(self):
+        return self.globalConf.get("seed", 12345)
+
+    @property
+    def dataType(self):
+        return DataType.of(self.globalConf.get("dataType", DataType.FLOAT))
+
+    def setDataType(self, d):
+        self.globalConf["dataType"] = DataType.of(d)
+
+    def toYaml(self):
+        import yaml
+        return yaml.safe_dump(json.loads(self.toJson()), sort_keys=True)
+
+    @staticmethod
+    def fromYaml(s):
+        import yaml
+        return _decode(yaml.safe_load(s))
+
+    @staticmethod
+    def fromJson(s):
+        return _decode(json.loads(s))
+
+
+class GraphBuilder:
+    def __init__(self, g):
+        self._g = g
+        self._inputs = []
+        self._outputs = []
+        self._vertices = {}
+        self._vertexInputs = {}
+        self._inputTypes = None
+        self._backprop = True
+        self._pretrain = False
+        self._bpType = BackpropType.Standard
+        self._fwd = 20
+        self._back = 20
+        self._order = []
+
+    def addInputs(self, *names):
+        self._inputs += [n for ns in names for n in (ns if isinstance(ns, (list, tuple)) else [ns])]
+        return self
+
+    def setOutputs(self, *names):
+        self._outputs = [n for ns in names for n in (ns if isinstance(ns, (list, tuple)) else [ns])]
+        return self
+
+    def addLayer(self, name, layer, *inputs):
+        pp = None
+        if inputs and not isinstance(inputs[0], str):
+            pp, inputs = inputs[0], inputs[1:]
+        if hasattr(layer, "build") and not isinstance(layer, Layer):
+            layer = layer.build()
+        layer = copy.deepcopy(layer)
+        if layer.layerName is None:
+            layer.layerName = name
+        self._vertices[name] = LayerVertex(layerConf=layer, preProcessor=pp)
+        self._vertexInputs[name] = list(inputs)
+        self._order.append(name)
+        return self
+
+    def layer(self, name, layer, *inputs):
+        return self.addLayer(name, layer, *inputs)
+
+    def addVertex(self, name, vertex, *inputs):
+        self._vertices[name] = copy.deepcopy(vertex)
+        self._vertexInputs[name] = list(inputs)
+        self._order.append(name)
+        return self
+
+    def removeVertex(self, name, removeConnections=True):
+        self._vertices.pop(name, None)
+        self._vertexInputs.pop(name, None)
+        self._order = [n for n in self._order if n != name]
+        if removeConnections:
+            for k in self._vertexInputs:
+                self._vertexInputs[k] = [i for i in self._vertexInputs[k] if i != name]
+            self._outputs = [o for o in self._outputs if o != name]
+        return self
+
+    def setInputTypes(self, *types):
+        self._inputTypes = list(types)
+        return self
+
+    def inputPreProcessor(self, name, pp):
+        self._vertices[name].preProcessor = pp
+        return self
+
+    def backprop(self, b):
+        self._backprop = bool(b)
+        return self
+
+    def pretrain(self, b):
+        self._pretrain = bool(b)
+        return self
+
+    def backpropType(self, t):
+        self._bpType = BackpropType.of(t)
+        return self
+
+    def tBPTTLength(self, n):
+        self._fwd = self._back = int(n)
+        return self
+
+    def tBPTTForwardLength(self, n):
+        self._fwd = int(n)
+        return self
+
+    def tBPTTBackwardLength(self, n):
+        self._back = int(n)
+        return self
+
+    def build(self):
+        if not self._inputs:
+            raise ValueError("ComputationGraph must have at least one input (addInputs)")
+        if not self._outputs:
+            raise ValueError("ComputationGraph must have at least one output (setOutputs)")
+        names = set(self._vertices) | set(self._inputs)
+        for v, ins in self._vertexInputs.items():
+            for i in ins:
+                if i not in names:
+                    raise ValueError(f"Vertex {v!r} has unknown input {i!r}")
+        for o in self._outputs:
+            if o not in self._vertices:
+                raise ValueError(f"Output {o!r} is not a vertex")
+        conf = ComputationGraphConfiguration(
+            vertices={k: self._vertices[k] for k in self._order}, vertexInputs=dict(self._vertexInputs),
+            networkInputs=list(self._inputs), networkOutputs=list(self._outputs), backprop=self._backprop,
+            pretrain=self._pretrain, backpropType=self._bpType, tbpttFwdLength=self._fwd,
+            tbpttBackLength=self._back, globalConf={k: v for k, v in self._g.items() if k in _NET_KEYS},
+            inputTypes=self._inputTypes)
+        for v in conf.vertices.values():
+            if isinstance(v, LayerVertex):
+                v.layerConf.applyGlobal(self._g)
+        if self._inputTypes is not None:
+            conf.addPreProcessorsAndInferNIn()
+        for v in conf.vertices.values():
+            if isinstance(v, LayerVertex) and hasattr(v.layerConf, "finalize_defaults"):
+                v.layerConf.finalize_defaults()
+        return conf
+
+
+class ComputationGraphConfiguration(Config):
+    FIELDS = {"vertices": {}, "vertexInputs": {}, "networkInputs": [], "networkOutputs": [], "backprop": True,
+              "pretrain": False, "backpropType": BackpropType.Standard, "tbpttFwdLength": 20,
+              "tbpttBackLength": 20, "globalConf": {}, "iterationCount": 0, "epochCount": 0, "inputTypes": None}
+
+    @property
+    def seed(self):
+        return self.globalConf.get("seed", 12345)
+
+    @property
+    def dataType(self):
+        return DataType.of(self.globalConf.get("dataType", DataType.FLOAT))
+
+    def setDataType(self, d):
+        self.globalConf["dataType"] = DataType.of(d)
+
+    def topologicalOrder(self):
+        """Kahn's algorithm, ties broken by insertion order (reference ComputationGraph.java:1216-1318)."""
+        all_names = list(self.networkInputs) + [k for k in self.vertices]
+        indeg = {n: 0 for n in all_names}
+        outs = {n: [] for n in all_names}
+        for v, ins in self.vertexInputs.items():
+            for i in ins:
+                indeg[v] += 1
+                outs[i].append(v)
+        queue = [n for n in all_names if indeg[n] == 0]
+        order = []
+        while queue:
+            n = queue.pop(0)
+            order.append(n)
+            for m in outs[n]:
+                indeg[m] -= 1
+                if indeg[m] == 0:
+                    queue.append(m)
+        if len(order) != len(all_names):
+            raise ValueError("Invalid ComputationGraph configuration: graph contains a cycle")
+        return order
+
+    def addPreProcessorsAndInferNIn(self):
+        types = {}
+        for name, t in zip(self.networkInputs, self.inputTypes):
+            types[name] = t
+        for i, name in enumerate(self.topologicalOrder()):
+            if name in self.networkInputs:
+                continue
+            v = self.vertices[name]
+            ins = [types[x] for x in self.vertexInputs[name]]
+            if isinstance(v, LayerVertex):
+                t = ins[0]
+                if len(ins) > 1:
+                    from .graph import MergeVertex
+                    t = MergeVertex().getOutputType(i, *ins)
+                if v.preProcessor is None:
+                    v.preProcessor = v.layerConf.getPreProcessorForInputType(t)
+                if v.preProcessor is not None:
+                    t = v.preProcessor.getOutputType(t)
+                v.layerConf.setNIn(t, False)
+                types[name] = v.layerConf.getOutputType(i, t)
+            else:
+                types[name] = v.getOutputType(i, *ins)
+        self._types = types
+        return types
+
+    def getLayerActivationTypes(self):
+        return getattr(self, "_types", None) or self.addPreProcessorsAndInferNIn()
+
+    @staticmethod
+    def fromJson(s):
+        return _decode(json.loads(s))
+
+    def toYaml(self):
+        import yaml
+        return yaml.safe_dump(json.loads(self.toJson()), sort_keys=True)
+
+    @staticmethod
+    def fromYaml(s):
+        import yaml
+        return _decode(yaml.safe_load(s))
+
+
+_ = (GraphVertex, InputType)

@@ -1,0 +1,212 @@
+"""Dropout variants, weight noise and parameter constraints.
+
+Reference: nn/conf/dropout/{Dropout,AlphaDropout,GaussianDropout,GaussianNoise}.java (Dropout.java:84
+uses inverted dropout with *retain* probability p), nn/conf/weightnoise/{DropConnect,WeightNoise}.java,
+nn/conf/constraint/{MaxNorm,MinMaxNorm,NonNegative,UnitNorm}Constraint.java.
+"""
+import math
+
+import torch
+
+from .base import Config
+from .weights import Distribution, NormalDistribution
+
+
+class IDropout(Config):
+    """applyDropout(x, iteration, epoch, training) -> x'; backprop(grad) uses the saved mask."""
+
+    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+        raise NotImplementedError
+
+    def backprop(self, grad):
+        raise NotImplementedError
+
+    def clear(self):
+        self._mask = None
+
+
+def _pval(p, iteration, epoch):
+    return p.valueAt(iteration, epoch) if hasattr(p, "valueAt") else p
+
+
+class Dropout(IDropout):
+    """Inverted dropout, p = probability of RETAINING an activation (reference Dropout.java:84)."""
+    FIELDS = {"p": 0.5}
+
+    def __init__(self, p=0.5, **kw):
+        super().__init__(p=p, **kw)
+
+    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+        if not training:
+            return x
+        p = _pval(self.p, iteration, epoch)
+        if p >= 1.0:
+            self._mask = None
+            return x
+        self._mask = (torch.rand_like(x, dtype=torch.float32) < p).to(x.dtype) / p
+        return x * self._mask
+
+    def backprop(self, grad):
+        m = getattr(self, "_mask", None)
+        return grad if m is None else grad * m
+
+
+class AlphaDropout(IDropout):
+    """Alpha dropout for SELU networks (Klambauer et al. 2017), reference AlphaDropout.java:113."""
+    FIELDS = {"p": 0.5}
+    ALPHA = 1.6732632423543772848170429916717
+    LAMBDA = 1.0507009873554804934193349852946
+
+    def __init__(self, p=0.5, **kw):
+        super().__init__(p=p, **kw)
+
+    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+        if not training:
+            return x
+        p = _pval(self.p, iteration, epoch)
+        alpha_p = -self.LAMBDA * self.ALPHA
+        a = 1.0 / math.sqrt(p + alpha_p * alpha_p * p * (1 - p))
+        b = -a * alpha_p * (1 - p)
+        keep = (torch.rand_like(x, dtype=torch.float32) < p).to(x.dtype)
+        self._mask = keep * a
+        return a * (x * keep + alpha_p * (1 - keep)) + b
+
+    def backprop(self, grad):
+        return grad * self._mask
+
+
+class GaussianDropout(IDropout):
+    """Multiplicative N(1, rate/(1-rate)) noise (reference GaussianDropout.java:66)."""
+    FIELDS = {"rate": 0.5}
+
+    def __init__(self, rate=0.5, **kw):
+        super().__init__(rate=rate, **kw)
+
+    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+        if not training:
+            return x
+        r = _pval(self.rate, iteration, epoch)
+        std = math.sqrt(r / (1 - r))
+        self._mask = (torch.randn_like(x, dtype=torch.float32) * std + 1.0).to(x.dtype)
+        return x * self._mask
+
+    def backprop(self, grad):
+        return grad * self._mask
+
+
+class GaussianNoise(IDropout):
+    """Additive zero-mean Gaussian noise (reference GaussianNoise.java:53)."""
+    FIELDS = {"stddev": 0.1}
+
+    def __init__(self, stddev=0.1, **kw):
+        super().__init__(stddev=stddev, **kw)
+
+    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+        if not training:
+            return x
+        s = _pval(self.stddev, iteration, epoch)
+        return x + torch.randn_like(x) * s
+
+    def backprop(self, grad):
+        return grad
+
+
+def to_dropout(d):
+    if d is None or isinstance(d, IDropout):
+        return d
+    d = float(d)
+    if d == 0.0 or d == 1.0:     # reference: dropOut(0) and dropOut(1) both mean "no dropout"
+        return None
+    return Dropout(d)
+
+
+# ------------------------------------------------------------------------------- weight noise
+class IWeightNoise(Config):
+    def getParameter(self, layer, key, param, iteration, epoch, training):
+        raise NotImplementedError
+
+
+class DropConnect(IWeightNoise):
+    FIELDS = {"weightRetainProb": 0.5, "applyToBiases": False}
+
+    def __init__(self, weightRetainProb=0.5, **kw):
+        super().__init__(weightRetainProb=weightRetainProb, **kw)
+
+    def getParameter(self, layer, key, param, iteration, epoch, training):
+        if not training or (key == "b" and not self.applyToBiases):
+            return param
+        p = _pval(self.weightRetainProb, iteration, epoch)
+        return param * (torch.rand_like(param, dtype=torch.float32) < p).to(param.dtype)
+
+
+class WeightNoise(IWeightNoise):
+    FIELDS = {"distribution": None, "applyToBias": False, "additive": True}
+
+    def __init__(self, distribution=None, **kw):
+        super().__init__(distribution=distribution or NormalDistribution(0, 1), **kw)
+
+    def getParameter(self, layer, key, param, iteration, epoch, training):
+        if not training or (key == "b" and not self.applyToBias):
+            return param
+        noise = torch.empty(param.shape, dtype=torch.float32)
+        self.distribution.sample_(noise)
+        noise = noise.to(param.device, param.dtype)
+        return param + noise if self.additive else param * noise
+
+
+# --------------------------------------------------------------------------------- constraints
+class LayerConstraint(Config):
+    FIELDS = {"params": None, "dimensions": [1]}
+
+    def apply_(self, key, p):
+        raise NotImplementedError
+
+    def applies_to(self, key, is_bias):
+        if self.params:
+            return key in self.params
+        return not is_bias
+
+    def _norm_dims(self, p):
+        dims = [d for d in (self.dimensions or [1]) if d < p.dim()]
+        return dims or list(range(1, p.dim())) or [0]
+
+
+class MaxNormConstraint(LayerConstraint):
+    FIELDS = {"maxNorm": 1.0}
+
+    def __init__(self, maxNorm=1.0, *dims, **kw):
+        if dims:
+            kw["dimensions"] = list(dims)
+        super().__init__(maxNorm=maxNorm, **kw)
+
+    def apply_(self, key, p):
+        # reference MaxNormConstraint: norm over the input dimension(s) = all dims except the output one
+        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
+        n = p.norm(dim=dims, keepdim=True)
+        scale = torch.clamp(self.maxNorm / (n + 1e-6), max=1.0)
+        p.mul_(scale)
+
+
+class MinMaxNormConstraint(LayerConstraint):
+    FIELDS = {"min": 0.0, "max": 1.0, "rate": 1.0}
+
+    def apply_(self, key, p):
+        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
+        n = p.norm(dim=dims, keepdim=True)
+        clipped = torch.clamp(n, self.min, self.max)
+        target = self.rate * clipped + (1 - self.rate) * n
+        p.mul_(target / (n + 1e-6))
+
+
+class NonNegativeConstraint(LayerConstraint):
+    def apply_(self, key, p):
+        p.clamp_(min=0)
+
+
+class UnitNormConstraint(LayerConstraint):
+    def apply_(self, key, p):
+        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
+        p.div_(p.norm(dim=dims, keepdim=True) + 1e-6)
+
+
+_ = Distribution  # re-export convenience

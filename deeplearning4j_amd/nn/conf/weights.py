@@ -1,0 +1,190 @@
+"""Weight initialisation schemes and distributions.
+
+Reference: nn/weights/WeightInit.java:68-71, nn/weights/WeightInitUtil.java:64-144 (formulas below are
+the same), nn/conf/distribution/*.java.  Initialisation fills a view of the flat parameter vector
+in place (no copies), as WeightInitUtil does.
+"""
+import math
+from enum import Enum
+
+import torch
+
+from .base import Config, register_enum
+
+
+class Distribution(Config):
+    def sample_(self, t, gen=None):
+        raise NotImplementedError
+
+
+class NormalDistribution(Distribution):
+    FIELDS = {"mean": 0.0, "std": 1.0}
+
+    def __init__(self, mean=0.0, std=1.0, **kw):
+        super().__init__(mean=mean, std=std, **kw)
+
+    def sample_(self, t, gen=None):
+        return t.normal_(self.mean, self.std, generator=gen)
+
+
+class GaussianDistribution(NormalDistribution):
+    pass
+
+
+class UniformDistribution(Distribution):
+    FIELDS = {"lower": 0.0, "upper": 1.0}
+
+    def __init__(self, lower=0.0, upper=1.0, **kw):
+        super().__init__(lower=lower, upper=upper, **kw)
+
+    def sample_(self, t, gen=None):
+        return t.uniform_(self.lower, self.upper, generator=gen)
+
+
+class ConstantDistribution(Distribution):
+    FIELDS = {"value": 0.0}
+
+    def __init__(self, value=0.0, **kw):
+        super().__init__(value=value, **kw)
+
+    def sample_(self, t, gen=None):
+        return t.fill_(self.value)
+
+
+class BinomialDistribution(Distribution):
+    FIELDS = {"numberOfTrials": 1, "probabilityOfSuccess": 0.5}
+
+    def __init__(self, numberOfTrials=1, probabilityOfSuccess=0.5, **kw):
+        super().__init__(numberOfTrials=numberOfTrials, probabilityOfSuccess=probabilityOfSuccess, **kw)
+
+    def sample_(self, t, gen=None):
+        p = torch.full(t.shape, self.probabilityOfSuccess, dtype=torch.float64)
+        s = torch.distributions.Binomial(self.numberOfTrials, p).sample()
+        return t.copy_(s)
+
+
+class LogNormalDistribution(Distribution):
+    FIELDS = {"mean": 0.0, "std": 1.0}
+
+    def __init__(self, mean=0.0, std=1.0, **kw):
+        super().__init__(mean=mean, std=std, **kw)
+
+    def sample_(self, t, gen=None):
+        return t.log_normal_(self.mean, self.std, generator=gen)
+
+
+class TruncatedNormalDistribution(Distribution):
+    FIELDS = {"mean": 0.0, "std": 1.0}
+
+    def __init__(self, mean=0.0, std=1.0, **kw):
+        super().__init__(mean=mean, std=std, **kw)
+
+    def sample_(self, t, gen=None):
+        tmp = torch.empty(t.shape, dtype=torch.float32)
+        torch.nn.init.trunc_normal_(tmp, self.mean, self.std, self.mean - 2 * self.std, self.mean + 2 * self.std,
+                                    generator=gen)
+        return t.copy_(tmp)
+
+
+class OrthogonalDistribution(Distribution):
+    FIELDS = {"gain": 1.0}
+
+    def __init__(self, gain=1.0, **kw):
+        super().__init__(gain=gain, **kw)
+
+    def sample_(self, t, gen=None):
+        tmp = torch.empty(t.shape if t.dim() >= 2 else (1, t.numel()), dtype=torch.float32)
+        torch.nn.init.orthogonal_(tmp, self.gain, generator=gen)
+        return t.copy_(tmp.reshape(t.shape))
+
+
+@register_enum
+class WeightInit(Enum):
+    DISTRIBUTION = "DISTRIBUTION"
+    ZERO = "ZERO"
+    ONES = "ONES"
+    SIGMOID_UNIFORM = "SIGMOID_UNIFORM"
+    NORMAL = "NORMAL"
+    LECUN_NORMAL = "LECUN_NORMAL"
+    UNIFORM = "UNIFORM"
+    XAVIER = "XAVIER"
+    XAVIER_UNIFORM = "XAVIER_UNIFORM"
+    XAVIER_FAN_IN = "XAVIER_FAN_IN"
+    XAVIER_LEGACY = "XAVIER_LEGACY"
+    RELU = "RELU"
+    RELU_UNIFORM = "RELU_UNIFORM"
+    IDENTITY = "IDENTITY"
+    LECUN_UNIFORM = "LECUN_UNIFORM"
+    VAR_SCALING_NORMAL_FAN_IN = "VAR_SCALING_NORMAL_FAN_IN"
+    VAR_SCALING_NORMAL_FAN_OUT = "VAR_SCALING_NORMAL_FAN_OUT"
+    VAR_SCALING_NORMAL_FAN_AVG = "VAR_SCALING_NORMAL_FAN_AVG"
+    VAR_SCALING_UNIFORM_FAN_IN = "VAR_SCALING_UNIFORM_FAN_IN"
+    VAR_SCALING_UNIFORM_FAN_OUT = "VAR_SCALING_UNIFORM_FAN_OUT"
+    VAR_SCALING_UNIFORM_FAN_AVG = "VAR_SCALING_UNIFORM_FAN_AVG"
+
+
+def init_weights_(view, fan_in, fan_out, shape, scheme, dist=None, gen=None):
+    """Fill ``view`` (any shape, numel == prod(shape)) in place. Sampling happens in fp32 on the host
+    generator for reproducibility across devices, then copies into the (device) view."""
+    scheme = WeightInit[scheme] if isinstance(scheme, str) else scheme
+    n = view.numel()
+    tmp = torch.empty(n, dtype=torch.float64 if view.dtype == torch.float64 else torch.float32)
+
+    def U(a):
+        tmp.uniform_(-a, a, generator=gen)
+
+    def N(std):
+        tmp.normal_(0.0, std, generator=gen)
+
+    W = WeightInit
+    if scheme == W.DISTRIBUTION:
+        if dist is None:
+            raise ValueError("WeightInit.DISTRIBUTION requires a distribution (dist)")
+        dist.sample_(tmp, gen)
+    elif scheme == W.RELU:
+        N(math.sqrt(2.0 / fan_in))
+    elif scheme == W.RELU_UNIFORM:
+        U(math.sqrt(6.0 / fan_in))
+    elif scheme == W.SIGMOID_UNIFORM:
+        U(4.0 * math.sqrt(6.0 / (fan_in + fan_out)))
+    elif scheme == W.UNIFORM:
+        U(1.0 / math.sqrt(fan_in))
+    elif scheme == W.LECUN_UNIFORM:
+        U(3.0 / math.sqrt(fan_in))
+    elif scheme == W.XAVIER:
+        N(math.sqrt(2.0 / (fan_in + fan_out)))
+    elif scheme == W.XAVIER_UNIFORM:
+        U(math.sqrt(6.0) / math.sqrt(fan_in + fan_out))
+    elif scheme in (W.LECUN_NORMAL, W.NORMAL, W.XAVIER_FAN_IN, W.VAR_SCALING_NORMAL_FAN_IN):
+        N(1.0 / math.sqrt(fan_in))
+    elif scheme == W.XAVIER_LEGACY:
+        N(1.0 / math.sqrt(shape[0] + shape[1]))
+    elif scheme == W.ZERO:
+        tmp.zero_()
+    elif scheme == W.ONES:
+        tmp.fill_(1.0)
+    elif scheme == W.IDENTITY:
+        if len(shape) != 2 or shape[0] != shape[1]:
+            raise ValueError(f"Cannot use IDENTITY init with parameters of shape {shape}")
+        tmp.copy_(torch.eye(shape[0]).reshape(-1))
+    elif scheme == W.VAR_SCALING_NORMAL_FAN_OUT:
+        N(1.0 / math.sqrt(fan_out))
+    elif scheme == W.VAR_SCALING_NORMAL_FAN_AVG:
+        N(1.0 / math.sqrt((fan_in + fan_out) / 2))
+    elif scheme == W.VAR_SCALING_UNIFORM_FAN_IN:
+        U(3.0 / math.sqrt(fan_in))
+    elif scheme == W.VAR_SCALING_UNIFORM_FAN_OUT:
+        U(3.0 / math.sqrt(fan_out))
+    elif scheme == W.VAR_SCALING_UNIFORM_FAN_AVG:
+        U(3.0 / math.sqrt((fan_in + fan_out) / 2))
+    else:
+        raise ValueError(f"Illegal weight init value: {scheme}")
+    with torch.no_grad():
+        view.copy_(tmp.reshape(view.shape).to(view.dtype))
+    return view
+
+
+def to_weight_init(w):
+    if w is None or isinstance(w, WeightInit):
+        return w
+    return WeightInit[str(w).upper()]

@@ -1,0 +1,429 @@
+"""ComputationGraph: DAG model (reference nn/graph/ComputationGraph.java, 3904 LoC).
+
+* topological order by Kahn's algorithm (:1216-1318); flat params in topological order (:401-470)
+* forward in topological order (:1577-1700); backward in reverse topological order with epsilon
+  summation for fan-out (:1947-2107, sum at :2044-2063)
+* multi-input / multi-output; score = sum of output-layer losses + L1/L2 once (:1360-1373)
+* TBPTT (:2894), rnnTimeStep (:2720)
+Planner: BatchNormalization -> ActivationLayer(ReLU) pairs where the BN output has a single consumer
+are fused so the HIP BN kernel applies the ReLU (ResNet-50: 49 such pairs).
+"""
+import torch
+
+from ...datasets.dataset import DataSet, MultiDataSet
+from ..conf.enums import BackpropType
+from ..conf.graph import LayerVertex
+from ..conf.layers import ActivationLayer, BatchNormalization
+from ..layers.output import BaseOutputLayerImpl
+from ..network_base import BaseNetwork
+
+
+class ComputationGraph(BaseNetwork):
+    _key_by_name = True
+
+    def __init__(self, conf, params=None):
+        super().__init__(conf)
+        self._init_params = params
+        self.inputs = None
+        self.labels = None
+        self.inputMaskArrays = None
+        self.labelMaskArrays = None
+
+    # ------------------------------------------------------------------------------ init
+    def init(self, parameters=None, cloneParametersArray=False, device=None):
+        if self.initCalled and parameters is None:
+            return
+        parameters = parameters if parameters is not None else self._init_params
+        conf = self.conf
+        if conf.inputTypes is not None and not hasattr(conf, "_types"):
+            conf.addPreProcessorsAndInferNIn()
+        self.topo = [n for n in conf.topologicalOrder() if n not in conf.networkInputs]
+        self.vertex_inputs = conf.vertexInputs
+        self.consumers = {n: [] for n in list(conf.networkInputs) + self.topo}
+        for v in self.topo:
+            for i in self.vertex_inputs[v]:
+                self.consumers[i].append(v)
+        self.layers_by_name = {}
+        layer_list = []
+        for idx, name in enumerate(self.topo):
+            v = conf.vertices[name]
+            if isinstance(v, LayerVertex):
+                impl = v.layerConf.instantiate(index=idx, net=self)
+                self.layers_by_name[name] = impl
+                layer_list.append((idx, name, impl))
+        self._setup_flat(layer_list, parameters, cloneParametersArray, device)
+        self.outputs = list(conf.networkOutputs)
+        self._plan_fusions()
+        for l in self.layers_by_name.values():
+            if hasattr(l, "bind"):
+                l.bind()
+
+    def _plan_fusions(self):
+        from ..conf.activations import ActivationReLU
+        self._passthrough = set()
+        for name in self.topo:
+            v = self.conf.vertices[name]
+            if not (isinstance(v, LayerVertex) and isinstance(v.layerConf, BatchNormalization)):
+                continue
+            cons = self.consumers[name]
+            if len(cons) != 1 or name in self.outputs:
+                continue
+            nxt = self.conf.vertices[cons[0]]
+            if isinstance(nxt, LayerVertex) and isinstance(nxt.layerConf, ActivationLayer) and \
+                    isinstance(nxt.layerConf.activation, ActivationReLU) and nxt.preProcessor is None and \
+                    nxt.layerConf.idropout is None and v.layerConf.idropout is None and len(self.vertex_inputs[cons[0]]) == 1:
+                self.layers_by_name[name].fuse_relu = True
+                self._passthrough.add(cons[0])
+
+    def getLayers(self):
+        return list(self.layers_by_name.values())
+
+    def getLayer(self, name):
+        if isinstance(name, int):
+            return self.getLayers()[name]
+        return self.layers_by_name[name]
+
+    def getVertex(self, name):
+        return self.conf.vertices[name]
+
+    def getNumLayers(self):
+        return len(self.layers_by_name)
+
+    def getOutputLayer(self, i):
+        return self.layers_by_name[self.outputs[i]]
+
+    def getConfiguration(self):
+        return self.conf
+
+    # ------------------------------------------------------------------------------ forward
+    def _prep_inputs(self, inputs):
+        if torch.is_tensor(inputs) or not isinstance(inputs, (list, tuple)):
+            inputs = [inputs]
+        out = []
+        for x in inputs:
+            if not torch.is_tensor(x):
+                import numpy as np
+                x = torch.from_numpy(np.asarray(x))
+            out.append(self._to_dev(x, self._feat_dtype()) if x.is_floating_point() else self._to_dev(x))
+        return out
+
+    def feedForward(self, inputs=None, train=False, masks=None, stored_state=False, store_last_for_tbptt=False,
+                    layerTillIndex=None):
+        inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
+        acts = {}
+        amask = {}
+        mb = inputs[0].shape[0]
+        for i, n in enumerate(self.conf.networkInputs):
+            acts[n] = inputs[i]
+            amask[n] = masks[i] if masks is not None and i < len(masks) else None
+        self._ctx = {}
+        for name in self.topo:
+            v = self.conf.vertices[name]
+            ins = [acts[i] for i in self.vertex_inputs[name]]
+            ms = [amask.get(i) for i in self.vertex_inputs[name]]
+            if isinstance(v, LayerVertex):
+                x = ins[0] if len(ins) == 1 else torch.cat(ins, dim=1)
+                if len(ins) > 1:
+                    self._ctx[name] = ("merge", [t.shape[1] for t in ins])
+                mask = ms[0] if ms else None
+                if v.preProcessor is not None:
+                    x = v.preProcessor.preProcess(x, mb, train)
+                    if mask is not None:
+                        mask, _ = v.preProcessor.feedForwardMaskArray(mask, None, mb)
+                if name in self._passthrough:
+                    acts[name] = x
+                    amask[name] = mask
+                    continue
+                layer = self.layers_by_name[name]
+                layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
+                if stored_state and hasattr(layer, "tBpttStateMap"):
+                    out = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
+                else:
+                    out = layer.activate(x, train, mask)
+                acts[name] = out
+                amask[name], _ = layer.feedForwardMaskArray(mask, None, mb)
+            else:
+                from ..conf.graph import DuplicateToTimeSeriesVertex
+                if isinstance(v, DuplicateToTimeSeriesVertex):
+                    v._T = acts[v.inputName].shape[2]
+                out, ctx = v.forward(ins, train, ms)
+                self._ctx[name] = ("vertex", ctx)
+                acts[name] = out
+                amask[name] = v.feedForwardMask(ms)
+        self._acts_masks = amask
+        return acts
+
+    def output(self, *inputs, train=False, masks=None):
+        if len(inputs) == 1 and isinstance(inputs[0], (list, tuple)):
+            inputs = inputs[0]
+        with torch.no_grad():
+            acts = self.feedForward(list(inputs), train, masks)
+        outs = [acts[o].float() for o in self.outputs]
+        return outs
+
+    def outputSingle(self, *inputs, train=False):
+        return self.output(*inputs, train=train)[0]
+
+    # ------------------------------------------------------------------------------ backward
+    def _backprop(self, tbptt_back=None):
+        eps_acc = {}
+
+        def add(name, e):
+            if e is None:
+                return
+            if name in eps_acc:
+                eps_acc[name] = eps_acc[name] + e
+            else:
+                eps_acc[name] = e
+
+        self._begin_backward()
+        for name in reversed(self.topo):
+            v = self.conf.vertices[name]
+            if isinstance(v, LayerVertex):
+                layer = self.layers_by_name.get(name)
+                if name in self.outputs and isinstance(layer, BaseOutputLayerImpl):
+                    _, e = layer.backpropGradient(None)
+                    self._grad_ready(name)
+                    if name in eps_acc:
+                        e = e + eps_acc.pop(name) if e is not None else eps_acc.pop(name)
+                elif name in self._passthrough:
+                    e = eps_acc.pop(name, None)
+                else:
+                    e_in = eps_acc.pop(name, None)
+                    if e_in is None:
+                        continue
+                    if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
+                        _, e = layer.backpropGradient(e_in, tbptt_back=tbptt_back)
+                    else:
+                        _, e = layer.backpropGradient(e_in)
+                    self._grad_ready(name)
+                if e is None:
+                    continue
+                if v.preProcessor is not None:
+                    e = v.preProcessor.backprop(e, self._mb)
+                ins = self.vertex_inputs[name]
+                if len(ins) > 1:
+                    parts = torch.split(e, self._ctx[name][1], dim=1)
+                    for i, p in zip(ins, parts):
+                        add(i, p)
+                else:
+                    add(ins[0], e)
+            else:
+                e_in = eps_acc.pop(name, None)
+                if e_in is None:
+                    continue
+                es = v.backward(e_in, self._ctx[name][1])
+                for i, ei in zip(self.vertex_inputs[name], es):
+                    add(i, ei)
+        for l in self.listeners:
+            if hasattr(l, "onBackwardPass"):
+                l.onBackwardPass(self)
+        self._input_eps = [eps_acc.get(n) for n in self.conf.networkInputs]
+        return self._input_eps
+
+    def computeGradientAndScore(self, inputs=None, labels=None, fmasks=None, lmasks=None, stored_state=False,
+                                store_last_for_tbptt=False, tbptt_back=None):
+        inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
+        labels = self.labels if labels is None else labels
+        if torch.is_tensor(labels):
+            labels = [labels]
+        self._mb = inputs[0].shape[0]
+        fm = [self._to_dev(m) for m in fmasks] if fmasks else None
+        acts = self.feedForward(inputs, True, fm, stored_state, store_last_for_tbptt)
+        for l in self.listeners:
+            if hasattr(l, "onForwardPass"):
+                l.onForwardPass(self, acts)
+        for i, o in enumerate(self.outputs):
+            layer = self.layers_by_name[o]
+            layer.setLabels(self._to_dev(labels[i], self.master_dtype))
+            lm = lmasks[i] if lmasks is not None and i < len(lmasks) else None
+            if lm is not None:
+                layer.maskArray = self._to_dev(lm)
+        self._backprop(tbptt_back)
+        l1, l2 = self._regularization_terms()
+        score = None
+        for i, o in enumerate(self.outputs):
+            layer = self.layers_by_name[o]
+            s = layer.computeScore(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0, True)
+            score = s if score is None else score + s
+        self._score_t = score
+        self._score_val = None
+        return score
+
+    def _fit_batch(self, inputs, labels, fmasks=None, lmasks=None):
+        x0 = inputs[0] if isinstance(inputs, (list, tuple)) else inputs
+        if self.conf.backpropType == BackpropType.TruncatedBPTT and x0.dim() == 3:
+            return self._fit_tbptt(inputs, labels, fmasks, lmasks)
+        self.computeGradientAndScore(inputs, labels, fmasks, lmasks)
+        self._apply_update(x0.shape[0])
+        self._iteration_done()
+
+    def _fit_tbptt(self, inputs, labels, fmasks, lmasks):
+        inputs = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+        labels = labels if isinstance(labels, (list, tuple)) else [labels]
+        T = inputs[0].shape[2]
+        fwd, back = self.conf.tbpttFwdLength, self.conf.tbpttBackLength
+        self.rnnClearPreviousState()
+        for s in range((T + fwd - 1) // fwd):
+            t0, t1 = s * fwd, min(T, (s + 1) * fwd)
+            xs = [x[:, :, t0:t1] if x.dim() == 3 else x for x in inputs]
+            ys = [y[:, :, t0:t1] if y.dim() == 3 else y for y in labels]
+            fm = [m[:, t0:t1] if m is not None else None for m in fmasks] if fmasks else None
+            lm = [m[:, t0:t1] if m is not None else None for m in lmasks] if lmasks else None
+            self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
+                                         tbptt_back=back)
+            self._apply_update(inputs[0].shape[0])
+            self._iteration_done()
+        self.rnnClearPreviousState()
+
+    def fit(self, data, labels=None, numEpochs=None, featureMaskArrays=None, labelMaskArrays=None):
+        if not self.initCalled:
+            self.init()
+        if labels is not None and not isinstance(labels, int):
+            self._fit_batch(data, labels, featureMaskArrays, labelMaskArrays)
+            return self
+        if isinstance(labels, int):
+            numEpochs = labels
+        if numEpochs is not None:
+            for _ in range(numEpochs):
+                self.fit(data)
+            return self
+        if isinstance(data, DataSet):
+            self._fit_batch([data.features], [data.labels],
+                            None if data.featuresMask is None else [data.featuresMask],
+                            None if data.labelsMask is None else [data.labelsMask])
+            return self
+        if isinstance(data, MultiDataSet):
+            self._fit_batch(data.features, data.labels, data.featuresMasks, data.labelsMasks)
+            return self
+        self._fit_iterator(data)
+        return self
+
+    def _fit_iterator(self, it):
+        from ...datasets.iterators import AsyncDataSetIterator
+        wrap = it
+        if getattr(it, "asyncSupported", lambda: False)() and not isinstance(it, AsyncDataSetIterator) and \
+                type(it).__name__ not in ("BenchmarkDataSetIterator", "BenchmarkMultiDataSetIterator",
+                                          "ListDataSetIterator"):
+            wrap = AsyncDataSetIterator(it, 2, self.device)
+        for l in self.listeners:
+            if hasattr(l, "onEpochStart"):
+                l.onEpochStart(self)
+        wrap.reset()
+        t0 = self._timer()
+        while wrap.hasNext():
+            ds = wrap.next()
+            self.lastEtlTime = (self._timer() - t0) * 1000.0
+            if isinstance(ds, MultiDataSet):
+                self._fit_batch(ds.features, ds.labels, ds.featuresMasks, ds.labelsMasks)
+            else:
+                self._fit_batch([ds.features], [ds.labels], None if ds.featuresMask is None else [ds.featuresMask],
+                                None if ds.labelsMask is None else [ds.labelsMask])
+            t0 = self._timer()
+        if wrap is not it and hasattr(wrap, "shutdown"):
+            wrap.shutdown()
+        for l in self.listeners:
+            if hasattr(l, "onEpochEnd"):
+                l.onEpochEnd(self)
+        self.incrementEpochCount()
+
+    # ------------------------------------------------------------------------------ scoring / eval
+    def _score_dataset(self, ds, training=False):
+        if isinstance(ds, DataSet):
+            ds = MultiDataSet.fromDataSet(ds)
+        with torch.no_grad():
+            self._mb = ds.features[0].shape[0]
+            self.feedForward(ds.features, training)
+            l1, l2 = self._regularization_terms()
+            score = 0.0
+            for i, o in enumerate(self.outputs):
+                layer = self.layers_by_name[o]
+                layer.setLabels(self._to_dev(ds.labels[i], self.master_dtype))
+                score += float(layer.computeScore(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0, training))
+            return score
+
+    def evaluate(self, it, labelsList=None, topN=1):
+        from ...eval.evaluation import Evaluation
+        return self.doEvaluation(it, Evaluation(labelsList, topN=topN))[0]
+
+    def evaluateRegression(self, it):
+        from ...eval.regression import RegressionEvaluation
+        return self.doEvaluation(it, RegressionEvaluation())[0]
+
+    def evaluateROC(self, it, steps=0):
+        from ...eval.roc import ROC
+        return self.doEvaluation(it, ROC(steps))[0]
+
+    def doEvaluation(self, it, *evals):
+        items = [it] if isinstance(it, (DataSet, MultiDataSet)) else it
+        if not isinstance(it, (DataSet, MultiDataSet)):
+            it.reset()
+        for ds in items:
+            if isinstance(ds, MultiDataSet):
+                out = self.output(ds.features)[0]
+                lab = ds.labels[0]
+                lm = ds.labelsMasks[0] if ds.labelsMasks else None
+            else:
+                out = self.output(ds.features)[0]
+                lab, lm = ds.labels, ds.labelsMask
+            for e in evals:
+                e.eval(lab, out, lm)
+        return list(evals)
+
+    # ------------------------------------------------------------------------------ rnn
+    def rnnTimeStep(self, *inputs):
+        inputs = self._prep_inputs(list(inputs))
+        acts = {n: inputs[i] for i, n in enumerate(self.conf.networkInputs)}
+        with torch.no_grad():
+            for name in self.topo:
+                v = self.conf.vertices[name]
+                ins = [acts[i] for i in self.vertex_inputs[name]]
+                if isinstance(v, LayerVertex):
+                    x = ins[0] if len(ins) == 1 else torch.cat(ins, 1)
+                    if v.preProcessor is not None:
+                        x = v.preProcessor.preProcess(x, x.shape[0], False)
+                    layer = self.layers_by_name[name]
+                    if name in self._passthrough:
+                        acts[name] = x
+                    elif hasattr(layer, "rnnTimeStep"):
+                        acts[name] = layer.rnnTimeStep(x)
+                    else:
+                        acts[name] = layer.activate(x, False)
+                else:
+                    acts[name], _ = v.forward(ins, False, None)
+        return [acts[o].float() for o in self.outputs]
+
+    def rnnClearPreviousState(self):
+        for l in self.layers_by_name.values():
+            if hasattr(l, "rnnClearPreviousState"):
+                l.rnnClearPreviousState()
+
+    # ------------------------------------------------------------------------------ misc
+    def clone(self):
+        import copy
+        net = ComputationGraph(copy.deepcopy(self.conf))
+        net.init(self.params().clone(), device=self.device)
+        net.updater.setStateViewArray(self.updater.getStateViewArray().clone())
+        return net
+
+    def setInputs(self, *x):
+        self.inputs = list(x)
+
+    def setLabels(self, *y):
+        self.labels = list(y)
+
+    def setLearningRate(self, lr, layerName=None):
+        self.updater.setLearningRate(lr, layerName)
+
+    def save(self, path, saveUpdater=True):
+        from ...utils.model_serializer import ModelSerializer
+        ModelSerializer.writeModel(self, path, saveUpdater)
+
+    @staticmethod
+    def load(path, loadUpdater=True):
+        from ...utils.model_serializer import ModelSerializer
+        return ModelSerializer.restoreComputationGraph(path, loadUpdater)
+
+    def clear(self):
+        for l in self.layers_by_name.values():
+            l.clear()

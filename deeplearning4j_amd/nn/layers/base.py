@@ -1,0 +1,165 @@
+"""Runtime layer base (reference nn/api/Layer.java:54-288, nn/layers/AbstractLayer.java, BaseLayer.java).
+
+A runtime layer owns *views* into the network's flat parameter vector (master precision), the flat
+gradient vector, and — for reduced-precision compute — the flat bf16/fp16 shadow of the parameters.
+``activate`` runs the forward pass and caches what backprop needs; ``backpropGradient(eps)`` writes
+dL/dparam into the gradient views (sums over the minibatch, not means) and returns dL/dinput.
+"""
+import torch
+
+from ..gradient import Gradient
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+class LayerImpl:
+    def __init__(self, conf, index=0, net=None):
+        self.conf = conf
+        self.index = index
+        self.net = net
+        self.params = {}      # key -> master view (fp32/fp64)
+        self.cparams = {}     # key -> compute-dtype view (shadow) ; == params when no shadow
+        self.grads = {}       # key -> gradient view
+        self.input = None
+        self.maskArray = None
+        self.maskState = None
+        self.training = False
+        self.iteration = 0
+        self.epoch = 0
+        self.listeners = []
+        self.helperCountFail = 0
+        self.dropoutApplied = False
+
+    # -------------------------------------------------------------------------- params
+    def numParams(self):
+        return self.conf.numParams()
+
+    def paramTable(self):
+        return dict(self.params)
+
+    def getParam(self, key):
+        return self.params[key]
+
+    def setParam(self, key, val):
+        with torch.no_grad():
+            self.params[key].copy_(val.reshape(self.params[key].shape))
+            if self.cparams.get(key) is not None and self.cparams[key] is not self.params[key]:
+                self.cparams[key].copy_(self.params[key])
+
+    def setParamTable(self, table):
+        for k, v in table.items():
+            self.setParam(k, v)
+
+    def W(self, key="W"):
+        """Compute-dtype view of parameter ``key`` (with weight noise / DropConnect applied when training)."""
+        p = self.cparams.get(key, self.params.get(key))
+        wn = getattr(self.conf, "weightNoise", None)
+        if wn is not None and self.training:
+            p = wn.getParameter(self, key, p, self.iteration, self.epoch, True)
+        return p
+
+    def type(self):
+        return "FEED_FORWARD"
+
+    def layerId(self):
+        return f"(layer name: {self.conf.layerName}, index: {self.index}, type: {type(self).__name__})"
+
+    @property
+    def compute_dtype(self):
+        return self.net.compute_dtype if self.net is not None else torch.float32
+
+    # -------------------------------------------------------------------------- forward/backward
+    def applyDropOutIfNecessary(self, x, training):
+        d = getattr(self.conf, "idropout", None)
+        if training and d is not None:
+            self.dropoutApplied = True
+            return d.applyDropout(x, self.iteration, self.epoch, True)
+        self.dropoutApplied = False
+        return x
+
+    def backpropDropOut(self, eps):
+        d = getattr(self.conf, "idropout", None)
+        if self.dropoutApplied and d is not None:
+            return d.backprop(eps)
+        return eps
+
+    def activate(self, x, training=False, mask=None):
+        raise NotImplementedError
+
+    def backpropGradient(self, epsilon):
+        raise NotImplementedError
+
+    def preOutput(self, x, training=False):
+        raise NotImplementedError(f"preOutput not supported by {type(self).__name__}")
+
+    def make_gradient(self):
+        g = Gradient()
+        for k, v in self.grads.items():
+            g.setGradientFor(k, v)
+        return g
+
+    def clear(self):
+        self.input = None
+        self.maskArray = None
+
+    def setInput(self, x):
+        self.input = x
+
+    def getInput(self):
+        return self.input
+
+    # -------------------------------------------------------------------------- masks
+    def setMaskArray(self, m):
+        self.maskArray = m
+
+    def feedForwardMaskArray(self, mask, state, mb):
+        self.maskArray = mask
+        self.maskState = state
+        return mask, state
+
+    # -------------------------------------------------------------------------- misc
+    def isPretrainLayer(self):
+        return False
+
+    def calcL1(self, backprop_params_only=True):
+        s = 0.0
+        for k, p in self.params.items():
+            l1 = self.conf.l1For(k)
+            if l1 > 0:
+                s += l1 * p.abs().sum().item()
+        return s
+
+    def calcL2(self, backprop_params_only=True):
+        s = 0.0
+        for k, p in self.params.items():
+            l2 = self.conf.l2For(k)
+            if l2 > 0:
+                s += 0.5 * l2 * (_acc(p) * _acc(p)).sum().item()
+        return s
+
+    def applyConstraints(self, iteration, epoch):
+        cs = getattr(self.conf, "constraints", None)
+        if not cs:
+            return
+        with torch.no_grad():
+            for c in cs:
+                for k, p in self.params.items():
+                    if c.params == ["*"] or (c.params and k in c.params) or \
+                            (not c.params and not self.conf.is_bias(k)):
+                        if p.numel() == 0:
+                            continue
+                        c.apply_(k, p)
+                        if self.cparams.get(k) is not None and self.cparams[k] is not p:
+                            self.cparams[k].copy_(p)
+
+
+def matmul(a, b):
+    return torch.matmul(a, b)
+
+
+def add_row(z, b):
+    return z + b.reshape(1, -1).to(z.dtype)
+
+
+def copy_grad_(view, value):
+    """Write a gradient into a (possibly 'f'-ordered) gradient view."""
+    view.copy_(value.reshape(view.shape))

@@ -1,0 +1,318 @@
+"""Convolution-family runtime layers (reference nn/layers/convolution/*).
+
+ConvolutionLayer: forward = conv + bias (+activation), backward = (dW, db, dx)
+(ConvolutionLayer.java:131-265,290-428; helper SPI :173-200,345-375). Same mode pads
+top/left = floor(total/2) exactly like ConvolutionUtils.getSameModeTopLeftPadding.
+Activations are NCHW logically; on GPU they are kept channels-last in memory (NHWC) so the HIP
+implicit-GEMM kernels read contiguous channel vectors.
+"""
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ..conf.enums import ConvolutionMode
+from ..conf.layers import conv_out_size, same_padding
+from .base import LayerImpl, copy_grad_
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+def _cl(x):
+    if x.is_cuda and x.dim() == 4:
+        return x.contiguous(memory_format=torch.channels_last)
+    return x
+
+
+def compute_pad4(conf, h, w, kernel=None, stride=None, dilation=None):
+    kernel = kernel or conf.kernelSize
+    stride = stride or conf.stride
+    dilation = dilation or getattr(conf, "dilation", [1, 1]) or [1, 1]
+    if conf.convolutionMode == ConvolutionMode.Same:
+        oh = conv_out_size(h, kernel[0], stride[0], 0, dilation[0], ConvolutionMode.Same)
+        ow = conv_out_size(w, kernel[1], stride[1], 0, dilation[1], ConvolutionMode.Same)
+        pt, pb = same_padding(h, oh, kernel[0], stride[0], dilation[0])
+        pl, pr = same_padding(w, ow, kernel[1], stride[1], dilation[1])
+        return (pt, pb, pl, pr)
+    p = conf.padding
+    # validate (raises for Strict mode mismatches, as the reference does)
+    conv_out_size(h, kernel[0], stride[0], p[0], dilation[0], conf.convolutionMode)
+    conv_out_size(w, kernel[1], stride[1], p[1], dilation[1], conf.convolutionMode)
+    return (p[0], p[0], p[1], p[1])
+
+
+def _truncate_input(conf, x, kernel, stride, pad4, dilation):
+    """Truncate mode: crop rows/cols that no window reaches so the library conv sees an exact fit."""
+    if conf.convolutionMode == ConvolutionMode.Same:
+        return x
+    h, w = x.shape[2], x.shape[3]
+    oh = conv_out_size(h, kernel[0], stride[0], pad4[0], dilation[0], ConvolutionMode.Truncate)
+    ow = conv_out_size(w, kernel[1], stride[1], pad4[2], dilation[1], ConvolutionMode.Truncate)
+    need_h = (oh - 1) * stride[0] + (kernel[0] - 1) * dilation[0] + 1 - 2 * pad4[0]
+    need_w = (ow - 1) * stride[1] + (kernel[1] - 1) * dilation[1] + 1 - 2 * pad4[2]
+    if need_h < h or need_w < w:
+        return x[:, :, :max(need_h, 0) if need_h < h else h, :max(need_w, 0) if need_w < w else w]
+    return x
+
+
+class ConvolutionLayerImpl(LayerImpl):
+    def type(self):
+        return "CONVOLUTIONAL"
+
+    def _geom(self, x):
+        c = self.conf
+        pad4 = compute_pad4(c, x.shape[2], x.shape[3])
+        return list(c.kernelSize), list(c.stride), pad4, list(c.dilation)
+
+    def preOutput(self, x, training=False):
+        k, s, pad4, d = self._geom(x)
+        W = self.W("W")
+        b = self.W("b").reshape(-1) if "b" in self.params else None
+        xt = _truncate_input(self.conf, x, k, s, pad4, d)
+        self._xt = xt
+        self._geom_cache = (s, pad4, d)
+        return ops.conv2d_forward(_cl(xt.to(W.dtype)), W, b.to(W.dtype) if b is not None else None, s, pad4, d)
+
+    def activate(self, x, training=False, mask=None):
+        if x.dim() != 4:
+            raise ValueError(f"Got rank {x.dim()} array as input to ConvolutionLayer {self.layerId()}; "
+                             "expected rank 4 [minibatch, channels, height, width]")
+        if x.shape[1] != self.conf.nIn:
+            raise ValueError(f"Cannot do forward pass in Convolution layer {self.layerId()}: input depth "
+                             f"{x.shape[1]} does not match nIn {self.conf.nIn}")
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
+        self.input = x
+        z = self.preOutput(x, training)
+        self._z = z
+        return self.conf.activation.getActivation(z, training)
+
+    def backpropGradient(self, eps):
+        delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
+        s, pad4, d = self._geom_cache
+        W = self.W("W")
+        xt = _cl(self._xt.to(W.dtype))
+        dx, dW, db = ops.conv2d_backward(xt, W, _cl(delta.to(W.dtype)), s, pad4, d, True, True, "b" in self.grads)
+        copy_grad_(self.grads["W"], _acc(dW))
+        if "b" in self.grads:
+            copy_grad_(self.grads["b"], _acc(db))
+        if dx.shape[2:] != self.input.shape[2:]:
+            full = torch.zeros(self.input.shape, dtype=dx.dtype, device=dx.device)
+            full[:, :, :dx.shape[2], :dx.shape[3]] = dx
+            dx = full
+        return self.make_gradient(), self.backpropDropOut(dx)
+
+
+class Convolution1DLayerImpl(ConvolutionLayerImpl):
+    """[mb, nIn, T] -> conv over T with a [k,1] kernel."""
+
+    def activate(self, x, training=False, mask=None):
+        self._was3d = x.dim() == 3
+        x4 = x.unsqueeze(3) if x.dim() == 3 else x
+        out = super().activate(x4, training, None)
+        out = out.squeeze(3)
+        if mask is not None:
+            out = out * mask.unsqueeze(1).to(out.dtype)[:, :, :out.shape[2]]
+        return out
+
+    def backpropGradient(self, eps):
+        g, dx = super().backpropGradient(eps.unsqueeze(3))
+        return g, dx.squeeze(3)
+
+
+class Deconvolution2DImpl(ConvolutionLayerImpl):
+    def preOutput(self, x, training=False):
+        c = self.conf
+        W = self.W("W")
+        b = self.W("b").reshape(-1) if "b" in self.params else None
+        pad = [0, 0] if c.convolutionMode == ConvolutionMode.Same else c.padding
+        self._xt = x
+        out = F.conv_transpose2d(x.to(W.dtype), W, b, tuple(c.stride), tuple(pad), 0, 1, tuple(c.dilation))
+        if c.convolutionMode == ConvolutionMode.Same:
+            out = out[:, :, :x.shape[2] * c.stride[0], :x.shape[3] * c.stride[1]]
+        return out
+
+    def backpropGradient(self, eps):
+        delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
+        x = self.input.detach().to(delta.dtype).requires_grad_(True)
+        W = self.W("W").detach().requires_grad_(True)
+        b = self.W("b").detach().requires_grad_(True) if "b" in self.params else None
+        with torch.enable_grad():
+            c = self.conf
+            pad = [0, 0] if c.convolutionMode == ConvolutionMode.Same else c.padding
+            out = F.conv_transpose2d(x, W.to(delta.dtype), b.to(delta.dtype) if b is not None else None,
+                                     tuple(c.stride), tuple(pad), 0, 1, tuple(c.dilation))
+            if c.convolutionMode == ConvolutionMode.Same:
+                out = out[:, :, :x.shape[2] * c.stride[0], :x.shape[3] * c.stride[1]]
+            grads = torch.autograd.grad(out, [x, W] + ([b] if b is not None else []), delta)
+        copy_grad_(self.grads["W"], _acc(grads[1]))
+        if b is not None:
+            copy_grad_(self.grads["b"], _acc(grads[2]))
+        return self.make_gradient(), self.backpropDropOut(grads[0])
+
+
+class _AutogradConvBase(ConvolutionLayerImpl):
+    """Shared autograd-backed backward for the less common conv variants."""
+
+    def _forward_fn(self, x, P):
+        raise NotImplementedError
+
+    def preOutput(self, x, training=False):
+        P = {k: self.W(k) for k in self.params}
+        return self._forward_fn(x.to(next(iter(P.values())).dtype), P)
+
+    def backpropGradient(self, eps):
+        delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
+        x = self.input.detach().to(delta.dtype).requires_grad_(True)
+        keys = list(self.params)
+        P = {k: self.W(k).detach().to(delta.dtype).requires_grad_(True) for k in keys}
+        with torch.enable_grad():
+            out = self._forward_fn(x, P)
+            grads = torch.autograd.grad(out, [x] + [P[k] for k in keys], delta)
+        for k, g in zip(keys, grads[1:]):
+            copy_grad_(self.grads[k], _acc(g))
+        return self.make_gradient(), self.backpropDropOut(grads[0])
+
+
+class SeparableConvolution2DImpl(_AutogradConvBase):
+    def _forward_fn(self, x, P):
+        c = self.conf
+        pad4 = compute_pad4(c, x.shape[2], x.shape[3])
+        dm = c.depthMultiplier
+        C = x.shape[1]
+        wd = P["W"].permute(1, 0, 2, 3).reshape(C * dm, 1, c.kernelSize[0], c.kernelSize[1])
+        xp = F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
+        y = F.conv2d(xp, wd, None, tuple(c.stride), 0, tuple(c.dilation), groups=C)
+        y = F.conv2d(y, P["pW"], P["b"].reshape(-1) if "b" in P else None)
+        return y
+
+
+class DepthwiseConvolution2DImpl(_AutogradConvBase):
+    def _forward_fn(self, x, P):
+        c = self.conf
+        pad4 = compute_pad4(c, x.shape[2], x.shape[3])
+        dm = c.depthMultiplier
+        C = x.shape[1]
+        wd = P["W"].permute(1, 0, 2, 3).reshape(C * dm, 1, c.kernelSize[0], c.kernelSize[1])
+        xp = F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
+        return F.conv2d(xp, wd, P["b"].reshape(-1) if "b" in P else None, tuple(c.stride), 0,
+                        tuple(c.dilation), groups=C)
+
+
+class SubsamplingLayerImpl(LayerImpl):
+    def type(self):
+        return "SUBSAMPLING"
+
+    def activate(self, x, training=False, mask=None):
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
+        self.input = x
+        c = self.conf
+        pad4 = compute_pad4(c, x.shape[2], x.shape[3], c.kernelSize, c.stride, c.dilation)
+        xt = _truncate_input(c, x, c.kernelSize, c.stride, pad4, c.dilation)
+        self._xshape = x.shape
+        y, self._ctx = ops.pool2d_forward(_cl(xt), c.poolingType.value, c.kernelSize, c.stride, pad4, c.dilation,
+                                          c.pnorm, c.eps)
+        return y
+
+    def backpropGradient(self, eps):
+        dx = ops.pool2d_backward(_cl(eps), self._ctx)
+        if dx.shape[2:] != self._xshape[2:]:
+            full = torch.zeros(self._xshape, dtype=dx.dtype, device=dx.device)
+            full[:, :, :dx.shape[2], :dx.shape[3]] = dx
+            dx = full
+        return self.make_gradient(), self.backpropDropOut(dx)
+
+
+class Subsampling1DLayerImpl(SubsamplingLayerImpl):
+    def activate(self, x, training=False, mask=None):
+        out = super().activate(x.unsqueeze(3), training, None).squeeze(3)
+        if mask is not None:
+            from ..util.time_series import reverse_time_series  # noqa: F401 (keeps import graph simple)
+        return out
+
+    def backpropGradient(self, eps):
+        g, dx = super().backpropGradient(eps.unsqueeze(3))
+        return g, dx.squeeze(3)
+
+
+class ZeroPaddingLayerImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        t, b, l, r = self.conf.padding
+        self._pad = (t, b, l, r)
+        return _cl(F.pad(x, (l, r, t, b)))
+
+    def backpropGradient(self, eps):
+        t, b, l, r = self._pad
+        H, W = eps.shape[2], eps.shape[3]
+        return self.make_gradient(), eps[:, :, t:H - b, l:W - r]
+
+
+class ZeroPadding1DLayerImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        l, r = self.conf.padding
+        self._pad = (l, r)
+        return F.pad(x, (l, r))
+
+    def backpropGradient(self, eps):
+        l, r = self._pad
+        return self.make_gradient(), eps[:, :, l:eps.shape[2] - r]
+
+
+class Cropping2DImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        t, b, l, r = self.conf.cropping
+        self._shape = x.shape
+        return x[:, :, t:x.shape[2] - b, l:x.shape[3] - r]
+
+    def backpropGradient(self, eps):
+        t, b, l, r = self.conf.cropping
+        g = torch.zeros(self._shape, dtype=eps.dtype, device=eps.device)
+        g[:, :, t:self._shape[2] - b, l:self._shape[3] - r] = eps
+        return self.make_gradient(), g
+
+
+class Upsampling2DImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        s = self.conf.size
+        return x.repeat_interleave(s[0], dim=2).repeat_interleave(s[1], dim=3)
+
+    def backpropGradient(self, eps):
+        s = self.conf.size
+        n, c, h, w = eps.shape
+        return self.make_gradient(), eps.reshape(n, c, h // s[0], s[0], w // s[1], s[1]).sum(dim=(3, 5))
+
+
+class Upsampling1DImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        return x.repeat_interleave(self.conf.size[0], dim=2)
+
+    def backpropGradient(self, eps):
+        s = self.conf.size[0]
+        n, c, T = eps.shape
+        return self.make_gradient(), eps.reshape(n, c, T // s, s).sum(dim=3)
+
+
+class SpaceToDepthImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        return F.pixel_unshuffle(x, self.conf.blockSize)
+
+    def backpropGradient(self, eps):
+        return self.make_gradient(), F.pixel_shuffle(eps, self.conf.blockSize)
+
+
+class SpaceToBatchImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        (pt, pb), (pl, pr) = self.conf.padding
+        bh, bw = self.conf.blocks
+        xp = F.pad(x, (pl, pr, pt, pb))
+        n, c, H, W = xp.shape
+        self._shape = (x.shape, xp.shape)
+        y = xp.reshape(n, c, H // bh, bh, W // bw, bw).permute(3, 5, 0, 1, 2, 4)
+        return y.reshape(bh * bw * n, c, H // bh, W // bw)
+
+    def backpropGradient(self, eps):
+        (pt, pb), (pl, pr) = self.conf.padding
+        bh, bw = self.conf.blocks
+        xs, xps = self._shape
+        n, c, H, W = xps
+        g = eps.reshape(bh, bw, n, c, H // bh, W // bw).permute(2, 3, 4, 0, 5, 1).reshape(n, c, H, W)
+        return self.make_gradient(), g[:, :, pt:pt + xs[2], pl:pl + xs[3]]

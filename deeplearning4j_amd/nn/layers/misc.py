@@ -1,0 +1,83 @@
+"""Wrapper / utility runtime layers: FrozenLayer, MaskLayer, MaskZeroLayer
+(reference nn/layers/FrozenLayer.java:472, nn/layers/util/{MaskLayer,MaskZeroLayer}.java)."""
+import torch
+
+from .base import LayerImpl
+
+
+class FrozenLayerImpl(LayerImpl):
+    """Delegates forward to the wrapped layer (always in inference mode for dropout) and blocks
+    parameter gradients; epsilons still flow so earlier layers can train."""
+
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.inner = conf.underlying.instantiate(index=index, net=net)
+
+    def bind(self):
+        self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
+        self.inner.net = self.net
+
+    def getInsideLayer(self):
+        return self.inner
+
+    def activate(self, x, training=False, mask=None, **kw):
+        self.bind()
+        return self.inner.activate(x, False, mask)
+
+    def backpropGradient(self, eps, **kw):
+        self.bind()
+        saved = {k: v.clone() for k, v in self.grads.items()}
+        g, dx = self.inner.backpropGradient(eps)
+        for k, v in self.grads.items():
+            v.zero_()
+        _ = saved
+        return self.make_gradient(), dx
+
+    def __getattr__(self, name):
+        if name in ("inner",):
+            raise AttributeError(name)
+        return getattr(self.inner, name)
+
+
+class MaskLayerImpl(LayerImpl):
+    """Applies the current feature mask to activations (and to epsilons in backprop)."""
+
+    def _apply(self, x, mask):
+        if mask is None:
+            return x
+        if x.dim() == 3:
+            return x * mask.reshape(mask.shape[0], 1, -1).to(x.dtype)
+        if x.dim() == 2:
+            return x * mask.reshape(-1, 1).to(x.dtype)
+        return x * mask.reshape(mask.shape[0], 1, 1, 1).to(x.dtype)
+
+    def activate(self, x, training=False, mask=None, **kw):
+        self.maskArray = mask
+        return self._apply(x, mask)
+
+    def backpropGradient(self, eps, **kw):
+        return self.make_gradient(), self._apply(eps, self.maskArray)
+
+
+class MaskZeroLayerImpl(LayerImpl):
+    """Derives a [mb, T] mask from time steps whose features all equal maskingValue, then runs the
+    wrapped recurrent layer with that mask."""
+
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.inner = conf.underlying.instantiate(index=index, net=net)
+
+    def activate(self, x, training=False, mask=None, **kw):
+        self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
+        m = (x != self.conf.maskingValue).any(dim=1).to(x.dtype)      # [mb, T]
+        return self.inner.activate(x, training, m)
+
+    def backpropGradient(self, eps, **kw):
+        return self.inner.backpropGradient(eps)
+
+    def rnnClearPreviousState(self):
+        if hasattr(self.inner, "rnnClearPreviousState"):
+            self.inner.rnnClearPreviousState()
+
+
+_ = torch

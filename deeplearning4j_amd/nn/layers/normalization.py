@@ -1,0 +1,99 @@
+"""Normalization runtime layers: BatchNormalization (+ fused ReLU), LocalResponseNormalization,
+LayerNormalization.
+
+BatchNormalization: reference nn/layers/normalization/BatchNormalization.java (forward :250-370,
+backward :131-210; mean/var "gradients" are zero :164-167,205-208). The HIP helper
+(csrc/batchnorm.hip) does stats + normalize + affine (+ReLU when the network planner fused the
+following ActivationLayer(ReLU) into this layer) in NHWC, and the backward in two passes.
+"""
+import torch
+
+from ... import ops
+from .base import LayerImpl, copy_grad_
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+class BatchNormalizationImpl(LayerImpl):
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.fuse_relu = False
+
+    def type(self):
+        return "NORMALIZATION"
+
+    def _gb(self):
+        c = self.conf
+        if c.lockGammaBeta:
+            return c.gamma, c.beta
+        return self.params["gamma"], self.params["beta"]
+
+    def activate(self, x, training=False, mask=None):
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
+        self.input = x
+        if x.dim() not in (2, 4):
+            raise ValueError(f"BatchNormalization on activations of rank {x.dim()} not supported {self.layerId()}")
+        g, b = self._gb()
+        c = self.conf
+        # the reference BN layer applies no activation function of its own (BatchNormalization.java:225,398)
+        y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
+                                      relu=self.fuse_relu)
+        return y
+
+    def backpropGradient(self, eps):
+        dx, dgamma, dbeta = ops.bn_backward(eps, self._ctx)
+        if "gamma" in self.grads:
+            copy_grad_(self.grads["gamma"], dgamma)
+            copy_grad_(self.grads["beta"], dbeta)
+        self.grads["mean"].zero_()
+        self.grads["var"].zero_()
+        return self.make_gradient(), self.backpropDropOut(dx)
+
+
+def _is_identity(a):
+    from ..conf.activations import ActivationIdentity
+    return a is None or isinstance(a, ActivationIdentity)
+
+
+class LocalResponseNormalizationImpl(LayerImpl):
+    """Cross-channel LRN: y = x / (k + alpha * sum_{window n} x^2)^beta (reference
+    LocalResponseNormalization.java:47,187; cudnnLRNCrossChannel semantics without the /n)."""
+
+    def _fwd(self, x):
+        c = self.conf
+        half = int(c.n) // 2
+        sq = (_acc(x) ** 2)
+        pad = torch.nn.functional.pad(sq, (0, 0, 0, 0, half, half))
+        s = torch.zeros_like(sq)
+        for i in range(int(c.n)):
+            s = s + pad[:, i:i + x.shape[1]]
+        unit = c.k + c.alpha * s
+        return (_acc(x) * unit ** (-c.beta)), unit
+
+    def activate(self, x, training=False, mask=None):
+        self.input = x
+        y, self._unit = self._fwd(x)
+        return y.to(x.dtype)
+
+    def backpropGradient(self, eps):
+        x = _acc(self.input.detach()).requires_grad_(True)
+        with torch.enable_grad():
+            y, _ = self._fwd(x)
+            (dx,) = torch.autograd.grad(y, [x], _acc(eps))
+        return self.make_gradient(), dx.to(eps.dtype)
+
+
+class LayerNormalizationImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None):
+        self.input = x
+        y, self._ctx = ops.layer_norm_forward(x, self.params["gamma"], self.params["beta"], self.conf.eps)
+        self._pre = y
+        return self.conf.activation.getActivation(y, training) if not _is_identity(self.conf.activation) else y
+
+    def backpropGradient(self, eps):
+        if not _is_identity(self.conf.activation):
+            eps = self.conf.activation.backprop(self._pre, eps)
+        dx, dg, db = ops.layer_norm_backward(eps, self._ctx)
+        copy_grad_(self.grads["gamma"], dg)
+        copy_grad_(self.grads["beta"], db)
+        return self.make_gradient(), dx

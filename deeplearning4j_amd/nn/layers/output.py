@@ -1,0 +1,220 @@
+"""Output / loss layers (reference nn/layers/BaseOutputLayer.java:82-92,147-178, LossLayer.java,
+RnnOutputLayer, RnnLossLayer, CnnLossLayer, CenterLossOutputLayer).
+
+score = (sum_examples loss + fullNetworkL1 + fullNetworkL2) / minibatch  (BaseOutputLayer.computeScore)
+MCXENT/NLL + softmax goes through the fused softmax-cross-entropy kernel (ops.softmax_xent).
+"""
+import torch
+
+from ...ops import softmax_xent
+from ..conf.activations import ActivationSoftmax
+from ..conf.losses import LossMCXENT
+from .base import LayerImpl, add_row, copy_grad_
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+def _rnn_to_2d(x):
+    mb, n, T = x.shape
+    return x.permute(2, 0, 1).reshape(T * mb, n)
+
+
+def _2d_to_rnn(x, mb):
+    n = x.shape[1]
+    T = x.shape[0] // mb
+    return x.reshape(T, mb, n).permute(1, 2, 0)
+
+
+def _mask_rnn_to_2d(mask):
+    if mask is None:
+        return None
+    return mask.t().reshape(-1, 1) if mask.dim() == 2 else mask
+
+
+class BaseOutputLayerImpl(LayerImpl):
+    has_params = True
+
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.labels = None
+
+    def setLabels(self, labels):
+        self.labels = labels
+
+    def getLabels(self):
+        return self.labels
+
+    def _fused(self):
+        return isinstance(self.conf.lossFn, LossMCXENT) and isinstance(self.conf.activation, ActivationSoftmax) \
+            and self.conf.lossFn.weights is None
+
+    def preOutput2d(self, x):
+        if not self.has_params:
+            return x
+        W = self.W("W")
+        z = torch.matmul(x.to(W.dtype), W)
+        if "b" in self.params:
+            z = add_row(z, self.W("b"))
+        return z
+
+    # 2d views of input / labels / mask -------------------------------------------------------
+    def _in2d(self, x):
+        return x
+
+    def _lab2d(self, y):
+        return y
+
+    def _mask2d(self, m):
+        return m
+
+    def _out_from2d(self, a):
+        return a
+
+    def activate(self, x, training=False, mask=None):
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
+        self.input = x
+        self.maskArray = mask
+        x2 = self._in2d(x)
+        self._x2 = x2
+        z = self.preOutput2d(x2)
+        self._z = z
+        self._cache = None
+        return self._out_from2d(self.conf.activation.getActivation(z, training))
+
+    def output(self, x, training=False):
+        return self.activate(x, training)
+
+    def _loss_and_grad(self):
+        if self._cache is not None:
+            return self._cache
+        y = self._lab2d(self.labels)
+        mask = self._mask2d(self.maskArray)
+        if self._fused():
+            s, g, _ = softmax_xent(self._z, y.to(self._z.device), mask, self.conf.lossFn.softmaxClipEps)
+        else:
+            s = self.conf.lossFn.computeScoreArray(y, self._z, self.conf.activation, mask)
+            g = self.conf.lossFn.computeGradient(y, self._z, self.conf.activation, mask)
+        self._cache = (s, g)
+        return self._cache
+
+    def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
+        s, _ = self._loss_and_grad()
+        mb = self.input.shape[0]
+        return (s.sum() + fullNetworkL1 + fullNetworkL2) / mb
+
+    def computeScoreForExamples(self, fullNetworkL1=0.0, fullNetworkL2=0.0):
+        s, _ = self._loss_and_grad()
+        return s + (fullNetworkL1 + fullNetworkL2)
+
+    def backpropGradient(self, eps=None):
+        _, delta = self._loss_and_grad()
+        if self.has_params:
+            x = self._x2.to(delta.dtype)
+            copy_grad_(self.grads["W"], _acc(torch.matmul(x.t(), delta)))
+            if "b" in self.grads:
+                copy_grad_(self.grads["b"], _acc(delta).sum(dim=0))
+            W = self.W("W")
+            eps2 = torch.matmul(delta.to(W.dtype), W.t())
+        else:
+            eps2 = delta
+        return self.make_gradient(), self.backpropDropOut(self._eps_from2d(eps2))
+
+    def _eps_from2d(self, e):
+        return e
+
+    def clear(self):
+        super().clear()
+        self.labels = None
+        self._cache = None
+
+
+class OutputLayerImpl(BaseOutputLayerImpl):
+    pass
+
+
+class LossLayerImpl(BaseOutputLayerImpl):
+    has_params = False
+
+
+class RnnOutputLayerImpl(BaseOutputLayerImpl):
+    def _in2d(self, x):
+        self._mb = x.shape[0]
+        return _rnn_to_2d(x) if x.dim() == 3 else x
+
+    def _lab2d(self, y):
+        return _rnn_to_2d(y) if y.dim() == 3 else y
+
+    def _mask2d(self, m):
+        return _mask_rnn_to_2d(m)
+
+    def _out_from2d(self, a):
+        return _2d_to_rnn(a, self._mb) if self.input.dim() == 3 else a
+
+    def _eps_from2d(self, e):
+        return _2d_to_rnn(e, self._mb) if self.input.dim() == 3 else e
+
+    def computeScoreForExamples(self, fullNetworkL1=0.0, fullNetworkL2=0.0):
+        s, _ = self._loss_and_grad()
+        if self.input.dim() == 3:
+            s = s.reshape(-1, self._mb).sum(dim=0)
+        return s + (fullNetworkL1 + fullNetworkL2)
+
+
+class RnnLossLayerImpl(RnnOutputLayerImpl):
+    has_params = False
+
+
+class CnnLossLayerImpl(BaseOutputLayerImpl):
+    has_params = False
+
+    def _in2d(self, x):
+        self._shape = x.shape
+        return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
+    def _lab2d(self, y):
+        return y.permute(0, 2, 3, 1).reshape(-1, y.shape[1])
+
+    def _mask2d(self, m):
+        if m is None:
+            return None
+        return m.reshape(-1, 1) if m.dim() == 3 or (m.dim() == 4 and m.shape[1] == 1) else m.permute(
+            0, 2, 3, 1).reshape(-1, m.shape[1])
+
+    def _out_from2d(self, a):
+        n, c, h, w = self._shape
+        return a.reshape(n, h, w, c).permute(0, 3, 1, 2)
+
+    def _eps_from2d(self, e):
+        return self._out_from2d(e)
+
+    def computeScoreForExamples(self, fullNetworkL1=0.0, fullNetworkL2=0.0):
+        s, _ = self._loss_and_grad()
+        n = self._shape[0]
+        return s.reshape(n, -1).sum(dim=1) + (fullNetworkL1 + fullNetworkL2)
+
+
+class CenterLossOutputLayerImpl(BaseOutputLayerImpl):
+    """Adds lambda/2 * ||x - c_y||^2 to the score; centers move toward class means with rate alpha."""
+
+    def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
+        base = super().computeScore(fullNetworkL1, fullNetworkL2, training)
+        c = self.params["cL"]
+        y = _acc(self.labels)
+        centers = y @ _acc(c)
+        d = _acc(self._x2) - centers
+        return base + 0.5 * self.conf.lambda_ * (d * d).sum() / self.input.shape[0]
+
+    def backpropGradient(self, eps=None):
+        g, eps_prev = super().backpropGradient(eps)
+        c = self.params["cL"]
+        y = _acc(self.labels)
+        x = _acc(self._x2)
+        d = x - y @ _acc(c)
+        eps_prev = eps_prev + (self.conf.lambda_ * d).to(eps_prev.dtype)
+        with torch.no_grad():
+            counts = y.sum(dim=0).clamp(min=1).reshape(-1, 1)
+            delta_c = (y.t() @ (-d)) / (counts + 1)
+            c.sub_((self.conf.alpha * delta_c).to(c.dtype))
+        if "cL" in self.grads:
+            self.grads["cL"].zero_()
+        return g, eps_prev

@@ -1,0 +1,80 @@
+"""GlobalPoolingLayer: masked MAX/AVG/SUM/PNORM over time (RNN) or space (CNN)
+(reference nn/layers/pooling/GlobalPoolingLayer.java, nn/util/MaskedReductionUtil.java:39-53)."""
+import torch
+
+from ..conf.enums import PoolingType
+from .base import LayerImpl
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+class GlobalPoolingLayerImpl(LayerImpl):
+    def _dims(self, x):
+        if self.conf.poolingDimensions:
+            return tuple(self.conf.poolingDimensions)
+        return (2,) if x.dim() == 3 else (2, 3)
+
+    def activate(self, x, training=False, mask=None):
+        self.input = x
+        dims = self._dims(x)
+        pt = self.conf.poolingType
+        xf = _acc(x)
+        m = None
+        if mask is not None and x.dim() == 3:
+            m = _acc(mask).unsqueeze(1)                                  # [mb,1,T]
+        self._mask = m
+        if pt == PoolingType.MAX:
+            xm = xf if m is None else xf.masked_fill(m == 0, float("-inf"))
+            out = xm.amax(dim=dims, keepdim=True)
+            self._argmask = (xm == out)
+            cnt = self._argmask.sum(dim=dims, keepdim=True).clamp(min=1)
+            self._argmask = _acc(self._argmask) / cnt
+        elif pt == PoolingType.AVG:
+            if m is None:
+                out = xf.mean(dim=dims, keepdim=True)
+                self._n = 1
+                for d in dims:
+                    self._n *= x.shape[d]
+            else:
+                self._n = m.sum(dim=dims, keepdim=True).clamp(min=1)
+                out = (xf * m).sum(dim=dims, keepdim=True) / self._n
+        elif pt == PoolingType.SUM:
+            out = (xf if m is None else xf * m).sum(dim=dims, keepdim=True)
+        elif pt == PoolingType.PNORM:
+            p = self.conf.pnorm
+            xa = torch.abs(xf) ** p
+            if m is not None:
+                xa = xa * m
+            out = xa.sum(dim=dims, keepdim=True) ** (1.0 / p)
+            self._pn = out
+        else:
+            raise ValueError(pt)
+        self._keep_shape = out.shape
+        if self.conf.collapseDimensions:
+            out = out.reshape(out.shape[0], out.shape[1])
+        return out.to(x.dtype)
+
+    def backpropGradient(self, eps):
+        x = self.input
+        e = _acc(eps).reshape(self._keep_shape)
+        pt = self.conf.poolingType
+        if pt == PoolingType.MAX:
+            g = e * self._argmask
+        elif pt == PoolingType.AVG:
+            g = (e / self._n).expand(x.shape).clone()
+            if self._mask is not None:
+                g = g * self._mask
+        elif pt == PoolingType.SUM:
+            g = e.expand(x.shape).clone()
+            if self._mask is not None:
+                g = g * self._mask
+        else:
+            p = self.conf.pnorm
+            xf = _acc(x)
+            g = e * torch.abs(xf) ** (p - 1) * torch.sign(xf) * torch.clamp(self._pn, min=1e-12) ** (1 - p)
+            if self._mask is not None:
+                g = g * self._mask
+        return self.make_gradient(), g.to(eps.dtype)
+
+    def feedForwardMaskArray(self, mask, state, mb):
+        self.maskArray = mask
+        return None, state

@@ -1,0 +1,404 @@
+"""Recurrent runtime layers: LSTM, GravesLSTM (peepholes), GravesBidirectionalLSTM, SimpleRnn,
+Bidirectional, LastTimeStep.
+
+LSTM math = reference nn/layers/recurrent/LSTMHelpers.java (forward :189-358, backward :392-690):
+gate blocks in the 4H axis are [a (cell input, layer activation) | f (forget) | o (output) |
+g (input-modulation)], peepholes (Graves) are RW columns 4H (wFF), 4H+1 (wOO), 4H+2 (wGG):
+    a = act(z_a); f = gate(z_f + wFF*c_prev); g = gate(z_g + wGG*c_prev)
+    c = f*c_prev + g*a; o = gate(z_o + wOO*c); h = o*act(c)
+MI355X structure: ONE big input-projection GEMM for all T steps ([T*mb, nIn] x [nIn, 4H]), then the
+recurrent loop does one [mb,H]x[H,4H] GEMM + the fused gate kernel per step (csrc/lstm.hip on GPU);
+backward accumulates dW, dRW and dX as single big GEMMs after the time loop. TBPTT stops the
+backward time loop at ``tbpttBackLength`` steps (LSTMHelpers.java:484).
+"""
+import torch
+
+from ... import ops
+from ..conf.activations import ActivationSigmoid, ActivationTanH
+from .base import LayerImpl, copy_grad_
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc, acc_dtype  # noqa: E402
+
+
+def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache):
+    """x: [mb, nIn, T]. Returns out [mb, H, T], (hT, cT), cache."""
+    mb, nIn, T = x.shape
+    dt = W.dtype
+    _adt = acc_dtype(W)
+    xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
+    zx = (xt @ W + b.reshape(1, -1).to(dt)).reshape(T, mb, 4 * H)          # input projection, all steps
+    RWg = RW[:, :4 * H]
+    if peephole:
+        wFF, wOO, wGG = _acc(RW[:, 4 * H]), _acc(RW[:, 4 * H + 1]), _acc(RW[:, 4 * H + 2])
+    h = torch.zeros(mb, H, dtype=_adt, device=x.device) if h0 is None else _acc(h0)
+    c = torch.zeros(mb, H, dtype=_adt, device=x.device) if c0 is None else _acc(c0)
+    outs = []
+    cache = {"z": [], "a": [], "f": [], "g": [], "o": [], "c": [], "c_prev": [], "h_prev": [], "cact": []} \
+        if need_cache else None
+    std = isinstance(act, ActivationTanH) and isinstance(gate_act, ActivationSigmoid)
+    for t in range(T):
+        z = _acc(zx[t]) + _acc((h.to(dt) @ RWg))
+        if std and not peephole and not need_cache and z.is_cuda and _native_cell(z):
+            from ...ops import native
+            h_new, c_new = native.lstm_cell_fwd(z, c)
+            a = f = g = o = cact = None
+        else:
+            za, zf, zo, zg = z[:, :H], z[:, H:2 * H], z[:, 2 * H:3 * H], z[:, 3 * H:]
+            if peephole:
+                zf = zf + c * wFF
+                zg = zg + c * wGG
+            a = act.getActivation(za, True)
+            f = gate_act.getActivation(zf, True)
+            g = gate_act.getActivation(zg, True)
+            c_new = f * c + g * a
+            if peephole:
+                zo = zo + c_new * wOO
+            o = gate_act.getActivation(zo, True)
+            cact = act.getActivation(c_new, True)
+            h_new = o * cact
+            z = torch.cat([za, zf, zo, zg], dim=1)
+        if mask is not None:
+            m = _acc(mask[:, t]).reshape(-1, 1)
+            h_new = h_new * m
+            c_new = c_new * m
+        if need_cache:
+            cache["z"].append(z)
+            cache["a"].append(a)
+            cache["f"].append(f)
+            cache["g"].append(g)
+            cache["o"].append(o)
+            cache["c"].append(c_new)
+            cache["c_prev"].append(c)
+            cache["h_prev"].append(h)
+            cache["cact"].append(cact)
+        h, c = h_new, c_new
+        outs.append(h)
+    out = torch.stack(outs, dim=2).to(x.dtype if x.is_floating_point() else dt)
+    if need_cache:
+        cache["xt"] = xt
+    return out, (h, c), cache
+
+
+def _lstm_bwd(eps, cache, W, RW, H, peephole, act, gate_act, mask, tbptt_back, grads_prefix, grads, dh_last=None,
+              dc_last=None):
+    """eps: [mb, H, T]. Writes dW/dRW/db into grads views; returns eps_in [mb, nIn, T]."""
+    mb, _, T = eps.shape
+    dt = W.dtype
+    _adt = acc_dtype(W)
+    RWg = _acc(RW[:, :4 * H])
+    if peephole:
+        wFF, wOO, wGG = _acc(RW[:, 4 * H]), _acc(RW[:, 4 * H + 1]), _acc(RW[:, 4 * H + 2])
+        dwFF = torch.zeros(H, device=eps.device, dtype=_adt)
+        dwOO = torch.zeros(H, device=eps.device, dtype=_adt)
+        dwGG = torch.zeros(H, device=eps.device, dtype=_adt)
+    dh_next = torch.zeros(mb, H, device=eps.device, dtype=_adt) if dh_last is None else _acc(dh_last)
+    dc_next = torch.zeros(mb, H, device=eps.device, dtype=_adt) if dc_last is None else _acc(dc_last)
+    dz_all = torch.zeros(T, mb, 4 * H, device=eps.device, dtype=_adt)
+    t_end = max(0, T - tbptt_back) if tbptt_back else 0
+    e = _acc(eps)
+    for t in range(T - 1, t_end - 1, -1):
+        dh = e[:, :, t] + dh_next
+        dc = dc_next
+        if mask is not None:
+            m = _acc(mask[:, t]).reshape(-1, 1)
+            dh = dh * m
+            dc = dc * m
+        z = cache["z"][t]
+        a, f, g, o = cache["a"][t], cache["f"][t], cache["g"][t], cache["o"][t]
+        c, c_prev, cact = cache["c"][t], cache["c_prev"][t], cache["cact"][t]
+        za, zf, zo, zg = z[:, :H], z[:, H:2 * H], z[:, 2 * H:3 * H], z[:, 3 * H:]
+        do = dh * cact
+        dzo = gate_act.backprop(zo, do)
+        dc = dc + act.backprop(c, dh * o)
+        if peephole:
+            dc = dc + dzo * wOO
+        dzf = gate_act.backprop(zf, dc * c_prev)
+        dzg = gate_act.backprop(zg, dc * a)
+        dza = act.backprop(za, dc * g)
+        dc_next = dc * f
+        if peephole:
+            dc_next = dc_next + dzf * wFF + dzg * wGG
+            dwFF += (dzf * c_prev).sum(dim=0)
+            dwGG += (dzg * c_prev).sum(dim=0)
+            dwOO += (dzo * c).sum(dim=0)
+        dz = torch.cat([dza, dzf, dzo, dzg], dim=1)
+        dz_all[t] = dz
+        dh_next = dz @ RWg.t()
+    hprev = torch.stack(cache["h_prev"], 0)                       # [T, mb, H]
+    dzf2 = dz_all.reshape(T * mb, 4 * H)
+    gW = grads[grads_prefix + "W"]
+    gRW = grads[grads_prefix + "RW"]
+    gb = grads[grads_prefix + "b"]
+    copy_grad_(gW, _acc(cache["xt"]).t() @ dzf2)
+    dRW = hprev.reshape(T * mb, H).t() @ dzf2
+    if peephole:
+        dRW = torch.cat([dRW, dwFF.reshape(-1, 1), dwOO.reshape(-1, 1), dwGG.reshape(-1, 1)], dim=1)
+    copy_grad_(gRW, dRW)
+    copy_grad_(gb, dzf2.sum(dim=0))
+    dx = (dzf2.to(dt) @ W.t()).reshape(T, mb, -1).permute(1, 2, 0)
+    return dx, dh_next, dc_next
+
+
+def _native_cell(z):
+    from ...ops import rnn_native
+    return rnn_native.available and ops.use_native(z, "lstm")
+
+
+class BaseRecurrentImpl(LayerImpl):
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.stateMap = {}
+        self.tBpttStateMap = {}
+
+    def type(self):
+        return "RECURRENT"
+
+    def rnnClearPreviousState(self):
+        self.stateMap = {}
+        self.tBpttStateMap = {}
+
+    def rnnGetPreviousState(self):
+        return dict(self.stateMap)
+
+    def rnnSetPreviousState(self, s):
+        self.stateMap = dict(s)
+
+    def rnnGetTBPTTState(self):
+        return dict(self.tBpttStateMap)
+
+    def rnnSetTBPTTState(self, s):
+        self.tBpttStateMap = dict(s)
+
+
+class LSTMImpl(BaseRecurrentImpl):
+    PEEPHOLE = False
+
+    def _run(self, x, training, h0, c0, need_cache, mask):
+        H = self.conf.nOut
+        return _lstm_fwd(x, self.W("W"), self.W("RW"), self.W("b"), h0, c0, H, self.PEEPHOLE, self.conf.activation,
+                         self.conf.gateActivationFn, mask, need_cache)
+
+    def activate(self, x, training=False, mask=None, stored_state=False, store_last_for_tbptt=False):
+        if x.dim() == 2:
+            x = x.unsqueeze(2)
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
+        self.input = x
+        self.maskArray = mask
+        h0 = c0 = None
+        if stored_state:
+            h0, c0 = self.tBpttStateMap.get("prevAct"), self.tBpttStateMap.get("prevMem")
+        out, (h, c), cache = self._run(x, training, h0, c0, training, mask)
+        self._cache = cache
+        if store_last_for_tbptt:
+            self.tBpttStateMap = {"prevAct": h.detach(), "prevMem": c.detach()}
+        return out
+
+    def rnnTimeStep(self, x, mask=None):
+        is2d = x.dim() == 2
+        if is2d:
+            x = x.unsqueeze(2)
+        out, (h, c), _ = self._run(x, False, self.stateMap.get("prevAct"), self.stateMap.get("prevMem"), False, mask)
+        self.stateMap = {"prevAct": h, "prevMem": c}
+        return out[:, :, 0] if is2d else out
+
+    def backpropGradient(self, eps, tbptt_back=None):
+        if eps.dim() == 2:
+            eps = eps.unsqueeze(2)
+        H = self.conf.nOut
+        dx, _, _ = _lstm_bwd(eps, self._cache, self.W("W"), self.W("RW"), H, self.PEEPHOLE, self.conf.activation,
+                             self.conf.gateActivationFn, self.maskArray, tbptt_back, "", self.grads)
+        return self.make_gradient(), self.backpropDropOut(dx.to(eps.dtype))
+
+
+class GravesLSTMImpl(LSTMImpl):
+    PEEPHOLE = True
+
+
+class GravesBidirectionalLSTMImpl(BaseRecurrentImpl):
+    def activate(self, x, training=False, mask=None, **kw):
+        from ..util.time_series import reverse_time_series
+        self.training = training
+        self.input = x
+        self.maskArray = mask
+        H = self.conf.nOut
+        a, ga = self.conf.activation, self.conf.gateActivationFn
+        fw, _, self._cf = _lstm_fwd(x, self.W("WF"), self.W("RWF"), self.W("bF"), None, None, H, True, a, ga, mask,
+                                    training)
+        xr = reverse_time_series(x, mask)
+        mr = reverse_time_series(mask, mask) if mask is not None else None
+        bw, _, self._cb = _lstm_fwd(xr, self.W("WB"), self.W("RWB"), self.W("bB"), None, None, H, True, a, ga, mr,
+                                    training)
+        self._mr = mr
+        return fw + reverse_time_series(bw, mask)
+
+    def backpropGradient(self, eps, tbptt_back=None):
+        from ..util.time_series import reverse_time_series
+        H = self.conf.nOut
+        a, ga = self.conf.activation, self.conf.gateActivationFn
+        dxf, _, _ = _lstm_bwd(eps, self._cf, self.W("WF"), self.W("RWF"), H, True, a, ga, self.maskArray, tbptt_back,
+                              "", {"W": self.grads["WF"], "RW": self.grads["RWF"], "b": self.grads["bF"]})
+        er = reverse_time_series(eps, self.maskArray)
+        dxb, _, _ = _lstm_bwd(er, self._cb, self.W("WB"), self.W("RWB"), H, True, a, ga, self._mr, tbptt_back, "",
+                              {"W": self.grads["WB"], "RW": self.grads["RWB"], "b": self.grads["bB"]})
+        return self.make_gradient(), (dxf + reverse_time_series(dxb, self.maskArray)).to(eps.dtype)
+
+    def rnnTimeStep(self, x, mask=None):
+        raise NotImplementedError("GravesBidirectionalLSTM does not support rnnTimeStep (needs the full sequence)")
+
+
+class SimpleRnnImpl(BaseRecurrentImpl):
+    def _fwd(self, x, h0, mask, need_cache):
+        mb, nIn, T = x.shape
+        _adt = acc_dtype(self.W("W"))
+        W, RW, b = self.W("W"), self.W("RW"), self.W("b")
+        dt = W.dtype
+        xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
+        zx = (xt @ W + b.reshape(1, -1).to(dt)).reshape(T, mb, -1)
+        h = torch.zeros(mb, self.conf.nOut, device=x.device, dtype=_adt) if h0 is None else _acc(h0)
+        zs, hs, outs = [], [], []
+        for t in range(T):
+            z = _acc(zx[t]) + _acc((h.to(dt) @ RW))
+            hn = self.conf.activation.getActivation(z, True)
+            if mask is not None:
+                hn = hn * _acc(mask[:, t]).reshape(-1, 1)
+            zs.append(z)
+            hs.append(h)
+            h = hn
+            outs.append(h)
+        self._c = {"z": zs, "hprev": hs, "xt": xt} if need_cache else None
+        return torch.stack(outs, 2).to(x.dtype), h
+
+    def activate(self, x, training=False, mask=None, stored_state=False, store_last_for_tbptt=False):
+        if x.dim() == 2:
+            x = x.unsqueeze(2)
+        self.input = x
+        self.maskArray = mask
+        h0 = self.tBpttStateMap.get("prevAct") if stored_state else None
+        out, h = self._fwd(x, h0, mask, training)
+        if store_last_for_tbptt:
+            self.tBpttStateMap = {"prevAct": h.detach()}
+        return out
+
+    def rnnTimeStep(self, x, mask=None):
+        is2d = x.dim() == 2
+        if is2d:
+            x = x.unsqueeze(2)
+        out, h = self._fwd(x, self.stateMap.get("prevAct"), mask, False)
+        self.stateMap = {"prevAct": h}
+        return out[:, :, 0] if is2d else out
+
+    def backpropGradient(self, eps, tbptt_back=None):
+        mb, H, T = eps.shape
+        _adt = acc_dtype(self.W("W"))
+        RW = _acc(self.W("RW"))
+        c = self._c
+        dh_next = torch.zeros(mb, H, device=eps.device, dtype=_adt)
+        dz_all = torch.zeros(T, mb, H, device=eps.device, dtype=_adt)
+        t_end = max(0, T - tbptt_back) if tbptt_back else 0
+        for t in range(T - 1, t_end - 1, -1):
+            dh = _acc(eps[:, :, t]) + dh_next
+            if self.maskArray is not None:
+                dh = dh * _acc(self.maskArray[:, t]).reshape(-1, 1)
+            dz = self.conf.activation.backprop(c["z"][t], dh)
+            dz_all[t] = dz
+            dh_next = dz @ RW.t()
+        dzf = dz_all.reshape(T * mb, H)
+        copy_grad_(self.grads["W"], _acc(c["xt"]).t() @ dzf)
+        copy_grad_(self.grads["RW"], torch.stack(c["hprev"], 0).reshape(T * mb, H).t() @ dzf)
+        copy_grad_(self.grads["b"], dzf.sum(0))
+        dx = (dzf.to(self.W("W").dtype) @ self.W("W").t()).reshape(T, mb, -1).permute(1, 2, 0)
+        return self.make_gradient(), dx.to(eps.dtype)
+
+
+class _SubView(LayerImpl):
+    """A child layer sharing a prefix-filtered view of the parent's params/grads."""
+
+
+class BidirectionalImpl(BaseRecurrentImpl):
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.fwd = conf.underlying.instantiate(index=index, net=net)
+        self.bwd = conf.underlying.instantiate(index=index, net=net)
+
+    def bind(self):
+        for d, layer in (("f", self.fwd), ("b", self.bwd)):
+            layer.params = {k[1:]: v for k, v in self.params.items() if k.startswith(d)}
+            layer.cparams = {k[1:]: v for k, v in self.cparams.items() if k.startswith(d)}
+            layer.grads = {k[1:]: v for k, v in self.grads.items() if k.startswith(d)}
+
+    def activate(self, x, training=False, mask=None, **kw):
+        from ..util.time_series import reverse_time_series
+        self.bind()
+        self.maskArray = mask
+        of = self.fwd.activate(x, training, mask)
+        xr = reverse_time_series(x, mask)
+        ob = reverse_time_series(self.bwd.activate(xr, training, reverse_time_series(mask, mask) if mask is not None
+                                                   else None), mask)
+        self._of, self._ob = of, ob
+        m = self.conf.mode.upper()
+        if m == "CONCAT":
+            return torch.cat([of, ob], dim=1)
+        if m == "ADD":
+            return of + ob
+        if m == "MUL":
+            return of * ob
+        if m == "AVERAGE":
+            return (of + ob) / 2
+        raise ValueError(m)
+
+    def backpropGradient(self, eps, tbptt_back=None):
+        from ..util.time_series import reverse_time_series
+        m = self.conf.mode.upper()
+        if m == "CONCAT":
+            n = self._of.shape[1]
+            ef, eb = eps[:, :n], eps[:, n:]
+        elif m == "ADD":
+            ef = eb = eps
+        elif m == "MUL":
+            ef, eb = eps * self._ob, eps * self._of
+        else:
+            ef = eb = eps / 2
+        _, dxf = self.fwd.backpropGradient(ef)
+        _, dxb = self.bwd.backpropGradient(reverse_time_series(eb, self.maskArray))
+        return self.make_gradient(), dxf + reverse_time_series(dxb, self.maskArray)
+
+    def rnnClearPreviousState(self):
+        self.fwd.rnnClearPreviousState() if hasattr(self.fwd, "rnnClearPreviousState") else None
+        self.bwd.rnnClearPreviousState() if hasattr(self.bwd, "rnnClearPreviousState") else None
+
+
+class LastTimeStepImpl(LayerImpl):
+    def __init__(self, conf, index=0, net=None):
+        super().__init__(conf, index, net)
+        self.inner = conf.underlying.instantiate(index=index, net=net)
+
+    def bind(self):
+        self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
+
+    def activate(self, x, training=False, mask=None, **kw):
+        from ..util.time_series import last_time_step
+        self.bind()
+        out = self.inner.activate(x, training, mask)
+        self._shape = out.shape
+        self.maskArray = mask
+        if mask is None:
+            self._idx = None
+            return out[:, :, -1]
+        self._idx = mask.reshape(mask.shape[0], -1).sum(dim=1).long().clamp(min=1) - 1
+        return last_time_step(out, mask)
+
+    def backpropGradient(self, eps, tbptt_back=None):
+        g = torch.zeros(self._shape, dtype=eps.dtype, device=eps.device)
+        if self._idx is None:
+            g[:, :, -1] = eps
+        else:
+            g[torch.arange(self._shape[0], device=eps.device), :, self._idx] = eps
+        return self.inner.backpropGradient(g)
+
+    def feedForwardMaskArray(self, mask, state, mb):
+        self.maskArray = mask
+        return None, state
+
+    def rnnClearPreviousState(self):
+        if hasattr(self.inner, "rnnClearPreviousState"):
+            self.inner.rnnClearPreviousState()

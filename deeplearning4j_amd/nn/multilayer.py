@@ -1,0 +1,382 @@
+"""MultiLayerNetwork: sequential model (reference nn/multilayer/MultiLayerNetwork.java, 3545 LoC).
+
+init (:549-663) -> flat params/gradients + per-layer views, updater blocks;
+fit (:1268-1360) -> per minibatch: forward (feedForwardToLayer :955-1041), backward
+(calcBackpropGradients :1378-1519), score, fused update; TBPTT (doTruncatedBPTT :1521-1593);
+output (:2031), rnnTimeStep (:2806), evaluate (:2985-3057).
+"""
+import torch
+
+from ..datasets.dataset import DataSet, DataSetIterator
+from .conf.enums import BackpropType
+from .conf.layers import ActivationLayer, BatchNormalization
+from .layers.output import BaseOutputLayerImpl
+from .network_base import BaseNetwork
+
+
+class MultiLayerNetwork(BaseNetwork):
+    _key_by_name = False
+
+    def __init__(self, conf, params=None):
+        super().__init__(conf)
+        self.layers = []
+        self._init_params = params
+        self.input = None
+        self.labels = None
+        self.mask = None
+        self.labelsMask = None
+
+    # ------------------------------------------------------------------------------ init
+    def init(self, parameters=None, cloneParametersArray=False, device=None):
+        if self.initCalled and parameters is None:
+            return
+        parameters = parameters if parameters is not None else self._init_params
+        self.layers = [c.instantiate(index=i, net=self) for i, c in enumerate(self.conf.confs)]
+        self._setup_flat([(i, self.conf.confs[i].layerName, l) for i, l in enumerate(self.layers)], parameters,
+                         cloneParametersArray, device)
+        self._plan_fusions()
+        for l in self.layers:
+            if hasattr(l, "bind"):
+                l.bind()
+
+    def _plan_fusions(self):
+        """BN -> ActivationLayer(ReLU): run the ReLU inside the BN kernel (forward and backward)."""
+        from .conf.activations import ActivationReLU
+        self._fused_passthrough = set()
+        for i in range(len(self.layers) - 1):
+            a, b = self.conf.confs[i], self.conf.confs[i + 1]
+            if isinstance(a, BatchNormalization) and isinstance(b, ActivationLayer) and \
+                    isinstance(b.activation, ActivationReLU) and (i + 1) not in self.conf.inputPreProcessors \
+                    and b.idropout is None:
+                if a.idropout is None:
+                    self.layers[i].fuse_relu = True
+                    self._fused_passthrough.add(i + 1)
+
+    def getLayers(self):
+        return self.layers
+
+    def getLayer(self, i):
+        if isinstance(i, str):
+            for l in self.layers:
+                if l.conf.layerName == i:
+                    return l
+            raise KeyError(i)
+        return self.layers[i]
+
+    def getnLayers(self):
+        return len(self.layers)
+
+    def getOutputLayer(self):
+        return self.layers[-1]
+
+    def getLayerWiseConfigurations(self):
+        return self.conf
+
+    # ------------------------------------------------------------------------------ forward
+    def _pp(self, i, x, mb, training):
+        pp = self.conf.inputPreProcessors.get(i)
+        return pp.preProcess(x, mb, training) if pp is not None else x
+
+    def _mask_for(self, i, mask, mb):
+        pp = self.conf.inputPreProcessors.get(i)
+        if pp is not None and mask is not None:
+            mask, _ = pp.feedForwardMaskArray(mask, None, mb)
+        return mask
+
+    def feedForwardToLayer(self, layerNum, x, train=False, fmask=None, stored_state=False,
+                           store_last_for_tbptt=False):
+        """Activations of layers 0..layerNum (inclusive); index 0 of the returned list is the input."""
+        x = self._to_dev(x, self._feat_dtype()) if x.is_floating_point() else self._to_dev(x)
+        mb = x.shape[0]
+        acts = [x]
+        mask = fmask
+        for i in range(layerNum + 1):
+            layer = self.layers[i]
+            x = self._pp(i, x, mb, train)
+            mask = self._mask_for(i, mask, mb)
+            if i in self._fused_passthrough:
+                acts.append(x)
+                continue
+            layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
+            if stored_state and hasattr(layer, "tBpttStateMap"):
+                x = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
+            else:
+                x = layer.activate(x, train, mask)
+            mask, _ = layer.feedForwardMaskArray(mask, None, mb)
+            acts.append(x)
+        return acts
+
+    def feedForward(self, x=None, train=False, fmask=None):
+        x = self.input if x is None else x
+        acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, fmask)
+        for l in self.listeners:
+            if hasattr(l, "onForwardPass"):
+                l.onForwardPass(self, acts)
+        return acts
+
+    def output(self, x, train=False, featuresMask=None, labelsMask=None):
+        if isinstance(x, DataSetIterator):
+            return [self.output(ds.features, train, ds.featuresMask) for ds in x]
+        with torch.no_grad():
+            acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, featuresMask)
+        out = acts[-1]
+        return out.float() if out.is_floating_point() else out
+
+    def activate(self, x, train=False):
+        return self.output(x, train)
+
+    def predict(self, x):
+        return torch.argmax(self.output(x), dim=1)
+
+    def labelProbabilities(self, x):
+        return self.output(x)
+
+    # ------------------------------------------------------------------------------ backward
+    def _backprop(self, tbptt_back=None):
+        """Reverse pass from the output layer; gradients land in the flat gradient views."""
+        n = len(self.layers)
+        out_layer = self.layers[-1]
+        if not isinstance(out_layer, BaseOutputLayerImpl):
+            raise ValueError("Cannot calculate gradient and score with respect to labels: final layer is not an "
+                             "IOutputLayer")
+        self._begin_backward()
+        _, eps = out_layer.backpropGradient(None)
+        self._grad_ready(n - 1)
+        mb = self._mb
+        for i in range(n - 2, -1, -1):
+            pp = self.conf.inputPreProcessors.get(i + 1)
+            if pp is not None:
+                eps = pp.backprop(eps, mb)
+            if i in self._fused_passthrough:
+                continue
+            layer = self.layers[i]
+            if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
+                _, eps = layer.backpropGradient(eps, tbptt_back=tbptt_back)
+            else:
+                _, eps = layer.backpropGradient(eps)
+            self._grad_ready(i)
+            if eps is None:
+                break
+        for l in self.listeners:
+            if hasattr(l, "onBackwardPass"):
+                l.onBackwardPass(self)
+        return eps
+
+    def computeGradientAndScore(self, x=None, y=None, fmask=None, lmask=None, stored_state=False,
+                                store_last_for_tbptt=False, tbptt_back=None):
+        x = self.input if x is None else x
+        y = self.labels if y is None else y
+        fmask = self.mask if fmask is None else fmask
+        lmask = self.labelsMask if lmask is None else lmask
+        self._mb = x.shape[0]
+        acts = self.feedForwardToLayer(len(self.layers) - 1, x, True, self._to_dev(fmask), stored_state,
+                                       store_last_for_tbptt)
+        for l in self.listeners:
+            if hasattr(l, "onForwardPass"):
+                l.onForwardPass(self, acts)
+        out = self.layers[-1]
+        out.setLabels(self._to_dev(y, self.master_dtype))
+        if lmask is not None:
+            out.maskArray = self._to_dev(lmask)
+        elif fmask is not None and out.maskArray is None:
+            out.maskArray = self._to_dev(fmask)
+        self._backprop(tbptt_back)
+        l1, l2 = self._regularization_terms()
+        self._score_t = out.computeScore(l1, l2, True)
+        self._score_val = None
+        return self._score_t
+
+    def _fit_batch(self, x, y, fmask=None, lmask=None):
+        if self.conf.backpropType == BackpropType.TruncatedBPTT and x.dim() == 3:
+            return self._fit_tbptt(x, y, fmask, lmask)
+        self.computeGradientAndScore(x, y, fmask, lmask)
+        self._apply_update(x.shape[0])
+        self._iteration_done()
+
+    def _fit_tbptt(self, x, y, fmask, lmask):
+        """Reference doTruncatedBPTT (MultiLayerNetwork.java:1521-1593)."""
+        T = x.shape[2]
+        fwd = self.conf.tbpttFwdLength
+        back = self.conf.tbpttBackLength
+        n_sub = (T + fwd - 1) // fwd
+        self.rnnClearPreviousState()
+        for s in range(n_sub):
+            t0, t1 = s * fwd, min(T, (s + 1) * fwd)
+            xs = x[:, :, t0:t1]
+            ys = y[:, :, t0:t1] if y.dim() == 3 else y
+            fm = fmask[:, t0:t1] if fmask is not None else None
+            lm = lmask[:, t0:t1] if lmask is not None else None
+            self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
+                                         tbptt_back=back)
+            self._apply_update(x.shape[0])
+            self._iteration_done()
+        self.rnnClearPreviousState()
+
+    def fit(self, data, labels=None, numEpochs=None, featuresMask=None, labelsMask=None):
+        """fit(DataSetIterator[, numEpochs]) | fit(DataSet) | fit(features, labels)."""
+        if not self.initCalled:
+            self.init()
+        if labels is not None:
+            return self.fit(DataSet(data, labels, featuresMask, labelsMask))
+        if isinstance(data, DataSet):
+            self._fit_batch(data.features, data.labels, data.featuresMask, data.labelsMask)
+            return self
+        if isinstance(labels, int) or (numEpochs is not None):
+            for _ in range(numEpochs or labels):
+                self.fit(data)
+            return self
+        self._fit_iterator(data)
+        return self
+
+    def _fit_iterator(self, it):
+        from ..datasets.iterators import AsyncDataSetIterator
+        wrap = it
+        if getattr(it, "asyncSupported", lambda: False)() and not isinstance(it, AsyncDataSetIterator) and \
+                type(it).__name__ not in ("BenchmarkDataSetIterator", "ListDataSetIterator"):
+            wrap = AsyncDataSetIterator(it, 2, self.device)
+        for l in self.listeners:
+            if hasattr(l, "onEpochStart"):
+                l.onEpochStart(self)
+        if hasattr(wrap, "reset"):
+            wrap.reset()
+        t0 = self._timer()
+        while wrap.hasNext():
+            ds = wrap.next()
+            self.lastEtlTime = (self._timer() - t0) * 1000.0
+            self._fit_batch(ds.features, ds.labels, ds.featuresMask, ds.labelsMask)
+            t0 = self._timer()
+        if wrap is not it and hasattr(wrap, "shutdown"):
+            wrap.shutdown()
+        for l in self.listeners:
+            if hasattr(l, "onEpochEnd"):
+                l.onEpochEnd(self)
+        self.incrementEpochCount()
+
+    # ------------------------------------------------------------------------------ scoring
+    def _score_dataset(self, ds, training=False):
+        with torch.no_grad():
+            self._mb = ds.features.shape[0]
+            self.feedForwardToLayer(len(self.layers) - 1, ds.features, training, self._to_dev(ds.featuresMask))
+            out = self.layers[-1]
+            out.setLabels(self._to_dev(ds.labels, self.master_dtype))
+            if ds.labelsMask is not None:
+                out.maskArray = self._to_dev(ds.labelsMask)
+            l1, l2 = self._regularization_terms()
+            return float(out.computeScore(l1, l2, training))
+
+    def scoreExamples(self, data, addRegularizationTerms=True):
+        ds = data if isinstance(data, DataSet) else data.next()
+        with torch.no_grad():
+            self.feedForwardToLayer(len(self.layers) - 1, ds.features, False, self._to_dev(ds.featuresMask))
+            out = self.layers[-1]
+            out.setLabels(self._to_dev(ds.labels, self.master_dtype))
+            l1, l2 = self._regularization_terms() if addRegularizationTerms else (0.0, 0.0)
+            return out.computeScoreForExamples(l1, l2)
+
+    def f1Score(self, ds):
+        from ..eval.evaluation import Evaluation
+        e = Evaluation()
+        e.eval(ds.labels, self.output(ds.features))
+        return e.f1()
+
+    # ------------------------------------------------------------------------------ rnn
+    def rnnTimeStep(self, x):
+        x = self._to_dev(x, self._feat_dtype())
+        mb = x.shape[0]
+        with torch.no_grad():
+            for i, layer in enumerate(self.layers):
+                x = self._pp(i, x, mb, False)
+                if hasattr(layer, "rnnTimeStep"):
+                    x = layer.rnnTimeStep(x)
+                else:
+                    x = layer.activate(x, False)
+        return x.float()
+
+    def rnnClearPreviousState(self):
+        for l in self.layers:
+            if hasattr(l, "rnnClearPreviousState"):
+                l.rnnClearPreviousState()
+
+    def rnnGetPreviousState(self, layer):
+        return self.layers[layer].rnnGetPreviousState()
+
+    def rnnSetPreviousState(self, layer, state):
+        self.layers[layer].rnnSetPreviousState(state)
+
+    # ------------------------------------------------------------------------------ evaluation
+    def evaluate(self, it, labelsList=None, topN=1):
+        from ..eval.evaluation import Evaluation
+        e = Evaluation(labelsList, topN=topN)
+        return self.doEvaluation(it, e)[0]
+
+    def evaluateRegression(self, it):
+        from ..eval.regression import RegressionEvaluation
+        return self.doEvaluation(it, RegressionEvaluation())[0]
+
+    def evaluateROC(self, it, rocThresholdSteps=0):
+        from ..eval.roc import ROC
+        return self.doEvaluation(it, ROC(rocThresholdSteps))[0]
+
+    def evaluateROCMultiClass(self, it, rocThresholdSteps=0):
+        from ..eval.roc import ROCMultiClass
+        return self.doEvaluation(it, ROCMultiClass(rocThresholdSteps))[0]
+
+    def doEvaluation(self, it, *evals):
+        if isinstance(it, DataSet):
+            items = [it]
+        else:
+            it.reset()
+            items = it
+        for ds in items:
+            out = self.output(ds.features, False, ds.featuresMask)
+            for e in evals:
+                e.eval(ds.labels, out, ds.labelsMask)
+        return list(evals)
+
+    # ------------------------------------------------------------------------------ misc
+    def clone(self):
+        import copy
+        conf = copy.deepcopy(self.conf)
+        net = MultiLayerNetwork(conf)
+        net.init(self.params().clone(), device=self.device)
+        net.updater.setStateViewArray(self.updater.getStateViewArray().clone())
+        return net
+
+    def setLearningRate(self, lr, layer=None):
+        name = None
+        if layer is not None:
+            name = self.conf.confs[layer].layerName if isinstance(layer, int) else layer
+        self.updater.setLearningRate(lr, name)
+
+    def getLearningRate(self, layer):
+        u = self.conf.confs[layer].updater
+        return u.getLearningRate(self.conf.iterationCount, self.conf.epochCount) if u is not None else None
+
+    def setInput(self, x):
+        self.input = x
+
+    def setLabels(self, y):
+        self.labels = y
+
+    def setLayerMaskArrays(self, fmask, lmask):
+        self.mask, self.labelsMask = fmask, lmask
+
+    def clearLayerMaskArrays(self):
+        self.mask = self.labelsMask = None
+
+    def toComputationGraph(self):
+        from ..utils.network_utils import to_computation_graph
+        return to_computation_graph(self)
+
+    def save(self, path, saveUpdater=True):
+        from ..utils.model_serializer import ModelSerializer
+        ModelSerializer.writeModel(self, path, saveUpdater)
+
+    @staticmethod
+    def load(path, loadUpdater=True):
+        from ..utils.model_serializer import ModelSerializer
+        return ModelSerializer.restoreMultiLayerNetwork(path, loadUpdater)
+
+    def clear(self):
+        for l in self.layers:
+            l.clear()

@@ -1,0 +1,326 @@
+"""Shared machinery of MultiLayerNetwork and ComputationGraph.
+
+* ONE flat parameter vector [1, P] (master fp32, fp64 for gradient checks), ONE flat gradient vector,
+  ONE flat updater-state vector; every layer holds views (reference MultiLayerNetwork.java:584-637,691-720).
+* Reduced-precision compute (DataType.BFLOAT16/HALF): a flat bf16 shadow of the parameters that the
+  fused updater kernel rewrites in the same pass that updates the master weights.
+* Parameters are allocated once on the device in HBM; on MI355X (288 GB/GPU) the whole training state
+  of every zoo model stays resident.
+* Score is kept on device (no host sync per iteration); ``score()`` syncs lazily.
+"""
+import os
+import time
+
+import torch
+
+from .conf.enums import DataType
+from .conf.weights import WeightInit, init_weights_
+from .updater import NetworkUpdater, build_entries
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+def default_device():
+    d = os.environ.get("DL4J_AMD_DEVICE")
+    if d:
+        return torch.device(d)
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def make_view(flat, off, spec):
+    n = spec.numel
+    v = flat[off:off + n]
+    if spec.order == "f" and len(spec.shape) == 2:
+        return v.reshape(spec.shape[1], spec.shape[0]).t()
+    if spec.order == "f":
+        return v.reshape(list(reversed(spec.shape))).permute(*reversed(range(len(spec.shape))))
+    return v.reshape(spec.shape)
+
+
+def init_param_(view, spec, conf, gen):
+    kind = spec.kind
+    if kind in ("weight", "recurrent"):
+        scheme = conf.weightInit
+        dist = getattr(conf, "dist", None)
+        if kind == "recurrent" and getattr(conf, "weightInitRecurrent", None) is not None:
+            scheme = conf.weightInitRecurrent
+            dist = getattr(conf, "distRecurrent", None) or dist
+        if scheme is None:
+            scheme = WeightInit.XAVIER
+        shape = spec.shape
+        init_weights_(view, spec.fan_in, spec.fan_out, shape, scheme, dist, gen)
+    elif kind == "bias":
+        view.fill_(float(getattr(conf, "biasInit", 0.0) or 0.0))
+    elif kind == "const":
+        view.fill_(float(spec.value))
+    elif kind == "zero":
+        view.zero_()
+    elif kind == "lstm_bias":
+        view.zero_()
+        H = spec.numel // 4
+        view.reshape(-1)[H:2 * H].fill_(float(spec.value))
+    else:
+        raise ValueError(kind)
+
+
+class BaseNetwork:
+    def __init__(self, conf):
+        self.conf = conf
+        self.listeners = []
+        self.initCalled = False
+        self._score_t = None
+        self._score_val = None
+        self.lastEtlTime = 0
+        self.device = None
+
+    # ------------------------------------------------------------------------------ setup
+    @property
+    def dataType(self):
+        return self.conf.dataType
+
+    def _setup_flat(self, layer_list, params=None, clone=False, device=None):
+        """layer_list: [(idx, name, impl)] in flattening order."""
+        self.device = torch.device(device) if device is not None else default_device()
+        dt = self.conf.dataType
+        self.master_dtype = dt.master_dtype()
+        self.compute_dtype = dt.torch_dtype()
+        if self.device.type == "cpu" and self.compute_dtype in (torch.bfloat16, torch.float16) and \
+                os.environ.get("DL4J_AMD_CPU_LOWP", "0") != "1":
+            # CPU reference path computes in fp32 (bf16 GEMMs on CPU are slow and not the target)
+            self.compute_dtype = torch.float32
+        total = sum(impl.conf.numParams() for _, _, impl in layer_list)
+        self._numParams = total
+        if params is not None:
+            p = params.reshape(-1)
+            if p.numel() != total:
+                raise ValueError(f"Invalid parameters: expected {total} params, got {p.numel()}")
+            flat = p.to(self.device, self.master_dtype)
+            flat = flat.clone() if (clone or flat.data_ptr() == p.data_ptr()) else flat
+            init = False
+        else:
+            flat = torch.zeros(total, dtype=self.master_dtype, device=self.device)
+            init = True
+        self.flattenedParams = flat
+        self.flattenedGradients = torch.zeros(total, dtype=self.master_dtype, device=self.device)
+        self.shadow = None
+        if self.compute_dtype != self.master_dtype:
+            self.shadow = torch.empty(total, dtype=self.compute_dtype, device=self.device)
+        gen = torch.Generator().manual_seed(int(self.conf.seed))
+        off = 0
+        self._layer_offsets = []
+        self._offset_of = {}
+        for idx, name, impl in layer_list:
+            impl.net = self
+            self._layer_offsets.append((idx, name, impl, off))
+            self._offset_of[idx] = off
+            self._offset_of[name] = off
+            o = off
+            impl.params, impl.grads, impl.cparams = {}, {}, {}
+            for spec in impl.conf.param_specs():
+                v = make_view(flat, o, spec)
+                if init:
+                    host = torch.empty(spec.numel, dtype=self.master_dtype)
+                    hv = make_view(host, 0, spec)
+                    iconf = impl.conf
+                    while getattr(iconf, "underlying", None) is not None:   # wrappers (Bidirectional, Frozen...)
+                        iconf = iconf.underlying
+                    init_param_(hv, spec, iconf, gen)
+                    with torch.no_grad():
+                        flat[o:o + spec.numel].copy_(host.to(self.device))
+                impl.params[spec.key] = v
+                impl.grads[spec.key] = make_view(self.flattenedGradients, o, spec)
+                if self.shadow is not None:
+                    impl.cparams[spec.key] = make_view(self.shadow, o, spec)
+                else:
+                    impl.cparams[spec.key] = v
+                o += spec.numel
+            off = o
+        if self.shadow is not None:
+            with torch.no_grad():
+                self.shadow.copy_(flat)
+        self.updater = NetworkUpdater(self, build_entries(self._layer_offsets))
+        self.updater.init_state(self.device, self.master_dtype)
+        self.initCalled = True
+
+    def sync_shadow(self):
+        if self.shadow is not None:
+            with torch.no_grad():
+                self.shadow.copy_(self.flattenedParams)
+
+    # ------------------------------------------------------------------------------ params API
+    def numParams(self, backwards=False):
+        return self._numParams
+
+    def params(self):
+        return self.flattenedParams.reshape(1, -1)
+
+    def setParams(self, p):
+        with torch.no_grad():
+            self.flattenedParams.copy_(p.reshape(-1).to(self.flattenedParams))
+        self.sync_shadow()
+
+    def setParameters(self, p):
+        self.setParams(p)
+
+    def getGradientsViewArray(self):
+        return self.flattenedGradients.reshape(1, -1)
+
+    def getUpdater(self):
+        return self.updater
+
+    def setUpdater(self, u):
+        self.updater = u
+
+    def paramTable(self, backpropOnly=False):
+        out = {}
+        for idx, name, impl, _ in self._layer_offsets:
+            for k, v in impl.params.items():
+                out[f"{name if self._key_by_name else idx}_{k}"] = v
+        return out
+
+    def getParam(self, key):
+        return self.paramTable()[key]
+
+    def setParam(self, key, val):
+        with torch.no_grad():
+            self.paramTable()[key].copy_(val.reshape(self.paramTable()[key].shape))
+        self.sync_shadow()
+
+    def gradient(self):
+        from .gradient import Gradient
+        g = Gradient(self.flattenedGradients.reshape(1, -1))
+        for idx, name, impl, _ in self._layer_offsets:
+            for k, v in impl.grads.items():
+                g.setGradientFor(f"{name if self._key_by_name else idx}_{k}", v)
+        return g
+
+    # ------------------------------------------------------------------------------ listeners
+    def setListeners(self, *ls):
+        self.listeners = [x for l in ls for x in (l if isinstance(l, (list, tuple)) else [l])]
+
+    def addListeners(self, *ls):
+        self.listeners += [x for l in ls for x in (l if isinstance(l, (list, tuple)) else [l])]
+
+    def getListeners(self):
+        return self.listeners
+
+    # ------------------------------------------------------------------------------ score
+    def score(self, dataset=None, training=False):
+        if dataset is not None:
+            return self._score_dataset(dataset, training)
+        if self._score_val is None and self._score_t is not None:
+            self._score_val = float(self._score_t)
+        return self._score_val
+
+    def setScore(self, s):
+        self._score_t = None
+        self._score_val = s
+
+    def _regularization_terms(self):
+        """(l1, l2) summed over the whole network, as device tensors (no host sync)."""
+        l1 = None
+        l2 = None
+        for _, _, impl, _ in self._layer_offsets:
+            for k, p in impl.params.items():
+                c1 = impl.conf.l1For(k)
+                c2 = impl.conf.l2For(k)
+                if c1 > 0:
+                    t = p.abs().sum() * c1
+                    l1 = t if l1 is None else l1 + t
+                if c2 > 0:
+                    t = (_acc(p) * _acc(p)).sum() * (0.5 * c2)
+                    l2 = t if l2 is None else l2 + t
+        z = torch.zeros((), device=self.device)
+        return (l1 if l1 is not None else z), (l2 if l2 is not None else z)
+
+    def calcL1(self, backpropOnly=True):
+        return float(self._regularization_terms()[0])
+
+    def calcL2(self, backpropOnly=True):
+        return float(self._regularization_terms()[1])
+
+    # ------------------------------------------------------------------------------ iteration counters
+    def getIterationCount(self):
+        return self.conf.iterationCount
+
+    def setIterationCount(self, n):
+        self.conf.iterationCount = n
+
+    def getEpochCount(self):
+        return self.conf.epochCount
+
+    def setEpochCount(self, n):
+        self.conf.epochCount = n
+
+    def incrementEpochCount(self):
+        self.conf.epochCount += 1
+
+    # ------------------------------------------------------------------------------ DP hooks
+    def _begin_backward(self):
+        acc = getattr(self, "gradientsAccumulator", None)
+        if acc is not None and hasattr(acc, "begin_backward"):
+            acc.begin_backward(self)
+
+    def _grad_ready(self, key):
+        acc = getattr(self, "gradientsAccumulator", None)
+        if acc is not None and hasattr(acc, "grad_ready"):
+            acc.grad_ready(self, self._offset_of.get(key, 0))
+
+    def setGradientsAccumulator(self, acc):
+        self.gradientsAccumulator = acc
+
+    # ------------------------------------------------------------------------------ update step
+    def _apply_update(self, batch_size):
+        it, ep = self.conf.iterationCount, self.conf.epochCount
+        for l in self.listeners:
+            if hasattr(l, "onGradientCalculation"):
+                l.onGradientCalculation(self)
+        acc = getattr(self, "gradientsAccumulator", None)
+        if acc is not None:
+            acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
+            batch_size = batch_size * acc.world_size
+        self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow)
+        for _, _, impl, _ in self._layer_offsets:
+            if getattr(impl.conf, "constraints", None):
+                impl.applyConstraints(it, ep)
+
+    def _iteration_done(self):
+        self.conf.iterationCount += 1
+        for l in self.listeners:
+            if hasattr(l, "iterationDone"):
+                l.iterationDone(self, self.conf.iterationCount, self.conf.epochCount)
+
+    def _to_dev(self, t, dtype=None):
+        if t is None:
+            return None
+        if not torch.is_tensor(t):
+            import numpy as np
+            t = torch.from_numpy(np.asarray(t))
+        t = t.to(self.device, non_blocking=True)
+        if dtype is not None and t.is_floating_point():
+            t = t.to(dtype)
+        if t.dim() == 4 and t.is_cuda:
+            t = t.contiguous(memory_format=torch.channels_last)
+        return t
+
+    def _feat_dtype(self):
+        return self.compute_dtype
+
+    def summary(self):
+        lines = [f"{'idx':>4} {'name':<28} {'type':<32} {'nParams':>12}"]
+        total = 0
+        for idx, name, impl, _ in self._layer_offsets:
+            n = impl.conf.numParams()
+            total += n
+            lines.append(f"{idx:>4} {str(name):<28} {type(impl.conf).__name__:<32} {n:>12,}")
+        lines.append(f"Total Parameters: {total:,}")
+        lines.append(f"Compute dtype: {self.compute_dtype}, device: {self.device}")
+        return "\n".join(lines)
+
+    def memoryReport(self, minibatch=1):
+        from .conf.memory import network_memory_report
+        return network_memory_report(self, minibatch)
+
+    def _timer(self):
+        return time.perf_counter()

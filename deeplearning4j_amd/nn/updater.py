@@ -1,0 +1,171 @@
+"""Network updater: UpdaterBlocks over the flat gradient + one fused update kernel.
+
+Reference: nn/updater/BaseMultiLayerUpdater.java:54-161 (block grouping: contiguous (layer,param)
+pairs with equal updater config share one block and one contiguous state slice), :223-309 (update
+order), :322-382 (gradient normalization preApply), UpdaterBlock.java:142-193.
+"""
+import math
+
+import torch
+
+from ..nn.conf.enums import GradientNormalization
+from ..nn.conf.updaters import NoOp
+from ..ops.update import Segment, UpdatePlan, fused_update
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+def updater_configs_equal(a, b):
+    """Reference UpdaterUtils.updaterConfigurationsEquals: same class and identical hyperparameters."""
+    if a is None or b is None:
+        return a is b
+    return type(a) is type(b) and a.to_dict() == b.to_dict()
+
+
+class ParamEntry:
+    __slots__ = ("layer_idx", "layer_name", "key", "p_off", "n", "updater", "l1", "l2", "layer")
+
+    def __init__(self, layer_idx, layer_name, key, p_off, n, updater, l1, l2, layer):
+        self.layer_idx, self.layer_name, self.key, self.p_off, self.n = layer_idx, layer_name, key, p_off, n
+        self.updater, self.l1, self.l2, self.layer = updater, l1, l2, layer
+
+
+class UpdaterBlock:
+    def __init__(self, p_start, p_end, st_off, updater, entries):
+        self.paramOffsetStart, self.paramOffsetEnd = p_start, p_end
+        self.st_off = st_off
+        self.updater = updater
+        self.entries = entries
+
+    def getLayersAndVariablesInBlock(self):
+        return [(e.layer_name, e.key) for e in self.entries]
+
+    def getGradientUpdater(self):
+        return self.updater
+
+    @property
+    def stateSize(self):
+        return self.updater.stateSize(self.paramOffsetEnd - self.paramOffsetStart)
+
+
+class NetworkUpdater:
+    """Shared implementation of MultiLayerUpdater / ComputationGraphUpdater."""
+
+    def __init__(self, net, entries):
+        self.net = net
+        self.entries = entries
+        self.blocks = []
+        cur = []
+        st = 0
+        for e in entries:
+            if cur and updater_configs_equal(cur[-1].updater, e.updater) and cur[-1].p_off + cur[-1].n == e.p_off:
+                cur.append(e)
+            else:
+                if cur:
+                    self._close(cur, st)
+                    st += self.blocks[-1].stateSize
+                cur = [e]
+        if cur:
+            self._close(cur, st)
+            st += self.blocks[-1].stateSize
+        self.state_size = st
+        segs = []
+        for bi, b in enumerate(self.blocks):
+            for e in b.entries:
+                segs.append(Segment(e.p_off, e.n, b.st_off, e.p_off - b.paramOffsetStart,
+                                    b.paramOffsetEnd - b.paramOffsetStart, b.updater, e.l1, e.l2, bi))
+        self.plan = UpdatePlan(segs, [(b.paramOffsetStart, b.paramOffsetEnd, b.st_off, b.updater)
+                                      for b in self.blocks])
+        self.state = None
+        self._gn_layers = self._collect_gn()
+
+    def _close(self, cur, st):
+        self.blocks.append(UpdaterBlock(cur[0].p_off, cur[-1].p_off + cur[-1].n, st, cur[0].updater, list(cur)))
+
+    def init_state(self, device, dtype):
+        self.state = torch.zeros(max(self.state_size, 1), dtype=dtype, device=device)[:self.state_size]
+
+    def getStateViewArray(self):
+        return self.state.reshape(1, -1)
+
+    def setStateViewArray(self, arr):
+        with torch.no_grad():
+            self.state.copy_(arr.reshape(-1).to(self.state.dtype))
+
+    def getUpdaterBlocks(self):
+        return self.blocks
+
+    def _collect_gn(self):
+        out = {}
+        for e in self.entries:
+            conf = e.layer.conf
+            gn = getattr(conf, "gradientNormalization", None)
+            if gn is None and hasattr(conf, "underlying"):
+                gn = getattr(conf.underlying, "gradientNormalization", None)
+            if gn is not None and gn != GradientNormalization.None_:
+                thr = getattr(conf, "gradientNormalizationThreshold", None) or \
+                    getattr(getattr(conf, "underlying", None), "gradientNormalizationThreshold", 1.0) or 1.0
+                out.setdefault(e.layer_name, (gn, thr, []))[2].append(e)
+        return out
+
+    def preApply(self, grad):
+        """Per-layer gradient normalization / clipping (reference BaseMultiLayerUpdater.java:322-382)."""
+        for name, (gn, thr, ents) in self._gn_layers.items():
+            views = [grad[e.p_off:e.p_off + e.n] for e in ents if not isinstance(e.updater, NoOp)]
+            if not views:
+                continue
+            G = GradientNormalization
+            if gn == G.RenormalizeL2PerLayer:
+                n = torch.sqrt(sum((_acc(v) ** 2).sum() for v in views))
+                for v in views:
+                    v.div_(n)
+            elif gn == G.RenormalizeL2PerParamType:
+                for v in views:
+                    v.div_(v.norm())
+            elif gn == G.ClipElementWiseAbsoluteValue:
+                for v in views:
+                    v.clamp_(-thr, thr)
+            elif gn == G.ClipL2PerLayer:
+                n = torch.sqrt(sum((_acc(v) ** 2).sum() for v in views))
+                scale = torch.clamp(thr / n, max=1.0)
+                for v in views:
+                    v.mul_(scale)
+            elif gn == G.ClipL2PerParamType:
+                for v in views:
+                    n = v.norm()
+                    v.mul_(torch.clamp(thr / n, max=1.0))
+
+    def update(self, params, grad, iteration, epoch, batch_size, shadow=None):
+        """Apply the whole update (preApply -> updater -> l1/l2 -> /batch -> params -= u) in place."""
+        if self._gn_layers:
+            self.preApply(grad)
+        fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
+                     self.net.conf.globalConf.get("miniBatch", True), shadow)
+
+    # learning-rate control (reference MultiLayerNetwork.setLearningRate :3411-3459)
+    def setLearningRate(self, lr, layer_name=None):
+        for b in self.blocks:
+            for e in b.entries:
+                if layer_name is None or e.layer_name == layer_name:
+                    if hasattr(e.updater, "learningRate"):
+                        e.updater.learningRate = lr
+                        e.updater.learningRateSchedule = None
+
+
+def build_entries(layer_list):
+    """layer_list: [(idx, name, layer_impl, p_off)] in flat order -> ParamEntry list."""
+    entries = []
+    for idx, name, layer, off in layer_list:
+        conf = layer.conf
+        o = off
+        for spec in conf.param_specs():
+            upd = conf.updaterFor(spec.key) if spec.trainable else NoOp()
+            if upd is None:
+                from ..nn.conf.updaters import Sgd
+                upd = Sgd(1e-3)
+            entries.append(ParamEntry(idx, name, spec.key, o, spec.numel, upd, conf.l1For(spec.key),
+                                      conf.l2For(spec.key), layer))
+            o += spec.numel
+    return entries
+
+
+_ = math

@@ -1,0 +1,26 @@
+"""Time-series helpers (reference nn/util/TimeSeriesUtils.java:149,188 — reverse with/without mask)."""
+import torch
+
+
+def reverse_time_series(x, mask=None):
+    """Reverse along the time axis (dim 2 for [mb, size, T]; dim 1 for [mb, T] masks). With a mask,
+    each example's valid (mask==1, left-aligned) prefix is reversed in place and padding stays put."""
+    tdim = x.dim() - 1
+    if mask is None:
+        return torch.flip(x, [tdim])
+    T = x.shape[tdim]
+    lengths = mask.reshape(mask.shape[0], -1).sum(dim=1).long()            # [mb]
+    t = torch.arange(T, device=x.device).unsqueeze(0)                       # [1, T]
+    src = torch.where(t < lengths.unsqueeze(1), lengths.unsqueeze(1) - 1 - t, t)  # [mb, T]
+    if x.dim() == 3:
+        idx = src.unsqueeze(1).expand(x.shape[0], x.shape[1], T)
+    else:
+        idx = src
+    return torch.gather(x, tdim, idx)
+
+
+def last_time_step(x, mask=None):
+    if mask is None:
+        return x[:, :, -1]
+    lengths = mask.reshape(mask.shape[0], -1).sum(dim=1).long().clamp(min=1)
+    return x[torch.arange(x.shape[0], device=x.device), :, lengths - 1]

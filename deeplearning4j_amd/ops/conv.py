@@ -1,0 +1,63 @@
+"""Convolution ops (reference ConvolutionLayer.java:131-265,290-428 im2col+GEMM path and the
+CudnnConvolutionHelper contract, CUDA:convolution/CudnnConvolutionHelper.java:297-306,424-470).
+
+``conv2d_forward(x, w, b, stride, pad4, dilation, act)`` — NCHW logical, channels-last physical on GPU.
+``conv2d_backward(...)`` -> (dx, dw, db).  pad4 = (top, bottom, left, right) so Same mode's
+asymmetric padding is exact.
+
+GPU: bf16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_implicit_gemm.hip``) when the shape is
+supported, else the torch/MIOpen library path.  CPU: torch reference (fp32/fp64).
+"""
+import torch
+import torch.nn.functional as F
+
+from .dispatch import use_native
+
+
+def _sym(pad4):
+    pt, pb, pl, pr = pad4
+    return pt == pb and pl == pr
+
+
+def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1):
+    if use_native(x, "conv") and groups == 1:
+        from . import native
+        y = native.conv2d_fwd(x, w, b, stride, pad4, dilation)
+        if y is not None:
+            return y
+    pt, pb, pl, pr = pad4
+    if _sym(pad4):
+        return F.conv2d(x, w, b, tuple(stride), (pt, pl), tuple(dilation), groups)
+    xp = F.pad(x, (pl, pr, pt, pb))
+    return F.conv2d(xp, w, b, tuple(stride), 0, tuple(dilation), groups)
+
+
+def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_dw=True, need_db=True,
+                    groups=1):
+    if use_native(x, "conv") and groups == 1:
+        from . import native
+        r = native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
+        if r is not None:
+            return r
+    pt, pb, pl, pr = pad4
+    sym = _sym(pad4)
+    xin = x if sym else F.pad(x, (pl, pr, pt, pb))
+    padding = [pt, pl] if sym else [0, 0]
+    dy = dy.contiguous(memory_format=torch.channels_last) if x.is_cuda and dy.dim() == 4 else dy
+    dx, dw, db = torch.ops.aten.convolution_backward(
+        dy, xin, w, [w.shape[0]] if need_db else None, list(stride), padding, list(dilation), False, [0, 0],
+        groups, [need_dx, need_dw, need_db])
+    if need_dx and not sym:
+        dx = dx[:, :, pt:pt + x.shape[2], pl:pl + x.shape[3]]
+    return dx, dw, db
+
+
+def conv_transpose2d_forward(x, w, b, stride, padding, dilation=(1, 1)):
+    return F.conv_transpose2d(x, w, b, tuple(stride), tuple(padding), 0, 1, tuple(dilation))
+
+
+def depthwise_conv2d_forward(x, w, b, stride, pad4, dilation, depth_mult):
+    """w: [dm, C, kh, kw] (reference sconv2d layout) -> grouped conv with C groups."""
+    C = x.shape[1]
+    wg = w.permute(1, 0, 2, 3).reshape(C * depth_mult, 1, w.shape[2], w.shape[3])
+    return conv2d_forward(x, wg, b, stride, pad4, dilation, groups=C)

@@ -1,0 +1,246 @@
+"""ctypes bindings of ``libdl4j_amd_kernels.so`` (gfx950 HIP kernels, C ABI) + torch-facing wrappers.
+
+Every wrapper launches on torch's current HIP stream (so HIP-graph capture and stream ordering work),
+allocates outputs/workspaces through torch's caching allocator, and returns ``None`` when a shape is
+outside what the kernel supports (the caller then uses the torch/library path).
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .build import KERNEL_LIB
+
+_lib = None
+c_void_p, c_int, c_ll, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(KERNEL_LIB):
+        if os.environ.get("DL4J_AMD_AUTOBUILD", "1") == "1":
+            from .build import build_kernels
+            build_kernels(verbose=False)
+        else:
+            raise FileNotFoundError(KERNEL_LIB)
+    lib = ctypes.CDLL(KERNEL_LIB)
+    sigs = {
+        "dl4j_fused_update": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int,
+                              c_void_p],
+        "dl4j_segdesc_size": [],
+        "dl4j_bn_workspace_floats": [c_ll, c_int],
+        "dl4j_bn_fwd": [c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p,
+                        c_void_p, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
+        "dl4j_bn_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                        c_void_p, c_void_p],
+        "dl4j_softmax_xent": [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                              c_void_p],
+        "dl4j_pool_fwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 13 + [c_void_p],
+        "dl4j_pool_bwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 13 + [c_void_p],
+    }
+    for name, args in sigs.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = c_int
+    for name, args in _EXTRA_SIGS.items():
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = c_int
+    _lib = lib
+    return lib
+
+
+_EXTRA_SIGS = {}
+
+
+def register_sig(name, args):
+    _EXTRA_SIGS[name] = args
+    if _lib is not None and hasattr(_lib, name):
+        f = getattr(_lib, name)
+        f.argtypes = args
+        f.restype = c_int
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"HIP kernel {what} failed with code {rc}")
+
+
+def _dt(t):
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    return None
+
+
+def _as_rows_nhwc(x):
+    """View a 4-D channels-last (or 2-D row-major) tensor as [M, C] rows without copying; None if impossible."""
+    if x.dim() == 2:
+        return x if x.is_contiguous() else None
+    if x.dim() == 4:
+        if x.is_contiguous(memory_format=torch.channels_last):
+            return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+        return None
+    return None
+
+
+def _like_rows(x):
+    if x.dim() == 4:
+        return torch.empty_like(x, memory_format=torch.channels_last)
+    return torch.empty_like(x)
+
+
+# ------------------------------------------------------------------------------------ fused updater
+class _SegTableCache:
+    def __init__(self):
+        self.dev = None
+        self.host_bytes = None
+
+
+_SEG_DTYPE = np.dtype([("p_off", "<i8"), ("n", "<i8"), ("st_off", "<i8"), ("in_block", "<i8"), ("block_n", "<i8"),
+                       ("op", "<i4"), ("pad", "<i4"), ("h", "<f4", 4), ("l1", "<f4"), ("l2", "<f4")])
+
+
+def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update):
+    lib = load()
+    if lib.dl4j_segdesc_size() != _SEG_DTYPE.itemsize:
+        raise RuntimeError("SegDesc layout mismatch between python and HIP")
+    from ..nn.conf.updaters import kernel_params
+    segs = plan.segments
+    arr = np.zeros(len(segs), dtype=_SEG_DTYPE)
+    for i, s in enumerate(segs):
+        op, h0, h1, h2, h3 = kernel_params(s.updater, iteration, epoch)
+        arr[i] = (s.p_off, s.n, s.st_off, s.in_block, s.block_n, op, 0, (h0, h1, h2, h3), s.l1, s.l2)
+    b = arr.tobytes()
+    cache = plan.__dict__.setdefault("_native_cache", _SegTableCache())
+    if cache.dev is None or cache.dev.device != params.device or cache.host_bytes != b:
+        host = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        if cache.dev is None or cache.dev.numel() != len(b) or cache.dev.device != params.device:
+            cache.dev = torch.empty(len(b), dtype=torch.uint8, device=params.device)
+        cache.dev.copy_(host, non_blocking=False)
+        cache.host_bytes = b
+    max_n = max((s.n for s in segs), default=0)
+    sk = 0
+    if shadow is not None:
+        if shadow.dtype != torch.bfloat16:
+            return False
+        sk = 1
+    rc = lib.dl4j_fused_update(_ptr(cache.dev), len(segs), max_n, _ptr(params), _ptr(grad), _ptr(state),
+                               _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _stream())
+    _check(rc, "fused_update")
+    return True
+
+
+# ------------------------------------------------------------------------------------------ batch norm
+def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu):
+    dt = _dt(x)
+    xr = _as_rows_nhwc(x) if dt is not None else None
+    if xr is None:
+        return None
+    M, C = xr.shape
+    if C % 8 != 0 or C // 8 > 256 or run_mean.dtype != torch.float32:
+        return None
+    lib = load()
+    y = _like_rows(x)
+    ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+    ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+    g = gamma if torch.is_tensor(gamma) else None
+    b = beta if torch.is_tensor(beta) else None
+    rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(y), M, C, _ptr(g), _ptr(b), float(gamma) if g is None else 1.0,
+                         float(beta) if b is None else 0.0, _ptr(run_mean), _ptr(run_var), float(decay), float(eps),
+                         1 if training else 0, 1 if relu else 0, _ptr(ws), _ptr(ctx), _stream())
+    _check(rc, "bn_fwd")
+    return y, ("NATIVE", x, ctx, relu, M, C)
+
+
+def bn_bwd(dy, ctx):
+    _, x, c, relu, M, C = ctx
+    if not dy.is_contiguous(memory_format=torch.channels_last if dy.dim() == 4 else torch.contiguous_format):
+        dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+    dy = dy.to(x.dtype)
+    lib = load()
+    dx = _like_rows(x)
+    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+    rc = lib.dl4j_bn_bwd(_dt(x), _ptr(_as_rows_nhwc(x)), _ptr(_as_rows_nhwc(dy)), _ptr(dx), M, C, _ptr(c),
+                         _ptr(dgamma), _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())
+    _check(rc, "bn_bwd")
+    return dx, dgamma, dbeta
+
+
+# ------------------------------------------------------------------------------------------ softmax-xent
+def softmax_xent(logits, labels, clip_eps):
+    dt = _dt(logits)
+    if dt is None or not logits.is_contiguous():
+        return None
+    B, V = logits.shape
+    lab = labels.contiguous().float()
+    grad = torch.empty_like(logits)
+    score = torch.empty(B, dtype=torch.float32, device=logits.device)
+    rc = load().dl4j_softmax_xent(dt, _ptr(logits), _ptr(lab), B, V, _ptr(grad), _ptr(score), None,
+                                  float(clip_eps or 0.0), _stream())
+    _check(rc, "softmax_xent")
+    return score, grad, None
+
+
+# ------------------------------------------------------------------------------------------ pooling
+def pool2d_fwd(x, ptype, kernel, stride, pad4):
+    dt = _dt(x)
+    if dt is None or x.dim() != 4 or x.shape[1] % 8 != 0:
+        return None
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    N, C, H, W = x.shape
+    pt, pb, pl, pr = pad4
+    kh, kw = kernel
+    sh, sw = stride
+    OH = (H + pt + pb - kh) // sh + 1
+    OW = (W + pl + pr - kw) // sw + 1
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    mode = 0 if ptype == "MAX" else 1
+    am = torch.empty(N * OH * OW * C if mode == 0 else 8, dtype=torch.uint8, device=x.device)
+    rc = load().dl4j_pool_fwd(dt, mode, _ptr(x), _ptr(y), _ptr(am), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
+                              _stream())
+    _check(rc, "pool_fwd")
+    return y, ("NATIVE", mode, am, x.shape, x.dtype, (kh, kw, sh, sw, pt, pl), (OH, OW))
+
+
+def pool2d_bwd(dy, ctx):
+    _, mode, am, xshape, xdt, (kh, kw, sh, sw, pt, pl), (OH, OW) = ctx
+    N, C, H, W = xshape
+    dy = dy.to(xdt).contiguous(memory_format=torch.channels_last)
+    dx = torch.empty(xshape, dtype=xdt, device=dy.device, memory_format=torch.channels_last)
+    rc = load().dl4j_pool_bwd(1 if xdt == torch.bfloat16 else 0, mode, _ptr(dy), _ptr(am), _ptr(dx), N, H, W, C, OH,
+                              OW, kh, kw, sh, sw, pt, pl, _stream())
+    _check(rc, "pool_bwd")
+    return dx
+
+
+# ------------------------------------------------------------------------------------------ conv (MFMA)
+def conv2d_fwd(x, w, b, stride, pad4, dilation):
+    from . import conv_native
+    return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation)
+
+
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+    from . import conv_native
+    return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
+
+
+def lstm_cell_fwd(z, c):
+    from . import rnn_native
+    return rnn_native.lstm_cell_fwd(z, c)

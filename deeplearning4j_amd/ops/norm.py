@@ -1,0 +1,114 @@
+"""Batch normalization ops (reference nn/layers/normalization/BatchNormalization.java:131-210 backward,
+:250-370 forward; CudnnBatchNormalizationHelper SPATIAL mode).
+
+Numerics contract (reference): batch var is the *biased* variance; eps is added before the sqrt and
+the running variance tracks (var + eps), so inference uses std = sqrt(running_var):
+    running_mean = decay*running_mean + (1-decay)*mean
+    running_var  = decay*running_var  + (1-decay)*(var + eps)
+``relu=True`` fuses the following ActivationLayer(ReLU) (forward max(0,.), backward mask) — the
+HIP kernel does it in the same pass (``csrc/batchnorm.hip``).
+"""
+import torch
+
+from .dispatch import use_native
+from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+
+
+def _dims(x):
+    return (0,) if x.dim() == 2 else (0, 2, 3)
+
+
+def _bshape(x):
+    return (1, -1) if x.dim() == 2 else (1, -1, 1, 1)
+
+
+def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=False):
+    """Returns (y, ctx). gamma/beta may be python floats (lockGammaBeta). Running stats updated in place
+    when training."""
+    if use_native(x, "bn") and x.dim() == 4 and torch.is_tensor(gamma):
+        from . import native
+        r = native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu)
+        if r is not None:
+            return r
+    xf = _acc(x)
+    dims = _dims(x)
+    bs = _bshape(x)
+    if training:
+        mean = xf.mean(dim=dims)
+        var = xf.var(dim=dims, unbiased=False) + eps
+        with torch.no_grad():
+            run_mean.mul_(decay).add_(mean.reshape(run_mean.shape).to(run_mean.dtype) * (1 - decay))
+            run_var.mul_(decay).add_(var.reshape(run_var.shape).to(run_var.dtype) * (1 - decay))
+    else:
+        mean = _acc(run_mean.reshape(-1))
+        var = _acc(run_var.reshape(-1))
+    invstd = torch.rsqrt(var)
+    g = _acc(gamma.reshape(-1)) if torch.is_tensor(gamma) else torch.full_like(mean, float(gamma))
+    b = _acc(beta.reshape(-1)) if torch.is_tensor(beta) else torch.full_like(mean, float(beta))
+    xhat = (xf - mean.reshape(bs)) * invstd.reshape(bs)
+    y = xhat * g.reshape(bs) + b.reshape(bs)
+    if relu:
+        y = torch.relu(y)
+    y = y.to(x.dtype)
+    if x.dim() == 4 and x.is_cuda:
+        y = y.contiguous(memory_format=torch.channels_last)
+    return y, ("REF", x, mean, invstd, g, b, relu, y if relu else None)
+
+
+def bn_backward(dy, ctx):
+    """Returns (dx, dgamma, dbeta) — dgamma/dbeta are sums over the batch (not averaged)."""
+    if ctx[0] == "NATIVE":
+        from . import native
+        return native.bn_bwd(dy, ctx)
+    _, x, mean, invstd, g, b, relu, y = ctx
+    dims = _dims(x)
+    bs = _bshape(x)
+    dyf = _acc(dy)
+    if relu:
+        dyf = dyf * (y > 0).to(dyf.dtype)
+    xhat = (_acc(x) - mean.reshape(bs)) * invstd.reshape(bs)
+    m = x.numel() // x.shape[1]
+    dbeta = dyf.sum(dim=dims)
+    dgamma = (dyf * xhat).sum(dim=dims)
+    dx = (g * invstd).reshape(bs) * (dyf - dbeta.reshape(bs) / m - xhat * (dgamma.reshape(bs) / m))
+    dx = dx.to(dy.dtype)
+    if x.dim() == 4 and x.is_cuda:
+        dx = dx.contiguous(memory_format=torch.channels_last)
+    return dx, dgamma, dbeta
+
+
+def bn_forward_inference_only(x, gamma, beta, run_mean, run_var, relu=False):
+    y, _ = bn_forward(x, gamma, beta, run_mean, run_var, False, 0.0, 0.0, relu)
+    return y
+
+
+def layer_norm_forward(x, gamma, beta, eps):
+    """LayerNorm over dim 1 of [mb, n] (or [mb, n, T]); returns (y, ctx)."""
+    xf = _acc(x)
+    if x.dim() == 3:
+        xf = xf.transpose(1, 2)
+    mean = xf.mean(dim=-1, keepdim=True)
+    var = xf.var(dim=-1, unbiased=False, keepdim=True)
+    invstd = torch.rsqrt(var + eps)
+    xhat = (xf - mean) * invstd
+    y = xhat * _acc(gamma.reshape(-1)) + _acc(beta.reshape(-1))
+    if x.dim() == 3:
+        y = y.transpose(1, 2)
+    return y.to(x.dtype), (xhat, invstd, _acc(gamma.reshape(-1)), x.dim())
+
+
+def layer_norm_backward(dy, ctx):
+    xhat, invstd, g, nd = ctx
+    d = _acc(dy)
+    if nd == 3:
+        d = d.transpose(1, 2)
+    n = xhat.shape[-1]
+    red = tuple(range(d.dim() - 1))
+    dgamma = (d * xhat).sum(dim=red)
+    dbeta = d.sum(dim=red)
+    dxhat = d * g
+    dx = invstd * (dxhat - dxhat.mean(dim=-1, keepdim=True) - xhat * (dxhat * xhat).mean(dim=-1, keepdim=True))
+    if nd == 3:
+        dx = dx.transpose(1, 2)
+    _ = n
+    return dx.to(dy.dtype), dgamma, dbeta

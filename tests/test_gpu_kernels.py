@@ -1,0 +1,147 @@
+"""HIP kernel numerics vs the plain-torch fp32 reference of the same op (run on a real MI355X).
+
+Reference-vs-helper parity is the reference's own strategy for its cuDNN helpers
+(CUDAT:convolution/TestConvolution.java:72-147, CUDAT:lstm/ValidateCudnnLSTM.java:32-246)."""
+import pytest
+import torch
+
+from deeplearning4j_amd import ops
+from deeplearning4j_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = max(1.0, b.abs().max().item())
+    assert err <= tol * scale, f"max abs err {err} (scale {scale})"
+
+
+def test_native_library_loaded(cuda):
+    assert ops.native_lib() is not None
+    assert ops.use_native(torch.zeros(1, device=cuda), "bn")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("shape", [(4, 64, 9, 7), (2, 256, 5, 5), (3, 2048, 2, 2), (16, 24)])
+def test_batchnorm_fwd_bwd(cuda, dtype, relu, shape):
+    g = torch.Generator().manual_seed(0)
+    x = (torch.randn(*shape, generator=g) * 3 + 1.5)
+    C = shape[1]
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    dy = torch.randn(*shape, generator=g)
+    rm_c, rv_c = torch.zeros(C), torch.ones(C)
+    xr = x.to(dtype)
+    y_ref, ctx_ref = ops.bn_forward(xr.float(), gamma, beta, rm_c, rv_c, True, 0.9, 1e-5, relu)
+    dx_ref, dg_ref, db_ref = ops.bn_backward(dy.to(dtype).float(), ctx_ref)
+    xd = xr.to(cuda)
+    if xd.dim() == 4:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, ctx = ops.bn_forward(xd, gamma.to(cuda), beta.to(cuda), rm, rv, True, 0.9, 1e-5, relu)
+    assert ctx[0] == "NATIVE"
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, y_ref, tol)
+    _close(rm, rm_c, 1e-4)
+    _close(rv, rv_c, 1e-4)
+    dyd = dy.to(dtype).to(cuda)
+    if dyd.dim() == 4:
+        dyd = dyd.contiguous(memory_format=torch.channels_last)
+    dx, dgm, dbt = ops.bn_backward(dyd, ctx)
+    _close(dx, dx_ref, tol * 2)
+    _close(dgm, dg_ref, 1e-3 if dtype == torch.float32 else 3e-2)
+    _close(dbt, db_ref, 1e-3 if dtype == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ptype", ["MAX", "AVG"])
+@pytest.mark.parametrize("geom", [((3, 3), (2, 2), (0, 0, 0, 0)), ((2, 2), (2, 2), (0, 0, 0, 0)),
+                                  ((3, 3), (1, 1), (1, 1, 1, 1)), ((3, 3), (2, 2), (0, 1, 0, 1))])
+def test_pool(cuda, dtype, ptype, geom):
+    k, s, p = geom
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 16, 11, 9, generator=g).to(dtype)
+    y_ref, ctx_ref = ops.pool2d_forward(x.float(), ptype, k, s, p)
+    xd = x.to(cuda).contiguous(memory_format=torch.channels_last)
+    y, ctx = ops.pool2d_forward(xd, ptype, k, s, p)
+    assert ctx[0] == "NATIVE"
+    _close(y, y_ref, 1e-6 if dtype == torch.float32 else 1e-2)
+    dy = torch.randn(y_ref.shape, generator=g).to(dtype)
+    dx_ref = ops.pool2d_backward(dy.float(), ctx_ref)
+    dx = ops.pool2d_backward(dy.to(cuda).contiguous(memory_format=torch.channels_last), ctx)
+    _close(dx, dx_ref, 1e-5 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_softmax_xent(cuda, dtype):
+    g = torch.Generator().manual_seed(2)
+    z = (torch.randn(37, 1000, generator=g) * 4).to(dtype)
+    y = torch.zeros(37, 1000)
+    y[torch.arange(37), torch.randint(0, 1000, (37,), generator=g)] = 1
+    s_ref, g_ref, _ = ops.softmax_xent(z.float(), y, None, 1e-10)
+    s, gr, _ = ops.softmax_xent(z.to(cuda), y.to(cuda), None, 1e-10)
+    _close(s, s_ref, 1e-4)
+    _close(gr, g_ref, 1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("upd", ["Sgd", "Nesterovs", "Adam", "AdaMax", "Nadam", "AdaGrad", "AdaDelta", "RmsProp",
+                                 "NoOp"])
+def test_fused_updater_matches_reference(cuda, upd):
+    from deeplearning4j_amd.nn.conf import updaters as U
+    from deeplearning4j_amd.ops.update import Segment, UpdatePlan, fused_update
+    u = getattr(U, upd)()
+    n1, n2 = 1000, 3001
+    nb = n1 + n2
+    segs = [Segment(0, n1, 0, 0, nb, u, 0.01, 0.0, 0), Segment(n1, n2, 0, n1, nb, u, 0.0, 0.02, 0)]
+    plan = UpdatePlan(segs, [(0, nb, 0, u)])
+    g = torch.Generator().manual_seed(3)
+    p = torch.randn(nb, generator=g)
+    st = torch.rand(u.stateSize(nb), generator=g)
+    for it in range(3):
+        gr = torch.randn(nb, generator=g)
+        pc, gc, sc = p.clone(), gr.clone(), st.clone()
+        fused_update(plan, pc, gc, sc, it, 0, 8)
+        pd, gd, sd = p.to(cuda), gr.to(cuda), st.to(cuda)
+        shadow = torch.empty(nb, dtype=torch.bfloat16, device=cuda)
+        fused_update(plan, pd, gd, sd, it, 0, 8, shadow=shadow)
+        _close(pd, pc, 1e-5)
+        _close(gd, gc, 1e-5)
+        _close(sd, sc, 1e-5)
+        _close(shadow, pc, 1e-2)
+        p, st = pc, sc
+
+
+def test_resnet50_step_bf16(cuda):
+    from deeplearning4j_amd.models import ResNet50
+    from deeplearning4j_amd.nn.conf import DataType
+    net = ResNet50(numLabels=10, dataType=DataType.BFLOAT16).init(device=cuda)
+    x = torch.rand(4, 3, 224, 224, device=cuda)
+    y = torch.zeros(4, 10, device=cuda)
+    y[torch.arange(4), torch.tensor([1, 2, 3, 4])] = 1
+    s = []
+    for _ in range(3):
+        net.fit([x], [y])
+        s.append(net.score())
+    assert all(v == v for v in s)
+    assert net.shadow is not None and net.shadow.dtype == torch.bfloat16
+    assert (net.shadow.float() - net.flattenedParams).abs().max().item() < 0.05
+
+
+def test_lenet_gpu_matches_cpu(cuda):
+    """Same LeNet, same data: fp32 GPU (native BN-free path: pool + softmax-xent + fused updater) vs CPU."""
+    from deeplearning4j_amd.models import LeNet
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(16, 1, 28, 28, generator=g)
+    y = torch.zeros(16, 10)
+    y[torch.arange(16), torch.randint(0, 10, (16,), generator=g)] = 1
+    a = LeNet().init(device=torch.device("cpu"))
+    b = LeNet().init(device=cuda)
+    _close(b.params(), a.params(), 0)
+    for _ in range(3):
+        a.fit(x.reshape(16, -1), y)
+        b.fit(x.reshape(16, -1), y)
+    _close(b.params(), a.params(), 2e-3)
+    assert abs(a.score() - b.score()) < 1e-3
