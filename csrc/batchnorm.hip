@@ -1,28 +1,31 @@
 // Batch normalization for channels-last activations viewed as a row-major [M, C] matrix
-// (M = N*H*W, C % 8 == 0), bf16 or fp32 storage, fp32 math. Optional fused ReLU.
+// (M = N*H*W, C % 8 == 0), bf16 or fp32 storage, fp32 math.
+// Optional fused epilogues (chosen by the graph planner):
+//   RELU:  y = relu(bn(x))                       (BN -> ActivationLayer(ReLU))
+//   RES:   y = relu(bn(x) + r)                   (BN -> ElementWiseVertex(Add, shortcut) -> ReLU: ResNet blocks)
 //
 // Semantics = reference nn/layers/normalization/BatchNormalization.java (biased batch variance, eps added
 // before sqrt, running stats: run = decay*run + (1-decay)*stat, running var tracks var+eps).
 //
-// Forward (training): stats_partial -> finalize (mean, invstd, running stats, per-channel scale/shift)
-//                     -> apply (y = x*scale + shift [+relu]).  3 launches, x read twice, y written once.
-// Backward:           bwd_partial (sum dy', sum dy'*xhat; dy' = relu-masked dy, mask recomputed from x)
-//                     -> bwd_finalize (dgamma, dbeta into the flat gradient) -> bwd_apply.
-// Each thread owns 8 consecutive channels (one 16-byte vector); a block covers R = 256/(C/8) rows per
-// sweep, so every wave issues fully coalesced dwordx4 loads. Partial sums go to a [nblk, C] fp32
-// workspace (no atomics -> bitwise reproducible).
+// Forward (training): stats_partial -> finalize -> apply.   Backward: bwd_partial -> bwd_finalize -> bwd_apply.
+// Each thread owns 8 consecutive channels (one 16-byte vector); a block covers R = 256/(C/8) rows per sweep,
+// so every wave issues fully coalesced dwordx4 loads. Per-block partial sums go to a [nblk, C] fp32
+// workspace (no atomics -> bitwise reproducible); finalize reduces them with 4 row-groups x 64 channels per
+// block. The ReLU mask in backward is recomputed from x (and r), so no activation needs to be stored.
 #include "common.h"
 
+// --------------------------------------------------------------------------------------------- forward
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x, long long M, int C,
                                                         long long rows_per_blk, float* __restrict__ part_s1,
-                                                        float* __restrict__ part_s2, const float* __restrict__ shiftv) {
+                                                        float* __restrict__ part_s2) {
   const int T8 = C >> 3;
   const int R = 256 / T8;                       // rows per sweep
   const int cg = threadIdx.x % T8, r0 = threadIdx.x / T8;
   float s1[8], s2[8], sh[8];
+  Vec8<T>::load(x + cg * 8, sh);                // row 0 is the shift: sums of (x - x0) avoid cancellation
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s1[i] = 0.f; s2[i] = 0.f; sh[i] = shiftv[cg * 8 + i]; }
+  for (int i = 0; i < 8; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
   const long long rbeg = (long long)blockIdx.x * rows_per_blk;
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
@@ -34,15 +37,14 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
       for (int i = 0; i < 8; ++i) { const float d = v[i] - sh[i]; s1[i] += d; s2[i] += d * d; }
     }
   }
-  // reduce the R partials of each channel group through LDS
   __shared__ float red1[2048];
   __shared__ float red2[2048];
+#pragma unroll
   for (int i = 0; i < 8; ++i) {
     red1[threadIdx.x * 8 + i] = (r0 < R) ? s1[i] : 0.f;
     red2[threadIdx.x * 8 + i] = (r0 < R) ? s2[i] : 0.f;
   }
   __syncthreads();
-  // thread t < C sums channel t over the R sweeps
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c >> 3, k = c & 7;
     float a = 0.f, b = 0.f;
@@ -52,26 +54,37 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
   }
 }
 
-template <typename T>
-__global__ void bn_shift_init(const T* __restrict__ x, int C, float* __restrict__ shiftv) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) shiftv[c] = ld1<T>(x + c);  // row 0 as the shift
+// Reduce [nblk, C] partials: block = 64 channels x 4 row groups.
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ p1, const float* __restrict__ p2, int nblk,
+                                                int C, int c, double& a, double& b) {
+  const int grp = threadIdx.x >> 6;
+  a = 0.0; b = 0.0;
+  if (c < C)
+    for (int i = grp; i < nblk; i += 4) { a += p1[(long long)i * C + c]; b += p2[(long long)i * C + c]; }
+  __shared__ double ra[256], rb[256];
+  ra[threadIdx.x] = a; rb[threadIdx.x] = b;
+  __syncthreads();
+  if (grp == 0) {
+    a = ra[threadIdx.x] + ra[threadIdx.x + 64] + ra[threadIdx.x + 128] + ra[threadIdx.x + 192];
+    b = rb[threadIdx.x] + rb[threadIdx.x + 64] + rb[threadIdx.x + 128] + rb[threadIdx.x + 192];
+  }
 }
 
-// training=1: reduce partials -> mean/var; update running stats. training=0: use running stats.
-__global__ void bn_finalize(const float* __restrict__ part_s1, const float* __restrict__ part_s2, int nblk, int C,
-                            long long M, const float* __restrict__ shiftv, const float* __restrict__ gamma,
-                            const float* __restrict__ beta, float gconst, float bconst, float* __restrict__ run_mean,
-                            float* __restrict__ run_var, float decay, float eps, int training,
-                            float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale,
-                            float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+template <typename T>
+__global__ __launch_bounds__(256) void bn_finalize(const float* __restrict__ part_s1, const float* __restrict__ part_s2,
+                                                   int nblk, int C, long long M, const T* __restrict__ x,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float gconst, float bconst, float* __restrict__ run_mean,
+                                                   float* __restrict__ run_var, float decay, float eps, int training,
+                                                   float* __restrict__ ctx) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a = 0.0, b = 0.0;
+  if (training) reduce_partials(part_s1, part_s2, nblk, C, c, a, b);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
   float mean, var;
   if (training) {
-    double a = 0.0, b = 0.0;
-    for (int i = 0; i < nblk; ++i) { a += part_s1[(long long)i * C + c]; b += part_s2[(long long)i * C + c]; }
     const double m1 = a / (double)M;
-    mean = (float)(shiftv[c] + m1);
+    mean = (float)((double)ld1<T>(x + c) + m1);
     double v = b / (double)M - m1 * m1;
     if (v < 0) v = 0;
     var = (float)v + eps;
@@ -84,37 +97,40 @@ __global__ void bn_finalize(const float* __restrict__ part_s1, const float* __re
   const float inv = rsqrtf(var);
   const float g = gamma ? gamma[c] : gconst;
   const float bb = beta ? beta[c] : bconst;
-  mean_out[c] = mean;
-  invstd_out[c] = inv;
-  scale[c] = g * inv;
-  shift[c] = bb - mean * g * inv;
+  ctx[c] = mean;
+  ctx[C + c] = inv;
+  ctx[2 * C + c] = g * inv;                 // scale
+  ctx[3 * C + c] = bb - mean * g * inv;     // shift
 }
 
-template <typename T, bool RELU>
-__global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, T* __restrict__ y, long long M, int C,
-                                                const float* __restrict__ scale, const float* __restrict__ shift) {
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
+                                                long long M, int C, const float* __restrict__ ctx) {
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
+  const float* scale = ctx + 2 * C;
+  const float* shift = ctx + 3 * C;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(v % T8);
-    float a[8];
+    const int c0 = (int)(v % T8) * 8;
+    float a[8], r[8];
     Vec8<T>::load(x + v * 8, a);
+    if (RES) Vec8<T>::load(res + v * 8, r);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float t = a[i] * scale[cg * 8 + i] + shift[cg * 8 + i];
+      float t = a[i] * scale[c0 + i] + shift[c0 + i];
+      if (RES) t += r[i];
       a[i] = RELU ? fmaxf(t, 0.f) : t;
     }
     Vec8<T>::store(y + v * 8, a);
   }
 }
 
-// ---------------------------------------------------------------------------------------- backward
-template <typename T, bool RELU>
-__global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, const T* __restrict__ dy, long long M,
-                                                      int C, long long rows_per_blk, const float* __restrict__ mean,
-                                                      const float* __restrict__ invstd, const float* __restrict__ scale,
-                                                      const float* __restrict__ shift, float* __restrict__ part_db,
-                                                      float* __restrict__ part_dg) {
+// -------------------------------------------------------------------------------------------- backward
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, const T* __restrict__ res,
+                                                      const T* __restrict__ dy, long long M, int C,
+                                                      long long rows_per_blk, const float* __restrict__ ctx,
+                                                      float* __restrict__ part_db, float* __restrict__ part_dg) {
   const int T8 = C >> 3;
   const int R = 256 / T8;
   const int cg = threadIdx.x % T8, r0 = threadIdx.x / T8;
@@ -122,21 +138,26 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     db[i] = 0.f; dg[i] = 0.f;
-    mu[i] = mean[cg * 8 + i]; is[i] = invstd[cg * 8 + i];
-    sc[i] = scale[cg * 8 + i]; sf[i] = shift[cg * 8 + i];
+    mu[i] = ctx[cg * 8 + i]; is[i] = ctx[C + cg * 8 + i];
+    sc[i] = ctx[2 * C + cg * 8 + i]; sf[i] = ctx[3 * C + cg * 8 + i];
   }
   const long long rbeg = (long long)blockIdx.x * rows_per_blk;
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
   if (r0 < R) {
     for (long long r = rbeg + r0; r < rend; r += R) {
-      float xv[8], gv[8];
+      float xv[8], gv[8], rv[8];
       Vec8<T>::load(x + r * C + cg * 8, xv);
       Vec8<T>::load(dy + r * C + cg * 8, gv);
+      if (RES) Vec8<T>::load(res + r * C + cg * 8, rv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float d = gv[i];
-        if (RELU) d = (xv[i] * sc[i] + sf[i] > 0.f) ? d : 0.f;
+        if (RELU) {
+          float t = xv[i] * sc[i] + sf[i];
+          if (RES) t += rv[i];
+          d = t > 0.f ? d : 0.f;
+        }
         db[i] += d;
         dg[i] += d * (xv[i] - mu[i]) * is[i];
       }
@@ -144,6 +165,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   }
   __shared__ float red1[2048];
   __shared__ float red2[2048];
+#pragma unroll
   for (int i = 0; i < 8; ++i) {
     red1[threadIdx.x * 8 + i] = (r0 < R) ? db[i] : 0.f;
     red2[threadIdx.x * 8 + i] = (r0 < R) ? dg[i] : 0.f;
@@ -158,51 +180,59 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   }
 }
 
-__global__ void bn_bwd_finalize(const float* __restrict__ part_db, const float* __restrict__ part_dg, int nblk, int C,
-                                long long M, float* __restrict__ dbeta, float* __restrict__ dgamma,
-                                float* __restrict__ cdb, float* __restrict__ cdg) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int i = 0; i < nblk; ++i) { a += part_db[(long long)i * C + c]; b += part_dg[(long long)i * C + c]; }
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__ part_db,
+                                                       const float* __restrict__ part_dg, int nblk, int C, long long M,
+                                                       float* __restrict__ dbeta, float* __restrict__ dgamma,
+                                                       float* __restrict__ cdb, float* __restrict__ cdg) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double a, b;
+  reduce_partials(part_db, part_dg, nblk, C, c, a, b);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
   if (dbeta) dbeta[c] = (float)a;
   if (dgamma) dgamma[c] = (float)b;
   cdb[c] = (float)(a / (double)M);
   cdg[c] = (float)(b / (double)M);
 }
 
-template <typename T, bool RELU>
-__global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
-                                                    long long M, int C, const float* __restrict__ mean,
-                                                    const float* __restrict__ invstd, const float* __restrict__ scale,
-                                                    const float* __restrict__ shift, const float* __restrict__ cdb,
-                                                    const float* __restrict__ cdg) {
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ res,
+                                                    const T* __restrict__ dy, T* __restrict__ dx, T* __restrict__ dres,
+                                                    long long M, int C, const float* __restrict__ ctx,
+                                                    const float* __restrict__ cdb, const float* __restrict__ cdg) {
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
+  const float *mean = ctx, *invstd = ctx + C, *scale = ctx + 2 * C, *shift = ctx + 3 * C;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
     const int c0 = (int)(v % T8) * 8;
-    float xv[8], gv[8];
+    float xv[8], gv[8], rv[8];
     Vec8<T>::load(x + v * 8, xv);
     Vec8<T>::load(dy + v * 8, gv);
+    if (RES) Vec8<T>::load(res + v * 8, rv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int c = c0 + i;
       float d = gv[i];
-      if (RELU) d = (xv[i] * scale[c] + shift[c] > 0.f) ? d : 0.f;
+      if (RELU) {
+        float t = xv[i] * scale[c] + shift[c];
+        if (RES) t += rv[i];
+        d = t > 0.f ? d : 0.f;
+      }
+      if (RES) rv[i] = d;
       const float xh = (xv[i] - mean[c]) * invstd[c];
-      // dx = gamma*invstd * (dy' - mean(dy') - xhat*mean(dy'*xhat));  gamma*invstd == scale
+      // dx = gamma*invstd * (dy' - mean(dy') - xhat*mean(dy'*xhat)); gamma*invstd == scale
       xv[i] = scale[c] * (d - cdb[c] - xh * cdg[c]);
     }
     Vec8<T>::store(dx + v * 8, xv);
+    if (RES) Vec8<T>::store(dres + v * 8, rv);
   }
 }
 
 static inline void bn_grid(long long M, int C, int* nblk, long long* rows_per_blk) {
   const int T8 = C / 8;
   const long long work = M * T8;                  // vector loads
-  long long nb = work / (256LL * 32);             // >= 32 vector loads per thread
+  long long nb = work / (256LL * 64);             // >= 64 vector loads per thread
   if (nb < 1) nb = 1;
-  if (nb > 1024) nb = 1024;
+  if (nb > 512) nb = 512;
   long long rpb = (M + nb - 1) / nb;
   nb = (M + rpb - 1) / rpb;
   *nblk = (int)nb;
@@ -222,58 +252,70 @@ DL4J_API int dl4j_bn_workspace_floats(long long M, int C) {
   return 2 * nblk * C + 8 * C;
 }
 
+#define BN_DISPATCH3(KERNEL, T, relu, res, ...)                                         \
+  do {                                                                                  \
+    if (res) hipLaunchKernelGGL((KERNEL<T, true, true>), __VA_ARGS__);                 \
+    else if (relu) hipLaunchKernelGGL((KERNEL<T, true, false>), __VA_ARGS__);          \
+    else hipLaunchKernelGGL((KERNEL<T, false, false>), __VA_ARGS__);                   \
+  } while (0)
+
 // dtype: 0 fp32, 1 bf16. ws: >= dl4j_bn_workspace_floats floats. ctx_out: 4*C floats (mean, invstd, scale, shift)
-DL4J_API int dl4j_bn_fwd(int dtype, const void* x, void* y, long long M, int C, const float* gamma, const float* beta,
-                         float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
-                         int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
+// res: optional residual (same layout as x) -> y = relu(bn(x) + res) (relu forced on).
+DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                         const float* beta, float gconst, float bconst, float* run_mean, float* run_var, float decay,
+                         float eps, int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256) return -1;
+  if (res) relu = 1;
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
-  float* shiftv = p2 + (long long)nblk * C;
-  float *mean = ctx_out, *inv = ctx_out + C, *scale = ctx_out + 2 * C, *shift = ctx_out + 3 * C;
-  if (training) {
-    if (dtype == 1) {
-      hipLaunchKernelGGL(bn_shift_init<bf16>, dim3(1), dim3(256), 0, s, (const bf16*)x, C, shiftv);
-      hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, (const bf16*)x, M, C, rpb, p1, p2, shiftv);
-    } else {
-      hipLaunchKernelGGL(bn_shift_init<float>, dim3(1), dim3(256), 0, s, (const float*)x, C, shiftv);
-      hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, (const float*)x, M, C, rpb, p1, p2, shiftv);
-    }
-  }
-  hipLaunchKernelGGL(bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, p1, p2, nblk, C, M, shiftv, gamma, beta, gconst,
-                     bconst, run_mean, run_var, decay, eps, training, mean, inv, scale, shift);
+  const dim3 fg((C + 63) / 64);
   const int ag = apply_grid(M, C);
   if (dtype == 1) {
-    if (relu) hipLaunchKernelGGL((bn_apply<bf16, true>), dim3(ag), dim3(256), 0, s, (const bf16*)x, (bf16*)y, M, C, scale, shift);
-    else hipLaunchKernelGGL((bn_apply<bf16, false>), dim3(ag), dim3(256), 0, s, (const bf16*)x, (bf16*)y, M, C, scale, shift);
+    const bf16* xb = (const bf16*)x;
+    if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
+    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
+                       run_mean, run_var, decay, eps, training, ctx_out);
+    BN_DISPATCH3(bn_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, xb, (const bf16*)res, (bf16*)y, M, C, ctx_out);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_apply<float, true>), dim3(ag), dim3(256), 0, s, (const float*)x, (float*)y, M, C, scale, shift);
-    else hipLaunchKernelGGL((bn_apply<float, false>), dim3(ag), dim3(256), 0, s, (const float*)x, (float*)y, M, C, scale, shift);
+    const float* xf = (const float*)x;
+    if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
+    hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
+                       run_mean, run_var, decay, eps, training, ctx_out);
+    BN_DISPATCH3(bn_apply, float, relu, res, dim3(ag), dim3(256), 0, s, xf, (const float*)res, (float*)y, M, C,
+                 ctx_out);
   }
   return (int)hipGetLastError();
 }
 
-DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* dy, void* dx, long long M, int C, const float* ctx,
-                         float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
+// dres: gradient w.r.t. the fused residual input (required when res != nullptr).
+DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres, long long M,
+                         int C, const float* ctx, float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256) return -1;
+  if (res) relu = 1;
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
   float* cdb = p2 + (long long)nblk * C;
   float* cdg = cdb + C;
-  const float *mean = ctx, *inv = ctx + C, *scale = ctx + 2 * C, *shift = ctx + 3 * C;
-#define BWD_PART(T, R) hipLaunchKernelGGL((bn_bwd_partial<T, R>), dim3(nblk), dim3(256), 0, s, (const T*)x, (const T*)dy, M, C, rpb, mean, inv, scale, shift, p1, p2)
-  if (dtype == 1) { if (relu) BWD_PART(bf16, true); else BWD_PART(bf16, false); }
-  else { if (relu) BWD_PART(float, true); else BWD_PART(float, false); }
-#undef BWD_PART
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb, cdg);
   const int ag = apply_grid(M, C);
-#define BWD_APPLY(T, R) hipLaunchKernelGGL((bn_bwd_apply<T, R>), dim3(ag), dim3(256), 0, s, (const T*)x, (const T*)dy, (T*)dx, M, C, mean, inv, scale, shift, cdb, cdg)
-  if (dtype == 1) { if (relu) BWD_APPLY(bf16, true); else BWD_APPLY(bf16, false); }
-  else { if (relu) BWD_APPLY(float, true); else BWD_APPLY(float, false); }
-#undef BWD_APPLY
+  if (dtype == 1) {
+    BN_DISPATCH3(bn_bwd_partial, bf16, relu, res, dim3(nblk), dim3(256), 0, s, (const bf16*)x, (const bf16*)res,
+                 (const bf16*)dy, M, C, rpb, ctx, p1, p2);
+  } else {
+    BN_DISPATCH3(bn_bwd_partial, float, relu, res, dim3(nblk), dim3(256), 0, s, (const float*)x, (const float*)res,
+                 (const float*)dy, M, C, rpb, ctx, p1, p2);
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
+                     cdg);
+  if (dtype == 1) {
+    BN_DISPATCH3(bn_bwd_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, (const bf16*)x, (const bf16*)res,
+                 (const bf16*)dy, (bf16*)dx, (bf16*)dres, M, C, ctx, cdb, cdg);
+  } else {
+    BN_DISPATCH3(bn_bwd_apply, float, relu, res, dim3(ag), dim3(256), 0, s, (const float*)x, (const float*)res,
+                 (const float*)dy, (float*)dx, (float*)dres, M, C, ctx, cdb, cdg);
+  }
   return (int)hipGetLastError();
 }

@@ -22,8 +22,10 @@ enum { OP_NOOP = 0, OP_SGD = 1, OP_NESTEROVS = 2, OP_ADAM = 3, OP_ADAMAX = 4, OP
 template <typename TS>
 __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __restrict__ segs, float* __restrict__ p,
                                                            float* __restrict__ g, float* __restrict__ st,
-                                                           TS* __restrict__ shadow, float inv_div, int write_update) {
+                                                           TS* __restrict__ shadow, float inv_div, int write_update,
+                                                           float* __restrict__ reg_out) {
   const SegDesc s = segs[blockIdx.y];
+  float reg = 0.f;   // l1*|p| + 0.5*l2*p^2 of the PRE-update params (the score's regularisation term)
   const long long stride = (long long)gridDim.x * blockDim.x;
   float* s1 = st + s.st_off + s.in_block;
   float* s2 = st + s.st_off + s.block_n + s.in_block;
@@ -80,17 +82,24 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
     }
     if (s.l2 > 0.f) u += s.l2 * pv;
     if (s.l1 > 0.f) u += s.l1 * ((pv > 0.f) - (pv < 0.f));
+    reg += s.l1 * fabsf(pv) + 0.5f * s.l2 * pv * pv;
     u *= inv_div;
     pv -= u;
     p[pi] = pv;
     if (shadow) st1<TS>(shadow + pi, pv);
     if (write_update) g[pi] = u;
   }
+  if (reg_out != nullptr && (s.l1 > 0.f || s.l2 > 0.f)) {
+    __shared__ float red[4];
+    reg = block_reduce<false>(reg, red);
+    if (threadIdx.x == 0) atomicAdd(reg_out, reg);
+  }
 }
 
 // segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (treated as bf16 layout not supported -> none)
 DL4J_API int dl4j_fused_update(const void* segs, int nseg, long long max_n, float* p, float* g, float* st,
-                               void* shadow, int shadow_kind, float inv_div, int write_update, hipStream_t stream) {
+                               void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
+                               hipStream_t stream) {
   if (nseg <= 0) return 0;
   long long bx = (max_n + 256 * 4 - 1) / (256 * 4);
   if (bx < 1) bx = 1;
@@ -98,10 +107,10 @@ DL4J_API int dl4j_fused_update(const void* segs, int nseg, long long max_n, floa
   dim3 grid((unsigned)bx, (unsigned)nseg);
   if (shadow_kind == 1)
     hipLaunchKernelGGL(fused_update_kernel<bf16>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
-                       (bf16*)shadow, inv_div, write_update);
+                       (bf16*)shadow, inv_div, write_update, reg_out);
   else
     hipLaunchKernelGGL(fused_update_kernel<float>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
-                       (float*)nullptr, inv_div, write_update);
+                       (float*)nullptr, inv_div, write_update, reg_out);
   return (int)hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 Planner: BatchNormalization -> ActivationLayer(ReLU) pairs where the BN output has a single consumer
 are fused so the HIP BN kernel applies the ReLU (ResNet-50: 49 such pairs).
 """
+import os
+
 import torch
 
 from ...datasets.dataset import DataSet, MultiDataSet
@@ -59,21 +61,66 @@ class ComputationGraph(BaseNetwork):
                 l.bind()
 
     def _plan_fusions(self):
+        """Graph-level fusion planner (MI355X: fewer HBM passes over the activations).
+
+        * BN -> ActivationLayer(ReLU)                      => ReLU inside the BN apply kernel
+        * BN -> ElementWiseVertex(Add, shortcut) -> ReLU   => y = relu(bn(x) + shortcut) in ONE kernel
+          (every ResNet bottleneck block); backward emits d(shortcut) from the same pass.
+        Fused-away vertices become passthroughs: forward copies the producer's activation, backward routes
+        epsilon to that single producer. Also computes which vertices need an input gradient at all
+        (nothing trainable upstream => skip dL/dinput, e.g. the stem conv's backward-data)."""
         from ..conf.activations import ActivationReLU
-        self._passthrough = set()
+        from ..conf.graph import ElementWiseVertex
+        self._passthrough = {}
+        self._residual_of = {}
+        pos = {n: i for i, n in enumerate(self.topo)}
+        for n in self.conf.networkInputs:
+            pos[n] = -1
+
+        def is_relu_layer(n):
+            vv = self.conf.vertices.get(n)
+            return isinstance(vv, LayerVertex) and isinstance(vv.layerConf, ActivationLayer) and \
+                isinstance(vv.layerConf.activation, ActivationReLU) and vv.preProcessor is None and \
+                vv.layerConf.idropout is None and len(self.vertex_inputs[n]) == 1
+
         for name in self.topo:
             v = self.conf.vertices[name]
             if not (isinstance(v, LayerVertex) and isinstance(v.layerConf, BatchNormalization)):
                 continue
+            if v.layerConf.idropout is not None:
+                continue
             cons = self.consumers[name]
             if len(cons) != 1 or name in self.outputs:
                 continue
-            nxt = self.conf.vertices[cons[0]]
-            if isinstance(nxt, LayerVertex) and isinstance(nxt.layerConf, ActivationLayer) and \
-                    isinstance(nxt.layerConf.activation, ActivationReLU) and nxt.preProcessor is None and \
-                    nxt.layerConf.idropout is None and v.layerConf.idropout is None and len(self.vertex_inputs[cons[0]]) == 1:
+            nxt_name = cons[0]
+            nxt = self.conf.vertices[nxt_name]
+            if isinstance(nxt, ElementWiseVertex) and nxt.op == "Add" and len(self.vertex_inputs[nxt_name]) == 2 \
+                    and nxt_name not in self.outputs and len(self.consumers[nxt_name]) == 1 \
+                    and is_relu_layer(self.consumers[nxt_name][0]) and os.environ.get("DL4J_AMD_FUSE_RES", "1") == "1":
+                ins = self.vertex_inputs[nxt_name]
+                other = ins[1] if ins[0] == name else ins[0]
+                relu_name = self.consumers[nxt_name][0]
+                if other != name and pos[other] < pos[name] and relu_name not in self.outputs:
+                    self.layers_by_name[name].fuse_relu = True
+                    self._residual_of[name] = other
+                    self._passthrough[nxt_name] = name
+                    self._passthrough[relu_name] = nxt_name
+                    continue
+            if is_relu_layer(nxt_name) and nxt_name not in self.outputs:
                 self.layers_by_name[name].fuse_relu = True
-                self._passthrough.add(cons[0])
+                self._passthrough[nxt_name] = name
+        # which vertices must produce an input gradient
+        flows = {n: False for n in self.conf.networkInputs}
+        self._need_input_grad = {}
+        for name in self.topo:
+            ins = self.vertex_inputs[name]
+            need = any(flows.get(i, False) for i in ins)
+            self._need_input_grad[name] = need
+            layer = self.layers_by_name.get(name)
+            own = layer is not None and layer.conf.numParams() > 0
+            flows[name] = need or own
+        for name, layer in self.layers_by_name.items():
+            layer.need_input_grad = self._need_input_grad[name]
 
     def getLayers(self):
         return list(self.layers_by_name.values())
@@ -131,17 +178,22 @@ class ComputationGraph(BaseNetwork):
                     if mask is not None:
                         mask, _ = v.preProcessor.feedForwardMaskArray(mask, None, mb)
                 if name in self._passthrough:
-                    acts[name] = x
+                    acts[name] = acts[self._passthrough[name]]
                     amask[name] = mask
                     continue
                 layer = self.layers_by_name[name]
                 layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
+                if name in self._residual_of:
+                    layer.residual = acts[self._residual_of[name]]
                 if stored_state and hasattr(layer, "tBpttStateMap"):
                     out = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
                 else:
                     out = layer.activate(x, train, mask)
                 acts[name] = out
                 amask[name], _ = layer.feedForwardMaskArray(mask, None, mb)
+            elif name in self._passthrough:
+                acts[name] = acts[self._passthrough[name]]
+                amask[name] = ms[0] if ms else None
             else:
                 from ..conf.graph import DuplicateToTimeSeriesVertex
                 if isinstance(v, DuplicateToTimeSeriesVertex):
@@ -179,25 +231,29 @@ class ComputationGraph(BaseNetwork):
         self._begin_backward()
         for name in reversed(self.topo):
             v = self.conf.vertices[name]
+            if name in self._passthrough:
+                add(self._passthrough[name], eps_acc.pop(name, None))
+                continue
             if isinstance(v, LayerVertex):
                 layer = self.layers_by_name.get(name)
                 if name in self.outputs and isinstance(layer, BaseOutputLayerImpl):
                     _, e = layer.backpropGradient(None)
                     self._grad_ready(name)
-                    if name in eps_acc:
-                        e = e + eps_acc.pop(name) if e is not None else eps_acc.pop(name)
-                elif name in self._passthrough:
-                    e = eps_acc.pop(name, None)
                 else:
                     e_in = eps_acc.pop(name, None)
                     if e_in is None:
+                        continue
+                    if not self._need_input_grad[name] and layer.conf.numParams() == 0:
                         continue
                     if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
                         _, e = layer.backpropGradient(e_in, tbptt_back=tbptt_back)
                     else:
                         _, e = layer.backpropGradient(e_in)
                     self._grad_ready(name)
-                if e is None:
+                    if name in self._residual_of:
+                        add(self._residual_of[name], layer.dresidual)
+                        layer.dresidual = None
+                if e is None or not self._need_input_grad[name]:
                     continue
                 if v.preProcessor is not None:
                     e = v.preProcessor.backprop(e, self._mb)
@@ -210,7 +266,7 @@ class ComputationGraph(BaseNetwork):
                     add(ins[0], e)
             else:
                 e_in = eps_acc.pop(name, None)
-                if e_in is None:
+                if e_in is None or not self._need_input_grad[name]:
                     continue
                 es = v.backward(e_in, self._ctx[name][1])
                 for i, ei in zip(self.vertex_inputs[name], es):
@@ -222,7 +278,7 @@ class ComputationGraph(BaseNetwork):
         return self._input_eps
 
     def computeGradientAndScore(self, inputs=None, labels=None, fmasks=None, lmasks=None, stored_state=False,
-                                store_last_for_tbptt=False, tbptt_back=None):
+                                store_last_for_tbptt=False, tbptt_back=None, defer_reg=False):
         inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
         labels = self.labels if labels is None else labels
         if torch.is_tensor(labels):
@@ -240,12 +296,13 @@ class ComputationGraph(BaseNetwork):
             if lm is not None:
                 layer.maskArray = self._to_dev(lm)
         self._backprop(tbptt_back)
-        l1, l2 = self._regularization_terms()
+        l1, l2 = (0.0, 0.0) if defer_reg else self._regularization_terms()
         score = None
         for i, o in enumerate(self.outputs):
             layer = self.layers_by_name[o]
             s = layer.computeScore(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0, True)
             score = s if score is None else score + s
+        self._loss_part = score
         self._score_t = score
         self._score_val = None
         return score
@@ -254,7 +311,7 @@ class ComputationGraph(BaseNetwork):
         x0 = inputs[0] if isinstance(inputs, (list, tuple)) else inputs
         if self.conf.backpropType == BackpropType.TruncatedBPTT and x0.dim() == 3:
             return self._fit_tbptt(inputs, labels, fmasks, lmasks)
-        self.computeGradientAndScore(inputs, labels, fmasks, lmasks)
+        self.computeGradientAndScore(inputs, labels, fmasks, lmasks, defer_reg=True)
         self._apply_update(x0.shape[0])
         self._iteration_done()
 
@@ -271,7 +328,7 @@ class ComputationGraph(BaseNetwork):
             fm = [m[:, t0:t1] if m is not None else None for m in fmasks] if fmasks else None
             lm = [m[:, t0:t1] if m is not None else None for m in lmasks] if lmasks else None
             self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
-                                         tbptt_back=back)
+                                         tbptt_back=back, defer_reg=True)
             self._apply_update(inputs[0].shape[0])
             self._iteration_done()
         self.rnnClearPreviousState()
@@ -377,15 +434,18 @@ class ComputationGraph(BaseNetwork):
         with torch.no_grad():
             for name in self.topo:
                 v = self.conf.vertices[name]
+                if name in self._passthrough:
+                    acts[name] = acts[self._passthrough[name]]
+                    continue
                 ins = [acts[i] for i in self.vertex_inputs[name]]
                 if isinstance(v, LayerVertex):
                     x = ins[0] if len(ins) == 1 else torch.cat(ins, 1)
                     if v.preProcessor is not None:
                         x = v.preProcessor.preProcess(x, x.shape[0], False)
                     layer = self.layers_by_name[name]
-                    if name in self._passthrough:
-                        acts[name] = x
-                    elif hasattr(layer, "rnnTimeStep"):
+                    if name in self._residual_of:
+                        layer.residual = acts[self._residual_of[name]]
+                    if hasattr(layer, "rnnTimeStep"):
                         acts[name] = layer.rnnTimeStep(x)
                     else:
                         acts[name] = layer.activate(x, False)

@@ -90,10 +90,15 @@ class ConvolutionLayerImpl(LayerImpl):
         s, pad4, d = self._geom_cache
         W = self.W("W")
         xt = _cl(self._xt.to(W.dtype))
-        dx, dW, db = ops.conv2d_backward(xt, W, _cl(delta.to(W.dtype)), s, pad4, d, True, True, "b" in self.grads)
-        copy_grad_(self.grads["W"], _acc(dW))
-        if "b" in self.grads:
-            copy_grad_(self.grads["b"], _acc(db))
+        need_dx = getattr(self, "need_input_grad", True)
+        dx, dW, db = ops.conv2d_backward(xt, W, _cl(delta.to(W.dtype)), s, pad4, d, need_dx, True,
+                                         "b" in self.grads, gW=self.grads["W"], gb=self.grads.get("b"))
+        if dW is not None:
+            copy_grad_(self.grads["W"], dW)
+        if "b" in self.grads and db is not None:
+            copy_grad_(self.grads["b"], db)
+        if not need_dx:
+            return self.make_gradient(), None
         if dx.shape[2:] != self.input.shape[2:]:
             full = torch.zeros(self.input.shape, dtype=dx.dtype, device=dx.device)
             full[:, :, :dx.shape[2], :dx.shape[3]] = dx

@@ -36,6 +36,8 @@ class DenseLayerImpl(LayerImpl):
             copy_grad_(self.grads["W"], _acc(torch.matmul(x.t(), delta)))
         if "b" in self.grads:
             copy_grad_(self.grads["b"], _acc(delta).sum(dim=0))
+        if not getattr(self, "need_input_grad", True):
+            return self.make_gradient(), None
         W = self.W("W")
         eps_prev = torch.matmul(delta.to(W.dtype), W.t())
         eps_prev = self.backpropDropOut(eps_prev)

@@ -36,12 +36,14 @@ class BatchNormalizationImpl(LayerImpl):
         g, b = self._gb()
         c = self.conf
         # the reference BN layer applies no activation function of its own (BatchNormalization.java:225,398)
+        res = getattr(self, "residual", None)
         y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
-                                      relu=self.fuse_relu)
+                                      relu=self.fuse_relu, residual=res)
+        self.residual = None
         return y
 
     def backpropGradient(self, eps):
-        dx, dgamma, dbeta = ops.bn_backward(eps, self._ctx)
+        dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx)
         if "gamma" in self.grads:
             copy_grad_(self.grads["gamma"], dgamma)
             copy_grad_(self.grads["beta"], dbeta)

@@ -51,6 +51,10 @@ class MultiLayerNetwork(BaseNetwork):
                 if a.idropout is None:
                     self.layers[i].fuse_relu = True
                     self._fused_passthrough.add(i + 1)
+        seen_params = False
+        for l in self.layers:
+            l.need_input_grad = seen_params       # nothing trainable upstream => skip dL/dinput
+            seen_params = seen_params or l.conf.numParams() > 0
 
     def getLayers(self):
         return self.layers
@@ -163,7 +167,7 @@ class MultiLayerNetwork(BaseNetwork):
         return eps
 
     def computeGradientAndScore(self, x=None, y=None, fmask=None, lmask=None, stored_state=False,
-                                store_last_for_tbptt=False, tbptt_back=None):
+                                store_last_for_tbptt=False, tbptt_back=None, defer_reg=False):
         x = self.input if x is None else x
         y = self.labels if y is None else y
         fmask = self.mask if fmask is None else fmask
@@ -181,15 +185,19 @@ class MultiLayerNetwork(BaseNetwork):
         elif fmask is not None and out.maskArray is None:
             out.maskArray = self._to_dev(fmask)
         self._backprop(tbptt_back)
-        l1, l2 = self._regularization_terms()
-        self._score_t = out.computeScore(l1, l2, True)
+        if defer_reg:      # regularisation term comes out of the fused updater kernel (see _apply_update)
+            self._loss_part = out.computeScore(0.0, 0.0, True)
+            self._score_t = self._loss_part
+        else:
+            l1, l2 = self._regularization_terms()
+            self._score_t = out.computeScore(l1, l2, True)
         self._score_val = None
         return self._score_t
 
     def _fit_batch(self, x, y, fmask=None, lmask=None):
         if self.conf.backpropType == BackpropType.TruncatedBPTT and x.dim() == 3:
             return self._fit_tbptt(x, y, fmask, lmask)
-        self.computeGradientAndScore(x, y, fmask, lmask)
+        self.computeGradientAndScore(x, y, fmask, lmask, defer_reg=True)
         self._apply_update(x.shape[0])
         self._iteration_done()
 
@@ -207,7 +215,7 @@ class MultiLayerNetwork(BaseNetwork):
             fm = fmask[:, t0:t1] if fmask is not None else None
             lm = lmask[:, t0:t1] if lmask is not None else None
             self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
-                                         tbptt_back=back)
+                                         tbptt_back=back, defer_reg=True)
             self._apply_update(x.shape[0])
             self._iteration_done()
         self.rnnClearPreviousState()

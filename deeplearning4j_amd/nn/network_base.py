@@ -280,7 +280,15 @@ class BaseNetwork:
         if acc is not None:
             acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
             batch_size = batch_size * acc.world_size
-        self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow)
+        mb_local = batch_size if acc is None else batch_size // acc.world_size
+        reg = None
+        if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
+            reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)
+        self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow, reg)
+        if getattr(self, "_loss_part", None) is not None:
+            self._score_t = self._loss_part + (reg[0] / mb_local if reg is not None else 0.0)
+            self._loss_part = None
+            self._score_val = None
         for _, _, impl, _ in self._layer_offsets:
             if getattr(impl.conf, "constraints", None):
                 impl.applyConstraints(it, ep)

@@ -134,12 +134,12 @@ class NetworkUpdater:
                     n = v.norm()
                     v.mul_(torch.clamp(thr / n, max=1.0))
 
-    def update(self, params, grad, iteration, epoch, batch_size, shadow=None):
+    def update(self, params, grad, iteration, epoch, batch_size, shadow=None, reg_out=None):
         """Apply the whole update (preApply -> updater -> l1/l2 -> /batch -> params -= u) in place."""
         if self._gn_layers:
             self.preApply(grad)
         fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
-                     self.net.conf.globalConf.get("miniBatch", True), shadow)
+                     self.net.conf.globalConf.get("miniBatch", True), shadow, reg_out=reg_out)
 
     # learning-rate control (reference MultiLayerNetwork.setLearningRate :3411-3459)
     def setLearningRate(self, lr, layer_name=None):

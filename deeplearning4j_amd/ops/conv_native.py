@@ -8,5 +8,5 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return None
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None):
     return None

@@ -29,17 +29,17 @@ def load():
     lib = ctypes.CDLL(KERNEL_LIB)
     sigs = {
         "dl4j_fused_update": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int,
-                              c_void_p],
+                              c_void_p, c_void_p],
         "dl4j_segdesc_size": [],
         "dl4j_bn_workspace_floats": [c_ll, c_int],
-        "dl4j_bn_fwd": [c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_float, c_float, c_void_p,
-                        c_void_p, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
-        "dl4j_bn_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                        c_void_p, c_void_p],
+        "dl4j_bn_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_float, c_float,
+                        c_void_p, c_void_p, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
+        "dl4j_bn_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
+                        c_void_p, c_int, c_void_p, c_void_p],
         "dl4j_softmax_xent": [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
                               c_void_p],
-        "dl4j_pool_fwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 13 + [c_void_p],
-        "dl4j_pool_bwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 13 + [c_void_p],
+        "dl4j_pool_fwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p],
+        "dl4j_pool_bwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p],
     }
     for name, args in sigs.items():
         f = getattr(lib, name)
@@ -114,7 +114,7 @@ _SEG_DTYPE = np.dtype([("p_off", "<i8"), ("n", "<i8"), ("st_off", "<i8"), ("in_b
                        ("op", "<i4"), ("pad", "<i4"), ("h", "<f4", 4), ("l1", "<f4"), ("l2", "<f4")])
 
 
-def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update):
+def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out=None):
     lib = load()
     if lib.dl4j_segdesc_size() != _SEG_DTYPE.itemsize:
         raise RuntimeError("SegDesc layout mismatch between python and HIP")
@@ -139,13 +139,22 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
             return False
         sk = 1
     rc = lib.dl4j_fused_update(_ptr(cache.dev), len(segs), max_n, _ptr(params), _ptr(grad), _ptr(state),
-                               _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _stream())
+                               _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out), _stream())
     _check(rc, "fused_update")
     return True
 
 
 # ------------------------------------------------------------------------------------------ batch norm
-def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu):
+def _rows_like(t, ref):
+    """``t`` as [M, C] rows in the same memory layout as ``ref`` (converting if needed)."""
+    if t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    elif t.dim() == 2 and not t.is_contiguous():
+        t = t.contiguous()
+    return t.to(ref.dtype)
+
+
+def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual=None):
     dt = _dt(x)
     xr = _as_rows_nhwc(x) if dt is not None else None
     if xr is None:
@@ -159,27 +168,28 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu):
     ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
     g = gamma if torch.is_tensor(gamma) else None
     b = beta if torch.is_tensor(beta) else None
-    rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(y), M, C, _ptr(g), _ptr(b), float(gamma) if g is None else 1.0,
-                         float(beta) if b is None else 0.0, _ptr(run_mean), _ptr(run_var), float(decay), float(eps),
-                         1 if training else 0, 1 if relu else 0, _ptr(ws), _ptr(ctx), _stream())
+    res = _rows_like(residual, x) if residual is not None else None
+    rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
+                         float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
+                         _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
+                         _ptr(ctx), _stream())
     _check(rc, "bn_fwd")
-    return y, ("NATIVE", x, ctx, relu, M, C)
+    return y, ("NATIVE", x, ctx, relu, M, C, res)
 
 
 def bn_bwd(dy, ctx):
-    _, x, c, relu, M, C = ctx
-    if not dy.is_contiguous(memory_format=torch.channels_last if dy.dim() == 4 else torch.contiguous_format):
-        dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
-    dy = dy.to(x.dtype)
+    _, x, c, relu, M, C, res = ctx
+    dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
+    dres = _like_rows(x) if res is not None else None
     dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
     dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
-    rc = lib.dl4j_bn_bwd(_dt(x), _ptr(_as_rows_nhwc(x)), _ptr(_as_rows_nhwc(dy)), _ptr(dx), M, C, _ptr(c),
-                         _ptr(dgamma), _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())
+    rc = lib.dl4j_bn_bwd(_dt(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
+                         _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())
     _check(rc, "bn_bwd")
-    return dx, dgamma, dbeta
+    return dx, dgamma, dbeta, dres
 
 
 # ------------------------------------------------------------------------------------------ softmax-xent
@@ -236,9 +246,9 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation)
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None):
     from . import conv_native
-    return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
+    return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb)
 
 
 def lstm_cell_fwd(z, c):

@@ -22,12 +22,14 @@ def _bshape(x):
     return (1, -1) if x.dim() == 2 else (1, -1, 1, 1)
 
 
-def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=False):
+def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=False, residual=None):
     """Returns (y, ctx). gamma/beta may be python floats (lockGammaBeta). Running stats updated in place
-    when training."""
-    if use_native(x, "bn") and x.dim() == 4 and torch.is_tensor(gamma):
+    when training. ``residual``: fused shortcut, y = relu(bn(x) + residual) (relu implied)."""
+    if residual is not None:
+        relu = True
+    if use_native(x, "bn") and x.dim() in (2, 4) and torch.is_tensor(gamma):
         from . import native
-        r = native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu)
+        r = native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual)
         if r is not None:
             return r
     xf = _acc(x)
@@ -47,20 +49,23 @@ def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=Fal
     b = _acc(beta.reshape(-1)) if torch.is_tensor(beta) else torch.full_like(mean, float(beta))
     xhat = (xf - mean.reshape(bs)) * invstd.reshape(bs)
     y = xhat * g.reshape(bs) + b.reshape(bs)
+    if residual is not None:
+        y = y + _acc(residual)
     if relu:
         y = torch.relu(y)
     y = y.to(x.dtype)
     if x.dim() == 4 and x.is_cuda:
         y = y.contiguous(memory_format=torch.channels_last)
-    return y, ("REF", x, mean, invstd, g, b, relu, y if relu else None)
+    return y, ("REF", x, mean, invstd, g, b, relu, y if relu else None, residual is not None)
 
 
 def bn_backward(dy, ctx):
-    """Returns (dx, dgamma, dbeta) — dgamma/dbeta are sums over the batch (not averaged)."""
+    """Returns (dx, dgamma, dbeta, dresidual) — dgamma/dbeta are sums over the batch (not averaged);
+    dresidual is None unless the forward fused a residual."""
     if ctx[0] == "NATIVE":
         from . import native
         return native.bn_bwd(dy, ctx)
-    _, x, mean, invstd, g, b, relu, y = ctx
+    _, x, mean, invstd, g, b, relu, y, has_res = ctx
     dims = _dims(x)
     bs = _bshape(x)
     dyf = _acc(dy)
@@ -74,7 +79,8 @@ def bn_backward(dy, ctx):
     dx = dx.to(dy.dtype)
     if x.dim() == 4 and x.is_cuda:
         dx = dx.contiguous(memory_format=torch.channels_last)
-    return dx, dgamma, dbeta
+    dres = dyf.to(dy.dtype) if has_res else None
+    return dx, dgamma, dbeta, dres
 
 
 def bn_forward_inference_only(x, gamma, beta, run_mean, run_var, relu=False):

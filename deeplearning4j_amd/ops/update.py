@@ -45,14 +45,25 @@ class UpdatePlan:
 
 
 def fused_update(plan, params, grad, state, iteration, epoch, batch_size, mini_batch=True, shadow=None,
-                 write_update=True):
-    """params/grad/state: flat 1-D fp32 (or fp64) tensors. shadow: optional bf16 flat copy of params."""
+                 write_update=True, reg_out=None):
+    """params/grad/state: flat 1-D fp32 (or fp64) tensors. shadow: optional bf16 flat copy of params.
+    reg_out: optional zeroed 1-element tensor that receives sum(l1*|p| + 0.5*l2*p^2) of the pre-update
+    params (the score's regularisation term) — computed inside the same kernel pass on GPU."""
     div = float(batch_size) if mini_batch else 1.0
     if use_native(params, "update") and params.dtype == torch.float32:
         from . import native
-        if native.fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update):
+        if native.fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out):
             return
     with torch.no_grad():
+        if reg_out is not None:
+            r = torch.zeros((), dtype=params.dtype, device=params.device)
+            for s in plan.segments:
+                if s.l1 > 0 or s.l2 > 0:
+                    p = params[s.p_off:s.p_off + s.n]
+                    r = r + s.l1 * p.abs().sum() + 0.5 * s.l2 * (p * p).sum()
+            reg_out.fill_(r.item() if reg_out.device.type == "cpu" else 0.0)
+            if reg_out.device.type != "cpu":
+                reg_out.copy_(r.reshape(reg_out.shape))
         for (p0, p1, st_off, upd) in plan.blocks:
             if p1 <= p0:
                 continue

@@ -36,7 +36,7 @@ def test_batchnorm_fwd_bwd(cuda, dtype, relu, shape):
     rm_c, rv_c = torch.zeros(C), torch.ones(C)
     xr = x.to(dtype)
     y_ref, ctx_ref = ops.bn_forward(xr.float(), gamma, beta, rm_c, rv_c, True, 0.9, 1e-5, relu)
-    dx_ref, dg_ref, db_ref = ops.bn_backward(dy.to(dtype).float(), ctx_ref)
+    dx_ref, dg_ref, db_ref, _ = ops.bn_backward(dy.to(dtype).float(), ctx_ref)
     xd = xr.to(cuda)
     if xd.dim() == 4:
         xd = xd.contiguous(memory_format=torch.channels_last)
@@ -50,7 +50,7 @@ def test_batchnorm_fwd_bwd(cuda, dtype, relu, shape):
     dyd = dy.to(dtype).to(cuda)
     if dyd.dim() == 4:
         dyd = dyd.contiguous(memory_format=torch.channels_last)
-    dx, dgm, dbt = ops.bn_backward(dyd, ctx)
+    dx, dgm, dbt, _ = ops.bn_backward(dyd, ctx)
     _close(dx, dx_ref, tol * 2)
     _close(dgm, dg_ref, 1e-3 if dtype == torch.float32 else 3e-2)
     _close(dbt, db_ref, 1e-3 if dtype == torch.float32 else 3e-2)
@@ -145,3 +145,27 @@ def test_lenet_gpu_matches_cpu(cuda):
         b.fit(x.reshape(16, -1), y)
     _close(b.params(), a.params(), 2e-3)
     assert abs(a.score() - b.score()) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_batchnorm_residual_relu_fused(cuda, dtype):
+    g = torch.Generator().manual_seed(7)
+    shape = (4, 64, 6, 5)
+    x = (torch.randn(*shape, generator=g) * 2 + 0.5).to(dtype)
+    r = torch.randn(*shape, generator=g).to(dtype)
+    dy = torch.randn(*shape, generator=g).to(dtype)
+    gamma, beta = torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g)
+    y_ref, c_ref = ops.bn_forward(x.float(), gamma, beta, torch.zeros(64), torch.ones(64), True, 0.9, 1e-5,
+                                  residual=r.float())
+    dx_ref, dg_ref, db_ref, dr_ref = ops.bn_backward(dy.float(), c_ref)
+    cl = lambda t: t.to(cuda).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    y, c = ops.bn_forward(cl(x), gamma.to(cuda), beta.to(cuda), torch.zeros(64, device=cuda),
+                          torch.ones(64, device=cuda), True, 0.9, 1e-5, residual=cl(r))
+    assert c[0] == "NATIVE"
+    dx, dgm, dbt, dr = ops.bn_backward(cl(dy), c)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, y_ref, tol)
+    _close(dx, dx_ref, 2 * tol)
+    _close(dr, dr_ref, tol)
+    _close(dgm, dg_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)
+    _close(dbt, db_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)

@@ -218,6 +218,29 @@ def test_cg_l2_vertex_stack_unstack():
     assert checkGradients(net, input=[a, b], labels=[torch.randn(3, 1, dtype=torch.float64)], print_results=True)
 
 
+def test_fused_bn_add_relu_residual():
+    """ResNet bottleneck tail: BN -> Add(shortcut) -> ReLU is planned into ONE fused BN kernel."""
+    conf = (NeuralNetConfiguration.Builder().seed(3).dataType(DataType.DOUBLE).updater(NoOp())
+            .weightInit(NormalDistribution(0, 0.5)).activation(Activation.IDENTITY)
+            .convolutionMode(ConvolutionMode.Same).graphBuilder()
+            .addInputs("in").setInputTypes(InputType.convolutional(4, 4, 3))
+            .addLayer("c0", ConvolutionLayer.Builder([1, 1]).nOut(4).build(), "in")
+            .addLayer("c1", ConvolutionLayer.Builder([3, 3]).nOut(4).build(), "c0")
+            .addLayer("bn1", BatchNormalization(), "c1")
+            .addVertex("add", ElementWiseVertex(ElementWiseVertex.Op.Add), "bn1", "c0")
+            .addLayer("relu", ActivationLayer(Activation.RELU), "add")
+            .addLayer("out", OutputLayer.Builder(LossFunction.MSE).nOut(2).activation(Activation.IDENTITY).build(),
+                      "relu")
+            .setOutputs("out").build())
+    net = ComputationGraph(conf)
+    net.init(device=DEV)
+    assert net._residual_of == {"bn1": "c0"}
+    assert net._passthrough == {"add": "bn1", "relu": "add"}
+    x = torch.randn(3, 3, 4, 4, dtype=torch.float64)
+    y = torch.randn(3, 2, dtype=torch.float64)
+    assert checkGradients(net, input=[x], labels=[y], print_results=True, minAbsoluteError=1e-7)
+
+
 def test_resnet_style_residual_graph():
     conf = (NeuralNetConfiguration.Builder().seed(1).dataType(DataType.DOUBLE).updater(NoOp())
             .weightInit(NormalDistribution(0, 0.5)).activation(Activation.IDENTITY)
