@@ -1,0 +1,463 @@
+// Implicit-GEMM convolution on MFMA (gfx950 / CDNA4), NHWC bf16 activations, fp32 accumulation.
+//
+// Replaces the reference's im2col + GEMM path (ConvolutionLayer.java:385-417 forward, :215-257 backward) and
+// the cuDNN helper (CudnnConvolutionHelper.java:297-306,424-470) with three kernels that never materialise
+// im2col in HBM:
+//
+//   FWD   D[n][m]  = sum_k Wkrsc[n][k] * im2col(X)[m][k]      (+bias[n])  -> Y[m][n]        (NHWC)
+//   BWD-D D[c][m'] = sum_k Wflip[c][k] * im2col(dY)[m'][k]               -> dX[m'][c]
+//         (stride-1: transposed conv = conv of dY with the flipped CRSK weights and pad' = R-1-pad;
+//          1x1 stride-s: plain GEMM over dY rows + strided scatter of the output rows)
+//   WRW   dW[k][rsc] = sum_m dY[m][k] * im2col(X)[m][rsc]   (split over m, fp32 atomics straight into the
+//         network's flat fp32 gradient in DL4J's [K][C][R][S] order; conv-bias gradient fused as column sums)
+//
+// GEMM core: 256 threads = 4 waves in a 2x2 arrangement, block tile 128(n) x 128(m) x 32(k), each wave a
+// 64x64 sub-tile = 2x2 v_mfma_f32_32x32x16_bf16 accumulators. Operand tiles are register-staged into a
+// double-buffered LDS ring (global loads for step k+1 are issued before the MFMAs of step k). K-contiguous
+// tiles use an XOR chunk swizzle so every ds_read_b128 lane group hits 16 distinct bank slots; the WRW tiles
+// (m-contiguous) are read with ds_read_b64_tr_b16 (hardware transpose) from rows padded to 320 B, which makes
+// the 4 rows of each half-wave read land on disjoint banks. Block ids are remapped so that consecutive tiles
+// (sharing the weight panel) run on the same XCD (T1).
+#include "common.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+struct ConvGeom {
+  int N, H, W, C;       // input image (NHWC)
+  int OH, OW, K;        // output image / out channels
+  int R, S, sh, sw, ph, pw, dh, dw;
+};
+
+#define TILE_N 128
+#define TILE_M 128
+#define TILE_K 32
+#define NTHREADS 256
+
+// bijective XCD-aware remap of a linear block id (guide §5, "XCD swizzle must be bijective")
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// byte offset of (row, 16-byte chunk) in a swizzled [rows][4 chunks] K-contiguous tile
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// ------------------------------------------------------------------------------------------------------
+// FWD / BWD-DATA kernel.  A operand = weight rows [Nout][Kred] (K contiguous), B operand = im2col pixels.
+//   geometry g describes the "input" image the im2col reads (X for fwd, dY for bwd-data) and the output grid.
+//   scatter > 0: 1x1 bwd-data with stride `scatter`: output pixel m=(n,oh,ow) goes to row (n, oh*s, ow*s) of
+//   an image with dims (g.OH*s', g.OW*s') given by out_H/out_W.
+// ------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                                                              const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                              ConvGeom g, int Kred, int scatter, int out_H, int out_W) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_N * TILE_K * 2];   // 2 buffers x (A + B) = 32 KB
+  const int M = g.N * g.OH * g.OW;
+  const int Nout = g.K;
+  const int tiles_m = (M + TILE_M - 1) / TILE_M;
+  const int tiles_n = (Nout + TILE_N - 1) / TILE_N;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // n-major inside an XCD chunk: consecutive blocks share the pixel panel? -> pixel panels are bigger, so
+  // iterate n fastest to reuse the im2col tile from L2 across the Nout tiles.
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  if (tm >= tiles_m) return;
+  const int n0 = tn * TILE_N, m0 = tm * TILE_M;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 1, wm = wid & 1;
+
+  // ---- per-thread load assignment: 2 rows (r0, r0+64) x chunk c of each 128x32 tile
+  const int lrow = tid >> 2, lchunk = tid & 3;
+  // weight rows
+  const bf16* wrow[2];
+  bool wok[2];
+  for (int i = 0; i < 2; ++i) {
+    const int n = n0 + lrow + 64 * i;
+    wok[i] = n < Nout;
+    wrow[i] = Wt + (long long)(wok[i] ? n : 0) * Kred;
+  }
+  // pixel rows: (image n, ih0, iw0)
+  int pn[2], pih[2], piw[2];
+  bool pok[2];
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    pok[i] = m < M;
+    const int mm = pok[i] ? m : 0;
+    const int ow = mm % g.OW, t = mm / g.OW;
+    const int oh = t % g.OH;
+    pn[i] = t / g.OH;
+    pih[i] = oh * g.sh - g.ph;
+    piw[i] = ow * g.sw - g.pw;
+  }
+  // k -> (r, s, c) decomposition of this thread's chunk, advanced by TILE_K every step
+  int kc = lchunk * 8;
+  int cc = kc % g.C, rs = kc / g.C;
+  int rr = rs / g.S, ss = rs % g.S;
+
+  f32x16_t acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  uint4 wreg[2], xreg[2];
+  const int nk = (Kred + TILE_K - 1) / TILE_K;
+
+  auto gload = [&](int kt) {
+    const int k = kt * TILE_K + kc;
+    const bool kin = k < Kred;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (wok[i] && kin) wreg[i] = *reinterpret_cast<const uint4*>(wrow[i] + k);
+      else wreg[i] = make_uint4(0, 0, 0, 0);
+      const int ih = pih[i] + rr * g.dh, iw = piw[i] + ss * g.dw;
+      if (pok[i] && kin && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+        xreg[i] = *reinterpret_cast<const uint4*>(X + (((long long)pn[i] * g.H + ih) * g.W + iw) * g.C + cc);
+      else xreg[i] = make_uint4(0, 0, 0, 0);
+    }
+    // advance (r, s, c) by TILE_K for the next step
+    cc += TILE_K;
+    while (cc >= g.C) { cc -= g.C; if (++ss == g.S) { ss = 0; ++rr; } }
+  };
+  auto sstore = [&](int buf) {
+    char* A = smem + buf * (2 * TILE_N * TILE_K * 2);
+    char* B = A + TILE_N * TILE_K * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = lrow + 64 * i;
+      *reinterpret_cast<uint4*>(A + swz(row, lchunk)) = wreg[i];
+      *reinterpret_cast<uint4*>(B + swz(row, lchunk)) = xreg[i];
+    }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* A = smem + buf * (2 * TILE_N * TILE_K * 2);
+    const char* B = A + TILE_N * TILE_K * 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 2 + (lane >> 5);
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int row = wn * 64 + a * 32 + (lane & 31);
+        af[a] = *reinterpret_cast<const bf16x8_t*>(A + swz(row, chunk));
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int row = wm * 64 + b * 32 + (lane & 31);
+        bfr[b] = *reinterpret_cast<const bf16x8_t*>(B + swz(row, chunk));
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: D[n][m] -> Y[row(m)][n], 4 consecutive channels per 8-byte store
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int m = m0 + wm * 64 + b * 32 + (lane & 31);
+    if (m >= M) continue;
+    long long orow;
+    if (scatter > 0) {
+      const int ow = m % g.OW, t = m / g.OW;
+      const int oh = t % g.OH, n = t / g.OH;
+      orow = ((long long)n * out_H + oh * scatter) * out_W + ow * scatter;
+    } else {
+      orow = m;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * 64 + a * 32 + 8 * q + 4 * hh;
+        if (n >= Nout) continue;
+        u16 o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = acc[a][b][4 * q + j];
+          if (bias) v += bias[n + j];
+          o[j] = f2bf(v);
+        }
+        uint2 pk;
+        pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+        pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+        *reinterpret_cast<uint2*>(Y + orow * Nout + n) = pk;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// WRW: dW[k][rsc] += sum_m dY[m][k] * im2col(X)[m][rsc] over this block's m-range (split-K over pixels).
+// Tiles are m-major ([32 m][128 cols], rows padded to 320 B) and read with ds_read_b64_tr_b16.
+// ------------------------------------------------------------------------------------------------------
+#define WRW_ROW 320
+
+__global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                              float* __restrict__ dW, float* __restrict__ db,
+                                                              ConvGeom g, int m_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_K * WRW_ROW];   // 2 buffers x (A + B) = 40 KB
+  const int M = g.N * g.OH * g.OW;
+  const int Kout = g.K;
+  const int RSC = g.R * g.S * g.C;
+  const int tiles_k = (Kout + TILE_N - 1) / TILE_N;
+  const int tk = blockIdx.x % tiles_k, tj = blockIdx.x / tiles_k;
+  const int k0 = tk * TILE_N, j0 = tj * TILE_M;
+  const int mbeg = blockIdx.y * m_per_split;
+  int mend = mbeg + m_per_split;
+  if (mend > M) mend = M;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid >> 1, wj = wid & 1;
+
+  // loads: 32 rows x 16 chunks per tile; thread -> rows (tid>>4) and (tid>>4)+16, chunk tid&15
+  const int lrow = tid >> 4, lchunk = tid & 15;
+  const int kcol = k0 + lchunk * 8;
+  const bool kok = kcol < Kout;
+  // fixed im2col column chunk (r, s, c) of this thread
+  const int jcol = j0 + lchunk * 8;
+  const bool jok = jcol < RSC;
+  const int jc = jok ? jcol : 0;
+  const int cc = jc % g.C, rs = jc / g.C;
+  const int rr = rs / g.S, ss = rs % g.S;
+  // running pixel coordinates of the two rows
+  int pm[2], pn[2], poh[2], pow_[2];
+  for (int i = 0; i < 2; ++i) {
+    pm[i] = mbeg + lrow + 16 * i;
+    const int mm = pm[i] < M ? pm[i] : 0;
+    pow_[i] = mm % g.OW;
+    const int t = mm / g.OW;
+    poh[i] = t % g.OH;
+    pn[i] = t / g.OH;
+  }
+  float bsum[8];
+  const bool do_bias = (db != nullptr) && (tj == 0);
+  for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
+
+  f32x16_t acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+  uint4 areg[2], breg[2];
+  const int nsteps = (mend - mbeg + TILE_K - 1) / TILE_K;
+
+  auto gload = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool mok = pm[i] < mend;
+      if (mok && kok) areg[i] = *reinterpret_cast<const uint4*>(dY + (long long)pm[i] * Kout + kcol);
+      else areg[i] = make_uint4(0, 0, 0, 0);
+      const int ih = poh[i] * g.sh - g.ph + rr * g.dh, iw = pow_[i] * g.sw - g.pw + ss * g.dw;
+      if (mok && jok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
+        breg[i] = *reinterpret_cast<const uint4*>(X + (((long long)pn[i] * g.H + ih) * g.W + iw) * g.C + cc);
+      else breg[i] = make_uint4(0, 0, 0, 0);
+      if (do_bias && mok && kok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned w = e == 0 ? areg[i].x : e == 1 ? areg[i].y : e == 2 ? areg[i].z : areg[i].w;
+          bsum[2 * e] += bf2f((u16)(w & 0xffff));
+          bsum[2 * e + 1] += bf2f((u16)(w >> 16));
+        }
+      }
+      // advance this row by 32 pixels
+      pm[i] += TILE_K;
+      pow_[i] += TILE_K;
+      while (pow_[i] >= g.OW) { pow_[i] -= g.OW; if (++poh[i] == g.OH) { poh[i] = 0; ++pn[i]; } }
+    }
+  };
+  auto sstore = [&](int buf) {
+    char* A = smem + buf * (2 * TILE_K * WRW_ROW);
+    char* B = A + TILE_K * WRW_ROW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = lrow + 16 * i;
+      *reinterpret_cast<uint4*>(A + row * WRW_ROW + lchunk * 16) = areg[i];
+      *reinterpret_cast<uint4*>(B + row * WRW_ROW + lchunk * 16) = breg[i];
+    }
+  };
+  // transposed fragment read: lanes of 16-group gi read rows kb+4t+q, cols colbase+4p (see T10)
+  const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  auto frag = [&](const char* T, int colbase, int ks) -> bf16x8_t {
+    const int col = colbase + (grp & 1) * 16 + 4 * p;
+    const int r0 = ks * 16 + (grp >> 1) * 8 + q;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + r0 * WRW_ROW + col * 2));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + (r0 + 4) * WRW_ROW + col * 2));
+    bf16x8_t f;
+    const __bf16* l4 = reinterpret_cast<const __bf16*>(&lo);
+    const __bf16* h4 = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[e] = l4[e]; f[e + 4] = h4[e]; }
+    return f;
+  };
+
+  if (nsteps > 0) {
+    gload();
+    sstore(0);
+    __syncthreads();
+  }
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) gload();
+    const char* A = smem + buf * (2 * TILE_K * WRW_ROW);
+    const char* B = A + TILE_K * WRW_ROW;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = frag(A, wk * 64 + a * 32, ks);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = frag(B, wj * 64 + b * 32, ks);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    if (st + 1 < nsteps) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: atomically accumulate into dW laid out [K][C][R][S] (DL4J ConvolutionParamInitializer order)
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int j = j0 + wj * 64 + b * 32 + (lane & 31);
+    if (j >= RSC) continue;
+    const int c = j % g.C, t = j / g.C;
+    const int r = t / g.S, s = t % g.S;
+    const long long jo = (long long)c * g.R * g.S + r * g.S + s;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int k = k0 + wk * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (k < Kout) atomicAdd(dW + (long long)k * RSC + jo, acc[a][b][e]);
+      }
+    }
+  }
+  if (do_bias) {
+    // threads sharing a chunk column (same lchunk, 16 row-threads) reduce through LDS
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = bsum[e];
+    __syncthreads();
+    if (tid < 16) {
+      for (int e = 0; e < 8; ++e) {
+        float s = 0.f;
+        for (int rrow = 0; rrow < 16; ++rrow) s += red[(rrow * 16 + tid) * 8 + e];
+        const int k = k0 + tid * 8 + e;
+        if (k < Kout) atomicAdd(db + k, s);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Weight relayout (bf16): W[K][C][R][S] -> Wkrsc[K][R][S][C]  and  Wflip[C][R][S][K] = W[k][c][R-1-r][S-1-s]
+// ------------------------------------------------------------------------------------------------------
+__global__ void conv_w_relayout(const bf16* __restrict__ W, bf16* __restrict__ krsc, bf16* __restrict__ flip, int K,
+                                int C, int R, int S) {
+  const long long total = (long long)K * C * R * S;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int s = (int)(i % S);
+    long long t = i / S;
+    const int r = (int)(t % R);
+    t /= R;
+    const int c = (int)(t % C);
+    const int k = (int)(t / C);
+    const bf16 v = W[i];
+    if (krsc) krsc[(((long long)k * R + r) * S + s) * C + c] = v;
+    if (flip) flip[(((long long)c * R + (R - 1 - r)) * S + (S - 1 - s)) * K + k] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------ API
+static inline ConvGeom mk(int N, int H, int W, int C, int OH, int OW, int K, int R, int S, int sh, int sw, int ph, int pw,
+                          int dh, int dw) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.OH = OH; g.OW = OW; g.K = K; g.R = R; g.S = S;
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dw;
+  return g;
+}
+
+DL4J_API int dl4j_conv_w_relayout(const void* W, void* krsc, void* flip, int K, int C, int R, int S, hipStream_t s) {
+  const long long total = (long long)K * C * R * S;
+  long long gsz = (total + 255) / 256;
+  if (gsz > 4096) gsz = 4096;
+  hipLaunchKernelGGL(conv_w_relayout, dim3((unsigned)gsz), dim3(256), 0, s, (const bf16*)W, (bf16*)krsc, (bf16*)flip,
+                     K, C, R, S);
+  return (int)hipGetLastError();
+}
+
+// Forward: X NHWC [N,H,W,C] bf16, Wkrsc [K][R*S*C], bias fp32 [K] or null, Y NHWC [N,OH,OW,K].
+DL4J_API int dl4j_conv_fwd(const void* X, const void* Wkrsc, const float* bias, void* Y, int N, int H, int W, int C,
+                           int K, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int OH, int OW,
+                           hipStream_t s) {
+  if (C % 8 != 0 || K % 4 != 0) return -1;
+  ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
+  const long long M = (long long)N * OH * OW;
+  const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((K + TILE_N - 1) / TILE_N));
+  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)Wkrsc, bias,
+                     (bf16*)Y, g, R * S * C, 0, 0, 0);
+  return (int)hipGetLastError();
+}
+
+// Backward data, stride 1: dX[N,H,W,C] = conv(dY[N,OH,OW,K], Wflip[C][R][S][K], pad' = (R-1-ph, S-1-pw)).
+DL4J_API int dl4j_conv_bwd_data_s1(const void* dY, const void* Wflip, void* dX, int N, int H, int W, int C, int K,
+                                   int R, int S, int ph, int pw, int OH, int OW, hipStream_t s) {
+  if (K % 8 != 0 || C % 4 != 0) return -1;
+  // "input" image = dY (OH x OW x K); output grid = H x W x C; kernel R x S stride 1, pad R-1-ph
+  ConvGeom g = mk(N, OH, OW, K, H, W, C, R, S, 1, 1, R - 1 - ph, S - 1 - pw, 1, 1);
+  const long long M = (long long)N * H * W;
+  const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
+  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)dY, (const bf16*)Wflip,
+                     (const float*)nullptr, (bf16*)dX, g, R * S * K, 0, 0, 0);
+  return (int)hipGetLastError();
+}
+
+// Backward data, 1x1 kernel, stride s, no padding: dX (pre-zeroed) rows (n, oh*s, ow*s) = dY rows x Wflip[C][K].
+DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX, int N, int H, int W, int C, int K,
+                                    int stride, int OH, int OW, hipStream_t s) {
+  if (K % 8 != 0 || C % 4 != 0) return -1;
+  ConvGeom g = mk(N, OH, OW, K, OH, OW, C, 1, 1, 1, 1, 0, 0, 1, 1);
+  const long long M = (long long)N * OH * OW;
+  const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
+  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)dY, (const bf16*)Wflip,
+                     (const float*)nullptr, (bf16*)dX, g, K, stride, H, W);
+  return (int)hipGetLastError();
+}
+
+// Weight gradient: dW fp32 [K][C][R][S] (pre-zeroed, accumulated atomically), db fp32 [K] (pre-zeroed) or null.
+DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, int N, int H, int W, int C, int K,
+                           int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int OH, int OW, int splits,
+                           hipStream_t s) {
+  if (C % 8 != 0 || K % 8 != 0) return -1;
+  ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
+  const int M = N * OH * OW;
+  const int RSC = R * S * C;
+  const int tiles = ((K + TILE_N - 1) / TILE_N) * ((RSC + TILE_M - 1) / TILE_M);
+  if (splits <= 0) {
+    splits = (1024 + tiles - 1) / tiles;
+    const int maxs = (M + 255) / 256;
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+  }
+  int mps = (M + splits - 1) / splits;
+  mps = (mps + TILE_K - 1) / TILE_K * TILE_K;
+  splits = (M + mps - 1) / mps;
+  hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
+                     db, g, mps);
+  return (int)hipGetLastError();
+}

@@ -65,11 +65,11 @@ class ConvolutionLayerImpl(LayerImpl):
     def preOutput(self, x, training=False):
         k, s, pad4, d = self._geom(x)
         W = self.W("W")
-        b = self.W("b").reshape(-1) if "b" in self.params else None
-        xt = _truncate_input(self.conf, x, k, s, pad4, d)
+        b = self.params["b"].reshape(-1) if "b" in self.params else None      # master-precision bias
+        xt = x     # Truncate mode needs no cropping: output sizes use floor division everywhere
         self._xt = xt
         self._geom_cache = (s, pad4, d)
-        return ops.conv2d_forward(_cl(xt.to(W.dtype)), W, b.to(W.dtype) if b is not None else None, s, pad4, d)
+        return ops.conv2d_forward(_cl(xt.to(W.dtype)), W, b, s, pad4, d)
 
     def activate(self, x, training=False, mask=None):
         if x.dim() != 4:
@@ -212,7 +212,7 @@ class SubsamplingLayerImpl(LayerImpl):
         self.input = x
         c = self.conf
         pad4 = compute_pad4(c, x.shape[2], x.shape[3], c.kernelSize, c.stride, c.dilation)
-        xt = _truncate_input(c, x, c.kernelSize, c.stride, pad4, c.dilation)
+        xt = x     # floor-division output sizes already implement Truncate mode
         self._xshape = x.shape
         y, self._ctx = ops.pool2d_forward(_cl(xt), c.poolingType.value, c.kernelSize, c.stride, pad4, c.dilation,
                                           c.pnorm, c.eps)

@@ -147,6 +147,12 @@ class BaseNetwork:
         if self.shadow is not None:
             with torch.no_grad():
                 self.shadow.copy_(self.flattenedParams)
+        self._bump_weight_version()
+
+    @staticmethod
+    def _bump_weight_version():
+        from ..ops import conv_native
+        conv_native.bump_version()
 
     # ------------------------------------------------------------------------------ params API
     def numParams(self, backwards=False):
@@ -285,6 +291,7 @@ class BaseNetwork:
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
             reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)
         self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow, reg)
+        self._bump_weight_version()
         if getattr(self, "_loss_part", None) is not None:
             self._score_t = self._loss_part + (reg[0] / mb_local if reg is not None else 0.0)
             self._loss_part = None

@@ -26,6 +26,8 @@ def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1):
         if y is not None:
             return y
     pt, pb, pl, pr = pad4
+    if b is not None:
+        b = b.to(x.dtype)
     if _sym(pad4):
         return F.conv2d(x, w, b, tuple(stride), (pt, pl), tuple(dilation), groups)
     xp = F.pad(x, (pl, pr, pt, pb))

@@ -1,12 +1,152 @@
-"""Convolution through the hand-written MFMA implicit-GEMM kernels (csrc/conv_igemm.hip).
+"""Convolution through the hand-written MFMA implicit-GEMM kernels (``csrc/conv_igemm.hip``).
 
-Returns ``None`` for shapes the kernels do not cover, in which case ``ops.conv`` uses the library
-path (MIOpen through torch)."""
+Coverage (everything else returns ``None`` and ``ops.conv`` uses the library path):
+  * forward:        bf16 NHWC, C_in % 8 == 0, C_out % 4 == 0, any kernel/stride/padding/dilation
+  * backward-data:  stride 1 (any kernel, padding) via the flipped-weight transposed conv;
+                    1x1 kernels with any stride and no padding via a strided-scatter GEMM
+  * backward-weight: C_in % 8 == 0, C_out % 8 == 0, any geometry; fp32 result accumulated straight into the
+                    network's flat gradient view (DL4J [K][C][R][S] order), conv-bias gradient fused.
+Weights are re-laid-out once per parameter version (KRSC for forward, flipped CRSK for backward-data).
+"""
+import ctypes
+
+import torch
+
+from . import native
+from .native import _ptr, _stream, c_int, c_void_p
+
+native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
+native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p])
+native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
+native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
+native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
+
+# Bumped by every parameter update (BaseNetwork._apply_update / setParams): invalidates relayout caches.
+WEIGHT_VERSION = [0]
+_cache = {}
+
+
+def bump_version():
+    WEIGHT_VERSION[0] += 1
+
+
+def _relayout(w, want_krsc, want_flip):
+    key = (w.data_ptr(), tuple(w.shape))
+    ent = _cache.get(key)
+    if ent is None or ent[0] != WEIGHT_VERSION[0]:
+        ent = [WEIGHT_VERSION[0], None, None]
+        _cache[key] = ent
+    K, C, R, S = w.shape
+    need_k = want_krsc and ent[1] is None
+    need_f = want_flip and ent[2] is None
+    if need_k or need_f:
+        krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device) if need_k else None
+        flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device) if need_f else None
+        wc = w.contiguous()
+        rc = native.load().dl4j_conv_w_relayout(_ptr(wc), _ptr(krsc), _ptr(flip), K, C, R, S, _stream())
+        native._check(rc, "conv_w_relayout")
+        if need_k:
+            ent[1] = krsc
+        if need_f:
+            ent[2] = flip
+    return ent[1], ent[2]
+
+
+def _ok_act(t):
+    return t.dtype == torch.bfloat16 and t.dim() == 4 and t.is_cuda
+
+
+def _cl(t):
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+def _out_hw(H, W, R, S, stride, pad4, dilation):
+    pt, pb, pl, pr = pad4
+    OH = (H + pt + pb - ((R - 1) * dilation[0] + 1)) // stride[0] + 1
+    OW = (W + pl + pr - ((S - 1) * dilation[1] + 1)) // stride[1] + 1
+    return OH, OW
 
 
 def conv2d_fwd(x, w, b, stride, pad4, dilation):
-    return None
+    if not (_ok_act(x) and w.dtype == torch.bfloat16):
+        return None
+    N, C, H, W = x.shape
+    K, Cw, R, S = w.shape
+    if C != Cw or C % 8 != 0 or K % 4 != 0:
+        return None
+    OH, OW = _out_hw(H, W, R, S, stride, pad4, dilation)
+    if OH <= 0 or OW <= 0:
+        return None
+    krsc, _ = _relayout(w, True, False)
+    x = _cl(x)
+    y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    bias = b.float().contiguous() if b is not None else None
+    rc = native.load().dl4j_conv_fwd(_ptr(x), _ptr(krsc), _ptr(bias), _ptr(y), N, H, W, C, K, R, S, stride[0],
+                                     stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, _stream())
+    native._check(rc, "conv_fwd")
+    return y
 
 
 def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None):
-    return None
+    if not (_ok_act(x) and _ok_act(dy) and w.dtype == torch.bfloat16):
+        return None
+    N, C, H, W = x.shape
+    K, Cw, R, S = w.shape
+    if C != Cw or C % 8 != 0 or K % 8 != 0:
+        return None
+    OH, OW = dy.shape[2], dy.shape[3]
+    x = _cl(x)
+    dy = _cl(dy)
+    lib = native.load()
+    dx = None
+    if need_dx:
+        s1 = tuple(stride) == (1, 1) and tuple(dilation) == (1, 1)
+        pure_1x1 = R == 1 and S == 1 and not any(pad4) and tuple(dilation) == (1, 1)
+        if s1 and (H, W) == _out_hw_inv(OH, OW, R, S, pad4, H, W):
+            _, flip = _relayout(w, False, True)
+            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            rc = lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, R, S, pad4[0], pad4[2], OH,
+                                           OW, _stream())
+            native._check(rc, "conv_bwd_data_s1")
+        elif pure_1x1 and stride[0] == stride[1]:
+            _, flip = _relayout(w, False, True)
+            dx = torch.zeros((N, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
+                                            _stream())
+            native._check(rc, "conv_bwd_data_1x1")
+        else:
+            from .conv import _sym
+            import torch.nn.functional as F
+            sym = _sym(pad4)
+            xin = x if sym else F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
+            padding = [pad4[0], pad4[2]] if sym else [0, 0]
+            dx, _, _ = torch.ops.aten.convolution_backward(dy, xin, w, None, list(stride), padding, list(dilation),
+                                                           False, [0, 0], 1, [True, False, False])
+            if not sym:
+                dx = dx[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W]
+    dW_out = db_out = None
+    if need_dw:
+        direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
+        dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
+        dWt.zero_()
+        dbt = None
+        if need_db:
+            directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+            dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
+            dbt.zero_()
+        rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(dWt), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
+                               pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, 0, _stream())
+        native._check(rc, "conv_wrw")
+        dW_out = None if direct else dWt
+        if need_db:
+            db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
+    return dx, dW_out, db_out
+
+
+def _out_hw_inv(OH, OW, R, S, pad4, H, W):
+    """For stride 1: the input size that the transposed conv reproduces (must equal H, W)."""
+    pt, pb, pl, pr = pad4
+    return OH - 1 + R - pt - pb, OW - 1 + S - pl - pr
+
+
+_ = ctypes
