@@ -329,21 +329,19 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
     __syncthreads();
   }
 
-  // ---- epilogue: atomically accumulate into dW laid out [K][C][R][S] (DL4J ConvolutionParamInitializer order)
+  // ---- epilogue: atomically accumulate into the fp32 dW workspace laid out [K][R][S][C] (j contiguous), so
+  // every atomic wave-instruction covers two full 128-byte row segments (the full-rate atomic shape).
   const int hh = lane >> 5;
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int j = j0 + wj * 64 + b * 32 + (lane & 31);
     if (j >= RSC) continue;
-    const int c = j % g.C, t = j / g.C;
-    const int r = t / g.S, s = t % g.S;
-    const long long jo = (long long)c * g.R * g.S + r * g.S + s;
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int k = k0 + wk * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-        if (k < Kout) atomicAdd(dW + (long long)k * RSC + jo, acc[a][b][e]);
+        if (k < Kout) atomicAdd(dW + (long long)k * RSC + j, acc[a][b][e]);
       }
     }
   }
@@ -439,7 +437,30 @@ DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX,
   return (int)hipGetLastError();
 }
 
-// Weight gradient: dW fp32 [K][C][R][S] (pre-zeroed, accumulated atomically), db fp32 [K] (pre-zeroed) or null.
+// KRSC fp32 workspace -> DL4J [K][C][R][S] fp32 gradient view
+__global__ void conv_wrw_permute(const float* __restrict__ ws, float* __restrict__ dW, int K, int C, int R, int S) {
+  const long long total = (long long)K * C * R * S;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int k = (int)(t / R);
+    dW[(((long long)k * C + c) * R + r) * S + s] = ws[i];
+  }
+}
+
+DL4J_API int dl4j_conv_wrw_permute(const float* ws, float* dW, int K, int C, int R, int S, hipStream_t s) {
+  const long long total = (long long)K * C * R * S;
+  long long gsz = (total + 255) / 256;
+  if (gsz > 4096) gsz = 4096;
+  hipLaunchKernelGGL(conv_wrw_permute, dim3((unsigned)gsz), dim3(256), 0, s, ws, dW, K, C, R, S);
+  return (int)hipGetLastError();
+}
+
+// Weight gradient: dW fp32 workspace [K][R][S][C] (pre-zeroed, accumulated atomically; equal to the DL4J layout
+// when R == S == 1), db fp32 [K] (pre-zeroed) or null.
 DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, int N, int H, int W, int C, int K,
                            int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int OH, int OW, int splits,
                            hipStream_t s) {
@@ -449,8 +470,9 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
   const int RSC = R * S * C;
   const int tiles = ((K + TILE_N - 1) / TILE_N) * ((RSC + TILE_M - 1) / TILE_M);
   if (splits <= 0) {
-    splits = (1024 + tiles - 1) / tiles;
-    const int maxs = (M + 255) / 256;
+    // ~2 workgroups per CU in total; every split keeps >= 8 k-steps so the atomic epilogue stays amortised
+    splits = (512 + tiles - 1) / tiles;
+    const int maxs = (M + 8 * TILE_K - 1) / (8 * TILE_K);
     if (splits > maxs) splits = maxs;
     if (splits < 1) splits = 1;
   }

@@ -43,12 +43,18 @@ class BatchNormalizationImpl(LayerImpl):
         return y
 
     def backpropGradient(self, eps):
-        dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx)
-        if "gamma" in self.grads:
-            copy_grad_(self.grads["gamma"], dgamma)
-            copy_grad_(self.grads["beta"], dbeta)
-        self.grads["mean"].zero_()
-        self.grads["var"].zero_()
+        gg, gb = self.grads.get("gamma"), self.grads.get("beta")
+        dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx, gg, gb)
+        if gg is not None:
+            if dgamma is not gg:
+                copy_grad_(gg, dgamma)
+            if dbeta is not gb:
+                copy_grad_(gb, dbeta)
+        if not getattr(self, "_stat_grads_zero", False):
+            # running-stat "gradients" are zero (reference :164-167,205-208); their NoOp update keeps them so
+            self.grads["mean"].zero_()
+            self.grads["var"].zero_()
+            self._stat_grads_zero = True
         return self.make_gradient(), self.backpropDropOut(dx)
 
 

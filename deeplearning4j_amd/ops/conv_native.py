@@ -20,6 +20,7 @@ native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + 
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
+native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
 
 # Bumped by every parameter update (BaseNetwork._apply_update / setParams): invalidates relayout caches.
 WEIGHT_VERSION = [0]
@@ -110,7 +111,8 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
             native._check(rc, "conv_bwd_data_s1")
         elif pure_1x1 and stride[0] == stride[1]:
             _, flip = _relayout(w, False, True)
-            dx = torch.zeros((N, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
+                             memory_format=torch.channels_last).zero_()
             rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
                                             _stream())
             native._check(rc, "conv_bwd_data_1x1")
@@ -128,15 +130,20 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     if need_dw:
         direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
         dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
-        dWt.zero_()
+        # the kernel accumulates in [K][R][S][C]; identical to DL4J's [K][C][R][S] when R == S == 1
+        ws = dWt if (R == 1 and S == 1) else torch.empty((K, R, S, C), dtype=torch.float32, device=x.device)
+        ws.zero_()
         dbt = None
         if need_db:
             directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
             dbt.zero_()
-        rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(dWt), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
+        rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
                                pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, 0, _stream())
         native._check(rc, "conv_wrw")
+        if ws is not dWt:
+            rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, _stream())
+            native._check(rc, "conv_wrw_permute")
         dW_out = None if direct else dWt
         if need_db:
             db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt

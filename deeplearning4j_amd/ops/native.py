@@ -177,14 +177,15 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     return y, ("NATIVE", x, ctx, relu, M, C, res)
 
 
-def bn_bwd(dy, ctx):
+def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     _, x, c, relu, M, C, res = ctx
     dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
     dres = _like_rows(x) if res is not None else None
-    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-    dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+    ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
+    dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
     rc = lib.dl4j_bn_bwd(_dt(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
                          _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())

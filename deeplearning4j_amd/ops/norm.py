@@ -59,12 +59,13 @@ def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=Fal
     return y, ("REF", x, mean, invstd, g, b, relu, y if relu else None, residual is not None)
 
 
-def bn_backward(dy, ctx):
+def bn_backward(dy, ctx, dgamma_out=None, dbeta_out=None):
     """Returns (dx, dgamma, dbeta, dresidual) — dgamma/dbeta are sums over the batch (not averaged);
-    dresidual is None unless the forward fused a residual."""
+    dresidual is None unless the forward fused a residual. The native kernel writes dgamma/dbeta straight
+    into ``dgamma_out``/``dbeta_out`` (the layer's fp32 gradient views) when given."""
     if ctx[0] == "NATIVE":
         from . import native
-        return native.bn_bwd(dy, ctx)
+        return native.bn_bwd(dy, ctx, dgamma_out, dbeta_out)
     _, x, mean, invstd, g, b, relu, y, has_res = ctx
     dims = _dims(x)
     bs = _bshape(x)

@@ -109,7 +109,8 @@ def test_fused_updater_matches_reference(cuda, upd):
         fused_update(plan, pd, gd, sd, it, 0, 8, shadow=shadow)
         _close(pd, pc, 1e-5)
         _close(gd, gc, 1e-5)
-        _close(sd, sc, 1e-5)
+        if sc.numel():
+            _close(sd, sc, 1e-5)
         _close(shadow, pc, 1e-2)
         p, st = pc, sc
 
@@ -127,7 +128,8 @@ def test_resnet50_step_bf16(cuda):
         s.append(net.score())
     assert all(v == v for v in s)
     assert net.shadow is not None and net.shadow.dtype == torch.bfloat16
-    assert (net.shadow.float() - net.flattenedParams).abs().max().item() < 0.05
+    p = net.flattenedParams
+    assert ((net.shadow.float() - p).abs() <= 1e-2 * p.abs() + 1e-3).all()
 
 
 def test_lenet_gpu_matches_cpu(cuda):
