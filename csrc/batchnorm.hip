@@ -10,7 +10,8 @@
 // Forward (training): stats_partial -> finalize -> apply.   Backward: bwd_partial -> bwd_finalize -> bwd_apply.
 // Each thread owns 8 consecutive channels (one 16-byte vector); a block covers R = 256/(C/8) rows per sweep,
 // so every wave issues fully coalesced dwordx4 loads. Per-block partial sums go to a [nblk, C] fp32
-// workspace (no atomics -> bitwise reproducible); finalize reduces them with 4 row-groups x 64 channels per
+// workspace (no atomics -> bitwise reproducible); with many partial rows a level-1 kernel first folds every 32 rows
+// in parallel (bn_reduce_rows), then finalize reduces the rest in double with 4 row-groups x 64 channels per
 // block. The ReLU mask in backward is recomputed from x (and r), so no activation needs to be stored.
 #include "common.h"
 
@@ -30,7 +31,18 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
   if (r0 < R) {
-    for (long long r = rbeg + r0; r < rend; r += R) {
+    long long r = rbeg + r0;
+    // 4 independent 16-byte loads in flight per thread before any use (memory-level parallelism)
+    for (; r + 3 * R < rend; r += 4 * R) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Vec8<T>::load(x + (r + u * R) * C + cg * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float d = v[u][i] - sh[i]; s1[i] += d; s2[i] += d * d; }
+    }
+    for (; r < rend; r += R) {
       float v[8];
       Vec8<T>::load(x + r * C + cg * 8, v);
 #pragma unroll
@@ -51,6 +63,34 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
     for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 8 + k]; b += red2[(rr * T8 + g) * 8 + k]; }
     part_s1[(long long)blockIdx.x * C + c] = a;
     part_s2[(long long)blockIdx.x * C + c] = b;
+  }
+}
+
+// Level-1 partial reduction: [nblk, C] -> [ceil(nblk/32), C]. grid = (ceil(C/64), ceil(nblk/32)); each of the 4
+// row groups of a block sums 8 rows with independent loads (one HBM round trip), so even C = 64 spreads over
+// nblk/32 blocks instead of serialising nblk rows in one block.
+__global__ __launch_bounds__(256) void bn_reduce_rows(const float* __restrict__ p1, const float* __restrict__ p2,
+                                                      int nblk, int C, float* __restrict__ q1, float* __restrict__ q2) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * 32 + grp * 8;
+  float a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int r = r0 + u;
+    const bool ok = c < C && r < nblk;
+    a[u] = ok ? p1[(long long)r * C + c] : 0.f;
+    b[u] = ok ? p2[(long long)r * C + c] : 0.f;
+  }
+  float sa = 0.f, sb = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
+  __shared__ float ra[256], rb[256];
+  ra[threadIdx.x] = sa; rb[threadIdx.x] = sb;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    q1[(long long)blockIdx.y * C + c] = ra[threadIdx.x] + ra[threadIdx.x + 64] + ra[threadIdx.x + 128] + ra[threadIdx.x + 192];
+    q2[(long long)blockIdx.y * C + c] = rb[threadIdx.x] + rb[threadIdx.x + 64] + rb[threadIdx.x + 128] + rb[threadIdx.x + 192];
   }
 }
 
@@ -145,21 +185,34 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
   if (r0 < R) {
-    for (long long r = rbeg + r0; r < rend; r += R) {
-      float xv[8], gv[8], rv[8];
-      Vec8<T>::load(x + r * C + cg * 8, xv);
-      Vec8<T>::load(dy + r * C + cg * 8, gv);
-      if (RES) Vec8<T>::load(res + r * C + cg * 8, rv);
+    constexpr int U = RES ? 2 : 3;     // independent row groups in flight per thread
+    long long r = rbeg + r0;
+    for (; r < rend; r += U * R) {
+      float xv[U][8], gv[U][8], rv[U][8];
+      bool ok[U];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float d = gv[i];
-        if (RELU) {
-          float t = xv[i] * sc[i] + sf[i];
-          if (RES) t += rv[i];
-          d = t > 0.f ? d : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const long long ru = r + u * R;
+        ok[u] = ru < rend;
+        const long long o = (ok[u] ? ru : r) * C + cg * 8;
+        Vec8<T>::load(x + o, xv[u]);
+        Vec8<T>::load(dy + o, gv[u]);
+        if (RES) Vec8<T>::load(res + o, rv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float d = gv[u][i];
+          if (RELU) {
+            float t = xv[u][i] * sc[i] + sf[i];
+            if (RES) t += rv[u][i];
+            d = t > 0.f ? d : 0.f;
+          }
+          db[i] += d;
+          dg[i] += d * (xv[u][i] - mu[i]) * is[i];
         }
-        db[i] += d;
-        dg[i] += d * (xv[i] - mu[i]) * is[i];
       }
     }
   }
@@ -230,9 +283,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
 static inline void bn_grid(long long M, int C, int* nblk, long long* rows_per_blk) {
   const int T8 = C / 8;
   const long long work = M * T8;                  // vector loads
-  long long nb = work / (256LL * 64);             // >= 64 vector loads per thread
+  long long nb = work / (256LL * 24);             // ~24 vector loads per thread, up to 4 blocks per CU
   if (nb < 1) nb = 1;
-  if (nb > 512) nb = 512;
+  if (nb > 1024) nb = 1024;
   long long rpb = (M + nb - 1) / nb;
   nb = (M + rpb - 1) / rpb;
   *nblk = (int)nb;
@@ -249,7 +302,17 @@ static inline int apply_grid(long long M, int C) {
 DL4J_API int dl4j_bn_workspace_floats(long long M, int C) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
-  return 2 * nblk * C + 8 * C;
+  return 2 * nblk * C + 2 * ((nblk + 31) / 32) * C + 8 * C;
+}
+
+// Two-stage partial reduction when there are many partial rows; returns the buffers/rows finalize should read.
+static inline void bn_reduce_stage(float*& p1, float*& p2, int& nblk, int C, float* q, hipStream_t s) {
+  if (nblk <= 64) return;
+  const int S = (nblk + 31) / 32;
+  float* q1 = q;
+  float* q2 = q + (long long)S * C;
+  hipLaunchKernelGGL(bn_reduce_rows, dim3((C + 63) / 64, S), dim3(256), 0, s, p1, p2, nblk, C, q1, q2);
+  p1 = q1; p2 = q2; nblk = S;
 }
 
 #define BN_DISPATCH3(KERNEL, T, relu, res, ...)                                         \
@@ -270,17 +333,20 @@ DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, lon
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
+  float* q = p2 + (long long)nblk * C;
   const dim3 fg((C + 63) / 64);
   const int ag = apply_grid(M, C);
   if (dtype == 1) {
     const bf16* xb = (const bf16*)x;
     if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
+    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, training, ctx_out);
     BN_DISPATCH3(bn_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, xb, (const bf16*)res, (bf16*)y, M, C, ctx_out);
   } else {
     const float* xf = (const float*)x;
     if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
+    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, training, ctx_out);
     BN_DISPATCH3(bn_apply, float, relu, res, dim3(ag), dim3(256), 0, s, xf, (const float*)res, (float*)y, M, C,
@@ -298,7 +364,8 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
-  float* cdb = p2 + (long long)nblk * C;
+  float* q = p2 + (long long)nblk * C;
+  float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
   float* cdg = cdb + C;
   const int ag = apply_grid(M, C);
   if (dtype == 1) {
@@ -308,6 +375,7 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
     BN_DISPATCH3(bn_bwd_partial, float, relu, res, dim3(nblk), dim3(256), 0, s, (const float*)x, (const float*)res,
                  (const float*)dy, M, C, rpb, ctx, p1, p2);
   }
+  bn_reduce_stage(p1, p2, nblk, C, q, s);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
                      cdg);
   if (dtype == 1) {

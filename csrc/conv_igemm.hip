@@ -437,8 +437,10 @@ DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX,
   return (int)hipGetLastError();
 }
 
-// KRSC fp32 workspace -> DL4J [K][C][R][S] fp32 gradient view
-__global__ void conv_wrw_permute(const float* __restrict__ ws, float* __restrict__ dW, int K, int C, int R, int S) {
+// KRSC fp32 workspace -> DL4J [K][C][R][S] fp32 gradient view. With rezero the workspace is cleared as it is
+// read, so a cached workspace is already zero for the next atomic accumulation (no separate memset launch).
+__global__ void conv_wrw_permute(float* __restrict__ ws, float* __restrict__ dW, int K, int C, int R, int S,
+                                 int rezero) {
   const long long total = (long long)K * C * R * S;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
@@ -448,14 +450,15 @@ __global__ void conv_wrw_permute(const float* __restrict__ ws, float* __restrict
     const int r = (int)(t % R);
     const int k = (int)(t / R);
     dW[(((long long)k * C + c) * R + r) * S + s] = ws[i];
+    if (rezero) ws[i] = 0.f;
   }
 }
 
-DL4J_API int dl4j_conv_wrw_permute(const float* ws, float* dW, int K, int C, int R, int S, hipStream_t s) {
+DL4J_API int dl4j_conv_wrw_permute(float* ws, float* dW, int K, int C, int R, int S, int rezero, hipStream_t s) {
   const long long total = (long long)K * C * R * S;
   long long gsz = (total + 255) / 256;
   if (gsz > 4096) gsz = 4096;
-  hipLaunchKernelGGL(conv_wrw_permute, dim3((unsigned)gsz), dim3(256), 0, s, ws, dW, K, C, R, S);
+  hipLaunchKernelGGL(conv_wrw_permute, dim3((unsigned)gsz), dim3(256), 0, s, ws, dW, K, C, R, S, rezero);
   return (int)hipGetLastError();
 }
 

@@ -19,17 +19,25 @@ struct SegDesc {
 enum { OP_NOOP = 0, OP_SGD = 1, OP_NESTEROVS = 2, OP_ADAM = 3, OP_ADAMAX = 4, OP_NADAM = 5, OP_ADAGRAD = 6,
        OP_ADADELTA = 7, OP_RMSPROP = 8 };
 
+#define UPD_CHUNK 2048   // elements per workgroup (8 per thread)
+
+// btab[b] = (segment index, chunk index): a flat 1-D grid with exactly the blocks the segments need, so a
+// 64-element BN segment and a 2.4M-element conv weight cost one and 1150 workgroups respectively.
 template <typename TS>
-__global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __restrict__ segs, float* __restrict__ p,
+__global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __restrict__ segs,
+                                                           const int2* __restrict__ btab, float* __restrict__ p,
                                                            float* __restrict__ g, float* __restrict__ st,
                                                            TS* __restrict__ shadow, float inv_div, int write_update,
                                                            float* __restrict__ reg_out) {
-  const SegDesc s = segs[blockIdx.y];
+  const int2 bt = btab[blockIdx.x];
+  const SegDesc s = segs[bt.x];
   float reg = 0.f;   // l1*|p| + 0.5*l2*p^2 of the PRE-update params (the score's regularisation term)
-  const long long stride = (long long)gridDim.x * blockDim.x;
   float* s1 = st + s.st_off + s.in_block;
   float* s2 = st + s.st_off + s.block_n + s.in_block;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < s.n; i += stride) {
+  const long long ibeg = (long long)bt.y * UPD_CHUNK;
+  long long iend = ibeg + UPD_CHUNK;
+  if (iend > s.n) iend = s.n;
+  for (long long i = ibeg + threadIdx.x; i < iend; i += 256) {
     const long long pi = s.p_off + i;
     const float gi = g[pi];
     float pv = p[pi];
@@ -97,21 +105,20 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
 }
 
 // segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (treated as bf16 layout not supported -> none)
-DL4J_API int dl4j_fused_update(const void* segs, int nseg, long long max_n, float* p, float* g, float* st,
+// btab: device int2[nblocks] built by the host from the segment sizes (see dl4j_update_chunk).
+DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
                                void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
                                hipStream_t stream) {
-  if (nseg <= 0) return 0;
-  long long bx = (max_n + 256 * 4 - 1) / (256 * 4);
-  if (bx < 1) bx = 1;
-  if (bx > 512) bx = 512;
-  dim3 grid((unsigned)bx, (unsigned)nseg);
+  if (nblocks <= 0) return 0;
   if (shadow_kind == 1)
-    hipLaunchKernelGGL(fused_update_kernel<bf16>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
-                       (bf16*)shadow, inv_div, write_update, reg_out);
+    hipLaunchKernelGGL(fused_update_kernel<bf16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
+                       (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out);
   else
-    hipLaunchKernelGGL(fused_update_kernel<float>, grid, dim3(256), 0, stream, (const SegDesc*)segs, p, g, st,
-                       (float*)nullptr, inv_div, write_update, reg_out);
+    hipLaunchKernelGGL(fused_update_kernel<float>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
+                       (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out);
   return (int)hipGetLastError();
 }
+
+DL4J_API int dl4j_update_chunk() { return UPD_CHUNK; }
 
 DL4J_API int dl4j_segdesc_size() { return (int)sizeof(SegDesc); }

@@ -92,7 +92,8 @@ class ConvolutionLayerImpl(LayerImpl):
         xt = _cl(self._xt.to(W.dtype))
         need_dx = getattr(self, "need_input_grad", True)
         dx, dW, db = ops.conv2d_backward(xt, W, _cl(delta.to(W.dtype)), s, pad4, d, need_dx, True,
-                                         "b" in self.grads, gW=self.grads["W"], gb=self.grads.get("b"))
+                                         "b" in self.grads, gW=self.grads["W"], gb=self.grads.get("b"),
+                                         grads_zeroed=getattr(self.net, "_grads_zeroed", False))
         if dW is not None:
             copy_grad_(self.grads["W"], dW)
         if "b" in self.grads and db is not None:

@@ -264,6 +264,11 @@ class BaseNetwork:
 
     # ------------------------------------------------------------------------------ DP hooks
     def _begin_backward(self):
+        # On the GPU, clear the whole flat gradient with ONE fill so layers whose kernels accumulate (conv
+        # weight-gradient atomics, fused bias sums) need no per-layer memset launches.
+        self._grads_zeroed = self.flattenedGradients is not None and self.flattenedGradients.is_cuda
+        if self._grads_zeroed:
+            self.flattenedGradients.zero_()
         acc = getattr(self, "gradientsAccumulator", None)
         if acc is not None and hasattr(acc, "begin_backward"):
             acc.begin_backward(self)

@@ -20,11 +20,21 @@ native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + 
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
-native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
+native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p])
 
 # Bumped by every parameter update (BaseNetwork._apply_update / setParams): invalidates relayout caches.
 WEIGHT_VERSION = [0]
 _cache = {}
+_wrw_ws = {}   # (K, R, S, C, device) -> fp32 KRSC accumulation workspace, kept zero by the permute kernel
+
+
+def _zeroed_wrw_ws(K, R, S, C, device):
+    key = (K, R, S, C, str(device))
+    ws = _wrw_ws.get(key)
+    if ws is None:
+        ws = torch.zeros((K, R, S, C), dtype=torch.float32, device=device)
+        _wrw_ws[key] = ws
+    return ws
 
 
 def bump_version():
@@ -88,7 +98,9 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return y
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False):
+    """grads_zeroed: the caller guarantees gW/gb (flat-gradient views) are already zero (the network clears the
+    whole flat gradient with one fill per step), so no per-layer memset is launched."""
     if not (_ok_act(x) and _ok_act(dy) and w.dtype == torch.bfloat16):
         return None
     N, C, H, W = x.shape
@@ -131,18 +143,23 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
         direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
         dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
         # the kernel accumulates in [K][R][S][C]; identical to DL4J's [K][C][R][S] when R == S == 1
-        ws = dWt if (R == 1 and S == 1) else torch.empty((K, R, S, C), dtype=torch.float32, device=x.device)
-        ws.zero_()
+        if R == 1 and S == 1:
+            ws = dWt
+            if not (direct and grads_zeroed):
+                ws.zero_()
+        else:
+            ws = _zeroed_wrw_ws(K, R, S, C, x.device)
         dbt = None
         if need_db:
             directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
-            dbt.zero_()
+            if not (directb and grads_zeroed):
+                dbt.zero_()
         rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
                                pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, 0, _stream())
         native._check(rc, "conv_wrw")
         if ws is not dWt:
-            rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, _stream())
+            rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, 1, _stream())
             native._check(rc, "conv_wrw_permute")
         dW_out = None if direct else dWt
         if need_db:

@@ -28,8 +28,9 @@ def load():
             raise FileNotFoundError(KERNEL_LIB)
     lib = ctypes.CDLL(KERNEL_LIB)
     sigs = {
-        "dl4j_fused_update": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_int,
-                              c_void_p, c_void_p],
+        "dl4j_fused_update": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float,
+                              c_int, c_void_p, c_void_p],
+        "dl4j_update_chunk": [],
         "dl4j_segdesc_size": [],
         "dl4j_bn_workspace_floats": [c_ll, c_int],
         "dl4j_bn_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_float, c_float,
@@ -132,14 +133,19 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
             cache.dev = torch.empty(len(b), dtype=torch.uint8, device=params.device)
         cache.dev.copy_(host, non_blocking=False)
         cache.host_bytes = b
-    max_n = max((s.n for s in segs), default=0)
+    if getattr(cache, "btab", None) is None or cache.btab.device != params.device:
+        chunk = lib.dl4j_update_chunk()
+        rows = [(si, ci) for si, s in enumerate(segs) for ci in range((s.n + chunk - 1) // chunk)]
+        cache.btab = torch.tensor(rows if rows else [(0, 0)], dtype=torch.int32).to(params.device)
+        cache.nblocks = len(rows)
     sk = 0
     if shadow is not None:
         if shadow.dtype != torch.bfloat16:
             return False
         sk = 1
-    rc = lib.dl4j_fused_update(_ptr(cache.dev), len(segs), max_n, _ptr(params), _ptr(grad), _ptr(state),
-                               _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out), _stream())
+    rc = lib.dl4j_fused_update(_ptr(cache.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
+                               _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
+                               _stream())
     _check(rc, "fused_update")
     return True
 
@@ -247,9 +253,10 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation)
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False):
     from . import conv_native
-    return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb)
+    return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb,
+                                  grads_zeroed)
 
 
 def lstm_cell_fwd(z, c):
