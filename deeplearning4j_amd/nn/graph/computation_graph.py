@@ -307,7 +307,7 @@ class ComputationGraph(BaseNetwork):
         self._score_val = None
         return score
 
-    def _fit_batch(self, inputs, labels, fmasks=None, lmasks=None):
+    def _fit_batch_sgd(self, inputs, labels, fmasks=None, lmasks=None):
         x0 = inputs[0] if isinstance(inputs, (list, tuple)) else inputs
         if self.conf.backpropType == BackpropType.TruncatedBPTT and x0.dim() == 3:
             return self._fit_tbptt(inputs, labels, fmasks, lmasks)

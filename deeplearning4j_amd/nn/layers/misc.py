@@ -6,8 +6,8 @@ from .base import LayerImpl
 
 
 class FrozenLayerImpl(LayerImpl):
-    """Delegates forward to the wrapped layer (always in inference mode for dropout) and blocks
-    parameter gradients; epsilons still flow so earlier layers can train."""
+    """Delegates forward to the wrapped layer (always in inference mode for dropout); backprop stops here:
+    zero parameter gradient and no epsilon for earlier layers (reference FrozenLayer.java:80-82)."""
 
     def __init__(self, conf, index=0, net=None):
         super().__init__(conf, index, net)
@@ -25,13 +25,9 @@ class FrozenLayerImpl(LayerImpl):
         return self.inner.activate(x, False, mask)
 
     def backpropGradient(self, eps, **kw):
-        self.bind()
-        saved = {k: v.clone() for k, v in self.grads.items()}
-        g, dx = self.inner.backpropGradient(eps)
-        for k, v in self.grads.items():
+        for v in self.grads.values():
             v.zero_()
-        _ = saved
-        return self.make_gradient(), dx
+        return self.make_gradient(), None
 
     def __getattr__(self, name):
         if name in ("inner",):

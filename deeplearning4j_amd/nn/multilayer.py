@@ -194,7 +194,7 @@ class MultiLayerNetwork(BaseNetwork):
         self._score_val = None
         return self._score_t
 
-    def _fit_batch(self, x, y, fmask=None, lmask=None):
+    def _fit_batch_sgd(self, x, y, fmask=None, lmask=None):
         if self.conf.backpropType == BackpropType.TruncatedBPTT and x.dim() == 3:
             return self._fit_tbptt(x, y, fmask, lmask)
         self.computeGradientAndScore(x, y, fmask, lmask, defer_reg=True)
@@ -224,6 +224,8 @@ class MultiLayerNetwork(BaseNetwork):
         """fit(DataSetIterator[, numEpochs]) | fit(DataSet) | fit(features, labels)."""
         if not self.initCalled:
             self.init()
+        if isinstance(labels, int) and not torch.is_tensor(data):
+            numEpochs, labels = labels, None
         if labels is not None:
             return self.fit(DataSet(data, labels, featuresMask, labelsMask))
         if isinstance(data, DataSet):

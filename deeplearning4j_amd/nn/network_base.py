@@ -143,6 +143,31 @@ class BaseNetwork:
         self.updater.init_state(self.device, self.master_dtype)
         self.initCalled = True
 
+    def _params_changed(self):
+        """Parameters were modified outside the fused updater (line search, setParams): refresh the bf16 compute
+        shadow and invalidate weight relayout caches."""
+        self.sync_shadow()
+
+    def _fit_batch(self, x, y, fmask=None, lmask=None):
+        """One optimizer iteration on a minibatch: the fused SGD-family step, or a line-search optimizer
+        (LBFGS / CG / line GD) when the configuration asks for one (reference Solver.java:50-84)."""
+        from .conf.enums import OptimizationAlgorithm as OA
+        algo = self.conf.globalConf.get("optimizationAlgo") if hasattr(self.conf, "globalConf") else None
+        if algo is None or OA.of(algo) == OA.STOCHASTIC_GRADIENT_DESCENT:
+            return self._fit_batch_sgd(x, y, fmask, lmask)
+        if getattr(self, "_solver", None) is None:
+            from ..optimize.solvers import Solver
+            self._solver = Solver(self)
+        self._solver.optimize(x, y, fmask, lmask)
+
+    def _score_batch(self, x, y, fmask=None, lmask=None):
+        from ..datasets import DataSet, MultiDataSet
+        ds = MultiDataSet(x, y, fmask, lmask) if isinstance(x, (list, tuple)) else DataSet(x, y, fmask, lmask)
+        return self._score_dataset(ds, training=True)
+
+    def getLastEtlTime(self):
+        return getattr(self, "lastEtlTime", 0.0)
+
     def sync_shadow(self):
         if self.shadow is not None:
             with torch.no_grad():
