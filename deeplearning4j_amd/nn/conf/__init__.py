@@ -11,4 +11,5 @@ from .network import ComputationGraphConfiguration, MultiLayerConfiguration, Neu
 from .preprocessors import *  # noqa: F401,F403
 from .regularization import *  # noqa: F401,F403
 from .updaters import *  # noqa: F401,F403
+from .variational import *  # noqa: F401,F403
 from .weights import *  # noqa: F401,F403

@@ -1166,15 +1166,26 @@ class VariationalAutoencoder(FeedForwardLayer):
 
 class Yolo2OutputLayer(Layer):
     """YOLOv2 loss layer, reference nn/conf/layers/objdetect/Yolo2OutputLayer.java:70."""
-    FIELDS = {"lambdaCoord": 5.0, "lambdaNoObj": 0.5, "boundingBoxes": None}
+    FIELDS = {"lambdaCoord": 5.0, "lambdaNoObj": 0.5, "boundingBoxes": None, "lossPositionScale": None,
+              "lossClassPredictions": None}
+    _CONVERTERS = dict(Layer._CONVERTERS, lossPositionScale=to_loss, lossClassPredictions=to_loss)
     RUNTIME = "deeplearning4j_amd.nn.layers.objdetect:Yolo2OutputLayerImpl"
+
+    def getOutputType(self, layerIndex, inputType):
+        return inputType
+
+    def setNIn(self, inputType, override=False):
+        pass
+
+    def getPreProcessorForInputType(self, inputType):
+        return None
 
 
 class SameDiffLayerConf(Layer):
     """Base for user layers defined as a SameDiff-lite graph (reference BaseSameDiffLayer.java:43).
     Subclasses implement ``defineParameters(params)`` and ``defineLayer(sd, input, paramTable)``."""
-    FIELDS = {"nIn": 0, "nOut": 0, "weightInit": None, "updater": None, "biasUpdater": None, "l1": None,
-              "l2": None, "l1Bias": None, "l2Bias": None, "activation": None}
+    FIELDS = {"nIn": 0, "nOut": 0, "weightInit": None, "dist": None, "biasInit": 0.0, "updater": None,
+              "biasUpdater": None, "l1": None, "l2": None, "l1Bias": None, "l2Bias": None, "activation": None}
     _CONVERTERS = dict(Layer._CONVERTERS, weightInit=to_weight_init, updater=to_updater, biasUpdater=to_updater,
                        activation=to_activation)
     RUNTIME = "deeplearning4j_amd.samediff.layer:SameDiffLayerImpl"
@@ -1218,7 +1229,7 @@ class SameDiffLayerConf(Layer):
                 setattr(self, k, 0.0)
 
     def applyGlobal(self, g):
-        for k in ("weightInit", "updater", "biasUpdater", "l1", "l2", "l1Bias", "l2Bias", "activation"):
+        for k in ("weightInit", "dist", "updater", "biasUpdater", "l1", "l2", "l1Bias", "l2Bias", "activation"):
             if getattr(self, k) is None and g.get(k) is not None:
                 conv = self._CONVERTERS.get(k)
                 setattr(self, k, conv(g[k]) if conv else g[k])

@@ -236,7 +236,7 @@ class ComputationGraph(BaseNetwork):
                 continue
             if isinstance(v, LayerVertex):
                 layer = self.layers_by_name.get(name)
-                if name in self.outputs and isinstance(layer, BaseOutputLayerImpl):
+                if name in self.outputs and (isinstance(layer, BaseOutputLayerImpl) or hasattr(layer, "computeScore")):
                     _, e = layer.backpropGradient(None)
                     self._grad_ready(name)
                 else:

@@ -140,7 +140,7 @@ class MultiLayerNetwork(BaseNetwork):
         """Reverse pass from the output layer; gradients land in the flat gradient views."""
         n = len(self.layers)
         out_layer = self.layers[-1]
-        if not isinstance(out_layer, BaseOutputLayerImpl):
+        if not (isinstance(out_layer, BaseOutputLayerImpl) or hasattr(out_layer, "computeScore")):
             raise ValueError("Cannot calculate gradient and score with respect to labels: final layer is not an "
                              "IOutputLayer")
         self._begin_backward()
@@ -240,6 +240,10 @@ class MultiLayerNetwork(BaseNetwork):
 
     def _fit_iterator(self, it):
         from ..datasets.iterators import AsyncDataSetIterator
+        if getattr(self.conf, "pretrain", False):       # reference fit(): pretrain first when configured
+            self.pretrain(it)
+            if not getattr(self.conf, "backprop", True):
+                return
         wrap = it
         if getattr(it, "asyncSupported", lambda: False)() and not isinstance(it, AsyncDataSetIterator) and \
                 type(it).__name__ not in ("BenchmarkDataSetIterator", "ListDataSetIterator"):
@@ -373,6 +377,36 @@ class MultiLayerNetwork(BaseNetwork):
 
     def clearLayerMaskArrays(self):
         self.mask = self.labelsMask = None
+
+    # ------------------------------------------------------------------------------ pretraining
+    def pretrainLayer(self, layerIdx, data, numEpochs=1):
+        """Unsupervised pretraining of one AutoEncoder / VAE layer (reference MultiLayerNetwork.pretrainLayer):
+        inputs are the activations of layers [0, layerIdx) in inference mode."""
+        if not self.initCalled:
+            self.init()
+        impl = self.layers[layerIdx]
+        if not hasattr(impl, "computePretrainGradientAndScore"):
+            return self
+        for _ in range(numEpochs):
+            items = [data] if isinstance(data, DataSet) or torch.is_tensor(data) else data
+            if not isinstance(items, list):
+                items.reset()
+            for ds in items:
+                f = ds if torch.is_tensor(ds) else ds.features
+                x = self._to_dev(f, self._feat_dtype())
+                with torch.no_grad():
+                    if layerIdx > 0:
+                        x = self.feedForwardToLayer(layerIdx - 1, x, False)[-1]
+                    x = self._pp(layerIdx, x, x.shape[0], False)
+                self._pretrain_step(impl, x)
+        return self
+
+    def pretrain(self, data, numEpochs=1):
+        """Layer-wise pretraining of every pretrainable layer in order (reference MultiLayerNetwork.pretrain)."""
+        for i, l in enumerate(self.layers):
+            if hasattr(l, "computePretrainGradientAndScore"):
+                self.pretrainLayer(i, data, numEpochs)
+        return self
 
     def toComputationGraph(self):
         from ..utils.network_utils import to_computation_graph

@@ -165,6 +165,27 @@ class BaseNetwork:
         ds = MultiDataSet(x, y, fmask, lmask) if isinstance(x, (list, tuple)) else DataSet(x, y, fmask, lmask)
         return self._score_dataset(ds, training=True)
 
+    # ------------------------------------------------------------------------------ layer-wise pretraining
+    def _layer_range(self, impl):
+        for _, _, li, off in self._layer_offsets:
+            if li is impl:
+                n = sum(s.numel for s in impl.conf.param_specs())
+                return off, off + n
+        raise KeyError("layer not part of this network")
+
+    def _pretrain_step(self, impl, x):
+        """One unsupervised step of a pretrain layer (AutoEncoder / VAE) on its own input activations
+        (reference MultiLayerNetwork.pretrainLayer -> layer.fit): only that layer's params/state change."""
+        self.flattenedGradients.zero_()
+        score = impl.computePretrainGradientAndScore(x)
+        lo, hi = self._layer_range(impl)
+        self.updater.update_range(self.flattenedParams, self.flattenedGradients, self.conf.iterationCount,
+                                  self.conf.epochCount, x.shape[0], lo, hi)
+        self._params_changed()
+        self._score_t, self._score_val = score, None
+        self._iteration_done()
+        return score
+
     def getLastEtlTime(self):
         return getattr(self, "lastEtlTime", 0.0)
 

@@ -141,6 +141,25 @@ class NetworkUpdater:
         fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
                      self.net.conf.globalConf.get("miniBatch", True), shadow, reg_out=reg_out)
 
+    def update_range(self, params, grad, iteration, epoch, batch_size, lo, hi):
+        """Update only the parameters in the flat range [lo, hi) (layer-wise pretraining): the fused update
+        runs over everything, then parameters and updater state outside the range are restored."""
+        keep_p = params.clone()
+        keep_s = self.state.clone() if self.state is not None else None
+        self.update(params, grad, iteration, epoch, batch_size)
+        inside = torch.zeros(params.numel(), dtype=torch.bool, device=params.device)
+        inside[lo:hi] = True
+        params.copy_(torch.where(inside, params, keep_p))
+        if keep_s is not None and keep_s.numel():
+            smask = torch.zeros(keep_s.numel(), dtype=torch.bool, device=keep_s.device)
+            for sg in self.plan.segments:
+                if lo <= sg.p_off < hi and sg.block_n > 0:
+                    comps = sg.updater.stateSize(sg.block_n) // sg.block_n
+                    for c in range(comps):
+                        a = sg.st_off + c * sg.block_n + sg.in_block
+                        smask[a:a + sg.n] = True
+            self.state.copy_(torch.where(smask, self.state, keep_s))
+
     # learning-rate control (reference MultiLayerNetwork.setLearningRate :3411-3459)
     def setLearningRate(self, lr, layer_name=None):
         for b in self.blocks:
