@@ -334,6 +334,12 @@ class BaseNetwork:
             if hasattr(l, "onGradientCalculation"):
                 l.onGradientCalculation(self)
         acc = getattr(self, "gradientsAccumulator", None)
+        if acc is not None and getattr(acc, "handles_update", False):
+            # encoded update sharing: the accumulator runs updater -> encode -> exchange -> apply itself
+            acc.apply_update(self, batch_size, it, ep)
+            self._loss_part = None
+            self._score_val = None
+            return
         if acc is not None:
             acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
             batch_size = batch_size * acc.world_size

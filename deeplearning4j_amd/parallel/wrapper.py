@@ -1,0 +1,179 @@
+"""ParallelWrapper: single-node data-parallel training (reference PW:ParallelWrapper.java:123-904,
+PW:trainer/DefaultTrainer.java, PW:trainer/SymmetricTrainer.java).
+
+MI355X-first design: ONE PROCESS PER GPU (``torchrun --nproc-per-node 8``), each holding a full replica in its
+own HBM, talking over RCCL/xGMI. The reference's N worker threads sharing one JVM become N ranks; the
+round-robin feeding of DataSets to worker queues becomes a rank-strided view of the iterator (rank r trains on
+batches r, r+W, r+2W, ...), so W consecutive batches form one synchronous step exactly as the reference's
+"after every `workers` batches wait for all" loop.
+
+Training modes (ParallelWrapper.TrainingMode):
+  * SHARED_GRADIENTS (default here): synchronous DP. Dense bucketed all-reduce of the summed gradient, issued
+    during backward (AllReduceGradientsAccumulator), then one fused update with the GLOBAL minibatch —
+    numerically the single-GPU large-batch step.
+    ``gradientsAccumulator(EncodedGradientsAccumulator(...))`` selects the reference's threshold-encoded
+    update sharing instead (the post-updater update is residual-encoded and exchanged).
+  * AVERAGING: local SGD; every ``averagingFrequency`` iterations parameters (and updater state when
+    ``averageUpdaters``) are averaged with an all-reduce (reference Nd4j.averageAndPropagate, :316-376).
+  * CUSTOM: a user accumulator (any object with begin_backward/grad_ready/reduce_gradients or apply_update).
+Without an initialised process group (W == 1) the wrapper simply trains the model.
+"""
+import enum
+import logging
+
+from ..datasets.dataset import DataSet, MultiDataSet
+from .accumulation import AllReduceGradientsAccumulator, average_params_and_state
+from .distributed import barrier, is_dist, rank, world_size
+
+log = logging.getLogger("deeplearning4j_amd")
+
+
+class TrainingMode(enum.Enum):
+    AVERAGING = "AVERAGING"
+    SHARED_GRADIENTS = "SHARED_GRADIENTS"
+    CUSTOM = "CUSTOM"
+
+
+class _RankShard:
+    """Rank-strided view of a DataSetIterator: rank r sees batches r, r+W, ... Every rank sees the same number
+    of batches (a trailing partial round is dropped) so the collectives stay matched."""
+
+    def __init__(self, it, r, w):
+        self.it, self.r, self.w = it, r, w
+
+    def __iter__(self):
+        if hasattr(self.it, "reset"):
+            self.it.reset()
+        buf = []
+        while self.it.hasNext():
+            buf.append(self.it.next())
+            if len(buf) == self.w:
+                yield buf[self.r]
+                buf = []
+
+
+class ParallelWrapper:
+    TrainingMode = TrainingMode
+
+    def __init__(self, model, workers=None, prefetchBuffer=16, averagingFrequency=1, averageUpdaters=True,
+                 reportScoreAfterAveraging=False, trainingMode=TrainingMode.SHARED_GRADIENTS,
+                 gradientsAccumulator=None, bucket_mb=None):
+        self.model = model
+        self.workers = workers or world_size()
+        if is_dist() and self.workers != world_size():
+            log.warning("ParallelWrapper: workers=%d but world size is %d; one worker per rank is used",
+                        self.workers, world_size())
+            self.workers = world_size()
+        self.prefetchBuffer = prefetchBuffer
+        self.averagingFrequency = max(1, int(averagingFrequency))
+        self.averageUpdaters = averageUpdaters
+        self.reportScoreAfterAveraging = reportScoreAfterAveraging
+        self.trainingMode = trainingMode
+        self.accumulator = gradientsAccumulator
+        self.bucket_mb = bucket_mb
+        self._prepared = False
+        self._iter = 0
+        self.listeners = []
+
+    class Builder:
+        def __init__(self, model):
+            self._kw = {"model": model}
+
+        def workers(self, n):
+            self._kw["workers"] = int(n)
+            return self
+
+        def prefetchBuffer(self, n):
+            self._kw["prefetchBuffer"] = int(n)
+            return self
+
+        def averagingFrequency(self, n):
+            self._kw["averagingFrequency"] = int(n)
+            return self
+
+        def averageUpdaters(self, b):
+            self._kw["averageUpdaters"] = bool(b)
+            return self
+
+        def reportScoreAfterAveraging(self, b):
+            self._kw["reportScoreAfterAveraging"] = bool(b)
+            return self
+
+        def trainingMode(self, m):
+            self._kw["trainingMode"] = TrainingMode(m) if not isinstance(m, TrainingMode) else m
+            return self
+
+        def gradientsAccumulator(self, acc):
+            self._kw["gradientsAccumulator"] = acc
+            self._kw.setdefault("trainingMode", TrainingMode.CUSTOM)
+            return self
+
+        def bucketSizeMB(self, mb):
+            self._kw["bucket_mb"] = mb
+            return self
+
+        def build(self):
+            return ParallelWrapper(**self._kw)
+
+    def setListeners(self, *ls):
+        self.model.setListeners(*ls)
+
+    def _prepare(self):
+        if self._prepared:
+            return
+        m = self.model
+        if not m.initCalled:
+            m.init()
+        if is_dist():
+            # every replica starts from rank 0's parameters and updater state (DefaultTrainer.java:254-311)
+            AllReduceGradientsAccumulator().broadcast_params(m, 0)
+        if self.trainingMode == TrainingMode.SHARED_GRADIENTS and self.accumulator is None:
+            self.accumulator = AllReduceGradientsAccumulator(self.bucket_mb)
+        if self.trainingMode in (TrainingMode.SHARED_GRADIENTS, TrainingMode.CUSTOM) and self.accumulator is not None:
+            m.setGradientsAccumulator(self.accumulator)
+        self._prepared = True
+
+    def fit(self, source, numEpochs=1):
+        """Train on a DataSetIterator / MultiDataSetIterator (or a list of DataSets) for ``numEpochs``."""
+        self._prepare()
+        m = self.model
+        W, r = world_size(), rank()
+        for _ in range(int(numEpochs)):
+            for l in m.listeners:
+                if hasattr(l, "onEpochStart"):
+                    l.onEpochStart(m)
+            items = _RankShard(source, r, W) if W > 1 else (source if not hasattr(source, "reset") else
+                                                            _RankShard(source, 0, 1))
+            for ds in items:
+                self._step(ds)
+            for l in m.listeners:
+                if hasattr(l, "onEpochEnd"):
+                    l.onEpochEnd(m)
+            m.incrementEpochCount()
+        if self.trainingMode == TrainingMode.AVERAGING and self._iter % self.averagingFrequency != 0:
+            average_params_and_state(m, self.averageUpdaters)       # final sync so all replicas agree
+        barrier()
+        return m
+
+    def _step(self, ds):
+        m = self.model
+        if isinstance(ds, MultiDataSet):
+            m._fit_batch(ds.features, ds.labels, ds.featuresMasks, ds.labelsMasks)
+        elif isinstance(ds, DataSet):
+            if type(m).__name__ == "ComputationGraph":
+                m._fit_batch([ds.features], [ds.labels], None if ds.featuresMask is None else [ds.featuresMask],
+                             None if ds.labelsMask is None else [ds.labelsMask])
+            else:
+                m._fit_batch(ds.features, ds.labels, ds.featuresMask, ds.labelsMask)
+        else:
+            raise TypeError(f"unsupported batch type {type(ds)}")
+        self._iter += 1
+        if self.trainingMode == TrainingMode.AVERAGING and self._iter % self.averagingFrequency == 0:
+            average_params_and_state(m, self.averageUpdaters)
+            if self.reportScoreAfterAveraging:
+                log.info("Averaged score: %s", m.score())
+
+    def shutdown(self):
+        pass
+
+    close = shutdown

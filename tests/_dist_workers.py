@@ -1,0 +1,64 @@
+"""Worker bodies for the multi-process (gloo, world_size 2) data-parallel tests in test_parallel.py."""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def _setup(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def make_net(updater):
+    from deeplearning4j_amd import (Activation, DenseLayer, LossFunction, MultiLayerNetwork, NeuralNetConfiguration,
+                                    OutputLayer)
+    conf = (NeuralNetConfiguration.Builder().seed(11).updater(updater).l2(1e-3).list()
+            .layer(0, DenseLayer.Builder().nIn(5).nOut(12).activation(Activation.TANH).build())
+            .layer(1, OutputLayer.Builder(LossFunction.MCXENT).nIn(12).nOut(3).activation(Activation.SOFTMAX).build())
+            .build())
+    net = MultiLayerNetwork(conf)
+    net.init(device=torch.device("cpu"))
+    return net
+
+
+def make_batches(n_batches, bs, seed=5):
+    from deeplearning4j_amd import DataSet
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n_batches):
+        x = torch.randn(bs, 5, generator=g)
+        y = torch.zeros(bs, 3)
+        y[torch.arange(bs), torch.randint(0, 3, (bs,), generator=g)] = 1
+        out.append(DataSet(x, y))
+    return out
+
+
+def run_mode(rank, world, port, mode, result_path):
+    _setup(rank, world, port)
+    from deeplearning4j_amd import Adam, ListDataSetIterator
+    from deeplearning4j_amd.parallel import EncodedGradientsAccumulator, ParallelWrapper, TrainingMode
+    net = make_net(Adam(0.01) if mode != "encoded" else Adam(0.5))
+    if rank == 1:                                   # replicas must be synchronised from rank 0 by the wrapper
+        with torch.no_grad():
+            net.flattenedParams.add_(1.0)
+    batches = make_batches(8, 8)
+    it = ListDataSetIterator(batches, 8)
+    b = ParallelWrapper.Builder(net)
+    if mode == "shared":
+        b.trainingMode(TrainingMode.SHARED_GRADIENTS)
+    elif mode == "averaging":
+        b.trainingMode(TrainingMode.AVERAGING).averagingFrequency(2).averageUpdaters(True)
+    elif mode == "encoded":
+        b.gradientsAccumulator(EncodedGradientsAccumulator(threshold=1e-3))
+    pw = b.build()
+    pw.fit(it, 2)
+    p = net.params().clone()
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        torch.save({"params": [t.clone() for t in gathered], "iters": net.getIterationCount()}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -171,3 +171,28 @@ def test_batchnorm_residual_relu_fused(cuda, dtype):
     _close(dr, dr_ref, tol)
     _close(dgm, dg_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)
     _close(dbt, db_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)
+
+
+@pytest.mark.parametrize("n", [1000, 2048 * 37 + 5, 300000])
+def test_threshold_codec_gpu_matches_cpu(cuda, n):
+    from deeplearning4j_amd.ops import compression as C
+    g = torch.Generator().manual_seed(11)
+    r = torch.randn(n, generator=g) * 1e-3
+    thr = 1.2e-3
+    rc, rg = r.clone(), r.to(cuda)
+    assert C.threshold_count(rg, thr) == C.threshold_count(rc, thr)
+    mc = C.threshold_encode(rc, thr, capacity=n)
+    mg = C.threshold_encode(rg, thr, capacity=n)
+    assert torch.equal(mg.cpu(), mc)                    # deterministic, in-order compaction
+    assert torch.equal(rg.cpu(), rc)
+    dc = C.decode(mc, torch.zeros(n))
+    dg = C.decode(mg, torch.zeros(n, device=cuda))
+    assert torch.equal(dg.cpu(), dc)
+    r2c, r2g = r.clone(), r.to(cuda)
+    bc, bg = C.bitmap_encode(r2c, thr), C.bitmap_encode(r2g, thr)
+    assert torch.equal(bg.cpu(), bc) and torch.equal(r2g.cpu(), r2c)
+    assert torch.equal(C.decode(bg, torch.zeros(n, device=cuda)).cpu(), C.decode(bc, torch.zeros(n)))
+    r3 = r.to(cuda)
+    m3 = C.threshold_encode(r3, thr, capacity=17)       # capacity clamp keeps the rest in the residual
+    assert int(m3[0]) == 17
+    assert torch.allclose((C.decode(m3, torch.zeros(n, device=cuda)) + r3).cpu(), r, atol=1e-7)

@@ -1,0 +1,127 @@
+"""Data-parallel training and parallel inference (reference PW tests: ParallelWrapperTest.java,
+ParallelInferenceTest.java; NN: EncodedGradientsAccumulatorTest.java, threshold codec tests).
+Multi-process paths run with gloo, world_size 2, on CPU (the RCCL path is the same code with backend nccl)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from deeplearning4j_amd.ops import compression as C
+
+import _dist_workers as W
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(mode, tmp_path):
+    path = str(tmp_path / f"{mode}.pt")
+    mp.spawn(W.run_mode, args=(2, _port(), mode, path), nprocs=2, join=True)
+    return torch.load(path, weights_only=True)
+
+
+def test_threshold_codec_cpu():
+    g = torch.Generator().manual_seed(0)
+    r = torch.randn(10000, generator=g) * 1e-3
+    r0 = r.clone()
+    thr = 1.5e-3
+    n_expected = int((r.abs() >= thr).sum())
+    assert C.threshold_count(r, thr) == n_expected
+    msg = C.threshold_encode(r, thr, capacity=r.numel())
+    assert int(msg[0]) == n_expected and int(msg[3]) == C.SPARSE
+    idx = msg[4:4 + n_expected].long()
+    assert torch.equal(idx.abs() - 1, (r0.abs() >= thr).nonzero().reshape(-1))     # in-order
+    dec = C.decode(msg, torch.zeros_like(r))
+    assert torch.allclose(dec + r, r0, atol=1e-7)          # decoded + residual == original
+    # bitmap
+    r2 = r0.clone()
+    bm = C.bitmap_encode(r2, thr)
+    assert bm.numel() == C.bitmap_capacity(r0.numel()) and int(bm[0]) == n_expected
+    dec2 = C.decode(bm, torch.zeros_like(r0))
+    assert torch.allclose(dec2, dec) and torch.allclose(r2, r)
+    # capacity limit: only the first entries are emitted, the rest stay in the residual
+    r3 = r0.clone()
+    m3 = C.threshold_encode(r3, thr, capacity=5)
+    assert int(m3[0]) == 5
+    assert torch.allclose(C.decode(m3, torch.zeros_like(r0)) + r3, r0, atol=1e-7)
+
+
+def test_encoding_handler_switches_modes():
+    from deeplearning4j_amd.parallel import EncodingHandler
+    h = EncodingHandler(threshold=1e-2)
+    sparse = torch.zeros(3200)
+    sparse[::100] = 0.05
+    m = h.encodeUpdates(sparse.clone())
+    assert int(m[3]) == C.BITMAP          # starts in bitmap mode
+    assert not h.bitmapMode               # ...and switches to sparse because few values were encoded
+    m = h.encodeUpdates(sparse.clone())
+    assert int(m[3]) == C.SPARSE
+    dense = torch.full((3200,), 0.05)
+    m = h.encodeUpdates(dense)
+    assert int(m[3]) == C.BITMAP and h.bitmapMode
+
+
+def test_parallel_wrapper_shared_gradients_equals_large_batch(tmp_path):
+    res = _run("shared", tmp_path)
+    p0, p1 = res["params"]
+    assert torch.equal(p0, p1)                  # replicas identical
+    # single process, global batch = concat of the two ranks' batches, same number of steps
+    from deeplearning4j_amd import Adam, DataSet
+    net = W.make_net(Adam(0.01))
+    batches = W.make_batches(8, 8)
+    for _ in range(2):
+        for i in range(0, 8, 2):
+            a, b = batches[i], batches[i + 1]
+            net.fit(DataSet(torch.cat([a.features, b.features]), torch.cat([a.labels, b.labels])))
+    assert torch.allclose(net.params(), p0, atol=1e-5), (net.params() - p0).abs().max()
+    assert res["iters"] == 8
+
+
+def test_parallel_wrapper_averaging(tmp_path):
+    res = _run("averaging", tmp_path)
+    p0, p1 = res["params"]
+    assert torch.allclose(p0, p1, atol=1e-6)
+    init = W.make_net(__import__("deeplearning4j_amd").Adam(0.01)).params()
+    assert not torch.allclose(p0, init)
+
+
+def test_parallel_wrapper_encoded_updates(tmp_path):
+    res = _run("encoded", tmp_path)
+    p0, p1 = res["params"]
+    assert torch.equal(p0, p1)                  # every rank applies the same decoded sum
+    init = W.make_net(__import__("deeplearning4j_amd").Adam(0.5)).params()
+    assert not torch.allclose(p0, init)
+
+
+def test_parallel_inference_batched_and_sequential():
+    from deeplearning4j_amd import Adam
+    from deeplearning4j_amd.parallel import InferenceMode, ParallelInference
+    net = W.make_net(Adam(0.01))
+    xs = [torch.randn(3, 5) for _ in range(12)]
+    ref = [net.output(x) for x in xs]
+    for mode in (InferenceMode.BATCHED, InferenceMode.SEQUENTIAL):
+        pi = ParallelInference.Builder(net).inferenceMode(mode).batchLimit(8).devices(
+            [torch.device("cpu"), torch.device("cpu")]).build()
+        futs = [pi.submit(x) for x in xs]
+        outs = [f.result(timeout=60) for f in futs]
+        pi.shutdown()
+        for o, r in zip(outs, ref):
+            assert torch.allclose(o, r, atol=1e-6)
+
+
+@pytest.mark.skipif(os.environ.get("DL4J_AMD_SKIP_SLOW") == "1", reason="slow")
+def test_wrapper_single_process_trains():
+    from deeplearning4j_amd import Adam, ListDataSetIterator
+    from deeplearning4j_amd.parallel import ParallelWrapper
+    net = W.make_net(Adam(0.05))
+    it = ListDataSetIterator(W.make_batches(4, 16), 16)
+    s0 = net.score(W.make_batches(1, 64, seed=9)[0])
+    ParallelWrapper.Builder(net).build().fit(it, 5)
+    assert net.score(W.make_batches(1, 64, seed=9)[0]) < s0 + 0.5
