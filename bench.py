@@ -31,8 +31,8 @@ def main():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 256)), help="per-GPU batch")
     ap.add_argument("--variant", default=os.environ.get("BENCH_VARIANT", "dl4j"), choices=["dl4j", "canonical"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--graph", type=int, default=int(os.environ.get("BENCH_GRAPH", "0")),
-                    help="capture the training step in a HIP graph")
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("BENCH_GRAPH", "-1")),
+                    help="capture the training step in HIP graphs (1 on, 0 off, -1 auto = on for one process)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -53,6 +53,10 @@ def main():
         acc = AllReduceGradientsAccumulator()
         acc.broadcast_params(net)
         net.setGradientsAccumulator(acc)
+
+    use_graph = args.graph if args.graph >= 0 else int(world == 1 and device.type == "cuda")
+    if use_graph:
+        net.enableHipGraphs(True, warmup=1)
 
     B = args.batch
     g = torch.Generator(device="cpu").manual_seed(42 + rank)
@@ -102,6 +106,7 @@ def main():
             "config": {"model": model_name, "variant": args.variant, "global_batch": B * world, "per_gpu_batch": B,
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
                        "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
+                       "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
                        "final_score": final_score},
         }), flush=True)
     from deeplearning4j_amd.parallel.distributed import destroy

@@ -43,6 +43,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Division by a runtime-uniform divisor via multiply-high (CUTLASS-style FastDivmod); valid for n < 2^31.
+struct FastDiv {
+  unsigned d, mul, shr;
+};
+static inline FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) { f.mul = 0; f.shr = 0; return f; }
+  unsigned l = 0;
+  while ((1u << l) < d) ++l;                       // ceil(log2 d)
+  const unsigned p = 31 + l;
+  f.mul = (unsigned)(((1ull << p) + d - 1) / d);
+  f.shr = p - 32;
+  return f;
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+  return f.d == 1 ? n : (__umulhi(n, f.mul) >> f.shr);
+}
+
 // byte offset of (row, 16-byte chunk) in a swizzled [rows][4 chunks] K-contiguous tile
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
@@ -201,6 +220,265 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restr
 }
 
 // ------------------------------------------------------------------------------------------------------
+// FWD / BWD-DATA, LDS-DMA pipeline (v2). Same math and output as igemm_fwd_kernel, but operand tiles go
+// global -> LDS with global_load_lds_dwordx4 (no VGPR staging) through a G_STAGES-deep ring, so up to
+// G_STAGES-1 K-steps of loads are in flight per block. The ResNet convs here have only 2-72 K-steps and
+// 100-800 tiles: per-block load latency, not MFMA issue, sets their time, so the pipeline depth is the lever.
+// LDS image is lane-linear per wave-instruction (16 rows x 64 B); the XOR chunk swizzle is applied on the
+// SOURCE address (lane slot s of row r loads chunk s ^ f(r)) and undone by the same swz() on the read.
+// Padding / out-of-range lanes load from a 16-byte zero page, which keeps every DMA unconditional.
+// Waits: counted `s_waitcnt vmcnt` (4 DMAs per thread per stage) + raw s_barrier, never __syncthreads() (its
+// fence would drain the DMAs still in flight for the next stages).
+// ------------------------------------------------------------------------------------------------------
+#define G_STAGES 4
+#define G_STAGE_BYTES (2 * TILE_N * TILE_K * 2)
+
+__device__ __attribute__((aligned(64))) char g_zero_page[64];
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_stage(int ahead) {
+  // ahead = number of later stages whose 4 DMAs/thread may stay in flight
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// FAST (C % TILE_K == 0): every K-step stays inside one filter tap (r, s), so the step's source offset is a
+// wave-uniform scalar (SALU) added to a per-lane pixel base, and tap validity is one bit of a per-lane mask —
+// the DMA issue costs a handful of VALU ops instead of a division/while-loop/bounds-check chain per step.
+template <bool FAST>
+__global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                                                            const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                            ConvGeom g, int Kred, int scatter, int out_H, int out_W) {
+  __shared__ __attribute__((aligned(16))) char smem[G_STAGES * G_STAGE_BYTES];   // 64 KB -> 2 blocks / CU
+  const int M = g.N * g.OH * g.OW;
+  const int Nout = g.K;
+  const int tiles_m = (M + TILE_M - 1) / TILE_M;
+  const int tiles_n = (Nout + TILE_N - 1) / TILE_N;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  if (tm >= tiles_m) return;
+  const int n0 = tn * TILE_N, m0 = tm * TILE_M;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 1, wm = wid & 1;
+
+  // DMA assignment: round i covers rows (i*4 + wid)*16 + lane/4, lane slot lane&3 -> source chunk slot^f(row)
+  const bf16* wrow[2];
+  bool wok[2];
+  int chunk[2], pn[2], pih[2], piw[2], cc[2], rr[2], ss[2];
+  bool pok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (i * 4 + wid) * 16 + (lane >> 2);
+    chunk[i] = (lane & 3) ^ ((row >> 2) & 3);
+    const int n = n0 + row;
+    wok[i] = n < Nout;
+    wrow[i] = Wt + (long long)(wok[i] ? n : 0) * Kred + chunk[i] * 8;
+    const int m = m0 + row;
+    pok[i] = m < M;
+    const int mm = pok[i] ? m : 0;
+    const int ow = mm % g.OW, t = mm / g.OW;
+    const int oh = t % g.OH;
+    pn[i] = t / g.OH;
+    pih[i] = oh * g.sh - g.ph;
+    piw[i] = ow * g.sw - g.pw;
+    const int kc = chunk[i] * 8;
+    cc[i] = kc % g.C;
+    const int rs = kc / g.C;
+    rr[i] = rs / g.S;
+    ss[i] = rs % g.S;
+  }
+  const int nk = (Kred + TILE_K - 1) / TILE_K;
+  // FAST-path state: per-lane pixel base offsets + tap-validity masks, uniform tap counters
+  long long pbase[2];
+  unsigned long long vmask[2];
+  if (FAST) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      pbase[i] = (((long long)pn[i] * g.H + pih[i]) * g.W + piw[i]) * g.C + chunk[i] * 8;
+      unsigned long long mk = 0;
+      for (int r = 0; r < g.R; ++r)
+        for (int q = 0; q < g.S; ++q) {
+          const int ih = pih[i] + r * g.dh, iw = piw[i] + q * g.dw;
+          if (pok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) mk |= 1ull << (r * g.S + q);
+        }
+      vmask[i] = mk;
+    }
+  }
+  int u_c = 0, u_rs = 0, u_r = 0, u_s = 0;     // uniform: channel offset and tap of the next step to issue
+
+  auto issue = [&](int kt, int buf) {
+    char* A = smem + buf * G_STAGE_BYTES;
+    char* B = A + TILE_N * TILE_K * 2;
+    if (FAST) {
+      const long long uoff = ((long long)(u_r * g.dh) * g.W + u_s * g.dw) * g.C + u_c;
+      const int k0 = kt * TILE_K;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const void* sa = wok[i] ? (const void*)(wrow[i] + k0) : (const void*)g_zero_page;
+        const void* sb = ((vmask[i] >> u_rs) & 1ull) ? (const void*)(X + pbase[i] + uoff) : (const void*)g_zero_page;
+        glds16(sa, A + (i * 4 + wid) * 1024);
+        glds16(sb, B + (i * 4 + wid) * 1024);
+      }
+      u_c += TILE_K;
+      if (u_c == g.C) { u_c = 0; ++u_rs; if (++u_s == g.S) { u_s = 0; ++u_r; } }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = kt * TILE_K + chunk[i] * 8;
+      const bool kin = k < Kred;
+      const void* sa = (wok[i] && kin) ? (const void*)(wrow[i] + kt * TILE_K) : (const void*)g_zero_page;
+      const int ih = pih[i] + rr[i] * g.dh, iw = piw[i] + ss[i] * g.dw;
+      const bool bok = pok[i] && kin && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const void* sb = bok ? (const void*)(X + (((long long)pn[i] * g.H + ih) * g.W + iw) * g.C + cc[i])
+                           : (const void*)g_zero_page;
+      glds16(sa, A + (i * 4 + wid) * 1024);
+      glds16(sb, B + (i * 4 + wid) * 1024);
+      cc[i] += TILE_K;
+      while (cc[i] >= g.C) { cc[i] -= g.C; if (++ss[i] == g.S) { ss[i] = 0; ++rr[i]; } }
+    }
+  };
+
+  f32x16_t acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < G_STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(G_STAGES - 2, nk - 1 - kt);
+    wait_stage(ahead);
+    raw_barrier();
+    if (kt + G_STAGES - 1 < nk) issue(kt + G_STAGES - 1, (kt + G_STAGES - 1) % G_STAGES);
+    const char* A = smem + (kt % G_STAGES) * G_STAGE_BYTES;
+    const char* B = A + TILE_N * TILE_K * 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 2 + (lane >> 5);
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = *reinterpret_cast<const bf16x8_t*>(A + swz(wn * 64 + a * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = *reinterpret_cast<const bf16x8_t*>(B + swz(wm * 64 + b * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue through LDS: acc (D[n][m]) -> bf16 tile [m][n] (row pitch 272 B) -> 16-byte coalesced row
+  // stores (each output pixel row of the tile is 256 contiguous bytes in NHWC).
+  const int hh = lane >> 5;
+  if ((Nout & 7) == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();                                   // all waves are done reading the operand ring
+    char* T = smem;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ml = wm * 64 + b * 32 + (lane & 31);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = wn * 64 + a * 32 + 8 * q + 4 * hh;
+          const int n = n0 + nl;
+          u16 o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = acc[a][b][4 * q + j];
+            if (bias && n + j < Nout) v += bias[n + j];
+            o[j] = f2bf(v);
+          }
+          uint2 pk;
+          pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          *reinterpret_cast<uint2*>(T + ml * 272 + nl * 2) = pk;
+        }
+      }
+    }
+    raw_barrier();
+    const int ch = tid & 15;
+    const int n = n0 + ch * 8;
+#pragma unroll 2
+    for (int pass = 0; pass < 8; ++pass) {
+      const int ml = pass * 16 + (tid >> 4);
+      const int m = m0 + ml;
+      if (m >= M || n >= Nout) continue;
+      long long orow;
+      if (scatter > 0) {
+        const int ow = m % g.OW, t = m / g.OW;
+        const int oh = t % g.OH, nn = t / g.OH;
+        orow = ((long long)nn * out_H + oh * scatter) * out_W + ow * scatter;
+      } else {
+        orow = m;
+      }
+      *reinterpret_cast<uint4*>(Y + orow * Nout + n) = *reinterpret_cast<const uint4*>(T + ml * 272 + ch * 16);
+    }
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int m = m0 + wm * 64 + b * 32 + (lane & 31);
+    if (m >= M) continue;
+    long long orow;
+    if (scatter > 0) {
+      const int ow = m % g.OW, t = m / g.OW;
+      const int oh = t % g.OH, n = t / g.OH;
+      orow = ((long long)n * out_H + oh * scatter) * out_W + ow * scatter;
+    } else {
+      orow = m;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * 64 + a * 32 + 8 * q + 4 * hh;
+        if (n >= Nout) continue;
+        u16 o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = acc[a][b][4 * q + j];
+          if (bias) v += bias[n + j];
+          o[j] = f2bf(v);
+        }
+        uint2 pk;
+        pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+        pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+        *reinterpret_cast<uint2*>(Y + orow * Nout + n) = pk;
+      }
+    }
+  }
+}
+
+static int g_fwd_variant = 1;   // 1 = LDS-DMA pipeline (default), 0 = register-staged kernel
+DL4J_API void dl4j_conv_set_variant(int v) { g_fwd_variant = v; }
+
+#define LAUNCH_FWD(fast, grid, ...)                                                                        \
+  do {                                                                                                      \
+    if (g_fwd_variant == 1 && (fast))                                                                       \
+      hipLaunchKernelGGL(igemm_fwd_glds<true>, grid, dim3(NTHREADS), 0, s, __VA_ARGS__);                    \
+    else if (g_fwd_variant == 1) hipLaunchKernelGGL(igemm_fwd_glds<false>, grid, dim3(NTHREADS), 0, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL(igemm_fwd_kernel, grid, dim3(NTHREADS), 0, s, __VA_ARGS__);                    \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------------
 // WRW: dW[k][rsc] += sum_m dY[m][k] * im2col(X)[m][rsc] over this block's m-range (split-K over pixels).
 // Tiles are m-major ([32 m][128 cols], rows padded to 320 B) and read with ds_read_b64_tr_b16.
 // ------------------------------------------------------------------------------------------------------
@@ -208,7 +486,7 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restr
 
 __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                               float* __restrict__ dW, float* __restrict__ db,
-                                                              ConvGeom g, int m_per_split) {
+                                                              ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_K * WRW_ROW];   // 2 buffers x (A + B) = 40 KB
   const int M = g.N * g.OH * g.OW;
   const int Kout = g.K;
@@ -232,16 +510,10 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
   const int jc = jok ? jcol : 0;
   const int cc = jc % g.C, rs = jc / g.C;
   const int rr = rs / g.S, ss = rs % g.S;
-  // running pixel coordinates of the two rows
-  int pm[2], pn[2], poh[2], pow_[2];
-  for (int i = 0; i < 2; ++i) {
-    pm[i] = mbeg + lrow + 16 * i;
-    const int mm = pm[i] < M ? pm[i] : 0;
-    pow_[i] = mm % g.OW;
-    const int t = mm / g.OW;
-    poh[i] = t % g.OH;
-    pn[i] = t / g.OH;
-  }
+  // pixel rows of this thread (advanced by TILE_K per step; coordinates re-derived with multiply-high division)
+  int pm[2];
+  for (int i = 0; i < 2; ++i) pm[i] = mbeg + lrow + 16 * i;
+  const int rdh = rr * g.dh - g.ph, sdw = ss * g.dw - g.pw;
   float bsum[8];
   const bool do_bias = (db != nullptr) && (tj == 0);
   for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
@@ -259,9 +531,14 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
       const bool mok = pm[i] < mend;
       if (mok && kok) areg[i] = *reinterpret_cast<const uint4*>(dY + (long long)pm[i] * Kout + kcol);
       else areg[i] = make_uint4(0, 0, 0, 0);
-      const int ih = poh[i] * g.sh - g.ph + rr * g.dh, iw = pow_[i] * g.sw - g.pw + ss * g.dw;
+      const unsigned mm = mok ? (unsigned)pm[i] : 0u;
+      const unsigned t = fdiv(mm, fOW);
+      const int ow = (int)(mm - t * fOW.d);
+      const unsigned pn = fdiv(t, fOH);
+      const int oh = (int)(t - pn * fOH.d);
+      const int ih = oh * g.sh + rdh, iw = ow * g.sw + sdw;
       if (mok && jok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-        breg[i] = *reinterpret_cast<const uint4*>(X + (((long long)pn[i] * g.H + ih) * g.W + iw) * g.C + cc);
+        breg[i] = *reinterpret_cast<const uint4*>(X + (((long long)pn * g.H + ih) * g.W + iw) * g.C + cc);
       else breg[i] = make_uint4(0, 0, 0, 0);
       if (do_bias && mok && kok) {
 #pragma unroll
@@ -271,10 +548,7 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
           bsum[2 * e + 1] += bf2f((u16)(w >> 16));
         }
       }
-      // advance this row by 32 pixels
-      pm[i] += TILE_K;
-      pow_[i] += TILE_K;
-      while (pow_[i] >= g.OW) { pow_[i] -= g.OW; if (++poh[i] == g.OH) { poh[i] = 0; ++pn[i]; } }
+      pm[i] += TILE_K;                                  // advance this row by 32 pixels
     }
   };
   auto sstore = [&](int buf) {
@@ -407,8 +681,7 @@ DL4J_API int dl4j_conv_fwd(const void* X, const void* Wkrsc, const float* bias, 
   ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((K + TILE_N - 1) / TILE_N));
-  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)Wkrsc, bias,
-                     (bf16*)Y, g, R * S * C, 0, 0, 0);
+  LAUNCH_FWD(C % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)X, (const bf16*)Wkrsc, bias, (bf16*)Y, g, R * S * C, 0, 0, 0);
   return (int)hipGetLastError();
 }
 
@@ -420,8 +693,9 @@ DL4J_API int dl4j_conv_bwd_data_s1(const void* dY, const void* Wflip, void* dX, 
   ConvGeom g = mk(N, OH, OW, K, H, W, C, R, S, 1, 1, R - 1 - ph, S - 1 - pw, 1, 1);
   const long long M = (long long)N * H * W;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
-  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)dY, (const bf16*)Wflip,
-                     (const float*)nullptr, (bf16*)dX, g, R * S * K, 0, 0, 0);
+  LAUNCH_FWD(K % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr,
+             (bf16*)dX, g, R * S * K, 0, 0,
+             0);
   return (int)hipGetLastError();
 }
 
@@ -432,8 +706,9 @@ DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX,
   ConvGeom g = mk(N, OH, OW, K, OH, OW, C, 1, 1, 1, 1, 0, 0, 1, 1);
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
-  hipLaunchKernelGGL(igemm_fwd_kernel, dim3(tiles), dim3(NTHREADS), 0, s, (const bf16*)dY, (const bf16*)Wflip,
-                     (const float*)nullptr, (bf16*)dX, g, K, stride, H, W);
+  LAUNCH_FWD(K % TILE_K == 0, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr, (bf16*)dX, g, K,
+             stride, H,
+             W);
   return (int)hipGetLastError();
 }
 
@@ -483,6 +758,6 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
   mps = (mps + TILE_K - 1) / TILE_K * TILE_K;
   splits = (M + mps - 1) / mps;
   hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
-                     db, g, mps);
+                     db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
   return (int)hipGetLastError();
 }

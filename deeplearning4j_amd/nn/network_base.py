@@ -154,6 +154,11 @@ class BaseNetwork:
         from .conf.enums import OptimizationAlgorithm as OA
         algo = self.conf.globalConf.get("optimizationAlgo") if hasattr(self.conf, "globalConf") else None
         if algo is None or OA.of(algo) == OA.STOCHASTIC_GRADIENT_DESCENT:
+            if getattr(self, "_hipgraph_enabled", False):
+                xs = list(x) if isinstance(x, (list, tuple)) else [x]
+                ys = list(y) if isinstance(y, (list, tuple)) else [y]
+                if self._try_graph_step(xs, ys, fmask, lmask):
+                    return None
             return self._fit_batch_sgd(x, y, fmask, lmask)
         if getattr(self, "_solver", None) is None:
             from ..optimize.solvers import Solver
@@ -342,13 +347,21 @@ class BaseNetwork:
             return
         if acc is not None:
             acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
+        self._apply_update_kernels(batch_size)
+        self._bump_weight_version()
+
+    def _apply_update_kernels(self, batch_size):
+        """The device work of an update (fused updater + score's regularisation term + constraints); no host
+        bookkeeping, so it can be captured into a HIP graph."""
+        it, ep = self.conf.iterationCount, self.conf.epochCount
+        acc = getattr(self, "gradientsAccumulator", None)
+        mb_local = batch_size
+        if acc is not None:
             batch_size = batch_size * acc.world_size
-        mb_local = batch_size if acc is None else batch_size // acc.world_size
         reg = None
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
             reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)
         self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow, reg)
-        self._bump_weight_version()
         if getattr(self, "_loss_part", None) is not None:
             self._score_t = self._loss_part + (reg[0] / mb_local if reg is not None else 0.0)
             self._loss_part = None
@@ -356,6 +369,38 @@ class BaseNetwork:
         for _, _, impl, _ in self._layer_offsets:
             if getattr(impl.conf, "constraints", None):
                 impl.applyConstraints(it, ep)
+
+    # ------------------------------------------------------------------------------ HIP graphs
+    def enableHipGraphs(self, enabled=True, warmup=2):
+        """Capture the training iteration into HIP graphs after ``warmup`` eager iterations of a fixed batch
+        shape, then replay (see nn/hipgraph.py). Falls back to eager steps whenever a batch is not eligible."""
+        self._hipgraph_enabled = bool(enabled)
+        self._hipgraph_warmup = int(warmup)
+        self._hipgraph = None
+        self._hipgraph_seen = 0
+        return self
+
+    def _try_graph_step(self, inputs, labels, fmasks, lmasks):
+        if not getattr(self, "_hipgraph_enabled", False):
+            return False
+        from .hipgraph import CapturedTrainingStep, graph_eligible
+        inputs = [self._to_dev(t, self._feat_dtype()) for t in inputs]
+        labels = [self._to_dev(t, self.master_dtype) for t in labels]
+        if not graph_eligible(self, inputs, labels, fmasks, lmasks):
+            return False
+        cs = self._hipgraph
+        if cs is not None and cs.ok and cs.shapes_match(inputs, labels):
+            cs.step(inputs, labels)
+            return True
+        self._hipgraph_seen += 1
+        if self._hipgraph_seen <= self._hipgraph_warmup:
+            return False                           # eager warmup iterations populate every cache first
+        cs = CapturedTrainingStep(self, inputs, labels)
+        self._bump_weight_version()
+        cs.capture()                               # a failed capture leaves the stream unusable: let it raise
+        self._hipgraph = cs
+        cs.step(inputs, labels)
+        return True
 
     def _iteration_done(self):
         self.conf.iterationCount += 1

@@ -20,6 +20,7 @@ native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + 
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
+native.register_sig("dl4j_conv_set_variant", [c_int])
 native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p])
 
 # Bumped by every parameter update (BaseNetwork._apply_update / setParams): invalidates relayout caches.
@@ -35,6 +36,11 @@ def _zeroed_wrw_ws(K, R, S, C, device):
         ws = torch.zeros((K, R, S, C), dtype=torch.float32, device=device)
         _wrw_ws[key] = ws
     return ws
+
+
+def set_kernel_variant(v):
+    """1 = LDS-DMA pipelined forward/backward-data kernel (default), 0 = register-staged kernel (A/B testing)."""
+    native.load().dl4j_conv_set_variant(int(v))
 
 
 def bump_version():

@@ -74,9 +74,26 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_CAPTURE_DEBUG = os.environ.get("DL4J_AMD_CAPTURE_DEBUG", "0") == "1"
+_hip = None
+
+
+def capture_status():
+    """hipStreamIsCapturing of torch's current stream: 0 none, 1 active, 2 invalidated."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+        _hip.hipStreamIsCapturing.argtypes = [c_void_p, ctypes.POINTER(c_int)]
+    st = c_int(0)
+    _hip.hipStreamIsCapturing(c_void_p(_stream()), ctypes.byref(st))
+    return st.value
+
+
 def _check(rc, what):
     if rc != 0:
         raise RuntimeError(f"HIP kernel {what} failed with code {rc}")
+    if _CAPTURE_DEBUG and capture_status() == 2:
+        raise RuntimeError(f"stream capture invalidated at/after native call {what}")
 
 
 def _dt(t):
@@ -106,34 +123,108 @@ def _like_rows(x):
 
 # ------------------------------------------------------------------------------------ fused updater
 class _SegTableCache:
+    """Device copy of the updater's per-segment table. Eager: refreshed (pinned host -> device, async) only when
+    the hyperparameters change (schedules, Adam bias correction). Under HIP-graph capture each graph gets its own
+    pinned/device slot; the captured graph contains the copy from that slot's pinned buffer, so updating the
+    pinned bytes before a replay feeds the new iteration's hyperparameters into the graph."""
+
     def __init__(self):
-        self.dev = None
-        self.host_bytes = None
+        self.slots = {}
+        self.btab = None
+        self.nblocks = 0
+
+
+class _Slot:
+    def __init__(self, nbytes, device):
+        self.pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.bytes = None
+        self.event = None     # completes when the last copy out of ``pinned`` has finished
 
 
 _SEG_DTYPE = np.dtype([("p_off", "<i8"), ("n", "<i8"), ("st_off", "<i8"), ("in_block", "<i8"), ("block_n", "<i8"),
                        ("op", "<i4"), ("pad", "<i4"), ("h", "<f4", 4), ("l1", "<f4"), ("l2", "<f4")])
 
+# graph slot currently being captured / replayed (None = eager)
+GRAPH_SLOT = [None]
 
-def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out=None):
-    lib = load()
-    if lib.dl4j_segdesc_size() != _SEG_DTYPE.itemsize:
-        raise RuntimeError("SegDesc layout mismatch between python and HIP")
+
+def seg_table_bytes(plan, iteration, epoch):
     from ..nn.conf.updaters import kernel_params
     segs = plan.segments
     arr = np.zeros(len(segs), dtype=_SEG_DTYPE)
     for i, s in enumerate(segs):
         op, h0, h1, h2, h3 = kernel_params(s.updater, iteration, epoch)
         arr[i] = (s.p_off, s.n, s.st_off, s.in_block, s.block_n, op, 0, (h0, h1, h2, h3), s.l1, s.l2)
-    b = arr.tobytes()
+    return arr.tobytes()
+
+
+def _slot(cache, key, nbytes, device):
+    st = cache.slots.get(key)
+    if st is None or st.dev.numel() != nbytes or st.dev.device != device:
+        st = _Slot(nbytes, device)
+        cache.slots[key] = st
+    return st
+
+
+def _write_pinned(st, b):
+    if st.event is not None:
+        st.event.synchronize()          # the previous async copy out of this pinned buffer has finished
+    st.pinned.numpy()[:] = np.frombuffer(b, dtype=np.uint8)
+    st.bytes = b
+
+
+def prepare_graph_slots(plan, device, iteration, epoch, nslots=2):
+    """Allocate the pinned/device table slots BEFORE capture (pinned host allocation is not capturable)."""
     cache = plan.__dict__.setdefault("_native_cache", _SegTableCache())
-    if cache.dev is None or cache.dev.device != params.device or cache.host_bytes != b:
-        host = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        if cache.dev is None or cache.dev.numel() != len(b) or cache.dev.device != params.device:
-            cache.dev = torch.empty(len(b), dtype=torch.uint8, device=params.device)
-        cache.dev.copy_(host, non_blocking=False)
-        cache.host_bytes = b
-    if getattr(cache, "btab", None) is None or cache.btab.device != params.device:
+    b = seg_table_bytes(plan, iteration, epoch)
+    for k in range(nslots):
+        st = _slot(cache, ("graph", k), len(b), device)
+        _write_pinned(st, b)
+
+
+def refresh_graph_table(plan, slot, iteration, epoch):
+    """Before replaying graph ``slot``: put this iteration's hyperparameters into its pinned buffer."""
+    cache = plan.__dict__.get("_native_cache")
+    st = cache.slots[("graph", slot)]
+    b = seg_table_bytes(plan, iteration, epoch)
+    if b != st.bytes:
+        _write_pinned(st, b)
+
+
+def mark_graph_replayed(plan, slot):
+    cache = plan.__dict__.get("_native_cache")
+    st = cache.slots[("graph", slot)]
+    if st.event is None:
+        st.event = torch.cuda.Event()
+    st.event.record()
+
+
+def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out=None):
+    lib = load()
+    if lib.dl4j_segdesc_size() != _SEG_DTYPE.itemsize:
+        raise RuntimeError("SegDesc layout mismatch between python and HIP")
+    segs = plan.segments
+    b = seg_table_bytes(plan, iteration, epoch)
+    cache = plan.__dict__.setdefault("_native_cache", _SegTableCache())
+    gslot = GRAPH_SLOT[0]
+    if gslot is None:
+        st = _slot(cache, "eager", len(b), params.device)
+        if st.bytes != b:
+            _write_pinned(st, b)
+            st.dev.copy_(st.pinned, non_blocking=True)
+            if st.event is None:
+                st.event = torch.cuda.Event()
+            st.event.record()
+    else:                                  # capturing: the copy from this slot's pinned buffer is a graph node
+        st = cache.slots.get(("graph", gslot))
+        if st is None or st.dev.numel() != len(b):
+            raise RuntimeError("graph table slot not prepared before capture (prepare_graph_slots)")
+        if st.bytes != b:
+            st.pinned.numpy()[:] = np.frombuffer(b, dtype=np.uint8)
+            st.bytes = b
+        st.dev.copy_(st.pinned, non_blocking=True)
+    if cache.btab is None or cache.btab.device != params.device:
         chunk = lib.dl4j_update_chunk()
         rows = [(si, ci) for si, s in enumerate(segs) for ci in range((s.n + chunk - 1) // chunk)]
         cache.btab = torch.tensor(rows if rows else [(0, 0)], dtype=torch.int32).to(params.device)
@@ -143,7 +234,7 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
         if shadow.dtype != torch.bfloat16:
             return False
         sk = 1
-    rc = lib.dl4j_fused_update(_ptr(cache.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
+    rc = lib.dl4j_fused_update(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
                                _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
                                _stream())
     _check(rc, "fused_update")

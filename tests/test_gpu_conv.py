@@ -17,6 +17,8 @@ CASES = [
     (2, 8, 23, 23, 64, 7, 7, (2, 2), (3, 3, 3, 3)),
     (1, 256, 5, 5, 512, 3, 3, (1, 1), (1, 1, 1, 1)),
     (4, 512, 4, 4, 2048, 1, 1, (1, 1), (0, 0, 0, 0)),
+    (2, 48, 6, 6, 64, 3, 3, (1, 1), (1, 1, 1, 1)),
+    (3, 96, 9, 9, 64, 3, 3, (2, 2), (1, 1, 1, 1)),
 ]
 
 
@@ -65,3 +67,26 @@ def test_conv_layer_uses_native_kernels(cuda):
     assert ops.use_native(x, "conv")
     y = ops.conv2d_forward(x, w, None, (1, 1), (1, 1, 1, 1))
     assert y.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_kernel_variants_agree(cuda, case):
+    """LDS-DMA pipelined kernel (variant 1) == register-staged kernel (variant 0), bit for bit."""
+    N, C, H, W, K, R, S, stride, pad4 = case
+    if C % 8 != 0:
+        pytest.skip("native path needs C % 8 == 0")
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g).to(cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, S, generator=g) * 0.1).to(cuda).bfloat16()
+    outs = []
+    for v in (0, 1):
+        conv_native.set_kernel_variant(v)
+        conv_native.bump_version()
+        y = conv_native.conv2d_fwd(x, w, None, stride, pad4, (1, 1))
+        dy = torch.ones_like(y) * 0.01 + y * 0.1
+        dx, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False)
+        outs.append((y, dx))
+    conv_native.set_kernel_variant(1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])

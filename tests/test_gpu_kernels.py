@@ -196,3 +196,38 @@ def test_threshold_codec_gpu_matches_cpu(cuda, n):
     m3 = C.threshold_encode(r3, thr, capacity=17)       # capacity clamp keeps the rest in the residual
     assert int(m3[0]) == 17
     assert torch.allclose((C.decode(m3, torch.zeros(n, device=cuda)) + r3).cpu(), r, atol=1e-7)
+
+
+def test_hip_graph_training_matches_eager(cuda):
+    """Captured (HIP graph) training iterations == eager iterations, incl. Adam bias correction per step."""
+    from deeplearning4j_amd import (Activation, Adam, BatchNormalization, ConvolutionLayer, DataType, InputType,
+                                    LossFunction, MultiLayerNetwork, NeuralNetConfiguration, OutputLayer,
+                                    SubsamplingLayer)
+
+    def make():
+        conf = (NeuralNetConfiguration.Builder().seed(3).dataType(DataType.BFLOAT16).updater(Adam(1e-2)).l2(1e-4)
+                .list()
+                .layer(0, ConvolutionLayer.Builder([3, 3]).nOut(16).activation(Activation.IDENTITY).build())
+                .layer(1, BatchNormalization.Builder().build())
+                .layer(2, SubsamplingLayer.Builder([2, 2], [2, 2]).build())
+                .layer(3, OutputLayer.Builder(LossFunction.MCXENT).nOut(10).activation(Activation.SOFTMAX).build())
+                .setInputType(InputType.convolutional(12, 12, 8)).build())
+        n = MultiLayerNetwork(conf)
+        n.init(device=cuda)
+        return n
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.rand(16, 8, 12, 12, generator=g).to(cuda) for _ in range(6)]
+    ys = []
+    for _ in range(6):
+        y = torch.zeros(16, 10)
+        y[torch.arange(16), torch.randint(0, 10, (16,), generator=g)] = 1
+        ys.append(y.to(cuda))
+    eager, graphed = make(), make()
+    graphed.enableHipGraphs(True, warmup=1)
+    for x, y in zip(xs, ys):
+        eager.fit(x, y)
+        graphed.fit(x, y)
+    assert graphed._hipgraph is not None and graphed._hipgraph.k == 5
+    assert graphed.getIterationCount() == eager.getIterationCount() == 6
+    assert torch.allclose(graphed.params(), eager.params(), atol=2e-3, rtol=1e-2)
+    assert abs(graphed.score() - eager.score()) < 1e-2
