@@ -637,6 +637,144 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
 }
 
 // ------------------------------------------------------------------------------------------------------
+// WRW, LDS-DMA pipeline (v2): same math/output as igemm_wrw_kernel. Per stage: A = dY[32 m][128 k] and
+// B = im2col(X)[32 m][128 j], 256-byte rows, filled by global_load_lds (4 rows per wave-instruction, lane slot s
+// of row r holds 16-byte chunk s ^ 2(r&3): the 4 rows a transposed 16-lane read touches then cover 8 distinct
+// chunks = 32 distinct banks). Fragments are read with ds_read_b64_tr_b16 exactly as in the v1 kernel.
+// Every lane owns one fixed column chunk (fixed filter tap), so the per-step work is one multiply-high pixel
+// decode + bounds check per row.
+// ------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wrw_addr(int row, int col) {
+  return row * 256 + ((((col >> 3) ^ ((row & 3) << 1))) << 4) + (col & 7) * 2;
+}
+
+__global__ __launch_bounds__(NTHREADS) void igemm_wrw_glds(const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                            float* __restrict__ dW, float* __restrict__ db,
+                                                            ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH) {
+  __shared__ __attribute__((aligned(16))) char smem[G_STAGES * G_STAGE_BYTES];   // 4 x (8 KB + 8 KB)
+  const int M = g.N * g.OH * g.OW;
+  const int Kout = g.K;
+  const int RSC = g.R * g.S * g.C;
+  const int tiles_k = (Kout + TILE_N - 1) / TILE_N;
+  const int tk = blockIdx.x % tiles_k, tj = blockIdx.x / tiles_k;
+  const int k0 = tk * TILE_N, j0 = tj * TILE_M;
+  const int mbeg = blockIdx.y * m_per_split;
+  int mend = mbeg + m_per_split;
+  if (mend > M) mend = M;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid >> 1, wj = wid & 1;
+
+  int row[2], kcol[2], cc[2], rdh[2], sdw[2];
+  bool kok[2], jok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    row[i] = (i * 4 + wid) * 4 + (lane >> 4);
+    const int chunk = (lane & 15) ^ ((row[i] & 3) << 1);
+    kcol[i] = k0 + chunk * 8;
+    kok[i] = kcol[i] < Kout;
+    const int jcol = j0 + chunk * 8;
+    jok[i] = jcol < RSC;
+    const int jc = jok[i] ? jcol : 0;
+    cc[i] = jc % g.C;
+    const int rs = jc / g.C;
+    rdh[i] = (rs / g.S) * g.dh - g.ph;
+    sdw[i] = (rs % g.S) * g.dw - g.pw;
+  }
+  const int nsteps = (mend - mbeg + TILE_K - 1) / TILE_K;
+  const bool do_bias = (db != nullptr) && (tj == 0);
+  float bsum = 0.f;
+
+  auto issue = [&](int st, int buf) {
+    char* A = smem + buf * G_STAGE_BYTES;
+    char* B = A + TILE_K * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + st * TILE_K + row[i];
+      const bool mok = m < mend;
+      const void* sa = (mok && kok[i]) ? (const void*)(dY + (long long)m * Kout + kcol[i]) : (const void*)g_zero_page;
+      const unsigned mm = mok ? (unsigned)m : 0u;
+      const unsigned t = fdiv(mm, fOW);
+      const int ow = (int)(mm - t * fOW.d);
+      const unsigned pn = fdiv(t, fOH);
+      const int oh = (int)(t - pn * fOH.d);
+      const int ih = oh * g.sh + rdh[i], iw = ow * g.sw + sdw[i];
+      const bool bok = mok && jok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const void* sb = bok ? (const void*)(X + (((long long)pn * g.H + ih) * g.W + iw) * g.C + cc[i])
+                           : (const void*)g_zero_page;
+      glds16(sa, A + (i * 4 + wid) * 1024);
+      glds16(sb, B + (i * 4 + wid) * 1024);
+    }
+  };
+  const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  auto frag = [&](const char* T, int colbase, int ks) -> bf16x8_t {
+    const int col = colbase + (grp & 1) * 16 + 4 * p;
+    const int r0 = ks * 16 + (grp >> 1) * 8 + q;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + wrw_addr(r0, col)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + wrw_addr(r0 + 4, col)));
+    bf16x8_t f;
+    const __bf16* l4 = reinterpret_cast<const __bf16*>(&lo);
+    const __bf16* h4 = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[e] = l4[e]; f[e + 4] = h4[e]; }
+    return f;
+  };
+
+  f32x16_t acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+#pragma unroll
+  for (int st = 0; st < G_STAGES - 1; ++st)
+    if (st < nsteps) issue(st, st);
+
+  for (int st = 0; st < nsteps; ++st) {
+    const int ahead = min(G_STAGES - 2, nsteps - 1 - st);
+    wait_stage(ahead);
+    raw_barrier();
+    if (st + G_STAGES - 1 < nsteps) issue(st + G_STAGES - 1, (st + G_STAGES - 1) % G_STAGES);
+    const char* A = smem + (st % G_STAGES) * G_STAGE_BYTES;
+    const char* B = A + TILE_K * 256;
+    if (do_bias && tid < TILE_N) {                  // conv-bias gradient: column sums of the dY tile
+#pragma unroll 8
+      for (int r = 0; r < TILE_K; ++r) bsum += bf2f(*reinterpret_cast<const u16*>(A + wrw_addr(r, tid)));
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = frag(A, wk * 64 + a * 32, ks);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = frag(B, wj * 64 + b * 32, ks);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int j = j0 + wj * 64 + b * 32 + (lane & 31);
+    if (j >= RSC) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int k = k0 + wk * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (k < Kout) atomicAdd(dW + (long long)k * RSC + j, acc[a][b][e]);
+      }
+    }
+  }
+  if (do_bias && tid < TILE_N && k0 + tid < Kout) atomicAdd(db + k0 + tid, bsum);
+}
+
+static int g_wrw_variant = 0;   // v1 register-staged measured faster here (occupancy); v2 kept for A/B
+DL4J_API void dl4j_conv_set_wrw_variant(int v) { g_wrw_variant = v; }
+
+// ------------------------------------------------------------------------------------------------------
 // Weight relayout (bf16): W[K][C][R][S] -> Wkrsc[K][R][S][C]  and  Wflip[C][R][S][K] = W[k][c][R-1-r][S-1-s]
 // ------------------------------------------------------------------------------------------------------
 __global__ void conv_w_relayout(const bf16* __restrict__ W, bf16* __restrict__ krsc, bf16* __restrict__ flip, int K,
@@ -748,8 +886,9 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
   const int RSC = R * S * C;
   const int tiles = ((K + TILE_N - 1) / TILE_N) * ((RSC + TILE_M - 1) / TILE_M);
   if (splits <= 0) {
-    // ~2 workgroups per CU in total; every split keeps >= 8 k-steps so the atomic epilogue stays amortised
-    splits = (512 + tiles - 1) / tiles;
+    // ~1.5 workgroups per CU in total (measured sweet spot between fill and atomic traffic, tools/conv_bench.py
+    // --sweep-wrw); every split keeps >= 8 k-steps so the atomic epilogue stays amortised
+    splits = (384 + tiles - 1) / tiles;
     const int maxs = (M + 8 * TILE_K - 1) / (8 * TILE_K);
     if (splits > maxs) splits = maxs;
     if (splits < 1) splits = 1;
@@ -757,7 +896,11 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
   int mps = (M + splits - 1) / splits;
   mps = (mps + TILE_K - 1) / TILE_K * TILE_K;
   splits = (M + mps - 1) / mps;
-  hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
-                     db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
+  if (g_wrw_variant == 1)
+    hipLaunchKernelGGL(igemm_wrw_glds, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
+                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
+  else
+    hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
+                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
   return (int)hipGetLastError();
 }

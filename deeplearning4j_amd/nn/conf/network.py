@@ -291,6 +291,11 @@ class MultiLayerConfiguration(Config):
     def getConf(self, i):
         return self.confs[i]
 
+    def getMemoryReport(self, inputType=None):
+        """Per-layer memory estimates (reference MultiLayerConfiguration.getMemoryReport)."""
+        from .memory import mln_memory_report
+        return mln_memory_report(self, inputType)
+
     def getInputPreProcess(self, i):
         return self.inputPreProcessors.get(i)
 
@@ -455,6 +460,10 @@ class ComputationGraphConfiguration(Config):
 
     def setDataType(self, d):
         self.globalConf["dataType"] = DataType.of(d)
+
+    def getMemoryReport(self, *inputTypes):
+        from .memory import cg_memory_report
+        return cg_memory_report(self, list(inputTypes) or None)
 
     def topologicalOrder(self):
         """Kahn's algorithm, ties broken by insertion order (reference ComputationGraph.java:1216-1318)."""

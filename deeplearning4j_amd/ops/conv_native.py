@@ -21,7 +21,11 @@ native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
 native.register_sig("dl4j_conv_set_variant", [c_int])
+native.register_sig("dl4j_conv_set_wrw_variant", [c_int])
 native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p])
+
+# Optional per-shape override of the weight-gradient split count (tuning): {(N,H,W,C,K,R,S,stride): splits}
+WRW_SPLITS = {}
 
 # Bumped by every parameter update (BaseNetwork._apply_update / setParams): invalidates relayout caches.
 WEIGHT_VERSION = [0]
@@ -41,6 +45,11 @@ def _zeroed_wrw_ws(K, R, S, C, device):
 def set_kernel_variant(v):
     """1 = LDS-DMA pipelined forward/backward-data kernel (default), 0 = register-staged kernel (A/B testing)."""
     native.load().dl4j_conv_set_variant(int(v))
+
+
+def set_wrw_variant(v):
+    """0 = register-staged weight-gradient kernel (default), 1 = LDS-DMA pipelined variant."""
+    native.load().dl4j_conv_set_wrw_variant(int(v))
 
 
 def bump_version():
@@ -161,8 +170,9 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
             if not (directb and grads_zeroed):
                 dbt.zero_()
+        splits = WRW_SPLITS.get((N, H, W, C, K, R, S, tuple(stride)), 0)
         rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
-                               pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, 0, _stream())
+                               pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits, _stream())
         native._check(rc, "conv_wrw")
         if ws is not dWt:
             rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, 1, _stream())

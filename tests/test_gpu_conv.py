@@ -81,12 +81,20 @@ def test_conv_kernel_variants_agree(cuda, case):
     outs = []
     for v in (0, 1):
         conv_native.set_kernel_variant(v)
+        conv_native.set_wrw_variant(v)
         conv_native.bump_version()
         y = conv_native.conv2d_fwd(x, w, None, stride, pad4, (1, 1))
         dy = torch.ones_like(y) * 0.01 + y * 0.1
         dx, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False)
-        outs.append((y, dx))
+        gW = torch.zeros(K, C, R, S, device=cuda)
+        gb = torch.zeros(K, device=cuda)
+        conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), False, True, True, gW, gb)
+        outs.append((y, dx, gW, gb))
     conv_native.set_kernel_variant(1)
+    conv_native.set_wrw_variant(0)
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1], outs[1][1])
+    # weight/bias gradients accumulate with atomics in a different order: equal up to fp32 rounding
+    _close(outs[1][2], outs[0][2], 1e-5)
+    _close(outs[1][3], outs[0][3], 1e-5)

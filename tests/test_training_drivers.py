@@ -207,3 +207,24 @@ def test_normalizers():
     ts = torch.randn(4, 3, 7, generator=g) * 3 + 1
     nt = NormalizerStandardize().fit(DataSet(ts, torch.zeros(4, 2, 7)))
     assert torch.allclose(nt.getMean().float(), ts.permute(0, 2, 1).reshape(-1, 3).mean(0), atol=1e-5)
+
+
+def test_memory_report():
+    """NetworkMemoryReport semantics (reference CORET: nn/conf/memory/MemoryReportTest.java)."""
+    from deeplearning4j_amd.nn.conf.memory import MemoryType, MemoryUseMode
+    conf = (NeuralNetConfiguration.Builder().updater(Adam(1e-3)).list()
+            .layer(0, DenseLayer.Builder().nIn(10).nOut(20).build())
+            .layer(1, OutputLayer.Builder(LossFunction.MCXENT).nIn(20).nOut(5).activation(Activation.SOFTMAX).build())
+            .setInputType(InputType.feedForward(10)).build())
+    r = conf.getMemoryReport()
+    P = 10 * 20 + 20 + 20 * 5 + 5
+    assert r.getMemoryBytes(MemoryType.PARAMETERS, 1, MemoryUseMode.INFERENCE) == 4 * P
+    assert r.getMemoryBytes(MemoryType.UPDATER_STATE, 1, MemoryUseMode.TRAINING) == 4 * 2 * P   # Adam m+v
+    assert r.getMemoryBytes(MemoryType.UPDATER_STATE, 1, MemoryUseMode.INFERENCE) == 0
+    assert r.getMemoryBytes(MemoryType.ACTIVATIONS, 7, MemoryUseMode.INFERENCE) == 4 * 7 * (20 + 5)
+    tr = r.getTotalMemoryBytes(8, MemoryUseMode.TRAINING)
+    inf = r.getTotalMemoryBytes(8, MemoryUseMode.INFERENCE)
+    assert tr > inf > 0
+    assert r.getMemoryBytes(MemoryType.PARAMETERS, 1, MemoryUseMode.INFERENCE, None, "DOUBLE") == 8 * P
+    assert "Network Memory Report" in r.toString()
+    assert r.maxMinibatchFor(1 << 20) > 0

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--kernel-variant", type=int, default=1)
+    ap.add_argument("--sweep-wrw", action="store_true", help="time the weight-gradient kernel for several splits")
     a = ap.parse_args()
     from deeplearning4j_amd.ops import conv_native as CN
     dev = torch.device("cuda")
@@ -83,6 +84,16 @@ def main():
         f_ms = timeit(lambda: CN.conv2d_fwd(x, w, None, st, pad, dil), a.reps)
         d_ms = timeit(lambda: CN.conv2d_bwd(x, w, dy, st, pad, dil, True, False, False), a.reps)
         w_ms = timeit(lambda: CN.conv2d_bwd(x, w, dy, st, pad, dil, False, True, False, gW), a.reps)
+        if a.sweep_wrw:
+            key = (N, H, W, C, K, R, S, tuple(st))
+            res = []
+            for sp in (1, 2, 4, 8, 16, 32, 64, 128):
+                CN.WRW_SPLITS[key] = sp
+                res.append((timeit(lambda: CN.conv2d_bwd(x, w, dy, st, pad, dil, False, True, False, gW), a.reps), sp))
+            CN.WRW_SPLITS.pop(key)
+            M = N * OH * OW
+            tiles = ((K + 127) // 128) * ((R * S * C + 127) // 128)
+            print(f"   wrw sweep M={M} tiles={tiles}: " + " ".join(f"{sp}:{t*1e3:.0f}us" for t, sp in res))
         sym = pad[0] == pad[1] and pad[2] == pad[3]
         if sym:
             xm = x
