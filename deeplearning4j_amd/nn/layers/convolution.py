@@ -298,11 +298,21 @@ class Upsampling1DImpl(LayerImpl):
 
 
 class SpaceToDepthImpl(LayerImpl):
+    """TensorFlow depth ordering: output channel = (dy * b + dx) * C + c (block offset major), the layout the
+    reference's space_to_depth op and Keras-imported models use."""
+
     def activate(self, x, training=False, mask=None):
-        return F.pixel_unshuffle(x, self.conf.blockSize)
+        b = self.conf.blockSize
+        n, c, H, W = x.shape
+        y = x.reshape(n, c, H // b, b, W // b, b).permute(0, 3, 5, 1, 2, 4)
+        return y.reshape(n, b * b * c, H // b, W // b)
 
     def backpropGradient(self, eps):
-        return self.make_gradient(), F.pixel_shuffle(eps, self.conf.blockSize)
+        b = self.conf.blockSize
+        n, cc, h, w = eps.shape
+        c = cc // (b * b)
+        g = eps.reshape(n, b, b, c, h, w).permute(0, 3, 4, 1, 5, 2)
+        return self.make_gradient(), g.reshape(n, c, h * b, w * b)
 
 
 class SpaceToBatchImpl(LayerImpl):
