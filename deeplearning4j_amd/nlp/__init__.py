@@ -1,0 +1,7 @@
+"""NLP: tokenization, vocabularies and embedding learners (Word2Vec, ParagraphVectors, GloVe) on the native
+batcher + gfx950 embedding kernels; WordVectorSerializer formats."""
+from .text import *  # noqa: F401,F403
+from .vocab import AbstractCache, Huffman, InMemoryLookupCache, SequenceElement, VocabConstructor, VocabWord  # noqa
+from .embeddings import EmbeddingEngine, InMemoryLookupTable, WordVectorsImpl  # noqa: F401
+from .word2vec import (CBOW, DBOW, DM, ParagraphVectors, ScoreListener, SequenceVectors, SerializingListener,  # noqa
+                       SkipGram, VectorsConfiguration, VectorsListener, Word2Vec)
