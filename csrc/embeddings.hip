@@ -5,7 +5,9 @@
 // MI355X mapping: one 64-lane wavefront per work item; a D-dimensional row lives in registers as VPL values per
 // lane (D <= 64*VPL), dot products are wave reductions (xor shuffles within the wave), and every row update is a
 // coalesced 64-lane read-modify-write. Updates are Hogwild (no atomics between items) exactly like the reference's
-// concurrent worker threads; within an item the wave is the only writer. Work items come from the host batcher
+// concurrent worker threads; within an item the wave is the only writer. The caller caps the number of resident
+// waves relative to the vocabulary size (max_blocks) so that small vocabularies do not turn Hogwild into a storm of
+// lost updates on the same few rows. Work items come from the host batcher
 // (csrc/runtime/embeddings.cpp) and use the same per-item LCG seeds as the CPU applier there.
 #include "common.h"
 
@@ -261,11 +263,12 @@ inline int grid_for(long long n) {
 DL4J_API int dl4j_w2v_sg(const int32_t* item_in, const int32_t* item_tgt, const float* alpha, long long n,
                          float* syn0, float* syn1, float* syn1neg, int D, const uint8_t* codes, const int32_t* points,
                          const int32_t* codelen, int maxc, const int32_t* table, long long tsize, int negative,
-                         int flags, unsigned long long seed, long long item_base, float* loss_out,
+                         int flags, unsigned long long seed, long long item_base, float* loss_out, int max_blocks,
                          hipStream_t stream) {
   if (n <= 0) return 0;
   Out O{syn1, syn1neg, D, codes, points, codelen, maxc, table, tsize, negative, flags};
-  VPL_DISPATCH(D, hipLaunchKernelGGL(w2v_sg_kernel<V>, dim3(grid_for(n)), dim3(256), 0, stream, item_in, item_tgt,
+  const int grid = max_blocks > 0 && grid_for(n) > max_blocks ? max_blocks : grid_for(n);
+  VPL_DISPATCH(D, hipLaunchKernelGGL(w2v_sg_kernel<V>, dim3(grid), dim3(256), 0, stream, item_in, item_tgt,
                                      alpha, n, syn0, O, (uint64_t)seed, item_base, loss_out));
   return (int)hipGetLastError();
 }
@@ -274,11 +277,12 @@ DL4J_API int dl4j_w2v_cbow(const int32_t* item_tgt, const float* alpha, const in
                            long long n, float* syn0, float* syn1, float* syn1neg, int D, const uint8_t* codes,
                            const int32_t* points, const int32_t* codelen, int maxc, const int32_t* table,
                            long long tsize, int negative, int flags, unsigned long long seed, long long item_base,
-                           const float* extra_in, int n_extra, float* extra_grad, float* loss_out,
+                           const float* extra_in, int n_extra, float* extra_grad, float* loss_out, int max_blocks,
                            hipStream_t stream) {
   if (n <= 0) return 0;
   Out O{syn1, syn1neg, D, codes, points, codelen, maxc, table, tsize, negative, flags};
-  VPL_DISPATCH(D, hipLaunchKernelGGL(w2v_cbow_kernel<V>, dim3(grid_for(n)), dim3(256), 0, stream, item_tgt, alpha,
+  const int grid = max_blocks > 0 && grid_for(n) > max_blocks ? max_blocks : grid_for(n);
+  VPL_DISPATCH(D, hipLaunchKernelGGL(w2v_cbow_kernel<V>, dim3(grid), dim3(256), 0, stream, item_tgt, alpha,
                                      ctx_off, ctx, n, syn0, O, (uint64_t)seed, item_base, extra_in, n_extra,
                                      extra_grad, loss_out));
   return (int)hipGetLastError();
@@ -286,9 +290,10 @@ DL4J_API int dl4j_w2v_cbow(const int32_t* item_tgt, const float* alpha, const in
 
 DL4J_API int dl4j_glove(const int32_t* ei, const int32_t* ej, const float* ex, long long n, float* W, float* b,
                         float* hW, float* hb, int D, float lr, float xmax, float alpha, float* cost_out,
-                        hipStream_t stream) {
+                        int max_blocks, hipStream_t stream) {
   if (n <= 0) return 0;
-  VPL_DISPATCH(D, hipLaunchKernelGGL(glove_kernel<V>, dim3(grid_for(n)), dim3(256), 0, stream, ei, ej, ex, n, W, b,
+  const int grid = max_blocks > 0 && grid_for(n) > max_blocks ? max_blocks : grid_for(n);
+  VPL_DISPATCH(D, hipLaunchKernelGGL(glove_kernel<V>, dim3(grid), dim3(256), 0, stream, ei, ej, ex, n, W, b,
                                      hW, hb, D, lr, xmax, alpha, cost_out));
   return (int)hipGetLastError();
 }

@@ -47,10 +47,11 @@ def _native_kernels():
     lib = native.load()
     native.register_sig("dl4j_w2v_sg", [c_void_p, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_int, c_int, c_ull,
-                                        c_ll, c_void_p, c_void_p])
+                                        c_ll, c_void_p, c_int, c_void_p])
     native.register_sig("dl4j_w2v_cbow", [c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_void_p, c_void_p,
                                           c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll,
-                                          c_int, c_int, c_ull, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p])
+                                          c_int, c_int, c_ull, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                          c_void_p])
     return lib
 
 
@@ -187,6 +188,12 @@ class EmbeddingEngine:
         self.item_base = 0
         self.loss = 0.0
 
+    @staticmethod
+    def _max_blocks(rows):
+        # ~1 resident wave per 8 table rows (4 waves per block): keeps the Hogwild collision rate low for small
+        # vocabularies while large ones still fill all 256 CUs
+        return max(1, min(8192, rows // 32))
+
     def flags(self, update_out=True, update_in=True):
         t = self.t
         f = 0
@@ -238,25 +245,46 @@ class EmbeddingEngine:
         seed = int(t.seed) & 0xFFFFFFFFFFFFFFFF
         if self.gpu:
             dev = t.device
+            # host-side bounds check before a hand-written kernel dereferences these indices
+            rows, V = syn0.shape[0], int(t.codelen.numel())
+            if item_tgt.min() < 0 or item_tgt.max() >= V:
+                raise IndexError("embedding target index out of range")
+            if not cbow and (item_in.min() < 0 or item_in.max() >= rows):
+                raise IndexError("embedding input row out of range")
+            if cbow and (len(ctx) and (ctx.min() < 0 or ctx.max() >= rows) or ctx_off[0] != 0 or
+                         ctx_off[-1] != len(ctx) or np.any(np.diff(ctx_off) < 0)):
+                raise IndexError("CBOW context arrays inconsistent")
+            if (t.syn1 is None and flags & F_HS) or (t.syn1Neg is None and flags & F_NS):
+                raise ValueError("output table missing for the requested objective")
+            if extra is not None and extra.shape[1] != D:
+                raise ValueError("extra input width mismatch")
 
+            # device copies are held in locals until after the launch: a temporary's block would go back to the
+            # caching allocator and be reused by the next copy before the kernel reads it
             def up(a):
-                return torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
+                return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)
             s = torch.cuda.current_stream(dev).cuda_stream
+            d_tgt, d_alpha = up(item_tgt), up(item_alpha)
             if cbow:
-                rc = self.lib.dl4j_w2v_cbow(_t_ptr(up(item_tgt)), _t_ptr(up(item_alpha)), _t_ptr(up(ctx_off)),
-                                            _t_ptr(up(ctx) if len(ctx) else torch.zeros(1, dtype=torch.int32,
-                                                                                         device=dev)),
+                d_off = up(ctx_off)
+                d_ctx = up(ctx) if len(ctx) else torch.zeros(1, dtype=torch.int32, device=dev)
+                rc = self.lib.dl4j_w2v_cbow(_t_ptr(d_tgt), _t_ptr(d_alpha), _t_ptr(d_off), _t_ptr(d_ctx),
                                             n, _t_ptr(syn0), _t_ptr(t.syn1), _t_ptr(t.syn1Neg), D, _t_ptr(t.codes),
                                             _t_ptr(t.points), _t_ptr(t.codelen), t.maxc, _t_ptr(t.table),
                                             t.table.numel(), int(t.negative), flags, seed, self.item_base,
                                             _t_ptr(extra), 0 if extra is None else extra.shape[0],
-                                            _t_ptr(extra_grad), _t_ptr(self.loss_dev), c_void_p(s))
+                                            _t_ptr(extra_grad), _t_ptr(self.loss_dev), self._max_blocks(rows), c_void_p(s))
+                keep = (d_off, d_ctx)
             else:
-                rc = self.lib.dl4j_w2v_sg(_t_ptr(up(item_in)), _t_ptr(up(item_tgt)), _t_ptr(up(item_alpha)), n,
+                d_in = up(item_in)
+                rc = self.lib.dl4j_w2v_sg(_t_ptr(d_in), _t_ptr(d_tgt), _t_ptr(d_alpha), n,
                                           _t_ptr(syn0), _t_ptr(t.syn1), _t_ptr(t.syn1Neg), D, _t_ptr(t.codes),
                                           _t_ptr(t.points), _t_ptr(t.codelen), t.maxc, _t_ptr(t.table),
                                           t.table.numel(), int(t.negative), flags, seed, self.item_base,
-                                          _t_ptr(self.loss_dev), c_void_p(s))
+                                          _t_ptr(self.loss_dev), self._max_blocks(rows), c_void_p(s))
+                keep = (d_in,)
+            # the kernel is stream-ordered after these blocks; release them only once it has been enqueued
+            del keep, d_tgt, d_alpha
             if rc != 0:
                 raise RuntimeError(f"embedding kernel failed ({rc})")
         else:

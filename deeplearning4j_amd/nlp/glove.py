@@ -96,7 +96,7 @@ class Glove(Word2Vec):
             from ..ops import native
             lib = native.load()
             native.register_sig("dl4j_glove", [c_void_p, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_void_p,
-                                               c_void_p, c_int, c_float, c_float, c_float, c_void_p, c_void_p])
+                                               c_void_p, c_int, c_float, c_float, c_float, c_void_p, c_int, c_void_p])
             cost = torch.zeros(1, device=dev)
             di, dj, dx = (torch.from_numpy(a).to(dev) for a in (ei, ej, ex))
         rt = RT.load()
@@ -110,7 +110,7 @@ class Glove(Word2Vec):
                 cost.zero_()
                 rc = lib.dl4j_glove(_t_ptr(a), _t_ptr(bb), _t_ptr(x), len(ei), _t_ptr(W), _t_ptr(b), _t_ptr(hW),
                                     _t_ptr(hb), D, c.learningRate, self.xMax, self.alpha, _t_ptr(cost),
-                                    ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                                    max(1, min(8192, V // 32)), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
                 if rc != 0:
                     raise RuntimeError(f"dl4j_glove failed ({rc})")
                 self.lossHistory.append(float(cost.item()))

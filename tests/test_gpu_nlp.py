@@ -91,7 +91,7 @@ def test_glove_kernel_matches_cpu(cuda):
     lib = native.load()
     native.register_sig("dl4j_glove", [ctypes.c_void_p] * 3 + [ctypes.c_longlong] + [ctypes.c_void_p] * 4 +
                         [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
-                         ctypes.c_void_p])
+                         ctypes.c_int, ctypes.c_void_p])
     rt = RT.load()
     dev_e = [torch.from_numpy(a).to(cuda) for a in (ei, ej, ex)]
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -99,7 +99,7 @@ def test_glove_kernel_matches_cpu(cuda):
         rt.rt_glove_apply(_np_ptr(ei[k:k + 1]), _np_ptr(ej[k:k + 1]), _np_ptr(ex[k:k + 1]), 1, _t_ptr(W), _t_ptr(b),
                           _t_ptr(hW), _t_ptr(hb), D, 0.05, 100.0, 0.75, 1)
         assert lib.dl4j_glove(_t_ptr(dev_e[0][k:]), _t_ptr(dev_e[1][k:]), _t_ptr(dev_e[2][k:]), 1, _t_ptr(Wg),
-                              _t_ptr(bg), _t_ptr(hWg), _t_ptr(hbg), D, 0.05, 100.0, 0.75, None, s) == 0
+                              _t_ptr(bg), _t_ptr(hWg), _t_ptr(hbg), D, 0.05, 100.0, 0.75, None, 0, s) == 0
     torch.cuda.synchronize()
     torch.testing.assert_close(Wg.cpu(), W, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bg.cpu(), b, rtol=1e-4, atol=1e-5)
@@ -115,6 +115,17 @@ def test_word2vec_on_gpu(cuda, algo):
     s_out = np.mean([w2v.similarity("alpha0", w) for w in B])
     assert s_in > s_out + 0.3
     assert all(w.startswith("alpha") for w in w2v.wordsNearest("alpha0", 5))
+
+
+def test_glove_on_gpu(cuda):
+    from deeplearning4j_amd.nlp.glove import Glove
+    g = Glove.Builder().iterate(CollectionSentenceIterator(_corpus())).minWordFrequency(1).layerSize(24) \
+        .epochs(15).windowSize(4).seed(1).device(cuda).build()
+    g.fit()
+    assert g.lossHistory[-1] < g.lossHistory[0] * 0.1
+    s_in = np.mean([g.similarity("alpha0", w) for w in A[1:]])
+    s_out = np.mean([g.similarity("alpha0", w) for w in B])
+    assert s_in > s_out + 0.3
 
 
 def test_paragraph_vectors_and_deepwalk_on_gpu(cuda):
