@@ -1,0 +1,142 @@
+// Per-segment summary statistics and histograms of a flat parameter / gradient / update / activation array,
+// for the stats listener (reference: UIM:stats/BaseStatsListener.java:774 — Histogram op per parameter plus
+// mean / stdev / mean-magnitude reductions over every (layer, param) view of the flat arrays).
+//
+// One launch covers every segment: grid.y = segment, grid.x = chunks of a segment. Each 256-thread block reduces
+// its chunk with wave reductions (64 lanes, xor shuffles) and one LDS exchange, then merges into the segment's
+// accumulator with atomics (float add; order-preserving int atomics for min/max). Histograms bin into an LDS
+// histogram per block, flushed with one atomic per bin. Listener-only (runs every N iterations), so loads are
+// plain coalesced scalar reads of fp32 or bf16.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wmin(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// order-preserving float <-> int mapping for atomicMin/atomicMax on floats
+__device__ __forceinline__ int f2o(float f) {
+  int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void seg_stats_kernel(const T* __restrict__ x, const long long* __restrict__ off,
+                                                        float* __restrict__ acc, int* __restrict__ mm) {
+  const int s = blockIdx.y;
+  const long long a = off[s], b = off[s + 1];
+  float sum = 0.f, sq = 0.f, ab = 0.f, mn = INFINITY, mx = -INFINITY;
+  for (long long i = a + (long long)blockIdx.x * 256 + threadIdx.x; i < b; i += (long long)gridDim.x * 256) {
+    const float v = ld1<T>(x + i);
+    sum += v; sq += v * v; ab += fabsf(v);
+    mn = fminf(mn, v); mx = fmaxf(mx, v);
+  }
+  sum = wsum(sum); sq = wsum(sq); ab = wsum(ab); mn = wmin(mn); mx = wmax(mx);
+  __shared__ float red[4][5];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[w][0] = sum; red[w][1] = sq; red[w][2] = ab; red[w][3] = mn; red[w][4] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k) {
+      red[0][0] += red[k][0]; red[0][1] += red[k][1]; red[0][2] += red[k][2];
+      red[0][3] = fminf(red[0][3], red[k][3]); red[0][4] = fmaxf(red[0][4], red[k][4]);
+    }
+    atomicAdd(acc + 3 * s + 0, red[0][0]);
+    atomicAdd(acc + 3 * s + 1, red[0][1]);
+    atomicAdd(acc + 3 * s + 2, red[0][2]);
+    atomicMin(mm + 2 * s + 0, f2o(red[0][3]));
+    atomicMax(mm + 2 * s + 1, f2o(red[0][4]));
+  }
+}
+
+__global__ void seg_init_kernel(float* acc, int* mm, int nseg) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < nseg) {
+    acc[3 * s] = 0.f; acc[3 * s + 1] = 0.f; acc[3 * s + 2] = 0.f;
+    mm[2 * s] = f2o(INFINITY); mm[2 * s + 1] = f2o(-INFINITY);
+  }
+}
+
+// out[s] = {mean, stdev (population), mean |x|, min, max}
+__global__ void seg_final_kernel(const float* acc, const int* mm, const long long* off, int nseg, float* out) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  const float n = float(off[s + 1] - off[s]);
+  const float mean = n > 0 ? acc[3 * s] / n : 0.f;
+  const float var = n > 0 ? fmaxf(acc[3 * s + 1] / n - mean * mean, 0.f) : 0.f;
+  out[5 * s + 0] = mean;
+  out[5 * s + 1] = sqrtf(var);
+  out[5 * s + 2] = n > 0 ? acc[3 * s + 2] / n : 0.f;
+  out[5 * s + 3] = o2f(mm[2 * s]);
+  out[5 * s + 4] = o2f(mm[2 * s + 1]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void seg_hist_kernel(const T* __restrict__ x, const long long* __restrict__ off,
+                                                       const float* __restrict__ stats, int bins,
+                                                       unsigned* __restrict__ hist) {
+  extern __shared__ unsigned lh[];
+  const int s = blockIdx.y;
+  for (int k = threadIdx.x; k < bins; k += 256) lh[k] = 0;
+  __syncthreads();
+  const float lo = stats[5 * s + 3], hi = stats[5 * s + 4];
+  const float scale = hi > lo ? float(bins) / (hi - lo) : 0.f;
+  const long long a = off[s], b = off[s + 1];
+  for (long long i = a + (long long)blockIdx.x * 256 + threadIdx.x; i < b; i += (long long)gridDim.x * 256) {
+    const float v = ld1<T>(x + i);
+    int bin = int((v - lo) * scale);
+    bin = bin < 0 ? 0 : (bin >= bins ? bins - 1 : bin);
+    atomicAdd(&lh[bin], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < bins; k += 256)
+    if (lh[k]) atomicAdd(hist + (long long)s * bins + k, lh[k]);
+}
+
+int chunks_for(long long maxlen) {
+  long long c = (maxlen + 256 * 16 - 1) / (256 * 16);   // ~16 elements per thread
+  return int(c < 1 ? 1 : (c > 1024 ? 1024 : c));
+}
+
+}  // namespace
+
+// x: flat array (dtype 0 fp32, 1 bf16); off: [nseg+1] int64 element offsets (device); ws: 5*nseg floats (device)
+// out: [nseg, 5] {mean, std, meanAbs, min, max}; hist (optional): [nseg, bins] uint32.
+DL4J_API int dl4j_segment_stats(int dtype, const void* x, const long long* off, int nseg, long long maxlen,
+                                float* ws, float* out, int bins, unsigned* hist, hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  float* acc = ws;
+  int* mm = reinterpret_cast<int*>(ws + 3 * nseg);
+  hipLaunchKernelGGL(seg_init_kernel, dim3((nseg + 255) / 256), dim3(256), 0, stream, acc, mm, nseg);
+  dim3 grid(chunks_for(maxlen), nseg);
+  if (dtype == 1)
+    hipLaunchKernelGGL(seg_stats_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)x, off, acc, mm);
+  else
+    hipLaunchKernelGGL(seg_stats_kernel<float>, grid, dim3(256), 0, stream, (const float*)x, off, acc, mm);
+  hipLaunchKernelGGL(seg_final_kernel, dim3((nseg + 255) / 256), dim3(256), 0, stream, acc, mm, off, nseg, out);
+  if (hist && bins > 0) {
+    if (bins > 4096) return -2;
+    if (hipMemsetAsync(hist, 0, sizeof(unsigned) * size_t(nseg) * bins, stream) != hipSuccess) return -3;
+    const size_t lds = sizeof(unsigned) * bins;
+    if (dtype == 1)
+      hipLaunchKernelGGL(seg_hist_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, off, out, bins, hist);
+    else
+      hipLaunchKernelGGL(seg_hist_kernel<float>, grid, dim3(256), lds, stream, (const float*)x, off, out, bins,
+                         hist);
+  }
+  return (int)hipGetLastError();
+}

@@ -353,3 +353,28 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
 def lstm_cell_fwd(z, c):
     from . import rnn_native
     return rnn_native.lstm_cell_fwd(z, c)
+
+
+def segment_stats(flat, offsets, bins=0):
+    """Per-segment {mean, std, meanAbs, min, max} (+ optional ``bins``-bin histograms over [min, max]) of a flat
+    fp32/bf16 CUDA tensor, one fused HIP launch for all segments (csrc/stats.hip). ``offsets``: list of nseg+1
+    element offsets. Returns (stats [nseg, 5] float32, hist [nseg, bins] int64 or None) on the device."""
+    lib = load()
+    register_sig("dl4j_segment_stats", [c_int, c_void_p, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_int,
+                                        c_void_p, c_void_p])
+    dt = _dt(flat)
+    if dt is None or not flat.is_contiguous():
+        raise ValueError("segment_stats needs a contiguous fp32/bf16 tensor")
+    nseg = len(offsets) - 1
+    if offsets[0] < 0 or offsets[-1] > flat.numel() or any(b < a for a, b in zip(offsets[:-1], offsets[1:])):
+        raise IndexError("segment offsets outside the flat array")
+    dev = flat.device
+    off = torch.tensor(offsets, dtype=torch.int64, device=dev)
+    ws = torch.empty(5 * nseg, dtype=torch.float32, device=dev)
+    out = torch.empty(nseg, 5, dtype=torch.float32, device=dev)
+    hist = torch.empty(nseg, bins, dtype=torch.int32, device=dev) if bins > 0 else None
+    maxlen = max(b - a for a, b in zip(offsets[:-1], offsets[1:])) if nseg else 0
+    rc = lib.dl4j_segment_stats(dt, _ptr(flat), _ptr(off), nseg, maxlen, _ptr(ws), _ptr(out), bins, _ptr(hist),
+                                c_void_p(_stream()))
+    _check(rc, "segment_stats")
+    return out, (hist.to(torch.int64) if hist is not None else None)

@@ -1,0 +1,126 @@
+"""Stats listener + storage + UI server (reference: deeplearning4j-ui tests TestStatsListener / TestStatsStorage /
+TestRemoteReceiver): records flow from a training run into in-memory / SQLite storage, the UI API serves them, and
+the remote router posts them to a UI with the remote listener enabled."""
+import json
+import urllib.request
+
+import numpy as np
+import pytest
+import torch
+
+from deeplearning4j_amd.nn.conf import layers as L
+from deeplearning4j_amd.nn.conf.network import NeuralNetConfiguration
+from deeplearning4j_amd.nn.multilayer import MultiLayerNetwork
+from deeplearning4j_amd.nn.conf.updaters import Adam
+from deeplearning4j_amd.ui import (FileStatsStorage, InMemoryStatsStorage, RemoteUIStatsStorageRouter,
+                                   StatsListener, StatsStorageListener, UIServer, summarize)
+
+CPU = torch.device("cpu")
+
+
+def _net():
+    conf = NeuralNetConfiguration.Builder().seed(1).updater(Adam(1e-2)).list() \
+        .layer(0, L.DenseLayer(nIn=4, nOut=8, activation="tanh")) \
+        .layer(1, L.OutputLayer(nIn=8, nOut=3, activation="softmax", lossFn="MCXENT")).build()
+    n = MultiLayerNetwork(conf)
+    n.init(device=CPU)
+    return n
+
+
+def _fit(net, iters=6):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(16, 4, generator=g)
+    y = torch.eye(3)[torch.randint(0, 3, (16,), generator=g)]
+    for _ in range(iters):
+        net.fit(x, y)
+
+
+def test_summarize_cpu():
+    flat = torch.arange(10, dtype=torch.float32)
+    s = summarize(flat, ["a", "b"], [0, 4, 10], 3)
+    assert s["a"]["mean"] == 1.5 and s["b"]["min"] == 4 and s["b"]["max"] == 9
+    assert sum(s["b"]["histogram"]["counts"]) == 6
+    assert abs(s["a"]["stdev"] - float(torch.tensor([0., 1, 2, 3]).std(unbiased=False))) < 1e-6
+
+
+def test_stats_listener_in_memory():
+    st = InMemoryStatsStorage()
+    events = []
+
+    class L_(StatsStorageListener):
+        def notify(self, e):
+            events.append(e.eventType)
+    st.registerStatsStorageListener(L_())
+    net = _net()
+    net.setListeners(StatsListener(st, 2))
+    _fit(net, 6)
+    sid = st.listSessionIDs()[0]
+    w = st.listWorkerIDsForSession(sid)[0]
+    assert st.getNumUpdateRecordsFor(sid) == 3
+    static = st.getStaticInfo(sid, "StatsListener", w)
+    assert static.data["model"]["numParams"] == net.numParams()
+    assert static.data["model"]["paramNames"] == ["0_W", "0_b", "1_W", "1_b"]
+    u = st.getLatestUpdate(sid, "StatsListener", w)
+    d = u.data
+    assert d["iterationCount"] == 6
+    p = d["Parameters"]["0_W"]
+    w0 = net.getParam("0_W")
+    assert abs(p["mean"] - float(w0.mean())) < 1e-6
+    assert abs(p["meanMagnitude"] - float(w0.abs().mean())) < 1e-6
+    assert sum(p["histogram"]["counts"]) == w0.numel()
+    assert set(d["Gradients"]) == set(d["Updates"]) == {"0_W", "0_b", "1_W", "1_b"}
+    assert d["learningRates"]["0_W"] == pytest.approx(1e-2)
+    assert "0" in d["Activations"] and d["performance"]["totalMinibatches"] == 6
+    assert "PostUpdate" in events and "NewSessionID" in events
+
+
+def test_file_stats_storage_roundtrip(tmp_path):
+    p = str(tmp_path / "stats.db")
+    st = FileStatsStorage(p)
+    net = _net()
+    net.setListeners(StatsListener(st, 1))
+    _fit(net, 3)
+    sid = st.listSessionIDs()[0]
+    st.close()
+    re = FileStatsStorage(p)
+    assert re.listSessionIDs() == [sid]
+    assert re.getNumUpdateRecordsFor(sid) == 3
+    w = re.listWorkerIDsForSession(sid)[0]
+    assert re.getLatestUpdate(sid, "StatsListener", w).data["iterationCount"] == 3
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=10) as r:
+        return r.read()
+
+
+def test_ui_server_and_remote_router():
+    ui = UIServer(port=0).start()
+    try:
+        st = InMemoryStatsStorage()
+        ui.attach(st)
+        net = _net()
+        net.setListeners(StatsListener(st, 1))
+        _fit(net, 4)
+        sid = st.listSessionIDs()[0]
+        assert b"Training overview" in _get(ui.getAddress() + "/")
+        assert json.loads(_get(ui.getAddress() + "/api/sessions")) == [sid]
+        ov = json.loads(_get(f"{ui.getAddress()}/api/overview?sid={sid}"))
+        assert [s[0] for s in ov["score"]] == [1, 2, 3, 4]
+        assert "0_W" in ov["updateRatios"]
+        mv = json.loads(_get(f"{ui.getAddress()}/api/model?sid={sid}"))
+        assert mv["latest"]["iteration"] == 4 and mv["model"]["numParams"] == net.numParams()
+        sv = json.loads(_get(f"{ui.getAddress()}/api/system?sid={sid}"))
+        assert sv["workers"][0]["software"]["torch"] == torch.__version__
+        # remote: a second training run posts to the UI over HTTP
+        ui.enableRemoteListener()
+        net2 = _net()
+        net2.setListeners(StatsListener(RemoteUIStatsStorageRouter(ui.getAddress()), 1, sessionID="remote-run"))
+        _fit(net2, 2)
+        assert "remote-run" in json.loads(_get(ui.getAddress() + "/api/sessions"))
+        assert ui.remote_storage.getNumUpdateRecordsFor("remote-run") == 2
+        req = urllib.request.Request(ui.getAddress() + "/tsne/upload?name=t", b"0.1,0.2,cat\n0.3,0.4,dog\n")
+        assert json.loads(urllib.request.urlopen(req, timeout=10).read())["points"] == 2
+        assert json.loads(_get(ui.getAddress() + "/api/tsne"))["t"][1][2] == "dog"
+    finally:
+        ui.stop()
