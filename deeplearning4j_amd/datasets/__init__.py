@@ -3,4 +3,10 @@ from .dataset import (DataSet, DataSetIterator, ExistingDataSetIterator, Iterato
                       ListDataSetIterator, MultiDataSet, MultiDataSetIterator, SplitTestAndTrain)
 from .iterators import (AsyncDataSetIterator, AsyncMultiDataSetIterator, BenchmarkDataSetIterator,
                         BenchmarkMultiDataSetIterator, DoublesDataSetIterator, EarlyTerminationDataSetIterator,
-                        KFoldIterator, MultipleEpochsIterator, SamplingDataSetIterator)
+                        KFoldIterator, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
+                        FileDataSetIterator, ReconstructionDataSetIterator)
+from .fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator, LFWDataSetIterator,  # noqa
+                       MnistDataSetIterator, TinyImageNetDataSetIterator, UciSequenceDataSetIterator)
+from .datavec import (CSVRecordReader, CSVSequenceRecordReader, CollectionRecordReader, FileSplit,  # noqa: F401
+                      ImageRecordReader, RecordReaderDataSetIterator, RecordReaderMultiDataSetIterator,
+                      SequenceRecordReaderDataSetIterator)

@@ -97,6 +97,25 @@ class DataSet:
         yield self.features
         yield self.labels
 
+    def save(self, path):
+        """Write features / labels / masks (each optional) as a sequence of ND4J-binary arrays behind a presence
+        bitmask byte (DataSet.save(File) layout idea: flags, then arrays)."""
+        from ..utils import nd4j_io
+        parts = [self.features, self.labels, self.featuresMask, self.labelsMask]
+        with open(path, "wb") as fh:
+            fh.write(bytes([sum(1 << i for i, t in enumerate(parts) if t is not None)]))
+            for t in parts:
+                if t is not None:
+                    nd4j_io.write(t.detach().cpu(), fh)
+
+    @staticmethod
+    def load(path):
+        from ..utils import nd4j_io
+        with open(path, "rb") as fh:
+            flags = fh.read(1)[0]
+            parts = [nd4j_io.read(fh) if flags & (1 << i) else None for i in range(4)]
+        return DataSet(*parts)
+
 
 class SplitTestAndTrain:
     def __init__(self, train, test):

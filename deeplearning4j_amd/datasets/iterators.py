@@ -305,3 +305,77 @@ class DoublesDataSetIterator(DataSetIterator):
 
 class INDArrayDataSetIterator(DoublesDataSetIterator):
     pass
+
+
+class DataSetIteratorSplitter:
+    """Splits one iterator into train / test sub-iterators by batch count (DataSetIteratorSplitter.java):
+    the first ``ratio * totalBatches`` batches feed getTrainIterator(), the rest getTestIterator()."""
+
+    def __init__(self, base, totalBatches, ratio):
+        if not 0.0 < ratio < 1.0:
+            raise ValueError("ratio must be in (0, 1)")
+        self.base, self.total = base, int(totalBatches)
+        self.ntrain = int(self.total * ratio)
+        self._cache = None
+
+    def _batches(self):
+        if self._cache is None:
+            self.base.reset()
+            out = []
+            while self.base.hasNext() and len(out) < self.total:
+                out.append(self.base.next())
+            self._cache = out
+        return self._cache
+
+    def getTrainIterator(self):
+        from .dataset import ListDataSetIterator
+        return ListDataSetIterator(self._batches()[:self.ntrain])
+
+    def getTestIterator(self):
+        from .dataset import ListDataSetIterator
+        return ListDataSetIterator(self._batches()[self.ntrain:])
+
+
+MultiDataSetIteratorSplitter = DataSetIteratorSplitter
+
+
+class FileDataSetIterator(DataSetIterator):
+    """Iterates DataSet files written by DataSet.save (one minibatch per file, sorted by name)."""
+
+    def __init__(self, rootDir, pattern=".bin"):
+        import os
+        self.files = sorted(os.path.join(dp, f) for dp, _, fs in os.walk(rootDir) for f in fs if f.endswith(pattern))
+        self.i = 0
+
+    def hasNext(self):
+        return self.i < len(self.files)
+
+    def next(self, num=None):
+        from .dataset import DataSet
+        d = DataSet.load(self.files[self.i])
+        self.i += 1
+        return self._pp(d)
+
+    def reset(self):
+        self.i = 0
+
+
+class ReconstructionDataSetIterator(DataSetIterator):
+    """Wraps an iterator so labels = features (autoencoder training)."""
+
+    def __init__(self, base):
+        self.base = base
+
+    def hasNext(self):
+        return self.base.hasNext()
+
+    def next(self, num=None):
+        from .dataset import DataSet
+        d = self.base.next()
+        return self._pp(DataSet(d.features, d.features.clone(), d.featuresMask, d.featuresMask))
+
+    def reset(self):
+        self.base.reset()
+
+    def batch(self):
+        return self.base.batch()

@@ -284,6 +284,7 @@ class ComputationGraph(BaseNetwork):
         if torch.is_tensor(labels):
             labels = [labels]
         self._mb = inputs[0].shape[0]
+        self._prepare_conv_weights()
         fm = [self._to_dev(m) for m in fmasks] if fmasks else None
         acts = self.feedForward(inputs, True, fm, stored_state, store_last_for_tbptt)
         for l in self.listeners:

@@ -13,10 +13,30 @@ class GlobalPoolingLayerImpl(LayerImpl):
             return tuple(self.conf.poolingDimensions)
         return (2,) if x.dim() == 3 else (2, 3)
 
+    def _nhwc_fast(self, x, mask, dims, pt):
+        """AVG/SUM over H,W of a channels-last 4-D tensor: reduce the contiguous [N, H*W, C] view in fp32 without
+        materialising an fp32 copy (the generic path converts the whole activation and reduces over strided dims)."""
+        return (x.dim() == 4 and mask is None and dims == (2, 3) and pt in (PoolingType.AVG, PoolingType.SUM)
+                and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous())
+
     def activate(self, x, training=False, mask=None):
         self.input = x
         dims = self._dims(x)
         pt = self.conf.poolingType
+        if self._nhwc_fast(x, mask, dims, pt):
+            n, c, h, w = x.shape
+            v = x.permute(0, 2, 3, 1).reshape(n, h * w, c)
+            out = v.sum(dim=1, dtype=_acc(x[:0]).dtype)
+            if pt == PoolingType.AVG:
+                out = out / (h * w)
+            self._fast = (n, c, h, w)
+            self._mask = None
+            self._keep_shape = (n, c, 1, 1)
+            out = out.reshape(n, c, 1, 1)
+            if self.conf.collapseDimensions:
+                out = out.reshape(n, c)
+            return out.to(x.dtype)
+        self._fast = None
         xf = _acc(x)
         m = None
         if mask is not None and x.dim() == 3:
@@ -55,8 +75,15 @@ class GlobalPoolingLayerImpl(LayerImpl):
 
     def backpropGradient(self, eps):
         x = self.input
-        e = _acc(eps).reshape(self._keep_shape)
         pt = self.conf.poolingType
+        if getattr(self, "_fast", None) is not None:
+            n, c, h, w = self._fast
+            e = _acc(eps).reshape(n, 1, 1, c)
+            if pt == PoolingType.AVG:
+                e = e / (h * w)
+            g = e.to(eps.dtype).expand(n, h, w, c).contiguous().permute(0, 3, 1, 2)   # channels-last, one write
+            return self.make_gradient(), g
+        e = _acc(eps).reshape(self._keep_shape)
         if pt == PoolingType.MAX:
             g = e * self._argmask
         elif pt == PoolingType.AVG:

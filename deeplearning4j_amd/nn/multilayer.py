@@ -173,6 +173,7 @@ class MultiLayerNetwork(BaseNetwork):
         fmask = self.mask if fmask is None else fmask
         lmask = self.labelsMask if lmask is None else lmask
         self._mb = x.shape[0]
+        self._prepare_conv_weights()
         acts = self.feedForwardToLayer(len(self.layers) - 1, x, True, self._to_dev(fmask), stored_state,
                                        store_last_for_tbptt)
         for l in self.listeners:

@@ -109,6 +109,7 @@ class BaseNetwork:
         gen = torch.Generator().manual_seed(int(self.conf.seed))
         off = 0
         self._layer_offsets = []
+        self._conv_ws = None
         self._offset_of = {}
         for idx, name, impl in layer_list:
             impl.net = self
@@ -199,6 +200,20 @@ class BaseNetwork:
             with torch.no_grad():
                 self.shadow.copy_(self.flattenedParams)
         self._bump_weight_version()
+
+    def _prepare_conv_weights(self):
+        """Refresh the MFMA-kernel layouts of all conv weights in one batched launch before a training forward
+        pass (instead of one relayout launch per conv per direction)."""
+        if self.device is None or self.device.type != "cuda":
+            return
+        ws = getattr(self, "_conv_ws", None)
+        if ws is None:
+            ws = [impl.params["W"] for _, _, impl, _ in self._layer_offsets
+                  if type(impl.conf).__name__ == "ConvolutionLayer" and "W" in impl.params]
+            self._conv_ws = ws
+        if ws:
+            from ..ops import conv_native
+            conv_native.relayout_all(ws)
 
     @staticmethod
     def _bump_weight_version():

@@ -10,12 +10,16 @@ Weights are re-laid-out once per parameter version (KRSC for forward, flipped CR
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import native
-from .native import _ptr, _stream, c_int, c_void_p
+from .native import _ptr, _stream, c_int, c_ll, c_void_p
 
 native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
+native.register_sig("dl4j_conv_w_relayout_batched", [c_void_p, c_int, c_ll, c_void_p])
+native.register_sig("dl4j_conv_relayout_job_bytes", [])
+native.register_sig("dl4j_conv_relayout_per_block", [])
 native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
@@ -56,26 +60,95 @@ def bump_version():
     WEIGHT_VERSION[0] += 1
 
 
-def _relayout(w, want_krsc, want_flip):
+class _WEnt:
+    """Kernel-layout copies of one conv weight: persistent buffers (stable addresses for HIP graphs, no allocator
+    churn) plus the weight version each copy was last written for."""
+    __slots__ = ("krsc", "flip", "vk", "vf")
+
+    def __init__(self):
+        self.krsc = self.flip = None
+        self.vk = self.vf = -1
+
+
+def _ent(w):
     key = (w.data_ptr(), tuple(w.shape))
-    ent = _cache.get(key)
-    if ent is None or ent[0] != WEIGHT_VERSION[0]:
-        ent = [WEIGHT_VERSION[0], None, None]
-        _cache[key] = ent
+    e = _cache.get(key)
+    if e is None:
+        e = _cache[key] = _WEnt()
+    return e
+
+
+def _relayout(w, want_krsc, want_flip):
+    e = _ent(w)
+    v = WEIGHT_VERSION[0]
     K, C, R, S = w.shape
-    need_k = want_krsc and ent[1] is None
-    need_f = want_flip and ent[2] is None
+    need_k = want_krsc and e.vk != v
+    need_f = want_flip and e.vf != v
     if need_k or need_f:
-        krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device) if need_k else None
-        flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device) if need_f else None
+        if need_k and e.krsc is None:
+            e.krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device)
+        if need_f and e.flip is None:
+            e.flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device)
         wc = w.contiguous()
-        rc = native.load().dl4j_conv_w_relayout(_ptr(wc), _ptr(krsc), _ptr(flip), K, C, R, S, _stream())
+        rc = native.load().dl4j_conv_w_relayout(_ptr(wc), _ptr(e.krsc if need_k else None),
+                                                _ptr(e.flip if need_f else None), K, C, R, S, _stream())
         native._check(rc, "conv_w_relayout")
         if need_k:
-            ent[1] = krsc
+            e.vk = v
         if need_f:
-            ent[2] = flip
-    return ent[1], ent[2]
+            e.vf = v
+    return e.krsc, e.flip
+
+
+_plans = {}
+
+
+def relayout_all(weights, want_flip=True):
+    """Refresh the kernel-layout copies of every eligible conv weight in ONE launch (dl4j_conv_w_relayout_batched),
+    ahead of the forward pass; the per-conv lazy path then finds fresh copies. Returns the number of weights."""
+    ws = [w for w in weights if w.dtype == torch.bfloat16 and w.is_cuda and w.dim() == 4 and w.is_contiguous()
+          and w.shape[1] % 8 == 0 and w.shape[0] % 4 == 0]
+    if not ws:
+        return 0
+    key = (tuple((w.data_ptr(), tuple(w.shape)) for w in ws), bool(want_flip))
+    plan = _plans.get(key)
+    lib = native.load()
+    if plan is None:
+        per_block = lib.dl4j_conv_relayout_per_block()
+        assert lib.dl4j_conv_relayout_job_bytes() == 56
+        jt = np.dtype([("W", "<u8"), ("out", "<u8"), ("K", "<i4"), ("C", "<i4"), ("R", "<i4"), ("S", "<i4"),
+                       ("kind", "<i4"), ("pad", "<i4"), ("first", "<i8"), ("n", "<i8")])
+        rows, ents, nblk = [], [], 0
+        for w in ws:
+            K, C, R, S = w.shape
+            e = _ent(w)
+            if e.krsc is None:
+                e.krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device)
+            flip_ok = want_flip and K % 8 == 0
+            if flip_ok and e.flip is None:
+                e.flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device)
+            n = K * C * R * S
+            outs = [(0, e.krsc)] + ([(1, e.flip)] if flip_ok else [])
+            for kind, buf in outs:
+                rows.append((w.data_ptr(), buf.data_ptr(), K, C, R, S, kind, 0, nblk, n))
+                nblk += (n + per_block - 1) // per_block
+            ents.append((e, flip_ok))
+        arr = np.array(rows, dtype=jt)
+        dev_jobs = torch.from_numpy(arr.view(np.uint8).copy()).to(ws[0].device)
+        plan = [dev_jobs, len(rows), nblk, ents, -1]
+        _plans[key] = plan
+    dev_jobs, njobs, nblk, ents, done_v = plan
+    if done_v == WEIGHT_VERSION[0]:
+        return len(ws)                      # already fresh (e.g. several forward passes between updates)
+    rc = lib.dl4j_conv_w_relayout_batched(_ptr(dev_jobs), njobs, nblk, _stream())
+    native._check(rc, "conv_w_relayout_batched")
+    v = WEIGHT_VERSION[0]
+    plan[4] = v
+    for e, flip_ok in ents:
+        e.vk = v
+        if flip_ok:
+            e.vf = v
+    return len(ws)
 
 
 def _ok_act(t):

@@ -98,3 +98,21 @@ def test_conv_kernel_variants_agree(cuda, case):
     # weight/bias gradients accumulate with atomics in a different order: equal up to fp32 rounding
     _close(outs[1][2], outs[0][2], 1e-5)
     _close(outs[1][3], outs[0][3], 1e-5)
+
+
+def test_batched_relayout_matches_per_weight():
+    """dl4j_conv_w_relayout_batched (one launch for all weights) == the per-weight relayout kernel."""
+    from deeplearning4j_amd.ops import conv_native as cn
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    shapes = [(64, 64, 3, 3), (256, 64, 1, 1), (128, 256, 1, 1), (64, 8, 7, 7), (12, 16, 3, 3)]
+    ws = [torch.randn(s, generator=g).to(torch.bfloat16).to(dev) for s in shapes]
+    cn.bump_version()
+    assert cn.relayout_all(ws) == len(ws)
+    got = [(cn._ent(w).krsc.clone(), None if cn._ent(w).flip is None else cn._ent(w).flip.clone()) for w in ws]
+    for w, (k, f) in zip(ws, got):
+        K, C, R, S = w.shape
+        torch.testing.assert_close(k.cpu(), w.permute(0, 2, 3, 1).contiguous().cpu(), rtol=0, atol=0)
+        if K % 8 == 0:
+            ref = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+            torch.testing.assert_close(f.cpu(), ref.cpu(), rtol=0, atol=0)

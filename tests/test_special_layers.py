@@ -2,6 +2,7 @@
 YOLOv2 output layer. Gradient checks in double precision as the reference does
 (CORET: gradientcheck/{VaeGradientCheckTests,YoloGradientCheckTests}.java, nn/layers/samediff/TestSameDiffDense.java,
 nn/layers/variational/TestVAE.java, nn/layers/objdetect/TestYolo2OutputLayer.java)."""
+import pytest
 import torch
 
 from deeplearning4j_amd import *  # noqa: F401,F403
@@ -143,3 +144,23 @@ def test_yolo2_gradients_and_detection():
     assert out.shape == (2, B * (5 + C), H, W)
     objs = YoloUtils.getPredictedObjects(priors, out, 0.0, 0.5)
     assert objs and all(0 <= o.getPredictedClass() < C for o in objs)
+
+
+@pytest.mark.parametrize("pt", ["AVG", "SUM"])
+def test_global_pooling_channels_last_fast_path(pt):
+    """The channels-last AVG/SUM fast path equals the generic strided reduction (values and gradients)."""
+    from deeplearning4j_amd.nn.conf import layers as L
+    from deeplearning4j_amd.nn.layers.pooling import GlobalPoolingLayerImpl
+    conf = L.GlobalPoolingLayer(poolingType=pt)
+    impl = GlobalPoolingLayerImpl(conf)
+    x = torch.randn(3, 5, 4, 6)
+    xc = x.contiguous(memory_format=torch.channels_last)
+    out_fast = impl.activate(xc)
+    assert impl._fast is not None
+    eps = torch.randn_like(out_fast)
+    _, g_fast = impl.backpropGradient(eps)
+    out_ref = impl.activate(x)
+    assert impl._fast is None
+    _, g_ref = impl.backpropGradient(eps)
+    torch.testing.assert_close(out_fast, out_ref)
+    torch.testing.assert_close(g_fast, g_ref)

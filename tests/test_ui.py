@@ -124,3 +124,38 @@ def test_ui_server_and_remote_router():
         assert json.loads(_get(ui.getAddress() + "/api/tsne"))["t"][1][2] == "dog"
     finally:
         ui.stop()
+
+
+def test_components_render(tmp_path):
+    from deeplearning4j_amd.ui.components import (ChartHistogram, ChartLine, ChartTimeline, ComponentDiv,
+                                                  ComponentTable, ComponentText, DecoratorAccordion, StaticPageUtil)
+    line = ChartLine("score").addSeries("train", [0, 1, 2], [3.0, 2.0, 1.5])
+    hist = ChartHistogram("w").addBin(0, 1, 3).addBin(1, 2, 5)
+    tl = ChartTimeline("workers").addLaneData("w0", [(0, 5, "fit"), (5, 7, "sync")])
+    tab = ComponentTable(["k", "v"], [["lr", 0.1]], title="conf")
+    page = StaticPageUtil.renderHTML([ComponentDiv(line, hist), DecoratorAccordion("more", tab, tl,
+                                                                                   ComponentText("done"))])
+    assert page.count("<svg") == 3 and "<polyline" in page and "<table" in page and "done" in page
+    assert '"componentType": "ChartLine"' in line.toJson()
+    StaticPageUtil.saveHTMLFile(str(tmp_path / "r.html"), line)
+    assert (tmp_path / "r.html").read_text().startswith("<!doctype html>")
+
+
+def test_convolutional_listener_writes_png(tmp_path):
+    from deeplearning4j_amd.nn.conf.inputs import InputType
+    from deeplearning4j_amd.ui.convolutional import ConvolutionalIterationListener
+    conf = NeuralNetConfiguration.Builder().seed(1).list() \
+        .layer(0, L.ConvolutionLayer(nOut=4, kernelSize=[3, 3], activation="relu")) \
+        .layer(1, L.OutputLayer(nOut=2, activation="softmax", lossFn="MCXENT")) \
+        .setInputType(InputType.convolutional(8, 8, 1)).build()
+    net = MultiLayerNetwork(conf)
+    net.init(device=CPU)
+    lst = ConvolutionalIterationListener(2, str(tmp_path / "acts"))
+    net.setListeners(lst)
+    x = torch.randn(3, 1, 8, 8)
+    y = torch.eye(2)[torch.tensor([0, 1, 0])]
+    for _ in range(4):
+        net.fit(x, y)
+    assert len(lst.written) == 2
+    data = open(lst.written[0], "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"

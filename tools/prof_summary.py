@@ -16,7 +16,7 @@ def load(path):
         cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
         name_col = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else None)
         q = f"select {name_col}, start, end from kernels"
-        for n, s, e in c.execute(q):
+        for n, s, e in c.execute(q + " order by start"):
             rows.append((n, (e - s) / 1e6))
     else:
         with open(path) as fh:
@@ -35,8 +35,21 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--steady", type=int, default=0,
+                    help="only the last N complete training steps (split at the fused-updater kernel), so "
+                         "initialisation and warm-up dispatches do not dilute per-step numbers")
     a = ap.parse_args()
     rows = load(a.path)
+    if a.steady:
+        steps = [[]]
+        for r in rows:
+            steps[-1].append(r)
+            if "fused_update" in r[0]:
+                steps.append([])
+        full = steps[:-1]
+        sel = full[-a.steady:]
+        rows = [r for st in sel for r in st]
+        a.steps = len(sel)
     agg = collections.defaultdict(lambda: [0, 0.0])
     for n, ms in rows:
         k = short(n)
