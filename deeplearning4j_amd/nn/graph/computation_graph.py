@@ -109,6 +109,43 @@ class ComputationGraph(BaseNetwork):
             if is_relu_layer(nxt_name) and nxt_name not in self.outputs:
                 self.layers_by_name[name].fuse_relu = True
                 self._passthrough[nxt_name] = name
+        # ZeroPadding -> Convolution(Truncate): fold the zero padding into the convolution's own (possibly
+        # asymmetric) padding, so the padded activation is never materialised (ResNet-50 stem: a 40M-element copy)
+        from ..conf.layers import ConvolutionLayer, ZeroPaddingLayer
+        from ..conf.enums import ConvolutionMode
+        for name in self.topo:
+            v = self.conf.vertices[name]
+            if not (isinstance(v, LayerVertex) and isinstance(v.layerConf, ZeroPaddingLayer)) or \
+                    name in self.outputs or len(self.consumers[name]) != 1 or \
+                    os.environ.get("DL4J_AMD_FOLD_PAD", "1") != "1":
+                continue
+            cn = self.consumers[name][0]
+            cv = self.conf.vertices[cn]
+            if not (isinstance(cv, LayerVertex) and type(cv.layerConf) is ConvolutionLayer) or \
+                    cv.preProcessor is not None or cv.layerConf.convolutionMode != ConvolutionMode.Truncate or \
+                    len(self.vertex_inputs[cn]) != 1 or len(self.vertex_inputs[name]) != 1:
+                continue
+            p = list(v.layerConf.padding)
+            self.layers_by_name[cn].extra_pad4 = (p[0], p[1], p[2], p[3])
+            self._passthrough[name] = self.vertex_inputs[name][0]
+        # Conv(+bias, identity activation) -> training-mode BatchNormalization: the bias cancels inside the batch
+        # normalisation, so the conv skips the bias add while training and BN adds (1-decay)*bias to its running
+        # mean instead (exact; saves a full read+write of the conv output when the library conv is used)
+        for name in self.topo:
+            v = self.conf.vertices[name]
+            if not (isinstance(v, LayerVertex) and type(v.layerConf) is ConvolutionLayer) or name in self.outputs \
+                    or len(self.consumers[name]) != 1 or os.environ.get("DL4J_AMD_DEFER_BIAS", "1") != "1":
+                continue
+            impl = self.layers_by_name[name]
+            if "b" not in impl.params or type(v.layerConf.activation).__name__ != "ActivationIdentity":
+                continue
+            bn_name = self.consumers[name][0]
+            bv = self.conf.vertices[bn_name]
+            if not (isinstance(bv, LayerVertex) and isinstance(bv.layerConf, BatchNormalization)) or \
+                    bv.preProcessor is not None or len(self.vertex_inputs[bn_name]) != 1:
+                continue
+            impl.defer_bias = True
+            self.layers_by_name[bn_name].deferred_bias = impl
         # which vertices must produce an input gradient
         flows = {n: False for n in self.conf.networkInputs}
         self._need_input_grad = {}

@@ -57,15 +57,22 @@ class ConvolutionLayerImpl(LayerImpl):
     def type(self):
         return "CONVOLUTIONAL"
 
+    extra_pad4 = None     # set by the graph planner when a preceding ZeroPaddingLayer is folded into this conv
+    defer_bias = False    # set by the graph planner when a training-mode BatchNormalization absorbs the bias
+
     def _geom(self, x):
         c = self.conf
         pad4 = compute_pad4(c, x.shape[2], x.shape[3])
+        if self.extra_pad4 is not None:
+            pad4 = tuple(a + b for a, b in zip(pad4, self.extra_pad4))
         return list(c.kernelSize), list(c.stride), pad4, list(c.dilation)
 
     def preOutput(self, x, training=False):
         k, s, pad4, d = self._geom(x)
         W = self.W("W")
         b = self.params["b"].reshape(-1) if "b" in self.params else None      # master-precision bias
+        if self.defer_bias and training:
+            b = None
         xt = x     # Truncate mode needs no cropping: output sizes use floor division everywhere
         self._xt = xt
         self._geom_cache = (s, pad4, d)

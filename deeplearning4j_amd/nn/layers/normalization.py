@@ -40,6 +40,13 @@ class BatchNormalizationImpl(LayerImpl):
         y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
                                       relu=self.fuse_relu, residual=res)
         self.residual = None
+        db = getattr(self, "deferred_bias", None)
+        if training and db is not None:
+            # the producing conv skipped its bias (it cancels in the batch statistics): the running mean must
+            # still track E[conv + bias]
+            with torch.no_grad():
+                rm = self.params["mean"]
+                rm.add_(db.params["b"].reshape(rm.shape).to(rm.dtype), alpha=1.0 - c.decay)
         return y
 
     def backpropGradient(self, eps):

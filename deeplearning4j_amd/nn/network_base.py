@@ -208,8 +208,10 @@ class BaseNetwork:
             return
         ws = getattr(self, "_conv_ws", None)
         if ws is None:
-            ws = [impl.params["W"] for _, _, impl, _ in self._layer_offsets
-                  if type(impl.conf).__name__ == "ConvolutionLayer" and "W" in impl.params]
+            # the compute-dtype views (bf16 shadow of fp32 masters) are what the conv kernels consume
+            ws = [impl.cparams.get("W", impl.params["W"]) for _, _, impl, _ in self._layer_offsets
+                  if type(impl.conf).__name__ == "ConvolutionLayer" and "W" in impl.params
+                  and getattr(impl.conf, "weightNoise", None) is None]
             self._conv_ws = ws
         if ws:
             from ..ops import conv_native

@@ -116,3 +116,32 @@ def test_batched_relayout_matches_per_weight():
         if K % 8 == 0:
             ref = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
             torch.testing.assert_close(f.cpu(), ref.cpu(), rtol=0, atol=0)
+
+
+def test_network_uses_batched_relayout():
+    """A bf16 ResNet-50 training step refreshes every conv weight through the single batched relayout (the
+    per-weight kernel is then never needed)."""
+    from deeplearning4j_amd.models import ResNet50
+    from deeplearning4j_amd.nn.conf import DataType
+    from deeplearning4j_amd.ops import conv_native as cn
+    dev = torch.device("cuda", 0)
+    net = ResNet50(numLabels=10, dataType=DataType.BFLOAT16).init(device=dev)
+    calls = {"single": 0}
+    orig = cn.native.load().dl4j_conv_w_relayout
+
+    class Spy:
+        def __call__(self, *a):
+            calls["single"] += 1
+            return orig(*a)
+    lib = cn.native.load()
+    lib.dl4j_conv_w_relayout = Spy()
+    try:
+        x = torch.rand(2, 3, 224, 224, device=dev)
+        y = torch.zeros(2, 10, device=dev)
+        y[:, 1] = 1
+        net.fit([x], [y])
+        net.fit([x], [y])
+    finally:
+        lib.dl4j_conv_w_relayout = orig
+    assert len(net._conv_ws) == 53
+    assert calls["single"] <= 2          # only weights outside the batched criteria (the C=3 stem goes to MIOpen)
