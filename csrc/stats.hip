@@ -140,3 +140,53 @@ DL4J_API int dl4j_segment_stats(int dtype, const void* x, const long long* off, 
   }
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------------
+// Column sums of a row-major [M, C] bf16/fp32 matrix into fp32 out[C] (conv bias gradient on the library
+// conv path: dy in channels-last is exactly such a matrix). Each thread owns 8 consecutive channels (one 16-byte
+// load for bf16) of a row; a block sweeps rows in a grid-stride loop, reduces through LDS and issues one atomic
+// per channel. Requires C % 8 == 0 and C <= 2048.
+// ------------------------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ x, long long M, int C,
+                                                          float* __restrict__ out) {
+  extern __shared__ float red[];                         // [rows_per_iter][C]
+  const int groups = C / 8;                              // threads per row
+  const int rows_per_iter = 256 / groups;
+  const int g = threadIdx.x % groups, r0 = threadIdx.x / groups;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 < rows_per_iter) {
+    for (long long r = (long long)blockIdx.x * rows_per_iter + r0; r < M; r += (long long)gridDim.x * rows_per_iter) {
+      float v[8];
+      Vec8<T>::load(x + r * C + g * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    for (int j = 0; j < 8; ++j) red[r0 * C + g * 8 + j] = acc[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < rows_per_iter; ++k) s += red[k * C + c];
+    atomicAdd(out + c, s);
+  }
+}
+}  // namespace
+
+DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, float* out, hipStream_t stream) {
+  if (C % 8 != 0 || C > 2048 || M <= 0) return -1;
+  if (hipMemsetAsync(out, 0, sizeof(float) * C, stream) != hipSuccess) return -3;
+  const int rows_per_iter = 256 / (C / 8);
+  long long blocks = (M + rows_per_iter * 16 - 1) / (rows_per_iter * 16);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  const size_t lds = sizeof(float) * rows_per_iter * C;
+  if (dtype == 1)
+    hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3((unsigned)blocks), dim3(256), lds, stream, (const bf16*)x, M, C,
+                       out);
+  else
+    hipLaunchKernelGGL(channel_sum_kernel<float>, dim3((unsigned)blocks), dim3(256), lds, stream, (const float*)x, M,
+                       C, out);
+  return (int)hipGetLastError();
+}

@@ -12,7 +12,8 @@ from ..nn.conf import (Activation, ActivationLayer, AdaDelta, BackpropType, Batc
                        ConvolutionMode, DataType, DenseLayer, DropoutLayer, ElementWiseVertex, GlobalPoolingLayer,
                        GravesLSTM, InputType, LocalResponseNormalization, LossFunction, MergeVertex,
                        NeuralNetConfiguration, Nesterovs, NormalDistribution, OptimizationAlgorithm, OutputLayer,
-                       PoolingType, RmsProp, RnnOutputLayer, SubsamplingLayer, WeightInit, ZeroPaddingLayer, Adam)
+                       PoolingType, RmsProp, RnnOutputLayer, ScaleVertex, SubsamplingLayer, WeightInit, ZeroPaddingLayer,
+                       Adam)
 from ..nn.conf.enums import WorkspaceMode
 from ..nn.graph import ComputationGraph
 from ..nn.multilayer import MultiLayerNetwork
@@ -197,15 +198,15 @@ class SimpleCNN(ZooModel):
         layers = []
         for n, k in ((16, 7), (16, 7)):
             layers += [ConvolutionLayer.Builder([k, k]).nOut(n).build(), BatchNormalization(),
-                       ActivationLayer(Activation.RELU)]
+                       ActivationLayer(activation=Activation.RELU)]
         layers += [SubsamplingLayer.Builder(PoolingType.AVG, [2, 2], [2, 2]).build(), DropoutLayer.Builder(0.5).build()]
         for n, k in ((32, 5), (32, 5)):
             layers += [ConvolutionLayer.Builder([k, k]).nOut(n).build(), BatchNormalization(),
-                       ActivationLayer(Activation.RELU)]
+                       ActivationLayer(activation=Activation.RELU)]
         layers += [SubsamplingLayer.Builder(PoolingType.AVG, [2, 2], [2, 2]).build(), DropoutLayer.Builder(0.5).build()]
         for n, k in ((64, 3), (64, 3)):
             layers += [ConvolutionLayer.Builder([k, k]).nOut(n).build(), BatchNormalization(),
-                       ActivationLayer(Activation.RELU)]
+                       ActivationLayer(activation=Activation.RELU)]
         layers += [SubsamplingLayer.Builder(PoolingType.AVG, [2, 2], [2, 2]).build(), DropoutLayer.Builder(0.5).build()]
         layers += [ConvolutionLayer.Builder([3, 3]).nOut(self.numLabels).build(),
                    GlobalPoolingLayer.Builder(PoolingType.AVG).build(),
@@ -321,7 +322,7 @@ class Darknet19(ZooModel):
         g.addLayer(f"conv{name}", ConvolutionLayer.Builder([k, k]).nOut(n).hasBias(False)
                    .convolutionMode(ConvolutionMode.Same).build(), inp)
         g.addLayer(f"bn{name}", BatchNormalization(), f"conv{name}")
-        g.addLayer(f"act{name}", ActivationLayer(Activation.LEAKYRELU), f"bn{name}")
+        g.addLayer(f"act{name}", ActivationLayer(activation=Activation.LEAKYRELU), f"bn{name}")
         return f"act{name}"
 
     def graphBuilder(self):
@@ -417,5 +418,289 @@ class GoogLeNet(ZooModel):
         return net
 
 
+
+
+# ---------------------------------------------------------------------------------------- YOLO family
+def _darknet_cbl(g, n, k, nout, inp, pool=0, pool_stride=None):
+    """Darknet conv block (reference ZOO:model/helper/DarknetHelper.java): conv (Same, no bias) -> BN ->
+    leaky ReLU(0.1) [-> max pool (Same)]. Returns the block's output vertex name."""
+    from ..nn.conf.activations import ActivationLReLU
+    g.addLayer(f"convolution2d_{n}", ConvolutionLayer.Builder([k, k]).nOut(nout).hasBias(False)
+               .convolutionMode(ConvolutionMode.Same).weightInit(WeightInit.XAVIER)
+               .activation(Activation.IDENTITY).build(), inp)
+    g.addLayer(f"batchnormalization_{n}", BatchNormalization(), f"convolution2d_{n}")
+    g.addLayer(f"activation_{n}", ActivationLayer(activation=ActivationLReLU(alpha=0.1)), f"batchnormalization_{n}")
+    out = f"activation_{n}"
+    if pool:
+        s = pool_stride if pool_stride is not None else pool
+        g.addLayer(f"maxpooling2d_{n}", SubsamplingLayer.Builder(PoolingType.MAX, [pool, pool], [s, s])
+                   .convolutionMode(ConvolutionMode.Same).build(), out)
+        out = f"maxpooling2d_{n}"
+    return out
+
+
+class _YoloBase(ZooModel):
+    DEFAULT_SHAPE = [3, 416, 416]
+    PRIORS = None
+
+    def __init__(self, numLabels=20, seed=123, inputShape=None, **kw):
+        super().__init__(numLabels, seed, inputShape, **kw)
+
+    def _base(self):
+        import torch
+        c, h, w = self.inputShape
+        g = (self._builder().optimizationAlgo(OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT)
+             .gradientNormalization("RenormalizeL2PerLayer").gradientNormalizationThreshold(1.0)
+             .updater(Adam(1e-3)).l2(1e-5).activation(Activation.IDENTITY).graphBuilder())
+        g.addInputs("input").setInputTypes(InputType.convolutional(h, w, c))
+        return g, torch.tensor(self.PRIORS, dtype=torch.float32)
+
+    def _head(self, g, n, inp, priors):
+        from ..nn.conf.layers import Yolo2OutputLayer
+        nb = priors.shape[0]
+        g.addLayer(f"convolution2d_{n}", ConvolutionLayer.Builder([1, 1]).nOut(nb * (5 + self.numLabels))
+                   .convolutionMode(ConvolutionMode.Same).weightInit(WeightInit.RELU)
+                   .activation(Activation.IDENTITY).build(), inp)
+        g.addLayer("outputs", Yolo2OutputLayer(boundingBoxes=priors), f"convolution2d_{n}")
+        return g.setOutputs("outputs")
+
+    def gridWidth(self):
+        return self.inputShape[2] // 32
+
+    def gridHeight(self):
+        return self.inputShape[1] // 32
+
+    def conf(self):
+        return self.graphBuilder().build()
+
+    def init(self, device=None):
+        net = ComputationGraph(self.conf())
+        net.init(device=device)
+        return net
+
+
+class TinyYOLO(_YoloBase):
+    """Tiny YOLOv2 (reference ZOO:model/TinyYOLO.java): 9 Darknet conv blocks with 6 max pools (the last with
+    stride 1), a 1x1 conv to nBoxes*(5+classes) channels and a Yolo2OutputLayer with the VOC anchor priors."""
+    PRIORS = [[1.08, 1.19], [3.42, 4.41], [6.63, 11.38], [9.42, 5.11], [16.62, 10.52]]
+
+    def graphBuilder(self):
+        g, priors = self._base()
+        x = "input"
+        spec = [(16, 2, 2), (32, 2, 2), (64, 2, 2), (128, 2, 2), (256, 2, 2), (512, 2, 1), (1024, 0, 0),
+                (1024, 0, 0)]
+        for i, (nout, pool, ps) in enumerate(spec, start=1):
+            x = _darknet_cbl(g, i, 3, nout, x, pool, ps)
+        return self._head(g, 9, x, priors)
+
+
+class YOLO2(_YoloBase):
+    """YOLOv2 (reference ZOO:model/YOLO2.java): Darknet-19 trunk, the 26x26 passthrough route reorganised by
+    SpaceToDepth(2) and concatenated with the 13x13 features, then the detection head."""
+    PRIORS = [[0.57273, 0.677385], [1.87446, 2.06253], [3.33843, 5.47434], [7.88282, 3.52778],
+              [9.77052, 9.16828]]
+
+    def graphBuilder(self):
+        from ..nn.conf.layers import SpaceToDepthLayer
+        g, priors = self._base()
+        spec = [(3, 32, 2), (3, 64, 2), (3, 128, 0), (1, 64, 0), (3, 128, 2), (3, 256, 0), (1, 128, 0), (3, 256, 2),
+                (3, 512, 0), (1, 256, 0), (3, 512, 0), (1, 256, 0), (3, 512, 2), (3, 1024, 0), (1, 512, 0),
+                (3, 1024, 0), (1, 512, 0), (3, 1024, 0), (3, 1024, 0), (3, 1024, 0)]
+        x = "input"
+        for i, (k, nout, pool) in enumerate(spec, start=1):
+            x = _darknet_cbl(g, i, k, nout, x, pool)
+        route = _darknet_cbl(g, 21, 1, 64, "activation_13")           # passthrough from the 26x26 stage
+        g.addLayer("rearrange_21", SpaceToDepthLayer(blockSize=2), route)
+        g.addVertex("concatenate_21", MergeVertex(), "rearrange_21", x)
+        x = _darknet_cbl(g, 22, 3, 1024, "concatenate_21")
+        return self._head(g, 23, x, priors)
+
+
+# --------------------------------------------------------------------------------------- face models
+class FaceNetNN4Small2(ZooModel):
+    """FaceNet NN4.small2 (reference ZOO:model/FaceNetNN4Small2.java + helper/FaceNetHelper.java): conv stem with
+    LRN, inception modules 3a/3b/3c/4a/4e/5a/5b (1x1-reduce -> NxN branches, pooled 1x1 branch, MergeVertex),
+    3x3 average pool, 128-d bottleneck, L2-normalised embeddings, center-loss softmax output."""
+    DEFAULT_SHAPE = [3, 96, 96]
+
+    def __init__(self, numLabels=5749, seed=123, inputShape=None, embeddingSize=128, **kw):
+        super().__init__(numLabels, seed, inputShape, **kw)
+        self.embeddingSize = embeddingSize
+
+    @staticmethod
+    def _cbr(g, name, inp, k, nout, stride=1, bias_init=None):
+        b = ConvolutionLayer.Builder([k, k], [stride, stride]).nOut(nout)
+        if bias_init is not None:
+            b = b.biasInit(bias_init)
+        g.addLayer(name, b.build(), inp)
+        g.addLayer(name + "-norm", BatchNormalization.Builder().build(), name)
+        g.addLayer(name + "-act", ActivationLayer(activation=Activation.RELU), name + "-norm")
+        return name + "-act"
+
+    def _inception(self, g, mod, inp, branches, pool):
+        """branches: list of (kernel, stride, reduce, out); pool: (ptype, size, stride, pool_proj or None);
+        plus optional plain 1x1 branch via kernel 1 entries."""
+        outs = []
+        for i, (k, s, red, out) in enumerate(branches):
+            if k == 1:
+                outs.append(self._cbr(g, f"{mod}-1x1-{i}", inp, 1, out, s, 0.2))
+                continue
+            r = self._cbr(g, f"{mod}-{k}x{k}-reduce-{i}", inp, 1, red, 1, 0.2)
+            outs.append(self._cbr(g, f"{mod}-{k}x{k}-{i}", r, k, out, s, 0.2))
+        ptype, size, stride, proj = pool
+        pb = SubsamplingLayer.Builder(ptype, [size, size], [stride, stride])
+        if ptype == PoolingType.PNORM:
+            pb = pb.pnorm(2)
+        g.addLayer(f"{mod}-pool", pb.build(), inp)
+        outs.append(self._cbr(g, f"{mod}-pool-proj", f"{mod}-pool", 1, proj, 1, 0.2) if proj else f"{mod}-pool")
+        g.addVertex(f"inception-{mod}", MergeVertex(), *outs)
+        return f"inception-{mod}"
+
+    def graphBuilder(self):
+        from ..nn.conf.graph import L2NormalizeVertex
+        from ..nn.conf.layers import CenterLossOutputLayer
+        c, h, w = self.inputShape
+        g = (self._builder().activation(Activation.IDENTITY)
+             .optimizationAlgo(OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT)
+             .updater(Adam(0.1, 0.9, 0.999, 0.01)).weightInit(WeightInit.RELU).l2(5e-5).miniBatch(True)
+             .convolutionMode(ConvolutionMode.Same).graphBuilder())
+        g.addInputs("input1").setInputTypes(InputType.convolutional(h, w, c))
+        x = self._cbr(g, "stem-cnn1", "input1", 7, 64, 2)
+        g.addLayer("stem-pool1", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(), x)
+        g.addLayer("stem-lrn1", LocalResponseNormalization.Builder(1, 5, 1e-4, 0.75).build(), "stem-pool1")
+        x = self._cbr(g, "inception-2-cnn1", "stem-lrn1", 1, 64)
+        x = self._cbr(g, "inception-2-cnn2", x, 3, 192)
+        g.addLayer("inception-2-lrn1", LocalResponseNormalization.Builder(1, 5, 1e-4, 0.75).build(), x)
+        g.addLayer("inception-2-pool1", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(),
+                   "inception-2-lrn1")
+        M, P = PoolingType.MAX, PoolingType.PNORM
+        x = self._inception(g, "3a", "inception-2-pool1", [(3, 1, 96, 128), (5, 1, 16, 32), (1, 1, 0, 64)],
+                            (M, 3, 1, 32))
+        x = self._inception(g, "3b", x, [(3, 1, 96, 128), (5, 1, 32, 64), (1, 1, 0, 64)], (P, 3, 1, 64))
+        x = self._inception(g, "3c", x, [(3, 2, 128, 256), (5, 2, 32, 64)], (M, 3, 2, None))
+        x = self._inception(g, "4a", x, [(3, 1, 96, 192), (5, 1, 32, 64), (1, 1, 0, 256)], (P, 3, 1, 128))
+        x = self._inception(g, "4e", x, [(3, 2, 160, 256), (5, 2, 64, 128)], (M, 3, 2, None))
+        x = self._inception(g, "5a", x, [(3, 1, 96, 384), (1, 1, 0, 256)], (P, 3, 1, 96))
+        x = self._inception(g, "5b", x, [(3, 1, 96, 384), (1, 1, 0, 256)], (M, 3, 1, 96))
+        g.addLayer("avgpool", SubsamplingLayer.Builder(PoolingType.AVG, [3, 3], [3, 3]).build(), x)
+        g.addLayer("bottleneck", DenseLayer.Builder().nOut(self.embeddingSize).activation(Activation.IDENTITY)
+                   .build(), "avgpool")
+        g.addVertex("embeddings", L2NormalizeVertex(dimension=[1], eps=1e-6), "bottleneck")
+        g.addLayer("lossLayer", CenterLossOutputLayer.Builder().lossFunction(LossFunction.SQUARED_LOSS)
+                   .activation(Activation.SOFTMAX).nOut(self.numLabels).alpha(0.9).lambda_(1e-4)
+                   .gradientNormalization("RenormalizeL2PerLayer").build(), "embeddings")
+        return g.setOutputs("lossLayer")
+
+    def conf(self):
+        return self.graphBuilder().build()
+
+    def init(self, device=None):
+        net = ComputationGraph(self.conf())
+        net.init(device=device)
+        return net
+
+
+class InceptionResNetV1(ZooModel):
+    """Inception-ResNet-v1 (reference ZOO:model/InceptionResNetV1.java + helper/InceptionResNetHelper.java):
+    stem, 5x block35 (scale 0.17), reduction-A, 10x block17 (scale 0.10), reduction-B, 5x block8 (scale 0.20),
+    average pool, 128-d bottleneck, L2-normalised embeddings and a center-loss softmax output. Residual branches are
+    merged, projected by a linear 1x1 conv + BN, scaled (ScaleVertex) and added to the block input, then ReLU."""
+    DEFAULT_SHAPE = [3, 160, 160]
+
+    def __init__(self, numLabels=5749, seed=123, inputShape=None, embeddingSize=128, **kw):
+        super().__init__(numLabels, seed, inputShape, **kw)
+        self.embeddingSize = embeddingSize
+
+    @staticmethod
+    def _cb(g, name, inp, k, nout, stride=1, same=True, act=True):
+        kk = k if isinstance(k, (list, tuple)) else [k, k]
+        b = ConvolutionLayer.Builder(list(kk), [stride, stride]).nOut(nout)
+        if same:
+            b = b.convolutionMode(ConvolutionMode.Same)
+        g.addLayer(name, b.activation(Activation.IDENTITY).build(), inp)
+        g.addLayer(name + "-bn", BatchNormalization.Builder().decay(0.995).eps(1e-3).build(), name)
+        if act:
+            g.addLayer(name + "-relu", ActivationLayer(activation=Activation.RELU), name + "-bn")
+            return name + "-relu"
+        return name + "-bn"
+
+    def _res_block(self, g, name, inp, branches, nout, scale):
+        outs = []
+        for bi, chain in enumerate(branches):
+            x = inp
+            for ci, (k, n) in enumerate(chain):
+                x = self._cb(g, f"{name}-b{bi}-c{ci}", x, k, n)
+            outs.append(x)
+        g.addVertex(f"{name}-merge", MergeVertex(), *outs)
+        g.addLayer(f"{name}-up", ConvolutionLayer.Builder([1, 1]).nOut(nout).activation(Activation.IDENTITY)
+                   .convolutionMode(ConvolutionMode.Same).build(), f"{name}-merge")
+        g.addLayer(f"{name}-up-bn", BatchNormalization.Builder().decay(0.995).eps(1e-3).build(), f"{name}-up")
+        g.addVertex(f"{name}-scale", ScaleVertex(scale), f"{name}-up-bn")
+        g.addVertex(f"{name}-add", ElementWiseVertex(ElementWiseVertex.Op.Add), inp, f"{name}-scale")
+        g.addLayer(name, ActivationLayer(activation=Activation.RELU), f"{name}-add")
+        return name
+
+    def graphBuilder(self):
+        from ..nn.conf.graph import L2NormalizeVertex
+        from ..nn.conf.layers import CenterLossOutputLayer
+        c, h, w = self.inputShape
+        g = (self._builder().activation(Activation.RELU)
+             .optimizationAlgo(OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT)
+             .updater(RmsProp(0.1, 0.96, 0.001)).weightInit(NormalDistribution(0.0, 0.5)).l2(5e-5)
+             .miniBatch(True).convolutionMode(ConvolutionMode.Truncate).graphBuilder())
+        g.addInputs("input1").setInputTypes(InputType.convolutional(h, w, c))
+        x = self._cb(g, "stem-cnn1", "input1", 3, 32, 2, same=False)
+        x = self._cb(g, "stem-cnn2", x, 3, 32, 1, same=False)
+        x = self._cb(g, "stem-cnn3", x, 3, 64, 1)
+        g.addLayer("stem-pool4", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(), x)
+        x = self._cb(g, "stem-cnn5", "stem-pool4", 1, 80)
+        x = self._cb(g, "stem-cnn6", x, 3, 192, 1, same=False)
+        x = self._cb(g, "stem-cnn7", x, 3, 256, 2, same=False)
+        for i in range(5):                                                    # block35
+            x = self._res_block(g, f"resnetA-{i}", x, [[(1, 32)], [(1, 32), (3, 32)],
+                                                        [(1, 32), (3, 32), (3, 32)]], 256, 0.17)
+        a = self._cb(g, "reduceA-b0", x, 3, 384, 2, same=False)             # reduction-A
+        b = self._cb(g, "reduceA-b1-c0", x, 1, 192)
+        b = self._cb(g, "reduceA-b1-c1", b, 3, 192)
+        b = self._cb(g, "reduceA-b1-c2", b, 3, 256, 2, same=False)
+        g.addLayer("reduceA-pool", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(), x)
+        g.addVertex("reduceA", MergeVertex(), a, b, "reduceA-pool")
+        x = "reduceA"
+        for i in range(10):                                                   # block17
+            x = self._res_block(g, f"resnetB-{i}", x, [[(1, 128)], [(1, 128), ([1, 7], 128), ([7, 1], 128)]],
+                                896, 0.10)
+        b0 = self._cb(g, "reduceB-b0-c0", x, 1, 256)                          # reduction-B
+        b0 = self._cb(g, "reduceB-b0-c1", b0, 3, 384, 2, same=False)
+        b1 = self._cb(g, "reduceB-b1-c0", x, 1, 256)
+        b1 = self._cb(g, "reduceB-b1-c1", b1, 3, 256, 2, same=False)
+        b2 = self._cb(g, "reduceB-b2-c0", x, 1, 256)
+        b2 = self._cb(g, "reduceB-b2-c1", b2, 3, 256)
+        b2 = self._cb(g, "reduceB-b2-c2", b2, 3, 256, 2, same=False)
+        g.addLayer("reduceB-pool", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(), x)
+        g.addVertex("reduceB", MergeVertex(), b0, b1, b2, "reduceB-pool")
+        x = "reduceB"
+        for i in range(5):                                                    # block8
+            x = self._res_block(g, f"resnetC-{i}", x, [[(1, 192)], [(1, 192), ([1, 3], 192), ([3, 1], 192)]],
+                                1792, 0.20)
+        g.addLayer("avgpool", GlobalPoolingLayer.Builder(PoolingType.AVG).build(), x)
+        g.addLayer("bottleneck", DenseLayer.Builder().nOut(self.embeddingSize).activation(Activation.IDENTITY)
+                   .build(), "avgpool")
+        g.addVertex("embeddings", L2NormalizeVertex(dimension=[1], eps=1e-10), "bottleneck")
+        g.addLayer("outputLayer", CenterLossOutputLayer.Builder().lossFunction(LossFunction.NEGATIVELOGLIKELIHOOD)
+                   .activation(Activation.SOFTMAX).nOut(self.numLabels).alpha(0.9).lambda_(1e-4).build(),
+                   "embeddings")
+        return g.setOutputs("outputLayer")
+
+    def conf(self):
+        return self.graphBuilder().build()
+
+    def init(self, device=None):
+        net = ComputationGraph(self.conf())
+        net.init(device=device)
+        return net
+
+
 ZOO = {"ResNet50": ResNet50, "LeNet": LeNet, "SimpleCNN": SimpleCNN, "TextGenerationLSTM": TextGenerationLSTM,
-       "AlexNet": AlexNet, "VGG16": VGG16, "VGG19": VGG19, "Darknet19": Darknet19, "GoogLeNet": GoogLeNet}
+       "AlexNet": AlexNet, "VGG16": VGG16, "VGG19": VGG19, "Darknet19": Darknet19, "GoogLeNet": GoogLeNet,
+       "TinyYOLO": TinyYOLO, "YOLO2": YOLO2, "FaceNetNN4Small2": FaceNetNN4Small2,
+       "InceptionResNetV1": InceptionResNetV1}

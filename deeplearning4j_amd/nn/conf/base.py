@@ -85,6 +85,11 @@ class _AutoBuilder:
         name = cls._ALIASES.get(name, name)
         if name not in cls._all_fields():
             raise AttributeError(f"{cls.__name__}.Builder has no property {name!r}")
+        if name == "weightInit" and "dist" in cls._all_fields():
+            from .weights import Distribution, WeightInit
+            if isinstance(value, Distribution):       # layer.weightInit(dist) == dist(d) + WeightInit.DISTRIBUTION
+                self._kw["dist"] = value
+                value = WeightInit.DISTRIBUTION
         conv = cls._CONVERTERS.get(name)
         self._kw[name] = conv(value) if conv else value
 

@@ -699,6 +699,13 @@ class LocalResponseNormalization(Layer):
     FIELDS = {"k": 2.0, "n": 5.0, "alpha": 1e-4, "beta": 0.75, "cudnnAllowFallback": True}
     RUNTIME = "deeplearning4j_amd.nn.layers.normalization:LocalResponseNormalizationImpl"
 
+    @classmethod
+    def _builder_positional(cls, kw, *args):
+        """Builder(k, n, alpha, beta) or Builder(alpha, beta) (LocalResponseNormalization.java Builder ctors)."""
+        names = ["k", "n", "alpha", "beta"] if len(args) != 2 else ["alpha", "beta"]
+        for n, v in zip(names, args):
+            kw[n] = float(v)
+
 
 class LayerNormalization(FeedForwardLayer):
     """LayerNorm over the feature dim (new; needed by the BERT-base config of BASELINE.json)."""

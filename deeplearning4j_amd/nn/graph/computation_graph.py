@@ -139,6 +139,11 @@ class ComputationGraph(BaseNetwork):
             impl = self.layers_by_name[name]
             if "b" not in impl.params or type(v.layerConf.activation).__name__ != "ActivationIdentity":
                 continue
+            if v.layerConf.nIn % 8 == 0 and v.layerConf.nOut % 4 == 0 and \
+                    os.environ.get("DL4J_AMD_DEFER_BIAS", "1") != "all":
+                # the MFMA conv kernels fuse the bias into their epilogue for free; deferring would only add a
+                # small running-mean launch per layer. Defer where the library conv runs (e.g. the C=3 stem).
+                continue
             bn_name = self.consumers[name][0]
             bv = self.conf.vertices[bn_name]
             if not (isinstance(bv, LayerVertex) and isinstance(bv.layerConf, BatchNormalization)) or \

@@ -57,7 +57,11 @@ def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_
         # bias gradient as a column sum of the contiguous channels-last [N*H*W, K] view (the library reduces over
         # strided N,H,W dims: ~4x slower on the 411 MB ResNet stem gradient)
         K = dy.shape[1]
-        db = dy.permute(0, 2, 3, 1).reshape(-1, K).sum(0, dtype=torch.float32)
+        rows = dy.permute(0, 2, 3, 1).reshape(-1, K)
+        from . import native
+        db = native.channel_sum(rows) if use_native(dy, "conv") else None
+        if db is None:
+            db = rows.sum(0, dtype=torch.float32)
     if need_dx and not sym:
         dx = dx[:, :, pt:pt + x.shape[2], pl:pl + x.shape[3]]
     return dx, dw, db

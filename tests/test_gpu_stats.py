@@ -55,3 +55,12 @@ def test_stats_listener_on_gpu(cuda):
     w0 = net.getParam("0_W").float()
     assert abs(d["Parameters"]["0_W"]["meanMagnitude"] - float(w0.abs().mean())) < 1e-5
     assert d["memory"]["deviceMaxBytes"][0] > 0
+
+
+@pytest.mark.parametrize("C", [8, 64, 256, 24])
+def test_channel_sum_matches_torch(cuda, C):
+    from deeplearning4j_amd.ops import native
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(100_003, C, generator=g).to(torch.bfloat16).to(cuda)
+    got = native.channel_sum(x)
+    torch.testing.assert_close(got.cpu(), x.float().sum(0).cpu(), rtol=1e-4, atol=1e-2)

@@ -218,7 +218,7 @@ def test_conv_bias_deferred_into_batchnorm(monkeypatch):
     y = torch.randn(5, 2)
     monkeypatch.setenv("DL4J_AMD_DEFER_BIAS", "1")
     a = build()
-    assert a.layers_by_name["c"].defer_bias
+    assert a.layers_by_name["c"].defer_bias      # nIn = 3: the library-conv case
     monkeypatch.setenv("DL4J_AMD_DEFER_BIAS", "0")
     b = build()
     assert not b.layers_by_name["c"].defer_bias
