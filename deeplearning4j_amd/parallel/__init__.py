@@ -5,3 +5,5 @@ from .distributed import barrier, destroy, init_distributed, is_dist, rank, worl
 from .encoded import EncodedGradientsAccumulator, EncodingHandler
 from .inference import InferenceMode, ParallelInference
 from .wrapper import ParallelWrapper, TrainingMode
+from .cluster import (ParameterAveragingTrainingMaster, SharedTrainingMaster, SparkComputationGraph,  # noqa: F401
+                      SparkDl4jMultiLayer, StatsUtils, TrainingMaster, TrainingStats)

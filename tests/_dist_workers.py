@@ -62,3 +62,35 @@ def run_mode(rank, world, port, mode, result_path):
         torch.save({"params": [t.clone() for t in gathered], "iters": net.getIterationCount()}, result_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_cluster(rank, world, port, master, result_path):
+    """Cluster training masters (the dl4j-spark replacement) on a gloo process group."""
+    _setup(rank, world, port)
+    from deeplearning4j_amd import Adam
+    from deeplearning4j_amd.parallel.cluster import (ParameterAveragingTrainingMaster, SharedTrainingMaster,
+                                                     SparkDl4jMultiLayer, StatsUtils)
+    net = make_net(Adam(0.01))
+    if rank == 1:
+        with torch.no_grad():
+            net.flattenedParams.add_(1.0)
+    if master == "paramavg":
+        tm = ParameterAveragingTrainingMaster.Builder(1).batchSizePerWorker(8).averagingFrequency(2) \
+            .collectTrainingStats(True).build()
+    else:
+        tm = SharedTrainingMaster.Builder(1e-3).batchSizePerWorker(8).build()
+    spark = SparkDl4jMultiLayer(None, net, tm)
+    data = make_batches(8, 8)
+    spark.fit(data, 2)
+    ev = spark.evaluate(data)
+    score = spark.calculateScore(data)
+    p = net.params().clone()
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        if master == "paramavg":
+            StatsUtils.exportStatsAsHtml(tm.getTrainingStats(), result_path + ".html")
+        torch.save({"params": [t.clone() for t in gathered], "n_eval": int(ev.getNumRowCounter()),
+                    "score": score, "acc": float(ev.accuracy())}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -125,3 +125,42 @@ def test_wrapper_single_process_trains():
     s0 = net.score(W.make_batches(1, 64, seed=9)[0])
     ParallelWrapper.Builder(net).build().fit(it, 5)
     assert net.score(W.make_batches(1, 64, seed=9)[0]) < s0 + 0.5
+
+
+@pytest.mark.parametrize("master", ["paramavg", "shared"])
+def test_cluster_training_masters(tmp_path, master):
+    """ParameterAveraging / Shared training masters across 2 gloo ranks: replicas end identical (rank 1 started
+    from different weights), evaluation merges both shards (all 64 examples counted once)."""
+    path = str(tmp_path / f"{master}.pt")
+    mp.spawn(W.run_cluster, args=(2, _port(), master, path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    assert torch.allclose(r["params"][0], r["params"][1], atol=1e-6)
+    assert r["n_eval"] == 64
+    assert r["score"] == r["score"] and 0.0 <= r["acc"] <= 1.0
+    if master == "paramavg":
+        html = open(path + ".html").read()
+        assert "fit" in html and "average" in html
+
+
+def test_parallel_wrapper_main_cli(tmp_path):
+    """ParallelWrapperMain: restore a model zip, train from an iterator factory, write the result."""
+    import sys
+    from deeplearning4j_amd import Adam
+    from deeplearning4j_amd.parallel.main import main
+    from deeplearning4j_amd.utils.model_serializer import ModelSerializer
+    (tmp_path / "pwm_data.py").write_text(
+        "import torch\nfrom deeplearning4j_amd import DataSet, ListDataSetIterator\n"
+        "def make():\n    g = torch.Generator().manual_seed(0)\n    out = []\n"
+        "    for _ in range(4):\n        x = torch.randn(8, 5, generator=g)\n        y = torch.zeros(8, 3)\n"
+        "        y[:, 0] = 1\n        out.append(DataSet(x, y))\n    return ListDataSetIterator(out)\n")
+    sys.path.insert(0, str(tmp_path))
+    try:
+        net = W.make_net(Adam(0.01))
+        ModelSerializer.writeModel(net, str(tmp_path / "in.zip"), True)
+        out = main(["--modelPath", str(tmp_path / "in.zip"), "--dataSetIteratorFactoryClazz", "pwm_data:make",
+                    "--modelOutputPath", str(tmp_path / "out.zip"), "--epochs", "2"])
+        assert out.getIterationCount() == 8
+        re = ModelSerializer.restoreModel(str(tmp_path / "out.zip"))
+        assert torch.allclose(re.params(), out.params())
+    finally:
+        sys.path.remove(str(tmp_path))
