@@ -10,8 +10,10 @@ Training runs through EmbeddingEngine (native batcher + gfx950 kernels / threade
 import json
 import logging
 import time
+import zlib
 
 import numpy as np
+
 import torch
 
 from .embeddings import (EmbeddingEngine, InMemoryLookupTable, M_CBOW, M_DBOW, M_DM, M_SG, WordVectorsImpl,
@@ -427,7 +429,7 @@ class ParagraphVectors(Word2Vec):
                        dtype=np.int32)
         dev = self._lookup.device
         D = self._lookup.vectorLength
-        g = torch.Generator().manual_seed(abs(hash(" ".join(toks))) % (2 ** 31))
+        g = torch.Generator().manual_seed(zlib.crc32(" ".join(toks).encode()) % (2 ** 31))  # stable across processes
         vec = ((torch.rand(1, D, generator=g) - 0.5) / D).to(dev)
         if len(idx) == 0:
             return vec.reshape(-1)

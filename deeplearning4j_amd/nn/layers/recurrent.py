@@ -6,9 +6,10 @@ gate blocks in the 4H axis are [a (cell input, layer activation) | f (forget) | 
 g (input-modulation)], peepholes (Graves) are RW columns 4H (wFF), 4H+1 (wOO), 4H+2 (wGG):
     a = act(z_a); f = gate(z_f + wFF*c_prev); g = gate(z_g + wGG*c_prev)
     c = f*c_prev + g*a; o = gate(z_o + wOO*c); h = o*act(c)
-MI355X structure: ONE big input-projection GEMM for all T steps ([T*mb, nIn] x [nIn, 4H]), then the
-recurrent loop does one [mb,H]x[H,4H] GEMM + the fused gate kernel per step (csrc/lstm.hip on GPU);
-backward accumulates dW, dRW and dX as single big GEMMs after the time loop. TBPTT stops the
+MI355X structure: ONE big input-projection GEMM for all T steps ([T*mb, nIn] x [nIn, 4H]), then on GPU ONE
+launch of the whole-sequence recurrent kernel (csrc/lstm.hip: MFMA h·RW + fused gates, cell state in registers;
+the HIP replacement of the cuDNN LSTMHelper); the per-step torch loop below is the CPU/fp64 reference path.
+Backward runs the mirrored sequence kernel, then accumulates dW, dRW and dX as single big GEMMs. TBPTT stops the
 backward time loop at ``tbpttBackLength`` steps (LSTMHelpers.java:484).
 """
 import torch
@@ -19,6 +20,14 @@ from .base import LayerImpl, copy_grad_
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc, acc_dtype  # noqa: E402
 
 
+def _native_ok(x, W, act, gate_act, H):
+    """Whole-sequence HIP kernels apply: GPU tensor, tanh/sigmoid (the cuDNN helper's own restriction,
+    CudnnLSTMHelper.java:174-190 — peepholes are supported here), kernel-supported H/dtype."""
+    from ...ops import rnn_native
+    return (x.is_cuda and isinstance(act, ActivationTanH) and isinstance(gate_act, ActivationSigmoid)
+            and rnn_native.supported(H, W.dtype) and ops.use_native(x, "lstm"))
+
+
 def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache):
     """x: [mb, nIn, T]. Returns out [mb, H, T], (hT, cT), cache."""
     mb, nIn, T = x.shape
@@ -26,6 +35,17 @@ def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache)
     _adt = acc_dtype(W)
     xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
     zx = (xt @ W + b.reshape(1, -1).to(dt)).reshape(T, mb, 4 * H)          # input projection, all steps
+    if _native_ok(x, W, act, gate_act, H):
+        from ...ops import rnn_native
+        r = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, mask, need_cache)
+        if r is not None:
+            out_tmh, hT, cT, gates, call = r
+            out = out_tmh.permute(1, 2, 0).to(x.dtype if x.is_floating_point() else dt)
+            cache = None
+            if need_cache:
+                cache = {"native": True, "gates": gates, "call": call, "out": out_tmh, "h0": h0, "c0": c0,
+                         "xt": xt}
+            return out, (hT, cT), cache
     RWg = RW[:, :4 * H]
     if peephole:
         wFF, wOO, wGG = _acc(RW[:, 4 * H]), _acc(RW[:, 4 * H + 1]), _acc(RW[:, 4 * H + 2])
@@ -34,28 +54,22 @@ def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache)
     outs = []
     cache = {"z": [], "a": [], "f": [], "g": [], "o": [], "c": [], "c_prev": [], "h_prev": [], "cact": []} \
         if need_cache else None
-    std = isinstance(act, ActivationTanH) and isinstance(gate_act, ActivationSigmoid)
     for t in range(T):
         z = _acc(zx[t]) + _acc((h.to(dt) @ RWg))
-        if std and not peephole and not need_cache and z.is_cuda and _native_cell(z):
-            from ...ops import native
-            h_new, c_new = native.lstm_cell_fwd(z, c)
-            a = f = g = o = cact = None
-        else:
-            za, zf, zo, zg = z[:, :H], z[:, H:2 * H], z[:, 2 * H:3 * H], z[:, 3 * H:]
-            if peephole:
-                zf = zf + c * wFF
-                zg = zg + c * wGG
-            a = act.getActivation(za, True)
-            f = gate_act.getActivation(zf, True)
-            g = gate_act.getActivation(zg, True)
-            c_new = f * c + g * a
-            if peephole:
-                zo = zo + c_new * wOO
-            o = gate_act.getActivation(zo, True)
-            cact = act.getActivation(c_new, True)
-            h_new = o * cact
-            z = torch.cat([za, zf, zo, zg], dim=1)
+        za, zf, zo, zg = z[:, :H], z[:, H:2 * H], z[:, 2 * H:3 * H], z[:, 3 * H:]
+        if peephole:
+            zf = zf + c * wFF
+            zg = zg + c * wGG
+        a = act.getActivation(za, True)
+        f = gate_act.getActivation(zf, True)
+        g = gate_act.getActivation(zg, True)
+        c_new = f * c + g * a
+        if peephole:
+            zo = zo + c_new * wOO
+        o = gate_act.getActivation(zo, True)
+        cact = act.getActivation(c_new, True)
+        h_new = o * cact
+        z = torch.cat([za, zf, zo, zg], dim=1)
         if mask is not None:
             m = _acc(mask[:, t]).reshape(-1, 1)
             h_new = h_new * m
@@ -78,11 +92,53 @@ def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache)
     return out, (h, c), cache
 
 
+def _lstm_weight_grads(dzf2, xt, hprev, W, H, peephole, peep_grads, grads_prefix, grads, T, mb):
+    """The big library GEMMs after the time loop: dW = xᵀ·dz, dRW = hprevᵀ·dz (+ peephole columns), db = Σdz,
+    dX = dz·Wᵀ (LSTMHelpers.java:616-676)."""
+    dt = W.dtype
+    copy_grad_(grads[grads_prefix + "W"], _acc(xt).t() @ dzf2)
+    dRW = hprev.reshape(T * mb, H).t() @ dzf2
+    if peephole:
+        dRW = torch.cat([dRW] + [g.reshape(-1, 1) for g in peep_grads], dim=1)
+    copy_grad_(grads[grads_prefix + "RW"], dRW)
+    copy_grad_(grads[grads_prefix + "b"], dzf2.sum(dim=0))
+    return (dzf2.to(dt) @ W.t()).reshape(T, mb, -1).permute(1, 2, 0)
+
+
+def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last):
+    from ...ops import rnn_native
+    mb, _, T = eps.shape
+    t_end = max(0, T - tbptt_back) if tbptt_back else 0
+    r = rnn_native.lstm_seq_bwd(eps.permute(2, 0, 1), cache["gates"], cache["call"], cache["c0"], RW, H, peephole,
+                                mask, dh_last, dc_last, t_end)
+    if r is None:
+        return None
+    dz, dh0, dc0 = r
+    out = cache["out"]                                                # [T, mb, H] fp32
+    dev = eps.device
+    h0 = torch.zeros(1, mb, H, device=dev) if cache["h0"] is None else _acc(cache["h0"]).reshape(1, mb, H)
+    hprev = torch.cat([h0.to(out.dtype), out[:-1]], dim=0)
+    peep_grads = None
+    if peephole:
+        c0 = torch.zeros(1, mb, H, device=dev) if cache["c0"] is None else _acc(cache["c0"]).reshape(1, mb, H)
+        call = cache["call"]
+        cprev = torch.cat([c0.to(call.dtype), call[:-1]], dim=0)
+        dzf, dzo, dzg = dz[:, :, H:2 * H], dz[:, :, 2 * H:3 * H], dz[:, :, 3 * H:]
+        peep_grads = [(dzf * cprev).sum(dim=(0, 1)), (dzo * call).sum(dim=(0, 1)), (dzg * cprev).sum(dim=(0, 1))]
+    dx = _lstm_weight_grads(dz.reshape(T * mb, 4 * H), cache["xt"], hprev, W, H, peephole, peep_grads,
+                            grads_prefix, grads, T, mb)
+    return dx, dh0, dc0
+
+
 def _lstm_bwd(eps, cache, W, RW, H, peephole, act, gate_act, mask, tbptt_back, grads_prefix, grads, dh_last=None,
               dc_last=None):
     """eps: [mb, H, T]. Writes dW/dRW/db into grads views; returns eps_in [mb, nIn, T]."""
+    if cache.get("native"):
+        r = _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last)
+        if r is not None:
+            return r
+        raise RuntimeError("native LSTM forward cache but the backward kernel rejected the shape")
     mb, _, T = eps.shape
-    dt = W.dtype
     _adt = acc_dtype(W)
     RWg = _acc(RW[:, :4 * H])
     if peephole:
@@ -124,23 +180,9 @@ def _lstm_bwd(eps, cache, W, RW, H, peephole, act, gate_act, mask, tbptt_back, g
         dz_all[t] = dz
         dh_next = dz @ RWg.t()
     hprev = torch.stack(cache["h_prev"], 0)                       # [T, mb, H]
-    dzf2 = dz_all.reshape(T * mb, 4 * H)
-    gW = grads[grads_prefix + "W"]
-    gRW = grads[grads_prefix + "RW"]
-    gb = grads[grads_prefix + "b"]
-    copy_grad_(gW, _acc(cache["xt"]).t() @ dzf2)
-    dRW = hprev.reshape(T * mb, H).t() @ dzf2
-    if peephole:
-        dRW = torch.cat([dRW, dwFF.reshape(-1, 1), dwOO.reshape(-1, 1), dwGG.reshape(-1, 1)], dim=1)
-    copy_grad_(gRW, dRW)
-    copy_grad_(gb, dzf2.sum(dim=0))
-    dx = (dzf2.to(dt) @ W.t()).reshape(T, mb, -1).permute(1, 2, 0)
+    dx = _lstm_weight_grads(dz_all.reshape(T * mb, 4 * H), cache["xt"], hprev, W, H, peephole,
+                            [dwFF, dwOO, dwGG] if peephole else None, grads_prefix, grads, T, mb)
     return dx, dh_next, dc_next
-
-
-def _native_cell(z):
-    from ...ops import rnn_native
-    return rnn_native.available and ops.use_native(z, "lstm")
 
 
 class BaseRecurrentImpl(LayerImpl):

@@ -350,11 +350,6 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
                                   grads_zeroed)
 
 
-def lstm_cell_fwd(z, c):
-    from . import rnn_native
-    return rnn_native.lstm_cell_fwd(z, c)
-
-
 def segment_stats(flat, offsets, bins=0):
     """Per-segment {mean, std, meanAbs, min, max} (+ optional ``bins``-bin histograms over [min, max]) of a flat
     fp32/bf16 CUDA tensor, one fused HIP launch for all segments (csrc/stats.hip). ``offsets``: list of nseg+1

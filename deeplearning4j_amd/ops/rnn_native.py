@@ -1,6 +1,99 @@
-"""Fused LSTM cell kernels (csrc/lstm.hip). ``available`` flips on once the kernel is in the library."""
-available = False
+"""Whole-sequence fused LSTM / GravesLSTM kernels (csrc/lstm.hip): the MI355X counterpart of the reference's cuDNN
+``LSTMHelper`` (deeplearning4j-cuda/.../recurrent/CudnnLSTMHelper.java; SPI at nn/layers/recurrent/LSTM.java:66).
+
+``lstm_seq_fwd`` runs the recurrence of all T steps in one launch (one workgroup per 16 minibatch rows, MFMA
+h·RW, fused gates + peepholes + mask, cell state in registers). ``lstm_seq_bwd`` runs the backward time loop
+(gate deltas + dh = dz·RWᵀ per step) and returns the fp32 gate deltas for the weight GEMMs. Both return
+``None`` when the shape/dtype is outside the kernels (the caller then runs the per-step path).
+"""
+import torch
+
+from . import native
+from .native import _check, _ptr, _stream, c_int, c_void_p
+
+_SIG_FWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+            c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+_SIG_BWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
 
 
-def lstm_cell_fwd(z, c):
-    raise NotImplementedError
+def supported(H, dtype):
+    if dtype == torch.bfloat16:
+        ok_k = H % 32 == 0
+    elif dtype == torch.float32:
+        ok_k = H % 16 == 0
+    else:
+        return False
+    if not ok_k:
+        return False
+    return H // 16 <= 16 or (H % 32 == 0 and H // 32 <= 16) or (H % 64 == 0 and H // 64 <= 16)
+
+
+def _pack_b(m, dt):
+    """[N, K] matrix (B[k][n] = m[n][k]) -> the kernels' fragment-packed layout [N/16][K/KC][64 lanes][FE]: lane
+    l of k-step s holds m[16*tile + (l & 15)][KC*s + FE*(l >> 4) + j], j < FE, so each wave load is contiguous."""
+    fe = 8 if dt == torch.bfloat16 else 4
+    N, K = m.shape
+    return (m.to(dt).reshape(N // 16, 16, K // (4 * fe), 4, fe).permute(0, 2, 3, 1, 4).contiguous())
+
+
+def _f32c(t):
+    return None if t is None else t.detach().to(torch.float32).contiguous()
+
+
+def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=True):
+    """zx: [T, mb, 4H] (compute dtype, = x·W + b); RW: [H, 4H(+3)] view.
+    Returns (out [T, mb, H] fp32, hT, cT, gates [T,mb,4H] fp32 | None, call [T,mb,H] fp32 | None) or None."""
+    T, mb, H4 = zx.shape
+    dt = zx.dtype
+    if H4 != 4 * H or not supported(H, dt) or T < 1 or mb < 1:
+        return None
+    lib = native.load()
+    native.register_sig("dl4j_lstm_fwd", _SIG_FWD)
+    dev = zx.device
+    zx = zx.contiguous()
+    rwt = _pack_b(RW[:, :4 * H].t(), dt)                             # B[k][n] = RW[k][n], n over 4H
+    peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
+    h0c, c0c = _f32c(h0), _f32c(c0)
+    m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
+    if m is not None and m.shape[1] != T:
+        return None
+    out = torch.empty(T, mb, H, device=dev, dtype=torch.float32)
+    hT = torch.empty(mb, H, device=dev, dtype=torch.float32)
+    cT = torch.empty(mb, H, device=dev, dtype=torch.float32)
+    gates = torch.empty(T, mb, 4 * H, device=dev, dtype=torch.float32) if need_cache else None
+    call = torch.empty(T, mb, H, device=dev, dtype=torch.float32) if need_cache else None
+    rc = lib.dl4j_lstm_fwd(1 if dt == torch.bfloat16 else 0, _ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c),
+                           _ptr(m), _ptr(out), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), T, mb, H,
+                           c_void_p(_stream()))
+    if rc == -1:
+        return None
+    _check(rc, "lstm_fwd")
+    return out, hT, cT, gates, call
+
+
+def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=None, dc_last=None, t_end=0):
+    """eps_tmh: [T, mb, H] (any float dtype). Returns (dz [T, mb, 4H] fp32, dh0, dc0) or None."""
+    T, mb, _ = eps_tmh.shape
+    dt = RW.dtype
+    if not supported(H, dt) or t_end >= T:
+        return None
+    lib = native.load()
+    native.register_sig("dl4j_lstm_bwd", _SIG_BWD)
+    dev = eps_tmh.device
+    e = _f32c(eps_tmh)
+    rw = _pack_b(RW[:, :4 * H], dt)                                   # dh = dz·RWᵀ: B[k][n] = RW[n][k], k over 4H
+    peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
+    m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
+    dz = (torch.zeros if t_end > 0 else torch.empty)(T, mb, 4 * H, device=dev, dtype=torch.float32)
+    dh0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
+    dc0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
+    rc = lib.dl4j_lstm_bwd(1 if dt == torch.bfloat16 else 0, _ptr(e), _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
+                           _ptr(rw), _ptr(peep), _ptr(m), _ptr(_f32c(dh_last)), _ptr(_f32c(dc_last)), _ptr(dz),
+                           _ptr(dh0), _ptr(dc0), T, mb, H, int(t_end), c_void_p(_stream()))
+    if rc == -1:
+        return None
+    _check(rc, "lstm_bwd")
+    return dz, dh0, dc0
+
+

@@ -1,0 +1,79 @@
+"""Whole-sequence LSTM/GravesLSTM HIP kernels (csrc/lstm.hip) vs the per-step torch reference in fp64 on the CPU.
+
+Same strategy as the reference's cuDNN LSTM validation (CUDAT:lstm/ValidateCudnnLSTM.java:32-246): the helper's
+activations and gradients must match the built-in implementation."""
+import pytest
+import torch
+
+from deeplearning4j_amd.nn.conf.activations import ActivationSigmoid, ActivationTanH
+from deeplearning4j_amd.nn.layers import recurrent as R
+from deeplearning4j_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    a, b = a.double().cpu(), b.double().cpu()
+    err = (a - b).abs().max().item()
+    scale = max(1.0, b.abs().max().item())
+    assert err <= tol * scale, f"max abs err {err} (scale {scale})"
+
+
+def _params(nIn, H, peep, g):
+    W = torch.randn(nIn, 4 * H, generator=g, dtype=torch.float64) * 0.3
+    RW = torch.randn(H, 4 * H + (3 if peep else 0), generator=g, dtype=torch.float64) * 0.3 / (H ** 0.5) * 4
+    b = torch.randn(4 * H, generator=g, dtype=torch.float64) * 0.2
+    return W, RW, b
+
+
+def _run(x, W, RW, b, h0, c0, H, peep, mask, eps, tbptt):
+    act, gate = ActivationTanH(), ActivationSigmoid()
+    out, (hT, cT), cache = R._lstm_fwd(x, W, RW, b, h0, c0, H, peep, act, gate, mask, True)
+    grads = {"W": torch.zeros_like(W), "RW": torch.zeros_like(RW), "b": torch.zeros_like(b)}
+    dx, _, _ = R._lstm_bwd(eps, cache, W, RW, H, peep, act, gate, mask, tbptt, "", grads)
+    return out, hT, cT, dx, grads, cache
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 4e-2)])
+@pytest.mark.parametrize("H", [32, 64, 256, 512])
+@pytest.mark.parametrize("peep", [False, True])
+def test_lstm_seq_kernels_match_reference(cuda, dtype, tol, H, peep):
+    if dtype == torch.float32 and H == 512:
+        pytest.skip("covered by bf16")
+    g = torch.Generator().manual_seed(H + peep)
+    mb, nIn, T = 37, 24, 11                                      # mb not a multiple of 16: masked tail rows
+    W, RW, b = _params(nIn, H, peep, g)
+    x = torch.randn(mb, nIn, T, generator=g, dtype=torch.float64)
+    h0 = torch.randn(mb, H, generator=g, dtype=torch.float64) * 0.5
+    c0 = torch.randn(mb, H, generator=g, dtype=torch.float64) * 0.5
+    mask = (torch.rand(mb, T, generator=g) > 0.2).double()
+    eps = torch.randn(mb, H, T, generator=g, dtype=torch.float64)
+    # reference: fp64 per-step path on the CPU, with weights rounded like the device copy
+    Wd, RWd, bd = (t.to(dtype) for t in (W, RW, b))
+    ref = _run(x, Wd.double(), RWd.double(), bd.double(), h0, c0, H, peep, mask, eps, 6)
+    dev = [t.to(cuda) for t in (x.float(), Wd, RWd, bd, h0.float(), c0.float(), mask.float(), eps.float())]
+    got = _run(dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], H, peep, dev[6], dev[7], 6)
+    assert got[5].get("native"), "the HIP sequence kernel did not run"
+    _close(got[0], ref[0], tol)                                  # h for all t
+    _close(got[1], ref[1], tol)
+    _close(got[2], ref[2], tol)
+    _close(got[3], ref[3], tol * 4)                              # dx
+    for k in ("W", "RW", "b"):
+        _close(got[4][k], ref[4][k], tol * 8)
+
+
+def test_lstm_native_in_network_fit(cuda):
+    """GravesLSTM char-model fit on the GPU goes through the sequence kernels and the score decreases."""
+    from deeplearning4j_amd.models import TextGenerationLSTM
+    net = TextGenerationLSTM(numLabels=32, inputShape=[1, 32], seed=3).init(device=cuda)
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randint(0, 32, (8, 40), generator=g)
+    x = torch.nn.functional.one_hot(idx, 32).permute(0, 2, 1).float()
+    y = torch.nn.functional.one_hot(torch.roll(idx, -1, 1), 32).permute(0, 2, 1).float()
+    lib = native.load()
+    assert hasattr(lib, "dl4j_lstm_fwd")
+    scores = []
+    for _ in range(15):
+        net.fit(x.to(cuda), y.to(cuda))
+        scores.append(net.score())
+    assert scores[-1] < scores[0]
