@@ -18,6 +18,7 @@ from ..conf.graph import LayerVertex
 from ..conf.layers import ActivationLayer, BatchNormalization
 from ..layers.output import BaseOutputLayerImpl
 from ..network_base import BaseNetwork
+from ... import profiling as _prof
 
 
 class ComputationGraph(BaseNetwork):
@@ -227,10 +228,13 @@ class ComputationGraph(BaseNetwork):
                 layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
                 if name in self._residual_of:
                     layer.residual = acts[self._residual_of[name]]
+                tok = _prof.layer_begin("fwd", name, layer) if _prof.ACTIVE else None
                 if stored_state and hasattr(layer, "tBpttStateMap"):
                     out = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
                 else:
                     out = layer.activate(x, train, mask)
+                if tok is not None:
+                    _prof.layer_end(tok, "fwd", name, layer, out)
                 acts[name] = out
                 amask[name], _ = layer.feedForwardMaskArray(mask, None, mb)
             elif name in self._passthrough:
@@ -279,7 +283,10 @@ class ComputationGraph(BaseNetwork):
             if isinstance(v, LayerVertex):
                 layer = self.layers_by_name.get(name)
                 if name in self.outputs and (isinstance(layer, BaseOutputLayerImpl) or hasattr(layer, "computeScore")):
+                    tok = _prof.layer_begin("bwd", name, layer) if _prof.ACTIVE else None
                     _, e = layer.backpropGradient(None)
+                    if tok is not None:
+                        _prof.layer_end(tok, "bwd", name, layer, e)
                     self._grad_ready(name)
                 else:
                     e_in = eps_acc.pop(name, None)
@@ -287,10 +294,13 @@ class ComputationGraph(BaseNetwork):
                         continue
                     if not self._need_input_grad[name] and layer.conf.numParams() == 0:
                         continue
+                    tok = _prof.layer_begin("bwd", name, layer) if _prof.ACTIVE else None
                     if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
                         _, e = layer.backpropGradient(e_in, tbptt_back=tbptt_back)
                     else:
                         _, e = layer.backpropGradient(e_in)
+                    if tok is not None:
+                        _prof.layer_end(tok, "bwd", name, layer, e)
                     self._grad_ready(name)
                     if name in self._residual_of:
                         add(self._residual_of[name], layer.dresidual)

@@ -12,6 +12,7 @@ from .conf.enums import BackpropType
 from .conf.layers import ActivationLayer, BatchNormalization
 from .layers.output import BaseOutputLayerImpl
 from .network_base import BaseNetwork
+from .. import profiling as _prof
 
 
 class MultiLayerNetwork(BaseNetwork):
@@ -102,10 +103,13 @@ class MultiLayerNetwork(BaseNetwork):
                 acts.append(x)
                 continue
             layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
+            tok = _prof.layer_begin("fwd", i, layer) if _prof.ACTIVE else None
             if stored_state and hasattr(layer, "tBpttStateMap"):
                 x = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
             else:
                 x = layer.activate(x, train, mask)
+            if tok is not None:
+                _prof.layer_end(tok, "fwd", i, layer, x)
             mask, _ = layer.feedForwardMaskArray(mask, None, mb)
             acts.append(x)
         return acts
@@ -144,7 +148,10 @@ class MultiLayerNetwork(BaseNetwork):
             raise ValueError("Cannot calculate gradient and score with respect to labels: final layer is not an "
                              "IOutputLayer")
         self._begin_backward()
+        tok = _prof.layer_begin("bwd", n - 1, out_layer) if _prof.ACTIVE else None
         _, eps = out_layer.backpropGradient(None)
+        if tok is not None:
+            _prof.layer_end(tok, "bwd", n - 1, out_layer, eps)
         self._grad_ready(n - 1)
         mb = self._mb
         for i in range(n - 2, -1, -1):
@@ -154,10 +161,13 @@ class MultiLayerNetwork(BaseNetwork):
             if i in self._fused_passthrough:
                 continue
             layer = self.layers[i]
+            tok = _prof.layer_begin("bwd", i, layer) if _prof.ACTIVE else None
             if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
                 _, eps = layer.backpropGradient(eps, tbptt_back=tbptt_back)
             else:
                 _, eps = layer.backpropGradient(eps)
+            if tok is not None:
+                _prof.layer_end(tok, "bwd", i, layer, eps)
             self._grad_ready(i)
             if eps is None:
                 break

@@ -17,6 +17,7 @@ from .conf.enums import DataType
 from .conf.weights import WeightInit, init_weights_
 from .updater import NetworkUpdater, build_entries
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
+from .. import profiling as _prof
 
 
 def default_device():
@@ -363,8 +364,10 @@ class BaseNetwork:
             self._score_val = None
             return
         if acc is not None:
-            acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
-        self._apply_update_kernels(batch_size)
+            with _prof.range_("allreduce_gradients", "collective", self.device):
+                acc.reduce_gradients(self)   # data-parallel all-reduce of the summed gradient (parallel/)
+        with _prof.range_("updater", "update", self.device):
+            self._apply_update_kernels(batch_size)
         self._bump_weight_version()
 
     def _apply_update_kernels(self, batch_size):

@@ -15,6 +15,13 @@ _SIGS = {
     "rt_threshold_decode": ([c_void_p, c_void_p, c_float], None),
     "rt_bitmap_encode": ([c_void_p, c_ll, c_float, c_void_p], c_int),
     "rt_bitmap_decode": ([c_void_p, c_void_p, c_float], None),
+    "rt_ws_create": ([c_ll, c_ll, c_ll, c_double, c_int, c_int, c_int], c_ll),
+    "rt_ws_destroy": ([c_ll], None),
+    "rt_ws_alloc": ([c_ll, c_ll, ctypes.POINTER(c_ll), ctypes.POINTER(c_ll)], c_int),
+    "rt_ws_cycle_end": ([c_ll], c_ll),
+    "rt_ws_set_capacity": ([c_ll, c_ll], c_int),
+    "rt_ws_generation": ([c_ll], c_ll),
+    "rt_ws_stats": ([c_ll, ctypes.POINTER(c_ll)], c_int),
 }
 
 

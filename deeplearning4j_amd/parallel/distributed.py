@@ -26,6 +26,8 @@ def init_distributed(backend=None, timeout_s=600):
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a failed/hung RCCL collective aborts the communicator and raises instead of hanging
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if backend is None:
             backend = "nccl" if device.type == "cuda" else "gloo"
         kw = {}

@@ -153,3 +153,44 @@ class Nd4j:
     @staticmethod
     def argMax(x, dim):
         return torch.argmax(x, dim=dim)
+
+    # ------------------------------------------------------------------ executioner / memory
+    @staticmethod
+    def getExecutioner():
+        from ..profiling import getExecutioner
+        return getExecutioner()
+
+    @staticmethod
+    def getWorkspaceManager():
+        from ..memory import getWorkspaceManager
+        return getWorkspaceManager()
+
+    @staticmethod
+    def getMemoryManager():
+        return _MemoryManager()
+
+
+class _MemoryManager:
+    """Nd4j.getMemoryManager(): memset / current workspace / device memory info."""
+
+    @staticmethod
+    def memset(t):
+        with torch.no_grad():
+            t.zero_()
+
+    @staticmethod
+    def getCurrentWorkspace():
+        from ..memory import getWorkspaceManager
+        return getWorkspaceManager().getCurrentWorkspace()
+
+    @staticmethod
+    def invokeGc():
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.empty_cache()
+
+    @staticmethod
+    def getDeviceMemoryInfo(device=0):
+        """(free, total) bytes of the device (hipMemGetInfo)."""
+        if not torch.cuda.is_available():
+            return (0, 0)
+        return torch.cuda.mem_get_info(device)
