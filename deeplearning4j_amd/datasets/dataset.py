@@ -102,19 +102,30 @@ class DataSet:
         bitmask byte (DataSet.save(File) layout idea: flags, then arrays)."""
         from ..utils import nd4j_io
         parts = [self.features, self.labels, self.featuresMask, self.labelsMask]
-        with open(path, "wb") as fh:
+
+        def _w(fh):
             fh.write(bytes([sum(1 << i for i, t in enumerate(parts) if t is not None)]))
             for t in parts:
                 if t is not None:
                     nd4j_io.write(t.detach().cpu(), fh)
+        if hasattr(path, "write"):
+            _w(path)
+        else:
+            with open(path, "wb") as fh:
+                _w(fh)
 
     @staticmethod
     def load(path):
+        """From a path or a binary stream."""
         from ..utils import nd4j_io
-        with open(path, "rb") as fh:
+
+        def _r(fh):
             flags = fh.read(1)[0]
-            parts = [nd4j_io.read(fh) if flags & (1 << i) else None for i in range(4)]
-        return DataSet(*parts)
+            return DataSet(*[nd4j_io.read(fh) if flags & (1 << i) else None for i in range(4)])
+        if hasattr(path, "read"):
+            return _r(path)
+        with open(path, "rb") as fh:
+            return _r(fh)
 
 
 class SplitTestAndTrain:

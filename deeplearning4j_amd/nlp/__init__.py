@@ -5,3 +5,6 @@ from .vocab import AbstractCache, Huffman, InMemoryLookupCache, SequenceElement,
 from .embeddings import EmbeddingEngine, InMemoryLookupTable, WordVectorsImpl  # noqa: F401
 from .word2vec import (CBOW, DBOW, DM, ParagraphVectors, ScoreListener, SequenceVectors, SerializingListener,  # noqa
                        SkipGram, VectorsConfiguration, VectorsListener, Word2Vec)
+from .tokenization_ext import (BertWordPieceTokenizerFactory, ChineseTokenizerFactory,  # noqa: F401
+                               JapaneseTokenizerFactory, KoreanTokenizerFactory, PorterStemmer, StemmingPreprocessor)
+from .distributed import DistributedWord2Vec, SparkWord2Vec  # noqa: F401

@@ -221,14 +221,20 @@ class VocabConstructor:
             for ls in labels_per_seq:
                 for l in ls:
                     labels.setdefault(l, None)
+        return self.buildFromCounts(counts, docs, ndocs, list(labels), cache, buildHuffman)
+
+    def buildFromCounts(self, counts, docs, ndocs, labels=(), cache=None, buildHuffman=True):
+        """Vocabulary from (merged) element counts / document counts — the reduce step of the distributed
+        text pipeline (dl4j-spark-nlp TextPipeline + WordFreqAccumulator)."""
+        cache = AbstractCache() if cache is None else cache
         labels = list(labels)
         lset = set(labels)
-        words = [w for w, c in counts.items() if c >= self.minFreq and w not in lset]
+        words = [w for w, c in counts.items() if c >= self.minFreq and w not in lset and w not in self.stop]
         dropped = sum(c for w, c in counts.items() if c < self.minFreq)
         words.sort(key=lambda w: (-counts[w], w))
         for w in words:
             e = VocabWord(w, counts[w])
-            e.sequencesCount = docs[w]
+            e.sequencesCount = docs.get(w, 0)
             cache.addToken(e)
         if self.useUnknown and dropped > 0:
             e = VocabWord(self.unk, dropped)

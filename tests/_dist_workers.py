@@ -94,3 +94,29 @@ def run_cluster(rank, world, port, master, result_path):
                     "score": score, "acc": float(ev.accuracy())}, result_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_w2v(rank, world, port, result_path):
+    """Distributed Word2Vec: each rank trains on its shard; the averaged tables must be identical on both ranks and
+    still separate the two topic clusters of the synthetic corpus."""
+    _setup(rank, world, port)
+    import numpy as np
+    from deeplearning4j_amd.nlp import CollectionSentenceIterator, Word2Vec
+    from deeplearning4j_amd.nlp.distributed import DistributedWord2Vec
+    rng = np.random.RandomState(3)
+    A = [f"alpha{i}" for i in range(10)]
+    B = [f"beta{i}" for i in range(10)]
+    corpus = [" ".join(rng.choice(A if k % 2 == 0 else B, 12)) for k in range(600)]
+    shard = corpus[rank::world]
+    w2v = Word2Vec.Builder().minWordFrequency(1).layerSize(24).windowSize(4).seed(7).epochs(3) \
+        .iterate(CollectionSentenceIterator(shard)).device("cpu").build()
+    DistributedWord2Vec(w2v).fit()
+    syn0 = w2v.lookupTable().getSyn0().clone()
+    gathered = [torch.empty_like(syn0) for _ in range(world)]
+    dist.all_gather(gathered, syn0)
+    if rank == 0:
+        same = all(torch.equal(gathered[0], g) for g in gathered[1:])
+        sim_in = w2v.similarity("alpha1", "alpha2")
+        sim_out = w2v.similarity("alpha1", "beta2")
+        torch.save({"same": same, "in": sim_in, "out": sim_out, "n": w2v.vocab().numWords()}, result_path)
+    dist.destroy_process_group()
