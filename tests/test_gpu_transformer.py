@@ -1,0 +1,66 @@
+"""Transformer HIP kernels vs plain-torch fp32 references: flash-style attention forward/backward
+(csrc/attention.hip) and LayerNorm (+ fused residual) forward/backward (csrc/layernorm.hip)."""
+import pytest
+import torch
+
+from deeplearning4j_amd.ops import transformer_native as TN
+
+pytestmark = pytest.mark.gpu
+
+
+def _err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return (a - b).abs().max().item() / max(1.0, b.abs().max().item())
+
+
+@pytest.mark.parametrize("B,T,H,D", [(2, 64, 2, 64), (3, 77, 4, 64), (2, 200, 2, 128), (1, 512, 12, 64)])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_fwd_bwd_matches_reference(cuda, B, T, H, D, masked, causal):
+    g = torch.Generator().manual_seed(B * 1000 + T + D)
+    qkv = (torch.randn(B, T, 3 * H * D, generator=g) * 0.8).to(torch.bfloat16)
+    mask = None
+    if masked:
+        lens = torch.randint(T // 2, T + 1, (B,), generator=g)
+        mask = (torch.arange(T).reshape(1, T) < lens.reshape(B, 1)).float()
+    dout = torch.randn(B, T, H * D, generator=g).to(torch.bfloat16)
+    # reference (fp32 autograd on the bf16-rounded inputs)
+    qr = qkv.float().requires_grad_(True)
+    o_ref = TN.attention_reference(qr, H, mask, causal)
+    o_ref.backward(dout.float())
+    qd = qkv.to(cuda)
+    md = mask.to(cuda) if mask is not None else None
+    out, lse = TN.attn_fwd(qd, H, md, causal)
+    keep = torch.ones(B, T, 1)
+    assert _err(out.cpu() * keep, o_ref.detach() * keep) < 2e-2
+    dqkv = TN.attn_bwd(qd, out, lse, dout.to(cuda), H, md, causal)
+    E = H * D
+    for name, sl in (("dQ", slice(0, E)), ("dK", slice(E, 2 * E)), ("dV", slice(2 * E, 3 * E))):
+        e = _err(dqkv[..., sl].cpu(), qr.grad[..., sl])
+        assert e < 3e-2, (name, e)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("M,N", [(5, 64), (1000, 768), (37, 1032), (64, 4096)])
+@pytest.mark.parametrize("res", [False, True])
+def test_layernorm_fwd_bwd_matches_reference(cuda, dtype, tol, M, N, res):
+    g = torch.Generator().manual_seed(M + N)
+    x = (torch.randn(M, N, generator=g) * 2 + 0.5).to(dtype)
+    r = torch.randn(M, N, generator=g).to(dtype) if res else None
+    gamma = torch.rand(N, generator=g) + 0.5
+    beta = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g).to(dtype)
+    xr = x.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    s = xr + rr if res else xr
+    y_ref = torch.nn.functional.layer_norm(s, (N,), gr, br, 1e-12)
+    y_ref.backward(dy.float())
+    y, mean, rstd = TN.ln_fwd(x.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, r.to(cuda) if res else None)
+    assert _err(y, y_ref.detach()) < tol * 4
+    dx, dg, db = TN.ln_bwd(dy.to(cuda), x.to(cuda), gamma.to(cuda), mean, rstd, r.to(cuda) if res else None)
+    assert _err(dx, xr.grad) < tol * 8
+    if res:
+        assert _err(dx, rr.grad) < tol * 8
+    assert _err(dg, gr.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
+    assert _err(db, br.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
