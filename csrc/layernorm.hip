@@ -146,15 +146,28 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
-// out[0/1][N] = sum over P partial rows
+// out[0/1][N] = sum over P partial rows. Block = 32 columns x 8 row groups (coalesced 128-byte row reads), the 8
+// group sums combined through LDS.
 __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int P, int N,
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * N) return;
-  const int which = j / N, col = j - which * N;
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + cl;                          // over the concatenated [dgamma | dbeta] columns
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long long)p * 2 * N + which * N + col];
-  (which == 0 ? dgamma : dbeta)[col] = s;
+  if (j < 2 * N) {
+    const int which = j / N, col = j - which * N;
+    const float* src = part + which * N + col;
+    for (int p = rg; p < P; p += 8) s += src[(long long)p * 2 * N];
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && j < 2 * N) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][cl];
+    const int which = j / N, col = j - which * N;
+    (which == 0 ? dgamma : dbeta)[col] = t;
+  }
 }
 
 template <typename T, int CH>
@@ -185,7 +198,7 @@ static int bwd_l(const void* dy, const void* x, const void* r, const float* g, c
     hipLaunchKernelGGL((ln_bwd_kernel<T, CH, false, kRPW>), dim3((unsigned)blocks), dim3(256), 0, s, (const T*)dy,
                        (const T*)x, (const T*)nullptr, g, mean, rstd, (T*)dx, part, M, N);
   const int P = (int)(blocks * 4);
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * N + 255) / 256), dim3(256), 0, s, part, P, N, dgamma, dbeta);
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * N + 31) / 32), dim3(256), 0, s, part, P, N, dgamma, dbeta);
   return (int)hipGetLastError();
 }
 

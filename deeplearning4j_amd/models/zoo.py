@@ -704,3 +704,45 @@ ZOO = {"ResNet50": ResNet50, "LeNet": LeNet, "SimpleCNN": SimpleCNN, "TextGenera
        "AlexNet": AlexNet, "VGG16": VGG16, "VGG19": VGG19, "Darknet19": Darknet19, "GoogLeNet": GoogLeNet,
        "TinyYOLO": TinyYOLO, "YOLO2": YOLO2, "FaceNetNN4Small2": FaceNetNN4Small2,
        "InceptionResNetV1": InceptionResNetV1}
+
+
+# ------------------------------------------------------------------------------------------------ BertBase
+class BertBase(ZooModel):
+    """BERT encoder + [CLS] pooler + softmax classifier (BASELINE.json's BERT-base config; new relative to the
+    reference zoo). Defaults are BERT-base: 12 layers, hidden 768, 12 heads, FFN 3072, vocab 30522, 512 positions,
+    N(0, 0.02) init, Adam(2e-5). ``inputShape = [seqLen]``; input = token ids [mb, seqLen] (featuresMask [mb, T]
+    marks real tokens)."""
+    DEFAULT_SHAPE = [128]
+
+    def __init__(self, numLabels=2, seed=123, inputShape=None, vocabSize=30522, hidden=768, layers=12, heads=12,
+                 ffn=3072, maxPositions=512, learningRate=2e-5, **kw):
+        super().__init__(numLabels, seed, inputShape, **kw)
+        self.vocabSize, self.hidden, self.layers, self.heads = vocabSize, hidden, layers, heads
+        self.ffn, self.maxPositions, self.learningRate = ffn, maxPositions, learningRate
+
+    def graphBuilder(self):
+        from ..nn.conf import BertEmbeddingLayer, BertPoolerLayer, TransformerEncoderLayer
+        T = self.inputShape[0]
+        g = (self._builder().updater(Adam(self.learningRate)).weightInit(NormalDistribution(0.0, 0.02))
+             .graphBuilder())
+        g.addInputs("tokens")
+        g.addLayer("embeddings", BertEmbeddingLayer.Builder().nIn(self.vocabSize).nOut(self.hidden)
+                   .maxPositions(self.maxPositions).inputLength(T).build(), "tokens")
+        prev = "embeddings"
+        for i in range(self.layers):
+            g.addLayer(f"encoder_{i}", TransformerEncoderLayer.Builder().nIn(self.hidden).nOut(self.hidden)
+                       .nHeads(self.heads).ffnSize(self.ffn).build(), prev)
+            prev = f"encoder_{i}"
+        g.addLayer("pooler", BertPoolerLayer.Builder().nIn(self.hidden).nOut(self.hidden).build(), prev)
+        g.addLayer("classifier", OutputLayer.Builder(LossFunction.MCXENT).activation(Activation.SOFTMAX)
+                   .nIn(self.hidden).nOut(self.numLabels).build(), "pooler")
+        g.setOutputs("classifier")
+        return g
+
+    def conf(self):
+        return self.graphBuilder().build()
+
+    def init(self, device=None):
+        net = ComputationGraph(self.conf())
+        net.init(device=device)
+        return net

@@ -1280,3 +1280,80 @@ class SelfAttentionLayer(FeedForwardLayer):
 
     def is_bias(self, key):
         return key.startswith("b")
+
+
+# ------------------------------------------------------------------------------------------------ transformer
+class TransformerEncoderLayer(FeedForwardLayer):
+    """One post-LN transformer encoder block (BERT): fused QKV projection -> multi-head attention (flash-style HIP
+    kernel) -> output projection -> LayerNorm(+residual) -> FFN (GELU) -> LayerNorm(+residual). RNN-format
+    input/output [mb, nIn, T] (new: BERT-base config of BASELINE.json; not in the reference)."""
+    FIELDS = {"nHeads": 12, "ffnSize": 3072, "layerNormEps": 1e-12, "causal": False, "hiddenDropout": 0.0}
+    RUNTIME = "deeplearning4j_amd.nn.layers.transformer:TransformerEncoderLayerImpl"
+
+    def getOutputType(self, layerIndex, inputType):
+        T = inputType.timeSeriesLength if isinstance(inputType, InputTypeRecurrent) else -1
+        return InputType.recurrent(self.nOut, T)
+
+    def setNIn(self, inputType, override=False):
+        if self.nIn and not override:
+            return
+        self.nIn = inputType.size
+        self.nOut = self.nIn
+
+    def getPreProcessorForInputType(self, inputType):
+        return None
+
+    def param_specs(self):
+        E, F = self.nIn, self.ffnSize
+        return [ParamSpec("Wqkv", [E, 3 * E], "c", "weight", E, E), ParamSpec("bqkv", [1, 3 * E], "c", "bias"),
+                ParamSpec("Wo", [E, E], "c", "weight", E, E), ParamSpec("bo", [1, E], "c", "bias"),
+                ParamSpec("ln1g", [1, E], "c", "const", value=1.0), ParamSpec("ln1b", [1, E], "c", "const", value=0.0),
+                ParamSpec("W1", [E, F], "c", "weight", E, F), ParamSpec("b1", [1, F], "c", "bias"),
+                ParamSpec("W2", [F, E], "c", "weight", F, E), ParamSpec("b2", [1, E], "c", "bias"),
+                ParamSpec("ln2g", [1, E], "c", "const", value=1.0), ParamSpec("ln2b", [1, E], "c", "const", value=0.0)]
+
+    def is_bias(self, key):
+        return key.startswith("b") or key in ("ln1b", "ln2b")
+
+
+class BertEmbeddingLayer(FeedForwardLayer):
+    """Token ids [mb, T] -> LayerNorm(word + position + token-type(0) embeddings) as [mb, nOut, T]
+    (nIn = vocabulary size)."""
+    FIELDS = {"maxPositions": 512, "typeVocabSize": 2, "layerNormEps": 1e-12, "inputLength": -1}
+    RUNTIME = "deeplearning4j_amd.nn.layers.transformer:BertEmbeddingLayerImpl"
+
+    def getOutputType(self, layerIndex, inputType):
+        return InputType.recurrent(self.nOut, self.inputLength)
+
+    def setNIn(self, inputType, override=False):
+        return
+
+    def getPreProcessorForInputType(self, inputType):
+        return None
+
+    def param_specs(self):
+        E = self.nOut
+        return [ParamSpec("Wword", [self.nIn, E], "c", "weight", self.nIn, E),
+                ParamSpec("Wpos", [self.maxPositions, E], "c", "weight", self.maxPositions, E),
+                ParamSpec("Wtype", [self.typeVocabSize, E], "c", "weight", self.typeVocabSize, E),
+                ParamSpec("lng", [1, E], "c", "const", value=1.0), ParamSpec("lnb", [1, E], "c", "const", value=0.0)]
+
+    def is_bias(self, key):
+        return key == "lnb"
+
+
+class BertPoolerLayer(FeedForwardLayer):
+    """First ([CLS]) time step of [mb, nIn, T] -> tanh(x W + b) as [mb, nOut]."""
+    RUNTIME = "deeplearning4j_amd.nn.layers.transformer:BertPoolerLayerImpl"
+
+    def setNIn(self, inputType, override=False):
+        if self.nIn and not override:
+            return
+        self.nIn = inputType.size
+
+    def getPreProcessorForInputType(self, inputType):
+        return None
+
+    def param_specs(self):
+        return [ParamSpec("W", [self.nIn, self.nOut], "c", "weight", self.nIn, self.nOut),
+                ParamSpec("b", [1, self.nOut], "c", "bias")]

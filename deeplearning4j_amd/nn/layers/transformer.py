@@ -1,0 +1,253 @@
+"""Transformer runtime layers: BERT embeddings, post-LN encoder block, [CLS] pooler.
+
+Not in the reference snapshot (no attention or LayerNorm there); they implement the BERT-base
+config of BASELINE.json on the same layer SPI (activate / backpropGradient writing into flat gradient views).
+
+MI355X structure of one encoder block (token-major [B*T, E] activations, bf16 compute, fp32 master weights):
+  qkv = x·Wqkv + b          one fused projection GEMM (hipBLASLt)
+  ctx = attention(qkv)      flash-style HIP kernel reading Q/K/V in place (csrc/attention.hip)
+  h1  = LN(ctx·Wo + bo + x) output GEMM + LayerNorm-with-residual HIP kernel (csrc/layernorm.hip)
+  h2  = LN(gelu(h1·W1 + b1)·W2 + b2 + h1)
+The backward is written out by hand (no autograd): GEMMs produce fp32 weight gradients straight into the flat
+gradient views, attention/LN backward are the matching HIP kernels, and the residual gradients are summed in
+place. Activations cross layer boundaries as [mb, E, T] *views* of token-major memory, so stacking blocks costs
+no transposes. On CPU (and fp64 gradient checks) the same math runs on plain torch ops.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from .base import LayerImpl, copy_grad_
+
+
+def _native(x, op):
+    return x.is_cuda and x.dtype == torch.bfloat16 and ops.use_native(x, op)
+
+
+def _wgrad(view, a, b):
+    """view <- aᵀ·b. bf16 operands accumulate in fp32 and the GEMM writes the fp32 gradient view directly."""
+    if a.is_cuda and a.dtype == torch.bfloat16 and view.is_contiguous() and view.dtype == torch.float32:
+        try:
+            torch.mm(a.t(), b, out_dtype=torch.float32, out=view.view(a.shape[1], b.shape[1]))
+            return
+        except (RuntimeError, TypeError):
+            pass
+    copy_grad_(view, (a.t() @ b).to(view.dtype))
+
+
+def _bsum(view, d):
+    """view <- column sums of d, accumulated in the view's precision without a converted copy of d."""
+    if view.is_contiguous():
+        torch.sum(d, 0, dtype=view.dtype, out=view.view(-1))
+    else:
+        copy_grad_(view, d.sum(0, dtype=view.dtype))
+
+
+def _gelu_fwd(z):
+    if _native(z, "gelu"):
+        from ...ops import transformer_native as TN
+        r = TN.gelu(z)
+        if r is not None:
+            return r
+    return F.gelu(z)
+
+
+def _gelu_bwd(z, dy):
+    if _native(z, "gelu"):
+        from ...ops import transformer_native as TN
+        r = TN.gelu(z, dy.to(z.dtype).contiguous())
+        if r is not None:
+            return r
+    zf = z.float() if z.dtype != torch.float64 else z
+    cdf = 0.5 * (1.0 + torch.erf(zf * (1.0 / math.sqrt(2.0))))
+    pdf = torch.exp(-0.5 * zf * zf) * (1.0 / math.sqrt(2.0 * math.pi))
+    return (dy.to(zf.dtype) * (cdf + zf * pdf)).to(z.dtype)
+
+
+# ------------------------------------------------------------------------------------------------ LN helpers
+def _ln_fwd(x, res, g, b, eps):
+    if _native(x, "layernorm"):
+        from ...ops import transformer_native as TN
+        r = TN.ln_fwd(x, g, b, eps, res)
+        if r is not None:
+            y, mean, rstd = r
+            return y, ("native", mean, rstd)
+    s = x if res is None else x + res
+    sf = s.float() if s.dtype != torch.float64 else s
+    mean = sf.mean(-1, keepdim=True)
+    rstd = torch.rsqrt(sf.var(-1, unbiased=False, keepdim=True) + eps)
+    xhat = (sf - mean) * rstd
+    y = xhat * g.reshape(-1).to(sf.dtype) + b.reshape(-1).to(sf.dtype)
+    return y.to(x.dtype), ("torch", xhat, rstd)
+
+
+def _ln_bwd(dy, x, res, g, ctx, gview=None, bview=None):
+    """-> ds (gradient of x and of res); dgamma / dbeta land in the gradient views."""
+    if ctx[0] == "native":
+        from ...ops import transformer_native as TN
+        ds, dg, db = TN.ln_bwd(dy, x, g, ctx[1], ctx[2], res, gview, bview)
+        if dg.data_ptr() != gview.data_ptr():
+            copy_grad_(gview, dg)
+        if db.data_ptr() != bview.data_ptr():
+            copy_grad_(bview, db)
+        return ds
+    _, xhat, rstd = ctx
+    d = dy.to(xhat.dtype)
+    dg = (d * xhat).sum(0)
+    db = d.sum(0)
+    dxh = d * g.reshape(-1).to(xhat.dtype)
+    ds = rstd * (dxh - dxh.mean(-1, keepdim=True) - xhat * (dxh * xhat).mean(-1, keepdim=True))
+    copy_grad_(gview, dg)
+    copy_grad_(bview, db)
+    return ds.to(x.dtype)
+
+
+# ------------------------------------------------------------------------------------------------ attention
+def _attn_fwd(qkv, B, T, H, mask, causal):
+    if _native(qkv, "attention"):
+        from ...ops import transformer_native as TN
+        q3 = qkv.reshape(B, T, -1)
+        if TN.attn_supported(q3, H):
+            out, lse = TN.attn_fwd(q3, H, mask, causal)
+            return out.reshape(B * T, -1), ("native", out, lse)
+    from ...ops.transformer_native import attention_reference
+    with torch.enable_grad():
+        q = qkv.detach().reshape(B, T, -1).requires_grad_(True)
+        o = attention_reference(q, H, mask, causal).to(qkv.dtype)
+    return o.detach().reshape(B * T, -1), ("torch", q, o)
+
+
+def _attn_bwd(dctx, qkv, B, T, H, mask, causal, ctx):
+    if ctx[0] == "native":
+        from ...ops import transformer_native as TN
+        return TN.attn_bwd(qkv.reshape(B, T, -1), ctx[1], ctx[2], dctx.reshape(B, T, -1), H, mask,
+                           causal).reshape(B * T, -1)
+    _, q, o = ctx
+    (g,) = torch.autograd.grad(o, [q], dctx.reshape(o.shape).to(o.dtype))
+    return g.reshape(B * T, -1)
+
+
+def _token_major(x):
+    """[mb, E, T] (possibly a permuted view of token-major memory) -> contiguous [mb*T, E] (no copy when it is)."""
+    mb, E, T = x.shape
+    return x.permute(0, 2, 1).reshape(mb * T, E)
+
+
+class TransformerEncoderLayerImpl(LayerImpl):
+    def type(self):
+        return "RECURRENT"
+
+    def activate(self, x, training=False, mask=None, **kw):
+        c = self.conf
+        self.training = training
+        B, E, T = x.shape
+        H = c.nHeads
+        dt = self.W("Wqkv").dtype
+        xt = _token_major(x).to(dt)
+        m = mask.reshape(B, T) if mask is not None else None
+        qkv = torch.addmm(self.W("bqkv").reshape(-1), xt, self.W("Wqkv"))
+        ctx, actx = _attn_fwd(qkv, B, T, H, m, c.causal)
+        a = torch.addmm(self.W("bo").reshape(-1), ctx, self.W("Wo"))
+        h1, ln1 = _ln_fwd(a, xt, self.params["ln1g"], self.params["ln1b"], c.layerNormEps)
+        z1 = torch.addmm(self.W("b1").reshape(-1), h1, self.W("W1"))
+        f = _gelu_fwd(z1)
+        f2 = torch.addmm(self.W("b2").reshape(-1), f, self.W("W2"))
+        y, ln2 = _ln_fwd(f2, h1, self.params["ln2g"], self.params["ln2b"], c.layerNormEps)
+        self.maskArray = mask
+        if training:
+            self._c = (xt, qkv, actx, ctx, a, ln1, h1, z1, f, f2, ln2, B, T, m)
+        self.input = x
+        return y.reshape(B, T, E).permute(0, 2, 1)
+
+    def backpropGradient(self, eps, **kw):
+        c = self.conf
+        xt, qkv, actx, ctx, a, ln1, h1, z1, f, f2, ln2, B, T, m = self._c
+        self._c = None
+        g = self.grads
+        dt = xt.dtype
+        dy = _token_major(eps).to(dt)
+        ds2 = _ln_bwd(dy, f2, h1, self.params["ln2g"], ln2, g["ln2g"], g["ln2b"])
+        _wgrad(g["W2"], f, ds2)
+        _bsum(g["b2"], ds2)
+        dz1 = _gelu_bwd(z1, ds2 @ self.W("W2").t())
+        _wgrad(g["W1"], h1, dz1)
+        _bsum(g["b1"], dz1)
+        dh1 = torch.addmm(ds2, dz1, self.W("W1").t())
+        ds1 = _ln_bwd(dh1, a, xt, self.params["ln1g"], ln1, g["ln1g"], g["ln1b"])
+        _wgrad(g["Wo"], ctx, ds1)
+        _bsum(g["bo"], ds1)
+        dctx = ds1 @ self.W("Wo").t()
+        dqkv = _attn_bwd(dctx, qkv, B, T, c.nHeads, m, c.causal, actx)
+        _wgrad(g["Wqkv"], xt, dqkv)
+        _bsum(g["bqkv"], dqkv)
+        dx = torch.addmm(ds1, dqkv, self.W("Wqkv").t())
+        E = dx.shape[1]
+        return self.make_gradient(), dx.reshape(B, T, E).permute(0, 2, 1)
+
+
+class BertEmbeddingLayerImpl(LayerImpl):
+    def type(self):
+        return "RECURRENT"
+
+    def activate(self, x, training=False, mask=None, **kw):
+        c = self.conf
+        if x.dim() == 3:
+            x = x[:, 0, :]
+        idx = x.long()
+        B, T = idx.shape
+        dt = self.W("Wword").dtype
+        e = self.W("Wword")[idx.reshape(-1)] + self.W("Wpos")[:T].repeat(B, 1) + self.W("Wtype")[0].reshape(1, -1)
+        y, ln = _ln_fwd(e.to(dt).contiguous(), None, self.params["lng"], self.params["lnb"], c.layerNormEps)
+        if training:
+            self._c = (idx, e.to(dt).contiguous(), ln, B, T)
+        return y.reshape(B, T, -1).permute(0, 2, 1)
+
+    def backpropGradient(self, eps, **kw):
+        idx, e, ln, B, T = self._c
+        self._c = None
+        dy = _token_major(eps).to(e.dtype)
+        g = self.grads
+        de = _ln_bwd(dy, e, None, self.params["lng"], ln, g["lng"], g["lnb"])
+        de = de.to(g["Wword"].dtype)
+        if getattr(self.net, "_grads_zeroed", False) and g["Wword"].is_contiguous():
+            g["Wword"].index_add_(0, idx.reshape(-1), de)          # flat gradient already cleared this step
+        else:
+            gw = torch.zeros_like(g["Wword"])
+            gw.index_add_(0, idx.reshape(-1), de)
+            copy_grad_(g["Wword"], gw)
+        copy_grad_(g["Wpos"][:T], de.reshape(B, T, -1).sum(0).to(g["Wpos"].dtype))
+        if g["Wpos"].shape[0] > T:
+            g["Wpos"][T:].zero_()
+        gt = torch.zeros_like(g["Wtype"])
+        gt[0] = de.sum(0)
+        copy_grad_(g["Wtype"], gt)
+        return self.make_gradient(), None
+
+    def feedForwardMaskArray(self, mask, state, mb):
+        self.maskArray = mask
+        return mask, state
+
+
+class BertPoolerLayerImpl(LayerImpl):
+    def activate(self, x, training=False, mask=None, **kw):
+        self.input = x
+        x0 = x[:, :, 0].to(self.W("W").dtype)
+        y = torch.tanh(torch.addmm(self.W("b").reshape(-1), x0, self.W("W")))
+        if training:
+            self._c = (x0, y, x.shape)
+        return y
+
+    def backpropGradient(self, eps, **kw):
+        x0, y, shape = self._c
+        self._c = None
+        dz = (eps.to(y.dtype) * (1 - y * y))
+        _wgrad(self.grads["W"], x0, dz)
+        _bsum(self.grads["b"], dz)
+        dx = torch.zeros(shape, dtype=x0.dtype, device=x0.device)
+        dx[:, :, 0] = dz @ self.W("W").t()
+        return self.make_gradient(), dx
+
+    def feedForwardMaskArray(self, mask, state, mb):
+        return None, state

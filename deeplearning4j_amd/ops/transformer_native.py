@@ -92,7 +92,8 @@ def attention_reference(qkv, H, mask=None, causal=False, scale=None):
     E = E3 // 3
     D = E // H
     scale = scale if scale is not None else D ** -0.5
-    q, k, v = qkv.float().reshape(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
+    cd = torch.float64 if qkv.dtype == torch.float64 else torch.float32
+    q, k, v = qkv.to(cd).reshape(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
     s = (q @ k.transpose(-1, -2)) * scale
     keep = torch.ones(B, 1, T, T, dtype=torch.bool, device=qkv.device)
     if mask is not None:
@@ -132,16 +133,18 @@ def ln_fwd(x, gamma, beta, eps, residual=None):
     return y, mean, rstd
 
 
-def ln_bwd(dy, x, gamma, mean, rstd, residual=None):
-    """-> (dx [M, N] (also the residual's gradient), dgamma [N] fp32, dbeta [N] fp32)."""
+def ln_bwd(dy, x, gamma, mean, rstd, residual=None, dgamma_out=None, dbeta_out=None):
+    """-> (dx [M, N] (also the residual's gradient), dgamma [N] fp32, dbeta [N] fp32). ``dgamma_out`` /
+    ``dbeta_out``: contiguous fp32 views (e.g. the flat gradient) the kernel writes directly."""
     N = x.shape[-1]
     M = x.numel() // N
     lib = _lib()
     P = lib.dl4j_ln_partial_rows(M)
     part = torch.empty(P * 2 * N, device=x.device, dtype=torch.float32)
     dx = torch.empty_like(x)
-    dg = torch.empty(N, device=x.device, dtype=torch.float32)
-    db = torch.empty(N, device=x.device, dtype=torch.float32)
+    ok = lambda t: t is not None and t.is_contiguous() and t.dtype == torch.float32 and t.numel() == N  # noqa: E731
+    dg = dgamma_out.view(-1) if ok(dgamma_out) else torch.empty(N, device=x.device, dtype=torch.float32)
+    db = dbeta_out.view(-1) if ok(dbeta_out) else torch.empty(N, device=x.device, dtype=torch.float32)
     g = gamma.reshape(-1).to(torch.float32).contiguous()
     r = None if residual is None else residual.to(x.dtype).contiguous()
     rc = lib.dl4j_ln_bwd(_dt(x), _ptr(dy.to(x.dtype).contiguous()), _ptr(x), _ptr(r), _ptr(g), _ptr(mean), _ptr(rstd),
@@ -151,3 +154,18 @@ def ln_bwd(dy, x, gamma, mean, rstd, residual=None):
     _check(rc, "ln_bwd")
     return dx, dg, db
 
+
+
+# ------------------------------------------------------------------------------------------------ GELU
+def gelu(z, dy=None):
+    """Exact GELU (dy None) or its backward dy * gelu'(z) on the fused HIP kernel; None if unsupported."""
+    native.register_sig("dl4j_gelu", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_void_p])
+    d = _dt(z)
+    if d is None or not z.is_contiguous() or (dy is not None and (dy.dtype != z.dtype or not dy.is_contiguous())):
+        return None
+    out = torch.empty_like(z)
+    rc = native.load().dl4j_gelu(d, _ptr(z), _ptr(dy), _ptr(out), z.numel(), c_void_p(_stream()))
+    if rc == -1:
+        return None
+    _check(rc, "gelu")
+    return out

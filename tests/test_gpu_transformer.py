@@ -64,3 +64,27 @@ def test_layernorm_fwd_bwd_matches_reference(cuda, dtype, tol, M, N, res):
         assert _err(dx, rr.grad) < tol * 8
     assert _err(dg, gr.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
     assert _err(db, br.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
+
+
+def test_bert_block_gpu_bf16_matches_cpu_fp32(cuda):
+    """Encoder stack on the GPU (bf16 + flash-attention / LayerNorm kernels) vs the same weights on the CPU fp32
+    reference path: outputs and parameter gradients."""
+    from deeplearning4j_amd.models import BertBase
+    from deeplearning4j_amd.nn.conf import DataType
+    kw = dict(numLabels=3, inputShape=[40], vocabSize=97, hidden=128, layers=2, heads=2, ffn=256, maxPositions=64)
+    ref = BertBase(**kw).init(device="cpu")
+    gpu = BertBase(dataType=DataType.BFLOAT16, **kw).init(device=cuda)
+    gpu.setParams(ref.params().to(cuda))
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 97, (6, 40), generator=g)
+    y = torch.nn.functional.one_hot(torch.randint(0, 3, (6,), generator=g), 3).float()
+    m = torch.ones(6, 40)
+    m[2, 25:] = 0
+    out_r = ref.output(x, masks=[m])[0]
+    out_g = gpu.output(x.to(cuda), masks=[m.to(cuda)])[0]
+    assert _err(out_g, out_r) < 3e-2
+    ref.computeGradientAndScore([x], [y], [m])
+    gpu.computeGradientAndScore([x.to(cuda)], [y.to(cuda)], [m.to(cuda)])
+    gr, gg = ref.getGradientsViewArray().reshape(-1), gpu.getGradientsViewArray().reshape(-1).cpu()
+    rel = (gg - gr).norm() / gr.norm()
+    assert rel < 5e-2, rel
