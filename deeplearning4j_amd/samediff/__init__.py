@@ -136,11 +136,33 @@ class _NN:
         return self.sd._new(name, out)
 
     def layerNorm(self, name, x, gain=None, bias=None, eps=1e-5):
+        """LayerNorm over the last dim (LayerNorm HIP kernels on the GPU)."""
         if isinstance(name, SDVariable):
             name, x, gain, bias = None, name, x, gain
-        out = F.layer_norm(x.value, x.value.shape[-1:], gain.value.reshape(-1) if gain is not None else None,
-                           bias.value.reshape(-1) if bias is not None else None, eps)
+        from .native_ops import layer_norm
+        out = layer_norm(x.value, gain.value if gain is not None else None, bias.value if bias is not None else None,
+                         eps)
         return self.sd._new(name, out)
+
+    def fusedSelfAttention(self, name, qkv, nHeads, mask=None, causal=False):
+        """Multi-head self attention on a fused projection qkv [B, T, 3E] -> [B, T, E] (flash-attention kernel)."""
+        if isinstance(name, SDVariable):
+            name, qkv, nHeads = None, name, qkv
+        from .native_ops import self_attention
+        m = mask.value if isinstance(mask, SDVariable) else mask
+        return self.sd._new(name, self_attention(qkv.value, nHeads, m, causal))
+
+
+class _RNN:
+    def __init__(self, sd):
+        self.sd = sd
+
+    def lstmLayer(self, name, x, W, RW, b, h0=None, c0=None, peephole=False):
+        """Whole-sequence LSTM (DL4J gate order, tanh/sigmoid): x [mb, nIn, T] -> [mb, H, T]. Runs the fused
+        sequence HIP kernels on the GPU (csrc/lstm.hip); RW has 3 extra peephole columns when ``peephole``."""
+        from .native_ops import lstm_layer
+        v = lambda t: None if t is None else t.value  # noqa: E731
+        return self.sd._new(name, lstm_layer(x.value, W.value, RW.value, b.value, v(h0), v(c0), peephole))
 
 
 class _CNN:
@@ -198,6 +220,9 @@ class SameDiff:
 
     def cnn(self):
         return _CNN(self)
+
+    def rnn(self):
+        return _RNN(self)
 
     # common ops in the reference's sd.xxx(name, ...) form
     def mmul(self, name, a, b=None):

@@ -77,3 +77,25 @@ def test_lstm_native_in_network_fit(cuda):
         net.fit(x.to(cuda), y.to(cuda))
         scores.append(net.score())
     assert scores[-1] < scores[0]
+
+
+@pytest.mark.parametrize("peep", [False, True])
+def test_samediff_lstm_layer_gpu_matches_cpu(cuda, peep):
+    """SameDiff lstmLayer: the GPU path (sequence kernels under autograd) vs the CPU reference, values and grads."""
+    from deeplearning4j_amd.samediff import SameDiff
+    g = torch.Generator().manual_seed(5)
+    mb, nIn, T, H = 19, 12, 9, 64
+    base = {"x": torch.randn(mb, nIn, T, generator=g), "W": torch.randn(nIn, 4 * H, generator=g) * 0.3,
+            "RW": torch.randn(H, 4 * H + (3 if peep else 0), generator=g) * 0.1, "b": torch.randn(4 * H, generator=g) * 0.1}
+    res = {}
+    for dev in ("cpu", cuda):
+        sd = SameDiff.create()
+        vs = {k: sd.var(k, v.clone().to(dev).requires_grad_(True)) for k, v in base.items()}
+        h = sd.rnn().lstmLayer("h", vs["x"], vs["W"], vs["RW"], vs["b"], peephole=peep)
+        loss = sd._new("loss", (h.value * torch.linspace(-1, 1, T, device=h.value.device)).sum())
+        grads = sd.execBackwards(loss, list(vs.values()))
+        res[str(dev)] = (h.value.detach().cpu(), {k: v.cpu() for k, v in grads.items()})
+    (hc, gc), (hg, gg) = res["cpu"], res[str(cuda)]
+    _close(hg, hc, 1e-4)
+    for k in base:
+        _close(gg[k], gc[k], 1e-3)

@@ -230,3 +230,27 @@ def test_conv_bias_deferred_into_batchnorm(monkeypatch):
     oa = oa[0] if isinstance(oa, list) else oa
     ob = ob[0] if isinstance(ob, list) else ob
     torch.testing.assert_close(oa, ob, rtol=1e-5, atol=1e-6)
+
+
+def test_samediff_native_ops_cpu_reference():
+    """SameDiff lstmLayer / layerNorm / fusedSelfAttention (CPU reference path) agree with the layer runtimes."""
+    from deeplearning4j_amd.nn.conf.activations import ActivationSigmoid, ActivationTanH
+    from deeplearning4j_amd.nn.layers import recurrent as R
+    from deeplearning4j_amd.samediff import SameDiff
+    g = torch.Generator().manual_seed(0)
+    mb, nIn, T, H = 3, 5, 7, 8
+    x = torch.randn(mb, nIn, T, generator=g, dtype=torch.float64)
+    W = torch.randn(nIn, 4 * H, generator=g, dtype=torch.float64) * 0.4
+    RW = torch.randn(H, 4 * H + 3, generator=g, dtype=torch.float64) * 0.4
+    b = torch.randn(4 * H, generator=g, dtype=torch.float64) * 0.1
+    sd = SameDiff.create()
+    out = sd.rnn().lstmLayer("h", sd.var("x", x), sd.var("W", W), sd.var("RW", RW), sd.var("b", b), peephole=True)
+    ref, _, _ = R._lstm_fwd(x, W, RW, b, None, None, H, True, ActivationTanH(), ActivationSigmoid(), None, False)
+    assert torch.allclose(out.value, ref, atol=1e-10)
+    e = torch.randn(4, 6, 16, generator=g, dtype=torch.float64)
+    ln = sd.nn().layerNorm("ln", sd.var("e", e), sd.var("g", torch.ones(16, dtype=torch.float64)),
+                           sd.var("bb", torch.zeros(16, dtype=torch.float64)), 1e-5)
+    assert torch.allclose(ln.value, torch.nn.functional.layer_norm(e, (16,), eps=1e-5))
+    qkv = torch.randn(2, 5, 3 * 8, generator=g, dtype=torch.float64)
+    att = sd.nn().fusedSelfAttention("att", sd.var("qkv", qkv), 2)
+    assert att.value.shape == (2, 5, 8)
