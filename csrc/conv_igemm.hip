@@ -73,7 +73,8 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chu
 // ------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                               const float* __restrict__ bias, bf16* __restrict__ Y,
-                                                              ConvGeom g, int Kred, int scatter, int out_H, int out_W) {
+                                                              ConvGeom g, int Kred, int scatter, int out_H, int out_W,
+                                                              int accum) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_N * TILE_K * 2];   // 2 buffers x (A + B) = 32 KB
   const int M = g.N * g.OH * g.OW;
   const int Nout = g.K;
@@ -210,6 +211,13 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restr
           if (bias) v += bias[n + j];
           o[j] = f2bf(v);
         }
+        if (accum) {                                    // dX += result (fan-out gradient summed in place)
+          const uint2 old = *reinterpret_cast<const uint2*>(Y + orow * Nout + n);
+          o[0] = f2bf(bf2f(o[0]) + bf2f((u16)(old.x & 0xffff)));
+          o[1] = f2bf(bf2f(o[1]) + bf2f((u16)(old.x >> 16)));
+          o[2] = f2bf(bf2f(o[2]) + bf2f((u16)(old.y & 0xffff)));
+          o[3] = f2bf(bf2f(o[3]) + bf2f((u16)(old.y >> 16)));
+        }
         uint2 pk;
         pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
         pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
@@ -260,7 +268,8 @@ __device__ __forceinline__ void raw_barrier() {
 template <bool FAST>
 __global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                             const float* __restrict__ bias, bf16* __restrict__ Y,
-                                                            ConvGeom g, int Kred, int scatter, int out_H, int out_W) {
+                                                            ConvGeom g, int Kred, int scatter, int out_H, int out_W,
+                                                            int accum) {
   __shared__ __attribute__((aligned(16))) char smem[G_STAGES * G_STAGE_BYTES];   // 64 KB -> 2 blocks / CU
   const int M = g.N * g.OH * g.OW;
   const int Nout = g.K;
@@ -429,7 +438,19 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restric
       } else {
         orow = m;
       }
-      *reinterpret_cast<uint4*>(Y + orow * Nout + n) = *reinterpret_cast<const uint4*>(T + ml * 272 + ch * 16);
+      uint4 v = *reinterpret_cast<const uint4*>(T + ml * 272 + ch * 16);
+      if (accum) {                                      // dX += result: 8 bf16 read-modify-write, fp32 adds
+        const uint4 old = *reinterpret_cast<const uint4*>(Y + orow * Nout + n);
+        unsigned* pv = reinterpret_cast<unsigned*>(&v);
+        const unsigned* po = reinterpret_cast<const unsigned*>(&old);
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const u16 lo = f2bf(bf2f((u16)(pv[w2] & 0xffff)) + bf2f((u16)(po[w2] & 0xffff)));
+          const u16 hi = f2bf(bf2f((u16)(pv[w2] >> 16)) + bf2f((u16)(po[w2] >> 16)));
+          pv[w2] = (unsigned)lo | ((unsigned)hi << 16);
+        }
+      }
+      *reinterpret_cast<uint4*>(Y + orow * Nout + n) = v;
     }
     return;
   }
@@ -457,6 +478,13 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restric
           float v = acc[a][b][4 * q + j];
           if (bias) v += bias[n + j];
           o[j] = f2bf(v);
+        }
+        if (accum) {                                    // dX += result (fan-out gradient summed in place)
+          const uint2 old = *reinterpret_cast<const uint2*>(Y + orow * Nout + n);
+          o[0] = f2bf(bf2f(o[0]) + bf2f((u16)(old.x & 0xffff)));
+          o[1] = f2bf(bf2f(o[1]) + bf2f((u16)(old.x >> 16)));
+          o[2] = f2bf(bf2f(o[2]) + bf2f((u16)(old.y & 0xffff)));
+          o[3] = f2bf(bf2f(o[3]) + bf2f((u16)(old.y >> 16)));
         }
         uint2 pk;
         pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
@@ -878,34 +906,34 @@ DL4J_API int dl4j_conv_fwd(const void* X, const void* Wkrsc, const float* bias, 
   ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((K + TILE_N - 1) / TILE_N));
-  LAUNCH_FWD(C % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)X, (const bf16*)Wkrsc, bias, (bf16*)Y, g, R * S * C, 0, 0, 0);
+  LAUNCH_FWD(C % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)X, (const bf16*)Wkrsc, bias, (bf16*)Y, g, R * S * C, 0, 0, 0,
+             0);
   return (int)hipGetLastError();
 }
 
 // Backward data, stride 1: dX[N,H,W,C] = conv(dY[N,OH,OW,K], Wflip[C][R][S][K], pad' = (R-1-ph, S-1-pw)).
+// accum != 0: dX += result (dX already holds another consumer's gradient of the same tensor).
 DL4J_API int dl4j_conv_bwd_data_s1(const void* dY, const void* Wflip, void* dX, int N, int H, int W, int C, int K,
-                                   int R, int S, int ph, int pw, int OH, int OW, hipStream_t s) {
+                                   int R, int S, int ph, int pw, int OH, int OW, int accum, hipStream_t s) {
   if (K % 8 != 0 || C % 4 != 0) return -1;
   // "input" image = dY (OH x OW x K); output grid = H x W x C; kernel R x S stride 1, pad R-1-ph
   ConvGeom g = mk(N, OH, OW, K, H, W, C, R, S, 1, 1, R - 1 - ph, S - 1 - pw, 1, 1);
   const long long M = (long long)N * H * W;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
   LAUNCH_FWD(K % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr,
-             (bf16*)dX, g, R * S * K, 0, 0,
-             0);
+             (bf16*)dX, g, R * S * K, 0, 0, 0, accum);
   return (int)hipGetLastError();
 }
 
 // Backward data, 1x1 kernel, stride s, no padding: dX (pre-zeroed) rows (n, oh*s, ow*s) = dY rows x Wflip[C][K].
 DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX, int N, int H, int W, int C, int K,
-                                    int stride, int OH, int OW, hipStream_t s) {
+                                    int stride, int OH, int OW, int accum, hipStream_t s) {
   if (K % 8 != 0 || C % 4 != 0) return -1;
   ConvGeom g = mk(N, OH, OW, K, OH, OW, C, 1, 1, 1, 1, 0, 0, 1, 1);
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
   LAUNCH_FWD(K % TILE_K == 0, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr, (bf16*)dX, g, K,
-             stride, H,
-             W);
+             stride, H, W, accum);
   return (int)hipGetLastError();
 }
 

@@ -270,6 +270,8 @@ class ComputationGraph(BaseNetwork):
             if e is None:
                 return
             if name in eps_acc:
+                if eps_acc[name] is e:                 # already summed in place by the producing kernel
+                    return
                 eps_acc[name] = eps_acc[name] + e
             else:
                 eps_acc[name] = e
@@ -295,6 +297,10 @@ class ComputationGraph(BaseNetwork):
                     if not self._need_input_grad[name] and layer.conf.numParams() == 0:
                         continue
                     tok = _prof.layer_begin("bwd", name, layer) if _prof.ACTIVE else None
+                    ins0 = self.vertex_inputs[name]
+                    if len(ins0) == 1 and v.preProcessor is None and ins0[0] in eps_acc and \
+                            hasattr(layer, "dx_accum"):
+                        layer.dx_accum = eps_acc[ins0[0]]    # fan-out: let the conv kernel sum dX in place
                     if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
                         _, e = layer.backpropGradient(e_in, tbptt_back=tbptt_back)
                     else:

@@ -59,6 +59,7 @@ class ConvolutionLayerImpl(LayerImpl):
 
     extra_pad4 = None     # set by the graph planner when a preceding ZeroPaddingLayer is folded into this conv
     defer_bias = False    # set by the graph planner when a training-mode BatchNormalization absorbs the bias
+    dx_accum = None       # set by the graph for one backward call: existing gradient of x to accumulate into
 
     def _geom(self, x):
         c = self.conf
@@ -98,9 +99,12 @@ class ConvolutionLayerImpl(LayerImpl):
         W = self.W("W")
         xt = _cl(self._xt.to(W.dtype))
         need_dx = getattr(self, "need_input_grad", True)
+        acc = getattr(self, "dx_accum", None)       # set by the graph when x already has a gradient (fan-out)
+        self.dx_accum = None
         dx, dW, db = ops.conv2d_backward(xt, W, _cl(delta.to(W.dtype)), s, pad4, d, need_dx, True,
                                          "b" in self.grads, gW=self.grads["W"], gb=self.grads.get("b"),
-                                         grads_zeroed=getattr(self.net, "_grads_zeroed", False))
+                                         grads_zeroed=getattr(self.net, "_grads_zeroed", False),
+                                         dx_accum=acc if need_dx and self.conf.idropout is None else None)
         if dW is not None:
             copy_grad_(self.grads["W"], dW)
         if "b" in self.grads and db is not None:

@@ -35,13 +35,13 @@ def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1):
 
 
 def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_dw=True, need_db=True,
-                    groups=1, gW=None, gb=None, grads_zeroed=False):
+                    groups=1, gW=None, gb=None, grads_zeroed=False, dx_accum=None):
     """Returns (dx, dW, db). When the native kernels run and fp32 gradient views ``gW``/``gb`` are given,
     dW/db are written straight into them (fp32 accumulation) and returned as None."""
     if use_native(x, "conv") and groups == 1:
         from . import native
         r = native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb,
-                               grads_zeroed)
+                               grads_zeroed, dx_accum)
         if r is not None:
             return r
     pt, pb, pl, pr = pad4

@@ -21,8 +21,8 @@ native.register_sig("dl4j_conv_w_relayout_batched", [c_void_p, c_int, c_ll, c_vo
 native.register_sig("dl4j_conv_relayout_job_bytes", [])
 native.register_sig("dl4j_conv_relayout_per_block", [])
 native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p])
-native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p])
-native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p])
+native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
+native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 9 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
 native.register_sig("dl4j_conv_set_variant", [c_int])
 native.register_sig("dl4j_conv_set_wrw_variant", [c_int])
@@ -186,9 +186,12 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return y
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
+               dx_accum=None):
     """grads_zeroed: the caller guarantees gW/gb (flat-gradient views) are already zero (the network clears the
-    whole flat gradient with one fill per step), so no per-layer memset is launched."""
+    whole flat gradient with one fill per step), so no per-layer memset is launched.
+    dx_accum: an existing channels-last bf16 gradient of x (another consumer's contribution); when the bwd-data
+    kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx."""
     if not (_ok_act(x) and _ok_act(dy) and w.dtype == torch.bfloat16):
         return None
     N, C, H, W = x.shape
@@ -203,18 +206,24 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     if need_dx:
         s1 = tuple(stride) == (1, 1) and tuple(dilation) == (1, 1)
         pure_1x1 = R == 1 and S == 1 and not any(pad4) and tuple(dilation) == (1, 1)
+        acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
+            and dx_accum.is_contiguous(memory_format=torch.channels_last)
         if s1 and (H, W) == _out_hw_inv(OH, OW, R, S, pad4, H, W):
             _, flip = _relayout(w, False, True)
-            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            dx = dx_accum if acc else torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
+                                                  memory_format=torch.channels_last)
             rc = lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, R, S, pad4[0], pad4[2], OH,
-                                           OW, _stream())
+                                           OW, int(acc), _stream())
             native._check(rc, "conv_bwd_data_s1")
         elif pure_1x1 and stride[0] == stride[1]:
             _, flip = _relayout(w, False, True)
-            dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
-                             memory_format=torch.channels_last).zero_()
+            if acc:
+                dx = dx_accum                                # only the strided rows are touched (+=)
+            else:
+                dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
+                                 memory_format=torch.channels_last).zero_()
             rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
-                                            _stream())
+                                            int(acc), _stream())
             native._check(rc, "conv_bwd_data_1x1")
         else:
             from .conv import _sym

@@ -344,10 +344,11 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation)
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False):
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
+               dx_accum=None):
     from . import conv_native
     return conv_native.conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb,
-                                  grads_zeroed)
+                                  grads_zeroed, dx_accum)
 
 
 def segment_stats(flat, offsets, bins=0):

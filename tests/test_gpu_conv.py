@@ -145,3 +145,23 @@ def test_network_uses_batched_relayout():
         lib.dl4j_conv_w_relayout = orig
     assert len(net._conv_ws) == 53
     assert calls["single"] <= 2          # only weights outside the batched criteria (the C=3 stem goes to MIOpen)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[5] == c[6] and (c[7] == (1, 1) or c[5] == 1)])
+def test_conv_bwd_data_accumulates_in_place(cuda, case):
+    """dx_accum: the bwd-data kernel adds its result into an existing gradient of x (graph fan-out) in the epilogue."""
+    N, C, H, W, K, R, S, stride, pad4 = case
+    if R == 1 and any(pad4):
+        pytest.skip("padded 1x1 is not a native bwd-data path")
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g).to(cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, S, generator=g) * 0.1).to(cuda).bfloat16()
+    conv_native.bump_version()
+    y = conv_native.conv2d_fwd(x, w, None, stride, pad4, (1, 1))
+    dy = torch.randn(y.shape, generator=g).to(cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    other = torch.randn(x.shape, generator=g).to(cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    dx_ref, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False)
+    acc = other.clone()
+    dx, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False, dx_accum=acc)
+    assert dx is acc
+    _close(dx, other.float() + dx_ref.float(), 2e-2)
