@@ -94,6 +94,41 @@ __global__ __launch_bounds__(256) void bn_reduce_rows(const float* __restrict__ 
   }
 }
 
+// Per-tile statistics from the conv epilogue (csrc/conv_igemm.hip, planes [3][P][C]: S1, S2 about a per-partial
+// shift y_p, partial p = rows [64p, 64p+64)) -> the [ceil(P/32), C] partial-sum format of bn_stats_partial
+// (sums about the GLOBAL shift x0 = row 0). Re-centring uses d = y_p - x0 (both samples of the same channel, so
+// O(std), no cancellation): S1' = S1 + n d, S2' = S2 + 2 d S1 + n d^2. grid = (ceil(C/64), ceil(P/32)).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_tiles_reduce(const float* __restrict__ ts, long long P, int C, long long M,
+                                                       const T* __restrict__ x, float* __restrict__ q1,
+                                                       float* __restrict__ q2) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const long long p0 = (long long)blockIdx.y * 32 + grp * 8;
+  float sa = 0.f, sb = 0.f;
+  if (c < C) {
+    const float x0 = ld1<T>(x + c);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long p = p0 + u;
+      if (p >= P) break;
+      const long long nrow = M - 64 * p;
+      const float n = (float)(nrow < 64 ? (nrow < 0 ? 0 : nrow) : 64);
+      const float s1 = ts[p * C + c], s2 = ts[(P + p) * C + c], d = ts[(2 * P + p) * C + c] - x0;
+      sa += s1 + n * d;
+      sb += s2 + 2.f * d * s1 + n * d * d;
+    }
+  }
+  __shared__ float ra[256], rb[256];
+  ra[threadIdx.x] = sa;
+  rb[threadIdx.x] = sb;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    q1[(long long)blockIdx.y * C + c] = ra[threadIdx.x] + ra[threadIdx.x + 64] + ra[threadIdx.x + 128] + ra[threadIdx.x + 192];
+    q2[(long long)blockIdx.y * C + c] = rb[threadIdx.x] + rb[threadIdx.x + 64] + rb[threadIdx.x + 128] + rb[threadIdx.x + 192];
+  }
+}
+
 // Reduce [nblk, C] partials: block = 64 channels x 4 row groups.
 __device__ __forceinline__ void reduce_partials(const float* __restrict__ p1, const float* __restrict__ p2, int nblk,
                                                 int C, int c, double& a, double& b) {
@@ -352,6 +387,33 @@ DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, lon
     BN_DISPATCH3(bn_apply, float, relu, res, dim3(ag), dim3(256), 0, s, xf, (const float*)res, (float*)y, M, C,
                  ctx_out);
   }
+  return (int)hipGetLastError();
+}
+
+// Training forward with the statistics already reduced per tile by the producing conv kernel (tstats, P partials):
+// skips bn_stats_partial's full read of x. ws: >= dl4j_bn_tiles_workspace_floats(P, C) floats.
+DL4J_API long long dl4j_bn_tiles_workspace_floats(long long P, int C) {
+  const long long S = (P + 31) / 32;
+  return 2 * S * C + 2 * ((S + 31) / 32) * C + 8LL * C;
+}
+
+DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* y, long long M, int C,
+                               const float* tstats, long long P, const float* gamma, const float* beta, float gconst,
+                               float bconst, float* run_mean, float* run_var, float decay, float eps, int relu,
+                               float* ws, float* ctx_out, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || dtype != 1 || P < 1) return -1;
+  if (res) relu = 1;
+  int S = (int)((P + 31) / 32);
+  float* p1 = ws;
+  float* p2 = ws + (long long)S * C;
+  float* q = p2 + (long long)S * C;
+  const bf16* xb = (const bf16*)x;
+  hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2);
+  bn_reduce_stage(p1, p2, S, C, q, s);
+  hipLaunchKernelGGL(bn_finalize<bf16>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, S, C, M, xb, gamma, beta, gconst,
+                     bconst, run_mean, run_var, decay, eps, 1, ctx_out);
+  const int ag = apply_grid(M, C);
+  BN_DISPATCH3(bn_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, xb, (const bf16*)res, (bf16*)y, M, C, ctx_out);
   return (int)hipGetLastError();
 }
 

@@ -74,7 +74,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chu
 __global__ __launch_bounds__(NTHREADS) void igemm_fwd_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                               const float* __restrict__ bias, bf16* __restrict__ Y,
                                                               ConvGeom g, int Kred, int scatter, int out_H, int out_W,
-                                                              int accum) {
+                                                              int accum, float* __restrict__ tstats) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_N * TILE_K * 2];   // 2 buffers x (A + B) = 32 KB
   const int M = g.N * g.OH * g.OW;
   const int Nout = g.K;
@@ -269,7 +269,7 @@ template <bool FAST>
 __global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                             const float* __restrict__ bias, bf16* __restrict__ Y,
                                                             ConvGeom g, int Kred, int scatter, int out_H, int out_W,
-                                                            int accum) {
+                                                            int accum, float* __restrict__ tstats) {
   __shared__ __attribute__((aligned(16))) char smem[G_STAGES * G_STAGE_BYTES];   // 64 KB -> 2 blocks / CU
   const int M = g.N * g.OH * g.OW;
   const int Nout = g.K;
@@ -451,6 +451,47 @@ __global__ __launch_bounds__(NTHREADS) void igemm_fwd_glds(const bf16* __restric
         }
       }
       *reinterpret_cast<uint4*>(Y + orow * Nout + n) = v;
+    }
+    if (tstats) {
+      // BatchNorm statistics of this tile, straight from the bf16 tile in LDS (the exact values BN will read):
+      // per (64-row half, channel) shifted sums S1 = sum(y - y0), S2 = sum((y - y0)^2) and the shift y0 (first
+      // row of the half). Planes [3][P][Nout], P = 2 * tiles_m; reduced by bn_tiles_reduce (csrc/batchnorm.hip).
+      const int col = tid & 127, half = tid >> 7;
+      const int nn = n0 + col;
+      const int rbeg = half * 64;
+      const int rows = min(64, M - (m0 + rbeg));
+      const long long P = 2LL * tiles_m;
+      const long long pidx = 2LL * tm + half;
+      if (nn < Nout) {
+        float s1 = 0.f, s2 = 0.f, sh = 0.f;
+        if (rows > 0) {
+          sh = bf2f(*reinterpret_cast<const u16*>(T + rbeg * 272 + col * 2));
+          const char* src = T + rbeg * 272 + col * 2;
+          if (rows == 64) {
+            float a1 = 0.f, a2 = 0.f;
+#pragma unroll 16
+            for (int r = 0; r < 64; r += 2) {             // two independent chains, LDS reads batched by unrolling
+              const float d0 = bf2f(*reinterpret_cast<const u16*>(src + r * 272)) - sh;
+              const float d1 = bf2f(*reinterpret_cast<const u16*>(src + (r + 1) * 272)) - sh;
+              s1 += d0;
+              s2 = fmaf(d0, d0, s2);
+              a1 += d1;
+              a2 = fmaf(d1, d1, a2);
+            }
+            s1 += a1;
+            s2 += a2;
+          } else {
+            for (int r = 0; r < rows; ++r) {
+              const float d = bf2f(*reinterpret_cast<const u16*>(src + r * 272)) - sh;
+              s1 += d;
+              s2 = fmaf(d, d, s2);
+            }
+          }
+        }
+        tstats[pidx * Nout + nn] = s1;
+        tstats[(P + pidx) * Nout + nn] = s2;
+        tstats[(2 * P + pidx) * Nout + nn] = sh;
+      }
     }
     return;
   }
@@ -899,16 +940,20 @@ DL4J_API int dl4j_conv_w_relayout(const void* W, void* krsc, void* flip, int K, 
 }
 
 // Forward: X NHWC [N,H,W,C] bf16, Wkrsc [K][R*S*C], bias fp32 [K] or null, Y NHWC [N,OH,OW,K].
+// tstats (optional, fp32 [3][2*ceil(M/128)][K]): per-tile BatchNorm partial statistics of Y. Returns 1 when they
+// were written, 0 when not (unsupported variant), a HIP error code otherwise.
 DL4J_API int dl4j_conv_fwd(const void* X, const void* Wkrsc, const float* bias, void* Y, int N, int H, int W, int C,
                            int K, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int OH, int OW,
-                           hipStream_t s) {
+                           float* tstats, hipStream_t s) {
   if (C % 8 != 0 || K % 4 != 0) return -1;
   ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((K + TILE_N - 1) / TILE_N));
+  const int stats_ok = tstats != nullptr && g_fwd_variant == 1 && C % TILE_K == 0 && R * S <= 64 && K % 8 == 0;
   LAUNCH_FWD(C % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)X, (const bf16*)Wkrsc, bias, (bf16*)Y, g, R * S * C, 0, 0, 0,
-             0);
-  return (int)hipGetLastError();
+             0, stats_ok ? tstats : nullptr);
+  const int e = (int)hipGetLastError();
+  return e != 0 ? e : (stats_ok ? 1 : 0);
 }
 
 // Backward data, stride 1: dX[N,H,W,C] = conv(dY[N,OH,OW,K], Wflip[C][R][S][K], pad' = (R-1-ph, S-1-pw)).
@@ -921,7 +966,7 @@ DL4J_API int dl4j_conv_bwd_data_s1(const void* dY, const void* Wflip, void* dX, 
   const long long M = (long long)N * H * W;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
   LAUNCH_FWD(K % TILE_K == 0 && R * S <= 64, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr,
-             (bf16*)dX, g, R * S * K, 0, 0, 0, accum);
+             (bf16*)dX, g, R * S * K, 0, 0, 0, accum, (float*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -933,7 +978,7 @@ DL4J_API int dl4j_conv_bwd_data_1x1(const void* dY, const void* Wflip, void* dX,
   const long long M = (long long)N * OH * OW;
   const int tiles = (int)(((M + TILE_M - 1) / TILE_M) * ((C + TILE_N - 1) / TILE_N));
   LAUNCH_FWD(K % TILE_K == 0, dim3(tiles), (const bf16*)dY, (const bf16*)Wflip, (const float*)nullptr, (bf16*)dX, g, K,
-             stride, H, W, accum);
+             stride, H, W, accum, (float*)nullptr);
   return (int)hipGetLastError();
 }
 

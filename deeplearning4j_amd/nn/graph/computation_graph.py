@@ -152,6 +152,20 @@ class ComputationGraph(BaseNetwork):
                 continue
             impl.defer_bias = True
             self.layers_by_name[bn_name].deferred_bias = impl
+        # Conv (identity activation) -> training-mode BatchNormalization: the MFMA conv kernel emits per-tile BN
+        # statistics from its epilogue, so BN skips its own full statistics pass over the conv output
+        for name in self.topo:
+            v = self.conf.vertices[name]
+            if not (isinstance(v, LayerVertex) and type(v.layerConf) is ConvolutionLayer) or name in self.outputs \
+                    or len(self.consumers[name]) != 1 or os.environ.get("DL4J_AMD_CONV_BN_STATS", "1") != "1":
+                continue
+            if type(v.layerConf.activation).__name__ != "ActivationIdentity" or v.layerConf.idropout is not None:
+                continue
+            bv = self.conf.vertices[self.consumers[name][0]]
+            if isinstance(bv, LayerVertex) and isinstance(bv.layerConf, BatchNormalization) and \
+                    bv.preProcessor is None and bv.layerConf.idropout is None and \
+                    not getattr(bv.layerConf, "useLogStd", False):
+                self.layers_by_name[name].emit_bn_stats = True
         # which vertices must produce an input gradient
         flows = {n: False for n in self.conf.networkInputs}
         self._need_input_grad = {}

@@ -60,6 +60,7 @@ class ConvolutionLayerImpl(LayerImpl):
     extra_pad4 = None     # set by the graph planner when a preceding ZeroPaddingLayer is folded into this conv
     defer_bias = False    # set by the graph planner when a training-mode BatchNormalization absorbs the bias
     dx_accum = None       # set by the graph for one backward call: existing gradient of x to accumulate into
+    emit_bn_stats = False  # set by the graph planner when a training-mode BatchNormalization consumes the output
 
     def _geom(self, x):
         c = self.conf
@@ -77,7 +78,8 @@ class ConvolutionLayerImpl(LayerImpl):
         xt = x     # Truncate mode needs no cropping: output sizes use floor division everywhere
         self._xt = xt
         self._geom_cache = (s, pad4, d)
-        return ops.conv2d_forward(_cl(xt.to(W.dtype)), W, b, s, pad4, d)
+        return ops.conv2d_forward(_cl(xt.to(W.dtype)), W, b, s, pad4, d,
+                                  want_stats=bool(training and self.emit_bn_stats))
 
     def activate(self, x, training=False, mask=None):
         if x.dim() != 4:

@@ -19,10 +19,10 @@ def _sym(pad4):
     return pt == pb and pl == pr
 
 
-def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1):
+def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1, want_stats=False):
     if use_native(x, "conv") and groups == 1:
         from . import native
-        y = native.conv2d_fwd(x, w, b, stride, pad4, dilation)
+        y = native.conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats)
         if y is not None:
             return y
     pt, pb, pl, pr = pad4

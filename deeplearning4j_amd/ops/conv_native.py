@@ -20,7 +20,7 @@ native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int
 native.register_sig("dl4j_conv_w_relayout_batched", [c_void_p, c_int, c_ll, c_void_p])
 native.register_sig("dl4j_conv_relayout_job_bytes", [])
 native.register_sig("dl4j_conv_relayout_per_block", [])
-native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p])
+native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p, c_void_p])
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 9 + [c_void_p])
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
@@ -166,7 +166,9 @@ def _out_hw(H, W, R, S, stride, pad4, dilation):
     return OH, OW
 
 
-def conv2d_fwd(x, w, b, stride, pad4, dilation):
+def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
+    """want_stats: also emit per-tile BatchNorm statistics of the output from the kernel epilogue; they are attached
+    to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer."""
     if not (_ok_act(x) and w.dtype == torch.bfloat16):
         return None
     N, C, H, W = x.shape
@@ -180,8 +182,16 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation):
     x = _cl(x)
     y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     bias = b.float().contiguous() if b is not None else None
+    ts = None
+    if want_stats and C % 32 == 0 and R * S <= 64 and K % 8 == 0:
+        P = 2 * ((N * OH * OW + 127) // 128)
+        ts = torch.empty((3, P, K), dtype=torch.float32, device=x.device)
     rc = native.load().dl4j_conv_fwd(_ptr(x), _ptr(krsc), _ptr(bias), _ptr(y), N, H, W, C, K, R, S, stride[0],
-                                     stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, _stream())
+                                     stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, _ptr(ts),
+                                     _stream())
+    if rc == 1:
+        y._bn_tile_stats = (ts, ts.shape[1])
+        rc = 0
     native._check(rc, "conv_fwd")
     return y
 

@@ -266,6 +266,21 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     g = gamma if torch.is_tensor(gamma) else None
     b = beta if torch.is_tensor(beta) else None
     res = _rows_like(residual, x) if residual is not None else None
+    ts = getattr(x, "_bn_tile_stats", None)
+    if training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128):
+        # statistics already reduced per tile by the producing conv kernel's epilogue
+        register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_void_p,
+                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int,
+                                           c_void_p, c_void_p, c_void_p])
+        register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
+        lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
+        wst = torch.empty(lib.dl4j_bn_tiles_workspace_floats(ts[1], C), dtype=torch.float32, device=x.device)
+        rc = lib.dl4j_bn_fwd_tiles(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(ts[0]), ts[1], _ptr(g), _ptr(b),
+                                   float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0,
+                                   _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
+                                   _ptr(wst), _ptr(ctx), _stream())
+        _check(rc, "bn_fwd_tiles")
+        return y, ("NATIVE", x, ctx, relu, M, C, res)
     rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
                          float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                          _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
@@ -339,9 +354,9 @@ def pool2d_bwd(dy, ctx):
 
 
 # ------------------------------------------------------------------------------------------ conv (MFMA)
-def conv2d_fwd(x, w, b, stride, pad4, dilation):
+def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     from . import conv_native
-    return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation)
+    return conv_native.conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats)
 
 
 def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,

@@ -165,3 +165,41 @@ def test_conv_bwd_data_accumulates_in_place(cuda, case):
     dx, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False, dx_accum=acc)
     assert dx is acc
     _close(dx, other.float() + dx_ref.float(), 2e-2)
+
+
+def test_conv_epilogue_bn_stats_match_separate_pass(cuda, monkeypatch):
+    """Conv -> BN (training): statistics from the conv kernel epilogue give the same BN forward / running stats /
+    update as the separate statistics pass (DL4J_AMD_CONV_BN_STATS=0)."""
+    from deeplearning4j_amd import (Activation, ActivationLayer, BatchNormalization, ComputationGraph, ConvolutionLayer,
+                                    DataType, GlobalPoolingLayer, InputType, LossFunction, NeuralNetConfiguration,
+                                    OutputLayer, PoolingType, Sgd)
+
+    def build():
+        g = (NeuralNetConfiguration.Builder().seed(3).dataType(DataType.BFLOAT16).updater(Sgd(0.1)).graphBuilder()
+             .addInputs("in").setInputTypes(InputType.convolutional(20, 20, 64)))
+        g.addLayer("c1", ConvolutionLayer.Builder([3, 3]).padding([1, 1]).nOut(128)
+                   .activation(Activation.IDENTITY).build(), "in")
+        g.addLayer("bn1", BatchNormalization.Builder().build(), "c1")
+        g.addLayer("r1", ActivationLayer.Builder().activation(Activation.RELU).build(), "bn1")
+        g.addLayer("p", GlobalPoolingLayer.Builder(PoolingType.AVG).build(), "r1")
+        g.addLayer("out", OutputLayer.Builder(LossFunction.MCXENT).activation(Activation.SOFTMAX).nOut(5).build(), "p")
+        g.setOutputs("out")
+        n = ComputationGraph(g.build())
+        n.init(device=cuda)
+        return n
+
+    gen = torch.Generator().manual_seed(1)
+    x = (torch.randn(16, 64, 20, 20, generator=gen) + 0.7).to(cuda)
+    y = torch.nn.functional.one_hot(torch.randint(0, 5, (16,), generator=gen), 5).float().to(cuda)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_CONV_BN_STATS", flag)
+        net = build()
+        assert net.layers_by_name["c1"].emit_bn_stats == (flag == "1")
+        net.fit([x], [y])
+        torch.cuda.synchronize()
+        res.append((net.params().clone(), net.getParam("bn1_mean").clone(), net.getParam("bn1_var").clone()))
+    (p1, m1, v1), (p0, m0, v0) = res
+    _close(m1, m0, 1e-4)
+    _close(v1, v0, 1e-4)
+    _close(p1, p0, 1e-3)
