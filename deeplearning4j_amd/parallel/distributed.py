@@ -29,7 +29,8 @@ def init_distributed(backend=None, timeout_s=600):
         # a failed/hung RCCL collective aborts the communicator and raises instead of hanging
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if backend is None:
-            backend = "nccl" if device.type == "cuda" else "gloo"
+            # DL4J_AMD_DIST_BACKEND=gloo rehearses multi-rank runs on one GPU (RCCL needs one GPU per rank)
+            backend = os.environ.get("DL4J_AMD_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
