@@ -145,13 +145,18 @@ DL4J_API int dl4j_segment_stats(int dtype, const void* x, const long long* off, 
 // Column sums of a row-major [M, C] bf16/fp32 matrix into fp32 out[C] (conv bias gradient on the library
 // conv path: dy in channels-last is exactly such a matrix). Each thread owns 8 consecutive channels (one 16-byte
 // load for bf16) of a row; a block sweeps rows in a grid-stride loop, reduces through LDS and issues one atomic
-// per channel. Requires C % 8 == 0 and C <= 2048.
+// per channel. Requires C % 8 == 0; channels beyond 2048 are split over blockIdx.y chunks of 2048 (also the
+// transformer bias gradients: 768 / 2304 / 3072 columns).
 // ------------------------------------------------------------------------------------------------------
 namespace {
 template <typename T>
-__global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ x, long long M, int C,
-                                                          float* __restrict__ out) {
+__global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ xfull, long long M, int ld,
+                                                          float* __restrict__ outfull) {
   extern __shared__ float red[];                         // [rows_per_iter][C]
+  const int c0 = blockIdx.y * 2048;
+  const int C = min(2048, ld - c0);
+  const T* x = xfull + c0;
+  float* out = outfull + c0;
   const int groups = C / 8;                              // threads per row
   const int rows_per_iter = 256 / groups;
   const int g = threadIdx.x % groups, r0 = threadIdx.x / groups;
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ 
   if (r0 < rows_per_iter) {
     for (long long r = (long long)blockIdx.x * rows_per_iter + r0; r < M; r += (long long)gridDim.x * rows_per_iter) {
       float v[8];
-      Vec8<T>::load(x + r * C + g * 8, v);
+      Vec8<T>::load(x + r * ld + g * 8, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += v[j];
     }
@@ -175,18 +180,18 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ 
 }  // namespace
 
 DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, float* out, hipStream_t stream) {
-  if (C % 8 != 0 || C > 2048 || M <= 0) return -1;
+  if (C % 8 != 0 || M <= 0) return -1;
   if (hipMemsetAsync(out, 0, sizeof(float) * C, stream) != hipSuccess) return -3;
-  const int rows_per_iter = 256 / (C / 8);
+  const int Cc = C < 2048 ? C : 2048;                    // widest chunk; the last chunk may be narrower
+  const int rows_per_iter = 256 / (Cc / 8);
   long long blocks = (M + rows_per_iter * 16 - 1) / (rows_per_iter * 16);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  const size_t lds = sizeof(float) * rows_per_iter * C;
+  const size_t lds = sizeof(float) * 256 * 8;             // >= rows_per_iter * chunk width for every chunk
+  const dim3 grid((unsigned)blocks, (C + 2047) / 2048);
   if (dtype == 1)
-    hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3((unsigned)blocks), dim3(256), lds, stream, (const bf16*)x, M, C,
-                       out);
+    hipLaunchKernelGGL(channel_sum_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, M, C, out);
   else
-    hipLaunchKernelGGL(channel_sum_kernel<float>, dim3((unsigned)blocks), dim3(256), lds, stream, (const float*)x, M,
-                       C, out);
+    hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), lds, stream, (const float*)x, M, C, out);
   return (int)hipGetLastError();
 }

@@ -39,6 +39,10 @@ def _wgrad(view, a, b):
 
 def _bsum(view, d):
     """view <- column sums of d, accumulated in the view's precision without a converted copy of d."""
+    if d.is_cuda and view.is_contiguous() and view.dtype == torch.float32 and ops.use_native(d, "bias_grad"):
+        from ...ops import native
+        if native.channel_sum(d.contiguous(), out=view.view(-1)) is not None:
+            return
     if view.is_contiguous():
         torch.sum(d, 0, dtype=view.dtype, out=view.view(-1))
     else:

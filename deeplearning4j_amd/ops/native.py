@@ -391,14 +391,16 @@ def segment_stats(flat, offsets, bins=0):
     return out, (hist.to(torch.int64) if hist is not None else None)
 
 
-def channel_sum(rows):
-    """fp32 column sums of a contiguous [M, C] fp32/bf16 CUDA matrix (dl4j_channel_sum); None if unsupported."""
+def channel_sum(rows, out=None):
+    """fp32 column sums of a contiguous [M, C] fp32/bf16 CUDA matrix (dl4j_channel_sum); None if unsupported.
+    ``out``: optional contiguous fp32 [C] destination (e.g. a flat-gradient view)."""
     dt = _dt(rows)
-    if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] % 8 or rows.shape[1] > 2048:
+    if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] % 8:
         return None
     lib = load()
     register_sig("dl4j_channel_sum", [c_int, c_void_p, c_ll, c_int, c_void_p, c_void_p])
-    out = torch.empty(rows.shape[1], dtype=torch.float32, device=rows.device)
+    if out is None or not (out.is_contiguous() and out.dtype == torch.float32 and out.numel() == rows.shape[1]):
+        out = torch.empty(rows.shape[1], dtype=torch.float32, device=rows.device)
     _check(lib.dl4j_channel_sum(dt, _ptr(rows), rows.shape[0], rows.shape[1], _ptr(out), c_void_p(_stream())),
            "channel_sum")
     return out

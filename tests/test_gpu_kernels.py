@@ -231,3 +231,12 @@ def test_hip_graph_training_matches_eager(cuda):
     assert graphed.getIterationCount() == eager.getIterationCount() == 6
     assert torch.allclose(graphed.params(), eager.params(), atol=2e-3, rtol=1e-2)
     assert abs(graphed.score() - eager.score()) < 1e-2
+
+
+@pytest.mark.parametrize("M,C", [(4096, 768), (1000, 3072), (77, 2304), (513, 16)])
+def test_channel_sum_wide(cuda, M, C):
+    x = torch.randn(M, C, device=cuda).bfloat16()
+    out = torch.empty(C, device=cuda)
+    r = native.channel_sum(x, out=out)
+    assert r is not None and r.data_ptr() == out.data_ptr()
+    _close(out, x.float().sum(0), 1e-3)
