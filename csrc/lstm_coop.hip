@@ -1,0 +1,253 @@
+// Cooperative (multi-workgroup) LSTM recurrence for gfx950: the per-step RW·h GEMM is split over G workgroups per
+// 16-row minibatch tile so that each workgroup's slice of the recurrent weights stays RESIDENT IN LDS for the
+// whole sequence (128 KB per workgroup), instead of every step streaming all of RW from L2 (csrc/lstm.hip, which is
+// bound by ~70 GB/s of L2->CU traffic per workgroup: 7.4 us per step at H = 256).
+//
+// Per step, workgroup g of a tile computes the four gates of its U hidden units (MFMA 16x16x32 bf16, A = h_{t-1}
+// from LDS, B = its RW slice from LDS), keeps c in registers, and PUBLISHES its slice of h_t to the other G-1
+// workgroups through 8-byte "granules" {tag = step+1, 2 x bf16} stored with agent-scope atomics: the data is its
+// own flag (guide Guideline 16, R2), so there is no separate flag, fence or barrier between workgroups. Consumers
+// sweep the granules of h_{t-1} with agent-scope atomic loads until every tag matches; every spin is bounded by the
+// wall clock (a timeout sets *err and the kernel runs to completion instead of hanging). The exchange buffer is
+// double-buffered by step parity and zeroed by the host before every launch (tags start at 1).
+//
+// The grid (G x tiles workgroups, one per CU: LDS-bound) is launched with hipLaunchCooperativeKernel so that all
+// workgroups are guaranteed co-resident; shapes that do not fit fall back to csrc/lstm.hip.
+// Math, gate order [a|f|o|g], peepholes, masks and outputs are identical to lstm_fwd_kernel.
+#include "common.h"
+
+typedef __attribute__((ext_vector_type(4))) float f4c_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8c_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ float sigm_c(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_c(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf((1.f - e) / (1.f + e), x);
+}
+
+// U = hidden units per workgroup (16 per wave); KS = H / 32 k-steps
+template <int U, bool PEEP>
+__global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
+    const __bf16* __restrict__ zx, const __bf16* __restrict__ rwt, const float* __restrict__ peep,
+    const float* __restrict__ h0, const float* __restrict__ c0, const float* __restrict__ mask,
+    float* __restrict__ out, float* __restrict__ gates, float* __restrict__ call, float* __restrict__ hT,
+    float* __restrict__ cT, unsigned long long* exch_raw, unsigned* err_raw, int Tn, int mb, int H,
+    long long timeout_ticks) {
+  constexpr int NW = U / 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int KS = H / 32, H16 = H / 16, H4 = 4 * H;
+  bf16x8c_t* rws = reinterpret_cast<bf16x8c_t*>(smem);                       // [4][NW][KS][64] fragments
+  __bf16* hbuf = reinterpret_cast<__bf16*>(smem + (size_t)4 * NW * KS * 64 * 16);   // [1 or 2][16][H + 8]
+  const bool dbuf = H <= 256;        // double-buffered h tile when it fits next to the RW slice, else one more barrier
+  const int ldh = H + 8;
+  gu64* exch = (gu64*)exch_raw;
+  gu32* err = (gu32*)err_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
+  const int grp = blockIdx.x, tile = blockIdx.y, G = gridDim.x;
+  const int m0 = tile * 16;
+  const int u0 = grp * U;                                  // first hidden unit of this workgroup
+  const int j = u0 + wave * 16 + col;                      // this lane's hidden unit
+  // ---- resident RW slice: fragments of (gate, this wave's 16-unit tile, k-step)
+  for (int i = threadIdx.x; i < 4 * NW * KS * 64; i += blockDim.x) {
+    const int ln = i & 63, t1 = i >> 6;
+    const int ks = t1 % KS, t2 = t1 / KS;
+    const int w = t2 % NW, g = t2 / NW;
+    const long long gt = (long long)g * H16 + (u0 >> 4) + w;
+    rws[i] = *reinterpret_cast<const bf16x8c_t*>(rwt + ((gt * KS + ks) * 64 + ln) * 8);
+  }
+  int mrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mrow[r] = min(m0 + rg + r, mb - 1);
+  float c[4], wff = 0.f, woo = 0.f, wgg = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = (c0 && m0 + rg + r < mb) ? c0[(long long)mrow[r] * H + j] : 0.f;
+  if (PEEP) {
+    wff = peep[j];
+    woo = peep[H + j];
+    wgg = peep[2 * H + j];
+  }
+  float zv[4][4], mv[4];
+  auto load_step = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long zrow = ((long long)t * mb + mrow[r]) * H4;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) zv[g][r] = (float)zx[zrow + g * H + j];
+      mv[r] = mask ? mask[(long long)mrow[r] * Tn + t] : 1.f;
+    }
+  };
+  load_step(0);
+  const int npairs = 16 * (H / 2);                         // granules per step per tile
+  for (int t = 0; t < Tn; ++t) {
+    __bf16* hb = hbuf + (dbuf ? (t & 1) : 0) * 16 * ldh;
+    // ---- gather h_{t-1} (16 rows x H) into LDS
+    if (t == 0) {
+      for (int i = threadIdx.x; i < 16 * H; i += blockDim.x) {
+        const int r = i / H, k = i - r * H, m = m0 + r;
+        hb[r * ldh + k] = (__bf16)((h0 && m < mb) ? h0[(long long)m * H + k] : 0.f);
+      }
+    } else {
+      gu64* src = exch + ((long long)tile * 2 + ((t - 1) & 1)) * npairs;
+      const long long deadline = wall_clock64() + timeout_ticks;   // per step: long sequences never time out
+      // sweep: each thread issues its granule loads in batches of 8 (one round trip per batch), re-polling a batch
+      // until every tag matches (guide Guideline 16, R2 sweep_granules)
+      for (int base = 0; base < npairs; base += 8 * blockDim.x) {
+        unsigned long long v[8];
+        for (;;) {
+          bool ok = true;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int i = base + q * blockDim.x + threadIdx.x;
+            v[q] = i < npairs ? __hip_atomic_load(src + i, RLX_AGENT) : ((unsigned long long)t << 32);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == (unsigned)t;
+          if (ok) break;
+          if (wall_clock64() > deadline) {
+            __hip_atomic_store(err, 1u, RLX_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = base + q * blockDim.x + threadIdx.x;
+          if (i < npairs) {
+            const int r = i / (H / 2), k = (i - r * (H / 2)) * 2;
+            *reinterpret_cast<unsigned*>(hb + r * ldh + k) = (unsigned)v[q];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- z = h_{t-1} . RW (this wave's 16 units x 4 gates), operands from LDS
+    f4c_t acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f4c_t{0.f, 0.f, 0.f, 0.f};
+    const __bf16* hA = hb + col * ldh + 8 * hgrp;
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8c_t a = *reinterpret_cast<const bf16x8c_t*>(hA + ks * 32);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, rws[((g * NW + wave) * KS + ks) * 64 + lane], acc[g], 0,
+                                                         0, 0);
+    }
+    if (!dbuf) __syncthreads();                            // the next gather overwrites the only h tile
+    // ---- gates, state, outputs, publish h_t
+    gu64* dst = exch + ((long long)tile * 2 + (t & 1)) * npairs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = rg + r;
+      const bool valid = m0 + rr < mb;
+      const float za = acc[0][r] + zv[0][r];
+      float zf = acc[1][r] + zv[1][r];
+      float zo = acc[2][r] + zv[2][r];
+      float zg = acc[3][r] + zv[3][r];
+      const float cp = c[r];
+      if (PEEP) {
+        zf += cp * wff;
+        zg += cp * wgg;
+      }
+      const float a = tanh_c(za), f = sigm_c(zf), g = sigm_c(zg);
+      float cc = f * cp + g * a;
+      if (PEEP) zo += cc * woo;
+      const float o = sigm_c(zo);
+      float h = o * tanh_c(cc) * mv[r];
+      cc *= mv[r];
+      if (!valid) {
+        h = 0.f;
+        cc = 0.f;
+      }
+      c[r] = cc;
+      if (valid) {
+        const long long orow = ((long long)t * mb + m0 + rr) * H;
+        out[orow + j] = h;
+        if (call) call[orow + j] = cc;
+        if (gates) {
+          float* gp = gates + orow * 4 + j;
+          gp[0] = a;
+          gp[H] = f;
+          gp[2 * H] = o;
+          gp[3 * H] = g;
+        }
+      }
+      // granule = {tag t+1, bf16(h[j]) | bf16(h[j+1]) << 16}, written by the even-unit lane of each pair
+      const float hn = __shfl_xor(h, 1, 64);
+      if ((col & 1) == 0) {
+        const __bf16 lo = (__bf16)h, hi = (__bf16)hn;
+        const unsigned pay = (unsigned)(*reinterpret_cast<const unsigned short*>(&lo)) |
+                             ((unsigned)(*reinterpret_cast<const unsigned short*>(&hi)) << 16);
+        __hip_atomic_store(dst + rr * (H / 2) + (j >> 1), ((unsigned long long)(t + 1) << 32) | pay, RLX_AGENT);
+      }
+    }
+    if (t + 1 < Tn) load_step(t + 1);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + rg + r;
+    if (m < mb) {
+      if (cT) cT[(long long)m * H + j] = c[r];
+      if (hT) hT[(long long)m * H + j] = out[((long long)(Tn - 1) * mb + m) * H + j];
+    }
+  }
+  (void)G;
+}
+
+template <int U, bool PEEP>
+static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
+                           const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
+                           unsigned long long* exch, unsigned* err, int Tn, int mb, int H, hipStream_t s) {
+  const int KS = H / 32, NW = U / 16;
+  const size_t lds = (size_t)4 * NW * KS * 64 * 16 + (H <= 256 ? 2ull : 1ull) * 16 * (H + 8) * 2;
+  auto k = lstm_fwd_coop<U, PEEP>;
+  if (lds > 160 * 1024) return -1;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return -1;
+  const dim3 grid(H / U, (mb + 15) / 16), block(64 * NW);
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block.x, lds) != hipSuccess || per < 1) return -1;
+  // one workgroup per CU (LDS-bound); keep a margin: the occupancy API can over-report by one block per CU at high
+  // SGPR counts (MI355X_MICROARCH.md, correctness boundaries), so never rely on more than one block per CU
+  if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;
+  (void)per;
+  const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * 16 * (H / 2) * 8;
+  if (hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
+  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  long long timeout = 200LL * 1000 * 1000;                  // wall_clock64 runs at 100 MHz: 2 s per wait
+  void* args[] = {(void*)&zx, (void*)&rwt, (void*)&peep, (void*)&h0, (void*)&c0, (void*)&mask, (void*)&out,
+                  (void*)&gates, (void*)&call, (void*)&hT, (void*)&cT, (void*)&exch, (void*)&err, (void*)&Tn,
+                  (void*)&mb, (void*)&H, (void*)&timeout};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
+DL4J_API long long dl4j_lstm_coop_exch_bytes(int mb, int H) { return (long long)((mb + 15) / 16) * 2 * 16 * (H / 2) * 8; }
+
+// bf16 only; H in {128, 256} (U = 64) or 512 (U = 32). Returns -1 when the cooperative path does not apply.
+DL4J_API int dl4j_lstm_fwd_coop(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
+                                const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
+                                unsigned long long* exch, unsigned* err, int Tn, int mb, int H, hipStream_t s) {
+  if (Tn < 1 || mb < 1) return -1;
+  const bool pp = peep != nullptr;
+  if (H == 128 || H == 256)
+    return pp ? coop_fwd_launch<64, true>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, s)
+              : coop_fwd_launch<64, false>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H,
+                                           s);
+  if (H == 512)
+    return pp ? coop_fwd_launch<32, true>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, s)
+              : coop_fwd_launch<32, false>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H,
+                                           s);
+  return -1;
+}

@@ -6,6 +6,8 @@ h·RW, fused gates + peepholes + mask, cell state in registers). ``lstm_seq_bwd`
 (gate deltas + dh = dz·RWᵀ per step) and returns the fp32 gate deltas for the weight GEMMs. Both return
 ``None`` when the shape/dtype is outside the kernels (the caller then runs the per-step path).
 """
+import ctypes
+
 import torch
 
 from . import native
@@ -41,6 +43,34 @@ def _f32c(t):
     return None if t is None else t.detach().to(torch.float32).contiguous()
 
 
+_SIG_COOP = [c_void_p] * 13 + [c_int, c_int, c_int, c_void_p]
+
+
+def _coop_enabled():
+    import os
+    return os.environ.get("DL4J_AMD_LSTM_COOP", "1") == "1"
+
+
+def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
+    """Cooperative multi-workgroup kernel (csrc/lstm_coop.hip, RW resident in LDS); False if it does not apply."""
+    native.register_sig("dl4j_lstm_fwd_coop", _SIG_COOP)
+    native.register_sig("dl4j_lstm_coop_exch_bytes", [c_int, c_int])
+    lib.dl4j_lstm_coop_exch_bytes.restype = ctypes.c_longlong
+    nbytes = lib.dl4j_lstm_coop_exch_bytes(mb, H)
+    exch = torch.empty(nbytes // 8, dtype=torch.int64, device=zx.device)
+    err = torch.empty(1, dtype=torch.int32, device=zx.device)
+    rc = lib.dl4j_lstm_fwd_coop(_ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c), _ptr(m), _ptr(out), _ptr(gates),
+                                _ptr(call), _ptr(hT), _ptr(cT), _ptr(exch), _ptr(err), T, mb, H, c_void_p(_stream()))
+    if rc != 0:
+        return False
+    global last_coop_err
+    last_coop_err = err                                  # device word: 1 = a hand-off wait timed out
+    return True
+
+
+last_coop_err = None
+
+
 def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=True):
     """zx: [T, mb, 4H] (compute dtype, = x·W + b); RW: [H, 4H(+3)] view.
     Returns (out [T, mb, H] fp32, hT, cT, gates [T,mb,4H] fp32 | None, call [T,mb,H] fp32 | None) or None."""
@@ -63,6 +93,9 @@ def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=Tr
     cT = torch.empty(mb, H, device=dev, dtype=torch.float32)
     gates = torch.empty(T, mb, 4 * H, device=dev, dtype=torch.float32) if need_cache else None
     call = torch.empty(T, mb, H, device=dev, dtype=torch.float32) if need_cache else None
+    if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
+            _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
+        return out, hT, cT, gates, call
     rc = lib.dl4j_lstm_fwd(1 if dt == torch.bfloat16 else 0, _ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c),
                            _ptr(m), _ptr(out), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), T, mb, H,
                            c_void_p(_stream()))

@@ -99,3 +99,26 @@ def test_samediff_lstm_layer_gpu_matches_cpu(cuda, peep):
     _close(hg, hc, 1e-4)
     for k in base:
         _close(gg[k], gc[k], 1e-3)
+
+
+@pytest.mark.parametrize("H,mb,peep", [(256, 32, True), (256, 37, False), (512, 20, True)])
+def test_lstm_coop_kernel_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb, peep):
+    """Cooperative multi-workgroup forward (RW resident in LDS, granule hand-offs) == the single-workgroup kernel."""
+    from deeplearning4j_amd.ops import rnn_native
+    g = torch.Generator().manual_seed(H + mb)
+    T = 23
+    zx = (torch.randn(T, mb, 4 * H, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    RW = (torch.randn(H, 4 * H + (3 if peep else 0), generator=g) * (2.0 / H ** 0.5)).to(torch.bfloat16).to(cuda)
+    h0 = torch.randn(mb, H, generator=g).to(cuda) * 0.3
+    c0 = torch.randn(mb, H, generator=g).to(cuda) * 0.3
+    mask = (torch.rand(mb, T, generator=g) > 0.1).float().to(cuda)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_LSTM_COOP", flag)
+        rnn_native.last_coop_err = None
+        res[flag] = rnn_native.lstm_seq_fwd(zx, RW, H, peep, h0, c0, mask, True)
+        if flag == "1":
+            assert rnn_native.last_coop_err is not None, "cooperative kernel did not run"
+            assert int(rnn_native.last_coop_err.item()) == 0, "hand-off wait timed out"
+    for a, b in zip(res["1"], res["0"]):
+        _close(a, b, 1e-5)
