@@ -3,7 +3,7 @@ from .dataset import (DataSet, DataSetIterator, ExistingDataSetIterator, Iterato
                       ListDataSetIterator, MultiDataSet, MultiDataSetIterator, SplitTestAndTrain)
 from .iterators import (AsyncDataSetIterator, AsyncMultiDataSetIterator, BenchmarkDataSetIterator,
                         BenchmarkMultiDataSetIterator, DoublesDataSetIterator, EarlyTerminationDataSetIterator,
-                        KFoldIterator, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
+                        KFoldIterator, MultiDataSetIteratorAdapter, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
                         FileDataSetIterator, ReconstructionDataSetIterator)
 from .fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator, LFWDataSetIterator,  # noqa
                        MnistDataSetIterator, TinyImageNetDataSetIterator, UciSequenceDataSetIterator)

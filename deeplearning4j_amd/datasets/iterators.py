@@ -229,6 +229,47 @@ class EarlyTerminationDataSetIterator(DataSetIterator):
         return self.base.batch()
 
 
+class MultiDataSetIteratorAdapter:
+    """Presents a DataSetIterator as a MultiDataSetIterator (reference
+    datasets/iterator/impl/MultiDataSetIteratorAdapter.java:13-61): each DataSet becomes a single-input,
+    single-output MultiDataSet, so ComputationGraph APIs that take MultiDataSets accept plain iterators."""
+
+    def __init__(self, iter):
+        self.iter = iter
+        self.preProcessor = None
+
+    def hasNext(self):
+        return self.iter.hasNext()
+
+    def next(self, num=None):
+        from .dataset import MultiDataSet
+        ds = self.iter.next() if num is None else self.iter.next(num)
+        m = MultiDataSet.fromDataSet(ds)
+        if self.preProcessor is not None:
+            self.preProcessor.preProcess(m)
+        return m
+
+    def __iter__(self):
+        self.reset()
+        while self.hasNext():
+            yield self.next()
+
+    def reset(self):
+        self.iter.reset()
+
+    def resetSupported(self):
+        return getattr(self.iter, "resetSupported", lambda: True)()
+
+    def asyncSupported(self):
+        return getattr(self.iter, "asyncSupported", lambda: True)()
+
+    def setPreProcessor(self, p):
+        self.preProcessor = p
+
+    def getPreProcessor(self):
+        return self.preProcessor
+
+
 class SamplingDataSetIterator(DataSetIterator):
     def __init__(self, sampleFrom, batchSize, totalNumberSamples, seed=None):
         self.ds = sampleFrom

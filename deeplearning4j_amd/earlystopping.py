@@ -475,7 +475,9 @@ class EarlyStoppingTrainer:
             while self.iterator.hasNext():
                 ds = self.iterator.next()
                 try:
-                    self.model.fit(ds)
+                    if not self._fit_one(ds, it_count):
+                        it_count += 1
+                        continue
                 except Exception as e:   # reference: return an Error result with the best model so far
                     log.warning("Early stopping training terminated due to exception at epoch %d, iteration %d: %s",
                                 epoch, it_count, e)
@@ -487,6 +489,7 @@ class EarlyStoppingTrainer:
                         if cond.terminate(s):
                             term, reason = True, cond
                             break
+                    term = self._agree(term)
                 if term:
                     break
                 it_count += 1
@@ -527,6 +530,14 @@ class EarlyStoppingTrainer:
                         return res
             epoch += 1
 
+    def _fit_one(self, ds, it_count):
+        """Fit one minibatch; returns False when this process skipped it (data-parallel sharding)."""
+        self.model.fit(ds)
+        return True
+
+    def _agree(self, flag):
+        return flag
+
     def _best(self):
         try:
             return self.esConfig.modelSaver.getBestModel()
@@ -535,3 +546,55 @@ class EarlyStoppingTrainer:
 
 
 EarlyStoppingGraphTrainer = EarlyStoppingTrainer
+
+
+class EarlyStoppingParallelTrainer(EarlyStoppingTrainer):
+    """Early stopping over a data-parallel ParallelWrapper (reference: deeplearning4j-scaleout-parallelwrapper
+    ``EarlyStoppingParallelTrainer.java:51-120``, which wraps a ParallelWrapper with ``workers`` /
+    ``averagingFrequency`` and checks termination conditions from an averaging listener).
+
+    Here the "workers" are the ``torch.distributed`` ranks (one process per GPU, RCCL all-reduce of the flat
+    gradient, or parameter averaging every ``averagingFrequency`` steps). Minibatch i of an epoch is fitted by
+    rank ``i % world_size``; with shared gradients the replicas hold identical parameters, so every rank computes
+    the same validation score and takes the same termination decision without extra communication. On one
+    process this is exactly EarlyStoppingTrainer."""
+
+    def __init__(self, esConfig, net, train, trainMulti=None, listener=None, workers=None, prefetchBuffer=16,
+                 averagingFrequency=1, reportScoreAfterAveraging=True, useLegacyAveraging=True, trainingMode=None):
+        from .parallel.wrapper import ParallelWrapper, TrainingMode
+        super().__init__(esConfig, net, train if train is not None else trainMulti, listener)
+        mode = trainingMode if trainingMode is not None else TrainingMode.SHARED_GRADIENTS
+        self.wrapper = ParallelWrapper(net, workers=workers, prefetchBuffer=prefetchBuffer,
+                                       averagingFrequency=averagingFrequency,
+                                       reportScoreAfterAveraging=reportScoreAfterAveraging, trainingMode=mode)
+
+    def _fit_one(self, ds, it_count):
+        # rank r fits batch r of every group of W consecutive batches; a trailing partial group is dropped so every
+        # rank takes the same number of (collective) steps
+        from .parallel.distributed import rank, world_size
+        W = world_size()
+        self.wrapper._prepare()
+        if W == 1:
+            self.wrapper._step(ds)
+            return True
+        if it_count == 0:
+            self._group = []
+        self._group.append(ds)
+        if len(self._group) < W:
+            return False
+        mine, self._group = self._group[rank()], []
+        self.wrapper._step(mine)
+        return True
+
+    def _agree(self, flag):
+        # iteration scores differ per rank (different minibatches): terminate when any rank's condition fires
+        from .parallel.distributed import all_reduce_max, world_size
+        if world_size() == 1:
+            return flag
+        return bool(all_reduce_max(1.0 if flag else 0.0) > 0)
+
+    def fit(self):
+        res = super().fit()
+        from .parallel.distributed import barrier
+        barrier()
+        return res

@@ -1108,6 +1108,12 @@ class FrozenLayer(BaseWrapperLayer):
         return 0.0
 
 
+class FrozenLayerWithBackprop(FrozenLayer):
+    """FrozenLayer variant whose backprop still produces the input epsilon (later DL4J releases'
+    FrozenLayerWithBackprop; this reference snapshot only has FrozenLayer.java)."""
+    RUNTIME = "deeplearning4j_amd.nn.layers.misc:FrozenLayerWithBackpropImpl"
+
+
 class MaskLayer(NoParamLayer):
     RUNTIME = "deeplearning4j_amd.nn.layers.misc:MaskLayerImpl"
 

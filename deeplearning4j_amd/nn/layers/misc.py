@@ -35,6 +35,18 @@ class FrozenLayerImpl(LayerImpl):
         return getattr(self.inner, name)
 
 
+class FrozenLayerWithBackpropImpl(FrozenLayerImpl):
+    """Frozen parameters, but the epsilon still flows to earlier layers (so layers below a frozen block keep
+    training): the wrapped layer's backprop runs for its input gradient and its parameter gradient is discarded."""
+
+    def backpropGradient(self, eps, **kw):
+        self.bind()
+        _, eps_in = self.inner.backpropGradient(eps, **kw)
+        for v in self.grads.values():
+            v.zero_()
+        return self.make_gradient(), eps_in
+
+
 class MaskLayerImpl(LayerImpl):
     """Applies the current feature mask to activations (and to epsilons in backprop)."""
 

@@ -120,3 +120,26 @@ def run_w2v(rank, world, port, result_path):
         sim_out = w2v.similarity("alpha1", "beta2")
         torch.save({"same": same, "in": sim_in, "out": sim_out, "n": w2v.vocab().numWords()}, result_path)
     dist.destroy_process_group()
+
+
+def run_es_parallel(rank, world, port, result_path):
+    """EarlyStoppingParallelTrainer over 2 gloo ranks: replicas must end identical and agree on termination."""
+    _setup(rank, world, port)
+    from deeplearning4j_amd import Adam, ListDataSetIterator
+    from deeplearning4j_amd.earlystopping import (DataSetLossCalculator, EarlyStoppingConfiguration,
+                                                  EarlyStoppingParallelTrainer, InMemoryModelSaver,
+                                                  MaxEpochsTerminationCondition)
+    net = make_net(Adam(0.02))
+    train = ListDataSetIterator(make_batches(7, 8), 8)          # 7 batches: trailing partial group dropped
+    val = ListDataSetIterator(make_batches(2, 16, seed=9), 16)
+    conf = (EarlyStoppingConfiguration.Builder().epochTerminationConditions(MaxEpochsTerminationCondition(3))
+            .scoreCalculator(DataSetLossCalculator(val, True)).modelSaver(InMemoryModelSaver()).build())
+    res = EarlyStoppingParallelTrainer(conf, net, train).fit()
+    p = net.params().clone()
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        torch.save({"params": [t.clone() for t in gathered], "iters": net.getIterationCount(),
+                    "epochs": res.getTotalEpochs(), "scores": dict(res.getScoreVsEpoch())}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

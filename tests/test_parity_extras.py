@@ -1,0 +1,91 @@
+"""EarlyStoppingParallelTrainer (single process + gloo world_size 2), FrozenLayerWithBackprop and
+MultiDataSetIteratorAdapter."""
+import os
+import socket
+import sys
+
+import torch
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(__file__))
+import _dist_workers as W  # noqa: E402
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_early_stopping_parallel_single_process():
+    from deeplearning4j_amd import Adam, ListDataSetIterator
+    from deeplearning4j_amd.earlystopping import (DataSetLossCalculator, EarlyStoppingConfiguration,
+                                                  EarlyStoppingParallelTrainer, MaxEpochsTerminationCondition,
+                                                  TerminationReason)
+    net = W.make_net(Adam(0.05))
+    train = ListDataSetIterator(W.make_batches(6, 8), 8)
+    val = ListDataSetIterator(W.make_batches(2, 16, seed=9), 16)
+    conf = (EarlyStoppingConfiguration.Builder().epochTerminationConditions(MaxEpochsTerminationCondition(4))
+            .scoreCalculator(DataSetLossCalculator(val, True)).build())
+    res = EarlyStoppingParallelTrainer(conf, net, train, workers=1).fit()
+    assert res.getTerminationReason() == TerminationReason.EpochTerminationCondition
+    assert res.getTotalEpochs() == 4
+    sc = res.getScoreVsEpoch()
+    assert sc[3] < sc[0]
+    assert net.getIterationCount() == 24
+    assert res.getBestModel() is not None
+
+
+def test_early_stopping_parallel_two_ranks(tmp_path):
+    path = str(tmp_path / "es.pt")
+    mp.spawn(W.run_es_parallel, args=(2, _port(), path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    p0, p1 = r["params"]
+    assert torch.allclose(p0, p1, atol=1e-6)               # shared gradients keep the replicas identical
+    assert r["iters"] == 9                                   # 3 epochs x floor(7 / 2) steps per rank
+    assert r["epochs"] == 3
+
+
+def test_frozen_layer_with_backprop():
+    from deeplearning4j_amd import (Activation, DenseLayer, LossFunction, MultiLayerNetwork, NeuralNetConfiguration,
+                                    OutputLayer, Sgd)
+    from deeplearning4j_amd.nn.conf.layers import FrozenLayer, FrozenLayerWithBackprop
+
+    def build(wrapper):
+        conf = (NeuralNetConfiguration.Builder().seed(3).updater(Sgd(0.1)).list()
+                .layer(0, DenseLayer.Builder().nIn(4).nOut(6).activation(Activation.TANH).build())
+                .layer(1, wrapper(DenseLayer.Builder().nIn(6).nOut(6).activation(Activation.TANH).build()))
+                .layer(2, OutputLayer.Builder(LossFunction.MSE).nIn(6).nOut(2).activation(Activation.IDENTITY)
+                       .build())
+                .build())
+        net = MultiLayerNetwork(conf)
+        net.init(device=torch.device("cpu"))
+        return net
+
+    g = torch.Generator().manual_seed(0)
+    x, y = torch.randn(16, 4, generator=g), torch.randn(16, 2, generator=g)
+    for wrapper, below_trains in ((FrozenLayerWithBackprop, True), (FrozenLayer, False)):
+        net = build(wrapper)
+        p0 = {k: v.clone() for k, v in net.paramTable().items()}
+        net.fit(x, y)
+        p1 = net.paramTable()
+        assert torch.equal(p0["1_W"], p1["1_W"]) and torch.equal(p0["1_b"], p1["1_b"])
+        assert not torch.equal(p0["2_W"], p1["2_W"])
+        assert (not torch.equal(p0["0_W"], p1["0_W"])) == below_trains
+    # JSON round trip keeps the wrapper type
+    net = build(FrozenLayerWithBackprop)
+    from deeplearning4j_amd import MultiLayerConfiguration
+    c2 = MultiLayerConfiguration.fromJson(net.getLayerWiseConfigurations().toJson())
+    assert type(c2.getConf(1)).__name__ == "FrozenLayerWithBackprop"
+
+
+def test_multidataset_iterator_adapter():
+    from deeplearning4j_amd import ListDataSetIterator
+    from deeplearning4j_amd.datasets import MultiDataSetIteratorAdapter
+    it = MultiDataSetIteratorAdapter(ListDataSetIterator(W.make_batches(3, 4), 4))
+    got = list(it)
+    assert len(got) == 3
+    m = got[0]
+    assert len(m.features) == 1 and len(m.labels) == 1 and m.features[0].shape == (4, 5)
+    it.reset()
+    assert it.hasNext()
