@@ -7,6 +7,8 @@ import torch
 def as_tensor(x, dtype=None):
     if x is None:
         return None
+    if hasattr(x, "toTensor"):                           # nd4j.INDArray
+        x = x.toTensor()
     if torch.is_tensor(x):
         return x if dtype is None else x.to(dtype)
     t = torch.from_numpy(np.ascontiguousarray(x))

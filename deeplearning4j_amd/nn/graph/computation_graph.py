@@ -208,6 +208,7 @@ class ComputationGraph(BaseNetwork):
             if not torch.is_tensor(x):
                 import numpy as np
                 x = torch.from_numpy(np.asarray(x))
+            x = x.toTensor() if hasattr(x, "toTensor") else x
             out.append(self._to_dev(x, self._feat_dtype()) if x.is_floating_point() else self._to_dev(x))
         return out
 

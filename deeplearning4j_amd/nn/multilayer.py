@@ -91,6 +91,7 @@ class MultiLayerNetwork(BaseNetwork):
     def feedForwardToLayer(self, layerNum, x, train=False, fmask=None, stored_state=False,
                            store_last_for_tbptt=False):
         """Activations of layers 0..layerNum (inclusive); index 0 of the returned list is the input."""
+        x = x.toTensor() if hasattr(x, "toTensor") else x
         x = self._to_dev(x, self._feat_dtype()) if x.is_floating_point() else self._to_dev(x)
         mb = x.shape[0]
         acts = [x]

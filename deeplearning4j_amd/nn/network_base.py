@@ -431,6 +431,8 @@ class BaseNetwork:
     def _to_dev(self, t, dtype=None):
         if t is None:
             return None
+        if hasattr(t, "toTensor"):                       # nd4j.INDArray
+            t = t.toTensor()
         if not torch.is_tensor(t):
             import numpy as np
             t = torch.from_numpy(np.asarray(t))

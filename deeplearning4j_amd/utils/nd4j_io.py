@@ -47,7 +47,9 @@ def _read_buffer(inp):
 
 
 def write(arr, out, order="c"):
-    """Write a tensor/ndarray in ND4J's binary format to a binary stream ``out``."""
+    """Write a tensor/ndarray/INDArray in ND4J's binary format to a binary stream ``out``."""
+    if hasattr(arr, "toTensor"):
+        arr = arr.toTensor()
     if torch.is_tensor(arr):
         t = arr.detach().cpu()
         if t.dtype == torch.bfloat16:
@@ -101,96 +103,5 @@ def from_bytes(b):
     return read(io.BytesIO(b))
 
 
-class Nd4j:
-    """Minimal factory namespace mirroring the ND4J calls DL4J user code makes."""
-    write = staticmethod(write)
-    read = staticmethod(read)
-
-    @staticmethod
-    def create(*shape, dtype=torch.float32):
-        if len(shape) == 1 and isinstance(shape[0], (list, tuple, np.ndarray)):
-            return torch.tensor(np.asarray(shape[0]), dtype=dtype)
-        return torch.zeros(*shape, dtype=dtype)
-
-    @staticmethod
-    def zeros(*shape, dtype=torch.float32):
-        return torch.zeros(*shape, dtype=dtype)
-
-    @staticmethod
-    def ones(*shape, dtype=torch.float32):
-        return torch.ones(*shape, dtype=dtype)
-
-    @staticmethod
-    def rand(*shape, seed=None):
-        g = torch.Generator().manual_seed(seed) if seed is not None else None
-        return torch.rand(*shape, generator=g)
-
-    @staticmethod
-    def randn(*shape, seed=None):
-        g = torch.Generator().manual_seed(seed) if seed is not None else None
-        return torch.randn(*shape, generator=g)
-
-    @staticmethod
-    def linspace(a, b, n):
-        return torch.linspace(a, b, n)
-
-    @staticmethod
-    def hstack(*xs):
-        return torch.cat(xs, dim=1)
-
-    @staticmethod
-    def vstack(*xs):
-        return torch.cat(xs, dim=0)
-
-    @staticmethod
-    def concat(dim, *xs):
-        return torch.cat(xs, dim=dim)
-
-    @staticmethod
-    def getRandom():
-        return torch.random
-
-    @staticmethod
-    def argMax(x, dim):
-        return torch.argmax(x, dim=dim)
-
-    # ------------------------------------------------------------------ executioner / memory (SURVEY §5.1-5.2)
-    @staticmethod
-    def getExecutioner():
-        from ..profiling import getExecutioner
-        return getExecutioner()
-
-    @staticmethod
-    def getWorkspaceManager():
-        from ..memory import getWorkspaceManager
-        return getWorkspaceManager()
-
-    @staticmethod
-    def getMemoryManager():
-        return _MemoryManager()
-
-
-class _MemoryManager:
-    """Nd4j.getMemoryManager(): memset / current workspace / device memory info."""
-
-    @staticmethod
-    def memset(t):
-        with torch.no_grad():
-            t.zero_()
-
-    @staticmethod
-    def getCurrentWorkspace():
-        from ..memory import getWorkspaceManager
-        return getWorkspaceManager().getCurrentWorkspace()
-
-    @staticmethod
-    def invokeGc():
-        if torch.cuda.is_available() and torch.cuda.is_initialized():
-            torch.cuda.empty_cache()
-
-    @staticmethod
-    def getDeviceMemoryInfo(device=0):
-        """(free, total) bytes of the device (hipMemGetInfo)."""
-        if not torch.cuda.is_available():
-            return (0, 0)
-        return torch.cuda.mem_get_info(device)
+# The Nd4j factory namespace lives in deeplearning4j_amd.nd4j (INDArray API); re-exported for existing imports.
+from ..nd4j.factory import Nd4j  # noqa: E402,F401

@@ -8,7 +8,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_lstm.py -x -v --timeout 120
 tail -3 gpurun_out/pytest_lstm.log
 timeout -k 10 300 python tools/bench_lstm.py --steps 5 --warmup 2 > gpurun_out/bench_lstm.log 2>&1 || { echo BENCH_FAIL; tail -30 gpurun_out/bench_lstm.log; exit 1; }
 tail -1 gpurun_out/bench_lstm.log
-DL4J_AMD_KERNEL_LSTM=0 timeout -k 10 300 python tools/bench_lstm.py --steps 3 --warmup 1 > gpurun_out/bench_lstm_perstep.log 2>&1 || { echo BENCH2_FAIL; tail -30 gpurun_out/bench_lstm_perstep.log; exit 1; }
-tail -1 gpurun_out/bench_lstm_perstep.log
+DL4J_AMD_LSTM_COOP=0 timeout -k 10 300 python tools/bench_lstm.py --steps 5 --warmup 2 > gpurun_out/bench_lstm_nocoop.log 2>&1 || { echo BENCH2_FAIL; tail -30 gpurun_out/bench_lstm_nocoop.log; exit 1; }
+tail -1 gpurun_out/bench_lstm_nocoop.log
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_lstm" -o run -- python3 "$GRAFT_REPO_ROOT/tools/bench_lstm.py" --steps 2 --warmup 1 > "$GRAFT_REPO_ROOT/gpurun_out/prof_lstm.log" 2>&1 || { echo PROF_FAIL; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/prof_lstm.log"; exit 1; }
 echo PROF_OK

@@ -64,3 +64,17 @@ def test_device_workspace_arena(cuda):
                 assert ws.external_bytes == 0           # learned after the first cycle
     assert ws.stats()["capacity"] >= 1024 * 256 * 2 + 4096 * 4
     mgr.destroyAllWorkspacesForCurrentThread()
+
+
+def test_indarray_lives_on_device_and_matches_cpu(cuda):
+    from deeplearning4j_amd.nd4j import Nd4j as N, Transforms
+    a = N.rand(64, 96, seed=1)
+    b = N.rand(96, 32, seed=2)
+    assert a.toTensor().is_cuda and N.getAffinityManager().getDeviceForArray(a) == 0
+    c = a.mmul(b)
+    ref = a.toTensor().cpu().double() @ b.toTensor().cpu().double()
+    assert torch.allclose(c.toTensor().cpu().double(), ref, rtol=1e-2, atol=1e-2)
+    s = Transforms.softmax(c)
+    assert abs(s.sum(1).toTensor().cpu() - 1).max() < 1e-5
+    f = a.dup("f")
+    assert f.ordering() == "f" and f.toTensor().is_cuda and f.equals(a)
