@@ -233,6 +233,238 @@ static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, c
   return 0;
 }
 
+// ------------------------------------------------------------------------------------------------ backward
+// Cooperative backward time loop. The per-step product dh_{t-1} = dz_t . RW^T (K = 4H gate columns) is split over
+// the G = H/U workgroups of a tile BY K: workgroup g owns the 4U gate columns of its U hidden units, so its slice
+// of dz_t is produced locally (no exchange of dz), and its RW slice (RW[n][own gate columns] for all H outputs n,
+// 128 KB at H = 256 / U = 64) stays resident in LDS. Each workgroup computes a PARTIAL dh (16 rows x H, fp32) and
+// publishes it as {tag, fp32} granules addressed to the workgroup that owns each output unit; the owner sums the G
+// partials of its units in a fixed producer order (deterministic) directly into the lanes that need them for the
+// next step's gate deltas. Exchange per workgroup per step: 16 x H granules in, 16 x H out (vs 16 x 4H for
+// gathering dz), fp32 partials (no bf16 rounding of dh). Same hand-off/timeout/cooperative-launch rules as the
+// forward.
+template <int U, int H, bool PEEP>
+__global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
+    const float* __restrict__ eps, const float* __restrict__ gates, const float* __restrict__ call,
+    const float* __restrict__ c0, const __bf16* __restrict__ rw, const float* __restrict__ peep,
+    const float* __restrict__ mask, const float* __restrict__ dh_last, const float* __restrict__ dc_last,
+    float* __restrict__ dz, float* __restrict__ dh0, float* __restrict__ dc0, unsigned long long* exch_raw,
+    unsigned* err_raw, int Tn, int mb, int t_end, long long timeout_ticks) {
+  constexpr int NW = U / 16, G = H / U, NTW = (H / 16) / NW, KL = 4 * U / 32, KSG = 4 * H / 32, LDZ = 4 * U + 8;
+  constexpr int NE = 4 * G, BATCH = NE < 16 ? NE : 16;     // partial granules gathered per lane per step
+  constexpr int H4 = 4 * H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16x8c_t* rws = reinterpret_cast<bf16x8c_t*>(smem);                       // [H/16][KL][64] fragments
+  __bf16* zbuf = reinterpret_cast<__bf16*>(smem + (size_t)(H / 16) * KL * 64 * 16);   // [2][16][LDZ]
+  gu64* exch = (gu64*)exch_raw;
+  gu32* err = (gu32*)err_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
+  const int grp = blockIdx.x, tile = blockIdx.y;
+  const int m0 = tile * 16, u0 = grp * U;
+  const int ul = wave * 16 + col;                          // this lane's unit within the workgroup's U
+  const int j = u0 + ul;
+  // ---- resident RW slice: B[k][n] = RW[n][k] for k in this workgroup's gate columns, all n
+  for (int i = threadIdx.x; i < (H / 16) * KL * 64; i += blockDim.x) {
+    const int ln = i & 63, t1 = i >> 6;
+    const int sl = t1 % KL, nt = t1 / KL;
+    const int kg = ((32 * sl) / U) * (H / 32) + (u0 + (32 * sl) % U) / 32;   // global k-step of local k-step sl
+    rws[i] = *reinterpret_cast<const bf16x8c_t*>(rw + (((long long)nt * KSG + kg) * 64 + ln) * 8);
+  }
+  int mrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mrow[r] = min(m0 + rg + r, mb - 1);
+  float dhn[4], dcn[4], wff = 0.f, woo = 0.f, wgg = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool v = m0 + rg + r < mb;
+    dhn[r] = (dh_last && v) ? dh_last[(long long)mrow[r] * H + j] : 0.f;
+    dcn[r] = (dc_last && v) ? dc_last[(long long)mrow[r] * H + j] : 0.f;
+  }
+  if (PEEP) {
+    wff = peep[j];
+    woo = peep[H + j];
+    wgg = peep[2 * H + j];
+  }
+  float ev[4], av[4], fv[4], ov[4], gv[4], cv[4], pv[4], mv[4];
+  auto load_step = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long hrow = ((long long)t * mb + mrow[r]) * H, grow = hrow * 4;
+      ev[r] = eps[hrow + j];
+      av[r] = gates[grow + j];
+      fv[r] = gates[grow + H + j];
+      ov[r] = gates[grow + 2 * H + j];
+      gv[r] = gates[grow + 3 * H + j];
+      cv[r] = call[hrow + j];
+      pv[r] = t > 0 ? call[hrow - (long long)mb * H + j] : (c0 ? c0[(long long)mrow[r] * H + j] : 0.f);
+      mv[r] = mask ? mask[(long long)mrow[r] * Tn + t] : 1.f;
+    }
+  };
+  const long long slot_sz = (long long)G * G * 16 * U;     // granules per (tile, slot)
+  // sum of the G partials of (rows rg..rg+3, unit ul) published with tag `tag` into slot tag-1 & 1
+  auto gather = [&](int tag, float* res) {
+    const gu64* src = exch + ((long long)tile * 2 + ((tag - 1) & 1)) * slot_sz + (long long)grp * G * 16 * U;
+    const long long deadline = wall_clock64() + timeout_ticks;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) res[r] = 0.f;
+#pragma unroll
+    for (int b0 = 0; b0 < NE; b0 += BATCH) {
+      unsigned long long v[BATCH];
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+          const int e = b0 + q, g = e >> 2, r = e & 3;     // producer-major: fixed summation order per unit
+          v[q] = __hip_atomic_load(src + ((long long)g * 16 + rg + r) * U + ul, RLX_AGENT);
+        }
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) ok &= (unsigned)(v[q] >> 32) == (unsigned)tag;
+        if (ok) break;
+        if (wall_clock64() > deadline) {
+          __hip_atomic_store(err, 1u, RLX_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int q = 0; q < BATCH; ++q) res[(b0 + q) & 3] += __uint_as_float((unsigned)v[q]);
+    }
+  };
+  load_step(Tn - 1);
+  int it = 0;
+  for (int t = Tn - 1; t >= t_end; --t, ++it) {
+    if (it > 0) gather(it, dhn);                           // dh_t from the previous iteration's partials
+    __bf16* zb = zbuf + (it & 1) * 16 * LDZ;
+    float dza[4], dzf[4], dzo[4], dzg[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool valid = m0 + rg + r < mb;
+      const float dh = (ev[r] + dhn[r]) * mv[r];
+      float dc = dcn[r] * mv[r];
+      const float a = av[r], f = fv[r], o = ov[r], g = gv[r];
+      const float ca = tanh_c(cv[r]);
+      const float zo_ = dh * ca * o * (1.f - o);
+      dc += dh * o * (1.f - ca * ca);
+      if (PEEP) dc += zo_ * woo;
+      const float zf_ = dc * pv[r] * f * (1.f - f);
+      const float zg_ = dc * a * g * (1.f - g);
+      const float za_ = dc * g * (1.f - a * a);
+      float dcp = dc * f;
+      if (PEEP) dcp += zf_ * wff + zg_ * wgg;
+      dcn[r] = valid ? dcp : 0.f;
+      dza[r] = valid ? za_ : 0.f;
+      dzf[r] = valid ? zf_ : 0.f;
+      dzo[r] = valid ? zo_ : 0.f;
+      dzg[r] = valid ? zg_ : 0.f;
+    }
+    if (t - 1 >= t_end) load_step(t - 1);                  // next step's HBM operands in flight now
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = rg + r;
+      zb[rr * LDZ + ul] = (__bf16)dza[r];
+      zb[rr * LDZ + U + ul] = (__bf16)dzf[r];
+      zb[rr * LDZ + 2 * U + ul] = (__bf16)dzo[r];
+      zb[rr * LDZ + 3 * U + ul] = (__bf16)dzg[r];
+      if (m0 + rr < mb) {
+        float* dp = dz + ((long long)t * mb + m0 + rr) * H4 + j;
+        dp[0] = dza[r];
+        dp[H] = dzf[r];
+        dp[2 * H] = dzo[r];
+        dp[3 * H] = dzg[r];
+      }
+    }
+    __syncthreads();
+    if (t == t_end && !dh0) break;                         // nobody consumes the last partials
+    // ---- partial dh (16 rows x this wave's NTW output tiles) over the local gate columns
+    f4c_t acc[NTW];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4c_t{0.f, 0.f, 0.f, 0.f};
+    const __bf16* zA = zb + col * LDZ + 8 * hgrp;
+#pragma unroll
+    for (int sl = 0; sl < KL; ++sl) {
+      const bf16x8c_t a = *reinterpret_cast<const bf16x8c_t*>(zA + sl * 32);
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, rws[((wave * NTW + nt) * KL + sl) * 64 + lane], acc[nt],
+                                                          0, 0, 0);
+    }
+    // ---- publish: granule {tag it+1, fp32 partial} at [consumer][producer grp][row][unit in consumer]
+    gu64* dst = exch + ((long long)tile * 2 + (it & 1)) * slot_sz;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wave * NTW + nt) * 16 + col;
+      const int cons = n / U, un = n - cons * U;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __hip_atomic_store(dst + (((long long)cons * G + grp) * 16 + rg + r) * U + un,
+                           ((unsigned long long)(it + 1) << 32) | __float_as_uint(acc[nt][r]), RLX_AGENT);
+    }
+  }
+  const int iters = Tn - t_end;
+  if (dh0) gather(iters, dhn);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + rg + r;
+    if (m < mb) {
+      if (dh0) dh0[(long long)m * H + j] = dhn[r];
+      if (dc0) dc0[(long long)m * H + j] = dcn[r];
+    }
+  }
+}
+
+template <int U, int H, bool PEEP>
+static int coop_bwd_launch(const float* eps, const float* gates, const float* call, const float* c0, const void* rw,
+                           const float* peep, const float* mask, const float* dhl, const float* dcl, float* dz,
+                           float* dh0, float* dc0, unsigned long long* exch, unsigned* err, int Tn, int mb, int t_end,
+                           hipStream_t s) {
+  const size_t lds = (size_t)(H / 16) * (4 * U / 32) * 64 * 16 + 2ull * 16 * (4 * U + 8) * 2;
+  auto k = lstm_bwd_coop<U, H, PEEP>;
+  if (lds > 160 * 1024) return -1;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return -1;
+  const dim3 grid(H / U, (mb + 15) / 16), block(4 * U);
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block.x, lds) != hipSuccess || per < 1) return -1;
+  if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;    // one workgroup per CU, with margin
+  const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * (H / U) * 16 * H * 8;
+  if (hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
+  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  long long timeout = 200LL * 1000 * 1000;                  // 2 s per wait at 100 MHz
+  const __bf16* rwp = reinterpret_cast<const __bf16*>(rw);
+  void* args[] = {(void*)&eps, (void*)&gates, (void*)&call, (void*)&c0, (void*)&rwp, (void*)&peep, (void*)&mask,
+                  (void*)&dhl, (void*)&dcl, (void*)&dz, (void*)&dh0, (void*)&dc0, (void*)&exch, (void*)&err,
+                  (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
+DL4J_API long long dl4j_lstm_coop_bwd_exch_bytes(int mb, int H) {
+  const int U = H == 512 ? 32 : 64;
+  return (long long)((mb + 15) / 16) * 2 * (H / U) * 16 * H * 8;
+}
+
+// bf16 RW only; H in {256 (U = 64), 512 (U = 32)}. Returns -1 when the cooperative path does not apply.
+DL4J_API int dl4j_lstm_bwd_coop(const float* eps, const float* gates, const float* call, const float* c0,
+                                const void* rw, const float* peep, const float* mask, const float* dh_last,
+                                const float* dc_last, float* dz, float* dh0, float* dc0, unsigned long long* exch,
+                                unsigned* err, int Tn, int mb, int H, int t_end, hipStream_t s) {
+  if (Tn < 1 || mb < 1 || t_end < 0 || t_end >= Tn) return -1;
+  const bool pp = peep != nullptr;
+#define BWD_ARGS eps, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, exch, err, Tn, mb, t_end, s
+  if (H == 256) return pp ? coop_bwd_launch<64, 256, true>(BWD_ARGS) : coop_bwd_launch<64, 256, false>(BWD_ARGS);
+  if (H == 512) return pp ? coop_bwd_launch<32, 512, true>(BWD_ARGS) : coop_bwd_launch<32, 512, false>(BWD_ARGS);
+#undef BWD_ARGS
+  return -1;
+}
+
 DL4J_API long long dl4j_lstm_coop_exch_bytes(int mb, int H) { return (long long)((mb + 15) / 16) * 2 * 16 * (H / 2) * 8; }
 
 // bf16 only; H in {128, 256} (U = 64) or 512 (U = 32). Returns -1 when the cooperative path does not apply.

@@ -70,6 +70,29 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, 
 
 last_coop_err = None
 
+_SIG_BWD_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, c_int, c_void_p]
+
+
+def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, mb, H, t_end):
+    """Cooperative backward (csrc/lstm_coop.hip: K-split partial dh exchange, RW slice resident in LDS)."""
+    native.register_sig("dl4j_lstm_bwd_coop", _SIG_BWD_COOP)
+    native.register_sig("dl4j_lstm_coop_bwd_exch_bytes", [c_int, c_int])
+    lib.dl4j_lstm_coop_bwd_exch_bytes.restype = ctypes.c_longlong
+    nbytes = lib.dl4j_lstm_coop_bwd_exch_bytes(mb, H)
+    exch = torch.empty(nbytes // 8, dtype=torch.int64, device=e.device)
+    err = torch.empty(1, dtype=torch.int32, device=e.device)
+    rc = lib.dl4j_lstm_bwd_coop(_ptr(e), _ptr(gates), _ptr(call), _ptr(c0c), _ptr(rw), _ptr(peep), _ptr(m), _ptr(dhl),
+                                _ptr(dcl), _ptr(dz), _ptr(dh0), _ptr(dc0), _ptr(exch), _ptr(err), T, mb, H, int(t_end),
+                                c_void_p(_stream()))
+    if rc != 0:
+        return False
+    global last_coop_bwd_err
+    last_coop_bwd_err = err
+    return True
+
+
+last_coop_bwd_err = None
+
 
 def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=True):
     """zx: [T, mb, 4H] (compute dtype, = x·W + b); RW: [H, 4H(+3)] view.
@@ -121,6 +144,10 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
     dz = (torch.zeros if t_end > 0 else torch.empty)(T, mb, 4 * H, device=dev, dtype=torch.float32)
     dh0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
     dc0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
+    if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
+            _bwd_coop(lib, e, gates, call, _f32c(c0), rw, peep, m, _f32c(dh_last), _f32c(dc_last), dz, dh0, dc0, T, mb,
+                      H, t_end):
+        return dz, dh0, dc0
     rc = lib.dl4j_lstm_bwd(1 if dt == torch.bfloat16 else 0, _ptr(e), _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
                            _ptr(rw), _ptr(peep), _ptr(m), _ptr(_f32c(dh_last)), _ptr(_f32c(dc_last)), _ptr(dz),
                            _ptr(dh0), _ptr(dc0), T, mb, H, int(t_end), c_void_p(_stream()))

@@ -122,3 +122,32 @@ def test_lstm_coop_kernel_matches_single_workgroup_kernel(cuda, monkeypatch, H, 
             assert int(rnn_native.last_coop_err.item()) == 0, "hand-off wait timed out"
     for a, b in zip(res["1"], res["0"]):
         _close(a, b, 1e-5)
+
+
+@pytest.mark.parametrize("H,mb,peep,t_end", [(256, 32, True, 0), (256, 37, False, 5), (512, 20, True, 0)])
+def test_lstm_coop_bwd_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb, peep, t_end):
+    """Cooperative backward (K-split partial dh exchange) == the single-workgroup backward kernel, incl. TBPTT
+    truncation (t_end), carried dh/dc and masks. Partial sums are fp32 (the single-WG kernel rounds nothing else
+    differently), so only the summation order differs."""
+    from deeplearning4j_amd.ops import rnn_native
+    g = torch.Generator().manual_seed(H + mb + t_end)
+    T = 19
+    zx = (torch.randn(T, mb, 4 * H, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    RW = (torch.randn(H, 4 * H + (3 if peep else 0), generator=g) * (2.0 / H ** 0.5)).to(torch.bfloat16).to(cuda)
+    c0 = torch.randn(mb, H, generator=g).to(cuda) * 0.3
+    mask = (torch.rand(mb, T, generator=g) > 0.1).float().to(cuda)
+    monkeypatch.setenv("DL4J_AMD_LSTM_COOP", "0")
+    _, _, _, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peep, None, c0, mask, True)
+    eps = torch.randn(T, mb, H, generator=g).to(cuda)
+    dhl = torch.randn(mb, H, generator=g).to(cuda) * 0.2
+    dcl = torch.randn(mb, H, generator=g).to(cuda) * 0.2
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_LSTM_COOP", flag)
+        rnn_native.last_coop_bwd_err = None
+        res[flag] = rnn_native.lstm_seq_bwd(eps, gates, call, c0, RW, H, peep, mask, dhl, dcl, t_end)
+        if flag == "1":
+            assert rnn_native.last_coop_bwd_err is not None, "cooperative backward did not run"
+            assert int(rnn_native.last_coop_bwd_err.item()) == 0, "hand-off wait timed out"
+    for a, b in zip(res["1"], res["0"]):
+        _close(a, b, 2e-3)
