@@ -449,3 +449,252 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
   }
   return (int)hipGetLastError();
 }
+
+// -------------------------------------------------------------------------------------------- BN + ReLU + max pool
+// Fused stem tail (ResNet: conv7x7 -> BN -> ReLU -> maxpool 3x3/2). The BN output is never materialised:
+//   forward  : pooled = max over the window of relu(x*scale + shift); per pooled element also stores the window
+//              argmax byte (index | 0x80 when the max is > 0, i.e. the ReLU is active there) and x_hat at the
+//              argmax (bf16/fp32 like x).
+//   backward : (1) dbeta = sum(dy_p * active), dgamma = sum(dy_p * active * x_hat_p) over the POOLED tensor only:
+//              every input position receives the pooled gradients routed to it, and the routing is linear, so the
+//              BN reductions over the full-resolution gradient equal these sums over the pooled one;
+//              (2) one gather pass over x: g = sum of the active pooled gradients whose argmax is this position,
+//              dx = scale * (g - dbeta/M - x_hat * dgamma/M).
+// Replaces bn_apply + pool_fwd (fwd) and pool_bwd + bn_bwd_partial + bn_bwd_apply (bwd): ~2.6 fewer full-size
+// passes over the conv output.
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool_fwd(const T* __restrict__ x, T* __restrict__ y,
+                                                  unsigned char* __restrict__ am, T* __restrict__ xh,
+                                                  const float* __restrict__ ctx, int N, int H, int W, int C, int OH,
+                                                  int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  const int CG = C >> 3;
+  const long long total = (long long)N * OH * OW * CG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    long long r = t / CG;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float sc[8], sf[8], best[8], bx[8];
+    unsigned char idx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = ctx[2 * C + cg * 8 + i];
+      sf[i] = ctx[3 * C + cg * 8 + i];
+      best[i] = -INFINITY;
+      bx[i] = 0.f;
+      idx[i] = 0;
+    }
+    for (int i = 0; i < kh; ++i) {
+      const int ih = oh * sh - pt + i;
+      if (ih < 0 || ih >= H) continue;
+      for (int j = 0; j < kw; ++j) {
+        const int iw = ow * sw - pl + j;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        Vec8<T>::load(x + (((long long)n * H + ih) * W + iw) * C + cg * 8, v);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float a = fmaxf(v[c] * sc[c] + sf[c], 0.f);
+          if (a > best[c]) {                               // first maximum wins, as in pool_fwd
+            best[c] = a;
+            bx[c] = v[c];
+            idx[c] = (unsigned char)(i * kw + j);
+          }
+        }
+      }
+    }
+    Vec8<T>::store(y + t * 8, best);
+    if (am) {
+      unsigned long long pk = 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        pk |= ((unsigned long long)(idx[c] | (best[c] > 0.f ? 0x80 : 0))) << (8 * c);
+      *reinterpret_cast<unsigned long long*>(am + t * 8) = pk;
+    }
+    if (xh) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bx[c] = (bx[c] - ctx[cg * 8 + c]) * ctx[C + cg * 8 + c];
+      Vec8<T>::store(xh + t * 8, bx);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool_bwd_partial(const T* __restrict__ dy, const unsigned char* __restrict__ am,
+                                                          const T* __restrict__ xh, long long M, int C,
+                                                          long long rows_per_blk, float* __restrict__ part_db,
+                                                          float* __restrict__ part_dg) {
+  const int T8 = C >> 3;
+  const int R = 256 / T8;
+  const int cg = threadIdx.x % T8, r0 = threadIdx.x / T8;
+  float db[8], dg[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    db[i] = 0.f;
+    dg[i] = 0.f;
+  }
+  const long long rbeg = (long long)blockIdx.x * rows_per_blk;
+  long long rend = rbeg + rows_per_blk;
+  if (rend > M) rend = M;
+  if (r0 < R) {
+    for (long long r = rbeg + r0; r < rend; r += R) {
+      const long long o = r * C + cg * 8;
+      float gv[8], hv[8];
+      Vec8<T>::load(dy + o, gv);
+      Vec8<T>::load(xh + o, hv);
+      const unsigned long long pk = *reinterpret_cast<const unsigned long long*>(am + o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = ((pk >> (8 * i)) & 0x80) ? gv[i] : 0.f;
+        db[i] += d;
+        dg[i] += d * hv[i];
+      }
+    }
+  }
+  __shared__ float red1[2048];
+  __shared__ float red2[2048];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red1[threadIdx.x * 8 + i] = (r0 < R) ? db[i] : 0.f;
+    red2[threadIdx.x * 8 + i] = (r0 < R) ? dg[i] : 0.f;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c >> 3, k = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      a += red1[(rr * T8 + g) * 8 + k];
+      b += red2[(rr * T8 + g) * 8 + k];
+    }
+    part_db[(long long)blockIdx.x * C + c] = a;
+    part_dg[(long long)blockIdx.x * C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool_bwd_dx(const T* __restrict__ x, const T* __restrict__ dy,
+                                                     const unsigned char* __restrict__ am, T* __restrict__ dx,
+                                                     const float* __restrict__ ctx, const float* __restrict__ cdb,
+                                                     const float* __restrict__ cdg, int N, int H, int W, int C, int OH,
+                                                     int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  const int CG = C >> 3;
+  const long long total = (long long)N * H * W * CG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    long long r = t / CG;
+    const int iw = (int)(r % W);
+    r /= W;
+    const int ih = (int)(r % H);
+    const int n = (int)(r / H);
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+    const int hp = ih + pt, wp = iw + pl;
+    int oh0 = hp - kh + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
+    int ow0 = wp - kw + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
+    const int oh1 = min(hp / sh, OH - 1), ow1 = min(wp / sw, OW - 1);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const long long o = (((long long)n * OH + oh) * OW + ow) * C + cg * 8;
+        float g[8];
+        Vec8<T>::load(dy + o, g);
+        const unsigned long long pk = *reinterpret_cast<const unsigned long long*>(am + o);
+        const unsigned me = 0x80u | (unsigned)((hp - oh * sh) * kw + (wp - ow * sw));
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (((pk >> (8 * c)) & 0xff) == me) acc[c] += g[c];
+      }
+    }
+    float xv[8];
+    Vec8<T>::load(x + t * 8, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cg * 8 + i;
+      const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
+      xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
+    }
+    Vec8<T>::store(dx + t * 8, xv);
+  }
+}
+
+static inline int ew_grid(long long total) {
+  long long g = (total + 255) / 256;
+  if (g > 256 * 32) g = 256 * 32;
+  return (int)(g < 1 ? 1 : g);
+}
+
+// x: conv output NHWC [N,H,W,C]; y: pooled [N,OH,OW,C]; am / xh: per pooled element (training only, may be null).
+// ws: >= dl4j_bn_workspace_floats(N*H*W, C). ctx_out: 4*C floats.
+DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* am, void* xh, int N, int H, int W,
+                              int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
+                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
+                              float* run_var, float decay, float eps, int training, float* ws, float* ctx_out,
+                              hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127 || kh < 1 || kw < 1) return -1;
+  const long long M = (long long)N * H * W;
+  int nblk;
+  long long rpb;
+  bn_grid(M, C, &nblk, &rpb);
+  float* p1 = ws;
+  float* p2 = ws + (long long)nblk * C;
+  float* q = p2 + (long long)nblk * C;
+  const dim3 fg((C + 63) / 64);
+  const int pg = ew_grid((long long)N * OH * OW * (C / 8));
+  if (dtype == 1) {
+    const bf16* xb = (const bf16*)x;
+    if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
+    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
+    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
+                       run_mean, run_var, decay, eps, training, ctx_out);
+    hipLaunchKernelGGL(bnpool_fwd<bf16>, dim3(pg), dim3(256), 0, s, xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C,
+                       OH, OW, kh, kw, sh, sw, pt, pl);
+  } else {
+    const float* xf = (const float*)x;
+    if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
+    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
+    hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
+                       run_mean, run_var, decay, eps, training, ctx_out);
+    hipLaunchKernelGGL(bnpool_fwd<float>, dim3(pg), dim3(256), 0, s, xf, (float*)y, am, (float*)xh, ctx_out, N, H, W,
+                       C, OH, OW, kh, kw, sh, sw, pt, pl);
+  }
+  return (int)hipGetLastError();
+}
+
+// dy: gradient w.r.t. the pooled output; dx: w.r.t. x (the BN input). ws: >= dl4j_bn_workspace_floats(N*OH*OW, C).
+DL4J_API int dl4j_bn_pool_bwd(int dtype, const void* x, const void* dy, const unsigned char* am, const void* xh,
+                              void* dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw,
+                              int pt, int pl, const float* ctx, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127) return -1;
+  const long long Mp = (long long)N * OH * OW, M = (long long)N * H * W;
+  int nblk;
+  long long rpb;
+  bn_grid(Mp, C, &nblk, &rpb);
+  float* p1 = ws;
+  float* p2 = ws + (long long)nblk * C;
+  float* q = p2 + (long long)nblk * C;
+  float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
+  float* cdg = cdb + C;
+  const int g = ew_grid(M * (C / 8));
+  if (dtype == 1)
+    hipLaunchKernelGGL(bnpool_bwd_partial<bf16>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, am, (const bf16*)xh,
+                       Mp, C, rpb, p1, p2);
+  else
+    hipLaunchKernelGGL(bnpool_bwd_partial<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, am,
+                       (const float*)xh, Mp, C, rpb, p1, p2);
+  bn_reduce_stage(p1, p2, nblk, C, q, s);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
+                     cdg);
+  if (dtype == 1)
+    hipLaunchKernelGGL(bnpool_bwd_dx<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am, (bf16*)dx,
+                       ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+  else
+    hipLaunchKernelGGL(bnpool_bwd_dx<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
+                       (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+  return (int)hipGetLastError();
+}

@@ -67,6 +67,8 @@ class ComputationGraph(BaseNetwork):
         * BN -> ActivationLayer(ReLU)                      => ReLU inside the BN apply kernel
         * BN -> ElementWiseVertex(Add, shortcut) -> ReLU   => y = relu(bn(x) + shortcut) in ONE kernel
           (every ResNet bottleneck block); backward emits d(shortcut) from the same pass.
+        * BN -> ReLU -> SubsamplingLayer(MAX)             => BN + ReLU + max pool in one pass (ResNet stem); the
+          backward takes the BN reductions over the pooled gradient and gathers dx in one more pass.
         Fused-away vertices become passthroughs: forward copies the producer's activation, backward routes
         epsilon to that single producer. Also computes which vertices need an input gradient at all
         (nothing trainable upstream => skip dL/dinput, e.g. the stem conv's backward-data)."""
@@ -83,6 +85,16 @@ class ComputationGraph(BaseNetwork):
             return isinstance(vv, LayerVertex) and isinstance(vv.layerConf, ActivationLayer) and \
                 isinstance(vv.layerConf.activation, ActivationReLU) and vv.preProcessor is None and \
                 vv.layerConf.idropout is None and len(self.vertex_inputs[n]) == 1
+
+        def is_max_pool(n):
+            from ..conf.layers import SubsamplingLayer
+            vv = self.conf.vertices.get(n)
+            if not (isinstance(vv, LayerVertex) and type(vv.layerConf) is SubsamplingLayer) or \
+                    vv.preProcessor is not None or vv.layerConf.idropout is not None or \
+                    len(self.vertex_inputs[n]) != 1:
+                return False
+            lc = vv.layerConf
+            return lc.poolingType.value == "MAX" and tuple(lc.dilation) == (1, 1)
 
         for name in self.topo:
             v = self.conf.vertices[name]
@@ -110,6 +122,12 @@ class ComputationGraph(BaseNetwork):
             if is_relu_layer(nxt_name) and nxt_name not in self.outputs:
                 self.layers_by_name[name].fuse_relu = True
                 self._passthrough[nxt_name] = name
+                # BN -> ReLU -> max SubsamplingLayer (ResNet stem): pool inside the BN pass as well
+                pc = self.consumers[nxt_name]
+                if len(pc) == 1 and pc[0] not in self.outputs and is_max_pool(pc[0]) and \
+                        os.environ.get("DL4J_AMD_FUSE_POOL", "1") == "1":
+                    self.layers_by_name[name].fuse_pool = self.layers_by_name[pc[0]]
+                    self._passthrough[pc[0]] = nxt_name
         # ZeroPadding -> Convolution(Truncate): fold the zero padding into the convolution's own (possibly
         # asymmetric) padding, so the padded activation is never materialised (ResNet-50 stem: a 40M-element copy)
         from ..conf.layers import ConvolutionLayer, ZeroPaddingLayer

@@ -35,11 +35,28 @@ class BatchNormalizationImpl(LayerImpl):
             raise ValueError(f"BatchNormalization on activations of rank {x.dim()} not supported {self.layerId()}")
         g, b = self._gb()
         c = self.conf
+        pool = getattr(self, "fuse_pool", None)
+        if pool is not None and x.dim() == 4:
+            # planner fused the following ReLU and max SubsamplingLayer: BN -> ReLU -> pool in one pass
+            from .convolution import compute_pad4
+            pc = pool.conf
+            pad4 = compute_pad4(pc, x.shape[2], x.shape[3], pc.kernelSize, pc.stride, pc.dilation)
+            y, self._ctx = ops.bn_pool_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay,
+                                               c.eps, tuple(pc.kernelSize), tuple(pc.stride), pad4)
+            self._pool_fused = True
+            self._track_deferred_bias(training)
+            return y
+        self._pool_fused = False
         # the reference BN layer applies no activation function of its own (BatchNormalization.java:225,398)
         res = getattr(self, "residual", None)
         y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
                                       relu=self.fuse_relu, residual=res)
         self.residual = None
+        self._track_deferred_bias(training)
+        return y
+
+    def _track_deferred_bias(self, training):
+        c = self.conf
         db = getattr(self, "deferred_bias", None)
         if training and db is not None:
             # the producing conv skipped its bias (it cancels in the batch statistics): the running mean must
@@ -47,11 +64,14 @@ class BatchNormalizationImpl(LayerImpl):
             with torch.no_grad():
                 rm = self.params["mean"]
                 rm.add_(db.params["b"].reshape(rm.shape).to(rm.dtype), alpha=1.0 - c.decay)
-        return y
 
     def backpropGradient(self, eps):
         gg, gb = self.grads.get("gamma"), self.grads.get("beta")
-        dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx, gg, gb)
+        if getattr(self, "_pool_fused", False):
+            dx, dgamma, dbeta = ops.bn_pool_backward(eps, self._ctx, gg, gb)
+            self.dresidual = None
+        else:
+            dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx, gg, gb)
         if gg is not None:
             if dgamma is not gg:
                 copy_grad_(gg, dgamma)

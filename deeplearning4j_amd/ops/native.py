@@ -305,6 +305,60 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     return dx, dgamma, dbeta, dres
 
 
+def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel, stride, pad4):
+    """Fused BN -> ReLU -> max pool (csrc/batchnorm.hip bnpool_*). x: NHWC conv output. Returns (y_pooled, ctx)."""
+    dt = _dt(x)
+    if dt is None or x.dim() != 4 or not torch.is_tensor(gamma) or run_mean.dtype != torch.float32:
+        return None
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return None
+    N, C, H, W = x.shape
+    if C % 8 != 0 or C // 8 > 256:
+        return None
+    kh, kw = kernel
+    sh, sw = stride
+    pt, pb, pl, pr = pad4
+    OH = (H + pt + pb - kh) // sh + 1
+    OW = (W + pl + pr - kw) // sw + 1
+    if OH < 1 or OW < 1 or kh * kw > 127:
+        return None
+    lib = load()
+    register_sig("dl4j_bn_pool_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 +
+                 [c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p,
+                  c_void_p, c_void_p])
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    am = torch.empty(N * OH * OW * C, dtype=torch.uint8, device=x.device) if training else None
+    xh = torch.empty_like(y) if training else None
+    ws = torch.empty(lib.dl4j_bn_workspace_floats(N * H * W, C), dtype=torch.float32, device=x.device)
+    ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+    b = beta if torch.is_tensor(beta) else None
+    rc = lib.dl4j_bn_pool_fwd(dt, _ptr(x), _ptr(y), _ptr(am), _ptr(xh), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
+                              _ptr(gamma), _ptr(b), 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
+                              _ptr(run_var), float(decay), float(eps), 1 if training else 0, _ptr(ws), _ptr(ctx),
+                              _stream())
+    if rc == -1:
+        return None
+    _check(rc, "bn_pool_fwd")
+    return y, ("NATIVE_POOL", x, ctx, am, xh, (kh, kw, sh, sw, pt, pl), (OH, OW))
+
+
+def bn_pool_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
+    _, x, c, am, xh, (kh, kw, sh, sw, pt, pl), (OH, OW) = ctx
+    N, C, H, W = x.shape
+    dy = _rows_like(dy, xh)
+    lib = load()
+    register_sig("dl4j_bn_pool_bwd", [c_int] + [c_void_p] * 5 + [c_int] * 12 + [c_void_p] * 4 + [c_void_p])
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
+    dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(lib.dl4j_bn_workspace_floats(N * OH * OW, C), dtype=torch.float32, device=x.device)
+    rc = lib.dl4j_bn_pool_bwd(_dt(x), _ptr(x), _ptr(dy), _ptr(am), _ptr(xh), _ptr(dx), N, H, W, C, OH, OW, kh, kw,
+                              sh, sw, pt, pl, _ptr(c), _ptr(dgamma), _ptr(dbeta), _ptr(ws), _stream())
+    _check(rc, "bn_pool_bwd")
+    return dx, dgamma, dbeta
+
+
 # ------------------------------------------------------------------------------------------ softmax-xent
 def softmax_xent(logits, labels, clip_eps):
     dt = _dt(logits)

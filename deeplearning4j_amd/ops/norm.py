@@ -84,6 +84,37 @@ def bn_backward(dy, ctx, dgamma_out=None, dbeta_out=None):
     return dx, dgamma, dbeta, dres
 
 
+def bn_pool_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel, stride, pad4):
+    """Fused BatchNorm -> ReLU -> max pool (the ResNet stem tail). Returns (y_pooled, ctx). On the GPU one HIP
+    pass applies BN+ReLU and pools (the BN output is never materialised); elsewhere it composes the reference
+    ops, so results are identical up to rounding."""
+    if use_native(x, "bn") and x.dim() == 4 and torch.is_tensor(gamma):
+        from . import native
+        r = native.bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel, stride, pad4)
+        if r is not None:
+            return r
+    from .pool import pool2d_forward
+    y_bn, bctx = bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=True)
+    y, pctx = pool2d_forward(y_bn, "MAX", kernel, stride, pad4)
+    return y, ("COMPOSED", bctx, pctx, tuple(x.shape))
+
+
+def bn_pool_backward(dy, ctx, dgamma_out=None, dbeta_out=None):
+    """Returns (dx, dgamma, dbeta) for bn_pool_forward."""
+    if ctx[0] == "NATIVE_POOL":
+        from . import native
+        return native.bn_pool_bwd(dy, ctx, dgamma_out, dbeta_out)
+    from .pool import pool2d_backward
+    _, bctx, pctx, xshape = ctx
+    d = pool2d_backward(dy, pctx)
+    if tuple(d.shape[2:]) != tuple(xshape[2:]):                 # truncated windows: rows/cols never pooled
+        full = torch.zeros(xshape, dtype=d.dtype, device=d.device)
+        full[:, :, :d.shape[2], :d.shape[3]] = d
+        d = full
+    dx, dgamma, dbeta, _ = bn_backward(d, bctx, dgamma_out, dbeta_out)
+    return dx, dgamma, dbeta
+
+
 def bn_forward_inference_only(x, gamma, beta, run_mean, run_var, relu=False):
     y, _ = bn_forward(x, gamma, beta, run_mean, run_var, False, 0.0, 0.0, relu)
     return y

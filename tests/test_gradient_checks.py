@@ -241,6 +241,27 @@ def test_fused_bn_add_relu_residual():
     assert checkGradients(net, input=[x], labels=[y], print_results=True, minAbsoluteError=1e-7)
 
 
+def test_fused_bn_relu_maxpool_stem():
+    """ResNet stem tail: BN -> ReLU -> MaxPool(3x3/2) is planned into the BN layer (pool + relu passthroughs)."""
+    conf = (NeuralNetConfiguration.Builder().seed(3).dataType(DataType.DOUBLE).updater(NoOp())
+            .weightInit(NormalDistribution(0, 0.5)).activation(Activation.IDENTITY).graphBuilder()
+            .addInputs("in").setInputTypes(InputType.convolutional(9, 9, 3))
+            .addLayer("c1", ConvolutionLayer.Builder([3, 3]).nOut(4).build(), "in")
+            .addLayer("bn1", BatchNormalization(), "c1")
+            .addLayer("relu", ActivationLayer(Activation.RELU), "bn1")
+            .addLayer("pool", SubsamplingLayer.Builder(PoolingType.MAX, [3, 3], [2, 2]).build(), "relu")
+            .addLayer("out", OutputLayer.Builder(LossFunction.MSE).nOut(2).activation(Activation.IDENTITY).build(),
+                      "pool")
+            .setOutputs("out").build())
+    net = ComputationGraph(conf)
+    net.init(device=DEV)
+    assert net._passthrough == {"relu": "bn1", "pool": "relu"}
+    assert net.layers_by_name["bn1"].fuse_pool is net.layers_by_name["pool"]
+    x = torch.randn(3, 3, 9, 9, dtype=torch.float64)
+    y = torch.randn(3, 2, dtype=torch.float64)
+    assert checkGradients(net, input=[x], labels=[y], print_results=True, minAbsoluteError=1e-7)
+
+
 def test_resnet_style_residual_graph():
     conf = (NeuralNetConfiguration.Builder().seed(1).dataType(DataType.DOUBLE).updater(NoOp())
             .weightInit(NormalDistribution(0, 0.5)).activation(Activation.IDENTITY)
