@@ -89,4 +89,4 @@ def test_resnet_stem_fusion_in_network_matches_unfused(cuda, monkeypatch):
             assert net.layers_by_name["bn1"]._ctx[0] == "NATIVE_POOL", "fused HIP kernel did not run"
         res.append((out0, net.params().clone()))
     _close(res[0][0], res[1][0], 2e-2)
-    _close(res[0][1], res[1][1], 2e-3)
+    _close(res[0][1], res[1][1], 1e-2)                         # one bf16 ulp at |p| ~ 1 is 7.8e-3
