@@ -634,8 +634,8 @@ static inline int ew_grid(long long total) {
 DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* am, void* xh, int N, int H, int W,
                               int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                               const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
-                              float* run_var, float decay, float eps, int training, float* ws, float* ctx_out,
-                              hipStream_t s) {
+                              float* run_var, float decay, float eps, int training, const float* tstats,
+                              long long P, float* ws, float* ctx_out, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127 || kh < 1 || kw < 1) return -1;
   const long long M = (long long)N * H * W;
   int nblk;
@@ -646,6 +646,21 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
   float* q = p2 + (long long)nblk * C;
   const dim3 fg((C + 63) / 64);
   const int pg = ew_grid((long long)N * OH * OW * (C / 8));
+  if (dtype == 1 && training && tstats) {
+    // statistics already reduced per 64-row tile by the producing conv's epilogue (ws sized for P tiles)
+    nblk = (int)((P + 31) / 32);
+    p2 = ws + (long long)nblk * C;
+    q = p2 + (long long)nblk * C;
+    const bf16* xb = (const bf16*)x;
+    hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, nblk), dim3(256), 0, s, tstats, P, C, M, xb, p1,
+                       p2);
+    bn_reduce_stage(p1, p2, nblk, C, q, s);
+    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
+                       run_mean, run_var, decay, eps, 1, ctx_out);
+    hipLaunchKernelGGL(bnpool_fwd<bf16>, dim3(pg), dim3(256), 0, s, xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C,
+                       OH, OW, kh, kw, sh, sw, pt, pl);
+    return (int)hipGetLastError();
+  }
   if (dtype == 1) {
     const bf16* xb = (const bf16*)x;
     if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);

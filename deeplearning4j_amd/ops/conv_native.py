@@ -9,8 +9,10 @@ Coverage (everything else returns ``None`` and ``ops.conv`` uses the library pat
 Weights are re-laid-out once per parameter version (KRSC for forward, flipped CRSK for backward-data).
 """
 import ctypes
+import os
 
 import numpy as np
+
 import torch
 
 from . import native
@@ -173,6 +175,12 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
         return None
     N, C, H, W = x.shape
     K, Cw, R, S = w.shape
+    if C == 3 and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
+        from . import conv_stem
+        if conv_stem.supported(_cl(x), w, b, stride, pad4, dilation):
+            y = conv_stem.forward(_cl(x), w, want_stats)
+            if y is not None:
+                return y
     if C != Cw or C % 8 != 0 or K % 4 != 0:
         return None
     OH, OW = _out_hw(H, W, R, S, stride, pad4, dilation)

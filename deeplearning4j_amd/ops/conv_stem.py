@@ -1,0 +1,57 @@
+"""ResNet stem convolution (7x7 / stride 2 / pad 3, 3 -> 64 channels, NHWC bf16) on the dedicated MFMA kernel in
+csrc/conv_stem.hip (the generic implicit-GEMM kernels need C % 8 == 0). Weight layout for the kernel: B[k][n] with
+k = r*24 + s*3 + c (K padded to 192), fragment-packed as [4 n-tiles][6 k-steps][64 lanes][8]."""
+import torch
+
+from . import native
+from .native import _ptr, _stream, c_int, c_void_p
+
+_packed = {}
+
+
+def supported(x, w, b, stride, pad4, dilation):
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    N, C, H, W = x.shape
+    if tuple(w.shape) != (64, 3, 7, 7) or C != 3 or b is not None:
+        return False
+    if tuple(stride) != (2, 2) or tuple(pad4) != (3, 3, 3, 3) or tuple(dilation) != (1, 1):
+        return False
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    return OH % 4 == 0 and (4 * OW) % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+def pack_weights(w):
+    """[64, 3, 7, 7] -> fragment-packed bf16 [4, 6, 64, 8] (cached per weight buffer and weight version)."""
+    from .conv_native import WEIGHT_VERSION
+    key = (w.data_ptr(), str(w.device))
+    ent = _packed.get(key)
+    if ent is None:
+        k = torch.arange(147, device=w.device)
+        r, rem = k // 21, k % 21                                    # rem = s*3 + c
+        ent = _packed[key] = {"idx": r * 24 + rem, "full": torch.zeros(192, 64, dtype=torch.bfloat16,
+                                                                       device=w.device),
+                              "pk": torch.empty(4, 6, 64, 8, dtype=torch.bfloat16, device=w.device), "v": -1}
+    if ent["v"] != WEIGHT_VERSION[0]:
+        src = w.permute(2, 3, 1, 0).reshape(147, 64)               # rows (r, s, c)
+        ent["full"].index_copy_(0, ent["idx"], src)
+        ent["pk"].copy_(ent["full"].view(6, 4, 8, 4, 16).permute(3, 0, 1, 4, 2).reshape(4, 6, 64, 8))
+        ent["v"] = WEIGHT_VERSION[0]
+    return ent["pk"]
+
+
+def forward(x, w, want_stats=False):
+    N, _, H, W = x.shape
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    lib = native.load()
+    native.register_sig("dl4j_stem_conv_fwd", [c_void_p] * 4 + [c_int] * 5 + [c_void_p])
+    y = torch.empty((N, 64, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    ts = torch.empty((3, N * OH * OW // 64, 64), dtype=torch.float32, device=x.device) if want_stats else None
+    rc = lib.dl4j_stem_conv_fwd(_ptr(x), _ptr(pack_weights(w)), _ptr(y), _ptr(ts), N, H, W, OH, OW,
+                                c_void_p(_stream()))
+    if rc == -1:
+        return None
+    native._check(rc, "stem_conv_fwd")
+    if ts is not None:
+        y._bn_tile_stats = (ts, ts.shape[1])
+    return y

@@ -324,18 +324,28 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
         return None
     lib = load()
     register_sig("dl4j_bn_pool_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 +
-                 [c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p,
-                  c_void_p, c_void_p])
+                 [c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p, c_ll,
+                  c_void_p, c_void_p, c_void_p])
     y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     am = torch.empty(N * OH * OW * C, dtype=torch.uint8, device=x.device) if training else None
     xh = torch.empty_like(y) if training else None
-    ws = torch.empty(lib.dl4j_bn_workspace_floats(N * H * W, C), dtype=torch.float32, device=x.device)
+    ts = getattr(x, "_bn_tile_stats", None)
+    M = N * H * W
+    if not (training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128)):
+        ts = None
+    nws = lib.dl4j_bn_workspace_floats(M, C)
+    if ts is not None:
+        register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
+        lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
+        nws = max(nws, lib.dl4j_bn_tiles_workspace_floats(ts[1], C))
+    ws = torch.empty(nws, dtype=torch.float32, device=x.device)
     ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
     b = beta if torch.is_tensor(beta) else None
     rc = lib.dl4j_bn_pool_fwd(dt, _ptr(x), _ptr(y), _ptr(am), _ptr(xh), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
                               _ptr(gamma), _ptr(b), 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
-                              _ptr(run_var), float(decay), float(eps), 1 if training else 0, _ptr(ws), _ptr(ctx),
-                              _stream())
+                              _ptr(run_var), float(decay), float(eps), 1 if training else 0,
+                              _ptr(ts[0] if ts is not None else None), int(ts[1]) if ts is not None else 0, _ptr(ws),
+                              _ptr(ctx), _stream())
     if rc == -1:
         return None
     _check(rc, "bn_pool_fwd")

@@ -90,3 +90,30 @@ def test_resnet_stem_fusion_in_network_matches_unfused(cuda, monkeypatch):
         res.append((out0, net.params().clone()))
     _close(res[0][0], res[1][0], 2e-2)
     _close(res[0][1], res[1][1], 1e-2)                         # one bf16 ulp at |p| ~ 1 is 7.8e-3
+
+
+@pytest.mark.parametrize("N,H", [(2, 224), (3, 64), (1, 32)])
+def test_stem_conv_kernel_matches_reference(cuda, N, H):
+    """csrc/conv_stem.hip (7x7/2, pad 3, 3->64) vs fp32 F.conv2d, and its epilogue BN tile statistics vs the
+    batch statistics of the output."""
+    from deeplearning4j_amd.ops import conv_native, conv_stem
+    conv_native.bump_version()                                   # packed-weight cache is keyed by buffer + version
+    g = torch.Generator().manual_seed(N * H)
+    x = torch.randn(N, 3, H, H, generator=g).to(torch.bfloat16).to(cuda).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    assert conv_stem.supported(x, w, None, (2, 2), (3, 3, 3, 3), (1, 1))
+    y = conv_stem.forward(x, w, want_stats=True)
+    assert y is not None
+    ref = F.conv2d(x.float(), w.float(), None, 2, 3)
+    _close(y, ref, 1e-2)
+    ts, P = y._bn_tile_stats
+    M = N * y.shape[2] * y.shape[3]
+    assert P == M // 64
+    rows = y.permute(0, 2, 3, 1).reshape(-1, 64).float()
+    sh = ts[2]                                                   # [P, 64] per-tile shifts
+    n = 64.0
+    mean_t = sh + ts[0] / n                                      # per-tile means
+    mean = mean_t.mean(0)
+    _close(mean, rows.mean(0), 1e-4)
+    var = ((ts[1] + 2 * (sh - mean) * ts[0] + n * (sh - mean) ** 2).sum(0)) / M
+    _close(var, rows.var(0, unbiased=False), 1e-3)
