@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
   const float* scale = ctx + 2 * C;
   const float* shift = ctx + 3 * C;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(v % T8) * 8;
+    const int c0 = idx_mod(v, T8) * 8;
     float a[8], r[8];
     Vec8<T>::load(x + v * 8, a);
     if (RES) Vec8<T>::load(res + v * 8, r);
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
   const int T8 = C >> 3;
   const float *mean = ctx, *invstd = ctx + C, *scale = ctx + 2 * C, *shift = ctx + 3 * C;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(v % T8) * 8;
+    const int c0 = idx_mod(v, T8) * 8;
     float xv[8], gv[8], rv[8];
     Vec8<T>::load(x + v * 8, xv);
     Vec8<T>::load(dy + v * 8, gv);
@@ -471,12 +471,8 @@ __global__ __launch_bounds__(256) void bnpool_fwd(const T* __restrict__ x, T* __
   const long long total = (long long)N * OH * OW * CG;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % CG);
-    long long r = t / CG;
-    const int ow = (int)(r % OW);
-    r /= OW;
-    const int oh = (int)(r % OH);
-    const int n = (int)(r / OH);
+    int cg, ow, oh, n;
+    idx_decomp4(t, CG, OW, OH, cg, ow, oh, n);
     float sc[8], sf[8], best[8], bx[8];
     unsigned char idx[8];
 #pragma unroll
@@ -519,6 +515,193 @@ __global__ __launch_bounds__(256) void bnpool_fwd(const T* __restrict__ x, T* __
       for (int c = 0; c < 8; ++c) bx[c] = (bx[c] - ctx[cg * 8 + c]) * ctx[C + cg * 8 + c];
       Vec8<T>::store(xh + t * 8, bx);
     }
+  }
+}
+
+// Same as bnpool_fwd for a compile-time window: every window load is issued before any is consumed (clamped
+// addresses + validity flags), so a wave keeps KH*KW 16-byte loads in flight instead of one.
+template <typename T, int KH, int KW>
+__global__ __launch_bounds__(256) void bnpool_fwd_k(const T* __restrict__ x, T* __restrict__ y,
+                                                    unsigned char* __restrict__ am, T* __restrict__ xh,
+                                                    const float* __restrict__ ctx, int N, int H, int W, int C, int OH,
+                                                    int OW, int sh, int sw, int pt, int pl) {
+  const int CG = C >> 3;
+  const long long total = (long long)N * OH * OW * CG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    int cg, ow, oh, n;
+    idx_decomp4(t, CG, OW, OH, cg, ow, oh, n);
+    float v[KH * KW][8];
+    bool ok[KH * KW];
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+#pragma unroll
+      for (int j = 0; j < KW; ++j) {
+        const int ih = oh * sh - pt + i, iw = ow * sw - pl + j;
+        ok[i * KW + j] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+        Vec8<T>::load(x + (((long long)n * H + ihc) * W + iwc) * C + cg * 8, v[i * KW + j]);
+      }
+    float sc[8], sf[8], best[8], bx[8];
+    unsigned char idx[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      sc[c] = ctx[2 * C + cg * 8 + c];
+      sf[c] = ctx[3 * C + cg * 8 + c];
+      best[c] = -INFINITY;
+      bx[c] = 0.f;
+      idx[c] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < KH * KW; ++q) {
+      if (!ok[q]) continue;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float a = fmaxf(v[q][c] * sc[c] + sf[c], 0.f);
+        if (a > best[c]) {
+          best[c] = a;
+          bx[c] = v[q][c];
+          idx[c] = (unsigned char)q;
+        }
+      }
+    }
+    Vec8<T>::store(y + t * 8, best);
+    if (am) {
+      unsigned long long pk = 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        pk |= ((unsigned long long)(idx[c] | (best[c] > 0.f ? 0x80 : 0))) << (8 * c);
+      *reinterpret_cast<unsigned long long*>(am + t * 8) = pk;
+    }
+    if (xh) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bx[c] = (bx[c] - ctx[cg * 8 + c]) * ctx[C + cg * 8 + c];
+      Vec8<T>::store(xh + t * 8, bx);
+    }
+  }
+}
+
+// bnpool_bwd_dx when at most 2 windows per dimension contain an input position (kh <= 2*sh, kw <= 2*sw, e.g.
+// 3x3/2): the 4 candidate windows' gradient and argmax loads are issued together with the x load.
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool_bwd_dx2(const T* __restrict__ x, const T* __restrict__ dy,
+                                                      const unsigned char* __restrict__ am, T* __restrict__ dx,
+                                                      const float* __restrict__ ctx, const float* __restrict__ cdb,
+                                                      const float* __restrict__ cdg, int N, int H, int W, int C,
+                                                      int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl) {
+  const int CG = C >> 3;
+  const long long total = (long long)N * H * W * CG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    int cg, iw, ih, n;
+    idx_decomp4(t, CG, W, H, cg, iw, ih, n);
+    const int hp = ih + pt, wp = iw + pl;
+    int oh0 = hp - kh + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
+    int ow0 = wp - kw + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
+    const int oh1 = min(hp / sh, OH - 1), ow1 = min(wp / sw, OW - 1);
+    float g[4][8], xv[8];
+    unsigned long long pk[4];
+    unsigned me[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh0 + a, ow = ow0 + b, q = a * 2 + b;
+        const bool ok = oh <= oh1 && ow <= ow1;
+        const long long o = (((long long)n * OH + min(oh, OH - 1)) * OW + min(ow, OW - 1)) * C + cg * 8;
+        Vec8<T>::load(dy + o, g[q]);
+        pk[q] = *reinterpret_cast<const unsigned long long*>(am + o);
+        me[q] = ok ? (0x80u | (unsigned)((hp - oh * sh) * kw + (wp - ow * sw))) : 0x100u;   // 0x100: never matches
+      }
+    Vec8<T>::load(x + t * 8, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (((pk[q] >> (8 * i)) & 0xff) == me[q]) acc += g[q][i];
+      const int c = cg * 8 + i;
+      const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
+      xv[i] = ctx[2 * C + c] * (acc - cdb[c] - xhat * cdg[c]);
+    }
+    Vec8<T>::store(dx + t * 8, xv);
+  }
+}
+
+// bnpool_bwd_dx2 with the pooled gradient and argmax rows STAGED IN LDS: a workgroup owns 2 input rows of one
+// image, copies the (<= 3) pooled rows whose windows cover them once (coalesced 8/16-byte copies), then gathers
+// the candidate windows from LDS. Cuts the L2->CU traffic of the 4-candidate gather (~4x the pooled tensor) to
+// ~1.5x, leaving the kernel bound by its x read + dx write.
+template <typename T>
+__global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x, const T* __restrict__ dy,
+                                                         const unsigned char* __restrict__ am, T* __restrict__ dx,
+                                                         const float* __restrict__ ctx, const float* __restrict__ cdb,
+                                                         const float* __restrict__ cdg, int N, int H, int W, int C,
+                                                         int OH, int OW, int kh, int kw, int sh, int sw, int pt,
+                                                         int pl, int maxrows) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int CG = C >> 3, RB = 2;
+  const int rows_per_img = (H + RB - 1) / RB;
+  const int n = blockIdx.x / rows_per_img, ih0 = (blockIdx.x - n * rows_per_img) * RB;
+  int oh_lo = ih0 + pt - kh + 1;
+  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + sh - 1) / sh;
+  const int oh_hi = min((min(ih0 + RB, H) - 1 + pt) / sh, OH - 1);
+  const int nrows = oh_hi - oh_lo + 1;                     // <= maxrows (host-checked)
+  T* sdy = reinterpret_cast<T*>(smem);                                        // [maxrows][OW*C]
+  unsigned char* sam = smem + (size_t)maxrows * OW * C * sizeof(T);           // [maxrows][OW*C]
+  const int row_elems = OW * C;
+  if (nrows > 0) {
+    const long long g0 = ((long long)n * OH + oh_lo) * row_elems;
+    const int nv = nrows * row_elems / 8;                  // 8-element vectors
+    for (int i = threadIdx.x; i < nv; i += 256) {
+      if (sizeof(T) == 2)
+        reinterpret_cast<uint4*>(sdy)[i] = reinterpret_cast<const uint4*>(dy + g0)[i];
+      else {
+        reinterpret_cast<uint4*>(sdy)[2 * i] = reinterpret_cast<const uint4*>(dy + g0)[2 * i];
+        reinterpret_cast<uint4*>(sdy)[2 * i + 1] = reinterpret_cast<const uint4*>(dy + g0)[2 * i + 1];
+      }
+      reinterpret_cast<uint2*>(sam)[i] = reinterpret_cast<const uint2*>(am + g0)[i];
+    }
+  }
+  __syncthreads();
+  const int items = min(RB, H - ih0) * W * CG;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int cg = it % CG, q1 = it / CG, iw = q1 % W, ih = ih0 + q1 / W;
+    const int hp = ih + pt, wp = iw + pl;
+    int oh0 = hp - kh + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
+    int ow0 = wp - kw + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
+    const int oh1 = min(hp / sh, OH - 1), ow1 = min(wp / sw, OW - 1);
+    const long long t = (((long long)n * H + ih) * W + iw) * CG + cg;
+    float xv[8], acc[8];
+    Vec8<T>::load(x + t * 8, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh0 + a, ow = ow0 + b;
+        if (oh > oh1 || ow > ow1) continue;
+        const int o = ((oh - oh_lo) * OW + ow) * C + cg * 8;
+        float g[8];
+        Vec8<T>::load(sdy + o, g);
+        const unsigned long long pk = *reinterpret_cast<const unsigned long long*>(sam + o);
+        const unsigned me = 0x80u | (unsigned)((hp - oh * sh) * kw + (wp - ow * sw));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (((pk >> (8 * i)) & 0xff) == me) acc[i] += g[i];
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cg * 8 + i;
+      const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
+      xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
+    }
+    Vec8<T>::store(dx + t * 8, xv);
   }
 }
 
@@ -584,12 +767,8 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx(const T* __restrict__ x, co
   const long long total = (long long)N * H * W * CG;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % CG);
-    long long r = t / CG;
-    const int iw = (int)(r % W);
-    r /= W;
-    const int ih = (int)(r % H);
-    const int n = (int)(r / H);
+    int cg, iw, ih, n;
+    idx_decomp4(t, CG, W, H, cg, iw, ih, n);
     float acc[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[c] = 0.f;
@@ -629,6 +808,20 @@ static inline int ew_grid(long long total) {
   return (int)(g < 1 ? 1 : g);
 }
 
+template <typename T>
+static void bnpool_fwd_launch(const T* x, T* y, unsigned char* am, T* xh, const float* ctx, int N, int H, int W, int C,
+                              int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl, int pg, hipStream_t s) {
+  if (kh == 3 && kw == 3)
+    hipLaunchKernelGGL((bnpool_fwd_k<T, 3, 3>), dim3(pg), dim3(256), 0, s, x, y, am, xh, ctx, N, H, W, C, OH, OW, sh,
+                       sw, pt, pl);
+  else if (kh == 2 && kw == 2)
+    hipLaunchKernelGGL((bnpool_fwd_k<T, 2, 2>), dim3(pg), dim3(256), 0, s, x, y, am, xh, ctx, N, H, W, C, OH, OW, sh,
+                       sw, pt, pl);
+  else
+    hipLaunchKernelGGL(bnpool_fwd<T>, dim3(pg), dim3(256), 0, s, x, y, am, xh, ctx, N, H, W, C, OH, OW, kh, kw, sh, sw,
+                       pt, pl);
+}
+
 // x: conv output NHWC [N,H,W,C]; y: pooled [N,OH,OW,C]; am / xh: per pooled element (training only, may be null).
 // ws: >= dl4j_bn_workspace_floats(N*H*W, C). ctx_out: 4*C floats.
 DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* am, void* xh, int N, int H, int W,
@@ -657,8 +850,7 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
     bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, 1, ctx_out);
-    hipLaunchKernelGGL(bnpool_fwd<bf16>, dim3(pg), dim3(256), 0, s, xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C,
-                       OH, OW, kh, kw, sh, sw, pt, pl);
+    bnpool_fwd_launch<bf16>(xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg, s);
     return (int)hipGetLastError();
   }
   if (dtype == 1) {
@@ -667,16 +859,15 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
     if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, training, ctx_out);
-    hipLaunchKernelGGL(bnpool_fwd<bf16>, dim3(pg), dim3(256), 0, s, xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C,
-                       OH, OW, kh, kw, sh, sw, pt, pl);
+    bnpool_fwd_launch<bf16>(xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg, s);
   } else {
     const float* xf = (const float*)x;
     if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
     if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, training, ctx_out);
-    hipLaunchKernelGGL(bnpool_fwd<float>, dim3(pg), dim3(256), 0, s, xf, (float*)y, am, (float*)xh, ctx_out, N, H, W,
-                       C, OH, OW, kh, kw, sh, sw, pt, pl);
+    bnpool_fwd_launch<float>(xf, (float*)y, am, (float*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg,
+                             s);
   }
   return (int)hipGetLastError();
 }
@@ -705,11 +896,34 @@ DL4J_API int dl4j_bn_pool_bwd(int dtype, const void* x, const void* dy, const un
   bn_reduce_stage(p1, p2, nblk, C, q, s);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
                      cdg);
-  if (dtype == 1)
-    hipLaunchKernelGGL(bnpool_bwd_dx<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am, (bf16*)dx,
-                       ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
-  else
-    hipLaunchKernelGGL(bnpool_bwd_dx<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
-                       (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+  const bool two = kh <= 2 * sh && kw <= 2 * sw;
+  // staged variant: pooled rows covering 2 input rows, all in LDS
+  const int maxrows = (2 - 1 + kh - 1) / sh + 1;
+  const size_t lds = (size_t)maxrows * OW * C * ((dtype == 1 ? 2 : 4) + 1);
+  if (two && lds <= 64 * 1024) {
+    const int nb = N * ((H + 1) / 2);
+    if (dtype == 1)
+      hipLaunchKernelGGL(bnpool_bwd_dx_lds<bf16>, dim3(nb), dim3(256), lds, s, (const bf16*)x, (const bf16*)dy, am,
+                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, maxrows);
+    else
+      hipLaunchKernelGGL(bnpool_bwd_dx_lds<float>, dim3(nb), dim3(256), lds, s, (const float*)x, (const float*)dy, am,
+                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, maxrows);
+    return (int)hipGetLastError();
+  }
+  if (dtype == 1) {
+    if (two)
+      hipLaunchKernelGGL(bnpool_bwd_dx2<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am,
+                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+    else
+      hipLaunchKernelGGL(bnpool_bwd_dx<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am,
+                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+  } else {
+    if (two)
+      hipLaunchKernelGGL(bnpool_bwd_dx2<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
+                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+    else
+      hipLaunchKernelGGL(bnpool_bwd_dx<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
+                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
+  }
   return (int)hipGetLastError();
 }

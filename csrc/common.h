@@ -83,3 +83,30 @@ __device__ __forceinline__ float block_reduce(float v, float* red) {
 }
 
 #define HIP_LAUNCH_CHECK() (hipGetLastError())
+
+// Index decomposition for grid-stride elementwise loops: 64-bit division by a runtime divisor is a long emulated
+// sequence on CDNA, so indices below 2^31 (every realistic activation) take the 32-bit path.
+// t = ((a3 * D2 + a2) * D1 + a1) * D0 + a0
+__device__ __forceinline__ void idx_decomp4(long long t, int D0, int D1, int D2, int& a0, int& a1, int& a2, int& a3) {
+  if (t < 0x7fffffffLL) {
+    unsigned u = (unsigned)t;
+    const unsigned q0 = u / (unsigned)D0;
+    a0 = (int)(u - q0 * (unsigned)D0);
+    const unsigned q1 = q0 / (unsigned)D1;
+    a1 = (int)(q0 - q1 * (unsigned)D1);
+    const unsigned q2 = q1 / (unsigned)D2;
+    a2 = (int)(q1 - q2 * (unsigned)D2);
+    a3 = (int)q2;
+  } else {
+    a0 = (int)(t % D0);
+    long long r = t / D0;
+    a1 = (int)(r % D1);
+    r /= D1;
+    a2 = (int)(r % D2);
+    a3 = (int)(r / D2);
+  }
+}
+
+__device__ __forceinline__ int idx_mod(long long t, int D) {
+  return t < 0x7fffffffLL ? (int)((unsigned)t % (unsigned)D) : (int)(t % D);
+}

@@ -850,12 +850,8 @@ __global__ void conv_w_relayout(const bf16* __restrict__ W, bf16* __restrict__ k
                                 int C, int R, int S) {
   const long long total = (long long)K * C * R * S;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int s = (int)(i % S);
-    long long t = i / S;
-    const int r = (int)(t % R);
-    t /= R;
-    const int c = (int)(t % C);
-    const int k = (int)(t / C);
+    int s, r, c, k;
+    idx_decomp4(i, S, R, C, s, r, c, k);
     const bf16 v = W[i];
     if (krsc) krsc[(((long long)k * R + r) * S + s) * C + c] = v;
     if (flip) flip[(((long long)c * R + (R - 1 - r)) * S + (S - 1 - s)) * K + k] = v;
@@ -893,18 +889,12 @@ __global__ __launch_bounds__(256) void conv_w_relayout_batched(const RelayoutJob
     if (o >= J.n) break;
     long long src;
     if (J.kind == 0) {                    // o = ((k*R + r)*S + s)*C + c
-      const int c = (int)(o % C);
-      long long q = o / C;
-      const int sx = (int)(q % S); q /= S;
-      const int r = (int)(q % R);
-      const int k = (int)(q / R);
+      int c, sx, r, k;
+      idx_decomp4(o, C, S, R, c, sx, r, k);
       src = (((long long)k * C + c) * R + r) * S + sx;
     } else {                              // o = ((c*R + r')*S + s')*K + k, source tap (R-1-r', S-1-s')
-      const int k = (int)(o % K);
-      long long q = o / K;
-      const int sx = (int)(q % S); q /= S;
-      const int r = (int)(q % R);
-      const int c = (int)(q / R);
+      int k, sx, r, c;
+      idx_decomp4(o, K, S, R, k, sx, r, c);
       src = (((long long)k * C + c) * R + (R - 1 - r)) * S + (S - 1 - sx);
     }
     J.out[o] = J.W[src];
@@ -988,12 +978,8 @@ __global__ void conv_wrw_permute(float* __restrict__ ws, float* __restrict__ dW,
                                  int rezero) {
   const long long total = (long long)K * C * R * S;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long long t = i / C;
-    const int s = (int)(t % S);
-    t /= S;
-    const int r = (int)(t % R);
-    const int k = (int)(t / R);
+    int c, s, r, k;
+    idx_decomp4(i, C, S, R, c, s, r, k);
     dW[(((long long)k * C + c) * R + r) * S + s] = ws[i];
     if (rezero) ws[i] = 0.f;
   }

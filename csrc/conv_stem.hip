@@ -6,8 +6,8 @@
 //  * K layout k = r*24 + q, q = s*3 + c (< 21 valid, rows 21..23 and r = 7 are zero weights): for a fixed filter
 //    row r the 21 inputs of an output pixel are CONTIGUOUS in NHWC memory, so every 8-value A fragment is one
 //    contiguous 16-byte LDS read; K = 192 (6 MFMA k-steps of 32).
-//  * A workgroup owns 4 output rows (4*OW pixels) of one image: it stages the 13(+1) input rows it needs once in
-//    LDS (zero padded), keeps the whole 192x64 weight matrix as MFMA B fragments in registers (24 fragments per
+//  * A (persistent) workgroup walks blocks of 4 output rows (4*OW pixels) of one image: it stages the 13(+1) input
+//    rows a block needs in LDS (8-byte copies, zero padded), keeps the whole 192x64 weight matrix as MFMA B fragments in registers (24 fragments per
 //    lane), and emits 64-pixel rounds: 4 waves x 16 pixels x 64 channels with mfma_f32_16x16x32_bf16.
 //  * Each round's 64x64 bf16 tile goes through LDS for 16-byte coalesced stores, and its per-channel BatchNorm
 //    partial statistics (S1, S2 about the round's first pixel) are written in the tile-stats format of
@@ -32,84 +32,102 @@ __global__ void __launch_bounds__(256) stem_conv_fwd(const u16* __restrict__ x, 
   u16* ot = xin + IN_ROWS * RS;                                              // [64][OUT_LD]
   float* red = reinterpret_cast<float*>(ot + 64 * OUT_LD);                   // [2][4][64]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hg = lane >> 4;
-  const int blocks_per_img = OH / ROWS_PER_WG;
-  const int n = blockIdx.x / blocks_per_img, oh0 = (blockIdx.x % blocks_per_img) * ROWS_PER_WG;
-  // ---- weights: B fragments for 4 output-channel tiles x 6 k-steps, resident in registers
+  const int blocks_per_img = OH / ROWS_PER_WG, nblocks = N * blocks_per_img;
+  // ---- weights: B fragments for 4 output-channel tiles x 6 k-steps, resident in registers for all blocks
   bf16x8s_t b[4][KS];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) b[nt][ks] = wpk[(nt * KS + ks) * 64 + lane];
-  // ---- stage input rows ih = 2*oh0 - 3 + rr, columns iw in [-3, RS/3 - 3), zero outside the image.
-  // element (rr, iw, c) at rr*RS + (iw + 3)*3 + c, so the window of output column ow starts at rr*RS + 6*ow.
-  for (int e = threadIdx.x; e < IN_ROWS * RS; e += 256) {
-    const int rr = e / RS, off = e - rr * RS, pc = off / 3, c = off - pc * 3;
-    const int ih = 2 * oh0 - 3 + rr, iw = pc - 3;
-    u16 v = 0;
-    if (rr < IN_ROWS - 1 && ih >= 0 && ih < H && iw >= 0 && iw < W) v = x[(((long long)n * H + ih) * W + iw) * 3 + c];
-    xin[e] = v;
-  }
-  __syncthreads();
+  const int row_elems = 3 * W, row_u2 = row_elems / 4;                     // 8-byte chunks of one image row
   const int pix_per_wg = ROWS_PER_WG * OW;
-  const long long m_base = ((long long)n * OH + oh0) * OW;                  // first output pixel of this workgroup
-  for (int rnd = 0; rnd < pix_per_wg / 64; ++rnd) {
-    // ---- MFMA: this wave's 16 pixels x 64 channels
-    const int ml = rnd * 64 + wave * 16 + col;                               // A row (pixel) of this lane
-    const int ohl = ml / OW, ow = ml - ohl * OW;
-    const u16* abase = xin + (2 * ohl) * RS + 6 * ow;
-    f4s_t acc[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = f4s_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int k0 = ks * 32 + hg * 8, r = k0 / 24, q0 = k0 - r * 24;
-      const unsigned* ap = reinterpret_cast<const unsigned*>(abase + r * RS + q0);   // 4-byte aligned (even)
-      union {
-        unsigned u[4];
-        bf16x8s_t v;
-      } a;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a.u[j] = ap[j];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b[nt][ks], acc[nt], 0, 0, 0);
+  // persistent: each workgroup walks 4-output-row blocks (weights loaded once per workgroup)
+  for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const int n = blk / blocks_per_img, oh0 = (blk - n * blocks_per_img) * ROWS_PER_WG;
+    // ---- stage input rows ih = 2*oh0 - 3 + rr; element (rr, iw, c) at rr*RS + (iw + 4)*3 + c: the image row
+    // starts 24 bytes in (8-byte aligned copies), pads [0, 12) and [12 + 3W, RS) are zero
+    __syncthreads();                                                         // previous block done with xin
+    for (int i = threadIdx.x; i < (IN_ROWS - 1) * row_u2; i += 256) {
+      const int rr = i / row_u2, j = i - rr * row_u2;
+      const int ih = 2 * oh0 - 3 + rr;
+      uint2 v = make_uint2(0u, 0u);
+      if (ih >= 0 && ih < H) v = *reinterpret_cast<const uint2*>(x + ((long long)n * H + ih) * row_elems + 4 * j);
+      *reinterpret_cast<uint2*>(xin + rr * RS + 12 + 4 * j) = v;
     }
-    // ---- C tile -> LDS (bf16): lane holds rows 4*hg + j, column nt*16 + col
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ot[(wave * 16 + hg * 4 + j) * OUT_LD + nt * 16 + col] = f2bf(acc[nt][j]);
+    const int tail = RS - 12 - row_elems;                                    // zero columns per row (even)
+    for (int i = threadIdx.x; i < IN_ROWS * (6 + tail / 2); i += 256) {
+      const int rr = i / (6 + tail / 2), j = i - rr * (6 + tail / 2);
+      const int e = j < 6 ? 2 * j : 12 + row_elems + 2 * (j - 6);
+      *reinterpret_cast<unsigned*>(xin + rr * RS + e) = 0u;
+    }
+    for (int i = threadIdx.x; i < row_u2; i += 256)                          // last (r = 7 only) row: zero
+      *reinterpret_cast<uint2*>(xin + (IN_ROWS - 1) * RS + 12 + 4 * i) = make_uint2(0u, 0u);
     __syncthreads();
-    // ---- BN tile statistics over the 64 rounded outputs of each channel (shift = the round's first pixel)
-    if (tstats) {
-      const int c = threadIdx.x & 63, qg = threadIdx.x >> 6;
-      const float sh = bf2f(ot[c]);
-      float s1 = 0.f, s2 = 0.f;
+    const long long m_base = ((long long)n * OH + oh0) * OW;
+    for (int rnd = 0; rnd < pix_per_wg / 64; ++rnd) {
+      // ---- MFMA: this wave's 16 pixels x 64 channels; window of output column ow starts at element 6*ow + 3 (odd):
+      // read 5 aligned dwords and realign by 16 bits
+      const int ml = rnd * 64 + wave * 16 + col;
+      const int ohl = ml / OW, ow = ml - ohl * OW;
+      const unsigned* abase = reinterpret_cast<const unsigned*>(xin + (2 * ohl) * RS + 6 * ow + 2);
+      f4s_t acc[4];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float d = bf2f(ot[(qg * 16 + i) * OUT_LD + c]) - sh;
-        s1 += d;
-        s2 += d * d;
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = f4s_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k0 = ks * 32 + hg * 8, r = k0 / 24, q0 = k0 - r * 24;
+        const unsigned* ap = abase + (r * RS + q0) / 2;
+        unsigned d[5];
+#pragma unroll
+        for (int jj = 0; jj < 5; ++jj) d[jj] = ap[jj];
+        union {
+          unsigned u[4];
+          bf16x8s_t v;
+        } a;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) a.u[jj] = __builtin_amdgcn_alignbit(d[jj + 1], d[jj], 16);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b[nt][ks], acc[nt], 0, 0, 0);
       }
-      red[qg * 64 + c] = s1;
-      red[256 + qg * 64 + c] = s2;
-    }
-    // ---- 16-byte coalesced stores of the 64 x 64 tile
-    const long long m0 = m_base + rnd * 64;
+      // ---- C tile -> LDS (bf16): lane holds rows 4*hg + j, column nt*16 + col
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int id = threadIdx.x + 256 * j, row = id >> 3, c8 = id & 7;
-      *reinterpret_cast<bf16x8*>(y + (m0 + row) * 64 + c8 * 8) =
-          *reinterpret_cast<const bf16x8*>(ot + row * OUT_LD + c8 * 8);
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ot[(wave * 16 + hg * 4 + j) * OUT_LD + nt * 16 + col] = f2bf(acc[nt][j]);
+      __syncthreads();
+      // ---- BN tile statistics over the 64 rounded outputs of each channel (shift = the round's first pixel)
+      if (tstats) {
+        const int c = threadIdx.x & 63, qg = threadIdx.x >> 6;
+        const float sh = bf2f(ot[c]);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float dd = bf2f(ot[(qg * 16 + i) * OUT_LD + c]) - sh;
+          s1 += dd;
+          s2 += dd * dd;
+        }
+        red[qg * 64 + c] = s1;
+        red[256 + qg * 64 + c] = s2;
+      }
+      // ---- 16-byte coalesced stores of the 64 x 64 tile
+      const long long m0 = m_base + rnd * 64;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int id = threadIdx.x + 256 * j, row = id >> 3, c8 = id & 7;
+        *reinterpret_cast<bf16x8*>(y + (m0 + row) * 64 + c8 * 8) =
+            *reinterpret_cast<const bf16x8*>(ot + row * OUT_LD + c8 * 8);
+      }
+      __syncthreads();
+      if (tstats && threadIdx.x < 64) {
+        const int c = threadIdx.x;
+        const long long p = m0 / 64;
+        tstats[p * 64 + c] = red[c] + red[64 + c] + red[128 + c] + red[192 + c];
+        tstats[(P + p) * 64 + c] = red[256 + c] + red[320 + c] + red[384 + c] + red[448 + c];
+        tstats[(2 * P + p) * 64 + c] = bf2f(ot[c]);
+      }
+      __syncthreads();                                                       // ot / red reused next round
     }
-    __syncthreads();
-    if (tstats && threadIdx.x < 64) {
-      const int c = threadIdx.x;
-      const long long p = m0 / 64;
-      tstats[p * 64 + c] = red[c] + red[64 + c] + red[128 + c] + red[192 + c];
-      tstats[(P + p) * 64 + c] = red[256 + c] + red[320 + c] + red[384 + c] + red[448 + c];
-      tstats[(2 * P + p) * 64 + c] = bf2f(ot[c]);
-    }
-    __syncthreads();                                                         // ot / red reused next round
   }
 }
 
@@ -118,14 +136,24 @@ __global__ void __launch_bounds__(256) stem_conv_fwd(const u16* __restrict__ x, 
 DL4J_API int dl4j_stem_conv_fwd(const void* x, const void* wpk, void* y, float* tstats, int N, int H, int W,
                                       int OH, int OW, hipStream_t s) {
   if (N < 1 || OH % ROWS_PER_WG != 0 || (ROWS_PER_WG * OW) % 64 != 0 || OH != (H - 1) / 2 + 1 ||
-      OW != (W - 1) / 2 + 1)
+      OW != (W - 1) / 2 + 1 || (3 * W) % 4 != 0)
     return -1;
-  int RS = (2 * OW + 6) * 3 + 8;                  // covers window reads up to q = 23 of the last column
-  RS = (RS + 7) & ~7;                             // even (4-byte aligned rows), 16-byte multiple
+  // row: 12 zero elements, the 3W image elements, zero tail covering window reads up to q = 23 (+1 realign dword)
+  int RS = 12 + 3 * W;
+  const int need = 6 * (OW - 1) + 3 + 24 + 2;
+  if (RS < need) RS = need;
+  RS = (RS + 15) & ~15;                           // 32-byte rows
   const size_t lds = (size_t)IN_ROWS * RS * 2 + 64 * OUT_LD * 2 + 512 * 4;
   if (lds > 64 * 1024) return -1;
   const long long P = (long long)N * OH * OW / 64;
-  hipLaunchKernelGGL(stem_conv_fwd, dim3(N * (OH / ROWS_PER_WG)), dim3(256), lds, s, (const u16*)x,
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  int per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, stem_conv_fwd, 256, lds) != hipSuccess || per < 1) per = 1;
+  const int nblocks = N * (OH / ROWS_PER_WG);
+  const int grid = nblocks < per * ncu ? nblocks : per * ncu;
+  hipLaunchKernelGGL(stem_conv_fwd, dim3(grid), dim3(256), lds, s, (const u16*)x,
                      (const bf16x8s_t*)wpk, (u16*)y, tstats, N, H, W, OH, OW, RS, P);
   return (int)hipGetLastError();
 }

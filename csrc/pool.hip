@@ -12,11 +12,8 @@ __global__ __launch_bounds__(256) void pool_fwd(const T* __restrict__ x, T* __re
   const int CG = C >> 3;
   const long long total = (long long)N * OH * OW * CG;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % CG);
-    long long r = t / CG;
-    const int ow = (int)(r % OW); r /= OW;
-    const int oh = (int)(r % OH);
-    const int n = (int)(r / OH);
+    int cg, ow, oh, n;
+    idx_decomp4(t, CG, OW, OH, cg, ow, oh, n);
     float acc[8];
     unsigned char idx[8];
 #pragma unroll
@@ -59,11 +56,8 @@ __global__ __launch_bounds__(256) void pool_bwd(const T* __restrict__ dy, const 
   const long long total = (long long)N * H * W * CG;
   const float inv = 1.f / (float)(kh * kw);
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % CG);
-    long long r = t / CG;
-    const int iw = (int)(r % W); r /= W;
-    const int ih = (int)(r % H);
-    const int n = (int)(r / H);
+    int cg, iw, ih, n;
+    idx_decomp4(t, CG, W, H, cg, iw, ih, n);
     float acc[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[c] = 0.f;
