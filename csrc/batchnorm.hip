@@ -95,13 +95,13 @@ __global__ __launch_bounds__(256) void bn_reduce_rows(const float* __restrict__ 
 }
 
 // Per-tile statistics from the conv epilogue (csrc/conv_igemm.hip, planes [3][P][C]: S1, S2 about a per-partial
-// shift y_p, partial p = rows [64p, 64p+64)) -> the [ceil(P/32), C] partial-sum format of bn_stats_partial
+// shift y_p, partial p = rows [rpp*p, rpp*p + rpp), rpp = 64 for the igemm kernels, one output row for the stem) -> the [ceil(P/32), C] partial-sum format of bn_stats_partial
 // (sums about the GLOBAL shift x0 = row 0). Re-centring uses d = y_p - x0 (both samples of the same channel, so
 // O(std), no cancellation): S1' = S1 + n d, S2' = S2 + 2 d S1 + n d^2. grid = (ceil(C/64), ceil(P/32)).
 template <typename T>
 __global__ __launch_bounds__(256) void bn_tiles_reduce(const float* __restrict__ ts, long long P, int C, long long M,
                                                        const T* __restrict__ x, float* __restrict__ q1,
-                                                       float* __restrict__ q2) {
+                                                       float* __restrict__ q2, int rpp) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
   const long long p0 = (long long)blockIdx.y * 32 + grp * 8;
@@ -112,8 +112,8 @@ __global__ __launch_bounds__(256) void bn_tiles_reduce(const float* __restrict__
     for (int u = 0; u < 8; ++u) {
       const long long p = p0 + u;
       if (p >= P) break;
-      const long long nrow = M - 64 * p;
-      const float n = (float)(nrow < 64 ? (nrow < 0 ? 0 : nrow) : 64);
+      const long long nrow = M - (long long)rpp * p;
+      const float n = (float)(nrow < rpp ? (nrow < 0 ? 0 : nrow) : rpp);
       const float s1 = ts[p * C + c], s2 = ts[(P + p) * C + c], d = ts[(2 * P + p) * C + c] - x0;
       sa += s1 + n * d;
       sb += s2 + 2.f * d * s1 + n * d * d;
@@ -408,7 +408,7 @@ DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* 
   float* p2 = ws + (long long)S * C;
   float* q = p2 + (long long)S * C;
   const bf16* xb = (const bf16*)x;
-  hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2);
+  hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2, 64);
   bn_reduce_stage(p1, p2, S, C, q, s);
   hipLaunchKernelGGL(bn_finalize<bf16>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, S, C, M, xb, gamma, beta, gconst,
                      bconst, run_mean, run_var, decay, eps, 1, ctx_out);
@@ -828,7 +828,7 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
                               int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                               const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
                               float* run_var, float decay, float eps, int training, const float* tstats,
-                              long long P, float* ws, float* ctx_out, hipStream_t s) {
+                              long long P, int rpp, float* ws, float* ctx_out, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127 || kh < 1 || kw < 1) return -1;
   const long long M = (long long)N * H * W;
   int nblk;
@@ -846,7 +846,7 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
     q = p2 + (long long)nblk * C;
     const bf16* xb = (const bf16*)x;
     hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, nblk), dim3(256), 0, s, tstats, P, C, M, xb, p1,
-                       p2);
+                       p2, rpp);
     bn_reduce_stage(p1, p2, nblk, C, q, s);
     hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, 1, ctx_out);

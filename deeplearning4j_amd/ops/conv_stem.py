@@ -46,12 +46,12 @@ def forward(x, w, want_stats=False):
     lib = native.load()
     native.register_sig("dl4j_stem_conv_fwd", [c_void_p] * 4 + [c_int] * 5 + [c_void_p])
     y = torch.empty((N, 64, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-    ts = torch.empty((3, N * OH * OW // 64, 64), dtype=torch.float32, device=x.device) if want_stats else None
+    ts = torch.empty((3, N * OH, 64), dtype=torch.float32, device=x.device) if want_stats else None
     rc = lib.dl4j_stem_conv_fwd(_ptr(x), _ptr(pack_weights(w)), _ptr(y), _ptr(ts), N, H, W, OH, OW,
                                 c_void_p(_stream()))
     if rc == -1:
         return None
     native._check(rc, "stem_conv_fwd")
     if ts is not None:
-        y._bn_tile_stats = (ts, ts.shape[1])
+        y._bn_tile_stats = (ts, ts.shape[1], OW)                # one partial per output row
     return y

@@ -267,7 +267,8 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     b = beta if torch.is_tensor(beta) else None
     res = _rows_like(residual, x) if residual is not None else None
     ts = getattr(x, "_bn_tile_stats", None)
-    if training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128):
+    if training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
+            (len(ts) < 3 or ts[2] == 64):
         # statistics already reduced per tile by the producing conv kernel's epilogue
         register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_void_p,
                                            c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int,
@@ -325,13 +326,15 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
     lib = load()
     register_sig("dl4j_bn_pool_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 +
                  [c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p, c_ll,
-                  c_void_p, c_void_p, c_void_p])
+                  c_int, c_void_p, c_void_p, c_void_p])
     y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
     am = torch.empty(N * OH * OW * C, dtype=torch.uint8, device=x.device) if training else None
     xh = torch.empty_like(y) if training else None
     ts = getattr(x, "_bn_tile_stats", None)
     M = N * H * W
-    if not (training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128)):
+    rpp = ts[2] if ts is not None and len(ts) > 2 else 64
+    if not (training and ts is not None and dt == 1 and ts[0].shape[2] == C and
+            (ts[1] * rpp == M if rpp != 64 else ts[1] == 2 * ((M + 127) // 128))):
         ts = None
     nws = lib.dl4j_bn_workspace_floats(M, C)
     if ts is not None:
@@ -344,8 +347,8 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
     rc = lib.dl4j_bn_pool_fwd(dt, _ptr(x), _ptr(y), _ptr(am), _ptr(xh), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
                               _ptr(gamma), _ptr(b), 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                               _ptr(run_var), float(decay), float(eps), 1 if training else 0,
-                              _ptr(ts[0] if ts is not None else None), int(ts[1]) if ts is not None else 0, _ptr(ws),
-                              _ptr(ctx), _stream())
+                              _ptr(ts[0] if ts is not None else None), int(ts[1]) if ts is not None else 0, int(rpp),
+                              _ptr(ws), _ptr(ctx), _stream())
     if rc == -1:
         return None
     _check(rc, "bn_pool_fwd")
