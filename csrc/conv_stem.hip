@@ -181,3 +181,211 @@ DL4J_API int dl4j_stem_conv_fwd(const void* x, const void* wpk, void* y, float* 
                      (const bf16x8s_t*)wpk, (u16*)y, tstats, N, H, W, OH, OW, RS, P);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------ weight gradient
+// dW[co][k] = sum over output pixels m of dy[m][co] * A[m][k] (A = the same contiguous-K im2col as the forward).
+// MFMA view: C[co][k] (4 x 12 tiles of 16), reduction over pixels in chunks of 32:
+//   A operand = dy^T (co rows): staged per 64-pixel round as dyT[64][64 + 8] in LDS (16-byte reads per fragment),
+//   B operand = im2col (pixel rows, k columns): 8 pixels of one k per lane, gathered from the staged input rows
+//   (8 x 2-byte LDS reads at a 12-byte stride).
+// Wave w owns k-tiles 3w..3w+2 for all 4 co-tiles (12 accumulators). Each (persistent) workgroup writes its partial
+// [64][192] sums (and the bias column sums) to a workspace; stem_wrw_reduce sums the partials in a fixed order
+// (deterministic) straight into the DL4J [64][3][7][7] fp32 gradient.
+__global__ void __launch_bounds__(256, 2) stem_conv_wrw(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                        float* __restrict__ part, float* __restrict__ part_db, int N,
+                                                        int H, int W, int OH, int OW, int RS) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  u16* xin = reinterpret_cast<u16*>(smem);                                   // [IN_ROWS][RS]
+  u16* dyt = xin + IN_ROWS * RS;                                             // [2][64][OUT_LD]
+  float* dbs = reinterpret_cast<float*>(dyt + 2 * 64 * OUT_LD);              // [256][8]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hg = lane >> 4;
+  const int blocks_per_img = OH / ROWS_PER_WG, nblocks = N * blocks_per_img;
+  const int row_elems = 3 * W, row_u2 = row_elems / 4;
+  const int nchunks = (IN_ROWS - 1) * row_u2;
+  const int rounds = ROWS_PER_WG * OW / 64;
+  {  // zero pads and the r = 7 row once
+    const int tail = RS - 12 - row_elems, per_row = 6 + tail / 2;
+    for (int i = threadIdx.x; i < IN_ROWS * per_row; i += 256) {
+      const int rb = i / per_row, j = i - rb * per_row;
+      const int e = j < 6 ? 2 * j : 12 + row_elems + 2 * (j - 6);
+      *reinterpret_cast<unsigned*>(xin + rb * RS + e) = 0u;
+    }
+    for (int i = threadIdx.x; i < row_u2; i += 256)
+      *reinterpret_cast<uint2*>(xin + (IN_ROWS - 1) * RS + 12 + 4 * i) = make_uint2(0u, 0u);
+  }
+  // per lane: element offsets (within a window) of its 3 k columns; (r, q) of k = kt*16 + col
+  int koff[3];
+#pragma unroll
+  for (int t3 = 0; t3 < 3; ++t3) {
+    const int k = (wave * 3 + t3) * 16 + col, r = k / 24, q = k - r * 24;
+    koff[t3] = r * RS + q;
+  }
+  f4s_t acc[4][3];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3) acc[ct][t3] = f4s_t{0.f, 0.f, 0.f, 0.f};
+  float dbacc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dbacc[i] = 0.f;
+  uint2 pre[STAGE_SLOTS];
+  for (int blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const int n = blk / blocks_per_img, oh0 = (blk - n * blocks_per_img) * ROWS_PER_WG;
+    __syncthreads();                                                         // previous block done with xin / dyt
+#pragma unroll
+    for (int q = 0; q < STAGE_SLOTS; ++q) {
+      const int i = threadIdx.x + q * 256;
+      const int rr = i / row_u2, j = i - rr * row_u2;
+      const int ih = 2 * oh0 - 3 + rr;
+      pre[q] = make_uint2(0u, 0u);
+      if (i < nchunks && ih >= 0 && ih < H)
+        pre[q] = *reinterpret_cast<const uint2*>(x + ((long long)n * H + ih) * row_elems + 4 * j);
+    }
+#pragma unroll
+    for (int q = 0; q < STAGE_SLOTS; ++q) {
+      const int i = threadIdx.x + q * 256;
+      const int rr = i / row_u2, j = i - rr * row_u2;
+      if (i < nchunks) *reinterpret_cast<uint2*>(xin + rr * RS + 12 + 4 * j) = pre[q];
+    }
+    const long long m_base = ((long long)n * OH + oh0) * OW;
+    // dy of round 0 in flight
+    uint4 g[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) g[j] = *reinterpret_cast<const uint4*>(dy + (m_base + (threadIdx.x >> 3) + 32 * j) * 64 +
+                                                                       (threadIdx.x & 7) * 8);
+    for (int rnd = 0; rnd < rounds; ++rnd) {
+      u16* dt = dyt + (rnd & 1) * 64 * OUT_LD;
+      // ---- transpose this round's dy tile into dyT[c][px]; bias column sums on the way
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int px = (threadIdx.x >> 3) + 32 * j, c8 = threadIdx.x & 7;
+        const u16* hv = reinterpret_cast<const u16*>(&g[j]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          dt[(c8 * 8 + i) * OUT_LD + px] = hv[i];
+          dbacc[i] += bf2f(hv[i]);
+        }
+      }
+      if (rnd + 1 < rounds) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          g[j] = *reinterpret_cast<const uint4*>(dy + (m_base + (rnd + 1) * 64 + (threadIdx.x >> 3) + 32 * j) * 64 +
+                                                 (threadIdx.x & 7) * 8);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        // B fragments: pixels p = rnd*64 + ch*32 + 8*hg + j (same output row: OW % 8 == 0)
+        const int p0 = rnd * 64 + ch * 32 + 8 * hg;
+        const int ohl = p0 / OW, ow0 = p0 - ohl * OW;
+        const u16* wb = xin + 2 * ohl * RS + (2 * ow0 + 1) * 3;
+        bf16x8s_t bfr[3];
+#pragma unroll
+        for (int t3 = 0; t3 < 3; ++t3) {
+          union {
+            u16 h[8];
+            bf16x8s_t v;
+          } bb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bb.h[j] = wb[koff[t3] + 6 * j];
+          bfr[t3] = bb.v;
+        }
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const bf16x8s_t a = *reinterpret_cast<const bf16x8s_t*>(dt + (ct * 16 + col) * OUT_LD + ch * 32 + 8 * hg);
+#pragma unroll
+          for (int t3 = 0; t3 < 3; ++t3)
+            acc[ct][t3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[t3], acc[ct][t3], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // ---- partial dW: lane holds C[co = ct*16 + 4*hg + j][k = (3*wave + t3)*16 + col]
+  float* pw = part + (long long)blockIdx.x * 64 * 192;
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t3 = 0; t3 < 3; ++t3)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pw[(ct * 16 + 4 * hg + j) * 192 + (3 * wave + t3) * 16 + col] = acc[ct][t3][j];
+  // ---- partial bias sums: threads with the same channel group (threadIdx.x & 7) combine through LDS
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dbs[threadIdx.x * 8 + i] = dbacc[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c8 = threadIdx.x >> 3, i = threadIdx.x & 7;
+    float sum = 0.f;
+    for (int t = c8; t < 256; t += 8) sum += dbs[t * 8 + i];
+    part_db[(long long)blockIdx.x * 64 + c8 * 8 + i] = sum;
+  }
+}
+
+// dW[co][c][r][s] = sum_g part[g][co][r*24 + s*3 + c]; db[co] = sum_g part_db[g][co]. A block covers 16 outputs x
+// 16 partial slices (each thread sums every 16th partial, 4 loads in flight), then the 16 slice sums are added in a
+// fixed order through LDS: deterministic, and ~600 blocks instead of 37 serial-latency-bound ones.
+__global__ void __launch_bounds__(256) stem_wrw_reduce(const float* __restrict__ part, const float* __restrict__ part_db,
+                                                       int G, float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float red[16][17];
+  const int ol = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + ol;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (o < 64 * 147) {
+    const int co = o / 147, rem = o - co * 147, c = rem / 49, rs = rem - c * 49, r = rs / 7, s = rs - r * 7;
+    const float* src = part + co * 192 + r * 24 + s * 3 + c;
+    int g = sl;
+    for (; g + 48 < G; g += 64) {
+      a0 += src[(long long)g * 12288];
+      a1 += src[(long long)(g + 16) * 12288];
+      a2 += src[(long long)(g + 32) * 12288];
+      a3 += src[(long long)(g + 48) * 12288];
+    }
+    for (; g < G; g += 16) a0 += src[(long long)g * 12288];
+  } else if (db && o < 64 * 147 + 64) {
+    const int co = o - 64 * 147;
+    for (int g = sl; g < G; g += 16) a0 += part_db[(long long)g * 64 + co];
+  }
+  red[ol][sl] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[ol][i];
+    if (o < 64 * 147) dW[o] = t;
+    else if (db && o < 64 * 147 + 64) db[o - 64 * 147] = t;
+  }
+}
+
+DL4J_API long long dl4j_stem_wrw_workspace_floats(int N, int OH) {
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const long long G = 2LL * ncu;
+  return G * (64 * 192 + 64);
+}
+
+// x: [N,H,W,3] bf16 input; dy: [N,OH,OW,64] bf16; dW: [64][3][7][7] fp32 (overwritten); db: [64] fp32 or null.
+// ws: >= dl4j_stem_wrw_workspace_floats floats. Returns -1 when the shape is not the stem's.
+DL4J_API int dl4j_stem_conv_wrw(const void* x, const void* dy, float* dW, float* db, float* ws, int N, int H, int W,
+                                int OH, int OW, hipStream_t s) {
+  if (N < 1 || OH % ROWS_PER_WG != 0 || OW % 16 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 ||
+      (3 * W) % 4 != 0 || (ROWS_PER_WG * OW) % 64 != 0)
+    return -1;
+  int RS = 12 + 3 * W;
+  const int need = 6 * (OW - 1) + 3 + 24 + 2;
+  if (RS < need) RS = need;
+  RS = (RS + 15) & ~15;
+  const size_t lds = (size_t)IN_ROWS * RS * 2 + 2 * 64 * OUT_LD * 2 + 256 * 8 * 4;
+  if (lds > 64 * 1024 || (IN_ROWS - 1) * (3 * W / 4) > STAGE_SLOTS * 256) return -1;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int nblocks = N * (OH / ROWS_PER_WG);
+  const int G = nblocks < 2 * ncu ? nblocks : 2 * ncu;
+  float* part = ws;
+  float* part_db = ws + (long long)G * 64 * 192;
+  hipLaunchKernelGGL(stem_conv_wrw, dim3(G), dim3(256), lds, s, (const u16*)x, (const u16*)dy, part, part_db, N, H, W,
+                     OH, OW, RS);
+  hipLaunchKernelGGL(stem_wrw_reduce, dim3((64 * 147 + 64 + 15) / 16), dim3(256), 0, s, part, part_db, G, dW, db);
+  return (int)hipGetLastError();
+}

@@ -214,6 +214,12 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
         return None
     N, C, H, W = x.shape
     K, Cw, R, S = w.shape
+    if C == 3 and not need_dx and need_dw and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
+        from . import conv_stem
+        if conv_stem.supported(_cl(x), w, None, stride, pad4, dilation) and _cl(dy).shape[1] == 64:
+            r = conv_stem.backward_weight(_cl(x), _cl(dy), gW, gb, need_db)
+            if r != "unsupported":
+                return None, r[0], r[1]
     if C != Cw or C % 8 != 0 or K % 8 != 0:
         return None
     OH, OW = dy.shape[2], dy.shape[3]

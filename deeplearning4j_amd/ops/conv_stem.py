@@ -1,6 +1,8 @@
 """ResNet stem convolution (7x7 / stride 2 / pad 3, 3 -> 64 channels, NHWC bf16) on the dedicated MFMA kernel in
 csrc/conv_stem.hip (the generic implicit-GEMM kernels need C % 8 == 0). Weight layout for the kernel: B[k][n] with
 k = r*24 + s*3 + c (K padded to 192), fragment-packed as [4 n-tiles][6 k-steps][64 lanes][8]."""
+import ctypes
+
 import torch
 
 from . import native
@@ -55,3 +57,37 @@ def forward(x, w, want_stats=False):
     if ts is not None:
         y._bn_tile_stats = (ts, ts.shape[1], OW)                # one partial per output row
     return y
+
+
+_ws = {}
+
+
+def backward_weight(x, dy, gW=None, gb=None, need_db=False):
+    """dW (and db) of the stem conv. Writes into the fp32 gradient views gW / gb when given (overwrite); returns
+    (dW_or_None, db_or_None) like conv_native.conv2d_bwd (None = written in place)."""
+    N, _, H, W = x.shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    lib = native.load()
+    native.register_sig("dl4j_stem_conv_wrw", [c_void_p] * 5 + [c_int] * 5 + [c_void_p])
+    native.register_sig("dl4j_stem_wrw_workspace_floats", [c_int, c_int])
+    lib.dl4j_stem_wrw_workspace_floats.restype = ctypes.c_longlong
+    key = str(x.device)
+    nws = lib.dl4j_stem_wrw_workspace_floats(N, OH)
+    ws = _ws.get(key)
+    if ws is None or ws.numel() < nws:
+        ws = _ws[key] = torch.empty(nws, dtype=torch.float32, device=x.device)
+    direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous() and gW.numel() == 64 * 147
+    dW = gW if direct else torch.empty((64, 3, 7, 7), dtype=torch.float32, device=x.device)
+    db = None
+    if need_db:
+        directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous() and gb.numel() == 64
+        db = gb.reshape(-1) if directb else torch.empty(64, dtype=torch.float32, device=x.device)
+    rc = lib.dl4j_stem_conv_wrw(_ptr(x), _ptr(dy), _ptr(dW), _ptr(db), _ptr(ws), N, H, W, OH, OW,
+                                c_void_p(_stream()))
+    if rc == -1:
+        return "unsupported"
+    native._check(rc, "stem_conv_wrw")
+    db_out = None
+    if need_db:
+        db_out = None if (gb is not None and db.data_ptr() == gb.data_ptr()) else db
+    return (None if direct else dW), db_out

@@ -117,3 +117,23 @@ def test_stem_conv_kernel_matches_reference(cuda, N, H):
     _close(mean, rows.mean(0), 1e-4)
     var = ((ts[1] + 2 * (sh - mean) * ts[0] + n * (sh - mean) ** 2).sum(0)) / M
     _close(var, rows.var(0, unbiased=False), 1e-3)
+
+
+@pytest.mark.parametrize("N,H", [(2, 224), (3, 64)])
+def test_stem_conv_weight_gradient_matches_reference(cuda, N, H):
+    """Stem weight/bias gradient kernel (csrc/conv_stem.hip stem_conv_wrw + fixed-order reduce) vs fp32 autograd."""
+    from deeplearning4j_amd.ops import conv_stem
+    g = torch.Generator().manual_seed(N + H)
+    x = torch.randn(N, 3, H, H, generator=g).to(torch.bfloat16).to(cuda).contiguous(memory_format=torch.channels_last)
+    OH = (H - 1) // 2 + 1
+    dy = torch.randn(N, 64, OH, OH, generator=g).to(torch.bfloat16).to(cuda).contiguous(
+        memory_format=torch.channels_last)
+    gW = torch.zeros(64, 3, 7, 7, device=cuda)
+    gb = torch.zeros(64, device=cuda)
+    r = conv_stem.backward_weight(x, dy, gW, gb, True)
+    assert r == (None, None), "gradients were not written in place"
+    w = torch.zeros(64, 3, 7, 7, device=cuda, requires_grad=True)
+    b = torch.zeros(64, device=cuda, requires_grad=True)
+    F.conv2d(x.float(), w, b, 2, 3).backward(dy.float())
+    _close(gW, w.grad, 2e-3)
+    _close(gb, b.grad, 2e-3)
