@@ -9,7 +9,9 @@
 // own flag (guide Guideline 16, R2), so there is no separate flag, fence or barrier between workgroups. Consumers
 // sweep the granules of h_{t-1} with agent-scope atomic loads until every tag matches; every spin is bounded by the
 // wall clock (a timeout sets *err and the kernel runs to completion instead of hanging). The exchange buffer is
-// double-buffered by step parity and zeroed by the host before every launch (tags start at 1).
+// double-buffered by step parity. Tags are tag_base + step + 1: the host keeps one persistent buffer and advances
+// tag_base past every launch's tags, so stale granules never match and no per-launch memset is needed (it zeroes
+// the buffer only on first use, on tag wrap-around, and under HIP-graph capture, where every replay reuses tags).
 //
 // The grid (G x tiles workgroups, one per CU: LDS-bound) is launched with hipLaunchCooperativeKernel so that all
 // workgroups are guaranteed co-resident; shapes that do not fit fall back to csrc/lstm.hip.
@@ -36,7 +38,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
     const float* __restrict__ h0, const float* __restrict__ c0, const float* __restrict__ mask,
     float* __restrict__ out, float* __restrict__ gates, float* __restrict__ call, float* __restrict__ hT,
     float* __restrict__ cT, unsigned long long* exch_raw, unsigned* err_raw, int Tn, int mb, int H,
-    long long timeout_ticks) {
+    long long timeout_ticks, unsigned tag_base) {
   constexpr int NW = U / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int KS = H / 32, H16 = H / 16, H4 = 4 * H;
@@ -102,10 +104,10 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int i = base + q * blockDim.x + threadIdx.x;
-            v[q] = i < npairs ? __hip_atomic_load(src + i, RLX_AGENT) : ((unsigned long long)t << 32);
+            v[q] = i < npairs ? __hip_atomic_load(src + i, RLX_AGENT) : ((unsigned long long)(tag_base + t) << 32);
           }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == (unsigned)t;
+          for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == tag_base + (unsigned)t;
           if (ok) break;
           if (wall_clock64() > deadline) {
             __hip_atomic_store(err, 1u, RLX_AGENT);
@@ -181,7 +183,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
         const __bf16 lo = (__bf16)h, hi = (__bf16)hn;
         const unsigned pay = (unsigned)(*reinterpret_cast<const unsigned short*>(&lo)) |
                              ((unsigned)(*reinterpret_cast<const unsigned short*>(&hi)) << 16);
-        __hip_atomic_store(dst + rr * (H / 2) + (j >> 1), ((unsigned long long)(t + 1) << 32) | pay, RLX_AGENT);
+        __hip_atomic_store(dst + rr * (H / 2) + (j >> 1), ((unsigned long long)(tag_base + t + 1) << 32) | pay, RLX_AGENT);
       }
     }
     if (t + 1 < Tn) load_step(t + 1);
@@ -200,7 +202,8 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
 template <int U, bool PEEP>
 static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
                            const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
-                           unsigned long long* exch, unsigned* err, int Tn, int mb, int H, hipStream_t s) {
+                           unsigned long long* exch, unsigned* err, int Tn, int mb, int H, unsigned tag_base,
+                           int reset, hipStream_t s) {
   const int KS = H / 32, NW = U / 16;
   const size_t lds = (size_t)4 * NW * KS * 64 * 16 + (H <= 256 ? 2ull : 1ull) * 16 * (H + 8) * 2;
   auto k = lstm_fwd_coop<U, PEEP>;
@@ -219,12 +222,12 @@ static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, c
   if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;
   (void)per;
   const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * 16 * (H / 2) * 8;
-  if (hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
-  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
   long long timeout = 200LL * 1000 * 1000;                  // wall_clock64 runs at 100 MHz: 2 s per wait
   void* args[] = {(void*)&zx, (void*)&rwt, (void*)&peep, (void*)&h0, (void*)&c0, (void*)&mask, (void*)&out,
                   (void*)&gates, (void*)&call, (void*)&hT, (void*)&cT, (void*)&exch, (void*)&err, (void*)&Tn,
-                  (void*)&mb, (void*)&H, (void*)&timeout};
+                  (void*)&mb, (void*)&H, (void*)&timeout, (void*)&tag_base};
   const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -249,7 +252,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
     const float* __restrict__ c0, const __bf16* __restrict__ rw, const float* __restrict__ peep,
     const float* __restrict__ mask, const float* __restrict__ dh_last, const float* __restrict__ dc_last,
     float* __restrict__ dz, float* __restrict__ dh0, float* __restrict__ dc0, unsigned long long* exch_raw,
-    unsigned* err_raw, int Tn, int mb, int t_end, long long timeout_ticks) {
+    unsigned* err_raw, int Tn, int mb, int t_end, long long timeout_ticks, unsigned tag_base) {
   constexpr int NW = U / 16, G = H / U, NTW = (H / 16) / NW, KL = 4 * U / 32, KSG = 4 * H / 32, LDZ = 4 * U + 8;
   constexpr int NE = 4 * G, BATCH = NE < 16 ? NE : 16;     // partial granules gathered per lane per step
   constexpr int H4 = 4 * H;
@@ -318,7 +321,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
           v[q] = __hip_atomic_load(src + ((long long)g * 16 + rg + r) * U + ul, RLX_AGENT);
         }
 #pragma unroll
-        for (int q = 0; q < BATCH; ++q) ok &= (unsigned)(v[q] >> 32) == (unsigned)tag;
+        for (int q = 0; q < BATCH; ++q) ok &= (unsigned)(v[q] >> 32) == tag_base + (unsigned)tag;
         if (ok) break;
         if (wall_clock64() > deadline) {
           __hip_atomic_store(err, 1u, RLX_AGENT);
@@ -397,7 +400,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         __hip_atomic_store(dst + (((long long)cons * G + grp) * 16 + rg + r) * U + un,
-                           ((unsigned long long)(it + 1) << 32) | __float_as_uint(acc[nt][r]), RLX_AGENT);
+                           ((unsigned long long)(tag_base + it + 1) << 32) | __float_as_uint(acc[nt][r]), RLX_AGENT);
     }
   }
   const int iters = Tn - t_end;
@@ -416,7 +419,7 @@ template <int U, int H, bool PEEP>
 static int coop_bwd_launch(const float* eps, const float* gates, const float* call, const float* c0, const void* rw,
                            const float* peep, const float* mask, const float* dhl, const float* dcl, float* dz,
                            float* dh0, float* dc0, unsigned long long* exch, unsigned* err, int Tn, int mb, int t_end,
-                           hipStream_t s) {
+                           unsigned tag_base, int reset, hipStream_t s) {
   const size_t lds = (size_t)(H / 16) * (4 * U / 32) * 64 * 16 + 2ull * 16 * (4 * U + 8) * 2;
   auto k = lstm_bwd_coop<U, H, PEEP>;
   if (lds > 160 * 1024) return -1;
@@ -431,13 +434,13 @@ static int coop_bwd_launch(const float* eps, const float* gates, const float* ca
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block.x, lds) != hipSuccess || per < 1) return -1;
   if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;    // one workgroup per CU, with margin
   const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * (H / U) * 16 * H * 8;
-  if (hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
-  if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
   long long timeout = 200LL * 1000 * 1000;                  // 2 s per wait at 100 MHz
   const __bf16* rwp = reinterpret_cast<const __bf16*>(rw);
   void* args[] = {(void*)&eps, (void*)&gates, (void*)&call, (void*)&c0, (void*)&rwp, (void*)&peep, (void*)&mask,
                   (void*)&dhl, (void*)&dcl, (void*)&dz, (void*)&dh0, (void*)&dc0, (void*)&exch, (void*)&err,
-                  (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout};
+                  (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout, (void*)&tag_base};
   const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -455,10 +458,12 @@ DL4J_API long long dl4j_lstm_coop_bwd_exch_bytes(int mb, int H) {
 DL4J_API int dl4j_lstm_bwd_coop(const float* eps, const float* gates, const float* call, const float* c0,
                                 const void* rw, const float* peep, const float* mask, const float* dh_last,
                                 const float* dc_last, float* dz, float* dh0, float* dc0, unsigned long long* exch,
-                                unsigned* err, int Tn, int mb, int H, int t_end, hipStream_t s) {
+                                unsigned* err, int Tn, int mb, int H, int t_end, unsigned tag_base, int reset,
+                                hipStream_t s) {
   if (Tn < 1 || mb < 1 || t_end < 0 || t_end >= Tn) return -1;
   const bool pp = peep != nullptr;
-#define BWD_ARGS eps, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, exch, err, Tn, mb, t_end, s
+#define BWD_ARGS eps, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, exch, err, Tn, mb, t_end, tag_base, \
+                 reset, s
   if (H == 256) return pp ? coop_bwd_launch<64, 256, true>(BWD_ARGS) : coop_bwd_launch<64, 256, false>(BWD_ARGS);
   if (H == 512) return pp ? coop_bwd_launch<32, 512, true>(BWD_ARGS) : coop_bwd_launch<32, 512, false>(BWD_ARGS);
 #undef BWD_ARGS
@@ -470,16 +475,13 @@ DL4J_API long long dl4j_lstm_coop_exch_bytes(int mb, int H) { return (long long)
 // bf16 only; H in {128, 256} (U = 64) or 512 (U = 32). Returns -1 when the cooperative path does not apply.
 DL4J_API int dl4j_lstm_fwd_coop(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
                                 const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
-                                unsigned long long* exch, unsigned* err, int Tn, int mb, int H, hipStream_t s) {
+                                unsigned long long* exch, unsigned* err, int Tn, int mb, int H, unsigned tag_base,
+                                int reset, hipStream_t s) {
   if (Tn < 1 || mb < 1) return -1;
   const bool pp = peep != nullptr;
-  if (H == 128 || H == 256)
-    return pp ? coop_fwd_launch<64, true>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, s)
-              : coop_fwd_launch<64, false>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H,
-                                           s);
-  if (H == 512)
-    return pp ? coop_fwd_launch<32, true>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, s)
-              : coop_fwd_launch<32, false>(zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H,
-                                           s);
+#define FWD_ARGS zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, tag_base, reset, s
+  if (H == 128 || H == 256) return pp ? coop_fwd_launch<64, true>(FWD_ARGS) : coop_fwd_launch<64, false>(FWD_ARGS);
+  if (H == 512) return pp ? coop_fwd_launch<32, true>(FWD_ARGS) : coop_fwd_launch<32, false>(FWD_ARGS);
+#undef FWD_ARGS
   return -1;
 }

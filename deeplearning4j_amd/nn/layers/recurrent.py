@@ -96,6 +96,20 @@ def _lstm_weight_grads(dzf2, xt, hprev, W, H, peephole, peep_grads, grads_prefix
     """The big library GEMMs after the time loop: dW = xᵀ·dz, dRW = hprevᵀ·dz (+ peephole columns), db = Σdz,
     dX = dz·Wᵀ (LSTMHelpers.java:616-676)."""
     dt = W.dtype
+    if dzf2.is_cuda and dt == torch.bfloat16:
+        # mixed precision: bf16 operands, fp32 accumulation straight into the fp32 gradient views
+        from .transformer import _bsum, _wgrad
+        dzb = dzf2.to(dt)
+        _wgrad(grads[grads_prefix + "W"], xt.to(dt), dzb)
+        hb = hprev.reshape(T * mb, H).to(dt)
+        gRW = grads[grads_prefix + "RW"]
+        if peephole:
+            dRW = torch.mm(hb.t(), dzb, out_dtype=torch.float32)
+            copy_grad_(gRW, torch.cat([dRW] + [g.reshape(-1, 1) for g in peep_grads], dim=1))
+        else:
+            _wgrad(gRW, hb, dzb)
+        _bsum(grads[grads_prefix + "b"], dzf2)
+        return (dzb @ W.t()).reshape(T, mb, -1).permute(1, 2, 0)
     copy_grad_(grads[grads_prefix + "W"], _acc(xt).t() @ dzf2)
     dRW = hprev.reshape(T * mb, H).t() @ dzf2
     if peephole:

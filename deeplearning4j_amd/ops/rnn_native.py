@@ -43,7 +43,37 @@ def _f32c(t):
     return None if t is None else t.detach().to(torch.float32).contiguous()
 
 
-_SIG_COOP = [c_void_p] * 13 + [c_int, c_int, c_int, c_void_p]
+_SIG_COOP = [c_void_p] * 13 + [c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
+
+
+class _CoopBuf:
+    """Persistent exchange buffer + error word of the cooperative kernels, and the next unused granule tag."""
+
+    def __init__(self, nbytes, device):
+        self.exch = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
+        self.err = torch.empty(1, dtype=torch.int32, device=device)
+        self.next_tag = None                               # None: contents undefined -> the next launch zeroes them
+
+
+_coop_bufs = {}
+
+
+def _coop_buf(kind, nbytes, device, steps):
+    """(buffer, tag_base, reset) for one launch that uses ``steps`` + 1 tags."""
+    key = (kind, str(device))
+    b = _coop_bufs.get(key)
+    if b is None or b.exch.numel() * 8 < nbytes:
+        b = _coop_bufs[key] = _CoopBuf(nbytes, device)
+    if torch.cuda.is_current_stream_capturing():
+        b.next_tag = None                                  # every graph replay reuses the same tags: zero each time
+        return b, 0, 1
+    need = steps + 2
+    if b.next_tag is None or b.next_tag + need >= 0xFFFFFFF0:
+        b.next_tag = need
+        return b, 0, 1
+    base = b.next_tag
+    b.next_tag += need
+    return b, base, 0
 
 
 def _coop_enabled():
@@ -57,20 +87,21 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, 
     native.register_sig("dl4j_lstm_coop_exch_bytes", [c_int, c_int])
     lib.dl4j_lstm_coop_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_exch_bytes(mb, H)
-    exch = torch.empty(nbytes // 8, dtype=torch.int64, device=zx.device)
-    err = torch.empty(1, dtype=torch.int32, device=zx.device)
+    b, base, reset = _coop_buf("fwd", nbytes, zx.device, T)
     rc = lib.dl4j_lstm_fwd_coop(_ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c), _ptr(m), _ptr(out), _ptr(gates),
-                                _ptr(call), _ptr(hT), _ptr(cT), _ptr(exch), _ptr(err), T, mb, H, c_void_p(_stream()))
+                                _ptr(call), _ptr(hT), _ptr(cT), _ptr(b.exch), _ptr(b.err), T, mb, H, base, reset,
+                                c_void_p(_stream()))
     if rc != 0:
+        b.next_tag = None
         return False
     global last_coop_err
-    last_coop_err = err                                  # device word: 1 = a hand-off wait timed out
+    last_coop_err = b.err                                # device word: 1 = a hand-off wait timed out (sticky)
     return True
 
 
 last_coop_err = None
 
-_SIG_BWD_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, c_int, c_void_p]
+_SIG_BWD_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
 
 
 def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, mb, H, t_end):
@@ -79,15 +110,15 @@ def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, 
     native.register_sig("dl4j_lstm_coop_bwd_exch_bytes", [c_int, c_int])
     lib.dl4j_lstm_coop_bwd_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_bwd_exch_bytes(mb, H)
-    exch = torch.empty(nbytes // 8, dtype=torch.int64, device=e.device)
-    err = torch.empty(1, dtype=torch.int32, device=e.device)
+    b, base, reset = _coop_buf("bwd", nbytes, e.device, T)
     rc = lib.dl4j_lstm_bwd_coop(_ptr(e), _ptr(gates), _ptr(call), _ptr(c0c), _ptr(rw), _ptr(peep), _ptr(m), _ptr(dhl),
-                                _ptr(dcl), _ptr(dz), _ptr(dh0), _ptr(dc0), _ptr(exch), _ptr(err), T, mb, H, int(t_end),
-                                c_void_p(_stream()))
+                                _ptr(dcl), _ptr(dz), _ptr(dh0), _ptr(dc0), _ptr(b.exch), _ptr(b.err), T, mb, H,
+                                int(t_end), base, reset, c_void_p(_stream()))
     if rc != 0:
+        b.next_tag = None
         return False
     global last_coop_bwd_err
-    last_coop_bwd_err = err
+    last_coop_bwd_err = b.err
     return True
 
 
