@@ -3,6 +3,8 @@ inference. See SURVEY §2.6 for the mapping from the reference's ParallelWrapper
 from .accumulation import AllReduceGradientsAccumulator, average_params_and_state
 from .distributed import barrier, destroy, init_distributed, is_dist, rank, world_size
 from .encoded import EncodedGradientsAccumulator, EncodingHandler
+from .factory import (DefaultTrainerContext, ParameterServerTrainerContext, SymmetricTrainerContext,  # noqa: F401
+                      Trainer, TrainerContext)
 from .inference import InferenceMode, ParallelInference
 from .wrapper import ParallelWrapper, TrainingMode
 from .cluster import (ParameterAveragingTrainingMaster, SharedTrainingMaster, SparkComputationGraph,  # noqa: F401

@@ -57,8 +57,10 @@ class ParallelWrapper:
 
     def __init__(self, model, workers=None, prefetchBuffer=16, averagingFrequency=1, averageUpdaters=True,
                  reportScoreAfterAveraging=False, trainingMode=TrainingMode.SHARED_GRADIENTS,
-                 gradientsAccumulator=None, bucket_mb=None):
+                 gradientsAccumulator=None, bucket_mb=None, trainerContext=None):
         self.model = model
+        self.trainerContext = trainerContext
+        self._trainer = None
         self.workers = workers or world_size()
         if is_dist() and self.workers != world_size():
             log.warning("ParallelWrapper: workers=%d but world size is %d; one worker per rank is used",
@@ -112,6 +114,13 @@ class ParallelWrapper:
             self._kw["bucket_mb"] = mb
             return self
 
+        def trainerFactory(self, ctx):
+            """A parallel.factory.TrainerContext (Default / Symmetric / ParameterServer) that owns the per-step
+            synchronisation instead of trainingMode."""
+            self._kw["trainerContext"] = ctx
+            self._kw.setdefault("trainingMode", TrainingMode.CUSTOM)
+            return self
+
         def build(self):
             return ParallelWrapper(**self._kw)
 
@@ -131,6 +140,10 @@ class ParallelWrapper:
             self.accumulator = AllReduceGradientsAccumulator(self.bucket_mb)
         if self.trainingMode in (TrainingMode.SHARED_GRADIENTS, TrainingMode.CUSTOM) and self.accumulator is not None:
             m.setGradientsAccumulator(self.accumulator)
+        if self.trainerContext is not None:
+            self.trainerContext.init(m)
+            self._trainer = self.trainerContext.create(None, rank(), m, rank(), False, self, self.trainingMode,
+                                                       self.averagingFrequency)
         self._prepared = True
 
     def fit(self, source, numEpochs=1):
@@ -150,13 +163,21 @@ class ParallelWrapper:
                 if hasattr(l, "onEpochEnd"):
                     l.onEpochEnd(m)
             m.incrementEpochCount()
-        if self.trainingMode == TrainingMode.AVERAGING and self._iter % self.averagingFrequency != 0:
+        if self._trainer is not None:
+            self.trainerContext.finalizeTraining(m)
+        elif self.trainingMode == TrainingMode.AVERAGING and self._iter % self.averagingFrequency != 0:
             average_params_and_state(m, self.averageUpdaters)       # final sync so all replicas agree
         barrier()
         return m
 
     def _step(self, ds):
         m = self.model
+        if self._trainer is not None:
+            self._trainer.feedDataSet(ds)
+            self._iter += 1
+            if self._iter % self.averagingFrequency == 0:
+                self.trainerContext.finalizeRound(m)
+            return
         if isinstance(ds, MultiDataSet):
             m._fit_batch(ds.features, ds.labels, ds.featuresMasks, ds.labelsMasks)
         elif isinstance(ds, DataSet):

@@ -53,6 +53,12 @@ def run_mode(rank, world, port, mode, result_path):
         b.trainingMode(TrainingMode.AVERAGING).averagingFrequency(2).averageUpdaters(True)
     elif mode == "encoded":
         b.gradientsAccumulator(EncodedGradientsAccumulator(threshold=1e-3))
+    elif mode in ("ctx_default", "ctx_sym", "ctx_ps"):
+        from deeplearning4j_amd.parallel import (DefaultTrainerContext, ParameterServerTrainerContext,
+                                                 SymmetricTrainerContext)
+        ctx = {"ctx_default": DefaultTrainerContext(), "ctx_sym": SymmetricTrainerContext(),
+               "ctx_ps": ParameterServerTrainerContext()}[mode]
+        b.trainerFactory(ctx).averagingFrequency(2)
     pw = b.build()
     pw.fit(it, 2)
     p = net.params().clone()

@@ -4,6 +4,7 @@ import os
 import socket
 import sys
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -89,3 +90,25 @@ def test_multidataset_iterator_adapter():
     assert len(m.features) == 1 and len(m.labels) == 1 and m.features[0].shape == (4, 5)
     it.reset()
     assert it.hasNext()
+
+
+@pytest.mark.parametrize("mode", ["ctx_default", "ctx_sym", "ctx_ps"])
+def test_parallel_wrapper_trainer_contexts(tmp_path, mode):
+    """ParallelWrapper.Builder.trainerFactory(Default / Symmetric / ParameterServer TrainerContext) over 2 gloo
+    ranks: replicas end identical and actually trained."""
+    path = str(tmp_path / f"{mode}.pt")
+    mp.spawn(W.run_mode, args=(2, _port(), mode, path), nprocs=2, join=True)
+    r = torch.load(path, weights_only=True)
+    p0, p1 = r["params"]
+    assert torch.allclose(p0, p1, atol=1e-6)
+    init = W.make_net(__import__("deeplearning4j_amd").Adam(0.01)).params()
+    assert not torch.allclose(p0, init)
+
+
+def test_parallel_wrapper_symmetric_context_equals_shared_gradients(tmp_path):
+    ps = {}
+    for mode in ("ctx_sym", "shared"):
+        path = str(tmp_path / f"{mode}.pt")
+        mp.spawn(W.run_mode, args=(2, _port(), mode, path), nprocs=2, join=True)
+        ps[mode] = torch.load(path, weights_only=True)["params"][0]
+    assert torch.allclose(ps["ctx_sym"], ps["shared"], atol=1e-5)
