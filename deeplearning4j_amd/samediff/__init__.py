@@ -358,16 +358,25 @@ class SameDiff:
         dev = vs[0].value.device
         n = sum(v.value.numel() for v in vs)
         flat = torch.empty(n, dtype=torch.float32, device=dev)
+        # bf16 variables train in mixed precision: fp32 master weights, the fused updater writes the bf16 copy the
+        # graph computes with (its "shadow") in the same pass
+        mixed = all(v.value.dtype == torch.bfloat16 for v in vs)
+        shadow = torch.empty(n, dtype=torch.bfloat16, device=dev) if mixed else None
         segs, off = [], 0
         for i, v in enumerate(vs):
             k = v.value.numel()
             flat[off:off + k].copy_(v.value.detach().reshape(-1).float())
-            v.value = flat[off:off + k].view(v.value.shape)
+            if mixed:
+                shadow[off:off + k].copy_(v.value.detach().reshape(-1))
+                v.value = shadow[off:off + k].view(v.value.shape)
+            else:
+                v.value = flat[off:off + k].view(v.value.shape)
             segs.append(Segment(off, k, off * cfg.updater.STATE_MULT, off, n, cfg.updater, cfg.l1, cfg.l2, 0))
             off += k
         state = torch.zeros(max(1, cfg.updater.stateSize(n)), dtype=torch.float32, device=dev)
         plan = UpdatePlan(segs, [(0, n, 0, cfg.updater)])
-        self._train_state = {"flat": flat, "grad": torch.zeros_like(flat), "state": state, "plan": plan}
+        self._train_state = {"flat": flat, "grad": torch.zeros_like(flat), "state": state, "plan": plan,
+                             "shadow": shadow}
 
     def fit(self, data, numEpochs=1):
         """Train on a DataSet / MultiDataSet, an iterator of them, or a list. Returns the last loss value."""
@@ -413,7 +422,7 @@ class SameDiff:
                     for v in vs:
                         v.value.requires_grad_(False)
                     fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount,
-                                 self.epochCount, 1, mini_batch=False)
+                                 self.epochCount, 1, mini_batch=False, shadow=st["shadow"])
                 self.iterationCount += 1
                 last = float(loss.detach())
             self.epochCount += 1

@@ -151,3 +151,21 @@ def test_lstm_coop_bwd_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb,
             assert int(rnn_native.last_coop_bwd_err.item()) == 0, "hand-off wait timed out"
     for a, b in zip(res["1"], res["0"]):
         _close(a, b, 2e-3)
+
+
+def test_samediff_char_lm_trains_on_gpu(cuda):
+    """The SameDiff char-LM of tools/bench_samediff_lstm.py: bf16 with fp32 masters, sequence kernels under autograd,
+    loss decreases when fitting one window repeatedly."""
+    import sys as _sys
+    import os as _os
+    _sys.path.insert(0, _os.path.join(_os.path.dirname(__file__), "..", "tools"))
+    import bench_samediff_lstm as B
+    from deeplearning4j_amd import DataSet
+    sd = B.build(cuda, 8, 20, 77, 256)
+    g = torch.Generator().manual_seed(3)
+    idx = torch.randint(0, 77, (8, 21), generator=g)
+    X = torch.nn.functional.one_hot(idx[:, :-1], 77).permute(0, 2, 1).to(torch.bfloat16).to(cuda)
+    Y = torch.nn.functional.one_hot(idx[:, 1:], 77).to(torch.bfloat16).to(cuda)
+    losses = [sd.fit(DataSet(X, Y)) for _ in range(40)]
+    assert losses[-1] < 0.7 * losses[0], losses[::10]
+    assert sd._train_state["shadow"] is not None            # mixed precision: bf16 compute copy of fp32 masters
