@@ -371,7 +371,7 @@ class SameDiff:
                 v.value = shadow[off:off + k].view(v.value.shape)
             else:
                 v.value = flat[off:off + k].view(v.value.shape)
-            segs.append(Segment(off, k, off * cfg.updater.STATE_MULT, off, n, cfg.updater, cfg.l1, cfg.l2, 0))
+            segs.append(Segment(off, k, 0, off, n, cfg.updater, cfg.l1, cfg.l2, 0))   # one block: state offset 0
             off += k
         state = torch.zeros(max(1, cfg.updater.stateSize(n)), dtype=torch.float32, device=dev)
         plan = UpdatePlan(segs, [(0, n, 0, cfg.updater)])
