@@ -114,3 +114,72 @@ def copy_bert_weights(net, sd, layers):
         put("classifier_b", sd["classifier.bias"])
     net.sync_shadow()
     return net
+
+
+def importBertSameDiff(src, config=None, numLabels=None, seqLen=128, device=None, dtype=torch.float32, batch=1):
+    """Import a HuggingFace BERT checkpoint as a SameDiff graph (BASELINE.json "BERT-base SameDiff import").
+
+    Placeholders ``input_ids`` [B, T] (int), ``attention_mask`` [B, T] (1 = token, 0 = padding) and ``labels``
+    [B, numLabels] (one-hot). Outputs ``probabilities`` and the loss variable ``loss``
+    (softmax cross entropy). The encoder uses the same fused ops as the ComputationGraph import: one fused QKV
+    projection per layer, ``nn().fusedSelfAttention`` (flash-attention kernel), ``nn().layerNorm`` (LayerNorm
+    kernel) and GELU. Train it with ``setTrainingConfig`` + ``fit`` (mapping features -> input_ids, attention_mask;
+    labels -> labels)."""
+    from ..samediff import SameDiff
+    sd_ = _load_state(src)
+    sd_ = {(k[5:] if k.startswith("bert.") else k): v for k, v in sd_.items()}
+    cfg = _load_config(config, src)
+    if numLabels is None:
+        numLabels = sd_["classifier.weight"].shape[0] if "classifier.weight" in sd_ else 2
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    E, L, nh = cfg["hidden_size"], cfg["num_hidden_layers"], cfg["num_attention_heads"]
+    eps = float(cfg.get("layer_norm_eps", 1e-12))
+
+    def w(t):
+        return t.detach().to(dtype).to(dev).contiguous()
+
+    g = SameDiff.create()
+    ids = g.placeHolder("input_ids", torch.zeros(batch, seqLen, dtype=torch.long, device=dev))
+    am = g.placeHolder("attention_mask", torch.ones(batch, seqLen, device=dev))
+    labels = g.placeHolder("labels", torch.zeros(batch, numLabels, dtype=dtype, device=dev))
+    wword = g.var("embeddings_Wword", w(sd_["embeddings.word_embeddings.weight"]))
+    wpos = g.var("embeddings_Wpos", w(sd_["embeddings.position_embeddings.weight"]))
+    wtype = g.var("embeddings_Wtype", w(sd_["embeddings.token_type_embeddings.weight"]))
+    x = g.gather("emb_word", wword, ids)
+    x = x.add("emb_pos", wpos.get(slice(0, seqLen)))
+    x = x.add("emb_type", wtype.get(slice(0, 1)))               # token type 0 for every position
+    x = g.nn().layerNorm("emb_ln", x, g.var("embeddings_lng", w(sd_["embeddings.LayerNorm.weight"])),
+                         g.var("embeddings_lnb", w(sd_["embeddings.LayerNorm.bias"])), eps)
+    for i in range(L):
+        p = f"encoder.layer.{i}."
+        a = p + "attention."
+        e = f"encoder_{i}_"
+        wqkv = torch.cat([sd_[a + f"self.{n}.weight"].t() for n in ("query", "key", "value")], dim=1)
+        bqkv = torch.cat([sd_[a + f"self.{n}.bias"] for n in ("query", "key", "value")])
+        qkv = g.nn().linear(e + "qkv", x, g.var(e + "Wqkv", w(wqkv)), g.var(e + "bqkv", w(bqkv)))
+        att = g.nn().fusedSelfAttention(e + "attn", qkv, nh, am)
+        o = g.nn().linear(e + "attn_out", att, g.var(e + "Wo", w(sd_[a + "output.dense.weight"].t())),
+                          g.var(e + "bo", w(sd_[a + "output.dense.bias"])))
+        x = g.nn().layerNorm(e + "ln1", o.add(e + "res1", x), g.var(e + "ln1g", w(sd_[a + "output.LayerNorm.weight"])),
+                             g.var(e + "ln1b", w(sd_[a + "output.LayerNorm.bias"])), eps)
+        hdn = g.nn().gelu(e + "gelu", g.nn().linear(e + "ffn1", x, g.var(e + "W1", w(sd_[p + "intermediate.dense.weight"].t())),
+                                                    g.var(e + "b1", w(sd_[p + "intermediate.dense.bias"]))))
+        f2 = g.nn().linear(e + "ffn2", hdn, g.var(e + "W2", w(sd_[p + "output.dense.weight"].t())),
+                           g.var(e + "b2", w(sd_[p + "output.dense.bias"])))
+        x = g.nn().layerNorm(e + "ln2", f2.add(e + "res2", x), g.var(e + "ln2g", w(sd_[p + "output.LayerNorm.weight"])),
+                             g.var(e + "ln2b", w(sd_[p + "output.LayerNorm.bias"])), eps)
+    cls = x.get(slice(None), 0)
+    if "pooler.dense.weight" in sd_:
+        pw, pb = sd_["pooler.dense.weight"].t(), sd_["pooler.dense.bias"]
+    else:
+        pw, pb = torch.eye(E), torch.zeros(E)
+    pooled = g.nn().tanh("pooled", g.nn().linear("pooler", cls, g.var("pooler_W", w(pw)), g.var("pooler_b", w(pb))))
+    if "classifier.weight" in sd_:
+        cw, cb = sd_["classifier.weight"].t(), sd_["classifier.bias"]
+    else:
+        gen = torch.Generator().manual_seed(0)
+        cw, cb = torch.randn(E, numLabels, generator=gen) * 0.02, torch.zeros(numLabels)
+    logits = g.nn().linear("logits", pooled, g.var("classifier_W", w(cw)), g.var("classifier_b", w(cb)))
+    g.nn().softmax("probabilities", logits)
+    g.loss().softmaxCrossEntropy("loss", labels, logits)
+    return g

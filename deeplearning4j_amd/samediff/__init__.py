@@ -80,6 +80,10 @@ class SDVariable:
     def transpose(self):
         return self.sd._op(None, lambda t: t.transpose(-1, -2), self)
 
+    def get(self, *idx):
+        """Python-style indexing / slicing (e.g. ``h.get(slice(None), 0)`` = the first token of every row)."""
+        return self.sd._op(None, lambda t: t[idx], self)
+
     def getShape(self):
         return list(self.value.shape)
 
@@ -489,6 +493,12 @@ class SameDiff:
 
     def mean(self, name, x, *dims):
         return self._op(name, lambda t: t.mean(dim=dims) if dims else t.mean(), x)
+
+    def gather(self, name, params, indices, axis=0):
+        """Rows of ``params`` selected by integer ``indices`` (embedding lookup when axis == 0)."""
+        if axis == 0:
+            return self._op(name, lambda p, i: torch.nn.functional.embedding(i.long(), p), params, indices)
+        return self._op(name, lambda p, i: torch.index_select(p, axis, i.long().reshape(-1)), params, indices)
 
     def concat(self, name, dim, *xs):
         return self._op(name, lambda *ts: torch.cat(ts, dim=dim), *xs)

@@ -59,3 +59,35 @@ def test_samediff_lstm_char_model_trains_cpu():
     Y = torch.nn.functional.one_hot(idx[:, 1:], nOut).float()
     losses = [sd.fit(DataSet(X, Y)) for _ in range(60)]
     assert losses[-1] < 0.5 * losses[0]
+
+
+def test_bert_samediff_import_matches_transformers():
+    """BERT imported as a SameDiff graph == HuggingFace BertForSequenceClassification (random init, no download),
+    then one SameDiff fit step lowers the loss on the same batch."""
+    import pytest
+    transformers = pytest.importorskip("transformers")
+    from deeplearning4j_amd.modelimport.bert import importBertSameDiff
+    cfg = transformers.BertConfig(vocab_size=60, hidden_size=32, num_hidden_layers=2, num_attention_heads=4,
+                                  intermediate_size=48, max_position_embeddings=24, num_labels=3)
+    torch.manual_seed(0)
+    hf = transformers.BertForSequenceClassification(cfg).eval()
+    sd = importBertSameDiff(hf.state_dict(), cfg.to_dict(), seqLen=10)
+    gen = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 60, (4, 10), generator=gen)
+    am = torch.ones(4, 10, dtype=torch.long)
+    am[1, 7:] = 0
+    am[3, 4:] = 0
+    with torch.no_grad():
+        ref = torch.softmax(hf(input_ids=ids, attention_mask=am).logits, dim=-1)
+    got = sd.output({"input_ids": ids, "attention_mask": am.float()}, "probabilities")["probabilities"]
+    assert torch.allclose(got, ref, atol=2e-5), (got - ref).abs().max()
+    from deeplearning4j_amd import Adam, MultiDataSet
+    sd.setTrainingConfig(TrainingConfig.builder().updater(Adam(1e-3)).dataSetFeatureMapping("input_ids",
+                                                                                            "attention_mask")
+                         .dataSetLabelMapping("labels").build())
+    y = torch.nn.functional.one_hot(torch.tensor([0, 1, 2, 1]), 3).float()
+    mds = MultiDataSet([ids, am.float()], [y])
+    l0 = sd.fit(mds)
+    for _ in range(5):
+        l1 = sd.fit(mds)
+    assert l1 < l0
