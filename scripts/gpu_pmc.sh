@@ -15,9 +15,9 @@ run() {  # name pass counters cmd...
   local rc=$?; cd "$R"; [ $rc -eq 0 ] || { echo "PMC_FAIL $name $pass rc=$rc"; tail -5 "$R/gpurun_out/pmc/$name.$pass.log"; exit 1; }
   echo "PMC_OK $name $pass"
 }
-for p in 1 2 3; do
+for p in ${PMC_PASSES:-1 2 3}; do
   eval C=\$P$p
   run resnet p$p "$C" python3 "$R/bench.py" --steps 2 --warmup 1 --batch 256 --graph 0
   run bert p$p "$C" python3 "$R/tools/bench_bert.py" --steps 2 --warmup 1
-  run lstm p$p "$C" python3 "$R/tools/bench_lstm.py" --steps 1 --warmup 1 --length 200
+  [ -n "$PMC_LSTM" ] && run lstm p$p "$C" python3 "$R/tools/bench_lstm.py" --steps 1 --warmup 1 --length 200
 done
