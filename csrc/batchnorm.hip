@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
   if (r0 < R) {
-    constexpr int U = RES ? 2 : 3;     // independent row groups in flight per thread
+    constexpr int U = RES ? 3 : 4;     // independent row groups in flight per thread
     long long r = rbeg + r0;
     for (; r < rend; r += U * R) {
       float xv[U][8], gv[U][8], rv[U][8];
@@ -320,7 +320,7 @@ static inline void bn_grid(long long M, int C, int* nblk, long long* rows_per_bl
   const long long work = M * T8;                  // vector loads
   long long nb = work / (256LL * 24);             // ~24 vector loads per thread, up to 4 blocks per CU
   if (nb < 1) nb = 1;
-  if (nb > 1024) nb = 1024;
+  if (nb > 2048) nb = 2048;
   long long rpb = (M + nb - 1) / nb;
   nb = (M + rpb - 1) / rpb;
   *nblk = (int)nb;
