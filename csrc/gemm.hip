@@ -1,0 +1,974 @@
+// General matrix multiply on MFMA (gfx950 / CDNA4): the `mmul` / gemm of the array engine.
+//
+// Replaces the library GEMM behind every dense-style product of the framework (reference call sites:
+// nn/layers/BaseLayer.java:86,97,334-336 preOutput / backprop, BaseOutputLayer.java:151,178,
+// recurrent/LSTMHelpers.java:206,212,522,616-676, SameDiff mmul) with in-tree kernels:
+//
+//   C[m][n] = act( alpha * sum_k A(m,k) B(k,n)  + bias  + beta * C[m][n] )      (optional pre-activation Z)
+//
+// Operand layouts are flags, not copies: A is either K-contiguous (A[m*lda + k]) or M-contiguous (A[k*lda + m]),
+// B is K-contiguous (B[n*ldb + k]) or N-contiguous (B[k*ldb + n]); a transposed torch view is just the other flag.
+// A column-major output is produced by the host wrapper as C^T = B^T A^T (swap operands and flags).
+//
+// gemm_glds  (bf16 / fp16 inputs, fp32 accumulation; fp32 / bf16 / fp16 output)
+//   * block tile BM x BN x 64, 4 or 8 waves, each wave a (BM/WGM) x (BN/WGN) sub-tile of
+//     v_mfma_f32_32x32x16 accumulators; the MFMA's A operand is the n-side fragment so every lane ends up holding
+//     4 consecutive output columns of one row (8/16-byte stores).
+//   * operands go global -> LDS with global_load_lds_dwordx4 (no VGPR staging) through a STAGES-deep ring; the
+//     wait for a stage is a counted `s_waitcnt vmcnt(N)` + raw s_barrier (never __syncthreads(), whose fence would
+//     drain the stages still in flight).
+//   * K-contiguous images: [rows][64 k] with 128-byte rows, 16-byte chunk c of row r stored at slot c ^ ((r>>1)&7)
+//     (each ds_read_b128 lane group then covers the 16 slots of a bank row). M/N-contiguous images: [rows/128]
+//     sub-images of [64 k][128] with 256-byte rows, chunk c of k-row r at slot c ^ ((r&3)<<2), read with
+//     ds_read_b64_tr_b16 (hardware transpose; the 16 (row, chunk) pairs of a half-wave read are distinct slots).
+//     glds writes lane-linearly, so the swizzle is applied on the per-lane SOURCE address and undone on the read.
+//   * XCD-aware, grouped block raster (consecutive block ids of one XCD share A row panels in its L2).
+//   * split-K over grid.y: fp32 partial slabs + a deterministic fixed-order reduce kernel that applies the epilogue.
+// gemm_simple (any dtype incl. fp32, any strides / shapes / alignment)
+//   * 64 x 64 x 16 tile, operands converted to fp32 in LDS, exact-fp32 v_mfma_f32_32x32x2_f32; used for fp32
+//     networks and for shapes the fast kernel's 16-byte DMA cannot address.
+#include "common.h"
+#include <hip/hip_fp16.h>
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+namespace {
+
+__device__ __attribute__((aligned(64))) char gemm_zero_page[64];
+
+template <int V> struct IC { static constexpr int value = V; };
+// compile-time loop: f(IC<I>{}) for I in [B, E) — keeps register arrays statically indexed
+template <int B, int E, typename F> __device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(IC<B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+template <int DT> struct MfmaT;
+template <> struct MfmaT<1> {
+  typedef __attribute__((ext_vector_type(8))) __bf16 v8;
+  static __device__ __forceinline__ f32x16_t mma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MfmaT<2> {
+  typedef __attribute__((ext_vector_type(8))) _Float16 v8;
+  static __device__ __forceinline__ f32x16_t mma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  void* Z;                 // optional pre-activation output (same dtype / ldc as C)
+  const float* bias;       // fp32, per column (bias_mode 1) or per row (bias_mode 2)
+  float* ws;               // split-K slabs [splits][M][N] fp32
+  long long lda, ldb, ldc;
+  long long sA, sB, sC;    // batch strides (elements)
+  int M, N, K;
+  int kps;                 // K per split (multiple of 64)
+  int splits;
+  float alpha, beta;
+  int bias_mode, act, out_dt;
+  int tiles_m, tiles_n;
+  int coalesce;             // 1: epilogue through LDS with 16-byte row stores (host-checked alignment)
+};
+
+__device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+// ----------------------------------------------------------------------------------------------- epilogue
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case 1: return fmaxf(v, 0.f);
+    case 2: return tanhf(v);
+    case 3: return 1.f / (1.f + __expf(-v));
+    case 4: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float ld_out(const void* C, int dt, long long i) {
+  if (dt == 0) return reinterpret_cast<const float*>(C)[i];
+  const u16 u = reinterpret_cast<const u16*>(C)[i];
+  if (dt == 1) return bf2f(u);
+  return __half2float(__ushort_as_half(u));
+}
+
+__device__ __forceinline__ u16 to16(float v, int dt) {
+  return dt == 1 ? f2bf(v) : __half_as_ushort(__float2half(v));
+}
+
+// 4 consecutive outputs (m, n..n+3) of one row: vector store when aligned and fully in range.
+__device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int m, int n, float* v) {
+  const long long base = (long long)m * g.ldc + n;
+  const bool full = (n + 3 < g.N);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x = v[j] * g.alpha;
+    if (g.bias_mode == 1 && n + j < g.N) x += g.bias[n + j];
+    else if (g.bias_mode == 2) x += g.bias[m];
+    if (g.beta != 0.f && n + j < g.N) x += g.beta * ld_out(C, g.out_dt, base + j);
+    v[j] = x;
+  }
+  const bool vec = full && ((g.ldc & 3) == 0) && ((n & 3) == 0);
+  if (Z) {
+    if (g.out_dt == 0) {
+      float* z = reinterpret_cast<float*>(Z) + base;
+      if (vec) *reinterpret_cast<float4*>(z) = make_float4(v[0], v[1], v[2], v[3]);
+      else for (int j = 0; j < 4; ++j) if (n + j < g.N) z[j] = v[j];
+    } else {
+      u16* z = reinterpret_cast<u16*>(Z) + base;
+      if (vec) {
+        uint2 pk;
+        pk.x = (unsigned)to16(v[0], g.out_dt) | ((unsigned)to16(v[1], g.out_dt) << 16);
+        pk.y = (unsigned)to16(v[2], g.out_dt) | ((unsigned)to16(v[3], g.out_dt) << 16);
+        *reinterpret_cast<uint2*>(z) = pk;
+      } else {
+        for (int j = 0; j < 4; ++j) if (n + j < g.N) z[j] = to16(v[j], g.out_dt);
+      }
+    }
+  }
+  if (g.act)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = apply_act(v[j], g.act);
+  if (g.out_dt == 0) {
+    float* c = reinterpret_cast<float*>(C) + base;
+    if (vec) *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+    else for (int j = 0; j < 4; ++j) if (n + j < g.N) c[j] = v[j];
+  } else {
+    u16* c = reinterpret_cast<u16*>(C) + base;
+    if (vec) {
+      uint2 pk;
+      pk.x = (unsigned)to16(v[0], g.out_dt) | ((unsigned)to16(v[1], g.out_dt) << 16);
+      pk.y = (unsigned)to16(v[2], g.out_dt) | ((unsigned)to16(v[3], g.out_dt) << 16);
+      *reinterpret_cast<uint2*>(c) = pk;
+    } else {
+      for (int j = 0; j < 4; ++j) if (n + j < g.N) c[j] = to16(v[j], g.out_dt);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- fast kernel
+// LDS byte offsets
+__device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+__device__ __forceinline__ int mc_off(int k, int col) {
+  return (col >> 7) * (64 * 256) + k * 256 + (((((col & 127) >> 3) ^ ((k & 3) << 2))) << 4) + (col & 7) * 2;
+}
+
+template <int DT, bool KC>
+__device__ __forceinline__ typename MfmaT<DT>::v8 read_frag(const char* T, int rbase, int s, int lane) {
+  typedef typename MfmaT<DT>::v8 v8;
+  if constexpr (KC) {
+    const int r = rbase + (lane & 31);
+    return *reinterpret_cast<const v8*>(T + kc_off(r, 2 * s + (lane >> 5)));
+  } else {
+    const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int col = rbase + (grp & 1) * 16 + 4 * p;
+    const int k0 = 16 * s + (grp >> 1) * 8 + q;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + mc_off(k0, col)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + mc_off(k0 + 4, col)));
+    s16x8_t f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(v8, f);
+  }
+}
+
+template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES>
+__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_glds(GemmArgs g) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int FM = WTM / 32, FN = WTN / 32;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128, SBYTES = ABYTES + BBYTES;
+  constexpr int NIA = BM / 8 / NW, NIB = BN / 8 / NW;     // 1-KB DMA instructions per wave per stage
+  static_assert(NIA * NW * 8 == BM && NIB * NW * 8 == BN, "tile / wave count mismatch");
+  typedef typename MfmaT<DT>::v8 v8;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SBYTES];
+
+  const int per_group = 8 * g.tiles_n;
+  const int bid = xcd_remap_g(blockIdx.x, gridDim.x);
+  const int grp_id = bid / per_group, first_m = grp_id * 8;
+  const int gsz = min(g.tiles_m - first_m, 8);
+  const int in_g = bid - grp_id * per_group;
+  const int tm = first_m + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int z = blockIdx.y, bz = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = (kend - kbeg + 63) / 64;
+
+  typedef unsigned short E;
+  const E* A = reinterpret_cast<const E*>(g.A) + (long long)bz * g.sA;
+  const E* B = reinterpret_cast<const E*>(g.B) + (long long)bz * g.sB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // ---- per-lane DMA sources (fixed for the whole K loop; advanced by 64 along K per stage)
+  const E* ap[NIA];
+  int akey[NIA];       // K-contig: k offset of this lane's chunk; M-contig: k row of this lane
+  bool aok[NIA];
+#pragma unroll
+  for (int j = 0; j < NIA; ++j) {
+    const int i = wid + NW * j;
+    if constexpr (AKC) {
+      const int row = 8 * i + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      aok[j] = m0 + row < g.M;
+      ap[j] = A + (long long)(aok[j] ? m0 + row : 0) * g.lda + kbeg + ch * 8;
+      akey[j] = kbeg + ch * 8;
+    } else {
+      const int sub = i >> 4, kr = 4 * (i & 15) + (lane >> 4);
+      const int ch = (lane & 15) ^ ((kr & 3) << 2);
+      const int col = m0 + sub * 128 + ch * 8;
+      aok[j] = col < g.M;
+      ap[j] = A + (long long)(kbeg + kr) * g.lda + (aok[j] ? col : 0);
+      akey[j] = kbeg + kr;
+    }
+  }
+  const E* bp[NIB];
+  int bkey[NIB];
+  bool bok[NIB];
+#pragma unroll
+  for (int j = 0; j < NIB; ++j) {
+    const int i = wid + NW * j;
+    if constexpr (BKC) {
+      const int row = 8 * i + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      bok[j] = n0 + row < g.N;
+      bp[j] = B + (long long)(bok[j] ? n0 + row : 0) * g.ldb + kbeg + ch * 8;
+      bkey[j] = kbeg + ch * 8;
+    } else {
+      const int sub = i >> 4, kr = 4 * (i & 15) + (lane >> 4);
+      const int ch = (lane & 15) ^ ((kr & 3) << 2);
+      const int col = n0 + sub * 128 + ch * 8;
+      bok[j] = col < g.N;
+      bp[j] = B + (long long)(kbeg + kr) * g.ldb + (bok[j] ? col : 0);
+      bkey[j] = kbeg + kr;
+    }
+  }
+  const long long astep = AKC ? 64 : 64 * g.lda;
+  const long long bstep = BKC ? 64 : 64 * g.ldb;
+
+  auto issue = [&](int kt, int st) {
+    char* sa = smem + st * SBYTES;
+    char* sb = sa + ABYTES;
+    const int kof = kt * 64;
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+      const void* src = (aok[j] && akey[j] + kof < kend) ? (const void*)(ap[j] + kt * astep) : (const void*)gemm_zero_page;
+      glds16(src, sa + (wid + NW * j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+      const void* src = (bok[j] && bkey[j] + kof < kend) ? (const void*)(bp[j] + kt * bstep) : (const void*)gemm_zero_page;
+      glds16(src, sb + (wid + NW * j) * 1024);
+    }
+  };
+
+  const int wm = wid / WGN, wn = wid % WGN;
+  f32x16_t acc[FN][FM];
+#pragma unroll
+  for (int a = 0; a < FN; ++a)
+#pragma unroll
+    for (int b = 0; b < FM; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  constexpr int LPS = NIA + NIB;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (STAGES > 2 && kt + 1 < nk) wait_vm<(STAGES > 2 ? (STAGES - 2) * LPS : 0)>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* sa = smem + (kt % STAGES) * SBYTES;
+    const char* sb = sa + ABYTES;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      v8 fm[FM], fn[FN];
+#pragma unroll
+      for (int b = 0; b < FM; ++b) fm[b] = read_frag<DT, AKC>(sa, wm * WTM + 32 * b, s, lane);
+#pragma unroll
+      for (int a = 0; a < FN; ++a) fn[a] = read_frag<DT, BKC>(sb, wn * WTN + 32 * a, s, lane);
+#pragma unroll
+      for (int a = 0; a < FN; ++a)
+#pragma unroll
+        for (int b = 0; b < FM; ++b) acc[a][b] = MfmaT<DT>::mma(fn[a], fm[b], acc[a][b]);
+    }
+  }
+
+  // ---- epilogue: acc[a][b] reg e <-> n = 32a + (e&3) + 8(e>>2) + 4h, m = 32b + (lane&31) within the wave tile
+  const int h = lane >> 5;
+  if (g.splits > 1) {
+    float* ws = g.ws + (long long)z * g.M * g.N;
+#pragma unroll
+    for (int b = 0; b < FM; ++b) {
+      const int m = m0 + wm * WTM + 32 * b + (lane & 31);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int a = 0; a < FN; ++a)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + wn * WTN + 32 * a + 8 * q + 4 * h;
+          float* p = ws + (long long)m * g.N + n;
+          if (n + 3 < g.N && (g.N & 3) == 0)
+            *reinterpret_cast<float4*>(p) = make_float4(acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2],
+                                                        acc[a][b][4 * q + 3]);
+          else
+            for (int j = 0; j < 4; ++j) if (n + j < g.N) p[j] = acc[a][b][4 * q + j];
+        }
+    }
+    return;
+  }
+  void* C = reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2);
+  void* Zp = g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2) : nullptr;
+#pragma unroll
+  for (int b = 0; b < FM; ++b) {
+    const int m = m0 + wm * WTM + 32 * b + (lane & 31);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int a = 0; a < FN; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * WTN + 32 * a + 8 * q + 4 * h;
+        if (n >= g.N) continue;
+        float v[4] = {acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]};
+        store4(g, C, Zp, m, n, v);
+      }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- LDS epilogue
+// Finished fp32 accumulators leave a block through LDS: pass P, the waves owning tile rows [P*RPP, (P+1)*RPP)
+// store their raw accumulators into an fp32 [RPP][BN] image (row pitch BN*4 + 16 bytes), then every thread takes
+// 8-column chunks of whole rows, applies alpha / bias / beta*C / pre-activation Z / activation once per element
+// (bias as vector loads), converts, and writes 16-byte row segments. Direct 8-byte stores from the MFMA fragment
+// layout (16-32 rows per instruction) ran at ~1 TB/s; register pressure stays at the accumulators themselves.
+struct EpiOut {
+  char* dst;          // C (or the split-K slab)
+  long long ld;       // destination row stride (elements)
+  int dt;             // destination dtype (0 f32, 1 bf16, 2 f16)
+  bool raw;           // split-K slab: no epilogue math
+  bool vec;           // 16-byte aligned rows (ld and base) for vector stores
+};
+
+__device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, void* Zp, int m, int n, float* v) {
+  if (!o.raw) {
+    float b[8];
+    if (g.bias_mode == 1) {
+      if (n + 8 <= g.N && ((n & 3) == 0)) {
+        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+      } else {
+        for (int j = 0; j < 8; ++j) b[j] = n + j < g.N ? g.bias[n + j] : 0.f;
+      }
+    } else {
+      const float bm = g.bias_mode == 2 ? g.bias[m] : 0.f;
+      for (int j = 0; j < 8; ++j) b[j] = bm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * g.alpha + b[j];
+    if (g.beta != 0.f)
+      for (int j = 0; j < 8; ++j) if (n + j < g.N) v[j] += g.beta * ld_out(o.dst, o.dt, (long long)m * o.ld + n + j);
+    if (Zp)
+      for (int j = 0; j < 8; ++j)
+        if (n + j < g.N) {
+          const long long i = (long long)m * o.ld + n + j;
+          if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
+          else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
+        }
+    if (g.act)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
+  }
+  char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
+  if (o.vec && n + 8 <= g.N) {
+    if (o.dt == 0) {
+      reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      uint4 pk;
+      pk.x = (unsigned)to16(v[0], o.dt) | ((unsigned)to16(v[1], o.dt) << 16);
+      pk.y = (unsigned)to16(v[2], o.dt) | ((unsigned)to16(v[3], o.dt) << 16);
+      pk.z = (unsigned)to16(v[4], o.dt) | ((unsigned)to16(v[5], o.dt) << 16);
+      pk.w = (unsigned)to16(v[6], o.dt) | ((unsigned)to16(v[7], o.dt) << 16);
+      *reinterpret_cast<uint4*>(p) = pk;
+    }
+  } else {
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N) {
+        if (o.dt == 0) reinterpret_cast<float*>(p)[j] = v[j];
+        else reinterpret_cast<u16*>(p)[j] = to16(v[j], o.dt);
+      }
+  }
+}
+
+// Read-out of one pass: RPP rows x BN columns of the fp32 LDS image.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_readout(const GemmArgs& g, const EpiOut& o, void* Zp, const char* T, int mrow0,
+                                            int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int CPR = BN / 8;
+  for (int idx = tid; idx < RPP * CPR; idx += NT) {
+    const int r = idx / CPR, c = idx - (idx / CPR) * CPR;
+    const int m = mrow0 + r, n = n0 + c * 8;
+    if (m >= g.M || n >= g.N) continue;
+    const float4 a = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32);
+    const float4 b = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32 + 16);
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    epi_chunk8(g, o, Zp, m, n, v);
+  }
+}
+
+// split-K reduce: out = epilogue(sum_z ws[z]) in fixed z order (deterministic)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g) {
+  const long long MN = (long long)g.M * g.N;
+  const int nq = (g.N + 3) / 4;
+  const long long total = (long long)g.M * nq;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(t / nq);
+    const int n = (int)(t - (long long)m * nq) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < g.splits; ++z) {
+      const float* p = g.ws + z * MN + (long long)m * g.N + n;
+      if (n + 3 < g.N && (g.N & 3) == 0) {
+        const float4 x = *reinterpret_cast<const float4*>(p);
+        v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+      } else {
+        for (int j = 0; j < 4; ++j) if (n + j < g.N) v[j] += p[j];
+      }
+    }
+    store4(g, g.C, g.Z, m, n, v);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- 8-phase kernel
+// 256 x 256 x 64 tile, 8 waves (2 along M x 4 along N, 128 x 64 outputs each), v_mfma_f32_16x16x32, LDS-DMA staging
+// in half-tiles with loads kept in flight across barriers (guide §5 "The 256² 8-phase template", T2-T5).
+//   * LDS (128 KB, one array): [2 K-tile buffers][A h0, A h1, B h0, B h1] x 16 KB. Half-tile h of A holds the rows
+//     {wr*128 + h*64 + 0..63} of both wave rows, half h of B the columns {wc*64 + h*32 + 0..31} of all four wave
+//     columns, so the quadrant (h, h') a wave computes in one phase reads exactly A half h and B half h'.
+//   * one iteration = 2 K-tiles = 8 phases. Phase p: ds_read this phase's register sub-tile -> stage ONE half-tile
+//     (2 DMAs per thread) -> [counted vmcnt(6) in phases 4 and 8] -> s_barrier -> lgkmcnt(0) -> 16 MFMAs -> s_barrier.
+//     Reads: P1 A-h0 + B-h0, P2 B-h1, P3 A-h1 (into the A-h0 registers), P4 none; P5-P8 the same on the odd buffer.
+//     Staging: P1 odd A-h1 (tile 2i+1), P2-P5 even A-h0, B-h0, B-h1, A-h1 (tile 2i+2), P6-P8 odd A-h0, B-h0, B-h1
+//     (tile 2i+3). Every restage is >= 1 phase after the last read of that half (retired by that phase's
+//     lgkmcnt(0) before its second barrier); the vmcnt(6) of P4 retires the odd tile (3 younger half-tiles may stay
+//     in flight), that of P8 the next even tile, each one barrier before its first reader.
+//   * past the last K-tile every DMA reads the zero page, so the wait counts never change (K-tile count padded to
+//     even with zeros).
+// Requirements: K % 64 == 0 (per split), operand element offsets < 2^31.
+__device__ __forceinline__ int mc16_off(int k, int col) {
+  return k * 256 + (((col >> 3) ^ (((k & 3) << 2) | (((k >> 3) & 1) << 1))) << 4) + (col & 7) * 2;
+}
+
+template <int DT, bool KC>
+__device__ __forceinline__ typename MfmaT<DT>::v8 frag16(const char* T, int rbase, int ks, int lane) {
+  typedef typename MfmaT<DT>::v8 v8;
+  if constexpr (KC) {
+    return *reinterpret_cast<const v8*>(T + kc_off(rbase + (lane & 15), 4 * ks + (lane >> 4)));
+  } else {
+    // the swizzled transposed-read address is not base + immediate: recompute it per read from an opaque copy of
+    // the lane id instead of letting the compiler hoist 24 live address registers out of the K loop.
+    // Inline asm, not the builtin: hipcc treats the builtin's LDS read as aliasing the in-flight LDS-DMA stages and
+    // drains them (vmcnt(0)) before every such read. The caller's lgkmcnt(0) + sched_barrier(0) orders the result.
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int g = ln >> 4, q = (ln & 15) >> 2, p = ln & 3;
+    const int col = rbase + 4 * p;
+    const int k = 32 * ks + 8 * g + q;
+    typedef __attribute__((address_space(3))) const char* lds_cptr;
+    const unsigned a0 = (unsigned)(uintptr_t)((lds_cptr)T + mc16_off(k, col));
+    const unsigned a1 = (unsigned)(uintptr_t)((lds_cptr)T + mc16_off(k + 4, col));
+    s16x8_t f;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"(a1));
+    return __builtin_bit_cast(v8, f);
+  }
+}
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+template <int DT> struct Mfma16;
+template <> struct Mfma16<1> {
+  static __device__ __forceinline__ f32x4_t mma(MfmaT<1>::v8 a, MfmaT<1>::v8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma16<2> {
+  static __device__ __forceinline__ f32x4_t mma(MfmaT<2>::v8 a, MfmaT<2>::v8 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <int DT, bool AKC, bool BKC>
+__global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
+  typedef typename MfmaT<DT>::v8 v8;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * 16384 + 8192];   // + pad rows of the epilogue tile
+
+  const int per_group = 8 * g.tiles_n;
+  const int bid = xcd_remap_g(blockIdx.x, gridDim.x);
+  const int grp_id = bid / per_group, first_m = grp_id * 8;
+  const int gsz = min(g.tiles_m - first_m, 8);
+  const int in_g = bid - grp_id * per_group;
+  const int tm = first_m + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int z = blockIdx.y, bz = blockIdx.z;
+  const int kbeg = z * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nk = (kend - kbeg) / 64;
+  const int niter = (nk + 1) / 2;
+
+  typedef unsigned short E;
+  const E* A = reinterpret_cast<const E*>(g.A) + (long long)bz * g.sA;
+  const E* B = reinterpret_cast<const E*>(g.B) + (long long)bz * g.sB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // Per-lane DMA source: one base element offset per operand (k = kbeg) plus the lane's row/column within the
+  // half-tile pattern; half h and instruction j only add wave-uniform offsets (keeps the loop free of spills).
+  // K-contig A: rows m0 + j*128 + h*64 + rl, rl = 8*wid + lane/8; K-contig B: n0 + j*128 + h*32 + rl', with
+  // rl' = (rl/32)*64 + rl%32. M/N-contig: k-row 32j + 4*wid + lane/16, column (lc/64)*128 + h*64 + lc%64 (A) or
+  // (lc/32)*64 + h*32 + lc%32 (B), lc = 8 * (swizzled chunk).
+  int a_base, a_lim, b_base, b_lim;
+  long long a_js, b_js;            // element offset between the j = 0 and j = 1 instruction
+  int a_hs, b_hs;                  // element offset between half 0 and half 1
+  {
+    const int rl = 8 * wid + (lane >> 3);
+    const int ch8 = (lane & 7) ^ ((rl >> 1) & 7);
+    const int kl = 4 * wid + (lane >> 4);
+    const int ch16 = (lane & 15) ^ (((kl & 3) << 2) | (((kl >> 3) & 1) << 1));
+    if constexpr (AKC) {
+      a_lim = g.M - m0 - rl;                                   // valid iff j*128 + h*64 < a_lim
+      a_base = (int)((long long)(m0 + rl) * g.lda + kbeg + ch8 * 8);
+      a_js = 128LL * g.lda;
+      a_hs = 64 * (int)g.lda;
+    } else {
+      const int lc = ch16 * 8;
+      const int cl = (lc >> 6) * 128 + (lc & 63);
+      a_lim = g.M - m0 - cl;                                   // valid iff h*64 < a_lim
+      a_base = (int)((long long)(kbeg + kl) * g.lda + m0 + cl);
+      a_js = 32LL * g.lda;
+      a_hs = 64;
+    }
+    if constexpr (BKC) {
+      const int rr = (rl >> 5) * 64 + (rl & 31);
+      b_lim = g.N - n0 - rr;
+      b_base = (int)((long long)(n0 + rr) * g.ldb + kbeg + ch8 * 8);
+      b_js = 128LL * g.ldb;
+      b_hs = 32 * (int)g.ldb;
+    } else {
+      const int lc = ch16 * 8;
+      const int cl = (lc >> 5) * 64 + (lc & 31);
+      b_lim = g.N - n0 - cl;
+      b_base = (int)((long long)(kbeg + kl) * g.ldb + n0 + cl);
+      b_js = 32LL * g.ldb;
+      b_hs = 32;
+    }
+  }
+  const long long astep = AKC ? 64 : 64 * g.lda;
+  const long long bstep = BKC ? 64 : 64 * g.ldb;
+
+  // stage half-tile (op 0 = A, 1 = B; half h) of K-tile kt into buffer kt & 1
+  auto stage = [&](int kt, int op, int h) {
+    char* dst = smem + (kt & 1) * 65536 + (op * 2 + h) * 16384 + wid * 1024;
+    const bool live = kt < nk;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bool ok;
+      const void* src;
+      if (op == 0) {
+        ok = live && (AKC ? (j * 128 + h * 64 < a_lim) : (h * 64 < a_lim));
+        src = A + (long long)a_base + j * a_js + h * a_hs + kt * astep;
+      } else {
+        ok = live && (BKC ? (j * 128 + h * 32 < b_lim) : (h * 32 < b_lim));
+        src = B + (long long)b_base + j * b_js + h * b_hs + kt * bstep;
+      }
+      glds16(ok ? src : (const void*)gemm_zero_page, dst + j * 8192);
+    }
+  };
+
+  f32x4_t acc[4][8];      // [n-block: h'*2 + cb][m-block: h*4 + rb]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  v8 af[4][2], bf0[2][2], bf1[2][2];
+
+  auto readA = [&](const char* T) {
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[rb][ks] = frag16<DT, AKC>(T, wr * 64 + rb * 16, ks, lane);
+  };
+  auto readB = [&](const char* T, v8 (&bf)[2][2]) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf[cb][ks] = frag16<DT, BKC>(T, wc * 32 + cb * 16, ks, lane);
+  };
+  auto quad = [&](int h, int hp, v8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[hp * 2 + cb][h * 4 + rb] = Mfma16<DT>::mma(bf[cb][ks], af[rb][ks], acc[hp * 2 + cb][h * 4 + rb]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar_lgkm = [&]() {
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // retire this phase's A reads before its first barrier (the A half is restaged one phase later; with the
+  // staggered wave groups the other group may pass that barrier before our lgkmcnt(0) after it)
+  auto wait_b_only = [&]() {
+    if constexpr (BKC) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  };
+
+  // prologue: even tile 0 (4 halves) + odd tile 1 (A-h0, B-h0, B-h1); retire the even tile
+  stage(0, 0, 0); stage(0, 1, 0); stage(0, 1, 1); stage(0, 0, 1);
+  stage(1, 0, 0); stage(1, 1, 0); stage(1, 1, 1);
+  wait_vm<6>();
+  raw_barrier();
+  // stagger the two wave rows by one barrier: while one group runs its MFMA cluster the other issues its reads
+  const bool late = __builtin_amdgcn_readfirstlane(wr) == 1;
+  if (late) raw_barrier();
+
+  for (int it = 0; it < niter; ++it) {
+    const int ke = 2 * it, ko = 2 * it + 1;
+    const char* E0 = smem;
+    const char* O0 = smem + 65536;
+    // P1
+    readA(E0 + 0 * 16384); readB(E0 + 2 * 16384, bf0);
+    stage(ko, 0, 1);
+    wait_b_only();
+    bar_lgkm(); quad(0, 0, bf0); raw_barrier();
+    // P2
+    readB(E0 + 3 * 16384, bf1);
+    stage(ke + 2, 0, 0);
+    bar_lgkm(); quad(0, 1, bf1); raw_barrier();
+    // P3
+    readA(E0 + 1 * 16384);
+    stage(ke + 2, 1, 0);
+    bar_lgkm(); quad(1, 1, bf1); raw_barrier();
+    // P4
+    stage(ke + 2, 1, 1);
+    wait_vm<6>();
+    raw_barrier(); quad(1, 0, bf0); raw_barrier();
+    // P5
+    readA(O0 + 0 * 16384); readB(O0 + 2 * 16384, bf0);
+    stage(ke + 2, 0, 1);
+    wait_b_only();
+    bar_lgkm(); quad(0, 0, bf0); raw_barrier();
+    // P6
+    readB(O0 + 3 * 16384, bf1);
+    stage(ko + 2, 0, 0);
+    bar_lgkm(); quad(0, 1, bf1); raw_barrier();
+    // P7
+    readA(O0 + 1 * 16384);
+    stage(ko + 2, 1, 0);
+    bar_lgkm(); quad(1, 1, bf1); raw_barrier();
+    // P8
+    stage(ko + 2, 1, 1);
+    wait_vm<6>();
+    raw_barrier(); quad(1, 0, bf0); raw_barrier();
+  }
+  if (!late) raw_barrier();
+  wait_vm<0>();
+
+  // epilogue (see epi_readout): pass P = wave row wr. acc[nb][mb] reg e <-> tile row wr*128 + (mb>>2)*64 +
+  // (mb&3)*16 + (lane&15), tile column wc*64 + (nb>>1)*32 + (nb&1)*16 + (lane>>4)*4 + e.
+  {
+    const bool split = g.splits > 1;
+    EpiOut o;
+    o.raw = split;
+    o.dt = split ? 0 : g.out_dt;
+    o.dst = split ? reinterpret_cast<char*>(g.ws + (long long)z * g.M * g.N)
+                  : reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2);
+    o.ld = split ? g.N : g.ldc;
+    o.vec = split ? ((g.N & 3) == 0) : (g.coalesce != 0);
+    void* Zp = (!split && g.Z) ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2) : nullptr;
+    constexpr int PITCH = 256 * 4 + 16;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();                                   // every wave is done reading the operand stages
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      if (wr == P) {
+        sfor<0, 8>([&](auto MB) {
+          constexpr int mb = decltype(MB)::value;
+          const int lr = (mb >> 2) * 64 + (mb & 3) * 16 + (lane & 15);
+          sfor<0, 4>([&](auto NB) {
+            constexpr int nb = decltype(NB)::value;
+            const int lc = wc * 64 + (nb >> 1) * 32 + (nb & 1) * 16 + (lane >> 4) * 4;
+            *reinterpret_cast<f32x4_t*>(smem + lr * PITCH + lc * 4) = acc[nb][mb];
+          });
+        });
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      epi_readout<128, 256, 512>(g, o, Zp, smem, m0 + P * 128, n0, tid);
+      if (P == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- simple kernel
+struct SimpleArgs {
+  const void* A;
+  const void* B;
+  long long sam, sak, sbk, sbn;     // element strides
+  long long bA, bB, bC;             // batch strides
+  int in_dt;                        // 0 f32, 1 bf16, 2 f16
+};
+
+__device__ __forceinline__ float ld_in(const void* p, int dt, long long i) {
+  if (dt == 0) return reinterpret_cast<const float*>(p)[i];
+  const u16 u = reinterpret_cast<const u16*>(p)[i];
+  return dt == 1 ? bf2f(u) : __half2float(__ushort_as_half(u));
+}
+
+// 64x64 output tile, BK = 16, 4 waves (2x2) each 32x32 via v_mfma_f32_32x32x2_f32 (exact fp32 products).
+__global__ __launch_bounds__(256) void gemm_simple(GemmArgs g, SimpleArgs s) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int tiles_n = (g.N + 63) / 64;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * 64, n0 = tn * 64;
+  const int bz = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const long long aoff = (long long)bz * s.bA, boff = (long long)bz * s.bB;
+  f32x16_t acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  // loader: 1024 elements per operand tile = 4 per thread; element (kk, r) with r fastest when the operand is
+  // contiguous along m/n, kk fastest otherwise (coalesced either way)
+  const bool a_mfast = s.sam == 1, b_nfast = s.sbn == 1;
+  for (int k0 = 0; k0 < g.K; k0 += 16) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      int kk, r;
+      if (a_mfast) { kk = e >> 6; r = e & 63; } else { r = e >> 4; kk = e & 15; }
+      const int m = m0 + r, k = k0 + kk;
+      As[kk][r] = (m < g.M && k < g.K) ? ld_in(s.A, s.in_dt, aoff + m * s.sam + k * s.sak) : 0.f;
+      if (b_nfast) { kk = e >> 6; r = e & 63; } else { r = e >> 4; kk = e & 15; }
+      const int n = n0 + r, k2 = k0 + kk;
+      Bs[kk][r] = (n < g.N && k2 < g.K) ? ld_in(s.B, s.in_dt, boff + k2 * s.sbk + n * s.sbn) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk += 2) {
+      const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C/D map: row (m) = (e&3) + 8(e>>2) + 4h, col (n) = lane&31
+  const int h = lane >> 5;
+  void* C = reinterpret_cast<char*>(g.C) + (long long)bz * s.bC * (g.out_dt == 0 ? 4 : 2);
+  void* Zp = g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * s.bC * (g.out_dt == 0 ? 4 : 2) : nullptr;
+  const int n = n0 + wn * 32 + (lane & 31);
+  if (n >= g.N) return;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    if (m >= g.M) continue;
+    float x = acc[e] * g.alpha;
+    if (g.bias_mode == 1) x += g.bias[n];
+    else if (g.bias_mode == 2) x += g.bias[m];
+    const long long o = (long long)m * g.ldc + n;
+    if (g.beta != 0.f) x += g.beta * ld_out(C, g.out_dt, o);
+    if (Zp) {
+      if (g.out_dt == 0) reinterpret_cast<float*>(Zp)[o] = x;
+      else reinterpret_cast<u16*>(Zp)[o] = to16(x, g.out_dt);
+    }
+    x = apply_act(x, g.act);
+    if (g.out_dt == 0) reinterpret_cast<float*>(C)[o] = x;
+    else reinterpret_cast<u16*>(C)[o] = to16(x, g.out_dt);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- dispatch
+struct Cfg {
+  int bm, bn;
+};
+// cfg ids: 0 = 256x256 (8 waves 2x4, 2 stages), 1 = 256x128 (8 waves 4x2, 3 stages),
+//          2 = 128x128 (4 waves 2x2, 2 stages, 2 blocks/CU), 3 = 128x64 (4 waves 2x2 of 64x32, 3 stages)
+//          4 = 256x256 8-phase (8 waves, 16x16x32 MFMA, K % 64 == 0)
+const Cfg kCfg[5] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}};
+
+template <int DT, bool AKC, bool BKC>
+int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
+  const int tiles = g.tiles_m * g.tiles_n;
+  dim3 grid(tiles, g.splits, batch);
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((gemm_glds<DT, 256, 256, 2, 4, AKC, BKC, 2>), grid, dim3(512), 0, s, g); break;
+    case 1: hipLaunchKernelGGL((gemm_glds<DT, 256, 128, 4, 2, AKC, BKC, 3>), grid, dim3(512), 0, s, g); break;
+    case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 2>), grid, dim3(256), 0, s, g); break;
+    case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC>), grid, dim3(512), 0, s, g); break;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int DT>
+int launch_fast_l(int cfg, int akc, int bkc, const GemmArgs& g, int batch, hipStream_t s) {
+  if (akc && bkc) return launch_fast<DT, true, true>(cfg, g, batch, s);
+  if (akc) return launch_fast<DT, true, false>(cfg, g, batch, s);
+  if (bkc) return launch_fast<DT, false, true>(cfg, g, batch, s);
+  return launch_fast<DT, false, false>(cfg, g, batch, s);
+}
+
+// Choose tile config + split-K. The 8-phase 256x256 kernel when it can fill >= half the chip (split-K over >= 8
+// K-tiles per split if needed), else the biggest 2/3-stage tile that reaches one block per CU.
+void plan(int M, int N, int K, int batch, int* cfg, int* splits) {
+  const int CUS = 256;
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
+  if (K % 64 == 0) {
+    int sp = 1;
+    if (batch == 1 && t256 < 224) {
+      sp = (int)((CUS + t256 - 1) / t256);
+      const int maxs = K / 512;
+      if (sp > maxs) sp = maxs;
+      if (sp > 16) sp = 16;
+      if (sp < 1) sp = 1;
+    }
+    if (t256 * sp >= 128) { *cfg = 4; *splits = sp; return; }
+  }
+  int best = 3;
+  for (int c = 0; c < 4; ++c) {
+    const long long t = (long long)((M + kCfg[c].bm - 1) / kCfg[c].bm) * ((N + kCfg[c].bn - 1) / kCfg[c].bn) * batch;
+    if (t >= CUS) { best = c; break; }
+  }
+  *cfg = best;
+  const long long t = (long long)((M + kCfg[best].bm - 1) / kCfg[best].bm) * ((N + kCfg[best].bn - 1) / kCfg[best].bn) * batch;
+  int sp = 1;
+  if (batch == 1 && t < CUS) {
+    sp = (int)((CUS + t - 1) / t);
+    const int maxs = K / 512;                  // keep >= 8 K-tiles per split
+    if (sp > maxs) sp = maxs;
+    if (sp < 1) sp = 1;
+    if (sp > 16) sp = 16;
+  }
+  *splits = sp;
+}
+
+}  // namespace
+
+// Returns the workspace bytes the fast path needs for (M, N, K, batch) with config (cfg, splits) chosen by plan().
+DL4J_API long long dl4j_gemm_plan(int M, int N, int K, int batch, int* cfg, int* splits) {
+  plan(M, N, K, batch, cfg, splits);
+  if (*splits <= 1) return 0;
+  int kps = (K + *splits - 1) / *splits;
+  kps = (kps + 63) / 64 * 64;
+  *splits = (K + kps - 1) / kps;
+  return *splits > 1 ? (long long)(*splits) * M * N * 4 : 0;
+}
+
+// Fast path. in_dt: 1 bf16, 2 f16. out_dt: 0 f32, 1 bf16, 2 f16. akc/bkc: operand layout flags (see top).
+// Requirements (else -1): lda/ldb multiples of 8 elements and 16-byte aligned bases; K % 8 == 0 for K-contiguous
+// operands, M % 8 == 0 (N % 8 == 0) for an M- (N-) contiguous A (B); batch > 1 only without split-K.
+DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, const void* A, long long lda, int akc,
+                       long long sA, const void* B, long long ldb, int bkc, long long sB, void* C, long long ldc,
+                       long long sC, float alpha, float beta, const float* bias, int bias_mode, int act, void* Z,
+                       int cfg, int splits, float* ws, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (in_dt != 1 && in_dt != 2) return -1;
+  if ((lda & 7) || (ldb & 7) || (reinterpret_cast<uintptr_t>(A) & 15) || (reinterpret_cast<uintptr_t>(B) & 15)) return -1;
+  if (batch > 1 && ((sA & 7) || (sB & 7))) return -1;
+  if ((akc && (K & 7)) || (!akc && (M & 7)) || (bkc && (K & 7)) || (!bkc && (N & 7))) return -1;
+  if (K <= 0) return -1;
+  if (cfg < 0 || cfg > 4 || splits < 1) plan(M, N, K, batch, &cfg, &splits);
+  if (cfg == 3 && !bkc) cfg = 2;                 // the 64-wide tile has no N-contiguous image
+  if (cfg == 4) {                                // 8-phase: K % 64 and 32-bit element offsets
+    const long long ea = akc ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M;
+    const long long eb = bkc ? (long long)(N - 1) * ldb + K : (long long)(K - 1) * ldb + N;
+    if (K % 64 != 0 || ea >= 0x7fffffffLL || eb >= 0x7fffffffLL) { cfg = 0; }
+  }
+  if (batch > 1) splits = 1;
+  GemmArgs g;
+  g.A = A; g.B = B; g.C = C; g.Z = Z; g.bias = bias; g.ws = ws;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.sA = sA; g.sB = sB; g.sC = sC;
+  g.M = M; g.N = N; g.K = K;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + 63) / 64 * 64;
+  splits = (K + kps - 1) / kps;
+  if (splits > 1 && ws == nullptr) return -2;
+  g.kps = kps; g.splits = splits;
+  g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
+  {
+    const int esz = out_dt == 0 ? 4 : 2;
+    g.coalesce = ((ldc * esz) % 16 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0 &&
+                  (batch == 1 || (sC * esz) % 16 == 0)) ? 1 : 0;
+  }
+  g.tiles_m = (M + kCfg[cfg].bm - 1) / kCfg[cfg].bm;
+  g.tiles_n = (N + kCfg[cfg].bn - 1) / kCfg[cfg].bn;
+  const int e = in_dt == 1 ? launch_fast_l<1>(cfg, akc, bkc, g, batch, s) : launch_fast_l<2>(cfg, akc, bkc, g, batch, s);
+  if (e || splits <= 1) return e;
+  const long long total = (long long)M * ((N + 3) / 4);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g);
+  return (int)hipGetLastError();
+}
+
+// Generic path: any dtype (0 f32 / 1 bf16 / 2 f16 input), any element strides, exact fp32 MFMA.
+DL4J_API int dl4j_gemm_simple(int in_dt, int out_dt, int M, int N, int K, int batch, const void* A, long long sam,
+                              long long sak, long long sA, const void* B, long long sbk, long long sbn, long long sB,
+                              void* C, long long ldc, long long sC, float alpha, float beta, const float* bias,
+                              int bias_mode, int act, void* Z, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  GemmArgs g = {};
+  g.C = C; g.Z = Z; g.bias = bias; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
+  g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
+  SimpleArgs sa;
+  sa.A = A; sa.B = B; sa.sam = sam; sa.sak = sak; sa.sbk = sbk; sa.sbn = sbn;
+  sa.bA = sA; sa.bB = sB; sa.bC = sC; sa.in_dt = in_dt;
+  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  hipLaunchKernelGGL(gemm_simple, dim3(tiles, 1, batch), dim3(256), 0, s, g, sa);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,268 @@
+"""``mmul`` — the framework's matrix multiply, on the in-tree MFMA kernels of ``csrc/gemm.hip``.
+
+    C = act(alpha * A @ B + bias + beta * C)          A [.., M, K], B [.., K, N]  (optional 3-D batch)
+
+Reference call sites this serves: nn/layers/BaseLayer.java:86,97,334-336 (preOutput, backprop dW / eps),
+BaseOutputLayer.java:151,178, recurrent/LSTMHelpers.java:206,212,522,616-676, SameDiff ``mmul``.
+
+* Transposes are free: a transposed torch view only changes the operand-layout flag handed to the kernel
+  (K- vs M/N-contiguous). A column-major destination (e.g. a DL4J 'f'-order weight-gradient view) is filled as
+  C^T = B^T A^T by swapping the operands.
+* bf16 / fp16 operands with 16-byte-addressable layouts run the LDS-DMA MFMA kernel (fp32 accumulation, split-K
+  with a deterministic reduce when the tile grid alone cannot fill 256 CUs); fp32 operands and odd layouts run the
+  exact-fp32 MFMA kernel. fp64 (gradient checks) and CPU tensors use torch — on a GPU tensor that is counted as a
+  helper fallback (``ops.fallback``).
+* Everything launches on torch's current stream (HIP-graph capturable); split-K slabs come from torch's caching
+  allocator.
+"""
+import ctypes
+import os
+
+import torch
+
+from . import fallback
+from .dispatch import use_native
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+ACT = {None: 0, "identity": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "gelu": 4}
+_c = ctypes
+_sig_done = [False]
+_env = os.environ.get("DL4J_AMD_GEMM_CFG")          # "cfg,splits" override for tuning sweeps
+_FORCE_CFG = tuple(int(v) for v in _env.split(",")) if _env else None
+
+
+def _lib():
+    from . import native
+    lib = native.load()
+    if not _sig_done[0]:
+        V, I, LL, F = _c.c_void_p, _c.c_int, _c.c_longlong, _c.c_float
+        lib.dl4j_gemm_plan.argtypes = [I, I, I, I, _c.POINTER(I), _c.POINTER(I)]
+        lib.dl4j_gemm_plan.restype = LL
+        lib.dl4j_gemm.argtypes = [I, I, I, I, I, I, V, LL, I, LL, V, LL, I, LL, V, LL, LL, F, F, V, I, I, V, I, I, V, V]
+        lib.dl4j_gemm.restype = I
+        lib.dl4j_gemm_simple.argtypes = [I, I, I, I, I, I, V, LL, LL, LL, V, LL, LL, LL, V, LL, LL, F, F, V, I, I, V, V]
+        lib.dl4j_gemm_simple.restype = I
+        _sig_done[0] = True
+    return lib
+
+
+_TUNED = {}                                            # problem key -> (cfg, splits), filled by _autotune
+_TUNE = os.environ.get("DL4J_AMD_GEMM_TUNE", "1") == "1"
+
+
+def _plan(lib, M, N, K, batch):
+    cfg, sp = _c.c_int(-1), _c.c_int(0)
+    lib.dl4j_gemm_plan(M, N, K, batch, _c.byref(cfg), _c.byref(sp))
+    return cfg.value, sp.value
+
+
+def _candidates(M, N, K, batch, default):
+    c = [default]
+    if K % 64 == 0:
+        c += [(4, s) for s in (1, 2, 3, 4, 6, 8) if s == 1 or (batch == 1 and K // s >= 256)]
+    c += [(x, 1) for x in (0, 1, 2, 3)]
+    if batch == 1:
+        c += [(x, s) for x in (1, 2, 3) for s in (2, 4) if K // s >= 256]
+    seen, out = set(), []
+    for x in c:
+        if x not in seen:
+            seen.add(x)
+            out.append(x)
+    return out
+
+
+def _autotune(launch, c_t, M, N, K, batch, default):
+    """First eager call of a problem shape: time every kernel configuration (tile shape x split-K) on a scratch
+    destination and keep the fastest (hipBLASLt-style heuristics replaced by measurement). Never runs while a HIP
+    graph is being captured; the cost-model plan is used there."""
+    tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
+    best, best_t = default, None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for cand in _candidates(M, N, K, batch, default):
+        if launch(cand[0], cand[1], tmp, 0.0, None) != 0:
+            continue
+        ev0.record()
+        for _ in range(3):
+            launch(cand[0], cand[1], tmp, 0.0, None)
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1)
+        if best_t is None or t < best_t:
+            best, best_t = cand, t
+    return best
+
+
+def _p(t):
+    return None if t is None else _c.c_void_p(t.data_ptr())
+
+
+def _a_layout(t):
+    """(kc, ld) for an [M, K] operand view, or None when neither dimension is unit-stride."""
+    M, K = t.shape[-2], t.shape[-1]
+    s0, s1 = t.stride(-2), t.stride(-1)
+    if s1 == 1 or K == 1:
+        return True, (s0 if M > 1 else (K + 7) // 8 * 8)
+    if s0 == 1 or M == 1:
+        return False, (s1 if K > 1 else (M + 7) // 8 * 8)
+    return None
+
+
+def _b_layout(t):
+    """(kc, ld) for a [K, N] operand view: kc=True when K is the unit-stride dimension."""
+    K, N = t.shape[-2], t.shape[-1]
+    s0, s1 = t.stride(-2), t.stride(-1)
+    if s0 == 1 or K == 1:
+        return True, (s1 if N > 1 else (K + 7) // 8 * 8)
+    if s1 == 1 or N == 1:
+        return False, (s0 if K > 1 else (N + 7) // 8 * 8)
+    return None
+
+
+def _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z):
+    cd = a.dtype if a.dtype in (torch.float64, torch.float32) else torch.float32
+    r = torch.matmul(a.to(cd), b.to(cd))
+    if alpha != 1.0:
+        r = r * alpha
+    if bias is not None:
+        r = r + (bias.to(cd).reshape(1, -1) if bias_dim == 1 else bias.to(cd).reshape(-1, 1))
+    if beta != 0.0 and out is not None:
+        r = r + beta * out.to(cd)
+    if z is not None:
+        z.copy_(r)
+    r = _torch_act(r, act)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r.to(out_dtype)
+
+
+def _torch_act(r, act):
+    if act in (None, "identity"):
+        return r
+    if act == "relu":
+        return torch.relu(r)
+    if act == "tanh":
+        return torch.tanh(r)
+    if act == "sigmoid":
+        return torch.sigmoid(r)
+    if act == "gelu":
+        return torch.nn.functional.gelu(r)
+    raise ValueError(act)
+
+
+def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, out_dtype=None, z=None):
+    """``out = act(alpha * a @ b + bias + beta * out)``; returns ``out`` (allocated row-major when None).
+
+    a: [M, K] or [B, M, K]; b: [K, N] or [B, K, N]; bias: [N] (bias_dim=1) or [M] (bias_dim=0);
+    z: optional tensor like ``out`` receiving the pre-activation; out_dtype defaults to a.dtype.
+    """
+    if b.dtype != a.dtype:
+        b = b.to(a.dtype)
+    out_dtype = out.dtype if out is not None else (out_dtype or a.dtype)
+    if not use_native(a, "gemm"):
+        return _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z)
+    if a.dtype not in _DT or out_dtype not in _DT or (z is not None and z.dtype != out_dtype):
+        fallback.record("gemm", f"dtype {a.dtype}->{out_dtype}")
+        return _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z)
+    batched = a.dim() == 3 or b.dim() == 3
+    if batched:
+        if a.dim() == 2:
+            a = a.unsqueeze(0).expand(b.shape[0], -1, -1)
+        if b.dim() == 2:
+            b = b.unsqueeze(0).expand(a.shape[0], -1, -1)
+        batch = a.shape[0]
+    else:
+        batch = 1
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    if b.shape[-2] != K:
+        raise ValueError(f"mmul shape mismatch {tuple(a.shape)} x {tuple(b.shape)}")
+    if out is None:
+        out = torch.empty(((batch,) if batched else ()) + (M, N), dtype=out_dtype, device=a.device)
+        if beta != 0.0:
+            raise ValueError("beta != 0 needs an existing out")
+    if M == 0 or N == 0:
+        return out
+    if K == 0:
+        out.zero_() if beta == 0.0 else out.mul_(beta)
+        return out
+    if bias is not None:
+        bias = bias.reshape(-1)
+        if bias.dtype != torch.float32 or not bias.is_contiguous():
+            bias = bias.to(torch.float32).contiguous()
+    bmode = 0 if bias is None else (1 if bias_dim == 1 else 2)
+    c_t = out
+    swap = False
+    if out.stride(-1) == 1 or N == 1:
+        ldc = out.stride(-2) if M > 1 else N
+    elif out.stride(-2) == 1 or M == 1:
+        swap = True
+        ldc = out.stride(-1) if N > 1 else M
+    else:
+        c_t = torch.empty(out.shape, dtype=out_dtype, device=a.device)
+        ldc = N
+        if beta != 0.0:
+            c_t.copy_(out)
+    if z is not None and (z.shape != out.shape or z.stride() != c_t.stride()):
+        fallback.record("gemm", "pre-activation layout differs from output")
+        return _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z)
+    la, lb = _a_layout(a), _b_layout(b)
+    sA = a.stride(0) if batched else 0
+    sB = b.stride(0) if batched else 0
+    sC = c_t.stride(0) if batched else 0
+    lib = _lib()
+    from .native import _stream
+    actc = ACT[act]
+    if swap:
+        # C^T [N, M] = B^T A^T
+        Mx, Nx = N, M
+        A_, B_ = b, a
+        la_, lb_ = lb, la
+        sA_, sB_ = sB, sA
+        bmode = {0: 0, 1: 2, 2: 1}[bmode]
+    else:
+        Mx, Nx = M, N
+        A_, B_ = a, b
+        la_, lb_ = la, lb
+        sA_, sB_ = sA, sB
+    in_dt = _DT[a.dtype]
+    rc = -1
+    if in_dt != 0 and la_ is not None and lb_ is not None:
+        def launch(cfg, sp, dst, bt, zz):
+            ws = torch.empty(Mx * Nx * sp, dtype=torch.float32, device=a.device) if sp > 1 else None
+            return lib.dl4j_gemm(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), la_[1], int(la_[0]), sA_, _p(B_),
+                                 lb_[1], int(lb_[0]), sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc,
+                                 _p(zz), cfg, sp, _p(ws), _stream())
+
+        key = (Mx, Nx, K, batch, in_dt, _DT[out_dtype], la_[0], lb_[0], la_[1] % 64 == 0, lb_[1] % 64 == 0)
+        if _FORCE_CFG is not None:
+            cfg = _FORCE_CFG
+        else:
+            cfg = _TUNED.get(key)
+            if cfg is None:
+                cfg = _plan(lib, Mx, Nx, K, batch)
+                if _TUNE and not torch.cuda.is_current_stream_capturing():
+                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg)
+                    _TUNED[key] = cfg
+        rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
+    if rc == -1:
+        # exact-fp32 MFMA kernel: any dtype / strides
+        if swap:
+            sam, sak = A_.stride(-1), A_.stride(-2)
+            sbk, sbn = B_.stride(-1), B_.stride(-2)
+        else:
+            sam, sak = A_.stride(-2), A_.stride(-1)
+            sbk, sbn = B_.stride(-2), B_.stride(-1)
+        rc = lib.dl4j_gemm_simple(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), sam, sak, sA_, _p(B_), sbk, sbn,
+                                  sB_, _p(c_t), ldc, sC, float(alpha), float(beta), _p(bias), bmode, actc, _p(z),
+                                  _stream())
+    if rc != 0:
+        raise RuntimeError(f"HIP gemm failed with code {rc} (M={M} N={N} K={K} batch={batch})")
+    if c_t is not out:
+        out.copy_(c_t)
+    return out
+
+
+def linear(x, W, b=None, act=None, z=None, out_dtype=None):
+    """x [M, K] @ W [K, N] + b — DL4J preOutput (BaseLayer.java:334-336) with a fused bias / activation epilogue."""
+    return mmul(x, W, bias=b, act=act, z=z, out_dtype=out_dtype)

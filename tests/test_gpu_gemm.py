@@ -1,0 +1,175 @@
+"""GPU numerics of the in-tree MFMA GEMM (csrc/gemm.hip) against a plain fp32 torch reference.
+
+Covers the four operand layouts (K- vs M/N-contiguous A and B, i.e. every transpose combination), bf16 / fp16 /
+fp32 inputs, fp32 / bf16 outputs, bias (per column / per row), activations, beta-accumulate, column-major
+('f'-order) destinations, 3-D batches, split-K, odd shapes (generic kernel) and the bench shapes of BERT-base,
+the char-LSTM and the ResNet-50 classifier. Asymmetric random operands (guide §3: A=I with asymmetric B catches a
+transposed C-write).
+"""
+import pytest
+import torch
+
+from deeplearning4j_amd.ops import fallback, gemm
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ref(a, b, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, c0=None):
+    r = alpha * (a.float() @ b.float())
+    if bias is not None:
+        r = r + (bias.float().reshape(1, -1) if bias_dim == 1 else bias.float().reshape(-1, 1))
+    if beta:
+        r = r + beta * c0.float()
+    return gemm._torch_act(r, act)
+
+
+def _tol(dt, K):
+    if dt == torch.float32:
+        return 1e-4 * max(1.0, K ** 0.5)
+    return (2e-2 if dt == torch.bfloat16 else 4e-3) * max(1.0, (K / 64) ** 0.5)
+
+
+def _mk(shape, dt, contig_last=True):
+    """Operand with the requested logical shape; contig_last=False gives the transposed-view layout."""
+    if contig_last:
+        return torch.randn(*shape, device=DEV).to(dt)
+    return torch.randn(*shape[::-1], device=DEV).to(dt).t()
+
+
+def _check(out, ref, dt, K, what=""):
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= _tol(dt, K) * scale, f"{what}: max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+def test_layouts(dt, a_kc, b_kc):
+    torch.manual_seed(0)
+    M, N, K = 320, 264, 200
+    a = _mk((M, K), dt, contig_last=a_kc)
+    b = _mk((K, N), dt, contig_last=not b_kc)
+    fallback.reset()
+    out = gemm.mmul(a, b, out_dtype=torch.float32)
+    _check(out, _ref(a, b), dt, K, f"layout a_kc={a_kc} b_kc={b_kc}")
+    assert fallback.count() == 0
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(4096, 2304, 768), (4096, 768, 768), (4096, 3072, 768), (4096, 768, 3072),
+                                   (768, 2304, 4096), (3072, 768, 4096), (512, 1000, 2048), (2048, 1000, 512),
+                                   (4096, 1024, 256), (1024, 256, 4096), (8, 16, 64), (1, 8, 8)])
+def test_bench_shapes(dt, shape):
+    torch.manual_seed(1)
+    M, N, K = shape
+    a = torch.randn(M, K, device=DEV).to(dt)
+    b = torch.randn(K, N, device=DEV).to(dt)
+    out = gemm.mmul(a, b)
+    _check(out, _ref(a, b), dt, K, f"shape {shape}")
+
+
+@pytest.mark.parametrize("act", [None, "relu", "tanh", "sigmoid", "gelu"])
+def test_epilogue_bias_act_z(act):
+    torch.manual_seed(2)
+    M, N, K = 777, 520, 256
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16() * 0.1
+    bias = torch.randn(N, device=DEV)
+    z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    out = gemm.mmul(a, b, bias=bias, act=act, z=z)
+    ref_z = _ref(a, b, bias)
+    _check(z, ref_z, torch.bfloat16, K, "pre-activation")
+    _check(out, gemm._torch_act(ref_z, act), torch.bfloat16, K, f"act {act}")
+
+
+def test_row_bias_alpha_beta_fp32_out():
+    torch.manual_seed(3)
+    M, N, K = 512, 384, 1024
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16().t()
+    c0 = torch.randn(M, N, device=DEV)
+    bias = torch.randn(M, device=DEV)
+    out = c0.clone()
+    gemm.mmul(a, b, out=out, bias=bias, bias_dim=0, alpha=0.5, beta=1.0)
+    _check(out, _ref(a, b, bias, 0, None, 0.5, 1.0, c0), torch.bfloat16, K, "alpha/beta/row-bias")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_column_major_destination(dt):
+    """dW = x^T delta written straight into an 'f'-order [nIn, nOut] view (DL4J Dense gradient layout)."""
+    torch.manual_seed(4)
+    mb, nIn, nOut = 384, 200, 136
+    x = torch.randn(mb, nIn, device=DEV).to(dt)
+    d = torch.randn(mb, nOut, device=DEV).to(dt)
+    flat = torch.zeros(nIn * nOut, device=DEV)
+    view = flat.view(nOut, nIn).t()                     # column-major [nIn, nOut]
+    gemm.mmul(x.t(), d, out=view)
+    _check(view, _ref(x.t(), d), dt, mb, "column-major dW")
+
+
+def test_batched():
+    torch.manual_seed(5)
+    a = torch.randn(6, 128, 64, device=DEV).bfloat16()
+    b = torch.randn(6, 96, 64, device=DEV).bfloat16().transpose(1, 2)
+    out = gemm.mmul(a, b, out_dtype=torch.float32)
+    ref = torch.bmm(a.float(), b.float())
+    _check(out, ref, torch.bfloat16, 64, "batched")
+
+
+def test_split_k_deterministic():
+    torch.manual_seed(6)
+    a = torch.randn(256, 8192, device=DEV).bfloat16()
+    b = torch.randn(8192, 256, device=DEV).bfloat16()
+    o1 = gemm.mmul(a, b, out_dtype=torch.float32)
+    o2 = gemm.mmul(a, b, out_dtype=torch.float32)
+    assert torch.equal(o1, o2)
+    _check(o1, _ref(a, b), torch.bfloat16, 8192, "split-K")
+
+
+def test_identity_asymmetric():
+    """A = I, asymmetric B: a transposed C-write would show."""
+    n = 256
+    eye = torch.eye(n, device=DEV).bfloat16()
+    b = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 97).bfloat16()
+    out = gemm.mmul(eye, b, out_dtype=torch.float32)
+    assert torch.equal(out, b.float())
+
+
+def test_odd_shapes_generic_kernel():
+    torch.manual_seed(7)
+    for (M, N, K) in [(3, 5, 7), (33, 17, 9), (130, 1, 70)]:
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        b = torch.randn(K, N, device=DEV).bfloat16()
+        _check(gemm.mmul(a, b, out_dtype=torch.float32), _ref(a, b), torch.bfloat16, K, f"odd {M},{N},{K}")
+
+
+def test_graph_capture():
+    torch.manual_seed(8)
+    a = torch.randn(1024, 2048, device=DEV).bfloat16()
+    b = torch.randn(2048, 512, device=DEV).bfloat16()
+    out = torch.empty(1024, 512, device=DEV, dtype=torch.float32)
+    gemm.mmul(a, b, out=out)                       # warm (allocates split-K workspace outside capture)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gemm.mmul(a, b, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    _check(out, _ref(a, b), torch.bfloat16, 2048, "graph replay")
+
+
+@pytest.mark.parametrize("cfg", [(0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (4, 3), (2, 2)])
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
+    """Each kernel configuration (incl. the 8-phase 256x256 one and split-K) on every layout, with M/N tails."""
+    torch.manual_seed(9)
+    M, N, K = 552, 328, 384
+    a = _mk((M, K), torch.bfloat16, contig_last=a_kc)
+    b = _mk((K, N), torch.bfloat16, contig_last=not b_kc)
+    monkeypatch.setattr(gemm, "_FORCE_CFG", cfg)
+    out = gemm.mmul(a, b, out_dtype=torch.float32)
+    _check(out, _ref(a, b), torch.bfloat16, K, f"cfg {cfg} a_kc={a_kc} b_kc={b_kc}")
