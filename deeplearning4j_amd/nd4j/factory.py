@@ -250,12 +250,13 @@ class Nd4j:
         A, B = _unwrap(a), _unwrap(b)
         A = A.t() if transposeA else A
         B = B.t() if transposeB else B
-        r = alpha * (A @ B)
+        from ..ops.gemm import mmul as _mm
         if c is not None:
             ct = _unwrap(c)
             with torch.no_grad():
-                ct.copy_(r + beta * ct if beta != 0 else r)
+                _mm(A, B.to(A.dtype), out=ct, alpha=alpha, beta=beta)
             return c
+        r = _mm(A, B.to(A.dtype), alpha=alpha)
         return INDArray(r)
 
     @staticmethod

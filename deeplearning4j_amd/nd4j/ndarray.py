@@ -536,7 +536,9 @@ class INDArray:
 
     # matrix products
     def mmul(self, other, result=None):
-        r = torch.matmul(self._t, _unwrap(other))
+        from ..ops.gemm import mmul as _mm
+        o = _unwrap(other)
+        r = _mm(self._t, o) if self._t.dim() == 2 and o.dim() == 2 else torch.matmul(self._t, o)
         if result is not None:
             result.assign(r)
             return result

@@ -152,8 +152,32 @@ class LayerImpl:
                             self.cparams[k].copy_(p)
 
 
-def matmul(a, b):
-    return torch.matmul(a, b)
+def matmul(a, b, bias=None, out_dtype=None, act=None, z=None):
+    """``a @ b (+ bias)`` on the in-tree MFMA GEMM (ops/gemm.py); torch reference on CPU."""
+    from ...ops.gemm import mmul
+    if bias is not None:
+        bias = bias.reshape(-1)
+    return mmul(a, b, bias=bias, out_dtype=out_dtype, act=act, z=z)
+
+
+def weight_grad_(view, a, b):
+    """Gradient view <- a @ b, accumulated in fp32 by the GEMM and written straight into the (possibly 'f'-ordered)
+    flat-gradient view — no bf16 rounding of the product before the master-precision gradient."""
+    from ...ops.gemm import mmul
+    if view.dim() == 2 and tuple(view.shape) == (a.shape[-2], b.shape[-1]) and view.device == a.device:
+        mmul(a, b, out=view)
+    else:
+        copy_grad_(view, mmul(a, b, out_dtype=torch.float64 if view.dtype == torch.float64 else torch.float32))
+
+
+def bias_grad_(view, delta):
+    """Bias gradient = column sums of delta [M, N] (fp32), on the channel-sum HIP kernel when on the GPU."""
+    if delta.is_cuda and delta.dim() == 2 and delta.dtype in (torch.float32, torch.bfloat16) and delta.is_contiguous() \
+            and view.dtype == torch.float32 and view.is_contiguous() and delta.shape[1] % 8 == 0:
+        from ...ops import native
+        if native.channel_sum(delta, out=view.reshape(-1)) is not None:
+            return
+    copy_grad_(view, _acc(delta).sum(dim=0))
 
 
 def add_row(z, b):

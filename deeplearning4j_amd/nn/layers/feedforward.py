@@ -2,21 +2,19 @@
 
 Dense (reference nn/layers/BaseLayer.java:86,97,334-336): z = xW + b; a = act(z);
 backward: delta = act'(z)*eps; dW = x^T delta; db = sum(delta); eps_prev = delta W^T.
-The GEMMs are plain library GEMMs (hipBLASLt through torch); the bf16 path keeps W as a bf16 shadow.
+The GEMMs run on the in-tree MFMA kernels (ops/gemm.py): bias fused into the forward epilogue, dW accumulated in
+fp32 straight into the 'f'-ordered gradient view; the bf16 path keeps W as a bf16 shadow.
 """
 import torch
 
-from .base import LayerImpl, add_row, copy_grad_
+from .base import LayerImpl, add_row, bias_grad_, copy_grad_, matmul, weight_grad_
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
 class DenseLayerImpl(LayerImpl):
     def preOutput(self, x, training=False):
         W = self.W("W")
-        z = torch.matmul(x.to(W.dtype), W)
-        if "b" in self.params:
-            z = add_row(z, self.W("b"))
-        return z
+        return matmul(x.to(W.dtype), W, bias=self.W("b") if "b" in self.params else None)
 
     def activate(self, x, training=False, mask=None):
         self.training = training
@@ -33,13 +31,13 @@ class DenseLayerImpl(LayerImpl):
         delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
         x = self.input.to(delta.dtype)
         if "W" in self.grads:
-            copy_grad_(self.grads["W"], _acc(torch.matmul(x.t(), delta)))
+            weight_grad_(self.grads["W"], x.t(), delta)
         if "b" in self.grads:
-            copy_grad_(self.grads["b"], _acc(delta).sum(dim=0))
+            bias_grad_(self.grads["b"], delta)
         if not getattr(self, "need_input_grad", True):
             return self.make_gradient(), None
         W = self.W("W")
-        eps_prev = torch.matmul(delta.to(W.dtype), W.t())
+        eps_prev = matmul(delta.to(W.dtype), W.t())
         eps_prev = self.backpropDropOut(eps_prev)
         return self.make_gradient(), eps_prev
 

@@ -9,7 +9,7 @@ import torch
 from ...ops import softmax_xent
 from ..conf.activations import ActivationSoftmax
 from ..conf.losses import LossMCXENT
-from .base import LayerImpl, add_row, copy_grad_
+from .base import LayerImpl, add_row, bias_grad_, copy_grad_, matmul, weight_grad_
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
@@ -51,10 +51,7 @@ class BaseOutputLayerImpl(LayerImpl):
         if not self.has_params:
             return x
         W = self.W("W")
-        z = torch.matmul(x.to(W.dtype), W)
-        if "b" in self.params:
-            z = add_row(z, self.W("b"))
-        return z
+        return matmul(x.to(W.dtype), W, bias=self.W("b") if "b" in self.params else None)
 
     # 2d views of input / labels / mask -------------------------------------------------------
     def _in2d(self, x):
@@ -110,11 +107,11 @@ class BaseOutputLayerImpl(LayerImpl):
         _, delta = self._loss_and_grad()
         if self.has_params:
             x = self._x2.to(delta.dtype)
-            copy_grad_(self.grads["W"], _acc(torch.matmul(x.t(), delta)))
+            weight_grad_(self.grads["W"], x.t(), delta)
             if "b" in self.grads:
-                copy_grad_(self.grads["b"], _acc(delta).sum(dim=0))
+                bias_grad_(self.grads["b"], delta)
             W = self.W("W")
-            eps2 = torch.matmul(delta.to(W.dtype), W.t())
+            eps2 = matmul(delta.to(W.dtype), W.t())
         else:
             eps2 = delta
         return self.make_gradient(), self.backpropDropOut(self._eps_from2d(eps2))

@@ -4,7 +4,7 @@ Not in the reference snapshot (no attention or LayerNorm t
 config of BASELINE.json on the same layer SPI (activate / backpropGradient writing into flat gradient views).
 
 MI355X structure of one encoder block (token-major [B*T, E] activations, bf16 compute, fp32 master weights):
-  qkv = x·Wqkv + b          one fused projection GEMM (hipBLASLt)
+  qkv = x·Wqkv + b          one fused projection GEMM (in-tree MFMA GEMM, bias in the epilogue)
   ctx = attention(qkv)      flash-style HIP kernel reading Q/K/V in place (csrc/attention.hip)
   h1  = LN(ctx·Wo + bo + x) output GEMM + LayerNorm-with-residual HIP kernel (csrc/layernorm.hip)
   h2  = LN(gelu(h1·W1 + b1)·W2 + b2 + h1)
@@ -19,7 +19,8 @@ import torch
 import torch.nn.functional as F
 
 from ... import ops
-from .base import LayerImpl, copy_grad_
+from .base import LayerImpl, copy_grad_, matmul, weight_grad_
+from ...ops.gemm import mmul
 
 
 def _native(x, op):
@@ -27,14 +28,8 @@ def _native(x, op):
 
 
 def _wgrad(view, a, b):
-    """view <- aᵀ·b. bf16 operands accumulate in fp32 and the GEMM writes the fp32 gradient view directly."""
-    if a.is_cuda and a.dtype == torch.bfloat16 and view.is_contiguous() and view.dtype == torch.float32:
-        try:
-            torch.mm(a.t(), b, out_dtype=torch.float32, out=view.view(a.shape[1], b.shape[1]))
-            return
-        except (RuntimeError, TypeError):
-            pass
-    copy_grad_(view, (a.t() @ b).to(view.dtype))
+    """view <- aᵀ·b on the in-tree GEMM: fp32 accumulation written straight into the fp32 gradient view."""
+    weight_grad_(view, a.t(), b)
 
 
 def _bsum(view, d):
@@ -151,13 +146,14 @@ class TransformerEncoderLayerImpl(LayerImpl):
         dt = self.W("Wqkv").dtype
         xt = _token_major(x).to(dt)
         m = mask.reshape(B, T) if mask is not None else None
-        qkv = torch.addmm(self.W("bqkv").reshape(-1), xt, self.W("Wqkv"))
+        qkv = matmul(xt, self.W("Wqkv"), bias=self.W("bqkv"))
         ctx, actx = _attn_fwd(qkv, B, T, H, m, c.causal)
-        a = torch.addmm(self.W("bo").reshape(-1), ctx, self.W("Wo"))
+        a = matmul(ctx, self.W("Wo"), bias=self.W("bo"))
         h1, ln1 = _ln_fwd(a, xt, self.params["ln1g"], self.params["ln1b"], c.layerNormEps)
-        z1 = torch.addmm(self.W("b1").reshape(-1), h1, self.W("W1"))
-        f = _gelu_fwd(z1)
-        f2 = torch.addmm(self.W("b2").reshape(-1), f, self.W("W2"))
+        # FFN-1 with bias + exact GELU fused into the GEMM epilogue; the pre-activation z1 is kept for backward
+        z1 = torch.empty(h1.shape[0], self.W("W1").shape[1], dtype=h1.dtype, device=h1.device)
+        f = matmul(h1, self.W("W1"), bias=self.W("b1"), act="gelu", z=z1)
+        f2 = matmul(f, self.W("W2"), bias=self.W("b2"))
         y, ln2 = _ln_fwd(f2, h1, self.params["ln2g"], self.params["ln2b"], c.layerNormEps)
         self.maskArray = mask
         if training:
@@ -175,18 +171,18 @@ class TransformerEncoderLayerImpl(LayerImpl):
         ds2 = _ln_bwd(dy, f2, h1, self.params["ln2g"], ln2, g["ln2g"], g["ln2b"])
         _wgrad(g["W2"], f, ds2)
         _bsum(g["b2"], ds2)
-        dz1 = _gelu_bwd(z1, ds2 @ self.W("W2").t())
+        dz1 = _gelu_bwd(z1, matmul(ds2, self.W("W2").t()))
         _wgrad(g["W1"], h1, dz1)
         _bsum(g["b1"], dz1)
-        dh1 = torch.addmm(ds2, dz1, self.W("W1").t())
+        dh1 = mmul(dz1, self.W("W1").t(), out=ds2, beta=1.0)          # residual gradient summed in place
         ds1 = _ln_bwd(dh1, a, xt, self.params["ln1g"], ln1, g["ln1g"], g["ln1b"])
         _wgrad(g["Wo"], ctx, ds1)
         _bsum(g["bo"], ds1)
-        dctx = ds1 @ self.W("Wo").t()
+        dctx = matmul(ds1, self.W("Wo").t())
         dqkv = _attn_bwd(dctx, qkv, B, T, c.nHeads, m, c.causal, actx)
         _wgrad(g["Wqkv"], xt, dqkv)
         _bsum(g["bqkv"], dqkv)
-        dx = torch.addmm(ds1, dqkv, self.W("Wqkv").t())
+        dx = mmul(dqkv, self.W("Wqkv").t(), out=ds1, beta=1.0)
         E = dx.shape[1]
         return self.make_gradient(), dx.reshape(B, T, E).permute(0, 2, 1)
 
@@ -238,7 +234,7 @@ class BertPoolerLayerImpl(LayerImpl):
     def activate(self, x, training=False, mask=None, **kw):
         self.input = x
         x0 = x[:, :, 0].to(self.W("W").dtype)
-        y = torch.tanh(torch.addmm(self.W("b").reshape(-1), x0, self.W("W")))
+        y = matmul(x0, self.W("W"), bias=self.W("b"), act="tanh")
         if training:
             self._c = (x0, y, x.shape)
         return y
@@ -250,7 +246,7 @@ class BertPoolerLayerImpl(LayerImpl):
         _wgrad(self.grads["W"], x0, dz)
         _bsum(self.grads["b"], dz)
         dx = torch.zeros(shape, dtype=x0.dtype, device=x0.device)
-        dx[:, :, 0] = dz @ self.W("W").t()
+        dx[:, :, 0] = matmul(dz, self.W("W").t())
         return self.make_gradient(), dx
 
     def feedForwardMaskArray(self, mask, state, mb):

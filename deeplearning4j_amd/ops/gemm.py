@@ -118,6 +118,22 @@ def _b_layout(t):
     return None
 
 
+def _fast_ok(t, lay, K, is_a):
+    """Mirror of dl4j_gemm's addressing requirements for one operand (16-byte DMA chunks)."""
+    if lay is None or t.data_ptr() % 16 or lay[1] % 8:
+        return False
+    if t.dim() == 3 and t.stride(0) % 8:
+        return False
+    return K % 8 == 0 if lay[0] else True
+
+
+def _pad_kc(t, K, K8):
+    """[.., R, K] operand -> contiguous [.., R, K8] copy with zeros in columns K..K8-1."""
+    p = torch.zeros(t.shape[:-1] + (K8,), dtype=t.dtype, device=t.device)
+    p[..., :K].copy_(t)
+    return p
+
+
 def _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z):
     cd = a.dtype if a.dtype in (torch.float64, torch.float32) else torch.float32
     r = torch.matmul(a.to(cd), b.to(cd))
@@ -207,6 +223,17 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         fallback.record("gemm", "pre-activation layout differs from output")
         return _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z)
     la, lb = _a_layout(a), _b_layout(b)
+    if a.dtype != torch.float32 and not (_fast_ok(a, la, K, True) and _fast_ok(b, lb, K, False)):
+        # odd K / leading dimensions: zero-padded K-contiguous copies (usually a small operand such as a one-hot
+        # input) keep the product on the MFMA LDS-DMA kernel instead of the scalar-load generic one
+        K8 = (K + 7) // 8 * 8
+        if K8 != K or not _fast_ok(a, la, K, True):
+            a = _pad_kc(a, K, K8)
+            la = (True, K8)
+        if K8 != K or not _fast_ok(b, lb, K, False):
+            b = _pad_kc(b.transpose(-1, -2), K, K8).transpose(-1, -2)
+            lb = (True, K8)
+        K = K8
     sA = a.stride(0) if batched else 0
     sB = b.stride(0) if batched else 0
     sC = c_t.stride(0) if batched else 0

@@ -4,7 +4,7 @@ sequences/sec and tokens/sec of a full fine-tuning step (forward, backward, Adam
 MI355X, bf16 compute / fp32 master weights, synthetic token ids, random-init weights.
 
   --impl dl4j   this framework: BertBase ComputationGraph (flash-attention + LayerNorm HIP kernels, fused QKV,
-                hipBLASLt GEMMs, fused HIP Adam updater)
+                in-tree MFMA GEMMs, fused HIP Adam updater)
   --impl torch  like-for-like PyTorch-ROCm comparator: transformers.BertForSequenceClassification in bf16 with
                 torch.optim.AdamW(fused=True) and SDPA attention
 
@@ -34,6 +34,9 @@ def run_dl4j(args, dev):
     g = torch.Generator().manual_seed(0)
     x = torch.randint(0, 30522, (args.batch, args.seq), generator=g).to(dev)
     y = torch.nn.functional.one_hot(torch.randint(0, 2, (args.batch,), generator=g), 2).float().to(dev)
+
+    if args.graph:
+        net.enableHipGraphs(True, warmup=2)
 
     def step():
         net.fit([x], [y])
@@ -71,6 +74,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", type=int, default=1, help="capture the dl4j training step in HIP graphs")
     args = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     step, nparams, score = (run_dl4j if args.impl == "dl4j" else run_torch)(args, dev)
@@ -87,7 +91,7 @@ def main():
         "metric": "BERT-base fine-tuning throughput on one MI355X", "value": round(sps * args.seq, 1),
         "unit": "tokens/sec", "sequences_per_sec": round(sps, 2), "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1000, 2), "higher_is_better": True,
-        "dtype": args.dtype, "impl": args.impl, "data": "synthetic token ids; random-init weights",
+        "dtype": args.dtype, "impl": args.impl, "hip_graph": bool(args.graph and args.impl == "dl4j"), "data": "synthetic token ids; random-init weights",
         "config": {"model": f"BERT-base ({args.layers} layers, 768 hidden, 12 heads) + classifier",
                    "batch": args.batch, "seq_len": args.seq, "params": nparams}, "final_score": score()}),
           flush=True)

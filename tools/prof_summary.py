@@ -26,6 +26,7 @@ def load(path):
 
 
 def short(n):
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
     n = n.split("(")[0]
     return n[:90]
 
