@@ -79,6 +79,8 @@ struct GemmArgs {
   int bias_mode, act, out_dt;
   int tiles_m, tiles_n;
   int coalesce;             // 1: epilogue through LDS with 16-byte row stores (host-checked alignment)
+  float* tstats;           // optional BatchNorm partial statistics of the output (8-phase kernel, no split-K)
+  int stats_P;              // number of 64-row partials (planes [3][stats_P][N])
 };
 
 __device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
@@ -176,6 +178,121 @@ __device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int 
     } else {
       for (int j = 0; j < 4; ++j) if (n + j < g.N) c[j] = to16(v[j], g.out_dt);
     }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- LDS epilogue
+// Finished fp32 accumulators leave a block through LDS: pass P, the waves owning tile rows [P*RPP, (P+1)*RPP)
+// store their raw accumulators into an fp32 [RPP][BN] image (row pitch BN*4 + 16 bytes), then every thread takes
+// 8-column chunks of whole rows, applies alpha / bias / beta*C / pre-activation Z / activation once per element
+// (bias as vector loads), converts, and writes 16-byte row segments. Direct 8-byte stores from the MFMA fragment
+// layout (16-32 rows per instruction) ran at ~1 TB/s; register pressure stays at the accumulators themselves.
+struct EpiOut {
+  char* dst;          // C (or the split-K slab)
+  long long ld;       // destination row stride (elements)
+  int dt;             // destination dtype (0 f32, 1 bf16, 2 f16)
+  bool raw;           // split-K slab: no epilogue math
+  bool vec;           // 16-byte aligned rows (ld and base) for vector stores
+};
+
+__device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, void* Zp, int m, int n, float* v) {
+  if (!o.raw) {
+    float b[8];
+    if (g.bias_mode == 1) {
+      if (n + 8 <= g.N && ((n & 3) == 0)) {
+        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+      } else {
+        for (int j = 0; j < 8; ++j) b[j] = n + j < g.N ? g.bias[n + j] : 0.f;
+      }
+    } else {
+      const float bm = g.bias_mode == 2 ? g.bias[m] : 0.f;
+      for (int j = 0; j < 8; ++j) b[j] = bm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * g.alpha + b[j];
+    if (g.beta != 0.f)
+      for (int j = 0; j < 8; ++j) if (n + j < g.N) v[j] += g.beta * ld_out(o.dst, o.dt, (long long)m * o.ld + n + j);
+    if (Zp)
+      for (int j = 0; j < 8; ++j)
+        if (n + j < g.N) {
+          const long long i = (long long)m * o.ld + n + j;
+          if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
+          else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
+        }
+    if (g.act)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
+  }
+  char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
+  if (o.vec && n + 8 <= g.N) {
+    if (o.dt == 0) {
+      reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      uint4 pk;
+      pk.x = (unsigned)to16(v[0], o.dt) | ((unsigned)to16(v[1], o.dt) << 16);
+      pk.y = (unsigned)to16(v[2], o.dt) | ((unsigned)to16(v[3], o.dt) << 16);
+      pk.z = (unsigned)to16(v[4], o.dt) | ((unsigned)to16(v[5], o.dt) << 16);
+      pk.w = (unsigned)to16(v[6], o.dt) | ((unsigned)to16(v[7], o.dt) << 16);
+      *reinterpret_cast<uint4*>(p) = pk;
+    }
+  } else {
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N) {
+        if (o.dt == 0) reinterpret_cast<float*>(p)[j] = v[j];
+        else reinterpret_cast<u16*>(p)[j] = to16(v[j], o.dt);
+      }
+  }
+}
+
+// Read-out of one pass: RPP rows x BN columns of the fp32 LDS image.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_readout(const GemmArgs& g, const EpiOut& o, void* Zp, const char* T, int mrow0,
+                                            int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int CPR = BN / 8;
+  for (int idx = tid; idx < RPP * CPR; idx += NT) {
+    const int r = idx / CPR, c = idx - (idx / CPR) * CPR;
+    const int m = mrow0 + r, n = n0 + c * 8;
+    if (m >= g.M || n >= g.N) continue;
+    const float4 a = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32);
+    const float4 b = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32 + 16);
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    epi_chunk8(g, o, Zp, m, n, v);
+  }
+}
+
+// BatchNorm partial statistics of the bf16 outputs held in an fp32 LDS image (conv epilogue -> consuming BN layer):
+// per (64-row partial, column) shifted sums S1 = sum(y - y0), S2 = sum((y - y0)^2) and the shift y0 (first row),
+// y = bf16(alpha*acc + bias) exactly as stored. Planes [3][stats_P][N]; reduced by bn_tiles_reduce.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int PARTS = RPP / 64;
+  for (int task = tid; task < PARTS * BN; task += NT) {
+    const int col = task % BN, part = task / BN;
+    const int n = n0 + col;
+    const int rbeg = mrow0 + part * 64;
+    if (n >= g.N) continue;
+    const long long pidx = rbeg / 64;
+    if (pidx >= g.stats_P) continue;
+    const int rows = min(64, g.M - rbeg);
+    const float bb = g.bias_mode == 1 ? g.bias[n] : 0.f;
+    float s1 = 0.f, s2 = 0.f, sh = 0.f;
+    if (rows > 0) {
+      const char* src = T + (part * 64) * PITCH + col * 4;
+      sh = bf2f(to16(*reinterpret_cast<const float*>(src) * g.alpha + bb, 1));
+      for (int r = 0; r < rows; ++r) {
+        const float d = bf2f(to16(*reinterpret_cast<const float*>(src + r * PITCH) * g.alpha + bb, 1)) - sh;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+      }
+    }
+    g.tstats[pidx * g.N + n] = s1;
+    g.tstats[((long long)g.stats_P + pidx) * g.N + n] = s2;
+    g.tstats[(2LL * g.stats_P + pidx) * g.N + n] = sh;
   }
 }
 
@@ -329,127 +446,51 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_glds(GemmArgs g) {
     }
   }
 
-  // ---- epilogue: acc[a][b] reg e <-> n = 32a + (e&3) + 8(e>>2) + 4h, m = 32b + (lane&31) within the wave tile
-  const int h = lane >> 5;
-  if (g.splits > 1) {
-    float* ws = g.ws + (long long)z * g.M * g.N;
-#pragma unroll
-    for (int b = 0; b < FM; ++b) {
-      const int m = m0 + wm * WTM + 32 * b + (lane & 31);
-      if (m >= g.M) continue;
-#pragma unroll
-      for (int a = 0; a < FN; ++a)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int n = n0 + wn * WTN + 32 * a + 8 * q + 4 * h;
-          float* p = ws + (long long)m * g.N + n;
-          if (n + 3 < g.N && (g.N & 3) == 0)
-            *reinterpret_cast<float4*>(p) = make_float4(acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2],
-                                                        acc[a][b][4 * q + 3]);
-          else
-            for (int j = 0; j < 4; ++j) if (n + j < g.N) p[j] = acc[a][b][4 * q + j];
-        }
-    }
-    return;
-  }
-  void* C = reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2);
-  void* Zp = g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2) : nullptr;
-#pragma unroll
-  for (int b = 0; b < FM; ++b) {
-    const int m = m0 + wm * WTM + 32 * b + (lane & 31);
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int a = 0; a < FN; ++a)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = n0 + wn * WTN + 32 * a + 8 * q + 4 * h;
-        if (n >= g.N) continue;
-        float v[4] = {acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]};
-        store4(g, C, Zp, m, n, v);
-      }
-  }
-}
-
-// ----------------------------------------------------------------------------------------------- LDS epilogue
-// Finished fp32 accumulators leave a block through LDS: pass P, the waves owning tile rows [P*RPP, (P+1)*RPP)
-// store their raw accumulators into an fp32 [RPP][BN] image (row pitch BN*4 + 16 bytes), then every thread takes
-// 8-column chunks of whole rows, applies alpha / bias / beta*C / pre-activation Z / activation once per element
-// (bias as vector loads), converts, and writes 16-byte row segments. Direct 8-byte stores from the MFMA fragment
-// layout (16-32 rows per instruction) ran at ~1 TB/s; register pressure stays at the accumulators themselves.
-struct EpiOut {
-  char* dst;          // C (or the split-K slab)
-  long long ld;       // destination row stride (elements)
-  int dt;             // destination dtype (0 f32, 1 bf16, 2 f16)
-  bool raw;           // split-K slab: no epilogue math
-  bool vec;           // 16-byte aligned rows (ld and base) for vector stores
-};
-
-__device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, void* Zp, int m, int n, float* v) {
-  if (!o.raw) {
-    float b[8];
-    if (g.bias_mode == 1) {
-      if (n + 8 <= g.N && ((n & 3) == 0)) {
-        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
-        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
-      } else {
-        for (int j = 0; j < 8; ++j) b[j] = n + j < g.N ? g.bias[n + j] : 0.f;
-      }
-    } else {
-      const float bm = g.bias_mode == 2 ? g.bias[m] : 0.f;
-      for (int j = 0; j < 8; ++j) b[j] = bm;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * g.alpha + b[j];
-    if (g.beta != 0.f)
-      for (int j = 0; j < 8; ++j) if (n + j < g.N) v[j] += g.beta * ld_out(o.dst, o.dt, (long long)m * o.ld + n + j);
-    if (Zp)
-      for (int j = 0; j < 8; ++j)
-        if (n + j < g.N) {
-          const long long i = (long long)m * o.ld + n + j;
-          if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
-          else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
-        }
-    if (g.act)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
-  }
-  char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
-  if (o.vec && n + 8 <= g.N) {
-    if (o.dt == 0) {
-      reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
-      reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-      uint4 pk;
-      pk.x = (unsigned)to16(v[0], o.dt) | ((unsigned)to16(v[1], o.dt) << 16);
-      pk.y = (unsigned)to16(v[2], o.dt) | ((unsigned)to16(v[3], o.dt) << 16);
-      pk.z = (unsigned)to16(v[4], o.dt) | ((unsigned)to16(v[5], o.dt) << 16);
-      pk.w = (unsigned)to16(v[6], o.dt) | ((unsigned)to16(v[7], o.dt) << 16);
-      *reinterpret_cast<uint4*>(p) = pk;
-    }
-  } else {
-    for (int j = 0; j < 8; ++j)
-      if (n + j < g.N) {
-        if (o.dt == 0) reinterpret_cast<float*>(p)[j] = v[j];
-        else reinterpret_cast<u16*>(p)[j] = to16(v[j], o.dt);
-      }
-  }
-}
-
-// Read-out of one pass: RPP rows x BN columns of the fp32 LDS image.
-template <int RPP, int BN, int NT>
-__device__ __forceinline__ void epi_readout(const GemmArgs& g, const EpiOut& o, void* Zp, const char* T, int mrow0,
-                                            int n0, int tid) {
+  // ---- epilogue through LDS (see epi_readout): acc[a][b] reg e <-> tile column wn*WTN + 32a + (e&3) + 8(e>>2) +
+  // 4h, tile row wm*WTM + 32b + (lane&31); passes of RPP rows sized to the operand ring's LDS
   constexpr int PITCH = BN * 4 + 16;
-  constexpr int CPR = BN / 8;
-  for (int idx = tid; idx < RPP * CPR; idx += NT) {
-    const int r = idx / CPR, c = idx - (idx / CPR) * CPR;
-    const int m = mrow0 + r, n = n0 + c * 8;
-    if (m >= g.M || n >= g.N) continue;
-    const float4 a = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32);
-    const float4 b = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32 + 16);
-    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    epi_chunk8(g, o, Zp, m, n, v);
+  constexpr int RPP0 = (STAGES * SBYTES) / PITCH;
+  constexpr int RPP = RPP0 >= BM ? BM : (RPP0 >= BM / 2 ? BM / 2 : BM / 4);
+  static_assert(RPP >= 64 && RPP % 64 == 0, "epilogue pass too small");
+  const int h = lane >> 5;
+  const bool split = g.splits > 1;
+  EpiOut o;
+  o.raw = split;
+  o.dt = split ? 0 : g.out_dt;
+  o.dst = split ? reinterpret_cast<char*>(g.ws + (long long)z * g.M * g.N)
+                : reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2);
+  o.ld = split ? g.N : g.ldc;
+  o.vec = split ? ((g.N & 3) == 0) : (g.coalesce != 0);
+  void* Zp = (!split && g.Z) ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2) : nullptr;
+  wait_vm<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+#pragma unroll
+  for (int P = 0; P < BM / RPP; ++P) {
+    sfor<0, FM>([&](auto B_) {
+      constexpr int b = decltype(B_)::value;
+      const int r0 = wm * WTM + 32 * b;
+      if (r0 / RPP == P) {
+        const int lr = r0 - P * RPP + (lane & 31);
+        sfor<0, FN>([&](auto A_) {
+          constexpr int a = decltype(A_)::value;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int lc = wn * WTN + 32 * a + 8 * q + 4 * h;
+            *reinterpret_cast<float4*>(smem + lr * PITCH + lc * 4) =
+                make_float4(acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]);
+          }
+        });
+      }
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (g.tstats) epi_stats<RPP, BN, WGM * WGN * 64>(g, smem, m0 + P * RPP, n0, tid);
+    epi_readout<RPP, BN, WGM * WGN * 64>(g, o, Zp, smem, m0 + P * RPP, n0, tid);
+    if (P + 1 < BM / RPP) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+    }
   }
 }
 
@@ -745,6 +786,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
+      if (g.tstats) epi_stats<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
       epi_readout<128, 256, 512>(g, o, Zp, smem, m0 + P * 128, n0, tid);
       if (P == 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -874,7 +916,7 @@ void plan(int M, int N, int K, int batch, int* cfg, int* splits) {
       sp = (int)((CUS + t256 - 1) / t256);
       const int maxs = K / 512;
       if (sp > maxs) sp = maxs;
-      if (sp > 16) sp = 16;
+      if (sp > 256) sp = 256;
       if (sp < 1) sp = 1;
     }
     if (t256 * sp >= 128) { *cfg = 4; *splits = sp; return; }
@@ -892,7 +934,7 @@ void plan(int M, int N, int K, int batch, int* cfg, int* splits) {
     const int maxs = K / 512;                  // keep >= 8 K-tiles per split
     if (sp > maxs) sp = maxs;
     if (sp < 1) sp = 1;
-    if (sp > 16) sp = 16;
+    if (sp > 256) sp = 256;
   }
   *splits = sp;
 }
@@ -915,7 +957,7 @@ DL4J_API long long dl4j_gemm_plan(int M, int N, int K, int batch, int* cfg, int*
 DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, const void* A, long long lda, int akc,
                        long long sA, const void* B, long long ldb, int bkc, long long sB, void* C, long long ldc,
                        long long sC, float alpha, float beta, const float* bias, int bias_mode, int act, void* Z,
-                       int cfg, int splits, float* ws, hipStream_t s) {
+                       int cfg, int splits, float* ws, float* tstats, int stats_P, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (in_dt != 1 && in_dt != 2) return -1;
   if ((lda & 7) || (ldb & 7) || (reinterpret_cast<uintptr_t>(A) & 15) || (reinterpret_cast<uintptr_t>(B) & 15)) return -1;
@@ -942,6 +984,13 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   if (splits > 1 && ws == nullptr) return -2;
   g.kps = kps; g.splits = splits;
   g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
+  g.tstats = nullptr;
+  g.stats_P = 0;
+  if (tstats) {                                   // statistics only from the 8-phase epilogue without split-K
+    if (splits > 1 || batch > 1) return -3;
+    g.tstats = tstats;
+    g.stats_P = stats_P;
+  }
   {
     const int esz = out_dt == 0 ? 4 : 2;
     g.coalesce = ((ldc * esz) % 16 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0 &&

@@ -109,7 +109,8 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
 #pragma unroll
           for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == tag_base + (unsigned)t;
           if (ok) break;
-          if (wall_clock64() > deadline) {
+          // once any hand-off has timed out the launch is already invalid: stop waiting at every later step
+          if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
             __hip_atomic_store(err, 1u, RLX_AGENT);
             break;
           }
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
 #pragma unroll
         for (int q = 0; q < BATCH; ++q) ok &= (unsigned)(v[q] >> 32) == tag_base + (unsigned)tag;
         if (ok) break;
-        if (wall_clock64() > deadline) {
+        if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
           __hip_atomic_store(err, 1u, RLX_AGENT);
           break;
         }

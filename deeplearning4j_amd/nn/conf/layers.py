@@ -235,7 +235,9 @@ class EmbeddingLayer(FeedForwardLayer):
     RUNTIME = "deeplearning4j_amd.nn.layers.feedforward:EmbeddingLayerImpl"
 
     def param_specs(self):
-        specs = [ParamSpec("W", [self.nIn, self.nOut], "c", "weight", self.nIn, self.nOut)]
+        # 'f' like every DefaultParamInitializer weight (DefaultParamInitializer.java:139 reshape('f', nIn, nOut)):
+        # the coefficients.bin segment then matches a reference checkpoint element for element
+        specs = [ParamSpec("W", [self.nIn, self.nOut], "f", "weight", self.nIn, self.nOut)]
         if self.hasBias:
             specs.append(ParamSpec("b", [1, self.nOut], "c", "bias"))
         return specs

@@ -376,8 +376,10 @@ class BaseNetwork:
         it, ep = self.conf.iterationCount, self.conf.epochCount
         acc = getattr(self, "gradientsAccumulator", None)
         mb_local = batch_size
-        if acc is not None:
-            batch_size = batch_size * acc.world_size
+        if acc is not None and not getattr(acc, "average", False):
+            # summed gradients of every replica: divide by the global batch (an averaging accumulator already did
+            # the 1/world part); user accumulators without a world_size count as one replica
+            batch_size = batch_size * getattr(acc, "world_size", 1)
         reg = None
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
             reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)

@@ -186,6 +186,22 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     OH, OW = _out_hw(H, W, R, S, stride, pad4, dilation)
     if OH <= 0 or OW <= 0:
         return None
+    if _is_pointwise(R, S, stride, pad4, dilation) and GEMM_1X1:
+        # 1x1 stride-1 conv in NHWC is a plain GEMM: Y[M, K] = X[M, C] . W[K, C]^T on the 8-phase MFMA kernel, bias
+        # and the BatchNorm tile statistics in its epilogue; no weight relayout ([K][C][1][1] is already K-major)
+        from .gemm import mmul
+        x = _cl(x)
+        M = N * H * W
+        y = torch.empty((N, K, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        ts = None
+        if want_stats and C % 64 == 0 and K % 8 == 0:
+            P = 2 * ((M + 127) // 128)
+            ts = torch.empty((3, P, K), dtype=torch.float32, device=x.device)
+        mmul(x.permute(0, 2, 3, 1).reshape(M, C), w.reshape(K, C).t(),
+             out=y.permute(0, 2, 3, 1).reshape(M, K), bias=b.float() if b is not None else None, stats=ts)
+        if ts is not None:
+            y._bn_tile_stats = (ts, ts.shape[1])
+        return y
     krsc, _ = _relayout(w, True, False)
     x = _cl(x)
     y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
@@ -227,7 +243,18 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     dy = _cl(dy)
     lib = native.load()
     dx = None
-    if need_dx:
+    pw = _is_pointwise(R, S, stride, pad4, dilation) and GEMM_1X1
+    if need_dx and pw:
+        from .gemm import mmul
+        M = N * H * W
+        acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
+            and dx_accum.is_contiguous(memory_format=torch.channels_last)
+        dx = dx_accum if acc else torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
+                                              memory_format=torch.channels_last)
+        # dX[M, C] = dY[M, K] . W[K, C]  (+= the other consumer's gradient through beta)
+        mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
+             beta=1.0 if acc else 0.0)
+    elif need_dx:
         s1 = tuple(stride) == (1, 1) and tuple(dilation) == (1, 1)
         pure_1x1 = R == 1 and S == 1 and not any(pad4) and tuple(dilation) == (1, 1)
         acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
@@ -260,6 +287,21 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
             if not sym:
                 dx = dx[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W]
     dW_out = db_out = None
+    if need_dw and pw:
+        # dW[K, C] = dY^T[K, M] . X[M, C], fp32 straight into the flat-gradient view; bias = column sums of dY
+        from .gemm import mmul
+        M = N * H * W
+        direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
+        dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
+        dy_rows = dy.permute(0, 2, 3, 1).reshape(M, K)
+        mmul(dy_rows.t(), x.permute(0, 2, 3, 1).reshape(M, C), out=dWt.reshape(K, C))
+        dW_out = None if direct else dWt
+        if need_db:
+            directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+            dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
+            native.channel_sum(dy_rows, out=dbt)
+            db_out = None if directb else dbt
+        return dx, dW_out, db_out
     if need_dw:
         direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
         dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
@@ -287,6 +329,13 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
         if need_db:
             db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
     return dx, dW_out, db_out
+
+
+GEMM_1X1 = os.environ.get("DL4J_AMD_CONV1X1_GEMM", "1") == "1"
+
+
+def _is_pointwise(R, S, stride, pad4, dilation):
+    return R == 1 and S == 1 and tuple(stride) == (1, 1) and not any(pad4) and tuple(dilation) == (1, 1)
 
 
 def _out_hw_inv(OH, OW, R, S, pad4, H, W):

@@ -38,7 +38,8 @@ def _lib():
         V, I, LL, F = _c.c_void_p, _c.c_int, _c.c_longlong, _c.c_float
         lib.dl4j_gemm_plan.argtypes = [I, I, I, I, _c.POINTER(I), _c.POINTER(I)]
         lib.dl4j_gemm_plan.restype = LL
-        lib.dl4j_gemm.argtypes = [I, I, I, I, I, I, V, LL, I, LL, V, LL, I, LL, V, LL, LL, F, F, V, I, I, V, I, I, V, V]
+        lib.dl4j_gemm.argtypes = [I, I, I, I, I, I, V, LL, I, LL, V, LL, I, LL, V, LL, LL, F, F, V, I, I, V, I, I, V, V, I,
+                                  V]
         lib.dl4j_gemm.restype = I
         lib.dl4j_gemm_simple.argtypes = [I, I, I, I, I, I, V, LL, LL, LL, V, LL, LL, LL, V, LL, LL, F, F, V, I, I, V, V]
         lib.dl4j_gemm_simple.restype = I
@@ -58,11 +59,14 @@ def _plan(lib, M, N, K, batch):
 
 def _candidates(M, N, K, batch, default):
     c = [default]
+    t256 = ((M + 255) // 256) * ((N + 255) // 256) * batch
+    t128 = ((M + 127) // 128) * ((N + 127) // 128) * batch
+    splits = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     if K % 64 == 0:
-        c += [(4, s) for s in (1, 2, 3, 4, 6, 8) if s == 1 or (batch == 1 and K // s >= 256)]
+        c += [(4, s) for s in splits if s == 1 or (batch == 1 and K // s >= 512 and t256 * s <= 1024)]
     c += [(x, 1) for x in (0, 1, 2, 3)]
     if batch == 1:
-        c += [(x, s) for x in (1, 2, 3) for s in (2, 4) if K // s >= 256]
+        c += [(x, s) for x in (1, 2, 3) for s in splits[1:] if K // s >= 512 and t128 * s <= 2048]
     seen, out = set(), []
     for x in c:
         if x not in seen:
@@ -71,7 +75,7 @@ def _candidates(M, N, K, batch, default):
     return out
 
 
-def _autotune(launch, c_t, M, N, K, batch, default):
+def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True):
     """First eager call of a problem shape: time every kernel configuration (tile shape x split-K) on a scratch
     destination and keep the fastest (hipBLASLt-style heuristics replaced by measurement). Never runs while a HIP
     graph is being captured; the cost-model plan is used there."""
@@ -79,6 +83,8 @@ def _autotune(launch, c_t, M, N, K, batch, default):
     best, best_t = default, None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for cand in _candidates(M, N, K, batch, default):
+        if cand[1] > 1 and not splits_ok:
+            continue
         if launch(cand[0], cand[1], tmp, 0.0, None) != 0:
             continue
         ev0.record()
@@ -166,11 +172,13 @@ def _torch_act(r, act):
     raise ValueError(act)
 
 
-def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, out_dtype=None, z=None):
+def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, out_dtype=None, z=None, stats=None):
     """``out = act(alpha * a @ b + bias + beta * out)``; returns ``out`` (allocated row-major when None).
 
     a: [M, K] or [B, M, K]; b: [K, N] or [B, K, N]; bias: [N] (bias_dim=1) or [M] (bias_dim=0);
     z: optional tensor like ``out`` receiving the pre-activation; out_dtype defaults to a.dtype.
+    stats: optional fp32 [3, P, N] tensor (P = ceil(M/64)) receiving per-64-row BatchNorm partial statistics of the
+    bf16 output (conv -> BN fusion; 8-phase kernel).
     """
     if b.dtype != a.dtype:
         b = b.to(a.dtype)
@@ -255,13 +263,30 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     in_dt = _DT[a.dtype]
     rc = -1
     if in_dt != 0 and la_ is not None and lb_ is not None:
-        def launch(cfg, sp, dst, bt, zz):
+        def launch(cfg, sp, dst, bt, zz, ts=None):
             ws = torch.empty(Mx * Nx * sp, dtype=torch.float32, device=a.device) if sp > 1 else None
             return lib.dl4j_gemm(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), la_[1], int(la_[0]), sA_, _p(B_),
                                  lb_[1], int(lb_[0]), sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc,
-                                 _p(zz), cfg, sp, _p(ws), _stream())
+                                 _p(zz), cfg, sp, _p(ws), _p(ts), 0 if ts is None else ts.shape[1], _stream())
 
         key = (Mx, Nx, K, batch, in_dt, _DT[out_dtype], la_[0], lb_[0], la_[1] % 64 == 0, lb_[1] % 64 == 0)
+        if stats is not None:
+            if swap or batch != 1:
+                raise ValueError("GEMM BatchNorm statistics need a row-major, unbatched destination")
+            kst = key + ("stats",)
+            cfg = (_FORCE_CFG[0], 1) if _FORCE_CFG is not None else _TUNED.get(kst)
+            if cfg is None:
+                cfg = (4, 1) if K % 64 == 0 else (2, 1)
+                if _TUNE and not torch.cuda.is_current_stream_capturing():
+                    cfg = _autotune(lambda c_, s_, d_, bt_, zz_: launch(c_, s_, d_, bt_, zz_, stats), c_t, Mx, Nx, K,
+                                    batch, cfg, splits_ok=False)
+                    _TUNED[kst] = cfg
+            rc = launch(cfg[0], 1, c_t, float(beta), z, stats)
+            if rc != 0:
+                raise RuntimeError(f"HIP gemm (stats) failed with code {rc}")
+            if c_t is not out:
+                out.copy_(c_t)
+            return out
         if _FORCE_CFG is not None:
             cfg = _FORCE_CFG
         else:

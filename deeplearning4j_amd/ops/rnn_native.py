@@ -7,6 +7,7 @@ h·RW, fused gates + peepholes + mask, cell state in registers). ``lstm_seq_bwd`
 ``None`` when the shape/dtype is outside the kernels (the caller then runs the per-step path).
 """
 import ctypes
+import threading
 
 import torch
 
@@ -47,33 +48,75 @@ _SIG_COOP = [c_void_p] * 13 + [c_int, c_int, c_int, ctypes.c_uint, c_int, c_void
 
 
 class _CoopBuf:
-    """Persistent exchange buffer + error word of the cooperative kernels, and the next unused granule tag."""
+    """Persistent exchange buffer + error word of the cooperative kernels, and the next unused granule tag.
+    A pinned host copy of the error word is refreshed asynchronously after every eager launch and checked before
+    the next one, so a hand-off timeout surfaces as an exception instead of silently wrong results."""
 
     def __init__(self, nbytes, device):
         self.exch = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
         self.err = torch.empty(1, dtype=torch.int32, device=device)
+        self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.err_ev = None
         self.next_tag = None                               # None: contents undefined -> the next launch zeroes them
 
 
+class CoopTimeoutError(RuntimeError):
+    pass
+
+
 _coop_bufs = {}
+# Buffers are never freed once handed to a launch: a captured HIP graph embeds their addresses (exchange memset +
+# kernel arguments), so a buffer outgrown by a later, bigger launch is retired here instead of going back to the
+# caching allocator (ADVICE r1: replaying a graph must never write into memory another tensor owns).
+_RETIRED = []
+_lock = threading.Lock()
 
 
 def _coop_buf(kind, nbytes, device, steps):
-    """(buffer, tag_base, reset) for one launch that uses ``steps`` + 1 tags."""
-    key = (kind, str(device))
-    b = _coop_bufs.get(key)
-    if b is None or b.exch.numel() * 8 < nbytes:
-        b = _coop_bufs[key] = _CoopBuf(nbytes, device)
+    """(buffer, tag_base, reset) for one launch that uses ``steps`` + 1 tags. Buffers are per (kind, device, stream)
+    so concurrent ParallelInference workers on one device never share granules; tag allocation is locked."""
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (kind, str(device), torch.cuda.current_stream(device).cuda_stream)
+    with _lock:
+        b = _coop_bufs.get(key)
+        if b is None or b.exch.numel() * 8 < nbytes:
+            if b is not None:
+                _RETIRED.append(b)
+            b = _coop_bufs[key] = _CoopBuf(nbytes, device)
+        if not capturing and b.err_ev is not None and b.err_ev.query() and int(b.err_host[0]) != 0:
+            b.err_ev = None
+            b.next_tag = None
+            raise CoopTimeoutError(f"cooperative LSTM {kind} kernel: a cross-workgroup hand-off timed out (the "
+                                   "workgroups were not co-resident); results of that launch are invalid")
+        if capturing:
+            b.next_tag = None                              # every graph replay reuses the same tags: zero each time
+            return b, 0, 1
+        need = steps + 2
+        if b.next_tag is None or b.next_tag + need >= 0xFFFFFFF0:
+            b.next_tag = need
+            return b, 0, 1
+        base = b.next_tag
+        b.next_tag += need
+        return b, base, 0
+
+
+def _post_launch(b):
+    """Eager launches: queue an async copy of the error word into pinned memory (checked at the next launch)."""
     if torch.cuda.is_current_stream_capturing():
-        b.next_tag = None                                  # every graph replay reuses the same tags: zero each time
-        return b, 0, 1
-    need = steps + 2
-    if b.next_tag is None or b.next_tag + need >= 0xFFFFFFF0:
-        b.next_tag = need
-        return b, 0, 1
-    base = b.next_tag
-    b.next_tag += need
-    return b, base, 0
+        return
+    b.err_host.copy_(b.err, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    b.err_ev = ev
+
+
+def check_coop_errors():
+    """Synchronously raise if any cooperative LSTM launch so far hit a hand-off timeout."""
+    for b in list(_coop_bufs.values()):
+        if b.err_ev is not None:
+            b.err_ev.synchronize()
+            if int(b.err_host[0]) != 0:
+                raise CoopTimeoutError("cooperative LSTM kernel: a cross-workgroup hand-off timed out")
 
 
 def _coop_enabled():
@@ -94,6 +137,7 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, 
     if rc != 0:
         b.next_tag = None
         return False
+    _post_launch(b)
     global last_coop_err
     last_coop_err = b.err                                # device word: 1 = a hand-off wait timed out (sticky)
     return True
@@ -117,6 +161,7 @@ def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, 
     if rc != 0:
         b.next_tag = None
         return False
+    _post_launch(b)
     global last_coop_bwd_err
     last_coop_bwd_err = b.err
     return True

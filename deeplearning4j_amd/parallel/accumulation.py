@@ -77,6 +77,8 @@ class AllReduceGradientsAccumulator:
             w.wait()
         self._pending = []
         self._next = 0
+        if self.average:                   # mean over replicas (the update then divides by the local batch only)
+            net.flattenedGradients.div_(self.world_size)
 
     def broadcast_params(self, net, src=0):
         """Make every replica start from rank ``src``'s parameters and updater state."""

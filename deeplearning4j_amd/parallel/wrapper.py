@@ -42,6 +42,11 @@ class _RankShard:
         self.it, self.r, self.w = it, r, w
 
     def __iter__(self):
+        if isinstance(self.it, (list, tuple)) or not hasattr(self.it, "hasNext"):
+            src = list(self.it)                  # a list (or any iterable) of DataSets: stride it directly
+            for i in range(0, len(src) - len(src) % self.w, self.w):
+                yield src[i + self.r]
+            return
         if hasattr(self.it, "reset"):
             self.it.reset()
         buf = []

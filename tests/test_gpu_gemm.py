@@ -173,3 +173,27 @@ def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
     monkeypatch.setattr(gemm, "_FORCE_CFG", cfg)
     out = gemm.mmul(a, b, out_dtype=torch.float32)
     _check(out, _ref(a, b), torch.bfloat16, K, f"cfg {cfg} a_kc={a_kc} b_kc={b_kc}")
+
+
+@pytest.mark.parametrize("cfg", [None, (0, 1), (1, 1), (2, 1), (3, 1), (4, 1)])
+def test_bn_stats_epilogue(cfg, monkeypatch):
+    """Per-64-row BatchNorm partial statistics from the GEMM epilogue (conv -> BN fusion) match the stored output."""
+    torch.manual_seed(10)
+    M, N, K = 1000, 192, 128
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16().t()
+    bias = torch.randn(N, device=DEV)
+    P = 2 * ((M + 127) // 128)
+    ts = torch.full((3, P, N), float("nan"), device=DEV)
+    monkeypatch.setattr(gemm, "_FORCE_CFG", cfg)
+    out = gemm.mmul(a, b, bias=bias, stats=ts)
+    y = out.float()
+    for p in range(P):
+        r0, r1 = p * 64, min(M, p * 64 + 64)
+        if r1 <= r0:
+            continue
+        blk = y[r0:r1]
+        sh = blk[0]
+        assert torch.allclose(ts[2, p], sh, atol=0, rtol=0)
+        assert torch.allclose(ts[0, p], (blk - sh).sum(0), atol=1e-2, rtol=1e-4)
+        assert torch.allclose(ts[1, p], ((blk - sh) ** 2).sum(0), atol=1e-1, rtol=1e-4)

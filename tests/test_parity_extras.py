@@ -112,3 +112,24 @@ def test_parallel_wrapper_symmetric_context_equals_shared_gradients(tmp_path):
         mp.spawn(W.run_mode, args=(2, _port(), mode, path), nprocs=2, join=True)
         ps[mode] = torch.load(path, weights_only=True)["params"][0]
     assert torch.allclose(ps["ctx_sym"], ps["shared"], atol=1e-5)
+
+
+def test_embedding_weight_flat_layout_is_f_order():
+    """EmbeddingLayer W must use DL4J's 'f' order in the flat parameter vector."""
+    import torch
+    from deeplearning4j_amd.nn.conf import NeuralNetConfiguration
+    from deeplearning4j_amd.nn.conf.layers import EmbeddingLayer, OutputLayer
+    from deeplearning4j_amd.nn.multilayer import MultiLayerNetwork
+    conf = (NeuralNetConfiguration.Builder().seed(1).list()
+            .layer(EmbeddingLayer.Builder().nIn(3).nOut(2).build())
+            .layer(OutputLayer.Builder().nIn(2).nOut(2).build()).build())
+    net = MultiLayerNetwork(conf)
+    net.init()
+    n = net.numParams()
+    net.setParams(torch.arange(n, dtype=torch.float32).reshape(1, -1))
+    W = net.getLayer(0).getParam("W")
+    for i in range(3):
+        for j in range(2):
+            assert float(W[i, j]) == float(j * 3 + i)           # column-major: W[i, j] at j*nIn + i
+    out = net.output(torch.tensor([[2.0]]))
+    assert out.shape == (1, 2)

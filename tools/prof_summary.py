@@ -36,11 +36,18 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--last", type=int, default=0,
+                    help="keep only the dispatches after the last N+1-th --marker kernel (steady-state steps)")
+    ap.add_argument("--marker", default="fused_update_kernel")
     ap.add_argument("--steady", type=int, default=0,
                     help="only the last N complete training steps (split at the fused-updater kernel), so "
                          "initialisation and warm-up dispatches do not dilute per-step numbers")
     a = ap.parse_args()
     rows = load(a.path)
+    if a.last:
+        idx = [i for i, (n, _) in enumerate(rows) if a.marker in n]
+        if len(idx) > a.last:
+            rows = rows[idx[-a.last - 1] + 1:]
     if a.steady:
         steps = [[]]
         for r in rows:
