@@ -168,7 +168,7 @@ def _out_hw(H, W, R, S, stride, pad4, dilation):
     return OH, OW
 
 
-def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
+def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True):
     """want_stats: also emit per-tile BatchNorm statistics of the output from the kernel epilogue; they are attached
     to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer."""
     if not (_ok_act(x) and w.dtype == torch.bfloat16):
@@ -186,7 +186,7 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     OH, OW = _out_hw(H, W, R, S, stride, pad4, dilation)
     if OH <= 0 or OW <= 0:
         return None
-    if _is_pointwise(R, S, stride, pad4, dilation) and GEMM_1X1:
+    if _is_pointwise(R, S, stride, pad4, dilation) and use_gemm:
         # 1x1 stride-1 conv in NHWC is a plain GEMM: Y[M, K] = X[M, C] . W[K, C]^T on the 8-phase MFMA kernel, bias
         # and the BatchNorm tile statistics in its epilogue; no weight relayout ([K][C][1][1] is already K-major)
         from .gemm import mmul
@@ -220,8 +220,8 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     return y
 
 
-def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
-               dx_accum=None):
+def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
+                dx_accum=None, gemm_dx=True, gemm_dw=True):
     """grads_zeroed: the caller guarantees gW/gb (flat-gradient views) are already zero (the network clears the
     whole flat gradient with one fill per step), so no per-layer memset is launched.
     dx_accum: an existing channels-last bf16 gradient of x (another consumer's contribution); when the bwd-data
@@ -243,8 +243,8 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     dy = _cl(dy)
     lib = native.load()
     dx = None
-    pw = _is_pointwise(R, S, stride, pad4, dilation) and GEMM_1X1
-    if need_dx and pw:
+    pw = _is_pointwise(R, S, stride, pad4, dilation)
+    if need_dx and pw and gemm_dx:
         from .gemm import mmul
         M = N * H * W
         acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
@@ -287,7 +287,7 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
             if not sym:
                 dx = dx[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W]
     dW_out = db_out = None
-    if need_dw and pw:
+    if need_dw and pw and gemm_dw:
         # dW[K, C] = dY^T[K, M] . X[M, C], fp32 straight into the flat-gradient view; bias = column sums of dY
         from .gemm import mmul
         M = N * H * W
@@ -336,6 +336,79 @@ GEMM_1X1 = os.environ.get("DL4J_AMD_CONV1X1_GEMM", "1") == "1"
 
 def _is_pointwise(R, S, stride, pad4, dilation):
     return R == 1 and S == 1 and tuple(stride) == (1, 1) and not any(pad4) and tuple(dilation) == (1, 1)
+
+
+# ------------------------------------------------------------------ per-shape choice: GEMM vs implicit-GEMM kernel
+# A 1x1 stride-1 conv runs either as a plain GEMM (ops/gemm.py) or on the implicit-GEMM conv kernels; which one is
+# faster depends on the shape (small K/N layers are streaming-bound and favour different tiles). The first eager
+# call of each (direction, shape) times both on scratch outputs and remembers the winner; calls made while a HIP
+# graph is being captured use the remembered choice (GEMM when none).
+_CHOICE = {}
+
+
+def _timed(fn, reps=2):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def _choose(key, run_gemm, run_old):
+    c = _CHOICE.get(key)
+    if c is None:
+        if not GEMM_1X1:
+            return False
+        if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
+            return True
+        tg, to = _timed(run_gemm), _timed(run_old)
+        c = _CHOICE[key] = tg <= to
+    return c
+
+
+def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
+    """want_stats: also emit per-tile BatchNorm statistics of the output from the kernel epilogue; they are attached
+    to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer."""
+    use = True
+    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
+            _is_pointwise(1, 1, stride, pad4, dilation):
+        key = ("fwd", tuple(x.shape), tuple(w.shape), b is not None, bool(want_stats))
+        use = _choose(key, lambda: _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, True),
+                      lambda: _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, False))
+    return _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, use)
+
+
+def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
+               dx_accum=None):
+    """grads_zeroed: the caller guarantees gW/gb (flat-gradient views) are already zero (the network clears the
+    whole flat gradient with one fill per step), so no per-layer memset is launched.
+    dx_accum: an existing channels-last bf16 gradient of x (another consumer's contribution); when the bwd-data
+    kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx."""
+    gdx = gdw = True
+    if _ok_act(x) and _ok_act(dy) and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
+            _is_pointwise(1, 1, stride, pad4, dilation):
+        shp = (tuple(x.shape), tuple(w.shape))
+        if need_dx:
+            acc0 = dx_accum.clone() if dx_accum is not None else None
+            gdx = _choose(("dx", shp, dx_accum is not None),
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, True, False, False,
+                                              dx_accum=acc0, gemm_dx=True),
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, True, False, False,
+                                              dx_accum=acc0, gemm_dx=False))
+        if need_dw:
+            K, C = w.shape[0], w.shape[1]
+            sw = torch.zeros((K, C, 1, 1), dtype=torch.float32, device=x.device)
+            sb = torch.zeros((K,), dtype=torch.float32, device=x.device) if need_db else None
+            gdw = _choose(("dw", shp, need_db),
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, sw, sb, True,
+                                              gemm_dw=True),
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, sw, sb, True,
+                                              gemm_dw=False))
+    return _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, grads_zeroed, dx_accum,
+                       gdx, gdw)
 
 
 def _out_hw_inv(OH, OW, R, S, pad4, H, W):
