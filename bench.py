@@ -34,7 +34,10 @@ def main():
     ap.add_argument("--variant", default=os.environ.get("BENCH_VARIANT", "dl4j"), choices=["dl4j", "canonical"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", type=int, default=int(os.environ.get("BENCH_GRAPH", "-1")),
-                    help="capture the training step in HIP graphs (1 on, 0 off, -1 auto = on for one process)")
+                    help="capture the training step in HIP graphs (1 on, 0 off, -1 auto = on unless the collectives "
+                         "are not capturable, i.e. gloo)")
+    ap.add_argument("--comm-dtype", default=os.environ.get("BENCH_COMM_DTYPE", "fp32"), choices=["fp32", "bf16"],
+                    help="gradient all-reduce dtype for N > 1")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -52,11 +55,12 @@ def main():
     net = ResNet50(numLabels=1000, variant=args.variant, dataType=dt).init(device=device)
     acc = None
     if world > 1:
-        acc = AllReduceGradientsAccumulator()
+        # bucketed RCCL all-reduce overlapped with backward; captured into the step's HIP graph (nccl backend)
+        acc = AllReduceGradientsAccumulator(dtype=args.comm_dtype)
         acc.broadcast_params(net)
         net.setGradientsAccumulator(acc)
 
-    use_graph = args.graph if args.graph >= 0 else int(world == 1 and device.type == "cuda")
+    use_graph = args.graph if args.graph >= 0 else int(device.type == "cuda" and (acc is None or acc.capturable()))
     if use_graph:
         net.enableHipGraphs(True, warmup=1)
 

@@ -13,7 +13,9 @@ Design:
     A's previous replay has finished (event), while B keeps the GPU busy — no host sync in steady state.
   * All memory allocated inside the captured region comes from one private pool shared by both graphs.
   * Host-side bookkeeping (iteration count, weight-version bump, listeners' iterationDone) runs outside the graph.
-Eligibility: plain SGD-family optimizer, no TBPTT, no masks, no gradient accumulator (single process), no
+Data parallel: the AllReduceGradientsAccumulator's bucketed RCCL all-reduces are captured with the step (nccl
+backend only); gloo and custom accumulators run eager.
+Eligibility: plain SGD-family optimizer, no TBPTT, no masks, a capturable (or no) gradient accumulator, no
 listeners with per-pass hooks (onForwardPass/onBackwardPass/onGradientCalculation), CUDA device, fixed shapes.
 Anything else falls back to the eager step transparently.
 """
@@ -47,6 +49,9 @@ class CapturedTrainingStep:
             n.computeGradientAndScore(self.static_x, self.static_y, None, None, defer_reg=True)
         else:
             n.computeGradientAndScore(self.static_x[0], self.static_y[0], None, None, defer_reg=True)
+        acc = getattr(n, "gradientsAccumulator", None)
+        if acc is not None:
+            acc.reduce_gradients(n)                # bucketed RCCL all-reduces become graph nodes
         n._apply_update_kernels(self.static_x[0].shape[0])
         return n._score_t
 
@@ -100,8 +105,9 @@ def graph_eligible(net, inputs, labels, fmasks, lmasks):
         return False
     if fmasks or lmasks:
         return False
-    if getattr(net, "gradientsAccumulator", None) is not None:
-        return False
+    acc = getattr(net, "gradientsAccumulator", None)
+    if acc is not None and not (hasattr(acc, "capturable") and acc.capturable()):
+        return False                               # gloo / custom accumulators: eager steps
     algo = net.conf.globalConf.get("optimizationAlgo")
     if algo is not None and OA.of(algo) != OA.STOCHASTIC_GRADIENT_DESCENT:
         return False

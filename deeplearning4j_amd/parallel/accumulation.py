@@ -26,14 +26,39 @@ from .distributed import is_dist, world_size
 
 
 class AllReduceGradientsAccumulator:
-    def __init__(self, bucket_mb=None, average=False, dtype=None):
+    """SHARED_GRADIENTS data parallelism: bucketed all-reduce of the flat gradient, each bucket issued as soon as
+    backward has finished writing it (overlap with the rest of backward), over RCCL on GPUs.
+
+    * bucket_mb: bucket size (DL4J_AMD_BUCKET_MB, default 32 MB) — xGMI rings are per-link bound, so a few large
+      buckets beat many small ones; buckets run from the end of the flat vector (backward writes it back to front).
+    * average: all-reduce SUM then scale by 1/world here (the update then divides by the local batch only);
+      otherwise the update divides the summed gradient by the global batch (the default, numerically the
+      single-GPU large-batch step).
+    * dtype: communication dtype. torch.bfloat16 halves the bytes on the wire (each bucket is cast into a bf16
+      staging buffer, reduced, and copied back into the fp32 gradient); None keeps the gradient's own dtype.
+    * force: issue the collectives even in a one-process group (exercises the RCCL path on a single GPU);
+      DL4J_AMD_FORCE_COLLECTIVES=1 sets it.
+    Every call is stream-ordered on torch's current stream, so the whole step (collectives included) can be
+    captured into a HIP graph when the backend is nccl (RCCL supports stream capture).
+    """
+
+    def __init__(self, bucket_mb=None, average=False, dtype=None, force=None):
         self.world_size = world_size()
         self.bucket_bytes = int(float(bucket_mb or os.environ.get("DL4J_AMD_BUCKET_MB", 32)) * (1 << 20))
         self.average = average
+        if isinstance(dtype, str):
+            dtype = {"bf16": torch.bfloat16, "fp32": None, "float32": None}.get(dtype, None)
         self.comm_dtype = dtype
+        if force is None:
+            force = os.environ.get("DL4J_AMD_FORCE_COLLECTIVES", "0") == "1"
+        self.active = dist.is_available() and dist.is_initialized() and (self.world_size > 1 or bool(force))
         self._buckets = None
         self._pending = []
         self._next = 0
+
+    def capturable(self):
+        """True when the collectives can live inside a captured HIP graph (nccl/RCCL backend, or none issued)."""
+        return (not self.active) or dist.get_backend() == "nccl"
 
     def _plan(self, net):
         n = net.flattenedGradients.numel()
@@ -50,31 +75,41 @@ class AllReduceGradientsAccumulator:
         self._net = net
 
     def begin_backward(self, net):
-        if self.world_size <= 1:
+        if not self.active:
             return
         if self._buckets is None or self._net is not net:
             self._plan(net)
         self._pending = []
         self._next = 0
 
+    def _issue(self, g, s, e):
+        seg = g[s:e]
+        if self.comm_dtype is not None and self.comm_dtype != seg.dtype:
+            tmp = seg.to(self.comm_dtype)
+            self._pending.append((dist.all_reduce(tmp, op=dist.ReduceOp.SUM, async_op=True), tmp, seg))
+        else:
+            self._pending.append((dist.all_reduce(seg, op=dist.ReduceOp.SUM, async_op=True), None, None))
+
     def grad_ready(self, net, offset):
         """Called after a layer finished writing gradients at flat offset >= ``offset``."""
-        if self.world_size <= 1 or self._buckets is None:
+        if not self.active or self._buckets is None:
             return
         g = net.flattenedGradients
         while self._next < len(self._buckets) and self._buckets[self._next][0] >= offset:
             s, e = self._buckets[self._next]
-            self._pending.append(dist.all_reduce(g[s:e], op=dist.ReduceOp.SUM, async_op=True))
+            self._issue(g, s, e)
             self._next += 1
 
     def reduce_gradients(self, net):
-        if self.world_size <= 1:
+        if not self.active:
             return
         if self._buckets is None or self._net is not net:
             self._plan(net)
         self.grad_ready(net, -1)           # launch whatever is left
-        for w in self._pending:
+        for w, tmp, seg in self._pending:
             w.wait()
+            if tmp is not None:
+                seg.copy_(tmp)
         self._pending = []
         self._next = 0
         if self.average:                   # mean over replicas (the update then divides by the local batch only)

@@ -20,6 +20,7 @@ Without an initialised process group (W == 1) the wrapper simply trains the mode
 """
 import enum
 import logging
+import os
 
 from ..datasets.dataset import DataSet, MultiDataSet
 from .accumulation import AllReduceGradientsAccumulator, average_params_and_state
@@ -152,7 +153,14 @@ class ParallelWrapper:
         self._prepared = True
 
     def fit(self, source, numEpochs=1):
-        """Train on a DataSetIterator / MultiDataSetIterator (or a list of DataSets) for ``numEpochs``."""
+        """Train on a DataSetIterator / MultiDataSetIterator (or a list of DataSets) for ``numEpochs``.
+
+        Called from one plain process with ``workers > 1`` (no process group): the wrapper launches one child
+        process per worker / GPU and trains there (parallel/launcher.py), then loads the result into ``model``."""
+        if not is_dist() and self.workers > 1 and self.trainerContext is None and self.accumulator is None and \
+                os.environ.get("DL4J_AMD_PW_SPAWN", "1") == "1":
+            from .launcher import spawn_fit
+            return spawn_fit(self, source, numEpochs)
         self._prepare()
         m = self.model
         W, r = world_size(), rank()

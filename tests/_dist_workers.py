@@ -149,3 +149,57 @@ def run_es_parallel(rank, world, port, result_path):
                     "epochs": res.getTotalEpochs(), "scores": dict(res.getScoreVsEpoch())}, result_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def make_cg(seed=3, device=None):
+    """Residual conv ComputationGraph (no BatchNorm, so DP-2 equals one process at 2x batch exactly)."""
+    from deeplearning4j_amd import Activation, Adam, LossFunction, NeuralNetConfiguration
+    from deeplearning4j_amd.nn.conf.graph import ElementWiseVertex
+    from deeplearning4j_amd.nn.conf.inputs import InputType
+    from deeplearning4j_amd.nn.conf.layers import ConvolutionLayer, GlobalPoolingLayer, OutputLayer
+    from deeplearning4j_amd.nn.graph.computation_graph import ComputationGraph
+    conf = (NeuralNetConfiguration.Builder().seed(seed).updater(Adam(0.01)).graphBuilder()
+            .addInputs("in")
+            .addLayer("c1", ConvolutionLayer.Builder(3, 3).nIn(3).nOut(8).padding(1, 1)
+                      .activation(Activation.RELU).build(), "in")
+            .addLayer("c2", ConvolutionLayer.Builder(3, 3).nIn(8).nOut(8).padding(1, 1)
+                      .activation(Activation.IDENTITY).build(), "c1")
+            .addVertex("add", ElementWiseVertex(ElementWiseVertex.Op.Add), "c1", "c2")
+            .addLayer("gap", GlobalPoolingLayer.Builder().build(), "add")
+            .addLayer("out", OutputLayer.Builder(LossFunction.MCXENT).nIn(8).nOut(4)
+                      .activation(Activation.SOFTMAX).build(), "gap")
+            .setOutputs("out").setInputTypes(InputType.convolutional(8, 8, 3)).build())
+    net = ComputationGraph(conf)
+    net.init(device=device or torch.device("cpu"))
+    return net
+
+
+def make_image_batches(n, bs, seed=21):
+    from deeplearning4j_amd import DataSet
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        x = torch.randn(bs, 3, 8, 8, generator=g)
+        y = torch.zeros(bs, 4)
+        y[torch.arange(bs), torch.randint(0, 4, (bs,), generator=g)] = 1
+        out.append(DataSet(x, y))
+    return out
+
+
+def run_cg_shared(rank, world, port, result_path):
+    """SHARED_GRADIENTS on a ComputationGraph with small buckets (several all-reduces overlapped with backward)."""
+    _setup(rank, world, port)
+    from deeplearning4j_amd.parallel import ParallelWrapper, TrainingMode
+    net = make_cg()
+    if rank == 1:
+        with torch.no_grad():
+            net.flattenedParams.add_(0.5)
+    pw = ParallelWrapper.Builder(net).trainingMode(TrainingMode.SHARED_GRADIENTS).bucketSizeMB(0.0005).build()
+    pw.fit(make_image_batches(6, 4), 1)
+    p = net.params().clone()
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        torch.save({"params": [t.clone() for t in gathered], "nbuckets": len(pw.accumulator._buckets)}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

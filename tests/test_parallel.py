@@ -164,3 +164,37 @@ def test_parallel_wrapper_main_cli(tmp_path):
         assert torch.allclose(re.params(), out.params())
     finally:
         sys.path.remove(str(tmp_path))
+
+
+@pytest.mark.skipif(os.environ.get("DL4J_AMD_SKIP_SLOW") == "1", reason="slow")
+def test_parallel_wrapper_in_process_workers_spawn():
+    """ParallelWrapper.Builder(net).workers(2).build().fit(data) from ONE plain process: two child workers (gloo on
+    CPU here, RCCL on GPUs) train synchronously and the caller's model ends up equal to single-process training
+    on the concatenated batches (the reference's in-JVM ParallelWrapper contract, PW:ParallelWrapper.java:467-565)."""
+    from deeplearning4j_amd import Adam, DataSet
+    from deeplearning4j_amd.parallel import ParallelWrapper
+    batches = W.make_batches(8, 8)
+    net = W.make_net(Adam(0.01))
+    ParallelWrapper.Builder(net).workers(2).build().fit(batches, 2)       # a plain list source (ADVICE r1)
+    ref = W.make_net(Adam(0.01))
+    for _ in range(2):
+        for i in range(0, 8, 2):
+            a, b = batches[i], batches[i + 1]
+            ref.fit(DataSet(torch.cat([a.features, b.features]), torch.cat([a.labels, b.labels])))
+    assert torch.allclose(net.params(), ref.params(), atol=1e-5), (net.params() - ref.params()).abs().max()
+
+
+def test_cg_shared_gradients_bucketed_equals_large_batch(tmp_path):
+    """ComputationGraph DP-2 with several gradient buckets issued during backward == one process at 2x batch."""
+    from deeplearning4j_amd import DataSet
+    path = str(tmp_path / "cg.pt")
+    mp.spawn(W.run_cg_shared, args=(2, _port(), path), nprocs=2, join=True)
+    res = torch.load(path, weights_only=True)
+    p0, p1 = res["params"]
+    assert torch.equal(p0, p1)
+    assert res["nbuckets"] > 2
+    net = W.make_cg()
+    b = W.make_image_batches(6, 4)
+    for i in range(0, 6, 2):
+        net.fit(DataSet(torch.cat([b[i].features, b[i + 1].features]), torch.cat([b[i].labels, b[i + 1].labels])))
+    assert torch.allclose(net.params(), p0, atol=1e-5), (net.params() - p0).abs().max()
