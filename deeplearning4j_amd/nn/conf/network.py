@@ -320,11 +320,18 @@ class MultiLayerConfiguration(Config):
     @staticmethod
     def fromYaml(s):
         import yaml
-        return _decode(yaml.safe_load(s))
+        return MultiLayerConfiguration.fromJson(yaml.safe_load(s))
+
+    def toJson(self):
+        """DL4J's Jackson schema (see nn/conf/dl4j_json.py): readable by the reference's MultiLayerConfiguration."""
+        from .dl4j_json import to_json
+        return to_json(self)
 
     @staticmethod
     def fromJson(s):
-        return _decode(json.loads(s))
+        from .dl4j_json import from_json, is_dl4j_format
+        d = json.loads(s) if isinstance(s, str) else s
+        return from_json(d) if is_dl4j_format(d) else _decode(d)
 
 
 class GraphBuilder:
@@ -515,9 +522,17 @@ class ComputationGraphConfiguration(Config):
     def getLayerActivationTypes(self):
         return getattr(self, "_types", None) or self.addPreProcessorsAndInferNIn()
 
+    def toJson(self):
+        """DL4J's Jackson schema (see nn/conf/dl4j_json.py): readable by the reference's
+        ComputationGraphConfiguration."""
+        from .dl4j_json import to_json
+        return to_json(self)
+
     @staticmethod
     def fromJson(s):
-        return _decode(json.loads(s))
+        from .dl4j_json import from_json, is_dl4j_format
+        d = json.loads(s) if isinstance(s, str) else s
+        return from_json(d) if is_dl4j_format(d) else _decode(d)
 
     def toYaml(self):
         import yaml
@@ -526,7 +541,7 @@ class ComputationGraphConfiguration(Config):
     @staticmethod
     def fromYaml(s):
         import yaml
-        return _decode(yaml.safe_load(s))
+        return ComputationGraphConfiguration.fromJson(yaml.safe_load(s))
 
 
 _ = (GraphVertex, InputType)

@@ -32,6 +32,14 @@ def _open_out(f):
     return f, False
 
 
+def _config_from_json(text):
+    """configuration.json in DL4J's Jackson schema (nn/conf/dl4j_json.py) or this framework's earlier tagged form."""
+    from ..nn.conf.base import _decode
+    from ..nn.conf.dl4j_json import from_json, is_dl4j_format
+    d = json.loads(text)
+    return from_json(d) if is_dl4j_format(d) else _decode(d)
+
+
 class ModelSerializer:
     @staticmethod
     def writeModel(model, f, saveUpdater=True, dataNormalization=None):
@@ -68,8 +76,7 @@ class ModelSerializer:
         names = set(z.namelist())
         if CONFIG not in names:
             raise ValueError("Invalid model file: no configuration.json")
-        from ..nn.conf.base import _decode
-        cfg = _decode(json.loads(z.read(CONFIG).decode("utf-8")))
+        cfg = _config_from_json(z.read(CONFIG).decode("utf-8"))
         from ..nn.conf.network import ComputationGraphConfiguration, MultiLayerConfiguration
         if kind == "mln" and not isinstance(cfg, MultiLayerConfiguration):
             raise ValueError("File does not contain a MultiLayerNetwork (use restoreComputationGraph)")
@@ -165,9 +172,8 @@ class ModelGuesser:
 
     @staticmethod
     def loadConfigGuess(path):
-        from ..nn.conf.base import _decode
         with open(path) as fh:
-            return _decode(json.load(fh))
+            return _config_from_json(fh.read())
 
 
 _ = torch
