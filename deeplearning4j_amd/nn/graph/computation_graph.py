@@ -491,6 +491,25 @@ class ComputationGraph(BaseNetwork):
                 score += float(layer.computeScore(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0, training))
             return score
 
+    def scoreExamples(self, data, addRegularizationTerms=True):
+        """Per-example score, summed over the output layers (reference ComputationGraph.scoreExamples,
+        NN:nn/graph/ComputationGraph.java:2386-2403); regularisation terms added to every example when asked."""
+        ds = data if isinstance(data, (DataSet, MultiDataSet)) else data.next()
+        if isinstance(ds, DataSet):
+            ds = MultiDataSet.fromDataSet(ds)
+        with torch.no_grad():
+            self.feedForward(ds.features, False, ds.featuresMasks)
+            l1, l2 = self._regularization_terms() if addRegularizationTerms else (0.0, 0.0)
+            total = None
+            for i, o in enumerate(self.outputs):
+                layer = self.layers_by_name[o]
+                layer.setLabels(self._to_dev(ds.labels[i], self.master_dtype))
+                if ds.labelsMasks and i < len(ds.labelsMasks) and ds.labelsMasks[i] is not None:
+                    layer.maskArray = self._to_dev(ds.labelsMasks[i])
+                s = layer.computeScoreForExamples(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0)
+                total = s if total is None else total + s
+            return total
+
     def evaluate(self, it, labelsList=None, topN=1):
         from ...eval.evaluation import Evaluation
         return self.doEvaluation(it, Evaluation(labelsList, topN=topN))[0]
@@ -549,6 +568,59 @@ class ComputationGraph(BaseNetwork):
         for l in self.layers_by_name.values():
             if hasattr(l, "rnnClearPreviousState"):
                 l.rnnClearPreviousState()
+
+    def rnnGetPreviousState(self, layerName):
+        """Stored rnnTimeStep state of one recurrent layer (reference ComputationGraph.rnnGetPreviousState,
+        NN:nn/graph/ComputationGraph.java:2805-2855)."""
+        layer = self.layers_by_name[layerName] if isinstance(layerName, str) else self.getLayers()[layerName]
+        return layer.rnnGetPreviousState() if hasattr(layer, "rnnGetPreviousState") else None
+
+    def rnnSetPreviousState(self, layerName, state):
+        layer = self.layers_by_name[layerName] if isinstance(layerName, str) else self.getLayers()[layerName]
+        if not hasattr(layer, "rnnSetPreviousState"):
+            raise ValueError(f"layer {layerName} is not a recurrent layer")
+        layer.rnnSetPreviousState(state)
+
+    def rnnGetPreviousStates(self):
+        return {n: l.rnnGetPreviousState() for n, l in self.layers_by_name.items() if hasattr(l, "rnnGetPreviousState")}
+
+    def rnnSetPreviousStates(self, states):
+        for n, st in states.items():
+            self.rnnSetPreviousState(n, st)
+
+    # ------------------------------------------------------------------------------ pretraining
+    def pretrainLayer(self, layerName, data, numEpochs=1):
+        """Unsupervised pretraining of one AutoEncoder / VAE vertex (reference ComputationGraph.pretrainLayer,
+        NN:nn/graph/ComputationGraph.java:669-722): its input is the inference-mode activation of its input vertices."""
+        if not self.initCalled:
+            self.init()
+        impl = self.layers_by_name[layerName]
+        if not hasattr(impl, "computePretrainGradientAndScore"):
+            return self
+        v = self.conf.vertices[layerName]
+        for _ in range(int(numEpochs)):
+            items = [data] if isinstance(data, (DataSet, MultiDataSet)) else data
+            if not isinstance(items, list):
+                items.reset()
+            for ds in items:
+                feats = [ds.features] if isinstance(ds, DataSet) else ds.features
+                with torch.no_grad():
+                    acts = self.feedForward(feats, False)
+                    ins = [acts[i] for i in self.vertex_inputs[layerName]]
+                    x = ins[0] if len(ins) == 1 else torch.cat(ins, dim=1)
+                    if v.preProcessor is not None:
+                        x = v.preProcessor.preProcess(x, x.shape[0], False)
+                self._pretrain_step(impl, x)
+        return self
+
+    def pretrain(self, data, numEpochs=1):
+        """Layer-wise pretraining of every pretrainable vertex in topological order (reference
+        ComputationGraph.pretrain)."""
+        for name in self.topo:
+            l = self.layers_by_name.get(name)
+            if l is not None and hasattr(l, "computePretrainGradientAndScore"):
+                self.pretrainLayer(name, data, numEpochs)
+        return self
 
     # ------------------------------------------------------------------------------ misc
     def clone(self):

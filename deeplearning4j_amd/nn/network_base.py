@@ -392,6 +392,18 @@ class BaseNetwork:
             if getattr(impl.conf, "constraints", None):
                 impl.applyConstraints(it, ep)
 
+    # ------------------------------------------------------------------------------ helper fallbacks
+    def helperCountFail(self):
+        """Number of GPU op calls that could not run on an in-tree HIP kernel and took a library / torch path
+        (reference ConvolutionLayer.helperCountFail, NN:nn/layers/convolution/ConvolutionLayer.java:58,173-200 —
+        here counted process-wide per op; see ops/fallback.py, DL4J_AMD_STRICT_KERNELS=1 makes them errors)."""
+        from ..ops import fallback
+        return fallback.count()
+
+    def fallbackSummary(self):
+        from ..ops import fallback
+        return fallback.summary()
+
     # ------------------------------------------------------------------------------ HIP graphs
     def enableHipGraphs(self, enabled=True, warmup=2):
         """Capture the training iteration into HIP graphs after ``warmup`` eager iterations of a fixed batch

@@ -25,6 +25,8 @@ def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1, want_stats=
         y = native.conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats)
         if y is not None:
             return y
+    from .fallback import note
+    note(x, "conv", f"fwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4
     if b is not None:
         b = b.to(x.dtype)
@@ -44,6 +46,8 @@ def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_
                                grads_zeroed, dx_accum)
         if r is not None:
             return r
+    from .fallback import note
+    note(x, "conv", f"bwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4
     sym = _sym(pad4)
     xin = x if sym else F.pad(x, (pl, pr, pt, pb))
@@ -68,6 +72,8 @@ def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_
 
 
 def conv_transpose2d_forward(x, w, b, stride, padding, dilation=(1, 1)):
+    from .fallback import note
+    note(x, "deconv", "library transposed convolution")
     return F.conv_transpose2d(x, w, b, tuple(stride), tuple(padding), 0, 1, tuple(dilation))
 
 

@@ -278,7 +278,9 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             native._check(rc, "conv_bwd_data_1x1")
         else:
             from .conv import _sym
+            from .fallback import record
             import torch.nn.functional as F
+            record("conv", f"bwd-data stride {tuple(stride)} kernel {R}x{S}: library path")
             sym = _sym(pad4)
             xin = x if sym else F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
             padding = [pad4[0], pad4[2]] if sym else [0, 0]

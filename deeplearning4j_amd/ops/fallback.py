@@ -21,6 +21,13 @@ def record(op, reason):
         raise KernelFallbackError(f"{op}: no in-tree HIP kernel for this call ({reason})")
 
 
+def note(t, op, reason):
+    """Record a fallback when ``t`` lives on the GPU (CPU tensors always take the torch reference path)."""
+    import torch
+    if torch.is_tensor(t) and t.is_cuda:
+        record(op, reason)
+
+
 def count(op=None):
     if op is None:
         return sum(_COUNTS.values())

@@ -19,6 +19,8 @@ def softmax_xent(logits, labels, mask=None, clip_eps=1e-10):
         r = native.softmax_xent(logits, labels, clip_eps)
         if r is not None:
             return r
+    from .fallback import note
+    note(logits, "softmax_xent", f"{logits.dtype} mask={mask is not None}")
     z = _acc(logits)
     logp = torch.log_softmax(z, dim=1)
     if clip_eps:

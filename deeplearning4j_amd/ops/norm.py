@@ -32,6 +32,8 @@ def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=Fal
         r = native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual)
         if r is not None:
             return r
+    from .fallback import note
+    note(x, "bn", f"torch path ({x.dtype}, dim {x.dim()})")
     xf = _acc(x)
     dims = _dims(x)
     bs = _bshape(x)

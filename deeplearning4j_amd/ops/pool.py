@@ -18,6 +18,8 @@ def pool2d_forward(x, ptype, kernel, stride, pad4, dilation=(1, 1), pnorm=2, eps
         r = native.pool2d_fwd(x, ptype, kernel, stride, pad4)
         if r is not None:
             return r
+    from .fallback import note
+    note(x, "pool", f"{ptype} {x.dtype}")
     if ptype == "MAX":
         xp = F.pad(x, (pl, pr, pt, pb), value=float("-inf")) if any(pad4) else x
         y, idx = F.max_pool2d(xp, tuple(kernel), tuple(stride), 0, tuple(dilation), return_indices=True)
