@@ -1,15 +1,22 @@
-"""SameDiff-lite: a define-by-run differentiable graph API for user-defined layers.
+"""SameDiff: a graph-building differentiable API with its own reverse-mode autodiff.
 
-The reference's SameDiff layer bridge (nn/conf/layers/samediff/BaseSameDiffLayer.java:43,
-nn/layers/samediff/SameDiffLayer.java:58-87,195-215) lets a user describe a layer's forward pass with the
-``SameDiff`` op API; DL4J runs ``execAndEndResult`` forward and ``execBackwards`` for the gradients.
-Here ``SameDiff`` records the same calls eagerly on PyTorch-ROCm tensors (autograd supplies the backward),
-so a layer written against the reference API (``sd.mmul("mmul", x, w)``, ``z.add("z", b)``,
-``Activation.TANH.asSameDiff("out", sd, z)``, ``sd.nn().relu(...)``) runs unchanged on the GPU. Only the
-op surface the reference layer tests use plus the common math/NN ops is provided.
+The reference's SameDiff (used through the SameDiff layer bridge, NN:nn/conf/layers/samediff/BaseSameDiffLayer.java:43,
+NN:nn/layers/samediff/SameDiffLayer.java:58-87,195-215 execAndEndResult / execBackwards) records ops into a graph and
+differentiates it op by op. Here every op is an entry of the registry in ``samediff/autodiff.py`` with an explicit
+forward and backward (no torch.autograd); ``SameDiff`` records ``(output, op name, input variables, JSON attributes)``
+and executes eagerly at definition time (so ``eval``/``getArr`` work immediately), can re-execute the recorded graph
+for new placeholder values (``output``), differentiate it (``execBackwards``, ``calculateGradients``), train it
+(``setTrainingConfig`` + ``fit``: reverse pass + one fused HIP updater launch over all trainable variables) and
+save / load it (``save`` / ``SameDiff.load``: graph JSON + variable arrays). Heavy ops run on the framework's
+kernels in both directions (GEMM, conv, pooling, LayerNorm, flash attention, LSTM, softmax-xent).
 """
+import io
+import json
+import zipfile
+
 import torch
-import torch.nn.functional as F
+
+from .autodiff import REGISTRY
 
 
 class SDVariable:
@@ -17,42 +24,53 @@ class SDVariable:
         self.sd, self.name, self.value = sd, name, value
 
     # ------------------------------------------------------------ arithmetic (named and anonymous forms)
-    def _bin(self, name, other, fn):
+    def _bin(self, name, other, op):
         if isinstance(name, (SDVariable, int, float)) or torch.is_tensor(name):
             name, other = None, name
-        return self.sd._op(name, fn, self, other)
+        return self.sd._op(name, op, [self, other])
 
     def add(self, name, other=None):
-        return self._bin(name, other, torch.add)
+        return self._bin(name, other, "add")
 
     def sub(self, name, other=None):
-        return self._bin(name, other, torch.sub)
+        return self._bin(name, other, "sub")
 
     def mul(self, name, other=None):
-        return self._bin(name, other, torch.mul)
+        return self._bin(name, other, "mul")
 
     def div(self, name, other=None):
-        return self._bin(name, other, torch.div)
+        return self._bin(name, other, "div")
 
     def rsub(self, name, other=None):
-        return self._bin(name, other, lambda a, b: b - a)
+        return self._bin(name, other, "rsub")
 
     def rdiv(self, name, other=None):
-        return self._bin(name, other, lambda a, b: b / a)
+        return self._bin(name, other, "rdiv")
 
     def mmul(self, name, other=None):
-        return self._bin(name, other, torch.matmul)
+        return self._bin(name, other, "mmul")
 
     def pow(self, name, p=None):
-        return self._bin(name, p, torch.pow)
+        if not isinstance(name, str) and name is not None:
+            name, p = None, name
+        return self.sd._op(name, "pow", [self], {"p": float(p)})
 
     def __add__(self, o):
+        return self.add(None, o)
+
+    def __radd__(self, o):
         return self.add(None, o)
 
     def __sub__(self, o):
         return self.sub(None, o)
 
+    def __rsub__(self, o):
+        return self.rsub(None, o)
+
     def __mul__(self, o):
+        return self.mul(None, o)
+
+    def __rmul__(self, o):
         return self.mul(None, o)
 
     def __truediv__(self, o):
@@ -62,27 +80,30 @@ class SDVariable:
         return self.mmul(None, o)
 
     def __neg__(self):
-        return self.sd._op(None, torch.neg, self)
+        return self.sd._op(None, "neg", [self])
 
     # ------------------------------------------------------------ reductions / shape
     def sum(self, *dims):
-        return self.sd._op(None, lambda t: t.sum(dim=dims) if dims else t.sum(), self)
+        return self.sd._op(None, "sum", [self], {"dims": list(dims)})
 
     def mean(self, *dims):
-        return self.sd._op(None, lambda t: t.mean(dim=dims) if dims else t.mean(), self)
+        return self.sd._op(None, "mean", [self], {"dims": list(dims)})
 
     def reshape(self, *shape):
-        return self.sd._op(None, lambda t: t.reshape(*shape), self)
+        if len(shape) == 1 and isinstance(shape[0], (list, tuple)):
+            shape = tuple(shape[0])
+        return self.sd._op(None, "reshape", [self], {"shape": [int(s) for s in shape]})
 
     def permute(self, *dims):
-        return self.sd._op(None, lambda t: t.permute(*dims), self)
+        return self.sd._op(None, "permute", [self], {"dims": [int(d) for d in dims]})
 
     def transpose(self):
-        return self.sd._op(None, lambda t: t.transpose(-1, -2), self)
+        return self.sd._op(None, "transpose", [self])
 
     def get(self, *idx):
         """Python-style indexing / slicing (e.g. ``h.get(slice(None), 0)`` = the first token of every row)."""
-        return self.sd._op(None, lambda t: t[idx], self)
+        enc = [{"slice": [i.start, i.stop, i.step]} if isinstance(i, slice) else i for i in idx]
+        return self.sd._op(None, "get", [self], {"idx": enc})
 
     def getShape(self):
         return list(self.value.shape)
@@ -93,6 +114,10 @@ class SDVariable:
     def eval(self):
         return self.value.detach()
 
+    def gradient(self):
+        """Gradient of the loss w.r.t. this variable from the last ``execBackwards`` / ``fit`` reverse pass."""
+        return self.sd._last_grads.get(self.name)
+
     def __repr__(self):
         return f"SDVariable(name={self.name!r}, shape={list(self.value.shape)})"
 
@@ -101,53 +126,51 @@ class _NN:
     def __init__(self, sd):
         self.sd = sd
 
-    def _u(self, name, x, fn):
+    def _u(self, name, x, op, attrs=None):
         if isinstance(name, SDVariable):
             name, x = None, name
-        return self.sd._op(name, fn, x)
+        return self.sd._op(name, op, [x], attrs)
 
     def relu(self, name, x=None, cutoff=0.0):
-        return self._u(name, x, lambda t: torch.relu(t - cutoff) + cutoff if cutoff else torch.relu(t))
+        return self._u(name, x, "relu")
 
     def sigmoid(self, name, x=None):
-        return self._u(name, x, torch.sigmoid)
+        return self._u(name, x, "sigmoid")
 
     def tanh(self, name, x=None):
-        return self._u(name, x, torch.tanh)
+        return self._u(name, x, "tanh")
 
     def softmax(self, name, x=None):
-        return self._u(name, x, lambda t: torch.softmax(t, dim=-1))
+        return self._u(name, x, "softmax")
 
     def gelu(self, name, x=None):
-        return self._u(name, x, F.gelu)
+        return self._u(name, x, "gelu")
 
     def elu(self, name, x=None):
-        return self._u(name, x, F.elu)
+        return self._u(name, x, "elu")
 
     def leakyRelu(self, name, x=None, alpha=0.01):
-        return self._u(name, x, lambda t: F.leaky_relu(t, alpha))
+        return self._u(name, x, "leakyRelu", {"alpha": float(alpha)})
 
     def softplus(self, name, x=None):
-        return self._u(name, x, F.softplus)
+        return self._u(name, x, "softplus")
 
     def linear(self, name, x, w=None, b=None):
         if isinstance(name, SDVariable):
             name, x, w, b = None, name, x, w
-        return self.sd._op(name, lambda a, ww, bb: a @ ww if bb is None else a @ ww + bb, x, w, b)
+        return self.sd._op(name, "linear", [x, w, b])
 
     def layerNorm(self, name, x, gain=None, bias=None, eps=1e-5):
         """LayerNorm over the last dim (LayerNorm HIP kernels on the GPU)."""
         if isinstance(name, SDVariable):
             name, x, gain, bias = None, name, x, gain
-        from .native_ops import layer_norm
-        return self.sd._op(name, lambda t, g, bb: layer_norm(t, g, bb, eps), x, gain, bias)
+        return self.sd._op(name, "layerNorm", [x, gain, bias], {"eps": float(eps)})
 
-    def fusedSelfAttention(self, name, qkv, nHeads, mask=None, causal=False):
+    def fusedSelfAttention(self, name, qkv=None, nHeads=None, mask=None, causal=False):
         """Multi-head self attention on a fused projection qkv [B, T, 3E] -> [B, T, E] (flash-attention kernel)."""
         if isinstance(name, SDVariable):
-            name, qkv, nHeads = None, name, qkv
-        from .native_ops import self_attention
-        return self.sd._op(name, lambda q, m: self_attention(q, nHeads, m, causal), qkv, mask)
+            name, qkv, nHeads, mask = None, name, qkv, nHeads
+        return self.sd._op(name, "fusedSelfAttention", [qkv, mask], {"nHeads": int(nHeads), "causal": bool(causal)})
 
 
 class _RNN:
@@ -157,9 +180,7 @@ class _RNN:
     def lstmLayer(self, name, x, W, RW, b, h0=None, c0=None, peephole=False):
         """Whole-sequence LSTM (DL4J gate order, tanh/sigmoid): x [mb, nIn, T] -> [mb, H, T]. Runs the fused
         sequence HIP kernels on the GPU (csrc/lstm.hip); RW has 3 extra peephole columns when ``peephole``."""
-        from .native_ops import lstm_layer
-        return self.sd._op(name, lambda x_, w_, rw_, b_, h_, c_: lstm_layer(x_, w_, rw_, b_, h_, c_, peephole),
-                           x, W, RW, b, h0, c0)
+        return self.sd._op(name, "lstmLayer", [x, W, RW, b, h0, c0], {"peephole": bool(peephole)})
 
 
 class _CNN:
@@ -169,14 +190,16 @@ class _CNN:
     def conv2d(self, name, x, w, b=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
         if isinstance(name, SDVariable):
             name, x, w, b = None, name, x, w
-        return self.sd._op(name, lambda t, ww, bb: F.conv2d(t, ww, None if bb is None else bb.reshape(-1), tuple(stride),
-                                                            tuple(padding), tuple(dilation)), x, w, b)
+        return self.sd._op(name, "conv2d", [x, w, b], {"stride": list(stride), "padding": list(padding),
+                                                          "dilation": list(dilation)})
 
     def maxPooling2d(self, name, x, kernel, stride, padding=(0, 0)):
-        return self.sd._op(name, lambda t: F.max_pool2d(t, kernel, stride, padding), x)
+        return self.sd._op(name, "maxPooling2d", [x], {"kernel": list(kernel), "stride": list(stride),
+                                                        "padding": list(padding)})
 
     def avgPooling2d(self, name, x, kernel, stride, padding=(0, 0)):
-        return self.sd._op(name, lambda t: F.avg_pool2d(t, kernel, stride, padding), x)
+        return self.sd._op(name, "avgPooling2d", [x], {"kernel": list(kernel), "stride": list(stride),
+                                                        "padding": list(padding)})
 
 
 class _Loss:
@@ -191,21 +214,14 @@ class _Loss:
 
     def softmaxCrossEntropy(self, name, labels, logits, weights=None, labelSmoothing=0.0):
         """Softmax over the last dimension of ``logits``; labels one-hot (or soft) of the same shape."""
-        def f(y, z):
-            if labelSmoothing:
-                y = y * (1 - labelSmoothing) + labelSmoothing / y.shape[-1]
-            lp = torch.log_softmax(z.float(), dim=-1)
-            return -(y.float() * lp).sum(-1).mean()
-        return self._reg(self.sd._op(name, f, labels, logits))
+        return self._reg(self.sd._op(name, "softmaxCrossEntropy", [labels, logits],
+                                     {"labelSmoothing": float(labelSmoothing)}))
 
     def meanSquaredError(self, name, labels, predictions, weights=None):
-        return self._reg(self.sd._op(name, lambda y, z: ((z.float() - y.float()) ** 2).mean(), labels, predictions))
+        return self._reg(self.sd._op(name, "meanSquaredError", [labels, predictions]))
 
     def logLoss(self, name, labels, predictions, weights=None, epsilon=1e-7):
-        def f(y, p):
-            p = p.float().clamp(epsilon, 1 - epsilon)
-            return -(y * torch.log(p) + (1 - y) * torch.log(1 - p)).mean()
-        return self._reg(self.sd._op(name, f, labels, predictions))
+        return self._reg(self.sd._op(name, "logLoss", [labels, predictions], {"epsilon": float(epsilon)}))
 
 
 class TrainingConfig:
@@ -254,18 +270,18 @@ class TrainingConfig:
 
 
 class SameDiff:
-    """Define-by-run graph that also RECORDS every op: the values are computed eagerly on PyTorch-ROCm tensors (so
-    ``execBackwards`` / ``eval`` work immediately, as in SameDiff layers), and the recorded op list can be replayed
-    for new placeholder values (``output``) or trained (``setTrainingConfig`` + ``fit``; backward by autograd over the
-    replayed ops, one fused HIP updater launch over all trainable variables)."""
+    """A recorded differentiable graph (see module docstring)."""
 
     def __init__(self):
         self.variables = {}
+        self._kind = {}                 # name -> VARIABLE | PLACEHOLDER | CONSTANT | ARRAY
         self._n = 0
-        self._ops = []                  # (output name, fn, args) in definition order
+        self._ops = []                  # records: (output name, op name, input refs, attrs) in definition order
+        self._ctx = {}                  # output name -> saved forward context of its op
         self._placeholders = []
         self._trainable = []
         self._loss_names = []
+        self._last_grads = {}
         self.trainingConfig = None
         self._train_state = None
         self.iterationCount = 0
@@ -275,24 +291,50 @@ class SameDiff:
     def create():
         return SameDiff()
 
-    def _new(self, name, value):
+    # ------------------------------------------------------------------ definition
+    def _new(self, name, value, kind):
         if name is None:
             self._n += 1
             name = f"sd_var_{self._n}"
         v = SDVariable(self, name, value)
         self.variables[name] = v
+        self._kind[name] = kind
         return v
 
-    def _op(self, name, fn, *args):
-        vals = [a.value if isinstance(a, SDVariable) else a for a in args]
-        v = self._new(name, fn(*vals))
-        self._ops.append((v.name, fn, args))
+    def _ref(self, a):
+        """Input reference of an op: a variable name, a python scalar, or None."""
+        if a is None:
+            return None
+        if isinstance(a, SDVariable):
+            return a.name
+        if isinstance(a, (int, float, bool)):
+            return {"scalar": a}
+        if torch.is_tensor(a):
+            return self.constant(None, a).name
+        raise TypeError(f"unsupported SameDiff op input {type(a)}")
+
+    def _val(self, r):
+        if r is None:
+            return None
+        if isinstance(r, dict):
+            return r["scalar"]
+        return self.variables[r].value
+
+    def _op(self, name, op, args, attrs=None):
+        if op not in REGISTRY:
+            raise KeyError(f"unknown SameDiff op {op!r}")
+        refs = [self._ref(a) for a in args]
+        attrs = dict(attrs or {})
+        y, ctx = REGISTRY[op].fwd([self._val(r) for r in refs], attrs)
+        v = self._new(name, y, "ARRAY")
+        self._ctx[v.name] = ctx
+        self._ops.append((v.name, op, refs, attrs))
         return v
 
-    def var(self, name, value):
+    def var(self, name, value, *shape):
         if not torch.is_tensor(value):
-            value = torch.as_tensor(value)
-        v = self._new(name, value)
+            value = torch.as_tensor(value) if not shape else torch.zeros(shape)
+        v = self._new(name, value, "VARIABLE")
         self._trainable.append(v.name)
         return v
 
@@ -303,12 +345,12 @@ class SameDiff:
             dims = [1 if d is None or d < 0 else int(d) for d in shape] if shape else [1]
             dt = value if isinstance(value, torch.dtype) else torch.float32
             value = torch.zeros(dims, dtype=dt)
-        v = self._new(name, value)
+        v = self._new(name, value, "PLACEHOLDER")
         self._placeholders.append(v.name)
         return v
 
     def constant(self, name, value):
-        return self._new(name, torch.as_tensor(value).detach())
+        return self._new(name, torch.as_tensor(value).detach(), "CONSTANT")
 
     def loss(self):
         return _Loss(self)
@@ -322,33 +364,77 @@ class SameDiff:
     def trainableVariables(self):
         return [self.variables[n] for n in self._trainable]
 
-    # ------------------------------------------------------------------ replay
-    def _replay(self, feeds, targets=None):
-        """Re-run the recorded ops (only those ``targets`` depend on, when given) with new placeholder values."""
+    def ops(self):
+        """The recorded graph: [(output, op, inputs, attrs)]."""
+        return list(self._ops)
+
+    # ------------------------------------------------------------------ execution
+    def _needed(self, targets):
+        if targets is None:
+            return list(self._ops)
+        need = set(targets)
+        keep = []
+        for rec in reversed(self._ops):
+            if rec[0] in need:
+                keep.append(rec)
+                need.update(r for r in rec[2] if isinstance(r, str))
+        return keep[::-1]
+
+    def _exec(self, feeds, targets=None):
+        """Re-run the recorded ops (those ``targets`` depend on) with new placeholder values; saves contexts."""
         for k, v in feeds.items():
             self.variables[k].value = v
-        ops = self._ops
-        if targets is not None:
-            need = set(targets)
-            keep = []
-            for name, fn, args in reversed(self._ops):
-                if name in need:
-                    keep.append((name, fn, args))
-                    need.update(a.name for a in args if isinstance(a, SDVariable))
-            ops = keep[::-1]
-        for name, fn, args in ops:
-            vals = [self.variables[a.name].value if isinstance(a, SDVariable) else a for a in args]
-            self.variables[name].value = fn(*vals)
+        for out, op, refs, attrs in self._needed(targets):
+            y, ctx = REGISTRY[op].fwd([self._val(r) for r in refs], attrs)
+            self.variables[out].value = y
+            self._ctx[out] = ctx
+
+    def _backward(self, seeds, wrt, targets=None):
+        """Reverse pass from ``seeds`` {variable name: upstream gradient} over the recorded ops; returns
+        {name: gradient} for ``wrt`` (every op's explicit backward; no torch.autograd)."""
+        grads = dict(seeds)
+        for out, op, refs, attrs in reversed(self._needed(targets if targets is not None else list(seeds))):
+            g = grads.get(out)
+            if g is None:
+                continue
+            ins = [self._val(r) for r in refs]
+            gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
+            for r, gi in zip(refs, gins):
+                if gi is None or not isinstance(r, str):
+                    continue
+                prev = grads.get(r)
+                grads[r] = gi if prev is None else prev + gi
+        self._last_grads = {k: grads.get(k) for k in wrt}
+        return self._last_grads
 
     def output(self, placeholders, *outputs):
-        """Replay the recorded graph for new placeholder values; returns {name: value}."""
+        """Execute the recorded graph for new placeholder values; returns {name: value}."""
         names = [o.name if isinstance(o, SDVariable) else o for o in outputs]
         with torch.no_grad():
-            self._replay({k: _tensor(v) for k, v in placeholders.items()}, names)
+            self._exec({k: _tensor(v) for k, v in placeholders.items()}, names)
         return {n: self.variables[n].value for n in names}
 
     def outputSingle(self, placeholders, output):
         return next(iter(self.output(placeholders, output).values()))
+
+    def execAndEndResult(self, out):
+        return out.value.detach()
+
+    def execBackwards(self, loss, wrt=None, placeholders=None):
+        """Gradients of ``loss`` (seeded with ones) w.r.t. ``wrt`` (default: trainable variables)."""
+        if placeholders:
+            self._exec({k: _tensor(v) for k, v in placeholders.items()}, [loss.name])
+        wrt = [w.name if isinstance(w, SDVariable) else w for w in (wrt or self.trainableVariables())]
+        return self._backward({loss.name: torch.ones_like(loss.value)}, wrt, [loss.name])
+
+    def calculateGradients(self, placeholders, *variables):
+        if not self._loss_names:
+            raise ValueError("no loss variables")
+        if placeholders:
+            self._exec({k: _tensor(v) for k, v in placeholders.items()}, self._loss_names)
+        wrt = [w.name if isinstance(w, SDVariable) else w for w in variables] or list(self._trainable)
+        seeds = {n: torch.ones_like(self.variables[n].value) for n in self._loss_names}
+        return self._backward(seeds, wrt, list(self._loss_names))
 
     # ------------------------------------------------------------------ training
     def setTrainingConfig(self, cfg):
@@ -361,15 +447,16 @@ class SameDiff:
         vs = self.trainableVariables()
         dev = vs[0].value.device
         n = sum(v.value.numel() for v in vs)
-        flat = torch.empty(n, dtype=torch.float32, device=dev)
+        mdt = torch.float64 if all(v.value.dtype == torch.float64 for v in vs) else torch.float32
+        flat = torch.empty(n, dtype=mdt, device=dev)
         # bf16 variables train in mixed precision: fp32 master weights, the fused updater writes the bf16 copy the
         # graph computes with (its "shadow") in the same pass
         mixed = all(v.value.dtype == torch.bfloat16 for v in vs)
         shadow = torch.empty(n, dtype=torch.bfloat16, device=dev) if mixed else None
         segs, off = [], 0
-        for i, v in enumerate(vs):
+        for v in vs:
             k = v.value.numel()
-            flat[off:off + k].copy_(v.value.detach().reshape(-1).float())
+            flat[off:off + k].copy_(v.value.detach().reshape(-1).to(mdt))
             if mixed:
                 shadow[off:off + k].copy_(v.value.detach().reshape(-1))
                 v.value = shadow[off:off + k].view(v.value.shape)
@@ -377,7 +464,7 @@ class SameDiff:
                 v.value = flat[off:off + k].view(v.value.shape)
             segs.append(Segment(off, k, 0, off, n, cfg.updater, cfg.l1, cfg.l2, 0))   # one block: state offset 0
             off += k
-        state = torch.zeros(max(1, cfg.updater.stateSize(n)), dtype=torch.float32, device=dev)
+        state = torch.zeros(max(1, cfg.updater.stateSize(n)), dtype=mdt, device=dev)
         plan = UpdatePlan(segs, [(0, n, 0, cfg.updater)])
         self._train_state = {"flat": flat, "grad": torch.zeros_like(flat), "state": state, "plan": plan,
                              "shadow": shadow}
@@ -396,6 +483,7 @@ class SameDiff:
         st = self._train_state
         vs = self.trainableVariables()
         last = None
+        sign = 1.0 if cfg.minimize else -1.0
         for _ in range(int(numEpochs)):
             items = [data] if isinstance(data, DataSet) or hasattr(data, "features") else data
             if hasattr(items, "reset"):
@@ -406,31 +494,68 @@ class SameDiff:
                 feeds = {n: _tensor(t).to(st["flat"].device) for n, t in zip(cfg.dataSetFeatureMapping, feats)}
                 feeds.update({n: _tensor(t).to(st["flat"].device) for n, t in
                               zip(cfg.dataSetLabelMapping, labs)})
-                for v in vs:
-                    v.value.requires_grad_(True)
-                with torch.enable_grad():
-                    self._replay(feeds, self._loss_names)
-                    loss = sum(self.variables[n].value.float() for n in self._loss_names)
-                    if not cfg.minimize:
-                        loss = -loss
-                    grads = torch.autograd.grad(loss, [v.value for v in vs], allow_unused=True)
                 with torch.no_grad():
+                    self._exec(feeds, self._loss_names)
+                    seeds = {n: torch.full_like(self.variables[n].value, sign) for n in self._loss_names}
+                    grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
                     off = 0
-                    for v, g in zip(vs, grads):
+                    for v in vs:
                         k = v.value.numel()
+                        g = grads.get(v.name)
                         if g is None:
                             st["grad"][off:off + k].zero_()
                         else:
                             st["grad"][off:off + k].copy_(g.reshape(-1))
                         off += k
-                    for v in vs:
-                        v.value.requires_grad_(False)
                     fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount,
                                  self.epochCount, 1, mini_batch=False, shadow=st["shadow"])
+                    loss = sum(float(self.variables[n].value.float()) for n in self._loss_names)
                 self.iterationCount += 1
-                last = float(loss.detach())
+                last = loss
             self.epochCount += 1
         return last
+
+    # ------------------------------------------------------------------ save / load
+    def save(self, path, saveUpdaterState=False):
+        """Graph JSON (variables with kinds / shapes / dtypes, op records, loss variables) + variable arrays
+        (torch.save of a tensor dict, read back with weights_only=True)."""
+        graph = {
+            "format": "dl4j_amd.samediff/1",
+            "variables": [{"name": n, "kind": self._kind[n], "shape": list(v.value.shape),
+                           "dtype": str(v.value.dtype).replace("torch.", "")} for n, v in self.variables.items()],
+            "ops": [{"output": o, "op": op, "inputs": refs, "attrs": attrs} for o, op, refs, attrs in self._ops],
+            "losses": list(self._loss_names), "placeholders": list(self._placeholders),
+            "trainable": list(self._trainable), "iterationCount": self.iterationCount, "epochCount": self.epochCount,
+        }
+        arrays = {n: v.value.detach().cpu().clone() for n, v in self.variables.items() if self._kind[n] != "ARRAY"}
+        buf = io.BytesIO()
+        torch.save(arrays, buf)
+        with zipfile.ZipFile(path, "w") as z:
+            z.writestr("graph.json", json.dumps(graph, indent=1))
+            z.writestr("arrays.pt", buf.getvalue())
+
+    @staticmethod
+    def load(path, device=None):
+        with zipfile.ZipFile(path) as z:
+            graph = json.loads(z.read("graph.json"))
+            arrays = torch.load(io.BytesIO(z.read("arrays.pt")), weights_only=True)
+        sd = SameDiff()
+        for vd in graph["variables"]:
+            n = vd["name"]
+            if vd["kind"] == "ARRAY":
+                continue
+            t = arrays[n].to(device) if device is not None else arrays[n]
+            sd._new(n, t, vd["kind"])
+        sd._placeholders = list(graph["placeholders"])
+        sd._trainable = list(graph["trainable"])
+        sd._loss_names = list(graph["losses"])
+        sd.iterationCount, sd.epochCount = graph.get("iterationCount", 0), graph.get("epochCount", 0)
+        for rec in graph["ops"]:
+            y, ctx = REGISTRY[rec["op"]].fwd([sd._val(r) for r in rec["inputs"]], rec["attrs"])
+            sd._new(rec["output"], y, "ARRAY")
+            sd._ctx[rec["output"]] = ctx
+            sd._ops.append((rec["output"], rec["op"], rec["inputs"], rec["attrs"]))
+        return sd
 
     def getVariable(self, name):
         return self.variables[name]
@@ -448,72 +573,63 @@ class SameDiff:
     def mmul(self, name, a, b=None):
         if isinstance(name, SDVariable):
             name, a, b = None, name, a
-        return self._op(name, torch.matmul, a, b)
+        return self._op(name, "mmul", [a, b])
 
-    def _u(self, name, x, fn):
+    def _u(self, name, x, op, attrs=None):
         if isinstance(name, SDVariable):
             name, x = None, name
-        return self._op(name, fn, x)
+        return self._op(name, op, [x], attrs)
 
     def sigmoid(self, name, x=None):
-        return self._u(name, x, torch.sigmoid)
+        return self._u(name, x, "sigmoid")
 
     def tanh(self, name, x=None):
-        return self._u(name, x, torch.tanh)
+        return self._u(name, x, "tanh")
 
     def relu(self, name, x=None, cutoff=0.0):
-        return self._u(name, x, torch.relu)
+        return self._u(name, x, "relu")
 
     def softmax(self, name, x=None):
-        return self._u(name, x, lambda t: torch.softmax(t, dim=-1))
+        return self._u(name, x, "softmax")
 
     def exp(self, name, x=None):
-        return self._u(name, x, torch.exp)
+        return self._u(name, x, "exp")
 
     def log(self, name, x=None):
-        return self._u(name, x, torch.log)
+        return self._u(name, x, "log")
 
     def sqrt(self, name, x=None):
-        return self._u(name, x, torch.sqrt)
+        return self._u(name, x, "sqrt")
 
     def square(self, name, x=None):
-        return self._u(name, x, torch.square)
+        return self._u(name, x, "square")
 
     def abs(self, name, x=None):
-        return self._u(name, x, torch.abs)
+        return self._u(name, x, "abs")
 
     def neg(self, name, x=None):
-        return self._u(name, x, torch.neg)
+        return self._u(name, x, "neg")
 
     def identity(self, name, x=None):
-        return self._u(name, x, lambda t: t)
+        return self._u(name, x, "identity")
 
     def sum(self, name, x, *dims):
-        return self._op(name, lambda t: t.sum(dim=dims) if dims else t.sum(), x)
+        return self._op(name, "sum", [x], {"dims": list(dims)})
 
     def mean(self, name, x, *dims):
-        return self._op(name, lambda t: t.mean(dim=dims) if dims else t.mean(), x)
+        return self._op(name, "mean", [x], {"dims": list(dims)})
 
     def gather(self, name, params, indices, axis=0):
         """Rows of ``params`` selected by integer ``indices`` (embedding lookup when axis == 0)."""
-        if axis == 0:
-            return self._op(name, lambda p, i: torch.nn.functional.embedding(i.long(), p), params, indices)
-        return self._op(name, lambda p, i: torch.index_select(p, axis, i.long().reshape(-1)), params, indices)
+        return self._op(name, "gather", [params, indices], {"axis": int(axis)})
 
     def concat(self, name, dim, *xs):
-        return self._op(name, lambda *ts: torch.cat(ts, dim=dim), *xs)
+        return self._op(name, "concat", list(xs), {"dim": int(dim)})
 
     def activation(self, name, act, x):
         from ..nn.conf.activations import to_activation
         a = to_activation(act)
-        return self._op(name, lambda t: a.getActivation(t, True), x)
-
-    def execAndEndResult(self, out):
-        return out.value.detach()
-
-    def execBackwards(self, loss, wrt):
-        grads = torch.autograd.grad(loss.value, [w.value for w in wrt], allow_unused=True)
-        return {w.name: g for w, g in zip(wrt, grads)}
+        return self._op(name, "activation", [x], {"act": a.to_dict()})
 
 
 def _tensor(v):

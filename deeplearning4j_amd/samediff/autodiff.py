@@ -1,0 +1,559 @@
+"""SameDiff op registry with explicit reverse-mode derivatives (the reference's DifferentialFunction.doDiff contract,
+NN:nn/layers/samediff/SameDiffLayer.java:58-87,195-215 execAndEndResult / execBackwards).
+
+Every op is a pair of plain functions on device tensors — ``forward(inputs, attrs) -> (output, ctx)`` and
+``backward(ctx, grad_out, inputs, attrs) -> [grad per input or None]`` — registered under a stable name, so a graph
+is data (op name + input variable names + JSON attributes): it can be re-executed for new placeholder values,
+differentiated without torch.autograd, and saved / loaded. The heavy ops dispatch to the framework's kernels in both
+directions: ``mmul``/``linear`` -> in-tree MFMA GEMM (ops/gemm.py), ``conv2d`` -> implicit-GEMM conv kernels
+(ops/conv.py), pooling, ``layerNorm`` / ``fusedSelfAttention`` -> LayerNorm / flash-attention HIP kernels,
+``lstmLayer`` -> whole-sequence LSTM HIP kernels, ``softmaxCrossEntropy`` -> fused softmax-xent kernel. On CPU
+tensors (and fp64 gradient checks) the same ops run their torch reference math.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+REGISTRY = {}
+
+
+class OpDef:
+    def __init__(self, name, fwd, bwd):
+        self.name, self.fwd, self.bwd = name, fwd, bwd
+
+
+def register(name):
+    def deco(pair):
+        fwd, bwd = pair
+        REGISTRY[name] = OpDef(name, fwd, bwd)
+        return pair
+    return deco
+
+
+def _unbroadcast(g, shape):
+    """Sum a broadcast gradient back to ``shape``."""
+    if g is None:
+        return None
+    shape = tuple(shape)
+    if tuple(g.shape) == shape:
+        return g
+    while g.dim() > len(shape):
+        g = g.sum(0)
+    for i, s in enumerate(shape):
+        if s == 1 and g.shape[i] != 1:
+            g = g.sum(i, keepdim=True)
+    return g.reshape(shape)
+
+
+def _shape(x):
+    return tuple(x.shape) if torch.is_tensor(x) else ()
+
+
+def _g(g, x):
+    """Gradient for input ``x`` (None for python scalars / non-float inputs)."""
+    if not torch.is_tensor(x) or not x.is_floating_point():
+        return None
+    return _unbroadcast(g, x.shape).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------------------------- elementwise
+def _binary(name, f, da, db):
+    def fwd(ins, at):
+        a, b = ins
+        return f(a, b), None
+
+    def bwd(ctx, g, ins, at):
+        a, b = ins
+        return [_g(da(g, a, b), a), _g(db(g, a, b), b)]
+    register(name)((fwd, bwd))
+
+
+_binary("add", lambda a, b: a + b, lambda g, a, b: g, lambda g, a, b: g)
+_binary("sub", lambda a, b: a - b, lambda g, a, b: g, lambda g, a, b: -g)
+_binary("mul", lambda a, b: a * b, lambda g, a, b: g * b, lambda g, a, b: g * a)
+_binary("div", lambda a, b: a / b, lambda g, a, b: g / b, lambda g, a, b: -g * a / (b * b))
+_binary("rsub", lambda a, b: b - a, lambda g, a, b: -g, lambda g, a, b: g)
+_binary("rdiv", lambda a, b: b / a, lambda g, a, b: -g * b / (a * a), lambda g, a, b: g / a)
+
+
+def _unary(name, f, df_xy):
+    """df_xy(g, x, y) -> dL/dx."""
+    def fwd(ins, at):
+        y = f(ins[0], at)
+        return y, y
+
+    def bwd(ctx, g, ins, at):
+        return [df_xy(g, ins[0], ctx, at).to(ins[0].dtype)]
+    register(name)((fwd, bwd))
+
+
+_SQRT2 = math.sqrt(2.0)
+_unary("neg", lambda x, a: -x, lambda g, x, y, a: -g)
+_unary("identity", lambda x, a: x, lambda g, x, y, a: g)
+_unary("exp", lambda x, a: torch.exp(x), lambda g, x, y, a: g * y)
+_unary("log", lambda x, a: torch.log(x), lambda g, x, y, a: g / x)
+_unary("sqrt", lambda x, a: torch.sqrt(x), lambda g, x, y, a: g / (2 * y))
+_unary("square", lambda x, a: x * x, lambda g, x, y, a: 2 * g * x)
+_unary("abs", lambda x, a: torch.abs(x), lambda g, x, y, a: g * torch.sign(x))
+_unary("pow", lambda x, a: x ** a["p"], lambda g, x, y, a: g * a["p"] * x ** (a["p"] - 1))
+_unary("relu", lambda x, a: torch.relu(x), lambda g, x, y, a: g * (x > 0).to(g.dtype))
+_unary("sigmoid", lambda x, a: torch.sigmoid(x), lambda g, x, y, a: g * y * (1 - y))
+_unary("tanh", lambda x, a: torch.tanh(x), lambda g, x, y, a: g * (1 - y * y))
+_unary("softplus", lambda x, a: F.softplus(x), lambda g, x, y, a: g * torch.sigmoid(x))
+_unary("elu", lambda x, a: F.elu(x), lambda g, x, y, a: g * torch.where(x > 0, torch.ones_like(x), y + 1))
+_unary("leakyRelu", lambda x, a: F.leaky_relu(x, a.get("alpha", 0.01)),
+       lambda g, x, y, a: g * torch.where(x > 0, torch.ones_like(x), torch.full_like(x, a.get("alpha", 0.01))))
+_unary("gelu", lambda x, a: 0.5 * x * (1 + torch.erf(x / _SQRT2)),
+       lambda g, x, y, a: g * (0.5 * (1 + torch.erf(x / _SQRT2)) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)))
+_unary("softmax", lambda x, a: torch.softmax(x, dim=-1),
+       lambda g, x, y, a: y * (g - (g * y).sum(-1, keepdim=True)))
+
+
+# activation by DL4J IActivation (forward getActivation, backward IActivation.backprop)
+def _act_obj(at):
+    from ..nn.conf.activations import to_activation
+    from ..nn.conf.base import _decode
+    a = at["act"]
+    return to_activation(_decode(a) if isinstance(a, dict) else a)
+
+
+def _act_fwd(ins, at):
+    return _act_obj(at).getActivation(ins[0], True), None
+
+
+def _act_bwd(ctx, g, ins, at):
+    return [_act_obj(at).backprop(ins[0], g).to(ins[0].dtype)]
+
+
+register("activation")((_act_fwd, _act_bwd))
+
+
+# ----------------------------------------------------------------------------------------------- linear algebra
+def _mm(a, b, out_dtype=None):
+    from ..ops.gemm import mmul
+    if a.dim() <= 3 and b.dim() <= 3 and a.dim() >= 2 and b.dim() >= 2:
+        return mmul(a, b, out_dtype=out_dtype)
+    return torch.matmul(a, b)
+
+
+def _mmul_fwd(ins, at):
+    a, b = ins
+    return _mm(a, b), None
+
+
+def _mmul_bwd(ctx, g, ins, at):
+    a, b = ins
+    g = g.to(a.dtype)
+    da = _mm(g, b.transpose(-1, -2))
+    db = _mm(a.transpose(-1, -2), g)
+    return [_unbroadcast(da, a.shape), _unbroadcast(db, b.shape)]
+
+
+register("mmul")((_mmul_fwd, _mmul_bwd))
+
+
+def _linear_fwd(ins, at):
+    x, w, b = ins
+    from ..ops.gemm import mmul
+    return mmul(x, w, bias=None if b is None else b.reshape(-1)), None
+
+
+def _linear_bwd(ctx, g, ins, at):
+    x, w, b = ins
+    g2 = g.to(x.dtype).reshape(-1, g.shape[-1])
+    x2 = x.reshape(-1, x.shape[-1])
+    dx = _mm(g2, w.t()).reshape(x.shape)
+    dw = _mm(x2.t(), g2, out_dtype=torch.float32 if w.dtype != torch.float64 else None).to(w.dtype)
+    db = None if b is None else g2.float().sum(0).reshape(b.shape).to(b.dtype)
+    return [dx, dw, db]
+
+
+register("linear")((_linear_fwd, _linear_bwd))
+
+
+# ----------------------------------------------------------------------------------------------- shape / reduce
+def _dims(at, x):
+    d = at.get("dims") or []
+    return tuple(d) if d else tuple(range(x.dim()))
+
+
+register("sum")((lambda ins, at: (ins[0].sum(dim=_dims(at, ins[0])), None),
+                 lambda ctx, g, ins, at: [_expand_back(g, ins[0], _dims(at, ins[0]))]))
+register("mean")((lambda ins, at: (ins[0].mean(dim=_dims(at, ins[0])), None),
+                  lambda ctx, g, ins, at: [_expand_back(g, ins[0], _dims(at, ins[0])) /
+                                           math.prod(ins[0].shape[d] for d in _dims(at, ins[0]))]))
+
+
+def _expand_back(g, x, dims):
+    shp = list(x.shape)
+    for d in sorted(d % x.dim() for d in dims):
+        shp[d] = 1
+    return g.reshape(shp).expand(x.shape).to(x.dtype)
+
+
+register("reshape")((lambda ins, at: (ins[0].reshape(*at["shape"]), None),
+                     lambda ctx, g, ins, at: [g.reshape(ins[0].shape)]))
+register("permute")((lambda ins, at: (ins[0].permute(*at["dims"]), None),
+                     lambda ctx, g, ins, at: [g.permute(*_inv_perm(at["dims"]))]))
+register("transpose")((lambda ins, at: (ins[0].transpose(-1, -2), None),
+                       lambda ctx, g, ins, at: [g.transpose(-1, -2)]))
+
+
+def _inv_perm(p):
+    inv = [0] * len(p)
+    for i, d in enumerate(p):
+        inv[d] = i
+    return inv
+
+
+def _idx(at):
+    out = []
+    for e in at["idx"]:
+        if isinstance(e, dict) and "slice" in e:
+            out.append(slice(*e["slice"]))
+        elif e is None:
+            out.append(None)
+        else:
+            out.append(e)
+    return tuple(out)
+
+
+def _get_bwd(ctx, g, ins, at):
+    dx = torch.zeros_like(ins[0])
+    dx[_idx(at)] += g.to(dx.dtype)
+    return [dx]
+
+
+register("get")((lambda ins, at: (ins[0][_idx(at)], None), _get_bwd))
+
+
+def _concat_fwd(ins, at):
+    return torch.cat(ins, dim=at["dim"]), None
+
+
+def _concat_bwd(ctx, g, ins, at):
+    sizes = [t.shape[at["dim"]] for t in ins]
+    return list(torch.split(g, sizes, dim=at["dim"]))
+
+
+register("concat")((_concat_fwd, _concat_bwd))
+
+
+def _gather_fwd(ins, at):
+    p, i = ins
+    if at.get("axis", 0) == 0:
+        return p.index_select(0, i.long().reshape(-1)).reshape(tuple(i.shape) + tuple(p.shape[1:])), None
+    return torch.index_select(p, at["axis"], i.long().reshape(-1)), None
+
+
+def _gather_bwd(ctx, g, ins, at):
+    p, i = ins
+    dp = torch.zeros_like(p, dtype=torch.float32 if p.dtype != torch.float64 else p.dtype)
+    ax = at.get("axis", 0)
+    if ax == 0:
+        dp.index_add_(0, i.long().reshape(-1), g.reshape(-1, *p.shape[1:]).to(dp.dtype))
+    else:
+        dp.index_add_(ax, i.long().reshape(-1), g.to(dp.dtype))
+    return [dp.to(p.dtype), None]
+
+
+register("gather")((_gather_fwd, _gather_bwd))
+
+
+# ----------------------------------------------------------------------------------------------- NN blocks
+def _ln_fwd(ins, at):
+    x, gamma, beta = ins
+    eps = at.get("eps", 1e-5)
+    N = x.shape[-1]
+    from ..ops import transformer_native as TN
+    x2 = x.reshape(-1, N).contiguous()
+    if gamma is not None and beta is not None and TN.ln_supported(x2, N) and ops.use_native(x, "layernorm"):
+        y, mean, rstd = TN.ln_fwd(x2, gamma.reshape(-1), beta.reshape(-1), eps)
+        return y.reshape(x.shape), ("native", x2, mean, rstd)
+    xf = x2.float() if x.dtype != torch.float64 else x2
+    mean = xf.mean(-1, keepdim=True)
+    rstd = torch.rsqrt(((xf - mean) ** 2).mean(-1, keepdim=True) + eps)
+    xh = (xf - mean) * rstd
+    y = xh * (gamma.reshape(-1).to(xf.dtype) if gamma is not None else 1) + \
+        (beta.reshape(-1).to(xf.dtype) if beta is not None else 0)
+    return y.to(x.dtype).reshape(x.shape), ("ref", xh, rstd)
+
+
+def _ln_bwd(ctx, g, ins, at):
+    x, gamma, beta = ins
+    N = x.shape[-1]
+    g2 = g.reshape(-1, N).contiguous()
+    if ctx[0] == "native":
+        from ..ops import transformer_native as TN
+        _, x2, mean, rstd = ctx
+        dx, dg, db = TN.ln_bwd(g2.to(x.dtype), x2, gamma.reshape(-1), mean, rstd)
+        return [dx.reshape(x.shape), dg.to(gamma.dtype).reshape(gamma.shape), db.to(beta.dtype).reshape(beta.shape)]
+    _, xh, rstd = ctx
+    gf = g2.to(xh.dtype)
+    gam = gamma.reshape(-1).to(xh.dtype) if gamma is not None else torch.ones(N, dtype=xh.dtype, device=xh.device)
+    dxh = gf * gam
+    dx = rstd * (dxh - dxh.mean(-1, keepdim=True) - xh * (dxh * xh).mean(-1, keepdim=True))
+    dg = None if gamma is None else (gf * xh).sum(0).reshape(gamma.shape).to(gamma.dtype)
+    db = None if beta is None else gf.sum(0).reshape(beta.shape).to(beta.dtype)
+    return [dx.to(x.dtype).reshape(x.shape), dg, db]
+
+
+register("layerNorm")((_ln_fwd, _ln_bwd))
+
+
+def _attn_fwd(ins, at):
+    qkv, mask = ins
+    from ..ops import transformer_native as TN
+    H, causal = at["nHeads"], at.get("causal", False)
+    q = qkv.contiguous()
+    if TN.attn_supported(q, H) and ops.use_native(qkv, "attention"):
+        out, lse = TN.attn_fwd(q, H, mask, causal)
+        return out, ("native", q, out, lse)
+    B, T, E3 = qkv.shape
+    E = E3 // 3
+    D = E // H
+    cd = torch.float64 if qkv.dtype == torch.float64 else torch.float32
+    qq, kk, vv = qkv.to(cd).reshape(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
+    s = (qq @ kk.transpose(-1, -2)) * (D ** -0.5)
+    keep = torch.ones(B, 1, T, T, dtype=torch.bool, device=qkv.device)
+    if mask is not None:
+        keep = keep & (mask.reshape(B, 1, 1, T) != 0)
+    if causal:
+        keep = keep & torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril().reshape(1, 1, T, T)
+    p = torch.softmax(s.masked_fill(~keep, float("-inf")), dim=-1).nan_to_num(0.0)
+    o = (p @ vv).permute(0, 2, 1, 3).reshape(B, T, E)
+    return o.to(qkv.dtype), ("ref", qq, kk, vv, p)
+
+
+def _attn_bwd(ctx, g, ins, at):
+    qkv, mask = ins
+    H, causal = at["nHeads"], at.get("causal", False)
+    if ctx[0] == "native":
+        from ..ops import transformer_native as TN
+        _, q, out, lse = ctx
+        return [TN.attn_bwd(q, out, lse, g.to(q.dtype).contiguous(), H, mask, causal), None]
+    _, qq, kk, vv, p = ctx
+    B, T, E3 = qkv.shape
+    E = E3 // 3
+    D = E // H
+    go = g.to(p.dtype).reshape(B, T, H, D).permute(0, 2, 1, 3)
+    dv = p.transpose(-1, -2) @ go
+    dp = go @ vv.transpose(-1, -2)
+    ds = p * (dp - (dp * p).sum(-1, keepdim=True)) * (D ** -0.5)
+    dq = ds @ kk
+    dk = ds.transpose(-1, -2) @ qq
+    dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B, T, E3)
+    return [dqkv.to(qkv.dtype), None]
+
+
+register("fusedSelfAttention")((_attn_fwd, _attn_bwd))
+
+
+def _conv_fwd(ins, at):
+    x, w, b = ins
+    from ..ops.conv import conv2d_forward
+    st, pd, dl = at.get("stride", [1, 1]), at.get("padding", [0, 0]), at.get("dilation", [1, 1])
+    y = conv2d_forward(x, w, b.reshape(-1) if b is not None else None, st, (pd[0], pd[0], pd[1], pd[1]), dl)
+    return y, None
+
+
+def _conv_bwd(ctx, g, ins, at):
+    x, w, b = ins
+    from ..ops.conv import conv2d_backward
+    st, pd, dl = at.get("stride", [1, 1]), at.get("padding", [0, 0]), at.get("dilation", [1, 1])
+    gW = torch.zeros(w.shape, dtype=torch.float32 if w.dtype != torch.float64 else w.dtype, device=w.device)
+    gb = None if b is None else torch.zeros(b.numel(), dtype=gW.dtype, device=w.device)
+    g = g.to(x.dtype)
+    if x.is_cuda and g.dim() == 4:
+        g = g.contiguous(memory_format=torch.channels_last)
+    dx, dw, db = conv2d_backward(x, w, g, st, (pd[0], pd[0], pd[1], pd[1]), dl, True, True, b is not None,
+                                 gW=gW, gb=gb, grads_zeroed=True)
+    dw = gW if dw is None else dw
+    db = gb if db is None else db
+    return [dx, dw.to(w.dtype).reshape(w.shape), None if b is None else db.to(b.dtype).reshape(b.shape)]
+
+
+register("conv2d")((_conv_fwd, _conv_bwd))
+
+
+def _pool(kind):
+    def fwd(ins, at):
+        from ..ops.pool import pool2d_forward
+        k, s, p = at["kernel"], at["stride"], at.get("padding", [0, 0])
+        y, ctx = pool2d_forward(ins[0], kind, k, s, (p[0], p[0], p[1], p[1]))
+        return y, ctx
+
+    def bwd(ctx, g, ins, at):
+        from ..ops.pool import pool2d_backward
+        return [pool2d_backward(g.to(ins[0].dtype), ctx)]
+    return fwd, bwd
+
+
+register("maxPooling2d")(_pool("MAX"))
+register("avgPooling2d")(_pool("AVG"))
+
+
+def _lstm_fwd(ins, at):
+    """x [mb, nIn, T] -> h [mb, H, T]; DL4J gate order [a|f|o|g], tanh/sigmoid."""
+    x, W, RW, b, h0, c0 = ins
+    peephole = at.get("peephole", False)
+    mb, nIn, T = x.shape
+    H = RW.shape[0]
+    dt = W.dtype
+    xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
+    from ..ops.gemm import mmul
+    zx = mmul(xt, W, bias=b.reshape(-1)).reshape(T, mb, 4 * H)
+    from ..ops import rnn_native
+    if x.is_cuda and rnn_native.supported(H, dt) and ops.use_native(x, "lstm"):
+        out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True)
+        return out.permute(1, 2, 0).to(x.dtype), ("native", xt, zx, out, gates, call)
+    cd = torch.float64 if dt == torch.float64 else torch.float32
+    h = torch.zeros(mb, H, dtype=cd, device=x.device) if h0 is None else h0.to(cd)
+    c = torch.zeros(mb, H, dtype=cd, device=x.device) if c0 is None else c0.to(cd)
+    RWc = RW.to(cd)
+    hs, cs, gs = [h], [c], []
+    for t in range(T):
+        z = zx[t].to(cd) + h @ RWc[:, :4 * H]
+        za, zf, zo, zg = z[:, :H], z[:, H:2 * H], z[:, 2 * H:3 * H], z[:, 3 * H:]
+        if peephole:
+            zf = zf + c * RWc[:, 4 * H]
+            zg = zg + c * RWc[:, 4 * H + 2]
+        a, f, gg = torch.tanh(za), torch.sigmoid(zf), torch.sigmoid(zg)
+        c = f * c + gg * a
+        if peephole:
+            zo = zo + c * RWc[:, 4 * H + 1]
+        o = torch.sigmoid(zo)
+        tc = torch.tanh(c)
+        h = o * tc
+        hs.append(h)
+        cs.append(c)
+        gs.append((a, f, o, gg, tc))
+    out = torch.stack(hs[1:], 2)
+    return out.to(x.dtype), ("ref", xt, hs, cs, gs)
+
+
+def _lstm_bwd(ctx, g, ins, at):
+    x, W, RW, b, h0, c0 = ins
+    peephole = at.get("peephole", False)
+    mb, nIn, T = x.shape
+    H = RW.shape[0]
+    from ..ops.gemm import mmul
+    if ctx[0] == "native":
+        from ..ops import rnn_native
+        _, xt, zx, out, gates, call = ctx
+        dout = g.permute(2, 0, 1).contiguous().float()
+        dz, dh0, dc0 = rnn_native.lstm_seq_bwd(dout, gates, call, c0, RW, H, peephole)
+        h0f = h0.float().reshape(1, mb, H) if h0 is not None else torch.zeros(1, mb, H, device=x.device)
+        hprev = torch.cat([h0f, out[:-1].float()], 0).reshape(T * mb, H)
+        dzf = dz.reshape(T * mb, 4 * H)
+        lp = RW.dtype in (torch.bfloat16, torch.float16)
+        # low-precision operands with fp32 accumulation/output keep the recurrent-weight GEMM on the MFMA kernels
+        dRW = mmul(hprev.to(RW.dtype).t(), dzf.to(RW.dtype), out_dtype=torch.float32) if lp else mmul(hprev.t(), dzf)
+        if peephole:
+            c0f = c0.float().reshape(1, mb, H) if c0 is not None else torch.zeros(1, mb, H, device=x.device)
+            cprev = torch.cat([c0f, call[:-1]], 0)
+            dRW = torch.cat([dRW, (dz[:, :, H:2 * H] * cprev).sum((0, 1)).reshape(-1, 1),
+                             (dz[:, :, 2 * H:3 * H] * call).sum((0, 1)).reshape(-1, 1),
+                             (dz[:, :, 3 * H:] * cprev).sum((0, 1)).reshape(-1, 1)], 1)
+    else:
+        _, xt, hs, cs, gs = ctx
+        cd = hs[0].dtype
+        RWc = RW.to(cd)
+        go = g.to(cd)
+        dh = torch.zeros(mb, H, dtype=cd, device=x.device)
+        dc = torch.zeros(mb, H, dtype=cd, device=x.device)
+        dzs = [None] * T
+        dpeep = [torch.zeros(H, dtype=cd, device=x.device) for _ in range(3)]
+        for t in reversed(range(T)):
+            a, f, o, gg, tc = gs[t]
+            c_prev, c_t = cs[t], cs[t + 1]
+            dh = dh + go[:, :, t]
+            do = dh * tc
+            dzo = do * o * (1 - o)
+            dc = dc + dh * o * (1 - tc * tc)
+            if peephole:
+                dc = dc + dzo * RWc[:, 4 * H + 1]
+                dpeep[1] += (dzo * c_t).sum(0)
+            dza = dc * gg * (1 - a * a)
+            dzg = dc * a * gg * (1 - gg)
+            dzf = dc * c_prev * f * (1 - f)
+            dz = torch.cat([dza, dzf, dzo, dzg], 1)
+            dzs[t] = dz
+            dc = dc * f
+            if peephole:
+                dc = dc + dzf * RWc[:, 4 * H] + dzg * RWc[:, 4 * H + 2]
+                dpeep[0] += (dzf * c_prev).sum(0)
+                dpeep[2] += (dzg * c_prev).sum(0)
+            dh = dz @ RWc[:, :4 * H].t()
+        dz = torch.stack(dzs, 0)
+        dzf = dz.reshape(T * mb, 4 * H)
+        hprev = torch.stack(hs[:-1], 0).reshape(T * mb, H)
+        dRW = hprev.t() @ dzf
+        if peephole:
+            dRW = torch.cat([dRW] + [p.reshape(-1, 1) for p in dpeep], 1)
+        dh0, dc0 = dh, dc
+    dzc = dzf.to(W.dtype)
+    dW = mmul(xt.t(), dzc, out_dtype=torch.float32 if W.dtype != torch.float64 else None)
+    db = dzf.sum(0)
+    dx = mmul(dzc, W.t()).reshape(T, mb, nIn).permute(1, 2, 0)
+    return [dx.to(x.dtype), dW.to(W.dtype), dRW.to(RW.dtype).reshape(RW.shape), db.to(b.dtype).reshape(b.shape),
+            None if h0 is None else dh0.to(h0.dtype), None if c0 is None else dc0.to(c0.dtype)]
+
+
+register("lstmLayer")((_lstm_fwd, _lstm_bwd))
+
+
+# ----------------------------------------------------------------------------------------------- losses (scalar)
+def _sce_fwd(ins, at):
+    y, z = ins
+    ls = at.get("labelSmoothing", 0.0)
+    yy = y * (1 - ls) + ls / y.shape[-1] if ls else y
+    z2 = z.reshape(-1, z.shape[-1])
+    from ..ops.loss import softmax_xent
+    s, grad, _ = softmax_xent(z2.contiguous(), yy.reshape(-1, z.shape[-1]), None, 0.0)
+    n = z2.shape[0]
+    return s.sum() / n, (grad, n)
+
+
+def _sce_bwd(ctx, g, ins, at):
+    grad, n = ctx
+    return [None, (grad.float() * (g.float() / n)).to(ins[1].dtype).reshape(ins[1].shape)]
+
+
+register("softmaxCrossEntropy")((_sce_fwd, _sce_bwd))
+
+
+def _mse_fwd(ins, at):
+    y, z = ins
+    d = z.float() - y.float() if z.dtype != torch.float64 else z - y
+    return (d * d).mean(), d
+
+
+def _mse_bwd(ctx, g, ins, at):
+    d = ctx
+    return [None, (2.0 * d * g / d.numel()).to(ins[1].dtype)]
+
+
+register("meanSquaredError")((_mse_fwd, _mse_bwd))
+
+
+def _log_fwd(ins, at):
+    y, p = ins
+    eps = at.get("epsilon", 1e-7)
+    pc = p.float().clamp(eps, 1 - eps) if p.dtype != torch.float64 else p.clamp(eps, 1 - eps)
+    yy = y.to(pc.dtype)
+    return -(yy * torch.log(pc) + (1 - yy) * torch.log(1 - pc)).mean(), (pc, yy)
+
+
+def _log_bwd(ctx, g, ins, at):
+    pc, yy = ctx
+    eps = at.get("epsilon", 1e-7)
+    inside = ((ins[1] > eps) & (ins[1] < 1 - eps)).to(pc.dtype)
+    d = (-(yy / pc) + (1 - yy) / (1 - pc)) * inside / pc.numel()
+    return [None, (d * g).to(ins[1].dtype)]
+
+
+register("logLoss")((_log_fwd, _log_bwd))

@@ -1,8 +1,8 @@
 """SameDiff layer runtime (reference nn/layers/samediff/SameDiffLayer.java, conf/layers/samediff/SDLayerParams.java).
 
-Forward runs the user's ``defineLayer(sd, input, paramTable)`` on the layer's parameter views; backward
-re-uses the recorded autograd graph of the last training forward (or re-runs the forward under
-``enable_grad``) and writes the parameter gradients straight into the flat gradient views.
+Forward records the user's ``defineLayer(sd, input, paramTable)`` into a SameDiff graph over the layer's parameter
+views; backward runs that graph's reverse pass (each op's explicit derivative, samediff/autodiff.py) seeded with the
+layer's epsilon, and writes the parameter gradients straight into the flat gradient views.
 """
 import torch
 
@@ -33,42 +33,38 @@ class SDLayerParams:
 
 
 class SameDiffLayerImpl(LayerImpl):
-    def _run(self, x, grad):
+    def _run(self, x):
         sd = SameDiff()
-        keys = list(self.params.keys())
-        leaves = {}
-        for k in keys:
-            p = self.params[k].detach().to(x.dtype if x.is_floating_point() else self.params[k].dtype)
-            leaves[k] = p.requires_grad_(grad)
-        xin = x.detach().requires_grad_(grad)
-        with torch.set_grad_enabled(grad):
-            inp = sd.var("input", xin)
-            table = {k: sd.var(k, v) for k, v in leaves.items()}
-            out = self.conf.defineLayer(sd, inp, table)
-            if isinstance(out, (list, tuple)):
-                out = out[0]
-        return out.value, xin, leaves
+        inp = sd.placeHolder("input", x.detach())
+        table = {}
+        for k in self.params.keys():
+            p = self.params[k].detach()
+            table[k] = sd.var(k, p.to(x.dtype) if x.is_floating_point() else p)
+        out = self.conf.defineLayer(sd, inp, table)
+        if isinstance(out, (list, tuple)):
+            out = out[0]
+        return sd, out
 
     def activate(self, x, training=False, mask=None, **kw):
         self.input = x
-        if training:
-            self._out, self._xin, self._leaves = self._run(x, True)
-            return self._out.detach()
-        with torch.no_grad():
-            out, _, _ = self._run(x, False)
-        return out
+        sd, out = self._run(x)
+        self._sd, self._outv = (sd, out) if training else (None, None)
+        return out.value
 
     def backpropGradient(self, eps, **kw):
-        if getattr(self, "_out", None) is None:
-            self._out, self._xin, self._leaves = self._run(self.input, True)
-        keys = list(self._leaves)
-        grads = torch.autograd.grad(self._out, [self._xin] + [self._leaves[k] for k in keys], eps.to(self._out.dtype),
-                                    allow_unused=True)
-        dx = grads[0]
-        for k, g in zip(keys, grads[1:]):
+        if getattr(self, "_sd", None) is None:
+            self._sd, self._outv = self._run(self.input)
+        sd, out = self._sd, self._outv
+        keys = list(self.params.keys())
+        grads = sd._backward({out.name: eps.to(out.value.dtype)}, ["input"] + keys, [out.name])
+        dx = grads["input"]
+        for k in keys:
+            g = grads[k]
             if g is None:
                 self.grads[k].zero_()
             else:
                 self.grads[k].copy_(g.reshape(self.grads[k].shape))
-        self._out = None
+        self._sd = self._outv = None
+        if dx is None:
+            dx = torch.zeros_like(self.input)
         return self.make_gradient(), dx

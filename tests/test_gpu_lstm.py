@@ -81,7 +81,8 @@ def test_lstm_native_in_network_fit(cuda):
 
 @pytest.mark.parametrize("peep", [False, True])
 def test_samediff_lstm_layer_gpu_matches_cpu(cuda, peep):
-    """SameDiff lstmLayer: the GPU path (sequence kernels under autograd) vs the CPU reference, values and grads."""
+    """SameDiff lstmLayer: the GPU path (sequence kernels in both directions of SameDiff's own reverse pass) vs the
+    CPU reference, values and grads."""
     from deeplearning4j_amd.samediff import SameDiff
     g = torch.Generator().manual_seed(5)
     mb, nIn, T, H = 19, 12, 9, 64
@@ -90,9 +91,9 @@ def test_samediff_lstm_layer_gpu_matches_cpu(cuda, peep):
     res = {}
     for dev in ("cpu", cuda):
         sd = SameDiff.create()
-        vs = {k: sd.var(k, v.clone().to(dev).requires_grad_(True)) for k, v in base.items()}
+        vs = {k: sd.var(k, v.clone().to(dev)) for k, v in base.items()}
         h = sd.rnn().lstmLayer("h", vs["x"], vs["W"], vs["RW"], vs["b"], peephole=peep)
-        loss = sd._new("loss", (h.value * torch.linspace(-1, 1, T, device=h.value.device)).sum())
+        loss = (h * sd.constant("ramp", torch.linspace(-1, 1, T, device=h.value.device))).sum()
         grads = sd.execBackwards(loss, list(vs.values()))
         res[str(dev)] = (h.value.detach().cpu(), {k: v.cpu() for k, v in grads.items()})
     (hc, gc), (hg, gg) = res["cpu"], res[str(cuda)]
@@ -154,7 +155,7 @@ def test_lstm_coop_bwd_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb,
 
 
 def test_samediff_char_lm_trains_on_gpu(cuda):
-    """The SameDiff char-LM of tools/bench_samediff_lstm.py: bf16 with fp32 masters, sequence kernels under autograd,
+    """The SameDiff char-LM of tools/bench_samediff_lstm.py: bf16 with fp32 masters, sequence kernels in both passes,
     loss decreases when fitting one window repeatedly."""
     import sys as _sys
     import os as _os

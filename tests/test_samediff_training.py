@@ -1,5 +1,5 @@
 """SameDiff graphs recorded at definition time: replay for new placeholder values (``output``) and training with a
-TrainingConfig (``fit``: autograd over the replayed ops + the fused updater), incl. the LSTM layer op."""
+TrainingConfig (``fit``: the reverse pass over the recorded ops + the fused updater), incl. the LSTM layer op."""
 import torch
 
 from deeplearning4j_amd import Adam, DataSet
