@@ -13,7 +13,11 @@ from .weights import Distribution, NormalDistribution
 
 
 class IDropout(Config):
-    """applyDropout(x, iteration, epoch, training) -> x'; backprop(grad) uses the saved mask."""
+    """applyDropout(x, iteration, epoch, training) -> x'; backprop(grad) uses the saved mask.
+
+    On the GPU the whole family runs on one counter-based Philox kernel (csrc/nn_misc.hip): no mask is stored, the
+    backward regenerates it from the layer's (seed, device counter), and the counter advance is a device op, so
+    captured HIP-graph steps draw a fresh mask every replay. CPU tensors use torch's generator and a saved mask."""
 
     def applyDropout(self, x, iteration=0, epoch=0, training=True):
         raise NotImplementedError
@@ -23,6 +27,30 @@ class IDropout(Config):
 
     def clear(self):
         self._mask = None
+        self._native = None
+
+    def _gpu(self, x, mode, **kw):
+        """Native forward when x is a bf16/fp32 CUDA tensor; returns None otherwise."""
+        from ...ops.dispatch import use_native
+        if not use_native(x, "dropout") or x.dtype not in (torch.bfloat16, torch.float32):
+            self._native = None
+            return None
+        from ...ops import nn_misc
+        rng = getattr(self, "_rng", None)
+        if rng is None or rng.offset.device != x.device:
+            rng = self._rng = nn_misc.PhiloxStream(x.device)
+        rng.advance()
+        y = nn_misc.dropout_native(x, mode, rng, False, **kw)
+        self._native = (y, mode, kw)
+        return y
+
+    def _gpu_backprop(self, grad):
+        nat = getattr(self, "_native", None)
+        if nat is None or not grad.is_cuda:
+            return None
+        from ...ops import nn_misc
+        like, mode, kw = nat
+        return nn_misc.dropout_grad_native(grad, like, mode, self._rng, **kw).to(grad.dtype)
 
 
 def _pval(p, iteration, epoch):
@@ -41,12 +69,18 @@ class Dropout(IDropout):
             return x
         p = _pval(self.p, iteration, epoch)
         if p >= 1.0:
-            self._mask = None
+            self._mask = self._native = None
             return x
+        y = self._gpu(x, "dropout", p=p)
+        if y is not None:
+            return y
         self._mask = (torch.rand_like(x, dtype=torch.float32) < p).to(x.dtype) / p
         return x * self._mask
 
     def backprop(self, grad):
+        g = self._gpu_backprop(grad)
+        if g is not None:
+            return g
         m = getattr(self, "_mask", None)
         return grad if m is None else grad * m
 
@@ -67,12 +101,16 @@ class AlphaDropout(IDropout):
         alpha_p = -self.LAMBDA * self.ALPHA
         a = 1.0 / math.sqrt(p + alpha_p * alpha_p * p * (1 - p))
         b = -a * alpha_p * (1 - p)
+        y = self._gpu(x, "alpha", p=p, a=a, b=b, alpha_p=alpha_p)
+        if y is not None:
+            return y
         keep = (torch.rand_like(x, dtype=torch.float32) < p).to(x.dtype)
         self._mask = keep * a
         return a * (x * keep + alpha_p * (1 - keep)) + b
 
     def backprop(self, grad):
-        return grad * self._mask
+        g = self._gpu_backprop(grad)
+        return g if g is not None else grad * self._mask
 
 
 class GaussianDropout(IDropout):
@@ -87,11 +125,15 @@ class GaussianDropout(IDropout):
             return x
         r = _pval(self.rate, iteration, epoch)
         std = math.sqrt(r / (1 - r))
+        y = self._gpu(x, "gaussian_dropout", sd=std)
+        if y is not None:
+            return y
         self._mask = (torch.randn_like(x, dtype=torch.float32) * std + 1.0).to(x.dtype)
         return x * self._mask
 
     def backprop(self, grad):
-        return grad * self._mask
+        g = self._gpu_backprop(grad)
+        return g if g is not None else grad * self._mask
 
 
 class GaussianNoise(IDropout):
@@ -105,7 +147,8 @@ class GaussianNoise(IDropout):
         if not training:
             return x
         s = _pval(self.stddev, iteration, epoch)
-        return x + torch.randn_like(x) * s
+        y = self._gpu(x, "gaussian_noise", sd=s)
+        return y if y is not None else x + torch.randn_like(x) * s
 
     def backprop(self, grad):
         return grad

@@ -138,82 +138,101 @@ class Convolution1DLayerImpl(ConvolutionLayerImpl):
 
 
 class Deconvolution2DImpl(ConvolutionLayerImpl):
+    """Transposed convolution (reference Deconvolution2DLayer.java:112-225): forward is the conv bwd-data kernel on
+    the zero-interleaved input, backward is a forward conv (dx) plus a weight-gradient conv (dW) — all on the
+    implicit-GEMM HIP kernels for bf16 on the GPU; explicit backward everywhere (ops/nn_misc.py)."""
+
+    def _pad(self):
+        c = self.conf
+        return [0, 0] if c.convolutionMode == ConvolutionMode.Same else list(c.padding)
+
     def preOutput(self, x, training=False):
+        from ...ops.nn_misc import deconv_forward
         c = self.conf
         W = self.W("W")
         b = self.W("b").reshape(-1) if "b" in self.params else None
-        pad = [0, 0] if c.convolutionMode == ConvolutionMode.Same else c.padding
         self._xt = x
-        out = F.conv_transpose2d(x.to(W.dtype), W, b, tuple(c.stride), tuple(pad), 0, 1, tuple(c.dilation))
+        out = deconv_forward(_cl(x.to(W.dtype)), W, b, list(c.stride), self._pad(), list(c.dilation))
+        self._full_hw = out.shape[2:]
         if c.convolutionMode == ConvolutionMode.Same:
             out = out[:, :, :x.shape[2] * c.stride[0], :x.shape[3] * c.stride[1]]
         return out
 
     def backpropGradient(self, eps):
+        from ...ops.nn_misc import deconv_backward
+        c = self.conf
         delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
-        x = self.input.detach().to(delta.dtype).requires_grad_(True)
-        W = self.W("W").detach().requires_grad_(True)
-        b = self.W("b").detach().requires_grad_(True) if "b" in self.params else None
-        with torch.enable_grad():
-            c = self.conf
-            pad = [0, 0] if c.convolutionMode == ConvolutionMode.Same else c.padding
-            out = F.conv_transpose2d(x, W.to(delta.dtype), b.to(delta.dtype) if b is not None else None,
-                                     tuple(c.stride), tuple(pad), 0, 1, tuple(c.dilation))
-            if c.convolutionMode == ConvolutionMode.Same:
-                out = out[:, :, :x.shape[2] * c.stride[0], :x.shape[3] * c.stride[1]]
-            grads = torch.autograd.grad(out, [x, W] + ([b] if b is not None else []), delta)
-        copy_grad_(self.grads["W"], _acc(grads[1]))
-        if b is not None:
-            copy_grad_(self.grads["b"], _acc(grads[2]))
-        return self.make_gradient(), self.backpropDropOut(grads[0])
+        W = self.W("W")
+        if tuple(delta.shape[2:]) != tuple(self._full_hw):
+            full = torch.zeros(delta.shape[:2] + tuple(self._full_hw), dtype=delta.dtype, device=delta.device)
+            full[:, :, :delta.shape[2], :delta.shape[3]] = delta
+            delta = full
+        gW = self.grads["W"] if self.grads["W"].dtype == torch.float32 and self.grads["W"].is_contiguous() else None
+        dx, dW, db = deconv_backward(self._xt.to(W.dtype), W, delta.to(W.dtype), list(c.stride), self._pad(),
+                                     list(c.dilation), "b" in self.grads, gW=gW,
+                                     gb=self.grads["b"].reshape(-1) if "b" in self.grads else None)
+        if dW is not None and dW is not gW:
+            copy_grad_(self.grads["W"], _acc(dW))
+        if "b" in self.grads and db is not None:
+            copy_grad_(self.grads["b"], _acc(db))
+        return self.make_gradient(), self.backpropDropOut(dx)
 
 
-class _AutogradConvBase(ConvolutionLayerImpl):
-    """Shared autograd-backed backward for the less common conv variants."""
-
-    def _forward_fn(self, x, P):
-        raise NotImplementedError
+class DepthwiseConvolution2DImpl(ConvolutionLayerImpl):
+    """Depthwise conv, weights [depthMultiplier, C, kh, kw]; direct HIP stencil kernels (fwd, bwd-data,
+    bwd-weight) on the GPU, grouped library conv on CPU; explicit backward."""
 
     def preOutput(self, x, training=False):
-        P = {k: self.W(k) for k in self.params}
-        return self._forward_fn(x.to(next(iter(P.values())).dtype), P)
+        from ...ops.nn_misc import depthwise_forward
+        c = self.conf
+        W = self.W("W")
+        pad4 = compute_pad4(c, x.shape[2], x.shape[3])
+        self._xt = _cl(x.to(W.dtype))
+        self._geom_cache = (list(c.stride), pad4, list(c.dilation))
+        b = self.params["b"].reshape(-1) if "b" in self.params else None
+        return depthwise_forward(self._xt, W, b, *self._geom_cache)
 
     def backpropGradient(self, eps):
+        from ...ops.nn_misc import depthwise_backward
         delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
-        x = self.input.detach().to(delta.dtype).requires_grad_(True)
-        keys = list(self.params)
-        P = {k: self.W(k).detach().to(delta.dtype).requires_grad_(True) for k in keys}
-        with torch.enable_grad():
-            out = self._forward_fn(x, P)
-            grads = torch.autograd.grad(out, [x] + [P[k] for k in keys], delta)
-        for k, g in zip(keys, grads[1:]):
-            copy_grad_(self.grads[k], _acc(g))
-        return self.make_gradient(), self.backpropDropOut(grads[0])
+        W = self.W("W")
+        dx, dW, db = depthwise_backward(self._xt, W, _cl(delta.to(W.dtype)), *self._geom_cache,
+                                        need_db="b" in self.grads)
+        copy_grad_(self.grads["W"], dW)
+        if "b" in self.grads:
+            copy_grad_(self.grads["b"], db)
+        return self.make_gradient(), self.backpropDropOut(dx)
 
 
-class SeparableConvolution2DImpl(_AutogradConvBase):
-    def _forward_fn(self, x, P):
+class SeparableConvolution2DImpl(DepthwiseConvolution2DImpl):
+    """Depthwise conv (no bias) followed by a pointwise 1x1 conv with the bias (reference
+    SeparableConvolution2DLayer.java:126-236); the pointwise part runs on the conv/GEMM kernels."""
+
+    def preOutput(self, x, training=False):
+        from ...ops.nn_misc import depthwise_forward
         c = self.conf
+        W = self.W("W")
         pad4 = compute_pad4(c, x.shape[2], x.shape[3])
-        dm = c.depthMultiplier
-        C = x.shape[1]
-        wd = P["W"].permute(1, 0, 2, 3).reshape(C * dm, 1, c.kernelSize[0], c.kernelSize[1])
-        xp = F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
-        y = F.conv2d(xp, wd, None, tuple(c.stride), 0, tuple(c.dilation), groups=C)
-        y = F.conv2d(y, P["pW"], P["b"].reshape(-1) if "b" in P else None)
-        return y
+        self._xt = _cl(x.to(W.dtype))
+        self._geom_cache = (list(c.stride), pad4, list(c.dilation))
+        self._y1 = _cl(depthwise_forward(self._xt, W, None, *self._geom_cache))
+        b = self.params["b"].reshape(-1) if "b" in self.params else None
+        return ops.conv2d_forward(self._y1, self.W("pW"), b, (1, 1), (0, 0, 0, 0), (1, 1))
 
-
-class DepthwiseConvolution2DImpl(_AutogradConvBase):
-    def _forward_fn(self, x, P):
-        c = self.conf
-        pad4 = compute_pad4(c, x.shape[2], x.shape[3])
-        dm = c.depthMultiplier
-        C = x.shape[1]
-        wd = P["W"].permute(1, 0, 2, 3).reshape(C * dm, 1, c.kernelSize[0], c.kernelSize[1])
-        xp = F.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1]))
-        return F.conv2d(xp, wd, P["b"].reshape(-1) if "b" in P else None, tuple(c.stride), 0,
-                        tuple(c.dilation), groups=C)
+    def backpropGradient(self, eps):
+        from ...ops.nn_misc import depthwise_backward
+        delta = self.conf.activation.backprop(self._z, eps.to(self._z.dtype))
+        W, pW = self.W("W"), self.W("pW")
+        dy1, dpW, db = ops.conv2d_backward(self._y1, pW, _cl(delta.to(pW.dtype)), (1, 1), (0, 0, 0, 0), (1, 1),
+                                           True, True, "b" in self.grads, gW=self.grads["pW"],
+                                           gb=self.grads.get("b"))
+        if dpW is not None:
+            copy_grad_(self.grads["pW"], _acc(dpW))
+        if "b" in self.grads and db is not None:
+            copy_grad_(self.grads["b"], _acc(db))
+        dx, dW, _ = depthwise_backward(self._xt, W, _cl(dy1.to(W.dtype)), *self._geom_cache, need_db=False)
+        copy_grad_(self.grads["W"], dW)
+        return self.make_gradient(), self.backpropDropOut(dx)
 
 
 class SubsamplingLayerImpl(LayerImpl):

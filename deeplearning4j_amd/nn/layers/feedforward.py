@@ -81,26 +81,29 @@ class DropoutLayerImpl(LayerImpl):
 
 
 class EmbeddingLayerImpl(LayerImpl):
-    """Row gather forward (reference EmbeddingLayer.java:111 pullRows), scatter-add backward (:71)."""
+    """Row gather forward (reference EmbeddingLayer.java:111 pullRows), scatter-add backward (:71); HIP gather /
+    atomic scatter-add kernels on the GPU (csrc/nn_misc.hip)."""
 
     def activate(self, x, training=False, mask=None):
+        from ...ops.nn_misc import embedding_forward
         self.training = training
         idx = x.reshape(-1).long()
         self._idx = idx
         W = self.W("W")
-        z = W.index_select(0, idx)
+        z = embedding_forward(W, idx)
         if "b" in self.params:
             z = add_row(z, self.W("b"))
         self._z = z
         return self.conf.activation.getActivation(z, training)
 
     def backpropGradient(self, eps):
-        delta = _acc(self.conf.activation.backprop(self._z, eps))
+        from ...ops.nn_misc import embedding_backward_
+        delta = self.conf.activation.backprop(self._z, eps)
         gW = self.grads["W"]
         gW.zero_()
-        gW.index_add_(0, self._idx, delta.to(gW.dtype))
+        embedding_backward_(gW, self._idx, delta)
         if "b" in self.grads:
-            copy_grad_(self.grads["b"], delta.sum(dim=0))
+            bias_grad_(self.grads["b"], delta)
         return self.make_gradient(), None
 
 

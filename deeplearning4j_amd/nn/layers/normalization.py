@@ -92,30 +92,19 @@ def _is_identity(a):
 
 class LocalResponseNormalizationImpl(LayerImpl):
     """Cross-channel LRN: y = x / (k + alpha * sum_{window n} x^2)^beta (reference
-    LocalResponseNormalization.java:47,187; cudnnLRNCrossChannel semantics without the /n)."""
-
-    def _fwd(self, x):
-        c = self.conf
-        half = int(c.n) // 2
-        sq = (_acc(x) ** 2)
-        pad = torch.nn.functional.pad(sq, (0, 0, 0, 0, half, half))
-        s = torch.zeros_like(sq)
-        for i in range(int(c.n)):
-            s = s + pad[:, i:i + x.shape[1]]
-        unit = c.k + c.alpha * s
-        return (_acc(x) * unit ** (-c.beta)), unit
+    LocalResponseNormalization.java:47,187; cudnnLRNCrossChannel semantics without the /n). HIP kernels
+    (csrc/nn_misc.hip) on the GPU in both directions, torch reference on CPU; explicit backward."""
 
     def activate(self, x, training=False, mask=None):
+        from ...ops.nn_misc import lrn_forward
         self.input = x
-        y, self._unit = self._fwd(x)
+        c = self.conf
+        y, self._ctx = lrn_forward(x, c.n, c.k, c.alpha, c.beta)
         return y.to(x.dtype)
 
     def backpropGradient(self, eps):
-        x = _acc(self.input.detach()).requires_grad_(True)
-        with torch.enable_grad():
-            y, _ = self._fwd(x)
-            (dx,) = torch.autograd.grad(y, [x], _acc(eps))
-        return self.make_gradient(), dx.to(eps.dtype)
+        from ...ops.nn_misc import lrn_backward
+        return self.make_gradient(), lrn_backward(eps, self._ctx).to(eps.dtype)
 
 
 class LayerNormalizationImpl(LayerImpl):

@@ -371,9 +371,51 @@ def _choose(key, run_gemm, run_old):
     return c
 
 
+def _pad_ch(t, n, dim=1, cl=False):
+    """Zero-pad dim ``dim`` (channels of a 4-D activation with ``cl``=channels-last, or a weight's K / C dim)
+    up to ``n``."""
+    if t.shape[dim] == n:
+        return t
+    shp = list(t.shape)
+    shp[dim] = n
+    out = torch.zeros(shp, dtype=t.dtype, device=t.device,
+                      memory_format=torch.channels_last if cl else torch.contiguous_format)
+    out.narrow(dim, 0, t.shape[dim]).copy_(t)
+    return out
+
+
+def _r8(n):
+    return (n + 7) // 8 * 8
+
+
+def _stem_case(x, w, b, stride, pad4, dilation):
+    if x.shape[1] != 3 or os.environ.get("DL4J_AMD_KERNEL_STEM", "1") != "1":
+        return False
+    from . import conv_stem
+    return conv_stem.supported(_cl(x), w, b, stride, pad4, dilation)
+
+
 def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     """want_stats: also emit per-tile BatchNorm statistics of the output from the kernel epilogue; they are attached
-    to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer."""
+    to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer.
+    Input channel counts that are not a multiple of 8 (RGB / small first layers: AlexNet, LeNet, GoogLeNet stems)
+    are zero-padded to the next multiple of 8 so they still run on the MFMA kernels (exact: zero channels add 0)."""
+    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and x.shape[1] == w.shape[1] \
+            and x.shape[1] % 8 and not _stem_case(x, w, b, stride, pad4, dilation):
+        C8 = _r8(x.shape[1])
+        return conv2d_fwd(_pad_ch(_cl(x), C8, cl=True), _pad_ch(w, C8), b, stride, pad4, dilation, want_stats)
+    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and w.shape[0] % 4:
+        K = w.shape[0]
+        K8 = _r8(K)
+        bp = _pad_ch(b.reshape(-1), K8, 0) if b is not None else None
+        y = conv2d_fwd(x, _pad_ch(w, K8, 0), bp, stride, pad4, dilation, want_stats)
+        if y is None:
+            return None
+        out = y[:, :K].contiguous(memory_format=torch.channels_last)
+        if hasattr(y, "_bn_tile_stats"):
+            ts, P = y._bn_tile_stats
+            out._bn_tile_stats = (ts[:, :, :K].contiguous(), P)
+        return out
     use = True
     if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
             _is_pointwise(1, 1, stride, pad4, dilation):
@@ -388,7 +430,13 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     """grads_zeroed: the caller guarantees gW/gb (flat-gradient views) are already zero (the network clears the
     whole flat gradient with one fill per step), so no per-layer memset is launched.
     dx_accum: an existing channels-last bf16 gradient of x (another consumer's contribution); when the bwd-data
-    kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx."""
+    kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx.
+    Channel counts (C or K) that are not a multiple of 8 are zero-padded (see ``conv2d_fwd``); the padded weight
+    gradient is cropped into ``gW``."""
+    if _ok_act(x) and _ok_act(dy) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and \
+            x.shape[1] == w.shape[1] and (x.shape[1] % 8 or w.shape[0] % 8) and \
+            not (x.shape[1] == 3 and not need_dx and _stem_case(x, w, None, stride, pad4, dilation)):
+        return _conv2d_bwd_padded(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, dx_accum)
     gdx = gdw = True
     if _ok_act(x) and _ok_act(dy) and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
             _is_pointwise(1, 1, stride, pad4, dilation):
@@ -411,6 +459,33 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
                                               gemm_dw=False))
     return _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, grads_zeroed, dx_accum,
                        gdx, gdw)
+
+
+def _conv2d_bwd_padded(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, dx_accum):
+    K, C = w.shape[0], w.shape[1]
+    C8, K8 = _r8(C), _r8(K)
+    xp = _pad_ch(_cl(x), C8, cl=True)
+    wp = _pad_ch(_pad_ch(w, C8, 1), K8, 0)
+    dyp = _pad_ch(_cl(dy), K8, cl=True)
+    r = conv2d_bwd(xp, wp, dyp, stride, pad4, dilation, need_dx, need_dw, need_db)
+    if r is None:
+        return None
+    dx, dW, db = r
+    if dx is not None:
+        dx = dx[:, :C].contiguous(memory_format=torch.channels_last)
+        if dx_accum is not None:
+            dx = dx_accum.add_(dx)
+    if dW is not None:
+        dW = dW[:K, :C]
+        if gW is not None:
+            gW.copy_(dW.reshape(gW.shape))
+            dW = None
+    if db is not None:
+        db = db[:K]
+        if gb is not None:
+            gb.copy_(db.reshape(gb.shape))
+            db = None
+    return dx, dW, db
 
 
 def _out_hw_inv(OH, OW, R, S, pad4, H, W):

@@ -1,0 +1,206 @@
+"""GPU parity of the csrc/nn_misc.hip kernels (LRN, Philox dropout family, embedding gather/scatter-add, depthwise
+conv) and of the transposed / separable convs and odd-channel convs on the implicit-GEMM kernels, against plain fp32
+torch; plus a zero-fallback network step through every one of these layers."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deeplearning4j_amd.ops import fallback
+from deeplearning4j_amd.ops import nn_misc as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    a, b = a.double().cpu(), b.double().cpu()
+    err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-6))
+    assert err < tol, err
+
+
+def _lrn_ref(x, n, k, a, b):
+    xf = x.detach().double().cpu().requires_grad_(True)
+    half = n // 2
+    sq = F.pad((xf * xf).unsqueeze(0), (0, 0, 0, 0, half, half)).squeeze(0)
+    s = sum(sq[:, i:i + x.shape[1]] for i in range(n))
+    return xf, xf * (k + a * s) ** (-b)
+
+
+@pytest.mark.parametrize("dtype,cl", [(torch.float32, False), (torch.float32, True), (torch.bfloat16, True)])
+def test_lrn_matches_torch(cuda, dtype, cl):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(4, 24, 9, 7, generator=g)
+    gy = torch.randn(4, 24, 9, 7, generator=g)
+    xd = x.to(cuda, dtype)
+    if cl:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    fallback.reset()
+    y, ctx = M.lrn_forward(xd, 5, 2.0, 1e-3, 0.75)
+    dx = M.lrn_backward(gy.to(cuda, dtype), ctx)
+    assert fallback.count() == 0
+    xf, yr = _lrn_ref(xd.float(), 5, 2.0, 1e-3, 0.75)
+    (dxr,) = torch.autograd.grad(yr, [xf], gy.double())
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    _close(y, yr, tol)
+    _close(dx, dxr, tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_philox_dropout_family(cuda, dtype):
+    from deeplearning4j_amd.nn.conf.regularization import AlphaDropout, Dropout, GaussianDropout, GaussianNoise
+    x = torch.randn(1 << 20, device=cuda).to(dtype) + 2.0
+    fallback.reset()
+    d = Dropout(0.8)
+    y = d.applyDropout(x)
+    keep = y != 0
+    assert abs(keep.float().mean().item() - 0.8) < 5e-3
+    _close(y[keep], (x[keep].float() / 0.8), 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    gr = torch.ones_like(x)
+    gx = d.backprop(gr)
+    assert torch.equal(gx != 0, keep)                          # the regenerated mask is the forward one
+    y2 = d.applyDropout(x)
+    assert not torch.equal(y2 != 0, keep)                      # the counter advanced: a fresh mask
+    a = AlphaDropout(0.9)
+    z = torch.randn(1 << 20, device=cuda).to(dtype)
+    ya = a.applyDropout(z).float()
+    assert abs(ya.mean().item()) < 2e-2 and abs(ya.std().item() - 1.0) < 3e-2   # self-normalising
+    ga = a.backprop(torch.ones_like(z)).float()
+    assert torch.equal(ga == 0, (ya - ya.min()).abs() < 1e-3) or abs((ga == 0).float().mean().item() - 0.1) < 5e-3
+    gd = GaussianDropout(0.2)
+    yg = gd.applyDropout(torch.ones_like(x)).float()
+    assert abs(yg.mean().item() - 1.0) < 5e-3 and abs(yg.std().item() - (0.2 / 0.8) ** 0.5) < 1e-2
+    _close(gd.backprop(torch.ones_like(x)), yg, 1e-2)
+    gn = GaussianNoise(0.3)
+    yn = gn.applyDropout(torch.zeros_like(x)).float()
+    assert abs(yn.std().item() - 0.3) < 1e-2
+    assert torch.equal(gn.backprop(gr), gr)
+    assert fallback.count() == 0
+
+
+@pytest.mark.parametrize("dtype,forder", [(torch.float32, False), (torch.bfloat16, False), (torch.bfloat16, True)])
+def test_embedding_gather_scatter(cuda, dtype, forder):
+    g = torch.Generator().manual_seed(1)
+    V, D = 1000, 96
+    W = torch.randn(V, D, generator=g)
+    Wd = W.to(cuda, dtype)
+    if forder:
+        Wd = Wd.t().contiguous().t()                            # column-major, as DL4J lays out EmbeddingLayer W
+    idx = torch.randint(0, V, (4, 50), generator=g)
+    idx[0, :10] = 7                                             # repeated rows accumulate
+    fallback.reset()
+    out = M.embedding_forward(Wd, idx.to(cuda))
+    _close(out, W.to(dtype).float()[idx], 1e-6)
+    gy = torch.randn(4, 50, D, generator=g)
+    dW = torch.zeros(V, D, device=cuda)
+    M.embedding_backward_(dW, idx.to(cuda), gy.to(cuda, dtype))
+    ref = torch.zeros(V, D).index_add_(0, idx.reshape(-1), gy.to(dtype).float().reshape(-1, D))
+    _close(dW, ref, 1e-5)
+    assert fallback.count() == 0
+
+
+@pytest.mark.parametrize("dm,stride,pad,dil", [(1, 1, 1, 1), (2, 2, 1, 1), (1, 1, 2, 2), (3, 2, 0, 1)])
+def test_depthwise_conv_matches_torch(cuda, dm, stride, pad, dil):
+    g = torch.Generator().manual_seed(dm * 10 + stride)
+    N, C, H, W_, k = 4, 16, 15, 13, 3
+    x = torch.randn(N, C, H, W_, generator=g)
+    w = torch.randn(dm, C, k, k, generator=g) * 0.3
+    b = torch.randn(C * dm, generator=g)
+    pad4 = (pad, pad, pad, pad)
+    fallback.reset()
+    xd = x.to(cuda).contiguous(memory_format=torch.channels_last)
+    y = M.depthwise_forward(xd, w.to(cuda), b.to(cuda), (stride, stride), pad4, (dil, dil))
+    gy = torch.randn(y.shape, generator=g)
+    dx, dW, db = M.depthwise_backward(xd, w.to(cuda), gy.to(cuda), (stride, stride), pad4, (dil, dil), True, True)
+    assert fallback.count() == 0
+    xr = x.clone().requires_grad_(True)
+    wg = w.permute(1, 0, 2, 3).reshape(C * dm, 1, k, k).clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wg, br, stride, pad, dil, groups=C)
+    yr.backward(gy)
+    _close(y, yr, 1e-5)
+    _close(dx, xr.grad, 1e-5)
+    _close(dW, wg.grad.reshape(C, dm, k, k).permute(1, 0, 2, 3), 1e-5)
+    _close(db, br.grad, 1e-5)
+
+
+@pytest.mark.parametrize("stride,pad,k", [(2, 0, 2), (2, 1, 3), (1, 1, 3)])
+def test_deconv_on_conv_kernels_matches_torch(cuda, stride, pad, k):
+    g = torch.Generator().manual_seed(stride * 7 + k)
+    N, Cin, Cout, H = 4, 32, 16, 9
+    x = torch.randn(N, Cin, H, H, generator=g)
+    w = torch.randn(Cin, Cout, k, k, generator=g) * 0.2
+    b = torch.randn(Cout, generator=g)
+    bf = torch.bfloat16
+    fallback.reset()
+    xd = x.to(cuda, bf).contiguous(memory_format=torch.channels_last)
+    y = M.deconv_forward(xd, w.to(cuda, bf), b.to(cuda), (stride, stride), (pad, pad))
+    gy = torch.randn(y.shape, generator=g)
+    dx, dW, db = M.deconv_backward(xd, w.to(cuda, bf), gy.to(cuda, bf), (stride, stride), (pad, pad))
+    torch.cuda.synchronize()
+    assert fallback.count() == 0, fallback.summary()
+    xr = x.to(bf).float().requires_grad_(True)
+    wr = w.to(bf).float().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, b, stride, pad)
+    yr.backward(gy.to(bf).float())
+    _close(y, yr, 2e-2)
+    _close(dx, xr.grad, 2e-2)
+    _close(dW, wr.grad, 2e-2)
+    _close(db, gy.to(bf).float().sum((0, 2, 3)), 2e-2)
+
+
+@pytest.mark.parametrize("C,K", [(3, 64), (3, 20), (20, 50), (12, 12)])
+def test_odd_channel_conv_padded_onto_mfma(cuda, C, K):
+    from deeplearning4j_amd.ops import conv2d_backward, conv2d_forward
+    g = torch.Generator().manual_seed(C * 100 + K)
+    x = torch.randn(8, C, 20, 20, generator=g)
+    w = torch.randn(K, C, 5, 5, generator=g) * 0.1
+    b = torch.randn(K, generator=g)
+    bf = torch.bfloat16
+    fallback.reset()
+    xd = x.to(cuda, bf).contiguous(memory_format=torch.channels_last)
+    y = conv2d_forward(xd, w.to(cuda, bf), b.to(cuda), (1, 1), (2, 2, 2, 2))
+    gy = torch.randn(y.shape, generator=g)
+    dx, dW, db = conv2d_backward(xd, w.to(cuda, bf), gy.to(cuda, bf).contiguous(memory_format=torch.channels_last),
+                                 (1, 1), (2, 2, 2, 2))
+    torch.cuda.synchronize()
+    assert fallback.count() == 0, fallback.summary()
+    xr = x.to(bf).float().requires_grad_(True)
+    wr = w.to(bf).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, b, 1, 2)
+    yr.backward(gy.to(bf).float())
+    _close(y, yr, 2e-2)
+    _close(dx, xr.grad, 2e-2)
+    _close(dW, wr.grad, 2e-2)
+    _close(db, gy.to(bf).float().sum((0, 2, 3)), 2e-2)
+
+
+def test_misc_layers_network_step_has_no_fallback(cuda):
+    """conv(3->16) -> LRN -> depthwise -> separable -> deconv -> dropout -> dense/output, bf16, one fit step on the
+    in-tree kernels only (helperCountFail == 0), and the loss decreases."""
+    from deeplearning4j_amd import (Adam, ConvolutionLayer, DenseLayer, InputType, LocalResponseNormalization,
+                                    MultiLayerNetwork, NeuralNetConfiguration, OutputLayer)
+    from deeplearning4j_amd.nn.conf.layers import (Deconvolution2D, DepthwiseConvolution2D,
+                                                   SeparableConvolution2D)
+    from deeplearning4j_amd.nn.conf import DataType
+    from deeplearning4j_amd.nn.conf.regularization import Dropout
+    conf = (NeuralNetConfiguration.Builder().seed(3).updater(Adam(1e-3)).dataType(DataType.BFLOAT16).list()
+            .layer(ConvolutionLayer.Builder(3, 3).nOut(16).activation("RELU").build())
+            .layer(LocalResponseNormalization.Builder().build())
+            .layer(DepthwiseConvolution2D.Builder(3, 3).depthMultiplier(2).activation("RELU").build())
+            .layer(SeparableConvolution2D.Builder(3, 3).nOut(24).activation("RELU").build())
+            .layer(Deconvolution2D.Builder(2, 2).stride(2, 2).nOut(16).activation("RELU").build())
+            .layer(DenseLayer.Builder().nOut(32).activation("RELU").dropOut(Dropout(0.8)).build())
+            .layer(OutputLayer.Builder("MCXENT").nOut(5).activation("SOFTMAX").build())
+            .setInputType(InputType.convolutional(16, 16, 3)).build())
+    net = MultiLayerNetwork(conf)
+    net.init(device=cuda)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(16, 3, 16, 16, generator=g).to(cuda)
+    y = F.one_hot(torch.randint(0, 5, (16,), generator=g), 5).float().to(cuda)
+    fallback.reset()
+    scores = []
+    for _ in range(8):
+        net.fit(x, y)
+        scores.append(net.score())
+    torch.cuda.synchronize()
+    assert net.helperCountFail() == 0, net.fallbackSummary()
+    assert scores[-1] < scores[0]
