@@ -141,6 +141,11 @@ class BaseNetwork:
         if self.shadow is not None:
             with torch.no_grad():
                 self.shadow.copy_(flat)
+        if self.device.type == "cuda":
+            from ..ops import conv_native
+            conv_native.register_managed(flat)          # every update of these bumps the weight version
+            if self.shadow is not None:
+                conv_native.register_managed(self.shadow)
         self.updater = NetworkUpdater(self, build_entries(self._layer_offsets))
         self.updater.init_state(self.device, self.master_dtype)
         self.initCalled = True

@@ -9,6 +9,7 @@ Coverage (everything else returns ``None`` and ``ops.conv`` uses the library pat
 Weights are re-laid-out once per parameter version (KRSC for forward, flipped CRSK for backward-data).
 """
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -62,6 +63,25 @@ def bump_version():
     WEIGHT_VERSION[0] += 1
 
 
+# Parameter buffers whose every modification bumps WEIGHT_VERSION (a network's flat params / compute shadow).
+# Weights anywhere else (SameDiff variables, ad-hoc op calls, temporaries) are relaid out on every call: their
+# address may be reused by a different tensor and nothing reports their updates.
+_MANAGED = {}
+
+
+def register_managed(buf):
+    _MANAGED[buf.data_ptr()] = (buf.data_ptr() + buf.numel() * buf.element_size(), weakref.ref(buf))
+
+
+def is_managed(ptr):
+    for s, (e, r) in list(_MANAGED.items()):
+        if r() is None:
+            del _MANAGED[s]
+        elif s <= ptr < e:
+            return True
+    return False
+
+
 class _WEnt:
     """Kernel-layout copies of one conv weight: persistent buffers (stable addresses for HIP graphs, no allocator
     churn) plus the weight version each copy was last written for."""
@@ -84,8 +104,9 @@ def _relayout(w, want_krsc, want_flip):
     e = _ent(w)
     v = WEIGHT_VERSION[0]
     K, C, R, S = w.shape
-    need_k = want_krsc and e.vk != v
-    need_f = want_flip and e.vf != v
+    fresh = not is_managed(w.data_ptr())
+    need_k = want_krsc and (fresh or e.vk != v)
+    need_f = want_flip and (fresh or e.vf != v)
     if need_k or need_f:
         if need_k and e.krsc is None:
             e.krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device)
@@ -378,8 +399,8 @@ def _pad_ch(t, n, dim=1, cl=False):
         return t
     shp = list(t.shape)
     shp[dim] = n
-    out = torch.zeros(shp, dtype=t.dtype, device=t.device,
-                      memory_format=torch.channels_last if cl else torch.contiguous_format)
+    out = torch.empty(shp, dtype=t.dtype, device=t.device,
+                      memory_format=torch.channels_last if cl else torch.contiguous_format).zero_()
     out.narrow(dim, 0, t.shape[dim]).copy_(t)
     return out
 

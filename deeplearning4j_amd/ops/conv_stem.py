@@ -25,7 +25,7 @@ def supported(x, w, b, stride, pad4, dilation):
 
 def pack_weights(w):
     """[64, 3, 7, 7] -> fragment-packed bf16 [4, 6, 64, 8] (cached per weight buffer and weight version)."""
-    from .conv_native import WEIGHT_VERSION
+    from .conv_native import WEIGHT_VERSION, is_managed
     key = (w.data_ptr(), str(w.device))
     ent = _packed.get(key)
     if ent is None:
@@ -34,7 +34,7 @@ def pack_weights(w):
         ent = _packed[key] = {"idx": r * 24 + rem, "full": torch.zeros(192, 64, dtype=torch.bfloat16,
                                                                        device=w.device),
                               "pk": torch.empty(4, 6, 64, 8, dtype=torch.bfloat16, device=w.device), "v": -1}
-    if ent["v"] != WEIGHT_VERSION[0]:
+    if ent["v"] != WEIGHT_VERSION[0] or not is_managed(w.data_ptr()):
         src = w.permute(2, 3, 1, 0).reshape(147, 64)               # rows (r, s, c)
         ent["full"].index_copy_(0, ent["idx"], src)
         ent["pk"].copy_(ent["full"].view(6, 4, 8, 4, 16).permute(3, 0, 1, 4, 2).reshape(4, 6, 64, 8))

@@ -271,8 +271,8 @@ def deconv_forward(x, w, b, stride, pad, dilation=(1, 1)):
     if use_native(x, "deconv") and x.dtype == torch.bfloat16 and tuple(dilation) == (1, 1) and Cin % 8 == 0 and \
             Cout % 8 == 0 and pad[0] <= R - 1 and pad[1] <= S - 1:
         if (s0, s1) != (1, 1):
-            xz = torch.zeros((N, Cin, (H - 1) * s0 + 1, (W_ - 1) * s1 + 1), dtype=x.dtype, device=x.device,
-                             memory_format=torch.channels_last)
+            xz = torch.empty((N, Cin, (H - 1) * s0 + 1, (W_ - 1) * s1 + 1), dtype=x.dtype, device=x.device,
+                             memory_format=torch.channels_last).zero_()
             xz[:, :, ::s0, ::s1] = x
         else:
             xz = x.contiguous(memory_format=torch.channels_last)

@@ -282,6 +282,9 @@ class SameDiff:
         self._trainable = []
         self._loss_names = []
         self._last_grads = {}
+        self._plans = {}
+        self._executed = None           # target set of the last planned execution (whose contexts are live)
+        self.fusion = True
         self.trainingConfig = None
         self._train_state = None
         self.iterationCount = 0
@@ -328,6 +331,7 @@ class SameDiff:
         y, ctx = REGISTRY[op].fwd([self._val(r) for r in refs], attrs)
         v = self._new(name, y, "ARRAY")
         self._ctx[v.name] = ctx
+        self._executed = None
         self._ops.append((v.name, op, refs, attrs))
         return v
 
@@ -380,11 +384,53 @@ class SameDiff:
                 need.update(r for r in rec[2] if isinstance(r, str))
         return keep[::-1]
 
+    def _plan(self, targets):
+        """Execution plan for ``targets``: the needed records after the fusion pass, cached per target set.
+
+        Fusions (only where the intermediate has a single consumer and is not itself a target):
+          linear -> gelu          one GEMM with the GELU in its epilogue (pre-activation kept for the backward)
+          add(a, b) -> layerNorm  the residual sum done inside the LayerNorm kernel (same-shape operands)
+        Fused-away intermediates keep their definition-time values."""
+        key = (tuple(targets) if targets is not None else None, self.fusion)
+        hit = self._plans.get(key)
+        if hit is not None and hit[0] == len(self._ops):
+            return hit[1]
+        recs = self._needed(targets)
+        if self.fusion:
+            uses = {}
+            for _, _, refs, _ in recs:
+                for r in refs:
+                    if isinstance(r, str):
+                        uses[r] = uses.get(r, 0) + 1
+            for t in targets or ():
+                uses[t] = uses.get(t, 0) + 1
+            prod = {r[0]: i for i, r in enumerate(recs)}
+            out, drop = list(recs), set()
+            for i, (o, op, refs, attrs) in enumerate(recs):
+                src = refs[0] if refs and isinstance(refs[0], str) else None
+                j = prod.get(src)
+                if j is None or uses.get(src, 0) != 1 or j in drop:
+                    continue
+                po, pop, prefs, pattrs = recs[j]
+                if op == "gelu" and pop == "linear" and "act" not in pattrs:
+                    out[i] = (o, "linear", prefs, {**pattrs, "act": "gelu"})
+                    drop.add(j)
+                elif op == "layerNorm" and pop == "add" and len(refs) == 3 and \
+                        all(isinstance(r, str) for r in prefs):
+                    a, b = (self.variables[r].value for r in prefs)
+                    if a.shape == b.shape and a.dtype == b.dtype:
+                        out[i] = (o, "layerNorm", [prefs[0], refs[1], refs[2], prefs[1]], dict(attrs))
+                        drop.add(j)
+            recs = [r for k, r in enumerate(out) if k not in drop]
+        self._plans[key] = (len(self._ops), recs)
+        return recs
+
     def _exec(self, feeds, targets=None):
         """Re-run the recorded ops (those ``targets`` depend on) with new placeholder values; saves contexts."""
         for k, v in feeds.items():
             self.variables[k].value = v
-        for out, op, refs, attrs in self._needed(targets):
+        self._executed = tuple(targets) if targets is not None else None
+        for out, op, refs, attrs in self._plan(targets):
             y, ctx = REGISTRY[op].fwd([self._val(r) for r in refs], attrs)
             self.variables[out].value = y
             self._ctx[out] = ctx
@@ -393,7 +439,10 @@ class SameDiff:
         """Reverse pass from ``seeds`` {variable name: upstream gradient} over the recorded ops; returns
         {name: gradient} for ``wrt`` (every op's explicit backward; no torch.autograd)."""
         grads = dict(seeds)
-        for out, op, refs, attrs in reversed(self._needed(targets if targets is not None else list(seeds))):
+        tg = targets if targets is not None else list(seeds)
+        # the planned (fused) records only when their contexts come from a planned execution of these targets
+        recs = self._plan(tg) if self._executed == tuple(tg) else self._needed(tg)
+        for out, op, refs, attrs in reversed(recs):
             g = grads.get(out)
             if g is None:
                 continue
@@ -422,16 +471,14 @@ class SameDiff:
 
     def execBackwards(self, loss, wrt=None, placeholders=None):
         """Gradients of ``loss`` (seeded with ones) w.r.t. ``wrt`` (default: trainable variables)."""
-        if placeholders:
-            self._exec({k: _tensor(v) for k, v in placeholders.items()}, [loss.name])
+        self._exec({k: _tensor(v) for k, v in (placeholders or {}).items()}, [loss.name])
         wrt = [w.name if isinstance(w, SDVariable) else w for w in (wrt or self.trainableVariables())]
         return self._backward({loss.name: torch.ones_like(loss.value)}, wrt, [loss.name])
 
     def calculateGradients(self, placeholders, *variables):
         if not self._loss_names:
             raise ValueError("no loss variables")
-        if placeholders:
-            self._exec({k: _tensor(v) for k, v in placeholders.items()}, self._loss_names)
+        self._exec({k: _tensor(v) for k, v in (placeholders or {}).items()}, self._loss_names)
         wrt = [w.name if isinstance(w, SDVariable) else w for w in variables] or list(self._trainable)
         seeds = {n: torch.ones_like(self.variables[n].value) for n in self._loss_names}
         return self._backward(seeds, wrt, list(self._loss_names))
@@ -498,15 +545,20 @@ class SameDiff:
                     self._exec(feeds, self._loss_names)
                     seeds = {n: torch.full_like(self.variables[n].value, sign) for n in self._loss_names}
                     grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
-                    off = 0
-                    for v in vs:
-                        k = v.value.numel()
+                    if "views" not in st:
+                        off, st["views"] = 0, []
+                        for v in vs:
+                            st["views"].append(st["grad"][off:off + v.value.numel()].view(v.value.shape))
+                            off += v.value.numel()
+                    dst, src = [], []
+                    for v, view in zip(vs, st["views"]):
                         g = grads.get(v.name)
                         if g is None:
-                            st["grad"][off:off + k].zero_()
+                            view.zero_()
                         else:
-                            st["grad"][off:off + k].copy_(g.reshape(-1))
-                        off += k
+                            dst.append(view)
+                            src.append(g.reshape(view.shape))
+                    torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
                     fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount,
                                  self.epochCount, 1, mini_batch=False, shadow=st["shadow"])
                     loss = sum(float(self.variables[n].value.float()) for n in self._loss_names)

@@ -106,8 +106,19 @@ _unary("softplus", lambda x, a: F.softplus(x), lambda g, x, y, a: g * torch.sigm
 _unary("elu", lambda x, a: F.elu(x), lambda g, x, y, a: g * torch.where(x > 0, torch.ones_like(x), y + 1))
 _unary("leakyRelu", lambda x, a: F.leaky_relu(x, a.get("alpha", 0.01)),
        lambda g, x, y, a: g * torch.where(x > 0, torch.ones_like(x), torch.full_like(x, a.get("alpha", 0.01))))
-_unary("gelu", lambda x, a: 0.5 * x * (1 + torch.erf(x / _SQRT2)),
-       lambda g, x, y, a: g * (0.5 * (1 + torch.erf(x / _SQRT2)) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)))
+def _gelu(z, dy=None):
+    """Exact GELU or its backward on the fused HIP kernel (GPU bf16/fp32), torch reference otherwise."""
+    if z.is_cuda and ops.use_native(z, "gelu"):
+        from ..ops import transformer_native as TN
+        r = TN.gelu(z.contiguous(), None if dy is None else dy.to(z.dtype).contiguous())
+        if r is not None:
+            return r
+    if dy is None:
+        return 0.5 * z * (1 + torch.erf(z / _SQRT2))
+    return (dy * (0.5 * (1 + torch.erf(z / _SQRT2)) + z * torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi))).to(z.dtype)
+
+
+register("gelu")((lambda ins, at: (_gelu(ins[0]), None), lambda ctx, g, ins, at: [_gelu(ins[0], g)]))
 _unary("softmax", lambda x, a: torch.softmax(x, dim=-1),
        lambda g, x, y, a: y * (g - (g * y).sum(-1, keepdim=True)))
 
@@ -155,19 +166,46 @@ def _mmul_bwd(ctx, g, ins, at):
 register("mmul")((_mmul_fwd, _mmul_bwd))
 
 
+def _param_acc(w):
+    return torch.float64 if w.dtype == torch.float64 else torch.float32
+
+
+def _colsum(g2):
+    """fp32 column sums of a [M, N] gradient (channel-sum HIP kernel on the GPU)."""
+    if g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float32) and g2.shape[1] % 8 == 0:
+        from ..ops import native
+        r = native.channel_sum(g2.contiguous())
+        if r is not None:
+            return r
+    return g2.to(_param_acc(g2)).sum(0)
+
+
 def _linear_fwd(ins, at):
+    """y = act(x . w + b); attr ``act`` ("gelu", set by SameDiff's fusion pass for linear -> gelu) runs the
+    activation in the GEMM epilogue and keeps the pre-activation for the backward."""
     x, w, b = ins
     from ..ops.gemm import mmul
-    return mmul(x, w, bias=None if b is None else b.reshape(-1)), None
+    bias = None if b is None else b.reshape(-1)
+    act = at.get("act")
+    if act is None:
+        return mmul(x, w, bias=bias), None
+    if x.is_cuda:
+        z = torch.empty(x.shape[:-1] + (w.shape[1],), dtype=x.dtype, device=x.device)
+        y = mmul(x, w, bias=bias, act=act, z=z)
+        return y, z
+    z = mmul(x, w, bias=bias)
+    return _gelu(z), z
 
 
 def _linear_bwd(ctx, g, ins, at):
     x, w, b = ins
+    if at.get("act") is not None:
+        g = _gelu(ctx, g.to(ctx.dtype))
     g2 = g.to(x.dtype).reshape(-1, g.shape[-1])
     x2 = x.reshape(-1, x.shape[-1])
     dx = _mm(g2, w.t()).reshape(x.shape)
-    dw = _mm(x2.t(), g2, out_dtype=torch.float32 if w.dtype != torch.float64 else None).to(w.dtype)
-    db = None if b is None else g2.float().sum(0).reshape(b.shape).to(b.dtype)
+    dw = _mm(x2.t(), g2, out_dtype=None if w.dtype == torch.float64 else torch.float32)
+    db = None if b is None else _colsum(g2).reshape(b.shape)
     return [dx, dw, db]
 
 
@@ -245,19 +283,26 @@ register("concat")((_concat_fwd, _concat_bwd))
 def _gather_fwd(ins, at):
     p, i = ins
     if at.get("axis", 0) == 0:
+        if p.dim() == 2:
+            from ..ops.nn_misc import embedding_forward
+            return embedding_forward(p, i), None
         return p.index_select(0, i.long().reshape(-1)).reshape(tuple(i.shape) + tuple(p.shape[1:])), None
     return torch.index_select(p, at["axis"], i.long().reshape(-1)), None
 
 
 def _gather_bwd(ctx, g, ins, at):
     p, i = ins
-    dp = torch.zeros_like(p, dtype=torch.float32 if p.dtype != torch.float64 else p.dtype)
+    dp = torch.zeros(p.shape, dtype=_param_acc(p), device=p.device)
     ax = at.get("axis", 0)
     if ax == 0:
-        dp.index_add_(0, i.long().reshape(-1), g.reshape(-1, *p.shape[1:]).to(dp.dtype))
+        from ..ops.nn_misc import embedding_backward_
+        if p.dim() == 2:
+            embedding_backward_(dp, i, g)
+        else:
+            dp.index_add_(0, i.long().reshape(-1), g.reshape(-1, *p.shape[1:]).to(dp.dtype))
     else:
         dp.index_add_(ax, i.long().reshape(-1), g.to(dp.dtype))
-    return [dp.to(p.dtype), None]
+    return [dp, None]
 
 
 register("gather")((_gather_fwd, _gather_bwd))
@@ -265,14 +310,21 @@ register("gather")((_gather_fwd, _gather_bwd))
 
 # ----------------------------------------------------------------------------------------------- NN blocks
 def _ln_fwd(ins, at):
-    x, gamma, beta = ins
+    """LayerNorm over the last dim of x (+ residual: the 4th input, set by SameDiff's fusion pass for
+    add -> layerNorm, summed inside the LayerNorm kernel)."""
+    x, gamma, beta = ins[:3]
+    res = ins[3] if len(ins) > 3 else None
     eps = at.get("eps", 1e-5)
     N = x.shape[-1]
     from ..ops import transformer_native as TN
     x2 = x.reshape(-1, N).contiguous()
-    if gamma is not None and beta is not None and TN.ln_supported(x2, N) and ops.use_native(x, "layernorm"):
-        y, mean, rstd = TN.ln_fwd(x2, gamma.reshape(-1), beta.reshape(-1), eps)
-        return y.reshape(x.shape), ("native", x2, mean, rstd)
+    if gamma is not None and beta is not None and TN.ln_supported(x2, N) and ops.use_native(x, "layernorm") and \
+            (res is None or res.dtype == x.dtype):
+        r2 = None if res is None else res.reshape(-1, N).contiguous()
+        y, mean, rstd = TN.ln_fwd(x2, gamma.reshape(-1), beta.reshape(-1), eps, r2)
+        return y.reshape(x.shape), ("native", x2, r2, mean, rstd)
+    if res is not None:
+        x2 = x2 + res.reshape(-1, N)
     xf = x2.float() if x.dtype != torch.float64 else x2
     mean = xf.mean(-1, keepdim=True)
     rstd = torch.rsqrt(((xf - mean) ** 2).mean(-1, keepdim=True) + eps)
@@ -283,22 +335,26 @@ def _ln_fwd(ins, at):
 
 
 def _ln_bwd(ctx, g, ins, at):
-    x, gamma, beta = ins
+    x, gamma, beta = ins[:3]
+    res = ins[3] if len(ins) > 3 else None
     N = x.shape[-1]
     g2 = g.reshape(-1, N).contiguous()
     if ctx[0] == "native":
         from ..ops import transformer_native as TN
-        _, x2, mean, rstd = ctx
-        dx, dg, db = TN.ln_bwd(g2.to(x.dtype), x2, gamma.reshape(-1), mean, rstd)
-        return [dx.reshape(x.shape), dg.to(gamma.dtype).reshape(gamma.shape), db.to(beta.dtype).reshape(beta.shape)]
+        _, x2, r2, mean, rstd = ctx
+        dx, dg, db = TN.ln_bwd(g2.to(x.dtype), x2, gamma.reshape(-1), mean, rstd, r2)
+        dx = dx.reshape(x.shape)
+        out = [dx, dg.reshape(gamma.shape), db.reshape(beta.shape)]
+        return out + ([dx.to(res.dtype)] if res is not None else [])
     _, xh, rstd = ctx
     gf = g2.to(xh.dtype)
     gam = gamma.reshape(-1).to(xh.dtype) if gamma is not None else torch.ones(N, dtype=xh.dtype, device=xh.device)
     dxh = gf * gam
     dx = rstd * (dxh - dxh.mean(-1, keepdim=True) - xh * (dxh * xh).mean(-1, keepdim=True))
-    dg = None if gamma is None else (gf * xh).sum(0).reshape(gamma.shape).to(gamma.dtype)
-    db = None if beta is None else gf.sum(0).reshape(beta.shape).to(beta.dtype)
-    return [dx.to(x.dtype).reshape(x.shape), dg, db]
+    dg = None if gamma is None else (gf * xh).sum(0).reshape(gamma.shape)
+    db = None if beta is None else gf.sum(0).reshape(beta.shape)
+    dx = dx.to(x.dtype).reshape(x.shape)
+    return [dx, dg, db] + ([dx.to(res.dtype)] if res is not None else [])
 
 
 register("layerNorm")((_ln_fwd, _ln_bwd))
@@ -373,7 +429,7 @@ def _conv_bwd(ctx, g, ins, at):
                                  gW=gW, gb=gb, grads_zeroed=True)
     dw = gW if dw is None else dw
     db = gb if db is None else db
-    return [dx, dw.to(w.dtype).reshape(w.shape), None if b is None else db.to(b.dtype).reshape(b.shape)]
+    return [dx, dw.reshape(w.shape), None if b is None else db.reshape(b.shape)]
 
 
 register("conv2d")((_conv_fwd, _conv_bwd))
@@ -499,7 +555,7 @@ def _lstm_bwd(ctx, g, ins, at):
     dW = mmul(xt.t(), dzc, out_dtype=torch.float32 if W.dtype != torch.float64 else None)
     db = dzf.sum(0)
     dx = mmul(dzc, W.t()).reshape(T, mb, nIn).permute(1, 2, 0)
-    return [dx.to(x.dtype), dW.to(W.dtype), dRW.to(RW.dtype).reshape(RW.shape), db.to(b.dtype).reshape(b.shape),
+    return [dx.to(x.dtype), dW, dRW.reshape(RW.shape), db.reshape(b.shape),
             None if h0 is None else dh0.to(h0.dtype), None if c0 is None else dc0.to(c0.dtype)]
 
 

@@ -19,12 +19,12 @@ def _transformer_block(dev, dt, base):
     sd = SameDiff.create()
     x = sd.placeHolder("x", base["x"].to(dev, dt))
     y = sd.placeHolder("y", base["y"].to(dev, dt))
-    v = {k: sd.var(k, base[k].to(dev, dt)) for k in ("wqkv", "bqkv", "wo", "bo", "g", "b", "wc")}
+    v = {k: sd.var(k, base[k].to(dev, dt)) for k in ("wqkv", "bqkv", "wo", "bo", "g", "b", "wf", "bf", "wc")}
     qkv = sd.nn().linear(x, v["wqkv"], v["bqkv"])
     a = sd.nn().fusedSelfAttention(qkv, 2)
     h = sd.nn().linear(a, v["wo"], v["bo"]).add(x)
     h = sd.nn().layerNorm(h, v["g"], v["b"])
-    h = sd.nn().gelu(h)
+    h = sd.nn().gelu(sd.nn().linear(h, v["wf"], v["bf"]))        # fused: GELU in the GEMM epilogue
     logits = h.get(slice(None), 0).mmul(v["wc"])
     loss = sd.loss().softmaxCrossEntropy("loss", y, logits)
     return sd, loss
@@ -36,10 +36,13 @@ def test_samediff_transformer_block_bf16_gpu_matches_fp64(cuda):
     base = {"x": torch.randn(B, T, E, generator=g), "wqkv": torch.randn(E, 3 * E, generator=g) * E ** -0.5,
             "bqkv": torch.randn(3 * E, generator=g) * 0.02, "wo": torch.randn(E, E, generator=g) * E ** -0.5,
             "bo": torch.zeros(E), "g": 1 + 0.1 * torch.randn(E, generator=g), "b": 0.1 * torch.randn(E, generator=g),
-            "wc": torch.randn(E, C, generator=g) * E ** -0.5,
+            "wc": torch.randn(E, C, generator=g) * E ** -0.5, "wf": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bf": 0.02 * torch.randn(E, generator=g),
             "y": torch.nn.functional.one_hot(torch.randint(0, C, (B,), generator=g), C).float()}
     fallback.reset()
     sd, loss = _transformer_block(cuda, torch.bfloat16, base)
+    ops = [r[1] for r in sd._plan([loss.name])]
+    assert "gelu" not in ops and "add" not in ops, ops
     gg = sd.execBackwards(loss)
     torch.cuda.synchronize()
     assert fallback.count() == 0, fallback.summary()

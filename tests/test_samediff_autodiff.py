@@ -209,3 +209,38 @@ def test_fit_trains_and_save_load_roundtrip(tmp_path):
     g1, g2 = sd.execBackwards(loss), sd2.execBackwards(sd2.getVariable("loss"))
     for k in g1:
         torch.testing.assert_close(g1[k], g2[k])
+
+
+def test_fused_forms_grads():
+    """The fused records the planner emits: linear with the GELU epilogue, LayerNorm with a residual input."""
+    _fd_check("linear", [_r(2, 3, 4, seed=1), _r(4, 5, seed=2), _r(5, seed=3)], {"act": "gelu"}, [0, 1, 2])
+    _fd_check("layerNorm", [_r(4, 6, seed=1), _r(6, seed=2), _r(6, seed=3), _r(4, 6, seed=4)], {"eps": 1e-5},
+              [0, 1, 2, 3])
+
+
+def _block(fusion):
+    g = torch.Generator().manual_seed(7)
+    sd = SameDiff.create()
+    sd.fusion = fusion
+    x = sd.placeHolder("x", torch.randn(3, 5, 8, generator=g, dtype=D))
+    w1 = sd.var("w1", torch.randn(8, 16, generator=g, dtype=D) * 0.3)
+    b1 = sd.var("b1", torch.randn(16, generator=g, dtype=D) * 0.1)
+    w2 = sd.var("w2", torch.randn(16, 8, generator=g, dtype=D) * 0.3)
+    gam = sd.var("g", torch.ones(8, dtype=D))
+    bet = sd.var("b", torch.zeros(8, dtype=D))
+    h = sd.nn().gelu(sd.nn().linear(x, w1, b1))
+    y = sd.nn().layerNorm(h.mmul(w2).add(x), gam, bet)
+    loss = y.mul(y).sum()
+    return sd, loss
+
+
+def test_fusion_pass_is_exact_and_fuses():
+    sd0, l0 = _block(False)
+    sd1, l1 = _block(True)
+    g0, g1 = sd0.execBackwards(l0), sd1.execBackwards(l1)
+    ops = [r[1] for r in sd1._plan([l1.name])]
+    assert "gelu" not in ops and "add" not in ops, ops
+    for k in g0:
+        torch.testing.assert_close(g0[k], g1[k])
+    x = torch.randn(3, 5, 8, dtype=D)
+    torch.testing.assert_close(sd0.output({"x": x}, l0)[l0.name], sd1.output({"x": x}, l1)[l1.name])
