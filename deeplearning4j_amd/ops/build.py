@@ -76,6 +76,32 @@ def build_runtime(verbose=True):
     return RUNTIME_LIB
 
 
+SANITIZERS = ("address", "thread", "undefined")
+
+
+def build_runtime_sanitized(kind, verbose=True):
+    """Standalone self-test executable of the host runtime built with ``-fsanitize=<kind>`` (address / thread /
+    undefined): every csrc/runtime/*.cpp plus csrc/runtime/tests/selftest.cpp. A sanitizer cannot instrument a
+    ctypes-loaded library inside an uninstrumented Python, so the runtime is exercised by its own driver."""
+    if kind not in SANITIZERS:
+        raise ValueError(f"sanitize must be one of {SANITIZERS}")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    drv = os.path.join(CSRC, "runtime", "tests", "selftest.cpp")
+    out_dir = os.path.join(BUILD, f"san_{kind}")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "runtime_selftest")
+    headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    if os.path.exists(exe) and not any(_newer(s, exe, headers) for s in srcs + [drv]):
+        return exe
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={kind}", "-std=c++17", "-pthread"]
+    if kind == "undefined":
+        flags.append("-fno-sanitize-recover=all")
+    _run(["g++"] + flags + ["-o", exe] + srcs + [drv])
+    if verbose:
+        print(f"[build] {exe}", file=sys.stderr)
+    return exe
+
+
 def build_all(verbose=True):
     k = build_kernels(verbose)
     r = build_runtime(verbose)
@@ -83,4 +109,12 @@ def build_all(verbose=True):
 
 
 if __name__ == "__main__":
-    build_all()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sanitize", choices=SANITIZERS, default=None,
+                    help="build the host-runtime self-test under a sanitizer instead of the libraries")
+    a = ap.parse_args()
+    if a.sanitize:
+        print(build_runtime_sanitized(a.sanitize))
+    else:
+        build_all()
