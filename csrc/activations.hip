@@ -47,6 +47,7 @@ DL4J_API int dl4j_gelu(int dtype, const void* z, const void* dy, void* out, long
       (dy && (reinterpret_cast<uintptr_t>(dy) & 15)))
     return -1;
   if (dtype == 1) return gelu_l<bf16>(z, dy, out, n, s);
+  if (dtype == 2) return gelu_l<f16>(z, dy, out, n, s);
   if (dtype == 0) return gelu_l<float>(z, dy, out, n, s);
   return -1;
 }

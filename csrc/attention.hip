@@ -1,4 +1,5 @@
-// Fused multi-head attention (flash-style) for gfx950, hb in / fp32 accumulate, head dim D in {64, 128}.
+// Fused multi-head attention (flash-style) for gfx950, bf16 or fp16 in (template element type hb) / fp32 accumulate,
+// head dim D in {64, 128}.
 // Used by the transformer layers (BERT-base config of BASELINE.json; attention is new relative to the reference,
 // SURVEY §2.6 / §5.7).
 //
@@ -21,52 +22,55 @@
 #include "common.h"
 
 typedef __attribute__((ext_vector_type(4))) float f4_t;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
-typedef __bf16 hb;                        // element type of every bf16 buffer in this file
+template <typename T> using V8 = T __attribute__((ext_vector_type(8)));
+template <typename T> using V4 = T __attribute__((ext_vector_type(4)));
 
 static constexpr int BLK = 64;             // rows (queries or keys) per block
 static constexpr float kLog2e = 1.4426950408889634f;
 static constexpr float kNegInf = -INFINITY;
 
-__device__ __forceinline__ f4_t mma(bf16x8_t a, bf16x8_t b, f4_t c) {
+// v_mfma_f32_16x16x32_{bf16,f16}: same fragment layout for both element types
+__device__ __forceinline__ f4_t mma(V8<__bf16> a, V8<__bf16> b, f4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ __bf16 tobf(float v) { return (__bf16)v; }
+__device__ __forceinline__ f4_t mma(V8<_Float16> a, V8<_Float16> b, f4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+template <typename hb> __device__ __forceinline__ hb tobf(float v) { return (hb)v; }
 
 // fragment of 8 hb from a row-major LDS/global row (16-byte aligned)
-__device__ __forceinline__ bf16x8_t ld8(const hb* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+template <typename hb> __device__ __forceinline__ V8<hb> ld8(const hb* p) { return *reinterpret_cast<const V8<hb>*>(p); }
 // two 4-element pieces (keys 4h..4h+3 and 16+4h..16+4h+3 of a 32-key step) of a transposed row
-__device__ __forceinline__ bf16x8_t ld4x2(const hb* row, int h) {
-  const bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(row + 4 * h);
-  const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(row + 16 + 4 * h);
-  return bf16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+template <typename hb> __device__ __forceinline__ V8<hb> ld4x2(const hb* row, int h) {
+  const V4<hb> a = *reinterpret_cast<const V4<hb>*>(row + 4 * h);
+  const V4<hb> b = *reinterpret_cast<const V4<hb>*>(row + 16 + 4 * h);
+  return V8<hb>{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 // B fragment from two accumulator tiles (16 rows each) in the permuted k order matching ld4x2
-__device__ __forceinline__ bf16x8_t pack2(const f4_t& x, const f4_t& y) {
-  return bf16x8_t{tobf(x[0]), tobf(x[1]), tobf(x[2]), tobf(x[3]), tobf(y[0]), tobf(y[1]), tobf(y[2]), tobf(y[3])};
+template <typename hb> __device__ __forceinline__ V8<hb> pack2(const f4_t& x, const f4_t& y) {
+  return V8<hb>{(hb)x[0], (hb)x[1], (hb)x[2], (hb)x[3], (hb)y[0], (hb)y[1], (hb)y[2], (hb)y[3]};
 }
 
 // cooperative block loads: rows [r0, r0+64) of a [T, ld] matrix slice (D columns at col0) into LDS
-template <int D>
+template <int D, typename hb>
 __device__ __forceinline__ void stage_rows(hb* dst, int dld, const hb* src, long long src_ld, int r0, int T) {
   constexpr int CPR = D / 8;                                  // 16-byte chunks per row
   for (int i = threadIdx.x; i < BLK * CPR; i += blockDim.x) {
     const int r = i / CPR, c = i - r * CPR;
-    bf16x8_t v;
-    if (r0 + r < T) v = *reinterpret_cast<const bf16x8_t*>(src + (long long)(r0 + r) * src_ld + c * 8);
-    else v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    *reinterpret_cast<bf16x8_t*>(dst + r * dld + c * 8) = v;
+    V8<hb> v;
+    if (r0 + r < T) v = *reinterpret_cast<const V8<hb>*>(src + (long long)(r0 + r) * src_ld + c * 8);
+    else v = V8<hb>{0, 0, 0, 0, 0, 0, 0, 0};
+    *reinterpret_cast<V8<hb>*>(dst + r * dld + c * 8) = v;
   }
 }
-template <int D>
+template <int D, typename hb>
 __device__ __forceinline__ void stage_rows_t(hb* dst, int dld, const hb* src, long long src_ld, int r0, int T) {
   constexpr int CPR = D / 8;                                  // transposed: dst[d][row]
   for (int i = threadIdx.x; i < BLK * CPR; i += blockDim.x) {
     const int r = i % BLK, c = i / BLK;
-    bf16x8_t v;
-    if (r0 + r < T) v = *reinterpret_cast<const bf16x8_t*>(src + (long long)(r0 + r) * src_ld + c * 8);
-    else v = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    V8<hb> v;
+    if (r0 + r < T) v = *reinterpret_cast<const V8<hb>*>(src + (long long)(r0 + r) * src_ld + c * 8);
+    else v = V8<hb>{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 8; ++k) dst[(c * 8 + k) * dld + r] = v[k];
   }
@@ -82,7 +86,7 @@ __device__ __forceinline__ float wsum16(float v) {
 }
 
 // ------------------------------------------------------------------------------------------------ forward
-template <int D>
+template <int D, typename hb>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qkv, const float* __restrict__ mask,
                                                        hb* __restrict__ out, float* __restrict__ lse, int T, int H,
                                                        float scale2, int causal) {
@@ -97,7 +101,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qk
   const hb* base = qkv + (long long)b * T * ld3;
   const int q = blockIdx.x * BLK + wave * 16 + col;
   const int qc = min(q, T - 1);
-  bf16x8_t qf[KS];
+  V8<hb> qf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) qf[ks] = ld8(base + (long long)qc * ld3 + h * D + ks * 32 + 8 * hgrp);
   f4_t acc[DT];
@@ -148,7 +152,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qk
     for (int dt = 0; dt < DT; ++dt) acc[dt] *= alpha;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      const bf16x8_t pb = pack2(s[2 * k2], s[2 * k2 + 1]);
+      const V8<hb> pb = pack2<hb>(s[2 * k2], s[2 * k2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) acc[dt] = mma(ld4x2(Vt + (dt * 16 + col) * LDV + 32 * k2, hgrp), pb, acc[dt]);
     }
@@ -158,8 +162,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qk
     hb* orow = out + ((long long)b * T + q) * E + h * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const bf16x4_t v{tobf(acc[dt][0] * inv), tobf(acc[dt][1] * inv), tobf(acc[dt][2] * inv), tobf(acc[dt][3] * inv)};
-      *reinterpret_cast<bf16x4_t*>(orow + dt * 16 + hgrp * 4) = v;
+      const V4<hb> v{tobf<hb>(acc[dt][0] * inv), tobf<hb>(acc[dt][1] * inv), tobf<hb>(acc[dt][2] * inv), tobf<hb>(acc[dt][3] * inv)};
+      *reinterpret_cast<V4<hb>*>(orow + dt * 16 + hgrp * 4) = v;
     }
     if (hgrp == 0) lse[(long long)bh * T + q] = l > 0.f ? m + log2f(l) : 1e30f;
   }
@@ -167,7 +171,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qk
 
 // ------------------------------------------------------------------------------------------------ backward
 // Dq[b,h,q] = sum_d dO[q,d] * O[q,d]
-template <int D>
+template <int D, typename hb>
 __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const hb* __restrict__ o, const hb* __restrict__ dout,
                                                            float* __restrict__ dq_dot, int B, int T, int H) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // over B*H*T
@@ -179,17 +183,15 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const hb* __restrict_
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < D / 8; ++c) {
-    float a[8], g[8];
-    Vec8<bf16>::load(reinterpret_cast<const bf16*>(o + off + c * 8), a);
-    Vec8<bf16>::load(reinterpret_cast<const bf16*>(dout + off + c * 8), g);
+    const V8<hb> a = ld8(o + off + c * 8), g = ld8(dout + off + c * 8);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += a[k] * g[k];
+    for (int k = 0; k < 8; ++k) s += (float)a[k] * (float)g[k];
   }
   dq_dot[i] = s;
 }
 
 // dQ per query block (forward orientation: query on the lane)
-template <int D>
+template <int D, typename hb>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const hb* __restrict__ qkv, const hb* __restrict__ dout,
                                                           const float* __restrict__ mask, const float* __restrict__ lse,
                                                           const float* __restrict__ dq_dot, hb* __restrict__ dqkv,
@@ -206,7 +208,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const hb* __restrict__
   const hb* base = qkv + (long long)b * T * ld3;
   const int q = blockIdx.x * BLK + wave * 16 + col;
   const int qc = min(q, T - 1);
-  bf16x8_t qf[KS], df[KS];
+  V8<hb> qf[KS], df[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     qf[ks] = ld8(base + (long long)qc * ld3 + h * D + ks * 32 + 8 * hgrp);
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const hb* __restrict__
       }
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      const bf16x8_t sb = pack2(s[2 * k2], s[2 * k2 + 1]);
+      const V8<hb> sb = pack2<hb>(s[2 * k2], s[2 * k2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) acc[dt] = mma(ld4x2(Kt + (dt * 16 + col) * LDT + 32 * k2, hgrp), sb, acc[dt]);
     }
@@ -257,15 +259,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const hb* __restrict__
     hb* dst = dqkv + ((long long)b * T + q) * ld3 + h * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const bf16x4_t v{tobf(acc[dt][0] * scale), tobf(acc[dt][1] * scale), tobf(acc[dt][2] * scale),
-                       tobf(acc[dt][3] * scale)};
-      *reinterpret_cast<bf16x4_t*>(dst + dt * 16 + hgrp * 4) = v;
+      const V4<hb> v{tobf<hb>(acc[dt][0] * scale), tobf<hb>(acc[dt][1] * scale), tobf<hb>(acc[dt][2] * scale),
+                       tobf<hb>(acc[dt][3] * scale)};
+      *reinterpret_cast<V4<hb>*>(dst + dt * 16 + hgrp * 4) = v;
     }
   }
 }
 
 // dK, dV per key block (key on the lane)
-template <int D>
+template <int D, typename hb>
 __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const hb* __restrict__ qkv,
                                                             const hb* __restrict__ dout,
                                                             const float* __restrict__ mask,
@@ -290,7 +292,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const hb* __restrict
   const int kc = min(key, T - 1);
   bool kvalid = key < T;
   if (kvalid && mask) kvalid = mask[(long long)b * T + key] != 0.f;
-  bf16x8_t kf[KS], vf[KS];
+  V8<hb> kf[KS], vf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     kf[ks] = ld8(base + (long long)kc * ld3 + E + h * D + ks * 32 + 8 * hgrp);
@@ -337,8 +339,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const hb* __restrict
       }
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      const bf16x8_t pb = pack2(s[2 * k2], s[2 * k2 + 1]);
-      const bf16x8_t sb = pack2(ds[2 * k2], ds[2 * k2 + 1]);
+      const V8<hb> pb = pack2<hb>(s[2 * k2], s[2 * k2 + 1]);
+      const V8<hb> sb = pack2<hb>(ds[2 * k2], ds[2 * k2 + 1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         dv[dt] = mma(ld4x2(Dt + (dt * 16 + col) * LDT + 32 * k2, hgrp), pb, dv[dt]);
@@ -350,54 +352,71 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const hb* __restrict
     hb* dst = dqkv + ((long long)b * T + key) * ld3 + h * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const bf16x4_t kv{tobf(dk[dt][0] * scale), tobf(dk[dt][1] * scale), tobf(dk[dt][2] * scale),
-                        tobf(dk[dt][3] * scale)};
-      const bf16x4_t vv{tobf(dv[dt][0]), tobf(dv[dt][1]), tobf(dv[dt][2]), tobf(dv[dt][3])};
-      *reinterpret_cast<bf16x4_t*>(dst + E + dt * 16 + hgrp * 4) = kv;
-      *reinterpret_cast<bf16x4_t*>(dst + 2 * E + dt * 16 + hgrp * 4) = vv;
+      const V4<hb> kv{tobf<hb>(dk[dt][0] * scale), tobf<hb>(dk[dt][1] * scale), tobf<hb>(dk[dt][2] * scale),
+                        tobf<hb>(dk[dt][3] * scale)};
+      const V4<hb> vv{tobf<hb>(dv[dt][0]), tobf<hb>(dv[dt][1]), tobf<hb>(dv[dt][2]), tobf<hb>(dv[dt][3])};
+      *reinterpret_cast<V4<hb>*>(dst + E + dt * 16 + hgrp * 4) = kv;
+      *reinterpret_cast<V4<hb>*>(dst + 2 * E + dt * 16 + hgrp * 4) = vv;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------------ launch
-template <int D>
+template <int D, typename hb>
 static int fwd_l(const void* qkv, const float* mask, void* out, float* lse, int B, int T, int H, float scale,
                  int causal, hipStream_t s) {
   const dim3 grid((T + BLK - 1) / BLK, B * H);
-  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(256), 0, s, (const hb*)qkv, mask, (hb*)out, lse, T, H,
+  hipLaunchKernelGGL((attn_fwd_kernel<D, hb>), grid, dim3(256), 0, s, (const hb*)qkv, mask, (hb*)out, lse, T, H,
                      scale * kLog2e, causal);
   return (int)hipGetLastError();
 }
 
-template <int D>
+template <int D, typename hb>
 static int bwd_l(const void* qkv, const void* out, const void* dout, const float* mask, const float* lse,
                  float* dq_dot, void* dqkv, int B, int T, int H, float scale, int causal, hipStream_t s) {
   const long long n = (long long)B * H * T;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const hb*)out,
+  hipLaunchKernelGGL((attn_bwd_pre_kernel<D, hb>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const hb*)out,
                      (const hb*)dout, dq_dot, B, T, H);
   const dim3 grid((T + BLK - 1) / BLK, B * H);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, grid, dim3(256), 0, s, (const hb*)qkv, (const hb*)dout, mask, lse,
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, hb>), grid, dim3(256), 0, s, (const hb*)qkv, (const hb*)dout, mask, lse,
                      dq_dot, (hb*)dqkv, T, H, scale * kLog2e, scale, causal);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(256), 0, s, (const hb*)qkv, (const hb*)dout, mask, lse,
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, hb>), grid, dim3(256), 0, s, (const hb*)qkv, (const hb*)dout, mask, lse,
                      dq_dot, (hb*)dqkv, T, H, scale * kLog2e, scale, causal);
   return (int)hipGetLastError();
 }
 
-// qkv [B,T,3*H*D] hb; mask [B,T] fp32 or null; out [B,T,H*D] hb; lse [B,H,T] fp32. -1 = unsupported shape.
-DL4J_API int dl4j_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int T, int H, int D,
-                           float scale, int causal, hipStream_t s) {
-  if (B < 1 || T < 1 || H < 1) return -1;
-  if (D == 64) return fwd_l<64>(qkv, mask, out, lse, B, T, H, scale, causal, s);
-  if (D == 128) return fwd_l<128>(qkv, mask, out, lse, B, T, H, scale, causal, s);
+// dt: 1 = bf16, 2 = fp16. qkv [B,T,3*H*D]; mask [B,T] fp32 or null; out [B,T,H*D]; lse [B,H,T] fp32.
+// -1 = unsupported shape / dtype.
+DL4J_API int dl4j_attn_fwd_dt(int dt, const void* qkv, const float* mask, void* out, float* lse, int B, int T, int H,
+                              int D, float scale, int causal, hipStream_t s) {
+  if (B < 1 || T < 1 || H < 1 || (dt != 1 && dt != 2)) return -1;
+  if (D == 64) return dt == 1 ? fwd_l<64, __bf16>(qkv, mask, out, lse, B, T, H, scale, causal, s)
+                              : fwd_l<64, _Float16>(qkv, mask, out, lse, B, T, H, scale, causal, s);
+  if (D == 128) return dt == 1 ? fwd_l<128, __bf16>(qkv, mask, out, lse, B, T, H, scale, causal, s)
+                               : fwd_l<128, _Float16>(qkv, mask, out, lse, B, T, H, scale, causal, s);
   return -1;
 }
 
-// dout [B,T,H*D] hb; dq_dot: fp32 workspace [B,H,T]; dqkv [B,T,3*H*D] hb (fully written).
+// dout [B,T,H*D]; dq_dot: fp32 workspace [B,H,T]; dqkv [B,T,3*H*D] (fully written).
+DL4J_API int dl4j_attn_bwd_dt(int dt, const void* qkv, const void* out, const void* dout, const float* mask,
+                              const float* lse, float* dq_dot, void* dqkv, int B, int T, int H, int D, float scale,
+                              int causal, hipStream_t s) {
+  if (B < 1 || T < 1 || H < 1 || (dt != 1 && dt != 2)) return -1;
+  if (D == 64) return dt == 1 ? bwd_l<64, __bf16>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal, s)
+                              : bwd_l<64, _Float16>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal, s);
+  if (D == 128) return dt == 1 ? bwd_l<128, __bf16>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal, s)
+                               : bwd_l<128, _Float16>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal,
+                                                      s);
+  return -1;
+}
+
+DL4J_API int dl4j_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int T, int H, int D,
+                           float scale, int causal, hipStream_t s) {
+  return dl4j_attn_fwd_dt(1, qkv, mask, out, lse, B, T, H, D, scale, causal, s);
+}
+
 DL4J_API int dl4j_attn_bwd(const void* qkv, const void* out, const void* dout, const float* mask, const float* lse,
                            float* dq_dot, void* dqkv, int B, int T, int H, int D, float scale, int causal,
                            hipStream_t s) {
-  if (B < 1 || T < 1 || H < 1) return -1;
-  if (D == 64) return bwd_l<64>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal, s);
-  if (D == 128) return bwd_l<128>(qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, scale, causal, s);
-  return -1;
+  return dl4j_attn_bwd_dt(1, qkv, out, dout, mask, lse, dq_dot, dqkv, B, T, H, D, scale, causal, s);
 }

@@ -51,12 +51,31 @@ template <> struct Vec8<float> {
   }
 };
 
+// fp16 storage (IEEE half, the MFMA f16 operand type); math stays fp32.
+typedef _Float16 f16;
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+template <> struct Vec8<f16> {
+  static __device__ __forceinline__ void load(const f16* p, float* o) {
+    const f16x8_t v = *reinterpret_cast<const f16x8_t*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
+  static __device__ __forceinline__ void store(f16* p, const float* o) {
+    f16x8_t v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (f16)o[i];
+    *reinterpret_cast<f16x8_t*>(p) = v;
+  }
+};
+
 template <typename T> __device__ __forceinline__ float ld1(const T* p);
 template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld1<bf16>(const bf16* p) { return bf2f(*reinterpret_cast<const u16*>(p)); }
 template <typename T> __device__ __forceinline__ void st1(T* p, float v);
 template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
 template <> __device__ __forceinline__ void st1<bf16>(bf16* p, float v) { *reinterpret_cast<u16*>(p) = f2bf(v); }
+template <> __device__ __forceinline__ float ld1<f16>(const f16* p) { return (float)*p; }
+template <> __device__ __forceinline__ void st1<f16>(f16* p, float v) { *p = (f16)v; }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

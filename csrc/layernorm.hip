@@ -13,6 +13,10 @@ template <> struct V8<bf16> {
   static __device__ __forceinline__ void ld(const bf16* p, float* o) { Vec8<bf16>::load(p, o); }
   static __device__ __forceinline__ void st(bf16* p, const float* o) { Vec8<bf16>::store(p, o); }
 };
+template <> struct V8<f16> {
+  static __device__ __forceinline__ void ld(const f16* p, float* o) { Vec8<f16>::load(p, o); }
+  static __device__ __forceinline__ void st(f16* p, const float* o) { Vec8<f16>::store(p, o); }
+};
 template <> struct V8<float> {
   static __device__ __forceinline__ void ld(const float* p, float* o) { Vec8<float>::load(p, o); }
   static __device__ __forceinline__ void st(float* p, const float* o) { Vec8<float>::store(p, o); }
@@ -213,11 +217,12 @@ static int bwd_l(const void* dy, const void* x, const void* r, const float* g, c
 
 DL4J_API long long dl4j_ln_partial_rows(long long M) { return ln_bwd_partials(M); }
 
-// dtype 0 fp32, 1 bf16. r may be null (no residual). Returns -1 when N is unsupported (N % 8 or N > 4096).
+// dtype 0 fp32, 1 bf16, 2 fp16. r may be null (no residual). Returns -1 when N is unsupported (N % 8 or N > 4096).
 DL4J_API int dl4j_ln_fwd(int dtype, const void* x, const void* r, const float* gamma, const float* beta, void* y,
                          float* mean, float* rstd, long long M, int N, float eps, hipStream_t s) {
   if (N % 8 != 0 || N > 4096 || M < 1) return -1;
   if (dtype == 1) LN_CH_DISPATCH(fwd_l, bf16, x, r, gamma, beta, y, mean, rstd, M, N, eps, s);
+  if (dtype == 2) LN_CH_DISPATCH(fwd_l, f16, x, r, gamma, beta, y, mean, rstd, M, N, eps, s);
   LN_CH_DISPATCH(fwd_l, float, x, r, gamma, beta, y, mean, rstd, M, N, eps, s);
 }
 
@@ -227,5 +232,6 @@ DL4J_API int dl4j_ln_bwd(int dtype, const void* dy, const void* x, const void* r
                          long long M, int N, hipStream_t s) {
   if (N % 8 != 0 || N > 4096 || M < 1) return -1;
   if (dtype == 1) LN_CH_DISPATCH(bwd_l, bf16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
+  if (dtype == 2) LN_CH_DISPATCH(bwd_l, f16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
   LN_CH_DISPATCH(bwd_l, float, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
 }

@@ -289,6 +289,7 @@ static inline int grid_for(long long total, int per_block = 256) {
   do {                                                               \
     if ((dt) == 1) { typedef bf16 T; __VA_ARGS__; }                  \
     else if ((dt) == 0) { typedef float T; __VA_ARGS__; }            \
+    else if ((dt) == 2) { typedef f16 T; __VA_ARGS__; }              \
     else return 1;                                                   \
   } while (0)
 

@@ -42,6 +42,9 @@ DL4J_API int dl4j_softmax_xent(int dtype, const void* z, const float* y, int B, 
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_xent_kernel<bf16>, dim3(B), dim3(256), 0, s, (const bf16*)z, y, V, (bf16*)grad, score,
                        prob, le, l1);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(softmax_xent_kernel<f16>, dim3(B), dim3(256), 0, s, (const f16*)z, y, V, (f16*)grad, score,
+                       prob, le, l1);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)z, y, V, (float*)grad, score,
                        prob, le, l1);

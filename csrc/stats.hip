@@ -191,6 +191,8 @@ DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, floa
   const dim3 grid((unsigned)blocks, (C + 2047) / 2048);
   if (dtype == 1)
     hipLaunchKernelGGL(channel_sum_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, M, C, out);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(channel_sum_kernel<f16>, grid, dim3(256), lds, stream, (const f16*)x, M, C, out);
   else
     hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), lds, stream, (const float*)x, M, C, out);
   return (int)hipGetLastError();

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
   }
 }
 
-// segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (treated as bf16 layout not supported -> none)
+// segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (reduced-precision compute copy)
 // btab: device int2[nblocks] built by the host from the segment sizes (see dl4j_update_chunk).
 DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
                                void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
@@ -113,6 +113,9 @@ DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, 
   if (shadow_kind == 1)
     hipLaunchKernelGGL(fused_update_kernel<bf16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out);
+  else if (shadow_kind == 2)
+    hipLaunchKernelGGL(fused_update_kernel<f16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
+                       (const int2*)btab, p, g, st, (f16*)shadow, inv_div, write_update, reg_out);
   else
     hipLaunchKernelGGL(fused_update_kernel<float>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out);

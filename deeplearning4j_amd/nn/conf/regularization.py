@@ -32,7 +32,7 @@ class IDropout(Config):
     def _gpu(self, x, mode, **kw):
         """Native forward when x is a bf16/fp32 CUDA tensor; returns None otherwise."""
         from ...ops.dispatch import use_native
-        if not use_native(x, "dropout") or x.dtype not in (torch.bfloat16, torch.float32):
+        if not use_native(x, "dropout") or x.dtype not in (torch.bfloat16, torch.float32, torch.float16):
             self._native = None
             return None
         from ...ops import nn_misc

@@ -172,7 +172,8 @@ def weight_grad_(view, a, b):
 
 def bias_grad_(view, delta):
     """Bias gradient = column sums of delta [M, N] (fp32), on the channel-sum HIP kernel when on the GPU."""
-    if delta.is_cuda and delta.dim() == 2 and delta.dtype in (torch.float32, torch.bfloat16) and delta.is_contiguous() \
+    if delta.is_cuda and delta.dim() == 2 and delta.dtype in (torch.float32, torch.bfloat16, torch.float16) \
+            and delta.is_contiguous() \
             and view.dtype == torch.float32 and view.is_contiguous() and delta.shape[1] % 8 == 0:
         from ...ops import native
         if native.channel_sum(delta, out=view.reshape(-1)) is not None:

@@ -24,7 +24,7 @@ from ...ops.gemm import mmul
 
 
 def _native(x, op):
-    return x.is_cuda and x.dtype == torch.bfloat16 and ops.use_native(x, op)
+    return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and ops.use_native(x, op)
 
 
 def _wgrad(view, a, b):

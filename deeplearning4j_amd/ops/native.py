@@ -231,9 +231,9 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
         cache.nblocks = len(rows)
     sk = 0
     if shadow is not None:
-        if shadow.dtype != torch.bfloat16:
+        sk = {torch.bfloat16: 1, torch.float16: 2}.get(shadow.dtype)
+        if sk is None:
             return False
-        sk = 1
     rc = lib.dl4j_fused_update(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
                                _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
                                _stream())
@@ -373,8 +373,14 @@ def bn_pool_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
 
 
 # ------------------------------------------------------------------------------------------ softmax-xent
+def _dt16(t):
+    """Element-type code for the kernels that also take fp16 (LayerNorm, GELU, attention, softmax-xent,
+    channel sums, updater shadow): 0 fp32, 1 bf16, 2 fp16."""
+    return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(t.dtype)
+
+
 def softmax_xent(logits, labels, clip_eps):
-    dt = _dt(logits)
+    dt = _dt16(logits)
     if dt is None or not logits.is_contiguous():
         return None
     B, V = logits.shape
@@ -461,7 +467,7 @@ def segment_stats(flat, offsets, bins=0):
 def channel_sum(rows, out=None):
     """fp32 column sums of a contiguous [M, C] fp32/bf16 CUDA matrix (dl4j_channel_sum); None if unsupported.
     ``out``: optional contiguous fp32 [C] destination (e.g. a flat-gradient view)."""
-    dt = _dt(rows)
+    dt = _dt16(rows)
     if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] % 8:
         return None
     lib = load()

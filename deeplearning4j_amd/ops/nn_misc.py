@@ -42,7 +42,7 @@ def _lib():
 
 
 def _dt(t):
-    return {torch.bfloat16: 1, torch.float32: 0}.get(t.dtype)
+    return {torch.bfloat16: 1, torch.float32: 0, torch.float16: 2}.get(t.dtype)
 
 
 def _p(t):

@@ -7,9 +7,10 @@ from . import native
 from .native import _check, _ptr, _stream, c_float, c_int, c_ll, c_void_p
 
 _SIGS = {
-    "dl4j_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
-    "dl4j_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                      c_float, c_int, c_void_p],
+    "dl4j_attn_fwd_dt": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int,
+                         c_void_p],
+    "dl4j_attn_bwd_dt": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                         c_int, c_int, c_float, c_int, c_void_p],
     "dl4j_ln_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_float,
                     c_void_p],
     "dl4j_ln_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -28,7 +29,7 @@ def _lib():
 
 # ------------------------------------------------------------------------------------------------ attention
 def attn_supported(qkv, H):
-    if not (qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 3 and qkv.is_contiguous()):
+    if not (qkv.is_cuda and qkv.dtype in (torch.bfloat16, torch.float16) and qkv.dim() == 3 and qkv.is_contiguous()):
         return False
     E3 = qkv.shape[2]
     if E3 % (3 * H):
@@ -37,15 +38,15 @@ def attn_supported(qkv, H):
 
 
 def attn_fwd(qkv, H, mask=None, causal=False, scale=None):
-    """qkv [B, T, 3E] bf16 contiguous -> (out [B, T, E] bf16, lse [B, H, T] fp32)."""
+    """qkv [B, T, 3E] bf16/fp16 contiguous -> (out [B, T, E] same dtype, lse [B, H, T] fp32)."""
     B, T, E3 = qkv.shape
     D = E3 // (3 * H)
     scale = float(scale if scale is not None else D ** -0.5)
-    out = torch.empty(B, T, E3 // 3, device=qkv.device, dtype=torch.bfloat16)
+    out = torch.empty(B, T, E3 // 3, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
     m = None if mask is None else mask.reshape(B, T).to(torch.float32).contiguous()
-    rc = _lib().dl4j_attn_fwd(_ptr(qkv), _ptr(m), _ptr(out), _ptr(lse), B, T, H, D, scale, int(bool(causal)),
-                              c_void_p(_stream()))
+    rc = _lib().dl4j_attn_fwd_dt(_dt(qkv), _ptr(qkv), _ptr(m), _ptr(out), _ptr(lse), B, T, H, D, scale,
+                                 int(bool(causal)), c_void_p(_stream()))
     if rc == -1:
         return None
     _check(rc, "attn_fwd")
@@ -53,16 +54,16 @@ def attn_fwd(qkv, H, mask=None, causal=False, scale=None):
 
 
 def attn_bwd(qkv, out, lse, dout, H, mask=None, causal=False, scale=None):
-    """Returns dqkv [B, T, 3E] bf16 (dQ, dK, dV in the fused projection layout)."""
+    """Returns dqkv [B, T, 3E] in qkv's dtype (dQ, dK, dV in the fused projection layout)."""
     B, T, E3 = qkv.shape
     D = E3 // (3 * H)
     scale = float(scale if scale is not None else D ** -0.5)
-    dout = dout.to(torch.bfloat16).contiguous()
+    dout = dout.to(qkv.dtype).contiguous()
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(B, H, T, device=qkv.device, dtype=torch.float32)
     m = None if mask is None else mask.reshape(B, T).to(torch.float32).contiguous()
-    rc = _lib().dl4j_attn_bwd(_ptr(qkv), _ptr(out), _ptr(dout), _ptr(m), _ptr(lse), _ptr(ws), _ptr(dqkv), B, T, H, D,
-                              scale, int(bool(causal)), c_void_p(_stream()))
+    rc = _lib().dl4j_attn_bwd_dt(_dt(qkv), _ptr(qkv), _ptr(out), _ptr(dout), _ptr(m), _ptr(lse), _ptr(ws), _ptr(dqkv),
+                                 B, T, H, D, scale, int(bool(causal)), c_void_p(_stream()))
     if rc == -1:
         return None
     _check(rc, "attn_bwd")
@@ -108,7 +109,7 @@ def attention_reference(qkv, H, mask=None, causal=False, scale=None):
 
 # ------------------------------------------------------------------------------------------------ layernorm
 def _dt(t):
-    return 1 if t.dtype == torch.bfloat16 else (0 if t.dtype == torch.float32 else None)
+    return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(t.dtype)
 
 
 def ln_supported(x, N):

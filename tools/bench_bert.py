@@ -30,7 +30,8 @@ def run_dl4j(args, dev):
     from deeplearning4j_amd.models import BertBase
     from deeplearning4j_amd.nn.conf import DataType
     net = BertBase(numLabels=2, inputShape=[args.seq], layers=args.layers,
-                   dataType=DataType.BFLOAT16 if args.dtype == "bf16" else DataType.FLOAT).init(device=dev)
+                   dataType={"bf16": DataType.BFLOAT16, "fp16": DataType.HALF}.get(args.dtype, DataType.FLOAT)
+                   ).init(device=dev)
     g = torch.Generator().manual_seed(0)
     x = torch.randint(0, 30522, (args.batch, args.seq), generator=g).to(dev)
     y = torch.nn.functional.one_hot(torch.randint(0, 2, (args.batch,), generator=g), 2).float().to(dev)
@@ -47,8 +48,8 @@ def run_torch(args, dev):
     import transformers
     cfg = transformers.BertConfig(num_hidden_layers=args.layers, num_labels=2, attn_implementation="sdpa")
     model = transformers.BertForSequenceClassification(cfg).to(dev)
-    if args.dtype == "bf16":
-        model = model.to(torch.bfloat16)
+    if args.dtype in ("bf16", "fp16"):
+        model = model.to(torch.bfloat16 if args.dtype == "bf16" else torch.float16)
     model.train()
     opt = torch.optim.AdamW(model.parameters(), lr=2e-5, fused=dev.type == "cuda")
     g = torch.Generator().manual_seed(0)
@@ -73,7 +74,7 @@ def main():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--graph", type=int, default=1, help="capture the dl4j training step in HIP graphs")
     args = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
