@@ -166,7 +166,10 @@ class BaseNetwork:
                 ys = list(y) if isinstance(y, (list, tuple)) else [y]
                 if self._try_graph_step(xs, ys, fmask, lmask):
                     return None
-            return self._fit_batch_sgd(x, y, fmask, lmask)
+                return self._fit_batch_sgd(x, y, fmask, lmask)
+            from ..memory.arena import training_scope
+            with training_scope(self):                   # LOOP_FF_BP workspace for this iteration's activations
+                return self._fit_batch_sgd(x, y, fmask, lmask)
         if getattr(self, "_solver", None) is None:
             from ..optimize.solvers import Solver
             self._solver = Solver(self)

@@ -16,6 +16,8 @@ import numpy as np
 
 import torch
 
+from ..memory import arena
+
 from . import native
 from .native import _ptr, _stream, c_int, c_ll, c_void_p
 
@@ -213,7 +215,7 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
         from .gemm import mmul
         x = _cl(x)
         M = N * H * W
-        y = torch.empty((N, K, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        y = arena.empty((N, K, H, W), torch.bfloat16, x.device, channels_last=True)
         ts = None
         if want_stats and C % 64 == 0 and K % 8 == 0:
             P = 2 * ((M + 127) // 128)
@@ -225,7 +227,7 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
         return y
     krsc, _ = _relayout(w, True, False)
     x = _cl(x)
-    y = torch.empty((N, K, OH, OW), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    y = arena.empty((N, K, OH, OW), torch.bfloat16, x.device, channels_last=True)
     bias = b.float().contiguous() if b is not None else None
     ts = None
     if want_stats and C % 32 == 0 and R * S <= 64 and K % 8 == 0:
@@ -270,8 +272,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
         M = N * H * W
         acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
-        dx = dx_accum if acc else torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
-                                              memory_format=torch.channels_last)
+        dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
+                                              channels_last=True)
         # dX[M, C] = dY[M, K] . W[K, C]  (+= the other consumer's gradient through beta)
         mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
              beta=1.0 if acc else 0.0)
@@ -282,8 +284,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
         if s1 and (H, W) == _out_hw_inv(OH, OW, R, S, pad4, H, W):
             _, flip = _relayout(w, False, True)
-            dx = dx_accum if acc else torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
-                                                  memory_format=torch.channels_last)
+            dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
+                                                  channels_last=True)
             rc = lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, R, S, pad4[0], pad4[2], OH,
                                            OW, int(acc), _stream())
             native._check(rc, "conv_bwd_data_s1")
@@ -297,6 +299,18 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
                                             int(acc), _stream())
             native._check(rc, "conv_bwd_data_1x1")
+        elif tuple(dilation) == (1, 1) and max(stride) > 1 and pad4[0] <= R - 1 and pad4[1] <= R - 1 and \
+                pad4[2] <= S - 1 and pad4[3] <= S - 1 and \
+                H >= (OH - 1) * stride[0] + R - pad4[0] - pad4[1] and W >= (OW - 1) * stride[1] + S - pad4[2] - pad4[3]:
+            # strided bwd-data = stride-1 transposed conv of the zero-interleaved dY (extended by the rows / cols
+            # no window reached) on the MFMA kernel: s^2 more MACs than a phase-split kernel, but never the library
+            sh, sw = stride
+            eh = H - ((OH - 1) * sh + R - pad4[0] - pad4[1])
+            ew = W - ((OW - 1) * sw + S - pad4[2] - pad4[3])
+            dyz = torch.empty((N, K, (OH - 1) * sh + 1 + eh, (OW - 1) * sw + 1 + ew), dtype=torch.bfloat16,
+                              device=x.device, memory_format=torch.channels_last).zero_()
+            dyz[:, :, :(OH - 1) * sh + 1:sh, :(OW - 1) * sw + 1:sw] = dy
+            dx = _conv2d_bwd(x, w, dyz, (1, 1), pad4, dilation, True, False, False, dx_accum=dx_accum)[0]
         else:
             from .conv import _sym
             from .fallback import record

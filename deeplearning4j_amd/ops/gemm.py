@@ -155,6 +155,9 @@ def _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z):
     if out is not None:
         out.copy_(r)
         return out
+    from ..memory import arena
+    if arena.current() is not None:
+        return arena.empty(r.shape, out_dtype, r.device).copy_(r)
     return r.to(out_dtype)
 
 
@@ -202,7 +205,8 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     if b.shape[-2] != K:
         raise ValueError(f"mmul shape mismatch {tuple(a.shape)} x {tuple(b.shape)}")
     if out is None:
-        out = torch.empty(((batch,) if batched else ()) + (M, N), dtype=out_dtype, device=a.device)
+        from ..memory import arena
+        out = arena.empty(((batch,) if batched else ()) + (M, N), out_dtype, a.device)
         if beta != 0.0:
             raise ValueError("beta != 0 needs an existing out")
     if M == 0 or N == 0:

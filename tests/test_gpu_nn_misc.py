@@ -205,3 +205,27 @@ def test_misc_layers_network_step_has_no_fallback(cuda):
     torch.cuda.synchronize()
     assert net.helperCountFail() == 0, net.fallbackSummary()
     assert scores[-1] < scores[0]
+
+
+@pytest.mark.parametrize("H,k,s,p", [(56, 3, 2, 1), (28, 3, 2, 1), (15, 3, 2, 1), (14, 5, 2, 2), (17, 3, 3, 1)])
+def test_strided_bwd_data_on_mfma(cuda, H, k, s, p):
+    """Strided k x k bwd-data (canonical ResNet v1.5 stride-2 3x3 convs) on the stride-1 kernel over a
+    zero-interleaved dY, no library fallback, vs fp32 torch."""
+    from deeplearning4j_amd.ops import conv2d_backward, conv2d_forward
+    g = torch.Generator().manual_seed(H + k + s)
+    N, C, K = 8, 32, 64
+    x = torch.randn(N, C, H, H, generator=g)
+    w = torch.randn(K, C, k, k, generator=g) * 0.1
+    bf = torch.bfloat16
+    xd = x.to(cuda, bf).contiguous(memory_format=torch.channels_last)
+    fallback.reset()
+    y = conv2d_forward(xd, w.to(cuda, bf), None, (s, s), (p, p, p, p))
+    gy = torch.randn(y.shape, generator=g)
+    dx, _, _ = conv2d_backward(xd, w.to(cuda, bf), gy.to(cuda, bf).contiguous(memory_format=torch.channels_last),
+                               (s, s), (p, p, p, p), (1, 1), True, False, False)
+    torch.cuda.synchronize()
+    assert fallback.count() == 0, fallback.summary()
+    xr = x.to(bf).float().requires_grad_(True)
+    yr = F.conv2d(xr, w.to(bf).float(), None, s, p)
+    yr.backward(gy.to(bf).float())
+    _close(dx, xr.grad, 2e-2)
