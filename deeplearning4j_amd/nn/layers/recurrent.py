@@ -40,7 +40,7 @@ def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache)
         r = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, mask, need_cache)
         if r is not None:
             out_tmh, hT, cT, gates, call = r
-            out = out_tmh.permute(1, 2, 0).to(x.dtype if x.is_floating_point() else dt)
+            out = out_tmh.permute(1, 2, 0).to(dt)          # compute dtype (DL4J casts input to the net dtype)
             cache = None
             if need_cache:
                 cache = {"native": True, "gates": gates, "call": call, "out": out_tmh, "h0": h0, "c0": c0,
@@ -86,7 +86,7 @@ def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache)
             cache["cact"].append(cact)
         h, c = h_new, c_new
         outs.append(h)
-    out = torch.stack(outs, dim=2).to(x.dtype if x.is_floating_point() else dt)
+    out = torch.stack(outs, dim=2).to(dt)
     if need_cache:
         cache["xt"] = xt
     return out, (h, c), cache
@@ -130,6 +130,21 @@ def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_pre
     dz, dh0, dc0 = r
     out = cache["out"]                                                # [T, mb, H] fp32
     dev = eps.device
+    if W.dtype in (torch.bfloat16, torch.float16):
+        prep = rnn_native.lstm_bwd_prep(dz, out, cache["h0"], cache["call"], cache["c0"], peephole, W.dtype)
+        if prep is not None:
+            # one fused glue launch, then the three GEMMs write fp32 gradients straight into the flat views
+            from .transformer import _wgrad
+            dzb, hpb, db, dpeep = prep
+            _wgrad(grads[grads_prefix + "W"], cache["xt"].to(W.dtype), dzb)
+            gRW = grads[grads_prefix + "RW"]
+            if peephole:
+                _wgrad(gRW[:, :4 * H], hpb, dzb)
+                gRW[:, 4 * H:].copy_(dpeep.t())
+            else:
+                _wgrad(gRW, hpb, dzb)
+            copy_grad_(grads[grads_prefix + "b"], db)
+            return matmul(dzb, W.t()).reshape(T, mb, -1).permute(1, 2, 0), dh0, dc0
     h0 = torch.zeros(1, mb, H, device=dev) if cache["h0"] is None else _acc(cache["h0"]).reshape(1, mb, H)
     hprev = torch.cat([h0.to(out.dtype), out[:-1]], dim=0)
     peep_grads = None

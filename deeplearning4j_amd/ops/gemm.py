@@ -184,7 +184,10 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     bf16 output (conv -> BN fusion; 8-phase kernel).
     """
     if b.dtype != a.dtype:
-        b = b.to(a.dtype)
+        # mixed operands: compute in the 16-bit type (fp32 accumulation) rather than promoting to the exact-fp32 path
+        lo = [t for t in (a.dtype, b.dtype) if t in (torch.bfloat16, torch.float16)]
+        ct = lo[0] if lo and a.is_cuda else a.dtype
+        a, b = a.to(ct), b.to(ct)
     out_dtype = out.dtype if out is not None else (out_dtype or a.dtype)
     if not use_native(a, "gemm"):
         return _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z)

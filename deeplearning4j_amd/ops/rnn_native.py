@@ -233,3 +233,27 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
     return dz, dh0, dc0
 
 
+
+
+def lstm_bwd_prep(dz, out, h0, call, c0, peephole, dtype):
+    """One-launch LSTM backward glue (csrc/lstm_glue.hip): dz [T, mb, 4H] fp32, out / call [T, mb, H] fp32 (h_t,
+    c_t), h0 / c0 [mb, H] or None -> (dz in ``dtype`` [T*mb, 4H], h_{t-1} in ``dtype`` [T*mb, H], db [4H] fp32,
+    peephole grads [3, H] fp32). None when the dtype is not bf16/fp16."""
+    dt = {torch.bfloat16: 1, torch.float16: 2}.get(dtype)
+    if dt is None or dz.dtype != torch.float32 or out.dtype != torch.float32 or call.dtype != torch.float32:
+        return None
+    T, mb, G = dz.shape
+    H = G // 4
+    R = T * mb
+    lib = native.load()
+    native.register_sig("dl4j_lstm_bwd_prep", [c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_int, c_void_p])
+    dzb = torch.empty(R, G, dtype=dtype, device=dz.device)
+    hpb = torch.empty(R, H, dtype=dtype, device=dz.device)
+    db = torch.zeros(G, dtype=torch.float32, device=dz.device)
+    dpeep = torch.zeros(3, H, dtype=torch.float32, device=dz.device)
+    dzc, oc, cc = dz.contiguous(), out.contiguous(), call.contiguous()
+    h0f, c0f = _f32c(h0), _f32c(c0)
+    rc = lib.dl4j_lstm_bwd_prep(dt, _ptr(dzc), _ptr(oc), _ptr(h0f), _ptr(cc), _ptr(c0f), _ptr(dzb), _ptr(hpb), _ptr(db),
+                                _ptr(dpeep), R, mb, H, int(bool(peephole)), _stream())
+    _check(rc, "lstm_bwd_prep")
+    return dzb, hpb, db, dpeep
