@@ -476,22 +476,29 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     if _ok_act(x) and _ok_act(dy) and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
             _is_pointwise(1, 1, stride, pad4, dilation):
         shp = (tuple(x.shape), tuple(w.shape))
+        # scratch copies / buffers are made inside the candidates, i.e. only on the one timed call per shape
+        # (an unconditional clone of dx_accum here was a full-activation copy per conv per step)
+        def _acc_copy():
+            return dx_accum.clone() if dx_accum is not None else None
         if need_dx:
-            acc0 = dx_accum.clone() if dx_accum is not None else None
             gdx = _choose(("dx", shp, dx_accum is not None),
                           lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, True, False, False,
-                                              dx_accum=acc0, gemm_dx=True),
+                                              dx_accum=_acc_copy(), gemm_dx=True),
                           lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, True, False, False,
-                                              dx_accum=acc0, gemm_dx=False))
+                                              dx_accum=_acc_copy(), gemm_dx=False))
         if need_dw:
             K, C = w.shape[0], w.shape[1]
-            sw = torch.zeros((K, C, 1, 1), dtype=torch.float32, device=x.device)
-            sb = torch.zeros((K,), dtype=torch.float32, device=x.device) if need_db else None
+
+            def _sw():
+                return torch.zeros((K, C, 1, 1), dtype=torch.float32, device=x.device)
+
+            def _sb():
+                return torch.zeros((K,), dtype=torch.float32, device=x.device) if need_db else None
             gdw = _choose(("dw", shp, need_db),
-                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, sw, sb, True,
-                                              gemm_dw=True),
-                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, sw, sb, True,
-                                              gemm_dw=False))
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, _sw(), _sb(),
+                                              True, gemm_dw=True),
+                          lambda: _conv2d_bwd(x, w, dy, stride, pad4, dilation, False, True, need_db, _sw(), _sb(),
+                                              True, gemm_dw=False))
     return _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, grads_zeroed, dx_accum,
                        gdx, gdw)
 
