@@ -62,6 +62,12 @@ class CapturedTrainingStep:
         self.pool = torch.cuda.graph_pool_handle()
         native.prepare_graph_slots(plan, n.device, n.conf.iterationCount, n.conf.epochCount)
         torch.cuda.synchronize()
+        # no Python GC while capturing: a collected cycle that owns GPU resources (events, other pools' blocks,
+        # a previous network's buffers) would be released inside the capture and abort it
+        import gc
+        gc.collect()
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
         try:
             for slot in (0, 1):
                 n._bump_weight_version()           # every graph must contain its own weight-relayout kernels
@@ -75,6 +81,8 @@ class CapturedTrainingStep:
         finally:
             native.GRAPH_SLOT[0] = None
             n._capturing = False
+            if gc_was_enabled:
+                gc.enable()
         _ = plan
         return self.ok
 
