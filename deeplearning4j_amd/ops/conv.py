@@ -5,8 +5,9 @@ CudnnConvolutionHelper contract, CUDA:convolution/CudnnConvolutionHelper.java:29
 ``conv2d_backward(...)`` -> (dx, dw, db).  pad4 = (top, bottom, left, right) so Same mode's
 asymmetric padding is exact.
 
-GPU: bf16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_implicit_gemm.hip``) when the shape is
-supported, else the torch/MIOpen library path.  CPU: torch reference (fp32/fp64).
+GPU: bf16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_igemm.hip``) when the shape is supported; fp32 convs as
+im2col + the in-tree exact-fp32 MFMA GEMM; anything else takes the library path and is counted (ops/fallback.py).
+CPU: torch reference (fp32/fp64).
 """
 import torch
 import torch.nn.functional as F
@@ -19,12 +20,56 @@ def _sym(pad4):
     return pt == pb and pl == pr
 
 
+def _fp32_gemm_ok(x, groups):
+    return x.is_cuda and x.dtype == torch.float32 and groups == 1 and x.dim() == 4 and use_native(x, "conv")
+
+
+def _fp32_conv_fwd(x, w, b, stride, pad4, dilation):
+    """fp32 conv on the GPU without the library: im2col + the in-tree exact-fp32 MFMA GEMM (ops/gemm.py)."""
+    from .gemm import mmul
+    pt, pb, pl, pr = pad4
+    xp = F.pad(x, (pl, pr, pt, pb)) if any(pad4) else x
+    N, C, Hp, Wp = xp.shape
+    K, _, R, S = w.shape
+    OH = (Hp - dilation[0] * (R - 1) - 1) // stride[0] + 1
+    OW = (Wp - dilation[1] * (S - 1) - 1) // stride[1] + 1
+    cols = F.unfold(xp.contiguous(), (R, S), dilation=tuple(dilation), stride=tuple(stride))     # [N, CRS, L]
+    y = mmul(w.reshape(K, -1).to(torch.float32), cols)                                          # [N, K, L]
+    y = y.reshape(N, K, OH, OW)
+    if b is not None:
+        y = y + b.reshape(1, -1, 1, 1).to(y.dtype)
+    return y
+
+
+def _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+    from .gemm import mmul
+    pt, pb, pl, pr = pad4
+    xp = F.pad(x, (pl, pr, pt, pb)) if any(pad4) else x
+    N, C, Hp, Wp = xp.shape
+    K, _, R, S = w.shape
+    L = dy.shape[2] * dy.shape[3]
+    dy3 = dy.reshape(N, K, L).to(torch.float32).contiguous()
+    dx = dw = db = None
+    if need_dx:
+        dcols = mmul(w.reshape(K, -1).t().to(torch.float32), dy3)                                # [N, CRS, L]
+        dxp = F.fold(dcols, (Hp, Wp), (R, S), dilation=tuple(dilation), stride=tuple(stride))
+        dx = dxp[:, :, pt:pt + x.shape[2], pl:pl + x.shape[3]] if any(pad4) else dxp
+    if need_dw:
+        cols = F.unfold(xp.contiguous(), (R, S), dilation=tuple(dilation), stride=tuple(stride))
+        dw = mmul(dy3.permute(1, 0, 2).reshape(K, N * L), cols.permute(0, 2, 1).reshape(N * L, -1)).reshape(w.shape)
+    if need_db:
+        db = dy3.sum((0, 2))
+    return dx, dw, db
+
+
 def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1, want_stats=False):
     if use_native(x, "conv") and groups == 1:
         from . import native
         y = native.conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats)
         if y is not None:
             return y
+    if _fp32_gemm_ok(x, groups):
+        return _fp32_conv_fwd(x, w, b, stride, pad4, dilation)
     from .fallback import note
     note(x, "conv", f"fwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4
@@ -46,6 +91,8 @@ def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_
                                grads_zeroed, dx_accum)
         if r is not None:
             return r
+    if _fp32_gemm_ok(x, groups):
+        return _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
     from .fallback import note
     note(x, "conv", f"bwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4

@@ -15,6 +15,15 @@ def pool2d_forward(x, ptype, kernel, stride, pad4, dilation=(1, 1), pnorm=2, eps
     pt, pb, pl, pr = pad4
     if use_native(x, "pool") and ptype in ("MAX", "AVG") and tuple(dilation) == (1, 1):
         from . import native
+        C = x.shape[1] if x.dim() == 4 else 0
+        if x.dim() == 4 and C % 8:
+            # channel counts off the 8-wide vector (LeNet's 20 / 50): zero-padded channels through the same kernel
+            from .conv_native import _pad_ch, _r8
+            r = native.pool2d_fwd(_pad_ch(x.contiguous(memory_format=torch.channels_last), _r8(C), cl=True),
+                                  ptype, kernel, stride, pad4)
+            if r is not None:
+                y, ctx = r
+                return y[:, :C].contiguous(memory_format=torch.channels_last), ("PADC", C, ctx)
         r = native.pool2d_fwd(x, ptype, kernel, stride, pad4)
         if r is not None:
             return r
@@ -40,6 +49,11 @@ def pool2d_forward(x, ptype, kernel, stride, pad4, dilation=(1, 1), pnorm=2, eps
 
 def pool2d_backward(dy, ctx):
     kind = ctx[0]
+    if kind == "PADC":
+        from .conv_native import _pad_ch, _r8
+        C, inner = ctx[1], ctx[2]
+        dx = pool2d_backward(_pad_ch(dy.contiguous(memory_format=torch.channels_last), _r8(C), cl=True), inner)
+        return dx[:, :C].contiguous(memory_format=torch.channels_last)
     if kind == "NATIVE":
         from . import native
         return native.pool2d_bwd(dy, ctx)

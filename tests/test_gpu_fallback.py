@@ -48,3 +48,24 @@ def test_textgen_lstm_bf16_step_has_no_fallbacks():
     fallback.reset()
     net.fit(x, y)
     _assert_clean(net, "TextGenerationLSTM bf16")
+
+
+def test_lenet_fp32_gpu_no_fallbacks_and_matches_cpu():
+    """fp32 on the GPU never reaches the library conv: im2col + the exact-fp32 MFMA GEMM (ops/conv.py), fp32 pooling /
+    dense / softmax-xent kernels; a few SGD steps match the CPU run of the same network."""
+    from deeplearning4j_amd.models import LeNet
+    from deeplearning4j_amd.nn.conf import DataType
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(16, 1, 28, 28, generator=g)
+    y = torch.nn.functional.one_hot(torch.randint(0, 10, (16,), generator=g), 10).float()
+    nets = {}
+    for dev in ("cpu", "cuda"):
+        net = LeNet(numLabels=10, inputShape=[1, 28, 28], dataType=DataType.FLOAT).init(device=dev)
+        fallback.reset()
+        for _ in range(3):
+            net.fit(x.to(dev), y.to(dev))
+        if dev == "cuda":
+            _assert_clean(net, "LeNet fp32")
+        nets[dev] = net
+    pc, pg = nets["cpu"].params().cpu(), nets["cuda"].params().cpu()
+    assert torch.allclose(pc, pg, rtol=1e-3, atol=1e-4), (pc - pg).abs().max()
