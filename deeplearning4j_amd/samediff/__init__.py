@@ -496,10 +496,11 @@ class SameDiff:
         n = sum(v.value.numel() for v in vs)
         mdt = torch.float64 if all(v.value.dtype == torch.float64 for v in vs) else torch.float32
         flat = torch.empty(n, dtype=mdt, device=dev)
-        # bf16 variables train in mixed precision: fp32 master weights, the fused updater writes the bf16 copy the
-        # graph computes with (its "shadow") in the same pass
-        mixed = all(v.value.dtype == torch.bfloat16 for v in vs)
-        shadow = torch.empty(n, dtype=torch.bfloat16, device=dev) if mixed else None
+        # bf16 / fp16 variables train in mixed precision: fp32 master weights, the fused updater writes the 16-bit
+        # copy the graph computes with (its "shadow") in the same pass
+        lowp = vs[0].value.dtype
+        mixed = lowp in (torch.bfloat16, torch.float16) and all(v.value.dtype == lowp for v in vs)
+        shadow = torch.empty(n, dtype=lowp, device=dev) if mixed else None
         segs, off = [], 0
         for v in vs:
             k = v.value.numel()
@@ -542,30 +543,145 @@ class SameDiff:
                 feeds.update({n: _tensor(t).to(st["flat"].device) for n, t in
                               zip(cfg.dataSetLabelMapping, labs)})
                 with torch.no_grad():
-                    self._exec(feeds, self._loss_names)
-                    seeds = {n: torch.full_like(self.variables[n].value, sign) for n in self._loss_names}
-                    grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
-                    if "views" not in st:
-                        off, st["views"] = 0, []
-                        for v in vs:
-                            st["views"].append(st["grad"][off:off + v.value.numel()].view(v.value.shape))
-                            off += v.value.numel()
-                    dst, src = [], []
-                    for v, view in zip(vs, st["views"]):
-                        g = grads.get(v.name)
-                        if g is None:
-                            view.zero_()
-                        else:
-                            dst.append(view)
-                            src.append(g.reshape(view.shape))
-                    torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
-                    fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount,
-                                 self.epochCount, 1, mini_batch=False, shadow=st["shadow"])
-                    loss = sum(float(self.variables[n].value.float()) for n in self._loss_names)
+                    if self._graph_ready(feeds):
+                        loss = self._graph_replay(feeds)
+                    else:
+                        loss_t = self._train_body(feeds, sign)
+                        loss = float(loss_t)
+                        self._eager_steps += 1
                 self.iterationCount += 1
                 last = loss
             self.epochCount += 1
         return last
+
+    def _train_body(self, feeds, sign):
+        """One training iteration's device work: forward, reverse pass, gradient copy into the flat buffer,
+        cross-rank all-reduce, fused update. Returns the summed loss as a device tensor (capturable)."""
+        from ..ops.update import fused_update
+        st = self._train_state
+        vs = self.trainableVariables()
+        self._exec(feeds, self._loss_names)
+        seeds = {n: torch.full_like(self.variables[n].value, sign) for n in self._loss_names}
+        grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
+        if "views" not in st:
+            off, st["views"] = 0, []
+            for v in vs:
+                st["views"].append(st["grad"][off:off + v.value.numel()].view(v.value.shape))
+                off += v.value.numel()
+        dst, src = [], []
+        for v, view in zip(vs, st["views"]):
+            g = grads.get(v.name)
+            if g is None:
+                view.zero_()
+            else:
+                dst.append(view)
+                src.append(g.reshape(view.shape))
+        torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
+        self._allreduce(st)
+        fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount, self.epochCount, 1,
+                     mini_batch=False, shadow=st["shadow"])
+        out = None
+        for n in self._loss_names:
+            v = self.variables[n].value.float().reshape(())
+            out = v if out is None else out + v
+        return out
+
+    # ------------------------------------------------------------------ HIP graphs
+    def enableHipGraphs(self, enabled=True, warmup=2):
+        """Capture the training iteration into HIP graphs after ``warmup`` eager steps (fixed placeholder shapes,
+        CUDA variables, no gloo all-reduce): two graphs A/B alternate so the fused updater's iteration-dependent
+        table (pinned buffer + graph H2D node) is refreshed without a host sync, as nn/hipgraph.py does for
+        networks. The whole step - every op's forward and explicit backward, the gradient copy, RCCL all-reduce
+        and the update - replays with one launch."""
+        self._graphs_on = bool(enabled)
+        self._graph_warmup = int(warmup)
+        self._graph = None
+        return self
+
+    _graphs_on = False
+    _graph = None
+    _eager_steps = 0
+
+    def _graph_eligible(self, feeds):
+        import torch.distributed as dist
+        if not self._graphs_on or not all(t.is_cuda for t in feeds.values()):
+            return False
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 and \
+                dist.get_backend() != "nccl":
+            return False
+        return self._train_state["flat"].is_cuda
+
+    def _graph_ready(self, feeds):
+        if not self._graph_eligible(feeds):
+            return False
+        g = self._graph
+        if g is not None:
+            return g["ok"] and all(feeds[k].shape == g["static"][k].shape and feeds[k].dtype == g["static"][k].dtype
+                                   for k in feeds)
+        if self._eager_steps < self._graph_warmup:
+            return False
+        return self._graph_capture(feeds)
+
+    def _graph_capture(self, feeds):
+        import gc
+        from ..ops import native
+        st = self._train_state
+        sign = 1.0 if self.trainingConfig.minimize else -1.0
+        static = {k: v.detach().clone() for k, v in feeds.items()}
+        g = {"static": static, "graphs": [], "loss": [None, None], "k": 0, "ok": False,
+             "pool": torch.cuda.graph_pool_handle()}
+        native.prepare_graph_slots(st["plan"], st["flat"].device, self.iterationCount, self.epochCount)
+        torch.cuda.synchronize()
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            for slot in (0, 1):
+                cg = torch.cuda.CUDAGraph()
+                native.GRAPH_SLOT[0] = slot
+                with torch.cuda.graph(cg, pool=g["pool"]):
+                    g["loss"][slot] = self._train_body(static, sign)
+                g["graphs"].append(cg)
+            g["ok"] = True
+        except Exception as e:          # capture not possible for this graph: stay eager
+            import logging
+            logging.getLogger("deeplearning4j_amd").warning("SameDiff HIP-graph capture failed, eager steps: %s", e)
+            g["ok"] = False
+        finally:
+            native.GRAPH_SLOT[0] = None
+            if was:
+                gc.enable()
+        self._graph = g                 # (capture only records: parameters are untouched until the first replay)
+        return g["ok"]
+
+    def _graph_replay(self, feeds):
+        from ..ops import native
+        g = self._graph
+        st = self._train_state
+        for k, v in feeds.items():
+            g["static"][k].copy_(v, non_blocking=True)
+        slot = g["k"] & 1
+        native.refresh_graph_table(st["plan"], slot, self.iterationCount, self.epochCount)
+        g["graphs"][slot].replay()
+        native.mark_graph_replayed(st["plan"], slot)
+        g["k"] += 1
+        return float(g["loss"][slot])
+
+    def _allreduce(self, st):
+        """Data parallel (one process per GPU, torch.distributed over RCCL / gloo): average the flat fp32 gradient
+        across ranks in buckets before the fused update, so every rank applies the same step (the reference's
+        ParallelWrapper gradient sharing for SameDiff graphs). Bucket size: DL4J_AMD_BUCKET_MB (default 64 MB,
+        large buckets for xGMI rings)."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        import os
+        g = st["grad"]
+        world = dist.get_world_size()
+        step = max(1, int(float(os.environ.get("DL4J_AMD_BUCKET_MB", "64")) * (1 << 20)) // g.element_size())
+        for off in range(0, g.numel(), step):
+            dist.all_reduce(g[off:off + step])
+        g.div_(world)
 
     # ------------------------------------------------------------------ save / load
     def save(self, path, saveUpdaterState=False):

@@ -203,3 +203,44 @@ def run_cg_shared(rank, world, port, result_path):
         torch.save({"params": [t.clone() for t in gathered], "nbuckets": len(pw.accumulator._buckets)}, result_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def make_samediff(seed=4):
+    from deeplearning4j_amd import Sgd
+    from deeplearning4j_amd.samediff import SameDiff, TrainingConfig
+    g = torch.Generator().manual_seed(seed)
+    sd = SameDiff.create()
+    x = sd.placeHolder("x", torch.zeros(4, 6))
+    y = sd.placeHolder("y", torch.zeros(4, 3))
+    w0 = sd.var("w0", torch.randn(6, 8, generator=g) * 0.4)
+    b0 = sd.var("b0", torch.zeros(8))
+    w1 = sd.var("w1", torch.randn(8, 3, generator=g) * 0.4)
+    h = sd.nn().tanh(sd.nn().linear(x, w0, b0))
+    sd.loss().softmaxCrossEntropy("loss", y, h.mmul(w1))
+    sd.setTrainingConfig(TrainingConfig.builder().updater(Sgd(0.2)).dataSetFeatureMapping("x")
+                         .dataSetLabelMapping("y").build())
+    return sd
+
+
+def samediff_batches(n=5, bs=8, seed=9):
+    from deeplearning4j_amd import DataSet
+    g = torch.Generator().manual_seed(seed)
+    return [DataSet(torch.randn(bs, 6, generator=g),
+                    torch.nn.functional.one_hot(torch.randint(0, 3, (bs,), generator=g), 3).float()) for _ in range(n)]
+
+
+def run_samediff_dp(rank, world, port, result_path):
+    """SameDiff fit with the flat gradient all-reduced across ranks (samediff.SameDiff._allreduce)."""
+    _setup(rank, world, port)
+    from deeplearning4j_amd import DataSet
+    sd = make_samediff()
+    for ds in samediff_batches():
+        h = ds.features.shape[0] // world
+        sd.fit(DataSet(ds.features[rank * h:(rank + 1) * h], ds.labels[rank * h:(rank + 1) * h]))
+    p = torch.cat([v.value.reshape(-1) for v in sd.trainableVariables()])
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        torch.save({"params": [t.clone() for t in gathered]}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -83,3 +83,36 @@ def test_samediff_cnn_bf16_gpu_matches_fp64(cuda):
     g64 = sd64.execBackwards(loss64)
     for k in g64:
         assert _rel(gg[k], g64[k]) < 1e-1, (k, _rel(gg[k], g64[k]))
+
+
+def test_samediff_fit_hip_graph_matches_eager(cuda):
+    """sd.enableHipGraphs(): the captured step (every op's forward + explicit backward, gradient copy, fused Adam with
+    its iteration-dependent bias correction through the A/B graph tables) gives the same parameters as eager fits."""
+    from deeplearning4j_amd import Adam, DataSet
+    from deeplearning4j_amd.samediff import TrainingConfig
+    g = torch.Generator().manual_seed(0)
+    B, T, E, C = 4, 64, 128, 8
+    base = {"x": torch.randn(B, T, E, generator=g), "wqkv": torch.randn(E, 3 * E, generator=g) * E ** -0.5,
+            "bqkv": torch.randn(3 * E, generator=g) * 0.02, "wo": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bo": torch.zeros(E), "g": 1 + 0.1 * torch.randn(E, generator=g), "b": 0.1 * torch.randn(E, generator=g),
+            "wc": torch.randn(E, C, generator=g) * E ** -0.5, "wf": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bf": 0.02 * torch.randn(E, generator=g),
+            "y": torch.nn.functional.one_hot(torch.randint(0, C, (B,), generator=g), C).float()}
+    data = [DataSet(torch.randn(B, T, E, generator=g).to(cuda, torch.bfloat16),
+                    torch.nn.functional.one_hot(torch.randint(0, C, (B,), generator=g), C).to(cuda, torch.bfloat16))
+            for _ in range(6)]
+    res = []
+    for graphs in (False, True):
+        sd, loss = _transformer_block(cuda, torch.bfloat16, base)
+        sd.setTrainingConfig(TrainingConfig.builder().updater(Adam(1e-3)).dataSetFeatureMapping("x")
+                             .dataSetLabelMapping("y").build())
+        if graphs:
+            sd.enableHipGraphs(True, warmup=2)
+        losses = [sd.fit(ds) for ds in data]
+        torch.cuda.synchronize()
+        if graphs:
+            assert sd._graph is not None and sd._graph["ok"] and sd._graph["k"] == 4
+        res.append((losses, torch.cat([sd._train_state["flat"]])))
+    (l0, p0), (l1, p1) = res
+    assert all(abs(a - b) < 1e-3 * max(1.0, abs(a)) for a, b in zip(l0, l1)), (l0, l1)
+    assert torch.allclose(p0, p1, atol=1e-4), (p0 - p1).abs().max()

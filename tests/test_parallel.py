@@ -198,3 +198,17 @@ def test_cg_shared_gradients_bucketed_equals_large_batch(tmp_path):
     for i in range(0, 6, 2):
         net.fit(DataSet(torch.cat([b[i].features, b[i + 1].features]), torch.cat([b[i].labels, b[i + 1].labels])))
     assert torch.allclose(net.params(), p0, atol=1e-5), (net.params() - p0).abs().max()
+
+
+def test_samediff_data_parallel_equals_large_batch(tmp_path):
+    """SameDiff DP-2 (gloo): each rank fits half of every batch, gradients averaged across ranks before the fused
+    update == one process fitting the whole batch."""
+    path = str(tmp_path / "sd.pt")
+    mp.spawn(W.run_samediff_dp, args=(2, _port(), path), nprocs=2, join=True)
+    p0, p1 = torch.load(path, weights_only=True)["params"]
+    assert torch.equal(p0, p1)
+    sd = W.make_samediff()
+    for ds in W.samediff_batches():
+        sd.fit(ds)
+    ref = torch.cat([v.value.reshape(-1) for v in sd.trainableVariables()])
+    assert torch.allclose(ref, p0, atol=1e-5), (ref - p0).abs().max()
