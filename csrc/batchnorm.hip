@@ -185,7 +185,49 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
   const int T8 = C >> 3;
   const float* scale = ctx + 2 * C;
   const float* shift = ctx + 3 * C;
-  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long v0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (stride % T8 == 0) {
+    // every grid-stride step keeps this thread on the same 8 channels: per-channel factors live in registers and
+    // two independent vectors are in flight per iteration (instead of 16 L1 parameter loads per 16-byte vector)
+    const int c0 = idx_mod(v0, T8) * 8;
+    float sc[8], sf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+    long long v = v0;
+    for (; v + stride < nvec; v += 2 * stride) {
+      float a[2][8], r[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        Vec8<T>::load(x + (v + u * stride) * 8, a[u]);
+        if (RES) Vec8<T>::load(res + (v + u * stride) * 8, r[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float t = a[u][i] * sc[i] + sf[i];
+          if (RES) t += r[u][i];
+          a[u][i] = RELU ? fmaxf(t, 0.f) : t;
+        }
+        Vec8<T>::store(y + (v + u * stride) * 8, a[u]);
+      }
+    }
+    if (v < nvec) {
+      float a[8], r[8];
+      Vec8<T>::load(x + v * 8, a);
+      if (RES) Vec8<T>::load(res + v * 8, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float t = a[i] * sc[i] + sf[i];
+        if (RES) t += r[i];
+        a[i] = RELU ? fmaxf(t, 0.f) : t;
+      }
+      Vec8<T>::store(y + v * 8, a);
+    }
+    return;
+  }
+  for (long long v = v0; v < nvec; v += stride) {
     const int c0 = idx_mod(v, T8) * 8;
     float a[8], r[8];
     Vec8<T>::load(x + v * 8, a);
@@ -282,6 +324,20 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__
   cdg[c] = (float)(b / (double)M);
 }
 
+// one dx/dres element: d = relu'(.)*dy; dx = gamma*invstd*(d - mean(d) - xhat*mean(d*xhat)) written as
+// dx = A*d - B*x - Cq with per-channel A = scale (= gamma*invstd), B = scale*invstd*cdg, Cq = scale*(cdb - mean*invstd*cdg)
+template <bool RELU, bool RES>
+__device__ __forceinline__ void bn_bwd_elem(float& xv, float& gv, float& rv, float A, float B, float Cq, float sf) {
+  float d = gv;
+  if (RELU) {
+    float t = xv * A + sf;
+    if (RES) t += rv;
+    d = t > 0.f ? d : 0.f;
+  }
+  if (RES) rv = d;
+  xv = A * d - B * xv - Cq;
+}
+
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                     const T* __restrict__ dy, T* __restrict__ dx, T* __restrict__ dres,
@@ -290,26 +346,58 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
   const float *mean = ctx, *invstd = ctx + C, *scale = ctx + 2 * C, *shift = ctx + 3 * C;
-  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (long long)gridDim.x * blockDim.x) {
-    const int c0 = idx_mod(v, T8) * 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long v0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool fixed = stride % T8 == 0;   // the thread's channel group never changes: factors in registers
+  float A[8], B[8], Cq[8], sf[8];
+  if (fixed) {
+    const int c0 = idx_mod(v0, T8) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      A[i] = scale[c];
+      B[i] = scale[c] * invstd[c] * cdg[c];
+      Cq[i] = scale[c] * (cdb[c] - mean[c] * invstd[c] * cdg[c]);
+      sf[i] = shift[c];
+    }
+  }
+  long long v = v0;
+  if (fixed) {
+    for (; v + stride < nvec; v += 2 * stride) {   // two independent vectors in flight
+      float xv[2][8], gv[2][8], rv[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        Vec8<T>::load(x + (v + u * stride) * 8, xv[u]);
+        Vec8<T>::load(dy + (v + u * stride) * 8, gv[u]);
+        if (RES) Vec8<T>::load(res + (v + u * stride) * 8, rv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bn_bwd_elem<RELU, RES>(xv[u][i], gv[u][i], rv[u][i], A[i], B[i], Cq[i], sf[i]);
+        Vec8<T>::store(dx + (v + u * stride) * 8, xv[u]);
+        if (RES) Vec8<T>::store(dres + (v + u * stride) * 8, rv[u]);
+      }
+    }
+  }
+  for (; v < nvec; v += stride) {
+    if (!fixed) {
+      const int c0 = idx_mod(v, T8) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = c0 + i;
+        A[i] = scale[c];
+        B[i] = scale[c] * invstd[c] * cdg[c];
+        Cq[i] = scale[c] * (cdb[c] - mean[c] * invstd[c] * cdg[c]);
+        sf[i] = shift[c];
+      }
+    }
     float xv[8], gv[8], rv[8];
     Vec8<T>::load(x + v * 8, xv);
     Vec8<T>::load(dy + v * 8, gv);
     if (RES) Vec8<T>::load(res + v * 8, rv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      float d = gv[i];
-      if (RELU) {
-        float t = xv[i] * scale[c] + shift[c];
-        if (RES) t += rv[i];
-        d = t > 0.f ? d : 0.f;
-      }
-      if (RES) rv[i] = d;
-      const float xh = (xv[i] - mean[c]) * invstd[c];
-      // dx = gamma*invstd * (dy' - mean(dy') - xhat*mean(dy'*xhat)); gamma*invstd == scale
-      xv[i] = scale[c] * (d - cdb[c] - xh * cdg[c]);
-    }
+    for (int i = 0; i < 8; ++i) bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i]);
     Vec8<T>::store(dx + v * 8, xv);
     if (RES) Vec8<T>::store(dres + v * 8, rv);
   }

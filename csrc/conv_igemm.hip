@@ -555,15 +555,21 @@ DL4J_API void dl4j_conv_set_variant(int v) { g_fwd_variant = v; }
 
 __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                               float* __restrict__ dW, float* __restrict__ db,
-                                                              ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH) {
+                                                              ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH,
+                                                              int remap) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_K * WRW_ROW];   // 2 buffers x (A + B) = 40 KB
   const int M = g.N * g.OH * g.OW;
   const int Kout = g.K;
   const int RSC = g.R * g.S * g.C;
   const int tiles_k = (Kout + TILE_N - 1) / TILE_N;
-  const int tk = blockIdx.x % tiles_k, tj = blockIdx.x / tiles_k;
+  // XCD-aware order: logical ids are contiguous per XCD and tile-fastest, so every (k, j) tile of one pixel split
+  // runs on the same XCD and the split's dY/X rows are fetched into one L2 instead of one per tile.
+  const int hbid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int lbid = remap ? xcd_remap(hbid, gridDim.x * gridDim.y) : hbid;
+  const int tile = lbid % gridDim.x, split = lbid / gridDim.x;
+  const int tk = tile % tiles_k, tj = tile / tiles_k;
   const int k0 = tk * TILE_N, j0 = tj * TILE_M;
-  const int mbeg = blockIdx.y * m_per_split;
+  const int mbeg = split * m_per_split;
   int mend = mbeg + m_per_split;
   if (mend > M) mend = M;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -719,15 +725,21 @@ __device__ __forceinline__ int wrw_addr(int row, int col) {
 
 __global__ __launch_bounds__(NTHREADS) void igemm_wrw_glds(const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                             float* __restrict__ dW, float* __restrict__ db,
-                                                            ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH) {
+                                                            ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH,
+                                                            int remap) {
   __shared__ __attribute__((aligned(16))) char smem[G_STAGES * G_STAGE_BYTES];   // 4 x (8 KB + 8 KB)
   const int M = g.N * g.OH * g.OW;
   const int Kout = g.K;
   const int RSC = g.R * g.S * g.C;
   const int tiles_k = (Kout + TILE_N - 1) / TILE_N;
-  const int tk = blockIdx.x % tiles_k, tj = blockIdx.x / tiles_k;
+  // XCD-aware order: logical ids are contiguous per XCD and tile-fastest, so every (k, j) tile of one pixel split
+  // runs on the same XCD and the split's dY/X rows are fetched into one L2 instead of one per tile.
+  const int hbid = blockIdx.x + blockIdx.y * gridDim.x;
+  const int lbid = remap ? xcd_remap(hbid, gridDim.x * gridDim.y) : hbid;
+  const int tile = lbid % gridDim.x, split = lbid / gridDim.x;
+  const int tk = tile % tiles_k, tj = tile / tiles_k;
   const int k0 = tk * TILE_N, j0 = tj * TILE_M;
-  const int mbeg = blockIdx.y * m_per_split;
+  const int mbeg = split * m_per_split;
   int mend = mbeg + m_per_split;
   if (mend > M) mend = M;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -842,6 +854,8 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_glds(const bf16* __restric
 
 static int g_wrw_variant = 0;   // v1 register-staged measured faster here (occupancy); v2 kept for A/B
 DL4J_API void dl4j_conv_set_wrw_variant(int v) { g_wrw_variant = v; }
+static int g_wrw_remap = 1;     // 1 = XCD-aware block order (all tiles of a pixel split on one XCD), 0 = launch order
+DL4J_API void dl4j_conv_set_wrw_remap(int v) { g_wrw_remap = v; }
 
 // ------------------------------------------------------------------------------------------------------
 // Weight relayout (bf16): W[K][C][R][S] -> Wkrsc[K][R][S][C]  and  Wflip[C][R][S][K] = W[k][c][R-1-r][S-1-s]
@@ -1016,9 +1030,9 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
   splits = (M + mps - 1) / mps;
   if (g_wrw_variant == 1)
     hipLaunchKernelGGL(igemm_wrw_glds, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
-                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
+                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH), g_wrw_remap);
   else
     hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
-                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH));
+                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH), g_wrw_remap);
   return (int)hipGetLastError();
 }

@@ -31,6 +31,7 @@ native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [
 native.register_sig("dl4j_conv_wrw", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 16 + [c_void_p])
 native.register_sig("dl4j_conv_set_variant", [c_int])
 native.register_sig("dl4j_conv_set_wrw_variant", [c_int])
+native.register_sig("dl4j_conv_set_wrw_remap", [c_int])
 native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p])
 
 # Optional per-shape override of the weight-gradient split count (tuning): {(N,H,W,C,K,R,S,stride): splits}
@@ -59,6 +60,11 @@ def set_kernel_variant(v):
 def set_wrw_variant(v):
     """0 = register-staged weight-gradient kernel (default), 1 = LDS-DMA pipelined variant."""
     native.load().dl4j_conv_set_wrw_variant(int(v))
+
+
+def set_wrw_remap(v):
+    """1 = XCD-aware weight-gradient block order (default), 0 = plain launch order (A/B only)."""
+    native.load().dl4j_conv_set_wrw_remap(int(v))
 
 
 def bump_version():
@@ -355,7 +361,7 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
             if not (directb and grads_zeroed):
                 dbt.zero_()
-        splits = WRW_SPLITS.get((N, H, W, C, K, R, S, tuple(stride)), 0)
+        splits = _wrw_splits(lib, x, dy, ws, dbt, N, H, W, C, K, R, S, stride, pad4, dilation, OH, OW)
         rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
                                pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits, _stream())
         native._check(rc, "conv_wrw")
@@ -366,6 +372,37 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
         if need_db:
             db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
     return dx, dW_out, db_out
+
+
+def _wrw_default_splits(M, K, RSC):
+    """Mirror of dl4j_conv_wrw's split heuristic (~1.5 workgroups per CU, >= 8 k-steps per split)."""
+    tiles = ((K + 127) // 128) * ((RSC + 127) // 128)
+    maxs = max(1, (M + 8 * 32 - 1) // (8 * 32))
+    return max(1, min((384 + tiles - 1) // tiles, maxs)), maxs
+
+
+def _wrw_splits(lib, x, dy, ws, dbt, N, H, W, C, K, R, S, stride, pad4, dilation, OH, OW):
+    """Per-shape pixel-split count of the weight-gradient kernel. The first eager call of a shape times the heuristic
+    count and its neighbours (x0.5, x2, x4: fill vs fp32-atomic epilogue traffic trade differently per shape) on a
+    scratch accumulator and keeps the fastest; graph-captured calls use the remembered value (heuristic if none)."""
+    key = (N, H, W, C, K, R, S, tuple(stride))
+    sp = WRW_SPLITS.get(key)
+    if sp is not None:
+        return sp
+    if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
+        return 0
+    s0, maxs = _wrw_default_splits(N * OH * OW, K, R * S * C)
+    cands = sorted({c for c in (s0 // 2, s0, 2 * s0, 4 * s0) if 1 <= c <= maxs})
+    scratch = torch.zeros_like(ws)
+    sdb = torch.zeros_like(dbt) if dbt is not None else None
+
+    def run(c):
+        return lambda: native._check(
+            lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(scratch), _ptr(sdb), N, H, W, C, K, R, S, stride[0], stride[1],
+                              pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, c, _stream()), "conv_wrw")
+    best = min(cands, key=lambda c: _timed(run(c), reps=3))
+    WRW_SPLITS[key] = best
+    return best
 
 
 GEMM_1X1 = os.environ.get("DL4J_AMD_CONV1X1_GEMM", "1") == "1"

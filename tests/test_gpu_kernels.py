@@ -25,7 +25,10 @@ def test_native_library_loaded(cuda):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("shape", [(4, 64, 9, 7), (2, 256, 5, 5), (3, 2048, 2, 2), (16, 24)])
+@pytest.mark.parametrize("shape", [(4, 64, 9, 7), (2, 256, 5, 5), (3, 2048, 2, 2), (16, 24),
+                                   # grid-capped sizes: several grid-stride steps (register-resident factors,
+                                   # two vectors per step + tail) and an odd channel-group count (factors reloaded)
+                                   (200, 64, 32, 32), (500000, 24)])
 def test_batchnorm_fwd_bwd(cuda, dtype, relu, shape):
     g = torch.Generator().manual_seed(0)
     x = (torch.randn(*shape, generator=g) * 3 + 1.5)
@@ -150,9 +153,9 @@ def test_lenet_gpu_matches_cpu(cuda):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_batchnorm_residual_relu_fused(cuda, dtype):
+@pytest.mark.parametrize("shape", [(4, 64, 6, 5), (200, 64, 32, 32)])
+def test_batchnorm_residual_relu_fused(cuda, dtype, shape):
     g = torch.Generator().manual_seed(7)
-    shape = (4, 64, 6, 5)
     x = (torch.randn(*shape, generator=g) * 2 + 0.5).to(dtype)
     r = torch.randn(*shape, generator=g).to(dtype)
     dy = torch.randn(*shape, generator=g).to(dtype)
@@ -167,8 +170,14 @@ def test_batchnorm_residual_relu_fused(cuda, dtype):
     dx, dgm, dbt, dr = ops.bn_backward(cl(dy), c)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     _close(y, y_ref, tol)
-    _close(dx, dx_ref, 2 * tol)
-    _close(dr, dr_ref, tol)
+    # the kernel recomputes the ReLU pre-activation x*scale+shift+res; among millions of elements a few sit within
+    # rounding of 0 and may take the other side of the mask than the reference, so those are left out of dx / dres
+    _, xc, mu, istd, gm, bt = c_ref[:6]
+    pre = (xc.float() - mu.reshape(1, -1, 1, 1)) * istd.reshape(1, -1, 1, 1) * gm.reshape(1, -1, 1, 1) \
+        + bt.reshape(1, -1, 1, 1) + r.float()
+    keep = (pre.abs() > 1e-3).float()
+    _close(dx.float().cpu() * keep, dx_ref.float() * keep, 2 * tol)
+    _close(dr.float().cpu() * keep, dr_ref.float() * keep, tol)
     _close(dgm, dg_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)
     _close(dbt, db_ref, 3e-2 if dtype == torch.bfloat16 else 1e-3)
 

@@ -23,9 +23,9 @@ def capture_shapes(variant):
     shapes = []
     orig = ops.conv.conv2d_forward
 
-    def hook(x, w, b, stride, pad4, dilation=(1, 1), groups=1):
+    def hook(x, w, b, stride, pad4, dilation=(1, 1), groups=1, **kw):
         shapes.append((tuple(x.shape[1:]), tuple(w.shape), tuple(stride), tuple(pad4), tuple(dilation)))
-        return orig(x, w, b, stride, pad4, dilation, groups)
+        return orig(x, w, b, stride, pad4, dilation, groups, **kw)
     import deeplearning4j_amd.nn.layers.convolution as lc
     lc.ops.conv2d_forward = hook
     try:
