@@ -362,6 +362,7 @@ class ComputationGraph(BaseNetwork):
                 es = v.backward(e_in, self._ctx[name][1])
                 for i, ei in zip(self.vertex_inputs[name], es):
                     add(i, ei)
+        self._end_backward()
         for l in self.listeners:
             if hasattr(l, "onBackwardPass"):
                 l.onBackwardPass(self)

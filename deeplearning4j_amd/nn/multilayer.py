@@ -172,6 +172,7 @@ class MultiLayerNetwork(BaseNetwork):
             self._grad_ready(i)
             if eps is None:
                 break
+        self._end_backward()
         for l in self.listeners:
             if hasattr(l, "onBackwardPass"):
                 l.onBackwardPass(self)

@@ -349,10 +349,18 @@ class BaseNetwork:
         acc = getattr(self, "gradientsAccumulator", None)
         if acc is not None and hasattr(acc, "begin_backward"):
             acc.begin_backward(self)
+        from ..ops import side_stream
+        side_stream.begin(self.flattenedGradients)   # conv weight gradients overlap the rest of the reverse pass
+
+    def _end_backward(self):
+        from ..ops import side_stream
+        side_stream.end()
 
     def _grad_ready(self, key):
         acc = getattr(self, "gradientsAccumulator", None)
         if acc is not None and hasattr(acc, "grad_ready"):
+            from ..ops import side_stream
+            side_stream.join()                      # the bucket reads gradients the side stream may still write
             acc.grad_ready(self, self._offset_of.get(key, 0))
 
     def setGradientsAccumulator(self, acc):
@@ -381,6 +389,8 @@ class BaseNetwork:
     def _apply_update_kernels(self, batch_size):
         """The device work of an update (fused updater + score's regularisation term + constraints); no host
         bookkeeping, so it can be captured into a HIP graph."""
+        from ..ops import side_stream
+        side_stream.end()                           # a pass that raised mid-way must not leave dW launches unjoined
         it, ep = self.conf.iterationCount, self.conf.epochCount
         acc = getattr(self, "gradientsAccumulator", None)
         mb_local = batch_size

@@ -18,7 +18,7 @@ import torch
 
 from ..memory import arena
 
-from . import native
+from . import native, side_stream
 from .native import _ptr, _stream, c_int, c_ll, c_void_p
 
 native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
@@ -44,7 +44,9 @@ _wrw_ws = {}   # (K, R, S, C, device) -> fp32 KRSC accumulation workspace, kept 
 
 
 def _zeroed_wrw_ws(K, R, S, C, device):
-    key = (K, R, S, C, str(device))
+    # keyed by stream too: weight gradients on the overlap stream (ops/side_stream.py) and on the main stream must
+    # never share an accumulator
+    key = (K, R, S, C, str(device), torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0)
     ws = _wrw_ws.get(key)
     if ws is None:
         ws = torch.zeros((K, R, S, C), dtype=torch.float32, device=device)
@@ -329,8 +331,26 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
                                                            False, [0, 0], 1, [True, False, False])
             if not sym:
                 dx = dx[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W]
+    if not need_dw:
+        return dx, None, None
+    directw = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
+    directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+    if directw and (directb or not need_db) and side_stream.active():
+        # dW only writes the persistent fp32 gradient views: run it on the overlap stream next to dX
+        side_stream.run(lambda: _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW,
+                                            gb, grads_zeroed, pw and gemm_dw), x, dy)
+        return dx, None, None
+    dW_out, db_out = _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb,
+                                 grads_zeroed, pw and gemm_dw)
+    return dx, dW_out, db_out
+
+
+def _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb, grads_zeroed, use_gemm):
+    """Weight (and bias) gradient of a channels-last bf16 conv; returns (dW, db), each None when it was written
+    straight into the given fp32 view."""
+    lib = native.load()
     dW_out = db_out = None
-    if need_dw and pw and gemm_dw:
+    if use_gemm:
         # dW[K, C] = dY^T[K, M] . X[M, C], fp32 straight into the flat-gradient view; bias = column sums of dY
         from .gemm import mmul
         M = N * H * W
@@ -344,34 +364,33 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
             native.channel_sum(dy_rows, out=dbt)
             db_out = None if directb else dbt
-        return dx, dW_out, db_out
-    if need_dw:
-        direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
-        dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
-        # the kernel accumulates in [K][R][S][C]; identical to DL4J's [K][C][R][S] when R == S == 1
-        if R == 1 and S == 1:
-            ws = dWt
-            if not (direct and grads_zeroed):
-                ws.zero_()
-        else:
-            ws = _zeroed_wrw_ws(K, R, S, C, x.device)
-        dbt = None
-        if need_db:
-            directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
-            dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
-            if not (directb and grads_zeroed):
-                dbt.zero_()
-        splits = _wrw_splits(lib, x, dy, ws, dbt, N, H, W, C, K, R, S, stride, pad4, dilation, OH, OW)
-        rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
-                               pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits, _stream())
-        native._check(rc, "conv_wrw")
-        if ws is not dWt:
-            rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, 1, _stream())
-            native._check(rc, "conv_wrw_permute")
-        dW_out = None if direct else dWt
-        if need_db:
-            db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
-    return dx, dW_out, db_out
+        return dW_out, db_out
+    direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
+    dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
+    # the kernel accumulates in [K][R][S][C]; identical to DL4J's [K][C][R][S] when R == S == 1
+    if R == 1 and S == 1:
+        ws = dWt
+        if not (direct and grads_zeroed):
+            ws.zero_()
+    else:
+        ws = _zeroed_wrw_ws(K, R, S, C, x.device)
+    dbt = None
+    if need_db:
+        directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+        dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
+        if not (directb and grads_zeroed):
+            dbt.zero_()
+    splits = _wrw_splits(lib, x, dy, ws, dbt, N, H, W, C, K, R, S, stride, pad4, dilation, OH, OW)
+    rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
+                           pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits, _stream())
+    native._check(rc, "conv_wrw")
+    if ws is not dWt:
+        rc = lib.dl4j_conv_wrw_permute(_ptr(ws), _ptr(dWt), K, C, R, S, 1, _stream())
+        native._check(rc, "conv_wrw_permute")
+    dW_out = None if direct else dWt
+    if need_db:
+        db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
+    return dW_out, db_out
 
 
 def _wrw_default_splits(M, K, RSC):

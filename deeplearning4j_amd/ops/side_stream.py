@@ -1,0 +1,77 @@
+"""Weight-gradient overlap stream for the training backward pass.
+
+In a conv layer's backward the weight gradient (dW = dY^T . im2col(X)) and the data gradient (dX) are independent;
+the reference computes them back to back (ConvolutionLayer.java:215-257 — im2col GEMM for dW, then col2im for
+epsilon). On MI355X the small late-stage ResNet convs fill only part of the 256 CUs (e.g. 392 output tiles for a
+7x7x256 3x3 conv at batch 512), so running dW on a second HIP stream lets it fill the CUs the next layer's
+bwd-data / BatchNorm-backward kernels leave idle.
+
+Contract (``nn/network_base.py`` drives it):
+  * ``begin(ref)`` at the start of a backward pass (active only for CUDA networks, ``DL4J_AMD_WRW_STREAM`` != 0);
+  * ``run(fn, *keep)`` launches ``fn`` on the side stream after the main stream's pending work (its inputs) and keeps
+    ``keep`` (the X / dY operands) referenced until the next join, so the caching allocator cannot hand their memory
+    to later main-stream kernels while the side stream still reads it. ``fn`` must write only into persistent
+    buffers (the flat fp32 gradient views) — nothing it allocates is returned to the main stream;
+  * ``join()`` makes the main stream wait for every side launch (before a data-parallel bucket reads gradients) and
+    ``end()`` joins and closes the pass. Under HIP-graph capture the fork/join become graph edges (the side stream
+    joins the capture through the event wait), so the replayed graph runs dW and dX as parallel branches.
+"""
+import os
+import threading
+
+import torch
+
+_tl = threading.local()
+_streams = {}
+
+
+def enabled():
+    return os.environ.get("DL4J_AMD_WRW_STREAM", "1") == "1"
+
+
+def _side(dev):
+    s = _streams.get(dev.index)
+    if s is None:
+        s = _streams[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def begin(ref):
+    _tl.st = None
+    if enabled() and ref is not None and getattr(ref, "is_cuda", False):
+        _tl.st = {"dev": ref.device, "main": None, "refs": [], "pending": False}
+
+
+def active():
+    return getattr(_tl, "st", None) is not None
+
+
+def run(fn, *keep):
+    st = getattr(_tl, "st", None)
+    if st is None:
+        return fn()
+    main = torch.cuda.current_stream(st["dev"])
+    if st["main"] is None:
+        st["main"] = main
+    elif st["main"] != main:          # the caller switched streams mid-pass: stay on its stream
+        return fn()
+    side = _side(st["dev"])
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        r = fn()
+    st["refs"].extend(keep)
+    st["pending"] = True
+    return r
+
+
+def join():
+    st = getattr(_tl, "st", None)
+    if st is not None and st["pending"]:
+        st["main"].wait_stream(_side(st["dev"]))
+        st["pending"] = False
+        st["refs"].clear()
+
+
+def end():
+    join()
+    _tl.st = None
