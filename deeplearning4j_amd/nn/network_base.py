@@ -359,8 +359,9 @@ class BaseNetwork:
     def _grad_ready(self, key):
         acc = getattr(self, "gradientsAccumulator", None)
         if acc is not None and hasattr(acc, "grad_ready"):
-            from ..ops import side_stream
-            side_stream.join()                      # the bucket reads gradients the side stream may still write
+            if not getattr(acc, "joins_side_stream", False):
+                from ..ops import side_stream
+                side_stream.join()                  # a bucket may read gradients the side stream still writes
             acc.grad_ready(self, self._offset_of.get(key, 0))
 
     def setGradientsAccumulator(self, acc):

@@ -90,12 +90,19 @@ class AllReduceGradientsAccumulator:
         else:
             self._pending.append((dist.all_reduce(seg, op=dist.ReduceOp.SUM, async_op=True), None, None))
 
+    joins_side_stream = True   # grad_ready joins ops/side_stream itself, only when a bucket is issued
+
     def grad_ready(self, net, offset):
         """Called after a layer finished writing gradients at flat offset >= ``offset``."""
         if not self.active or self._buckets is None:
             return
         g = net.flattenedGradients
+        joined = False
         while self._next < len(self._buckets) and self._buckets[self._next][0] >= offset:
+            if not joined:                 # conv weight gradients still on the overlap stream land in this bucket
+                from ..ops import side_stream
+                side_stream.join()
+                joined = True
             s, e = self._buckets[self._next]
             self._issue(g, s, e)
             self._next += 1
