@@ -755,6 +755,19 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x
   }
   __syncthreads();
   const int items = min(RB, H - ih0) * W * CG;
+  // a thread keeps one channel group across its items when CG divides the block size: BN factors in registers
+  // (dx = A*acc - B*x - Cq, see bn_bwd_elem) instead of 40 L1 parameter loads per 8-channel item
+  const bool fixed = (256 % CG) == 0;
+  float A[8], B[8], Cq[8];
+  if (fixed) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = (threadIdx.x % CG) * 8 + i;
+      A[i] = ctx[2 * C + c];
+      B[i] = ctx[2 * C + c] * ctx[C + c] * cdg[c];
+      Cq[i] = ctx[2 * C + c] * (cdb[c] - ctx[c] * ctx[C + c] * cdg[c]);
+    }
+  }
   for (int it = threadIdx.x; it < items; it += 256) {
     const int cg = it % CG, q1 = it / CG, iw = q1 % W, ih = ih0 + q1 / W;
     const int hp = ih + pt, wp = iw + pl;
@@ -783,11 +796,16 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x
         for (int i = 0; i < 8; ++i)
           if (((pk >> (8 * i)) & 0xff) == me) acc[i] += g[i];
       }
+    if (fixed) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = cg * 8 + i;
-      const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
-      xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
+      for (int i = 0; i < 8; ++i) xv[i] = A[i] * acc[i] - B[i] * xv[i] - Cq[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = cg * 8 + i;
+        const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
+        xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
+      }
     }
     Vec8<T>::store(dx + t * 8, xv);
   }
