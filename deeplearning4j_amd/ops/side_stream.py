@@ -23,6 +23,7 @@ import torch
 
 _tl = threading.local()
 _streams = {}
+LAUNCHES = [0]   # side-stream launches so far (tests check the overlap path really ran)
 
 
 def enabled():
@@ -61,6 +62,7 @@ def run(fn, *keep):
         r = fn()
     st["refs"].extend(keep)
     st["pending"] = True
+    LAUNCHES[0] += 1
     return r
 
 

@@ -151,14 +151,19 @@ def run_es_parallel(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
-def make_cg(seed=3, device=None):
-    """Residual conv ComputationGraph (no BatchNorm, so DP-2 equals one process at 2x batch exactly)."""
+def make_cg(seed=3, device=None, dtype=None):
+    """Residual conv ComputationGraph (no BatchNorm, so DP-2 equals one process at 2x batch exactly). ``dtype``
+    (a DataType) sets the network compute dtype; bf16 puts c2 on the MFMA conv kernels and its weight gradient on
+    the overlap stream."""
     from deeplearning4j_amd import Activation, Adam, LossFunction, NeuralNetConfiguration
     from deeplearning4j_amd.nn.conf.graph import ElementWiseVertex
     from deeplearning4j_amd.nn.conf.inputs import InputType
     from deeplearning4j_amd.nn.conf.layers import ConvolutionLayer, GlobalPoolingLayer, OutputLayer
     from deeplearning4j_amd.nn.graph.computation_graph import ComputationGraph
-    conf = (NeuralNetConfiguration.Builder().seed(seed).updater(Adam(0.01)).graphBuilder()
+    b = NeuralNetConfiguration.Builder().seed(seed).updater(Adam(0.01))
+    if dtype is not None:
+        b = b.dataType(dtype)
+    conf = (b.graphBuilder()
             .addInputs("in")
             .addLayer("c1", ConvolutionLayer.Builder(3, 3).nIn(3).nOut(8).padding(1, 1)
                       .activation(Activation.RELU).build(), "in")
