@@ -556,7 +556,8 @@ DL4J_API void dl4j_conv_set_variant(int v) { g_fwd_variant = v; }
 __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                               float* __restrict__ dW, float* __restrict__ db,
                                                               ConvGeom g, int m_per_split, FastDiv fOW, FastDiv fOH,
-                                                              int remap) {
+                                                              int remap, float* __restrict__ part,
+                                                              float* __restrict__ partb) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_K * WRW_ROW];   // 2 buffers x (A + B) = 40 KB
   const int M = g.N * g.OH * g.OW;
   const int Kout = g.K;
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
   for (int i = 0; i < 2; ++i) pm[i] = mbeg + lrow + 16 * i;
   const int rdh = rr * g.dh - g.ph, sdw = ss * g.dw - g.pw;
   float bsum[8];
-  const bool do_bias = (db != nullptr) && (tj == 0);
+  const bool do_bias = (db != nullptr || partb != nullptr) && (tj == 0);
   for (int i = 0; i < 8; ++i) bsum[i] = 0.f;
 
   f32x16_t acc[2][2];
@@ -690,7 +691,9 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int k = k0 + wk * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-        if (k < Kout) atomicAdd(dW + (long long)k * RSC + j, acc[a][b][e]);
+        if (k >= Kout) continue;
+        if (part) part[((long long)split * Kout + k) * RSC + j] = acc[a][b][e];   // deterministic: own slab
+        else atomicAdd(dW + (long long)k * RSC + j, acc[a][b][e]);
       }
     }
   }
@@ -705,7 +708,10 @@ __global__ __launch_bounds__(NTHREADS) void igemm_wrw_kernel(const bf16* __restr
         float s = 0.f;
         for (int rrow = 0; rrow < 16; ++rrow) s += red[(rrow * 16 + tid) * 8 + e];
         const int k = k0 + tid * 8 + e;
-        if (k < Kout) atomicAdd(db + k, s);
+        if (k < Kout) {
+          if (partb) partb[(long long)split * Kout + k] = s;
+          else atomicAdd(db + k, s);
+        }
       }
     }
   }
@@ -1033,6 +1039,86 @@ DL4J_API int dl4j_conv_wrw(const void* X, const void* dY, float* dW, float* db, 
                        db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH), g_wrw_remap);
   else
     hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY, dW,
-                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH), g_wrw_remap);
+                       db, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH), g_wrw_remap,
+                       (float*)nullptr, (float*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Deterministic weight gradient (DL4J_AMD_DETERMINISTIC=1; the reference's cuDNN helper offers deterministic
+// backward-filter algorithms, CudnnConvolutionHelper.java:179-246). Every pixel split writes its own fp32 slab
+// part[split][K][R*S*C] with plain stores (no atomics), then conv_wrw_reduce sums the slabs in split order and
+// writes the DL4J [K][C][R][S] layout directly (no KRSC workspace / permute). Bitwise reproducible run to run.
+// ------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv_wrw_reduce(const float* __restrict__ part, const float* __restrict__ partb,
+                                                       float* __restrict__ dW, float* __restrict__ db, int splits,
+                                                       int K, int C, int RS) {
+  const long long total = (long long)K * C * RS;
+  const long long plane = total;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    // o indexes the DL4J layout [k][c][rs]; the slab layout is [k][rs][c]
+    const int rs = (int)(o % RS);
+    const long long t = o / RS;
+    const int c = (int)(t % C);
+    const long long k = t / C;
+    const long long src = (k * RS + rs) * C + c;
+    float a = 0.f;
+    for (int sp = 0; sp < splits; ++sp) a += part[sp * plane + src];
+    dW[o] = a;
+  }
+  if (db && blockIdx.x == 0) {
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      float a = 0.f;
+      for (int sp = 0; sp < splits; ++sp) a += partb[(long long)sp * K + k];
+      db[k] = a;
+    }
+  }
+}
+
+// Split count / slab sizes the deterministic path will use (host sizes the scratch from these).
+DL4J_API long long dl4j_conv_wrw_det_floats(int N, int C, int K, int R, int S, int OH, int OW, int splits) {
+  const int M = N * OH * OW;
+  const int RSC = R * S * C;
+  const int tiles = ((K + TILE_N - 1) / TILE_N) * ((RSC + TILE_M - 1) / TILE_M);
+  if (splits <= 0) {
+    splits = (384 + tiles - 1) / tiles;
+    const int maxs = (M + 8 * TILE_K - 1) / (8 * TILE_K);
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+  }
+  int mps = (M + splits - 1) / splits;
+  mps = (mps + TILE_K - 1) / TILE_K * TILE_K;
+  splits = (M + mps - 1) / mps;
+  return (long long)splits * K * (RSC + 1);
+}
+
+// dW: DL4J-layout fp32 [K][C][R][S] (written, not accumulated); db fp32 [K] or null; part: >= dl4j_conv_wrw_det_floats.
+DL4J_API int dl4j_conv_wrw_det(const void* X, const void* dY, float* dW, float* db, float* part, int N, int H, int W,
+                               int C, int K, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int OH,
+                               int OW, int splits, hipStream_t s) {
+  if (C % 8 != 0 || K % 8 != 0) return -1;
+  ConvGeom g = mk(N, H, W, C, OH, OW, K, R, S, sh, sw, ph, pw, dh, dw);
+  const int M = N * OH * OW;
+  const int RSC = R * S * C;
+  const int tiles = ((K + TILE_N - 1) / TILE_N) * ((RSC + TILE_M - 1) / TILE_M);
+  if (splits <= 0) {
+    splits = (384 + tiles - 1) / tiles;
+    const int maxs = (M + 8 * TILE_K - 1) / (8 * TILE_K);
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+  }
+  int mps = (M + splits - 1) / splits;
+  mps = (mps + TILE_K - 1) / TILE_K * TILE_K;
+  splits = (M + mps - 1) / mps;
+  float* partb = part + (long long)splits * K * RSC;
+  hipLaunchKernelGGL(igemm_wrw_kernel, dim3(tiles, splits), dim3(NTHREADS), 0, s, (const bf16*)X, (const bf16*)dY,
+                     (float*)nullptr, (float*)nullptr, g, mps, make_fastdiv((unsigned)OW), make_fastdiv((unsigned)OH),
+                     g_wrw_remap, part, db ? partb : (float*)nullptr);
+  // a split whose pixel range is empty never stores: only possible when splits > ceil(M / mps), excluded above
+  const long long total = (long long)K * RSC;
+  long long gsz = (total + 255) / 256;
+  if (gsz > 4096) gsz = 4096;
+  hipLaunchKernelGGL(conv_wrw_reduce, dim3((unsigned)gsz), dim3(256), 0, s, part, partb, dW, db, splits, K, C, R * S);
   return (int)hipGetLastError();
 }

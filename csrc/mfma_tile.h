@@ -1,0 +1,300 @@
+// Shared building blocks of the LDS-DMA MFMA tile kernels (csrc/gemm.hip GEMM, csrc/conv_gemm.hip implicit-GEMM
+// convolution): operand fragment reads from the swizzled K-contiguous / M-contiguous LDS images, the counted-vmcnt
+// helpers, and the LDS epilogue (alpha / bias / beta*C / pre-activation / activation, 16-byte row stores, BatchNorm
+// tile statistics). Everything lives in an anonymous namespace: each including translation unit gets its own copy.
+#pragma once
+#include "common.h"
+#include <hip/hip_fp16.h>
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+namespace {
+
+__device__ __attribute__((aligned(64))) char gemm_zero_page[64];
+
+template <int V> struct IC { static constexpr int value = V; };
+// compile-time loop: f(IC<I>{}) for I in [B, E) — keeps register arrays statically indexed
+template <int B, int E, typename F> __device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(IC<B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+template <int DT> struct MfmaT;
+template <> struct MfmaT<1> {
+  typedef __attribute__((ext_vector_type(8))) __bf16 v8;
+  static __device__ __forceinline__ f32x16_t mma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MfmaT<2> {
+  typedef __attribute__((ext_vector_type(8))) _Float16 v8;
+  static __device__ __forceinline__ f32x16_t mma(v8 a, v8 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  void* Z;                 // optional pre-activation output (same dtype / ldc as C)
+  const float* bias;       // fp32, per column (bias_mode 1) or per row (bias_mode 2)
+  float* ws;               // split-K slabs [splits][M][N] fp32
+  long long lda, ldb, ldc;
+  long long sA, sB, sC;    // batch strides (elements)
+  int M, N, K;
+  int kps;                 // K per split (multiple of 64)
+  int splits;
+  float alpha, beta;
+  int bias_mode, act, out_dt;
+  int tiles_m, tiles_n;
+  int coalesce;             // 1: epilogue through LDS with 16-byte row stores (host-checked alignment)
+  float* tstats;           // optional BatchNorm partial statistics of the output (8-phase kernel, no split-K)
+  int stats_P;              // number of 64-row partials (planes [3][stats_P][N])
+};
+
+__device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+// ----------------------------------------------------------------------------------------------- epilogue
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case 1: return fmaxf(v, 0.f);
+    case 2: return tanhf(v);
+    case 3: return 1.f / (1.f + __expf(-v));
+    case 4: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float ld_out(const void* C, int dt, long long i) {
+  if (dt == 0) return reinterpret_cast<const float*>(C)[i];
+  const u16 u = reinterpret_cast<const u16*>(C)[i];
+  if (dt == 1) return bf2f(u);
+  return __half2float(__ushort_as_half(u));
+}
+
+__device__ __forceinline__ u16 to16(float v, int dt) {
+  return dt == 1 ? f2bf(v) : __half_as_ushort(__float2half(v));
+}
+
+// 4 consecutive outputs (m, n..n+3) of one row: vector store when aligned and fully in range.
+__device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int m, int n, float* v) {
+  const long long base = (long long)m * g.ldc + n;
+  const bool full = (n + 3 < g.N);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x = v[j] * g.alpha;
+    if (g.bias_mode == 1 && n + j < g.N) x += g.bias[n + j];
+    else if (g.bias_mode == 2) x += g.bias[m];
+    if (g.beta != 0.f && n + j < g.N) x += g.beta * ld_out(C, g.out_dt, base + j);
+    v[j] = x;
+  }
+  const bool vec = full && ((g.ldc & 3) == 0) && ((n & 3) == 0);
+  if (Z) {
+    if (g.out_dt == 0) {
+      float* z = reinterpret_cast<float*>(Z) + base;
+      if (vec) *reinterpret_cast<float4*>(z) = make_float4(v[0], v[1], v[2], v[3]);
+      else for (int j = 0; j < 4; ++j) if (n + j < g.N) z[j] = v[j];
+    } else {
+      u16* z = reinterpret_cast<u16*>(Z) + base;
+      if (vec) {
+        uint2 pk;
+        pk.x = (unsigned)to16(v[0], g.out_dt) | ((unsigned)to16(v[1], g.out_dt) << 16);
+        pk.y = (unsigned)to16(v[2], g.out_dt) | ((unsigned)to16(v[3], g.out_dt) << 16);
+        *reinterpret_cast<uint2*>(z) = pk;
+      } else {
+        for (int j = 0; j < 4; ++j) if (n + j < g.N) z[j] = to16(v[j], g.out_dt);
+      }
+    }
+  }
+  if (g.act)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = apply_act(v[j], g.act);
+  if (g.out_dt == 0) {
+    float* c = reinterpret_cast<float*>(C) + base;
+    if (vec) *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+    else for (int j = 0; j < 4; ++j) if (n + j < g.N) c[j] = v[j];
+  } else {
+    u16* c = reinterpret_cast<u16*>(C) + base;
+    if (vec) {
+      uint2 pk;
+      pk.x = (unsigned)to16(v[0], g.out_dt) | ((unsigned)to16(v[1], g.out_dt) << 16);
+      pk.y = (unsigned)to16(v[2], g.out_dt) | ((unsigned)to16(v[3], g.out_dt) << 16);
+      *reinterpret_cast<uint2*>(c) = pk;
+    } else {
+      for (int j = 0; j < 4; ++j) if (n + j < g.N) c[j] = to16(v[j], g.out_dt);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- LDS epilogue
+// Finished fp32 accumulators leave a block through LDS: pass P, the waves owning tile rows [P*RPP, (P+1)*RPP)
+// store their raw accumulators into an fp32 [RPP][BN] image (row pitch BN*4 + 16 bytes), then every thread takes
+// 8-column chunks of whole rows, applies alpha / bias / beta*C / pre-activation Z / activation once per element
+// (bias as vector loads), converts, and writes 16-byte row segments. Direct 8-byte stores from the MFMA fragment
+// layout (16-32 rows per instruction) ran at ~1 TB/s; register pressure stays at the accumulators themselves.
+struct EpiOut {
+  char* dst;          // C (or the split-K slab)
+  long long ld;       // destination row stride (elements)
+  int dt;             // destination dtype (0 f32, 1 bf16, 2 f16)
+  bool raw;           // split-K slab: no epilogue math
+  bool vec;           // 16-byte aligned rows (ld and base) for vector stores
+};
+
+__device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, void* Zp, int m, int n, float* v) {
+  if (!o.raw) {
+    float b[8];
+    if (g.bias_mode == 1) {
+      if (n + 8 <= g.N && ((n & 3) == 0)) {
+        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
+        b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+      } else {
+        for (int j = 0; j < 8; ++j) b[j] = n + j < g.N ? g.bias[n + j] : 0.f;
+      }
+    } else {
+      const float bm = g.bias_mode == 2 ? g.bias[m] : 0.f;
+      for (int j = 0; j < 8; ++j) b[j] = bm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * g.alpha + b[j];
+    if (g.beta != 0.f)
+      for (int j = 0; j < 8; ++j) if (n + j < g.N) v[j] += g.beta * ld_out(o.dst, o.dt, (long long)m * o.ld + n + j);
+    if (Zp)
+      for (int j = 0; j < 8; ++j)
+        if (n + j < g.N) {
+          const long long i = (long long)m * o.ld + n + j;
+          if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
+          else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
+        }
+    if (g.act)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
+  }
+  char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
+  if (o.vec && n + 8 <= g.N) {
+    if (o.dt == 0) {
+      reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      uint4 pk;
+      pk.x = (unsigned)to16(v[0], o.dt) | ((unsigned)to16(v[1], o.dt) << 16);
+      pk.y = (unsigned)to16(v[2], o.dt) | ((unsigned)to16(v[3], o.dt) << 16);
+      pk.z = (unsigned)to16(v[4], o.dt) | ((unsigned)to16(v[5], o.dt) << 16);
+      pk.w = (unsigned)to16(v[6], o.dt) | ((unsigned)to16(v[7], o.dt) << 16);
+      *reinterpret_cast<uint4*>(p) = pk;
+    }
+  } else {
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N) {
+        if (o.dt == 0) reinterpret_cast<float*>(p)[j] = v[j];
+        else reinterpret_cast<u16*>(p)[j] = to16(v[j], o.dt);
+      }
+  }
+}
+
+// Read-out of one pass: RPP rows x BN columns of the fp32 LDS image.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_readout(const GemmArgs& g, const EpiOut& o, void* Zp, const char* T, int mrow0,
+                                            int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int CPR = BN / 8;
+  for (int idx = tid; idx < RPP * CPR; idx += NT) {
+    const int r = idx / CPR, c = idx - (idx / CPR) * CPR;
+    const int m = mrow0 + r, n = n0 + c * 8;
+    if (m >= g.M || n >= g.N) continue;
+    const float4 a = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32);
+    const float4 b = *reinterpret_cast<const float4*>(T + r * PITCH + c * 32 + 16);
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    epi_chunk8(g, o, Zp, m, n, v);
+  }
+}
+
+// BatchNorm partial statistics of the bf16 outputs held in an fp32 LDS image (conv epilogue -> consuming BN layer):
+// per (64-row partial, column) shifted sums S1 = sum(y - y0), S2 = sum((y - y0)^2) and the shift y0 (first row),
+// y = bf16(alpha*acc + bias) exactly as stored. Planes [3][stats_P][N]; reduced by bn_tiles_reduce.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int PARTS = RPP / 64;
+  for (int task = tid; task < PARTS * BN; task += NT) {
+    const int col = task % BN, part = task / BN;
+    const int n = n0 + col;
+    const int rbeg = mrow0 + part * 64;
+    if (n >= g.N) continue;
+    const long long pidx = rbeg / 64;
+    if (pidx >= g.stats_P) continue;
+    const int rows = min(64, g.M - rbeg);
+    const float bb = g.bias_mode == 1 ? g.bias[n] : 0.f;
+    float s1 = 0.f, s2 = 0.f, sh = 0.f;
+    if (rows > 0) {
+      const char* src = T + (part * 64) * PITCH + col * 4;
+      sh = bf2f(to16(*reinterpret_cast<const float*>(src) * g.alpha + bb, 1));
+      for (int r = 0; r < rows; ++r) {
+        const float d = bf2f(to16(*reinterpret_cast<const float*>(src + r * PITCH) * g.alpha + bb, 1)) - sh;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+      }
+    }
+    g.tstats[pidx * g.N + n] = s1;
+    g.tstats[((long long)g.stats_P + pidx) * g.N + n] = s2;
+    g.tstats[(2LL * g.stats_P + pidx) * g.N + n] = sh;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- fast kernel
+// LDS byte offsets
+__device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+__device__ __forceinline__ int mc_off(int k, int col) {
+  return (col >> 7) * (64 * 256) + k * 256 + (((((col & 127) >> 3) ^ ((k & 3) << 2))) << 4) + (col & 7) * 2;
+}
+
+template <int DT, bool KC>
+__device__ __forceinline__ typename MfmaT<DT>::v8 read_frag(const char* T, int rbase, int s, int lane) {
+  typedef typename MfmaT<DT>::v8 v8;
+  if constexpr (KC) {
+    const int r = rbase + (lane & 31);
+    return *reinterpret_cast<const v8*>(T + kc_off(r, 2 * s + (lane >> 5)));
+  } else {
+    const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int col = rbase + (grp & 1) * 16 + 4 * p;
+    const int k0 = 16 * s + (grp >> 1) * 8 + q;
+    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + mc_off(k0, col)));
+    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(T + mc_off(k0 + 4, col)));
+    s16x8_t f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(v8, f);
+  }
+}
+
+}  // namespace

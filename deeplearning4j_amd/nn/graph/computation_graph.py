@@ -21,6 +21,22 @@ from ..network_base import BaseNetwork
 from ... import profiling as _prof
 
 
+def _shares_storage(a, b):
+    """True when the bytes addressed by tensors a and b overlap. Spans, not storages: arena tensors are carved from
+    one shared storage (memory/arena.py) and must not count as aliases of each other."""
+    if a is None or b is None or not torch.is_tensor(a) or not torch.is_tensor(b) or a.device != b.device:
+        return False
+    if a.numel() == 0 or b.numel() == 0:
+        return False
+
+    def span(t):
+        n = 1 + sum((s - 1) * abs(st) for s, st in zip(t.shape, t.stride()))
+        return t.data_ptr(), t.data_ptr() + n * t.element_size()
+    a0, a1 = span(a)
+    b0, b1 = span(b)
+    return a0 < b1 and b0 < a1
+
+
 class ComputationGraph(BaseNetwork):
     _key_by_name = True
 
@@ -332,8 +348,14 @@ class ComputationGraph(BaseNetwork):
                     tok = _prof.layer_begin("bwd", name, layer) if _prof.ACTIVE else None
                     ins0 = self.vertex_inputs[name]
                     if len(ins0) == 1 and v.preProcessor is None and ins0[0] in eps_acc and \
-                            hasattr(layer, "dx_accum"):
-                        layer.dx_accum = eps_acc[ins0[0]]    # fan-out: let the conv kernel sum dX in place
+                            hasattr(layer, "dx_accum") and \
+                            not any(_shares_storage(eps_acc[ins0[0]], t) for t in
+                                    [e_in] + [t for k, t in eps_acc.items() if k != ins0[0]]):
+                        # fan-out: let the conv kernel sum dX in place. Never when the running sum is also this
+                        # layer's own incoming gradient or another vertex's pending one (x + conv(x) with an
+                        # identity activation hands one tensor to both branches): the kernel would overwrite a
+                        # gradient that is still to be read.
+                        layer.dx_accum = eps_acc[ins0[0]]
                     if tbptt_back is not None and hasattr(layer, "tBpttStateMap"):
                         _, e = layer.backpropGradient(e_in, tbptt_back=tbptt_back)
                     else:

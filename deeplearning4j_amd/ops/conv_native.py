@@ -33,6 +33,12 @@ native.register_sig("dl4j_conv_set_variant", [c_int])
 native.register_sig("dl4j_conv_set_wrw_variant", [c_int])
 native.register_sig("dl4j_conv_set_wrw_remap", [c_int])
 native.register_sig("dl4j_conv_wrw_permute", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p])
+native.register_sig("dl4j_conv_wrw_det", [c_void_p] * 5 + [c_int] * 17 + [c_void_p])
+native.register_sig("dl4j_conv_wrw_det_floats", [c_int] * 8, restype=c_ll)
+native.register_sig("dl4j_conv_fwd_v3", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 +
+                    [ctypes.c_float, c_void_p, c_int, c_void_p])
+native.register_sig("dl4j_conv_v3_num_variants", [])
+native.register_sig("dl4j_conv_v3_default_variant", [c_ll, c_int])
 
 # Optional per-shape override of the weight-gradient split count (tuning): {(N,H,W,C,K,R,S,stride): splits}
 WRW_SPLITS = {}
@@ -41,6 +47,24 @@ WRW_SPLITS = {}
 WEIGHT_VERSION = [0]
 _cache = {}
 _wrw_ws = {}   # (K, R, S, C, device) -> fp32 KRSC accumulation workspace, kept zero by the permute kernel
+
+
+def deterministic():
+    """DL4J_AMD_DETERMINISTIC=1: conv weight gradients without float atomics (per-split slabs + fixed-order reduce),
+    so a training step is bitwise reproducible (the data-parallel equivalence tests rely on it)."""
+    return os.environ.get("DL4J_AMD_DETERMINISTIC", "0") == "1"
+
+
+_det_ws = {}
+
+
+def _det_scratch(nfloats, device):
+    # one growing slab per (device, stream): the side-stream weight gradients never share it with the main stream
+    key = (str(device), torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0)
+    t = _det_ws.get(key)
+    if t is None or t.numel() < nfloats:
+        t = _det_ws[key] = torch.empty(int(nfloats), dtype=torch.float32, device=device)
+    return t
 
 
 def _zeroed_wrw_ws(K, R, S, C, device):
@@ -237,18 +261,79 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
     x = _cl(x)
     y = arena.empty((N, K, OH, OW), torch.bfloat16, x.device, channels_last=True)
     bias = b.float().contiguous() if b is not None else None
-    ts = None
-    if want_stats and C % 32 == 0 and R * S <= 64 and K % 8 == 0:
-        P = 2 * ((N * OH * OW + 127) // 128)
-        ts = torch.empty((3, P, K), dtype=torch.float32, device=x.device)
-    rc = native.load().dl4j_conv_fwd(_ptr(x), _ptr(krsc), _ptr(bias), _ptr(y), N, H, W, C, K, R, S, stride[0],
-                                     stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, _ptr(ts),
-                                     _stream())
+    stats = want_stats and C % 32 == 0 and R * S <= 64 and K % 8 == 0
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW)
+    v = -1
+    if _v3_ok(C, K, R, S):
+        key = ("fwd", geom, bias is not None, stats)
+        v = _v3_pick(key, lambda var, out, t: _fwd_launch(var, x, krsc, bias, out, geom, 0.0, t),
+                     y, lambda var: _stats_buf(var, N * OH * OW, K, x.device) if stats else None)
+    ts = _stats_buf(v, N * OH * OW, K, x.device) if stats else None
+    rc = _fwd_launch(v, x, krsc, bias, y, geom, 0.0, ts)
     if rc == 1:
         y._bn_tile_stats = (ts, ts.shape[1])
         rc = 0
     native._check(rc, "conv_fwd")
     return y
+
+
+# ------------------------------------------------------------------ round-3 tile engine (csrc/conv_gemm.hip)
+V3 = os.environ.get("DL4J_AMD_CONV_V3", "1") == "1"
+_V3_CHOICE = {}     # (direction, geometry, ...) -> variant id (-1 = round-2 kernel in csrc/conv_igemm.hip)
+
+
+def _v3_ok(C, K, R, S):
+    return V3 and C % 64 == 0 and K % 8 == 0 and R * S <= 64
+
+
+def _stats_buf(variant, M, K, device):
+    # BatchNorm tile partials, 64-row partials: the round-2 kernel pads to whole 128-row tiles
+    P = (M + 63) // 64 if variant >= 0 else 2 * ((M + 127) // 128)
+    return torch.empty((3, P, K), dtype=torch.float32, device=device)
+
+
+def _fwd_launch(variant, x, wk, bias, y, geom, beta, ts):
+    """One conv launch on the chosen kernel. Returns 1 when BN tile statistics were written to ts, 0 when not, a
+    negative code / HIP error otherwise."""
+    lib = native.load()
+    if variant >= 0:
+        rc = lib.dl4j_conv_fwd_v3(1, _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts), variant,
+                                  _stream())
+        return 1 if (rc == 0 and ts is not None) else rc
+    N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
+    if beta != 0.0:
+        return -1
+    return lib.dl4j_conv_fwd(_ptr(x), _ptr(wk), _ptr(bias), _ptr(y), N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH,
+                             OW, _ptr(ts), _stream())
+
+
+def _v3_pick(key, launch, out, make_ts):
+    """Per-shape kernel choice: the first eager call times every tile variant of the round-3 engine and the round-2
+    kernel on scratch outputs (inline on this stream) and keeps the fastest; calls under HIP-graph capture, or with
+    DL4J_AMD_CONV_TUNE=0, use the remembered choice or the engine's default tile."""
+    v = _V3_CHOICE.get(key)
+    if v is not None:
+        return v
+    lib = native.load()
+    geom = key[1]
+    M, K = geom[0] * geom[13] * geom[14], geom[4]
+    if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
+        return lib.dl4j_conv_v3_default_variant(M, K)
+    cands = list(range(lib.dl4j_conv_v3_num_variants())) + [-1]
+    scratch = torch.empty_like(out)
+    if key[0] == "bwd_acc":
+        scratch.copy_(out)
+    best, bt = None, None
+    with side_stream.suspended():
+        for var in cands:
+            ts = make_ts(var)
+            if launch(var, scratch, ts) not in (0, 1):
+                continue
+            t = _timed(lambda: launch(var, scratch, ts), reps=3)
+            if bt is None or t < bt:
+                best, bt = var, t
+    v = _V3_CHOICE[key] = best if best is not None else -1
+    return v
 
 
 def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=None, gb=None, grads_zeroed=False,
@@ -294,8 +379,18 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             _, flip = _relayout(w, False, True)
             dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
                                                   channels_last=True)
-            rc = lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, R, S, pad4[0], pad4[2], OH,
-                                           OW, int(acc), _stream())
+            # transposed conv: "input" dY (OH x OW x K), flipped CRSK weights, pad' = R-1-pad, output H x W x C
+            gb = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
+
+            def bwd_launch(var, out, _ts):
+                if var >= 0:
+                    return _fwd_launch(var, dy, flip, None, out, gb, 1.0 if acc else 0.0, None)
+                return lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(out), N, H, W, C, K, R, S, pad4[0],
+                                                 pad4[2], OH, OW, int(acc), _stream())
+            v = -1
+            if _v3_ok(K, C, R, S):
+                v = _v3_pick(("bwd_acc" if acc else "bwd", gb), bwd_launch, dx, lambda var: None)
+            rc = bwd_launch(v, dx, None)
             native._check(rc, "conv_bwd_data_s1")
         elif pure_1x1 and stride[0] == stride[1]:
             _, flip = _relayout(w, False, True)
@@ -367,6 +462,23 @@ def _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need
         return dW_out, db_out
     direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
     dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
+    if deterministic():
+        # per-split fp32 slabs + fixed-order reduce straight into the DL4J layout: bitwise reproducible
+        dbt = None
+        if need_db:
+            directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+            dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
+        splits = WRW_SPLITS.get((N, H, W, C, K, R, S, tuple(stride)), 0)
+        nf = lib.dl4j_conv_wrw_det_floats(N, C, K, R, S, OH, OW, splits)
+        part = _det_scratch(nf, x.device)
+        rc = lib.dl4j_conv_wrw_det(_ptr(x), _ptr(dy), _ptr(dWt), _ptr(dbt), _ptr(part), N, H, W, C, K, R, S,
+                                   stride[0], stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits,
+                                   _stream())
+        native._check(rc, "conv_wrw_det")
+        db_out = None
+        if need_db:
+            db_out = None if (gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()) else dbt
+        return (None if direct else dWt), db_out
     # the kernel accumulates in [K][R][S][C]; identical to DL4J's [K][C][R][S] when R == S == 1
     if R == 1 and S == 1:
         ws = dWt
@@ -457,7 +569,10 @@ def _choose(key, run_gemm, run_old):
             return False
         if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
             return True
-        tg, to = _timed(run_gemm), _timed(run_old)
+        # candidates run inline on this stream: on the overlap stream they would still be writing their scratch
+        # outputs after those are freed, and the main-stream timing events would not cover them
+        with side_stream.suspended():
+            tg, to = _timed(run_gemm), _timed(run_old)
         c = _CHOICE[key] = tg <= to
     return c
 

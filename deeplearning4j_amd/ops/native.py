@@ -46,11 +46,11 @@ def load():
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = c_int
-    for name, args in _EXTRA_SIGS.items():
+    for name, (args, restype) in _EXTRA_SIGS.items():
         if hasattr(lib, name):
             f = getattr(lib, name)
             f.argtypes = args
-            f.restype = c_int
+            f.restype = restype
     _lib = lib
     return lib
 
@@ -58,12 +58,12 @@ def load():
 _EXTRA_SIGS = {}
 
 
-def register_sig(name, args):
-    _EXTRA_SIGS[name] = args
+def register_sig(name, args, restype=c_int):
+    _EXTRA_SIGS[name] = (args, restype)
     if _lib is not None and hasattr(_lib, name):
         f = getattr(_lib, name)
         f.argtypes = args
-        f.restype = c_int
+        f.restype = restype
 
 
 def _stream():

@@ -66,6 +66,21 @@ def run(fn, *keep):
     return r
 
 
+class suspended:
+    """Run a block with the overlap stream off (every ``run`` executes inline on the caller's stream). Used while
+    the conv layer times candidate kernels on scratch buffers: a candidate sent to the side stream would outlive
+    its scratch outputs and escape the main-stream timing events."""
+
+    def __enter__(self):
+        self._st = getattr(_tl, "st", None)
+        _tl.st = None
+        return self
+
+    def __exit__(self, *exc):
+        _tl.st = self._st
+        return False
+
+
 def join():
     st = getattr(_tl, "st", None)
     if st is not None and st["pending"]:

@@ -1,0 +1,111 @@
+"""Round-3 implicit-GEMM conv tile engine (csrc/conv_gemm.hip): every tile variant, forward and stride-1
+backward-data, against a plain fp32 torch reference; BatchNorm tile statistics from its epilogue against a separate
+pass; per-shape variant choice actually used by the conv layer path (run on MI355X)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deeplearning4j_amd.ops import conv_native, native
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # N, C, H, W, K, R, S, stride, pad4 (t, b, l, r), dilation
+    (2, 64, 9, 9, 64, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (3, 128, 7, 7, 136, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (2, 64, 11, 13, 256, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+    (2, 192, 10, 10, 72, 3, 3, (2, 2), (1, 1, 1, 1), (1, 1)),
+    (1, 64, 12, 12, 64, 3, 3, (1, 1), (2, 2, 2, 2), (2, 2)),
+    (2, 64, 8, 8, 512, 5, 5, (1, 1), (2, 2, 2, 2), (1, 1)),
+    (5, 128, 6, 5, 128, 3, 3, (1, 1), (0, 1, 0, 1), (1, 1)),
+]
+
+
+def _nv():
+    return native.load().dl4j_conv_v3_num_variants()
+
+
+def _data(case, seed=3):
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, C, H, W, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, S, generator=g) * 0.1).cuda().bfloat16()
+    b = torch.randn(K, generator=g).cuda()
+    return x, w, b
+
+
+def _ref(x, w, b, stride, pad4, dil):
+    return F.conv2d(F.pad(x.float(), (pad4[2], pad4[3], pad4[0], pad4[1])), w.float(), b, stride, dilation=dil)
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max abs err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_v3_forward_every_variant(cuda, case):
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    x, w, b = _data(case)
+    yr = _ref(x, w, b, stride, pad4, dil)
+    OH, OW = yr.shape[2], yr.shape[3]
+    conv_native.bump_version()
+    krsc, _ = conv_native._relayout(w, True, False)
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dil[0], dil[1], OH, OW)
+    for v in range(_nv()):
+        y = torch.full((N, K, OH, OW), float("nan"), device=cuda).bfloat16().contiguous(
+            memory_format=torch.channels_last)
+        ts = conv_native._stats_buf(v, N * OH * OW, K, x.device)
+        rc = conv_native._fwd_launch(v, x, krsc, b, y, geom, 0.0, ts)
+        assert rc == 1, (v, rc)
+        torch.cuda.synchronize()
+        _close(y, yr, 2e-2)
+        # the epilogue statistics reduce to the batch mean / biased variance of the stored bf16 outputs
+        P = ts.shape[1]
+        rows = y.permute(0, 2, 3, 1).reshape(-1, K).float()
+        M = rows.shape[0]
+        cnt = torch.tensor([min(64, M - 64 * p) for p in range(P)], device=cuda, dtype=torch.float32)[:, None]
+        s1, s2, sh = ts[0], ts[1], ts[2]
+        mean = (s1 + cnt * sh).sum(0) / M
+        ex2 = (s2 + 2 * sh * s1 + cnt * sh * sh).sum(0) / M
+        _close(mean, rows.mean(0), 1e-3)
+        _close(ex2 - mean * mean, rows.var(0, unbiased=False), 1e-2)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[7] == (1, 1) and c[9] == (1, 1)])
+@pytest.mark.parametrize("accum", [False, True])
+def test_v3_backward_data_every_variant(cuda, case, accum):
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    if K % 64:
+        pytest.skip("transposed conv needs K % 64 == 0 on the v3 engine")
+    x, w, b = _data(case)
+    xr = x.float().requires_grad_(True)
+    yr = _ref(xr, w, None, stride, pad4, dil)
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(yr.shape, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    OH, OW = dy.shape[2], dy.shape[3]
+    conv_native.bump_version()
+    _, flip = conv_native._relayout(w, False, True)
+    gb = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
+    base = torch.randn(N, C, H, W, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    for v in range(_nv()):
+        dx = base.clone() if accum else torch.empty_like(base)
+        rc = conv_native._fwd_launch(v, dy, flip, None, dx, gb, 1.0 if accum else 0.0, None)
+        assert rc == 0, (v, rc)
+        torch.cuda.synchronize()
+        want = xr.grad + (base.float() if accum else 0)
+        _close(dx, want, 2e-2)
+
+
+def test_layer_path_picks_a_variant_and_matches(cuda):
+    case = (4, 64, 14, 14, 64, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1))
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    x, w, b = _data(case)
+    conv_native._V3_CHOICE.clear()
+    conv_native.bump_version()
+    y = conv_native.conv2d_fwd(x, w, b, stride, pad4, dil, want_stats=True)
+    assert any(k[0] == "fwd" for k in conv_native._V3_CHOICE), "the v3 chooser never ran"
+    _close(y, _ref(x, w, b, stride, pad4, dil), 2e-2)
+    assert hasattr(y, "_bn_tile_stats")

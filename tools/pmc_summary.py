@@ -12,6 +12,7 @@ import os
 
 
 def short(n):
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
     return n.split("(")[0][:70]
 
 
@@ -41,11 +42,12 @@ def main():
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
     times, calls = collections.defaultdict(float), collections.Counter()
-    for p in sorted(glob.glob(os.path.join(a.root, "p*"))):
+    passes = sorted(glob.glob(os.path.join(a.root, "p*"))) or [a.root]    # one pass directory, or p1/p2/p3
+    for p in passes:
         v, t, c = load_pass(p)
         for k, d in v.items():
             merged[k].update(d)
-        if p.endswith("p1"):
+        if p.endswith("p1") or p == a.root:
             times, calls = t, c
     total = sum(times.values()) or 1.0
     # MIOpen's find-mode benchmarking kernels (first call of a new shape) are not part of the steady state
@@ -58,7 +60,10 @@ def main():
         busy = d.get("SQ_BUSY_CYCLES", 0.0)
         gui = d.get("GRBM_GUI_ACTIVE", 0.0)
         mfma = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
-        tf = d.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512 / ns / 1e3 if ns else 0.0
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in d:
+            tf = d["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / ns / 1e3 if ns else 0.0
+        else:   # MFMA busy cycles (all SIMDs) x 1024 dense bf16 FLOP per SIMD-cycle (32x32x16 and 16x16x32 alike)
+            tf = mfma * 1024 / ns / 1e3 if ns else 0.0
         peak = 100.0 * tf / 2500.0                       # dense bf16 MFMA peak of an MI355X (no sparsity)
         lds_c = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, d.get("SQ_INSTS_LDS", 0.0))
         hbm = (d.get("FETCH_SIZE", 0.0) + d.get("WRITE_SIZE", 0.0)) * 1024 / ns if ns else 0.0
