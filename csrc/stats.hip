@@ -142,27 +142,36 @@ DL4J_API int dl4j_segment_stats(int dtype, const void* x, const long long* off, 
 }
 
 // ------------------------------------------------------------------------------------------------------
-// Column sums of a row-major [M, C] bf16/fp32 matrix into fp32 out[C] (conv bias gradient on the library
-// conv path: dy in channels-last is exactly such a matrix). Each thread owns 8 consecutive channels (one 16-byte
-// load for bf16) of a row; a block sweeps rows in a grid-stride loop, reduces through LDS and issues one atomic
-// per channel. Requires C % 8 == 0; channels beyond 2048 are split over blockIdx.y chunks of 2048 (also the
-// transformer bias gradients: 768 / 2304 / 3072 columns).
+// Column sums of a row-major [M, C] bf16/fp16/fp32 matrix into fp32 out[C] (conv / dense bias gradients: dy in
+// channels-last is exactly such a matrix). Each thread owns 8 consecutive channels (one 16-byte load for bf16) of a
+// row; a block sweeps rows in a grid-stride loop and reduces through LDS into its own partial row part[block][C]
+// (plain stores); channel_sum_reduce then sums the partial rows in block order. No float atomics: bitwise
+// reproducible (DL4J_AMD_DETERMINISTIC data-parallel equivalence). Requires C % 8 == 0; channels beyond 2048 are
+// split over blockIdx.y chunks of 2048 (transformer bias gradients: 768 / 2304 / 3072 columns).
 // ------------------------------------------------------------------------------------------------------
 namespace {
 template <typename T>
 __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ xfull, long long M, int ld,
-                                                          float* __restrict__ outfull) {
+                                                          float* __restrict__ part) {
   extern __shared__ float red[];                         // [rows_per_iter][C]
   const int c0 = blockIdx.y * 2048;
   const int C = min(2048, ld - c0);
   const T* x = xfull + c0;
-  float* out = outfull + c0;
   const int groups = C / 8;                              // threads per row
   const int rows_per_iter = 256 / groups;
   const int g = threadIdx.x % groups, r0 = threadIdx.x / groups;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < rows_per_iter) {
-    for (long long r = (long long)blockIdx.x * rows_per_iter + r0; r < M; r += (long long)gridDim.x * rows_per_iter) {
+    long long r = (long long)blockIdx.x * rows_per_iter + r0;
+    const long long step = (long long)gridDim.x * rows_per_iter;
+    for (; r + step < M; r += 2 * step) {                // two independent 16-byte loads in flight
+      float v[8], w[8];
+      Vec8<T>::load(x + r * ld + g * 8, v);
+      Vec8<T>::load(x + (r + step) * ld + g * 8, w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j] + w[j];
+    }
+    if (r < M) {
       float v[8];
       Vec8<T>::load(x + r * ld + g * 8, v);
 #pragma unroll
@@ -174,26 +183,56 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ 
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
     for (int k = 0; k < rows_per_iter; ++k) s += red[k * C + c];
-    atomicAdd(out + c, s);
+    part[(long long)blockIdx.x * ld + c0 + c] = s;
   }
+}
+
+// partial rows [nblk][C] -> out[C]: a block owns 64 channels, its 4 row groups sum every 4th partial row in a fixed
+// order and combine through LDS (the same shape as bn_reduce_rows; one thread per channel serialised 512 rows).
+__global__ __launch_bounds__(256) void channel_sum_reduce(const float* __restrict__ part, int nblk, int C,
+                                                          float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    int b = grp;
+    for (; b + 4 < nblk; b += 8) {
+      s0 += part[(long long)b * C + c];
+      s1 += part[(long long)(b + 4) * C + c];
+    }
+    if (b < nblk) s0 += part[(long long)b * C + c];
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = s0 + s1;
+  __syncthreads();
+  if (grp == 0 && c < C) out[c] = (red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192]);
+}
+
+int channel_sum_blocks(long long M, int C) {
+  const int Cc = C < 2048 ? C : 2048;                    // widest chunk; the last chunk may be narrower
+  const int rows_per_iter = 256 / (Cc / 8);
+  long long blocks = (M + rows_per_iter * 32 - 1) / (rows_per_iter * 32);
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
 }
 }  // namespace
 
-DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, float* out, hipStream_t stream) {
-  if (C % 8 != 0 || M <= 0) return -1;
-  if (hipMemsetAsync(out, 0, sizeof(float) * C, stream) != hipSuccess) return -3;
-  const int Cc = C < 2048 ? C : 2048;                    // widest chunk; the last chunk may be narrower
-  const int rows_per_iter = 256 / (Cc / 8);
-  long long blocks = (M + rows_per_iter * 16 - 1) / (rows_per_iter * 16);
-  if (blocks > 2048) blocks = 2048;
-  if (blocks < 1) blocks = 1;
+// Workspace floats dl4j_channel_sum needs for an [M, C] input.
+DL4J_API long long dl4j_channel_sum_ws_floats(long long M, int C) { return (long long)channel_sum_blocks(M, C) * C; }
+
+// ws: >= dl4j_channel_sum_ws_floats(M, C) fp32 scratch.
+DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, float* out, float* ws, hipStream_t stream) {
+  if (C % 8 != 0 || M <= 0 || !ws) return -1;
+  const int blocks = channel_sum_blocks(M, C);
   const size_t lds = sizeof(float) * 256 * 8;             // >= rows_per_iter * chunk width for every chunk
   const dim3 grid((unsigned)blocks, (C + 2047) / 2048);
   if (dtype == 1)
-    hipLaunchKernelGGL(channel_sum_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, M, C, out);
+    hipLaunchKernelGGL(channel_sum_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, M, C, ws);
   else if (dtype == 2)
-    hipLaunchKernelGGL(channel_sum_kernel<f16>, grid, dim3(256), lds, stream, (const f16*)x, M, C, out);
+    hipLaunchKernelGGL(channel_sum_kernel<f16>, grid, dim3(256), lds, stream, (const f16*)x, M, C, ws);
   else
-    hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), lds, stream, (const float*)x, M, C, out);
+    hipLaunchKernelGGL(channel_sum_kernel<float>, grid, dim3(256), lds, stream, (const float*)x, M, C, ws);
+  hipLaunchKernelGGL(channel_sum_reduce, dim3((C + 63) / 64), dim3(256), 0, stream, ws, blocks, C, out);
   return (int)hipGetLastError();
 }

@@ -39,6 +39,9 @@ native.register_sig("dl4j_conv_fwd_v3", [c_int, c_void_p, c_void_p, c_void_p, c_
                     [ctypes.c_float, c_void_p, c_int, c_void_p])
 native.register_sig("dl4j_conv_v3_num_variants", [])
 native.register_sig("dl4j_conv_v3_default_variant", [c_ll, c_int])
+native.register_sig("dl4j_conv_wrw_v3_num_variants", [])
+native.register_sig("dl4j_conv_wrw_v3_ws_floats", [c_int] * 9 + [ctypes.POINTER(c_int)], restype=c_ll)
+native.register_sig("dl4j_conv_wrw_v3", [c_int] + [c_void_p] * 5 + [c_int] * 17 + [c_void_p])
 
 # Optional per-shape override of the weight-gradient split count (tuning): {(N,H,W,C,K,R,S,stride): splits}
 WRW_SPLITS = {}
@@ -380,16 +383,16 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
                                                   channels_last=True)
             # transposed conv: "input" dY (OH x OW x K), flipped CRSK weights, pad' = R-1-pad, output H x W x C
-            gb = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
+            geo_b = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
 
             def bwd_launch(var, out, _ts):
                 if var >= 0:
-                    return _fwd_launch(var, dy, flip, None, out, gb, 1.0 if acc else 0.0, None)
+                    return _fwd_launch(var, dy, flip, None, out, geo_b, 1.0 if acc else 0.0, None)
                 return lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(out), N, H, W, C, K, R, S, pad4[0],
                                                  pad4[2], OH, OW, int(acc), _stream())
             v = -1
             if _v3_ok(K, C, R, S):
-                v = _v3_pick(("bwd_acc" if acc else "bwd", gb), bwd_launch, dx, lambda var: None)
+                v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b), bwd_launch, dx, lambda var: None)
             rc = bwd_launch(v, dx, None)
             native._check(rc, "conv_bwd_data_s1")
         elif pure_1x1 and stride[0] == stride[1]:
@@ -462,6 +465,74 @@ def _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need
         return dW_out, db_out
     direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
     dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW)
+    v = _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed) if V3 else -1
+    if v >= 0:
+        # round-3 tile engine: per-split fp32 slabs + fixed-order reduce into the DL4J layout (deterministic)
+        db_out = dbt = None
+        if need_db:
+            directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
+            dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
+            db_out = None if directb else dbt
+        native._check(_wrw_v3_launch(v, x, dy, dWt, geom, dbt), "conv_wrw_v3")
+        return (None if direct else dWt), db_out
+    return _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb,
+                          grads_zeroed, dWt, direct)
+
+
+_WRW_CHOICE = {}
+
+
+def _wrw_v3_launch(var, x, dy, dWt, geom, db=None):
+    lib = native.load()
+    N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
+    sp = ctypes.c_int(0)
+    nf = lib.dl4j_conv_wrw_v3_ws_floats(N, C, K, R, S, OH, OW, var, 0, ctypes.byref(sp))
+    ws = _det_scratch(nf, x.device)
+    return lib.dl4j_conv_wrw_v3(1, _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, 0, _stream())
+
+
+def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
+    """Per-shape weight-gradient kernel: the first eager call times the round-3 tile variants and the round-2
+    atomic kernel (on scratch outputs, inline on this stream) and keeps the fastest. Deterministic mode only
+    considers the round-3 engine (slab reduce, no atomics). Under HIP-graph capture: remembered choice or variant 0."""
+    det = deterministic()
+    key = (geom, det)
+    v = _WRW_CHOICE.get(key)
+    if v is not None:
+        return v
+    if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
+        return 0
+    lib = native.load()
+    N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
+    scratch = torch.empty_like(dWt)
+    sdb = torch.empty(K, dtype=torch.float32, device=dWt.device) if need_db else None
+    cands = list(range(lib.dl4j_conv_wrw_v3_num_variants())) + ([] if det else [-1])
+    best, bt = None, None
+    with side_stream.suspended():
+        for var in cands:
+            if var >= 0:
+                def run(var=var):
+                    return _wrw_v3_launch(var, x, dy, scratch, geom, sdb)
+            else:
+                def run():
+                    return _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, (sh, sw), (ph, 0, pw, 0), (dh, dw),
+                                          need_db, scratch, sdb, False, scratch, True) and 0
+            if (run() or 0) != 0:
+                continue
+            t = _timed(run, reps=3)
+            if bt is None or t < bt:
+                best, bt = var, t
+    v = _WRW_CHOICE[key] = best if best is not None else -1
+    return v
+
+
+def _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb, grads_zeroed, dWt,
+                   direct):
+    """Round-2 weight-gradient kernel (csrc/conv_igemm.hip): fp32 atomics into a KRSC workspace + permute, or the
+    deterministic per-split slab variant."""
+    lib = native.load()
+    db_out = None
     if deterministic():
         # per-split fp32 slabs + fixed-order reduce straight into the DL4J layout: bitwise reproducible
         dbt = None

@@ -471,9 +471,24 @@ def channel_sum(rows, out=None):
     if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] % 8:
         return None
     lib = load()
-    register_sig("dl4j_channel_sum", [c_int, c_void_p, c_ll, c_int, c_void_p, c_void_p])
+    register_sig("dl4j_channel_sum", [c_int, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p])
+    register_sig("dl4j_channel_sum_ws_floats", [c_ll, c_int], restype=c_ll)
     if out is None or not (out.is_contiguous() and out.dtype == torch.float32 and out.numel() == rows.shape[1]):
         out = torch.empty(rows.shape[1], dtype=torch.float32, device=rows.device)
-    _check(lib.dl4j_channel_sum(dt, _ptr(rows), rows.shape[0], rows.shape[1], _ptr(out), c_void_p(_stream())),
-           "channel_sum")
+    ws = _scratch(lib.dl4j_channel_sum_ws_floats(rows.shape[0], rows.shape[1]), rows.device)
+    _check(lib.dl4j_channel_sum(dt, _ptr(rows), rows.shape[0], rows.shape[1], _ptr(out), _ptr(ws),
+                                c_void_p(_stream())), "channel_sum")
     return out
+
+
+_scratch_bufs = {}
+
+
+def _scratch(nfloats, device):
+    """Growing fp32 scratch per (device, stream) for kernels that reduce through partial rows. A stream's work is
+    ordered, so consecutive launches may reuse it; the overlap stream gets its own."""
+    key = (str(device), torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0)
+    t = _scratch_bufs.get(key)
+    if t is None or t.numel() < nfloats:
+        t = _scratch_bufs[key] = torch.empty(max(int(nfloats), 1 << 16), dtype=torch.float32, device=device)
+    return t

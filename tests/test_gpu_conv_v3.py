@@ -109,3 +109,43 @@ def test_layer_path_picks_a_variant_and_matches(cuda):
     assert any(k[0] == "fwd" for k in conv_native._V3_CHOICE), "the v3 chooser never ran"
     _close(y, _ref(x, w, b, stride, pad4, dil), 2e-2)
     assert hasattr(y, "_bn_tile_stats")
+
+
+WRW_CASES = [
+    (2, 64, 9, 9, 64, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (3, 128, 7, 7, 136, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (2, 64, 11, 13, 256, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+    (2, 192, 10, 10, 72, 3, 3, (2, 2), (1, 1, 1, 1), (1, 1)),
+    (1, 64, 12, 12, 64, 3, 3, (1, 1), (2, 2, 2, 2), (2, 2)),
+    (4, 256, 8, 8, 64, 1, 1, (2, 2), (0, 0, 0, 0), (1, 1)),
+    (2, 8, 23, 23, 64, 7, 7, (2, 2), (3, 3, 3, 3), (1, 1)),
+]
+
+
+@pytest.mark.parametrize("case", WRW_CASES)
+def test_v3_weight_gradient_every_variant(cuda, case):
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    x, w, _ = _data(case)
+    wr = w.float().requires_grad_(True)
+    yr = _ref(x, wr, None, stride, pad4, dil)
+    g = torch.Generator().manual_seed(8)
+    dy = torch.randn(yr.shape, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    OH, OW = dy.shape[2], dy.shape[3]
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dil[0], dil[1], OH, OW)
+    nv = native.load().dl4j_conv_wrw_v3_num_variants()
+    outs = []
+    db_ref = dy.float().sum(dim=(0, 2, 3))
+    for v in range(nv):
+        dW = torch.full((K, C, R, S), 3.0, device=cuda)            # written, not accumulated
+        db = torch.full((K,), 3.0, device=cuda)
+        assert conv_native._wrw_v3_launch(v, x, dy, dW, geom, db if v % 2 else None) == 0
+        torch.cuda.synchronize()
+        _close(dW, wr.grad, 1e-2)
+        if v % 2:
+            _close(db, db_ref, 1e-3)
+        outs.append(dW)
+    again = torch.empty_like(outs[0])
+    conv_native._wrw_v3_launch(0, x, dy, again, geom)
+    torch.cuda.synchronize()
+    assert torch.equal(again, outs[0])                               # slab reduce: bitwise reproducible

@@ -5,6 +5,7 @@ import sys
 
 import torch
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
 from test_gpu_conv_safety import _data, _graph, _grad  # noqa: E402
 
