@@ -38,6 +38,9 @@ def main():
                          "are not capturable, i.e. gloo)")
     ap.add_argument("--comm-dtype", default=os.environ.get("BENCH_COMM_DTYPE", "fp32"), choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype for N > 1")
+    ap.add_argument("--comm", default=os.environ.get("BENCH_COMM", "torch"), choices=["torch", "rccl"],
+                    help="N > 1 transport: torch.distributed's RCCL process group, or the framework's own RCCL "
+                         "communicator (parallel/rccl.py, ncclCommInitRank with the id exchanged through the store)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -56,7 +59,11 @@ def main():
     acc = None
     if world > 1:
         # bucketed RCCL all-reduce overlapped with backward; captured into the step's HIP graph (nccl backend)
-        acc = AllReduceGradientsAccumulator(dtype=args.comm_dtype)
+        comm = None
+        if args.comm == "rccl" and device.type == "cuda":
+            from deeplearning4j_amd.parallel.rccl import RcclComm
+            comm = RcclComm.from_process_group(device)
+        acc = AllReduceGradientsAccumulator(dtype=args.comm_dtype, comm=comm)
         acc.broadcast_params(net)
         net.setGradientsAccumulator(acc)
 
@@ -110,7 +117,7 @@ def main():
             "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (random 224x224x3 images, one-hot labels; random-init weights)",
             "config": {"model": model_name, "variant": args.variant, "global_batch": B * world, "per_gpu_batch": B,
-                       "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
+                       "seq_len": None, "image_size": 224, "parallelism": f"dp{world}", "comm": args.comm,
                        "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                        "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
                        "final_score": final_score},

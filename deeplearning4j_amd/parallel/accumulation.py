@@ -42,8 +42,7 @@ class AllReduceGradientsAccumulator:
     captured into a HIP graph when the backend is nccl (RCCL supports stream capture).
     """
 
-    def __init__(self, bucket_mb=None, average=False, dtype=None, force=None):
-        self.world_size = world_size()
+    def __init__(self, bucket_mb=None, average=False, dtype=None, force=None, comm=None):
         self.bucket_bytes = int(float(bucket_mb or os.environ.get("DL4J_AMD_BUCKET_MB", 32)) * (1 << 20))
         self.average = average
         if isinstance(dtype, str):
@@ -51,14 +50,34 @@ class AllReduceGradientsAccumulator:
         self.comm_dtype = dtype
         if force is None:
             force = os.environ.get("DL4J_AMD_FORCE_COLLECTIVES", "0") == "1"
-        self.active = dist.is_available() and dist.is_initialized() and (self.world_size > 1 or bool(force))
+        self.force = bool(force)
+        # comm: an RcclComm / LoopbackComm (parallel/rccl.py) used instead of the torch.distributed default group
+        self.comm = comm
         self._buckets = None
+        self._staging = None
         self._pending = []
         self._next = 0
 
+    # ``active`` / ``world_size`` are looked up at use, not frozen at construction: an accumulator built before
+    # init_distributed() must still all-reduce once the group exists.
+    @property
+    def world_size(self):
+        return self.comm.nranks if self.comm is not None else world_size()
+
+    @property
+    def active(self):
+        if self.comm is not None:
+            return self.comm.nranks > 1 or self.force
+        return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or self.force)
+
     def capturable(self):
-        """True when the collectives can live inside a captured HIP graph (nccl/RCCL backend, or none issued)."""
-        return (not self.active) or dist.get_backend() == "nccl"
+        """True when the collectives can live inside a captured HIP graph: RCCL (through torch's nccl backend or a
+        direct RcclComm) is stream-ordered; a host loopback or gloo is not."""
+        if not self.active:
+            return True
+        if self.comm is not None:
+            return type(self.comm).__name__ == "RcclComm"
+        return dist.get_backend() == "nccl"
 
     def _plan(self, net):
         n = net.flattenedGradients.numel()
@@ -73,6 +92,11 @@ class AllReduceGradientsAccumulator:
             end = start
         self._buckets = b
         self._net = net
+        self._staging = None
+        if self.comm_dtype is not None and self.comm_dtype != net.flattenedGradients.dtype:
+            # persistent wire-format buffers, one per bucket (stable addresses for HIP graphs, no per-step alloc)
+            self._staging = [torch.empty(e - s, dtype=self.comm_dtype, device=net.flattenedGradients.device)
+                             for s, e in b]
 
     def begin_backward(self, net):
         if not self.active:
@@ -82,13 +106,20 @@ class AllReduceGradientsAccumulator:
         self._pending = []
         self._next = 0
 
-    def _issue(self, g, s, e):
+    def _issue(self, g, i):
+        s, e = self._buckets[i]
         seg = g[s:e]
-        if self.comm_dtype is not None and self.comm_dtype != seg.dtype:
-            tmp = seg.to(self.comm_dtype)
-            self._pending.append((dist.all_reduce(tmp, op=dist.ReduceOp.SUM, async_op=True), tmp, seg))
-        else:
-            self._pending.append((dist.all_reduce(seg, op=dist.ReduceOp.SUM, async_op=True), None, None))
+        tmp = self._staging[i] if self._staging is not None else None
+        if tmp is not None:
+            tmp.copy_(seg)
+        buf = tmp if tmp is not None else seg
+        if self.comm is not None:
+            # stream-ordered on the current stream: later kernels see the result, nothing to wait for on the host
+            self.comm.all_reduce(buf, "sum")
+            if tmp is not None:
+                seg.copy_(tmp)
+            return
+        self._pending.append((dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True), tmp, seg))
 
     joins_side_stream = True   # grad_ready joins ops/side_stream itself, only when a bucket is issued
 
@@ -103,8 +134,7 @@ class AllReduceGradientsAccumulator:
                 from ..ops import side_stream
                 side_stream.join()
                 joined = True
-            s, e = self._buckets[self._next]
-            self._issue(g, s, e)
+            self._issue(g, self._next)
             self._next += 1
 
     def reduce_gradients(self, net):
@@ -132,16 +162,23 @@ class AllReduceGradientsAccumulator:
         net.sync_shadow()
 
 
-def average_params_and_state(net, average_updaters=True):
-    """AVERAGING mode (reference ParallelWrapper averageAndPropagate, PW:ParallelWrapper.java:316-376)."""
-    if not is_dist():
+def average_params_and_state(net, average_updaters=True, comm=None):
+    """AVERAGING mode (reference ParallelWrapper averageAndPropagate, PW:ParallelWrapper.java:316-376): all-reduce
+    (sum) of the flat params and updater state, then 1/W. ``comm``: an RcclComm / LoopbackComm instead of the
+    torch.distributed default group."""
+    if comm is None and not is_dist():
         return
-    w = world_size()
-    dist.all_reduce(net.flattenedParams, op=dist.ReduceOp.SUM)
-    net.flattenedParams.div_(w)
+    w = comm.nranks if comm is not None else world_size()
+
+    def red(t):
+        if comm is not None:
+            comm.all_reduce(t, "sum")
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.div_(w)
+    red(net.flattenedParams)
     if average_updaters and net.updater.state is not None and net.updater.state.numel() > 0:
-        dist.all_reduce(net.updater.state, op=dist.ReduceOp.SUM)
-        net.updater.state.div_(w)
+        red(net.updater.state)
     net.sync_shadow()
 
 

@@ -1,0 +1,259 @@
+"""In-process ParallelWrapper: one host thread per device, fed round-robin from a streaming iterator.
+
+Reference: PW:ParallelWrapper.java:123-137 (worker threads pinned to devices), :467-565 (the fit loop: the master
+round-robins DataSets into per-worker queues of capacity 1, waits for all workers after every ``workers`` batches,
+averages every ``averagingFrequency`` rounds), PW:trainer/DefaultTrainer.java:254-311 (replica creation: worker 0
+trains the root model, the others train copies), :396-416 (worker exceptions rethrown to the master).
+
+MI355X design:
+  * replicas live on GPUs 0..N-1 of this process; their communicators come from ``ncclCommInitAll`` (RcclComm,
+    parallel/rccl.py) and every collective is enqueued on the worker's own HIP stream; on a host without N GPUs the
+    replicas run on the CPU over the in-process LoopbackComm (same code path, used by the CPU tests);
+  * SHARED_GRADIENTS: synchronous DP — each worker's bucketed gradient all-reduce runs during its backward
+    (AllReduceGradientsAccumulator with the worker's communicator), then the update with the global minibatch;
+  * AVERAGING: local steps, parameters (+ updater state) all-reduced and divided by N every k rounds;
+  * streaming: the master pulls one round (N batches) at a time from the iterator and hands batch i of the round to
+    worker i through a queue of capacity ``prefetchBuffer // N`` (>= 1); at most ``prefetchBuffer + 2N`` batches
+    (queued, in training, and the round being handed out) exist at once however long the iterator is. A trailing partial round is dropped (every worker must run the
+    same number of collectives);
+  * failure: a worker exception aborts every communicator (waiting ranks raise instead of hanging), the other
+    workers are drained and the master re-raises it.
+Listeners fire on worker 0, i.e. on the caller's own model (the reference attaches them to the root model too).
+"""
+import logging
+import queue
+import threading
+
+import torch
+
+from ..datasets.dataset import DataSet, MultiDataSet
+from .accumulation import AllReduceGradientsAccumulator, average_params_and_state
+
+log = logging.getLogger("deeplearning4j_amd")
+
+_STOP = object()
+
+
+def _replica(model, device):
+    """A copy of ``model`` (config, parameters, updater state) on ``device``."""
+    import copy
+    net = type(model)(copy.deepcopy(model.conf))
+    net.init(model.params().detach().to(device).clone(), device=device)
+    st = model.updater.getStateViewArray()
+    if st is not None and st.numel() > 0:
+        net.updater.setStateViewArray(st.detach().to(device).clone())
+    net.conf.iterationCount = model.conf.iterationCount
+    net.conf.epochCount = model.conf.epochCount
+    return net
+
+
+def _fit_one(m, ds):
+    if isinstance(ds, MultiDataSet):
+        m._fit_batch(ds.features, ds.labels, ds.featuresMasks, ds.labelsMasks)
+    elif isinstance(ds, DataSet):
+        if type(m).__name__ == "ComputationGraph":
+            m._fit_batch([ds.features], [ds.labels], None if ds.featuresMask is None else [ds.featuresMask],
+                         None if ds.labelsMask is None else [ds.labelsMask])
+        else:
+            m._fit_batch(ds.features, ds.labels, ds.featuresMask, ds.labelsMask)
+    else:
+        raise TypeError(f"unsupported batch type {type(ds)}")
+
+
+def devices_for(n):
+    """GPUs 0..n-1 when this process sees at least n, else the CPU for every worker."""
+    if torch.cuda.is_available() and torch.cuda.device_count() >= n:
+        return [torch.device("cuda", i) for i in range(n)]
+    return [torch.device("cpu")] * n
+
+
+def make_comms(devs):
+    if devs[0].type == "cuda":
+        from .rccl import RcclComm
+        return RcclComm.init_all([d.index for d in devs])
+    from .rccl import LoopbackComm
+    return LoopbackComm.create(len(devs))
+
+
+class InProcessTrainer:
+    """Owns the replicas, communicators and worker threads of one ParallelWrapper (created on first fit)."""
+
+    def __init__(self, wrapper, devices=None, comms=None):
+        self.w = wrapper
+        n = int(wrapper.workers)
+        self.devices = list(devices) if devices is not None else devices_for(n)
+        m = wrapper.model
+        if not m.initCalled:
+            m.init(device=self.devices[0])
+        self.comms = list(comms) if comms is not None else make_comms(self.devices)
+        # worker 0 trains the caller's model (DefaultTrainer.java:248-283); the rest train copies
+        self.models = [m] + [_replica(m, d) for d in self.devices[1:]]
+        from .wrapper import TrainingMode
+        self.shared = wrapper.trainingMode in (TrainingMode.SHARED_GRADIENTS,)
+        if self.shared:
+            for net, c in zip(self.models, self.comms):
+                net.setGradientsAccumulator(AllReduceGradientsAccumulator(wrapper.bucket_mb, comm=c))
+        self.queues = [queue.Queue(maxsize=max(1, int(wrapper.prefetchBuffer) // n)) for _ in range(n)]
+        self.errors = []
+        self.rounds_done = [0] * n
+        self.cv = threading.Condition()
+        self.max_live = 0           # most batches alive at once (tests check the streaming bound)
+        self._live = 0
+        self._threads = []
+
+    # ------------------------------------------------------------------------------------------------ workers
+    def _run(self, i):
+        net, comm, q, dev = self.models[i], self.comms[i], self.queues[i], self.devices[i]
+        from .wrapper import TrainingMode
+        avg = self.w.trainingMode == TrainingMode.AVERAGING
+        k = self.w.averagingFrequency
+        try:
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+            while True:
+                item = q.get()
+                if item is _STOP:
+                    break
+                ds, rnd = item
+                _fit_one(net, ds)                   # the network moves the batch to its device
+                with self.cv:
+                    self._live -= 1
+                if avg and (rnd + 1) % k == 0:
+                    average_params_and_state(net, self.w.averageUpdaters, comm=comm)
+                if dev.type == "cuda":
+                    torch.cuda.current_stream(dev).synchronize()
+                with self.cv:
+                    self.rounds_done[i] = rnd + 1
+                    self.cv.notify_all()
+        except BaseException as e:          # noqa: BLE001 — propagated to the master
+            with self.cv:
+                self.errors.append((i, e))
+                self.cv.notify_all()
+            for c in self.comms:
+                c.abort()
+            while True:                     # drain so the master's puts never block forever
+                try:
+                    if q.get(timeout=0.05) is _STOP:
+                        break
+                except queue.Empty:
+                    if not any(t.is_alive() for t in self._threads if t is not threading.current_thread()):
+                        break
+
+    def _start(self):
+        if self._threads:
+            return
+        for i in range(len(self.models)):
+            t = threading.Thread(target=self._run, args=(i,), name=f"dl4j-pw-worker-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
+
+    def _raise_if_failed(self):
+        if self.errors:
+            i, e = self.errors[0]
+            raise RuntimeError(f"ParallelWrapper worker {i} failed: {e!r}") from e
+
+    # ------------------------------------------------------------------------------------------------ master
+    def _put(self, i, item):
+        while True:
+            self._raise_if_failed()
+            try:
+                self.queues[i].put(item, timeout=0.1)
+                return
+            except queue.Full:
+                continue
+
+    def fit(self, source, numEpochs=1):
+        n = len(self.models)
+        m = self.models[0]
+        self._start()
+        rnd = 0
+        try:
+            for _ in range(int(numEpochs)):
+                for l in m.listeners:
+                    if hasattr(l, "onEpochStart"):
+                        l.onEpochStart(m)
+                for batch_round in _rounds(source, n):
+                    with self.cv:
+                        self._live += n             # pulled from the iterator and not yet trained on
+                        self.max_live = max(self.max_live, self._live)
+                    for i, ds in enumerate(batch_round):
+                        self._put(i, (ds, rnd))
+                    rnd += 1
+                self._wait_rounds(rnd)
+                for net in self.models:
+                    net.incrementEpochCount()
+                for l in m.listeners:
+                    if hasattr(l, "onEpochEnd"):
+                        l.onEpochEnd(m)
+            from .wrapper import TrainingMode
+            if self.w.trainingMode == TrainingMode.AVERAGING and rnd % self.w.averagingFrequency != 0:
+                self._collective_all(lambda net, c: average_params_and_state(net, self.w.averageUpdaters, comm=c))
+        finally:
+            self.shutdown()
+        self._raise_if_failed()
+        return m
+
+    def _wait_rounds(self, rnd):
+        with self.cv:
+            while min(self.rounds_done) < rnd and not self.errors:
+                self.cv.wait(timeout=0.5)
+        self._raise_if_failed()
+
+    def _collective_all(self, fn):
+        """Run fn(model_i, comm_i) on every replica concurrently (collectives need all ranks in flight)."""
+        errs = []
+
+        def run(i):
+            try:
+                if self.devices[i].type == "cuda":
+                    torch.cuda.set_device(self.devices[i])
+                fn(self.models[i], self.comms[i])
+                if self.devices[i].type == "cuda":
+                    torch.cuda.current_stream(self.devices[i]).synchronize()
+            except BaseException as e:      # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=run, args=(i,)) for i in range(len(self.models))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    def shutdown(self):
+        for i, t in enumerate(self._threads):
+            if t.is_alive():
+                try:
+                    self.queues[i].put(_STOP, timeout=1.0)
+                except queue.Full:
+                    pass
+        for t in self._threads:
+            t.join(timeout=30)
+        self._threads = []
+
+
+def _rounds(source, n):
+    """Stream complete rounds of n batches from a DataSetIterator / MultiDataSetIterator / iterable; a trailing
+    partial round is dropped."""
+    if isinstance(source, (DataSet, MultiDataSet)):
+        source = [source]
+    if hasattr(source, "hasNext"):
+        if hasattr(source, "reset"):
+            source.reset()
+
+        def gen():
+            while source.hasNext():
+                yield source.next()
+        it = gen()
+    else:
+        it = iter(source)
+    buf = []
+    dropped = 0
+    for ds in it:
+        buf.append(ds)
+        if len(buf) == n:
+            yield buf
+            buf = []
+    dropped = len(buf)
+    if dropped:
+        log.info("ParallelWrapper: %d trailing batch(es) of an incomplete round of %d dropped", dropped, n)

@@ -63,8 +63,10 @@ class ParallelWrapper:
 
     def __init__(self, model, workers=None, prefetchBuffer=16, averagingFrequency=1, averageUpdaters=True,
                  reportScoreAfterAveraging=False, trainingMode=TrainingMode.SHARED_GRADIENTS,
-                 gradientsAccumulator=None, bucket_mb=None, trainerContext=None):
+                 gradientsAccumulator=None, bucket_mb=None, trainerContext=None, inProcess=None):
         self.model = model
+        self.inProcess = inProcess
+        self._inproc = None
         self.trainerContext = trainerContext
         self._trainer = None
         self.workers = workers or world_size()
@@ -116,6 +118,12 @@ class ParallelWrapper:
             self._kw.setdefault("trainingMode", TrainingMode.CUSTOM)
             return self
 
+        def inProcess(self, b=True):
+            """True: one host thread per device in this process (RCCL communicators from ncclCommInitAll, or the
+            host loopback on CPU); False: one child process per device (parallel/launcher.py). Default: threads."""
+            self._kw["inProcess"] = bool(b)
+            return self
+
         def bucketSizeMB(self, mb):
             self._kw["bucket_mb"] = mb
             return self
@@ -152,15 +160,32 @@ class ParallelWrapper:
                                                        self.averagingFrequency)
         self._prepared = True
 
-    def fit(self, source, numEpochs=1):
+    def fit(self, source, numEpochs=1, presharded=False):
         """Train on a DataSetIterator / MultiDataSetIterator (or a list of DataSets) for ``numEpochs``.
 
-        Called from one plain process with ``workers > 1`` (no process group): the wrapper launches one child
-        process per worker / GPU and trains there (parallel/launcher.py), then loads the result into ``model``."""
-        if not is_dist() and self.workers > 1 and self.trainerContext is None and self.accumulator is None and \
-                os.environ.get("DL4J_AMD_PW_SPAWN", "1") == "1":
-            from .launcher import spawn_fit
-            return spawn_fit(self, source, numEpochs)
+        Called from one plain process with ``workers > 1`` (no process group), by default the wrapper trains with
+        one host thread per device in this process (parallel/inprocess.py: streaming round-robin feed, RCCL
+        communicators from ncclCommInitAll; listeners fire on this model). ``inProcess(False)`` (or
+        DL4J_AMD_PW_SPAWN=1) launches one child process per device instead (parallel/launcher.py: batches are
+        streamed to the children over sockets; listeners do not run there). Under torchrun (a process group) every
+        rank runs this method on its rank-strided share of the batches."""
+        if not is_dist() and self.workers > 1 and self.trainerContext is None and self.accumulator is None:
+            spawn = self.inProcess is False or (self.inProcess is None and
+                                                os.environ.get("DL4J_AMD_PW_SPAWN", "0") == "1")
+            if spawn:
+                from .launcher import spawn_fit
+                return spawn_fit(self, source, numEpochs)
+            if self.trainingMode not in (TrainingMode.SHARED_GRADIENTS, TrainingMode.AVERAGING):
+                raise ValueError("in-process ParallelWrapper supports SHARED_GRADIENTS and AVERAGING; CUSTOM "
+                                 "accumulators / trainer contexts need one process per device (torchrun)")
+            from .inprocess import InProcessTrainer
+            if self._inproc is None:
+                self._inproc = InProcessTrainer(self)
+            try:
+                return self._inproc.fit(source, numEpochs)
+            except BaseException:
+                self._inproc = None         # aborted communicators are not reusable: rebuild on the next fit
+                raise
         self._prepare()
         m = self.model
         W, r = world_size(), rank()
@@ -168,8 +193,11 @@ class ParallelWrapper:
             for l in m.listeners:
                 if hasattr(l, "onEpochStart"):
                     l.onEpochStart(m)
-            items = _RankShard(source, r, W) if W > 1 else (source if not hasattr(source, "reset") else
-                                                            _RankShard(source, 0, 1))
+            if presharded:                 # a launcher child: the parent already sent only this rank's batches
+                items = source
+            else:
+                items = _RankShard(source, r, W) if W > 1 else (source if not hasattr(source, "reset") else
+                                                                _RankShard(source, 0, 1))
             for ds in items:
                 self._step(ds)
             for l in m.listeners:

@@ -249,3 +249,60 @@ def run_samediff_dp(rank, world, port, result_path):
         torch.save({"params": [t.clone() for t in gathered]}, result_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def simulate_averaging(make, batches, world, freq, epochs, average_updaters=True):
+    """Reference semantics of AVERAGING (PW:ParallelWrapper.java:316-376) computed in one process: ``world``
+    replicas from the same init, replica r fits batches r, r+W, ... of each epoch, and after every ``freq`` rounds
+    parameters (+ updater state) are replaced by their mean; a final average if the last round was not one."""
+    reps = [make() for _ in range(world)]
+    base = reps[0].params().clone()
+    for n in reps[1:]:
+        n.setParams(base.clone())
+    rnd = 0
+    nr = len(batches) // world
+    for _ in range(epochs):
+        for k in range(nr):
+            for r in range(world):
+                reps[r].fit(batches[k * world + r])
+            rnd += 1
+            if rnd % freq == 0:
+                _avg(reps, average_updaters)
+    if rnd % freq:
+        _avg(reps, average_updaters)
+    return reps[0].params().clone()
+
+
+def _avg(reps, average_updaters):
+    p = sum(n.params() for n in reps) / len(reps)
+    for n in reps:
+        n.setParams(p.clone())
+    if average_updaters:
+        st = sum(n.updater.getStateViewArray() for n in reps) / len(reps)
+        for n in reps:
+            n.updater.getStateViewArray().copy_(st)
+
+
+def run_mode4(rank, world, port, mode, result_path):
+    """world-4 gloo runs: AVERAGING with averagingFrequency 3 (12 batches = 3 rounds per epoch, 2 epochs) and the
+    encoded (threshold) update sharing."""
+    _setup(rank, world, port)
+    from deeplearning4j_amd import Adam, ListDataSetIterator
+    from deeplearning4j_amd.parallel import EncodedGradientsAccumulator, ParallelWrapper, TrainingMode
+    net = make_net(Adam(0.01) if mode != "encoded" else Adam(0.5))
+    batches = make_batches(12, 8)
+    it = ListDataSetIterator(batches, 8)
+    b = ParallelWrapper.Builder(net)
+    if mode == "averaging3":
+        b.trainingMode(TrainingMode.AVERAGING).averagingFrequency(3).averageUpdaters(True)
+    elif mode == "encoded":
+        b.gradientsAccumulator(EncodedGradientsAccumulator(threshold=1e-3))
+    pw = b.build()
+    pw.fit(it, 2)
+    p = net.params().clone()
+    gathered = [torch.empty_like(p) for _ in range(world)]
+    dist.all_gather(gathered, p)
+    if rank == 0:
+        torch.save({"params": [t.clone() for t in gathered], "iters": net.getIterationCount()}, result_path)
+    dist.barrier()
+    dist.destroy_process_group()

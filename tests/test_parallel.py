@@ -167,21 +167,36 @@ def test_parallel_wrapper_main_cli(tmp_path):
 
 
 @pytest.mark.skipif(os.environ.get("DL4J_AMD_SKIP_SLOW") == "1", reason="slow")
-def test_parallel_wrapper_in_process_workers_spawn():
-    """ParallelWrapper.Builder(net).workers(2).build().fit(data) from ONE plain process: two child workers (gloo on
-    CPU here, RCCL on GPUs) train synchronously and the caller's model ends up equal to single-process training
-    on the concatenated batches (the reference's in-JVM ParallelWrapper contract, PW:ParallelWrapper.java:467-565)."""
+@pytest.mark.parametrize("in_process", [True, False])
+def test_parallel_wrapper_in_process_workers_spawn(in_process):
+    """ParallelWrapper.Builder(net).workers(2).build().fit(data) from ONE plain process — worker threads (host
+    loopback here, RCCL communicators on GPUs) or two child processes fed over sockets (gloo here, RCCL on GPUs) —
+    train synchronously and the caller's model ends up equal to single-process training on the concatenated
+    batches (the reference's in-JVM ParallelWrapper contract, PW:ParallelWrapper.java:467-565)."""
     from deeplearning4j_amd import Adam, DataSet
     from deeplearning4j_amd.parallel import ParallelWrapper
     batches = W.make_batches(8, 8)
     net = W.make_net(Adam(0.01))
-    ParallelWrapper.Builder(net).workers(2).build().fit(batches, 2)       # a plain list source (ADVICE r1)
+    ParallelWrapper.Builder(net).workers(2).inProcess(in_process).build().fit(batches, 2)   # a plain list source
     ref = W.make_net(Adam(0.01))
     for _ in range(2):
         for i in range(0, 8, 2):
             a, b = batches[i], batches[i + 1]
             ref.fit(DataSet(torch.cat([a.features, b.features]), torch.cat([a.labels, b.labels])))
     assert torch.allclose(net.params(), ref.params(), atol=1e-5), (net.params() - ref.params()).abs().max()
+    assert net.getIterationCount() == 8
+    assert net.score() == net.score() and net.score() > 0      # the trained replica's score, not a stale one
+
+
+def test_spawned_worker_failure_is_reported():
+    """A child that dies (bad batch) makes fit raise promptly instead of blocking on the other rank's collective."""
+    from deeplearning4j_amd import Adam, DataSet
+    from deeplearning4j_amd.parallel import ParallelWrapper
+    batches = W.make_batches(4, 8)
+    batches[3] = DataSet(torch.randn(8, 7), batches[3].labels)
+    net = W.make_net(Adam(0.01))
+    with pytest.raises(RuntimeError, match="worker"):
+        ParallelWrapper.Builder(net).workers(2).inProcess(False).build().fit(batches, 1)
 
 
 def test_cg_shared_gradients_bucketed_equals_large_batch(tmp_path):
