@@ -14,7 +14,36 @@ struct SegDesc {
   long long p_off, n, st_off, in_block, block_n;
   int op, pad;
   float h0, h1, h2, h3, l1, l2;
+  // gradient normalization (BaseMultiLayerUpdater.preApply, :322-382), applied to g before the updater:
+  //   0 none, 1 RenormalizeL2PerLayer, 2 RenormalizeL2PerParamType, 3 ClipElementWiseAbsoluteValue,
+  //   4 ClipL2PerLayer, 5 ClipL2PerParamType. [gn_b0, gn_b1): the update blocks (btab rows) of this segment's norm
+  //   group (the layer, or the segment itself); their sum-of-squares partials come from gn_sumsq_kernel.
+  int gn_mode, gn_b0, gn_b1;
+  float gn_thr;
 };
+
+__device__ __forceinline__ bool gn_needs_norm(int m) { return m == 1 || m == 2 || m == 4 || m == 5; }
+
+// pre-pass: partial[b] = sum of g^2 over update block b (0 for blocks whose segment needs no norm); same grid as
+// the update kernel, so every partial is one workgroup's chunk (fixed-order, atomic-free)
+__global__ __launch_bounds__(256) void gn_sumsq_kernel(const SegDesc* __restrict__ segs, const int2* __restrict__ btab,
+                                                       const float* __restrict__ g, float* __restrict__ partial) {
+  const int2 bt = btab[blockIdx.x];
+  const SegDesc s = segs[bt.x];
+  float acc = 0.f;
+  if (gn_needs_norm(s.gn_mode)) {
+    const long long ibeg = (long long)bt.y * 2048;
+    long long iend = ibeg + 2048;
+    if (iend > s.n) iend = s.n;
+    for (long long i = ibeg + threadIdx.x; i < iend; i += 256) {
+      const float v = g[s.p_off + i];
+      acc = fmaf(v, v, acc);
+    }
+  }
+  __shared__ float red[4];
+  acc = block_reduce<false>(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
 
 enum { OP_NOOP = 0, OP_SGD = 1, OP_NESTEROVS = 2, OP_ADAM = 3, OP_ADAMAX = 4, OP_NADAM = 5, OP_ADAGRAD = 6,
        OP_ADADELTA = 7, OP_RMSPROP = 8 };
@@ -28,10 +57,21 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
                                                            const int2* __restrict__ btab, float* __restrict__ p,
                                                            float* __restrict__ g, float* __restrict__ st,
                                                            TS* __restrict__ shadow, float inv_div, int write_update,
-                                                           float* __restrict__ reg_out) {
+                                                           float* __restrict__ reg_out,
+                                                           const float* __restrict__ gn_partial) {
   const int2 bt = btab[blockIdx.x];
   const SegDesc s = segs[bt.x];
   float reg = 0.f;   // l1*|p| + 0.5*l2*p^2 of the PRE-update params (the score's regularisation term)
+  // gradient normalization factor of this segment's group (block-uniform branch)
+  float gscale = 1.f;
+  if (gn_needs_norm(s.gn_mode)) {
+    __shared__ float gred[4];
+    float ss = 0.f;
+    for (int b = s.gn_b0 + threadIdx.x; b < s.gn_b1; b += 256) ss += gn_partial[b];
+    ss = block_reduce<false>(ss, gred);
+    const float nrm = sqrtf(ss);
+    gscale = (s.gn_mode == 1 || s.gn_mode == 2) ? 1.f / nrm : fminf(1.f, s.gn_thr / nrm);
+  }
   float* s1 = st + s.st_off + s.in_block;
   float* s2 = st + s.st_off + s.block_n + s.in_block;
   const long long ibeg = (long long)bt.y * UPD_CHUNK;
@@ -39,7 +79,9 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
   if (iend > s.n) iend = s.n;
   for (long long i = ibeg + threadIdx.x; i < iend; i += 256) {
     const long long pi = s.p_off + i;
-    const float gi = g[pi];
+    float gi = g[pi];
+    if (s.gn_mode == 3) gi = fminf(fmaxf(gi, -s.gn_thr), s.gn_thr);
+    else gi *= gscale;
     float pv = p[pi];
     float u;
     switch (s.op) {
@@ -106,19 +148,27 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
 
 // segs: device array of SegDesc. shadow_kind: 0 none, 1 bf16, 2 fp16 (reduced-precision compute copy)
 // btab: device int2[nblocks] built by the host from the segment sizes (see dl4j_update_chunk).
+// gn_partial: nblocks floats of scratch when any segment uses a norm-based gradient normalization (the pre-pass
+// writes it), else null.
 DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
                                void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
-                               hipStream_t stream) {
+                               float* gn_partial, hipStream_t stream) {
   if (nblocks <= 0) return 0;
+  if (gn_partial)
+    hipLaunchKernelGGL(gn_sumsq_kernel, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs, (const int2*)btab,
+                       (const float*)g, gn_partial);
   if (shadow_kind == 1)
     hipLaunchKernelGGL(fused_update_kernel<bf16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
-                       (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out);
+                       (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out,
+                       (const float*)gn_partial);
   else if (shadow_kind == 2)
     hipLaunchKernelGGL(fused_update_kernel<f16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
-                       (const int2*)btab, p, g, st, (f16*)shadow, inv_div, write_update, reg_out);
+                       (const int2*)btab, p, g, st, (f16*)shadow, inv_div, write_update, reg_out,
+                       (const float*)gn_partial);
   else
     hipLaunchKernelGGL(fused_update_kernel<float>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
-                       (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out);
+                       (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out,
+                       (const float*)gn_partial);
   return (int)hipGetLastError();
 }
 

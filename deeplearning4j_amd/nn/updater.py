@@ -10,7 +10,8 @@ import torch
 
 from ..nn.conf.enums import GradientNormalization
 from ..nn.conf.updaters import NoOp
-from ..ops.update import Segment, UpdatePlan, fused_update
+from ..ops.update import (GN_CLIP_ELEM, GN_CLIP_L2_LAYER, GN_CLIP_L2_PARAM, GN_NONE, GN_RENORM_LAYER,
+                          GN_RENORM_PARAM, Segment, UpdatePlan, fused_update, pre_apply)
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
@@ -68,15 +69,28 @@ class NetworkUpdater:
             self._close(cur, st)
             st += self.blocks[-1].stateSize
         self.state_size = st
+        self._gn_layers = self._collect_gn()
+        gn_of = {}
+        G = GradientNormalization
+        codes = {G.RenormalizeL2PerLayer: GN_RENORM_LAYER, G.RenormalizeL2PerParamType: GN_RENORM_PARAM,
+                 G.ClipElementWiseAbsoluteValue: GN_CLIP_ELEM, G.ClipL2PerLayer: GN_CLIP_L2_LAYER,
+                 G.ClipL2PerParamType: GN_CLIP_L2_PARAM}
+        for name, (gn, thr, ents) in self._gn_layers.items():
+            code = codes.get(gn, GN_NONE)
+            per_layer = code in (GN_RENORM_LAYER, GN_CLIP_L2_LAYER)
+            for e in ents:
+                if not isinstance(e.updater, NoOp):     # BN running statistics etc. are not normalised
+                    gn_of[id(e)] = (code, float(thr), name if per_layer else None)
         segs = []
         for bi, b in enumerate(self.blocks):
             for e in b.entries:
+                code, thr, grp = gn_of.get(id(e), (GN_NONE, 1.0, None))
                 segs.append(Segment(e.p_off, e.n, b.st_off, e.p_off - b.paramOffsetStart,
-                                    b.paramOffsetEnd - b.paramOffsetStart, b.updater, e.l1, e.l2, bi))
+                                    b.paramOffsetEnd - b.paramOffsetStart, b.updater, e.l1, e.l2, bi,
+                                    code, thr, grp))
         self.plan = UpdatePlan(segs, [(b.paramOffsetStart, b.paramOffsetEnd, b.st_off, b.updater)
                                       for b in self.blocks])
         self.state = None
-        self._gn_layers = self._collect_gn()
 
     def _close(self, cur, st):
         self.blocks.append(UpdaterBlock(cur[0].p_off, cur[-1].p_off + cur[-1].n, st, cur[0].updater, list(cur)))
@@ -108,36 +122,13 @@ class NetworkUpdater:
         return out
 
     def preApply(self, grad):
-        """Per-layer gradient normalization / clipping (reference BaseMultiLayerUpdater.java:322-382)."""
-        for name, (gn, thr, ents) in self._gn_layers.items():
-            views = [grad[e.p_off:e.p_off + e.n] for e in ents if not isinstance(e.updater, NoOp)]
-            if not views:
-                continue
-            G = GradientNormalization
-            if gn == G.RenormalizeL2PerLayer:
-                n = torch.sqrt(sum((_acc(v) ** 2).sum() for v in views))
-                for v in views:
-                    v.div_(n)
-            elif gn == G.RenormalizeL2PerParamType:
-                for v in views:
-                    v.div_(v.norm())
-            elif gn == G.ClipElementWiseAbsoluteValue:
-                for v in views:
-                    v.clamp_(-thr, thr)
-            elif gn == G.ClipL2PerLayer:
-                n = torch.sqrt(sum((_acc(v) ** 2).sum() for v in views))
-                scale = torch.clamp(thr / n, max=1.0)
-                for v in views:
-                    v.mul_(scale)
-            elif gn == G.ClipL2PerParamType:
-                for v in views:
-                    n = v.norm()
-                    v.mul_(torch.clamp(thr / n, max=1.0))
+        """Per-layer gradient normalization / clipping (reference BaseMultiLayerUpdater.java:322-382). ``update``
+        does not call this on the GPU: the fused updater kernel applies the same scaling in its own pass."""
+        pre_apply(self.plan, grad)
 
     def update(self, params, grad, iteration, epoch, batch_size, shadow=None, reg_out=None):
-        """Apply the whole update (preApply -> updater -> l1/l2 -> /batch -> params -= u) in place."""
-        if self._gn_layers:
-            self.preApply(grad)
+        """Apply the whole update (preApply -> updater -> l1/l2 -> /batch -> params -= u) in place; the gradient
+        normalization runs inside fused_update (kernel pass on the GPU, ``pre_apply`` on the host path)."""
         fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
                      self.net.conf.globalConf.get("miniBatch", True), shadow, reg_out=reg_out)
 

@@ -29,7 +29,7 @@ def load():
     lib = ctypes.CDLL(KERNEL_LIB)
     sigs = {
         "dl4j_fused_update": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float,
-                              c_int, c_void_p, c_void_p],
+                              c_int, c_void_p, c_void_p, c_void_p],
         "dl4j_update_chunk": [],
         "dl4j_segdesc_size": [],
         "dl4j_bn_workspace_floats": [c_ll, c_int],
@@ -143,7 +143,28 @@ class _Slot:
 
 
 _SEG_DTYPE = np.dtype([("p_off", "<i8"), ("n", "<i8"), ("st_off", "<i8"), ("in_block", "<i8"), ("block_n", "<i8"),
-                       ("op", "<i4"), ("pad", "<i4"), ("h", "<f4", 4), ("l1", "<f4"), ("l2", "<f4")])
+                       ("op", "<i4"), ("pad", "<i4"), ("h", "<f4", 4), ("l1", "<f4"), ("l2", "<f4"),
+                       ("gn_mode", "<i4"), ("gn_b0", "<i4"), ("gn_b1", "<i4"), ("gn_thr", "<f4")])
+
+
+def _gn_block_ranges(plan, chunk):
+    """Per segment: the [first, last) update-block range (btab rows) of its gradient-normalization group."""
+    cached = plan.__dict__.get("_gn_ranges")
+    if cached is not None and cached[0] == chunk:
+        return cached[1]
+    first, b = [], 0
+    for sg in plan.segments:
+        first.append(b)
+        b += (sg.n + chunk - 1) // chunk
+    first.append(b)
+    span = {}
+    for i, sg in enumerate(plan.segments):
+        key = sg.gn_group if sg.gn_group is not None else ("seg", i)
+        lo, hi = span.get(key, (first[i], first[i + 1]))
+        span[key] = (min(lo, first[i]), max(hi, first[i + 1]))
+    ranges = [span[sg.gn_group if sg.gn_group is not None else ("seg", i)] for i, sg in enumerate(plan.segments)]
+    plan._gn_ranges = (chunk, ranges)
+    return ranges
 
 # graph slot currently being captured / replayed (None = eager)
 GRAPH_SLOT = [None]
@@ -153,9 +174,11 @@ def seg_table_bytes(plan, iteration, epoch):
     from ..nn.conf.updaters import kernel_params
     segs = plan.segments
     arr = np.zeros(len(segs), dtype=_SEG_DTYPE)
+    ranges = _gn_block_ranges(plan, load().dl4j_update_chunk())
     for i, s in enumerate(segs):
         op, h0, h1, h2, h3 = kernel_params(s.updater, iteration, epoch)
-        arr[i] = (s.p_off, s.n, s.st_off, s.in_block, s.block_n, op, 0, (h0, h1, h2, h3), s.l1, s.l2)
+        arr[i] = (s.p_off, s.n, s.st_off, s.in_block, s.block_n, op, 0, (h0, h1, h2, h3), s.l1, s.l2,
+                  getattr(s, "gn_mode", 0), ranges[i][0], ranges[i][1], getattr(s, "gn_thr", 1.0))
     return arr.tobytes()
 
 
@@ -234,9 +257,15 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
         sk = {torch.bfloat16: 1, torch.float16: 2}.get(shadow.dtype)
         if sk is None:
             return False
+    gn_part = None
+    if any(getattr(sg, "gn_mode", 0) in (1, 2, 4, 5) for sg in segs):
+        gn_part = getattr(cache, "gn_partial", None)
+        if gn_part is None or gn_part.numel() < cache.nblocks or gn_part.device != params.device:
+            gn_part = cache.gn_partial = torch.empty(max(cache.nblocks, 1), dtype=torch.float32,
+                                                     device=params.device)
     rc = lib.dl4j_fused_update(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
                                _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
-                               _stream())
+                               _ptr(gn_part), _stream())
     _check(rc, "fused_update")
     return True
 

@@ -18,12 +18,45 @@ from ..nn.conf.updaters import kernel_params
 from .dispatch import use_native
 
 
-class Segment:
-    __slots__ = ("p_off", "n", "st_off", "in_block", "block_n", "updater", "l1", "l2", "block_id")
+# gradient normalization modes of a segment (kernel codes, csrc/updater.hip SegDesc.gn_mode)
+GN_NONE, GN_RENORM_LAYER, GN_RENORM_PARAM, GN_CLIP_ELEM, GN_CLIP_L2_LAYER, GN_CLIP_L2_PARAM = range(6)
 
-    def __init__(self, p_off, n, st_off, in_block, block_n, updater, l1, l2, block_id):
+
+class Segment:
+    __slots__ = ("p_off", "n", "st_off", "in_block", "block_n", "updater", "l1", "l2", "block_id", "gn_mode",
+                 "gn_thr", "gn_group")
+
+    def __init__(self, p_off, n, st_off, in_block, block_n, updater, l1, l2, block_id, gn_mode=GN_NONE, gn_thr=1.0,
+                 gn_group=None):
         self.p_off, self.n, self.st_off, self.in_block, self.block_n = p_off, n, st_off, in_block, block_n
         self.updater, self.l1, self.l2, self.block_id = updater, l1, l2, block_id
+        # gn_group: segments sharing a norm (one layer for the *PerLayer modes); None = the segment alone
+        self.gn_mode, self.gn_thr, self.gn_group = gn_mode, gn_thr, gn_group
+
+
+def pre_apply(plan, grad):
+    """Gradient normalization / clipping of the flat gradient (reference BaseMultiLayerUpdater.java:322-382) — the
+    host-side path; on the GPU the fused updater applies it inside its kernel pass."""
+    groups = {}
+    for i, sg in enumerate(plan.segments):
+        if sg.gn_mode != GN_NONE:
+            groups.setdefault(sg.gn_group if sg.gn_group is not None else ("seg", i), []).append(sg)
+    with torch.no_grad():
+        for segs in groups.values():
+            views = [grad[sg.p_off:sg.p_off + sg.n] for sg in segs]
+            mode, thr = segs[0].gn_mode, segs[0].gn_thr
+            if mode == GN_CLIP_ELEM:
+                for v in views:
+                    v.clamp_(-thr, thr)
+                continue
+            nrm = torch.sqrt(sum((v.double() ** 2).sum() for v in views)).to(grad.dtype)
+            scale = 1.0 / nrm if mode in (GN_RENORM_LAYER, GN_RENORM_PARAM) else torch.clamp(thr / nrm, max=1.0)
+            for v in views:
+                v.mul_(scale)
+
+
+def has_gn(plan):
+    return any(sg.gn_mode != GN_NONE for sg in plan.segments)
 
 
 class UpdatePlan:
@@ -54,6 +87,8 @@ def fused_update(plan, params, grad, state, iteration, epoch, batch_size, mini_b
         from . import native
         if native.fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out):
             return
+    if has_gn(plan):
+        pre_apply(plan, grad)
     with torch.no_grad():
         if reg_out is not None:
             r = torch.zeros((), dtype=params.dtype, device=params.device)
