@@ -442,6 +442,8 @@ class ComputationGraph(BaseNetwork):
             ys = [y[:, :, t0:t1] if y.dim() == 3 else y for y in labels]
             fm = [m[:, t0:t1] if m is not None else None for m in fmasks] if fmasks else None
             lm = [m[:, t0:t1] if m is not None else None for m in lmasks] if lmasks else None
+            if self._try_graph_step(xs, ys, fm, lm, tbptt_back=back):
+                continue                           # this window replayed as a HIP graph (nn/hipgraph.py)
             self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
                                          tbptt_back=back, defer_reg=True)
             self._apply_update(inputs[0].shape[0])

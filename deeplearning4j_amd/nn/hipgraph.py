@@ -15,9 +15,16 @@ Design:
   * Host-side bookkeeping (iteration count, weight-version bump, listeners' iterationDone) runs outside the graph.
 Data parallel: the AllReduceGradientsAccumulator's bucketed RCCL all-reduces are captured with the step (nccl
 backend only); gloo and custom accumulators run eager.
-Eligibility: plain SGD-family optimizer, no TBPTT, no masks, a capturable (or no) gradient accumulator, no
-listeners with per-pass hooks (onForwardPass/onBackwardPass/onGradientCalculation), CUDA device, fixed shapes.
-Anything else falls back to the eager step transparently.
+Masks: feature / label masks are static buffers like the inputs (their presence is part of the captured shape).
+Truncated BPTT (reference MultiLayerNetwork.doTruncatedBPTT, :1521-1593): every window shape gets its own captured
+step (the last window of a sequence may be shorter). The recurrent state carried between windows (each recurrent
+layer's tBpttStateMap: h, and c for LSTMs) lives in static buffers: the captured body reads them, and its last nodes
+copy the window's final state back into them, so consecutive replays chain the state on the GPU with no host work.
+Before a replay the buffers are refreshed from the layer's current map when an eager window (or a new sequence,
+state zero) came in between.
+Eligibility: plain SGD-family optimizer, a capturable (or no) gradient accumulator, no listeners with per-pass hooks
+(onForwardPass/onBackwardPass/onGradientCalculation), CUDA device, fixed shapes. Anything else falls back to the
+eager step transparently.
 """
 import logging
 
@@ -27,28 +34,61 @@ log = logging.getLogger("deeplearning4j_amd")
 
 
 class CapturedTrainingStep:
-    def __init__(self, net, inputs, labels):
+    def __init__(self, net, inputs, labels, fmasks=None, lmasks=None, tbptt_back=None):
         self.net = net
         self.is_graph = type(net).__name__ == "ComputationGraph"
         self.static_x = [t.detach().clone() for t in inputs]
         self.static_y = [t.detach().clone() for t in labels]
+        self.static_fm = [None if m is None else m.detach().clone() for m in (fmasks or [])]
+        self.static_lm = [None if m is None else m.detach().clone() for m in (lmasks or [])]
+        self.tbptt_back = tbptt_back
+        self.state = []            # (layer, key, static tensor): carried recurrent state of a TBPTT window graph
+        self.out_state = []        # per graph slot: (layer, key, tensor) the replayed window leaves as its state
         self.graphs = []
         self.pool = None
         self.score_t = [None, None]
         self.k = 0
         self.ok = False
 
-    def shapes_match(self, inputs, labels):
-        return len(inputs) == len(self.static_x) and len(labels) == len(self.static_y) and \
-            all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(inputs, self.static_x)) and \
-            all(a.shape == b.shape and a.dtype == b.dtype for a, b in zip(labels, self.static_y))
+    @staticmethod
+    def key(inputs, labels, fmasks, lmasks, tbptt_back):
+        def sig(ts):
+            return tuple(None if t is None else (tuple(t.shape), t.dtype) for t in (ts or []))
+        return sig(inputs), sig(labels), sig(fmasks), sig(lmasks), tbptt_back
+
+    def shapes_match(self, inputs, labels, fmasks=None, lmasks=None):
+        return self.key(inputs, labels, fmasks, lmasks, self.tbptt_back) == \
+            self.key(self.static_x, self.static_y, self.static_fm, self.static_lm, self.tbptt_back)
+
+    def _recurrent_layers(self):
+        return recurrent_layers(self.net)
+
+    def _bind_state(self):
+        """Static buffers for the recurrent state the previous (eager) window left in each layer's map."""
+        self.state = []
+        for l in self._recurrent_layers():
+            for k, v in list(l.tBpttStateMap.items()):
+                if torch.is_tensor(v):
+                    buf = v.detach().clone()
+                    self.state.append((l, k, buf))
+                    l.tBpttStateMap[k] = buf
 
     def _body(self):
         n = self.net
+        fm = self.static_fm or None
+        lm = self.static_lm or None
+        tb = self.tbptt_back is not None
+        kw = dict(stored_state=True, store_last_for_tbptt=True, tbptt_back=self.tbptt_back) if tb else {}
         if self.is_graph:
-            n.computeGradientAndScore(self.static_x, self.static_y, None, None, defer_reg=True)
+            n.computeGradientAndScore(self.static_x, self.static_y, fm, lm, defer_reg=True, **kw)
         else:
-            n.computeGradientAndScore(self.static_x[0], self.static_y[0], None, None, defer_reg=True)
+            n.computeGradientAndScore(self.static_x[0], self.static_y[0], fm[0] if fm else None,
+                                      lm[0] if lm else None, defer_reg=True, **kw)
+        for l, k, buf in self.state:               # the window's final state becomes the next replay's input
+            new = l.tBpttStateMap.get(k)
+            if new is not None and new is not buf:
+                buf.copy_(new)
+            l.tBpttStateMap[k] = buf
         acc = getattr(n, "gradientsAccumulator", None)
         if acc is not None:
             acc.reduce_gradients(n)                # bucketed RCCL all-reduces become graph nodes
@@ -61,6 +101,8 @@ class CapturedTrainingStep:
         plan = n.updater.plan
         self.pool = torch.cuda.graph_pool_handle()
         native.prepare_graph_slots(plan, n.device, n.conf.iterationCount, n.conf.epochCount)
+        if self.tbptt_back is not None:
+            self._bind_state()
         torch.cuda.synchronize()
         # no Python GC while capturing: a collected cycle that owns GPU resources (events, other pools' blocks,
         # a previous network's buffers) would be released inside the capture and abort it
@@ -68,8 +110,12 @@ class CapturedTrainingStep:
         gc.collect()
         gc_was_enabled = gc.isenabled()
         gc.disable()
+        # the recurrent state maps every slot's capture must start from (empty for a sequence's first window)
+        start_maps = [(l, dict(l.tBpttStateMap)) for l in self._recurrent_layers()]
         try:
             for slot in (0, 1):
+                for l, m in start_maps:            # not the outputs the previous slot's capture left behind
+                    l.tBpttStateMap = dict(m)
                 n._bump_weight_version()           # every graph must contain its own weight-relayout kernels
                 g = torch.cuda.CUDAGraph()
                 native.GRAPH_SLOT[0] = slot
@@ -77,6 +123,10 @@ class CapturedTrainingStep:
                 with torch.cuda.graph(g, pool=self.pool):
                     self.score_t[slot] = self._body()
                 self.graphs.append(g)
+                # the A and B graphs own different output tensors: remember which ones this slot writes
+                self.out_state.append([(l, k, v) for l in self._recurrent_layers()
+                                       for k, v in l.tBpttStateMap.items() if torch.is_tensor(v)]
+                                      if self.tbptt_back is not None else [])
             self.ok = True
         finally:
             native.GRAPH_SLOT[0] = None
@@ -86,18 +136,33 @@ class CapturedTrainingStep:
         _ = plan
         return self.ok
 
-    def step(self, inputs, labels):
+    def step(self, inputs, labels, fmasks=None, lmasks=None):
         from ..ops import native
         n = self.net
         for d, s in zip(self.static_x, inputs):
             d.copy_(s, non_blocking=True)
         for d, s in zip(self.static_y, labels):
             d.copy_(s, non_blocking=True)
+        for d, s in zip(self.static_fm, fmasks or []):
+            if d is not None:
+                d.copy_(s, non_blocking=True)
+        for d, s in zip(self.static_lm, lmasks or []):
+            if d is not None:
+                d.copy_(s, non_blocking=True)
+        for l, k, buf in self.state:               # state left by an eager window / a new sequence (none = zero)
+            cur = l.tBpttStateMap.get(k)
+            if cur is None:
+                buf.zero_()
+            elif cur is not buf:
+                buf.copy_(cur)
+            l.tBpttStateMap[k] = buf
         slot = self.k & 1
         plan = n.updater.plan
         native.refresh_graph_table(plan, slot, n.conf.iterationCount, n.conf.epochCount)
         self.graphs[slot].replay()
         native.mark_graph_replayed(plan, slot)
+        for l, k, v in self.out_state[slot]:
+            l.tBpttStateMap[k] = v
         self.k += 1
         n._score_t = self.score_t[slot]
         n._score_val = None
@@ -107,11 +172,21 @@ class CapturedTrainingStep:
         n._iteration_done()
 
 
-def graph_eligible(net, inputs, labels, fmasks, lmasks):
+def recurrent_layers(net):
+    by_name = getattr(net, "layers_by_name", None)
+    layers = list(by_name.values()) if by_name else list(getattr(net, "layers", None) or [])
+    return [l for l in layers if hasattr(l, "tBpttStateMap")]
+
+
+def carries_state(net):
+    """True when some recurrent layer holds TBPTT state from a previous window (the first window of a sequence
+    starts from zero state and is captured as a graph of its own)."""
+    return any(torch.is_tensor(v) for l in recurrent_layers(net) for v in l.tBpttStateMap.values())
+
+
+def graph_eligible(net, inputs, labels, fmasks, lmasks, tbptt_window=False):
     from .conf.enums import BackpropType, OptimizationAlgorithm as OA
     if net.device is None or net.device.type != "cuda":
-        return False
-    if fmasks or lmasks:
         return False
     acc = getattr(net, "gradientsAccumulator", None)
     if acc is not None and not (hasattr(acc, "capturable") and acc.capturable()):
@@ -119,14 +194,15 @@ def graph_eligible(net, inputs, labels, fmasks, lmasks):
     algo = net.conf.globalConf.get("optimizationAlgo")
     if algo is not None and OA.of(algo) != OA.STOCHASTIC_GRADIENT_DESCENT:
         return False
-    if net.conf.backpropType == BackpropType.TruncatedBPTT and inputs[0].dim() == 3:
-        return False
+    if tbptt_window is False and net.conf.backpropType == BackpropType.TruncatedBPTT and inputs[0].dim() == 3:
+        return False                               # whole sequences go through the window loop (graph per window)
     for l in net.listeners:
         for h in ("onForwardPass", "onBackwardPass", "onGradientCalculation"):
             f = getattr(type(l), h, None)
             if f is not None and f is not getattr(_NoHooks, h):
                 return False
-    return all(t.is_cuda for t in list(inputs) + list(labels))
+    ms = [m for m in list(fmasks or []) + list(lmasks or []) if m is not None]
+    return all(t.is_cuda for t in list(inputs) + list(labels) + ms)
 
 
 class _NoHooks:

@@ -227,6 +227,8 @@ class MultiLayerNetwork(BaseNetwork):
             ys = y[:, :, t0:t1] if y.dim() == 3 else y
             fm = fmask[:, t0:t1] if fmask is not None else None
             lm = lmask[:, t0:t1] if lmask is not None else None
+            if self._try_graph_step([xs], [ys], fm, lm, tbptt_back=back):
+                continue                           # this window replayed as a HIP graph (nn/hipgraph.py)
             self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
                                          tbptt_back=back, defer_reg=True)
             self._apply_update(x.shape[0])

@@ -431,28 +431,45 @@ class BaseNetwork:
         self._hipgraph_warmup = int(warmup)
         self._hipgraph = None
         self._hipgraph_seen = 0
+        self._hipgraphs = {}
+        self._hipgraph_seen_by = {}
         return self
 
-    def _try_graph_step(self, inputs, labels, fmasks, lmasks):
+    def _try_graph_step(self, inputs, labels, fmasks, lmasks, tbptt_back=None):
+        """One training iteration (or, with ``tbptt_back``, one TBPTT window) as a HIP-graph replay when eligible;
+        False = run it eagerly. One captured step per distinct shape signature (input / label / mask shapes and
+        the window), each captured after ``warmup`` eager iterations of that signature."""
         if not getattr(self, "_hipgraph_enabled", False):
             return False
-        from .hipgraph import CapturedTrainingStep, graph_eligible
+        from .hipgraph import CapturedTrainingStep, carries_state, graph_eligible
         inputs = [self._to_dev(t, self._feat_dtype()) for t in inputs]
         labels = [self._to_dev(t, self.master_dtype) for t in labels]
-        if not graph_eligible(self, inputs, labels, fmasks, lmasks):
+        fm = None if fmasks is None else [None if m is None else self._to_dev(m)
+                                          for m in (fmasks if isinstance(fmasks, (list, tuple)) else [fmasks])]
+        lm = None if lmasks is None else [None if m is None else self._to_dev(m)
+                                          for m in (lmasks if isinstance(lmasks, (list, tuple)) else [lmasks])]
+        if not graph_eligible(self, inputs, labels, fm, lm, tbptt_window=tbptt_back is not None):
             return False
-        cs = self._hipgraph
-        if cs is not None and cs.ok and cs.shapes_match(inputs, labels):
-            cs.step(inputs, labels)
+        key = CapturedTrainingStep.key(inputs, labels, fm, lm, tbptt_back)
+        if tbptt_back is not None:
+            key = key + (carries_state(self),)
+        graphs = self.__dict__.setdefault("_hipgraphs", {})
+        cs = graphs.get(key)
+        if cs is not None and cs.ok:
+            cs.step(inputs, labels, fm, lm)
+            self._hipgraph = cs
             return True
-        self._hipgraph_seen += 1
-        if self._hipgraph_seen <= self._hipgraph_warmup:
+        seen = self.__dict__.setdefault("_hipgraph_seen_by", {})
+        seen[key] = seen.get(key, 0) + 1
+        self._hipgraph_seen = seen[key]
+        if seen[key] <= self._hipgraph_warmup:
             return False                           # eager warmup iterations populate every cache first
-        cs = CapturedTrainingStep(self, inputs, labels)
+        cs = CapturedTrainingStep(self, inputs, labels, fm, lm, tbptt_back)
         self._bump_weight_version()
         cs.capture()                               # a failed capture leaves the stream unusable: let it raise
+        graphs[key] = cs
         self._hipgraph = cs
-        cs.step(inputs, labels)
+        cs.step(inputs, labels, fm, lm)
         return True
 
     def _iteration_done(self):

@@ -55,7 +55,9 @@ class _CoopBuf:
     def __init__(self, nbytes, device):
         self.exch = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
         self.err = torch.empty(1, dtype=torch.int32, device=device)
-        self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        # pinned host copy, created by the first EAGER launch (pinned allocation is illegal while a stream captures:
+        # the capture stream gets a buffer of its own)
+        self.err_host = None
         self.err_ev = None
         self.next_tag = None                               # None: contents undefined -> the next launch zeroes them
 
@@ -104,6 +106,8 @@ def _post_launch(b):
     """Eager launches: queue an async copy of the error word into pinned memory (checked at the next launch)."""
     if torch.cuda.is_current_stream_capturing():
         return
+    if b.err_host is None:
+        b.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
     b.err_host.copy_(b.err, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
@@ -113,7 +117,7 @@ def _post_launch(b):
 def check_coop_errors():
     """Synchronously raise if any cooperative LSTM launch so far hit a hand-off timeout."""
     for b in list(_coop_bufs.values()):
-        if b.err_ev is not None:
+        if b.err_ev is not None and b.err_host is not None:
             b.err_ev.synchronize()
             if int(b.err_host[0]) != 0:
                 raise CoopTimeoutError("cooperative LSTM kernel: a cross-workgroup hand-off timed out")

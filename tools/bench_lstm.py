@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--chars", type=int, default=77)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", type=int, default=1, help="replay TBPTT windows as HIP graphs (nn/hipgraph.py)")
     args = ap.parse_args()
 
     from deeplearning4j_amd.models import TextGenerationLSTM
@@ -39,6 +40,8 @@ def main():
     dt = DataType.BFLOAT16 if args.dtype == "bf16" else DataType.FLOAT
     net = TextGenerationLSTM(numLabels=args.chars, inputShape=[1, args.chars], hidden=args.hidden,
                              dataType=dt).init(device=dev)
+    if args.graph and dev.type == "cuda":
+        net.enableHipGraphs(True, warmup=1)
     g = torch.Generator().manual_seed(7)
     idx = torch.randint(0, args.chars, (args.batch, args.length + 1), generator=g)
     x = torch.nn.functional.one_hot(idx[:, :-1], args.chars).permute(0, 2, 1).float().to(dev)
@@ -63,6 +66,7 @@ def main():
         "ms_per_step": round(el / args.steps * 1000, 2), "higher_is_better": True, "dtype": args.dtype,
         "data": "synthetic one-hot characters; random-init weights",
         "lstm_kernel": "sequence-HIP" if os.environ.get("DL4J_AMD_KERNEL_LSTM", "1") != "0" else "per-step",
+        "hip_graph": bool(args.graph and dev.type == "cuda"),
         "config": {"model": "TextGenerationLSTM (2x GravesLSTM 256)", "batch": args.batch, "seq_len": args.length,
                    "chars": args.chars, "tbptt": 50}, "final_score": net.score()}), flush=True)
 
