@@ -1,7 +1,8 @@
 """Reconstruction distributions p(x|z) for the VariationalAutoencoder layer
 (reference nn/conf/layers/variational/{Gaussian,Bernoulli,Exponential,Composite}ReconstructionDistribution.java,
 LossFunctionWrapper.java). Each maps the decoder's pre-output ("distribution parameters") to a negative log
-likelihood; gradients come from autograd in the VAE runtime, so only the forward math lives here."""
+likelihood (``exampleNegLogProbability``) and gives its hand-derived gradient with respect to that pre-output
+(``gradient``, reference ReconstructionDistribution.gradient) for the VAE's explicit backward pass."""
 import math
 
 import torch
@@ -27,6 +28,10 @@ class ReconstructionDistribution(Config):
     def negLogProbability(self, x, preOut, average=True):
         s = self.exampleNegLogProbability(x, preOut).sum()
         return s / x.shape[0] if average else s
+
+    def gradient(self, x, preOut):
+        """d(sum of exampleNegLogProbability) / d preOut."""
+        raise NotImplementedError
 
     def generateAtMean(self, preOut):
         raise NotImplementedError
@@ -56,6 +61,14 @@ class GaussianReconstructionDistribution(ReconstructionDistribution):
         n = mean.shape[1]
         return 0.5 * logs2.sum(1) - n * NEG_HALF_LOG_2PI + ((x - mean) ** 2 / logs2.exp() / 2).sum(1)
 
+    def gradient(self, x, preOut):
+        mean, logs2 = self._split(preOut)
+        inv = (-logs2).exp()
+        d = x - mean
+        dmean = -d * inv                                  # d/dmean of (x - mean)^2 / (2 sigma^2)
+        dlogs2 = 0.5 - 0.5 * d * d * inv                  # d/dlog(sigma^2) of 0.5 log(sigma^2) + (x-mean)^2 e^-ls / 2
+        return self.activationFn.backprop(preOut, torch.cat([dmean, dlogs2], dim=1))
+
     def generateAtMean(self, preOut):
         return self._split(preOut)[0]
 
@@ -77,6 +90,13 @@ class BernoulliReconstructionDistribution(ReconstructionDistribution):
     def exampleNegLogProbability(self, x, preOut):
         p = self.activationFn.getActivation(preOut, True).clamp(1e-5, 1 - 1e-5)
         return -(x * p.log() + (1 - x) * (1 - p).log()).sum(1)
+
+    def gradient(self, x, preOut):
+        q = self.activationFn.getActivation(preOut, True)
+        inside = ((q >= 1e-5) & (q <= 1 - 1e-5)).to(q.dtype)          # the clamp passes no gradient outside
+        p = q.clamp(1e-5, 1 - 1e-5)
+        dp = (-x / p + (1 - x) / (1 - p)) * inside
+        return self.activationFn.backprop(preOut, dp)
 
     def generateAtMean(self, preOut):
         return self.activationFn.getActivation(preOut, False)
@@ -100,6 +120,10 @@ class ExponentialReconstructionDistribution(ReconstructionDistribution):
     def exampleNegLogProbability(self, x, preOut):
         gamma = self.activationFn.getActivation(preOut, True)
         return -(gamma - gamma.exp() * x).sum(1)
+
+    def gradient(self, x, preOut):
+        gamma = self.activationFn.getActivation(preOut, True)
+        return self.activationFn.backprop(preOut, gamma.exp() * x - 1.0)
 
     def generateAtMean(self, preOut):
         return 1.0 / self.activationFn.getActivation(preOut, False).exp()
@@ -144,6 +168,9 @@ class CompositeReconstructionDistribution(ReconstructionDistribution):
     def exampleNegLogProbability(self, x, preOut):
         return sum(d.exampleNegLogProbability(xs, ps) for d, xs, ps in self._chunks(x, preOut))
 
+    def gradient(self, x, preOut):
+        return torch.cat([d.gradient(xs, ps) for d, xs, ps in self._chunks(x, preOut)], dim=1)
+
     def generateAtMean(self, preOut):
         return torch.cat([d.generateAtMean(ps) for d, _, ps in self._chunks(None, preOut)], dim=1)
 
@@ -156,6 +183,10 @@ class LossFunctionWrapper(ReconstructionDistribution):
     FIELDS = {"activationFn": None, "lossFunction": None}
     _CONVERTERS = {"activationFn": to_activation, "lossFunction": to_loss}
 
+    def __init__(self, activationFn=None, lossFunction=None, **kw):
+        """Reference LossFunctionWrapper(IActivation activationFn, ILossFunction lossFunction)."""
+        super().__init__(activationFn=activationFn or ActivationIdentity(), lossFunction=lossFunction, **kw)
+
     def hasLossFunction(self):
         return True
 
@@ -164,6 +195,9 @@ class LossFunctionWrapper(ReconstructionDistribution):
 
     def exampleNegLogProbability(self, x, preOut):
         return self.lossFunction.computeScoreArray(x, preOut, self.activationFn, None)
+
+    def gradient(self, x, preOut):
+        return self.lossFunction.computeGradient(x, preOut, self.activationFn, None)
 
     def generateAtMean(self, preOut):
         return self.activationFn.getActivation(preOut, False)

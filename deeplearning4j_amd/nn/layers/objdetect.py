@@ -7,8 +7,14 @@ followed by the one-hot class; all-zero where no object.
 Loss (reference computeBackpropGradientAndScore): responsible box = argmax IOU over the B anchors in cells
 with an object; lambdaCoord * [L2(xy) + L2(sqrt wh)] + L2(conf vs IOU) + lambdaNoObj * L2(conf vs 0) for
 non-responsible boxes + class loss (softmax, L2 by default) for responsible boxes; divided by minibatch.
-The gradient is obtained by autograd through the same expression (it includes the dIOU/dxy, dIOU/dwh terms
-the reference derives by hand, restricted to responsible boxes because the no-object label is 0).
+The input gradient is derived by hand (reference computeBackpropGradientAndScore :256-340 and
+calculateIOULabelPredicted :364-480): position / size / class terms come from the configured loss functions'
+computeGradient, the confidence label IOU contributes the dIOU/d(xy), dIOU/d(wh) path through the
+intersection / union geometry, and sigmoid / exp(prior) / softmax are backpropagated in closed form.
+One deliberate difference: the reference's dLc/dIOU = 2 (IOU - conf) (1_obj + lambdaNoObj 1_noobj) also charges
+no-object anchors, whose confidence label is 0 and therefore independent of the IOU; here only the responsible
+anchor's term is kept, which is the exact derivative of the score (tests/test_explicit_backward.py gradient-checks
+the layer in fp64).
 """
 import torch
 
@@ -122,7 +128,8 @@ class Yolo2OutputLayerImpl(LayerImpl):
         self._cache = None
         return yolo_activate(self.conf.boundingBoxes, x)
 
-    def _loss(self, x, labels):
+    def _loss(self, x, labels, need_grad=False):
+        """Score of one minibatch (summed over examples); with ``need_grad`` also dScore/dx."""
         c = self.conf
         mb, ch, H, W = x.shape
         pri = _priors(c, x.device, x.dtype)
@@ -145,44 +152,80 @@ class Yolo2OutputLayerImpl(LayerImpl):
         grid = torch.stack([gx, gy], 0).reshape(1, 1, 2, H, W)
         pc = pxy + grid
         ptl, pbr = pc - 0.5 * pwh, pc + 0.5 * pwh
-        itl = torch.maximum(ptl, tl.unsqueeze(1))
-        ibr = torch.minimum(pbr, br.unsqueeze(1))
+        ltl, lbr = tl.unsqueeze(1), br.unsqueeze(1)
+        itl = torch.maximum(ptl, ltl)
+        ibr = torch.minimum(pbr, lbr)
         iwh = (ibr - itl).clamp_min(0)
-        inter = iwh[:, :, 0] * iwh[:, :, 1] * obj.unsqueeze(1)
+        obj1 = obj.unsqueeze(1)
+        inter = iwh[:, :, 0] * iwh[:, :, 1] * obj1
         area_p = pwh[:, :, 0] * pwh[:, :, 1]
         area_l = ((br - tl)[:, 0] * (br - tl)[:, 1]).unsqueeze(1)
         union = area_p + area_l - inter
-        iou = torch.where(union > 0, inter / union.clamp_min(1e-12), torch.zeros_like(inter)) * obj.unsqueeze(1)
-        resp = torch.nn.functional.one_hot(iou.detach().argmax(1), B).permute(0, 3, 1, 2).to(x.dtype)
-        resp = resp * obj.unsqueeze(1)                                    # mask1_ij_obj [mb, B, H, W]
+        valid = (union > 0).to(x.dtype) * obj1
+        iou = inter / union.clamp_min(1e-12) * valid
+        resp = torch.nn.functional.one_hot(iou.argmax(1), B).permute(0, 3, 1, 2).to(x.dtype)
+        resp = resp * obj1                                                # mask1_ij_obj [mb, B, H, W]
         noresp = 1 - resp
         l2 = c.lossPositionScale if getattr(c, "lossPositionScale", None) is not None else LossL2()
         lcls = c.lossClassPredictions if getattr(c, "lossClassPredictions", None) is not None else LossL2()
         ident = ActivationIdentity()
+        soft = ActivationSoftmax()
 
         def flat(t):   # [mb, B, k, H, W] -> [mb*B*H*W, k]
             return t.permute(0, 1, 3, 4, 2).reshape(-1, t.shape[2])
+
+        def unflat(t):
+            return t.reshape(mb, B, H, W, -1).permute(0, 1, 4, 2, 3)
         m2 = resp.reshape(-1, 1)
+        nr2 = noresp.reshape(-1, 1)
         rep = lambda t: t.unsqueeze(1).expand(mb, B, *t.shape[1:])  # noqa: E731
+        psq = pwh.sqrt()
         pos = l2.computeScore(flat(rep(center_in)), flat(pxy), ident, m2, False)
-        size = l2.computeScore(flat(rep(wh_lab_sqrt)), flat(pwh.sqrt()), ident, m2, False)
+        size = l2.computeScore(flat(rep(wh_lab_sqrt)), flat(psq), ident, m2, False)
         label_conf = (iou * resp).reshape(-1, 1)
         pc2 = pconf.reshape(-1, 1)
         lc = LossL2()
+        lam = c.lambdaNoObj
         conf_loss = lc.computeScore(label_conf, pc2, ident, m2, False) + \
-            c.lambdaNoObj * lc.computeScore(label_conf, pc2, ident, noresp.reshape(-1, 1), False)
-        cls_loss = lcls.computeScore(flat(rep(cls_lab)), flat(x5[:, :, 5:]), ActivationSoftmax(), m2, False)
-        return c.lambdaCoord * (pos + size) + conf_loss + cls_loss
+            lam * lc.computeScore(label_conf, pc2, ident, nr2, False)
+        cls_loss = lcls.computeScore(flat(rep(cls_lab)), flat(x5[:, :, 5:]), soft, m2, False)
+        loss = c.lambdaCoord * (pos + size) + conf_loss + cls_loss
+        if not need_grad:
+            return loss
+        lcd = c.lambdaCoord
+        g_xy = lcd * unflat(l2.computeGradient(flat(rep(center_in)), flat(pxy), ident, m2))
+        g_wh = lcd * unflat(l2.computeGradient(flat(rep(wh_lab_sqrt)), flat(psq), ident, m2)) * 0.5 / psq
+        g_conf = (lc.computeGradient(label_conf, pc2, ident, m2) +
+                  lam * lc.computeGradient(label_conf, pc2, ident, nr2)).reshape(mb, B, H, W)
+        # confidence label = IOU on the responsible anchor: d/dlabel = -d/dconf of the (label - conf)^2 terms
+        g_iou = -g_conf * resp
+        u2 = union.clamp_min(1e-12) ** 2
+        g_inter = g_iou * valid * (union + inter) / u2                    # d(inter / (A + L - inter))/d inter
+        g_area = -g_iou * valid * inter / u2
+        pos_w = ((ibr - itl) >= 0).to(x.dtype)                            # clamp_min(0) passes gradient at >= 0
+        g_iwh = torch.stack([g_inter * iwh[:, :, 1], g_inter * iwh[:, :, 0]], 2) * obj1.unsqueeze(2) * pos_w
+
+        def sel(a, b, lt):                                                # share of d min/max going to ``a``
+            return (a < b).to(x.dtype) + 0.5 * (a == b).to(x.dtype) if lt else \
+                (a > b).to(x.dtype) + 0.5 * (a == b).to(x.dtype)
+        g_pbr = g_iwh * sel(pbr, lbr, True)
+        g_ptl = -g_iwh * sel(ptl, ltl, False)
+        g_xy = g_xy + g_pbr + g_ptl
+        g_wh = g_wh + 0.5 * (g_pbr - g_ptl) + torch.stack([g_area * pwh[:, :, 1], g_area * pwh[:, :, 0]], 2)
+        d_xy = g_xy * pxy * (1 - pxy)
+        d_wh = g_wh * pwh
+        d_c = (g_conf * pconf * (1 - pconf)).unsqueeze(2)
+        d_cls = unflat(lcls.computeGradient(flat(rep(cls_lab)), flat(x5[:, :, 5:]), soft, m2))
+        dx = torch.cat([d_xy, d_wh, d_c, d_cls.to(x.dtype)], 2).reshape(mb, ch, H, W)
+        return loss, dx
 
     def _compute(self):
         if self._cache is not None:
             return self._cache
         dt = torch.float64 if self.input.dtype == torch.float64 else torch.float32
-        x = self.input.detach().to(dt).requires_grad_(True)
-        with torch.enable_grad():
-            loss = self._loss(x, self.labels.to(x.device))
-            (g,) = torch.autograd.grad(loss, [x])
-        self._cache = (loss.detach(), g)
+        with torch.no_grad():
+            loss, g = self._loss(self.input.detach().to(dt), self.labels.to(self.input.device), need_grad=True)
+        self._cache = (loss, g)
         return self._cache
 
     def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
