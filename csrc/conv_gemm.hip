@@ -336,8 +336,8 @@ __device__ __forceinline__ typename MfmaT<DT>::v8 frag_tr_asm(const char* T, int
   const unsigned a0 = (unsigned)(uintptr_t)((lds_cptr)T + mc_off(k0, col));
   const unsigned a1 = (unsigned)(uintptr_t)((lds_cptr)T + mc_off(k0 + 4, col));
   s16x8_t f;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a0));
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"(a1));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=&v"(f.lo) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=&v"(f.hi) : "v"(a1));
   return __builtin_bit_cast(v8, f);
 }
 
@@ -567,9 +567,16 @@ __global__ __launch_bounds__(256) void conv_wrw_reduce_v3(const float* __restric
                                                           const float* __restrict__ partb, float* __restrict__ db) {
   const long long total = (long long)K * C * RS;
   if (db && blockIdx.x == gridDim.x - 1) {
+    // fixed-order bias reduce, 8 independent loads in flight per thread (a serial split loop here was the tail)
     for (int k = threadIdx.x; k < K; k += blockDim.x) {
       float a = 0.f;
-      for (int sp = 0; sp < splits; ++sp) a += partb[(long long)sp * K + k];
+      for (int sp0 = 0; sp0 < splits; sp0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = partb[(long long)min(sp0 + u, splits - 1) * K + k];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += sp0 + u < splits ? v[u] : 0.f;
+      }
       db[k] = a;
     }
   }

@@ -269,8 +269,8 @@ __device__ __forceinline__ typename MfmaT<DT>::v8 frag16(const char* T, int rbas
     const unsigned a0 = (unsigned)(uintptr_t)((lds_cptr)T + mc16_off(k, col));
     const unsigned a1 = (unsigned)(uintptr_t)((lds_cptr)T + mc16_off(k + 4, col));
     s16x8_t f;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.lo) : "v"(a0));
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.hi) : "v"(a1));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=&v"(f.lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=&v"(f.hi) : "v"(a1));
     return __builtin_bit_cast(v8, f);
   }
 }

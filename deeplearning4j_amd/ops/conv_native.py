@@ -42,6 +42,8 @@ native.register_sig("dl4j_conv_v3_default_variant", [c_ll, c_int])
 native.register_sig("dl4j_conv_wrw_v3_num_variants", [])
 native.register_sig("dl4j_conv_wrw_v3_ws_floats", [c_int] * 9 + [ctypes.POINTER(c_int)], restype=c_ll)
 native.register_sig("dl4j_conv_wrw_v3", [c_int] + [c_void_p] * 5 + [c_int] * 17 + [c_void_p])
+native.register_sig("dl4j_conv_wrw_halo_ws_floats", [c_int] * 17 + [ctypes.POINTER(c_int)], restype=c_ll)
+native.register_sig("dl4j_conv_wrw_halo", [c_int] + [c_void_p] * 5 + [c_int] * 17 + [c_void_p])
 
 # Optional per-shape override of the weight-gradient split count (tuning): {(N,H,W,C,K,R,S,stride): splits}
 WRW_SPLITS = {}
@@ -466,54 +468,90 @@ def _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need
     direct = gW is not None and gW.dtype == torch.float32 and gW.is_contiguous()
     dWt = gW if direct else torch.empty((K, C, R, S), dtype=torch.float32, device=x.device)
     geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW)
-    v = _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed) if V3 else -1
-    if v >= 0:
-        # round-3 tile engine: per-split fp32 slabs + fixed-order reduce into the DL4J layout (deterministic)
+    v = _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed) if V3 else ("r2",)
+    if v[0] != "r2":
+        # round-3 engines (tile-engine v3 / halo): per-split fp32 slabs + fixed-order reduce into the DL4J layout
         db_out = dbt = None
         if need_db:
             directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
             dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
             db_out = None if directb else dbt
-        native._check(_wrw_v3_launch(v, x, dy, dWt, geom, dbt), "conv_wrw_v3")
+        native._check(_wrw_launch(v, x, dy, dWt, geom, dbt), "conv_wrw_" + v[0])
         return (None if direct else dWt), db_out
     return _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb,
                           grads_zeroed, dWt, direct)
 
 
 _WRW_CHOICE = {}
+HALO = os.environ.get("DL4J_AMD_WRW_HALO", "1") == "1"
 
 
-def _wrw_v3_launch(var, x, dy, dWt, geom, db=None):
+def _wrw_launch(choice, x, dy, dWt, geom, db=None):
+    """choice: ("v3", variant) tile engine (csrc/conv_gemm.hip) or ("halo", variant, splits) halo-staged engine
+    (csrc/conv_wrw.hip); returns the kernel status (-1: shape not supported)."""
     lib = native.load()
     N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
     sp = ctypes.c_int(0)
+    if choice[0] == "halo":
+        var, splits = choice[1], choice[2]
+        nf = lib.dl4j_conv_wrw_halo_ws_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW, var, splits,
+                                              ctypes.byref(sp))
+        if nf <= 0:
+            return -1
+        ws = _det_scratch(nf, x.device)
+        return lib.dl4j_conv_wrw_halo(1, _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, splits,
+                                      _stream())
+    var = choice[1]
     nf = lib.dl4j_conv_wrw_v3_ws_floats(N, C, K, R, S, OH, OW, var, 0, ctypes.byref(sp))
     ws = _det_scratch(nf, x.device)
     return lib.dl4j_conv_wrw_v3(1, _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, 0, _stream())
 
 
+def _wrw_v3_launch(var, x, dy, dWt, geom, db=None):
+    return _wrw_launch(("v3", var), x, dy, dWt, geom, db)
+
+
+def _halo_candidates(geom):
+    """Applicable halo-engine variants with their default split count and half / double of it."""
+    if not HALO:
+        return []
+    lib = native.load()
+    N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
+    out = []
+    for var in (1, 2, 3, 4):
+        sp = ctypes.c_int(0)
+        if lib.dl4j_conv_wrw_halo_ws_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW, var, 0,
+                                            ctypes.byref(sp)) <= 0:
+            continue
+        for s in sorted({sp.value, max(1, sp.value // 2), 2 * sp.value}):
+            out.append(("halo", var, s))
+    return out
+
+
 def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
-    """Per-shape weight-gradient kernel: the first eager call times the round-3 tile variants and the round-2
-    atomic kernel (on scratch outputs, inline on this stream) and keeps the fastest. Deterministic mode only
-    considers the round-3 engine (slab reduce, no atomics). Under HIP-graph capture: remembered choice or variant 0."""
+    """Per-shape weight-gradient kernel: the first eager call times the halo engine (variants x split counts), the
+    round-3 tile variants and the round-2 atomic kernel (on scratch outputs, inline on this stream) and keeps the
+    fastest. Deterministic mode excludes the round-2 atomic kernel. Under HIP-graph capture: the remembered choice,
+    else the first halo candidate, else tile variant 0."""
     det = deterministic()
     key = (geom, det)
     v = _WRW_CHOICE.get(key)
     if v is not None:
         return v
-    if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
-        return 0
     lib = native.load()
+    halo = _halo_candidates(geom)
+    if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
+        return halo[0] if halo else ("v3", 0)
     N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
     scratch = torch.empty_like(dWt)
     sdb = torch.empty(K, dtype=torch.float32, device=dWt.device) if need_db else None
-    cands = list(range(lib.dl4j_conv_wrw_v3_num_variants())) + ([] if det else [-1])
+    cands = halo + [("v3", i) for i in range(lib.dl4j_conv_wrw_v3_num_variants())] + ([] if det else [("r2",)])
     best, bt = None, None
     with side_stream.suspended():
-        for var in cands:
-            if var >= 0:
-                def run(var=var):
-                    return _wrw_v3_launch(var, x, dy, scratch, geom, sdb)
+        for c in cands:
+            if c[0] != "r2":
+                def run(c=c):
+                    return _wrw_launch(c, x, dy, scratch, geom, sdb)
             else:
                 def run():
                     return _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, (sh, sw), (ph, 0, pw, 0), (dh, dw),
@@ -522,8 +560,8 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
                 continue
             t = _timed(run, reps=3)
             if bt is None or t < bt:
-                best, bt = var, t
-    v = _WRW_CHOICE[key] = best if best is not None else -1
+                best, bt = c, t
+    v = _WRW_CHOICE[key] = best if best is not None else ("r2",)
     return v
 
 
@@ -623,14 +661,9 @@ _CHOICE = {}
 
 
 def _timed(fn, reps=2):
-    fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1)
+    """GPU milliseconds per call with the host enqueue hidden (ops/timing.py)."""
+    from .timing import gpu_time
+    return gpu_time(fn, reps=reps)
 
 
 def _choose(key, run_gemm, run_old):

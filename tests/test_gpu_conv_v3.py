@@ -149,3 +149,58 @@ def test_v3_weight_gradient_every_variant(cuda, case):
     conv_native._wrw_v3_launch(0, x, dy, again, geom)
     torch.cuda.synchronize()
     assert torch.equal(again, outs[0])                               # slab reduce: bitwise reproducible
+
+
+HALO_CASES = [
+    # the zoo ResNet-50 weight-gradient geometries at a small batch (3x3 halo chunks of 4 / 7 rows, 2 / 4 images)
+    (2, 64, 28, 28, 64, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (2, 128, 14, 14, 128, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (4, 256, 7, 7, 256, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (8, 512, 4, 4, 512, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),
+    (2, 64, 56, 56, 64, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),            # canonical stage-1 (TH = 1 chunks)
+    (3, 72, 10, 10, 136, 3, 3, (1, 1), (1, 1, 1, 1), (1, 1)),           # partial k / c tiles, odd N
+    (2, 64, 28, 28, 256, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+    (2, 256, 28, 28, 64, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+    (2, 256, 14, 14, 512, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+    (2, 256, 15, 15, 128, 1, 1, (2, 2), (0, 0, 0, 0), (1, 1)),          # strided 1x1 gather, partial last chunk
+    (3, 40, 9, 7, 24, 1, 1, (1, 1), (0, 0, 0, 0), (1, 1)),
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_halo_weight_gradient(cuda, case):
+    """csrc/conv_wrw.hip: every applicable variant and split count (auto, /2, x2) against the fp32 torch weight
+    gradient; conv-bias partials against sum(dY); bitwise reproducible."""
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    x, w, _ = _data(case)
+    wr = w.float().requires_grad_(True)
+    yr = _ref(x, wr, None, stride, pad4, dil)
+    g = torch.Generator().manual_seed(8)
+    dy = torch.randn(yr.shape, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    OH, OW = dy.shape[2], dy.shape[3]
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dil[0], dil[1], OH, OW)
+    cands = conv_native._halo_candidates(geom)
+    assert cands, "no halo variant accepted the shape"
+    db_ref = dy.float().sum(dim=(0, 2, 3))
+    for i, c in enumerate(cands):
+        dW = torch.full((K, C, R, S), 3.0, device=cuda)
+        db = torch.full((K,), 3.0, device=cuda)
+        assert conv_native._wrw_launch(c, x, dy, dW, geom, db if i % 2 == 0 else None) == 0, c
+        torch.cuda.synchronize()
+        _close(dW, wr.grad, 1e-2)
+        if i % 2 == 0:
+            _close(db, db_ref, 1e-3)
+        again = torch.empty_like(dW)
+        conv_native._wrw_launch(c, x, dy, again, geom)
+        torch.cuda.synchronize()
+        assert torch.equal(again, dW), c
+
+
+def test_halo_rejects_unsupported_shapes():
+    lib = native.load()
+    import ctypes
+    sp = ctypes.c_int(0)
+    # 3x3 stride 2 and 5x5 are not halo shapes: the chooser must see 0 and fall back
+    assert lib.dl4j_conv_wrw_halo_ws_floats(2, 9, 9, 64, 64, 3, 3, 2, 2, 1, 1, 1, 1, 5, 5, 0, 0, ctypes.byref(sp)) == 0
+    assert lib.dl4j_conv_wrw_halo_ws_floats(2, 9, 9, 64, 64, 5, 5, 1, 1, 2, 2, 1, 1, 9, 9, 0, 0, ctypes.byref(sp)) == 0

@@ -38,16 +38,9 @@ def capture_shapes(variant):
 
 
 def timeit(fn, reps):
-    for _ in range(3):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / reps
+    """GPU ms per call, host enqueue hidden behind a spin kernel (deeplearning4j_amd/ops/timing.py)."""
+    from deeplearning4j_amd.ops.timing import gpu_time
+    return gpu_time(fn, reps=reps, warmup=3)
 
 
 def main():
