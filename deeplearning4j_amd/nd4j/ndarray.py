@@ -410,8 +410,25 @@ class INDArray:
         return self
 
     # ------------------------------------------------------------------ arithmetic (copy and in-place forms)
-    def _bin(self, other, fn, inplace):
+    def _bin(self, other, fn, inplace, kop=None):
+        """GPU operands go through the ND4J broadcast / scalar kernels (csrc/nd4j_ops.hip, ``kop``); the result of
+        an in-place op is written straight into this array when the broadcast shape is its own."""
         o = _unwrap(other)
+        if kop is not None and self._t.is_cuda:
+            from ..ops import nd4j_kernels as K
+            ob = o if torch.is_tensor(o) or isinstance(o, (int, float)) else None
+            if ob is not None and not (torch.is_tensor(ob) and ob.dtype != self._t.dtype):
+                if inplace:
+                    with torch.no_grad():
+                        r = K.binary(self._t, ob, kop, out=self._t if self._t.is_contiguous() else None)
+                        if r is not None:
+                            if r is not self._t:
+                                self._t.copy_(r)
+                            return self
+                else:
+                    r = K.binary(self._t, ob, kop)
+                    if r is not None:
+                        return _wrap(r)
         if inplace:
             with torch.no_grad():
                 r = fn(self._t, o)
@@ -420,40 +437,40 @@ class INDArray:
         return _wrap(fn(self._t, o))
 
     def add(self, o):
-        return self._bin(o, torch.add, False)
+        return self._bin(o, torch.add, False, "add")
 
     def addi(self, o):
-        return self._bin(o, torch.add, True)
+        return self._bin(o, torch.add, True, "add")
 
     def sub(self, o):
-        return self._bin(o, torch.sub, False)
+        return self._bin(o, torch.sub, False, "sub")
 
     def subi(self, o):
-        return self._bin(o, torch.sub, True)
+        return self._bin(o, torch.sub, True, "sub")
 
     def mul(self, o):
-        return self._bin(o, torch.mul, False)
+        return self._bin(o, torch.mul, False, "mul")
 
     def muli(self, o):
-        return self._bin(o, torch.mul, True)
+        return self._bin(o, torch.mul, True, "mul")
 
     def div(self, o):
-        return self._bin(o, torch.div, False)
+        return self._bin(o, torch.div, False, "div")
 
     def divi(self, o):
-        return self._bin(o, torch.div, True)
+        return self._bin(o, torch.div, True, "div")
 
     def rsub(self, o):
-        return self._bin(o, lambda a, b: b - a, False)
+        return self._bin(o, lambda a, b: b - a, False, "rsub")
 
     def rsubi(self, o):
-        return self._bin(o, lambda a, b: b - a, True)
+        return self._bin(o, lambda a, b: b - a, True, "rsub")
 
     def rdiv(self, o):
-        return self._bin(o, lambda a, b: b / a, False)
+        return self._bin(o, lambda a, b: b / a, False, "rdiv")
 
     def rdivi(self, o):
-        return self._bin(o, lambda a, b: b / a, True)
+        return self._bin(o, lambda a, b: b / a, True, "rdiv")
 
     def neg(self):
         return _wrap(-self._t)
@@ -469,70 +486,70 @@ class INDArray:
     def remainder(self, o):
         return self._bin(o, torch.remainder, False)
 
-    # row / column vector broadcasts
+    # row / column vector broadcasts (GPU: the ND4J broadcast kernel)
     def _vec(self, v, row):
         t = _unwrap(v)
         return t.reshape(1, -1) if row else t.reshape(-1, 1)
 
     def addRowVector(self, v):
-        return _wrap(self._t + self._vec(v, True))
+        return self._bin(self._vec(v, True), torch.add, False, "add")
 
     def addiRowVector(self, v):
-        return self._bin(self._vec(v, True), torch.add, True)
+        return self._bin(self._vec(v, True), torch.add, True, "add")
 
     def subRowVector(self, v):
-        return _wrap(self._t - self._vec(v, True))
+        return self._bin(self._vec(v, True), torch.sub, False, "sub")
 
     def subiRowVector(self, v):
-        return self._bin(self._vec(v, True), torch.sub, True)
+        return self._bin(self._vec(v, True), torch.sub, True, "sub")
 
     def mulRowVector(self, v):
-        return _wrap(self._t * self._vec(v, True))
+        return self._bin(self._vec(v, True), torch.mul, False, "mul")
 
     def muliRowVector(self, v):
-        return self._bin(self._vec(v, True), torch.mul, True)
+        return self._bin(self._vec(v, True), torch.mul, True, "mul")
 
     def divRowVector(self, v):
-        return _wrap(self._t / self._vec(v, True))
+        return self._bin(self._vec(v, True), torch.div, False, "div")
 
     def diviRowVector(self, v):
-        return self._bin(self._vec(v, True), torch.div, True)
+        return self._bin(self._vec(v, True), torch.div, True, "div")
 
     def rsubRowVector(self, v):
-        return _wrap(self._vec(v, True) - self._t)
+        return self._bin(self._vec(v, True), lambda a, b: b - a, False, "rsub")
 
     def rdivRowVector(self, v):
-        return _wrap(self._vec(v, True) / self._t)
+        return self._bin(self._vec(v, True), lambda a, b: b / a, False, "rdiv")
 
     def addColumnVector(self, v):
-        return _wrap(self._t + self._vec(v, False))
+        return self._bin(self._vec(v, False), torch.add, False, "add")
 
     def addiColumnVector(self, v):
-        return self._bin(self._vec(v, False), torch.add, True)
+        return self._bin(self._vec(v, False), torch.add, True, "add")
 
     def subColumnVector(self, v):
-        return _wrap(self._t - self._vec(v, False))
+        return self._bin(self._vec(v, False), torch.sub, False, "sub")
 
     def subiColumnVector(self, v):
-        return self._bin(self._vec(v, False), torch.sub, True)
+        return self._bin(self._vec(v, False), torch.sub, True, "sub")
 
     def mulColumnVector(self, v):
-        return _wrap(self._t * self._vec(v, False))
+        return self._bin(self._vec(v, False), torch.mul, False, "mul")
 
     def muliColumnVector(self, v):
-        return self._bin(self._vec(v, False), torch.mul, True)
+        return self._bin(self._vec(v, False), torch.mul, True, "mul")
 
     def divColumnVector(self, v):
-        return _wrap(self._t / self._vec(v, False))
+        return self._bin(self._vec(v, False), torch.div, False, "div")
 
     def diviColumnVector(self, v):
-        return self._bin(self._vec(v, False), torch.div, True)
+        return self._bin(self._vec(v, False), torch.div, True, "div")
 
     def rsubColumnVector(self, v):
-        return _wrap(self._vec(v, False) - self._t)
+        return self._bin(self._vec(v, False), lambda a, b: b - a, False, "rsub")
 
     def rdivColumnVector(self, v):
-        return _wrap(self._vec(v, False) / self._t)
+        return self._bin(self._vec(v, False), lambda a, b: b / a, False, "rdiv")
 
     # matrix products
     def mmul(self, other, result=None):
@@ -628,8 +645,14 @@ class INDArray:
         return self.divi(o)
 
     # ------------------------------------------------------------------ reductions
-    def _red(self, fn, dims, keep2d=True):
+    def _red(self, fn, dims, keep2d=True, kop=None, bias_corrected=True):
         t = self._t
+        if kop is not None and t.is_cuda and t.is_floating_point():
+            from ..ops import nd4j_kernels as K
+            whole = not dims or (len(dims) == 1 and dims[0] == 2147483647)
+            r = K.reduce(t, kop, None if whole else _norm_dims(dims, t.dim()), bias_corrected=bias_corrected)
+            if r is not None:
+                return _wrap(r.reshape(1, 1) if whole else (_as_2d(r) if keep2d else r))
         if not t.is_floating_point():
             t = t.double()
         if not dims or (len(dims) == 1 and dims[0] == 2147483647):       # Integer.MAX_VALUE = whole array
@@ -639,53 +662,66 @@ class INDArray:
         return _wrap(_as_2d(r) if keep2d else r)
 
     def sum(self, *dims):
-        return self._red(lambda t, d: t.sum() if d is None else t.sum(d), dims)
+        return self._red(lambda t, d: t.sum() if d is None else t.sum(d), dims, kop="sum")
 
     def mean(self, *dims):
-        return self._red(lambda t, d: t.mean() if d is None else t.mean(d), dims)
+        return self._red(lambda t, d: t.mean() if d is None else t.mean(d), dims, kop="mean")
 
     def prod(self, *dims):
-        return self._red(lambda t, d: t.prod() if d is None else _multi(torch.prod, t, d), dims)
+        return self._red(lambda t, d: t.prod() if d is None else _multi(torch.prod, t, d), dims, kop="prod")
 
     def max(self, *dims):
-        return self._red(lambda t, d: t.max() if d is None else t.amax(d), dims)
+        return self._red(lambda t, d: t.max() if d is None else t.amax(d), dims, kop="max")
 
     def min(self, *dims):
-        return self._red(lambda t, d: t.min() if d is None else t.amin(d), dims)
+        return self._red(lambda t, d: t.min() if d is None else t.amin(d), dims, kop="min")
 
     def amax(self, *dims):
-        return self._red(lambda t, d: t.abs().max() if d is None else t.abs().amax(d), dims)
+        return self._red(lambda t, d: t.abs().max() if d is None else t.abs().amax(d), dims, kop="amax")
 
     def amin(self, *dims):
-        return self._red(lambda t, d: t.abs().min() if d is None else t.abs().amin(d), dims)
+        return self._red(lambda t, d: t.abs().min() if d is None else t.abs().amin(d), dims, kop="amin")
 
     def std(self, *dims, biasCorrected=True):
         if dims and isinstance(dims[0], bool):
             biasCorrected, dims = dims[0], dims[1:]
         c = 1 if biasCorrected else 0
-        return self._red(lambda t, d: t.std(correction=c) if d is None else t.std(d, correction=c), dims)
+        return self._red(lambda t, d: t.std(correction=c) if d is None else t.std(d, correction=c), dims,
+                         kop="std", bias_corrected=biasCorrected)
 
     def var(self, *dims, biasCorrected=True):
         if dims and isinstance(dims[0], bool):
             biasCorrected, dims = dims[0], dims[1:]
         c = 1 if biasCorrected else 0
-        return self._red(lambda t, d: t.var(correction=c) if d is None else t.var(d, correction=c), dims)
+        return self._red(lambda t, d: t.var(correction=c) if d is None else t.var(d, correction=c), dims,
+                         kop="var", bias_corrected=biasCorrected)
 
     def norm1(self, *dims):
-        return self._red(lambda t, d: t.abs().sum() if d is None else t.abs().sum(d), dims)
+        return self._red(lambda t, d: t.abs().sum() if d is None else t.abs().sum(d), dims, kop="norm1")
 
     def norm2(self, *dims):
-        return self._red(lambda t, d: t.pow(2).sum().sqrt() if d is None else t.pow(2).sum(d).sqrt(), dims)
+        return self._red(lambda t, d: t.pow(2).sum().sqrt() if d is None else t.pow(2).sum(d).sqrt(), dims,
+                         kop="norm2")
 
     def normmax(self, *dims):
         return self.amax(*dims)
 
     def argMax(self, *dims):
+        if self._t.is_cuda and self._t.is_floating_point():
+            from ..ops import nd4j_kernels as K
+            r = K.reduce(self._t, "argmax", [dims[0]] if dims else None)
+            if r is not None:
+                return _wrap(r.reshape(1, 1) if not dims else _as_2d(r))
         if not dims:
             return _wrap(self._t.reshape(-1).argmax().reshape(1, 1))
         return _wrap(_as_2d(self._t.argmax(dims[0])))
 
     def argMin(self, *dims):
+        if self._t.is_cuda and self._t.is_floating_point():
+            from ..ops import nd4j_kernels as K
+            r = K.reduce(self._t, "argmin", [dims[0]] if dims else None)
+            if r is not None:
+                return _wrap(r.reshape(1, 1) if not dims else _as_2d(r))
         if not dims:
             return _wrap(self._t.reshape(-1).argmin().reshape(1, 1))
         return _wrap(_as_2d(self._t.argmin(dims[0])))
@@ -756,40 +792,53 @@ class Transforms:
     vector similarity helpers."""
 
     @staticmethod
-    def _apply(x, fn, dup=True):
+    def _apply(x, fn, dup=True, kop=None, a0=0.0, a1=0.0):
+        """GPU arrays run the ND4J transform kernel ``kop`` (csrc/nd4j_ops.hip), in place when ``dup`` is False."""
+        t = _unwrap(x)
+        if kop is not None and torch.is_tensor(t) and t.is_cuda:
+            from ..ops import nd4j_kernels as K
+            with torch.no_grad():
+                r = K.transform(t, kop, a0, a1, out=None if dup or not t.is_contiguous() else t)
+            if r is not None:
+                if dup:
+                    return _wrap(r)
+                if r is not t:
+                    with torch.no_grad():
+                        x._t.copy_(r)
+                return x
         if dup:
-            return _wrap(fn(_unwrap(x)))
+            return _wrap(fn(t))
         with torch.no_grad():
             x._t.copy_(fn(x._t))
         return x
 
-    sigmoid = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sigmoid, dup))
-    tanh = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.tanh, dup))
-    relu = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.relu, dup))
-    exp = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.exp, dup))
-    log = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.log, dup))
-    abs = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.abs, dup))
-    sqrt = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sqrt, dup))
-    sign = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sign, dup))
-    floor = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.floor, dup))
-    ceil = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.ceil, dup))
-    round = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.round, dup))
-    sin = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sin, dup))
-    cos = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.cos, dup))
-    acos = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.acos, dup))
-    asin = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.asin, dup))
-    atan = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.atan, dup))
-    softplus = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.softplus, dup))
-    softsign = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.softsign, dup))
-    elu = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.elu, dup))
-    hardTanh = staticmethod(lambda x, dup=True: Transforms._apply(x, lambda t: t.clamp(-1, 1), dup))
+    sigmoid = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sigmoid, dup, "sigmoid"))
+    tanh = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.tanh, dup, "tanh"))
+    relu = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.relu, dup, "relu"))
+    exp = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.exp, dup, "exp"))
+    log = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.log, dup, "log"))
+    abs = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.abs, dup, "abs"))
+    sqrt = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sqrt, dup, "sqrt"))
+    sign = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sign, dup, "sign"))
+    floor = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.floor, dup, "floor"))
+    ceil = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.ceil, dup, "ceil"))
+    round = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.round, dup, "round"))
+    sin = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.sin, dup, "sin"))
+    cos = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.cos, dup, "cos"))
+    acos = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.acos, dup, "acos"))
+    asin = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.asin, dup, "asin"))
+    atan = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.atan, dup, "atan"))
+    softplus = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.softplus, dup, "softplus"))
+    softsign = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.softsign, dup, "softsign"))
+    elu = staticmethod(lambda x, dup=True: Transforms._apply(x, torch.nn.functional.elu, dup, "elu", 1.0))
+    hardTanh = staticmethod(lambda x, dup=True: Transforms._apply(x, lambda t: t.clamp(-1, 1), dup, "hardtanh"))
     identity = staticmethod(lambda x, dup=True: Transforms._apply(x, lambda t: t, dup))
     stabilize = staticmethod(lambda x, k=1.0, dup=True: Transforms._apply(
         x, lambda t: t.clamp(-1e4 / k, 1e4 / k), dup))
 
     @staticmethod
     def leakyRelu(x, alpha=0.01, dup=True):
-        return Transforms._apply(x, lambda t: torch.nn.functional.leaky_relu(t, alpha), dup)
+        return Transforms._apply(x, lambda t: torch.nn.functional.leaky_relu(t, alpha), dup, "leakyrelu", alpha)
 
     @staticmethod
     def pow(x, p, dup=True):

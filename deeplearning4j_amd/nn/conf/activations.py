@@ -15,6 +15,22 @@ from .base import Config, register_enum
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
+def _kf(x, op, a0=0.0, a1=0.0):
+    """GPU tensors (fp32 / bf16 / fp16, not tracked by autograd) run the ND4J transform kernel
+    (csrc/nd4j_ops.hip); anything else returns None and the torch expression below is used."""
+    if not (torch.is_tensor(x) and x.is_cuda):
+        return None
+    from deeplearning4j_amd.ops import nd4j_kernels
+    return nd4j_kernels.transform(x, op, a0, a1)
+
+
+def _kb(z, eps, op, a0=0.0):
+    if not (torch.is_tensor(z) and z.is_cuda and torch.is_tensor(eps) and eps.dtype == z.dtype):
+        return None
+    from deeplearning4j_amd.ops import nd4j_kernels
+    return nd4j_kernels.transform_bp(z, eps, op, a0)
+
+
 class IActivation(Config):
     def getActivation(self, x, training=False):
         raise NotImplementedError
@@ -37,17 +53,29 @@ class ActivationIdentity(IActivation):
 
 class ActivationReLU(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "relu", 0.0)
+        if r is not None:
+            return r
         return torch.relu(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "relu", 0.0)
+        if r is not None:
+            return r
         return torch.where(z > 0, epsilon, torch.zeros((), dtype=epsilon.dtype, device=epsilon.device))
 
 
 class ActivationReLU6(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "relu6", 0.0)
+        if r is not None:
+            return r
         return torch.clamp(x, 0.0, 6.0)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "relu6", 0.0)
+        if r is not None:
+            return r
         return epsilon * ((z > 0) & (z < 6)).to(epsilon.dtype)
 
 
@@ -55,9 +83,15 @@ class ActivationLReLU(IActivation):
     FIELDS = {"alpha": 0.01}
 
     def getActivation(self, x, training=False):
+        r = _kf(x, "leakyrelu", self.alpha)
+        if r is not None:
+            return r
         return torch.nn.functional.leaky_relu(x, self.alpha)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "leakyrelu", self.alpha)
+        if r is not None:
+            return r
         return torch.where(z > 0, epsilon, epsilon * self.alpha)
 
 
@@ -81,9 +115,15 @@ class ActivationELU(IActivation):
     FIELDS = {"alpha": 1.0}
 
     def getActivation(self, x, training=False):
+        r = _kf(x, "elu", self.alpha)
+        if r is not None:
+            return r
         return torch.nn.functional.elu(x, self.alpha)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "elu", self.alpha)
+        if r is not None:
+            return r
         return torch.where(z > 0, epsilon, epsilon * self.alpha * torch.exp(z))
 
 
@@ -92,43 +132,73 @@ class ActivationSELU(IActivation):
     S = 1.0507009873554804934193349852946
 
     def getActivation(self, x, training=False):
+        r = _kf(x, "selu", 0.0)
+        if r is not None:
+            return r
         return torch.selu(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "selu", 0.0)
+        if r is not None:
+            return r
         return epsilon * torch.where(z > 0, torch.full_like(z, self.S), self.S * self.A * torch.exp(z))
 
 
 class ActivationSigmoid(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "sigmoid", 0.0)
+        if r is not None:
+            return r
         return torch.sigmoid(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "sigmoid", 0.0)
+        if r is not None:
+            return r
         s = torch.sigmoid(z)
         return epsilon * s * (1 - s)
 
 
 class ActivationHardSigmoid(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "hardsigmoid", 0.0)
+        if r is not None:
+            return r
         return torch.clamp(0.2 * x + 0.5, 0.0, 1.0)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "hardsigmoid", 0.0)
+        if r is not None:
+            return r
         return epsilon * (0.2 * ((z > -2.5) & (z < 2.5)).to(epsilon.dtype))
 
 
 class ActivationTanH(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "tanh", 0.0)
+        if r is not None:
+            return r
         return torch.tanh(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "tanh", 0.0)
+        if r is not None:
+            return r
         t = torch.tanh(z)
         return epsilon * (1 - t * t)
 
 
 class ActivationHardTanH(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "hardtanh", 0.0)
+        if r is not None:
+            return r
         return torch.clamp(x, -1.0, 1.0)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "hardtanh", 0.0)
+        if r is not None:
+            return r
         return epsilon * ((z > -1) & (z < 1)).to(epsilon.dtype)
 
 
@@ -136,11 +206,17 @@ class ActivationRationalTanh(IActivation):
     """f(x) = 1.7159 * tanh_approx(2x/3), tanh_approx(y) = sgn(y)(1 - 1/(1+|y|+y^2+1.41645 y^4))."""
 
     def getActivation(self, x, training=False):
+        r = _kf(x, "rationaltanh", 0.0)
+        if r is not None:
+            return r
         y = 2.0 * x / 3.0
         a = torch.abs(y)
         return 1.7159 * torch.sign(y) * (1 - 1 / (1 + a + y * y + 1.41645 * y ** 4))
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "rationaltanh", 0.0)
+        if r is not None:
+            return r
         y = 2.0 * z / 3.0
         a = torch.abs(y)
         d = 1 + a + y * y + 1.41645 * y ** 4
@@ -150,43 +226,73 @@ class ActivationRationalTanh(IActivation):
 
 class ActivationRectifiedTanh(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "rectifiedtanh", 0.0)
+        if r is not None:
+            return r
         return torch.clamp(torch.tanh(x), min=0)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "rectifiedtanh", 0.0)
+        if r is not None:
+            return r
         t = torch.tanh(z)
         return torch.where(z > 0, epsilon * (1 - t * t), torch.zeros_like(epsilon))
 
 
 class ActivationSoftPlus(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "softplus", 0.0)
+        if r is not None:
+            return r
         return torch.nn.functional.softplus(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "softplus", 0.0)
+        if r is not None:
+            return r
         return epsilon * torch.sigmoid(z)
 
 
 class ActivationSoftSign(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "softsign", 0.0)
+        if r is not None:
+            return r
         return x / (1 + torch.abs(x))
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "softsign", 0.0)
+        if r is not None:
+            return r
         d = 1 + torch.abs(z)
         return epsilon / (d * d)
 
 
 class ActivationCube(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "cube", 0.0)
+        if r is not None:
+            return r
         return x * x * x
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "cube", 0.0)
+        if r is not None:
+            return r
         return epsilon * 3 * z * z
 
 
 class ActivationSwish(IActivation):
     def getActivation(self, x, training=False):
+        r = _kf(x, "swish", 0.0)
+        if r is not None:
+            return r
         return x * torch.sigmoid(x)
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "swish", 0.0)
+        if r is not None:
+            return r
         s = torch.sigmoid(z)
         return epsilon * (s + z * s * (1 - s))
 
@@ -196,9 +302,15 @@ class ActivationGELU(IActivation):
     FIELDS = {"precise": False}
 
     def getActivation(self, x, training=False):
+        r = _kf(x, "gelu" if self.precise else "gelu_tanh")
+        if r is not None:
+            return r
         return torch.nn.functional.gelu(x, approximate="none" if self.precise else "tanh")
 
     def backprop(self, z, epsilon):
+        r = _kb(z, epsilon, "gelu" if self.precise else "gelu_tanh")
+        if r is not None:
+            return r
         if self.precise:
             cdf = 0.5 * (1 + torch.erf(z / math.sqrt(2)))
             pdf = torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi)

@@ -70,6 +70,11 @@ class ElementWiseVertex(GraphVertex):
                 out = out + x
             return out / len(inputs), len(inputs)
         if op == "Max":
+            if inputs[0].is_cuda:
+                from deeplearning4j_amd.ops import nd4j_kernels as K
+                r = K.mergemax(list(inputs))                        # mergemax kernel (csrc/nd4j_ops.hip)
+                if r is not None:
+                    return r[0], ("mergemax", r[1], len(inputs))
             st = torch.stack(list(inputs), 0)
             out, idx = st.max(dim=0)
             return out, (idx, len(inputs))
@@ -94,6 +99,13 @@ class ElementWiseVertex(GraphVertex):
         if op == "Average":
             return [eps / ctx] * ctx
         if op == "Max":
+            if isinstance(ctx[0], str):
+                from deeplearning4j_amd.ops import nd4j_kernels as K
+                _, am, n = ctx
+                r = K.mergemax_bp(eps.to(am.device), am, n) if eps.is_cuda else None
+                if r is not None:
+                    return r
+                return [eps * (am == i).to(eps.dtype) for i in range(n)]
             idx, n = ctx
             return [eps * (idx == i).to(eps.dtype) for i in range(n)]
         raise ValueError(op)

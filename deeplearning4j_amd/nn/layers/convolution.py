@@ -308,14 +308,29 @@ class Cropping2DImpl(LayerImpl):
         return self.make_gradient(), g
 
 
+def _nd4j():
+    from ...ops import nd4j_kernels
+    return nd4j_kernels
+
+
 class Upsampling2DImpl(LayerImpl):
+    """GPU: one broadcast-copy kernel forward, one permute-copy + row-sum reduction backward (csrc/nd4j_ops.hip)."""
+
     def activate(self, x, training=False, mask=None):
         s = self.conf.size
+        if x.is_cuda:
+            y = _nd4j().upsample_nearest2d(x, s[0], s[1])
+            if y is not None:
+                return y
         return x.repeat_interleave(s[0], dim=2).repeat_interleave(s[1], dim=3)
 
     def backpropGradient(self, eps):
         s = self.conf.size
         n, c, h, w = eps.shape
+        if eps.is_cuda:
+            g = _nd4j().upsample_nearest2d_bp(eps, s[0], s[1])
+            if g is not None:
+                return self.make_gradient(), g
         return self.make_gradient(), eps.reshape(n, c, h // s[0], s[0], w // s[1], s[1]).sum(dim=(3, 5))
 
 
@@ -336,11 +351,19 @@ class SpaceToDepthImpl(LayerImpl):
     def activate(self, x, training=False, mask=None):
         b = self.conf.blockSize
         n, c, H, W = x.shape
+        if x.is_cuda:
+            y = _nd4j().space_to_depth(x, b)
+            if y is not None:
+                return y
         y = x.reshape(n, c, H // b, b, W // b, b).permute(0, 3, 5, 1, 2, 4)
         return y.reshape(n, b * b * c, H // b, W // b)
 
     def backpropGradient(self, eps):
         b = self.conf.blockSize
+        if eps.is_cuda:
+            g = _nd4j().depth_to_space(eps, b)
+            if g is not None:
+                return self.make_gradient(), g
         n, cc, h, w = eps.shape
         c = cc // (b * b)
         g = eps.reshape(n, b, b, c, h, w).permute(0, 3, 4, 1, 5, 2)
@@ -351,6 +374,11 @@ class SpaceToBatchImpl(LayerImpl):
     def activate(self, x, training=False, mask=None):
         (pt, pb), (pl, pr) = self.conf.padding
         bh, bw = self.conf.blocks
+        if x.is_cuda:
+            y = _nd4j().space_to_batch(x, (bh, bw), ((pt, pb), (pl, pr)))
+            if y is not None:
+                self._shape = (x.shape, (x.shape[0], x.shape[1], x.shape[2] + pt + pb, x.shape[3] + pl + pr))
+                return y
         xp = F.pad(x, (pl, pr, pt, pb))
         n, c, H, W = xp.shape
         self._shape = (x.shape, xp.shape)
@@ -362,5 +390,9 @@ class SpaceToBatchImpl(LayerImpl):
         bh, bw = self.conf.blocks
         xs, xps = self._shape
         n, c, H, W = xps
+        if eps.is_cuda:
+            g = _nd4j().batch_to_space(eps, (bh, bw), ((pt, pb), (pl, pr)))
+            if g is not None:
+                return self.make_gradient(), g
         g = eps.reshape(bh, bw, n, c, H // bh, W // bw).permute(2, 3, 4, 0, 5, 1).reshape(n, c, H, W)
         return self.make_gradient(), g[:, :, pt:pt + xs[2], pl:pl + xs[3]]

@@ -7,6 +7,11 @@ def reverse_time_series(x, mask=None):
     each example's valid (mask==1, left-aligned) prefix is reversed in place and padding stays put."""
     tdim = x.dim() - 1
     if mask is None:
+        if x.is_cuda:
+            from deeplearning4j_amd.ops import nd4j_kernels
+            r = nd4j_kernels.reverse(x, [tdim])                    # negative-stride copy kernel (nd4j_ops.hip)
+            if r is not None:
+                return r
         return torch.flip(x, [tdim])
     T = x.shape[tdim]
     lengths = mask.reshape(mask.shape[0], -1).sum(dim=1).long()            # [mb]
