@@ -445,37 +445,36 @@ static inline void bn_reduce_stage(float*& p1, float*& p2, int& nblk, int C, flo
     else hipLaunchKernelGGL((KERNEL<T, false, false>), __VA_ARGS__);                   \
   } while (0)
 
-// dtype: 0 fp32, 1 bf16. ws: >= dl4j_bn_workspace_floats floats. ctx_out: 4*C floats (mean, invstd, scale, shift)
-// res: optional residual (same layout as x) -> y = relu(bn(x) + res) (relu forced on).
-DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C, const float* gamma,
-                         const float* beta, float gconst, float bconst, float* run_mean, float* run_var, float decay,
-                         float eps, int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256) return -1;
-  if (res) relu = 1;
+// dtype: 0 fp32, 1 bf16, 2 fp16. ws: >= dl4j_bn_workspace_floats floats. ctx_out: 4*C floats (mean, invstd,
+// scale, shift). res: optional residual (same layout as x) -> y = relu(bn(x) + res) (relu forced on).
+template <typename T>
+static int bn_fwd_impl(const T* x, const T* res, T* y, long long M, int C, const float* gamma, const float* beta,
+                       float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
+                       int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
   float* q = p2 + (long long)nblk * C;
-  const dim3 fg((C + 63) / 64);
-  const int ag = apply_grid(M, C);
-  if (dtype == 1) {
-    const bf16* xb = (const bf16*)x;
-    if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
-    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
-    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
-                       run_mean, run_var, decay, eps, training, ctx_out);
-    BN_DISPATCH3(bn_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, xb, (const bf16*)res, (bf16*)y, M, C, ctx_out);
-  } else {
-    const float* xf = (const float*)x;
-    if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
-    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
-    hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
-                       run_mean, run_var, decay, eps, training, ctx_out);
-    BN_DISPATCH3(bn_apply, float, relu, res, dim3(ag), dim3(256), 0, s, xf, (const float*)res, (float*)y, M, C,
-                 ctx_out);
-  }
+  if (training) hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(256), 0, s, x, M, C, rpb, p1, p2);
+  if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
+  hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, x, gamma, beta, gconst,
+                     bconst, run_mean, run_var, decay, eps, training, ctx_out);
+  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C, ctx_out);
   return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                         const float* beta, float gconst, float bconst, float* run_mean, float* run_var, float decay,
+                         float eps, int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256) return -1;
+  if (res) relu = 1;
+#define BNF(T) return bn_fwd_impl<T>((const T*)x, (const T*)res, (T*)y, M, C, gamma, beta, gconst, bconst, run_mean, \
+                                     run_var, decay, eps, training, relu, ws, ctx_out, s)
+  if (dtype == 1) BNF(bf16);
+  if (dtype == 2) BNF(f16);
+  BNF(float);
+#undef BNF
 }
 
 // Training forward with the statistics already reduced per tile by the producing conv kernel (tstats, P partials):
@@ -485,31 +484,40 @@ DL4J_API long long dl4j_bn_tiles_workspace_floats(long long P, int C) {
   return 2 * S * C + 2 * ((S + 31) / 32) * C + 8LL * C;
 }
 
-DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* y, long long M, int C,
-                               const float* tstats, long long P, const float* gamma, const float* beta, float gconst,
-                               float bconst, float* run_mean, float* run_var, float decay, float eps, int relu,
-                               float* ws, float* ctx_out, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256 || dtype != 1 || P < 1) return -1;
-  if (res) relu = 1;
+template <typename T>
+static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C, const float* tstats, long long P,
+                             const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
+                             float* run_var, float decay, float eps, int relu, float* ws, float* ctx_out,
+                             hipStream_t s) {
   int S = (int)((P + 31) / 32);
   float* p1 = ws;
   float* p2 = ws + (long long)S * C;
   float* q = p2 + (long long)S * C;
-  const bf16* xb = (const bf16*)x;
-  hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2, 64);
+  hipLaunchKernelGGL(bn_tiles_reduce<T>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2, 64);
   bn_reduce_stage(p1, p2, S, C, q, s);
-  hipLaunchKernelGGL(bn_finalize<bf16>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, S, C, M, xb, gamma, beta, gconst,
+  hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, S, C, M, xb, gamma, beta, gconst,
                      bconst, run_mean, run_var, decay, eps, 1, ctx_out);
-  const int ag = apply_grid(M, C);
-  BN_DISPATCH3(bn_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, xb, (const bf16*)res, (bf16*)y, M, C, ctx_out);
+  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C, ctx_out);
   return (int)hipGetLastError();
 }
 
-// dres: gradient w.r.t. the fused residual input (required when res != nullptr).
-DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres, long long M,
-                         int C, const float* ctx, float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256) return -1;
+DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* y, long long M, int C,
+                               const float* tstats, long long P, const float* gamma, const float* beta, float gconst,
+                               float bconst, float* run_mean, float* run_var, float decay, float eps, int relu,
+                               float* ws, float* ctx_out, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || (dtype != 1 && dtype != 2) || P < 1) return -1;
   if (res) relu = 1;
+  if (dtype == 2)
+    return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, gamma, beta, gconst,
+                                  bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, s);
+  return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, gamma, beta, gconst,
+                                 bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, s);
+}
+
+// dres: gradient w.r.t. the fused residual input (required when res != nullptr).
+template <typename T>
+static int bn_bwd_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, long long M, int C, const float* ctx,
+                       float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
@@ -517,25 +525,25 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
   float* q = p2 + (long long)nblk * C;
   float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
   float* cdg = cdb + C;
-  const int ag = apply_grid(M, C);
-  if (dtype == 1) {
-    BN_DISPATCH3(bn_bwd_partial, bf16, relu, res, dim3(nblk), dim3(256), 0, s, (const bf16*)x, (const bf16*)res,
-                 (const bf16*)dy, M, C, rpb, ctx, p1, p2);
-  } else {
-    BN_DISPATCH3(bn_bwd_partial, float, relu, res, dim3(nblk), dim3(256), 0, s, (const float*)x, (const float*)res,
-                 (const float*)dy, M, C, rpb, ctx, p1, p2);
-  }
+  BN_DISPATCH3(bn_bwd_partial, T, relu, res, dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1, p2);
   bn_reduce_stage(p1, p2, nblk, C, q, s);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
                      cdg);
-  if (dtype == 1) {
-    BN_DISPATCH3(bn_bwd_apply, bf16, relu, res, dim3(ag), dim3(256), 0, s, (const bf16*)x, (const bf16*)res,
-                 (const bf16*)dy, (bf16*)dx, (bf16*)dres, M, C, ctx, cdb, cdg);
-  } else {
-    BN_DISPATCH3(bn_bwd_apply, float, relu, res, dim3(ag), dim3(256), 0, s, (const float*)x, (const float*)res,
-                 (const float*)dy, (float*)dx, (float*)dres, M, C, ctx, cdb, cdg);
-  }
+  BN_DISPATCH3(bn_bwd_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, dy, dx, dres, M, C, ctx,
+               cdb, cdg);
   return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres, long long M,
+                         int C, const float* ctx, float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256) return -1;
+  if (res) relu = 1;
+#define BNB(T) return bn_bwd_impl<T>((const T*)x, (const T*)res, (const T*)dy, (T*)dx, (T*)dres, M, C, ctx, dgamma, \
+                                     dbeta, relu, ws, s)
+  if (dtype == 1) BNB(bf16);
+  if (dtype == 2) BNB(f16);
+  BNB(float);
+#undef BNB
 }
 
 // -------------------------------------------------------------------------------------------- BN + ReLU + max pool
@@ -930,12 +938,12 @@ static void bnpool_fwd_launch(const T* x, T* y, unsigned char* am, T* xh, const 
 
 // x: conv output NHWC [N,H,W,C]; y: pooled [N,OH,OW,C]; am / xh: per pooled element (training only, may be null).
 // ws: >= dl4j_bn_workspace_floats(N*H*W, C). ctx_out: 4*C floats.
-DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* am, void* xh, int N, int H, int W,
-                              int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
-                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
-                              float* run_var, float decay, float eps, int training, const float* tstats,
-                              long long P, int rpp, float* ws, float* ctx_out, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127 || kh < 1 || kw < 1) return -1;
+template <typename T>
+static int bn_pool_fwd_impl(const T* xb, T* y, unsigned char* am, T* xh, int N, int H, int W, int C, int OH, int OW,
+                            int kh, int kw, int sh, int sw, int pt, int pl, const float* gamma, const float* beta,
+                            float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
+                            int training, const float* tstats, long long P, int rpp, float* ws, float* ctx_out,
+                            hipStream_t s) {
   const long long M = (long long)N * H * W;
   int nblk;
   long long rpb;
@@ -945,44 +953,46 @@ DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* 
   float* q = p2 + (long long)nblk * C;
   const dim3 fg((C + 63) / 64);
   const int pg = ew_grid((long long)N * OH * OW * (C / 8));
-  if (dtype == 1 && training && tstats) {
-    // statistics already reduced per 64-row tile by the producing conv's epilogue (ws sized for P tiles)
+  if (training && tstats && sizeof(T) == 2) {
+    // statistics already reduced per tile by the producing conv's epilogue (ws sized for P tiles)
     nblk = (int)((P + 31) / 32);
     p2 = ws + (long long)nblk * C;
     q = p2 + (long long)nblk * C;
-    const bf16* xb = (const bf16*)x;
-    hipLaunchKernelGGL(bn_tiles_reduce<bf16>, dim3((C + 63) / 64, nblk), dim3(256), 0, s, tstats, P, C, M, xb, p1,
-                       p2, rpp);
+    hipLaunchKernelGGL(bn_tiles_reduce<T>, dim3((C + 63) / 64, nblk), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2,
+                       rpp);
     bn_reduce_stage(p1, p2, nblk, C, q, s);
-    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
+    hipLaunchKernelGGL(bn_finalize<T>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, 1, ctx_out);
-    bnpool_fwd_launch<bf16>(xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg, s);
-    return (int)hipGetLastError();
-  }
-  if (dtype == 1) {
-    const bf16* xb = (const bf16*)x;
-    if (training) hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
-    if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
-    hipLaunchKernelGGL(bn_finalize<bf16>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
-                       run_mean, run_var, decay, eps, training, ctx_out);
-    bnpool_fwd_launch<bf16>(xb, (bf16*)y, am, (bf16*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg, s);
   } else {
-    const float* xf = (const float*)x;
-    if (training) hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(256), 0, s, xf, M, C, rpb, p1, p2);
+    if (training) hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(256), 0, s, xb, M, C, rpb, p1, p2);
     if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
-    hipLaunchKernelGGL(bn_finalize<float>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xf, gamma, beta, gconst, bconst,
+    hipLaunchKernelGGL(bn_finalize<T>, fg, dim3(256), 0, s, p1, p2, nblk, C, M, xb, gamma, beta, gconst, bconst,
                        run_mean, run_var, decay, eps, training, ctx_out);
-    bnpool_fwd_launch<float>(xf, (float*)y, am, (float*)xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg,
-                             s);
   }
+  bnpool_fwd_launch<T>(xb, y, am, xh, ctx_out, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, pg, s);
   return (int)hipGetLastError();
 }
 
+DL4J_API int dl4j_bn_pool_fwd(int dtype, const void* x, void* y, unsigned char* am, void* xh, int N, int H, int W,
+                              int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
+                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
+                              float* run_var, float decay, float eps, int training, const float* tstats,
+                              long long P, int rpp, float* ws, float* ctx_out, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127 || kh < 1 || kw < 1) return -1;
+#define BPF(T) return bn_pool_fwd_impl<T>((const T*)x, (T*)y, am, (T*)xh, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, \
+                                          gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, training,    \
+                                          tstats, P, rpp, ws, ctx_out, s)
+  if (dtype == 1) BPF(bf16);
+  if (dtype == 2) BPF(f16);
+  BPF(float);
+#undef BPF
+}
+
 // dy: gradient w.r.t. the pooled output; dx: w.r.t. x (the BN input). ws: >= dl4j_bn_workspace_floats(N*OH*OW, C).
-DL4J_API int dl4j_bn_pool_bwd(int dtype, const void* x, const void* dy, const unsigned char* am, const void* xh,
-                              void* dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw,
-                              int pt, int pl, const float* ctx, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127) return -1;
+template <typename T>
+static int bn_pool_bwd_impl(const T* x, const T* dy, const unsigned char* am, const T* xh, T* dx, int N, int H, int W,
+                            int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl, const float* ctx,
+                            float* dgamma, float* dbeta, float* ws, hipStream_t s) {
   const long long Mp = (long long)N * OH * OW, M = (long long)N * H * W;
   int nblk;
   long long rpb;
@@ -993,43 +1003,37 @@ DL4J_API int dl4j_bn_pool_bwd(int dtype, const void* x, const void* dy, const un
   float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
   float* cdg = cdb + C;
   const int g = ew_grid(M * (C / 8));
-  if (dtype == 1)
-    hipLaunchKernelGGL(bnpool_bwd_partial<bf16>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, am, (const bf16*)xh,
-                       Mp, C, rpb, p1, p2);
-  else
-    hipLaunchKernelGGL(bnpool_bwd_partial<float>, dim3(nblk), dim3(256), 0, s, (const float*)dy, am,
-                       (const float*)xh, Mp, C, rpb, p1, p2);
+  hipLaunchKernelGGL(bnpool_bwd_partial<T>, dim3(nblk), dim3(256), 0, s, dy, am, xh, Mp, C, rpb, p1, p2);
   bn_reduce_stage(p1, p2, nblk, C, q, s);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
                      cdg);
   const bool two = kh <= 2 * sh && kw <= 2 * sw;
   // staged variant: pooled rows covering 2 input rows, all in LDS
   const int maxrows = (2 - 1 + kh - 1) / sh + 1;
-  const size_t lds = (size_t)maxrows * OW * C * ((dtype == 1 ? 2 : 4) + 1);
+  const size_t lds = (size_t)maxrows * OW * C * (sizeof(T) + 1);
   if (two && lds <= 64 * 1024) {
     const int nb = N * ((H + 1) / 2);
-    if (dtype == 1)
-      hipLaunchKernelGGL(bnpool_bwd_dx_lds<bf16>, dim3(nb), dim3(256), lds, s, (const bf16*)x, (const bf16*)dy, am,
-                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, maxrows);
-    else
-      hipLaunchKernelGGL(bnpool_bwd_dx_lds<float>, dim3(nb), dim3(256), lds, s, (const float*)x, (const float*)dy, am,
-                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl, maxrows);
+    hipLaunchKernelGGL(bnpool_bwd_dx_lds<T>, dim3(nb), dim3(256), lds, s, x, dy, am, dx, ctx, cdb, cdg, N, H, W, C, OH,
+                       OW, kh, kw, sh, sw, pt, pl, maxrows);
     return (int)hipGetLastError();
   }
-  if (dtype == 1) {
-    if (two)
-      hipLaunchKernelGGL(bnpool_bwd_dx2<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am,
-                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
-    else
-      hipLaunchKernelGGL(bnpool_bwd_dx<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy, am,
-                         (bf16*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
-  } else {
-    if (two)
-      hipLaunchKernelGGL(bnpool_bwd_dx2<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
-                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
-    else
-      hipLaunchKernelGGL(bnpool_bwd_dx<float>, dim3(g), dim3(256), 0, s, (const float*)x, (const float*)dy, am,
-                         (float*)dx, ctx, cdb, cdg, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl);
-  }
+  if (two)
+    hipLaunchKernelGGL(bnpool_bwd_dx2<T>, dim3(g), dim3(256), 0, s, x, dy, am, dx, ctx, cdb, cdg, N, H, W, C, OH, OW,
+                       kh, kw, sh, sw, pt, pl);
+  else
+    hipLaunchKernelGGL(bnpool_bwd_dx<T>, dim3(g), dim3(256), 0, s, x, dy, am, dx, ctx, cdb, cdg, N, H, W, C, OH, OW,
+                       kh, kw, sh, sw, pt, pl);
   return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_bn_pool_bwd(int dtype, const void* x, const void* dy, const unsigned char* am, const void* xh,
+                              void* dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw,
+                              int pt, int pl, const float* ctx, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || kh * kw > 127) return -1;
+#define BPB(T) return bn_pool_bwd_impl<T>((const T*)x, (const T*)dy, am, (const T*)xh, (T*)dx, N, H, W, C, OH, OW, kh, \
+                                          kw, sh, sw, pt, pl, ctx, dgamma, dbeta, ws, s)
+  if (dtype == 1) BPB(bf16);
+  if (dtype == 2) BPB(f16);
+  BPB(float);
+#undef BPB
 }

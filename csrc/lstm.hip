@@ -39,6 +39,18 @@ template <> struct Mf<bf16> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
+// fp16: same fragment shapes as bf16 on v_mfma_f32_16x16x32_f16.
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8m_t;
+template <> struct Mf<f16> {
+  static constexpr int KC = 32, FE = 8;
+  typedef f16x8m_t frag;
+  static __device__ __forceinline__ frag load(const f16* p, int lane) {
+    return *reinterpret_cast<const frag*>(p + 8 * (lane >> 4));
+  }
+  static __device__ __forceinline__ f4_t mma(frag a, frag b, f4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 // fp32: four 16x16x4 MFMAs cover k = 16; lane group h = l>>4 supplies k = 4h + j for MFMA j (the same permuted
 // k order on A and B, so the sum is exact f32 fma chains).
 template <> struct Mf<float> {
@@ -58,6 +70,7 @@ template <> struct Mf<float> {
 template <typename T> __device__ __forceinline__ T cvt(float v);
 template <> __device__ __forceinline__ float cvt<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 cvt<bf16>(float v) { return __float2bfloat16(v); }
+template <> __device__ __forceinline__ f16 cvt<f16>(float v) { return (f16)v; }
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_f(float x) {
@@ -440,6 +453,11 @@ static int bwd_launch(const float* eps, const float* gates, const float* call, c
       if (nt == 2) return pp ? FN<bf16, 2, true>(__VA_ARGS__) : FN<bf16, 2, false>(__VA_ARGS__);  \
       return pp ? FN<bf16, 4, true>(__VA_ARGS__) : FN<bf16, 4, false>(__VA_ARGS__);          \
     }                                                                                       \
+    if (dtype == 2) {                                                                       \
+      if (nt == 1) return pp ? FN<f16, 1, true>(__VA_ARGS__) : FN<f16, 1, false>(__VA_ARGS__);  \
+      if (nt == 2) return pp ? FN<f16, 2, true>(__VA_ARGS__) : FN<f16, 2, false>(__VA_ARGS__);  \
+      return pp ? FN<f16, 4, true>(__VA_ARGS__) : FN<f16, 4, false>(__VA_ARGS__);           \
+    }                                                                                       \
     if (dtype == 0) {                                                                       \
       if (nt == 1) return pp ? FN<float, 1, true>(__VA_ARGS__) : FN<float, 1, false>(__VA_ARGS__); \
       if (nt == 2) return pp ? FN<float, 2, true>(__VA_ARGS__) : FN<float, 2, false>(__VA_ARGS__); \
@@ -452,7 +470,7 @@ static int bwd_launch(const float* eps, const float* gates, const float* call, c
 DL4J_API int dl4j_lstm_fwd(int dtype, const void* zx, const void* rwt, const float* peep, const float* h0,
                            const float* c0, const float* mask, float* out, float* gates, float* call, float* hT,
                            float* cT, int Tn, int mb, int H, hipStream_t s) {
-  if (Tn < 1 || mb < 1 || (dtype == 1 && H % 32 != 0)) return -1;
+  if (Tn < 1 || mb < 1 || (dtype != 0 && H % 32 != 0)) return -1;
   LSTM_DISPATCH(fwd_launch, zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, Tn, mb, H, s);
 }
 

@@ -258,11 +258,15 @@ __device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int 
     const int rows = min(64, g.M - rbeg);
     const float bb = g.bias_mode == 1 ? g.bias[n] : 0.f;
     float s1 = 0.f, s2 = 0.f, sh = 0.f;
+    // statistics of the values exactly as stored (bf16 or fp16 rounding of the output dtype)
+    auto stored = [&](float v) {
+      return g.out_dt == 2 ? __half2float(__float2half(v)) : (g.out_dt == 0 ? v : bf2f(to16(v, 1)));
+    };
     if (rows > 0) {
       const char* src = T + (part * 64) * PITCH + col * 4;
-      sh = bf2f(to16(*reinterpret_cast<const float*>(src) * g.alpha + bb, 1));
+      sh = stored(*reinterpret_cast<const float*>(src) * g.alpha + bb);
       for (int r = 0; r < rows; ++r) {
-        const float d = bf2f(to16(*reinterpret_cast<const float*>(src + r * PITCH) * g.alpha + bb, 1)) - sh;
+        const float d = stored(*reinterpret_cast<const float*>(src + r * PITCH) * g.alpha + bb) - sh;
         s1 += d;
         s2 = fmaf(d, d, s2);
       }

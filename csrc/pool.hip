@@ -98,6 +98,7 @@ DL4J_API int dl4j_pool_fwd(int dtype, int mode, const void* x, void* y, unsigned
   const int g = grid_for((long long)N * OH * OW * (C / 8));
 #define PF(T, M) hipLaunchKernelGGL((pool_fwd<T, M>), dim3(g), dim3(256), 0, s, (const T*)x, (T*)y, argmax, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl)
   if (dtype == 1) { if (mode == 0) PF(bf16, true); else PF(bf16, false); }
+  else if (dtype == 2) { if (mode == 0) PF(f16, true); else PF(f16, false); }
   else { if (mode == 0) PF(float, true); else PF(float, false); }
 #undef PF
   return (int)hipGetLastError();
@@ -109,6 +110,7 @@ DL4J_API int dl4j_pool_bwd(int dtype, int mode, const void* dy, const unsigned c
   const int g = grid_for((long long)N * H * W * (C / 8));
 #define PB(T, M) hipLaunchKernelGGL((pool_bwd<T, M>), dim3(g), dim3(256), 0, s, (const T*)dy, argmax, (T*)dx, N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl)
   if (dtype == 1) { if (mode == 0) PB(bf16, true); else PB(bf16, false); }
+  else if (dtype == 2) { if (mode == 0) PB(f16, true); else PB(f16, false); }
   else { if (mode == 0) PB(float, true); else PB(float, false); }
 #undef PB
   return (int)hipGetLastError();

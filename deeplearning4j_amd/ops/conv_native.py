@@ -148,9 +148,9 @@ def _relayout(w, want_krsc, want_flip):
     need_f = want_flip and (fresh or e.vf != v)
     if need_k or need_f:
         if need_k and e.krsc is None:
-            e.krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device)
+            e.krsc = torch.empty((K, R, S, C), dtype=w.dtype, device=w.device)
         if need_f and e.flip is None:
-            e.flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device)
+            e.flip = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
         wc = w.contiguous()
         rc = native.load().dl4j_conv_w_relayout(_ptr(wc), _ptr(e.krsc if need_k else None),
                                                 _ptr(e.flip if need_f else None), K, C, R, S, _stream())
@@ -168,7 +168,7 @@ _plans = {}
 def relayout_all(weights, want_flip=True):
     """Refresh the kernel-layout copies of every eligible conv weight in ONE launch (dl4j_conv_w_relayout_batched),
     ahead of the forward pass; the per-conv lazy path then finds fresh copies. Returns the number of weights."""
-    ws = [w for w in weights if w.dtype == torch.bfloat16 and w.is_cuda and w.dim() == 4 and w.is_contiguous()
+    ws = [w for w in weights if w.dtype in _KDT and w.is_cuda and w.dim() == 4 and w.is_contiguous()
           and w.shape[1] % 8 == 0 and w.shape[0] % 4 == 0]
     if not ws:
         return 0
@@ -185,10 +185,10 @@ def relayout_all(weights, want_flip=True):
             K, C, R, S = w.shape
             e = _ent(w)
             if e.krsc is None:
-                e.krsc = torch.empty((K, R, S, C), dtype=torch.bfloat16, device=w.device)
+                e.krsc = torch.empty((K, R, S, C), dtype=w.dtype, device=w.device)
             flip_ok = want_flip and K % 8 == 0
             if flip_ok and e.flip is None:
-                e.flip = torch.empty((C, R, S, K), dtype=torch.bfloat16, device=w.device)
+                e.flip = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
             n = K * C * R * S
             outs = [(0, e.krsc)] + ([(1, e.flip)] if flip_ok else [])
             for kind, buf in outs:
@@ -213,8 +213,22 @@ def relayout_all(weights, want_flip=True):
     return len(ws)
 
 
+_KDT = (torch.bfloat16, torch.float16)
+
+
 def _ok_act(t):
-    return t.dtype == torch.bfloat16 and t.dim() == 4 and t.is_cuda
+    return t.dtype in _KDT and t.dim() == 4 and t.is_cuda
+
+
+def _dtc(t):
+    """Kernel dtype code: 1 bf16, 2 fp16."""
+    return 2 if t.dtype == torch.float16 else 1
+
+
+def _q(t):
+    """Channel granularity the kernels need: bf16 runs every shape (round-2 kernels as the fallback tile), fp16 only
+    the round-3 engines, whose reduction tiles are 64 channels deep."""
+    return 64 if t.dtype == torch.float16 else 8
 
 
 def _cl(t):
@@ -231,11 +245,12 @@ def _out_hw(H, W, R, S, stride, pad4, dilation):
 def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True):
     """want_stats: also emit per-tile BatchNorm statistics of the output from the kernel epilogue; they are attached
     to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer."""
-    if not (_ok_act(x) and w.dtype == torch.bfloat16):
+    if not (_ok_act(x) and w.dtype == x.dtype):
         return None
     N, C, H, W = x.shape
     K, Cw, R, S = w.shape
-    if C == 3 and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
+    fp16 = x.dtype == torch.float16
+    if C == 3 and not fp16 and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
         from . import conv_stem
         if conv_stem.supported(_cl(x), w, b, stride, pad4, dilation):
             y = conv_stem.forward(_cl(x), w, want_stats)
@@ -252,7 +267,7 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
         from .gemm import mmul
         x = _cl(x)
         M = N * H * W
-        y = arena.empty((N, K, H, W), torch.bfloat16, x.device, channels_last=True)
+        y = arena.empty((N, K, H, W), x.dtype, x.device, channels_last=True)
         ts = None
         if want_stats and C % 64 == 0 and K % 8 == 0:
             P = 2 * ((M + 127) // 128)
@@ -262,15 +277,17 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
         if ts is not None:
             y._bn_tile_stats = (ts, ts.shape[1])
         return y
+    if fp16 and not _v3_ok(C, K, R, S):
+        return None                                    # fp16 runs on the round-3 engine only
     krsc, _ = _relayout(w, True, False)
     x = _cl(x)
-    y = arena.empty((N, K, OH, OW), torch.bfloat16, x.device, channels_last=True)
+    y = arena.empty((N, K, OH, OW), x.dtype, x.device, channels_last=True)
     bias = b.float().contiguous() if b is not None else None
     stats = want_stats and C % 32 == 0 and R * S <= 64 and K % 8 == 0
     geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dilation[0], dilation[1], OH, OW)
     v = -1
     if _v3_ok(C, K, R, S):
-        key = ("fwd", geom, bias is not None, stats)
+        key = ("fwd", geom, bias is not None, stats, x.dtype)
         v = _v3_pick(key, lambda var, out, t: _fwd_launch(var, x, krsc, bias, out, geom, 0.0, t),
                      y, lambda var: _stats_buf(var, N * OH * OW, K, x.device) if stats else None)
     ts = _stats_buf(v, N * OH * OW, K, x.device) if stats else None
@@ -302,11 +319,11 @@ def _fwd_launch(variant, x, wk, bias, y, geom, beta, ts):
     negative code / HIP error otherwise."""
     lib = native.load()
     if variant >= 0:
-        rc = lib.dl4j_conv_fwd_v3(1, _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts), variant,
-                                  _stream())
+        rc = lib.dl4j_conv_fwd_v3(_dtc(x), _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts),
+                                  variant, _stream())
         return 1 if (rc == 0 and ts is not None) else rc
     N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
-    if beta != 0.0:
+    if beta != 0.0 or x.dtype != torch.bfloat16:
         return -1
     return lib.dl4j_conv_fwd(_ptr(x), _ptr(wk), _ptr(bias), _ptr(y), N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH,
                              OW, _ptr(ts), _stream())
@@ -324,7 +341,7 @@ def _v3_pick(key, launch, out, make_ts):
     M, K = geom[0] * geom[13] * geom[14], geom[4]
     if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
         return lib.dl4j_conv_v3_default_variant(M, K)
-    cands = list(range(lib.dl4j_conv_v3_num_variants())) + [-1]
+    cands = list(range(lib.dl4j_conv_v3_num_variants())) + ([-1] if out.dtype == torch.bfloat16 else [])
     scratch = torch.empty_like(out)
     if key[0] == "bwd_acc":
         scratch.copy_(out)
@@ -347,11 +364,12 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
     whole flat gradient with one fill per step), so no per-layer memset is launched.
     dx_accum: an existing channels-last bf16 gradient of x (another consumer's contribution); when the bwd-data
     kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx."""
-    if not (_ok_act(x) and _ok_act(dy) and w.dtype == torch.bfloat16):
+    if not (_ok_act(x) and _ok_act(dy) and w.dtype == x.dtype and dy.dtype == x.dtype):
         return None
     N, C, H, W = x.shape
     K, Cw, R, S = w.shape
-    if C == 3 and not need_dx and need_dw and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
+    fp16 = x.dtype == torch.float16
+    if C == 3 and not fp16 and not need_dx and need_dw and os.environ.get("DL4J_AMD_KERNEL_STEM", "1") == "1":
         from . import conv_stem
         if conv_stem.supported(_cl(x), w, None, stride, pad4, dilation) and _cl(dy).shape[1] == 64:
             r = conv_stem.backward_weight(_cl(x), _cl(dy), gW, gb, need_db)
@@ -362,28 +380,27 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
     OH, OW = dy.shape[2], dy.shape[3]
     x = _cl(x)
     dy = _cl(dy)
+    adt = x.dtype
     lib = native.load()
     dx = None
     pw = _is_pointwise(R, S, stride, pad4, dilation)
     if need_dx and pw and gemm_dx:
         from .gemm import mmul
         M = N * H * W
-        acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
+        acc = dx_accum is not None and dx_accum.dtype == adt and tuple(dx_accum.shape) == (N, C, H, W) \
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
-        dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
-                                              channels_last=True)
+        dx = dx_accum if acc else arena.empty((N, C, H, W), adt, x.device, channels_last=True)
         # dX[M, C] = dY[M, K] . W[K, C]  (+= the other consumer's gradient through beta)
         mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
              beta=1.0 if acc else 0.0)
     elif need_dx:
         s1 = tuple(stride) == (1, 1) and tuple(dilation) == (1, 1)
         pure_1x1 = R == 1 and S == 1 and not any(pad4) and tuple(dilation) == (1, 1)
-        acc = dx_accum is not None and dx_accum.dtype == torch.bfloat16 and tuple(dx_accum.shape) == (N, C, H, W) \
+        acc = dx_accum is not None and dx_accum.dtype == adt and tuple(dx_accum.shape) == (N, C, H, W) \
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
-        if s1 and (H, W) == _out_hw_inv(OH, OW, R, S, pad4, H, W):
+        if s1 and (H, W) == _out_hw_inv(OH, OW, R, S, pad4, H, W) and (not fp16 or _v3_ok(K, C, R, S)):
             _, flip = _relayout(w, False, True)
-            dx = dx_accum if acc else arena.empty((N, C, H, W), torch.bfloat16, x.device,
-                                                  channels_last=True)
+            dx = dx_accum if acc else arena.empty((N, C, H, W), adt, x.device, channels_last=True)
             # transposed conv: "input" dY (OH x OW x K), flipped CRSK weights, pad' = R-1-pad, output H x W x C
             geo_b = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
 
@@ -394,10 +411,10 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
                                                  pad4[2], OH, OW, int(acc), _stream())
             v = -1
             if _v3_ok(K, C, R, S):
-                v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b), bwd_launch, dx, lambda var: None)
+                v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b, adt), bwd_launch, dx, lambda var: None)
             rc = bwd_launch(v, dx, None)
             native._check(rc, "conv_bwd_data_s1")
-        elif pure_1x1 and stride[0] == stride[1]:
+        elif pure_1x1 and stride[0] == stride[1] and not fp16:
             _, flip = _relayout(w, False, True)
             if acc:
                 dx = dx_accum                                # only the strided rows are touched (+=)
@@ -415,7 +432,7 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             sh, sw = stride
             eh = H - ((OH - 1) * sh + R - pad4[0] - pad4[1])
             ew = W - ((OW - 1) * sw + S - pad4[2] - pad4[3])
-            dyz = torch.empty((N, K, (OH - 1) * sh + 1 + eh, (OW - 1) * sw + 1 + ew), dtype=torch.bfloat16,
+            dyz = torch.empty((N, K, (OH - 1) * sh + 1 + eh, (OW - 1) * sw + 1 + ew), dtype=adt,
                               device=x.device, memory_format=torch.channels_last).zero_()
             dyz[:, :, :(OH - 1) * sh + 1:sh, :(OW - 1) * sw + 1:sw] = dy
             dx = _conv2d_bwd(x, w, dyz, (1, 1), pad4, dilation, True, False, False, dx_accum=dx_accum)[0]
@@ -499,12 +516,12 @@ def _wrw_launch(choice, x, dy, dWt, geom, db=None):
         if nf <= 0:
             return -1
         ws = _det_scratch(nf, x.device)
-        return lib.dl4j_conv_wrw_halo(1, _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, splits,
+        return lib.dl4j_conv_wrw_halo(_dtc(x), _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, splits,
                                       _stream())
     var = choice[1]
     nf = lib.dl4j_conv_wrw_v3_ws_floats(N, C, K, R, S, OH, OW, var, 0, ctypes.byref(sp))
     ws = _det_scratch(nf, x.device)
-    return lib.dl4j_conv_wrw_v3(1, _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, 0, _stream())
+    return lib.dl4j_conv_wrw_v3(_dtc(x), _ptr(x), _ptr(dy), _ptr(dWt), _ptr(db), _ptr(ws), *geom, var, 0, _stream())
 
 
 def _wrw_v3_launch(var, x, dy, dWt, geom, db=None):
@@ -534,7 +551,7 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
     fastest. Deterministic mode excludes the round-2 atomic kernel. Under HIP-graph capture: the remembered choice,
     else the first halo candidate, else tile variant 0."""
     det = deterministic()
-    key = (geom, det)
+    key = (geom, det, x.dtype)
     v = _WRW_CHOICE.get(key)
     if v is not None:
         return v
@@ -545,7 +562,8 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
     N, H, W, C, K, R, S, sh, sw, ph, pw, dh, dw, OH, OW = geom
     scratch = torch.empty_like(dWt)
     sdb = torch.empty(K, dtype=torch.float32, device=dWt.device) if need_db else None
-    cands = halo + [("v3", i) for i in range(lib.dl4j_conv_wrw_v3_num_variants())] + ([] if det else [("r2",)])
+    r2 = [] if det or x.dtype != torch.bfloat16 else [("r2",)]
+    cands = halo + [("v3", i) for i in range(lib.dl4j_conv_wrw_v3_num_variants())] + r2
     best, bt = None, None
     with side_stream.suspended():
         for c in cands:
@@ -561,7 +579,7 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
             t = _timed(run, reps=3)
             if bt is None or t < bt:
                 best, bt = c, t
-    v = _WRW_CHOICE[key] = best if best is not None else ("r2",)
+    v = _WRW_CHOICE[key] = best if best is not None else (("r2",) if x.dtype == torch.bfloat16 else ("v3", 0))
     return v
 
 
@@ -698,6 +716,10 @@ def _r8(n):
     return (n + 7) // 8 * 8
 
 
+def _rq(n, q):
+    return (n + q - 1) // q * q
+
+
 def _stem_case(x, w, b, stride, pad4, dilation):
     if x.shape[1] != 3 or os.environ.get("DL4J_AMD_KERNEL_STEM", "1") != "1":
         return False
@@ -710,11 +732,12 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     to the result as ``y._bn_tile_stats = (planes [3, P, K] fp32, P)`` for a consuming training-mode BN layer.
     Input channel counts that are not a multiple of 8 (RGB / small first layers: AlexNet, LeNet, GoogLeNet stems)
     are zero-padded to the next multiple of 8 so they still run on the MFMA kernels (exact: zero channels add 0)."""
-    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and x.shape[1] == w.shape[1] \
-            and x.shape[1] % 8 and not _stem_case(x, w, b, stride, pad4, dilation):
-        C8 = _r8(x.shape[1])
+    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == x.dtype and x.shape[1] == w.shape[1] \
+            and x.shape[1] % _q(x) and not (x.dtype == torch.bfloat16 and _stem_case(x, w, b, stride, pad4, dilation)):
+        C8 = _rq(x.shape[1], _q(x))
         return conv2d_fwd(_pad_ch(_cl(x), C8, cl=True), _pad_ch(w, C8), b, stride, pad4, dilation, want_stats)
-    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and w.shape[0] % 4:
+    if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.dtype == x.dtype and w.shape[0] % (4 if x.dtype ==
+                                                                                               torch.bfloat16 else 8):
         K = w.shape[0]
         K8 = _r8(K)
         bp = _pad_ch(b.reshape(-1), K8, 0) if b is not None else None
@@ -729,7 +752,7 @@ def conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False):
     use = True
     if _ok_act(x) and x.dim() == 4 and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
             _is_pointwise(1, 1, stride, pad4, dilation):
-        key = ("fwd", tuple(x.shape), tuple(w.shape), b is not None, bool(want_stats))
+        key = ("fwd", tuple(x.shape), tuple(w.shape), b is not None, bool(want_stats), x.dtype)
         use = _choose(key, lambda: _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, True),
                       lambda: _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, False))
     return _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats, use)
@@ -743,14 +766,15 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
     kernel can take it, the result is accumulated into it in the kernel epilogue and it is returned as dx.
     Channel counts (C or K) that are not a multiple of 8 are zero-padded (see ``conv2d_fwd``); the padded weight
     gradient is cropped into ``gW``."""
-    if _ok_act(x) and _ok_act(dy) and x.dim() == 4 and w.dim() == 4 and w.dtype == torch.bfloat16 and \
-            x.shape[1] == w.shape[1] and (x.shape[1] % 8 or w.shape[0] % 8) and \
-            not (x.shape[1] == 3 and not need_dx and _stem_case(x, w, None, stride, pad4, dilation)):
+    if _ok_act(x) and _ok_act(dy) and x.dim() == 4 and w.dim() == 4 and w.dtype == x.dtype and \
+            x.shape[1] == w.shape[1] and (x.shape[1] % _q(x) or w.shape[0] % _q(x)) and \
+            not (x.dtype == torch.bfloat16 and x.shape[1] == 3 and not need_dx and
+                 _stem_case(x, w, None, stride, pad4, dilation)):
         return _conv2d_bwd_padded(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, dx_accum)
     gdx = gdw = True
     if _ok_act(x) and _ok_act(dy) and w.dim() == 4 and w.shape[2] == 1 and w.shape[3] == 1 and \
             _is_pointwise(1, 1, stride, pad4, dilation):
-        shp = (tuple(x.shape), tuple(w.shape))
+        shp = (tuple(x.shape), tuple(w.shape), x.dtype)
         # scratch copies / buffers are made inside the candidates, i.e. only on the one timed call per shape
         # (an unconditional clone of dx_accum here was a full-activation copy per conv per step)
         def _acc_copy():
@@ -780,7 +804,7 @@ def conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=N
 
 def _conv2d_bwd_padded(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW, gb, dx_accum):
     K, C = w.shape[0], w.shape[1]
-    C8, K8 = _r8(C), _r8(K)
+    C8, K8 = _rq(C, _q(x)), _rq(K, _q(x))
     xp = _pad_ch(_cl(x), C8, cl=True)
     wp = _pad_ch(_pad_ch(w, C8, 1), K8, 0)
     dyp = _pad_ch(_cl(dy), K8, cl=True)

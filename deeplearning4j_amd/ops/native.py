@@ -281,7 +281,7 @@ def _rows_like(t, ref):
 
 
 def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual=None):
-    dt = _dt(x)
+    dt = _dt16(x)
     xr = _as_rows_nhwc(x) if dt is not None else None
     if xr is None:
         return None
@@ -296,7 +296,7 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     b = beta if torch.is_tensor(beta) else None
     res = _rows_like(residual, x) if residual is not None else None
     ts = getattr(x, "_bn_tile_stats", None)
-    if training and ts is not None and dt == 1 and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
+    if training and ts is not None and dt in (1, 2) and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
             (len(ts) < 3 or ts[2] == 64):
         # statistics already reduced per tile by the producing conv kernel's epilogue
         register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_void_p,
@@ -329,7 +329,7 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
-    rc = lib.dl4j_bn_bwd(_dt(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
+    rc = lib.dl4j_bn_bwd(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
                          _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())
     _check(rc, "bn_bwd")
     return dx, dgamma, dbeta, dres
@@ -337,7 +337,7 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
 
 def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel, stride, pad4):
     """Fused BN -> ReLU -> max pool (csrc/batchnorm.hip bnpool_*). x: NHWC conv output. Returns (y_pooled, ctx)."""
-    dt = _dt(x)
+    dt = _dt16(x)
     if dt is None or x.dim() != 4 or not torch.is_tensor(gamma) or run_mean.dtype != torch.float32:
         return None
     if not x.is_contiguous(memory_format=torch.channels_last):
@@ -362,7 +362,7 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
     ts = getattr(x, "_bn_tile_stats", None)
     M = N * H * W
     rpp = ts[2] if ts is not None and len(ts) > 2 else 64
-    if not (training and ts is not None and dt == 1 and ts[0].shape[2] == C and
+    if not (training and ts is not None and dt in (1, 2) and ts[0].shape[2] == C and
             (ts[1] * rpp == M if rpp != 64 else ts[1] == 2 * ((M + 127) // 128))):
         ts = None
     nws = lib.dl4j_bn_workspace_floats(M, C)
@@ -395,7 +395,7 @@ def bn_pool_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     ws = torch.empty(lib.dl4j_bn_workspace_floats(N * OH * OW, C), dtype=torch.float32, device=x.device)
-    rc = lib.dl4j_bn_pool_bwd(_dt(x), _ptr(x), _ptr(dy), _ptr(am), _ptr(xh), _ptr(dx), N, H, W, C, OH, OW, kh, kw,
+    rc = lib.dl4j_bn_pool_bwd(_dt16(x), _ptr(x), _ptr(dy), _ptr(am), _ptr(xh), _ptr(dx), N, H, W, C, OH, OW, kh, kw,
                               sh, sw, pt, pl, _ptr(c), _ptr(dgamma), _ptr(dbeta), _ptr(ws), _stream())
     _check(rc, "bn_pool_bwd")
     return dx, dgamma, dbeta
@@ -424,7 +424,7 @@ def softmax_xent(logits, labels, clip_eps):
 
 # ------------------------------------------------------------------------------------------ pooling
 def pool2d_fwd(x, ptype, kernel, stride, pad4):
-    dt = _dt(x)
+    dt = _dt16(x)
     if dt is None or x.dim() != 4 or x.shape[1] % 8 != 0:
         return None
     if not x.is_contiguous(memory_format=torch.channels_last):
@@ -449,7 +449,7 @@ def pool2d_bwd(dy, ctx):
     N, C, H, W = xshape
     dy = dy.to(xdt).contiguous(memory_format=torch.channels_last)
     dx = torch.empty(xshape, dtype=xdt, device=dy.device, memory_format=torch.channels_last)
-    rc = load().dl4j_pool_bwd(1 if xdt == torch.bfloat16 else 0, mode, _ptr(dy), _ptr(am), _ptr(dx), N, H, W, C, OH,
+    rc = load().dl4j_pool_bwd({torch.bfloat16: 1, torch.float16: 2}.get(xdt, 0), mode, _ptr(dy), _ptr(am), _ptr(dx), N, H, W, C, OH,
                               OW, kh, kw, sh, sw, pt, pl, _stream())
     _check(rc, "pool_bwd")
     return dx

@@ -20,8 +20,11 @@ _SIG_BWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c
             c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
 
 
+_DTC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
 def supported(H, dtype):
-    if dtype == torch.bfloat16:
+    if dtype in (torch.bfloat16, torch.float16):
         ok_k = H % 32 == 0
     elif dtype == torch.float32:
         ok_k = H % 16 == 0
@@ -35,7 +38,7 @@ def supported(H, dtype):
 def _pack_b(m, dt):
     """[N, K] matrix (B[k][n] = m[n][k]) -> the kernels' fragment-packed layout [N/16][K/KC][64 lanes][FE]: lane
     l of k-step s holds m[16*tile + (l & 15)][KC*s + FE*(l >> 4) + j], j < FE, so each wave load is contiguous."""
-    fe = 8 if dt == torch.bfloat16 else 4
+    fe = 8 if dt in (torch.bfloat16, torch.float16) else 4
     N, K = m.shape
     return (m.to(dt).reshape(N // 16, 16, K // (4 * fe), 4, fe).permute(0, 2, 3, 1, 4).contiguous())
 
@@ -199,7 +202,7 @@ def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=Tr
     if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
             _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
         return out, hT, cT, gates, call
-    rc = lib.dl4j_lstm_fwd(1 if dt == torch.bfloat16 else 0, _ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c),
+    rc = lib.dl4j_lstm_fwd(_DTC.get(dt, 0), _ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c),
                            _ptr(m), _ptr(out), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), T, mb, H,
                            c_void_p(_stream()))
     if rc == -1:
@@ -228,7 +231,7 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
             _bwd_coop(lib, e, gates, call, _f32c(c0), rw, peep, m, _f32c(dh_last), _f32c(dc_last), dz, dh0, dc0, T, mb,
                       H, t_end):
         return dz, dh0, dc0
-    rc = lib.dl4j_lstm_bwd(1 if dt == torch.bfloat16 else 0, _ptr(e), _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
+    rc = lib.dl4j_lstm_bwd(_DTC.get(dt, 0), _ptr(e), _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
                            _ptr(rw), _ptr(peep), _ptr(m), _ptr(_f32c(dh_last)), _ptr(_f32c(dc_last)), _ptr(dz),
                            _ptr(dh0), _ptr(dc0), T, mb, H, int(t_end), c_void_p(_stream()))
     if rc == -1:

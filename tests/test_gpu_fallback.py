@@ -69,3 +69,74 @@ def test_lenet_fp32_gpu_no_fallbacks_and_matches_cpu():
         nets[dev] = net
     pc, pg = nets["cpu"].params().cpu(), nets["cuda"].params().cpu()
     assert torch.allclose(pc, pg, rtol=1e-3, atol=1e-4), (pc - pg).abs().max()
+
+
+def test_resnet50_fp16_step_has_no_fallbacks():
+    """fp16 conv / BN / pool on the round-3 engines (v3 tile engine, halo weight gradient, fp16 BN / pool kernels;
+    the 3-channel stem is zero-padded to 64 channels): no library path, finite loss."""
+    from deeplearning4j_amd.models import ResNet50
+    from deeplearning4j_amd.nn.conf import DataType
+    net = ResNet50(numLabels=10, dataType=DataType.HALF).init(device=DEV)
+    x = torch.rand(4, 3, 224, 224, device=DEV).contiguous(memory_format=torch.channels_last).half()
+    y = torch.zeros(4, 10, device=DEV)
+    y[:, 3] = 1
+    fallback.reset()
+    p0 = net.params().clone()
+    net.fit([x], [y])
+    _assert_clean(net, "ResNet-50 fp16")
+    assert torch.isfinite(torch.tensor(net.score()))
+    assert not torch.equal(p0, net.params())
+
+
+def test_textgen_lstm_fp16_step_has_no_fallbacks():
+    from deeplearning4j_amd.models import TextGenerationLSTM
+    from deeplearning4j_amd.nn.conf import DataType
+    net = TextGenerationLSTM(numLabels=77, inputShape=[1, 77], dataType=DataType.HALF).init(device=DEV)
+    idx = torch.randint(0, 77, (8, 100))
+    x = torch.nn.functional.one_hot(idx, 77).permute(0, 2, 1).float().to(DEV)
+    y = torch.nn.functional.one_hot(torch.roll(idx, -1, 1), 77).permute(0, 2, 1).float().to(DEV)
+    fallback.reset()
+    net.fit(x, y)
+    _assert_clean(net, "TextGenerationLSTM fp16")
+    assert torch.isfinite(torch.tensor(net.score()))
+
+
+def test_small_cnn_fp16_matches_fp32_cpu():
+    """fp16 GPU forward / gradients of a conv -> BN -> ReLU -> max-pool -> 1x1 conv -> BN -> global pool net against
+    the same network in fp32 on the CPU (parameters copied)."""
+    from deeplearning4j_amd import (Activation, LossFunction, MultiLayerNetwork, NeuralNetConfiguration, OutputLayer,
+                                    Sgd)
+    from deeplearning4j_amd.nn.conf import DataType
+    from deeplearning4j_amd.nn.conf.inputs import InputType
+    from deeplearning4j_amd.nn.conf.layers import (BatchNormalization, ConvolutionLayer, GlobalPoolingLayer,
+                                                   SubsamplingLayer)
+
+    def build(dt, dev):
+        conf = (NeuralNetConfiguration.Builder().seed(11).dataType(dt).updater(Sgd(0.0)).list()
+                .layer(0, ConvolutionLayer.Builder([3, 3]).nOut(64).padding(1, 1).activation(Activation.IDENTITY).build())
+                .layer(1, BatchNormalization.Builder().activation(Activation.RELU).build())
+                .layer(2, SubsamplingLayer.Builder([2, 2], [2, 2]).build())
+                .layer(3, ConvolutionLayer.Builder([1, 1]).nOut(64).activation(Activation.IDENTITY).build())
+                .layer(4, BatchNormalization.Builder().activation(Activation.RELU).build())
+                .layer(5, GlobalPoolingLayer.Builder("AVG").build())
+                .layer(6, OutputLayer.Builder(LossFunction.MCXENT).nOut(5).activation(Activation.SOFTMAX).build())
+                .setInputType(InputType.convolutional(16, 16, 64)).build())
+        n = MultiLayerNetwork(conf)
+        n.init(device=dev)
+        return n
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(8, 64, 16, 16, generator=g)
+    y = torch.nn.functional.one_hot(torch.randint(0, 5, (8,), generator=g), 5).float()
+    ref = build(DataType.FLOAT, "cpu")
+    net = build(DataType.HALF, DEV)
+    net.setParams(ref.params().to(DEV))
+    fallback.reset()
+    oh = net.output(x.to(DEV).half()).float().cpu()
+    of = ref.output(x)
+    assert (oh - of).abs().max() <= 2e-2, (oh - of).abs().max()
+    net.computeGradientAndScore(x.to(DEV).half(), y.to(DEV))
+    ref.computeGradientAndScore(x, y)
+    gh, gf = net.gradient().gradient().float().cpu(), ref.gradient().gradient()
+    rel = (gh - gf).norm() / gf.norm()
+    assert rel <= 3e-2, rel
+    _assert_clean(net, "small CNN fp16")
