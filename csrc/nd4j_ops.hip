@@ -456,6 +456,41 @@ __global__ __launch_bounds__(256) void strided_copy(const T* __restrict__ x, T* 
   }
 }
 
+// ------------------------------------------------------------------------------------------------ col2im
+// x[n][c][h][w] = sum over the (r, s) taps whose window position lands on (h, w) of cols[n][(c*R + r)*S + s][oh*OW + ow]
+// (the adjoint of im2col / F.unfold layout); x is the PADDED image [N][C][Hp][Wp], gather form: no atomics.
+template <typename T>
+__global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ cols, T* __restrict__ x, int N, int C,
+                                                     int Hp, int Wp, int R, int S, int sh, int sw, int dh, int dw,
+                                                     int OH, int OW) {
+  const long long total = (long long)N * C * Hp * Wp;
+  const long long L = (long long)OH * OW;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int w = (int)(i % Wp);
+    long long t = i / Wp;
+    const int h = (int)(t % Hp);
+    t /= Hp;
+    const int c = (int)(t % C);
+    const long long n = t / C;
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const int ohn = h - r * dh;
+      if (ohn < 0 || ohn % sh) continue;
+      const int oh = ohn / sh;
+      if (oh >= OH) continue;
+      for (int q = 0; q < S; ++q) {
+        const int own = w - q * dw;
+        if (own < 0 || own % sw) continue;
+        const int ow = own / sw;
+        if (ow >= OW) continue;
+        acc += ldf(cols, (n * C * R * S + ((long long)c * R + r) * S + q) * L + (long long)oh * OW + ow);
+      }
+    }
+    stf(x, i, acc);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ mergemax
 struct PtrList {
   const void* p[8];
@@ -638,6 +673,18 @@ DL4J_API int dl4j_mergemax_bp(int dt, const void* eps, const unsigned char* am, 
   pl.n = nout;
   const int g = grid1(n);
 #define L(T) hipLaunchKernelGGL((mergemax_bp_kernel<T>), dim3(g), dim3(256), 0, s, (const T*)eps, am, pl, n)
+  DT_DISPATCH(dt, L);
+#undef L
+  return (int)hipGetLastError();
+}
+
+// cols [N][C*R*S][OH*OW] (F.unfold layout) -> padded image [N][C][Hp][Wp], summing overlapping windows.
+DL4J_API int dl4j_col2im(int dt, const void* cols, void* x, int N, int C, int Hp, int Wp, int R, int S, int sh, int sw,
+                         int dh, int dw, int OH, int OW, hipStream_t s) {
+  if (sh < 1 || sw < 1 || dh < 1 || dw < 1) return -1;
+  const int g = grid1((long long)N * C * Hp * Wp);
+#define L(T) hipLaunchKernelGGL((col2im_kernel<T>), dim3(g), dim3(256), 0, s, (const T*)cols, (T*)x, N, C, Hp, Wp, R, S, \
+                                sh, sw, dh, dw, OH, OW)
   DT_DISPATCH(dt, L);
 #undef L
   return (int)hipGetLastError();

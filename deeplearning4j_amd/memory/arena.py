@@ -8,6 +8,9 @@ outputs allocated through :func:`empty` — GEMM outputs (ops/gemm.py) and the c
 iteration, so after the first (learning) cycle every activation gets the same address each step. Arrays carved
 in an iteration are invalid after it: ``memory.workspace.check_scope`` raises (SCOPE_PANIC) on such a leaked
 array, and anything handed back to the user is allocated outside the scope.
+Recurrent networks: ``tbptt_scope`` gives every truncated-BPTT window its own LOOP_TBPTT arena (nested in the
+iteration's), and the LSTM sequence kernels' per-call buffers (outputs, gate / cell caches: the reference's LOOP_LSTM
+working memory) are carved from whichever arena is open; state carried past a scope is leveraged out of it.
 """
 import threading
 
@@ -36,7 +39,9 @@ def empty(shape, dtype, device, channels_last=False):
 
 
 def _eligible(net):
-    """Networks whose iteration carries no activation into the next one (no recurrent state / TBPTT)."""
+    """Training-workspace mode ENABLED and no layer whose pretraining / sampling keeps activations across calls
+    (AutoEncoder / VAE). Recurrent networks are eligible: the state they carry (TBPTT windows, rnnTimeStep) is
+    leveraged out of the arena when a scope closes (:func:`leverage_states`)."""
     from ..nn.conf.enums import WorkspaceMode
     g = getattr(net.conf, "globalConf", None) or {}
     mode = g.get("trainingWorkspaceMode", WorkspaceMode.ENABLED) if isinstance(g, dict) else WorkspaceMode.ENABLED
@@ -44,10 +49,94 @@ def _eligible(net):
         return False
     for _, _, impl, _ in getattr(net, "_layer_offsets", []):
         name = type(impl.conf).__name__
-        if any(k in name for k in ("LSTM", "Rnn", "Recurrent", "Bidirectional", "LastTimeStep", "AutoEncoder",
-                                   "Variational")):
+        if any(k in name for k in ("AutoEncoder", "Variational")):
             return False
     return True
+
+
+def _owned(ws, t):
+    """True when ``t``'s memory lies inside ``ws``'s arena buffer (views of carved arrays included)."""
+    b = getattr(ws, "_buf", None)
+    if b is None or not torch.is_tensor(t) or t.device != b.device or t.numel() == 0:
+        return False
+    p, s = t.data_ptr(), b.data_ptr()
+    return s <= p < s + b.numel()
+
+
+def _layer_impls(net):
+    todo = [impl for _, _, impl, _ in getattr(net, "_layer_offsets", [])]
+    while todo:
+        impl = todo.pop()
+        yield impl
+        for attr in ("fwd", "bwd", "inner", "underlying"):
+            sub = getattr(impl, attr, None)
+            if sub is not None and hasattr(sub, "conf"):
+                todo.append(sub)
+
+
+def leverage_states(net, ws):
+    """Recurrent state carried beyond a workspace cycle (``stateMap`` / ``tBpttStateMap``) that was carved from
+    ``ws`` is copied out of it before the cycle ends (reference: the TBPTT state is leveraged to the outer workspace,
+    MultiLayerNetwork.java:1556-1583). Returns the number of arrays moved."""
+    moved = 0
+    for impl in _layer_impls(net):
+        for attr in ("stateMap", "tBpttStateMap"):
+            m = getattr(impl, attr, None)
+            if not m:
+                continue
+            for k, v in list(m.items()):
+                if _owned(ws, v):
+                    m[k] = v.detach().clone()
+                    moved += 1
+    return moved
+
+
+def _loop_ws(net, attr, ws_id):
+    ws = getattr(net, attr, None)
+    if ws is None:
+        from .workspace import (AllocationPolicy, LearningPolicy, ResetPolicy, SpillPolicy, WorkspaceConfiguration,
+                                getWorkspaceManager)
+        conf = WorkspaceConfiguration(initialSize=0, overallocationLimit=0.2,
+                                      policyAllocation=AllocationPolicy.OVERALLOCATE,
+                                      policyLearning=LearningPolicy.FIRST_LOOP, policyReset=ResetPolicy.BLOCK_LEFT,
+                                      policySpill=SpillPolicy.REALLOCATE)
+        ws = getWorkspaceManager().getWorkspaceForCurrentThread(conf, f"{ws_id}_{id(net)}", device=net.device)
+        setattr(net, attr, ws)
+    return ws
+
+
+class tbptt_scope:
+    """One truncated-BPTT window in its own LOOP_TBPTT arena (reference MultiLayerNetwork.doTruncatedBPTT opens the
+    LOOP_TBPTT workspace per sub-sequence, :1556-1583): the window's activations, LSTM gate caches and gradients-in-
+    flight are carved from it and released at window end; the carried h / c state is leveraged out first."""
+
+    def __init__(self, net):
+        self.net = net
+        self.ws = None
+        self.prev = None
+
+    def __enter__(self):
+        net = self.net
+        ok = getattr(net, "_ws_ok", None)
+        if ok is None:
+            ok = net._ws_ok = _eligible(net)
+        if not ok:
+            return self
+        from .workspace import LOOP_TBPTT
+        ws = _loop_ws(net, "_tbptt_ws", LOOP_TBPTT)
+        if ws.active:
+            return self
+        self.prev = current()
+        ws.notifyScopeEntered()
+        _tl.ws = self.ws = ws
+        return self
+
+    def __exit__(self, *a):
+        if self.ws is not None:
+            leverage_states(self.net, self.ws)
+            _tl.ws = self.prev
+            self.ws.notifyScopeLeft()
+        return False
 
 
 class training_scope:
@@ -64,22 +153,14 @@ class training_scope:
             ok = net._ws_ok = _eligible(net)
         if not ok or current() is not None:
             return self
-        from .workspace import (AllocationPolicy, LearningPolicy, ResetPolicy, SpillPolicy, WorkspaceConfiguration,
-                                getWorkspaceManager)
-        ws = getattr(net, "_loop_ws", None)
-        if ws is None:
-            conf = WorkspaceConfiguration(initialSize=0, overallocationLimit=0.2,
-                                          policyAllocation=AllocationPolicy.OVERALLOCATE,
-                                          policyLearning=LearningPolicy.FIRST_LOOP, policyReset=ResetPolicy.BLOCK_LEFT,
-                                          policySpill=SpillPolicy.REALLOCATE)
-            ws = net._loop_ws = getWorkspaceManager().getWorkspaceForCurrentThread(
-                conf, f"LOOP_FF_BP_{id(net)}", device=net.device)
+        ws = _loop_ws(net, "_loop_ws", "LOOP_FF_BP")
         ws.notifyScopeEntered()
         _tl.ws = self.ws = ws
         return self
 
     def __exit__(self, *a):
         if self.ws is not None:
+            leverage_states(self.net, self.ws)
             _tl.ws = None
             self.ws.notifyScopeLeft()
         return False

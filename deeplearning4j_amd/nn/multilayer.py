@@ -229,9 +229,11 @@ class MultiLayerNetwork(BaseNetwork):
             lm = lmask[:, t0:t1] if lmask is not None else None
             if self._try_graph_step([xs], [ys], fm, lm, tbptt_back=back):
                 continue                           # this window replayed as a HIP graph (nn/hipgraph.py)
-            self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
-                                         tbptt_back=back, defer_reg=True)
-            self._apply_update(x.shape[0])
+            from ..memory.arena import tbptt_scope
+            with tbptt_scope(self):                  # LOOP_TBPTT arena for this window
+                self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
+                                             tbptt_back=back, defer_reg=True)
+                self._apply_update(x.shape[0])
             self._iteration_done()
         self.rnnClearPreviousState()
 

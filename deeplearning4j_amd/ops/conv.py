@@ -5,8 +5,10 @@ CudnnConvolutionHelper contract, CUDA:convolution/CudnnConvolutionHelper.java:29
 ``conv2d_backward(...)`` -> (dx, dw, db).  pad4 = (top, bottom, left, right) so Same mode's
 asymmetric padding is exact.
 
-GPU: bf16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_igemm.hip``) when the shape is supported; fp32 convs as
-im2col + the in-tree exact-fp32 MFMA GEMM; anything else takes the library path and is counted (ops/fallback.py).
+GPU: bf16 / fp16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_gemm.hip``, ``conv_igemm.hip``, ``conv_wrw.hip``)
+when the shape is supported; fp32 convs as im2col / col2im on the in-tree strided-copy and gather kernels
+(``csrc/nd4j_ops.hip``) + the in-tree exact-fp32 MFMA GEMM; anything else takes the library path and is counted
+(ops/fallback.py).
 CPU: torch reference (fp32/fp64).
 """
 import torch
@@ -25,40 +27,50 @@ def _fp32_gemm_ok(x, groups):
 
 
 def _fp32_conv_fwd(x, w, b, stride, pad4, dilation):
-    """fp32 conv on the GPU without the library: im2col + the in-tree exact-fp32 MFMA GEMM (ops/gemm.py)."""
+    """fp32 conv on the GPU without the library: im2col (zero-pad + strided-copy kernels, ops/nd4j_kernels.py) + the
+    in-tree exact-fp32 MFMA GEMM (ops/gemm.py) + the broadcast-add kernel for the bias."""
+    from . import nd4j_kernels as K
     from .gemm import mmul
+    Kc, _, R, S = w.shape
+    cols = K.im2col(x, R, S, stride, pad4, dilation)
+    if cols is None:
+        return None
+    N = x.shape[0]
     pt, pb, pl, pr = pad4
-    xp = F.pad(x, (pl, pr, pt, pb)) if any(pad4) else x
-    N, C, Hp, Wp = xp.shape
-    K, _, R, S = w.shape
-    OH = (Hp - dilation[0] * (R - 1) - 1) // stride[0] + 1
-    OW = (Wp - dilation[1] * (S - 1) - 1) // stride[1] + 1
-    cols = F.unfold(xp.contiguous(), (R, S), dilation=tuple(dilation), stride=tuple(stride))     # [N, CRS, L]
-    y = mmul(w.reshape(K, -1).to(torch.float32), cols)                                          # [N, K, L]
-    y = y.reshape(N, K, OH, OW)
+    OH = (x.shape[2] + pt + pb - dilation[0] * (R - 1) - 1) // stride[0] + 1
+    OW = (x.shape[3] + pl + pr - dilation[1] * (S - 1) - 1) // stride[1] + 1
+    y = mmul(w.reshape(Kc, -1).to(torch.float32), cols)                                          # [N, K, L]
+    y = y.reshape(N, Kc, OH, OW)
     if b is not None:
-        y = y + b.reshape(1, -1, 1, 1).to(y.dtype)
+        yb = K.binary(y, b.reshape(1, -1, 1, 1).to(y.dtype).contiguous(), "add")
+        y = yb if yb is not None else y + b.reshape(1, -1, 1, 1).to(y.dtype)
     return y
 
 
 def _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+    from . import nd4j_kernels as K
     from .gemm import mmul
     pt, pb, pl, pr = pad4
-    xp = F.pad(x, (pl, pr, pt, pb)) if any(pad4) else x
-    N, C, Hp, Wp = xp.shape
-    K, _, R, S = w.shape
-    L = dy.shape[2] * dy.shape[3]
-    dy3 = dy.reshape(N, K, L).to(torch.float32).contiguous()
+    N, C, H, W = x.shape
+    Hp, Wp = H + pt + pb, W + pl + pr
+    Kc, _, R, S = w.shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    L = OH * OW
+    dy3 = dy.reshape(N, Kc, L).to(torch.float32).contiguous()
     dx = dw = db = None
     if need_dx:
-        dcols = mmul(w.reshape(K, -1).t().to(torch.float32), dy3)                                # [N, CRS, L]
-        dxp = F.fold(dcols, (Hp, Wp), (R, S), dilation=tuple(dilation), stride=tuple(stride))
-        dx = dxp[:, :, pt:pt + x.shape[2], pl:pl + x.shape[3]] if any(pad4) else dxp
+        dcols = mmul(w.reshape(Kc, -1).t().to(torch.float32), dy3)                              # [N, CRS, L]
+        dxp = K.col2im(dcols, N, C, Hp, Wp, R, S, stride, dilation, OH, OW)
+        if dxp is None:
+            return None
+        dx = K.materialize(dxp[:, :, pt:pt + H, pl:pl + W]) if any(pad4) else dxp
     if need_dw:
-        cols = F.unfold(xp.contiguous(), (R, S), dilation=tuple(dilation), stride=tuple(stride))
-        dw = mmul(dy3.permute(1, 0, 2).reshape(K, N * L), cols.permute(0, 2, 1).reshape(N * L, -1)).reshape(w.shape)
+        cols = K.im2col(x, R, S, stride, pad4, dilation)
+        if cols is None:
+            return None
+        dw = mmul(dy3.permute(1, 0, 2).reshape(Kc, N * L), cols.permute(0, 2, 1).reshape(N * L, -1)).reshape(w.shape)
     if need_db:
-        db = dy3.sum((0, 2))
+        db = K.reduce(dy3, "sum", [0, 2])
     return dx, dw, db
 
 
@@ -69,7 +81,9 @@ def conv2d_forward(x, w, b, stride, pad4, dilation=(1, 1), groups=1, want_stats=
         if y is not None:
             return y
     if _fp32_gemm_ok(x, groups):
-        return _fp32_conv_fwd(x, w, b, stride, pad4, dilation)
+        y = _fp32_conv_fwd(x, w, b, stride, pad4, dilation)
+        if y is not None:
+            return y
     from .fallback import note
     note(x, "conv", f"fwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4
@@ -92,7 +106,9 @@ def conv2d_backward(x, w, dy, stride, pad4, dilation=(1, 1), need_dx=True, need_
         if r is not None:
             return r
     if _fp32_gemm_ok(x, groups):
-        return _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
+        r = _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db)
+        if r is not None:
+            return r
     from .fallback import note
     note(x, "conv", f"bwd {x.dtype} groups={groups}")
     pt, pb, pl, pr = pad4

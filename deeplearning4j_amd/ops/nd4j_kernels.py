@@ -26,6 +26,7 @@ native.register_sig("dl4j_reduce", [c_int, c_int, c_void_p, c_void_p, c_void_p, 
                                     c_void_p])
 native.register_sig("dl4j_strided_copy", [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_ll, c_void_p])
+native.register_sig("dl4j_col2im", [c_int, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
 native.register_sig("dl4j_mergemax", [c_int, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_void_p])
 native.register_sig("dl4j_mergemax_bp", [c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p])
 
@@ -354,3 +355,33 @@ def mergemax_bp(eps, am, n):
     _check(native.load().dl4j_mergemax_bp(DT[eps.dtype], _ptr(eps), _ptr(am), ptrs, n, eps.numel(), _stream()),
            "mergemax_bp")
     return outs
+
+
+def im2col(x, R, S, stride, pad4, dilation):
+    """[N, C*R*S, OH*OW] columns (F.unfold layout) of an NCHW image: zero-pad kernel + one strided copy."""
+    if not ok(x) or x.dim() != 4:
+        return None
+    pt, pb, pl, pr = pad4
+    xp = pad2d(x, (pt, pb, pl, pr)) if any(pad4) else x
+    if xp is None:
+        return None
+    N, C, Hp, Wp = xp.shape
+    sh, sw = stride
+    dh, dw = dilation
+    OH = (Hp - dh * (R - 1) - 1) // sh + 1
+    OW = (Wp - dw * (S - 1) - 1) // sw + 1
+    sN, sC, sH, sW = xp.stride()
+    v = xp.as_strided((N, C, R, S, OH, OW), (sN, sC, sH * dh, sW * dw, sH * sh, sW * sw), xp.storage_offset())
+    cols = materialize(v)
+    return None if cols is None else cols.reshape(N, C * R * S, OH * OW)
+
+
+def col2im(cols, N, C, Hp, Wp, R, S, stride, dilation, OH, OW):
+    """Adjoint of ``im2col`` onto the padded image [N, C, Hp, Wp] (overlapping windows summed, gather form)."""
+    if not ok(cols):
+        return None
+    cols = cols.contiguous()
+    x = torch.empty((N, C, Hp, Wp), dtype=cols.dtype, device=cols.device)
+    _check(native.load().dl4j_col2im(DT[cols.dtype], _ptr(cols), _ptr(x), N, C, Hp, Wp, R, S, stride[0], stride[1],
+                                     dilation[0], dilation[1], OH, OW, _stream()), "col2im")
+    return x

@@ -12,6 +12,7 @@ import threading
 import torch
 
 from . import native
+from ..memory import arena
 from .native import _check, _ptr, _stream, c_int, c_void_p
 
 _SIG_FWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -194,11 +195,13 @@ def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=Tr
     m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
     if m is not None and m.shape[1] != T:
         return None
-    out = torch.empty(T, mb, H, device=dev, dtype=torch.float32)
+    # per-call working memory (outputs, gate / cell caches for backward) from the open training / TBPTT arena
+    # (memory/arena.py: the reference's LOOP_LSTM working memory); the carried state hT / cT is not carved
+    out = arena.empty((T, mb, H), torch.float32, dev)
     hT = torch.empty(mb, H, device=dev, dtype=torch.float32)
     cT = torch.empty(mb, H, device=dev, dtype=torch.float32)
-    gates = torch.empty(T, mb, 4 * H, device=dev, dtype=torch.float32) if need_cache else None
-    call = torch.empty(T, mb, H, device=dev, dtype=torch.float32) if need_cache else None
+    gates = arena.empty((T, mb, 4 * H), torch.float32, dev) if need_cache else None
+    call = arena.empty((T, mb, H), torch.float32, dev) if need_cache else None
     if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
             _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
         return out, hT, cT, gates, call
@@ -224,7 +227,9 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
     rw = _pack_b(RW[:, :4 * H], dt)                                   # dh = dz·RWᵀ: B[k][n] = RW[n][k], k over 4H
     peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
     m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
-    dz = (torch.zeros if t_end > 0 else torch.empty)(T, mb, 4 * H, device=dev, dtype=torch.float32)
+    dz = arena.empty((T, mb, 4 * H), torch.float32, dev)
+    if t_end > 0:
+        dz.zero_()
     dh0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
     dc0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
     if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \

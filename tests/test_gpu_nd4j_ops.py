@@ -198,3 +198,32 @@ def test_shape_layers_and_max_vertex_on_gpu(cuda):
         grads = v.backward(torch.ones(3, 5, device=cuda), ctx)
         assert torch.equal(sum(gr.cpu() for gr in grads), torch.ones(3, 5))
     assert K.CALLS["strided_copy"] >= 4
+
+
+@pytest.mark.parametrize("case", [((2, 3, 9, 11), (4, 3, 3, 3), (1, 1), (1, 1, 1, 1), (1, 1)),
+                                  ((2, 5, 12, 10), (6, 5, 5, 3), (2, 1), (2, 1, 0, 2), (1, 2)),
+                                  ((1, 4, 8, 8), (3, 4, 1, 1), (2, 2), (0, 0, 0, 0), (1, 1))])
+def test_fp32_conv_im2col_col2im_kernels(cuda, case):
+    """fp32 conv forward / backward on the in-tree im2col (pad + strided copy) and gather col2im kernels + the fp32
+    MFMA GEMM, against torch's fp32 conv, with the kernels' launch counters advancing (no ATen unfold / fold)."""
+    from deeplearning4j_amd.ops import conv as C
+    xs, ws, st, pad4, dil = case
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(xs, generator=g).to(cuda)
+    w = torch.randn(ws, generator=g).to(cuda) * 0.2
+    b = torch.randn(ws[0], generator=g).to(cuda)
+    K.CALLS.clear()
+    y = C._fp32_conv_fwd(x, w, b, st, pad4, dil)
+    xr = torch.nn.functional.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1])).requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, br, st, 0, dil)
+    assert torch.allclose(y, yr, atol=1e-4, rtol=1e-4)
+    dy = torch.randn(yr.shape, generator=g).to(cuda)
+    yr.backward(dy)
+    dx, dw, db = C._fp32_conv_bwd(x, w, dy, st, pad4, dil, True, True, True)
+    H, W = xs[2], xs[3]
+    assert torch.allclose(dx, xr.grad[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W], atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dw, wr.grad, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(db, br.grad, atol=1e-4, rtol=1e-4)
+    assert K.CALLS["strided_copy"] >= 2 and K.CALLS["col2im"] == 1
