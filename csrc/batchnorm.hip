@@ -178,9 +178,12 @@ __global__ __launch_bounds__(256) void bn_finalize(const float* __restrict__ par
   ctx[3 * C + c] = bb - mean * g * inv;     // shift
 }
 
+// mask (optional, RES only): one byte per 8-channel vector, bit i = ReLU active for channel 8*(v % (C/8)) + i, so
+// the backward pass reads 1/16 of the residual's bytes instead of re-reading the residual.
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
-                                                long long M, int C, const float* __restrict__ ctx) {
+                                                long long M, int C, const float* __restrict__ ctx,
+                                                unsigned char* __restrict__ mask) {
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
   const float* scale = ctx + 2 * C;
@@ -204,26 +207,32 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        unsigned bits = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float t = a[u][i] * sc[i] + sf[i];
           if (RES) t += r[u][i];
+          bits |= (t > 0.f ? 1u : 0u) << i;
           a[u][i] = RELU ? fmaxf(t, 0.f) : t;
         }
         Vec8<T>::store(y + (v + u * stride) * 8, a[u]);
+        if (RES && mask) mask[v + u * stride] = (unsigned char)bits;
       }
     }
     if (v < nvec) {
       float a[8], r[8];
       Vec8<T>::load(x + v * 8, a);
       if (RES) Vec8<T>::load(res + v * 8, r);
+      unsigned bits = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float t = a[i] * sc[i] + sf[i];
         if (RES) t += r[i];
+        bits |= (t > 0.f ? 1u : 0u) << i;
         a[i] = RELU ? fmaxf(t, 0.f) : t;
       }
       Vec8<T>::store(y + v * 8, a);
+      if (RES && mask) mask[v] = (unsigned char)bits;
     }
     return;
   }
@@ -232,13 +241,16 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
     float a[8], r[8];
     Vec8<T>::load(x + v * 8, a);
     if (RES) Vec8<T>::load(res + v * 8, r);
+    unsigned bits = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float t = a[i] * scale[c0 + i] + shift[c0 + i];
       if (RES) t += r[i];
+      bits |= (t > 0.f ? 1u : 0u) << i;
       a[i] = RELU ? fmaxf(t, 0.f) : t;
     }
     Vec8<T>::store(y + v * 8, a);
+    if (RES && mask) mask[v] = (unsigned char)bits;
   }
 }
 
@@ -247,7 +259,8 @@ template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, const T* __restrict__ res,
                                                       const T* __restrict__ dy, long long M, int C,
                                                       long long rows_per_blk, const float* __restrict__ ctx,
-                                                      float* __restrict__ part_db, float* __restrict__ part_dg) {
+                                                      float* __restrict__ part_db, float* __restrict__ part_dg,
+                                                      const unsigned char* __restrict__ mask) {
   const int T8 = C >> 3;
   const int R = 256 / T8;
   const int cg = threadIdx.x % T8, r0 = threadIdx.x / T8;
@@ -266,15 +279,20 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
     long long r = rbeg + r0;
     for (; r < rend; r += U * R) {
       float xv[U][8], gv[U][8], rv[U][8];
+      unsigned mb[U];
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long ru = r + u * R;
         ok[u] = ru < rend;
-        const long long o = (ok[u] ? ru : r) * C + cg * 8;
+        const long long rr = ok[u] ? ru : r;
+        const long long o = rr * C + cg * 8;
         Vec8<T>::load(x + o, xv[u]);
         Vec8<T>::load(dy + o, gv[u]);
-        if (RES) Vec8<T>::load(res + o, rv[u]);
+        if (RES) {
+          if (mask) mb[u] = mask[rr * T8 + cg];
+          else Vec8<T>::load(res + o, rv[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -282,7 +300,9 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float d = gv[u][i];
-          if (RELU) {
+          if (RES && mask) {
+            d = (mb[u] >> i) & 1u ? d : 0.f;
+          } else if (RELU) {
             float t = xv[u][i] * sc[i] + sf[i];
             if (RES) t += rv[u][i];
             d = t > 0.f ? d : 0.f;
@@ -324,12 +344,180 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__
   cdg[c] = (float)(b / (double)M);
 }
 
+// ------------------------------------------------------------------------ fused partial fold + finalize
+// One launch replaces bn_reduce_rows + bn_finalize / bn_bwd_finalize: grid (ceil(C/64), S), each block folds 32
+// partial rows of 64 channels (4 row groups x 8 independent loads, same order as bn_reduce_rows) into q; with S > 1
+// the last block of each channel column (agent-scope ticket, release/acquire recipe of the CDNA guide: plain stores,
+// vmcnt drain, lane-0 release fence, relaxed fetch_add; reducer lane-0 acquire fence) sums the S folded rows in
+// double and finalizes. The ticket counters live in a zero-initialised device array, each launch draws a slot
+// round-robin on the host and the reducer resets its counter, so no per-call memset is needed.
+// SRC 0: p1/p2 are [nrows, C] partial sums about row 0 (bn_stats_partial / bn_bwd_partial).
+// SRC 1: p1 is the conv epilogue's [3][P][C] tile-statistics planes (bn_tiles_reduce's re-centring).
+struct BnFin {
+  long long M;
+  const void* x;                           // fwd: row 0 = the statistics shift
+  const float* gamma; const float* beta;
+  float gconst, bconst;
+  float* run_mean; float* run_var;
+  float decay, eps;
+  float* ctx;                              // fwd out: mean, invstd, scale, shift
+  float* dbeta; float* dgamma;             // bwd outs (optional)
+  float* cdb; float* cdg;                  // bwd out: mean(d), mean(d*xhat)
+  unsigned* ticket;                        // ceil(C/64) counters (S > 1 only)
+  int rpp;                                 // SRC 1: rows per tile partial
+};
+
+template <typename T, int FIN>
+__device__ __forceinline__ void bn_fin_store(int c, int C, double a, double b, const BnFin& f) {
+  if (FIN == 0) {
+    const double m1 = a / (double)f.M;
+    const float mean = (float)((double)ld1<T>((const T*)f.x + c) + m1);
+    double v = b / (double)f.M - m1 * m1;
+    if (v < 0) v = 0;
+    const float var = (float)v + f.eps;
+    f.run_mean[c] = f.decay * f.run_mean[c] + (1.f - f.decay) * mean;
+    f.run_var[c] = f.decay * f.run_var[c] + (1.f - f.decay) * var;
+    const float inv = rsqrtf(var);
+    const float g = f.gamma ? f.gamma[c] : f.gconst;
+    const float bb = f.beta ? f.beta[c] : f.bconst;
+    f.ctx[c] = mean;
+    f.ctx[C + c] = inv;
+    f.ctx[2 * C + c] = g * inv;
+    f.ctx[3 * C + c] = bb - mean * g * inv;
+  } else {
+    if (f.dbeta) f.dbeta[c] = (float)a;
+    if (f.dgamma) f.dgamma[c] = (float)b;
+    f.cdb[c] = (float)(a / (double)f.M);
+    f.cdg[c] = (float)(b / (double)f.M);
+  }
+}
+
+template <typename T, int SRC, int FIN>
+__global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, const float* __restrict__ p2,
+                                               long long nrows, int C, float* __restrict__ q1,
+                                               float* __restrict__ q2, BnFin f) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.y * 32 + grp * 8;
+  float sa = 0.f, sb = 0.f;
+  if (c < C) {
+    if (SRC == 0) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = r0 + u < nrows;
+        a[u] = ok ? p1[(r0 + u) * C + c] : 0.f;
+        b[u] = ok ? p2[(r0 + u) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
+    } else {
+      const float x0 = ld1<T>((const T*)f.x + c);
+      const long long P = nrows;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const long long pp = r0 + u;
+        if (pp >= P) break;
+        const long long nrow = f.M - (long long)f.rpp * pp;
+        const float n = (float)(nrow < f.rpp ? (nrow < 0 ? 0 : nrow) : f.rpp);
+        const float s1 = p1[pp * C + c], s2 = p1[(P + pp) * C + c], d = p1[(2 * P + pp) * C + c] - x0;
+        sa += s1 + n * d;
+        sb += s2 + 2.f * d * s1 + n * d * d;
+      }
+    }
+  }
+  __shared__ double rd[2][256];
+  float* rf = reinterpret_cast<float*>(&rd[0][0]);
+  rf[threadIdx.x] = sa;
+  rf[256 + threadIdx.x] = sb;
+  __syncthreads();
+  float ta = 0.f, tb = 0.f;
+  if (grp == 0) {
+    ta = rf[threadIdx.x] + rf[threadIdx.x + 64] + rf[threadIdx.x + 128] + rf[threadIdx.x + 192];
+    tb = rf[256 + threadIdx.x] + rf[256 + threadIdx.x + 64] + rf[256 + threadIdx.x + 128] + rf[256 + threadIdx.x + 192];
+  }
+  if (gridDim.y == 1) {
+    if (grp == 0 && c < C) bn_fin_store<T, FIN>(c, C, (double)ta, (double)tb, f);
+    return;
+  }
+  if (grp == 0 && c < C) {
+    q1[(long long)blockIdx.y * C + c] = ta;
+    q2[(long long)blockIdx.y * C + c] = tb;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                   // every wave's q stores drained; rf reads done
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(&f.ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == gridDim.y - 1;
+    if (last) {
+      __hip_atomic_store(&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    rf[0] = last ? 1.f : 0.f;                        // "I am last" through the existing LDS array
+  }
+  __syncthreads();
+  if (rf[0] == 0.f) return;
+  const int S = gridDim.y;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int i = grp; i < S; i += 4) { a += q1[(long long)i * C + c]; b += q2[(long long)i * C + c]; }
+  __syncthreads();
+  rd[0][threadIdx.x] = a;
+  rd[1][threadIdx.x] = b;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    a = rd[0][threadIdx.x] + rd[0][threadIdx.x + 64] + rd[0][threadIdx.x + 128] + rd[0][threadIdx.x + 192];
+    b = rd[1][threadIdx.x] + rd[1][threadIdx.x + 64] + rd[1][threadIdx.x + 128] + rd[1][threadIdx.x + 192];
+    bn_fin_store<T, FIN>(c, C, a, b, f);
+  }
+}
+
+// Ticket slots for bn_fold: 256 launches in flight x 32 channel columns (C <= 2048), one array per device.
+__device__ unsigned g_bn_ticket[256 * 32];
+
+static unsigned* bn_ticket_slot() {
+  static unsigned* base[64] = {nullptr};
+  static unsigned next = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bn_ticket)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  const unsigned k = __atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % 256u;
+  return base[dev] + 32 * k;
+}
+
+// Launches bn_fold over `nrows` partial rows; q: >= 2*ceil(nrows/32)*C floats of workspace.
+template <typename T, int SRC, int FIN>
+static int bn_fold_launch(const float* p1, const float* p2, long long nrows, int C, float* q, BnFin f,
+                          hipStream_t s) {
+  const long long S = (nrows + 31) / 32;
+  if (S > 65535) return -1;
+  f.ticket = nullptr;
+  if (S > 1) {
+    f.ticket = bn_ticket_slot();
+    if (!f.ticket) return -2;
+  }
+  hipLaunchKernelGGL((bn_fold<T, SRC, FIN>), dim3((C + 63) / 64, (unsigned)S), dim3(256), 0, s, p1, p2, nrows, C, q,
+                     q + S * C, f);
+  return 0;
+}
+
 // one dx/dres element: d = relu'(.)*dy; dx = gamma*invstd*(d - mean(d) - xhat*mean(d*xhat)) written as
 // dx = A*d - B*x - Cq with per-channel A = scale (= gamma*invstd), B = scale*invstd*cdg, Cq = scale*(cdb - mean*invstd*cdg)
 template <bool RELU, bool RES>
-__device__ __forceinline__ void bn_bwd_elem(float& xv, float& gv, float& rv, float A, float B, float Cq, float sf) {
+__device__ __forceinline__ void bn_bwd_elem(float& xv, float& gv, float& rv, float A, float B, float Cq, float sf,
+                                            int mbit) {
   float d = gv;
-  if (RELU) {
+  if (mbit >= 0) {
+    d = mbit ? d : 0.f;
+  } else if (RELU) {
     float t = xv * A + sf;
     if (RES) t += rv;
     d = t > 0.f ? d : 0.f;
@@ -342,7 +530,9 @@ template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                     const T* __restrict__ dy, T* __restrict__ dx, T* __restrict__ dres,
                                                     long long M, int C, const float* __restrict__ ctx,
-                                                    const float* __restrict__ cdb, const float* __restrict__ cdg) {
+                                                    const float* __restrict__ cdb, const float* __restrict__ cdg,
+                                                    const unsigned char* __restrict__ mask) {
+  const bool use_mask = RES && mask != nullptr;
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
   const float *mean = ctx, *invstd = ctx + C, *scale = ctx + 2 * C, *shift = ctx + 3 * C;
@@ -365,16 +555,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
   if (fixed) {
     for (; v + stride < nvec; v += 2 * stride) {   // two independent vectors in flight
       float xv[2][8], gv[2][8], rv[2][8];
+      unsigned mb[2] = {0u, 0u};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         Vec8<T>::load(x + (v + u * stride) * 8, xv[u]);
         Vec8<T>::load(dy + (v + u * stride) * 8, gv[u]);
-        if (RES) Vec8<T>::load(res + (v + u * stride) * 8, rv[u]);
+        if (use_mask) mb[u] = mask[v + u * stride];
+        else if (RES) Vec8<T>::load(res + (v + u * stride) * 8, rv[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) bn_bwd_elem<RELU, RES>(xv[u][i], gv[u][i], rv[u][i], A[i], B[i], Cq[i], sf[i]);
+        for (int i = 0; i < 8; ++i)
+          bn_bwd_elem<RELU, RES>(xv[u][i], gv[u][i], rv[u][i], A[i], B[i], Cq[i], sf[i],
+                                 use_mask ? (int)((mb[u] >> i) & 1u) : -1);
         Vec8<T>::store(dx + (v + u * stride) * 8, xv[u]);
         if (RES) Vec8<T>::store(dres + (v + u * stride) * 8, rv[u]);
       }
@@ -393,11 +587,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
       }
     }
     float xv[8], gv[8], rv[8];
+    unsigned mb = 0u;
     Vec8<T>::load(x + v * 8, xv);
     Vec8<T>::load(dy + v * 8, gv);
-    if (RES) Vec8<T>::load(res + v * 8, rv);
+    if (use_mask) mb = mask[v];
+    else if (RES) Vec8<T>::load(res + v * 8, rv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i]);
+    for (int i = 0; i < 8; ++i)
+      bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i], use_mask ? (int)((mb >> i) & 1u) : -1);
     Vec8<T>::store(dx + v * 8, xv);
     if (RES) Vec8<T>::store(dres + v * 8, rv);
   }
@@ -450,27 +647,37 @@ static inline void bn_reduce_stage(float*& p1, float*& p2, int& nblk, int C, flo
 template <typename T>
 static int bn_fwd_impl(const T* x, const T* res, T* y, long long M, int C, const float* gamma, const float* beta,
                        float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
-                       int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
+                       int training, int relu, float* ws, float* ctx_out, unsigned char* mask, hipStream_t s) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
   float* q = p2 + (long long)nblk * C;
-  if (training) hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(256), 0, s, x, M, C, rpb, p1, p2);
-  if (training) bn_reduce_stage(p1, p2, nblk, C, q, s);
-  hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, x, gamma, beta, gconst,
-                     bconst, run_mean, run_var, decay, eps, training, ctx_out);
-  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C, ctx_out);
+  if (training) {
+    hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(256), 0, s, x, M, C, rpb, p1, p2);
+    BnFin f{M, x, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
+            nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    const int rc = bn_fold_launch<T, 0, 0>(p1, p2, nblk, C, q, f, s);
+    if (rc) return rc;
+  } else {
+    hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, x, gamma, beta,
+                       gconst, bconst, run_mean, run_var, decay, eps, training, ctx_out);
+  }
+  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C, ctx_out,
+               mask);
   return (int)hipGetLastError();
 }
 
+// mask: optional (res != nullptr only) M*C/8-byte ReLU bitmask for dl4j_bn_bwd (bn_apply).
 DL4J_API int dl4j_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C, const float* gamma,
                          const float* beta, float gconst, float bconst, float* run_mean, float* run_var, float decay,
-                         float eps, int training, int relu, float* ws, float* ctx_out, hipStream_t s) {
+                         float eps, int training, int relu, float* ws, float* ctx_out, unsigned char* mask,
+                         hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256) return -1;
   if (res) relu = 1;
+  else mask = nullptr;
 #define BNF(T) return bn_fwd_impl<T>((const T*)x, (const T*)res, (T*)y, M, C, gamma, beta, gconst, bconst, run_mean, \
-                                     run_var, decay, eps, training, relu, ws, ctx_out, s)
+                                     run_var, decay, eps, training, relu, ws, ctx_out, mask, s)
   if (dtype == 1) BNF(bf16);
   if (dtype == 2) BNF(f16);
   BNF(float);
@@ -488,36 +695,45 @@ template <typename T>
 static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C, const float* tstats, long long P,
                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
                              float* run_var, float decay, float eps, int relu, float* ws, float* ctx_out,
-                             hipStream_t s) {
-  int S = (int)((P + 31) / 32);
-  float* p1 = ws;
-  float* p2 = ws + (long long)S * C;
-  float* q = p2 + (long long)S * C;
-  hipLaunchKernelGGL(bn_tiles_reduce<T>, dim3((C + 63) / 64, S), dim3(256), 0, s, tstats, P, C, M, xb, p1, p2, 64);
-  bn_reduce_stage(p1, p2, S, C, q, s);
-  hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, S, C, M, xb, gamma, beta, gconst,
-                     bconst, run_mean, run_var, decay, eps, 1, ctx_out);
-  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C, ctx_out);
+                             unsigned char* mask, hipStream_t s) {
+  const long long S = (P + 31) / 32;
+  BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
+          nullptr, nullptr, nullptr, nullptr, nullptr, 64};
+  int rc;
+  if (S <= 64) {
+    // one launch: tile re-centring + fold + finalize
+    rc = bn_fold_launch<T, 1, 0>(tstats, nullptr, P, C, ws, f, s);
+  } else {
+    float* p1 = ws;
+    float* p2 = ws + S * C;
+    hipLaunchKernelGGL(bn_tiles_reduce<T>, dim3((C + 63) / 64, (unsigned)S), dim3(256), 0, s, tstats, P, C, M, xb, p1,
+                       p2, 64);
+    rc = bn_fold_launch<T, 0, 0>(p1, p2, S, C, p2 + S * C, f, s);
+  }
+  if (rc) return rc;
+  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C, ctx_out,
+               mask);
   return (int)hipGetLastError();
 }
 
 DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* y, long long M, int C,
                                const float* tstats, long long P, const float* gamma, const float* beta, float gconst,
                                float bconst, float* run_mean, float* run_var, float decay, float eps, int relu,
-                               float* ws, float* ctx_out, hipStream_t s) {
+                               float* ws, float* ctx_out, unsigned char* mask, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256 || (dtype != 1 && dtype != 2) || P < 1) return -1;
   if (res) relu = 1;
+  else mask = nullptr;
   if (dtype == 2)
     return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, gamma, beta, gconst,
-                                  bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, s);
+                                  bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, mask, s);
   return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, gamma, beta, gconst,
-                                 bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, s);
+                                 bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, mask, s);
 }
 
 // dres: gradient w.r.t. the fused residual input (required when res != nullptr).
 template <typename T>
 static int bn_bwd_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, long long M, int C, const float* ctx,
-                       float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
+                       float* dgamma, float* dbeta, int relu, float* ws, const unsigned char* mask, hipStream_t s) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
@@ -525,21 +741,24 @@ static int bn_bwd_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, lo
   float* q = p2 + (long long)nblk * C;
   float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
   float* cdg = cdb + C;
-  BN_DISPATCH3(bn_bwd_partial, T, relu, res, dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1, p2);
-  bn_reduce_stage(p1, p2, nblk, C, q, s);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, dbeta, dgamma, cdb,
-                     cdg);
+  BN_DISPATCH3(bn_bwd_partial, T, relu, res, dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1, p2, mask);
+  BnFin f{M, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0.f, 0.f, nullptr, dbeta, dgamma, cdb, cdg,
+          nullptr, 0};
+  const int rc = bn_fold_launch<T, 0, 1>(p1, p2, nblk, C, q, f, s);
+  if (rc) return rc;
   BN_DISPATCH3(bn_bwd_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, dy, dx, dres, M, C, ctx,
-               cdb, cdg);
+               cdb, cdg, mask);
   return (int)hipGetLastError();
 }
 
 DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres, long long M,
-                         int C, const float* ctx, float* dgamma, float* dbeta, int relu, float* ws, hipStream_t s) {
+                         int C, const float* ctx, float* dgamma, float* dbeta, int relu, float* ws,
+                         const unsigned char* mask, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256) return -1;
   if (res) relu = 1;
+  else mask = nullptr;
 #define BNB(T) return bn_bwd_impl<T>((const T*)x, (const T*)res, (const T*)dy, (T*)dx, (T*)dres, M, C, ctx, dgamma, \
-                                     dbeta, relu, ws, s)
+                                     dbeta, relu, ws, mask, s)
   if (dtype == 1) BNB(bf16);
   if (dtype == 2) BNB(f16);
   BNB(float);

@@ -76,6 +76,12 @@ template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p =
 template <> __device__ __forceinline__ void st1<bf16>(bf16* p, float v) { *reinterpret_cast<u16*>(p) = f2bf(v); }
 template <> __device__ __forceinline__ float ld1<f16>(const f16* p) { return (float)*p; }
 template <> __device__ __forceinline__ void st1<f16>(f16* p, float v) { *p = (f16)v; }
+// element i of a buffer whose dtype is only known at run time (0 fp32, 1 bf16, 2 fp16); dt is wave-uniform
+__device__ __forceinline__ float ld_any(const void* p, int dt, long long i) {
+  if (dt == 1) return ld1<bf16>(reinterpret_cast<const bf16*>(p) + i);
+  if (dt == 2) return ld1<f16>(reinterpret_cast<const f16*>(p) + i);
+  return reinterpret_cast<const float*>(p)[i];
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

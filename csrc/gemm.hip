@@ -676,9 +676,17 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   if (in_dt != 1 && in_dt != 2) return -1;
   if ((lda & 7) || (ldb & 7) || (reinterpret_cast<uintptr_t>(A) & 15) || (reinterpret_cast<uintptr_t>(B) & 15)) return -1;
   if (batch > 1 && ((sA & 7) || (sB & 7))) return -1;
-  // K-contiguous operands need K % 8 (a 16-byte chunk must not straddle K); an M/N-contiguous operand only needs its
+  // K-contiguous operands need K % 8 (a 16-byte chunk must not straddle K) unless flagged (bit 1 of akc/bkc) as
+  // zero-padded to the next multiple of 8 inside their leading dimension: the straddling chunk then only brings zeros,
+  // and an M/N-contiguous partner reads its rows >= K from the zero page. An M/N-contiguous operand only needs its
   // leading dimension % 8: the chunk past M (N) stays inside the row stride and only feeds discarded outputs.
-  if ((akc && (K & 7)) || (bkc && (K & 7))) return -1;
+  {
+    const bool akz = (akc & 2) != 0, bkz = (bkc & 2) != 0;
+    akc &= 1;
+    bkc &= 1;
+    if ((akc && (K & 7) && !(akz && lda >= ((K + 7) & ~7))) || (bkc && (K & 7) && !(bkz && ldb >= ((K + 7) & ~7))))
+      return -1;
+  }
   if (K <= 0) return -1;
   if (cfg < 0 || cfg > 4 || splits < 1) plan(M, N, K, batch, &cfg, &splits);
   if (cfg == 3 && !bkc) cfg = 2;                 // the 64-wide tile has no N-contiguous image

@@ -101,8 +101,8 @@ template <typename T, int NT, bool PEEP>
 __global__ void __launch_bounds__(512) lstm_fwd_kernel(
     const T* __restrict__ zx, const T* __restrict__ rwt, const float* __restrict__ peep,
     const float* __restrict__ h0, const float* __restrict__ c0, const float* __restrict__ mask,
-    float* __restrict__ out, float* __restrict__ gates, float* __restrict__ call, float* __restrict__ hT,
-    float* __restrict__ cT, int Tn, int mb, int H) {
+    float* __restrict__ out, T* __restrict__ out16, float* __restrict__ gates, float* __restrict__ call,
+    float* __restrict__ hT, float* __restrict__ cT, int Tn, int mb, int H) {
   constexpr int KB = FWD_FRAGS / (4 * NT) > 0 ? FWD_FRAGS / (4 * NT) : 1;   // k-steps per load batch
   constexpr bool PF = NT < 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(512) lstm_fwd_kernel(
         if (valid) {
           const long long orow = ((long long)t * mb + m0 + rr) * H;
           out[orow + j] = h;
+          if (out16) out16[orow + j] = cvt<T>(h);
           if (call) call[orow + j] = cc;
           if (gates) {
             float* gp = gates + orow * 4 + j;
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(512) lstm_fwd_kernel(
 // ------------------------------------------------------------------------------------------------ backward
 template <typename T, int NT, bool PEEP>
 __global__ void __launch_bounds__(512) lstm_bwd_kernel(
-    const float* __restrict__ eps, const float* __restrict__ gates, const float* __restrict__ call,
+    const void* __restrict__ eps, int eps_dt, const float* __restrict__ gates, const float* __restrict__ call,
     const float* __restrict__ c0, const T* __restrict__ rw, const float* __restrict__ peep,
     const float* __restrict__ mask, const float* __restrict__ dh_last, const float* __restrict__ dc_last,
     float* __restrict__ dz, float* __restrict__ dh0, float* __restrict__ dc0, int Tn, int mb, int H, int t_end) {
@@ -291,7 +292,7 @@ __global__ void __launch_bounds__(512) lstm_bwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int j = hb + nt * 16 + col;
-        ev[nt][r] = eps[hrow + j];
+        ev[nt][r] = ld_any(eps, eps_dt, hrow + j);
         av[nt][r] = gates[grow + j];
         fv[nt][r] = gates[grow + H + j];
         ov[nt][r] = gates[grow + 2 * H + j];
@@ -419,26 +420,27 @@ static bool set_lds(K kern, size_t bytes) {
 
 template <typename T, int NT, bool PEEP>
 static int fwd_launch(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
-                      const float* mask, float* out, float* gates, float* call, float* hT, float* cT, int Tn, int mb,
-                      int H, hipStream_t s) {
+                      const float* mask, float* out, void* out16, float* gates, float* call, float* hT, float* cT,
+                      int Tn, int mb, int H, hipStream_t s) {
   const size_t lds = 2ull * 16 * (H + row_pad<T>()) * sizeof(T);
   auto k = lstm_fwd_kernel<T, NT, PEEP>;
   if (!set_lds(k, lds)) return -1;
   const int threads = 64 * (H / (16 * NT));
   hipLaunchKernelGGL(k, dim3((mb + 15) / 16), dim3(threads), lds, s, (const T*)zx, (const T*)rwt, peep, h0, c0, mask,
-                     out, gates, call, hT, cT, Tn, mb, H);
+                     out, (T*)out16, gates, call, hT, cT, Tn, mb, H);
   return (int)hipGetLastError();
 }
 
 template <typename T, int NT, bool PEEP>
-static int bwd_launch(const float* eps, const float* gates, const float* call, const float* c0, const void* rw,
+static int bwd_launch(const void* eps, int eps_dt, const float* gates, const float* call, const float* c0, const void* rw,
                       const float* peep, const float* mask, const float* dhl, const float* dcl, float* dz, float* dh0,
                       float* dc0, int Tn, int mb, int H, int t_end, hipStream_t s) {
   const size_t lds = 16ull * (4 * H + row_pad<T>()) * sizeof(T);
   auto k = lstm_bwd_kernel<T, NT, PEEP>;
   if (!set_lds(k, lds)) return -1;
   const int threads = 64 * (H / (16 * NT));
-  hipLaunchKernelGGL(k, dim3((mb + 15) / 16), dim3(threads), lds, s, eps, gates, call, c0, (const T*)rw, peep, mask,
+  hipLaunchKernelGGL(k, dim3((mb + 15) / 16), dim3(threads), lds, s, eps, eps_dt, gates, call, c0, (const T*)rw, peep,
+                     mask,
                      dhl, dcl, dz, dh0, dc0, Tn, mb, H, t_end);
   return (int)hipGetLastError();
 }
@@ -468,16 +470,17 @@ static int bwd_launch(const float* eps, const float* gates, const float* call, c
 
 // Returns 0 on success, -1 when the shape/dtype is outside the kernel (caller uses the per-step path).
 DL4J_API int dl4j_lstm_fwd(int dtype, const void* zx, const void* rwt, const float* peep, const float* h0,
-                           const float* c0, const float* mask, float* out, float* gates, float* call, float* hT,
-                           float* cT, int Tn, int mb, int H, hipStream_t s) {
+                           const float* c0, const float* mask, float* out, void* out16, float* gates, float* call,
+                           float* hT, float* cT, int Tn, int mb, int H, hipStream_t s) {
   if (Tn < 1 || mb < 1 || (dtype != 0 && H % 32 != 0)) return -1;
-  LSTM_DISPATCH(fwd_launch, zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, Tn, mb, H, s);
+  LSTM_DISPATCH(fwd_launch, zx, rwt, peep, h0, c0, mask, out, out16, gates, call, hT, cT, Tn, mb, H, s);
 }
 
-DL4J_API int dl4j_lstm_bwd(int dtype, const float* eps, const float* gates, const float* call, const float* c0,
+// eps_dt: dtype of eps (0 fp32, 1 bf16, 2 fp16), read directly so the caller needs no conversion pass.
+DL4J_API int dl4j_lstm_bwd(int dtype, const void* eps, int eps_dt, const float* gates, const float* call, const float* c0,
                            const void* rw, const float* peep, const float* mask, const float* dh_last,
                            const float* dc_last, float* dz, float* dh0, float* dc0, int Tn, int mb, int H, int t_end,
                            hipStream_t s) {
   if (Tn < 1 || mb < 1 || t_end < 0 || t_end >= Tn) return -1;
-  LSTM_DISPATCH(bwd_launch, eps, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, Tn, mb, H, t_end, s);
+  LSTM_DISPATCH(bwd_launch, eps, eps_dt, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, Tn, mb, H, t_end, s);
 }

@@ -13,10 +13,11 @@
 // tag_base past every launch's tags, so stale granules never match and no per-launch memset is needed (it zeroes
 // the buffer only on first use, on tag wrap-around, and under HIP-graph capture, where every replay reuses tags).
 //
-// The grid (G x tiles workgroups, one per CU: LDS-bound) is launched with hipLaunchCooperativeKernel so that all
-// workgroups are guaranteed co-resident; shapes that do not fit fall back to csrc/lstm.hip.
+// The grid (G x tiles workgroups, one per CU: LDS-bound, at most CUs - 8 of them) is launched stream-ordered (see
+// coop_launch); shapes that do not fit fall back to csrc/lstm.hip.
 // Math, gate order [a|f|o|g], peepholes, masks and outputs are identical to lstm_fwd_kernel.
 #include "common.h"
+#include <cstdlib>
 
 typedef __attribute__((ext_vector_type(4))) float f4c_t;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8c_t;
@@ -31,14 +32,30 @@ __device__ __forceinline__ float tanh_c(float x) {
   return copysignf((1.f - e) / (1.f + e), x);
 }
 
+// Launch path. The grid is at most (CUs - 8) workgroups of one-per-CU occupancy and every cross-workgroup wait is
+// bounded by the wall clock (a timeout sets *err, checked by the host), so a plain stream-ordered launch is safe:
+// the stream's previous kernel has drained before any workgroup starts, and the few workgroups always find CUs.
+// hipLaunchCooperativeKernel adds ~13 us of dispatch gap on each side of the kernel on this runtime (rocprofv3
+// kernel trace, profiles/r3_lstm_window_kernels.txt), i.e. ~100 us per TBPTT window of the 2-layer text model;
+// DL4J_AMD_LSTM_COOP_LAUNCH=coop restores the cooperative launch.
+static hipError_t coop_launch(const void* k, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("DL4J_AMD_LSTM_COOP_LAUNCH");
+    mode = (e && e[0] == 'c') ? 1 : 0;
+  }
+  if (mode == 1) return hipLaunchCooperativeKernel(k, grid, block, args, lds, s);
+  return hipLaunchKernel(k, grid, block, args, lds, s);
+}
+
 // U = hidden units per workgroup (16 per wave); KS = H / 32 k-steps
 template <int U, bool PEEP>
 __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
     const __bf16* __restrict__ zx, const __bf16* __restrict__ rwt, const float* __restrict__ peep,
     const float* __restrict__ h0, const float* __restrict__ c0, const float* __restrict__ mask,
-    float* __restrict__ out, float* __restrict__ gates, float* __restrict__ call, float* __restrict__ hT,
-    float* __restrict__ cT, unsigned long long* exch_raw, unsigned* err_raw, int Tn, int mb, int H,
-    long long timeout_ticks, unsigned tag_base) {
+    float* __restrict__ out, __bf16* __restrict__ out16, float* __restrict__ gates, float* __restrict__ call,
+    float* __restrict__ hT, float* __restrict__ cT, unsigned long long* exch_raw, unsigned* err_raw, int Tn, int mb,
+    int H, long long timeout_ticks, unsigned tag_base) {
   constexpr int NW = U / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int KS = H / 32, H16 = H / 16, H4 = 4 * H;
@@ -169,6 +186,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
       if (valid) {
         const long long orow = ((long long)t * mb + m0 + rr) * H;
         out[orow + j] = h;
+        if (out16) out16[orow + j] = (__bf16)h;
         if (call) call[orow + j] = cc;
         if (gates) {
           float* gp = gates + orow * 4 + j;
@@ -202,8 +220,8 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
 
 template <int U, bool PEEP>
 static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
-                           const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
-                           unsigned long long* exch, unsigned* err, int Tn, int mb, int H, unsigned tag_base,
+                           const float* mask, float* out, void* out16, float* gates, float* call, float* hT,
+                           float* cT, unsigned long long* exch, unsigned* err, int Tn, int mb, int H, unsigned tag_base,
                            int reset, hipStream_t s) {
   const int KS = H / 32, NW = U / 16;
   const size_t lds = (size_t)4 * NW * KS * 64 * 16 + (H <= 256 ? 2ull : 1ull) * 16 * (H + 8) * 2;
@@ -227,9 +245,9 @@ static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, c
   if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
   long long timeout = 200LL * 1000 * 1000;                  // wall_clock64 runs at 100 MHz: 2 s per wait
   void* args[] = {(void*)&zx, (void*)&rwt, (void*)&peep, (void*)&h0, (void*)&c0, (void*)&mask, (void*)&out,
-                  (void*)&gates, (void*)&call, (void*)&hT, (void*)&cT, (void*)&exch, (void*)&err, (void*)&Tn,
+                  (void*)&out16, (void*)&gates, (void*)&call, (void*)&hT, (void*)&cT, (void*)&exch, (void*)&err, (void*)&Tn,
                   (void*)&mb, (void*)&H, (void*)&timeout, (void*)&tag_base};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
+  const hipError_t e = coop_launch(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return -1;
@@ -249,7 +267,7 @@ static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, c
 // forward.
 template <int U, int H, bool PEEP>
 __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
-    const float* __restrict__ eps, const float* __restrict__ gates, const float* __restrict__ call,
+    const void* __restrict__ eps, int eps_dt, const float* __restrict__ gates, const float* __restrict__ call,
     const float* __restrict__ c0, const __bf16* __restrict__ rw, const float* __restrict__ peep,
     const float* __restrict__ mask, const float* __restrict__ dh_last, const float* __restrict__ dc_last,
     float* __restrict__ dz, float* __restrict__ dh0, float* __restrict__ dc0, unsigned long long* exch_raw,
@@ -294,7 +312,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const long long hrow = ((long long)t * mb + mrow[r]) * H, grow = hrow * 4;
-      ev[r] = eps[hrow + j];
+      ev[r] = ld_any(eps, eps_dt, hrow + j);
       av[r] = gates[grow + j];
       fv[r] = gates[grow + H + j];
       ov[r] = gates[grow + 2 * H + j];
@@ -417,7 +435,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
 }
 
 template <int U, int H, bool PEEP>
-static int coop_bwd_launch(const float* eps, const float* gates, const float* call, const float* c0, const void* rw,
+static int coop_bwd_launch(const void* eps, int eps_dt, const float* gates, const float* call, const float* c0, const void* rw,
                            const float* peep, const float* mask, const float* dhl, const float* dcl, float* dz,
                            float* dh0, float* dc0, unsigned long long* exch, unsigned* err, int Tn, int mb, int t_end,
                            unsigned tag_base, int reset, hipStream_t s) {
@@ -439,10 +457,10 @@ static int coop_bwd_launch(const float* eps, const float* gates, const float* ca
   if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
   long long timeout = 200LL * 1000 * 1000;                  // 2 s per wait at 100 MHz
   const __bf16* rwp = reinterpret_cast<const __bf16*>(rw);
-  void* args[] = {(void*)&eps, (void*)&gates, (void*)&call, (void*)&c0, (void*)&rwp, (void*)&peep, (void*)&mask,
+  void* args[] = {(void*)&eps, (void*)&eps_dt, (void*)&gates, (void*)&call, (void*)&c0, (void*)&rwp, (void*)&peep, (void*)&mask,
                   (void*)&dhl, (void*)&dcl, (void*)&dz, (void*)&dh0, (void*)&dc0, (void*)&exch, (void*)&err,
                   (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout, (void*)&tag_base};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
+  const hipError_t e = coop_launch(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return -1;
@@ -456,14 +474,14 @@ DL4J_API long long dl4j_lstm_coop_bwd_exch_bytes(int mb, int H) {
 }
 
 // bf16 RW only; H in {256 (U = 64), 512 (U = 32)}. Returns -1 when the cooperative path does not apply.
-DL4J_API int dl4j_lstm_bwd_coop(const float* eps, const float* gates, const float* call, const float* c0,
+DL4J_API int dl4j_lstm_bwd_coop(const void* eps, int eps_dt, const float* gates, const float* call, const float* c0,
                                 const void* rw, const float* peep, const float* mask, const float* dh_last,
                                 const float* dc_last, float* dz, float* dh0, float* dc0, unsigned long long* exch,
                                 unsigned* err, int Tn, int mb, int H, int t_end, unsigned tag_base, int reset,
                                 hipStream_t s) {
   if (Tn < 1 || mb < 1 || t_end < 0 || t_end >= Tn) return -1;
   const bool pp = peep != nullptr;
-#define BWD_ARGS eps, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, exch, err, Tn, mb, t_end, tag_base, \
+#define BWD_ARGS eps, eps_dt, gates, call, c0, rw, peep, mask, dh_last, dc_last, dz, dh0, dc0, exch, err, Tn, mb, t_end, tag_base, \
                  reset, s
   if (H == 256) return pp ? coop_bwd_launch<64, 256, true>(BWD_ARGS) : coop_bwd_launch<64, 256, false>(BWD_ARGS);
   if (H == 512) return pp ? coop_bwd_launch<32, 512, true>(BWD_ARGS) : coop_bwd_launch<32, 512, false>(BWD_ARGS);
@@ -475,12 +493,12 @@ DL4J_API long long dl4j_lstm_coop_exch_bytes(int mb, int H) { return (long long)
 
 // bf16 only; H in {128, 256} (U = 64) or 512 (U = 32). Returns -1 when the cooperative path does not apply.
 DL4J_API int dl4j_lstm_fwd_coop(const void* zx, const void* rwt, const float* peep, const float* h0, const float* c0,
-                                const float* mask, float* out, float* gates, float* call, float* hT, float* cT,
-                                unsigned long long* exch, unsigned* err, int Tn, int mb, int H, unsigned tag_base,
-                                int reset, hipStream_t s) {
+                                const float* mask, float* out, void* out16, float* gates, float* call, float* hT,
+                                float* cT, unsigned long long* exch, unsigned* err, int Tn, int mb, int H,
+                                unsigned tag_base, int reset, hipStream_t s) {
   if (Tn < 1 || mb < 1) return -1;
   const bool pp = peep != nullptr;
-#define FWD_ARGS zx, rwt, peep, h0, c0, mask, out, gates, call, hT, cT, exch, err, Tn, mb, H, tag_base, reset, s
+#define FWD_ARGS zx, rwt, peep, h0, c0, mask, out, out16, gates, call, hT, cT, exch, err, Tn, mb, H, tag_base, reset, s
   if (H == 128 || H == 256) return pp ? coop_fwd_launch<64, true>(FWD_ARGS) : coop_fwd_launch<64, false>(FWD_ARGS);
   if (H == 512) return pp ? coop_fwd_launch<32, true>(FWD_ARGS) : coop_fwd_launch<32, false>(FWD_ARGS);
 #undef FWD_ARGS

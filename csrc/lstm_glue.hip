@@ -61,3 +61,64 @@ DL4J_API int dl4j_lstm_bwd_prep(int dt, const float* dz, const float* out, const
     return -1;
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------ recurrent weight packing
+// One launch per layer per TBPTT window replaces the two permute-copies (forward B = RWᵀ, backward B = RW) and the
+// peephole gathers the sequence kernels need (ops/rnn_native.py _pack_b layout): for an [N, K] matrix m the packed
+// image is [N/16][K/KC][4][16][FE] with KC = 4*FE (FE = 8 for 16-bit T, 4 for fp32), element
+// (n, k) -> ((((n/16)*(K/KC) + k/KC)*4 + (k%KC)/FE)*16 + n%16)*FE + k%FE.
+//   forward : m[n][k] = RW[k][n], N = 4H, K = H        backward: m[n][k] = RW[n][k], N = H, K = 4H
+// RW is the [H, 4H(+3)] weight view with element strides (s0, s1) (DL4J 'f' order: s0 = 1, s1 = H); peep[i][h] =
+// RW[h][4H + i] in fp32. Each thread writes one element of each packed image (reads are strided gathers of a 0.5 MB
+// matrix: L2-resident).
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_pack_rw_kernel(const T* __restrict__ rw, long long s0, long long s1, int H,
+                                                           T* __restrict__ fwd, T* __restrict__ bwd,
+                                                           float* __restrict__ peep) {
+  constexpr int FE = sizeof(T) == 2 ? 8 : 4, KC = 4 * FE;
+  const long long total = 4LL * H * H;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (long long)gridDim.x * blockDim.x) {
+    // decode the packed position o -> (n, k) for an [N, K] image
+    const int e = (int)(o % FE);
+    long long q = o / FE;
+    const int n16 = (int)(q % 16); q /= 16;
+    const int sub = (int)(q % 4); q /= 4;
+    if (fwd) {                                            // N = 4H, K = H
+      const int KB = H / KC;
+      const int kb = (int)(q % KB), nb = (int)(q / KB);
+      const int n = nb * 16 + n16, k = kb * KC + sub * FE + e;
+      fwd[o] = rw[(long long)k * s0 + (long long)n * s1];
+    }
+    if (bwd) {                                            // N = H, K = 4H
+      const int KB = 4 * H / KC;
+      const int kb = (int)(q % KB), nb = (int)(q / KB);
+      const int n = nb * 16 + n16, k = kb * KC + sub * FE + e;
+      bwd[o] = rw[(long long)n * s0 + (long long)k * s1];
+    }
+    if (peep && o < 3LL * H) {
+      const int i = (int)(o / H), h = (int)(o % H);
+      peep[o] = ld1<T>(rw + (long long)h * s0 + (long long)(4 * H + i) * s1);
+    }
+  }
+}
+
+// dt: 0 fp32, 1 bf16, 2 fp16. fwd / bwd / peep may each be null. H % KC == 0 required (KC = 32 / 16).
+DL4J_API int dl4j_lstm_pack_rw(int dt, const void* rw, long long s0, long long s1, int H, void* fwd, void* bwd,
+                               float* peep, hipStream_t s) {
+  if (H <= 0 || H % (dt == 0 ? 16 : 32) != 0) return -1;
+  const long long total = 4LL * H * H;
+  long long g = (total + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (dt == 1)
+    hipLaunchKernelGGL(lstm_pack_rw_kernel<bf16>, dim3((unsigned)g), dim3(256), 0, s, (const bf16*)rw, s0, s1, H,
+                       (bf16*)fwd, (bf16*)bwd, peep);
+  else if (dt == 2)
+    hipLaunchKernelGGL(lstm_pack_rw_kernel<f16>, dim3((unsigned)g), dim3(256), 0, s, (const f16*)rw, s0, s1, H,
+                       (f16*)fwd, (f16*)bwd, peep);
+  else if (dt == 0)
+    hipLaunchKernelGGL(lstm_pack_rw_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, (const float*)rw, s0, s1, H,
+                       (float*)fwd, (float*)bwd, peep);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

@@ -439,8 +439,8 @@ struct CopyShape {
   long long base;        // source element offset of coordinate 0
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void strided_copy(const T* __restrict__ x, T* __restrict__ y, long long n,
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void strided_copy(const TI* __restrict__ x, TO* __restrict__ y, long long n,
                                                     CopyShape s) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -630,8 +630,20 @@ DL4J_API int dl4j_reduce(int dt, int op, const void* x, float* out, long long* i
 
 // out = contiguous tensor of shape[rank]; element at coordinate c reads x[base + sum_d (c_d + off_d) * st_d], or 0
 // when some lim_d > 0 and (c_d + off_d) is outside [0, lim_d).
+// Same with a dtype conversion: x in sdt, y in ddt (0 fp32, 1 bf16, 2 fp16) — e.g. permute + cast + zero-pad of a
+// GEMM operand in one pass.
+DL4J_API int dl4j_strided_copy2(int sdt, int ddt, const void* x, void* y, int rank, const long long* shape,
+                                const long long* st, const long long* off, const long long* lim, long long base,
+                                hipStream_t s);
+
 DL4J_API int dl4j_strided_copy(int dt, const void* x, void* y, int rank, const long long* shape, const long long* st,
                                const long long* off, const long long* lim, long long base, hipStream_t s) {
+  return dl4j_strided_copy2(dt, dt, x, y, rank, shape, st, off, lim, base, s);
+}
+
+DL4J_API int dl4j_strided_copy2(int sdt, int ddt, const void* x, void* y, int rank, const long long* shape,
+                                const long long* st, const long long* off, const long long* lim, long long base,
+                                hipStream_t s) {
   if (rank < 1 || rank > 8) return -1;
   CopyShape cs = {};
   cs.rank = rank;
@@ -646,9 +658,17 @@ DL4J_API int dl4j_strided_copy(int dt, const void* x, void* y, int rank, const l
   }
   if (n <= 0) return 0;
   const int g = grid1(n);
-#define L(T) hipLaunchKernelGGL((strided_copy<T>), dim3(g), dim3(256), 0, s, (const T*)x, (T*)y, n, cs)
-  DT_DISPATCH(dt, L);
-#undef L
+#define L2(TI, TO) hipLaunchKernelGGL((strided_copy<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, (TO*)y, n, cs)
+#define LO(TI)                          \
+  do {                                  \
+    if (ddt == 0) { L2(TI, float); }    \
+    else if (ddt == 1) { L2(TI, bf16); } \
+    else if (ddt == 2) { L2(TI, f16); }  \
+    else return -1;                     \
+  } while (0)
+  DT_DISPATCH(sdt, LO);
+#undef LO
+#undef L2
   return (int)hipGetLastError();
 }
 

@@ -35,6 +35,63 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__
   if (threadIdx.x == 0) score[row] = sc;
 }
 
+// Strided variant: logits rows with leading dimension ldz; label row r = t*mb + b (t = r / mb, b = r % mb) read at
+// y + b*ys_b + t*ys_t + j*ys_j, so the RNN output layer's [mb, V, T] labels are consumed in place (2-D labels: mb = B,
+// ys_t = 0); gradient rows have leading dimension ldg >= V with columns V..ldg-1 written as zeros — the gradient is
+// directly a zero-K-padded GEMM operand for dW = hᵀ·g and dx = g·Wᵀ (ops/gemm.py kz_view).
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_xent_strided(const T* __restrict__ z, int ldz, const float* __restrict__ y,
+                                                            long long ys_b, long long ys_t, long long ys_j, int mb,
+                                                            int V, T* __restrict__ grad, int ldg,
+                                                            float* __restrict__ score, float log_eps,
+                                                            float log_1m_eps) {
+  __shared__ float red[16];
+  const long long row = blockIdx.x;
+  const T* zr = z + row * ldz;
+  const float* yr = y + (row % mb) * ys_b + (row / mb) * ys_t;
+  float m = -INFINITY;
+  for (int j = threadIdx.x; j < V; j += blockDim.x) m = fmaxf(m, ld1<T>(zr + j));
+  m = block_reduce<true>(m, red);
+  float s = 0.f;
+  for (int j = threadIdx.x; j < V; j += blockDim.x) s += __expf(ld1<T>(zr + j) - m);
+  s = block_reduce<false>(s, red);
+  const float lse = m + __logf(s);
+  const float inv = 1.f / s;
+  float sc = 0.f;
+  for (int j = threadIdx.x; j < ldg; j += blockDim.x) {
+    if (j < V) {
+      const float zj = ld1<T>(zr + j);
+      const float p = __expf(zj - m) * inv;
+      const float yj = yr[j * ys_j];
+      float lp = zj - lse;
+      lp = fminf(fmaxf(lp, log_eps), log_1m_eps);
+      sc -= yj * lp;
+      st1<T>(grad + row * ldg + j, p - yj);
+    } else {
+      st1<T>(grad + row * ldg + j, 0.f);
+    }
+  }
+  sc = block_reduce<false>(sc, red);
+  if (threadIdx.x == 0) score[row] = sc;
+}
+
+DL4J_API int dl4j_softmax_xent_strided(int dtype, const void* z, int ldz, const float* y, long long ys_b,
+                                       long long ys_t, long long ys_j, int mb, int B, int V, void* grad, int ldg,
+                                       float* score, float clip_eps, hipStream_t s) {
+  if (B <= 0) return 0;
+  if (mb <= 0 || ldz < V || ldg < V) return -1;
+  const float le = clip_eps > 0.f ? logf(clip_eps) : -INFINITY;
+  const float l1 = clip_eps > 0.f ? log1pf(-clip_eps) : 0.f;
+#define SXS(T) hipLaunchKernelGGL(softmax_xent_strided<T>, dim3(B), dim3(256), 0, s, (const T*)z, ldz, y, ys_b, ys_t, \
+                                  ys_j, mb, V, (T*)grad, ldg, score, le, l1)
+  if (dtype == 1) SXS(bf16);
+  else if (dtype == 2) SXS(f16);
+  else if (dtype == 0) SXS(float);
+  else return -1;
+#undef SXS
+  return (int)hipGetLastError();
+}
+
 DL4J_API int dl4j_softmax_xent(int dtype, const void* z, const float* y, int B, int V, void* grad, float* score,
                                float* prob, float clip_eps, hipStream_t s) {
   const float le = clip_eps > 0.f ? logf(clip_eps) : -INFINITY;

@@ -172,6 +172,15 @@ def weight_grad_(view, a, b):
 
 def bias_grad_(view, delta):
     """Bias gradient = column sums of delta [M, N] (fp32), on the channel-sum HIP kernel when on the GPU."""
+    K8 = getattr(delta, "_dl4j_kz", 0)
+    if K8 and delta.is_cuda and delta.dim() == 2 and delta.stride() == (K8, 1) and view.dtype == torch.float32:
+        # zero-padded operand view (ops/gemm.py kz_view): column sums over the whole padded buffer, padding dropped
+        from ...ops import native
+        full = delta.as_strided((delta.shape[0], K8), (K8, 1))
+        tmp = native.channel_sum(full)
+        if tmp is not None:
+            view.copy_(tmp[:delta.shape[1]].reshape(view.shape))
+            return
     if delta.is_cuda and delta.dim() == 2 and delta.dtype in (torch.float32, torch.bfloat16, torch.float16) \
             and delta.is_contiguous() \
             and view.dtype == torch.float32 and view.is_contiguous() and delta.shape[1] % 8 == 0:

@@ -76,14 +76,48 @@ class BaseOutputLayerImpl(LayerImpl):
         z = self.preOutput2d(x2)
         self._z = z
         self._cache = None
+        if training and getattr(self, "_skip_train_output", False) and self._fused():
+            # training step whose output activation nobody reads (the fused loss recomputes the softmax from z):
+            # the pre-activation stands in for it
+            return self._out_from2d(z)
         return self._out_from2d(self.conf.activation.getActivation(z, training))
 
     def output(self, x, training=False):
         return self.activate(x, training)
 
+    def _lab_strided(self, y):
+        """(mb, (per-example, per-time-step, per-class) strides) addressing the 2-D label rows inside ``y`` in place,
+        or None when the rows are not a strided view of it."""
+        if y.dim() == 2:
+            return y.shape[0], (y.stride(0), 0, y.stride(1))
+        return None
+
+    def _loss_and_grad_strided(self):
+        """GPU fused softmax-MCXENT straight from the layer's label tensor (no 2-D label copy); the gradient comes
+        back as a zero-K-padded GEMM operand when nOut % 8 != 0."""
+        z = self._z
+        if not (z.is_cuda and z.dim() == 2 and self.maskArray is None and self.labels is not None):
+            return None
+        from ... import ops
+        if not ops.use_native(z, "softmax_xent"):
+            return None
+        y = self.labels
+        if y.device != z.device or y.dtype != torch.float32:
+            y = y.to(device=z.device, dtype=torch.float32)
+        ls = self._lab_strided(y)
+        if ls is None:
+            return None
+        from ...ops import native
+        return native.softmax_xent_strided(z, y, ls[0], ls[1], self.conf.lossFn.softmaxClipEps)
+
     def _loss_and_grad(self):
         if self._cache is not None:
             return self._cache
+        if self._fused():
+            r = self._loss_and_grad_strided()
+            if r is not None:
+                self._cache = r
+                return r
         y = self._lab2d(self.labels)
         mask = self._mask2d(self.maskArray)
         if self._fused():
@@ -140,6 +174,11 @@ class RnnOutputLayerImpl(BaseOutputLayerImpl):
 
     def _lab2d(self, y):
         return _rnn_to_2d(y) if y.dim() == 3 else y
+
+    def _lab_strided(self, y):
+        if y.dim() == 3:                                   # [mb, V, T]: row t*mb + b
+            return y.shape[0], (y.stride(0), y.stride(2), y.stride(1))
+        return super()._lab_strided(y)
 
     def _mask2d(self, m):
         return _mask_rnn_to_2d(m)

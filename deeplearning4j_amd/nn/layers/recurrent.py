@@ -28,23 +28,45 @@ def _native_ok(x, W, act, gate_act, H):
             and rnn_native.supported(H, W.dtype) and ops.use_native(x, "lstm"))
 
 
+def _time_major_rows(x, dt):
+    """[mb, nIn, T] -> [T*mb, nIn] rows in the compute dtype. On the GPU, when that takes a copy anyway (a cast, a
+    non-trivial permute, or nIn % 8 != 0), ONE launch permutes + casts + zero-pads the last dimension to a multiple of
+    8 (ops/nd4j_kernels.cast_pad_last): the rows are then a ``kz_view`` GEMM operand read in place by x·W and by
+    dW = xᵀ·dz (no padded copies inside the GEMMs)."""
+    mb, nIn, T = x.shape
+    xp = x.permute(2, 0, 1)
+    if x.is_cuda and dt in (torch.bfloat16, torch.float16) and (nIn % 8 or x.dtype != dt or not xp.is_contiguous()):
+        from ...memory import arena
+        from ...ops import nd4j_kernels as K
+        from ...ops.gemm import kz_view
+        K8 = (nIn + 7) // 8 * 8
+        buf = arena.empty((T, mb, K8), dt, x.device)
+        if K.cast_pad_last(xp, dt, K8, out=buf) is not None:
+            rows = buf.reshape(T * mb, K8)
+            return kz_view(rows, nIn) if K8 != nIn else rows
+    return xp.reshape(T * mb, nIn).to(dt)
+
+
 def _lstm_fwd(x, W, RW, b, h0, c0, H, peephole, act, gate_act, mask, need_cache):
     """x: [mb, nIn, T]. Returns out [mb, H, T], (hT, cT), cache."""
     mb, nIn, T = x.shape
     dt = W.dtype
     _adt = acc_dtype(W)
-    xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
+    xt = _time_major_rows(x, dt)
     zx = matmul(xt, W, bias=b).reshape(T, mb, 4 * H)          # input projection, all steps (bias in the epilogue)
     if _native_ok(x, W, act, gate_act, H):
         from ...ops import rnn_native
-        r = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, mask, need_cache)
+        # both packed images of RW (+ fp32 peepholes) in one launch; the backward pass reuses them
+        packs = rnn_native.pack_rw(RW, H, peephole, need_bwd=need_cache)
+        r = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, mask, need_cache, packs=packs, out16=True)
         if r is not None:
-            out_tmh, hT, cT, gates, call = r
-            out = out_tmh.permute(1, 2, 0).to(dt)          # compute dtype (DL4J casts input to the net dtype)
+            out_tmh, hT, cT, gates, call, o16 = r
+            # compute dtype (DL4J casts input to the net dtype); the kernel wrote the 16-bit copy itself
+            out = o16.permute(1, 2, 0) if o16 is not None else out_tmh.permute(1, 2, 0).to(dt)
             cache = None
             if need_cache:
                 cache = {"native": True, "gates": gates, "call": call, "out": out_tmh, "h0": h0, "c0": c0,
-                         "xt": xt}
+                         "xt": xt, "packs": packs}
             return out, (hT, cT), cache
     RWg = RW[:, :4 * H]
     if peephole:
@@ -119,12 +141,13 @@ def _lstm_weight_grads(dzf2, xt, hprev, W, H, peephole, peep_grads, grads_prefix
     return matmul(dzf2.to(dt), W.t()).reshape(T, mb, -1).permute(1, 2, 0)
 
 
-def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last):
+def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last,
+                     need_dx=True):
     from ...ops import rnn_native
     mb, _, T = eps.shape
     t_end = max(0, T - tbptt_back) if tbptt_back else 0
     r = rnn_native.lstm_seq_bwd(eps.permute(2, 0, 1), cache["gates"], cache["call"], cache["c0"], RW, H, peephole,
-                                mask, dh_last, dc_last, t_end)
+                                mask, dh_last, dc_last, t_end, packs=cache.get("packs"))
     if r is None:
         return None
     dz, dh0, dc0 = r
@@ -144,6 +167,8 @@ def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_pre
             else:
                 _wgrad(gRW, hpb, dzb)
             copy_grad_(grads[grads_prefix + "b"], db)
+            if not need_dx:                              # first layer: dL/dinput is never read
+                return None, dh0, dc0
             return matmul(dzb, W.t()).reshape(T, mb, -1).permute(1, 2, 0), dh0, dc0
     h0 = torch.zeros(1, mb, H, device=dev) if cache["h0"] is None else _acc(cache["h0"]).reshape(1, mb, H)
     hprev = torch.cat([h0.to(out.dtype), out[:-1]], dim=0)
@@ -160,10 +185,12 @@ def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_pre
 
 
 def _lstm_bwd(eps, cache, W, RW, H, peephole, act, gate_act, mask, tbptt_back, grads_prefix, grads, dh_last=None,
-              dc_last=None):
-    """eps: [mb, H, T]. Writes dW/dRW/db into grads views; returns eps_in [mb, nIn, T]."""
+              dc_last=None, need_dx=True):
+    """eps: [mb, H, T]. Writes dW/dRW/db into grads views; returns eps_in [mb, nIn, T] (None possible when
+    ``need_dx`` is False)."""
     if cache.get("native"):
-        r = _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last)
+        r = _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_prefix, grads, dh_last, dc_last,
+                             need_dx)
         if r is not None:
             return r
         raise RuntimeError("native LSTM forward cache but the backward kernel rejected the shape")
@@ -276,8 +303,12 @@ class LSTMImpl(BaseRecurrentImpl):
         if eps.dim() == 2:
             eps = eps.unsqueeze(2)
         H = self.conf.nOut
+        need_dx = getattr(self, "need_input_grad", True)
         dx, _, _ = _lstm_bwd(eps, self._cache, self.W("W"), self.W("RW"), H, self.PEEPHOLE, self.conf.activation,
-                             self.conf.gateActivationFn, self.maskArray, tbptt_back, "", self.grads)
+                             self.conf.gateActivationFn, self.maskArray, tbptt_back, "", self.grads,
+                             need_dx=need_dx)
+        if dx is None:
+            return self.make_gradient(), None
         return self.make_gradient(), self.backpropDropOut(dx.to(eps.dtype))
 
 

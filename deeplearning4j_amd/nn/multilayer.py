@@ -186,8 +186,14 @@ class MultiLayerNetwork(BaseNetwork):
         lmask = self.labelsMask if lmask is None else lmask
         self._mb = x.shape[0]
         self._prepare_conv_weights()
-        acts = self.feedForwardToLayer(len(self.layers) - 1, x, True, self._to_dev(fmask), stored_state,
-                                       store_last_for_tbptt)
+        out_l = self.layers[-1]
+        # nobody reads the output activation of a training forward unless a listener asks for the activations
+        out_l._skip_train_output = not any(hasattr(l, "onForwardPass") for l in self.listeners)
+        try:
+            acts = self.feedForwardToLayer(len(self.layers) - 1, x, True, self._to_dev(fmask), stored_state,
+                                           store_last_for_tbptt)
+        finally:
+            out_l._skip_train_output = False
         for l in self.listeners:
             if hasattr(l, "onForwardPass"):
                 l.onForwardPass(self, acts)

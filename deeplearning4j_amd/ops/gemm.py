@@ -66,7 +66,10 @@ def _candidates(M, N, K, batch, default):
         c += [(4, s) for s in splits if s == 1 or (batch == 1 and K // s >= 512 and t256 * s <= 1024)]
     c += [(x, 1) for x in (0, 1, 2, 3)]
     if batch == 1:
-        c += [(x, s) for x in (1, 2, 3) for s in splits[1:] if K // s >= 512 and t128 * s <= 2048]
+        # small output grids (e.g. the LSTM's [256 x 1024] weight gradients over K = T*mb = 1600) need deep split-K
+        # to fill the CUs: down to 128-deep K slices when the tile grid is under a quarter of the chip
+        kmin = 128 if t128 * 4 <= 256 else 512
+        c += [(x, s) for x in (1, 2, 3) for s in splits[1:] if K // s >= kmin and t128 * s <= 2048]
     seen, out = set(), []
     for x in c:
         if x not in seen:
@@ -79,20 +82,16 @@ def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True):
     """First eager call of a problem shape: time every kernel configuration (tile shape x split-K) on a scratch
     destination and keep the fastest (hipBLASLt-style heuristics replaced by measurement). Never runs while a HIP
     graph is being captured; the cost-model plan is used there."""
+    from .timing import gpu_time
     tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
     best, best_t = default, None
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for cand in _candidates(M, N, K, batch, default):
         if cand[1] > 1 and not splits_ok:
             continue
         if launch(cand[0], cand[1], tmp, 0.0, None) != 0:
             continue
-        ev0.record()
-        for _ in range(3):
-            launch(cand[0], cand[1], tmp, 0.0, None)
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1)
+        # GPU-side time (stream parked during the enqueue): small GEMMs are shorter than the host launch path
+        t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, None), reps=3, warmup=0)
         if best_t is None or t < best_t:
             best, best_t = cand, t
     return best
@@ -125,16 +124,34 @@ def _b_layout(t):
 
 
 def _fast_ok(t, lay, K, is_a):
-    """Mirror of dl4j_gemm's addressing requirements for one operand (16-byte DMA chunks)."""
+    """Mirror of dl4j_gemm's addressing requirements for one operand (16-byte DMA chunks). A K-contiguous operand
+    with K % 8 != 0 qualifies when it is a view of a buffer whose columns K..K8-1 are zeros (``kz_view``)."""
     if lay is None or t.data_ptr() % 16 or lay[1] % 8:
         return False
     if t.dim() == 3 and t.stride(0) % 8:
         return False
-    return K % 8 == 0 if lay[0] else True
+    if lay[0] and K % 8:
+        K8 = (K + 7) // 8 * 8
+        return getattr(t, "_dl4j_kz", 0) >= K8 and lay[1] >= K8
+    return True
+
+
+def kz_view(buf, K):
+    """[.., K] view of the [.., K8] buffer ``buf`` whose columns K..K8-1 are zero: the GEMM then reads the operand in
+    place (its 16-byte chunk past K only meets zeros) instead of making a padded copy."""
+    v = buf[..., :K]
+    v._dl4j_kz = buf.shape[-1]
+    return v
 
 
 def _pad_kc(t, K, K8):
-    """[.., R, K] operand -> contiguous [.., R, K8] copy with zeros in columns K..K8-1."""
+    """[.., R, K] operand -> contiguous [.., R, K8] copy with zeros in columns K..K8-1 (one strided-copy launch on the
+    GPU)."""
+    if t.is_cuda:
+        from . import nd4j_kernels as NK
+        r = NK.cast_pad_last(t, t.dtype, K8)
+        if r is not None:
+            return r
     p = torch.zeros(t.shape[:-1] + (K8,), dtype=t.dtype, device=t.device)
     p[..., :K].copy_(t)
     return p
@@ -242,13 +259,15 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         # odd K / leading dimensions: zero-padded K-contiguous copies (usually a small operand such as a one-hot
         # input) keep the product on the MFMA LDS-DMA kernel instead of the scalar-load generic one
         K8 = (K + 7) // 8 * 8
-        if K8 != K or not _fast_ok(a, la, K, True):
-            a = _pad_kc(a, K, K8)
+        if not _fast_ok(a, la, K, True):
+            a = _pad_kc(a, K, K8)[..., :K]
             la = (True, K8)
-        if K8 != K or not _fast_ok(b, lb, K, False):
-            b = _pad_kc(b.transpose(-1, -2), K, K8).transpose(-1, -2)
+        if not _fast_ok(b, lb, K, False):
+            b = _pad_kc(b.transpose(-1, -2), K, K8)[..., :K].transpose(-1, -2)
             lb = (True, K8)
-        K = K8
+    # K-contiguous operands with K % 8 != 0 are zero-padded to K8 here (flag 2 for dl4j_gemm); M/N-contiguous ones
+    # read rows >= K from the kernel's zero page
+    kzf = lambda lay: (2 if lay is not None and lay[0] and K % 8 else 0)  # noqa: E731
     sA = a.stride(0) if batched else 0
     sB = b.stride(0) if batched else 0
     sC = c_t.stride(0) if batched else 0
@@ -272,8 +291,8 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     if in_dt != 0 and la_ is not None and lb_ is not None:
         def launch(cfg, sp, dst, bt, zz, ts=None):
             ws = torch.empty(Mx * Nx * sp, dtype=torch.float32, device=a.device) if sp > 1 else None
-            return lib.dl4j_gemm(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), la_[1], int(la_[0]), sA_, _p(B_),
-                                 lb_[1], int(lb_[0]), sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc,
+            return lib.dl4j_gemm(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), la_[1], int(la_[0]) | kzf(la_),
+                                 sA_, _p(B_), lb_[1], int(lb_[0]) | kzf(lb_), sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc,
                                  _p(zz), cfg, sp, _p(ws), _p(ts), 0 if ts is None else ts.shape[1], _stream())
 
         key = (Mx, Nx, K, batch, in_dt, _DT[out_dtype], la_[0], lb_[0], la_[1] % 64 == 0, lb_[1] % 64 == 0)

@@ -34,9 +34,9 @@ def load():
         "dl4j_segdesc_size": [],
         "dl4j_bn_workspace_floats": [c_ll, c_int],
         "dl4j_bn_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_float, c_float,
-                        c_void_p, c_void_p, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
         "dl4j_bn_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
-                        c_void_p, c_int, c_void_p, c_void_p],
+                        c_void_p, c_int, c_void_p, c_void_p, c_void_p],
         "dl4j_softmax_xent": [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
                               c_void_p],
         "dl4j_pool_fwd": [c_int, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p],
@@ -295,32 +295,35 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     g = gamma if torch.is_tensor(gamma) else None
     b = beta if torch.is_tensor(beta) else None
     res = _rows_like(residual, x) if residual is not None else None
+    # training with a fused residual: bn_apply writes the ReLU bitmask (1 bit per element) so the backward pass
+    # never re-reads the residual
+    mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if res is not None and training else None
     ts = getattr(x, "_bn_tile_stats", None)
     if training and ts is not None and dt in (1, 2) and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
             (len(ts) < 3 or ts[2] == 64):
         # statistics already reduced per tile by the producing conv kernel's epilogue
         register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_void_p,
                                            c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int,
-                                           c_void_p, c_void_p, c_void_p])
+                                           c_void_p, c_void_p, c_void_p, c_void_p])
         register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
         wst = torch.empty(lib.dl4j_bn_tiles_workspace_floats(ts[1], C), dtype=torch.float32, device=x.device)
         rc = lib.dl4j_bn_fwd_tiles(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(ts[0]), ts[1], _ptr(g), _ptr(b),
                                    float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0,
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
-                                   _ptr(wst), _ptr(ctx), _stream())
+                                   _ptr(wst), _ptr(ctx), _ptr(mask), _stream())
         _check(rc, "bn_fwd_tiles")
-        return y, ("NATIVE", x, ctx, relu, M, C, res)
+        return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
     rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
                          float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                          _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
-                         _ptr(ctx), _stream())
+                         _ptr(ctx), _ptr(mask), _stream())
     _check(rc, "bn_fwd")
-    return y, ("NATIVE", x, ctx, relu, M, C, res)
+    return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
 
 
 def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
-    _, x, c, relu, M, C, res = ctx
+    _, x, c, relu, M, C, res, mask = ctx
     dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
@@ -330,7 +333,7 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
     rc = lib.dl4j_bn_bwd(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
-                         _ptr(dbeta), 1 if relu else 0, _ptr(ws), _stream())
+                         _ptr(dbeta), 1 if relu else 0, _ptr(ws), _ptr(mask), _stream())
     _check(rc, "bn_bwd")
     return dx, dgamma, dbeta, dres
 
@@ -420,6 +423,28 @@ def softmax_xent(logits, labels, clip_eps):
                                   float(clip_eps or 0.0), _stream())
     _check(rc, "softmax_xent")
     return score, grad, None
+
+
+def softmax_xent_strided(logits, y, mb, ys, clip_eps):
+    """Fused softmax + MCXENT over the rows of ``logits`` [B, V] (unit column stride) with labels read in place from
+    fp32 ``y`` at strides ys = (per-example, per-time-step, per-class) for row r = t*mb + b. Returns (score [B] fp32,
+    gradient [B, V]); when V % 8 != 0 the gradient is a zero-padded ``kz_view`` GEMM operand (ops/gemm.py)."""
+    dt = _dt16(logits)
+    if dt is None or logits.dim() != 2 or logits.stride(1) != 1 or y.dtype != torch.float32 or not y.is_cuda:
+        return None
+    B, V = logits.shape
+    register_sig("dl4j_softmax_xent_strided", [c_int, c_void_p, c_int, c_void_p, c_ll, c_ll, c_ll, c_int, c_int, c_int,
+                                               c_void_p, c_int, c_void_p, c_float, c_void_p])
+    from ..memory import arena
+    from .gemm import kz_view
+    V8 = (V + 7) // 8 * 8
+    buf = arena.empty((B, V8), logits.dtype, logits.device)
+    score = arena.empty((B,), torch.float32, logits.device)
+    rc = load().dl4j_softmax_xent_strided(dt, _ptr(logits), logits.stride(0) if B > 1 else V, _ptr(y), int(ys[0]),
+                                          int(ys[1]), int(ys[2]), int(mb), B, V, _ptr(buf), V8, _ptr(score),
+                                          float(clip_eps or 0.0), _stream())
+    _check(rc, "softmax_xent_strided")
+    return score, (kz_view(buf, V) if V8 != V else buf)
 
 
 # ------------------------------------------------------------------------------------------ pooling

@@ -26,6 +26,8 @@ native.register_sig("dl4j_reduce", [c_int, c_int, c_void_p, c_void_p, c_void_p, 
                                     c_void_p])
 native.register_sig("dl4j_strided_copy", [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_ll, c_void_p])
+native.register_sig("dl4j_strided_copy2", [c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_ll, c_void_p])
 native.register_sig("dl4j_col2im", [c_int, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
 native.register_sig("dl4j_mergemax", [c_int, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_void_p])
 native.register_sig("dl4j_mergemax_bp", [c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p])
@@ -238,6 +240,25 @@ def materialize(v):
     if not ok(v) or v.dim() > 8 or v.dim() == 0:
         return None
     return _copy(v, v.shape, v.stride(), v.storage_offset(), v.dtype)
+
+
+def cast_pad_last(v, dtype, K8, out=None):
+    """Contiguous ``dtype`` copy of the strided view ``v`` (any strides, any kernel dtype) with its last dimension
+    zero-padded from K to ``K8`` — permute + cast + pad of a GEMM operand in ONE launch (dl4j_strided_copy2).
+    ``out``: optional contiguous destination of that shape (e.g. from the open arena)."""
+    if not ok(v) or dtype not in DT or v.dim() > 8 or v.dim() == 0:
+        return None
+    shape = tuple(v.shape[:-1]) + (K8,)
+    y = out if out is not None else torch.empty(shape, dtype=dtype, device=v.device)
+    if y.numel() == 0:
+        return y
+    lim = [0] * (v.dim() - 1) + [v.shape[-1]]
+    rc = native.load().dl4j_strided_copy2(DT[v.dtype], DT[dtype], ctypes.c_void_p(v.untyped_storage().data_ptr()),
+                                          _ptr(y), v.dim(), _arr(shape), _arr(v.stride()), None, _arr(lim),
+                                          int(v.storage_offset()), _stream())
+    _check(rc, "strided_copy2")
+    CALLS["cast_pad_last"] += 1
+    return y
 
 
 def pad2d(x, pads):

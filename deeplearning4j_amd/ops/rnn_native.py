@@ -15,10 +15,9 @@ from . import native
 from ..memory import arena
 from .native import _check, _ptr, _stream, c_int, c_void_p
 
-_SIG_FWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-            c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
-_SIG_BWD = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-            c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]
+_SIG_FWD = [c_int] + [c_void_p] * 12 + [c_int, c_int, c_int, c_void_p]
+_SIG_BWD = [c_int, c_void_p, c_int] + [c_void_p] * 11 + [c_int, c_int, c_int, c_int, c_void_p]
+_SIG_PACK = [c_int, c_void_p, ctypes.c_longlong, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p]
 
 
 _DTC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -48,7 +47,45 @@ def _f32c(t):
     return None if t is None else t.detach().to(torch.float32).contiguous()
 
 
-_SIG_COOP = [c_void_p] * 13 + [c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
+def _eps_arg(t):
+    """(tensor, dtype code) for the backward kernels' eps operand: fp32 / bf16 / fp16 are read as they are."""
+    t = t.detach()
+    if t.dtype not in _DTC:
+        t = t.to(torch.float32)
+    return t.contiguous(), _DTC[t.dtype]
+
+
+class RWPacks:
+    """The sequence kernels' packed recurrent weights for one layer and one weight version (one TBPTT window):
+    forward B = RWᵀ, backward B = RW, fp32 peepholes [3, H] — built by ONE launch (csrc/lstm_glue.hip
+    lstm_pack_rw_kernel) in the forward pass and reused by the backward pass."""
+    __slots__ = ("fwd", "bwd", "peep", "H", "dtype")
+
+    def __init__(self, fwd, bwd, peep, H, dtype):
+        self.fwd, self.bwd, self.peep, self.H, self.dtype = fwd, bwd, peep, H, dtype
+
+
+def pack_rw(RW, H, peephole, need_bwd=True):
+    """RWPacks for the [H, 4H(+3)] weight view, or None when the kernels do not take this dtype/H."""
+    dt = RW.dtype
+    if not RW.is_cuda or not supported(H, dt) or RW.dim() != 2 or RW.shape[0] != H:
+        return None
+    lib = native.load()
+    native.register_sig("dl4j_lstm_pack_rw", _SIG_PACK)
+    fe = 8 if dt in (torch.bfloat16, torch.float16) else 4
+    shape = lambda n, k: (n // 16, k // (4 * fe), 4, 16, fe)  # noqa: E731
+    fwd = arena.empty(shape(4 * H, H), dt, RW.device)
+    bwd = arena.empty(shape(H, 4 * H), dt, RW.device) if need_bwd else None
+    peep = arena.empty((3, H), torch.float32, RW.device) if peephole else None
+    rc = lib.dl4j_lstm_pack_rw(_DTC[dt], _ptr(RW), RW.stride(0), RW.stride(1), H, _ptr(fwd), _ptr(bwd), _ptr(peep),
+                               _stream())
+    if rc == -1:
+        return None
+    _check(rc, "lstm_pack_rw")
+    return RWPacks(fwd, bwd, peep, H, dt)
+
+
+_SIG_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
 
 
 class _CoopBuf:
@@ -132,15 +169,15 @@ def _coop_enabled():
     return os.environ.get("DL4J_AMD_LSTM_COOP", "1") == "1"
 
 
-def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
+def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, out16, gates, call, hT, cT, T, mb, H):
     """Cooperative multi-workgroup kernel (csrc/lstm_coop.hip, RW resident in LDS); False if it does not apply."""
     native.register_sig("dl4j_lstm_fwd_coop", _SIG_COOP)
     native.register_sig("dl4j_lstm_coop_exch_bytes", [c_int, c_int])
     lib.dl4j_lstm_coop_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_exch_bytes(mb, H)
     b, base, reset = _coop_buf("fwd", nbytes, zx.device, T)
-    rc = lib.dl4j_lstm_fwd_coop(_ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c), _ptr(m), _ptr(out), _ptr(gates),
-                                _ptr(call), _ptr(hT), _ptr(cT), _ptr(b.exch), _ptr(b.err), T, mb, H, base, reset,
+    rc = lib.dl4j_lstm_fwd_coop(_ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c), _ptr(m), _ptr(out),
+                                _ptr(out16), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), _ptr(b.exch), _ptr(b.err), T, mb, H, base, reset,
                                 c_void_p(_stream()))
     if rc != 0:
         b.next_tag = None
@@ -153,17 +190,17 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, 
 
 last_coop_err = None
 
-_SIG_BWD_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
+_SIG_BWD_COOP = [c_void_p, c_int] + [c_void_p] * 13 + [c_int, c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
 
 
-def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, mb, H, t_end):
+def _bwd_coop(lib, e, edt, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, mb, H, t_end):
     """Cooperative backward (csrc/lstm_coop.hip: K-split partial dh exchange, RW slice resident in LDS)."""
     native.register_sig("dl4j_lstm_bwd_coop", _SIG_BWD_COOP)
     native.register_sig("dl4j_lstm_coop_bwd_exch_bytes", [c_int, c_int])
     lib.dl4j_lstm_coop_bwd_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_bwd_exch_bytes(mb, H)
     b, base, reset = _coop_buf("bwd", nbytes, e.device, T)
-    rc = lib.dl4j_lstm_bwd_coop(_ptr(e), _ptr(gates), _ptr(call), _ptr(c0c), _ptr(rw), _ptr(peep), _ptr(m), _ptr(dhl),
+    rc = lib.dl4j_lstm_bwd_coop(_ptr(e), edt, _ptr(gates), _ptr(call), _ptr(c0c), _ptr(rw), _ptr(peep), _ptr(m), _ptr(dhl),
                                 _ptr(dcl), _ptr(dz), _ptr(dh0), _ptr(dc0), _ptr(b.exch), _ptr(b.err), T, mb, H,
                                 int(t_end), base, reset, c_void_p(_stream()))
     if rc != 0:
@@ -178,9 +215,10 @@ def _bwd_coop(lib, e, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0, T, 
 last_coop_bwd_err = None
 
 
-def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=True):
-    """zx: [T, mb, 4H] (compute dtype, = x·W + b); RW: [H, 4H(+3)] view.
-    Returns (out [T, mb, H] fp32, hT, cT, gates [T,mb,4H] fp32 | None, call [T,mb,H] fp32 | None) or None."""
+def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=True, packs=None, out16=False):
+    """zx: [T, mb, 4H] (compute dtype, = x·W + b); RW: [H, 4H(+3)] view; packs: RWPacks of RW (else packed here).
+    Returns (out [T, mb, H] fp32, hT, cT, gates [T,mb,4H] fp32 | None, call [T,mb,H] fp32 | None, out16) or None;
+    out16 (with ``out16=True``) is h in the compute dtype, written by the same kernel (the next layer's input)."""
     T, mb, H4 = zx.shape
     dt = zx.dtype
     if H4 != 4 * H or not supported(H, dt) or T < 1 or mb < 1:
@@ -189,8 +227,11 @@ def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=Tr
     native.register_sig("dl4j_lstm_fwd", _SIG_FWD)
     dev = zx.device
     zx = zx.contiguous()
-    rwt = _pack_b(RW[:, :4 * H].t(), dt)                             # B[k][n] = RW[k][n], n over 4H
-    peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
+    if packs is not None and packs.dtype == dt and packs.H == H:
+        rwt, peep = packs.fwd, packs.peep
+    else:
+        rwt = _pack_b(RW[:, :4 * H].t(), dt)                         # B[k][n] = RW[k][n], n over 4H
+        peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
     h0c, c0c = _f32c(h0), _f32c(c0)
     m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
     if m is not None and m.shape[1] != T:
@@ -198,23 +239,25 @@ def lstm_seq_fwd(zx, RW, H, peephole, h0=None, c0=None, mask=None, need_cache=Tr
     # per-call working memory (outputs, gate / cell caches for backward) from the open training / TBPTT arena
     # (memory/arena.py: the reference's LOOP_LSTM working memory); the carried state hT / cT is not carved
     out = arena.empty((T, mb, H), torch.float32, dev)
+    o16 = arena.empty((T, mb, H), dt, dev) if out16 and dt != torch.float32 else None
     hT = torch.empty(mb, H, device=dev, dtype=torch.float32)
     cT = torch.empty(mb, H, device=dev, dtype=torch.float32)
     gates = arena.empty((T, mb, 4 * H), torch.float32, dev) if need_cache else None
     call = arena.empty((T, mb, H), torch.float32, dev) if need_cache else None
     if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
-            _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, gates, call, hT, cT, T, mb, H):
-        return out, hT, cT, gates, call
+            _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, o16, gates, call, hT, cT, T, mb, H):
+        return out, hT, cT, gates, call, o16
     rc = lib.dl4j_lstm_fwd(_DTC.get(dt, 0), _ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c),
-                           _ptr(m), _ptr(out), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), T, mb, H,
+                           _ptr(m), _ptr(out), _ptr(o16), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), T, mb, H,
                            c_void_p(_stream()))
     if rc == -1:
         return None
     _check(rc, "lstm_fwd")
-    return out, hT, cT, gates, call
+    return out, hT, cT, gates, call, o16
 
 
-def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=None, dc_last=None, t_end=0):
+def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=None, dc_last=None, t_end=0,
+                 packs=None):
     """eps_tmh: [T, mb, H] (any float dtype). Returns (dz [T, mb, 4H] fp32, dh0, dc0) or None."""
     T, mb, _ = eps_tmh.shape
     dt = RW.dtype
@@ -223,9 +266,12 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
     lib = native.load()
     native.register_sig("dl4j_lstm_bwd", _SIG_BWD)
     dev = eps_tmh.device
-    e = _f32c(eps_tmh)
-    rw = _pack_b(RW[:, :4 * H], dt)                                   # dh = dz·RWᵀ: B[k][n] = RW[n][k], k over 4H
-    peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
+    e, edt = _eps_arg(eps_tmh)
+    if packs is not None and packs.bwd is not None and packs.dtype == dt and packs.H == H:
+        rw, peep = packs.bwd, packs.peep
+    else:
+        rw = _pack_b(RW[:, :4 * H], dt)                               # dh = dz·RWᵀ: B[k][n] = RW[n][k], k over 4H
+        peep = RW[:, 4 * H:4 * H + 3].t().to(torch.float32).contiguous() if peephole else None
     m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
     dz = arena.empty((T, mb, 4 * H), torch.float32, dev)
     if t_end > 0:
@@ -233,10 +279,10 @@ def lstm_seq_bwd(eps_tmh, gates, call, c0, RW, H, peephole, mask=None, dh_last=N
     dh0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
     dc0 = torch.empty(mb, H, device=dev, dtype=torch.float32)
     if dt == torch.bfloat16 and H in (256, 512) and _coop_enabled() and \
-            _bwd_coop(lib, e, gates, call, _f32c(c0), rw, peep, m, _f32c(dh_last), _f32c(dc_last), dz, dh0, dc0, T, mb,
+            _bwd_coop(lib, e, edt, gates, call, _f32c(c0), rw, peep, m, _f32c(dh_last), _f32c(dc_last), dz, dh0, dc0, T, mb,
                       H, t_end):
         return dz, dh0, dc0
-    rc = lib.dl4j_lstm_bwd(_DTC.get(dt, 0), _ptr(e), _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
+    rc = lib.dl4j_lstm_bwd(_DTC.get(dt, 0), _ptr(e), edt, _ptr(gates), _ptr(call), _ptr(_f32c(c0)),
                            _ptr(rw), _ptr(peep), _ptr(m), _ptr(_f32c(dh_last)), _ptr(_f32c(dc_last)), _ptr(dz),
                            _ptr(dh0), _ptr(dc0), T, mb, H, int(t_end), c_void_p(_stream()))
     if rc == -1:

@@ -464,7 +464,7 @@ def _lstm_fwd(ins, at):
     zx = mmul(xt, W, bias=b.reshape(-1)).reshape(T, mb, 4 * H)
     from ..ops import rnn_native
     if x.is_cuda and rnn_native.supported(H, dt) and ops.use_native(x, "lstm"):
-        out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True)
+        out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True)[:5]
         return out.permute(1, 2, 0).to(x.dtype), ("native", xt, zx, out, gates, call)
     cd = torch.float64 if dt == torch.float64 else torch.float32
     h = torch.zeros(mb, H, dtype=cd, device=x.device) if h0 is None else h0.to(cd)

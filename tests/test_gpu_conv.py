@@ -167,9 +167,11 @@ def test_conv_bwd_data_accumulates_in_place(cuda, case):
     _close(dx, other.float() + dx_ref.float(), 2e-2)
 
 
-def test_conv_epilogue_bn_stats_match_separate_pass(cuda, monkeypatch):
+@pytest.mark.parametrize("batch", [16, 400])
+def test_conv_epilogue_bn_stats_match_separate_pass(cuda, monkeypatch, batch):
     """Conv -> BN (training): statistics from the conv kernel epilogue give the same BN forward / running stats /
-    update as the separate statistics pass (DL4J_AMD_CONV_BN_STATS=0)."""
+    update as the separate statistics pass (DL4J_AMD_CONV_BN_STATS=0). batch 16: <= 64 folded tile rows (one fused
+    fold+finalize launch); batch 400: 2500 tile partials (tile re-centring pass, then the ticketed fold)."""
     from deeplearning4j_amd import (Activation, ActivationLayer, BatchNormalization, ComputationGraph, ConvolutionLayer,
                                     DataType, GlobalPoolingLayer, InputType, LossFunction, NeuralNetConfiguration,
                                     OutputLayer, PoolingType, Sgd)
@@ -189,8 +191,8 @@ def test_conv_epilogue_bn_stats_match_separate_pass(cuda, monkeypatch):
         return n
 
     gen = torch.Generator().manual_seed(1)
-    x = (torch.randn(16, 64, 20, 20, generator=gen) + 0.7).to(cuda)
-    y = torch.nn.functional.one_hot(torch.randint(0, 5, (16,), generator=gen), 5).float().to(cuda)
+    x = (torch.randn(batch, 64, 20, 20, generator=gen) + 0.7).to(cuda)
+    y = torch.nn.functional.one_hot(torch.randint(0, 5, (batch,), generator=gen), 5).float().to(cuda)
     res = []
     for flag in ("1", "0"):
         monkeypatch.setenv("DL4J_AMD_CONV_BN_STATS", flag)

@@ -28,7 +28,9 @@ def test_native_library_loaded(cuda):
 @pytest.mark.parametrize("shape", [(4, 64, 9, 7), (2, 256, 5, 5), (3, 2048, 2, 2), (16, 24),
                                    # grid-capped sizes: several grid-stride steps (register-resident factors,
                                    # two vectors per step + tail) and an odd channel-group count (factors reloaded)
-                                   (200, 64, 32, 32), (500000, 24)])
+                                   (200, 64, 32, 32), (500000, 24),
+                                   # several channel columns x several folded partial rows: ticketed fold
+                                   (64, 256, 16, 16)])
 def test_batchnorm_fwd_bwd(cuda, dtype, relu, shape):
     g = torch.Generator().manual_seed(0)
     x = (torch.randn(*shape, generator=g) * 3 + 1.5)
@@ -276,3 +278,25 @@ def test_wrw_overlap_stream_matches_inline(cuda, monkeypatch):
     for g1 in grads["1"]:
         d = (g0 - g1).abs().max().item()
         assert d <= 2e-3 * scale + 1e-5, (d, scale)
+
+
+def test_batchnorm_fold_ticket_reuse(cuda):
+    """The fused fold+finalize draws its ticket counters round-robin from a fixed device array and the reducing block
+    resets them: 600 launches (slots reused twice) must give bitwise the same statistics and gradients."""
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(64, 256, 16, 16, generator=g) + 0.3).to(torch.bfloat16).to(cuda)
+    x = x.contiguous(memory_format=torch.channels_last)
+    r = torch.randn(64, 256, 16, 16, generator=g).to(torch.bfloat16).to(cuda).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(64, 256, 16, 16, generator=g).to(torch.bfloat16).to(cuda).contiguous(memory_format=torch.channels_last)
+    gamma, beta = torch.rand(256, device=cuda) + 0.5, torch.randn(256, device=cuda)
+    first = None
+    for _ in range(300):
+        y, c = ops.bn_forward(x, gamma, beta, torch.zeros(256, device=cuda), torch.ones(256, device=cuda), True, 0.9,
+                              1e-5, residual=r)
+        dx, dgm, dbt, dr = ops.bn_backward(dy, c)
+        cur = (y, dx, dgm, dbt, dr)
+        if first is None:
+            first = [t.clone() for t in cur]
+        else:
+            for a, b in zip(first, cur):
+                assert torch.equal(a, b)

@@ -117,12 +117,16 @@ def test_lstm_coop_kernel_matches_single_workgroup_kernel(cuda, monkeypatch, H, 
     for flag in ("1", "0"):
         monkeypatch.setenv("DL4J_AMD_LSTM_COOP", flag)
         rnn_native.last_coop_err = None
-        res[flag] = rnn_native.lstm_seq_fwd(zx, RW, H, peep, h0, c0, mask, True)
+        # cooperative run: weights packed by the one-launch pack kernel, bf16 copy of h written by the kernel
+        packs = rnn_native.pack_rw(RW, H, peep) if flag == "1" else None
+        res[flag] = rnn_native.lstm_seq_fwd(zx, RW, H, peep, h0, c0, mask, True, packs=packs, out16=flag == "1")
         if flag == "1":
             assert rnn_native.last_coop_err is not None, "cooperative kernel did not run"
             assert int(rnn_native.last_coop_err.item()) == 0, "hand-off wait timed out"
-    for a, b in zip(res["1"], res["0"]):
+    for a, b in zip(res["1"][:5], res["0"][:5]):
         _close(a, b, 1e-5)
+    assert res["0"][5] is None
+    assert torch.equal(res["1"][5], res["1"][0].to(torch.bfloat16))
 
 
 @pytest.mark.parametrize("H,mb,peep,t_end", [(256, 32, True, 0), (256, 37, False, 5), (512, 20, True, 0)])
@@ -138,7 +142,7 @@ def test_lstm_coop_bwd_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb,
     c0 = torch.randn(mb, H, generator=g).to(cuda) * 0.3
     mask = (torch.rand(mb, T, generator=g) > 0.1).float().to(cuda)
     monkeypatch.setenv("DL4J_AMD_LSTM_COOP", "0")
-    _, _, _, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peep, None, c0, mask, True)
+    _, _, _, gates, call, _ = rnn_native.lstm_seq_fwd(zx, RW, H, peep, None, c0, mask, True)
     eps = torch.randn(T, mb, H, generator=g).to(cuda)
     dhl = torch.randn(mb, H, generator=g).to(cuda) * 0.2
     dcl = torch.randn(mb, H, generator=g).to(cuda) * 0.2
@@ -146,7 +150,10 @@ def test_lstm_coop_bwd_matches_single_workgroup_kernel(cuda, monkeypatch, H, mb,
     for flag in ("1", "0"):
         monkeypatch.setenv("DL4J_AMD_LSTM_COOP", flag)
         rnn_native.last_coop_bwd_err = None
-        res[flag] = rnn_native.lstm_seq_bwd(eps, gates, call, c0, RW, H, peep, mask, dhl, dcl, t_end)
+        # cooperative run: packed weights from the pack kernel and bf16 eps read directly by the kernel
+        packs = rnn_native.pack_rw(RW, H, peep) if flag == "1" else None
+        e = eps.to(torch.bfloat16) if flag == "1" else eps.to(torch.bfloat16).float()
+        res[flag] = rnn_native.lstm_seq_bwd(e, gates, call, c0, RW, H, peep, mask, dhl, dcl, t_end, packs=packs)
         if flag == "1":
             assert rnn_native.last_coop_bwd_err is not None, "cooperative backward did not run"
             assert int(rnn_native.last_coop_bwd_err.item()) == 0, "hand-off wait timed out"
@@ -170,3 +177,20 @@ def test_samediff_char_lm_trains_on_gpu(cuda):
     losses = [sd.fit(DataSet(X, Y)) for _ in range(40)]
     assert losses[-1] < 0.7 * losses[0], losses[::10]
     assert sd._train_state["shadow"] is not None            # mixed precision: bf16 compute copy of fp32 masters
+
+
+@pytest.mark.parametrize("dtype,H", [(torch.bfloat16, 256), (torch.float16, 64), (torch.float32, 48)])
+@pytest.mark.parametrize("forder", [False, True])
+def test_lstm_pack_rw_matches_permute_pack(cuda, dtype, H, forder):
+    """One-launch packing kernel == the permute/contiguous packing of rnn_native._pack_b (both images + peepholes),
+    for row-major and DL4J 'f'-ordered weight views."""
+    from deeplearning4j_amd.ops import rnn_native
+    g = torch.Generator().manual_seed(H)
+    RW = torch.randn(H, 4 * H + 3, generator=g).to(dtype).to(cuda)
+    if forder:
+        RW = RW.t().contiguous().t()
+    p = rnn_native.pack_rw(RW, H, True)
+    assert p is not None
+    assert torch.equal(p.fwd, rnn_native._pack_b(RW[:, :4 * H].t(), dtype))
+    assert torch.equal(p.bwd, rnn_native._pack_b(RW[:, :4 * H], dtype))
+    assert torch.equal(p.peep, RW[:, 4 * H:].t().float())

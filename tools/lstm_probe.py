@@ -33,7 +33,7 @@ def main():
                 RW = (torch.randn(H, 4 * H + 3, device=dev) * 0.05).to(torch.bfloat16)
                 us_nc = timeit(lambda: rnn_native.lstm_seq_fwd(zx, RW, H, peep, need_cache=False))
                 us_c = timeit(lambda: rnn_native.lstm_seq_fwd(zx, RW, H, peep, need_cache=True))
-                out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peep, need_cache=True)
+                out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peep, need_cache=True)[:5]
                 eps = torch.randn(T, mb, H, device=dev)
                 us_b = timeit(lambda: rnn_native.lstm_seq_bwd(eps, gates, call, None, RW, H, peep))
                 print(f"H={H:4d} mb={mb:5d} fwd(nocache) {us_nc / T:7.2f} us/step  fwd(cache) {us_c / T:7.2f}  "
