@@ -14,6 +14,7 @@
 // in parallel (bn_reduce_rows), then finalize reduces the rest in double with 4 row-groups x 64 channels per
 // block. The ReLU mask in backward is recomputed from x (and r), so no activation needs to be stored.
 #include "common.h"
+#include <cstdlib>
 
 // --------------------------------------------------------------------------------------------- forward
 template <typename T>
@@ -493,10 +494,35 @@ static unsigned* bn_ticket_slot() {
   return base[dev] + 32 * k;
 }
 
+// DL4J_AMD_BN_FOLD=0: the previous separate launches (bn_reduce_rows + bn_finalize / bn_bwd_finalize) for A/B runs.
+static bool bn_fold_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DL4J_AMD_BN_FOLD");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static inline void bn_reduce_stage(float*& p1, float*& p2, int& nblk, int C, float* q, hipStream_t s);
+
 // Launches bn_fold over `nrows` partial rows; q: >= 2*ceil(nrows/32)*C floats of workspace.
 template <typename T, int SRC, int FIN>
 static int bn_fold_launch(const float* p1, const float* p2, long long nrows, int C, float* q, BnFin f,
                           hipStream_t s) {
+  if (SRC == 0 && !bn_fold_enabled() && nrows <= 0x7fffffff) {
+    float* a = const_cast<float*>(p1);
+    float* b = const_cast<float*>(p2);
+    int n = (int)nrows;
+    bn_reduce_stage(a, b, n, C, q, s);
+    if (FIN == 0)
+      hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, a, b, n, C, f.M, (const T*)f.x, f.gamma,
+                         f.beta, f.gconst, f.bconst, f.run_mean, f.run_var, f.decay, f.eps, 1, f.ctx);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(256), 0, s, a, b, n, C, f.M, f.dbeta, f.dgamma,
+                         f.cdb, f.cdg);
+    return 0;
+  }
   const long long S = (nrows + 31) / 32;
   if (S > 65535) return -1;
   f.ticket = nullptr;
@@ -700,7 +726,7 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
   BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
           nullptr, nullptr, nullptr, nullptr, nullptr, 64};
   int rc;
-  if (S <= 64) {
+  if (S <= 64 && bn_fold_enabled()) {
     // one launch: tile re-centring + fold + finalize
     rc = bn_fold_launch<T, 1, 0>(tstats, nullptr, P, C, ws, f, s);
   } else {

@@ -7,6 +7,7 @@
 // x and r); dgamma/dbeta column sums are accumulated per block in registers and written as per-block partials,
 // reduced by a second small kernel (no atomics: deterministic).
 #include "common.h"
+#include <cstdlib>
 
 template <typename T> struct V8;
 template <> struct V8<bf16> {
@@ -150,27 +151,127 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// Block-partial variant: W waves per block, wave w takes rows r0 + w, r0 + w + W, ... of the block's row range; the
+// W per-wave dgamma/dbeta partials are summed through LDS so each BLOCK writes one [2][N] partial row. With ~512
+// blocks of W = 8 waves every CU holds 16 waves of rows in flight (the per-wave-partial kernel above needs 16 rows
+// per wave to keep its partial buffer small, which left M = 4096 on 64 blocks: 476-700 GB/s).
+// DS: also the column sums of dx (a third partial plane): dx is the gradient of the dense layer that produced x
+// (transformer FFN-2 / attention output), so this is that layer's bias gradient without another pass over dx.
+template <typename T, int CH, bool RES, int W, bool DS>
+__global__ void __launch_bounds__(64 * W) ln_bwd_block(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const T* __restrict__ r, const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean_in,
+                                                       const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                       float* __restrict__ part, long long M, int N, long long rpb) {
+  constexpr int NP = DS ? 3 : 2;
+  extern __shared__ __attribute__((aligned(16))) float lsum[];     // [W][NP][N]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = N >> 3;
+  float dg[CH][8], db[CH][8], g[CH][8], dsum[DS ? CH : 1][8];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[c][k] = db[c][k] = 0.f;
+    if (DS) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dsum[DS ? c : 0][k] = 0.f;
+    }
+    if (ch < nch) Vec8<float>::load(gamma + ch * 8, g[c]);
+  }
+  const long long r0 = (long long)blockIdx.x * rpb;
+  long long r1 = r0 + rpb;
+  if (r1 > M) r1 = M;
+  for (long long row = r0 + wave; row < r1; row += W) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xv[CH][8], dv[CH][8], rv[CH][8];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {                      // all of the row's loads in flight before any use
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        V8<T>::ld(x + row * N + ch * 8, xv[c]);
+        if (RES) V8<T>::ld(r + row * N + ch * 8, rv[c]);
+        V8<T>::ld(dy + row * N + ch * 8, dv[c]);
+      }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      if (lane + c * 64 < nch) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xs = RES ? xv[c][k] + rv[c][k] : xv[c][k];
+          const float xh = (xs - mean) * rstd;
+          const float d = dv[c][k] * g[c][k];
+          xv[c][k] = xh;
+          s1 += d;
+          s2 += d * xh;
+          dg[c][k] += dv[c][k] * xh;
+          db[c][k] += dv[c][k];
+          dv[c][k] = d;
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / N, m2 = wave_sum(s2) / N;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[c][k] - m1 - xv[c][k] * m2);
+        V8<T>::st(dx + row * N + ch * 8, o);
+        if (DS) {
+          // sum what was stored (rounded to T), so the bias gradient matches a column sum of the stored dx
+          V8<T>::ld(dx + row * N + ch * 8, o);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dsum[DS ? c : 0][k] += o[k];
+        }
+      }
+    }
+  }
+  float* mine = lsum + (long long)wave * NP * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      Vec8<float>::store(mine + ch * 8, dg[c]);
+      Vec8<float>::store(mine + N + ch * 8, db[c]);
+      if (DS) Vec8<float>::store(mine + 2 * N + ch * 8, dsum[DS ? c : 0]);
+    }
+  }
+  __syncthreads();
+  float* out = part + (long long)blockIdx.x * NP * N;
+  for (int j = threadIdx.x; j < NP * N; j += 64 * W) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) t += lsum[w * NP * N + j];
+    out[j] = t;
+  }
+}
+
 // out[0/1][N] = sum over P partial rows. Block = 32 columns x 8 row groups (coalesced 128-byte row reads), the 8
 // group sums combined through LDS.
 __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int P, int N,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     float* __restrict__ dsum, int NP) {
   __shared__ float red[8][33];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int j = blockIdx.x * 32 + cl;                          // over the concatenated [dgamma | dbeta] columns
+  const int j = blockIdx.x * 32 + cl;                          // over the concatenated [dgamma | dbeta (| dsum)]
   float s = 0.f;
-  if (j < 2 * N) {
+  if (j < NP * N) {
     const int which = j / N, col = j - which * N;
     const float* src = part + which * N + col;
-    for (int p = rg; p < P; p += 8) s += src[(long long)p * 2 * N];
+    for (int p = rg; p < P; p += 8) s += src[(long long)p * NP * N];
   }
   red[rg][cl] = s;
   __syncthreads();
-  if (rg == 0 && j < 2 * N) {
+  if (rg == 0 && j < NP * N) {
     float t = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) t += red[g][cl];
     const int which = j / N, col = j - which * N;
-    (which == 0 ? dgamma : dbeta)[col] = t;
+    (which == 0 ? dgamma : (which == 1 ? dbeta : dsum))[col] = t;
   }
 }
 
@@ -189,11 +290,67 @@ static int fwd_l(const void* x, const void* r, const float* g, const float* b, v
 
 static constexpr int kRPW = 16;
 
-static long long ln_bwd_partials(long long M) { return ((M + 4 * kRPW - 1) / (4 * kRPW)) * 4; }
+// Block-partial kernel geometry: up to 512 blocks of W waves, at least one row per wave.
+static inline int ln_waves(int N) { return N <= 1024 ? 8 : (N <= 2048 ? 4 : 2); }
+static inline long long ln_blocks(long long M, int N) {
+  const int W = ln_waves(N);
+  long long b = (M + W - 1) / W;
+  return b > 512 ? 512 : (b < 1 ? 1 : b);
+}
+
+static long long ln_bwd_partials(long long M) {
+  const long long old = ((M + 4 * kRPW - 1) / (4 * kRPW)) * 4;
+  const long long blk = M < 512 ? M : 512;                   // the block kernel never needs more rows than this
+  return old > blk ? old : blk;
+}
+
+template <typename T, int CH, bool RES, int W>
+static void bwd_block_launch(const void* dy, const void* x, const void* r, const float* g, const float* mean,
+                             const float* rstd, void* dx, float* part, long long M, int N, long long blocks,
+                             long long rpb, bool ds, hipStream_t s) {
+  const size_t lds = (size_t)W * (ds ? 3 : 2) * N * sizeof(float);
+  if (lds > 64 * 1024) {                                       // > 64 KB of dynamic LDS must be opted into
+    static bool done[2] = {false, false};
+    if (!done[ds ? 1 : 0]) {
+      const void* k = ds ? reinterpret_cast<const void*>(ln_bwd_block<T, CH, RES, W, true>)
+                         : reinterpret_cast<const void*>(ln_bwd_block<T, CH, RES, W, false>);
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      done[ds ? 1 : 0] = true;
+    }
+  }
+  if (ds)
+    hipLaunchKernelGGL((ln_bwd_block<T, CH, RES, W, true>), dim3((unsigned)blocks), dim3(64 * W), lds, s,
+                       (const T*)dy, (const T*)x, (const T*)r, g, mean, rstd, (T*)dx, part, M, N, rpb);
+  else
+    hipLaunchKernelGGL((ln_bwd_block<T, CH, RES, W, false>), dim3((unsigned)blocks), dim3(64 * W), lds, s,
+                       (const T*)dy, (const T*)x, (const T*)r, g, mean, rstd, (T*)dx, part, M, N, rpb);
+}
 
 template <typename T, int CH>
 static int bwd_l(const void* dy, const void* x, const void* r, const float* g, const float* mean, const float* rstd,
-                 void* dx, float* part, float* dgamma, float* dbeta, long long M, int N, hipStream_t s) {
+                 void* dx, float* part, float* dgamma, float* dbeta, float* dsum, long long M, int N, hipStream_t s) {
+  static int mode = -1;                                       // DL4J_AMD_LN_BWD=wave: per-wave-partial kernel (A/B)
+  if (mode < 0) {
+    const char* e = getenv("DL4J_AMD_LN_BWD");
+    mode = (e && e[0] == 'w') ? 0 : 1;
+  }
+  if (mode == 1 || dsum) {
+    const int W = ln_waves(N);
+    const bool ds = dsum != nullptr;
+    const long long blocks = ln_blocks(M, N);
+    const long long rpb = (M + blocks - 1) / blocks;
+#define LNB(RS, WW) bwd_block_launch<T, CH, RS, WW>(dy, x, r, g, mean, rstd, dx, part, M, N, blocks, rpb, ds, s)
+    if (r) {
+      if (W == 8) LNB(true, 8); else if (W == 4) LNB(true, 4); else LNB(true, 2);
+    } else {
+      if (W == 8) LNB(false, 8); else if (W == 4) LNB(false, 4); else LNB(false, 2);
+    }
+#undef LNB
+    const int NP = ds ? 3 : 2;
+    hipLaunchKernelGGL(ln_bwd_reduce, dim3((NP * N + 31) / 32), dim3(256), 0, s, part, (int)blocks, N, dgamma, dbeta,
+                       dsum, NP);
+    return (int)hipGetLastError();
+  }
   const long long blocks = (M + 4 * kRPW - 1) / (4 * kRPW);
   if (r)
     hipLaunchKernelGGL((ln_bwd_kernel<T, CH, true, kRPW>), dim3((unsigned)blocks), dim3(256), 0, s, (const T*)dy,
@@ -202,7 +359,7 @@ static int bwd_l(const void* dy, const void* x, const void* r, const float* g, c
     hipLaunchKernelGGL((ln_bwd_kernel<T, CH, false, kRPW>), dim3((unsigned)blocks), dim3(256), 0, s, (const T*)dy,
                        (const T*)x, (const T*)nullptr, g, mean, rstd, (T*)dx, part, M, N);
   const int P = (int)(blocks * 4);
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * N + 31) / 32), dim3(256), 0, s, part, P, N, dgamma, dbeta);
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * N + 31) / 32), dim3(256), 0, s, part, P, N, dgamma, dbeta, nullptr, 2);
   return (int)hipGetLastError();
 }
 
@@ -226,12 +383,12 @@ DL4J_API int dl4j_ln_fwd(int dtype, const void* x, const void* r, const float* g
   LN_CH_DISPATCH(fwd_l, float, x, r, gamma, beta, y, mean, rstd, M, N, eps, s);
 }
 
-// part: fp32 workspace of dl4j_ln_partial_rows(M) * 2 * N floats.
+// part: fp32 workspace of dl4j_ln_partial_rows(M) * 3 * N floats. dsum (optional, [N] fp32): column sums of dx.
 DL4J_API int dl4j_ln_bwd(int dtype, const void* dy, const void* x, const void* r, const float* gamma,
                          const float* mean, const float* rstd, void* dx, float* part, float* dgamma, float* dbeta,
-                         long long M, int N, hipStream_t s) {
+                         float* dsum, long long M, int N, hipStream_t s) {
   if (N % 8 != 0 || N > 4096 || M < 1) return -1;
-  if (dtype == 1) LN_CH_DISPATCH(bwd_l, bf16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
-  if (dtype == 2) LN_CH_DISPATCH(bwd_l, f16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
-  LN_CH_DISPATCH(bwd_l, float, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, M, N, s);
+  if (dtype == 1) LN_CH_DISPATCH(bwd_l, bf16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, dsum, M, N, s);
+  if (dtype == 2) LN_CH_DISPATCH(bwd_l, f16, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, dsum, M, N, s);
+  LN_CH_DISPATCH(bwd_l, float, dy, x, r, gamma, mean, rstd, dx, part, dgamma, dbeta, dsum, M, N, s);
 }

@@ -82,15 +82,21 @@ def _ln_fwd(x, res, g, b, eps):
     return y.to(x.dtype), ("torch", xhat, rstd)
 
 
-def _ln_bwd(dy, x, res, g, ctx, gview=None, bview=None):
-    """-> ds (gradient of x and of res); dgamma / dbeta land in the gradient views."""
+def _ln_bwd(dy, x, res, g, ctx, gview=None, bview=None, dsum_view=None):
+    """-> ds (gradient of x and of res); dgamma / dbeta land in the gradient views. ``dsum_view``: the producing dense
+    layer's bias-gradient view, filled with the column sums of ds by the LayerNorm backward kernel itself when it
+    can (returns with ``dsum_view`` handled), else by _bsum."""
     if ctx[0] == "native":
         from ...ops import transformer_native as TN
-        ds, dg, db = TN.ln_bwd(dy, x, g, ctx[1], ctx[2], res, gview, bview)
+        dsv = dsum_view.view(-1) if dsum_view is not None and dsum_view.is_contiguous() and \
+            dsum_view.dtype == torch.float32 else None
+        ds, dg, db = TN.ln_bwd(dy, x, g, ctx[1], ctx[2], res, gview, bview, dsv)
         if dg.data_ptr() != gview.data_ptr():
             copy_grad_(gview, dg)
         if db.data_ptr() != bview.data_ptr():
             copy_grad_(bview, db)
+        if dsum_view is not None and dsv is None:
+            _bsum(dsum_view, ds)
         return ds
     _, xhat, rstd = ctx
     d = dy.to(xhat.dtype)
@@ -100,7 +106,10 @@ def _ln_bwd(dy, x, res, g, ctx, gview=None, bview=None):
     ds = rstd * (dxh - dxh.mean(-1, keepdim=True) - xhat * (dxh * xhat).mean(-1, keepdim=True))
     copy_grad_(gview, dg)
     copy_grad_(bview, db)
-    return ds.to(x.dtype)
+    ds = ds.to(x.dtype)
+    if dsum_view is not None:
+        _bsum(dsum_view, ds)
+    return ds
 
 
 # ------------------------------------------------------------------------------------------------ attention
@@ -168,16 +177,14 @@ class TransformerEncoderLayerImpl(LayerImpl):
         g = self.grads
         dt = xt.dtype
         dy = _token_major(eps).to(dt)
-        ds2 = _ln_bwd(dy, f2, h1, self.params["ln2g"], ln2, g["ln2g"], g["ln2b"])
+        ds2 = _ln_bwd(dy, f2, h1, self.params["ln2g"], ln2, g["ln2g"], g["ln2b"], g["b2"])   # + b2 gradient
         _wgrad(g["W2"], f, ds2)
-        _bsum(g["b2"], ds2)
         dz1 = _gelu_bwd(z1, matmul(ds2, self.W("W2").t()))
         _wgrad(g["W1"], h1, dz1)
         _bsum(g["b1"], dz1)
         dh1 = mmul(dz1, self.W("W1").t(), out=ds2, beta=1.0)          # residual gradient summed in place
-        ds1 = _ln_bwd(dh1, a, xt, self.params["ln1g"], ln1, g["ln1g"], g["ln1b"])
+        ds1 = _ln_bwd(dh1, a, xt, self.params["ln1g"], ln1, g["ln1g"], g["ln1b"], g["bo"])   # + bo gradient
         _wgrad(g["Wo"], ctx, ds1)
-        _bsum(g["bo"], ds1)
         dctx = matmul(ds1, self.W("Wo").t())
         dqkv = _attn_bwd(dctx, qkv, B, T, c.nHeads, m, c.causal, actx)
         _wgrad(g["Wqkv"], xt, dqkv)

@@ -14,7 +14,7 @@ _SIGS = {
     "dl4j_ln_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_float,
                     c_void_p],
     "dl4j_ln_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                    c_void_p, c_ll, c_int, c_void_p],
+                    c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "dl4j_ln_partial_rows": [c_ll],
 }
 
@@ -134,14 +134,15 @@ def ln_fwd(x, gamma, beta, eps, residual=None):
     return y, mean, rstd
 
 
-def ln_bwd(dy, x, gamma, mean, rstd, residual=None, dgamma_out=None, dbeta_out=None):
+def ln_bwd(dy, x, gamma, mean, rstd, residual=None, dgamma_out=None, dbeta_out=None, dsum_out=None):
     """-> (dx [M, N] (also the residual's gradient), dgamma [N] fp32, dbeta [N] fp32). ``dgamma_out`` /
-    ``dbeta_out``: contiguous fp32 views (e.g. the flat gradient) the kernel writes directly."""
+    ``dbeta_out``: contiguous fp32 views (e.g. the flat gradient) the kernel writes directly. ``dsum_out``: optional
+    contiguous fp32 [N] view receiving the column sums of dx (the producing dense layer's bias gradient)."""
     N = x.shape[-1]
     M = x.numel() // N
     lib = _lib()
     P = lib.dl4j_ln_partial_rows(M)
-    part = torch.empty(P * 2 * N, device=x.device, dtype=torch.float32)
+    part = torch.empty(P * 3 * N, device=x.device, dtype=torch.float32)
     dx = torch.empty_like(x)
     ok = lambda t: t is not None and t.is_contiguous() and t.dtype == torch.float32 and t.numel() == N  # noqa: E731
     dg = dgamma_out.view(-1) if ok(dgamma_out) else torch.empty(N, device=x.device, dtype=torch.float32)
@@ -149,7 +150,7 @@ def ln_bwd(dy, x, gamma, mean, rstd, residual=None, dgamma_out=None, dbeta_out=N
     g = gamma.reshape(-1).to(torch.float32).contiguous()
     r = None if residual is None else residual.to(x.dtype).contiguous()
     rc = lib.dl4j_ln_bwd(_dt(x), _ptr(dy.to(x.dtype).contiguous()), _ptr(x), _ptr(r), _ptr(g), _ptr(mean), _ptr(rstd),
-                         _ptr(dx), _ptr(part), _ptr(dg), _ptr(db), M, N, c_void_p(_stream()))
+                         _ptr(dx), _ptr(part), _ptr(dg), _ptr(db), _ptr(dsum_out), M, N, c_void_p(_stream()))
     if rc == -1:
         return None
     _check(rc, "ln_bwd")

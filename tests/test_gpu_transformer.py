@@ -43,7 +43,7 @@ def test_attention_fwd_bwd_matches_reference(cuda, B, T, H, D, masked, causal, d
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2), (torch.float16, 4e-3)])
-@pytest.mark.parametrize("M,N", [(5, 64), (1000, 768), (37, 1032), (64, 4096)])
+@pytest.mark.parametrize("M,N", [(5, 64), (1000, 768), (37, 1032), (64, 4096), (4096, 768), (5000, 768)])
 @pytest.mark.parametrize("res", [False, True])
 def test_layernorm_fwd_bwd_matches_reference(cuda, dtype, tol, M, N, res):
     g = torch.Generator().manual_seed(M + N)
@@ -66,6 +66,12 @@ def test_layernorm_fwd_bwd_matches_reference(cuda, dtype, tol, M, N, res):
         assert _err(dx, rr.grad) < tol * 8
     assert _err(dg, gr.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
     assert _err(db, br.grad) < tol * 8 * (1 if dtype == torch.float32 else 4)
+    # the dx column sums (the producing dense layer's bias gradient) from the same launch
+    dsum = torch.full((N,), float("nan"), device=cuda)
+    dx2, _, _ = TN.ln_bwd(dy.to(cuda), x.to(cuda), gamma.to(cuda), mean, rstd, r.to(cuda) if res else None,
+                          dsum_out=dsum)
+    assert torch.equal(dx2, dx)
+    assert _err(dsum, dx.float().sum(0)) < 1e-4
 
 
 def test_bert_block_gpu_bf16_matches_cpu_fp32(cuda):
