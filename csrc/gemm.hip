@@ -578,11 +578,15 @@ __global__ __launch_bounds__(256) void gemm_simple(GemmArgs g, SimpleArgs s) {
     else if (g.bias_mode == 2) x += g.bias[m];
     const long long o = (long long)m * g.ldc + n;
     if (g.beta != 0.f) x += g.beta * ld_out(C, g.out_dt, o);
-    if (Zp) {
-      if (g.out_dt == 0) reinterpret_cast<float*>(Zp)[o] = x;
-      else reinterpret_cast<u16*>(Zp)[o] = to16(x, g.out_dt);
+    if (g.act == kActDGelu) {
+      if (Zp) x *= dgelu(ld_out(Zp, g.out_dt, o));
+    } else {
+      if (Zp) {
+        if (g.out_dt == 0) reinterpret_cast<float*>(Zp)[o] = x;
+        else reinterpret_cast<u16*>(Zp)[o] = to16(x, g.out_dt);
+      }
+      x = apply_act(x, g.act);
     }
-    x = apply_act(x, g.act);
     if (g.out_dt == 0) reinterpret_cast<float*>(C)[o] = x;
     else reinterpret_cast<u16*>(C)[o] = to16(x, g.out_dt);
   }

@@ -9,9 +9,9 @@
 // own flag (guide Guideline 16, R2), so there is no separate flag, fence or barrier between workgroups. Consumers
 // sweep the granules of h_{t-1} with agent-scope atomic loads until every tag matches; every spin is bounded by the
 // wall clock (a timeout sets *err and the kernel runs to completion instead of hanging). The exchange buffer is
-// double-buffered by step parity. Tags are tag_base + step + 1: the host keeps one persistent buffer and advances
-// tag_base past every launch's tags, so stale granules never match and no per-launch memset is needed (it zeroes
-// the buffer only on first use, on tag wrap-around, and under HIP-graph capture, where every replay reuses tags).
+// double-buffered by step parity. Tags are tag_base + step + 1 over one persistent buffer; the base lives on the
+// device and the last workgroup of each launch advances it (coop_tag_end), so stale granules never match and no
+// per-launch memset is needed, eager or inside a replayed HIP graph (the host zeroes the buffer on first use only).
 //
 // The grid (G x tiles workgroups, one per CU: LDS-bound, at most CUs - 8 of them) is launched stream-ordered (see
 // coop_launch); shapes that do not fit fall back to csrc/lstm.hip.
@@ -48,6 +48,41 @@ static hipError_t coop_launch(const void* k, dim3 grid, dim3 block, void** args,
   return hipLaunchKernel(k, grid, block, args, lds, s);
 }
 
+// Device-side tag bookkeeping (tag argument == kDevTag): err[1] holds the tag base of the next launch and err[2]
+// counts finished workgroups. Every workgroup reads the base at entry; the LAST workgroup to finish (all others have
+// read it by then: no workgroup finishes before the launch's final exchange, and the counter spans every tile)
+// advances it past this launch's tags. Stream-ordered launches therefore never reuse a tag and need no per-launch
+// memset, eager or replayed inside a HIP graph. Before the 32-bit tags wrap, that last workgroup zeroes the exchange
+// buffer and restarts at 0 (zeroed granules carry tag 0, which never matches: tags start at base + 1).
+constexpr unsigned kDevTag = 0xFFFFFFFFu;
+
+__device__ __forceinline__ unsigned coop_tag_begin(gu32* err, unsigned tag_arg) {
+  return tag_arg == kDevTag ? __hip_atomic_load(err + 1, RLX_AGENT) : tag_arg;
+}
+
+// Called by every thread of the workgroup after its last exchange access; flag: any 4-byte LDS word.
+__device__ __forceinline__ void coop_tag_end(gu32* err, gu64* exch, long long exch_words, unsigned tag_arg,
+                                             unsigned base, unsigned used, unsigned* flag) {
+  if (tag_arg != kDevTag) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nwg = gridDim.x * gridDim.y;
+    const unsigned done = __hip_atomic_fetch_add(err + 2, 1u, RLX_AGENT);
+    *flag = done == nwg - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0u) return;
+  unsigned next = base + used;
+  if (next >= 0xF0000000u) {
+    for (long long i = threadIdx.x; i < exch_words; i += blockDim.x) __hip_atomic_store(exch + i, 0ull, RLX_AGENT);
+    next = 0;
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(err + 2, 0u, RLX_AGENT);
+    __hip_atomic_store(err + 1, next, RLX_AGENT);
+  }
+}
+
 // U = hidden units per workgroup (16 per wave); KS = H / 32 k-steps
 template <int U, bool PEEP>
 __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
@@ -55,7 +90,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
     const float* __restrict__ h0, const float* __restrict__ c0, const float* __restrict__ mask,
     float* __restrict__ out, __bf16* __restrict__ out16, float* __restrict__ gates, float* __restrict__ call,
     float* __restrict__ hT, float* __restrict__ cT, unsigned long long* exch_raw, unsigned* err_raw, int Tn, int mb,
-    int H, long long timeout_ticks, unsigned tag_base) {
+    int H, long long timeout_ticks, unsigned tag_arg, long long exch_words) {
   constexpr int NW = U / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int KS = H / 32, H16 = H / 16, H4 = 4 * H;
@@ -65,6 +100,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
   const int ldh = H + 8;
   gu64* exch = (gu64*)exch_raw;
   gu32* err = (gu32*)err_raw;
+  const unsigned tag_base = coop_tag_begin(err, tag_arg);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
   const int grp = blockIdx.x, tile = blockIdx.y, G = gridDim.x;
   const int m0 = tile * 16;
@@ -215,6 +251,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
       if (hT) hT[(long long)m * H + j] = out[((long long)(Tn - 1) * mb + m) * H + j];
     }
   }
+  coop_tag_end(err, exch, exch_words, tag_arg, tag_base, (unsigned)Tn + 2u, reinterpret_cast<unsigned*>(smem));
   (void)G;
 }
 
@@ -242,11 +279,12 @@ static int coop_fwd_launch(const void* zx, const void* rwt, const float* peep, c
   (void)per;
   const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * 16 * (H / 2) * 8;
   if (reset && hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
-  if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(err, 0, 16, s) != hipSuccess) return -1;
   long long timeout = 200LL * 1000 * 1000;                  // wall_clock64 runs at 100 MHz: 2 s per wait
+  long long exch_words = (long long)(exch_bytes / 8);
   void* args[] = {(void*)&zx, (void*)&rwt, (void*)&peep, (void*)&h0, (void*)&c0, (void*)&mask, (void*)&out,
                   (void*)&out16, (void*)&gates, (void*)&call, (void*)&hT, (void*)&cT, (void*)&exch, (void*)&err, (void*)&Tn,
-                  (void*)&mb, (void*)&H, (void*)&timeout, (void*)&tag_base};
+                  (void*)&mb, (void*)&H, (void*)&timeout, (void*)&tag_base, (void*)&exch_words};
   const hipError_t e = coop_launch(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -271,7 +309,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
     const float* __restrict__ c0, const __bf16* __restrict__ rw, const float* __restrict__ peep,
     const float* __restrict__ mask, const float* __restrict__ dh_last, const float* __restrict__ dc_last,
     float* __restrict__ dz, float* __restrict__ dh0, float* __restrict__ dc0, unsigned long long* exch_raw,
-    unsigned* err_raw, int Tn, int mb, int t_end, long long timeout_ticks, unsigned tag_base) {
+    unsigned* err_raw, int Tn, int mb, int t_end, long long timeout_ticks, unsigned tag_arg, long long exch_words) {
   constexpr int NW = U / 16, G = H / U, NTW = (H / 16) / NW, KL = 4 * U / 32, KSG = 4 * H / 32, LDZ = 4 * U + 8;
   constexpr int NE = 4 * G, BATCH = NE < 16 ? NE : 16;     // partial granules gathered per lane per step
   constexpr int H4 = 4 * H;
@@ -280,6 +318,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
   __bf16* zbuf = reinterpret_cast<__bf16*>(smem + (size_t)(H / 16) * KL * 64 * 16);   // [2][16][LDZ]
   gu64* exch = (gu64*)exch_raw;
   gu32* err = (gu32*)err_raw;
+  const unsigned tag_base = coop_tag_begin(err, tag_arg);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
   const int grp = blockIdx.x, tile = blockIdx.y;
   const int m0 = tile * 16, u0 = grp * U;
@@ -432,6 +471,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
       if (dc0) dc0[(long long)m * H + j] = dcn[r];
     }
   }
+  coop_tag_end(err, exch, exch_words, tag_arg, tag_base, (unsigned)Tn + 2u, reinterpret_cast<unsigned*>(smem));
 }
 
 template <int U, int H, bool PEEP>
@@ -454,12 +494,13 @@ static int coop_bwd_launch(const void* eps, int eps_dt, const float* gates, cons
   if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;    // one workgroup per CU, with margin
   const size_t exch_bytes = (size_t)((mb + 15) / 16) * 2 * (H / U) * 16 * H * 8;
   if (reset && hipMemsetAsync(exch, 0, exch_bytes, s) != hipSuccess) return -1;
-  if (reset && hipMemsetAsync(err, 0, 4, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(err, 0, 16, s) != hipSuccess) return -1;
+  long long exch_words = (long long)(exch_bytes / 8);
   long long timeout = 200LL * 1000 * 1000;                  // 2 s per wait at 100 MHz
   const __bf16* rwp = reinterpret_cast<const __bf16*>(rw);
   void* args[] = {(void*)&eps, (void*)&eps_dt, (void*)&gates, (void*)&call, (void*)&c0, (void*)&rwp, (void*)&peep, (void*)&mask,
                   (void*)&dhl, (void*)&dcl, (void*)&dz, (void*)&dh0, (void*)&dc0, (void*)&exch, (void*)&err,
-                  (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout, (void*)&tag_base};
+                  (void*)&Tn, (void*)&mb, (void*)&t_end, (void*)&timeout, (void*)&tag_base, (void*)&exch_words};
   const hipError_t e = coop_launch(reinterpret_cast<const void*>(k), grid, block, args, lds, s);
   if (e != hipSuccess) {
     (void)hipGetLastError();

@@ -97,6 +97,15 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// act 5 (DGELU, backward of exact GELU): v *= gelu'(z) with z READ from the pre-activation buffer Z (same layout as C),
+// so dz = (dy·Wᵀ) * gelu'(z) is one GEMM instead of a GEMM plus an elementwise pass.
+constexpr int kActDGelu = 5;
+__device__ __forceinline__ float dgelu(float z) {
+  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+  const float pdf = __expf(-0.5f * z * z) * 0.39894228040143268f;
+  return cdf + z * pdf;
+}
+
 __device__ __forceinline__ float ld_out(const void* C, int dt, long long i) {
   if (dt == 0) return reinterpret_cast<const float*>(C)[i];
   const u16 u = reinterpret_cast<const u16*>(C)[i];
@@ -121,7 +130,12 @@ __device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int 
     v[j] = x;
   }
   const bool vec = full && ((g.ldc & 3) == 0) && ((n & 3) == 0);
-  if (Z) {
+  if (g.act == kActDGelu) {
+    if (Z)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < g.N) v[j] *= dgelu(ld_out(Z, g.out_dt, base + j));
+  } else if (Z) {
     if (g.out_dt == 0) {
       float* z = reinterpret_cast<float*>(Z) + base;
       if (vec) *reinterpret_cast<float4*>(z) = make_float4(v[0], v[1], v[2], v[3]);
@@ -138,7 +152,7 @@ __device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int 
       }
     }
   }
-  if (g.act)
+  if (g.act && g.act != kActDGelu)
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = apply_act(v[j], g.act);
   if (g.out_dt == 0) {
@@ -191,16 +205,35 @@ __device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, v
     for (int j = 0; j < 8; ++j) v[j] = v[j] * g.alpha + b[j];
     if (g.beta != 0.f)
       for (int j = 0; j < 8; ++j) if (n + j < g.N) v[j] += g.beta * ld_out(o.dst, o.dt, (long long)m * o.ld + n + j);
-    if (Zp)
-      for (int j = 0; j < 8; ++j)
-        if (n + j < g.N) {
-          const long long i = (long long)m * o.ld + n + j;
-          if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
-          else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
-        }
-    if (g.act)
+    if (g.act == kActDGelu) {
+      if (Zp) {
+        const long long i0 = (long long)m * o.ld + n;
+        if (o.vec && n + 8 <= g.N && o.dt != 0) {
+          const uint4 zz = *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(Zp) + i0);
+          const unsigned w[4] = {zz.x, zz.y, zz.z, zz.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
+          for (int j = 0; j < 8; ++j) {
+            const u16 u = (u16)(w[j >> 1] >> (16 * (j & 1)));
+            const float z = o.dt == 1 ? bf2f(u) : __half2float(__ushort_as_half(u));
+            v[j] *= dgelu(z);
+          }
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (n + j < g.N) v[j] *= dgelu(ld_out(Zp, o.dt, i0 + j));
+        }
+      }
+    } else {
+      if (Zp)
+        for (int j = 0; j < 8; ++j)
+          if (n + j < g.N) {
+            const long long i = (long long)m * o.ld + n + j;
+            if (o.dt == 0) reinterpret_cast<float*>(Zp)[i] = v[j];
+            else reinterpret_cast<u16*>(Zp)[i] = to16(v[j], o.dt);
+          }
+      if (g.act)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = apply_act(v[j], g.act);
+    }
   }
   char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
   if (o.vec && n + 8 <= g.N) {

@@ -57,6 +57,14 @@ class LayerImpl:
             p = wn.getParameter(self, key, p, self.iteration, self.epoch, True)
         return p
 
+    def Wbias(self, key="b"):
+        """Bias for a GEMM epilogue: the fp32 master parameter itself when nothing perturbs it (the epilogue adds
+        fp32 bias, so a 16-bit shadow would only cost a conversion launch per call and precision), else W(key)."""
+        p = self.params.get(key)
+        if p is not None and p.dtype == torch.float32 and getattr(self.conf, "weightNoise", None) is None:
+            return p
+        return self.W(key)
+
     def type(self):
         return "FEED_FORWARD"
 

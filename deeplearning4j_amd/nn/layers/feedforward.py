@@ -14,7 +14,7 @@ from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 class DenseLayerImpl(LayerImpl):
     def preOutput(self, x, training=False):
         W = self.W("W")
-        return matmul(x.to(W.dtype), W, bias=self.W("b") if "b" in self.params else None)
+        return matmul(x.to(W.dtype), W, bias=self.Wbias("b") if "b" in self.params else None)
 
     def activate(self, x, training=False, mask=None):
         self.training = training

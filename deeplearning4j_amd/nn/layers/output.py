@@ -51,7 +51,7 @@ class BaseOutputLayerImpl(LayerImpl):
         if not self.has_params:
             return x
         W = self.W("W")
-        return matmul(x.to(W.dtype), W, bias=self.W("b") if "b" in self.params else None)
+        return matmul(x.to(W.dtype), W, bias=self.Wbias("b") if "b" in self.params else None)
 
     # 2d views of input / labels / mask -------------------------------------------------------
     def _in2d(self, x):
@@ -160,7 +160,7 @@ class BaseOutputLayerImpl(LayerImpl):
 
 
 class OutputLayerImpl(BaseOutputLayerImpl):
-    pass
+    GRADS_OVERWRITE = True
 
 
 class LossLayerImpl(BaseOutputLayerImpl):
@@ -168,6 +168,7 @@ class LossLayerImpl(BaseOutputLayerImpl):
 
 
 class RnnOutputLayerImpl(BaseOutputLayerImpl):
+    GRADS_OVERWRITE = True        # weight_grad_ / bias_grad_ write the whole W / b views
     def _in2d(self, x):
         self._mb = x.shape[0]
         return _rnn_to_2d(x) if x.dim() == 3 else x

@@ -269,10 +269,11 @@ class BaseRecurrentImpl(LayerImpl):
 
 class LSTMImpl(BaseRecurrentImpl):
     PEEPHOLE = False
+    GRADS_OVERWRITE = True        # W / RW / b gradient views are written whole every backward (no accumulation)
 
     def _run(self, x, training, h0, c0, need_cache, mask):
         H = self.conf.nOut
-        return _lstm_fwd(x, self.W("W"), self.W("RW"), self.W("b"), h0, c0, H, self.PEEPHOLE, self.conf.activation,
+        return _lstm_fwd(x, self.W("W"), self.W("RW"), self.Wbias("b"), h0, c0, H, self.PEEPHOLE, self.conf.activation,
                          self.conf.gateActivationFn, mask, need_cache)
 
     def activate(self, x, training=False, mask=None, stored_state=False, store_last_for_tbptt=False):

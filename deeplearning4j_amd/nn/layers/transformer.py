@@ -155,14 +155,14 @@ class TransformerEncoderLayerImpl(LayerImpl):
         dt = self.W("Wqkv").dtype
         xt = _token_major(x).to(dt)
         m = mask.reshape(B, T) if mask is not None else None
-        qkv = matmul(xt, self.W("Wqkv"), bias=self.W("bqkv"))
+        qkv = matmul(xt, self.W("Wqkv"), bias=self.Wbias("bqkv"))
         ctx, actx = _attn_fwd(qkv, B, T, H, m, c.causal)
-        a = matmul(ctx, self.W("Wo"), bias=self.W("bo"))
+        a = matmul(ctx, self.W("Wo"), bias=self.Wbias("bo"))
         h1, ln1 = _ln_fwd(a, xt, self.params["ln1g"], self.params["ln1b"], c.layerNormEps)
         # FFN-1 with bias + exact GELU fused into the GEMM epilogue; the pre-activation z1 is kept for backward
         z1 = torch.empty(h1.shape[0], self.W("W1").shape[1], dtype=h1.dtype, device=h1.device)
-        f = matmul(h1, self.W("W1"), bias=self.W("b1"), act="gelu", z=z1)
-        f2 = matmul(f, self.W("W2"), bias=self.W("b2"))
+        f = matmul(h1, self.W("W1"), bias=self.Wbias("b1"), act="gelu", z=z1)
+        f2 = matmul(f, self.W("W2"), bias=self.Wbias("b2"))
         y, ln2 = _ln_fwd(f2, h1, self.params["ln2g"], self.params["ln2b"], c.layerNormEps)
         self.maskArray = mask
         if training:
@@ -179,7 +179,11 @@ class TransformerEncoderLayerImpl(LayerImpl):
         dy = _token_major(eps).to(dt)
         ds2 = _ln_bwd(dy, f2, h1, self.params["ln2g"], ln2, g["ln2g"], g["ln2b"], g["b2"])   # + b2 gradient
         _wgrad(g["W2"], f, ds2)
-        dz1 = _gelu_bwd(z1, matmul(ds2, self.W("W2").t()))
+        if _native(ds2, "gemm") and z1.dtype == ds2.dtype:
+            # GELU backward in the GEMM epilogue: dz1 = (ds2 · W2ᵀ) * gelu'(z1)
+            dz1 = mmul(ds2, self.W("W2").t(), act="dgelu", z=z1)
+        else:
+            dz1 = _gelu_bwd(z1, matmul(ds2, self.W("W2").t()))
         _wgrad(g["W1"], h1, dz1)
         _bsum(g["b1"], dz1)
         dh1 = mmul(dz1, self.W("W1").t(), out=ds2, beta=1.0)          # residual gradient summed in place
@@ -241,7 +245,7 @@ class BertPoolerLayerImpl(LayerImpl):
     def activate(self, x, training=False, mask=None, **kw):
         self.input = x
         x0 = x[:, :, 0].to(self.W("W").dtype)
-        y = matmul(x0, self.W("W"), bias=self.W("b"), act="tanh")
+        y = matmul(x0, self.W("W"), bias=self.Wbias("b"), act="tanh")
         if training:
             self._c = (x0, y, x.shape)
         return y

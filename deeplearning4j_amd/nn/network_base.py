@@ -343,7 +343,8 @@ class BaseNetwork:
     def _begin_backward(self):
         # On the GPU, clear the whole flat gradient with ONE fill so layers whose kernels accumulate (conv
         # weight-gradient atomics, fused bias sums) need no per-layer memset launches.
-        self._grads_zeroed = self.flattenedGradients is not None and self.flattenedGradients.is_cuda
+        self._grads_zeroed = self.flattenedGradients is not None and self.flattenedGradients.is_cuda and \
+            self._grad_zero_needed()
         if self._grads_zeroed:
             self.flattenedGradients.zero_()
         acc = getattr(self, "gradientsAccumulator", None)
@@ -351,6 +352,17 @@ class BaseNetwork:
             acc.begin_backward(self)
         from ..ops import side_stream
         side_stream.begin(self.flattenedGradients)   # conv weight gradients overlap the rest of the reverse pass
+
+    def _grad_zero_needed(self):
+        """False when every layer of an MLN overwrites its whole gradient views (``GRADS_OVERWRITE``), so the
+        per-step fill of the flat gradient is skipped (e.g. LSTM + RNN-output networks)."""
+        v = getattr(self, "_grad_zero_cache", None)
+        if v is None:
+            layers = getattr(self, "layers", None)
+            v = not (isinstance(layers, list) and layers and
+                     all(getattr(l, "GRADS_OVERWRITE", False) or not getattr(l, "grads", None) for l in layers))
+            self._grad_zero_cache = v
+        return v
 
     def _end_backward(self):
         from ..ops import side_stream

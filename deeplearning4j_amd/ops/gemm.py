@@ -24,7 +24,8 @@ from . import fallback
 from .dispatch import use_native
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
-ACT = {None: 0, "identity": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "gelu": 4}
+ACT = {None: 0, "identity": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "gelu": 4,
+       "dgelu": 5}                                      # dgelu: out *= gelu'(z), z READ from the ``z`` buffer
 _c = ctypes
 _sig_done = [False]
 _env = os.environ.get("DL4J_AMD_GEMM_CFG")          # "cfg,splits" override for tuning sweeps
@@ -166,9 +167,12 @@ def _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z):
         r = r + (bias.to(cd).reshape(1, -1) if bias_dim == 1 else bias.to(cd).reshape(-1, 1))
     if beta != 0.0 and out is not None:
         r = r + beta * out.to(cd)
-    if z is not None:
-        z.copy_(r)
-    r = _torch_act(r, act)
+    if act == "dgelu":
+        r = r * _dgelu_ref(z.to(cd)) if z is not None else r
+    else:
+        if z is not None:
+            z.copy_(r)
+        r = _torch_act(r, act)
     if out is not None:
         out.copy_(r)
         return out
@@ -176,6 +180,12 @@ def _torch_mmul(a, b, out, bias, bias_dim, act, alpha, beta, out_dtype, z):
     if arena.current() is not None:
         return arena.empty(r.shape, out_dtype, r.device).copy_(r)
     return r.to(out_dtype)
+
+
+def _dgelu_ref(z):
+    cdf = 0.5 * (1.0 + torch.erf(z * 0.7071067811865476))
+    pdf = torch.exp(-0.5 * z * z) * 0.3989422804014327
+    return cdf + z * pdf
 
 
 def _torch_act(r, act):
@@ -196,7 +206,8 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     """``out = act(alpha * a @ b + bias + beta * out)``; returns ``out`` (allocated row-major when None).
 
     a: [M, K] or [B, M, K]; b: [K, N] or [B, K, N]; bias: [N] (bias_dim=1) or [M] (bias_dim=0);
-    z: optional tensor like ``out`` receiving the pre-activation; out_dtype defaults to a.dtype.
+    z: optional tensor like ``out`` receiving the pre-activation (act="dgelu": the pre-activation that is READ, out =
+    (a @ b) * gelu'(z)); out_dtype defaults to a.dtype.
     stats: optional fp32 [3, P, N] tensor (P = ceil(M/64)) receiving per-64-row BatchNorm partial statistics of the
     bf16 output (conv -> BN fusion; 8-phase kernel).
     """

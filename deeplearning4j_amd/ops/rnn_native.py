@@ -88,14 +88,19 @@ def pack_rw(RW, H, peephole, need_bwd=True):
 _SIG_COOP = [c_void_p] * 14 + [c_int, c_int, c_int, ctypes.c_uint, c_int, c_void_p]
 
 
+_DEV_TAG = 0xFFFFFFFF          # csrc/lstm_coop.hip kDevTag: granule tags tracked on the device (no per-launch memset)
+
+
 class _CoopBuf:
-    """Persistent exchange buffer + error word of the cooperative kernels, and the next unused granule tag.
-    A pinned host copy of the error word is refreshed asynchronously after every eager launch and checked before
-    the next one, so a hand-off timeout surfaces as an exception instead of silently wrong results."""
+    """Persistent exchange buffer + control words of the cooperative kernels: err[0] sticky hand-off timeout flag,
+    err[1] device-side tag base, err[2] finished-workgroup counter. ``next_tag`` is None while the contents are
+    undefined (the next launch zeroes them). A pinned host copy of the error word is refreshed asynchronously after
+    every eager launch and checked before the next one, so a hand-off timeout surfaces as an exception instead of
+    silently wrong results."""
 
     def __init__(self, nbytes, device):
         self.exch = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
-        self.err = torch.empty(1, dtype=torch.int32, device=device)
+        self.err = torch.empty(4, dtype=torch.int32, device=device)
         # pinned host copy, created by the first EAGER launch (pinned allocation is illegal while a stream captures:
         # the capture stream gets a buffer of its own)
         self.err_host = None
@@ -116,11 +121,18 @@ _lock = threading.Lock()
 
 
 def _coop_buf(kind, nbytes, device, steps):
-    """(buffer, tag_base, reset) for one launch that uses ``steps`` + 1 tags. Buffers are per (kind, device, stream)
-    so concurrent ParallelInference workers on one device never share granules; tag allocation is locked."""
+    """(buffer, tag argument, reset) for one launch. Buffers are per (kind, device, stream) so concurrent
+    ParallelInference workers on one device never share granules. Tags live on the device (_DEV_TAG), so only a
+    buffer's first launch zeroes it. A HIP-graph capture reuses an already-initialised buffer of the device's default
+    stream (the stream its replays run on) when one is big enough, so the captured graph holds no memset node."""
     capturing = torch.cuda.is_current_stream_capturing()
     key = (kind, str(device), torch.cuda.current_stream(device).cuda_stream)
     with _lock:
+        if capturing and key not in _coop_bufs:
+            dkey = (kind, str(device), torch.cuda.default_stream(device).cuda_stream)
+            d = _coop_bufs.get(dkey)
+            if d is not None and d.exch.numel() * 8 >= nbytes and d.next_tag is not None:
+                _coop_bufs[key] = d
         b = _coop_bufs.get(key)
         if b is None or b.exch.numel() * 8 < nbytes:
             if b is not None:
@@ -131,16 +143,10 @@ def _coop_buf(kind, nbytes, device, steps):
             b.next_tag = None
             raise CoopTimeoutError(f"cooperative LSTM {kind} kernel: a cross-workgroup hand-off timed out (the "
                                    "workgroups were not co-resident); results of that launch are invalid")
-        if capturing:
-            b.next_tag = None                              # every graph replay reuses the same tags: zero each time
-            return b, 0, 1
-        need = steps + 2
-        if b.next_tag is None or b.next_tag + need >= 0xFFFFFFF0:
-            b.next_tag = need
-            return b, 0, 1
-        base = b.next_tag
-        b.next_tag += need
-        return b, base, 0
+        if b.next_tag is None:                             # contents undefined: this launch zeroes them
+            b.next_tag = 0
+            return b, _DEV_TAG, 1
+        return b, _DEV_TAG, 0
 
 
 def _post_launch(b):
@@ -149,7 +155,7 @@ def _post_launch(b):
         return
     if b.err_host is None:
         b.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-    b.err_host.copy_(b.err, non_blocking=True)
+    b.err_host.copy_(b.err[:1], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
     b.err_ev = ev
@@ -184,7 +190,7 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, out16, gates, call, hT, cT, 
         return False
     _post_launch(b)
     global last_coop_err
-    last_coop_err = b.err                                # device word: 1 = a hand-off wait timed out (sticky)
+    last_coop_err = b.err[:1]                            # device word: 1 = a hand-off wait timed out (sticky)
     return True
 
 
@@ -208,7 +214,7 @@ def _bwd_coop(lib, e, edt, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0
         return False
     _post_launch(b)
     global last_coop_bwd_err
-    last_coop_bwd_err = b.err
+    last_coop_bwd_err = b.err[:1]
     return True
 
 
@@ -307,8 +313,8 @@ def lstm_bwd_prep(dz, out, h0, call, c0, peephole, dtype):
     native.register_sig("dl4j_lstm_bwd_prep", [c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_int, c_void_p])
     dzb = torch.empty(R, G, dtype=dtype, device=dz.device)
     hpb = torch.empty(R, H, dtype=dtype, device=dz.device)
-    db = torch.zeros(G, dtype=torch.float32, device=dz.device)
-    dpeep = torch.zeros(3, H, dtype=torch.float32, device=dz.device)
+    acc = torch.zeros(G + 3 * H, dtype=torch.float32, device=dz.device)   # one fill for both atomic accumulators
+    db, dpeep = acc[:G], acc[G:].view(3, H)
     dzc, oc, cc = dz.contiguous(), out.contiguous(), call.contiguous()
     h0f, c0f = _f32c(h0), _f32c(c0)
     rc = lib.dl4j_lstm_bwd_prep(dt, _ptr(dzc), _ptr(oc), _ptr(h0f), _ptr(cc), _ptr(c0f), _ptr(dzb), _ptr(hpb), _ptr(db),

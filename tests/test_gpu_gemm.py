@@ -197,3 +197,46 @@ def test_bn_stats_epilogue(cfg, monkeypatch):
         assert torch.allclose(ts[2, p], sh, atol=0, rtol=0)
         assert torch.allclose(ts[0, p], (blk - sh).sum(0), atol=1e-2, rtol=1e-4)
         assert torch.allclose(ts[1, p], ((blk - sh) ** 2).sum(0), atol=1e-1, rtol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(4096, 3072, 768), (300, 520, 256), (96, 64, 4096)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_dgelu_epilogue(shape, dt):
+    """act="dgelu": out = (a @ b) * gelu'(z) with the pre-activation z READ in the epilogue (transformer FFN
+    backward); z is left untouched. (96, 64, 4096) takes the split-K reduce epilogue."""
+    torch.manual_seed(5)
+    M, N, K = shape
+    a = torch.randn(M, K, device=DEV).to(dt) * 0.1
+    b = torch.randn(K, N, device=DEV).to(dt) * 0.1
+    z = (torch.randn(M, N, device=DEV) * 2).to(dt)
+    z0 = z.clone()
+    out = gemm.mmul(a, b, act="dgelu", z=z)
+    ref = (a.float() @ b.float()) * gemm._dgelu_ref(z.float())
+    assert torch.equal(z, z0)
+    _check(out, ref, dt, K, f"dgelu {shape}")
+
+
+@pytest.mark.parametrize("K", [77, 13])
+def test_zero_padded_k_operand(K):
+    """kz_view operands: a K-contiguous operand whose columns K..K8-1 are zeros is read in place (no padded copy)
+    with a row-major partner, and the result matches the reference."""
+    torch.manual_seed(6)
+    M, N = 1600, 1024
+    K8 = (K + 7) // 8 * 8
+    buf = torch.zeros(M, K8, device=DEV, dtype=torch.bfloat16)
+    buf[:, :K] = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    a = gemm.kz_view(buf, K)
+    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    calls = []
+    orig = gemm._pad_kc
+    gemm._pad_kc = lambda *args: calls.append(1) or orig(*args)
+    try:
+        out = gemm.mmul(a, b, out_dtype=torch.float32)
+    finally:
+        gemm._pad_kc = orig
+    assert not calls, "the zero-padded operand was copied"
+    _check(out, _ref(a, b), torch.bfloat16, K, f"kz K={K}")
+    # and transposed (M-contiguous) use of the same buffer as the A of a weight gradient
+    g = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    out2 = gemm.mmul(a.t(), g, out_dtype=torch.float32)
+    _check(out2, _ref(a.t(), g), torch.bfloat16, M, f"kz^T K={K}")

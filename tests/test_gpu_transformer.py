@@ -70,7 +70,7 @@ def test_layernorm_fwd_bwd_matches_reference(cuda, dtype, tol, M, N, res):
     dsum = torch.full((N,), float("nan"), device=cuda)
     dx2, _, _ = TN.ln_bwd(dy.to(cuda), x.to(cuda), gamma.to(cuda), mean, rstd, r.to(cuda) if res else None,
                           dsum_out=dsum)
-    assert torch.equal(dx2, dx)
+    assert _err(dx2, dx) < 1e-5   # the two template instances may contract FMAs differently
     assert _err(dsum, dx.float().sum(0)) < 1e-4
 
 
