@@ -276,42 +276,58 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   long long rend = rbeg + rows_per_blk;
   if (rend > M) rend = M;
   if (r0 < R) {
-    constexpr int U = RES ? 3 : 4;     // independent row groups in flight per thread
-    long long r = rbeg + r0;
-    for (; r < rend; r += U * R) {
-      float xv[U][8], gv[U][8], rv[U][8];
-      unsigned mb[U];
-      bool ok[U];
+    // U independent rows per batch; the next batch's loads are issued before the current batch is consumed, so a
+    // thread keeps 2U rows of x / dy in flight across the whole loop (the previous form waited for every batch:
+    // 1.4-2.7 TB/s on the ResNet-50 shapes)
+    constexpr int U = 4;
+    // loads stay packed until consumed (RawVec8): two batches in flight at ~half the registers of unpacked floats
+    struct Batch { RawVec8<T> xv[U], gv[U], rv[RES ? U : 1]; unsigned mb[U]; };
+    auto load = [&](long long r, Batch& b) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long ru = r + u * R;
-        ok[u] = ru < rend;
-        const long long rr = ok[u] ? ru : r;
+        const long long rr = ru < rend ? ru : rbeg + r0;       // clamped: always a valid row of this block
         const long long o = rr * C + cg * 8;
-        Vec8<T>::load(x + o, xv[u]);
-        Vec8<T>::load(dy + o, gv[u]);
+        b.xv[u].load(x + o);
+        b.gv[u].load(dy + o);
         if (RES) {
-          if (mask) mb[u] = mask[rr * T8 + cg];
-          else Vec8<T>::load(res + o, rv[u]);
+          if (mask) b.mb[u] = mask[rr * T8 + cg];
+          else b.rv[RES ? u : 0].load(res + o);
         }
       }
+    };
+    auto consume = [&](long long r, const Batch& b) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (!ok[u]) continue;
+        if (r + u * R >= rend) continue;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          float d = gv[u][i];
+          const float xf = b.xv[u].get(i);
+          float d = b.gv[u].get(i);
           if (RES && mask) {
-            d = (mb[u] >> i) & 1u ? d : 0.f;
+            d = (b.mb[u] >> i) & 1u ? d : 0.f;
           } else if (RELU) {
-            float t = xv[u][i] * sc[i] + sf[i];
-            if (RES) t += rv[u][i];
+            float t = xf * sc[i] + sf[i];
+            if (RES) t += b.rv[RES ? u : 0].get(i);
             d = t > 0.f ? d : 0.f;
           }
           db[i] += d;
-          dg[i] += d * (xv[u][i] - mu[i]) * is[i];
+          dg[i] += d * (xf - mu[i]) * is[i];
         }
       }
+    };
+    long long r = rbeg + r0;
+    Batch b0, b1;
+    if (r < rend) load(r, b0);
+    while (r < rend) {                                  // two batches per trip: b0 / b1 alternate, no copies
+      const long long r1 = r + U * R;
+      if (r1 < rend) load(r1, b1);
+      consume(r, b0);
+      if (r1 >= rend) break;
+      const long long r2 = r1 + U * R;
+      if (r2 < rend) load(r2, b0);
+      consume(r1, b1);
+      r = r2;
     }
   }
   __shared__ float red1[2048];
@@ -348,9 +364,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__
 // ------------------------------------------------------------------------ fused partial fold + finalize
 // One launch replaces bn_reduce_rows + bn_finalize / bn_bwd_finalize: grid (ceil(C/64), S), each block folds 32
 // partial rows of 64 channels (4 row groups x 8 independent loads, same order as bn_reduce_rows) into q; with S > 1
-// the last block of each channel column (agent-scope ticket, release/acquire recipe of the CDNA guide: plain stores,
-// vmcnt drain, lane-0 release fence, relaxed fetch_add; reducer lane-0 acquire fence) sums the S folded rows in
-// double and finalizes. The ticket counters live in a zero-initialised device array, each launch draws a slot
+// the last block of each channel column (agent-scope ticket; the folded rows are stored write-through with agent-scope
+// atomic stores and drained before the relaxed fetch_add, and the reducer reads them with agent-scope atomic loads —
+// the guide's sc1 hand-off form, so no block pays a release fence, i.e. an L2 write-back of everything the previous
+// kernel left dirty) sums the S folded rows in double and finalizes. The ticket counters live in a zero-initialised device array, each launch draws a slot
 // round-robin on the host and the reducer resets its counter, so no per-call memset is needed.
 // SRC 0: p1/p2 are [nrows, C] partial sums about row 0 (bn_stats_partial / bn_bwd_partial).
 // SRC 1: p1 is the conv epilogue's [3][P][C] tile-statistics planes (bn_tiles_reduce's re-centring).
@@ -441,30 +458,34 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
     if (grp == 0 && c < C) bn_fin_store<T, FIN>(c, C, (double)ta, (double)tb, f);
     return;
   }
+  typedef __attribute__((address_space(1))) unsigned gq32;
   if (grp == 0 && c < C) {
-    q1[(long long)blockIdx.y * C + c] = ta;
-    q2[(long long)blockIdx.y * C + c] = tb;
+    __hip_atomic_store((gq32*)(q1 + (long long)blockIdx.y * C + c), __float_as_uint(ta), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gq32*)(q2 + (long long)blockIdx.y * C + c), __float_as_uint(tb), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                                   // every wave's q stores drained; rf reads done
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(&f.ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add((gq32*)&f.ticket[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     const bool last = old == gridDim.y - 1;
-    if (last) {
-      __hip_atomic_store(&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store((gq32*)&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     rf[0] = last ? 1.f : 0.f;                        // "I am last" through the existing LDS array
   }
   __syncthreads();
   if (rf[0] == 0.f) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
   const int S = gridDim.y;
   double a = 0.0, b = 0.0;
   if (c < C)
-    for (int i = grp; i < S; i += 4) { a += q1[(long long)i * C + c]; b += q2[(long long)i * C + c]; }
+    for (int i = grp; i < S; i += 4) {
+      a += __uint_as_float(__hip_atomic_load((gq32*)(q1 + (long long)i * C + c), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+      b += __uint_as_float(__hip_atomic_load((gq32*)(q2 + (long long)i * C + c), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+    }
   __syncthreads();
   rd[0][threadIdx.x] = a;
   rd[1][threadIdx.x] = b;
@@ -579,24 +600,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
   }
   long long v = v0;
   if (fixed) {
-    for (; v + stride < nvec; v += 2 * stride) {   // two independent vectors in flight
-      float xv[2][8], gv[2][8], rv[2][8];
-      unsigned mb[2] = {0u, 0u};
+    // four independent vectors in flight, kept packed until used (RawVec8: half the registers of unpacked floats)
+    constexpr int U = 4;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+      RawVec8<T> xr[U], gr[U], rr[RES ? U : 1];
+      unsigned mb[U];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        Vec8<T>::load(x + (v + u * stride) * 8, xv[u]);
-        Vec8<T>::load(dy + (v + u * stride) * 8, gv[u]);
+      for (int u = 0; u < U; ++u) {
+        xr[u].load(x + (v + u * stride) * 8);
+        gr[u].load(dy + (v + u * stride) * 8);
+        mb[u] = 0u;
         if (use_mask) mb[u] = mask[v + u * stride];
-        else if (RES) Vec8<T>::load(res + (v + u * stride) * 8, rv[u]);
+        else if (RES) rr[RES ? u : 0].load(res + (v + u * stride) * 8);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
+        float xv[8], gv[8], rv[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          bn_bwd_elem<RELU, RES>(xv[u][i], gv[u][i], rv[u][i], A[i], B[i], Cq[i], sf[i],
+        for (int i = 0; i < 8; ++i) {
+          xv[i] = xr[u].get(i);
+          gv[i] = gr[u].get(i);
+          rv[i] = (RES && !use_mask) ? rr[RES ? u : 0].get(i) : 0.f;
+          bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i],
                                  use_mask ? (int)((mb[u] >> i) & 1u) : -1);
-        Vec8<T>::store(dx + (v + u * stride) * 8, xv[u]);
-        if (RES) Vec8<T>::store(dres + (v + u * stride) * 8, rv[u]);
+        }
+        Vec8<T>::store(dx + (v + u * stride) * 8, xv);
+        if (RES) Vec8<T>::store(dres + (v + u * stride) * 8, rv);
       }
     }
   }
@@ -638,6 +667,21 @@ static inline void bn_grid(long long M, int C, int* nblk, long long* rows_per_bl
   *rows_per_blk = rpb;
 }
 
+// Backward partial-sum grid: ~32 rows-vectors of x and dy per thread, and at least 256 blocks spread evenly (a
+// multiple of the 256 CUs once there is enough work, so no CU runs one block more than the others).
+static inline void bn_bwd_grid(long long M, int C, int* nblk, long long* rows_per_blk) {
+  const int T8 = C / 8;
+  const long long work = M * T8;
+  long long nb = work / (256LL * 32);
+  if (nb >= 256) nb = (nb + 255) / 256 * 256;
+  if (nb < 1) nb = 1;
+  if (nb > 2048) nb = 2048;
+  long long rpb = (M + nb - 1) / nb;
+  nb = (M + rpb - 1) / rpb;
+  *nblk = (int)nb;
+  *rows_per_blk = rpb;
+}
+
 static inline int apply_grid(long long M, int C) {
   long long nvec = M * (C / 8);
   long long g = (nvec + 255) / 256;
@@ -646,8 +690,10 @@ static inline int apply_grid(long long M, int C) {
 }
 
 DL4J_API int dl4j_bn_workspace_floats(long long M, int C) {
-  int nblk; long long rpb;
+  int nblk, nb2; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
+  bn_bwd_grid(M, C, &nb2, &rpb);
+  if (nb2 > nblk) nblk = nb2;
   return 2 * nblk * C + 2 * ((nblk + 31) / 32) * C + 8 * C;
 }
 
@@ -761,7 +807,7 @@ template <typename T>
 static int bn_bwd_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, long long M, int C, const float* ctx,
                        float* dgamma, float* dbeta, int relu, float* ws, const unsigned char* mask, hipStream_t s) {
   int nblk; long long rpb;
-  bn_grid(M, C, &nblk, &rpb);
+  bn_bwd_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
   float* p2 = ws + (long long)nblk * C;
   float* q = p2 + (long long)nblk * C;

@@ -51,9 +51,37 @@ template <> struct Vec8<float> {
   }
 };
 
+// Raw 8-element vectors kept packed in registers until used (half the VGPRs of the unpacked floats for 16-bit T):
+// RawVec8<T>::load issues the 16-byte (fp32: 2 x 16-byte) load, ::get unpacks element i.
+template <typename T> struct RawVec8;
+template <> struct RawVec8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ __forceinline__ float get(int i) const { return i < 4 ? a.v[i] : b.v[i - 4]; }
+};
+template <> struct RawVec8<bf16> {
+  uint4 q;
+  __device__ __forceinline__ void load(const bf16* p) { q = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ float get(int i) const {
+    const unsigned w = i < 2 ? q.x : (i < 4 ? q.y : (i < 6 ? q.z : q.w));
+    return __uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16));
+  }
+};
+
 // fp16 storage (IEEE half, the MFMA f16 operand type); math stays fp32.
 typedef _Float16 f16;
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+template <> struct RawVec8<f16> {
+  uint4 q;
+  __device__ __forceinline__ void load(const f16* p) { q = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ float get(int i) const {
+    const unsigned w = i < 2 ? q.x : (i < 4 ? q.y : (i < 6 ? q.z : q.w));
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)((i & 1) ? (w >> 16) : (w & 0xffffu)));
+  }
+};
 template <> struct Vec8<f16> {
   static __device__ __forceinline__ void load(const f16* p, float* o) {
     const f16x8_t v = *reinterpret_cast<const f16x8_t*>(p);

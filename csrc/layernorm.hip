@@ -275,6 +275,77 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   }
 }
 
+// Partial-row fold for the block kernel's [P][NP*N] partials: grid (ceil(NP*N/64), S = ceil(P/32)); each block sums
+// 32 rows of 64 columns (4 row groups x 8 independent loads) and hands its row to the last block of its column chunk
+// (agent-scope ticket; write-through atomic stores drained before the relaxed ticket add, atomic loads in the reducer:
+// no fence), which sums the S rows in fixed order and writes dgamma / dbeta / dsum. ~36 x 16 blocks for BERT-base
+// (P = 512, N = 768) instead of ln_bwd_reduce's 72 latency-bound blocks.
+typedef __attribute__((address_space(1))) unsigned lq32;
+__device__ unsigned g_ln_ticket[64 * 128];
+
+__global__ void __launch_bounds__(256) ln_bwd_fold(const float* __restrict__ part, int P, int NPN, int N,
+                                                   float* __restrict__ q, unsigned* __restrict__ ticket,
+                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                   float* __restrict__ dsum) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * 32 + grp * 8;
+  float v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = (j < NPN && r0 + u < P) ? part[(long long)(r0 + u) * NPN + j] : 0.f;
+  float sacc = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) sacc += v[u];
+  red[grp][cl] = sacc;
+  __syncthreads();
+  const float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  auto out = [&](float x) {
+    const int which = j / N, col = j - which * N;
+    (which == 0 ? dgamma : (which == 1 ? dbeta : dsum))[col] = x;
+  };
+  if (gridDim.y == 1) {
+    if (grp == 0 && j < NPN) out(t);
+    return;
+  }
+  if (grp == 0 && j < NPN)
+    __hip_atomic_store((lq32*)(q + (long long)blockIdx.y * NPN + j), __float_as_uint(t), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add((lq32*)&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == gridDim.y - 1;
+    if (last) __hip_atomic_store((lq32*)&ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[0][0] = last ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (red[0][0] == 0.f) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (grp == 0 && j < NPN) {
+    float x = 0.f;
+    for (int i = 0; i < (int)gridDim.y; ++i)
+      x += __uint_as_float(__hip_atomic_load((lq32*)(q + (long long)i * NPN + j), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+    out(x);
+  }
+}
+
+static unsigned* ln_ticket_slot(int cols) {
+  static unsigned* base[64] = {nullptr};
+  static unsigned next = 0;
+  int dev = 0;
+  if (cols > 128 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ln_ticket)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  const unsigned k = __atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % 64u;
+  return base[dev] + 128 * k;
+}
+
 template <typename T, int CH>
 static int fwd_l(const void* x, const void* r, const float* g, const float* b, void* y, float* mean, float* rstd,
                  long long M, int N, float eps, hipStream_t s) {
@@ -300,7 +371,8 @@ static inline long long ln_blocks(long long M, int N) {
 
 static long long ln_bwd_partials(long long M) {
   const long long old = ((M + 4 * kRPW - 1) / (4 * kRPW)) * 4;
-  const long long blk = M < 512 ? M : 512;                   // the block kernel never needs more rows than this
+  long long blk = M < 512 ? M : 512;                         // the block kernel never needs more rows than this,
+  blk += (blk + 31) / 32;                                    // plus the fold's ceil(rows / 32) rows of q
   return old > blk ? old : blk;
 }
 
@@ -347,8 +419,17 @@ static int bwd_l(const void* dy, const void* x, const void* r, const float* g, c
     }
 #undef LNB
     const int NP = ds ? 3 : 2;
-    hipLaunchKernelGGL(ln_bwd_reduce, dim3((NP * N + 31) / 32), dim3(256), 0, s, part, (int)blocks, N, dgamma, dbeta,
-                       dsum, NP);
+    const int cols = (NP * N + 63) / 64, S = (int)((blocks + 31) / 32);
+    unsigned* tk = S > 1 ? ln_ticket_slot(cols) : nullptr;
+    if (S == 1 || tk) {
+      // q (the folded rows) lives right after the partial rows in the caller's workspace (see ln_bwd_partials)
+      float* q = part + blocks * NP * N;
+      hipLaunchKernelGGL(ln_bwd_fold, dim3(cols, S), dim3(256), 0, s, part, (int)blocks, NP * N, N, q, tk, dgamma,
+                         dbeta, dsum);
+    } else {
+      hipLaunchKernelGGL(ln_bwd_reduce, dim3((NP * N + 31) / 32), dim3(256), 0, s, part, (int)blocks, N, dgamma,
+                         dbeta, dsum, NP);
+    }
     return (int)hipGetLastError();
   }
   const long long blocks = (M + 4 * kRPW - 1) / (4 * kRPW);

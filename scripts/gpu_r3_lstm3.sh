@@ -15,3 +15,9 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/r3_prof_
 cd "$R" && python3 tools/prof_laststep.py gpurun_out/r3_prof_lstm3/run_results.db --top 40 > gpurun_out/r3_prof_lstm3_step.txt && python3 tools/prof_steplist.py gpurun_out/r3_prof_lstm3/run_results.db > gpurun_out/r3_prof_lstm3_list.txt && rm -f gpurun_out/r3_prof_lstm3/run_results.db && head -20 gpurun_out/r3_prof_lstm3_step.txt
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/r3_prof_bert3" -o run -- python3 "$R/tools/bench_bert.py" --steps 4 --warmup 3 > "$R/gpurun_out/r3_prof_bert3.log" 2>&1 || { tail -5 "$R/gpurun_out/r3_prof_bert3.log"; exit 1; }
 cd "$R" && python3 tools/prof_laststep.py gpurun_out/r3_prof_bert3/run_results.db --top 40 > gpurun_out/r3_prof_bert3_step.txt && rm -f gpurun_out/r3_prof_bert3/run_results.db && head -30 gpurun_out/r3_prof_bert3_step.txt
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_conv.py -x -q --timeout 300 --timeout-method thread -k "batchnorm or bn_stats or resnet" > gpurun_out/r3_tests_bn3.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/r3_tests_bn3.log | head -30; tail -5 gpurun_out/r3_tests_bn3.log; exit 1; }
+tail -1 gpurun_out/r3_tests_bn3.log
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r3_bench_bn3.log 2>&1 || { tail -20 gpurun_out/r3_bench_bn3.log; exit 1; }
+tail -1 gpurun_out/r3_bench_bn3.log
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/r3_prof_bn3" -o run -- python3 "$R/bench.py" --steps 4 --warmup 3 > "$R/gpurun_out/r3_prof_bn3.log" 2>&1 || { tail -5 "$R/gpurun_out/r3_prof_bn3.log"; exit 1; }
+cd "$R" && python3 tools/prof_laststep.py gpurun_out/r3_prof_bn3/run_results.db --top 45 > gpurun_out/r3_prof_bn3_step.txt && rm -f gpurun_out/r3_prof_bn3/run_results.db && grep -E "bn_|one step" gpurun_out/r3_prof_bn3_step.txt
