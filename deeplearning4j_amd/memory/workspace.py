@@ -23,6 +23,21 @@ import torch
 from ..ops import runtime as _rt
 
 
+
+def _device_buffer(nbytes, device):
+    """The workspace's device memory: a block of the native engine's caching allocator (csrc/engine.hip, the N1
+    layer) on the GPU, a torch tensor elsewhere (or when the engine cannot serve the request)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        try:
+            from ..runtime import device_buffer
+            t = device_buffer(nbytes, dev)
+            if t is not None:
+                return t
+        except Exception:
+            pass
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev)
+
 class AllocationPolicy(enum.Enum):
     STRICT = 0
     OVERALLOCATE = 1
@@ -140,8 +155,7 @@ class MemoryWorkspace:
         overalloc = conf.overallocationLimit if conf.policyAllocation == AllocationPolicy.OVERALLOCATE else 0.0
         self._h = lib.rt_ws_create(conf.initialSize, maxb, conf.alignment, overalloc, conf.policyLearning.value,
                                    conf.policyReset.value, conf.cyclesBeforeInitialization)
-        self._buf = torch.empty(max(conf.initialSize, 0), dtype=torch.uint8, device=self.device) \
-            if conf.initialSize > 0 else None
+        self._buf = _device_buffer(max(conf.initialSize, 0), self.device) if conf.initialSize > 0 else None
         self.active = False
         self.parent = None
         self.external_bytes = 0
@@ -161,7 +175,8 @@ class MemoryWorkspace:
         want = self._lib.rt_ws_cycle_end(self._h)
         cap = self._buf.numel() if self._buf is not None else 0
         if want > cap:
-            self._buf = torch.empty(want, dtype=torch.uint8, device=self.device)
+            self._buf = None                                  # the old block returns to the engine first
+            self._buf = _device_buffer(want, self.device)
             self._lib.rt_ws_set_capacity(self._h, want)
         self.external_bytes = 0
 
