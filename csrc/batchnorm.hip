@@ -471,21 +471,33 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
     const unsigned old = __hip_atomic_fetch_add((gq32*)&f.ticket[blockIdx.x], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
     const bool last = old == gridDim.y - 1;
-    if (last) __hip_atomic_store((gq32*)&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) {
+      __hip_atomic_store((gq32*)&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // one acquire for the block, then PLAIN loads that can all be in flight together (atomic loads are issued
+      // one after another: 16-64 dependent round trips made the reducer the slowest block)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     rf[0] = last ? 1.f : 0.f;                        // "I am last" through the existing LDS array
   }
   __syncthreads();
   if (rf[0] == 0.f) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
   const int S = gridDim.y;
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int i = grp; i < S; i += 4) {
-      a += __uint_as_float(__hip_atomic_load((gq32*)(q1 + (long long)i * C + c), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-      b += __uint_as_float(__hip_atomic_load((gq32*)(q2 + (long long)i * C + c), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
+  if (c < C) {
+    constexpr int UL = 8;
+    for (int i0 = grp; i0 < S; i0 += 4 * UL) {
+      float va[UL], vb[UL];
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const int i = i0 + 4 * u;
+        va[u] = i < S ? q1[(long long)i * C + c] : 0.f;
+        vb[u] = i < S ? q2[(long long)i * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UL; ++u) { a += va[u]; b += vb[u]; }
     }
+  }
   __syncthreads();
   rd[0][threadIdx.x] = a;
   rd[1][threadIdx.x] = b;

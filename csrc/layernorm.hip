@@ -317,19 +317,31 @@ __global__ void __launch_bounds__(256) ln_bwd_fold(const float* __restrict__ par
     const unsigned old = __hip_atomic_fetch_add((lq32*)&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
     const bool last = old == gridDim.y - 1;
-    if (last) __hip_atomic_store((lq32*)&ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) {
+      __hip_atomic_store((lq32*)&ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // one acquire, then plain loads all in flight
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     red[0][0] = last ? 1.f : 0.f;
   }
   __syncthreads();
   if (red[0][0] == 0.f) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (grp == 0 && j < NPN) {
-    float x = 0.f;
-    for (int i = 0; i < (int)gridDim.y; ++i)
-      x += __uint_as_float(__hip_atomic_load((lq32*)(q + (long long)i * NPN + j), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-    out(x);
+  __syncthreads();                                               // everyone has read the flag before red is reused
+  const int S = gridDim.y;
+  float x = 0.f;
+  if (j < NPN) {
+    constexpr int UL = 8;
+    for (int i0 = grp; i0 < S; i0 += 4 * UL) {
+      float v2[UL];
+#pragma unroll
+      for (int u = 0; u < UL; ++u) v2[u] = i0 + 4 * u < S ? q[(long long)(i0 + 4 * u) * NPN + j] : 0.f;
+#pragma unroll
+      for (int u = 0; u < UL; ++u) x += v2[u];
+    }
   }
+  red[grp][cl] = x;
+  __syncthreads();
+  if (grp == 0 && j < NPN) out(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
 }
 
 static unsigned* ln_ticket_slot(int cols) {
@@ -361,12 +373,17 @@ static int fwd_l(const void* x, const void* r, const float* g, const float* b, v
 
 static constexpr int kRPW = 16;
 
-// Block-partial kernel geometry: up to 512 blocks of W waves, at least one row per wave.
+// Block-partial kernel geometry: up to g_ln_cap (512) blocks of W waves, at least one row per wave.
+static int g_ln_cap = 512, g_ln_fold = 1;
+DL4J_API void dl4j_ln_set_config(int block_cap, int fold) {
+  g_ln_cap = block_cap < 1 ? 1 : (block_cap > 512 ? 512 : block_cap);
+  g_ln_fold = fold;
+}
 static inline int ln_waves(int N) { return N <= 1024 ? 8 : (N <= 2048 ? 4 : 2); }
 static inline long long ln_blocks(long long M, int N) {
   const int W = ln_waves(N);
   long long b = (M + W - 1) / W;
-  return b > 512 ? 512 : (b < 1 ? 1 : b);
+  return b > g_ln_cap ? g_ln_cap : (b < 1 ? 1 : b);
 }
 
 static long long ln_bwd_partials(long long M) {
@@ -420,8 +437,8 @@ static int bwd_l(const void* dy, const void* x, const void* r, const float* g, c
 #undef LNB
     const int NP = ds ? 3 : 2;
     const int cols = (NP * N + 63) / 64, S = (int)((blocks + 31) / 32);
-    unsigned* tk = S > 1 ? ln_ticket_slot(cols) : nullptr;
-    if (S == 1 || tk) {
+    unsigned* tk = S > 1 && g_ln_fold ? ln_ticket_slot(cols) : nullptr;
+    if (g_ln_fold && (S == 1 || tk)) {
       // q (the folded rows) lives right after the partial rows in the caller's workspace (see ln_bwd_partials)
       float* q = part + blocks * NP * N;
       hipLaunchKernelGGL(ln_bwd_fold, dim3(cols, S), dim3(256), 0, s, part, (int)blocks, NP * N, N, q, tk, dgamma,

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 R=$(pwd)
-timeout -k 10 500 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_conv.py tests/test_gpu_bnpool.py tests/test_gpu_transformer.py tests/test_gpu_fallback.py -x -q --timeout 300 --timeout-method thread -k "batchnorm or bn or resnet or layernorm or bert or fp16" > gpurun_out/r3_tests_bn4.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/r3_tests_bn4.log | head -30; tail -5 gpurun_out/r3_tests_bn4.log; exit 1; }
+timeout -k 10 500 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_conv.py tests/test_gpu_bnpool.py tests/test_gpu_transformer.py tests/test_gpu_fallback.py tests/test_gpu_engine.py -x -q --timeout 300 --timeout-method thread -k "batchnorm or bn or resnet or layernorm or bert or fp16 or engine or alloc or dlpack or graph or stream or device" > gpurun_out/r3_tests_bn4.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/r3_tests_bn4.log | head -30; tail -5 gpurun_out/r3_tests_bn4.log; exit 1; }
 tail -1 gpurun_out/r3_tests_bn4.log
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r3_bench_bn4.log 2>&1 || { tail -20 gpurun_out/r3_bench_bn4.log; exit 1; }
 tail -1 gpurun_out/r3_bench_bn4.log
