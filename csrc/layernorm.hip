@@ -374,7 +374,7 @@ static int fwd_l(const void* x, const void* r, const float* g, const float* b, v
 static constexpr int kRPW = 16;
 
 // Block-partial kernel geometry: up to g_ln_cap (512) blocks of W waves, at least one row per wave.
-static int g_ln_cap = 512, g_ln_fold = 1;
+static int g_ln_cap = 128, g_ln_fold = 0;   // measured: tools/ln_bench.py (profiles/r3_ln_bwd_bench.log)
 DL4J_API void dl4j_ln_set_config(int block_cap, int fold) {
   g_ln_cap = block_cap < 1 ? 1 : (block_cap > 512 ? 512 : block_cap);
   g_ln_fold = fold;

@@ -164,14 +164,17 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ 
   if (r0 < rows_per_iter) {
     long long r = (long long)blockIdx.x * rows_per_iter + r0;
     const long long step = (long long)gridDim.x * rows_per_iter;
-    for (; r + step < M; r += 2 * step) {                // two independent 16-byte loads in flight
-      float v[8], w[8];
-      Vec8<T>::load(x + r * ld + g * 8, v);
-      Vec8<T>::load(x + (r + step) * ld + g * 8, w);
+    constexpr int U = 8;                                  // eight independent 16-byte loads in flight, kept packed
+    for (; r + (U - 1) * step < M; r += U * step) {
+      RawVec8<T> v[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j] + w[j];
+      for (int u = 0; u < U; ++u) v[u].load(x + (r + u * step) * ld + g * 8);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[u].get(j);
     }
-    if (r < M) {
+    for (; r < M; r += step) {
       float v[8];
       Vec8<T>::load(x + r * ld + g * 8, v);
 #pragma unroll

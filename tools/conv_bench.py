@@ -112,6 +112,10 @@ def main():
         tot["miopen_wrw"] += n * mw
         del x, w, y, dy, gW
     print("totals (ms, weighted by count):", {k: round(v, 3) for k, v in tot.items()})
+    for k, v in CN._V3_CHOICE.items():
+        g = k[1]
+        print(f"choice {k[0]:8s} N{g[0]} {g[3]}x{g[1]}x{g[2]} -> K{g[4]} {g[5]}x{g[6]}/{g[7]}: "
+              f"{'igemm(r2)' if v < 0 else f'v3 variant {v}'}")
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"rows": rows, "totals": tot}, f, indent=1)

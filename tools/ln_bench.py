@@ -32,7 +32,7 @@ def main():
             err = max((dg - ref[0]).abs().max().item(), (ds - ref[1]).abs().max().item())
             t = gpu_time(lambda: TN.ln_bwd(dy, x, g, mean, rstd, r, None, None, ds), reps=20) * 1e3
             print(f"cap {cap:4d} fold {fold}: {t:7.1f} us  (max diff vs first {err:.2e})")
-    L.dl4j_ln_set_config(512, 1)
+    L.dl4j_ln_set_config(128, 0)
 
 
 if __name__ == "__main__":
