@@ -16,18 +16,38 @@ def short(n):
     return n.split("(")[0][:70]
 
 
-def load_pass(d):
+def last_step_ids(d, marker="fused_update"):
+    """Dispatch ids of ONE steady-state step: between the last two ``marker`` dispatches of the kernel trace (the
+    first-call kernel tuning of earlier steps is excluded)."""
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), r.get("Dispatch_Id"), r["Kernel_Name"]))
+    rows.sort()
+    idx = [i for i, r in enumerate(rows) if marker in r[2]]
+    if len(idx) < 2 or rows[0][1] is None:
+        return None
+    return {r[1] for r in rows[idx[-2] + 1:idx[-1] + 1]}
+
+
+def load_pass(d, last_step=False):
     """{kernel: {counter: sum}}, {kernel: total_ns}, {kernel: calls} for one pass directory."""
+    keep = last_step_ids(d) if last_step else None
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
+                if keep is not None and r.get("Dispatch_Id") not in keep:
+                    continue
                 vals[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
     times = collections.defaultdict(float)
     calls = collections.Counter()
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
+                if keep is not None and r.get("Dispatch_Id") not in keep:
+                    continue
                 k = short(r["Kernel_Name"])
                 times[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
                 calls[k] += 1
@@ -39,12 +59,13 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--cus", type=int, default=256)
+    ap.add_argument("--last-step", action="store_true", help="only the dispatches of the last training step")
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
     times, calls = collections.defaultdict(float), collections.Counter()
     passes = sorted(glob.glob(os.path.join(a.root, "p*"))) or [a.root]    # one pass directory, or p1/p2/p3
     for p in passes:
-        v, t, c = load_pass(p)
+        v, t, c = load_pass(p, a.last_step)
         for k, d in v.items():
             merged[k].update(d)
         if p.endswith("p1") or p == a.root:
