@@ -50,18 +50,18 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
       for (int i = 0; i < 8; ++i) { const float d = v[i] - sh[i]; s1[i] += d; s2[i] += d * d; }
     }
   }
-  __shared__ float red1[2048];
-  __shared__ float red2[2048];
+  __shared__ float red1[256 * 9];   // row pitch 9 floats: conflict-free 8-float stores
+  __shared__ float red2[256 * 9];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    red1[threadIdx.x * 8 + i] = (r0 < R) ? s1[i] : 0.f;
-    red2[threadIdx.x * 8 + i] = (r0 < R) ? s2[i] : 0.f;
+    red1[threadIdx.x * 9 + i] = (r0 < R) ? s1[i] : 0.f;
+    red2[threadIdx.x * 9 + i] = (r0 < R) ? s2[i] : 0.f;
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c >> 3, k = c & 7;
     float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 8 + k]; b += red2[(rr * T8 + g) * 8 + k]; }
+    for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 9 + k]; b += red2[(rr * T8 + g) * 9 + k]; }
     part_s1[(long long)blockIdx.x * C + c] = a;
     part_s2[(long long)blockIdx.x * C + c] = b;
   }
@@ -330,18 +330,18 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
       r = r2;
     }
   }
-  __shared__ float red1[2048];
-  __shared__ float red2[2048];
+  __shared__ float red1[256 * 9];   // row pitch 9 floats: conflict-free 8-float stores
+  __shared__ float red2[256 * 9];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    red1[threadIdx.x * 8 + i] = (r0 < R) ? db[i] : 0.f;
-    red2[threadIdx.x * 8 + i] = (r0 < R) ? dg[i] : 0.f;
+    red1[threadIdx.x * 9 + i] = (r0 < R) ? db[i] : 0.f;
+    red2[threadIdx.x * 9 + i] = (r0 < R) ? dg[i] : 0.f;
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c >> 3, k = c & 7;
     float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 8 + k]; b += red2[(rr * T8 + g) * 8 + k]; }
+    for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 9 + k]; b += red2[(rr * T8 + g) * 9 + k]; }
     part_db[(long long)blockIdx.x * C + c] = a;
     part_dg[(long long)blockIdx.x * C + c] = b;
   }
@@ -1154,20 +1154,20 @@ __global__ __launch_bounds__(256) void bnpool_bwd_partial(const T* __restrict__ 
       }
     }
   }
-  __shared__ float red1[2048];
-  __shared__ float red2[2048];
+  __shared__ float red1[256 * 9];   // row pitch 9 floats: conflict-free 8-float stores
+  __shared__ float red2[256 * 9];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    red1[threadIdx.x * 8 + i] = (r0 < R) ? db[i] : 0.f;
-    red2[threadIdx.x * 8 + i] = (r0 < R) ? dg[i] : 0.f;
+    red1[threadIdx.x * 9 + i] = (r0 < R) ? db[i] : 0.f;
+    red2[threadIdx.x * 9 + i] = (r0 < R) ? dg[i] : 0.f;
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c >> 3, k = c & 7;
     float a = 0.f, b = 0.f;
     for (int rr = 0; rr < R; ++rr) {
-      a += red1[(rr * T8 + g) * 8 + k];
-      b += red2[(rr * T8 + g) * 8 + k];
+      a += red1[(rr * T8 + g) * 9 + k];
+      b += red2[(rr * T8 + g) * 9 + k];
     }
     part_db[(long long)blockIdx.x * C + c] = a;
     part_dg[(long long)blockIdx.x * C + c] = b;
