@@ -424,6 +424,9 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
                                             int(acc), _stream())
             native._check(rc, "conv_bwd_data_1x1")
+        elif max(stride) > 1 and (ph := _phase_plan(H, W, OH, OW, R, S, stride, pad4, dilation)) is not None and \
+                all(_v3_ok(K, C, p[2], p[3]) or not fp16 for p in ph):
+            dx = _bwd_data_phases(dy, w, ph, N, H, W, C, K, OH, OW, stride, dx_accum if acc else None, adt)
         elif tuple(dilation) == (1, 1) and max(stride) > 1 and pad4[0] <= R - 1 and pad4[1] <= R - 1 and \
                 pad4[2] <= S - 1 and pad4[3] <= S - 1 and \
                 H >= (OH - 1) * stride[0] + R - pad4[0] - pad4[1] and W >= (OW - 1) * stride[1] + S - pad4[2] - pad4[3]:
@@ -460,6 +463,81 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
     dW_out, db_out = _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb,
                                  grads_zeroed, pw and gemm_dw)
     return dx, dW_out, db_out
+
+
+_PHASE = os.environ.get("DL4J_AMD_CONV_PHASE", "1") == "1"
+
+
+def _phase_1d(n_in, n_out, R, s, p):
+    """Phases of a stride-s bwd-data along one dimension. Input index i has phase f = (i + p) mod s and receives only
+    the taps r = f + s*t (t < R_f = ceil((R - f) / s)) from dY rows base_f + j - t, i = i0 + s*j. Each phase is
+    therefore a stride-1 transposed conv of dY with the sub-kernel w[f::s] and top pad ``base_f``. Returns
+    [(i0, n_f, R_f, u0, base_f)] (u0: first tap of the sub-kernel in the flipped full kernel), or None when a phase
+    needs a negative pad."""
+    out = []
+    for f in range(s):
+        i0 = (f - p) % s
+        n_f = (n_in - i0 + s - 1) // s if i0 < n_in else 0
+        R_f = (R - f + s - 1) // s if f < R else 0
+        base = (i0 + p - f) // s
+        if n_f and R_f and R_f - 1 - base < 0:
+            return None
+        out.append((i0, n_f, R_f, R - 1 - f - s * (R_f - 1) if R_f else 0, base))
+    return out
+
+
+def _phase_plan(H, W, OH, OW, R, S, stride, pad4, dilation):
+    """Phase-split plan of a strided bwd-data (s^2 stride-1 sub-problems, s^2 fewer MACs than zero-interleaving dY);
+    None when it does not apply. Entries: (i0h, i0w, Rf, Sf, Hf, Wf, u0h, u0w, pad_h, pad_w) per non-empty phase."""
+    if not _PHASE or tuple(dilation) != (1, 1):
+        return None
+    ph = _phase_1d(H, OH, R, stride[0], pad4[0])
+    pw = _phase_1d(W, OW, S, stride[1], pad4[2])
+    if ph is None or pw is None:
+        return None
+    plan = []
+    for (i0h, nh, Rf, u0h, bh) in ph:
+        for (i0w, nw, Sf, u0w, bw) in pw:
+            if nh and nw:
+                plan.append((i0h, i0w, Rf, Sf, nh, nw, u0h, u0w, Rf - 1 - bh, Sf - 1 - bw))
+    return plan
+
+
+def _bwd_data_phases(dy, w, plan, N, H, W, C, K, OH, OW, stride, dx_accum, adt):
+    """Strided bwd-data as one stride-1 transposed conv per phase (sub-kernels sliced out of the flipped [C,R,S,K]
+    weight), each written to a dense phase buffer and scattered into the strided positions of dX."""
+    lib = native.load()
+    sh, sw = stride
+    _, flip = _relayout(w, False, True)
+    zero_taps = any(p[2] == 0 or p[3] == 0 for p in plan)
+    if dx_accum is not None:
+        dx = dx_accum
+    else:
+        dx = arena.empty((N, C, H, W), adt, dy.device, channels_last=True)
+        if zero_taps or len(plan) < sh * sw:
+            dx.zero_()
+    for (i0h, i0w, Rf, Sf, Hf, Wf, u0h, u0w, pth, ptw) in plan:
+        if Rf == 0 or Sf == 0:
+            continue
+        sub = flip[:, u0h::sh, u0w::sw, :][:, :Rf, :Sf, :].contiguous()
+        buf = torch.empty((N, C, Hf, Wf), dtype=adt, device=dy.device, memory_format=torch.channels_last)
+        geo = (N, OH, OW, K, C, Rf, Sf, 1, 1, pth, ptw, 1, 1, Hf, Wf)
+
+        def launch(var, out, _ts, sub=sub, geo=geo, Rf=Rf, Sf=Sf, pth=pth, ptw=ptw, Hf=Hf, Wf=Wf):
+            if var >= 0:
+                return _fwd_launch(var, dy, sub, None, out, geo, 0.0, None)
+            return lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(sub), _ptr(out), N, Hf, Wf, C, K, Rf, Sf, Rf - 1 - pth,
+                                             Sf - 1 - ptw, OH, OW, 0, _stream())
+        v = -1
+        if _v3_ok(K, C, Rf, Sf):
+            v = _v3_pick(("bwd_phase", geo, adt), launch, buf, lambda var: None)
+        native._check(launch(v, buf, None), "conv_bwd_data_phase")
+        view = dx[:, :, i0h::sh, i0w::sw]
+        if dx_accum is not None:
+            view.add_(buf)
+        else:
+            view.copy_(buf)
+    return dx
 
 
 def _conv2d_wrw(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, need_db, gW, gb, grads_zeroed, use_gemm):

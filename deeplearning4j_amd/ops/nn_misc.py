@@ -260,8 +260,8 @@ def depthwise_backward(x, w, dy, stride, pad4, dilation, need_dx=True, need_db=F
 
 # ------------------------------------------------------------------------------------------------ transposed conv
 def deconv_forward(x, w, b, stride, pad, dilation=(1, 1)):
-    """Transposed conv, w [nIn, nOut, kh, kw]. On the GPU it is the conv bwd-data kernel (stride 1) applied to the
-    zero-interleaved input, i.e. the transposed conv of ``Deconvolution2DLayer`` on MFMA."""
+    """Transposed conv, w [nIn, nOut, kh, kw]. On the GPU it is the conv bwd-data path (ops/conv_native.py; strided
+    deconvs phase-split), i.e. the transposed conv of ``Deconvolution2DLayer`` on MFMA."""
     from .conv import conv2d_backward
     N, Cin, H, W_ = x.shape
     _, Cout, R, S = w.shape
@@ -270,14 +270,11 @@ def deconv_forward(x, w, b, stride, pad, dilation=(1, 1)):
     OW = (W_ - 1) * s1 - 2 * pad[1] + dilation[1] * (S - 1) + 1
     if use_native(x, "deconv") and x.dtype == torch.bfloat16 and tuple(dilation) == (1, 1) and Cin % 8 == 0 and \
             Cout % 8 == 0 and pad[0] <= R - 1 and pad[1] <= S - 1:
-        if (s0, s1) != (1, 1):
-            xz = torch.empty((N, Cin, (H - 1) * s0 + 1, (W_ - 1) * s1 + 1), dtype=x.dtype, device=x.device,
-                             memory_format=torch.channels_last).zero_()
-            xz[:, :, ::s0, ::s1] = x
-        else:
-            xz = x.contiguous(memory_format=torch.channels_last)
+        # transposed conv = bwd-data of the conv with the same stride: strided cases run phase-split (one stride-1
+        # sub-conv per output phase), not on a zero-interleaved input
+        xz = x.contiguous(memory_format=torch.channels_last)
         shape_x = torch.empty((N, Cout, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        y, _, _ = conv2d_backward(shape_x, w.to(x.dtype), xz, (1, 1), (pad[0], pad[0], pad[1], pad[1]), (1, 1),
+        y, _, _ = conv2d_backward(shape_x, w.to(x.dtype), xz, (s0, s1), (pad[0], pad[0], pad[1], pad[1]), (1, 1),
                                   True, False, False)
         if b is not None:
             y = y + b.reshape(1, -1, 1, 1).to(y.dtype)

@@ -205,3 +205,53 @@ def test_conv_epilogue_bn_stats_match_separate_pass(cuda, monkeypatch, batch):
     _close(m1, m0, 1e-4)
     _close(v1, v0, 1e-4)
     _close(p1, p0, 1e-3)
+
+
+PHASE_CASES = [
+    # N, C, H, W, K, R, S, stride, pad4 — strided bwd-data through the phase-split path (canonical ResNet-50's 3x3/2,
+    # odd sizes, 5x5/2, a 2x2/2 deconv-style kernel and a 7x7/2 stem-like conv)
+    (2, 64, 56, 56, 64, 3, 3, (2, 2), (1, 1, 1, 1)),
+    (2, 128, 15, 13, 64, 3, 3, (2, 2), (1, 1, 1, 1)),
+    (2, 64, 17, 17, 128, 5, 5, (2, 2), (2, 2, 2, 2)),
+    (2, 64, 16, 16, 64, 2, 2, (2, 2), (0, 0, 0, 0)),
+    (2, 64, 29, 29, 64, 3, 3, (2, 2), (0, 0, 0, 0)),
+    (2, 64, 30, 30, 64, 7, 7, (2, 2), (3, 3, 3, 3)),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", PHASE_CASES)
+def test_strided_bwd_data_phase_split(cuda, case, dtype, monkeypatch):
+    """Phase-split strided bwd-data (one stride-1 sub-conv per phase) == fp32 torch, == the zero-interleave path, and
+    accumulates into dx_accum."""
+    N, C, H, W, K, R, S, stride, pad4 = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, C, H, W, generator=g).to(cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, S, generator=g) * 0.1).to(cuda).to(dtype)
+    xr = x.float().requires_grad_(True)
+    yr = _ref(xr, w.float(), None, stride, pad4)
+    dy = torch.randn(yr.shape, generator=g).to(cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    conv_native.bump_version()
+    plan = conv_native._phase_plan(H, W, dy.shape[2], dy.shape[3], R, S, stride, pad4, (1, 1))
+    assert plan is not None
+    calls = {"n": 0}
+    orig = conv_native._bwd_data_phases
+
+    def spy(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+    monkeypatch.setattr(conv_native, "_bwd_data_phases", spy)
+    dx, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False)
+    if dtype == torch.float16 and calls["n"] == 0:
+        pytest.skip("fp16 sub-kernel outside the round-3 engine")
+    assert calls["n"] == 1
+    _close(dx, xr.grad, 2e-2)
+    other = torch.randn(x.shape, generator=g).to(cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    acc = other.clone()
+    dx2, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False, dx_accum=acc)
+    _close(dx2, other.float() + xr.grad, 2e-2)
+    if dtype == torch.bfloat16:
+        monkeypatch.setattr(conv_native, "_PHASE", False)
+        dxz, _, _ = conv_native.conv2d_bwd(x, w, dy, stride, pad4, (1, 1), True, False, False)
+        _close(dx, dxz.float(), 1e-2)
