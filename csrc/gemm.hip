@@ -35,7 +35,7 @@
 namespace {
 
 template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES>
-__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_glds(GemmArgs g) {
+__global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_glds(GemmArgs g) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int FM = WTM / 32, FN = WTN / 32;
@@ -139,11 +139,23 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_glds(GemmArgs g) {
 
   constexpr int LPS = NIA + NIB;
   for (int kt = 0; kt < nk; ++kt) {
-    if (STAGES > 2 && kt + 1 < nk) wait_vm<(STAGES > 2 ? (STAGES - 2) * LPS : 0)>();
-    else wait_vm<0>();
+    if constexpr (STAGES == 1) {
+      // single buffer (small-K streaming shapes, 4+ blocks per CU hide the latency instead of a ring):
+      // every wave's fragment reads of the previous K-tile are done before the DMA overwrites the buffer
+      if (kt > 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+      }
+      issue(kt, 0);
+      wait_vm<0>();
+    } else {
+      if (STAGES > 2 && kt + 1 < nk) wait_vm<(STAGES > 2 ? (STAGES - 2) * LPS : 0)>();
+      else wait_vm<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    if constexpr (STAGES > 1)
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const char* sa = smem + (kt % STAGES) * SBYTES;
     const char* sb = sa + ABYTES;
 #pragma unroll
@@ -164,7 +176,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_glds(GemmArgs g) {
   // 4h, tile row wm*WTM + 32b + (lane&31); passes of RPP rows sized to the operand ring's LDS
   constexpr int PITCH = BN * 4 + 16;
   constexpr int RPP0 = (STAGES * SBYTES) / PITCH;
-  constexpr int RPP = RPP0 >= BM ? BM : (RPP0 >= BM / 2 ? BM / 2 : BM / 4);
+  constexpr int RPP = RPP0 >= BM ? BM : (RPP0 >= BM / 2 ? BM / 2 : (RPP0 >= BM / 4 ? BM / 4 : 64));
   static_assert(RPP >= 64 && RPP % 64 == 0, "epilogue pass too small");
   const int h = lane >> 5;
   const bool split = g.splits > 1;
@@ -599,7 +611,8 @@ struct Cfg {
 // cfg ids: 0 = 256x256 (8 waves 2x4, 2 stages), 1 = 256x128 (8 waves 4x2, 3 stages),
 //          2 = 128x128 (4 waves 2x2, 2 stages, 2 blocks/CU), 3 = 128x64 (4 waves 2x2 of 64x32, 3 stages)
 //          4 = 256x256 8-phase (8 waves, 16x16x32 MFMA, K % 64 == 0)
-const Cfg kCfg[5] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}};
+//          5 = 128x64 single-buffered (24 KB LDS, up to 4 blocks/CU: memory-bound skinny / small-K shapes)
+const Cfg kCfg[6] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}, {128, 64}};
 
 template <int DT, bool AKC, bool BKC>
 int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
@@ -610,6 +623,7 @@ int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
     case 1: hipLaunchKernelGGL((gemm_glds<DT, 256, 128, 4, 2, AKC, BKC, 3>), grid, dim3(512), 0, s, g); break;
     case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 2>), grid, dim3(256), 0, s, g); break;
     case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
+    case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 1>), grid, dim3(256), 0, s, g); break;
     default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC>), grid, dim3(512), 0, s, g); break;
   }
   return (int)hipGetLastError();
@@ -692,8 +706,8 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
       return -1;
   }
   if (K <= 0) return -1;
-  if (cfg < 0 || cfg > 4 || splits < 1) plan(M, N, K, batch, &cfg, &splits);
-  if (cfg == 3 && !bkc) cfg = 2;                 // the 64-wide tile has no N-contiguous image
+  if (cfg < 0 || cfg > 5 || splits < 1) plan(M, N, K, batch, &cfg, &splits);
+  if ((cfg == 3 || cfg == 5) && !bkc) cfg = 2;   // the 64-wide tile has no N-contiguous image
   if (cfg == 4) {                                // 8-phase: K % 64 and 32-bit element offsets
     const long long ea = akc ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M;
     const long long eb = bkc ? (long long)(N - 1) * ldb + K : (long long)(K - 1) * ldb + N;

@@ -277,8 +277,104 @@ __device__ __forceinline__ void epi_readout(const GemmArgs& g, const EpiOut& o, 
 // BatchNorm partial statistics of the bf16 outputs held in an fp32 LDS image (conv epilogue -> consuming BN layer):
 // per (64-row partial, column) shifted sums S1 = sum(y - y0), S2 = sum((y - y0)^2) and the shift y0 (first row),
 // y = bf16(alpha*acc + bias) exactly as stored. Planes [3][stats_P][N]; reduced by bn_tiles_reduce.
+//
+// Work split: one wave per (64-row partial, 64-column slab) item; lane = 16*q + c takes columns slab*64 + 4c..4c+3 of
+// rows 16q..16q+15 (float4 LDS reads: the 16 lanes of a quarter read one contiguous 256-byte row segment), and the
+// four row quarters are combined with two cross-lane xor-shuffles (same shift y0 -> plain sums): 16 independent
+// float4 reads per lane instead of 64 dependent scalar ones per column. The per-column loop below (kept for tiles
+// with BN % 64 != 0) added 25-120 us to a 400k-row 1x1 conv (tools/skinny_probe.py).
+template <int DTO>
+__device__ __forceinline__ float stored_as(float v) {
+  if constexpr (DTO == 2) return __half2float(__float2half(v));
+  else if constexpr (DTO == 1) return bf2f(to16(v, 1));
+  else return v;
+}
+
+template <int RPP, int BN, int NT, int DTO>
+__device__ __forceinline__ void epi_stats_wave(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int PARTS = RPP / 64, SLABS = BN / 64, NW = NT / 64;
+  const int lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  for (int item = w; item < PARTS * SLABS; item += NW) {
+    const int part = item / SLABS, slab = item - (item / SLABS) * SLABS;
+    const int rbeg = mrow0 + part * 64;
+    const long long pidx = rbeg / 64;
+    if (pidx >= g.stats_P) continue;
+    const int rows = min(64, g.M - rbeg);
+    const int col = slab * 64 + 4 * c;
+    const int n = n0 + col;
+    float bb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias_mode == 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[j] = n + j < g.N ? g.bias[n + j] : 0.f;
+    float sh[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    const char* src = T + (part * 64) * PITCH + col * 4;
+    if (rows > 0) {
+      const float4 y0 = *reinterpret_cast<const float4*>(src);
+      sh[0] = stored_as<DTO>(y0.x * g.alpha + bb[0]);
+      sh[1] = stored_as<DTO>(y0.y * g.alpha + bb[1]);
+      sh[2] = stored_as<DTO>(y0.z * g.alpha + bb[2]);
+      sh[3] = stored_as<DTO>(y0.w * g.alpha + bb[3]);
+      const int r0 = 16 * q;
+      if (r0 + 16 <= rows) {
+        float4 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = *reinterpret_cast<const float4*>(src + (r0 + r) * PITCH);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = stored_as<DTO>(e[j] * g.alpha + bb[j]) - sh[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+        }
+      } else {
+        for (int r = r0; r < rows; ++r) {
+          const float4 x = *reinterpret_cast<const float4*>(src + r * PITCH);
+          const float e[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = stored_as<DTO>(e[j] * g.alpha + bb[j]) - sh[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16);
+      s2[j] += __shfl_xor(s2[j], 16);
+      s1[j] += __shfl_xor(s1[j], 32);
+      s2[j] += __shfl_xor(s2[j], 32);
+    }
+    if (q == 0) {
+      float* p1 = g.tstats + pidx * g.N + n;
+      float* p2 = g.tstats + ((long long)g.stats_P + pidx) * g.N + n;
+      float* p3 = g.tstats + (2LL * g.stats_P + pidx) * g.N + n;
+      if (n + 4 <= g.N && (g.N & 3) == 0) {
+        *reinterpret_cast<float4*>(p1) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+        *reinterpret_cast<float4*>(p2) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+        *reinterpret_cast<float4*>(p3) = make_float4(sh[0], sh[1], sh[2], sh[3]);
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (n + j < g.N) { p1[j] = s1[j]; p2[j] = s2[j]; p3[j] = sh[j]; }
+      }
+    }
+  }
+}
+
 template <int RPP, int BN, int NT>
 __device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  if constexpr (BN % 64 == 0) {
+    if (g.out_dt == 1) epi_stats_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
+    else if (g.out_dt == 2) epi_stats_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);
+    else epi_stats_wave<RPP, BN, NT, 0>(g, T, mrow0, n0, tid);
+    return;
+  }
   constexpr int PITCH = BN * 4 + 16;
   constexpr int PARTS = RPP / 64;
   for (int task = tid; task < PARTS * BN; task += NT) {

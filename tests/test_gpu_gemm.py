@@ -161,7 +161,7 @@ def test_graph_capture():
     _check(out, _ref(a, b), torch.bfloat16, 2048, "graph replay")
 
 
-@pytest.mark.parametrize("cfg", [(0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (4, 3), (2, 2)])
+@pytest.mark.parametrize("cfg", [(0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (4, 3), (2, 2), (5, 1)])
 @pytest.mark.parametrize("a_kc", [True, False])
 @pytest.mark.parametrize("b_kc", [True, False])
 def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
@@ -175,7 +175,7 @@ def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
     _check(out, _ref(a, b), torch.bfloat16, K, f"cfg {cfg} a_kc={a_kc} b_kc={b_kc}")
 
 
-@pytest.mark.parametrize("cfg", [None, (0, 1), (1, 1), (2, 1), (3, 1), (4, 1)])
+@pytest.mark.parametrize("cfg", [None, (0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (5, 1)])
 def test_bn_stats_epilogue(cfg, monkeypatch):
     """Per-64-row BatchNorm partial statistics from the GEMM epilogue (conv -> BN fusion) match the stored output."""
     torch.manual_seed(10)
