@@ -849,6 +849,45 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
 #undef BNB
 }
 
+// Backward with the partial sums already produced by the epilogue of the kernel that wrote dy (csrc/mfma_tile.h
+// epi_bnbwd_wave, armed by dl4j_bnb_arm): planes [2][P][C] of sum(d), sum(d*xhat) per 64-row partial. One fold +
+// finalize launch and the apply pass; bn_bwd_partial's full read of x and dy is gone. No fused residual.
+DL4J_API long long dl4j_bn_bwd_planes_workspace_floats(long long P, int C) {
+  return 2 * ((P + 31) / 32) * (long long)C + 4LL * C;
+}
+
+template <typename T>
+static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, long long M, int C, const float* ctx, float* dgamma,
+                              float* dbeta, int relu, const float* planes, long long P, float* ws, hipStream_t s) {
+  float* q = ws;
+  float* cdb = q + 2 * ((P + 31) / 32) * (long long)C;
+  float* cdg = cdb + C;
+  BnFin f{M, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0.f, 0.f, nullptr, dbeta, dgamma, cdb, cdg,
+          nullptr, 0};
+  const int rc = bn_fold_launch<T, 0, 1>(planes, planes + P * C, P, C, q, f, s);
+  if (rc) return rc;
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply<T, true, false>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
+                       nullptr, M, C, ctx, cdb, cdg, nullptr);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<T, false, false>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
+                       nullptr, M, C, ctx, cdb, cdg, nullptr);
+  return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_bn_bwd_planes(int dtype, const void* x, const void* dy, void* dx, long long M, int C,
+                                const float* ctx, float* dgamma, float* dbeta, int relu, const float* planes,
+                                long long P, float* ws, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || P < 1 || P != (M + 63) / 64) return -1;
+  if (dtype == 1)
+    return bn_bwd_planes_impl<bf16>((const bf16*)x, (const bf16*)dy, (bf16*)dx, M, C, ctx, dgamma, dbeta, relu,
+                                    planes, P, ws, s);
+  if (dtype == 2)
+    return bn_bwd_planes_impl<f16>((const f16*)x, (const f16*)dy, (f16*)dx, M, C, ctx, dgamma, dbeta, relu, planes,
+                                   P, ws, s);
+  return -1;
+}
+
 // -------------------------------------------------------------------------------------------- BN + ReLU + max pool
 // Fused stem tail (ResNet: conv7x7 -> BN -> ReLU -> maxpool 3x3/2). The BN output is never materialised:
 //   forward  : pooled = max over the window of relu(x*scale + shift); per pooled element also stores the window

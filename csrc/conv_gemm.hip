@@ -284,6 +284,12 @@ DL4J_API int dl4j_conv_fwd_v3(int dt, const void* X, const void* Wkrsc, const fl
   g.coalesce = 1;                                   // K % 8 == 0 and a 16-byte aligned Y: 16-byte row stores
   g.tstats = tstats;
   g.stats_P = tstats ? (int)((M + 63) / 64) : 0;
+  if (tstats && bnb_armed().mode) {                 // BN-backward sums of dX (stride-1 bwd-data as a transposed conv)
+    if (beta != 0.f || bias || K % 4 != 0) return -1;
+    g.bnx = bnb_armed().x;
+    g.bnctx = bnb_armed().ctx;
+    g.bnb = bnb_armed().mode;
+  }
   ConvA ca;
   ca.X = X;
   ca.N = N; ca.H = H; ca.W = W; ca.C = C; ca.OH = OH; ca.OW = OW;

@@ -683,6 +683,22 @@ DL4J_API long long dl4j_gemm_plan(int M, int N, int K, int batch, int* cfg, int*
   return *splits > 1 ? (long long)(*splits) * M * N * 4 : 0;
 }
 
+BnbArm& bnb_armed() {
+  static thread_local BnbArm a{nullptr, nullptr, 0};
+  return a;
+}
+
+// Arms (mode 1: plain, 2: ReLU recomputed from x) or disarms (mode 0) BatchNorm-backward statistics for the next
+// dl4j_gemm / dl4j_conv_fwd_v3 launches of this thread that pass a statistics buffer: planes [2][P][N] of
+// sum(d), sum(d*xhat) of the stored output instead of the forward [3][P][N] tile statistics. x: the BN layer's input,
+// laid out like the output; ctx: its forward [mean | invstd | scale | shift] (csrc/batchnorm.hip).
+DL4J_API void dl4j_bnb_arm(const void* x, const float* ctx, int mode) {
+  BnbArm& a = bnb_armed();
+  a.x = mode ? x : nullptr;
+  a.ctx = mode ? ctx : nullptr;
+  a.mode = (x && ctx) ? mode : 0;
+}
+
 // Fast path. in_dt: 1 bf16, 2 f16. out_dt: 0 f32, 1 bf16, 2 f16. akc/bkc: operand layout flags (see top).
 // Requirements (else -1): lda/ldb multiples of 8 elements and 16-byte aligned bases; K % 8 == 0 for K-contiguous
 // operands, M % 8 == 0 (N % 8 == 0) for an M- (N-) contiguous A (B); batch > 1 only without split-K.
@@ -726,10 +742,16 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
   g.tstats = nullptr;
   g.stats_P = 0;
+  g.bnx = nullptr; g.bnctx = nullptr; g.bnb = 0;
   if (tstats) {                                   // statistics only from the 8-phase epilogue without split-K
     if (splits > 1 || batch > 1) return -3;
     g.tstats = tstats;
     g.stats_P = stats_P;
+    const BnbArm& ba = bnb_armed();
+    if (ba.mode) {                                // BN-backward sums of the stored output (mfma_tile.h epi_bnbwd_wave)
+      if (beta != 0.f || bias || act || (N & 3) || (ldc & 3) || (out_dt != 1 && out_dt != 2)) return -3;
+      g.bnx = ba.x; g.bnctx = ba.ctx; g.bnb = ba.mode;
+    }
   }
   {
     const int esz = out_dt == 0 ? 4 : 2;

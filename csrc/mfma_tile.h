@@ -57,7 +57,24 @@ struct GemmArgs {
   int coalesce;             // 1: epilogue through LDS with 16-byte row stores (host-checked alignment)
   float* tstats;           // optional BatchNorm partial statistics of the output (8-phase kernel, no split-K)
   int stats_P;              // number of 64-row partials (planes [3][stats_P][N])
+  // BatchNorm-backward statistics instead (bnb 1: plain, 2: ReLU recomputed from x): the output is the gradient of a
+  // BN layer's output, bnx that layer's input (same layout as C), bnctx its forward [mean|invstd|scale|shift];
+  // planes [2][stats_P][N] (see epi_bnbwd_wave)
+  const void* bnx;
+  const float* bnctx;
+  int bnb;
 };
+
+// The BN-backward epilogue request armed by dl4j_bnb_arm (csrc/gemm.hip) for the next GEMM / conv launches of this
+// host thread (read into GemmArgs at launch time, so HIP-graph capture records it by value).
+}  // namespace
+struct BnbArm {
+  const void* x;
+  const float* ctx;
+  int mode;
+};
+BnbArm& bnb_armed();                 // defined once, in csrc/gemm.hip
+namespace {
 
 __device__ __forceinline__ int xcd_remap_g(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
@@ -367,8 +384,89 @@ __device__ __forceinline__ void epi_stats_wave(const GemmArgs& g, const char* T,
   }
 }
 
+// BatchNorm BACKWARD partial sums from the epilogue of the GEMM / bwd-data conv that produces dy, the gradient of a
+// training BN layer's output (reference NN:nn/layers/normalization/BatchNormalization.java:131-210): per (64-row
+// partial, column) S1 = sum(d) and S2 = sum(d * (x - mean) * invstd), d = dy exactly as stored (bf16 / fp16 rounding),
+// zeroed where relu(x*scale + shift) was inactive (bnb == 2). x (g.bnx, the BN input, same layout as C) is read from
+// global memory: 8 bytes per lane-row, the 16 lanes of a row quarter cover one 128-byte segment. Planes [2][stats_P][N]
+// are folded by bn_fold<SRC 0, FIN 1> (dl4j_bn_bwd_planes): bn_bwd_partial's full re-read of dy and x disappears.
+// Same wave / lane split as epi_stats_wave. Requires beta == 0, N % 4 == 0, ldc % 4 == 0 (host-checked).
+template <int RPP, int BN, int NT, int DTO>
+__device__ __forceinline__ void epi_bnbwd_wave(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  constexpr int PITCH = BN * 4 + 16;
+  constexpr int PARTS = RPP / 64, SLABS = BN / 64, NW = NT / 64;
+  const int lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  const u16* xb = reinterpret_cast<const u16*>(g.bnx);
+  const float* ctx = g.bnctx;
+  for (int item = w; item < PARTS * SLABS; item += NW) {
+    const int part = item / SLABS, slab = item - (item / SLABS) * SLABS;
+    const int rbeg = mrow0 + part * 64;
+    const long long pidx = rbeg / 64;
+    if (pidx >= g.stats_P) continue;
+    const int rows = min(64, g.M - rbeg);
+    const int col = slab * 64 + 4 * c;
+    const int n = n0 + col;
+    const bool cok = n < g.N;
+    float mu[4], is[4], sc[4], sf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cc = cok ? n + j : 0;
+      mu[j] = ctx[cc];
+      is[j] = ctx[g.N + cc];
+      sc[j] = ctx[2 * g.N + cc];
+      sf[j] = ctx[3 * g.N + cc];
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int r0 = 16 * q;
+    if (cok && rows > r0) {
+      const int nr = min(16, rows - r0);
+      const char* src = T + (part * 64 + r0) * PITCH + col * 4;
+      const u16* xp = xb + (long long)(rbeg + r0) * g.ldc + n;
+      uint2 xv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        xv[r] = r < nr ? *reinterpret_cast<const uint2*>(xp + (long long)r * g.ldc) : make_uint2(0u, 0u);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r >= nr) break;
+        const float4 v = *reinterpret_cast<const float4*>(src + r * PITCH);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        const unsigned xw[2] = {xv[r].x, xv[r].y};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u16 u = (u16)(xw[j >> 1] >> (16 * (j & 1)));
+          const float xf = DTO == 2 ? __half2float(__ushort_as_half(u)) : bf2f(u);
+          float d = stored_as<DTO>(e[j] * g.alpha);
+          if (g.bnb == 2 && !(xf * sc[j] + sf[j] > 0.f)) d = 0.f;
+          s1[j] += d;
+          s2[j] = fmaf(d, (xf - mu[j]) * is[j], s2[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16);
+      s2[j] += __shfl_xor(s2[j], 16);
+      s1[j] += __shfl_xor(s1[j], 32);
+      s2[j] += __shfl_xor(s2[j], 32);
+    }
+    if (q == 0 && cok) {
+      *reinterpret_cast<float4*>(g.tstats + pidx * g.N + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+      *reinterpret_cast<float4*>(g.tstats + ((long long)g.stats_P + pidx) * g.N + n) =
+          make_float4(s2[0], s2[1], s2[2], s2[3]);
+    }
+  }
+}
+
 template <int RPP, int BN, int NT>
 __device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  if (g.bnb) {
+    static_assert(BN % 64 == 0, "BN-backward statistics need 64-column slabs");
+    if (g.out_dt == 2) epi_bnbwd_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);
+    else epi_bnbwd_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
+    return;
+  }
   if constexpr (BN % 64 == 0) {
     if (g.out_dt == 1) epi_stats_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
     else if (g.out_dt == 2) epi_stats_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);

@@ -10,6 +10,7 @@ Weights are re-laid-out once per parameter version (KRSC for forward, flipped CR
 """
 import ctypes
 import weakref
+import contextlib
 import os
 
 import numpy as np
@@ -378,12 +379,18 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
     if C != Cw or C % 8 != 0 or K % 8 != 0:
         return None
     OH, OW = dy.shape[2], dy.shape[3]
+    bnb = getattr(x, "_bn_bwd_req", None) if need_dx else None   # x is a training BN layer's output (ops/native.py)
     x = _cl(x)
     dy = _cl(dy)
     adt = x.dtype
     lib = native.load()
     dx = None
     pw = _is_pointwise(R, S, stride, pad4, dilation)
+    if dx_accum is not None and hasattr(dx_accum, "_bn_bwd_stats"):
+        del dx_accum._bn_bwd_stats                     # about to be summed into: its BN-backward sums go stale
+    if bnb is not None and (dx_accum is not None or adt not in (torch.bfloat16, torch.float16) or
+                            tuple(bnb[0].shape) != (N * H * W, C) or bnb[0].dtype != adt):
+        bnb = None
     if need_dx and pw and gemm_dx:
         from .gemm import mmul
         M = N * H * W
@@ -391,8 +398,16 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
         dx = dx_accum if acc else arena.empty((N, C, H, W), adt, x.device, channels_last=True)
         # dX[M, C] = dY[M, K] . W[K, C]  (+= the other consumer's gradient through beta)
-        mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
-             beta=1.0 if acc else 0.0)
+        if bnb is not None:
+            # ... with the consuming BN layer's backward partial sums from the epilogue
+            planes = torch.empty((2, (M + 63) // 64, C), dtype=torch.float32, device=x.device)
+            with native.bnb_armed(bnb):
+                mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
+                     stats=planes, stats_tag="bnb")
+            native.bnb_tag(dx, planes, bnb)
+        else:
+            mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
+                 beta=1.0 if acc else 0.0)
     elif need_dx:
         s1 = tuple(stride) == (1, 1) and tuple(dilation) == (1, 1)
         pure_1x1 = R == 1 and S == 1 and not any(pad4) and tuple(dilation) == (1, 1)
@@ -404,15 +419,23 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             # transposed conv: "input" dY (OH x OW x K), flipped CRSK weights, pad' = R-1-pad, output H x W x C
             geo_b = (N, OH, OW, K, C, R, S, 1, 1, R - 1 - pad4[0], S - 1 - pad4[2], 1, 1, H, W)
 
-            def bwd_launch(var, out, _ts):
+            def bwd_launch(var, out, ts):
                 if var >= 0:
-                    return _fwd_launch(var, dy, flip, None, out, geo_b, 1.0 if acc else 0.0, None)
+                    return _fwd_launch(var, dy, flip, None, out, geo_b, 1.0 if acc else 0.0, ts)
                 return lib.dl4j_conv_bwd_data_s1(_ptr(dy), _ptr(flip), _ptr(out), N, H, W, C, K, R, S, pad4[0],
                                                  pad4[2], OH, OW, int(acc), _stream())
             v = -1
-            if _v3_ok(K, C, R, S):
-                v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b, adt), bwd_launch, dx, lambda var: None)
-            rc = bwd_launch(v, dx, None)
+            P = (N * H * W + 63) // 64
+            mk = (lambda var: torch.empty((2, P, C), dtype=torch.float32, device=x.device) if var >= 0 else None) \
+                if bnb is not None else (lambda var: None)
+            with (native.bnb_armed(bnb) if bnb is not None else contextlib.nullcontext()):
+                if _v3_ok(K, C, R, S):
+                    v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b, adt, bnb is not None), bwd_launch, dx, mk)
+                planes = mk(v)
+                rc = bwd_launch(v, dx, planes)
+            if rc == 1:
+                native.bnb_tag(dx, planes, bnb)
+                rc = 0
             native._check(rc, "conv_bwd_data_s1")
         elif pure_1x1 and stride[0] == stride[1] and not fp16:
             _, flip = _relayout(w, False, True)

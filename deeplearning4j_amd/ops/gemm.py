@@ -202,14 +202,16 @@ def _torch_act(r, act):
     raise ValueError(act)
 
 
-def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, out_dtype=None, z=None, stats=None):
+def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, out_dtype=None, z=None, stats=None,
+         stats_tag=None):
     """``out = act(alpha * a @ b + bias + beta * out)``; returns ``out`` (allocated row-major when None).
 
     a: [M, K] or [B, M, K]; b: [K, N] or [B, K, N]; bias: [N] (bias_dim=1) or [M] (bias_dim=0);
     z: optional tensor like ``out`` receiving the pre-activation (act="dgelu": the pre-activation that is READ, out =
     (a @ b) * gelu'(z)); out_dtype defaults to a.dtype.
     stats: optional fp32 [3, P, N] tensor (P = ceil(M/64)) receiving per-64-row BatchNorm partial statistics of the
-    bf16 output (conv -> BN fusion; 8-phase kernel).
+    bf16 output (conv -> BN fusion; 8-phase kernel). With the BN-backward epilogue armed (ops/native.py bnb_armed)
+    the buffer is [2, P, N] and receives the BN backward sums instead; stats_tag keeps its tuned tile separate.
     """
     if b.dtype != a.dtype:
         # mixed operands: compute in the 16-bit type (fp32 accumulation) rather than promoting to the exact-fp32 path
@@ -310,7 +312,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         if stats is not None:
             if swap or batch != 1:
                 raise ValueError("GEMM BatchNorm statistics need a row-major, unbatched destination")
-            kst = key + ("stats",)
+            kst = key + ("stats", stats_tag)
             cfg = (_FORCE_CFG[0], 1) if _FORCE_CFG is not None else _TUNED.get(kst)
             if cfg is None:
                 cfg = (4, 1) if K % 64 == 0 else (2, 1)

@@ -313,17 +313,67 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
                                    _ptr(wst), _ptr(ctx), _ptr(mask), _stream())
         _check(rc, "bn_fwd_tiles")
+        _bnb_request(y, xr, ctx, relu, res, training, dt)
         return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
     rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
                          float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                          _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
                          _ptr(ctx), _ptr(mask), _stream())
     _check(rc, "bn_fwd")
+    _bnb_request(y, xr, ctx, relu, res, training, dt)
     return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
+
+
+# ------------------------------------------------------------------ BN backward sums from the producer's epilogue
+# A training BN layer without a fused residual tags its output with ``_bn_bwd_req = (x rows, ctx, relu)``. The conv /
+# GEMM that consumes that output computes, in the epilogue of its backward-data launch, the BN backward partial sums of
+# the dX it stores (csrc/mfma_tile.h epi_bnbwd_wave) and tags dX with ``_bn_bwd_stats``; bn_bwd then folds those planes
+# (dl4j_bn_bwd_planes) instead of re-reading dy and x in bn_bwd_partial. Any other route (fan-out sums, in-place
+# edits, layouts the kernels do not take) simply lacks the tag and runs the full backward.
+BNB = os.environ.get("DL4J_AMD_BN_BWD_EPILOGUE", "1") == "1"
+
+
+def _bnb_request(y, xr, ctx, relu, res, training, dt):
+    if BNB and training and res is None and dt in (1, 2) and xr.dim() == 2:
+        y._bn_bwd_req = (xr, ctx, bool(relu))
+
+
+class bnb_armed:
+    """Context manager: arms the BN-backward epilogue (dl4j_bnb_arm) for the GEMM / conv launches in its body that
+    pass a statistics buffer; always disarmed on exit."""
+
+    def __init__(self, req):
+        self.req = req
+
+    def __enter__(self):
+        register_sig("dl4j_bnb_arm", [c_void_p, c_void_p, c_int])
+        xr, ctx, relu = self.req
+        load().dl4j_bnb_arm(_ptr(xr), _ptr(ctx), 2 if relu else 1)
+        return self
+
+    def __exit__(self, *exc):
+        load().dl4j_bnb_arm(None, None, 0)
+        return False
+
+
+def bnb_tag(dx, planes, req):
+    """Marks dx as carrying BN-backward planes for the BN layer whose forward context is req[1]."""
+    dx._bn_bwd_stats = (planes, req[1], planes.shape[1], dx._version)
+
+
+def _bnb_planes(dy, c, res, M, C):
+    st = getattr(dy, "_bn_bwd_stats", None)
+    if st is None or res is not None:
+        return None
+    planes, ctx_t, P, ver = st
+    if ctx_t is not c or ver != dy._version or P != (M + 63) // 64 or tuple(planes.shape) != (2, P, C):
+        return None
+    return planes
 
 
 def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     _, x, c, relu, M, C, res, mask = ctx
+    planes = _bnb_planes(dy, c, res, M, C)
     dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
@@ -331,6 +381,17 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
     dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
     dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
+    if planes is not None:
+        register_sig("dl4j_bn_bwd_planes_workspace_floats", [c_ll, c_int])
+        lib.dl4j_bn_bwd_planes_workspace_floats.restype = c_ll
+        register_sig("dl4j_bn_bwd_planes", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
+                                            c_void_p, c_int, c_void_p, c_ll, c_void_p, c_void_p])
+        P = planes.shape[1]
+        ws = torch.empty(lib.dl4j_bn_bwd_planes_workspace_floats(P, C), dtype=torch.float32, device=x.device)
+        rc = lib.dl4j_bn_bwd_planes(_dt16(x), _ptr(x), _ptr(dy), _ptr(dx), M, C, _ptr(c), _ptr(dgamma), _ptr(dbeta),
+                                    1 if relu else 0, _ptr(planes), P, _ptr(ws), _stream())
+        _check(rc, "bn_bwd_planes")
+        return dx, dgamma, dbeta, None
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
     rc = lib.dl4j_bn_bwd(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
                          _ptr(dbeta), 1 if relu else 0, _ptr(ws), _ptr(mask), _stream())
