@@ -383,6 +383,7 @@ struct BnFin {
   float* cdb; float* cdg;                  // bwd out: mean(d), mean(d*xhat)
   unsigned* ticket;                        // ceil(C/64) counters (S > 1 only)
   int rpp;                                 // SRC 1: rows per tile partial
+  int rpb;                                 // SRC 0: partial rows folded per block (multiple of 32; set by the launcher)
 };
 
 template <typename T, int FIN>
@@ -420,15 +421,21 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
   float sa = 0.f, sb = 0.f;
   if (c < C) {
     if (SRC == 0) {
-      float a[8], b[8];
+      // rpb rows per block: each of the 4 row groups takes rpb/4 consecutive rows, 8 loads in flight per trip
+      const int q4 = f.rpb / 4;
+      const long long rg = (long long)blockIdx.y * f.rpb + grp * q4;
+      for (int k = 0; k < q4; k += 8) {
+        float a[8], b[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const bool ok = r0 + u < nrows;
-        a[u] = ok ? p1[(r0 + u) * C + c] : 0.f;
-        b[u] = ok ? p2[(r0 + u) * C + c] : 0.f;
+        for (int u = 0; u < 8; ++u) {
+          const long long r = rg + k + u;
+          const bool ok = r < nrows;
+          a[u] = ok ? p1[r * C + c] : 0.f;
+          b[u] = ok ? p2[r * C + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
     } else {
       const float x0 = ld1<T>((const T*)f.x + c);
       const long long P = nrows;
@@ -556,7 +563,10 @@ static int bn_fold_launch(const float* p1, const float* p2, long long nrows, int
                          f.cdb, f.cdg);
     return 0;
   }
-  const long long S = (nrows + 31) / 32;
+  // SRC 0 with many partial rows (the conv epilogue's 64-row planes): 128 rows per block keeps the reducer's serial
+  // pass short
+  f.rpb = (SRC == 0 && nrows > 4096) ? 128 : 32;
+  const long long S = (nrows + f.rpb - 1) / f.rpb;
   if (S > 65535) return -1;
   f.ticket = nullptr;
   if (S > 1) {
@@ -851,14 +861,16 @@ DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* 
 
 // Backward with the partial sums already produced by the epilogue of the kernel that wrote dy (csrc/mfma_tile.h
 // epi_bnbwd_wave, armed by dl4j_bnb_arm): planes [2][P][C] of sum(d), sum(d*xhat) per 64-row partial. One fold +
-// finalize launch and the apply pass; bn_bwd_partial's full read of x and dy is gone. No fused residual.
+// finalize launch and the apply pass; bn_bwd_partial's full read of x and dy is gone. With a fused residual (res
+// flag) the ReLU comes from the forward's bitmask and dres (the masked dy) is written as in dl4j_bn_bwd.
 DL4J_API long long dl4j_bn_bwd_planes_workspace_floats(long long P, int C) {
   return 2 * ((P + 31) / 32) * (long long)C + 4LL * C;
 }
 
 template <typename T>
-static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, long long M, int C, const float* ctx, float* dgamma,
-                              float* dbeta, int relu, const float* planes, long long P, float* ws, hipStream_t s) {
+static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, T* dres, const unsigned char* mask, long long M, int C,
+                              const float* ctx, float* dgamma, float* dbeta, int relu, const float* planes,
+                              long long P, float* ws, hipStream_t s) {
   float* q = ws;
   float* cdb = q + 2 * ((P + 31) / 32) * (long long)C;
   float* cdg = cdb + C;
@@ -866,7 +878,10 @@ static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, long long M, int C
           nullptr, 0};
   const int rc = bn_fold_launch<T, 0, 1>(planes, planes + P * C, P, C, q, f, s);
   if (rc) return rc;
-  if (relu)
+  if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<T, true, true>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
+                       dres, M, C, ctx, cdb, cdg, mask);
+  else if (relu)
     hipLaunchKernelGGL((bn_bwd_apply<T, true, false>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
                        nullptr, M, C, ctx, cdb, cdg, nullptr);
   else
@@ -875,16 +890,17 @@ static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, long long M, int C
   return (int)hipGetLastError();
 }
 
-DL4J_API int dl4j_bn_bwd_planes(int dtype, const void* x, const void* dy, void* dx, long long M, int C,
-                                const float* ctx, float* dgamma, float* dbeta, int relu, const float* planes,
-                                long long P, float* ws, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256 || P < 1 || P != (M + 63) / 64) return -1;
+// dres / mask: both or neither (residual BN layers: dres = the masked dy, ReLU from the forward's bitmask).
+DL4J_API int dl4j_bn_bwd_planes(int dtype, const void* x, const void* dy, void* dx, void* dres,
+                                const unsigned char* mask, long long M, int C, const float* ctx, float* dgamma,
+                                float* dbeta, int relu, const float* planes, long long P, float* ws, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || P < 1 || P != (M + 63) / 64 || ((dres == nullptr) != (mask == nullptr))) return -1;
   if (dtype == 1)
-    return bn_bwd_planes_impl<bf16>((const bf16*)x, (const bf16*)dy, (bf16*)dx, M, C, ctx, dgamma, dbeta, relu,
-                                    planes, P, ws, s);
+    return bn_bwd_planes_impl<bf16>((const bf16*)x, (const bf16*)dy, (bf16*)dx, (bf16*)dres, mask, M, C, ctx, dgamma,
+                                    dbeta, relu, planes, P, ws, s);
   if (dtype == 2)
-    return bn_bwd_planes_impl<f16>((const f16*)x, (const f16*)dy, (f16*)dx, M, C, ctx, dgamma, dbeta, relu, planes,
-                                   P, ws, s);
+    return bn_bwd_planes_impl<f16>((const f16*)x, (const f16*)dy, (f16*)dx, (f16*)dres, mask, M, C, ctx, dgamma,
+                                   dbeta, relu, planes, P, ws, s);
   return -1;
 }
 

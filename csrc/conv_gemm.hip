@@ -29,7 +29,7 @@ struct ConvA {
   int R, S, sh, sw, ph, pw, dh, dw;
 };
 
-template <int DT, int BM, int BN, int WGM, int WGN, int STAGES>
+template <int DT, int BM, int BN, int WGM, int WGN, int STAGES, bool BNB = false>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_glds(GemmArgs g, ConvA ca) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -192,7 +192,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_glds(GemmArgs g, ConvA 
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (g.tstats) epi_stats<RPP, BN, NW * 64>(g, smem, m0 + P * RPP, n0, tid);
+    if constexpr (BNB) epi_bnbwd<RPP, BN, NW * 64>(g, smem, m0 + P * RPP, n0, tid);
+    else if (g.tstats) epi_stats<RPP, BN, NW * 64>(g, smem, m0 + P * RPP, n0, tid);
     epi_readout<RPP, BN, NW * 64>(g, o, nullptr, smem, m0 + P * RPP, n0, tid);
     if (P + 1 < BM / RPP) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -211,17 +212,22 @@ struct TileCfg {
 constexpr int kNumVariants = 5;
 const TileCfg kTiles[kNumVariants] = {{256, 128}, {128, 128}, {256, 64}, {128, 64}, {128, 256}};
 
-template <int DT>
-int launch_conv(int v, const GemmArgs& g, const ConvA& ca, hipStream_t s) {
+template <int DT, bool BNB>
+int launch_conv_t(int v, const GemmArgs& g, const ConvA& ca, hipStream_t s) {
   dim3 grid(g.tiles_m * g.tiles_n);
   switch (v) {
-    case 0: hipLaunchKernelGGL((conv_glds<DT, 256, 128, 4, 2, 3>), grid, dim3(512), 0, s, g, ca); break;
-    case 1: hipLaunchKernelGGL((conv_glds<DT, 128, 128, 2, 2, 2>), grid, dim3(256), 0, s, g, ca); break;
-    case 2: hipLaunchKernelGGL((conv_glds<DT, 256, 64, 4, 1, 3>), grid, dim3(256), 0, s, g, ca); break;
-    case 3: hipLaunchKernelGGL((conv_glds<DT, 128, 64, 2, 2, 3>), grid, dim3(256), 0, s, g, ca); break;
-    default: hipLaunchKernelGGL((conv_glds<DT, 128, 256, 2, 4, 3>), grid, dim3(512), 0, s, g, ca); break;
+    case 0: hipLaunchKernelGGL((conv_glds<DT, 256, 128, 4, 2, 3, BNB>), grid, dim3(512), 0, s, g, ca); break;
+    case 1: hipLaunchKernelGGL((conv_glds<DT, 128, 128, 2, 2, 2, BNB>), grid, dim3(256), 0, s, g, ca); break;
+    case 2: hipLaunchKernelGGL((conv_glds<DT, 256, 64, 4, 1, 3, BNB>), grid, dim3(256), 0, s, g, ca); break;
+    case 3: hipLaunchKernelGGL((conv_glds<DT, 128, 64, 2, 2, 3, BNB>), grid, dim3(256), 0, s, g, ca); break;
+    default: hipLaunchKernelGGL((conv_glds<DT, 128, 256, 2, 4, 3, BNB>), grid, dim3(512), 0, s, g, ca); break;
   }
   return (int)hipGetLastError();
+}
+
+template <int DT>
+int launch_conv(int v, const GemmArgs& g, const ConvA& ca, hipStream_t s) {
+  return g.bnb ? launch_conv_t<DT, true>(v, g, ca, s) : launch_conv_t<DT, false>(v, g, ca, s);
 }
 
 // Default tile when the host has no timing for the shape: the largest tile whose width fits the channel count and
@@ -285,9 +291,10 @@ DL4J_API int dl4j_conv_fwd_v3(int dt, const void* X, const void* Wkrsc, const fl
   g.tstats = tstats;
   g.stats_P = tstats ? (int)((M + 63) / 64) : 0;
   if (tstats && bnb_armed().mode) {                 // BN-backward sums of dX (stride-1 bwd-data as a transposed conv)
-    if (beta != 0.f || bias || K % 4 != 0) return -1;
+    if (bias || K % 4 != 0) return -1;             // beta != 0: sums of the stored dX + beta*Y (fan-out)
     g.bnx = bnb_armed().x;
     g.bnctx = bnb_armed().ctx;
+    g.bnmask = bnb_armed().mask;
     g.bnb = bnb_armed().mode;
   }
   ConvA ca;

@@ -34,7 +34,7 @@
 
 namespace {
 
-template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES>
+template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES, bool BNB = false>
 __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_glds(GemmArgs g) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -211,7 +211,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_gld
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
-    if (g.tstats) epi_stats<RPP, BN, WGM * WGN * 64>(g, smem, m0 + P * RPP, n0, tid);
+    if constexpr (BNB) epi_bnbwd<RPP, BN, WGM * WGN * 64>(g, smem, m0 + P * RPP, n0, tid);
+    else if (g.tstats) epi_stats<RPP, BN, WGM * WGN * 64>(g, smem, m0 + P * RPP, n0, tid);
     epi_readout<RPP, BN, WGM * WGN * 64>(g, o, Zp, smem, m0 + P * RPP, n0, tid);
     if (P + 1 < BM / RPP) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -301,7 +302,7 @@ template <> struct Mfma16<2> {
   }
 };
 
-template <int DT, bool AKC, bool BKC>
+template <int DT, bool AKC, bool BKC, bool BNB = false>
 __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   typedef typename MfmaT<DT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * 16384 + 8192];   // + pad rows of the epilogue tile
@@ -512,7 +513,8 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
-      if (g.tstats) epi_stats<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
+      if constexpr (BNB) epi_bnbwd<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
+      else if (g.tstats) epi_stats<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
       epi_readout<128, 256, 512>(g, o, Zp, smem, m0 + P * 128, n0, tid);
       if (P == 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -629,8 +631,24 @@ int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// BN-backward epilogue instantiations: only the 1x1 bwd-data layout (dY rows K-contiguous, W [K][C] N-contiguous)
+template <int DT>
+int launch_fast_bnb(int cfg, const GemmArgs& g, hipStream_t s) {
+  dim3 grid(g.tiles_m * g.tiles_n, 1, 1);
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((gemm_glds<DT, 256, 256, 2, 4, true, false, 2, true>), grid, dim3(512), 0, s, g); break;
+    case 1: hipLaunchKernelGGL((gemm_glds<DT, 256, 128, 4, 2, true, false, 3, true>), grid, dim3(512), 0, s, g); break;
+    case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, true, false, 2, true>), grid, dim3(256), 0, s, g); break;
+    case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, true, false, 3, true>), grid, dim3(256), 0, s, g); break;
+    case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, true, false, 1, true>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm_8ph<DT, true, false, true>), grid, dim3(512), 0, s, g); break;
+  }
+  return (int)hipGetLastError();
+}
+
 template <int DT>
 int launch_fast_l(int cfg, int akc, int bkc, const GemmArgs& g, int batch, hipStream_t s) {
+  if (g.bnb) return (akc && !bkc && batch == 1) ? launch_fast_bnb<DT>(cfg, g, s) : -3;
   if (akc && bkc) return launch_fast<DT, true, true>(cfg, g, batch, s);
   if (akc) return launch_fast<DT, true, false>(cfg, g, batch, s);
   if (bkc) return launch_fast<DT, false, true>(cfg, g, batch, s);
@@ -684,19 +702,22 @@ DL4J_API long long dl4j_gemm_plan(int M, int N, int K, int batch, int* cfg, int*
 }
 
 BnbArm& bnb_armed() {
-  static thread_local BnbArm a{nullptr, nullptr, 0};
+  static thread_local BnbArm a{nullptr, nullptr, nullptr, 0};
   return a;
 }
 
-// Arms (mode 1: plain, 2: ReLU recomputed from x) or disarms (mode 0) BatchNorm-backward statistics for the next
-// dl4j_gemm / dl4j_conv_fwd_v3 launches of this thread that pass a statistics buffer: planes [2][P][N] of
-// sum(d), sum(d*xhat) of the stored output instead of the forward [3][P][N] tile statistics. x: the BN layer's input,
-// laid out like the output; ctx: its forward [mean | invstd | scale | shift] (csrc/batchnorm.hip).
-DL4J_API void dl4j_bnb_arm(const void* x, const float* ctx, int mode) {
+// Arms (mode 1: plain, 2: ReLU recomputed from x, 3: ReLU from the forward's bitmask) or disarms (mode 0)
+// BatchNorm-backward statistics for the next dl4j_gemm / dl4j_conv_fwd_v3 launches of this thread that pass a
+// statistics buffer: planes [2][P][N] of sum(d), sum(d*xhat) of the stored output instead of the forward [3][P][N]
+// tile statistics. x: the BN layer's input, laid out like the output; ctx: its forward [mean | invstd | scale | shift]
+// (csrc/batchnorm.hip); mask: bn_apply's ReLU bitmask (mode 3).
+DL4J_API void dl4j_bnb_arm(const void* x, const float* ctx, const unsigned char* mask, int mode) {
   BnbArm& a = bnb_armed();
-  a.x = mode ? x : nullptr;
-  a.ctx = mode ? ctx : nullptr;
-  a.mode = (x && ctx) ? mode : 0;
+  const bool ok = mode && x && ctx && (mode != 3 || mask);
+  a.x = ok ? x : nullptr;
+  a.ctx = ok ? ctx : nullptr;
+  a.mask = ok ? mask : nullptr;
+  a.mode = ok ? mode : 0;
 }
 
 // Fast path. in_dt: 1 bf16, 2 f16. out_dt: 0 f32, 1 bf16, 2 f16. akc/bkc: operand layout flags (see top).
@@ -742,15 +763,17 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
   g.tstats = nullptr;
   g.stats_P = 0;
-  g.bnx = nullptr; g.bnctx = nullptr; g.bnb = 0;
+  g.bnx = nullptr; g.bnctx = nullptr; g.bnmask = nullptr; g.bnb = 0;
   if (tstats) {                                   // statistics only from the 8-phase epilogue without split-K
     if (splits > 1 || batch > 1) return -3;
     g.tstats = tstats;
     g.stats_P = stats_P;
     const BnbArm& ba = bnb_armed();
     if (ba.mode) {                                // BN-backward sums of the stored output (mfma_tile.h epi_bnbwd_wave)
-      if (beta != 0.f || bias || act || (N & 3) || (ldc & 3) || (out_dt != 1 && out_dt != 2)) return -3;
-      g.bnx = ba.x; g.bnctx = ba.ctx; g.bnb = ba.mode;
+      if (bias || act || (N & 3) || (ldc & 3) || (out_dt != 1 && out_dt != 2) || (ba.mode == 3 && ldc != N) ||
+          (reinterpret_cast<uintptr_t>(C) & 7))
+        return -3;
+      g.bnx = ba.x; g.bnctx = ba.ctx; g.bnmask = ba.mask; g.bnb = ba.mode;
     }
   }
   {

@@ -62,6 +62,7 @@ struct GemmArgs {
   // planes [2][stats_P][N] (see epi_bnbwd_wave)
   const void* bnx;
   const float* bnctx;
+  const unsigned char* bnmask;   // bnb 3: the forward's ReLU bitmask (1 byte per 8 channels, residual BN layers)
   int bnb;
 };
 
@@ -71,6 +72,7 @@ struct GemmArgs {
 struct BnbArm {
   const void* x;
   const float* ctx;
+  const unsigned char* mask;
   int mode;
 };
 BnbArm& bnb_armed();                 // defined once, in csrc/gemm.hip
@@ -387,10 +389,14 @@ __device__ __forceinline__ void epi_stats_wave(const GemmArgs& g, const char* T,
 // BatchNorm BACKWARD partial sums from the epilogue of the GEMM / bwd-data conv that produces dy, the gradient of a
 // training BN layer's output (reference NN:nn/layers/normalization/BatchNormalization.java:131-210): per (64-row
 // partial, column) S1 = sum(d) and S2 = sum(d * (x - mean) * invstd), d = dy exactly as stored (bf16 / fp16 rounding),
-// zeroed where relu(x*scale + shift) was inactive (bnb == 2). x (g.bnx, the BN input, same layout as C) is read from
-// global memory: 8 bytes per lane-row, the 16 lanes of a row quarter cover one 128-byte segment. Planes [2][stats_P][N]
-// are folded by bn_fold<SRC 0, FIN 1> (dl4j_bn_bwd_planes): bn_bwd_partial's full re-read of dy and x disappears.
-// Same wave / lane split as epi_stats_wave. Requires beta == 0, N % 4 == 0, ldc % 4 == 0 (host-checked).
+// zeroed where relu(x*scale + shift) was inactive (bnb == 2) or where the forward's ReLU bitmask is clear (bnb == 3:
+// a BN layer with a fused residual, whose ReLU input is not recomputable from x alone). x (g.bnx, the BN input, same
+// layout as C) is read from global memory: 8 bytes per lane-row, the 16 lanes of a row quarter cover one 128-byte
+// segment. With beta != 0 (dX summed into another consumer's gradient, the last contribution) the old C is read the
+// same way and d is the stored sum; the caller then separates these reads from the readout's stores by a barrier.
+// Planes [2][stats_P][N] are folded by bn_fold<SRC 0, FIN 1> (dl4j_bn_bwd_planes): bn_bwd_partial's full re-read of dy
+// and x disappears. Same wave / lane split as epi_stats_wave. Requires N % 4 == 0, ldc % 4 == 0 (bnb 3: ldc == N),
+// no bias / activation (host-checked).
 template <int RPP, int BN, int NT, int DTO>
 __device__ __forceinline__ void epi_bnbwd_wave(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
   constexpr int PITCH = BN * 4 + 16;
@@ -420,27 +426,51 @@ __device__ __forceinline__ void epi_bnbwd_wave(const GemmArgs& g, const char* T,
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
     const int r0 = 16 * q;
     if (cok && rows > r0) {
+      // 4 rows per trip (x, old C and mask loads of the 4 in flight together, then consumed): the accumulators of the
+      // later epilogue passes are still live here, and 16 rows at once spilled to scratch
       const int nr = min(16, rows - r0);
+      const bool acc = g.beta != 0.f;
+      const long long row0 = (long long)(rbeg + r0);
       const char* src = T + (part * 64 + r0) * PITCH + col * 4;
-      const u16* xp = xb + (long long)(rbeg + r0) * g.ldc + n;
-      uint2 xv[16];
+      const u16* xp = xb + row0 * g.ldc + n;
+      const u16* cp = reinterpret_cast<const u16*>(g.C) + row0 * g.ldc + n;
+      const unsigned char* mp = g.bnb == 3 ? g.bnmask + row0 * (g.N >> 3) + (n >> 3) : nullptr;
+#pragma unroll 1
+      for (int rb = 0; rb < nr; rb += 4) {
+        uint2 xv[4], cv[4];
+        unsigned mb[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        xv[r] = r < nr ? *reinterpret_cast<const uint2*>(xp + (long long)r * g.ldc) : make_uint2(0u, 0u);
+        for (int i = 0; i < 4; ++i) {
+          const int r = rb + i;
+          const bool ok = r < nr;
+          xv[i] = ok ? *reinterpret_cast<const uint2*>(xp + (long long)r * g.ldc) : make_uint2(0u, 0u);
+          cv[i] = (ok && acc) ? *reinterpret_cast<const uint2*>(cp + (long long)r * g.ldc) : make_uint2(0u, 0u);
+          mb[i] = (ok && mp) ? ((unsigned)mp[(long long)r * (g.N >> 3)] >> (n & 7)) : 0u;
+        }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r >= nr) break;
-        const float4 v = *reinterpret_cast<const float4*>(src + r * PITCH);
-        const float e[4] = {v.x, v.y, v.z, v.w};
-        const unsigned xw[2] = {xv[r].x, xv[r].y};
+        for (int i = 0; i < 4; ++i) {
+          const int r = rb + i;
+          if (r < nr) {
+            const float4 v = *reinterpret_cast<const float4*>(src + r * PITCH);
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            const unsigned xw[2] = {xv[i].x, xv[i].y};
+            const unsigned cw[2] = {cv[i].x, cv[i].y};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const u16 u = (u16)(xw[j >> 1] >> (16 * (j & 1)));
-          const float xf = DTO == 2 ? __half2float(__ushort_as_half(u)) : bf2f(u);
-          float d = stored_as<DTO>(e[j] * g.alpha);
-          if (g.bnb == 2 && !(xf * sc[j] + sf[j] > 0.f)) d = 0.f;
-          s1[j] += d;
-          s2[j] = fmaf(d, (xf - mu[j]) * is[j], s2[j]);
+            for (int j = 0; j < 4; ++j) {
+              const u16 u = (u16)(xw[j >> 1] >> (16 * (j & 1)));
+              const float xf = DTO == 2 ? __half2float(__ushort_as_half(u)) : bf2f(u);
+              float t = e[j] * g.alpha + 0.f;
+              if (acc) {
+                const u16 uc = (u16)(cw[j >> 1] >> (16 * (j & 1)));
+                t += g.beta * (DTO == 2 ? __half2float(__ushort_as_half(uc)) : bf2f(uc));
+              }
+              float d = stored_as<DTO>(t);
+              if (g.bnb == 2 && !(xf * sc[j] + sf[j] > 0.f)) d = 0.f;
+              if (g.bnb == 3 && !((mb[i] >> j) & 1u)) d = 0.f;
+              s1[j] += d;
+              s2[j] = fmaf(d, (xf - mu[j]) * is[j], s2[j]);
+            }
+          }
         }
       }
     }
@@ -459,14 +489,18 @@ __device__ __forceinline__ void epi_bnbwd_wave(const GemmArgs& g, const char* T,
   }
 }
 
+// Only in the kernels' BNB instantiations (template flag): its loads in flight would otherwise raise the register
+// count, and so cut the occupancy, of every launch of the plain kernels.
+template <int RPP, int BN, int NT>
+__device__ __forceinline__ void epi_bnbwd(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
+  static_assert(BN % 64 == 0, "BN-backward statistics need 64-column slabs");
+  if (g.out_dt == 2) epi_bnbwd_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);
+  else epi_bnbwd_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
+  if (g.beta != 0.f) raw_barrier();   // every wave's reads of the old C precede the readout's stores
+}
+
 template <int RPP, int BN, int NT>
 __device__ __forceinline__ void epi_stats(const GemmArgs& g, const char* T, int mrow0, int n0, int tid) {
-  if (g.bnb) {
-    static_assert(BN % 64 == 0, "BN-backward statistics need 64-column slabs");
-    if (g.out_dt == 2) epi_bnbwd_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);
-    else epi_bnbwd_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
-    return;
-  }
   if constexpr (BN % 64 == 0) {
     if (g.out_dt == 1) epi_stats_wave<RPP, BN, NT, 1>(g, T, mrow0, n0, tid);
     else if (g.out_dt == 2) epi_stats_wave<RPP, BN, NT, 2>(g, T, mrow0, n0, tid);

@@ -330,7 +330,7 @@ def _fwd_launch(variant, x, wk, bias, y, geom, beta, ts):
                              OW, _ptr(ts), _stream())
 
 
-def _v3_pick(key, launch, out, make_ts):
+def _v3_pick(key, launch, out, make_ts, allow_r2=True):
     """Per-shape kernel choice: the first eager call times every tile variant of the round-3 engine and the round-2
     kernel on scratch outputs (inline on this stream) and keeps the fastest; calls under HIP-graph capture, or with
     DL4J_AMD_CONV_TUNE=0, use the remembered choice or the engine's default tile."""
@@ -342,7 +342,9 @@ def _v3_pick(key, launch, out, make_ts):
     M, K = geom[0] * geom[13] * geom[14], geom[4]
     if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
         return lib.dl4j_conv_v3_default_variant(M, K)
-    cands = list(range(lib.dl4j_conv_v3_num_variants())) + ([-1] if out.dtype == torch.bfloat16 else [])
+    # allow_r2=False: the round-2 kernel lacks an epilogue the caller needs (BN-backward sums), so its lower kernel
+    # time would not be the lower step time
+    cands = list(range(lib.dl4j_conv_v3_num_variants())) + ([-1] if out.dtype == torch.bfloat16 and allow_r2 else [])
     scratch = torch.empty_like(out)
     if key[0] == "bwd_acc":
         scratch.copy_(out)
@@ -388,8 +390,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
     pw = _is_pointwise(R, S, stride, pad4, dilation)
     if dx_accum is not None and hasattr(dx_accum, "_bn_bwd_stats"):
         del dx_accum._bn_bwd_stats                     # about to be summed into: its BN-backward sums go stale
-    if bnb is not None and (dx_accum is not None or adt not in (torch.bfloat16, torch.float16) or
-                            tuple(bnb[0].shape) != (N * H * W, C) or bnb[0].dtype != adt):
+    if bnb is not None and (adt not in (torch.bfloat16, torch.float16) or tuple(bnb[0].shape) != (N * H * W, C) or
+                            bnb[0].dtype != adt or (dx_accum is not None and native.BNB_MODE < 2)):
         bnb = None
     if need_dx and pw and gemm_dx:
         from .gemm import mmul
@@ -398,12 +400,12 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             and dx_accum.is_contiguous(memory_format=torch.channels_last)
         dx = dx_accum if acc else arena.empty((N, C, H, W), adt, x.device, channels_last=True)
         # dX[M, C] = dY[M, K] . W[K, C]  (+= the other consumer's gradient through beta)
-        if bnb is not None:
-            # ... with the consuming BN layer's backward partial sums from the epilogue
+        if bnb is not None and (acc or dx_accum is None):
+            # ... with the consuming BN layer's backward partial sums (of the stored sum) from the epilogue
             planes = torch.empty((2, (M + 63) // 64, C), dtype=torch.float32, device=x.device)
             with native.bnb_armed(bnb):
                 mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
-                     stats=planes, stats_tag="bnb")
+                     beta=1.0 if acc else 0.0, stats=planes, stats_tag="bnb_acc" if acc else "bnb")
             native.bnb_tag(dx, planes, bnb)
         else:
             mmul(dy.permute(0, 2, 3, 1).reshape(M, K), w.reshape(K, C), out=dx.permute(0, 2, 3, 1).reshape(M, C),
@@ -430,7 +432,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
                 if bnb is not None else (lambda var: None)
             with (native.bnb_armed(bnb) if bnb is not None else contextlib.nullcontext()):
                 if _v3_ok(K, C, R, S):
-                    v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b, adt, bnb is not None), bwd_launch, dx, mk)
+                    v = _v3_pick(("bwd_acc" if acc else "bwd", geo_b, adt, bnb is not None), bwd_launch, dx, mk,
+                                 allow_r2=bnb is None)
                 planes = mk(v)
                 rc = bwd_launch(v, dx, planes)
             if rc == 1:

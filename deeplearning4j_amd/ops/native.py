@@ -313,29 +313,35 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
                                    _ptr(wst), _ptr(ctx), _ptr(mask), _stream())
         _check(rc, "bn_fwd_tiles")
-        _bnb_request(y, xr, ctx, relu, res, training, dt)
+        _bnb_request(y, xr, ctx, relu, res, mask, training, dt)
         return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
     rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
                          float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                          _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
                          _ptr(ctx), _ptr(mask), _stream())
     _check(rc, "bn_fwd")
-    _bnb_request(y, xr, ctx, relu, res, training, dt)
+    _bnb_request(y, xr, ctx, relu, res, mask, training, dt)
     return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
 
 
 # ------------------------------------------------------------------ BN backward sums from the producer's epilogue
-# A training BN layer without a fused residual tags its output with ``_bn_bwd_req = (x rows, ctx, relu)``. The conv /
-# GEMM that consumes that output computes, in the epilogue of its backward-data launch, the BN backward partial sums of
-# the dX it stores (csrc/mfma_tile.h epi_bnbwd_wave) and tags dX with ``_bn_bwd_stats``; bn_bwd then folds those planes
-# (dl4j_bn_bwd_planes) instead of re-reading dy and x in bn_bwd_partial. Any other route (fan-out sums, in-place
-# edits, layouts the kernels do not take) simply lacks the tag and runs the full backward.
-BNB = os.environ.get("DL4J_AMD_BN_BWD_EPILOGUE", "1") == "1"
+# A training BN layer tags its output with ``_bn_bwd_req = (x rows, ctx, relu, mask)`` (mask: the forward's ReLU
+# bitmask of a layer with a fused residual). The conv / GEMM that consumes that output computes, in the epilogue of its
+# backward-data launch, the BN backward partial sums of the dX it stores (csrc/mfma_tile.h epi_bnbwd_wave; when it sums
+# into another consumer's gradient, of the stored sum) and tags dX with ``_bn_bwd_stats``; bn_bwd then folds those
+# planes (dl4j_bn_bwd_planes) instead of re-reading dy and x in bn_bwd_partial. A later contribution to that gradient
+# (a kernel summing into it drops the tag; a torch sum makes a new, untagged tensor), an in-place edit (version
+# counter), or a layout the kernels do not take leaves no valid tag, and the full backward runs.
+# DL4J_AMD_BN_BWD_EPILOGUE: 0 off, 1 plain BN layers only (no fused residual, no fan-out sum), 2 also residual layers
+# and summed gradients (their epilogue reads the old sum and the mask besides x: no less traffic than bn_bwd_partial)
+BNB_MODE = int(os.environ.get("DL4J_AMD_BN_BWD_EPILOGUE", "1") or 0)
+BNB = BNB_MODE > 0
 
 
-def _bnb_request(y, xr, ctx, relu, res, training, dt):
-    if BNB and training and res is None and dt in (1, 2) and xr.dim() == 2:
-        y._bn_bwd_req = (xr, ctx, bool(relu))
+def _bnb_request(y, xr, ctx, relu, res, mask, training, dt):
+    if BNB and training and (res is None or (mask is not None and BNB_MODE >= 2)) and dt in (1, 2) and \
+            xr.dim() == 2:
+        y._bn_bwd_req = (xr, ctx, bool(relu), mask)
 
 
 class bnb_armed:
@@ -346,13 +352,13 @@ class bnb_armed:
         self.req = req
 
     def __enter__(self):
-        register_sig("dl4j_bnb_arm", [c_void_p, c_void_p, c_int])
-        xr, ctx, relu = self.req
-        load().dl4j_bnb_arm(_ptr(xr), _ptr(ctx), 2 if relu else 1)
+        register_sig("dl4j_bnb_arm", [c_void_p, c_void_p, c_void_p, c_int])
+        xr, ctx, relu, mask = self.req
+        load().dl4j_bnb_arm(_ptr(xr), _ptr(ctx), _ptr(mask), 3 if mask is not None else (2 if relu else 1))
         return self
 
     def __exit__(self, *exc):
-        load().dl4j_bnb_arm(None, None, 0)
+        load().dl4j_bnb_arm(None, None, None, 0)
         return False
 
 
@@ -361,9 +367,9 @@ def bnb_tag(dx, planes, req):
     dx._bn_bwd_stats = (planes, req[1], planes.shape[1], dx._version)
 
 
-def _bnb_planes(dy, c, res, M, C):
+def _bnb_planes(dy, c, res, M, C, mask=None):
     st = getattr(dy, "_bn_bwd_stats", None)
-    if st is None or res is not None:
+    if st is None or (res is not None and mask is None):
         return None
     planes, ctx_t, P, ver = st
     if ctx_t is not c or ver != dy._version or P != (M + 63) // 64 or tuple(planes.shape) != (2, P, C):
@@ -373,7 +379,7 @@ def _bnb_planes(dy, c, res, M, C):
 
 def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     _, x, c, relu, M, C, res, mask = ctx
-    planes = _bnb_planes(dy, c, res, M, C)
+    planes = _bnb_planes(dy, c, res, M, C, mask)
     dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
@@ -384,14 +390,16 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     if planes is not None:
         register_sig("dl4j_bn_bwd_planes_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_bwd_planes_workspace_floats.restype = c_ll
-        register_sig("dl4j_bn_bwd_planes", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
-                                            c_void_p, c_int, c_void_p, c_ll, c_void_p, c_void_p])
+        register_sig("dl4j_bn_bwd_planes", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int,
+                                            c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_void_p, c_void_p])
         P = planes.shape[1]
         ws = torch.empty(lib.dl4j_bn_bwd_planes_workspace_floats(P, C), dtype=torch.float32, device=x.device)
-        rc = lib.dl4j_bn_bwd_planes(_dt16(x), _ptr(x), _ptr(dy), _ptr(dx), M, C, _ptr(c), _ptr(dgamma), _ptr(dbeta),
-                                    1 if relu else 0, _ptr(planes), P, _ptr(ws), _stream())
+        rc = lib.dl4j_bn_bwd_planes(_dt16(x), _ptr(x), _ptr(dy), _ptr(dx), _ptr(dres), _ptr(mask if dres is not None
+                                                                                               else None), M, C,
+                                    _ptr(c), _ptr(dgamma), _ptr(dbeta), 1 if relu else 0, _ptr(planes), P, _ptr(ws),
+                                    _stream())
         _check(rc, "bn_bwd_planes")
-        return dx, dgamma, dbeta, None
+        return dx, dgamma, dbeta, dres
     ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
     rc = lib.dl4j_bn_bwd(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
                          _ptr(dbeta), 1 if relu else 0, _ptr(ws), _ptr(mask), _stream())

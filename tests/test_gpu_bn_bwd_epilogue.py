@@ -30,6 +30,7 @@ def _cl(t):
 def test_bn_bwd_epilogue_matches_full(cuda, monkeypatch, dtype, relu, R, shape, K):
     monkeypatch.setenv("DL4J_AMD_CONV_TUNE", "0")       # default tiles: the round-3 engine, which has the epilogue
     monkeypatch.setattr(native, "BNB", True)
+    monkeypatch.setattr(native, "BNB_MODE", 2)
     g = torch.Generator().manual_seed(1)
     N, C, H, W = shape
     x = _cl((torch.randn(*shape, generator=g) * 2 + 0.5).to(dtype).to(cuda))
@@ -59,25 +60,41 @@ def test_bn_bwd_epilogue_matches_full(cuda, monkeypatch, dtype, relu, R, shape, 
     _close(got[2], db_r, 3e-2)
 
 
-def test_bn_bwd_epilogue_skipped_when_accumulating(cuda, monkeypatch):
-    """A dX summed into another consumer's gradient (fan-out) never carries planes: the sums would be of one term."""
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_bwd_epilogue_of_accumulated_gradient(cuda, monkeypatch, residual):
+    """Fan-out: the 1x1 bwd-data GEMM sums dX into another consumer's gradient (beta = 1) and its epilogue sums are
+    those of the stored SUM; a BN layer with a fused residual takes its ReLU from the forward's bitmask. Both match
+    the full backward (dx, dgamma, dbeta, dresidual); an in-place edit afterwards invalidates the planes."""
     monkeypatch.setenv("DL4J_AMD_CONV_TUNE", "0")
     monkeypatch.setattr(native, "BNB", True)
+    monkeypatch.setattr(native, "BNB_MODE", 2)
     g = torch.Generator().manual_seed(2)
-    x = _cl(torch.randn(4, 64, 8, 8, generator=g).to(torch.bfloat16).to(cuda))
-    C = 64
-    y, ctx = ops.bn_forward(x, torch.ones(C, device=cuda), torch.zeros(C, device=cuda), torch.zeros(C, device=cuda),
-                            torch.ones(C, device=cuda), True, 0.9, 1e-5, True)
-    w = (torch.randn(64, 64, 1, 1, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
-    dz = _cl(torch.randn(4, 64, 8, 8, generator=g).to(torch.bfloat16).to(cuda))
-    d1, _, _ = ops.conv2d_backward(y, w, dz, (1, 1), (0, 0, 0, 0), need_dx=True, need_dw=False, need_db=False)
-    assert hasattr(d1, "_bn_bwd_stats")
-    d2, _, _ = ops.conv2d_backward(y, w, dz, (1, 1), (0, 0, 0, 0), need_dx=True, need_dw=False, need_db=False,
-                                   dx_accum=d1)
-    assert not hasattr(d2, "_bn_bwd_stats") and not hasattr(d1, "_bn_bwd_stats")
-    d3, _, _ = ops.conv2d_backward(y, w, dz, (1, 1), (0, 0, 0, 0), need_dx=True, need_dw=False, need_db=False)
-    d3.mul_(1.0)                                         # an in-place edit after the launch: planes are stale
-    assert native._bnb_planes(d3, ctx[2], None, ctx[4], ctx[5]) is None
+    C, K = 128, 64
+    x = _cl((torch.randn(4, C, 9, 8, generator=g) + 0.3).to(torch.bfloat16).to(cuda))
+    res = _cl(torch.randn(4, C, 9, 8, generator=g).to(torch.bfloat16).to(cuda)) if residual else None
+    gamma = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    beta = torch.randn(C, generator=g).to(cuda)
+    y, ctx = ops.bn_forward(x, gamma, beta, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), True, 0.9, 1e-5,
+                            True, residual=res)
+    assert hasattr(y, "_bn_bwd_req") and (y._bn_bwd_req[3] is not None) == residual
+    w = (torch.randn(K, C, 1, 1, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    dz = _cl(torch.randn(4, K, 9, 8, generator=g).to(torch.bfloat16).to(cuda))
+    other = _cl(torch.randn(4, C, 9, 8, generator=g).to(torch.bfloat16).to(cuda))   # another consumer's gradient
+    acc = other.clone()
+    d, _, _ = ops.conv2d_backward(y, w, dz, (1, 1), (0, 0, 0, 0), need_dx=True, need_dw=False, need_db=False,
+                                  dx_accum=acc)
+    assert d is acc and hasattr(d, "_bn_bwd_stats")
+    plain, _, _ = ops.conv2d_backward(y, w, dz, (1, 1), (0, 0, 0, 0), need_dx=True, need_dw=False, need_db=False)
+    _close(d, plain.float() + other.float(), 2e-2)
+    got = ops.bn_backward(d, ctx)
+    ref = ops.bn_backward(d.clone(), ctx)
+    _close(got[0], ref[0], 2e-2)
+    _close(got[1], ref[1], 2e-3)
+    _close(got[2], ref[2], 2e-3)
+    if residual:
+        _close(got[3], ref[3], 1e-6)
+    d.mul_(1.0)                                          # an in-place edit after the launch: planes are stale
+    assert native._bnb_planes(d, ctx[2], ctx[6], ctx[4], ctx[5], ctx[7]) is None
 
 
 def test_resnet_gradients_with_bn_bwd_epilogue_match_full(cuda, monkeypatch):
@@ -102,12 +119,13 @@ def test_resnet_gradients_with_bn_bwd_epilogue_match_full(cuda, monkeypatch):
     grads = []
     for flag in (False, True):
         monkeypatch.setattr(native, "BNB", flag)
+        monkeypatch.setattr(native, "BNB_MODE", 2 if flag else 0)
         net = ResNet50(numLabels=10, seed=11, dataType=DataType.BFLOAT16).init(device=cuda)
         net.computeGradientAndScore([x], [y])
         grads.append(net.flattenedGradients.float().clone())
         if not flag:
             assert calls["planes"] == 0
-    assert calls["planes"] >= 32, calls                 # 2 non-residual BNs per bottleneck x 16 blocks
+    assert calls["planes"] >= 32, calls                 # >= 2 non-residual BNs per bottleneck x 16 blocks
     g0, g1 = grads
     rel = ((g1 - g0).norm() / g0.norm()).item()
     assert rel < 2e-2, rel
