@@ -332,9 +332,12 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
 # planes (dl4j_bn_bwd_planes) instead of re-reading dy and x in bn_bwd_partial. A later contribution to that gradient
 # (a kernel summing into it drops the tag; a torch sum makes a new, untagged tensor), an in-place edit (version
 # counter), or a layout the kernels do not take leaves no valid tag, and the full backward runs.
-# DL4J_AMD_BN_BWD_EPILOGUE: 0 off, 1 plain BN layers only (no fused residual, no fan-out sum), 2 also residual layers
-# and summed gradients (their epilogue reads the old sum and the mask besides x: no less traffic than bn_bwd_partial)
-BNB_MODE = int(os.environ.get("DL4J_AMD_BN_BWD_EPILOGUE", "1") or 0)
+# DL4J_AMD_BN_BWD_EPILOGUE: 0 off (default), 1 plain BN layers only (no fused residual, no fan-out sum), 2 also residual
+# layers and summed gradients (their epilogue reads the old sum and the mask besides x: no less traffic than
+# bn_bwd_partial). Off by default: on the ResNet-50 bench (bf16, batch 512) mode 0 / 1 / 2 measured 31.1k / 30.5k /
+# 29.1k images/s (profiles/r3_bench_bnbmode*.log) — bn_bwd_partial already streams at ~5 TB/s, and the epilogue's
+# exposed load latency costs more than the dy re-read it saves.
+BNB_MODE = int(os.environ.get("DL4J_AMD_BN_BWD_EPILOGUE", "0") or 0)
 BNB = BNB_MODE > 0
 
 
