@@ -417,7 +417,6 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
                                                float* __restrict__ q2, BnFin f) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
-  const long long r0 = (long long)blockIdx.y * 32 + grp * 8;
   float sa = 0.f, sb = 0.f;
   if (c < C) {
     if (SRC == 0) {
@@ -437,17 +436,30 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
         for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
       }
     } else {
+      // same rpb split; a partial past P contributes zeros (n = 0, d = 0)
       const float x0 = ld1<T>((const T*)f.x + c);
       const long long P = nrows;
+      const int q4 = f.rpb / 4;
+      const long long rg = (long long)blockIdx.y * f.rpb + grp * q4;
+      for (int k = 0; k < q4; k += 8) {
+        float s1v[8], s2v[8], dv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const long long pp = r0 + u;
-        if (pp >= P) break;
-        const long long nrow = f.M - (long long)f.rpp * pp;
-        const float n = (float)(nrow < f.rpp ? (nrow < 0 ? 0 : nrow) : f.rpp);
-        const float s1 = p1[pp * C + c], s2 = p1[(P + pp) * C + c], d = p1[(2 * P + pp) * C + c] - x0;
-        sa += s1 + n * d;
-        sb += s2 + 2.f * d * s1 + n * d * d;
+        for (int u = 0; u < 8; ++u) {
+          const long long pp = rg + k + u;
+          const bool ok = pp < P;
+          s1v[u] = ok ? p1[pp * C + c] : 0.f;
+          s2v[u] = ok ? p1[(P + pp) * C + c] : 0.f;
+          dv[u] = ok ? p1[(2 * P + pp) * C + c] : x0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const long long pp = rg + k + u;
+          const long long nrow = pp < P ? f.M - (long long)f.rpp * pp : 0;
+          const float n = (float)(nrow < f.rpp ? (nrow < 0 ? 0 : nrow) : f.rpp);
+          const float d = dv[u] - x0;
+          sa += s1v[u] + n * d;
+          sb += s2v[u] + 2.f * d * s1v[u] + n * d * d;
+        }
       }
     }
   }
@@ -563,9 +575,10 @@ static int bn_fold_launch(const float* p1, const float* p2, long long nrows, int
                          f.cdb, f.cdg);
     return 0;
   }
-  // SRC 0 with many partial rows (the conv epilogue's 64-row planes): 128 rows per block keeps the reducer's serial
-  // pass short
-  f.rpb = (SRC == 0 && nrows > 4096) ? 128 : 32;
+  // many partial rows (the conv epilogues' 64-row tile partials): 128 rows per block keeps the reducer's serial pass
+  // short (stage-1 ResNet-50 tiles: 6272 partials -> 49 folded rows instead of 196)
+  // (bn_bwd_partial's <= 2048 block rows fold faster 32 to a block: measured 0.56 vs 0.66 ms/step)
+  f.rpb = ((SRC == 1 && nrows > 512) || nrows > 4096) ? 128 : 32;
   const long long S = (nrows + f.rpb - 1) / f.rpb;
   if (S > 65535) return -1;
   f.ticket = nullptr;
@@ -794,7 +807,7 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
   BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
           nullptr, nullptr, nullptr, nullptr, nullptr, 64};
   int rc;
-  if (S <= 64 && bn_fold_enabled()) {
+  if ((P + 127) / 128 <= 64 && bn_fold_enabled()) {
     // one launch: tile re-centring + fold + finalize
     rc = bn_fold_launch<T, 1, 0>(tstats, nullptr, P, C, ws, f, s);
   } else {
