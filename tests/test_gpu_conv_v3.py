@@ -204,3 +204,30 @@ def test_halo_rejects_unsupported_shapes():
     # 3x3 stride 2 and 5x5 are not halo shapes: the chooser must see 0 and fall back
     assert lib.dl4j_conv_wrw_halo_ws_floats(2, 9, 9, 64, 64, 3, 3, 2, 2, 1, 1, 1, 1, 5, 5, 0, 0, ctypes.byref(sp)) == 0
     assert lib.dl4j_conv_wrw_halo_ws_floats(2, 9, 9, 64, 64, 5, 5, 1, 1, 2, 2, 1, 1, 9, 9, 0, 0, ctypes.byref(sp)) == 0
+
+
+@pytest.mark.parametrize("N,H", [(2, 20), (16, 50), (8, 256), (9, 256)])
+def test_conv_tile_statistics_feed_batchnorm(cuda, N, H):
+    """Conv epilogue tile statistics -> BN forward at partial counts that take each fold path: one block (P <= 32),
+    128-row fold blocks (P = 625), the single-launch limit (P = 8192) and the two-stage reduce above it (P = 9216).
+    Running mean / var and the normalised output against fp32 torch (reference NN:nn/layers/normalization/
+    BatchNormalization.java:250-370)."""
+    from deeplearning4j_amd import ops
+    C = K = 64
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(N, C, H, H, generator=g) + 0.2).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 3, 3, generator=g) * 0.05).cuda().bfloat16()
+    y = conv_native.conv2d_fwd(x, w, None, (1, 1), (1, 1, 1, 1), (1, 1), want_stats=True)
+    assert hasattr(y, "_bn_tile_stats")
+    gamma = (torch.rand(K, generator=g) + 0.5).cuda()
+    beta = torch.randn(K, generator=g).cuda()
+    rm, rv = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
+    out, ctx = ops.bn_forward(y, gamma, beta, rm, rv, True, 0.9, 1e-5, True)
+    yf = y.float()
+    mean = yf.mean(dim=(0, 2, 3))
+    var = yf.var(dim=(0, 2, 3), unbiased=False)
+    _close(rm, 0.1 * mean, 1e-4)
+    _close(rv, 0.9 + 0.1 * (var + 1e-5), 1e-4)
+    ref = torch.relu((yf - mean.view(1, -1, 1, 1)) * torch.rsqrt(var + 1e-5).view(1, -1, 1, 1) * gamma.view(1, -1, 1, 1)
+                     + beta.view(1, -1, 1, 1))
+    _close(out, ref, 3e-2)
