@@ -192,18 +192,26 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ 
 
 // partial rows [nblk][C] -> out[C]: a block owns 64 channels, its 4 row groups sum every 4th partial row in a fixed
 // order and combine through LDS (the same shape as bn_reduce_rows; one thread per channel serialised 512 rows).
+// Eight independent loads per trip: two per trip left the 128-row BERT reduces latency-bound (6.5 us a launch).
 __global__ __launch_bounds__(256) void channel_sum_reduce(const float* __restrict__ part, int nblk, int C,
                                                           float* __restrict__ out) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
   float s0 = 0.f, s1 = 0.f;
   if (c < C) {
-    int b = grp;
-    for (; b + 4 < nblk; b += 8) {
-      s0 += part[(long long)b * C + c];
-      s1 += part[(long long)(b + 4) * C + c];
+    for (int b0 = grp; b0 < nblk; b0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < nblk ? part[(long long)b * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u];
+        s1 += v[u + 1];
+      }
     }
-    if (b < nblk) s0 += part[(long long)b * C + c];
   }
   __shared__ float red[256];
   red[threadIdx.x] = s0 + s1;
