@@ -251,7 +251,8 @@ __global__ void __launch_bounds__(64 * W) ln_bwd_block(const T* __restrict__ dy,
 }
 
 // out[0/1][N] = sum over P partial rows. Block = 32 columns x 8 row groups (coalesced 128-byte row reads), the 8
-// group sums combined through LDS.
+// group sums combined through LDS. Eight independent row loads per trip (one per trip was latency-bound: 16
+// dependent round trips for BERT's 128 partials).
 __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ part, int P, int N,
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                      float* __restrict__ dsum, int NP) {
@@ -262,7 +263,16 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce(const float* __restrict__ p
   if (j < NP * N) {
     const int which = j / N, col = j - which * N;
     const float* src = part + which * N + col;
-    for (int p = rg; p < P; p += 8) s += src[(long long)p * NP * N];
+    for (int p0 = rg; p0 < P; p0 += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + 8 * u;
+        v[u] = p < P ? src[(long long)p * NP * N] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
   }
   red[rg][cl] = s;
   __syncthreads();
