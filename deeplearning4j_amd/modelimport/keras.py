@@ -310,7 +310,9 @@ def _map_layer(kl, ctx):
     act = lambda: _act(cfg.get("activation", "linear"))  # noqa: E731
     if cls == "InputLayer":
         return _KLayer(name, "input", keras_class=cls, cfg=cfg)
-    if cls == "Dense":
+    if cls in ("Dense", "TimeDistributedDense"):
+        # Keras 1's TimeDistributedDense maps to the same DL4J DenseLayer (KER:utils/KerasLayerUtils.java:199-201);
+        # on a recurrent input the layer gets the usual RnnToFeedForward preprocessor
         units = cfg.get("units", cfg.get("output_dim"))
         hb = cfg.get("use_bias", cfg.get("bias", True))
         lay = L.DenseLayer(nOut=int(units), activation=act(), hasBias=bool(hb)) if "hasBias" in \
@@ -458,8 +460,11 @@ def _map_layer(kl, ctx):
                 _set(p, d + "b", np.asarray(bb).reshape(1, -1))
         return _KLayer(name, "layer", lay, setter=setter, keras_class=cls, cfg=cfg)
     if cls == "Embedding":
+        # input_length null = variable-length sequences: recurrent output type with unknown length (-1)
+        il = cfg.get("input_length")
+        il = il[0] if isinstance(il, (list, tuple)) else il
         lay = L.EmbeddingSequenceLayer(nIn=int(cfg["input_dim"]), nOut=int(cfg["output_dim"]),
-                                       inputLength=int(cfg.get("input_length") or 1), hasBias=False,
+                                       inputLength=int(il) if il is not None else -1, hasBias=False,
                                        activation=Activation.IDENTITY)
         return _KLayer(name, "layer", lay, setter=_embedding_setter, keras_class=cls, cfg=cfg)
     if cls == "ZeroPadding2D":
@@ -520,6 +525,8 @@ def _map_layer(kl, ctx):
 def _input_type(shape, channels_last=True):
     dims = [d for d in shape[1:]]
     if len(dims) == 1:
+        if dims[0] is None:                  # [mb, null]: variable-length index sequence
+            return InputType.recurrent(1, -1)
         return InputType.feedForward(int(dims[0]))
     if len(dims) == 2:
         T = dims[0] if dims[0] is not None else -1
@@ -562,27 +569,40 @@ class KerasModel:
 
     # ------------------------------------------------------------------ weights
     def _weights_for(self, lname):
+        """Keras weight arrays of one layer keyed by their parameter name ('kernel', 'W', 'W_i', ...).
+
+        Weight names carry optional TensorFlow name scopes in front of the layer name and the layer name itself
+        may contain '/' ('global/shared/dense_1/xxx/yyy_W:0' for layer 'dense_1/xxx/yyy'): the parameter name is
+        what follows the LAST occurrence of '<layer>_' or '<layer>/' (KER:utils/KerasModelUtils.java:170-300)."""
         if self.weights_root is None:
             return None
         root = self.weights_root
         if "model_weights" in root:
             root = root["model_weights"]
-        if lname not in root:
+        try:
+            grp = root[lname]
+        except (KeyError, Exception):
             return {}
-        grp = root[lname]
         names = grp.attrs.get("weight_names")
         out = {}
         if names is None:
             names = []
             grp.visit(lambda p, n: names.append(p) if isinstance(n, hdf5.Dataset) else None)
         for full in list(names):
+            full = full.decode() if isinstance(full, bytes) else str(full)
             ds = grp[full]
-            short = full.split("/")
-            key = short[-1].split(":")[0]
-            if len(short) >= 3:        # bidirectional: layer/forward_lstm_1/kernel:0
-                key = short[-2] + "/" + key
-            elif key.startswith(lname + "_"):
-                key = key[len(lname) + 1:]
+            stem = full.split(":")[0]
+            key = None
+            for sep in ("_", "/"):
+                i = stem.rfind(lname + sep)
+                if i >= 0 and (i == 0 or stem[i - 1] == "/"):
+                    key = stem[i + len(lname) + 1:]
+                    break
+            if key is None:
+                short = stem.split("/")
+                key = short[-1]
+                if len(short) >= 3:        # bidirectional: layer/forward_lstm_1/kernel:0
+                    key = short[-2] + "/" + key
             out[key] = ds.read()
         return out
 
@@ -606,10 +626,12 @@ class KerasModel:
                 shape = kl["config"]["batch_input_shape"]
                 continue
             mapped.append(_map_layer(kl, self.ctx))
-        t = _input_type(shape, cl)
-        if mapped and mapped[0].keras_class == "Embedding" and isinstance(t, InputTypeRecurrent) is False:
-            T = int(shape[1]) if len(shape) > 1 and shape[1] is not None else 1
-            t = InputType.recurrent(1, T)
+        if mapped and mapped[0].keras_class == "Embedding":
+            # index input [mb, T]: T may be null (variable length)
+            T = shape[1] if len(shape) > 1 else None
+            t = InputType.recurrent(1, int(T) if T is not None else -1)
+        else:
+            t = _input_type(shape, cl)
         b = NeuralNetConfiguration.Builder().weightInit("XAVIER").list()
         idx = 0
         pending = None
@@ -820,18 +842,20 @@ class KerasModelImport:
 
     @staticmethod
     def importKerasModelConfiguration(jsonOrPath, enforceTrainingConfig=False):
-        km = KerasModel(_load_json(jsonOrPath), enforce=enforceTrainingConfig)
+        cfg = _load_json(jsonOrPath)
+        km = KerasModel(cfg, keras_version=cfg.get("keras_version", "2"), enforce=enforceTrainingConfig)
         return km.getComputationGraphConfiguration()
 
     @staticmethod
     def importKerasSequentialConfiguration(jsonOrPath, enforceTrainingConfig=False):
-        km = KerasModel(_load_json(jsonOrPath), enforce=enforceTrainingConfig)
+        cfg = _load_json(jsonOrPath)
+        km = KerasModel(cfg, keras_version=cfg.get("keras_version", "2"), enforce=enforceTrainingConfig)
         return km.getMultiLayerConfiguration()
 
     @staticmethod
     def _model(modelHdf5OrJson, weightsHdf5, enforce):
-        p = str(modelHdf5OrJson)
-        if p.endswith(".json") or (isinstance(modelHdf5OrJson, str) and modelHdf5OrJson.lstrip().startswith("{")):
+        # JSON or HDF5 by content, not by extension ('model.json.with.tensorflow.scope' is JSON)
+        if isinstance(modelHdf5OrJson, dict) or _is_json(modelHdf5OrJson):
             cfg = _load_json(modelHdf5OrJson)
             w = hdf5.File(weightsHdf5) if weightsHdf5 else None
             kv = cfg.get("keras_version", "2") if isinstance(cfg, dict) else "2"
@@ -839,6 +863,18 @@ class KerasModelImport:
         f, mc, tc, kv, backend = _read_h5(modelHdf5OrJson)
         w = hdf5.File(weightsHdf5) if weightsHdf5 else f
         return KerasModel(mc, w, tc, kv, enforce, backend)
+
+
+def _is_json(x):
+    s = str(x)
+    if s.lstrip().startswith("{"):
+        return True
+    try:
+        with open(s, "rb") as fh:
+            head = fh.read(64).lstrip()
+    except OSError:
+        return s.endswith(".json")
+    return head.startswith(b"{")
 
 
 def _load_json(x):

@@ -10,6 +10,8 @@ import csv
 import glob
 import os
 
+PEAK_TF = 2500.0     # dense bf16 MFMA peak of an MI355X (no sparsity)
+
 
 def short(n):
     n = n.replace("(anonymous namespace)::", "").replace("void ", "")
@@ -59,6 +61,8 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--cus", type=int, default=256)
+    ap.add_argument("--hbm-tbs", type=float, default=8.0, help="HBM peak for the roofline (spec 8.0)")
+    ap.add_argument("--raw-fetch", action="store_true", help="do not double FETCH_SIZE")
     ap.add_argument("--last-step", action="store_true", help="only the dispatches of the last training step")
     a = ap.parse_args()
     merged = collections.defaultdict(dict)
@@ -74,26 +78,39 @@ def main():
     # MIOpen's find-mode benchmarking kernels (first call of a new shape) are not part of the steady state
     rows = [kv for kv in sorted(times.items(), key=lambda kv: -kv[1]) if not kv[0].startswith(("naive_conv", "_ZN2ck"))]
     rows = rows[:a.top]
-    print(f"{'kernel':<70} {'calls':>5} {'ms':>8} {'bf16 TF':>8} {'%peak':>6} {'LDSconf/inst':>12} "
-          f"{'HBM GB/s':>9} {'L2hit%':>6}")
+    print(f"{'kernel':<60} {'calls':>5} {'ms':>7} {'bf16 TF':>7} {'%peak':>5} {'LDSc/i':>6} {'rdMB':>8} {'wrMB':>8} "
+          f"{'GB/s':>7} {'L2hit%':>6} {'bound':>5} {'%roof':>5}")
+    tot_ns = tot_roof = 0.0
     for k, ns in rows:
         d = merged.get(k, {})
-        busy = d.get("SQ_BUSY_CYCLES", 0.0)
-        gui = d.get("GRBM_GUI_ACTIVE", 0.0)
         mfma = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
         if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in d:
-            tf = d["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / ns / 1e3 if ns else 0.0
+            flop = d["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512
         else:   # MFMA busy cycles (all SIMDs) x 1024 dense bf16 FLOP per SIMD-cycle (32x32x16 and 16x16x32 alike)
-            tf = mfma * 1024 / ns / 1e3 if ns else 0.0
-        peak = 100.0 * tf / 2500.0                       # dense bf16 MFMA peak of an MI355X (no sparsity)
+            flop = mfma * 1024
+        tf = flop / ns / 1e3 if ns else 0.0
+        peak = 100.0 * tf / PEAK_TF
         lds_c = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, d.get("SQ_INSTS_LDS", 0.0))
-        hbm = (d.get("FETCH_SIZE", 0.0) + d.get("WRITE_SIZE", 0.0)) * 1024 / ns if ns else 0.0
+        # FETCH_SIZE / WRITE_SIZE are KiB. gfx950 FETCH_SIZE tallies a wide coalesced stream at half its bytes
+        # (MI355X_MICROARCH.md, HBM): the read column is FETCH_SIZE x 2 (x1 with --raw-fetch)
+        rd = d.get("FETCH_SIZE", 0.0) * 1024 * (1 if a.raw_fetch else 2)
+        wr = d.get("WRITE_SIZE", 0.0) * 1024
+        gbs = (rd + wr) / ns if ns else 0.0
         hit, miss = d.get("TCC_HIT_sum", 0.0), d.get("TCC_MISS_sum", 0.0)
         l2 = 100.0 * hit / (hit + miss) if hit + miss else float("nan")
-        _ = (gui, total, mfma, busy)
-        print(f"{k:<70} {calls[k]:5d} {ns / 1e6:8.3f} {tf:8.1f} {peak:6.1f} {lds_c:12.3f} {hbm:9.1f} "
-              f"{l2:6.1f}")
-
+        # roofline: the kernel's own lower bound max(FLOP / MFMA peak, bytes / HBM peak)
+        t_mfma = flop / (PEAK_TF * 1e12) * 1e9
+        t_mem = (rd + wr) / (a.hbm_tbs * 1e12) * 1e9
+        t_roof = max(t_mfma, t_mem)
+        bound = "mfma" if t_mfma >= t_mem else "hbm"
+        roof = 100.0 * t_roof / ns if ns else 0.0
+        tot_ns += ns
+        tot_roof += t_roof
+        print(f"{k[:60]:<60} {calls[k]:5d} {ns / 1e6:7.3f} {tf:7.1f} {peak:5.1f} {lds_c:6.2f} {rd / 1e6:8.1f} "
+              f"{wr / 1e6:8.1f} {gbs:7.0f} {l2:6.1f} {bound:>5} {roof:5.1f}")
+    print(f"listed kernels: {tot_ns / 1e6:.3f} ms, roofline bound {tot_roof / 1e6:.3f} ms "
+          f"({100.0 * tot_roof / max(tot_ns, 1.0):.1f} %); all kernels {total / 1e6:.3f} ms; "
+          f"peaks {PEAK_TF:.0f} TF/s bf16 dense, {a.hbm_tbs:.1f} TB/s HBM")
 
 if __name__ == "__main__":
     main()
