@@ -41,7 +41,13 @@ def main():
     ap.add_argument("--comm", default=os.environ.get("BENCH_COMM", "torch"), choices=["torch", "rccl"],
                     help="N > 1 transport: torch.distributed's RCCL process group, or the framework's own RCCL "
                          "communicator (parallel/rccl.py, ncclCommInitRank with the id exchanged through the store)")
+    ap.add_argument("--inprocess", action="store_true",
+                    help="one process, one host thread per GPU (ParallelWrapper.inProcess: replicas on GPUs 0..N-1, "
+                         "RCCL communicators from ncclCommInitAll, graph-captured steps per worker); ignored under "
+                         "torchrun")
     args = ap.parse_args()
+    if args.inprocess and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        return main_inprocess(args)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from deeplearning4j_amd.models import ResNet50
@@ -80,8 +86,19 @@ def main():
     y = torch.zeros(B, 1000, device=device)
     y[torch.arange(B), torch.randint(0, 1000, (B,), generator=g).to(device)] = 1.0
 
+    # experiment switch: run the training step on a high-priority stream (the weight-gradient side stream keeps
+    # the default priority, so the main chain's kernels are dispatched first when both are queued)
+    prio_stream = None
+    if os.environ.get("DL4J_AMD_MAIN_PRIO", "0") == "1" and device.type == "cuda":
+        prio_stream = torch.cuda.Stream(device, priority=-1)
+        prio_stream.wait_stream(torch.cuda.current_stream(device))
+
     def step():
-        net.fit([x], [y])
+        if prio_stream is not None:
+            with torch.cuda.stream(prio_stream):
+                net.fit([x], [y])
+        else:
+            net.fit([x], [y])
 
     def sync():
         if device.type == "cuda":
@@ -124,6 +141,64 @@ def main():
         }), flush=True)
     from deeplearning4j_amd.parallel.distributed import destroy
     destroy()
+
+
+def main_inprocess(args):
+    """``--inprocess``: the reference's ParallelWrapper design on one node — N worker threads in this process, each
+    training a replica on its own GPU (parallel/inprocess.py), gradients all-reduced in buckets over RCCL
+    (ncclCommInitAll) on a per-device comm stream overlapping backward. Same model, batch per GPU and timing rule as
+    the torchrun path: W untimed warmup rounds, then K timed rounds between device synchronisations."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from deeplearning4j_amd.datasets.dataset import DataSet
+    from deeplearning4j_amd.models import ResNet50
+    from deeplearning4j_amd.nn.conf import DataType
+    from deeplearning4j_amd.parallel import ParallelWrapper, TrainingMode
+    N = args.gpus
+    torch.manual_seed(1234)
+    dt = DataType.BFLOAT16 if args.dtype == "bf16" else DataType.FLOAT
+    dev0 = torch.device("cuda", 0)
+    net = ResNet50(numLabels=1000, variant=args.variant, dataType=dt).init(device=dev0)
+    if args.graph != 0:
+        net.enableHipGraphs(True, warmup=1)
+    B = args.batch
+    g = torch.Generator(device="cpu").manual_seed(42)
+    per_dev = []
+    for i in range(N):            # one fixed batch per worker, already on its GPU (BenchmarkDataSetIterator)
+        d = torch.device("cuda", i)
+        x = torch.rand(B, 3, 224, 224, generator=g).to(d).contiguous(memory_format=torch.channels_last)
+        y = torch.zeros(B, 1000, device=d)
+        y[torch.arange(B), torch.randint(0, 1000, (B,), generator=g).to(d)] = 1.0
+        per_dev.append(DataSet(x.to(net.compute_dtype), y))
+    pw = (ParallelWrapper.Builder(net).workers(N).inProcess(True).prefetchBuffer(2 * N)
+          .trainingMode(TrainingMode.SHARED_GRADIENTS).build())
+
+    def sync():
+        for i in range(N):
+            torch.cuda.synchronize(i)
+    t_w = time.perf_counter()
+    pw.fit([per_dev[i % N] for i in range(N * max(1, args.warmup))], 1)
+    sync()
+    print(f"[bench] in-process warmup done, {time.perf_counter() - t_w:.1f}s", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    pw.fit([per_dev[i % N] for i in range(N * args.steps)], 1)
+    sync()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / args.steps * 1000.0
+    ips = B * N * args.steps / elapsed
+    model_name = "ResNet-50 (DL4J zoo ResNet50 graph)" if args.variant == "dl4j" else "ResNet-50 (canonical)"
+    print(json.dumps({
+        "metric": "images/sec (whole node) ResNet-50 training at 1/2/4/8 MI355X",
+        "value": round(ips, 2), "unit": "images/sec", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (random 224x224x3 images, one-hot labels; random-init weights)",
+        "config": {"model": model_name, "variant": args.variant, "global_batch": B * N, "per_gpu_batch": B,
+                   "seq_len": None, "image_size": 224, "parallelism": f"dp{N} (in-process threads)",
+                   "comm": "rccl (ncclCommInitAll)",
+                   "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
+                   "hip_graph": bool(args.graph != 0 and getattr(net, "_hipgraph", None) is not None),
+                   "final_score": net.score()},
+    }), flush=True)
 
 
 if __name__ == "__main__":

@@ -411,77 +411,101 @@ __device__ __forceinline__ void bn_fin_store(int c, int C, double a, double b, c
   }
 }
 
+// Work split (float4 over channels): a block covers 64 channels (blockIdx.x) and f.rpb partial rows (blockIdx.y);
+// lane q = tid & 15 owns channels 4q..4q+3 of the column, row group g = tid >> 4 takes rows g, g+16, ... of the
+// block's range, 8 rows (SRC 1: 3 planes x 8 float4) in flight per trip. The 16 row groups are summed in a fixed order
+// through LDS, the block's folded row goes out write-through (sc1 stores), and the last block of a column (ticket)
+// reads all S folded rows with the same 16-group split, sums in double and finalizes. Every sum has a fixed order, so
+// the result is bitwise reproducible. (The scalar-per-channel version read 4 bytes per lane per load and left the
+// many-partial folds latency-bound: 12 us per launch for 6272 tile partials.)
 template <typename T, int SRC, int FIN>
 __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, const float* __restrict__ p2,
                                                long long nrows, int C, float* __restrict__ q1,
                                                float* __restrict__ q2, BnFin f) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int grp = threadIdx.x >> 6;
-  float sa = 0.f, sb = 0.f;
-  if (c < C) {
+  const int lq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + 4 * lq;
+  const bool cok = c < C;                                  // C % 4 == 0 (host-checked)
+  float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+  const long long rbeg = (long long)blockIdx.y * f.rpb;
+  const long long rend = rbeg + f.rpb < nrows ? rbeg + f.rpb : nrows;
+  if (cok) {
     if (SRC == 0) {
-      // rpb rows per block: each of the 4 row groups takes rpb/4 consecutive rows, 8 loads in flight per trip
-      const int q4 = f.rpb / 4;
-      const long long rg = (long long)blockIdx.y * f.rpb + grp * q4;
-      for (int k = 0; k < q4; k += 8) {
-        float a[8], b[8];
+      for (long long r0 = rbeg + rg; r0 < rend; r0 += 16 * 8) {
+        float4 va[8], vb[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const long long r = rg + k + u;
-          const bool ok = r < nrows;
-          a[u] = ok ? p1[r * C + c] : 0.f;
-          b[u] = ok ? p2[r * C + c] : 0.f;
+          const long long r = r0 + 16 * u;
+          const bool ok = r < rend;
+          va[u] = ok ? *reinterpret_cast<const float4*>(p1 + r * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          vb[u] = ok ? *reinterpret_cast<const float4*>(p2 + r * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { sa += a[u]; sb += b[u]; }
+        for (int u = 0; u < 8; ++u) {
+          sa[0] += va[u].x; sa[1] += va[u].y; sa[2] += va[u].z; sa[3] += va[u].w;
+          sb[0] += vb[u].x; sb[1] += vb[u].y; sb[2] += vb[u].z; sb[3] += vb[u].w;
+        }
       }
     } else {
-      // same rpb split; a partial past P contributes zeros (n = 0, d = 0)
-      const float x0 = ld1<T>((const T*)f.x + c);
+      // tile partials: s1 = sum(y - y0), s2 = sum((y - y0)^2) about the tile's own shift y0 (plane 3), re-centred
+      // on the global shift x0 (row 0 of x); a tile holds f.rpp rows except the last
+      float x0[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x0[j] = ld1<T>((const T*)f.x + c + j);
       const long long P = nrows;
-      const int q4 = f.rpb / 4;
-      const long long rg = (long long)blockIdx.y * f.rpb + grp * q4;
-      for (int k = 0; k < q4; k += 8) {
-        float s1v[8], s2v[8], dv[8];
+      for (long long r0 = rbeg + rg; r0 < rend; r0 += 16 * 8) {
+        float4 v1[8], v2[8], vd[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const long long pp = rg + k + u;
-          const bool ok = pp < P;
-          s1v[u] = ok ? p1[pp * C + c] : 0.f;
-          s2v[u] = ok ? p1[(P + pp) * C + c] : 0.f;
-          dv[u] = ok ? p1[(2 * P + pp) * C + c] : x0;
+          const long long pp = r0 + 16 * u;
+          const bool ok = pp < rend;
+          v1[u] = ok ? *reinterpret_cast<const float4*>(p1 + pp * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          v2[u] = ok ? *reinterpret_cast<const float4*>(p1 + (P + pp) * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          vd[u] = ok ? *reinterpret_cast<const float4*>(p1 + (2 * P + pp) * C + c)
+                     : make_float4(x0[0], x0[1], x0[2], x0[3]);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const long long pp = rg + k + u;
-          const long long nrow = pp < P ? f.M - (long long)f.rpp * pp : 0;
+          const long long pp = r0 + 16 * u;
+          const long long nrow = pp < rend ? f.M - (long long)f.rpp * pp : 0;
           const float n = (float)(nrow < f.rpp ? (nrow < 0 ? 0 : nrow) : f.rpp);
-          const float d = dv[u] - x0;
-          sa += s1v[u] + n * d;
-          sb += s2v[u] + 2.f * d * s1v[u] + n * d * d;
+          const float e1[4] = {v1[u].x, v1[u].y, v1[u].z, v1[u].w};
+          const float e2[4] = {v2[u].x, v2[u].y, v2[u].z, v2[u].w};
+          const float ed[4] = {vd[u].x, vd[u].y, vd[u].z, vd[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = ed[j] - x0[j];
+            sa[j] += e1[j] + n * d;
+            sb[j] += e2[j] + 2.f * d * e1[j] + n * d * d;
+          }
         }
       }
     }
   }
-  __shared__ double rd[2][256];
+  // fixed-order sum of the 16 row groups: LDS [2][16][64] floats
+  __shared__ double rd[2][16 * 64];
   float* rf = reinterpret_cast<float*>(&rd[0][0]);
-  rf[threadIdx.x] = sa;
-  rf[256 + threadIdx.x] = sb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rf[rg * 64 + 4 * lq + j] = sa[j];
+    rf[1024 + rg * 64 + 4 * lq + j] = sb[j];
+  }
   __syncthreads();
+  const int ch = threadIdx.x & 63;                         // threads 0..63: one channel each
+  const int cc = blockIdx.x * 64 + ch;
   float ta = 0.f, tb = 0.f;
-  if (grp == 0) {
-    ta = rf[threadIdx.x] + rf[threadIdx.x + 64] + rf[threadIdx.x + 128] + rf[threadIdx.x + 192];
-    tb = rf[256 + threadIdx.x] + rf[256 + threadIdx.x + 64] + rf[256 + threadIdx.x + 128] + rf[256 + threadIdx.x + 192];
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) { ta += rf[g * 64 + ch]; tb += rf[1024 + g * 64 + ch]; }
   }
   if (gridDim.y == 1) {
-    if (grp == 0 && c < C) bn_fin_store<T, FIN>(c, C, (double)ta, (double)tb, f);
+    if (threadIdx.x < 64 && cc < C) bn_fin_store<T, FIN>(cc, C, (double)ta, (double)tb, f);
     return;
   }
   typedef __attribute__((address_space(1))) unsigned gq32;
-  if (grp == 0 && c < C) {
-    __hip_atomic_store((gq32*)(q1 + (long long)blockIdx.y * C + c), __float_as_uint(ta), __ATOMIC_RELAXED,
+  if (threadIdx.x < 64 && cc < C) {
+    __hip_atomic_store((gq32*)(q1 + (long long)blockIdx.y * C + cc), __float_as_uint(ta), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gq32*)(q2 + (long long)blockIdx.y * C + c), __float_as_uint(tb), __ATOMIC_RELAXED,
+    __hip_atomic_store((gq32*)(q2 + (long long)blockIdx.y * C + cc), __float_as_uint(tb), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -492,8 +516,7 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
     const bool last = old == gridDim.y - 1;
     if (last) {
       __hip_atomic_store((gq32*)&f.ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // one acquire for the block, then PLAIN loads that can all be in flight together (atomic loads are issued
-      // one after another: 16-64 dependent round trips made the reducer the slowest block)
+      // one acquire for the block, then PLAIN loads that can all be in flight together
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -501,30 +524,36 @@ __global__ __launch_bounds__(256) void bn_fold(const float* __restrict__ p1, con
   }
   __syncthreads();
   if (rf[0] == 0.f) return;
+  __syncthreads();                                   // rf[0] read by every wave before the array is reused
   const int S = gridDim.y;
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    constexpr int UL = 8;
-    for (int i0 = grp; i0 < S; i0 += 4 * UL) {
-      float va[UL], vb[UL];
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+  if (cok) {
+    for (int i0 = rg; i0 < S; i0 += 16 * 8) {
+      float4 va[8], vb[8];
 #pragma unroll
-      for (int u = 0; u < UL; ++u) {
-        const int i = i0 + 4 * u;
-        va[u] = i < S ? q1[(long long)i * C + c] : 0.f;
-        vb[u] = i < S ? q2[(long long)i * C + c] : 0.f;
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 16 * u;
+        va[u] = i < S ? *reinterpret_cast<const float4*>(q1 + (long long)i * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        vb[u] = i < S ? *reinterpret_cast<const float4*>(q2 + (long long)i * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < UL; ++u) { a += va[u]; b += vb[u]; }
+      for (int u = 0; u < 8; ++u) {
+        a[0] += va[u].x; a[1] += va[u].y; a[2] += va[u].z; a[3] += va[u].w;
+        b[0] += vb[u].x; b[1] += vb[u].y; b[2] += vb[u].z; b[3] += vb[u].w;
+      }
     }
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rd[0][rg * 64 + 4 * lq + j] = a[j];
+    rd[1][rg * 64 + 4 * lq + j] = b[j];
+  }
   __syncthreads();
-  rd[0][threadIdx.x] = a;
-  rd[1][threadIdx.x] = b;
-  __syncthreads();
-  if (grp == 0 && c < C) {
-    a = rd[0][threadIdx.x] + rd[0][threadIdx.x + 64] + rd[0][threadIdx.x + 128] + rd[0][threadIdx.x + 192];
-    b = rd[1][threadIdx.x] + rd[1][threadIdx.x + 64] + rd[1][threadIdx.x + 128] + rd[1][threadIdx.x + 192];
-    bn_fin_store<T, FIN>(c, C, a, b, f);
+  if (threadIdx.x < 64 && cc < C) {
+    double ra = 0.0, rb = 0.0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) { ra += rd[0][g * 64 + ch]; rb += rd[1][g * 64 + ch]; }
+    bn_fin_store<T, FIN>(cc, C, ra, rb, f);
   }
 }
 
@@ -578,7 +607,11 @@ static int bn_fold_launch(const float* p1, const float* p2, long long nrows, int
   // many partial rows (the conv epilogues' 64-row tile partials): 128 rows per block keeps the reducer's serial pass
   // short (stage-1 ResNet-50 tiles: 6272 partials -> 49 folded rows instead of 196)
   // (bn_bwd_partial's <= 2048 block rows fold faster 32 to a block: measured 0.56 vs 0.66 ms/step)
-  f.rpb = ((SRC == 1 && nrows > 512) || nrows > 4096) ? 128 : 32;
+  // 128 rows per block (one trip of 8 rows x 16 row groups); more per block once that would exceed 1024 blocks
+  // per channel column, so the last block's serial pass stays short
+  if (C % 4 != 0) return -1;
+  f.rpb = 128;
+  while ((nrows + f.rpb - 1) / f.rpb > 1024) f.rpb *= 2;
   const long long S = (nrows + f.rpb - 1) / f.rpb;
   if (S > 65535) return -1;
   f.ticket = nullptr;
@@ -807,7 +840,7 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
   BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
           nullptr, nullptr, nullptr, nullptr, nullptr, 64};
   int rc;
-  if ((P + 127) / 128 <= 64 && bn_fold_enabled()) {
+  if (bn_fold_enabled()) {
     // one launch: tile re-centring + fold + finalize
     rc = bn_fold_launch<T, 1, 0>(tstats, nullptr, P, C, ws, f, s);
   } else {

@@ -26,11 +26,67 @@ Eligibility: plain SGD-family optimizer, a capturable (or no) gradient accumulat
 (onForwardPass/onBackwardPass/onGradientCalculation), CUDA device, fixed shapes. Anything else falls back to the
 eager step transparently.
 """
+import contextlib
+import gc
 import logging
+import threading
 
 import torch
 
 log = logging.getLogger("deeplearning4j_amd")
+
+# Python GC stays off while ANY thread captures (a collected cycle owning GPU resources, released inside a capture,
+# would abort it); refcounted so that concurrent captures of the in-process ParallelWrapper's workers nest.
+_gc_lock = threading.Lock()
+_gc_state = {"n": 0, "was": False}
+
+# Captures use thread-local mode: each worker thread of the in-process ParallelWrapper captures its own replica's
+# step on its own device, and one thread's capture must not turn another thread's (legal) calls into errors.
+CAPTURE_MODE = "thread_local"
+
+
+_cap_streams = threading.local()
+
+
+def capture(g, pool, fn, device=None):
+    """Capture ``fn()`` into CUDAGraph ``g`` (memory from ``pool``) on a capture stream owned by THIS thread and
+    device, in thread-local capture mode, and return fn's result.
+
+    torch.cuda.graph's context manager is not used: it captures on ONE process-wide default capture stream and
+    enters with a device-wide synchronize + empty_cache, which breaks concurrent captures by the in-process
+    ParallelWrapper's worker threads (one per GPU)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    streams = _cap_streams.__dict__.setdefault("s", {})
+    s = streams.get(dev.index)
+    if s is None:
+        s = streams[dev.index] = torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        g.capture_begin(pool=pool, capture_error_mode=CAPTURE_MODE)
+        try:
+            out = fn()
+        finally:
+            g.capture_end()
+    cur.wait_stream(s)
+    return out
+
+
+@contextlib.contextmanager
+def capture_gc_guard():
+    with _gc_lock:
+        if _gc_state["n"] == 0:
+            gc.collect()
+            _gc_state["was"] = gc.isenabled()
+            gc.disable()
+        _gc_state["n"] += 1
+    try:
+        yield
+    finally:
+        with _gc_lock:
+            _gc_state["n"] -= 1
+            if _gc_state["n"] == 0 and _gc_state["was"]:
+                gc.enable()
 
 
 class CapturedTrainingStep:
@@ -103,13 +159,11 @@ class CapturedTrainingStep:
         native.prepare_graph_slots(plan, n.device, n.conf.iterationCount, n.conf.epochCount)
         if self.tbptt_back is not None:
             self._bind_state()
-        torch.cuda.synchronize()
+        torch.cuda.current_stream(n.device).synchronize()
         # no Python GC while capturing: a collected cycle that owns GPU resources (events, other pools' blocks,
         # a previous network's buffers) would be released inside the capture and abort it
-        import gc
-        gc.collect()
-        gc_was_enabled = gc.isenabled()
-        gc.disable()
+        guard = capture_gc_guard()
+        guard.__enter__()
         # the recurrent state maps every slot's capture must start from (empty for a sequence's first window)
         start_maps = [(l, dict(l.tBpttStateMap)) for l in self._recurrent_layers()]
         try:
@@ -120,8 +174,7 @@ class CapturedTrainingStep:
                 g = torch.cuda.CUDAGraph()
                 native.GRAPH_SLOT[0] = slot
                 n._capturing = True
-                with torch.cuda.graph(g, pool=self.pool):
-                    self.score_t[slot] = self._body()
+                self.score_t[slot] = capture(g, self.pool, self._body, n.device)
                 self.graphs.append(g)
                 # the A and B graphs own different output tensors: remember which ones this slot writes
                 self.out_state.append([(l, k, v) for l in self._recurrent_layers()
@@ -131,8 +184,7 @@ class CapturedTrainingStep:
         finally:
             native.GRAPH_SLOT[0] = None
             n._capturing = False
-            if gc_was_enabled:
-                gc.enable()
+            guard.__exit__(None, None, None)
         _ = plan
         return self.ok
 
@@ -191,6 +243,8 @@ def graph_eligible(net, inputs, labels, fmasks, lmasks, tbptt_window=False):
     acc = getattr(net, "gradientsAccumulator", None)
     if acc is not None and not (hasattr(acc, "capturable") and acc.capturable()):
         return False                               # gloo / custom accumulators: eager steps
+    if acc is not None and getattr(acc, "participants", None):
+        return False                               # partial data-parallel round: its divisor is not the captured one
     algo = net.conf.globalConf.get("optimizationAlgo")
     if algo is not None and OA.of(algo) != OA.STOCHASTIC_GRADIENT_DESCENT:
         return False

@@ -379,6 +379,19 @@ class BaseNetwork:
     def setGradientsAccumulator(self, acc):
         self.gradientsAccumulator = acc
 
+    def _zero_contribution_step(self, batch_size):
+        """A data-parallel replica with no batch in the trailing partial round of an epoch (reference
+        PW:ParallelWrapper.java:514-578 trains such a round on the first ``locker`` workers only): it contributes a
+        zero gradient to the round's all-reduce and applies the same update as the replicas that trained, so all
+        replicas stay identical."""
+        self.flattenedGradients.zero_()
+        acc = getattr(self, "gradientsAccumulator", None)
+        if acc is not None and hasattr(acc, "begin_backward"):
+            acc.begin_backward(self)
+        self._loss_part = None
+        self._apply_update(batch_size)
+        self._iteration_done()
+
     # ------------------------------------------------------------------------------ update step
     def _apply_update(self, batch_size):
         it, ep = self.conf.iterationCount, self.conf.epochCount
@@ -410,7 +423,8 @@ class BaseNetwork:
         if acc is not None and not getattr(acc, "average", False):
             # summed gradients of every replica: divide by the global batch (an averaging accumulator already did
             # the 1/world part); user accumulators without a world_size count as one replica
-            batch_size = batch_size * getattr(acc, "world_size", 1)
+            # (a partial data-parallel round divides by the replicas that really trained: ``participants``)
+            batch_size = batch_size * (getattr(acc, "participants", None) or getattr(acc, "world_size", 1))
         reg = None
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
             reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)

@@ -7,6 +7,8 @@ outside what the kernel supports (the caller then uses the torch/library path).
 import ctypes
 import os
 
+import threading
+
 import numpy as np
 import torch
 
@@ -166,8 +168,27 @@ def _gn_block_ranges(plan, chunk):
     plan._gn_ranges = (chunk, ranges)
     return ranges
 
-# graph slot currently being captured / replayed (None = eager)
-GRAPH_SLOT = [None]
+class _ThreadSlot(threading.local):
+    """``GRAPH_SLOT[0]``: the graph slot THIS host thread is capturing (None = eager). Thread-local, so the
+    in-process ParallelWrapper's workers (one thread per GPU) can capture their replicas' steps concurrently
+    without seeing each other's slot."""
+
+    def __init__(self):
+        self.v = None
+
+    def __getitem__(self, i):
+        if i != 0:
+            raise IndexError(i)
+        return self.v
+
+    def __setitem__(self, i, val):
+        if i != 0:
+            raise IndexError(i)
+        self.v = val
+
+
+# graph slot currently being captured / replayed by this thread (None = eager)
+GRAPH_SLOT = _ThreadSlot()
 
 
 def seg_table_bytes(plan, iteration, epoch):

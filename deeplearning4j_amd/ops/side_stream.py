@@ -22,7 +22,6 @@ import threading
 import torch
 
 _tl = threading.local()
-_streams = {}
 LAUNCHES = [0]   # side-stream launches so far (tests check the overlap path really ran)
 
 
@@ -31,9 +30,12 @@ def enabled():
 
 
 def _side(dev):
-    s = _streams.get(dev.index)
+    # one side stream per (host thread, device): a stream shared by two threads would join one thread's HIP-graph
+    # capture and pull the other thread's weight-gradient launches into it (in-process ParallelWrapper workers)
+    streams = _tl.__dict__.setdefault("streams", {})
+    s = streams.get(dev.index)
     if s is None:
-        s = _streams[dev.index] = torch.cuda.Stream(dev)
+        s = streams[dev.index] = torch.cuda.Stream(dev)
     return s
 
 

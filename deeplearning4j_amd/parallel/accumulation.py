@@ -57,6 +57,11 @@ class AllReduceGradientsAccumulator:
         self._staging = None
         self._pending = []
         self._next = 0
+        # replicas that trained in this round (None = all): set by the in-process wrapper for a trailing partial
+        # round, where idle replicas contribute zero gradients and the divisor counts only the active ones
+        self.participants = None
+        self._comm_streams = {}
+        self._comm_forked = None
 
     # ``active`` / ``world_size`` are looked up at use, not frozen at construction: an accumulator built before
     # init_distributed() must still all-reduce once the group exists.
@@ -106,19 +111,40 @@ class AllReduceGradientsAccumulator:
         self._pending = []
         self._next = 0
 
+    def _comm_stream(self, dev):
+        """High-priority stream per device for the direct-RCCL buckets: a bucket forks from the compute stream
+        (event), so its all-reduce overlaps the rest of backward, and reduce_gradients joins it back before the
+        update reads the gradients. Both edges are events, so a HIP-graph capture records them as graph edges."""
+        s = self._comm_streams.get(dev.index)
+        if s is None:
+            s = self._comm_streams[dev.index] = torch.cuda.Stream(dev, priority=-1)
+        return s
+
     def _issue(self, g, i):
         s, e = self._buckets[i]
         seg = g[s:e]
         tmp = self._staging[i] if self._staging is not None else None
-        if tmp is not None:
-            tmp.copy_(seg)
         buf = tmp if tmp is not None else seg
         if self.comm is not None:
-            # stream-ordered on the current stream: later kernels see the result, nothing to wait for on the host
+            if g.is_cuda:
+                cs = self._comm_stream(g.device)
+                cs.wait_stream(torch.cuda.current_stream(g.device))
+                self._comm_forked = cs
+                with torch.cuda.stream(cs):
+                    if tmp is not None:
+                        tmp.copy_(seg)
+                    self.comm.all_reduce(buf, "sum")
+                    if tmp is not None:
+                        seg.copy_(tmp)
+                return
+            if tmp is not None:
+                tmp.copy_(seg)
             self.comm.all_reduce(buf, "sum")
             if tmp is not None:
                 seg.copy_(tmp)
             return
+        if tmp is not None:
+            tmp.copy_(seg)
         self._pending.append((dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True), tmp, seg))
 
     joins_side_stream = True   # grad_ready joins ops/side_stream itself, only when a bucket is issued
@@ -149,8 +175,11 @@ class AllReduceGradientsAccumulator:
                 seg.copy_(tmp)
         self._pending = []
         self._next = 0
+        if self._comm_forked is not None:  # join the direct-RCCL comm stream before anything reads the gradients
+            torch.cuda.current_stream(net.flattenedGradients.device).wait_stream(self._comm_forked)
+            self._comm_forked = None
         if self.average:                   # mean over replicas (the update then divides by the local batch only)
-            net.flattenedGradients.div_(self.world_size)
+            net.flattenedGradients.div_(self.participants or self.world_size)
 
     def broadcast_params(self, net, src=0):
         """Make every replica start from rank ``src``'s parameters and updater state."""

@@ -14,12 +14,19 @@ MI355X design:
   * AVERAGING: local steps, parameters (+ updater state) all-reduced and divided by N every k rounds;
   * streaming: the master pulls one round (N batches) at a time from the iterator and hands batch i of the round to
     worker i through a queue of capacity ``prefetchBuffer // N`` (>= 1); at most ``prefetchBuffer + 2N`` batches
-    (queued, in training, and the round being handed out) exist at once however long the iterator is. A trailing partial round is dropped (every worker must run the
-    same number of collectives);
+    (queued, in training, and the round being handed out) exist at once however long the iterator is;
+  * a trailing partial round of L < N batches trains on the first L workers (reference :514-578,
+    ``registerConsumers(locker)``); the other workers still run the round's collectives with a zero gradient, and the
+    update divides by the L batches that were really trained on (SHARED_GRADIENTS), so every replica stays equal;
+  * HIP graphs: replicas inherit the caller's ``enableHipGraphs`` mode and each worker thread captures its own
+    replica's step (thread-local capture mode, per-thread capture streams and graph slots, nn/hipgraph.py);
+  * no per-batch host sync: each worker records an event per step and waits only for the step ``max_inflight``
+    rounds back, so the next batch's host work and H2D copy overlap the GPU;
   * failure: a worker exception aborts every communicator (waiting ranks raise instead of hanging), the other
     workers are drained and the master re-raises it.
 Listeners fire on worker 0, i.e. on the caller's own model (the reference attaches them to the root model too).
 """
+import collections
 import logging
 import queue
 import threading
@@ -44,6 +51,8 @@ def _replica(model, device):
         net.updater.setStateViewArray(st.detach().to(device).clone())
     net.conf.iterationCount = model.conf.iterationCount
     net.conf.epochCount = model.conf.epochCount
+    if getattr(model, "_hipgraph_enabled", False):       # replicas train exactly like the caller's model
+        net.enableHipGraphs(True, warmup=getattr(model, "_hipgraph_warmup", 2))
     return net
 
 
@@ -60,10 +69,16 @@ def _fit_one(m, ds):
         raise TypeError(f"unsupported batch type {type(ds)}")
 
 
-def devices_for(n):
-    """GPUs 0..n-1 when this process sees at least n, else the CPU for every worker."""
+def devices_for(n, model=None):
+    """GPUs 0..n-1 when this process sees at least n; the CPU for every worker when the model itself lives on the
+    CPU. A model on a GPU with fewer than n GPUs visible is an error (mixing one GPU worker with CPU replicas would
+    be silently far slower): use fewer workers, or one process per device (torchrun / inProcess(False))."""
     if torch.cuda.is_available() and torch.cuda.device_count() >= n:
         return [torch.device("cuda", i) for i in range(n)]
+    dev = getattr(model, "device", None) if model is not None else None
+    if dev is not None and torch.device(dev).type == "cuda":
+        raise RuntimeError(f"in-process ParallelWrapper: {n} workers need {n} visible GPUs, this process sees "
+                           f"{torch.cuda.device_count()}; reduce workers() or use one process per device")
     return [torch.device("cpu")] * n
 
 
@@ -81,7 +96,7 @@ class InProcessTrainer:
     def __init__(self, wrapper, devices=None, comms=None):
         self.w = wrapper
         n = int(wrapper.workers)
-        self.devices = list(devices) if devices is not None else devices_for(n)
+        self.devices = list(devices) if devices is not None else devices_for(n, wrapper.model)
         m = wrapper.model
         if not m.initCalled:
             m.init(device=self.devices[0])
@@ -100,6 +115,7 @@ class InProcessTrainer:
         self.max_live = 0           # most batches alive at once (tests check the streaming bound)
         self._live = 0
         self._threads = []
+        self.max_inflight = 2       # GPU steps a worker may have queued before it waits on the oldest one
 
     # ------------------------------------------------------------------------------------------------ workers
     def _run(self, i):
@@ -107,6 +123,7 @@ class InProcessTrainer:
         from .wrapper import TrainingMode
         avg = self.w.trainingMode == TrainingMode.AVERAGING
         k = self.w.averagingFrequency
+        inflight = collections.deque()
         try:
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
@@ -114,17 +131,34 @@ class InProcessTrainer:
                 item = q.get()
                 if item is _STOP:
                     break
-                ds, rnd = item
-                _fit_one(net, ds)                   # the network moves the batch to its device
-                with self.cv:
-                    self._live -= 1
+                ds, rnd, active, bsz = item
+                acc = getattr(net, "gradientsAccumulator", None)
+                if active < len(self.models) and acc is not None:
+                    acc.participants = active           # partial round: divide by the batches trained on
+                try:
+                    if ds is not None:
+                        _fit_one(net, ds)               # the network moves the batch to its device
+                    elif self.shared:
+                        net._zero_contribution_step(bsz)
+                finally:
+                    if acc is not None:
+                        acc.participants = None
+                if ds is not None:
+                    with self.cv:
+                        self._live -= 1
                 if avg and (rnd + 1) % k == 0:
                     average_params_and_state(net, self.w.averageUpdaters, comm=comm)
                 if dev.type == "cuda":
-                    torch.cuda.current_stream(dev).synchronize()
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    inflight.append(ev)
+                    while len(inflight) > self.max_inflight:
+                        inflight.popleft().synchronize()
                 with self.cv:
                     self.rounds_done[i] = rnd + 1
                     self.cv.notify_all()
+            while inflight:
+                inflight.popleft().synchronize()
         except BaseException as e:          # noqa: BLE001 — propagated to the master
             with self.cv:
                 self.errors.append((i, e))
@@ -173,11 +207,13 @@ class InProcessTrainer:
                     if hasattr(l, "onEpochStart"):
                         l.onEpochStart(m)
                 for batch_round in _rounds(source, n):
+                    L = len(batch_round)
+                    bsz = _batch_size(batch_round[0])
                     with self.cv:
-                        self._live += n             # pulled from the iterator and not yet trained on
+                        self._live += L             # pulled from the iterator and not yet trained on
                         self.max_live = max(self.max_live, self._live)
-                    for i, ds in enumerate(batch_round):
-                        self._put(i, (ds, rnd))
+                    for i in range(n):
+                        self._put(i, (batch_round[i] if i < L else None, rnd, L, bsz))
                     rnd += 1
                 self._wait_rounds(rnd)
                 for net in self.models:
@@ -232,9 +268,17 @@ class InProcessTrainer:
         self._threads = []
 
 
+def _batch_size(ds):
+    if ds is None:
+        return 1
+    f = ds.features
+    f = f[0] if isinstance(f, (list, tuple)) else f
+    return int(f.shape[0])
+
+
 def _rounds(source, n):
-    """Stream complete rounds of n batches from a DataSetIterator / MultiDataSetIterator / iterable; a trailing
-    partial round is dropped."""
+    """Stream rounds of n batches from a DataSetIterator / MultiDataSetIterator / iterable; the last round may be
+    partial (fewer than n batches)."""
     if isinstance(source, (DataSet, MultiDataSet)):
         source = [source]
     if hasattr(source, "hasNext"):
@@ -248,12 +292,12 @@ def _rounds(source, n):
     else:
         it = iter(source)
     buf = []
-    dropped = 0
     for ds in it:
         buf.append(ds)
         if len(buf) == n:
             yield buf
             buf = []
-    dropped = len(buf)
-    if dropped:
-        log.info("ParallelWrapper: %d trailing batch(es) of an incomplete round of %d dropped", dropped, n)
+    if buf:
+        log.debug("ParallelWrapper: trailing round of %d batch(es) trains on the first %d of %d workers",
+                  len(buf), len(buf), n)
+        yield buf

@@ -435,24 +435,45 @@ class SameDiff:
             self.variables[out].value = y
             self._ctx[out] = ctx
 
-    def _backward(self, seeds, wrt, targets=None):
+    def _backward(self, seeds, wrt, targets=None, on_final=None):
         """Reverse pass from ``seeds`` {variable name: upstream gradient} over the recorded ops; returns
-        {name: gradient} for ``wrt`` (every op's explicit backward; no torch.autograd)."""
+        {name: gradient} for ``wrt`` (every op's explicit backward; no torch.autograd).
+
+        ``on_final(name, grad)``: called for each ``wrt`` variable as soon as its gradient is complete, i.e. right
+        after the reverse pass has processed the EARLIEST recorded op that reads it (later ops were processed
+        first). Data-parallel training uses it to start each gradient bucket's all-reduce while the rest of the
+        reverse pass still runs."""
         grads = dict(seeds)
         tg = targets if targets is not None else list(seeds)
         # the planned (fused) records only when their contexts come from a planned execution of these targets
         recs = self._plan(tg) if self._executed == tuple(tg) else self._needed(tg)
-        for out, op, refs, attrs in reversed(recs):
+        final_at = {}
+        if on_final is not None:
+            want = set(wrt)
+            for i, (_, _, refs, _) in enumerate(recs):
+                for r in refs:
+                    if isinstance(r, str) and r in want and r not in final_at:
+                        final_at[r] = i
+            by_pos = {}
+            for name, i in final_at.items():
+                by_pos.setdefault(i, []).append(name)
+            for name in wrt:                    # read by no op on the path to the targets: final (None) now
+                if name not in final_at:
+                    on_final(name, grads.get(name))
+        for i in range(len(recs) - 1, -1, -1):
+            out, op, refs, attrs = recs[i]
             g = grads.get(out)
-            if g is None:
-                continue
-            ins = [self._val(r) for r in refs]
-            gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
-            for r, gi in zip(refs, gins):
-                if gi is None or not isinstance(r, str):
-                    continue
-                prev = grads.get(r)
-                grads[r] = gi if prev is None else prev + gi
+            if g is not None:
+                ins = [self._val(r) for r in refs]
+                gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
+                for r, gi in zip(refs, gins):
+                    if gi is None or not isinstance(r, str):
+                        continue
+                    prev = grads.get(r)
+                    grads[r] = gi if prev is None else prev + gi
+            if on_final is not None:
+                for name in by_pos.get(i, ()):
+                    on_final(name, grads.get(name))
         self._last_grads = {k: grads.get(k) for k in wrt}
         return self._last_grads
 
@@ -562,22 +583,29 @@ class SameDiff:
         vs = self.trainableVariables()
         self._exec(feeds, self._loss_names)
         seeds = {n: torch.full_like(self.variables[n].value, sign) for n in self._loss_names}
-        grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
         if "views" not in st:
             off, st["views"] = 0, []
             for v in vs:
                 st["views"].append(st["grad"][off:off + v.value.numel()].view(v.value.shape))
                 off += v.value.numel()
-        dst, src = [], []
-        for v, view in zip(vs, st["views"]):
-            g = grads.get(v.name)
-            if g is None:
-                view.zero_()
-            else:
-                dst.append(view)
-                src.append(g.reshape(view.shape))
-        torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
-        self._allreduce(st)
+        dp = self._dp_buckets(st)
+        if dp is not None:
+            # data parallel: each variable's gradient goes into the flat buffer as soon as it is final, and a bucket's
+            # all-reduce starts once all of its variables are, overlapping the rest of the reverse pass
+            dp.begin()
+            self._backward(seeds, [v.name for v in vs], list(self._loss_names), on_final=dp.final)
+            dp.finish()
+        else:
+            grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
+            dst, src = [], []
+            for v, view in zip(vs, st["views"]):
+                g = grads.get(v.name)
+                if g is None:
+                    view.zero_()
+                else:
+                    dst.append(view)
+                    src.append(g.reshape(view.shape))
+            torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
         fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount, self.epochCount, 1,
                      mini_batch=False, shadow=st["shadow"])
         out = None
@@ -623,7 +651,6 @@ class SameDiff:
         return self._graph_capture(feeds)
 
     def _graph_capture(self, feeds):
-        import gc
         from ..ops import native
         st = self._train_state
         sign = 1.0 if self.trainingConfig.minimize else -1.0
@@ -631,16 +658,16 @@ class SameDiff:
         g = {"static": static, "graphs": [], "loss": [None, None], "k": 0, "ok": False,
              "pool": torch.cuda.graph_pool_handle()}
         native.prepare_graph_slots(st["plan"], st["flat"].device, self.iterationCount, self.epochCount)
-        torch.cuda.synchronize()
-        gc.collect()
-        was = gc.isenabled()
-        gc.disable()
+        torch.cuda.current_stream(st["flat"].device).synchronize()
+        from ..nn.hipgraph import capture, capture_gc_guard
+        guard = capture_gc_guard()
+        guard.__enter__()
         try:
             for slot in (0, 1):
                 cg = torch.cuda.CUDAGraph()
                 native.GRAPH_SLOT[0] = slot
-                with torch.cuda.graph(cg, pool=g["pool"]):
-                    g["loss"][slot] = self._train_body(static, sign)
+                g["loss"][slot] = capture(cg, g["pool"], lambda: self._train_body(static, sign),
+                                          st["flat"].device)
                 g["graphs"].append(cg)
             g["ok"] = True
         except Exception as e:          # capture not possible for this graph: stay eager
@@ -649,8 +676,7 @@ class SameDiff:
             g["ok"] = False
         finally:
             native.GRAPH_SLOT[0] = None
-            if was:
-                gc.enable()
+            guard.__exit__(None, None, None)
         self._graph = g                 # (capture only records: parameters are untouched until the first replay)
         return g["ok"]
 
@@ -667,22 +693,18 @@ class SameDiff:
         g["k"] += 1
         return float(g["loss"][slot])
 
-    def _allreduce(self, st):
-        """Data parallel (one process per GPU, torch.distributed over RCCL / gloo): average the flat fp32 gradient
-        across ranks in buckets before the fused update, so every rank applies the same step (the reference's
-        ParallelWrapper gradient sharing for SameDiff graphs). Bucket size: DL4J_AMD_BUCKET_MB (default 64 MB,
-        large buckets for xGMI rings)."""
+    def _dp_buckets(self, st):
+        """The data-parallel bucket plan (one process per GPU, torch.distributed over RCCL / gloo), or None when
+        training on one rank. See _SDGradBuckets."""
         import torch.distributed as dist
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-            return
-        import os
-        g = st["grad"]
-        world = dist.get_world_size()
-        step = max(1, int(float(os.environ.get("DL4J_AMD_BUCKET_MB", "64")) * (1 << 20)) // g.element_size())
-        for off in range(0, g.numel(), step):
-            dist.all_reduce(g[off:off + step])
-        g.div_(world)
+            return None
+        b = st.get("dp")
+        if b is None:
+            b = st["dp"] = _SDGradBuckets(self, st)
+        return b
 
+    # ------------------------------------------------------------------ save / load
     # ------------------------------------------------------------------ save / load
     def save(self, path, saveUpdaterState=False):
         """Graph JSON (variables with kinds / shapes / dtypes, op records, loss variables) + variable arrays
@@ -820,3 +842,83 @@ def _install():
 _install()
 
 __all__ = ["SameDiff", "SDVariable", "TrainingConfig"]
+
+
+class _SDGradBuckets:
+    """Bucketed, overlapped gradient all-reduce for SameDiff data parallelism (the reference shares SameDiff
+    gradients through ParallelWrapper; SURVEY §5.8: buckets overlap the reverse pass).
+
+    The flat fp32 gradient is cut into buckets of whole variables (DL4J_AMD_BUCKET_MB, default 32 MB). The reverse
+    pass reports each trainable variable the moment its gradient is final (SameDiff._backward ``on_final``); the
+    gradient is copied into its flat view and, once every variable of a bucket is in, the bucket's all-reduce is
+    issued asynchronously (torch.distributed: RCCL's own stream on GPUs, so it runs while the reverse pass goes on).
+    ``finish`` waits for all buckets and averages by the world size. Wire dtype: DL4J_AMD_SD_COMM_DTYPE=bf16|fp16
+    halves the bytes (persistent staging buffers, stable addresses for HIP-graph capture)."""
+
+    def __init__(self, sd, st):
+        import os
+        self.st = st
+        vs = sd.trainableVariables()
+        g = st["grad"]
+        per = max(1, int(float(os.environ.get("DL4J_AMD_BUCKET_MB", "32")) * (1 << 20)) // g.element_size())
+        self.var_bucket = {}
+        self.view = {}
+        self.buckets = []            # [start, end, n_vars]
+        off = 0
+        cur = None
+        for v, view in zip(vs, st["views"]):
+            k = v.value.numel()
+            if cur is None or cur[1] - cur[0] >= per:
+                cur = [off, off, 0]
+                self.buckets.append(cur)
+            cur[1] = off + k
+            cur[2] += 1
+            self.var_bucket[v.name] = len(self.buckets) - 1
+            self.view[v.name] = view
+            off += k
+        wire = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(os.environ.get("DL4J_AMD_SD_COMM_DTYPE", ""))
+        self.staging = None
+        if wire is not None and wire != g.dtype:
+            self.staging = [torch.empty(e - s, dtype=wire, device=g.device) for s, e, _ in self.buckets]
+        self.left = []
+        self.pending = []
+
+    def begin(self):
+        self.left = [n for _, _, n in self.buckets]
+        self.pending = []
+
+    def final(self, name, grad):
+        b = self.var_bucket.get(name)
+        if b is None:
+            return
+        view = self.view[name]
+        if grad is None:
+            view.zero_()
+        else:
+            view.copy_(grad.reshape(view.shape))
+        self.left[b] -= 1
+        if self.left[b] == 0:
+            self._issue(b)
+
+    def _issue(self, b):
+        import torch.distributed as dist
+        s, e, _ = self.buckets[b]
+        seg = self.st["grad"][s:e]
+        tmp = self.staging[b] if self.staging is not None else None
+        if tmp is not None:
+            tmp.copy_(seg)
+        work = dist.all_reduce(tmp if tmp is not None else seg, async_op=True)
+        self.pending.append((work, tmp, seg))
+
+    def finish(self):
+        import torch.distributed as dist
+        for b, n in enumerate(self.left):      # buckets whose variables got no report (defensive): issue now
+            if n > 0:
+                self.left[b] = 0
+                self._issue(b)
+        for work, tmp, seg in self.pending:
+            work.wait()
+            if tmp is not None:
+                seg.copy_(tmp)
+        self.pending = []
+        self.st["grad"].div_(dist.get_world_size())

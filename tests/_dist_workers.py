@@ -246,7 +246,8 @@ def run_samediff_dp(rank, world, port, result_path):
     gathered = [torch.empty_like(p) for _ in range(world)]
     dist.all_gather(gathered, p)
     if rank == 0:
-        torch.save({"params": [t.clone() for t in gathered]}, result_path)
+        torch.save({"params": [t.clone() for t in gathered],
+                    "nbuckets": len(sd._train_state["dp"].buckets)}, result_path)
     dist.barrier()
     dist.destroy_process_group()
 

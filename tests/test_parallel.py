@@ -215,12 +215,18 @@ def test_cg_shared_gradients_bucketed_equals_large_batch(tmp_path):
     assert torch.allclose(net.params(), p0, atol=1e-5), (net.params() - p0).abs().max()
 
 
-def test_samediff_data_parallel_equals_large_batch(tmp_path):
+@pytest.mark.parametrize("bucket_mb", ["32", "0.00002"])
+def test_samediff_data_parallel_equals_large_batch(tmp_path, monkeypatch, bucket_mb):
     """SameDiff DP-2 (gloo): each rank fits half of every batch, gradients averaged across ranks before the fused
-    update == one process fitting the whole batch."""
+    update == one process fitting the whole batch. With tiny buckets every variable is its own bucket, issued from
+    the reverse pass the moment its gradient is final (samediff _SDGradBuckets)."""
+    monkeypatch.setenv("DL4J_AMD_BUCKET_MB", bucket_mb)
     path = str(tmp_path / "sd.pt")
     mp.spawn(W.run_samediff_dp, args=(2, _port(), path), nprocs=2, join=True)
-    p0, p1 = torch.load(path, weights_only=True)["params"]
+    res = torch.load(path, weights_only=True)
+    p0, p1 = res["params"]
+    if bucket_mb != "32":
+        assert res["nbuckets"] > 2
     assert torch.equal(p0, p1)
     sd = W.make_samediff()
     for ds in W.samediff_batches():

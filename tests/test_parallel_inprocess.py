@@ -126,3 +126,45 @@ def test_gloo_world4_encoded_updates(tmp_path):
     for p in ps[1:]:
         assert torch.equal(p, ps[0])                 # every rank applies the same decoded sum of 4 messages
     assert not torch.allclose(ps[0], W.make_net(Adam(0.5)).params())
+
+
+def test_inprocess_partial_round_trains_on_first_workers():
+    """10 batches over 4 workers: 2 full rounds + a trailing round of 2. The reference (PW:ParallelWrapper.java:
+    514-578) trains the trailing batches on the first ``locker`` workers; here the idle replicas contribute zero
+    gradients to the round's all-reduce and the update divides by the 2 trained batches, i.e. the trailing round is
+    the large-batch step over those 2 batches, and every replica ends identical."""
+    from deeplearning4j_amd import Adam, DataSet
+    net = W.make_net(Adam(0.01))
+    batches = W.make_batches(10, 8)
+    pw = _pw(net, 4)
+    pw.fit(batches, 1)
+    ref = W.make_net(Adam(0.01))
+    for grp in (batches[0:4], batches[4:8], batches[8:10]):
+        ref.fit(DataSet(torch.cat([b.features for b in grp]), torch.cat([b.labels for b in grp])))
+    assert torch.allclose(net.params(), ref.params(), atol=1e-5), (net.params() - ref.params()).abs().max()
+    assert net.getIterationCount() == 3
+
+
+def test_inprocess_fewer_batches_than_workers():
+    """An epoch with fewer batches than workers still trains (the round-3 wrapper dropped the whole round)."""
+    from deeplearning4j_amd import Sgd
+    net = W.make_net(Sgd(0.1))
+    before = net.params().clone()
+    _pw(net, 4, averaging=1).fit(W.make_batches(3, 8), 1)
+    assert not torch.allclose(net.params(), before)
+
+
+def test_devices_for_refuses_mixed_gpu_cpu_replicas(monkeypatch):
+    """A model on a GPU with fewer visible GPUs than workers is an error, not N-1 CPU replicas."""
+    from deeplearning4j_amd.parallel import inprocess
+
+    class M:
+        device = torch.device("cuda", 0)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(RuntimeError, match="visible GPUs"):
+        inprocess.devices_for(4, M())
+
+    class C:
+        device = torch.device("cpu")
+    assert inprocess.devices_for(4, C()) == [torch.device("cpu")] * 4
