@@ -38,14 +38,47 @@ __device__ __forceinline__ float tanh_c(float x) {
 // hipLaunchCooperativeKernel adds ~13 us of dispatch gap on each side of the kernel on this runtime (rocprofv3
 // kernel trace, profiles/r3_lstm_window_kernels.txt), i.e. ~100 us per TBPTT window of the 2-layer text model;
 // DL4J_AMD_LSTM_COOP_LAUNCH=coop restores the cooperative launch.
+// That argument holds only while nothing on ANOTHER stream can hold CUs during the launch (a conv weight-gradient
+// overlap stream, RCCL kernels of a data-parallel step): the host then asks for the cooperative launch
+// (dl4j_lstm_coop_launch_mode, ops/rnn_native.py decides per launch). Either way a timed-out hand-off also raises the
+// device-wide step guard below, and the fused updater skips its update while the guard is set, so the invalid
+// outputs of such a launch never reach the parameters (the host raises at its next check).
+static int g_coop_mode = -1;      // -1: environment default, 0: plain, 1: cooperative
+
 static hipError_t coop_launch(const void* k, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
-  static int mode = -1;
+  int mode = g_coop_mode;
   if (mode < 0) {
     const char* e = getenv("DL4J_AMD_LSTM_COOP_LAUNCH");
     mode = (e && e[0] == 'c') ? 1 : 0;
   }
   if (mode == 1) return hipLaunchCooperativeKernel(k, grid, block, args, lds, s);
   return hipLaunchKernel(k, grid, block, args, lds, s);
+}
+
+DL4J_API void dl4j_lstm_coop_launch_mode(int mode) { g_coop_mode = mode < -1 ? -1 : (mode > 1 ? 1 : mode); }
+
+// Device-wide step guard: set (never cleared on the device) by any cooperative LSTM launch whose hand-off timed out;
+// read by fused_update_kernel (csrc/updater.hip), which then leaves parameters and state untouched. The host clears
+// it (dl4j_lstm_step_guard_reset) when it reports the failure.
+__device__ unsigned g_lstm_step_guard;
+
+unsigned* lstm_step_guard_ptr() {
+  static unsigned* base[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_lstm_step_guard)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  return base[dev];
+}
+
+DL4J_API unsigned* dl4j_lstm_step_guard() { return lstm_step_guard_ptr(); }
+
+DL4J_API int dl4j_lstm_step_guard_reset(hipStream_t s) {
+  unsigned* g = lstm_step_guard_ptr();
+  return g ? (int)hipMemsetAsync(g, 0, sizeof(unsigned), s) : -1;
 }
 
 // Device-side tag bookkeeping (tag argument == kDevTag): err[1] holds the tag base of the next launch and err[2]
@@ -165,6 +198,7 @@ __global__ void __launch_bounds__(4 * U) lstm_fwd_coop(
           // once any hand-off has timed out the launch is already invalid: stop waiting at every later step
           if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
             __hip_atomic_store(err, 1u, RLX_AGENT);
+            __hip_atomic_store((gu32*)&g_lstm_step_guard, 1u, RLX_AGENT);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -383,6 +417,7 @@ __global__ void __launch_bounds__(4 * U) lstm_bwd_coop(
         if (ok) break;
         if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
           __hip_atomic_store(err, 1u, RLX_AGENT);
+          __hip_atomic_store((gu32*)&g_lstm_step_guard, 1u, RLX_AGENT);
           break;
         }
         __builtin_amdgcn_s_sleep(1);

@@ -58,7 +58,11 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
                                                            float* __restrict__ g, float* __restrict__ st,
                                                            TS* __restrict__ shadow, float inv_div, int write_update,
                                                            float* __restrict__ reg_out,
-                                                           const float* __restrict__ gn_partial) {
+                                                           const float* __restrict__ gn_partial,
+                                                           const unsigned* __restrict__ guard) {
+  // a cooperative LSTM launch of this step timed out (csrc/lstm_coop.hip step guard): its outputs are invalid, so
+  // parameters, updater state and shadow stay as they were; the host reports the failure
+  if (guard && __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   const int2 bt = btab[blockIdx.x];
   const SegDesc s = segs[bt.x];
   float reg = 0.f;   // l1*|p| + 0.5*l2*p^2 of the PRE-update params (the score's regularisation term)
@@ -150,25 +154,28 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
 // btab: device int2[nblocks] built by the host from the segment sizes (see dl4j_update_chunk).
 // gn_partial: nblocks floats of scratch when any segment uses a norm-based gradient normalization (the pre-pass
 // writes it), else null.
+unsigned* lstm_step_guard_ptr();      // csrc/lstm_coop.hip
+
 DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
                                void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
                                float* gn_partial, hipStream_t stream) {
   if (nblocks <= 0) return 0;
+  const unsigned* guard = lstm_step_guard_ptr();
   if (gn_partial)
     hipLaunchKernelGGL(gn_sumsq_kernel, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs, (const int2*)btab,
                        (const float*)g, gn_partial);
   if (shadow_kind == 1)
     hipLaunchKernelGGL(fused_update_kernel<bf16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out,
-                       (const float*)gn_partial);
+                       (const float*)gn_partial, guard);
   else if (shadow_kind == 2)
     hipLaunchKernelGGL(fused_update_kernel<f16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (f16*)shadow, inv_div, write_update, reg_out,
-                       (const float*)gn_partial);
+                       (const float*)gn_partial, guard);
   else
     hipLaunchKernelGGL(fused_update_kernel<float>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out,
-                       (const float*)gn_partial);
+                       (const float*)gn_partial, guard);
   return (int)hipGetLastError();
 }
 

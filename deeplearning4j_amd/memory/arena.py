@@ -164,3 +164,77 @@ class training_scope:
             _tl.ws = None
             self.ws.notifyScopeLeft()
         return False
+
+
+# ----------------------------------------------------------------------------------- HIP-graph training arenas
+def _activation_estimate(net, minibatch):
+    """Training-memory estimate of one iteration at ``minibatch`` from the network's memory report (reference
+    NN:nn/conf/memory/NetworkMemoryReport.java:58-95), in the compute dtype; 0 when no report is available."""
+    try:
+        from ..nn.conf.memory import MemoryUseMode
+        dt = {torch.bfloat16: "BFLOAT16", torch.float16: "HALF", torch.float64: "DOUBLE"}.get(
+            getattr(net, "compute_dtype", torch.float32), "FLOAT")
+        return int(net.memoryReport(minibatch).getTotalMemoryBytes(minibatch, MemoryUseMode.TRAINING, None, dt))
+    except Exception:
+        return 0
+
+
+def graph_workspace(net, minibatch, key):
+    """The LOOP_FF_BP arena a captured training step owns (nn/hipgraph.py): every activation, BN / pooling buffer
+    and gradient-in-flight the captured iteration allocates is carved from it, so the graph's private memory IS the
+    workspace. Sized from what the eager warmup iterations' LOOP_FF_BP arena learned (its peak, +5 %), or from the
+    memory report when that arena is not available; creation fails early, with the numbers, when the size exceeds
+    the free HBM (hipMemGetInfo). The arena is frozen: its buffer never moves while graphs hold its addresses, and an
+    allocation beyond it falls back to the graph's own pool. Returns None for networks without a training arena."""
+    ok = getattr(net, "_ws_ok", None)
+    if ok is None:
+        ok = net._ws_ok = _eligible(net)
+    if not ok or net.device is None or net.device.type != "cuda":
+        return None
+    eager = getattr(net, "_loop_ws", None)
+    learned = int(eager.stats()["maxPeak"]) if eager is not None else 0
+    est = _activation_estimate(net, minibatch)
+    need = int(learned * 1.05) + (1 << 20) if learned > 0 else int(est)
+    if need <= (1 << 20):
+        return None
+    free, total = torch.cuda.mem_get_info(net.device)
+    # the eager arena's buffer is released below, so it counts as free for the graph's arena
+    reusable = eager._buf.numel() if eager is not None and eager._buf is not None else 0
+    if need > free + reusable:
+        raise MemoryError(f"training step of {type(net).__name__} at minibatch {minibatch}: its workspace needs "
+                          f"{need / 2**30:.2f} GiB (learned peak {learned / 2**30:.2f} GiB, memory-report estimate "
+                          f"{est / 2**30:.2f} GiB) but only {(free + reusable) / 2**30:.2f} GiB of "
+                          f"{total / 2**30:.1f} GiB HBM are free; reduce the minibatch")
+    if eager is not None and eager._buf is not None and not eager.active:
+        eager._buf = None                               # the eager arena re-learns if an eager step comes again
+        eager._lib.rt_ws_set_capacity(eager._h, 0)
+    from .workspace import (AllocationPolicy, LearningPolicy, MemoryWorkspace, ResetPolicy, SpillPolicy,
+                            WorkspaceConfiguration)
+    conf = WorkspaceConfiguration(initialSize=need, overallocationLimit=0.0, policyAllocation=AllocationPolicy.STRICT,
+                                  policyLearning=LearningPolicy.NONE, policyReset=ResetPolicy.BLOCK_LEFT,
+                                  policySpill=SpillPolicy.EXTERNAL)
+    ws = MemoryWorkspace(conf, f"LOOP_FF_BP_GRAPH_{id(net)}_{abs(hash(key))}", device=net.device)
+    ws.frozen = True
+    ws.estimate_bytes = est
+    return ws
+
+
+class graph_scope:
+    """Open ``ws`` (a graph_workspace) as this thread's training arena around one capture."""
+
+    def __init__(self, net, ws):
+        self.net, self.ws, self.prev = net, ws, None
+
+    def __enter__(self):
+        if self.ws is not None:
+            self.prev = current()
+            self.ws.notifyScopeEntered()
+            _tl.ws = self.ws
+        return self
+
+    def __exit__(self, *a):
+        if self.ws is not None:
+            leverage_states(self.net, self.ws)
+            _tl.ws = self.prev
+            self.ws.notifyScopeLeft()
+        return False

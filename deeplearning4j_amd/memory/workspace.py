@@ -159,6 +159,9 @@ class MemoryWorkspace:
         self.active = False
         self.parent = None
         self.external_bytes = 0
+        # frozen: the buffer never moves (a captured HIP graph holds its addresses): no growth at cycle end, and an
+        # allocation beyond it spills to the caching allocator (captured into the graph's own pool)
+        self.frozen = False
 
     # ------------------------------------------------------------------ scope
     def notifyScopeEntered(self):
@@ -174,7 +177,7 @@ class MemoryWorkspace:
             self.manager._current = self.parent
         want = self._lib.rt_ws_cycle_end(self._h)
         cap = self._buf.numel() if self._buf is not None else 0
-        if want > cap:
+        if want > cap and not self.frozen:
             self._buf = None                                  # the old block returns to the engine first
             self._buf = _device_buffer(want, self.device)
             self._lib.rt_ws_set_capacity(self._h, want)
@@ -211,7 +214,7 @@ class MemoryWorkspace:
         if rc == 0 and self._buf is not None and off.value + nbytes <= self._buf.numel():
             t = self._buf[off.value:off.value + nbytes].view(dtype).view(shape)
         else:
-            if self.conf.policySpill == SpillPolicy.FAIL:
+            if self.conf.policySpill == SpillPolicy.FAIL and not self.frozen:
                 raise ND4JWorkspaceException(f"workspace {self.id}: allocation of {nbytes} bytes exceeds the arena "
                                              f"and policySpill=FAIL")
             t = torch.empty(shape, dtype=dtype, device=self.device)   # EXTERNAL / REALLOCATE: grown at cycle end

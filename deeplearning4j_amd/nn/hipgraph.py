@@ -105,6 +105,7 @@ class CapturedTrainingStep:
         self.score_t = [None, None]
         self.k = 0
         self.ok = False
+        self.ws = None             # the step's own LOOP_FF_BP arena (memory/arena.py graph_workspace)
 
     @staticmethod
     def key(inputs, labels, fmasks, lmasks, tbptt_back):
@@ -160,6 +161,10 @@ class CapturedTrainingStep:
         if self.tbptt_back is not None:
             self._bind_state()
         torch.cuda.current_stream(n.device).synchronize()
+        from ..memory import arena
+        self.ws = arena.graph_workspace(n, self.static_x[0].shape[0],
+                                        self.key(self.static_x, self.static_y, self.static_fm, self.static_lm,
+                                                 self.tbptt_back))
         # no Python GC while capturing: a collected cycle that owns GPU resources (events, other pools' blocks,
         # a previous network's buffers) would be released inside the capture and abort it
         guard = capture_gc_guard()
@@ -174,7 +179,8 @@ class CapturedTrainingStep:
                 g = torch.cuda.CUDAGraph()
                 native.GRAPH_SLOT[0] = slot
                 n._capturing = True
-                self.score_t[slot] = capture(g, self.pool, self._body, n.device)
+                with arena.graph_scope(n, self.ws):   # activations carved from the step's own arena
+                    self.score_t[slot] = capture(g, self.pool, self._body, n.device)
                 self.graphs.append(g)
                 # the A and B graphs own different output tensors: remember which ones this slot writes
                 self.out_state.append([(l, k, v) for l in self._recurrent_layers()
@@ -213,6 +219,8 @@ class CapturedTrainingStep:
         native.refresh_graph_table(plan, slot, n.conf.iterationCount, n.conf.epochCount)
         self.graphs[slot].replay()
         native.mark_graph_replayed(plan, slot)
+        from ..ops import rnn_native
+        rnn_native.check_step_guard(n.device)
         for l, k, v in self.out_state[slot]:
             l.tBpttStateMap[k] = v
         self.k += 1

@@ -114,27 +114,25 @@ def _ln_bwd(dy, x, res, g, ctx, gview=None, bview=None, dsum_view=None):
 
 # ------------------------------------------------------------------------------------------------ attention
 def _attn_fwd(qkv, B, T, H, mask, causal):
+    from ...ops import transformer_native as TN
     if _native(qkv, "attention"):
-        from ...ops import transformer_native as TN
         q3 = qkv.reshape(B, T, -1)
         if TN.attn_supported(q3, H):
             out, lse = TN.attn_fwd(q3, H, mask, causal)
             return out.reshape(B * T, -1), ("native", out, lse)
-    from ...ops.transformer_native import attention_reference
-    with torch.enable_grad():
-        q = qkv.detach().reshape(B, T, -1).requires_grad_(True)
-        o = attention_reference(q, H, mask, causal).to(qkv.dtype)
-    return o.detach().reshape(B * T, -1), ("torch", q, o)
+    if qkv.is_cuda:
+        from ...ops import fallback
+        fallback.record("attention", f"head size {qkv.shape[-1] // (3 * H)} / dtype {qkv.dtype}: explicit torch path")
+    o, ctx = TN.attention_fwd_explicit(qkv.reshape(B, T, -1), H, mask, causal)
+    return o.reshape(B * T, -1), ("explicit", ctx)
 
 
 def _attn_bwd(dctx, qkv, B, T, H, mask, causal, ctx):
+    from ...ops import transformer_native as TN
     if ctx[0] == "native":
-        from ...ops import transformer_native as TN
         return TN.attn_bwd(qkv.reshape(B, T, -1), ctx[1], ctx[2], dctx.reshape(B, T, -1), H, mask,
                            causal).reshape(B * T, -1)
-    _, q, o = ctx
-    (g,) = torch.autograd.grad(o, [q], dctx.reshape(o.shape).to(o.dtype))
-    return g.reshape(B * T, -1)
+    return TN.attention_bwd_explicit(ctx[1], dctx.reshape(B, T, -1), qkv.dtype).reshape(B * T, -1)
 
 
 def _token_major(x):

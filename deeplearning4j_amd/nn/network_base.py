@@ -166,7 +166,9 @@ class BaseNetwork:
                 ys = list(y) if isinstance(y, (list, tuple)) else [y]
                 if self._try_graph_step(xs, ys, fmask, lmask):
                     return None
-                return self._fit_batch_sgd(x, y, fmask, lmask)
+                from ..memory.arena import training_scope
+                with training_scope(self):               # eager warmup: learns the iteration's workspace size
+                    return self._fit_batch_sgd(x, y, fmask, lmask)
             from ..memory.arena import training_scope
             with training_scope(self):                   # LOOP_FF_BP workspace for this iteration's activations
                 return self._fit_batch_sgd(x, y, fmask, lmask)

@@ -117,10 +117,15 @@ def _as_rows_nhwc(x):
     return None
 
 
+def _ae(shape, dtype, device, channels_last=False):
+    """Per-iteration buffer from the open training workspace (memory/arena.py; the LOOP_FF_BP arena, or a captured
+    HIP graph's own arena), else from the caching allocator."""
+    from ..memory import arena
+    return arena.empty(tuple(shape), dtype, device, channels_last=channels_last)
+
+
 def _like_rows(x):
-    if x.dim() == 4:
-        return torch.empty_like(x, memory_format=torch.channels_last)
-    return torch.empty_like(x)
+    return _ae(x.shape, x.dtype, x.device, channels_last=x.dim() == 4)
 
 
 # ------------------------------------------------------------------------------------ fused updater
@@ -288,6 +293,8 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
                                _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
                                _ptr(gn_part), _stream())
     _check(rc, "fused_update")
+    from . import rnn_native
+    rnn_native.check_step_guard(params.device)     # a timed-out cooperative LSTM launch skips the update: report it
     return True
 
 
@@ -311,14 +318,14 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
         return None
     lib = load()
     y = _like_rows(x)
-    ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
-    ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+    ws = _ae((lib.dl4j_bn_workspace_floats(M, C),), torch.float32, x.device)
+    ctx = _ae((4 * C,), torch.float32, x.device)
     g = gamma if torch.is_tensor(gamma) else None
     b = beta if torch.is_tensor(beta) else None
     res = _rows_like(residual, x) if residual is not None else None
     # training with a fused residual: bn_apply writes the ReLU bitmask (1 bit per element) so the backward pass
     # never re-reads the residual
-    mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if res is not None and training else None
+    mask = _ae((M * C // 8,), torch.uint8, x.device) if res is not None and training else None
     ts = getattr(x, "_bn_tile_stats", None)
     if training and ts is not None and dt in (1, 2) and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
             (len(ts) < 3 or ts[2] == 64):
@@ -328,7 +335,7 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
                                            c_void_p, c_void_p, c_void_p, c_void_p])
         register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
-        wst = torch.empty(lib.dl4j_bn_tiles_workspace_floats(ts[1], C), dtype=torch.float32, device=x.device)
+        wst = _ae((lib.dl4j_bn_tiles_workspace_floats(ts[1], C),), torch.float32, x.device)
         rc = lib.dl4j_bn_fwd_tiles(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(ts[0]), ts[1], _ptr(g), _ptr(b),
                                    float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0,
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
@@ -409,22 +416,22 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     dx = _like_rows(x)
     dres = _like_rows(x) if res is not None else None
     ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
-    dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
-    dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
+    dgamma = dgamma_out if ok(dgamma_out) else _ae((C,), torch.float32, x.device)
+    dbeta = dbeta_out if ok(dbeta_out) else _ae((C,), torch.float32, x.device)
     if planes is not None:
         register_sig("dl4j_bn_bwd_planes_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_bwd_planes_workspace_floats.restype = c_ll
         register_sig("dl4j_bn_bwd_planes", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int,
                                             c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_void_p, c_void_p])
         P = planes.shape[1]
-        ws = torch.empty(lib.dl4j_bn_bwd_planes_workspace_floats(P, C), dtype=torch.float32, device=x.device)
+        ws = _ae((lib.dl4j_bn_bwd_planes_workspace_floats(P, C),), torch.float32, x.device)
         rc = lib.dl4j_bn_bwd_planes(_dt16(x), _ptr(x), _ptr(dy), _ptr(dx), _ptr(dres), _ptr(mask if dres is not None
                                                                                                else None), M, C,
                                     _ptr(c), _ptr(dgamma), _ptr(dbeta), 1 if relu else 0, _ptr(planes), P, _ptr(ws),
                                     _stream())
         _check(rc, "bn_bwd_planes")
         return dx, dgamma, dbeta, dres
-    ws = torch.empty(lib.dl4j_bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+    ws = _ae((lib.dl4j_bn_workspace_floats(M, C),), torch.float32, x.device)
     rc = lib.dl4j_bn_bwd(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c), _ptr(dgamma),
                          _ptr(dbeta), 1 if relu else 0, _ptr(ws), _ptr(mask), _stream())
     _check(rc, "bn_bwd")
@@ -452,9 +459,9 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
     register_sig("dl4j_bn_pool_fwd", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 12 +
                  [c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p, c_ll,
                   c_int, c_void_p, c_void_p, c_void_p])
-    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-    am = torch.empty(N * OH * OW * C, dtype=torch.uint8, device=x.device) if training else None
-    xh = torch.empty_like(y) if training else None
+    y = _ae((N, C, OH, OW), x.dtype, x.device, channels_last=True)
+    am = _ae((N * OH * OW * C,), torch.uint8, x.device) if training else None
+    xh = _ae((N, C, OH, OW), x.dtype, x.device, channels_last=True) if training else None
     ts = getattr(x, "_bn_tile_stats", None)
     M = N * H * W
     rpp = ts[2] if ts is not None and len(ts) > 2 else 64
@@ -466,8 +473,8 @@ def bn_pool_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, kernel,
         register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
         nws = max(nws, lib.dl4j_bn_tiles_workspace_floats(ts[1], C))
-    ws = torch.empty(nws, dtype=torch.float32, device=x.device)
-    ctx = torch.empty(4 * C, dtype=torch.float32, device=x.device)
+    ws = _ae((nws,), torch.float32, x.device)
+    ctx = _ae((4 * C,), torch.float32, x.device)
     b = beta if torch.is_tensor(beta) else None
     rc = lib.dl4j_bn_pool_fwd(dt, _ptr(x), _ptr(y), _ptr(am), _ptr(xh), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
                               _ptr(gamma), _ptr(b), 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
@@ -486,11 +493,11 @@ def bn_pool_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     dy = _rows_like(dy, xh)
     lib = load()
     register_sig("dl4j_bn_pool_bwd", [c_int] + [c_void_p] * 5 + [c_int] * 12 + [c_void_p] * 4 + [c_void_p])
-    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    dx = _ae(x.shape, x.dtype, x.device, channels_last=True)
     ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
-    dgamma = dgamma_out if ok(dgamma_out) else torch.empty(C, dtype=torch.float32, device=x.device)
-    dbeta = dbeta_out if ok(dbeta_out) else torch.empty(C, dtype=torch.float32, device=x.device)
-    ws = torch.empty(lib.dl4j_bn_workspace_floats(N * OH * OW, C), dtype=torch.float32, device=x.device)
+    dgamma = dgamma_out if ok(dgamma_out) else _ae((C,), torch.float32, x.device)
+    dbeta = dbeta_out if ok(dbeta_out) else _ae((C,), torch.float32, x.device)
+    ws = _ae((lib.dl4j_bn_workspace_floats(N * OH * OW, C),), torch.float32, x.device)
     rc = lib.dl4j_bn_pool_bwd(_dt16(x), _ptr(x), _ptr(dy), _ptr(am), _ptr(xh), _ptr(dx), N, H, W, C, OH, OW, kh, kw,
                               sh, sw, pt, pl, _ptr(c), _ptr(dgamma), _ptr(dbeta), _ptr(ws), _stream())
     _check(rc, "bn_pool_bwd")
@@ -510,8 +517,8 @@ def softmax_xent(logits, labels, clip_eps):
         return None
     B, V = logits.shape
     lab = labels.contiguous().float()
-    grad = torch.empty_like(logits)
-    score = torch.empty(B, dtype=torch.float32, device=logits.device)
+    grad = _ae(logits.shape, logits.dtype, logits.device)
+    score = _ae((B,), torch.float32, logits.device)
     rc = load().dl4j_softmax_xent(dt, _ptr(logits), _ptr(lab), B, V, _ptr(grad), _ptr(score), None,
                                   float(clip_eps or 0.0), _stream())
     _check(rc, "softmax_xent")
@@ -553,9 +560,9 @@ def pool2d_fwd(x, ptype, kernel, stride, pad4):
     sh, sw = stride
     OH = (H + pt + pb - kh) // sh + 1
     OW = (W + pl + pr - kw) // sw + 1
-    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    y = _ae((N, C, OH, OW), x.dtype, x.device, channels_last=True)
     mode = 0 if ptype == "MAX" else 1
-    am = torch.empty(N * OH * OW * C if mode == 0 else 8, dtype=torch.uint8, device=x.device)
+    am = _ae((N * OH * OW * C if mode == 0 else 8,), torch.uint8, x.device)
     rc = load().dl4j_pool_fwd(dt, mode, _ptr(x), _ptr(y), _ptr(am), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
                               _stream())
     _check(rc, "pool_fwd")
@@ -566,7 +573,7 @@ def pool2d_bwd(dy, ctx):
     _, mode, am, xshape, xdt, (kh, kw, sh, sw, pt, pl), (OH, OW) = ctx
     N, C, H, W = xshape
     dy = dy.to(xdt).contiguous(memory_format=torch.channels_last)
-    dx = torch.empty(xshape, dtype=xdt, device=dy.device, memory_format=torch.channels_last)
+    dx = _ae(xshape, xdt, dy.device, channels_last=True)
     rc = load().dl4j_pool_bwd({torch.bfloat16: 1, torch.float16: 2}.get(xdt, 0), mode, _ptr(dy), _ptr(am), _ptr(dx), N, H, W, C, OH,
                               OW, kh, kw, sh, sw, pt, pl, _stream())
     _check(rc, "pool_bwd")

@@ -170,6 +170,71 @@ def check_coop_errors():
                 raise CoopTimeoutError("cooperative LSTM kernel: a cross-workgroup hand-off timed out")
 
 
+# ---- launch mode and step guard (csrc/lstm_coop.hip)
+# counts components that run kernels on OTHER streams during training (data-parallel comm streams, in-process
+# multi-worker trainers); while any is live, and while the conv weight-gradient overlap stream is active, the
+# cooperative kernels use the cooperative launch so that every workgroup is co-resident.
+CONCURRENT_STREAMS = [0]
+_guard = {}          # device index -> [pinned int32 snapshot, event]
+USED_COOP = [False]
+
+
+def _concurrent_streams():
+    from . import side_stream
+    if CONCURRENT_STREAMS[0] > 0 or side_stream.active():
+        return True
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _launch_mode(lib):
+    native.register_sig("dl4j_lstm_coop_launch_mode", [c_int])
+    lib.dl4j_lstm_coop_launch_mode(1 if _concurrent_streams() else -1)
+    USED_COOP[0] = True
+
+
+def check_step_guard(device):
+    """Called once per training step after the fused update has been queued: reads the previous step's snapshot of
+    the device-wide step guard (set by a timed-out cooperative LSTM launch; the fused updater then skipped that
+    update), raises CoopTimeoutError after clearing it, and queues a snapshot of the current value."""
+    if not USED_COOP[0] or device is None or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return
+    lib = native.load()
+    native.register_sig("dl4j_lstm_step_guard", [])
+    native.register_sig("dl4j_lstm_step_guard_reset", [c_void_p])
+    lib.dl4j_lstm_step_guard.restype = c_void_p
+    g = _guard.get(device.index)
+    if g is not None and g[1].query() and int(g[0][0]) != 0:
+        lib.dl4j_lstm_step_guard_reset(c_void_p(_stream()))
+        g[0][0] = 0
+        raise CoopTimeoutError("cooperative LSTM kernel: a cross-workgroup hand-off timed out; the fused updater "
+                               "skipped that step's update (parameters unchanged)")
+    if g is None:
+        g = _guard[device.index] = [torch.zeros(1, dtype=torch.int32, pin_memory=True), None]
+    ptr = lib.dl4j_lstm_step_guard()
+    if not ptr:
+        return
+    import ctypes as _ct
+    hip = _hip()
+    hip.hipMemcpyAsync(_ct.c_void_p(g[0].data_ptr()), _ct.c_void_p(ptr), _ct.c_size_t(4), 2, _ct.c_void_p(_stream()))
+    ev = torch.cuda.Event()
+    ev.record()
+    g[1] = ev
+
+
+_hiplib = []
+
+
+def _hip():
+    if not _hiplib:
+        import ctypes as _ct
+        lib = _ct.CDLL("libamdhip64.so")
+        lib.hipMemcpyAsync.argtypes = [_ct.c_void_p, _ct.c_void_p, _ct.c_size_t, _ct.c_int, _ct.c_void_p]
+        lib.hipMemcpyAsync.restype = _ct.c_int
+        _hiplib.append(lib)
+    return _hiplib[0]
+
+
 def _coop_enabled():
     import os
     return os.environ.get("DL4J_AMD_LSTM_COOP", "1") == "1"
@@ -182,6 +247,7 @@ def _fwd_coop(lib, zx, rwt, peep, h0c, c0c, m, out, out16, gates, call, hT, cT, 
     lib.dl4j_lstm_coop_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_exch_bytes(mb, H)
     b, base, reset = _coop_buf("fwd", nbytes, zx.device, T)
+    _launch_mode(lib)
     rc = lib.dl4j_lstm_fwd_coop(_ptr(zx), _ptr(rwt), _ptr(peep), _ptr(h0c), _ptr(c0c), _ptr(m), _ptr(out),
                                 _ptr(out16), _ptr(gates), _ptr(call), _ptr(hT), _ptr(cT), _ptr(b.exch), _ptr(b.err), T, mb, H, base, reset,
                                 c_void_p(_stream()))
@@ -206,6 +272,7 @@ def _bwd_coop(lib, e, edt, gates, call, c0c, rw, peep, m, dhl, dcl, dz, dh0, dc0
     lib.dl4j_lstm_coop_bwd_exch_bytes.restype = ctypes.c_longlong
     nbytes = lib.dl4j_lstm_coop_bwd_exch_bytes(mb, H)
     b, base, reset = _coop_buf("bwd", nbytes, e.device, T)
+    _launch_mode(lib)
     rc = lib.dl4j_lstm_bwd_coop(_ptr(e), edt, _ptr(gates), _ptr(call), _ptr(c0c), _ptr(rw), _ptr(peep), _ptr(m), _ptr(dhl),
                                 _ptr(dcl), _ptr(dz), _ptr(dh0), _ptr(dc0), _ptr(b.exch), _ptr(b.err), T, mb, H,
                                 int(t_end), base, reset, c_void_p(_stream()))

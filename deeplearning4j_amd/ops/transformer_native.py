@@ -107,6 +107,47 @@ def attention_reference(qkv, H, mask=None, causal=False, scale=None):
     return o.permute(0, 2, 1, 3).reshape(B, T, E)
 
 
+def attention_fwd_explicit(qkv, H, mask=None, causal=False, scale=None):
+    """Attention core with an explicitly derived backward (no torch.autograd): the path for shapes / dtypes outside
+    the flash kernel (CPU, fp32 / fp64, head sizes other than 64 / 128). qkv [B, T, 3E] in the fused projection
+    layout. Returns (out [B, T, E] in qkv's dtype, ctx) for attention_bwd_explicit; ctx keeps the probabilities
+    P [B, H, T, T] (fp32, or fp64 for fp64 inputs)."""
+    B, T, E3 = qkv.shape
+    E = E3 // 3
+    D = E // H
+    scale = float(scale if scale is not None else D ** -0.5)
+    cd = torch.float64 if qkv.dtype == torch.float64 else torch.float32
+    q, k, v = qkv.to(cd).reshape(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)      # [B, H, T, D]
+    s = (q @ k.transpose(-1, -2)) * scale
+    keep = None
+    if mask is not None:
+        keep = (mask.reshape(B, 1, 1, T) != 0)
+    if causal:
+        tri = torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril().reshape(1, 1, T, T)
+        keep = tri if keep is None else (keep & tri)
+    if keep is not None:
+        s = s.masked_fill(~keep, float("-inf"))
+    p = torch.softmax(s, dim=-1).nan_to_num(0.0)          # fully masked rows: zero output
+    o = p @ v
+    out = o.permute(0, 2, 1, 3).reshape(B, T, E).to(qkv.dtype)
+    return out, (q, k, v, p, scale)
+
+
+def attention_bwd_explicit(ctx, dout, qkv_dtype):
+    """dqkv [B, T, 3E] for attention_fwd_explicit:  dV = P^T dO,  dP = dO V^T,  dS = P * (dP - rowsum(dP * P)),
+    dQ = scale dS K,  dK = scale dS^T Q."""
+    q, k, v, p, scale = ctx
+    B, H, T, D = q.shape
+    do = dout.to(q.dtype).reshape(B, T, H, D).permute(0, 2, 1, 3)
+    dv = p.transpose(-1, -2) @ do
+    dp = do @ v.transpose(-1, -2)
+    ds = p * (dp - (dp * p).sum(-1, keepdim=True))
+    dq = (ds @ k) * scale
+    dk = (ds.transpose(-1, -2) @ q) * scale
+    dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B, T, 3 * H * D)
+    return dqkv.to(qkv_dtype)
+
+
 # ------------------------------------------------------------------------------------------------ layernorm
 def _dt(t):
     return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(t.dtype)

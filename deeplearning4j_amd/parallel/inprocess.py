@@ -176,6 +176,10 @@ class InProcessTrainer:
     def _start(self):
         if self._threads:
             return
+        if len(self.models) > 1 and self.devices[0].type == "cuda":
+            from ..ops import rnn_native
+            rnn_native.CONCURRENT_STREAMS[0] += 1      # RCCL kernels on other streams: cooperative LSTM launches
+            self._concurrent = True
         for i in range(len(self.models)):
             t = threading.Thread(target=self._run, args=(i,), name=f"dl4j-pw-worker-{i}", daemon=True)
             t.start()
@@ -266,6 +270,10 @@ class InProcessTrainer:
         for t in self._threads:
             t.join(timeout=30)
         self._threads = []
+        if getattr(self, "_concurrent", False):
+            from ..ops import rnn_native
+            rnn_native.CONCURRENT_STREAMS[0] -= 1
+            self._concurrent = False
 
 
 def _batch_size(ds):

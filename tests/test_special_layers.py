@@ -73,6 +73,25 @@ def test_self_attention_gradients():
     assert checkGradients(net, input=x, labels=y, print_results=True, minAbsoluteError=1e-7)
 
 
+@pytest.mark.parametrize("causal,masked", [(True, False), (False, True), (True, True)])
+def test_self_attention_gradients_causal_and_masked(causal, masked):
+    """The hand-derived backward (nn/layers/attention.py, ops/transformer_native.attention_bwd_explicit) against
+    fp64 numerical gradients, with a causal mask and / or padded keys (masked query rows produce zeros)."""
+    net = _mln([SelfAttentionLayer.Builder().nIn(6).nOut(6).nHeads(3).causal(causal)
+                .activation(Activation.TANH).build(),
+                RnnOutputLayer.Builder(LossFunction.MCXENT).nIn(6).nOut(3).activation(Activation.SOFTMAX).build()])
+    x = torch.randn(3, 6, 5, dtype=torch.float64)
+    y = torch.zeros(3, 3, 5, dtype=torch.float64)
+    y[:, 1, :] = 1
+    mask = None
+    if masked:
+        mask = torch.ones(3, 5, dtype=torch.float64)
+        mask[1, 3:] = 0
+        mask[2, 1:] = 0
+    assert checkGradients(net, input=x, labels=y, inputMask=mask, labelMask=mask, print_results=True,
+                          minAbsoluteError=1e-7)
+
+
 def test_autoencoder_supervised_gradients_and_pretrain():
     ae = AutoEncoder.Builder().nIn(6).nOut(4).activation(Activation.SIGMOID).corruptionLevel(0.0).build()
     net = _mln([ae, OutputLayer.Builder(LossFunction.MSE).nIn(4).nOut(2).activation(Activation.IDENTITY).build()])
