@@ -614,7 +614,10 @@ struct Cfg {
 //          2 = 128x128 (4 waves 2x2, 2 stages, 2 blocks/CU), 3 = 128x64 (4 waves 2x2 of 64x32, 3 stages)
 //          4 = 256x256 8-phase (8 waves, 16x16x32 MFMA, K % 64 == 0)
 //          5 = 128x64 single-buffered (24 KB LDS, up to 4 blocks/CU: memory-bound skinny / small-K shapes)
-const Cfg kCfg[6] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}, {128, 64}};
+//          6 = 128x128 3 stages (96 KB, 1 block/CU: two K-tiles in flight across each barrier instead of one)
+//          7 = 128x128 4 stages (128 KB: three K-tiles in flight) — latency-bound small-grid / split-K shapes
+constexpr int kNumCfg = 8;
+const Cfg kCfg[kNumCfg] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}, {128, 64}, {128, 128}, {128, 128}};
 
 template <int DT, bool AKC, bool BKC>
 int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
@@ -626,6 +629,8 @@ int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
     case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 2>), grid, dim3(256), 0, s, g); break;
     case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
     case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 1>), grid, dim3(256), 0, s, g); break;
+    case 6: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
+    case 7: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 4>), grid, dim3(256), 0, s, g); break;
     default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC>), grid, dim3(512), 0, s, g); break;
   }
   return (int)hipGetLastError();
@@ -634,6 +639,7 @@ int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
 // BN-backward epilogue instantiations: only the 1x1 bwd-data layout (dY rows K-contiguous, W [K][C] N-contiguous)
 template <int DT>
 int launch_fast_bnb(int cfg, const GemmArgs& g, hipStream_t s) {
+  if (cfg >= 6) return -1;                      // the deep-ring 128x128 tiles have no BN-backward instantiation
   dim3 grid(g.tiles_m * g.tiles_n, 1, 1);
   switch (cfg) {
     case 0: hipLaunchKernelGGL((gemm_glds<DT, 256, 256, 2, 4, true, false, 2, true>), grid, dim3(512), 0, s, g); break;
@@ -743,7 +749,7 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
       return -1;
   }
   if (K <= 0) return -1;
-  if (cfg < 0 || cfg > 5 || splits < 1) plan(M, N, K, batch, &cfg, &splits);
+  if (cfg < 0 || cfg >= kNumCfg || splits < 1) plan(M, N, K, batch, &cfg, &splits);
   if ((cfg == 3 || cfg == 5) && !bkc) cfg = 2;   // the 64-wide tile has no N-contiguous image
   if (cfg == 4) {                                // 8-phase: K % 64 and 32-bit element offsets
     const long long ea = akc ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M;

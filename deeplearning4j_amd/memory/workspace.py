@@ -179,6 +179,15 @@ class MemoryWorkspace:
         cap = self._buf.numel() if self._buf is not None else 0
         if want > cap and not self.frozen:
             self._buf = None                                  # the old block returns to the engine first
+            if self.device.type == "cuda":
+                # ... and the engine hands it back to the driver (hipFree, which also waits for every stream that
+                # may still read it, the weight-gradient overlap stream included), so the caching allocator of torch
+                # can reuse the memory instead of failing while the engine sits on a free segment
+                try:
+                    from ..runtime import allocator
+                    allocator(self.device.index or 0).empty_cache()
+                except Exception:
+                    pass
             self._buf = _device_buffer(want, self.device)
             self._lib.rt_ws_set_capacity(self._h, want)
         self.external_bytes = 0

@@ -25,6 +25,15 @@ def _unwrap(x):
     return x._t if isinstance(x, INDArray) else x
 
 
+def _partial_overlap(a, b):
+    """True when ``b`` shares memory with ``a`` other than as the very same element-for-element view (in-place ops
+    write ``a`` while reading ``b``; identical views are safe elementwise, anything else races)."""
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return False
+    same = (a.shape == b.shape and a.stride() == b.stride() and a.storage_offset() == b.storage_offset())
+    return not same
+
+
 def _wrap(t):
     return INDArray(t)
 
@@ -419,6 +428,10 @@ class INDArray:
             ob = o if torch.is_tensor(o) or isinstance(o, (int, float)) else None
             if ob is not None and not (torch.is_tensor(ob) and ob.dtype != self._t.dtype):
                 if inplace:
+                    if torch.is_tensor(ob) and _partial_overlap(self._t, ob):
+                        # the operand is another view of this array's memory (x.subiRowVector(x.getRow(0)),
+                        # x.addi(x.T)): the kernel would read elements it already overwrote, so read a copy
+                        ob = ob.clone()
                     with torch.no_grad():
                         r = K.binary(self._t, ob, kop, out=self._t if self._t.is_contiguous() else None)
                         if r is not None:

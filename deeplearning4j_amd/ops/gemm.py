@@ -65,12 +65,14 @@ def _candidates(M, N, K, batch, default):
     splits = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     if K % 64 == 0:
         c += [(4, s) for s in splits if s == 1 or (batch == 1 and K // s >= 512 and t256 * s <= 1024)]
-    c += [(x, 1) for x in (0, 1, 2, 3, 5)]
+    c += [(x, 1) for x in (0, 1, 2, 3, 5, 6, 7)]
     if batch == 1:
         # small output grids (e.g. the LSTM's [256 x 1024] weight gradients over K = T*mb = 1600) need deep split-K
         # to fill the CUs: down to 128-deep K slices when the tile grid is under a quarter of the chip
         kmin = 128 if t128 * 4 <= 256 else 512
         c += [(x, s) for x in (1, 2, 3, 5) for s in splits[1:] if K // s >= kmin and t128 * s <= 2048]
+        # deep-ring 128x128 tiles (cfg 6 / 7): one block per CU, so splits that keep the grid near 1-2 waves of CUs
+        c += [(x, s) for x in (6, 7) for s in splits[1:] if K // s >= 256 and 128 <= t128 * s <= 768]
     seen, out = set(), []
     for x in c:
         if x not in seen:

@@ -173,6 +173,22 @@ def test_framework_paths_use_the_kernels(cuda):
     assert K.CALLS["transform_bp"] >= 5
 
 
+def test_inplace_ops_with_overlapping_operands(cuda):
+    """In-place ops whose operand is another view of the same array: the result equals the CPU one
+    (the operand is read from a copy), not an order-dependent race inside the kernel."""
+    from deeplearning4j_amd.nd4j.ndarray import INDArray
+    g = torch.Generator().manual_seed(8)
+    xc = torch.randn(64, 64, generator=g)
+    ga, ca = INDArray(xc.to(cuda)), INDArray(xc.clone())
+    ga.subiRowVector(ga.getRow(0))
+    ca.subiRowVector(ca.getRow(0))
+    assert torch.equal(ga.toTensor().cpu(), ca.toTensor())
+    gb, cb = INDArray(xc.to(cuda)), INDArray(xc.clone())
+    gb.addi(gb.transpose())
+    cb.addi(cb.transpose())
+    assert torch.allclose(gb.toTensor().cpu(), cb.toTensor(), atol=0, rtol=0)
+
+
 def test_shape_layers_and_max_vertex_on_gpu(cuda):
     from deeplearning4j_amd.nn.conf import layers as L
     from deeplearning4j_amd.nn.conf.graph import ElementWiseVertex
