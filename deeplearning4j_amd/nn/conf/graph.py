@@ -162,10 +162,38 @@ class StackVertex(GraphVertex):
     """Stack along dim 0 (minibatch)."""
 
     def forward(self, inputs, training=False, masks=None):
-        return torch.cat(list(inputs), dim=0), [x.shape[0] for x in inputs]
+        """Time series of different lengths are zero-padded to the longest (reference StackVertex.doForward); the
+        stacked mask marks the padding."""
+        inputs = list(inputs)
+        self._mask_shapes = [(x.shape[0], x.shape[2] if x.dim() == 3 else None) for x in inputs]
+        if inputs[0].dim() == 3:
+            T = max(x.shape[2] for x in inputs)
+            if any(x.shape[2] != T for x in inputs):
+                self._Tmax = T
+                padded = [torch.nn.functional.pad(x, (0, T - x.shape[2])) for x in inputs]
+                return torch.cat(padded, dim=0), ([x.shape[0] for x in inputs], [x.shape[2] for x in inputs])
+        self._Tmax = None
+        return torch.cat(inputs, dim=0), [x.shape[0] for x in inputs]
 
     def backward(self, eps, ctx):
+        if isinstance(ctx, tuple):
+            ns, Ts = ctx
+            return [e[:, :, :T] for e, T in zip(torch.split(eps, ns, dim=0), Ts)]
         return list(torch.split(eps, ctx, dim=0))
+
+    def feedForwardMask(self, masks):
+        """Masks are stacked like the activations (reference StackVertex.feedForwardMaskArrays): an input without a
+        mask contributes ones; no mask at all stays None."""
+        masks = list(masks or [])
+        if not any(m is not None for m in masks):
+            return None
+        ref = next(m for m in masks if m is not None)
+        shapes = getattr(self, "_mask_shapes", None) or [(ref.shape[0], ref.shape[1])] * len(masks)
+        out = [m if m is not None else torch.ones(n, T if T is not None else ref.shape[1], dtype=ref.dtype,
+                                                  device=ref.device) for m, (n, T) in zip(masks, shapes)]
+        Tmax = max(m.shape[1] for m in out)
+        out = [torch.nn.functional.pad(m, (0, Tmax - m.shape[1])) if m.shape[1] != Tmax else m for m in out]
+        return torch.cat(out, dim=0)
 
 
 class UnstackVertex(GraphVertex):
@@ -178,6 +206,13 @@ class UnstackVertex(GraphVertex):
         x = inputs[0]
         n = x.shape[0] // self.stackSize
         return x[self.from_ * n:(self.from_ + 1) * n], (x.shape, n)
+
+    def feedForwardMask(self, masks):
+        m = (masks or [None])[0]
+        if m is None:
+            return None
+        n = m.shape[0] // self.stackSize
+        return m[self.from_ * n:(self.from_ + 1) * n]
 
     def backward(self, eps, ctx):
         shape, n = ctx

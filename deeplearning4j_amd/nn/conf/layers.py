@@ -288,7 +288,10 @@ class CenterLossOutputLayer(BaseOutputLayer):
     RUNTIME = "deeplearning4j_amd.nn.layers.output:CenterLossOutputLayerImpl"
 
     def param_specs(self):
-        return super().param_specs() + [ParamSpec("cL", [self.nOut, self.nIn], "c", "zero", trainable=False)]
+        # gradientCheck: the centers are checked like any parameter (dL/dc = lambda * sum(c_y - x)) and are not
+        # moved by the forward-backward pass (reference CenterLossOutputLayer.java:217-223)
+        return super().param_specs() + [ParamSpec("cL", [self.nOut, self.nIn], "c", "zero",
+                                                  trainable=bool(self.gradientCheck))]
 
 
 class LossLayer(FeedForwardLayer):

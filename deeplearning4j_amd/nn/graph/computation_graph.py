@@ -444,7 +444,7 @@ class ComputationGraph(BaseNetwork):
             lm = [m[:, t0:t1] if m is not None else None for m in lmasks] if lmasks else None
             if self._try_graph_step(xs, ys, fm, lm, tbptt_back=back):
                 continue                           # this window replayed as a HIP graph (nn/hipgraph.py)
-            from ..memory.arena import tbptt_scope
+            from ...memory.arena import tbptt_scope
             with tbptt_scope(self):                  # LOOP_TBPTT arena for this window
                 self.computeGradientAndScore(xs, ys, fm, lm, stored_state=True, store_last_for_tbptt=True,
                                              tbptt_back=back, defer_reg=True)

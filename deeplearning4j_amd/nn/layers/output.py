@@ -248,6 +248,11 @@ class CenterLossOutputLayerImpl(BaseOutputLayerImpl):
         x = _acc(self._x2)
         d = x - y @ _acc(c)
         eps_prev = eps_prev + (self.conf.lambda_ * d).to(eps_prev.dtype)
+        if self.conf.gradientCheck:
+            # the exact gradient of the center term w.r.t. the centers; the centers themselves stay put
+            if "cL" in self.grads:
+                self.grads["cL"].copy_((self.conf.lambda_ * (y.t() @ (-d))).to(self.grads["cL"].dtype))
+            return g, eps_prev
         with torch.no_grad():
             counts = y.sum(dim=0).clamp(min=1).reshape(-1, 1)
             delta_c = (y.t() @ (-d)) / (counts + 1)
