@@ -621,6 +621,19 @@ class Subsampling1DLayer(SubsamplingLayer):
             a = a[0] if isinstance(a, (list, tuple)) else a
             kw[n] = [int(a), 1] if n != "padding" else [int(a), 0]
 
+    def _post_init(self):
+        # setter-built sizes (.kernelSize(2).stride(1)) arrive as square 2-D pairs: the second dim is the dummy
+        # width of the [mb, C, T, 1] view
+        for n in ("kernelSize", "stride", "padding", "dilation"):
+            v = getattr(self, n, None)
+            if v is None or len(v) != 2 or v[0] != v[1]:
+                continue
+            if n == "padding":
+                if v[1] != 0:
+                    setattr(self, n, [v[0], 0])
+            elif v[1] != 1:
+                setattr(self, n, [v[0], 1])
+
     def getOutputType(self, layerIndex, inputType):
         mode = self.convolutionMode or ConvolutionMode.Truncate
         T = inputType.timeSeriesLength

@@ -252,6 +252,7 @@ class ComputationGraph(BaseNetwork):
         acts = {}
         amask = {}
         mb = inputs[0].shape[0]
+        self._prep_mb = mb
         for i, n in enumerate(self.conf.networkInputs):
             acts[n] = inputs[i]
             amask[n] = masks[i] if masks is not None and i < len(masks) else None
@@ -404,9 +405,11 @@ class ComputationGraph(BaseNetwork):
         for l in self.listeners:
             if hasattr(l, "onForwardPass"):
                 l.onForwardPass(self, acts)
+        mb_in = self._prep_mb if getattr(self, "_prep_mb", None) else None
         for i, o in enumerate(self.outputs):
             layer = self.layers_by_name[o]
             layer.setLabels(self._to_dev(labels[i], self.master_dtype))
+            layer.inputMiniBatchSize = mb_in
             lm = lmasks[i] if lmasks is not None and i < len(lmasks) else None
             if lm is not None:
                 layer.maskArray = self._to_dev(lm)
@@ -515,6 +518,7 @@ class ComputationGraph(BaseNetwork):
             for i, o in enumerate(self.outputs):
                 layer = self.layers_by_name[o]
                 layer.setLabels(self._to_dev(ds.labels[i], self.master_dtype))
+                layer.inputMiniBatchSize = self._mb
                 score += float(layer.computeScore(l1 if i == 0 else 0.0, l2 if i == 0 else 0.0, training))
             return score
 

@@ -134,7 +134,7 @@ class Convolution1DLayerImpl(ConvolutionLayerImpl):
 
     def backpropGradient(self, eps):
         g, dx = super().backpropGradient(eps.unsqueeze(3))
-        return g, dx.squeeze(3)
+        return g, (dx.squeeze(3) if dx is not None else None)
 
 
 class Deconvolution2DImpl(ConvolutionLayerImpl):

@@ -25,8 +25,12 @@ def _2d_to_rnn(x, mb):
 
 
 def _mask_rnn_to_2d(mask):
+    """[mb, T] per-time-step mask -> [T*mb, 1]; [mb, nOut, T] per-output mask (reference
+    GradientCheckTestsMasking.testPerOutputMaskingRnn) -> [T*mb, nOut], rows ordered like _rnn_to_2d."""
     if mask is None:
         return None
+    if mask.dim() == 3:
+        return _rnn_to_2d(mask)
     return mask.t().reshape(-1, 1) if mask.dim() == 2 else mask
 
 
@@ -128,10 +132,16 @@ class BaseOutputLayerImpl(LayerImpl):
         self._cache = (s, g)
         return self._cache
 
+    def _score_mb(self):
+        """The score is averaged over the NETWORK's input minibatch (reference BaseOutputLayer.computeScore divides
+        by getInputMiniBatchSize()), which the updater also divides the gradient by; it differs from this layer's
+        own input rows after a minibatch-changing layer such as SpaceToBatch."""
+        mb = getattr(self, "inputMiniBatchSize", None)
+        return mb if mb else self.input.shape[0]
+
     def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
         s, _ = self._loss_and_grad()
-        mb = self.input.shape[0]
-        return (s.sum() + fullNetworkL1 + fullNetworkL2) / mb
+        return (s.sum() + fullNetworkL1 + fullNetworkL2) / self._score_mb()
 
     def computeScoreForExamples(self, fullNetworkL1=0.0, fullNetworkL2=0.0):
         s, _ = self._loss_and_grad()
@@ -239,7 +249,7 @@ class CenterLossOutputLayerImpl(BaseOutputLayerImpl):
         y = _acc(self.labels)
         centers = y @ _acc(c)
         d = _acc(self._x2) - centers
-        return base + 0.5 * self.conf.lambda_ * (d * d).sum() / self.input.shape[0]
+        return base + 0.5 * self.conf.lambda_ * (d * d).sum() / self._score_mb()
 
     def backpropGradient(self, eps=None):
         g, eps_prev = super().backpropGradient(eps)

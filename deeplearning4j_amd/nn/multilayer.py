@@ -199,9 +199,12 @@ class MultiLayerNetwork(BaseNetwork):
                 l.onForwardPass(self, acts)
         out = self.layers[-1]
         out.setLabels(self._to_dev(y, self.master_dtype))
+        out.inputMiniBatchSize = self._mb
         if lmask is not None:
             out.maskArray = self._to_dev(lmask)
-        elif fmask is not None and out.maskArray is None:
+        elif fmask is not None and out.maskArray is None and out.input is not None and out.input.dim() == 3:
+            # the feature mask doubles as the label mask of a time-series output; a layer that consumed the mask
+            # on the way (LastTimeStep, global pooling) left a 2-D output that has none
             out.maskArray = self._to_dev(fmask)
         self._backprop(tbptt_back)
         if defer_reg:      # regularisation term comes out of the fused updater kernel (see _apply_update)
@@ -296,6 +299,7 @@ class MultiLayerNetwork(BaseNetwork):
             self.feedForwardToLayer(len(self.layers) - 1, ds.features, training, self._to_dev(ds.featuresMask))
             out = self.layers[-1]
             out.setLabels(self._to_dev(ds.labels, self.master_dtype))
+            out.inputMiniBatchSize = self._mb
             if ds.labelsMask is not None:
                 out.maskArray = self._to_dev(ds.labelsMask)
             l1, l2 = self._regularization_terms()
