@@ -7,9 +7,12 @@
 template <typename T>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__ z, const float* __restrict__ y, int V,
                                                            T* __restrict__ grad, float* __restrict__ score,
-                                                           float* __restrict__ prob, float log_eps, float log_1m_eps) {
+                                                           float* __restrict__ prob, float log_eps, float log_1m_eps,
+                                                           const float* __restrict__ rmask) {
   __shared__ float red[16];
   const long long row = blockIdx.x;
+  // per-row mask (masked time steps of an RNN output): the row's score and gradient are scaled by it
+  const float mr = rmask ? rmask[row] : 1.f;
   const T* zr = z + row * V;
   const float* yr = y + row * V;
   float m = -INFINITY;
@@ -28,11 +31,11 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__
     float lp = zj - lse;
     lp = fminf(fmaxf(lp, log_eps), log_1m_eps);
     sc -= yj * lp;
-    st1<T>(grad + row * V + j, p - yj);
+    st1<T>(grad + row * V + j, (p - yj) * mr);
     if (prob) prob[row * V + j] = p;
   }
   sc = block_reduce<false>(sc, red);
-  if (threadIdx.x == 0) score[row] = sc;
+  if (threadIdx.x == 0) score[row] = sc * mr;
 }
 
 // Strided variant: logits rows with leading dimension ldz; label row r = t*mb + b (t = r / mb, b = r % mb) read at
@@ -92,18 +95,30 @@ DL4J_API int dl4j_softmax_xent_strided(int dtype, const void* z, int ldz, const 
   return (int)hipGetLastError();
 }
 
-DL4J_API int dl4j_softmax_xent(int dtype, const void* z, const float* y, int B, int V, void* grad, float* score,
-                               float* prob, float clip_eps, hipStream_t s) {
+static int softmax_xent_launch(int dtype, const void* z, const float* y, int B, int V, void* grad, float* score,
+                               float* prob, float clip_eps, const float* rmask, hipStream_t s) {
   const float le = clip_eps > 0.f ? logf(clip_eps) : -INFINITY;
   const float l1 = clip_eps > 0.f ? log1pf(-clip_eps) : 0.f;
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_xent_kernel<bf16>, dim3(B), dim3(256), 0, s, (const bf16*)z, y, V, (bf16*)grad, score,
-                       prob, le, l1);
+                       prob, le, l1, rmask);
   else if (dtype == 2)
     hipLaunchKernelGGL(softmax_xent_kernel<f16>, dim3(B), dim3(256), 0, s, (const f16*)z, y, V, (f16*)grad, score,
-                       prob, le, l1);
+                       prob, le, l1, rmask);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)z, y, V, (float*)grad, score,
-                       prob, le, l1);
+                       prob, le, l1, rmask);
   return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_softmax_xent(int dtype, const void* z, const float* y, int B, int V, void* grad, float* score,
+                               float* prob, float clip_eps, hipStream_t s) {
+  return softmax_xent_launch(dtype, z, y, B, V, grad, score, prob, clip_eps, nullptr, s);
+}
+
+// rmask: fp32 [B] per-row mask (RNN output time-step masks as [T*mb] rows)
+DL4J_API int dl4j_softmax_xent_masked(int dtype, const void* z, const float* y, int B, int V, void* grad, float* score,
+                                      const float* rmask, float clip_eps, hipStream_t s) {
+  if (!rmask) return -1;
+  return softmax_xent_launch(dtype, z, y, B, V, grad, score, nullptr, clip_eps, rmask, s);
 }

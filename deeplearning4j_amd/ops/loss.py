@@ -14,11 +14,13 @@ from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 def softmax_xent(logits, labels, mask=None, clip_eps=1e-10):
     """Returns (per_example_score [mb] fp32, dL/dz same dtype as logits, probabilities fp32 or None)."""
-    if use_native(logits, "softmax_xent") and logits.dim() == 2 and mask is None:
+    if use_native(logits, "softmax_xent") and logits.dim() == 2:
         from . import native
-        r = native.softmax_xent(logits, labels, clip_eps)
-        if r is not None:
-            return r
+        per_row = mask is not None and mask.numel() == logits.shape[0]
+        if mask is None or per_row:            # per-time-step masks of RNN outputs: rows scaled in the kernel
+            r = native.softmax_xent(logits, labels, clip_eps, row_mask=mask if per_row else None)
+            if r is not None:
+                return r
     from .fallback import note
     note(logits, "softmax_xent", f"{logits.dtype} mask={mask is not None}")
     z = _acc(logits)

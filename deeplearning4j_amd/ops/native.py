@@ -511,7 +511,8 @@ def _dt16(t):
     return {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(t.dtype)
 
 
-def softmax_xent(logits, labels, clip_eps):
+def softmax_xent(logits, labels, clip_eps, row_mask=None):
+    """row_mask: optional fp32 per-row mask ([B] or [B, 1]) applied to each row's score and gradient."""
     dt = _dt16(logits)
     if dt is None or not logits.is_contiguous():
         return None
@@ -519,6 +520,16 @@ def softmax_xent(logits, labels, clip_eps):
     lab = labels.contiguous().float()
     grad = _ae(logits.shape, logits.dtype, logits.device)
     score = _ae((B,), torch.float32, logits.device)
+    if row_mask is not None:
+        m = row_mask.reshape(-1).to(torch.float32).contiguous()
+        if m.numel() != B:
+            return None
+        register_sig("dl4j_softmax_xent_masked", [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                                  c_void_p, c_float, c_void_p])
+        rc = load().dl4j_softmax_xent_masked(dt, _ptr(logits), _ptr(lab), B, V, _ptr(grad), _ptr(score), _ptr(m),
+                                             float(clip_eps or 0.0), _stream())
+        _check(rc, "softmax_xent_masked")
+        return score, grad, None
     rc = load().dl4j_softmax_xent(dt, _ptr(logits), _ptr(lab), B, V, _ptr(grad), _ptr(score), None,
                                   float(clip_eps or 0.0), _stream())
     _check(rc, "softmax_xent")

@@ -90,6 +90,15 @@ def test_softmax_xent(cuda, dtype):
     s, gr, _ = ops.softmax_xent(z.to(cuda), y.to(cuda), None, 1e-10)
     _close(s, s_ref, 1e-4)
     _close(gr, g_ref, 1e-5 if dtype == torch.float32 else 1e-2)
+    # per-row mask (RNN output time steps) on the kernel: no fallback, rows scaled
+    from deeplearning4j_amd.ops import fallback
+    m = (torch.rand(37, 1, generator=g) > 0.3).float()
+    s_ref, g_ref, _ = ops.softmax_xent(z.float(), y, m, 1e-10)
+    n0 = fallback.count()
+    s, gr, _ = ops.softmax_xent(z.to(cuda), y.to(cuda), m.to(cuda), 1e-10)
+    assert fallback.count() == n0
+    _close(s, s_ref, 1e-4)
+    _close(gr, g_ref, 1e-5 if dtype == torch.float32 else 1e-2)
 
 
 @pytest.mark.parametrize("upd", ["Sgd", "Nesterovs", "Adam", "AdaMax", "Nadam", "AdaGrad", "AdaDelta", "RmsProp",
