@@ -15,3 +15,5 @@ timeout -k 10 300 python3 tools/bench_bert_samediff.py --steps 10 --warmup 3 > g
 echo "bert samediff: $(tail -1 gpurun_out/r4_bert_sd.log | cut -c1-160)"
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/r4_sd_prof" -o run -- python3 "$R/tools/bench_bert_samediff.py" --steps 4 --warmup 3 > "$R/gpurun_out/r4_sd_prof.log" 2>&1 || { tail -5 "$R/gpurun_out/r4_sd_prof.log"; exit 1; }
 cd "$R" && python3 tools/prof_laststep.py gpurun_out/r4_sd_prof/run_results.db --top 40 > gpurun_out/r4_sd_step.txt && rm -rf gpurun_out/r4_sd_prof && head -30 gpurun_out/r4_sd_step.txt
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/r4_eager_prof" -o run -- python3 "$R/bench.py" --steps 4 --warmup 3 > "$R/gpurun_out/r4_eager_prof.log" 2>&1 || { tail -5 "$R/gpurun_out/r4_eager_prof.log"; exit 1; }
+cd "$R" && python3 tools/prof_laststep.py gpurun_out/r4_eager_prof/run_results.db --top 45 > gpurun_out/r4_eager_step.txt && python3 tools/prof_steplist.py gpurun_out/r4_eager_prof/run_results.db > gpurun_out/r4_eager_steplist.txt && rm -rf gpurun_out/r4_eager_prof && head -30 gpurun_out/r4_eager_step.txt
