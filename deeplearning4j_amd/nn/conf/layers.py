@@ -23,6 +23,8 @@ from .inputs import (InputType, InputTypeConvolutional, InputTypeConvolutionalFl
 from .losses import to_loss
 from .regularization import to_dropout
 from .updaters import to_updater
+from .validation import validate_kernel_geometry
+from ...exceptions import DL4JInvalidConfigException
 from .weights import to_weight_init
 
 
@@ -363,9 +365,10 @@ def conv_out_size(in_size, k, s, p, d, mode):
         return int(math.ceil(in_size / s))
     num = in_size - k_eff + 2 * p
     if num < 0:
-        raise ValueError(f"Invalid input size {in_size} for kernel {k_eff}, padding {p}")
+        raise DL4JInvalidConfigException(f"Invalid input size {in_size} for kernel {k_eff}, padding {p}: the "
+                                         f"kernel is larger than the padded input")
     if mode == ConvolutionMode.Strict and num % s != 0:
-        raise ValueError(
+        raise DL4JInvalidConfigException(
             f"Invalid input/configuration for ConvolutionMode.Strict: (in={in_size} - k={k_eff} + 2*p={p})"
             f" / s={s} is not an integer. Use ConvolutionMode.Truncate or Same.")
     return num // s + 1
@@ -385,6 +388,27 @@ class ConvolutionLayer(FeedForwardLayer):
     _CONVERTERS = dict(FeedForwardLayer._CONVERTERS, kernelSize=int_pair, stride=int_pair, padding=int_pair,
                        dilation=int_pair, convolutionMode=ConvolutionMode.of, cudnnAlgoMode=AlgoMode.of)
     RUNTIME = "deeplearning4j_amd.nn.layers.convolution:ConvolutionLayerImpl"
+    _GEOM_DIMS = 2
+
+    @classmethod
+    def _geom_hook(cls, kw, name, v):
+        """Builder setter of a 2-D geometry field: exactly two values (reference ConvolutionLayer.Builder /
+        SubsamplingLayer.Builder -> ValidationUtils.validate2NonNegative; IllegalStateException)."""
+        if cls._GEOM_DIMS == 2 and not isinstance(v, (list, tuple)):
+            raise DL4JInvalidConfigException(f"{cls.__name__}: {name} needs 2 values, got the single value {v}")
+        kw[name] = int_pair(v)
+
+    @classmethod
+    def _builder_hook_kernelSize(cls, kw, v):
+        cls._geom_hook(kw, "kernelSize", v)
+
+    @classmethod
+    def _builder_hook_stride(cls, kw, v):
+        cls._geom_hook(kw, "stride", v)
+
+    @classmethod
+    def _builder_hook_padding(cls, kw, v):
+        cls._geom_hook(kw, "padding", v)
 
     @classmethod
     def _builder_positional(cls, kw, *args):
@@ -395,6 +419,9 @@ class ConvolutionLayer(FeedForwardLayer):
             args = [vals[i:i + 2] for i in range(0, len(vals), 2)]
         for n, a in zip(names, args):
             kw[n] = int_pair(a)
+
+    def _post_init(self):
+        validate_kernel_geometry(self)
 
     def finalize_defaults(self):
         super().finalize_defaults()
@@ -516,6 +543,7 @@ class DepthwiseConvolution2D(ConvolutionLayer):
 class Convolution1DLayer(ConvolutionLayer):
     """1D conv over RNN-format input [mb, nIn, T] (reference Convolution1DLayer.java:50)."""
     RUNTIME = "deeplearning4j_amd.nn.layers.convolution:Convolution1DLayerImpl"
+    _GEOM_DIMS = 1
 
     @classmethod
     def _builder_positional(cls, kw, *args):
@@ -531,6 +559,7 @@ class Convolution1DLayer(ConvolutionLayer):
                 setattr(self, n, [v[0], 1])
             elif v is not None and len(v) == 2 and n == "padding" and v[0] == v[1] and v[1] != 0:
                 setattr(self, n, [v[0], 0])
+        validate_kernel_geometry(self)
 
     def getOutputType(self, layerIndex, inputType):
         mode = self.convolutionMode or ConvolutionMode.Truncate
@@ -570,6 +599,11 @@ class SubsamplingLayer(Layer):
     _CONVERTERS = dict(Layer._CONVERTERS, kernelSize=int_pair, stride=int_pair, padding=int_pair,
                        dilation=int_pair, convolutionMode=ConvolutionMode.of, poolingType=PoolingType.of)
     RUNTIME = "deeplearning4j_amd.nn.layers.convolution:SubsamplingLayerImpl"
+    _GEOM_DIMS = 2
+    _geom_hook = ConvolutionLayer.__dict__["_geom_hook"]
+    _builder_hook_kernelSize = ConvolutionLayer.__dict__["_builder_hook_kernelSize"]
+    _builder_hook_stride = ConvolutionLayer.__dict__["_builder_hook_stride"]
+    _builder_hook_padding = ConvolutionLayer.__dict__["_builder_hook_padding"]
 
     @classmethod
     def _builder_positional(cls, kw, *args):
@@ -578,6 +612,9 @@ class SubsamplingLayer(Layer):
             kw["poolingType"] = PoolingType.of(args.pop(0))
         for n, a in zip(["kernelSize", "stride", "padding"], args):
             kw[n] = int_pair(a)
+
+    def _post_init(self):
+        validate_kernel_geometry(self)
 
     def finalize_defaults(self):
         if self.convolutionMode is None:
@@ -611,6 +648,7 @@ class Pooling2D(SubsamplingLayer):
 
 class Subsampling1DLayer(SubsamplingLayer):
     RUNTIME = "deeplearning4j_amd.nn.layers.convolution:Subsampling1DLayerImpl"
+    _GEOM_DIMS = 1
 
     @classmethod
     def _builder_positional(cls, kw, *args):
@@ -633,6 +671,7 @@ class Subsampling1DLayer(SubsamplingLayer):
                     setattr(self, n, [v[0], 0])
             elif v[1] != 1:
                 setattr(self, n, [v[0], 1])
+        validate_kernel_geometry(self)
 
     def getOutputType(self, layerIndex, inputType):
         mode = self.convolutionMode or ConvolutionMode.Truncate

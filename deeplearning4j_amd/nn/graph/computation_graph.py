@@ -16,6 +16,8 @@ from ...datasets.dataset import DataSet, MultiDataSet
 from ..conf.enums import BackpropType
 from ..conf.graph import LayerVertex
 from ..conf.layers import ActivationLayer, BatchNormalization
+from ..conf.validation import check_layer_input, validate_network_conf
+from ...exceptions import DL4JInvalidInputException
 from ..layers.output import BaseOutputLayerImpl
 from ..network_base import BaseNetwork
 from ... import profiling as _prof
@@ -57,6 +59,8 @@ class ComputationGraph(BaseNetwork):
         if conf.inputTypes is not None and not hasattr(conf, "_types"):
             conf.addPreProcessorsAndInferNIn()
         self.topo = [n for n in conf.topologicalOrder() if n not in conf.networkInputs]
+        validate_network_conf({n: conf.vertices[n].layerConf for n in self.topo
+                               if isinstance(conf.vertices[n], LayerVertex)})
         self.vertex_inputs = conf.vertexInputs
         self.consumers = {n: [] for n in list(conf.networkInputs) + self.topo}
         for v in self.topo:
@@ -249,6 +253,11 @@ class ComputationGraph(BaseNetwork):
     def feedForward(self, inputs=None, train=False, masks=None, stored_state=False, store_last_for_tbptt=False,
                     layerTillIndex=None):
         inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
+        if len(inputs) != len(self.conf.networkInputs):
+            raise DL4JInvalidInputException(f"ComputationGraph has {len(self.conf.networkInputs)} inputs "
+                                            f"{list(self.conf.networkInputs)}, got {len(inputs)} arrays")
+        chk = self._input_check(inputs)
+        idx = self._index_checked()
         acts = {}
         amask = {}
         mb = inputs[0].shape[0]
@@ -270,6 +279,8 @@ class ComputationGraph(BaseNetwork):
                     x = v.preProcessor.preProcess(x, mb, train)
                     if mask is not None:
                         mask, _ = v.preProcessor.feedForwardMaskArray(mask, None, mb)
+                if chk is not None or name in idx:
+                    check_layer_input(v.layerConf, x, name)
                 if name in self._passthrough:
                     acts[name] = acts[self._passthrough[name]]
                     amask[name] = mask
@@ -298,6 +309,8 @@ class ComputationGraph(BaseNetwork):
                 self._ctx[name] = ("vertex", ctx)
                 acts[name] = out
                 amask[name] = v.feedForwardMask(ms)
+        if chk is not None:
+            self._validated = chk
         self._acts_masks = amask
         return acts
 

@@ -9,6 +9,7 @@ import torch
 from ...ops import softmax_xent
 from ..conf.activations import ActivationSoftmax
 from ..conf.losses import LossMCXENT
+from ..conf.validation import check_labels
 from .base import LayerImpl, add_row, bias_grad_, copy_grad_, matmul, weight_grad_
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
@@ -117,6 +118,8 @@ class BaseOutputLayerImpl(LayerImpl):
     def _loss_and_grad(self):
         if self._cache is not None:
             return self._cache
+        if self.has_params:
+            check_labels(self.conf, self.labels, self.index)
         if self._fused():
             r = self._loss_and_grad_strided()
             if r is not None:

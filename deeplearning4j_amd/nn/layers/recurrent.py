@@ -254,6 +254,16 @@ class BaseRecurrentImpl(LayerImpl):
         self.stateMap = {}
         self.tBpttStateMap = {}
 
+    def _check_state_mb(self, x):
+        """rnnTimeStep continues the stored state, so the minibatch size cannot change between calls without
+        rnnClearPreviousState() (reference TestInvalidInput.testInvalidRnnTimeStep: DL4JInvalidInputException)."""
+        h = self.stateMap.get("prevAct")
+        if h is not None and h.shape[0] != x.shape[0]:
+            from ...exceptions import DL4JInvalidInputException
+            raise DL4JInvalidInputException(
+                f"rnnTimeStep on layer {self.index} ({type(self.conf).__name__}): minibatch size {x.shape[0]} differs "
+                f"from the stored state's {h.shape[0]}; call rnnClearPreviousState() before changing it")
+
     def rnnGetPreviousState(self):
         return dict(self.stateMap)
 
@@ -293,6 +303,7 @@ class LSTMImpl(BaseRecurrentImpl):
         return out
 
     def rnnTimeStep(self, x, mask=None):
+        self._check_state_mb(x)
         is2d = x.dim() == 2
         if is2d:
             x = x.unsqueeze(2)
@@ -383,6 +394,7 @@ class SimpleRnnImpl(BaseRecurrentImpl):
         return out
 
     def rnnTimeStep(self, x, mask=None):
+        self._check_state_mb(x)
         is2d = x.dim() == 2
         if is2d:
             x = x.unsqueeze(2)

@@ -10,6 +10,7 @@ import torch
 from ..datasets.dataset import DataSet, DataSetIterator
 from .conf.enums import BackpropType
 from .conf.layers import ActivationLayer, BatchNormalization
+from .conf.validation import check_layer_input, validate_network_conf
 from .layers.output import BaseOutputLayerImpl
 from .network_base import BaseNetwork
 from .. import profiling as _prof
@@ -32,6 +33,7 @@ class MultiLayerNetwork(BaseNetwork):
         if self.initCalled and parameters is None:
             return
         parameters = parameters if parameters is not None else self._init_params
+        validate_network_conf(self.conf.confs)
         self.layers = [c.instantiate(index=i, net=self) for i, c in enumerate(self.conf.confs)]
         self._setup_flat([(i, self.conf.confs[i].layerName, l) for i, l in enumerate(self.layers)], parameters,
                          cloneParametersArray, device)
@@ -96,10 +98,14 @@ class MultiLayerNetwork(BaseNetwork):
         mb = x.shape[0]
         acts = [x]
         mask = fmask
+        chk = self._input_check([x])
+        idx = self._index_checked()
         for i in range(layerNum + 1):
             layer = self.layers[i]
             x = self._pp(i, x, mb, train)
             mask = self._mask_for(i, mask, mb)
+            if chk is not None or i in idx:
+                check_layer_input(self.conf.confs[i], x, i)
             if i in self._fused_passthrough:
                 acts.append(x)
                 continue
@@ -113,6 +119,8 @@ class MultiLayerNetwork(BaseNetwork):
                 _prof.layer_end(tok, "fwd", i, layer, x)
             mask, _ = layer.feedForwardMaskArray(mask, None, mb)
             acts.append(x)
+        if chk is not None and layerNum == len(self.layers) - 1:
+            self._validated = chk
         return acts
 
     def feedForward(self, x=None, train=False, fmask=None):
@@ -327,6 +335,7 @@ class MultiLayerNetwork(BaseNetwork):
         with torch.no_grad():
             for i, layer in enumerate(self.layers):
                 x = self._pp(i, x, mb, False)
+                check_layer_input(self.conf.confs[i], x, i)
                 if hasattr(layer, "rnnTimeStep"):
                     x = layer.rnnTimeStep(x)
                 else:

@@ -134,6 +134,7 @@ class BaseNetwork:
                 impl.grads[spec.key] = make_view(self.flattenedGradients, o, spec)
                 if self.shadow is not None:
                     impl.cparams[spec.key] = make_view(self.shadow, o, spec)
+                    v._dl4j_shadow = impl.cparams[spec.key]     # a library GEMM's bias epilogue takes the 16-bit copy
                 else:
                     impl.cparams[spec.key] = v
                 o += spec.numel
@@ -523,6 +524,25 @@ class BaseNetwork:
 
     def _feat_dtype(self):
         return self.compute_dtype
+
+    def _input_check(self, inputs):
+        """True when this forward must run the per-layer input checks (conf/validation.py): the first time each
+        network-input shape signature is seen. Layer shapes downstream are a function of it, so repeated steps of
+        the same shape skip the host checks; ``_validated`` is set by the caller once a full forward succeeded."""
+        key = tuple(tuple(t.shape) for t in inputs)
+        if getattr(self, "_validated", None) == key:
+            return None
+        return key
+
+    def _index_checked(self):
+        """Layers whose input VALUES are checked on every forward (embedding index range, host tensors only)."""
+        if getattr(self, "_idx_layers", None) is None:
+            from .conf.layers import EmbeddingLayer
+            confs = self.conf.confs if hasattr(self.conf, "confs") else {
+                n: v.layerConf for n, v in self.conf.vertices.items() if hasattr(v, "layerConf")}
+            items = enumerate(confs) if isinstance(confs, list) else confs.items()
+            self._idx_layers = {k for k, c in items if isinstance(c, EmbeddingLayer)}
+        return self._idx_layers
 
     def summary(self):
         lines = [f"{'idx':>4} {'name':<28} {'type':<32} {'nParams':>12}"]

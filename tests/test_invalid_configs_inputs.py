@@ -1,0 +1,202 @@
+"""Invalid configurations and inputs fail loudly with the DL4J exception types (reference
+CORET:exceptions/TestInvalidConfigurations.java and TestInvalidInput.java, scenario for scenario).
+
+Divergence: a bare ``Builder.kernelSize(3)`` on a 2-D layer raises (as the reference does), and DL4JInvalid*Exception
+also derive from ValueError; label-width mismatches raise ValueError (the reference's IllegalArgumentException from
+the loss function)."""
+import pytest
+import torch
+
+from deeplearning4j_amd import *  # noqa: F401,F403
+from deeplearning4j_amd.exceptions import DL4JException, DL4JInvalidConfigException, DL4JInvalidInputException
+
+
+def _mln(*layers, input_type=None, mode=None, pre=None):
+    b = NeuralNetConfiguration.Builder()
+    if mode is not None:
+        b = b.convolutionMode(mode)
+    lb = b.list()
+    for i, l in enumerate(layers):
+        lb.layer(i, l)
+    if pre:
+        for i, p in pre.items():
+            lb.inputPreProcessor(i, p)
+    if input_type is not None:
+        lb.setInputType(input_type)
+    net = MultiLayerNetwork(lb.build())
+    net.init()
+    return net
+
+
+def _out(nin=None, nout=10):
+    b = OutputLayer.Builder().nOut(nout)
+    return (b.nIn(nin) if nin else b).build()
+
+
+# ------------------------------------------------------------------------------------------------ configurations
+@pytest.mark.parametrize("case", ["dense_nin0", "dense_nout0", "output_nin0", "rnnout_nin0", "lstm_nin0",
+                                  "lstm_nout0", "conv_nin0", "conv_nout0"])
+def test_zero_sizes(case):
+    layers = {
+        "dense_nin0": [DenseLayer.Builder().nIn(0).nOut(10).build(), _out(10)],
+        "dense_nout0": [DenseLayer.Builder().nIn(10).nOut(0).build(), _out(10)],
+        "output_nin0": [DenseLayer.Builder().nIn(10).nOut(10).build(),
+                        OutputLayer.Builder().nIn(0).nOut(10).build()],
+        "rnnout_nin0": [GravesLSTM.Builder().nIn(10).nOut(10).build(),
+                        RnnOutputLayer.Builder().nIn(0).nOut(10).build()],
+        "lstm_nin0": [GravesLSTM.Builder().nIn(0).nOut(10).build(), RnnOutputLayer.Builder().nIn(10).nOut(10).build()],
+        "lstm_nout0": [GravesLSTM.Builder().nIn(10).nOut(0).build(), RnnOutputLayer.Builder().nIn(10).nOut(10).build()],
+        "conv_nin0": [ConvolutionLayer.Builder().nIn(0).nOut(5).build(), _out(5 * 6 * 6)],
+        "conv_nout0": [ConvolutionLayer.Builder().nIn(3).nOut(0).build(), _out(5 * 6 * 6)],
+    }[case]
+    with pytest.raises(DL4JException) as e:
+        _mln(*layers)
+    assert "nIn" in str(e.value) or "nOut" in str(e.value)
+    assert isinstance(e.value, DL4JInvalidConfigException)
+
+
+@pytest.mark.parametrize("kernel", [(3, 2), (2, 3)])
+def test_cnn_strict_mode_bad_padding_strides(kernel):
+    """10x10 input, stride 2: one of (10 - 3)/2 and (10 - 2)/2 is fractional -> Strict fails at init; Truncate builds."""
+    mk = lambda mode: _mln(ConvolutionLayer.Builder().kernelSize(*kernel).stride(2, 2).padding(0, 0).nOut(5).build(),
+                           _out(), input_type=InputType.convolutional(10, 10, 3), mode=mode)
+    mk(None)
+    with pytest.raises(DL4JException):
+        mk(ConvolutionMode.Strict)
+
+
+def test_subsampling_strict_mode_bad_strides():
+    with pytest.raises(DL4JException):
+        _mln(SubsamplingLayer.Builder().kernelSize(2, 3).stride(2, 2).padding(0, 0).build(), _out(),
+             input_type=InputType.convolutional(10, 10, 3), mode=ConvolutionMode.Strict)
+
+
+def test_cnn_data_smaller_than_kernel():
+    net = _mln(ConvolutionLayer.Builder().kernelSize(7, 7).stride(1, 1).padding(0, 0).nOut(5).build(), _out(),
+               input_type=InputType.convolutional(10, 10, 3))
+    with pytest.raises(DL4JException):
+        net.feedForward(torch.zeros(3, 3, 5, 5))
+
+
+def test_cnn_bad_strides_without_input_type():
+    net = _mln(ConvolutionLayer.Builder().kernelSize(3, 3).stride(2, 2).padding(0, 0).nIn(3).nOut(5).build(),
+               _out(5 * 4 * 4), mode=ConvolutionMode.Strict, pre={1: CnnToFeedForwardPreProcessor(inputHeight=4, inputWidth=4, numChannels=5)})
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.zeros(3, 3, 10, 10))
+
+
+@pytest.mark.parametrize("make", [
+    lambda: ConvolutionLayer.Builder().kernelSize(3, 0).build(),
+    lambda: ConvolutionLayer.Builder().kernelSize(2, 2, 2).build(),
+    lambda: ConvolutionLayer.Builder().kernelSize(3, 3).stride(0, 1).build(),
+    lambda: ConvolutionLayer.Builder().kernelSize(3, 3).stride(1).build(),
+    lambda: ConvolutionLayer.Builder().kernelSize(3, 3).stride(1, 1).padding(-1, 0).build(),
+    lambda: ConvolutionLayer.Builder().kernelSize(3, 3).stride(1, 1).padding(0, 0, 0).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(3, 0).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(2).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(3, 3).stride(0, 1).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(3, 3).stride(1, 1, 1).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(3, 3).stride(1, 1).padding(-1, 0).build(),
+    lambda: SubsamplingLayer.Builder().kernelSize(3, 3).stride(1, 1).padding(0).build(),
+], ids=["cnn_kernel", "cnn_kernel3", "cnn_stride", "cnn_stride1", "cnn_padding", "cnn_padding3", "pool_kernel",
+        "pool_kernel1", "pool_stride", "pool_stride3", "pool_padding", "pool_padding1"])
+def test_builder_geometry(make):
+    with pytest.raises(DL4JInvalidConfigException):
+        make()
+
+
+def test_one_d_layers_keep_scalar_setters():
+    c = Convolution1DLayer.Builder().kernelSize(3).stride(2).nIn(2).nOut(4).build()
+    p = Subsampling1DLayer.Builder().kernelSize(2).stride(1).build()
+    assert c.kernelSize == [3, 1] and c.stride == [2, 1] and p.kernelSize == [2, 1]
+
+
+# ------------------------------------------------------------------------------------------------ inputs
+def test_input_nin_mismatch_dense():
+    net = _mln(DenseLayer.Builder().nIn(10).nOut(10).build(), _out(10))
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.zeros(1, 20))
+    net.feedForward(torch.zeros(1, 10))                       # the valid shape still works after the failure
+
+
+def test_input_nin_mismatch_output_layer():
+    net = _mln(DenseLayer.Builder().nIn(10).nOut(20).build(), _out(10))
+    with pytest.raises(DL4JInvalidInputException) as e:
+        net.feedForward(torch.zeros(1, 10))
+    assert "layer 1" in str(e.value)
+
+
+def test_labels_nout_mismatch_output_layer():
+    net = _mln(DenseLayer.Builder().nIn(10).nOut(10).build(), _out(10))
+    with pytest.raises(ValueError):
+        net.fit(torch.zeros(1, 10), torch.zeros(1, 20))
+
+
+def test_labels_nout_mismatch_rnn_output_layer():
+    net = _mln(GravesLSTM.Builder().nIn(5).nOut(5).build(), RnnOutputLayer.Builder().nIn(5).nOut(5).build())
+    with pytest.raises(ValueError):
+        net.fit(torch.zeros(1, 5, 8), torch.zeros(1, 10, 8))
+
+
+def test_input_nin_mismatch_convolutional():
+    net = _mln(ConvolutionLayer.Builder().nIn(3).nOut(5).build(), _out(),
+               input_type=InputType.convolutional(16, 16, 3))
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.zeros(1, 5, 16, 16))
+
+
+@pytest.mark.parametrize("first", ["conv", "pool"])
+def test_rank2_into_cnn(first):
+    l0 = ConvolutionLayer.Builder().nIn(3).nOut(5).build() if first == "conv" else \
+        SubsamplingLayer.Builder().kernelSize(2, 2).build()
+    net = _mln(l0, _out(), input_type=InputType.convolutional(16, 16, 3))
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.zeros(1, 5 * 16 * 16))
+
+
+@pytest.mark.parametrize("rnn", ["lstm", "bidir", "bidir_wrapper"])
+def test_input_nin_mismatch_rnn(rnn):
+    l0 = {"lstm": lambda: GravesLSTM.Builder().nIn(5).nOut(5).build(),
+          "bidir": lambda: GravesBidirectionalLSTM.Builder().nIn(5).nOut(5).build(),
+          "bidir_wrapper": lambda: Bidirectional(LSTM.Builder().nIn(5).nOut(5).build(), mode="ADD")}[rnn]()
+    net = _mln(l0, RnnOutputLayer.Builder().nIn(5).nOut(5).build())
+    with pytest.raises(DL4JInvalidInputException):
+        net.fit(torch.zeros(1, 10, 5), torch.zeros(1, 5, 5))
+
+
+def test_input_mismatch_embedding():
+    net = _mln(EmbeddingLayer.Builder().nIn(10).nOut(10).build(), _out(10))
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.zeros(10, 5))
+    with pytest.raises(DL4JInvalidInputException):
+        net.feedForward(torch.tensor([[3.0], [10.0]]))          # index == nIn
+    net.feedForward(torch.tensor([[3.0], [9.0]]))
+
+
+def test_invalid_rnn_time_step():
+    net = _mln(GravesLSTM.Builder().nIn(5).nOut(5).build(), RnnOutputLayer.Builder().nIn(5).nOut(5).build())
+    net.rnnTimeStep(torch.zeros(3, 5, 10))
+    with pytest.raises(DL4JInvalidInputException):
+        net.rnnTimeStep(torch.zeros(5, 5, 10))
+    net.rnnClearPreviousState()
+    net.rnnTimeStep(torch.zeros(5, 5, 10))
+
+
+def test_computation_graph_input_checks():
+    conf = (NeuralNetConfiguration.Builder().graphBuilder().addInputs("a", "b")
+            .addLayer("d", DenseLayer.Builder().nIn(4).nOut(3).build(), "a")
+            .addLayer("e", DenseLayer.Builder().nIn(2).nOut(3).build(), "b")
+            .addVertex("m", MergeVertex(), "d", "e")
+            .addLayer("out", OutputLayer.Builder().nIn(6).nOut(2).build(), "m").setOutputs("out").build())
+    cg = ComputationGraph(conf)
+    cg.init()
+    with pytest.raises(DL4JInvalidInputException):
+        cg.output(torch.zeros(2, 4))                              # one array for two inputs
+    with pytest.raises(DL4JInvalidInputException):
+        cg.output(torch.zeros(2, 4), torch.zeros(2, 3))           # "e" has nIn 2
+    assert cg.output(torch.zeros(2, 4), torch.zeros(2, 2))[0].shape == (2, 2)
+    bad = (NeuralNetConfiguration.Builder().graphBuilder().addInputs("a")
+           .addLayer("d", DenseLayer.Builder().nIn(4).nOut(0).build(), "a")
+           .addLayer("out", OutputLayer.Builder().nIn(3).nOut(2).build(), "d").setOutputs("out").build())
+    with pytest.raises(DL4JInvalidConfigException):
+        ComputationGraph(bad).init()
