@@ -1,11 +1,11 @@
 """Training UI server.
 
-Reference: PLAY:play/PlayUIServer.java (UIServer.getInstance(), attach/detach StatsStorage, enableRemoteListener,
-port flag / org.deeplearning4j.ui.port), modules train (overview: score vs iteration, update:parameter ratios,
-examples/sec; model: per-layer parameter/update stats and histograms; system: memory and hardware/software info),
-tsne (upload and view coordinates) and remote receiver (RemoteReceiverModule: POST records from
-RemoteUIStatsStorageRouter). Stdlib threaded HTTP server serving JSON APIs plus one self-contained HTML page
-(inline SVG charts; no external assets, the box has no network).
+Reference: PLAY:play/PlayUIServer.java:53-278 (UIServer.getInstance(), attach/detach StatsStorage,
+enableRemoteListener, port flag / org.deeplearning4j.ui.port, the module list and its routes). The server is a stdlib
+threaded HTTP server assembled from UI modules (ui/modules.py): train (overview / model / system / help pages, their
+JSON data, session + worker selection, language switch), convolutional activations, t-SNE, remote receiver and the
+default redirect; plus the flat JSON API (/api/sessions, /api/overview, /api/model, /api/system, /api/tsne).
+Attached storages forward their events to the modules that registered for the event's type ID.
 """
 import json
 import math
@@ -14,7 +14,9 @@ import threading
 import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
-from .storage import InMemoryStatsStorage, Persistable, StatsStorageEvent
+from .modules import (ConvolutionalListenerModule, DefaultModule, RemoteReceiverModule, Request, Response,
+                      TrainModule, TsneModule)
+from .storage import InMemoryStatsStorage, StatsStorageEvent
 from .stats import TYPE_ID
 
 
@@ -76,41 +78,6 @@ def system_view(storage, sid):
             "memory": overview(storage, sid)["memory"]}
 
 
-_PAGE = """<!doctype html><html><head><meta charset="utf-8"><title>DL4J-AMD Training UI</title>
-<style>body{font-family:sans-serif;margin:16px;background:#fafafa}h2{margin:8px 0}.c{background:#fff;border:1px solid
-#ddd;padding:8px;margin:8px 0}svg{background:#fff}table{border-collapse:collapse}td,th{border:1px solid #ddd;
-padding:2px 6px;font-size:12px}</style></head><body>
-<h2>Training overview</h2><div>Session: <select id="sid"></select></div>
-<div class="c"><b>Score vs iteration</b><div id="score"></div></div>
-<div class="c"><b>log10(update : parameter) mean magnitude ratio</b><div id="ratio"></div></div>
-<div class="c"><b>Examples / second</b><div id="perf"></div></div>
-<div class="c"><b>Model (latest report)</b><div id="model"></div></div>
-<div class="c"><b>System</b><pre id="sys"></pre></div>
-<script>
-function line(el, series, w, h){var xs=[],ys=[];series.forEach(function(s){s.pts.forEach(function(p){if(p[1]!=null){
-xs.push(p[0]);ys.push(p[1]);}})});if(!xs.length){el.innerHTML='(no data)';return;}var x0=Math.min.apply(null,xs),
-x1=Math.max.apply(null,xs),y0=Math.min.apply(null,ys),y1=Math.max.apply(null,ys);if(x1==x0)x1=x0+1;if(y1==y0)y1=y0+1;
-var svg='<svg width="'+w+'" height="'+h+'">';var cols=['#1f77b4','#ff7f0e','#2ca02c','#d62728','#9467bd','#8c564b'];
-series.forEach(function(s,i){var d=s.pts.filter(function(p){return p[1]!=null}).map(function(p){return ((p[0]-x0)/(x1-x0)
-*(w-50)+40).toFixed(1)+','+(h-20-(p[1]-y0)/(y1-y0)*(h-30)).toFixed(1)}).join(' ');svg+='<polyline fill="none" stroke="'+
-cols[i%cols.length]+'" points="'+d+'"/>';});svg+='<text x="2" y="12" font-size="10">'+y1.toPrecision(4)+'</text><text x="2"'
-+' y="'+(h-22)+'" font-size="10">'+y0.toPrecision(4)+'</text></svg>';el.innerHTML=svg;}
-function load(){var sid=document.getElementById('sid').value;fetch('api/overview?sid='+sid).then(function(r){return r.json()})
-.then(function(d){line(document.getElementById('score'),[{pts:d.score}],700,220);var rs=[];for(var k in d.updateRatios)
-rs.push({pts:d.updateRatios[k]});line(document.getElementById('ratio'),rs,700,220);line(document.getElementById('perf'),
-[{pts:d.performance}],700,160);});fetch('api/model?sid='+sid).then(function(r){return r.json()}).then(function(d){
-if(!d.latest){return;}var t='<table><tr><th>param</th><th>mean</th><th>stdev</th><th>mean |x|</th><th>update mean |x|</th>'
-+'</tr>';var P=d.latest.stats.Parameters,U=d.latest.stats.Updates||{};for(var k in P){t+='<tr><td>'+k+'</td><td>'+
-(P[k].mean||0).toExponential(3)+'</td><td>'+(P[k].stdev||0).toExponential(3)+'</td><td>'+(P[k].meanMagnitude||0)
-.toExponential(3)+'</td><td>'+((U[k]||{}).meanMagnitude||0).toExponential(3)+'</td></tr>';}document.getElementById('model')
-.innerHTML='iteration '+d.latest.iteration+t+'</table>';});fetch('api/system?sid='+sid).then(function(r){return r.json()})
-.then(function(d){document.getElementById('sys').textContent=JSON.stringify(d.workers,null,1);});}
-fetch('api/sessions').then(function(r){return r.json()}).then(function(s){var e=document.getElementById('sid');
-s.forEach(function(x){var o=document.createElement('option');o.value=x;o.text=x;e.appendChild(o);});e.onchange=load;
-load();setInterval(load,5000);});
-</script></body></html>"""
-
-
 class UIServer:
     _instance = None
     _lock = threading.Lock()
@@ -121,6 +88,10 @@ class UIServer:
         self.remote_storage = None
         self.tsne = {}
         self.httpd = None
+        self.modules = [DefaultModule(), TrainModule(self), ConvolutionalListenerModule(self), TsneModule(self),
+                        RemoteReceiverModule(self)]
+        self._routes = [r for m in self.modules for r in m.getRoutes()]
+        self._listeners = {}
 
     @staticmethod
     def getInstance(port=None):
@@ -132,9 +103,49 @@ class UIServer:
     def attach(self, storage):
         if storage not in self.storages:
             self.storages.append(storage)
+            for m in self.modules:
+                m.onAttach(storage)
+            if hasattr(storage, "registerStatsStorageListener"):
+                lst = _ModuleEventRouter(self.modules)
+                self._listeners[id(storage)] = lst
+                storage.registerStatsStorageListener(lst)
 
     def detach(self, storage):
         self.storages = [s for s in self.storages if s is not storage]
+        lst = self._listeners.pop(id(storage), None)
+        if lst is not None and hasattr(storage, "deregisterStatsStorageListener"):
+            storage.deregisterStatsStorageListener(lst)
+        for m in self.modules:
+            m.onDetach(storage)
+
+    def getModules(self):
+        return list(self.modules)
+
+    def dispatch(self, method, raw_path, body=b""):
+        """Route one request through the modules (then the flat /api endpoints); returns a Response."""
+        u = urllib.parse.urlparse(raw_path)
+        q = dict(urllib.parse.parse_qsl(u.query))
+        path = u.path.rstrip("/") or "/"
+        req = Request(method, path, q, body)
+        for r in self._routes:
+            params = r.match(method, path)
+            if params is not None:
+                return r.fn(req, params)
+        if method == "GET":
+            if path == "/api/sessions":
+                return Response.ok([s for s, _ in _sessions(self.storages)])
+            if path == "/api/tsne":
+                return Response.ok(self.tsne)
+            if path in ("/api/overview", "/api/model", "/api/system"):
+                st = self._find(q.get("sid", ""))
+                if st is None:
+                    return Response.not_found("unknown session")
+                if path == "/api/overview":
+                    return Response.ok(overview(st, q["sid"]))
+                if path == "/api/model":
+                    return Response.ok(model_view(st, q["sid"], q.get("param")))
+                return Response.ok(system_view(st, q["sid"]))
+        return Response.not_found()
 
     def isAttached(self, storage):
         return storage in self.storages
@@ -173,60 +184,23 @@ class UIServer:
             def log_message(self, *a):
                 pass
 
-            def _send(self, code, body, ctype="application/json"):
-                b = body if isinstance(body, bytes) else (body.encode() if isinstance(body, str) else
-                                                          json.dumps(body).encode())
-                self.send_response(code)
-                self.send_header("Content-Type", ctype)
-                self.send_header("Content-Length", str(len(b)))
+            def _serve(self, method):
+                n = int(self.headers.get("Content-Length", 0) or 0)
+                body = self.rfile.read(n) if n else b""
+                r = ui.dispatch(method, self.path, body)
+                self.send_response(r.code)
+                self.send_header("Content-Type", r.ctype)
+                for k, v in r.headers.items():
+                    self.send_header(k, v)
+                self.send_header("Content-Length", str(len(r.body)))
                 self.end_headers()
-                self.wfile.write(b)
+                self.wfile.write(r.body)
 
             def do_GET(self):
-                u = urllib.parse.urlparse(self.path)
-                q = dict(urllib.parse.parse_qsl(u.query))
-                path = u.path.rstrip("/") or "/"
-                if path in ("/", "/train", "/train/overview"):
-                    return self._send(200, _PAGE, "text/html; charset=utf-8")
-                if path == "/api/sessions":
-                    return self._send(200, [s for s, _ in _sessions(ui.storages)])
-                if path == "/api/tsne":
-                    return self._send(200, ui.tsne)
-                st = ui._find(q.get("sid", ""))
-                if st is None:
-                    return self._send(404, {"error": "unknown session"})
-                if path == "/api/overview":
-                    return self._send(200, overview(st, q["sid"]))
-                if path == "/api/model":
-                    return self._send(200, model_view(st, q["sid"], q.get("param")))
-                if path == "/api/system":
-                    return self._send(200, system_view(st, q["sid"]))
-                return self._send(404, {"error": "not found"})
+                self._serve("GET")
 
             def do_POST(self):
-                n = int(self.headers.get("Content-Length", 0))
-                raw = self.rfile.read(n)
-                if self.path == "/remoteReceive":
-                    if ui.remote_storage is None:
-                        return self._send(403, {"error": "remote listener not enabled"})
-                    try:
-                        msg = json.loads(raw)
-                        r = Persistable.decode(json.dumps(msg["record"]))
-                        {"meta": ui.remote_storage.putStorageMetaData, "static": ui.remote_storage.putStaticInfo,
-                         "update": ui.remote_storage.putUpdate}[msg["type"]](r)
-                        return self._send(200, {"status": "ok"})
-                    except (KeyError, ValueError) as e:
-                        return self._send(400, {"error": str(e)})
-                if self.path.startswith("/tsne/upload"):
-                    name = dict(urllib.parse.parse_qsl(urllib.parse.urlparse(self.path).query)).get("name", "upload")
-                    rows = []
-                    for line in raw.decode("utf-8").splitlines():
-                        p = line.strip().split(",")
-                        if len(p) >= 3:
-                            rows.append([float(p[0]), float(p[1]), ",".join(p[2:]).strip()])
-                    ui.tsne[name] = rows
-                    return self._send(200, {"status": "ok", "points": len(rows)})
-                return self._send(404, {"error": "not found"})
+                self._serve("POST")
         return H
 
     def start(self):
@@ -243,6 +217,18 @@ class UIServer:
         with UIServer._lock:
             if UIServer._instance is self:
                 UIServer._instance = None
+
+
+class _ModuleEventRouter:
+    """StatsStorage listener forwarding each event to the modules registered for its type ID."""
+
+    def __init__(self, modules):
+        self.modules = modules
+
+    def notify(self, event):
+        for m in self.modules:
+            if getattr(event, "typeID", None) in m.getCallbackTypeIDs():
+                m.reportStorageEvents([event])
 
 
 _ = StatsStorageEvent
