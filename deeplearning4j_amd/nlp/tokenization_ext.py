@@ -2,13 +2,14 @@
 StemmingPreprocessor / PoS tokenizers, deeplearning4j-nlp-japanese (Kuromoji), -chinese (ansj), -korean), plus a
 BERT WordPiece tokenizer for the transformer path.
 
-The reference's Japanese/Chinese/Korean modules ship large morphological dictionaries; none are in this image, so
-these are dictionary-free segmenters with the same TokenizerFactory API:
-* Japanese: script-run segmentation (kanji / hiragana / katakana / latin / digits), hiragana particle splitting.
+Japanese: the lattice / Viterbi morphological analyser of ``nlp/kuromoji.py`` (Kuromoji's algorithm; MeCab/IPADIC
+dictionaries load from their source files, a small built-in lexicon otherwise). The Chinese and Korean modules'
+dictionaries are not in this image, so those two are dictionary-free segmenters with the same TokenizerFactory API:
 * Chinese: one token per Han character (the standard dictionary-free baseline), latin/digit runs kept whole.
 * Korean: whitespace eojeol split with trailing postposition (josa) stripping.
 The Porter stemmer (English) is the algorithm behind the UIMA module's StemmingPreprocessor.
 """
+import os
 import re
 import unicodedata
 
@@ -166,39 +167,35 @@ class _SegmentingFactory(TokenizerFactory):
         return Tokenizer(self.segment(text), self.pre)
 
 
-_JA_PARTICLES = ("は", "が", "を", "に", "へ", "で", "と", "も", "の", "や", "から", "まで", "より")
-
-
 class JapaneseTokenizerFactory(_SegmentingFactory):
-    """Script-run segmentation; hiragana runs that start with a particle are split after it."""
+    """Morphological analysis on the lattice / Viterbi analyser of ``nlp/kuromoji.py`` (reference
+    deeplearning4j-nlp-japanese JapaneseTokenizerFactory / JapaneseTokenizer, Kuromoji IPADIC tokenizer).
+
+    useBaseForm: emit each token's dictionary form (``驚い`` -> ``驚く``). lexicon: a ``kuromoji.Lexicon`` (default:
+    the MeCab/IPADIC directory named by ``DL4J_AMD_JA_DICT`` when set, else the small built-in lexicon).
+    userDictionary: a ``kuromoji.UserDictionary`` or its text. mode: ``kuromoji.Mode.NORMAL`` / ``SEARCH``."""
+
+    def __init__(self, useBaseForm=False, lexicon=None, userDictionary=None, mode="NORMAL"):
+        super().__init__()
+        from . import kuromoji as K
+        if lexicon is None:
+            d = os.environ.get("DL4J_AMD_JA_DICT")
+            lexicon = K.Lexicon.from_mecab_dir(d) if d else K.builtin_lexicon()
+        if isinstance(userDictionary, str):
+            userDictionary = K.UserDictionary.parse(userDictionary)
+        self.useBaseForm = useBaseForm
+        self.analyzer = K.LatticeTokenizer(lexicon, userDictionary, mode)
+
+    def tokens(self, text):
+        """The analyser's Token objects (surface, features, base form, reading)."""
+        return self.analyzer.tokenize(text)
 
     def segment(self, text):
-        toks, cur, cs = [], "", None
-        for ch in unicodedata.normalize("NFKC", text):
-            s = _script(ch)
-            if s in ("space", "punct"):
-                if cur:
-                    toks.append(cur)
-                cur, cs = "", None
-                continue
-            if cs is not None and s != cs:
-                toks.append(cur)
-                cur = ""
-            cur += ch
-            cs = s
-        if cur:
-            toks.append(cur)
         out = []
-        for t in toks:
-            if _script(t[0]) == "hira":
-                for p in sorted(_JA_PARTICLES, key=len, reverse=True):
-                    if t.startswith(p) and len(t) > len(p):
-                        out.extend([p, t[len(p):]])
-                        break
-                else:
-                    out.append(t)
-            else:
-                out.append(t)
+        for t in self.analyzer.tokenize(text):
+            if t.surface.isspace():
+                continue
+            out.append(t.getBaseForm() if self.useBaseForm else t.surface)
         return out
 
 
