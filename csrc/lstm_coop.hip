@@ -580,3 +580,482 @@ DL4J_API int dl4j_lstm_fwd_coop(const void* zx, const void* rwt, const float* pe
 #undef FWD_ARGS
   return -1;
 }
+
+// ================================================================================================ two-layer stack
+// Pipelined two-layer LSTM (the text models' GravesLSTM -> GravesLSTM stack, reference MultiLayerNetwork.java:
+// 1521-1593 rnnTimeStep / TBPTT over stacked layers): ONE launch runs both layers' recurrences, layer 2 at step t
+// concurrently with layer 1 at step t+1, so the serial chain of a window is T + 1 steps instead of 2T.
+//   grid.x = 2G workgroups per 16-row tile (G = H / 32): blockIdx.x < G are layer 1, the rest layer 2; U = 32 units
+//   per workgroup (2 waves), so layer 2's RW slice AND its input-weight slice fit in LDS together.
+// Forward: layer 1 runs as lstm_fwd_coop and also publishes h1_t into a T-slot "cross ring" of tagged granules;
+// layer 2 gathers h2_{t-1} (own exchange) and h1_t (cross ring) into one [16][2H] LDS row block and computes
+// z = [h2_{t-1} | h1_t] . [RW2 ; W2] + b2 in one MFMA loop (its input projection moves into the recurrence).
+// Backward: layer 2 runs as lstm_bwd_coop and additionally multiplies its dz2_t slice by its W2^T slice: those
+// K-split partials of eps1_t = dz2_t . W2^T go through a T-slot cross ring to the layer-1 workgroup owning each unit,
+// which sums them in a fixed producer order (deterministic) instead of reading eps from memory.
+// Tags, timeouts, the step guard and the launch rules are those of the single-layer kernels; both rings are indexed
+// by the time step (no slot reuse inside a launch), so the stack path is used for T <= kStackMaxT.
+constexpr int kStackMaxT = 128;
+
+struct Stack2Fwd {
+  const __bf16* zx1; const __bf16* rw1; const __bf16* rw2; const __bf16* w2;
+  const float* b2; const float* peep1; const float* peep2;
+  const float* h0_1; const float* c0_1; const float* h0_2; const float* c0_2;
+  const float* mask;
+  float* out1; __bf16* o16_1; float* gates1; float* call1; float* hT1; float* cT1;
+  float* out2; __bf16* o16_2; float* gates2; float* call2; float* hT2; float* cT2;
+  unsigned long long* exch; unsigned* err;
+  int Tn, mb;
+  long long timeout;
+  unsigned tag_arg;
+  long long exch_words;
+};
+
+template <int H, bool PEEP>
+__global__ void __launch_bounds__(128) lstm_fwd_stack2(Stack2Fwd a) {
+  constexpr int U = 32, NW = 2, G = H / U, KS = H / 32, H16 = H / 16, H4 = 4 * H;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int role = blockIdx.x / G, grp = blockIdx.x - role * G, tile = blockIdx.y, tiles = gridDim.y;
+  const int KSR = role ? 2 * KS : KS;
+  bf16x8c_t* rws = reinterpret_cast<bf16x8c_t*>(smem);                        // [4][NW][KSR][64]
+  __bf16* hbuf = reinterpret_cast<__bf16*>(smem + (size_t)4 * NW * KSR * 64 * 16);
+  const int ldh = role ? 2 * H + 8 : H + 8;                                   // role 1: [h2_{t-1} | h1_t]
+  gu64* exch = (gu64*)a.exch;
+  gu32* err = (gu32*)a.err;
+  const unsigned tag_base = coop_tag_begin(err, a.tag_arg);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
+  const int m0 = tile * 16, u0 = grp * U, j = u0 + wave * 16 + col;
+  const int Tn = a.Tn, mb = a.mb;
+  const __bf16* RWp = role ? a.rw2 : a.rw1;
+  for (int i = threadIdx.x; i < 4 * NW * KSR * 64; i += blockDim.x) {
+    const int ln = i & 63, t1 = i >> 6;
+    const int ks = t1 % KSR, t2 = t1 / KSR;
+    const int w = t2 % NW, g = t2 / NW;
+    const long long gt = (long long)g * H16 + (u0 >> 4) + w;
+    const __bf16* src = ks < KS ? RWp : a.w2;
+    rws[i] = *reinterpret_cast<const bf16x8c_t*>(src + ((gt * KS + (ks % KS)) * 64 + ln) * 8);
+  }
+  const float* peep = role ? a.peep2 : a.peep1;
+  const float* h0 = role ? a.h0_2 : a.h0_1;
+  const float* c0 = role ? a.c0_2 : a.c0_1;
+  float* out = role ? a.out2 : a.out1;
+  __bf16* out16 = role ? a.o16_2 : a.o16_1;
+  float* gates = role ? a.gates2 : a.gates1;
+  float* call = role ? a.call2 : a.call1;
+  int mrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mrow[r] = min(m0 + rg + r, mb - 1);
+  float c[4], wff = 0.f, woo = 0.f, wgg = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[r] = (c0 && m0 + rg + r < mb) ? c0[(long long)mrow[r] * H + j] : 0.f;
+  if (PEEP) {
+    wff = peep[j];
+    woo = peep[H + j];
+    wgg = peep[2 * H + j];
+  }
+  float zv[4][4], mv[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (role) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bv[g] = a.b2 ? a.b2[g * H + j] : 0.f;
+  }
+  auto load_step = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (role == 0) {
+        const long long zrow = ((long long)t * mb + mrow[r]) * H4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) zv[g][r] = (float)a.zx1[zrow + g * H + j];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) zv[g][r] = bv[g];
+      }
+      mv[r] = a.mask ? a.mask[(long long)mrow[r] * Tn + t] : 1.f;
+    }
+  };
+  load_step(0);
+  constexpr int npairs = 16 * (H / 2);
+  gu64* own = exch + ((long long)role * tiles + tile) * 2 * npairs;
+  gu64* ring = exch + 2LL * tiles * 2 * npairs + (long long)tile * Tn * npairs;
+  // sweep the tagged granules of one [16][H] bf16 tile into columns [coff, coff + H) of hb
+  auto sweep = [&](gu64* src, unsigned tag, __bf16* hb, int coff) {
+    const long long deadline = wall_clock64() + a.timeout;
+    for (int base = 0; base < npairs; base += 8 * blockDim.x) {
+      unsigned long long v[8];
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int i = base + q * blockDim.x + threadIdx.x;
+          v[q] = i < npairs ? __hip_atomic_load(src + i, RLX_AGENT) : ((unsigned long long)tag << 32);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == tag;
+        if (ok) break;
+        if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
+          __hip_atomic_store(err, 1u, RLX_AGENT);
+          __hip_atomic_store((gu32*)&g_lstm_step_guard, 1u, RLX_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = base + q * blockDim.x + threadIdx.x;
+        if (i < npairs) {
+          const int r = i / (H / 2), k = (i - r * (H / 2)) * 2;
+          *reinterpret_cast<unsigned*>(hb + r * ldh + coff + k) = (unsigned)v[q];
+        }
+      }
+    }
+  };
+  for (int t = 0; t < Tn; ++t) {
+    __bf16* hb = hbuf + (role == 0 ? (t & 1) * 16 * ldh : 0);
+    if (t == 0) {
+      for (int i = threadIdx.x; i < 16 * H; i += blockDim.x) {
+        const int r = i / H, k = i - r * H, m = m0 + r;
+        hb[r * ldh + k] = (__bf16)((h0 && m < mb) ? h0[(long long)m * H + k] : 0.f);
+      }
+    } else {
+      sweep(own + (long long)((t - 1) & 1) * npairs, tag_base + (unsigned)t, hb, 0);
+    }
+    if (role) sweep(ring + (long long)t * npairs, tag_base + (unsigned)t + 1u, hb, H);
+    __syncthreads();
+    f4c_t acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f4c_t{0.f, 0.f, 0.f, 0.f};
+    const __bf16* hA = hb + col * ldh + 8 * hgrp;
+    for (int ks = 0; ks < KSR; ++ks) {
+      const bf16x8c_t av = *reinterpret_cast<const bf16x8c_t*>(hA + ks * 32);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, rws[((g * NW + wave) * KSR + ks) * 64 + lane], acc[g], 0,
+                                                         0, 0);
+    }
+    if (role) __syncthreads();                             // single h tile: the next sweep overwrites it
+    gu64* dst = own + (long long)(t & 1) * npairs;
+    gu64* rdst = ring + (long long)t * npairs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = rg + r;
+      const bool valid = m0 + rr < mb;
+      const float za = acc[0][r] + zv[0][r];
+      float zf = acc[1][r] + zv[1][r];
+      float zo = acc[2][r] + zv[2][r];
+      float zg = acc[3][r] + zv[3][r];
+      const float cp = c[r];
+      if (PEEP) {
+        zf += cp * wff;
+        zg += cp * wgg;
+      }
+      const float av = tanh_c(za), f = sigm_c(zf), g = sigm_c(zg);
+      float cc = f * cp + g * av;
+      if (PEEP) zo += cc * woo;
+      const float o = sigm_c(zo);
+      float h = o * tanh_c(cc) * mv[r];
+      cc *= mv[r];
+      if (!valid) {
+        h = 0.f;
+        cc = 0.f;
+      }
+      c[r] = cc;
+      if (valid) {
+        const long long orow = ((long long)t * mb + m0 + rr) * H;
+        out[orow + j] = h;
+        if (out16) out16[orow + j] = (__bf16)h;
+        if (call) call[orow + j] = cc;
+        if (gates) {
+          float* gp = gates + orow * 4 + j;
+          gp[0] = av;
+          gp[H] = f;
+          gp[2 * H] = o;
+          gp[3 * H] = g;
+        }
+      }
+      const float hn = __shfl_xor(h, 1, 64);
+      if ((col & 1) == 0) {
+        const __bf16 lo = (__bf16)h, hi = (__bf16)hn;
+        const unsigned pay = (unsigned)(*reinterpret_cast<const unsigned short*>(&lo)) |
+                             ((unsigned)(*reinterpret_cast<const unsigned short*>(&hi)) << 16);
+        const unsigned long long gv = ((unsigned long long)(tag_base + t + 1) << 32) | pay;
+        __hip_atomic_store(dst + rr * (H / 2) + (j >> 1), gv, RLX_AGENT);
+        if (role == 0) __hip_atomic_store(rdst + rr * (H / 2) + (j >> 1), gv, RLX_AGENT);
+      }
+    }
+    if (t + 1 < Tn) load_step(t + 1);
+  }
+  float* hT = role ? a.hT2 : a.hT1;
+  float* cT = role ? a.cT2 : a.cT1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + rg + r;
+    if (m < mb) {
+      if (cT) cT[(long long)m * H + j] = c[r];
+      if (hT) hT[(long long)m * H + j] = out[((long long)(Tn - 1) * mb + m) * H + j];
+    }
+  }
+  coop_tag_end(err, exch, a.exch_words, a.tag_arg, tag_base, (unsigned)Tn + 2u, reinterpret_cast<unsigned*>(smem));
+}
+
+struct Stack2Bwd {
+  const void* eps2; int eps_dt; int pad_;
+  const float* gates1; const float* call1; const float* c0_1;
+  const float* gates2; const float* call2; const float* c0_2;
+  const __bf16* rw1; const __bf16* rw2; const __bf16* w2;                     // backward (B = RW / W) images
+  const float* peep1; const float* peep2; const float* mask;
+  const float* dhl1; const float* dcl1; const float* dhl2; const float* dcl2;
+  float* dz1; float* dz2; float* dh0_1; float* dc0_1; float* dh0_2; float* dc0_2;
+  unsigned long long* exch; unsigned* err;
+  int Tn, mb, t_end;
+  long long timeout;
+  unsigned tag_arg;
+  long long exch_words;
+};
+
+template <int H, bool PEEP>
+__global__ void __launch_bounds__(128) lstm_bwd_stack2(Stack2Bwd a) {
+  constexpr int U = 32, NW = 2, G = H / U, NTW = (H / 16) / NW, KL = 4 * U / 32, KSG = 4 * H / 32, LDZ = 4 * U + 8;
+  constexpr int NE = 4 * G, BATCH = NE < 16 ? NE : 16;
+  constexpr int H4 = 4 * H;
+  constexpr int RWS = (H / 16) * KL * 64;                 // fragments of one resident slice
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int role = blockIdx.x / G, grp = blockIdx.x - role * G, tile = blockIdx.y, tiles = gridDim.y;
+  bf16x8c_t* rws = reinterpret_cast<bf16x8c_t*>(smem);                       // RW^T slice (+ W2^T slice, role 1)
+  __bf16* zbuf = reinterpret_cast<__bf16*>(smem + (size_t)(role ? 2 : 1) * RWS * 16);   // [2][16][LDZ]
+  gu64* exch = (gu64*)a.exch;
+  gu32* err = (gu32*)a.err;
+  const unsigned tag_base = coop_tag_begin(err, a.tag_arg);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4, rg = hgrp * 4;
+  const int m0 = tile * 16, u0 = grp * U;
+  const int ul = wave * 16 + col, j = u0 + ul;
+  const int Tn = a.Tn, mb = a.mb, t_end = a.t_end;
+  const __bf16* RWp = role ? a.rw2 : a.rw1;
+  for (int i = threadIdx.x; i < (role ? 2 : 1) * RWS; i += blockDim.x) {
+    const int ii = i % RWS;
+    const int ln = ii & 63, t1 = ii >> 6;
+    const int sl = t1 % KL, nt = t1 / KL;
+    const int kg = ((32 * sl) / U) * (H / 32) + (u0 + (32 * sl) % U) / 32;
+    const __bf16* src = i < RWS ? RWp : a.w2;
+    rws[i] = *reinterpret_cast<const bf16x8c_t*>(src + (((long long)nt * KSG + kg) * 64 + ln) * 8);
+  }
+  const float* gates = role ? a.gates2 : a.gates1;
+  const float* call = role ? a.call2 : a.call1;
+  const float* c0 = role ? a.c0_2 : a.c0_1;
+  const float* peep = role ? a.peep2 : a.peep1;
+  const float* dh_last = role ? a.dhl2 : a.dhl1;
+  const float* dc_last = role ? a.dcl2 : a.dcl1;
+  float* dz = role ? a.dz2 : a.dz1;
+  float* dh0 = role ? a.dh0_2 : a.dh0_1;
+  float* dc0 = role ? a.dc0_2 : a.dc0_1;
+  int mrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mrow[r] = min(m0 + rg + r, mb - 1);
+  float dhn[4], dcn[4], wff = 0.f, woo = 0.f, wgg = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool v = m0 + rg + r < mb;
+    dhn[r] = (dh_last && v) ? dh_last[(long long)mrow[r] * H + j] : 0.f;
+    dcn[r] = (dc_last && v) ? dc_last[(long long)mrow[r] * H + j] : 0.f;
+  }
+  if (PEEP) {
+    wff = peep[j];
+    woo = peep[H + j];
+    wgg = peep[2 * H + j];
+  }
+  float ev[4], av[4], fv[4], ov[4], gv[4], cv[4], pv[4], mv[4];
+  auto load_step = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long hrow = ((long long)t * mb + mrow[r]) * H, grow = hrow * 4;
+      if (role) ev[r] = ld_any(a.eps2, a.eps_dt, hrow + j);
+      av[r] = gates[grow + j];
+      fv[r] = gates[grow + H + j];
+      ov[r] = gates[grow + 2 * H + j];
+      gv[r] = gates[grow + 3 * H + j];
+      cv[r] = call[hrow + j];
+      pv[r] = t > 0 ? call[hrow - (long long)mb * H + j] : (c0 ? c0[(long long)mrow[r] * H + j] : 0.f);
+      mv[r] = a.mask ? a.mask[(long long)mrow[r] * Tn + t] : 1.f;
+    }
+  };
+  const long long slot_sz = (long long)G * G * 16 * U;
+  gu64* own = exch + ((long long)role * tiles + tile) * 2 * slot_sz;
+  gu64* ring = exch + 2LL * tiles * 2 * slot_sz + (long long)tile * Tn * slot_sz;
+  // sum of the G producers' partials of (rows rg..rg+3, unit ul) in slot `src` carrying tag `tag`
+  auto gather = [&](const gu64* slot, unsigned tag, float* res) {
+    const gu64* src = slot + (long long)grp * G * 16 * U;
+    const long long deadline = wall_clock64() + a.timeout;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) res[r] = 0.f;
+#pragma unroll
+    for (int b0 = 0; b0 < NE; b0 += BATCH) {
+      unsigned long long v[BATCH];
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+          const int e = b0 + q, g = e >> 2, r = e & 3;
+          v[q] = __hip_atomic_load(src + ((long long)g * 16 + rg + r) * U + ul, RLX_AGENT);
+        }
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) ok &= (unsigned)(v[q] >> 32) == tag;
+        if (ok) break;
+        if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
+          __hip_atomic_store(err, 1u, RLX_AGENT);
+          __hip_atomic_store((gu32*)&g_lstm_step_guard, 1u, RLX_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int q = 0; q < BATCH; ++q) res[(b0 + q) & 3] += __uint_as_float((unsigned)v[q]);
+    }
+  };
+  // K-split partial of (16 rows x H) = zb . B over this workgroup's gate columns, published to the owners' slots
+  auto partial = [&](const __bf16* zb, const bf16x8c_t* B, gu64* slot, unsigned tag) {
+    f4c_t acc[NTW];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4c_t{0.f, 0.f, 0.f, 0.f};
+    const __bf16* zA = zb + col * LDZ + 8 * hgrp;
+#pragma unroll
+    for (int sl = 0; sl < KL; ++sl) {
+      const bf16x8c_t av_ = *reinterpret_cast<const bf16x8c_t*>(zA + sl * 32);
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av_, B[((wave * NTW + nt) * KL + sl) * 64 + lane], acc[nt],
+                                                          0, 0, 0);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wave * NTW + nt) * 16 + col;
+      const int cons = n / U, un = n - cons * U;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __hip_atomic_store(slot + (((long long)cons * G + grp) * 16 + rg + r) * U + un,
+                           ((unsigned long long)tag << 32) | __float_as_uint(acc[nt][r]), RLX_AGENT);
+    }
+  };
+  load_step(Tn - 1);
+  int it = 0;
+  for (int t = Tn - 1; t >= t_end; --t, ++it) {
+    if (it > 0) gather(own + (long long)((it - 1) & 1) * slot_sz, tag_base + (unsigned)it, dhn);
+    if (role == 0) gather(ring + (long long)t * slot_sz, tag_base + (unsigned)t + 1u, ev);   // eps1_t from layer 2
+    __bf16* zb = zbuf + (it & 1) * 16 * LDZ;
+    float dza[4], dzf[4], dzo[4], dzg[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool valid = m0 + rg + r < mb;
+      const float dh = (ev[r] + dhn[r]) * mv[r];
+      float dc = dcn[r] * mv[r];
+      const float a_ = av[r], f = fv[r], o = ov[r], g = gv[r];
+      const float ca = tanh_c(cv[r]);
+      const float zo_ = dh * ca * o * (1.f - o);
+      dc += dh * o * (1.f - ca * ca);
+      if (PEEP) dc += zo_ * woo;
+      const float zf_ = dc * pv[r] * f * (1.f - f);
+      const float zg_ = dc * a_ * g * (1.f - g);
+      const float za_ = dc * g * (1.f - a_ * a_);
+      float dcp = dc * f;
+      if (PEEP) dcp += zf_ * wff + zg_ * wgg;
+      dcn[r] = valid ? dcp : 0.f;
+      dza[r] = valid ? za_ : 0.f;
+      dzf[r] = valid ? zf_ : 0.f;
+      dzo[r] = valid ? zo_ : 0.f;
+      dzg[r] = valid ? zg_ : 0.f;
+    }
+    if (t - 1 >= t_end) load_step(t - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = rg + r;
+      zb[rr * LDZ + ul] = (__bf16)dza[r];
+      zb[rr * LDZ + U + ul] = (__bf16)dzf[r];
+      zb[rr * LDZ + 2 * U + ul] = (__bf16)dzo[r];
+      zb[rr * LDZ + 3 * U + ul] = (__bf16)dzg[r];
+      if (m0 + rr < mb) {
+        float* dp = dz + ((long long)t * mb + m0 + rr) * H4 + j;
+        dp[0] = dza[r];
+        dp[H] = dzf[r];
+        dp[2 * H] = dzo[r];
+        dp[3 * H] = dzg[r];
+      }
+    }
+    __syncthreads();
+    if (role) partial(zb, rws + RWS, ring + (long long)t * slot_sz, tag_base + (unsigned)t + 1u);   // eps1_t
+    if (t == t_end && !dh0) break;
+    partial(zb, rws, own + (long long)(it & 1) * slot_sz, tag_base + (unsigned)it + 1u);           // dh_{t-1}
+  }
+  const int iters = Tn - t_end;
+  if (dh0) gather(own + (long long)((iters - 1) & 1) * slot_sz, tag_base + (unsigned)iters, dhn);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + rg + r;
+    if (m < mb) {
+      if (dh0) dh0[(long long)m * H + j] = dhn[r];
+      if (dc0) dc0[(long long)m * H + j] = dcn[r];
+    }
+  }
+  coop_tag_end(err, exch, a.exch_words, a.tag_arg, tag_base, (unsigned)Tn + 2u, reinterpret_cast<unsigned*>(smem));
+}
+
+static long long stack2_fwd_exch_words(int mb, int H, int Tn) {
+  const long long tiles = (mb + 15) / 16, npairs = 16LL * (H / 2);
+  return 2 * tiles * 2 * npairs + tiles * Tn * npairs;
+}
+
+static long long stack2_bwd_exch_words(int mb, int H, int Tn) {
+  const long long tiles = (mb + 15) / 16, G = H / 32, slot = G * G * 16 * 32;
+  return 2 * tiles * 2 * slot + tiles * Tn * slot;
+}
+
+DL4J_API long long dl4j_lstm_stack2_exch_bytes(int mb, int H, int Tn, int bwd) {
+  return 8 * (bwd ? stack2_bwd_exch_words(mb, H, Tn) : stack2_fwd_exch_words(mb, H, Tn));
+}
+
+DL4J_API int dl4j_lstm_stack2_max_t() { return kStackMaxT; }
+
+template <typename K, typename A>
+static int stack2_launch(K k, A& args, size_t lds, int H, int mb, int reset, long long words, hipStream_t s) {
+  if (lds > 160 * 1024) return -1;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return -1;
+  const dim3 grid(2 * (H / 32), (mb + 15) / 16), block(128);
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    return -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, block.x, lds) != hipSuccess || per < 1) return -1;
+  if ((long long)grid.x * grid.y > (long long)ncu - 8) return -1;
+  if (reset && hipMemsetAsync(args.exch, 0, (size_t)words * 8, s) != hipSuccess) return -1;
+  if (reset && hipMemsetAsync(args.err, 0, 16, s) != hipSuccess) return -1;
+  void* kargs[] = {(void*)&args};
+  const hipError_t e = coop_launch(reinterpret_cast<const void*>(k), grid, block, kargs, lds, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return 0;
+}
+
+// bf16, H = 256 only, T <= kStackMaxT. Pointers of the per-layer outputs may be null where the single-layer kernel
+// allows it (out16, gates, call, hT, cT). Returns -1 when the stack path does not apply.
+DL4J_API int dl4j_lstm_fwd_stack2(const Stack2Fwd* p, int H, int reset, hipStream_t s) {
+  Stack2Fwd a = *p;
+  if (H != 256 || a.Tn < 1 || a.Tn > kStackMaxT || a.mb < 1) return -1;
+  a.timeout = 200LL * 1000 * 1000;
+  a.exch_words = stack2_fwd_exch_words(a.mb, H, a.Tn);
+  constexpr int KS = 256 / 32;
+  const size_t lds = (size_t)4 * 2 * (2 * KS) * 64 * 16 + 16ull * (2 * 256 + 8) * 2;   // role 1 (the larger)
+  return a.peep1 ? stack2_launch(lstm_fwd_stack2<256, true>, a, lds, H, a.mb, reset, a.exch_words, s)
+                 : stack2_launch(lstm_fwd_stack2<256, false>, a, lds, H, a.mb, reset, a.exch_words, s);
+}
+
+DL4J_API int dl4j_lstm_bwd_stack2(const Stack2Bwd* p, int H, int reset, hipStream_t s) {
+  Stack2Bwd a = *p;
+  if (H != 256 || a.Tn < 1 || a.Tn > kStackMaxT || a.mb < 1 || a.t_end < 0 || a.t_end >= a.Tn) return -1;
+  a.timeout = 200LL * 1000 * 1000;
+  a.exch_words = stack2_bwd_exch_words(a.mb, H, a.Tn);
+  const size_t lds = (size_t)2 * (256 / 16) * 4 * 64 * 16 + 2ull * 16 * (4 * 32 + 8) * 2;
+  return a.peep1 ? stack2_launch(lstm_bwd_stack2<256, true>, a, lds, H, a.mb, reset, a.exch_words, s)
+                 : stack2_launch(lstm_bwd_stack2<256, false>, a, lds, H, a.mb, reset, a.exch_words, s);
+}
+
+DL4J_API int dl4j_lstm_stack2_struct_bytes(int bwd) { return bwd ? (int)sizeof(Stack2Bwd) : (int)sizeof(Stack2Fwd); }

@@ -151,8 +151,16 @@ def _lstm_bwd_native(eps, cache, W, RW, H, peephole, mask, tbptt_back, grads_pre
     if r is None:
         return None
     dz, dh0, dc0 = r
+    return _native_weight_grads(dz, cache, W, H, peephole, grads_prefix, grads, need_dx, dh0, dc0)
+
+
+def _native_weight_grads(dz, cache, W, H, peephole, grads_prefix, grads, need_dx, dh0, dc0):
+    """Weight / bias / peephole gradients (and dL/dinput when ``need_dx``) from the sequence kernels' gate deltas
+    dz [T, mb, 4H] fp32 (LSTMHelpers.java:616-676)."""
+    from ...ops import rnn_native
+    T, mb = dz.shape[0], dz.shape[1]
     out = cache["out"]                                                # [T, mb, H] fp32
-    dev = eps.device
+    dev = dz.device
     if W.dtype in (torch.bfloat16, torch.float16):
         prep = rnn_native.lstm_bwd_prep(dz, out, cache["h0"], cache["call"], cache["c0"], peephole, W.dtype)
         if prep is not None:
@@ -296,11 +304,79 @@ class LSTMImpl(BaseRecurrentImpl):
         h0 = c0 = None
         if stored_state:
             h0, c0 = self.tBpttStateMap.get("prevAct"), self.tBpttStateMap.get("prevMem")
-        out, (h, c), cache = self._run(x, training, h0, c0, training, mask)
+        pend = getattr(self, "_stack_pending", None)
+        self._stack_pending = None
+        if pend is not None and pend[0] is x:
+            out, (h, c), cache = pend[1]              # computed by the layer below in one stacked launch
+        else:
+            nxt = getattr(self, "_stack_next", None)
+            r = self._stack_forward(nxt, x, h0, c0, mask, stored_state, training) if nxt is not None else None
+            if r is None:
+                r = self._run(x, training, h0, c0, training, mask)
+            out, (h, c), cache = r
         self._cache = cache
         if store_last_for_tbptt:
             self.tBpttStateMap = {"prevAct": h.detach(), "prevMem": c.detach()}
         return out
+
+    # ---- pipelined two-layer stack (csrc/lstm_coop.hip lstm_fwd_stack2 / lstm_bwd_stack2)
+    def _stack_forward(self, nxt, x, h0, c0, mask, stored_state, need_cache):
+        """This layer and ``nxt`` (planned by MultiLayerNetwork._plan_fusions) in ONE launch: layer 2 runs step t
+        while this layer runs step t+1, and layer 2's input projection happens inside the recurrence. Returns this
+        layer's (out, (hT, cT), cache) and leaves layer 2's result pending for its activate; None when the stack
+        kernel does not apply (both layers then run on their own)."""
+        from ...ops import rnn_native
+        H = self.conf.nOut
+        W1, RW1, W2, RW2 = self.W("W"), self.W("RW"), nxt.W("W"), nxt.W("RW")
+        T = x.shape[2]
+        if not (_native_ok(x, W1, self.conf.activation, self.conf.gateActivationFn, H)
+                and rnn_native.stack2_supported(H, W1.dtype, T) and W2.dtype == W1.dtype
+                and tuple(W2.shape) == (H, 4 * H)):
+            return None
+        mb = x.shape[0]
+        xt = _time_major_rows(x, W1.dtype)
+        zx1 = matmul(xt, W1, bias=self.Wbias("b")).reshape(T, mb, 4 * H)
+        p1 = rnn_native.pack_rw(RW1, H, self.PEEPHOLE, need_bwd=need_cache)
+        p2 = rnn_native.pack_rw(RW2, H, nxt.PEEPHOLE, need_bwd=need_cache)
+        pw = rnn_native.pack_rw(W2, H, False, need_bwd=need_cache)
+        if p1 is None or p2 is None or pw is None:
+            return None
+        h02 = c02 = None
+        if stored_state:
+            h02, c02 = nxt.tBpttStateMap.get("prevAct"), nxt.tBpttStateMap.get("prevMem")
+        r = rnn_native.lstm2_seq_fwd(zx1, p1, p2, pw, nxt.Wbias("b").reshape(-1), H, (h0, h02), (c0, c02), mask,
+                                     need_cache)
+        if r is None:
+            return None
+        (o1, hT1, cT1, g1, ca1, s1), (o2, hT2, cT2, g2, ca2, s2) = r
+        out1, out2 = s1.permute(1, 2, 0), s2.permute(1, 2, 0)
+        c1 = c2 = None
+        if need_cache:
+            tag = object()                                 # pairs the two caches of one launch
+            c1 = {"native": True, "gates": g1, "call": ca1, "out": o1, "h0": h0, "c0": c0, "xt": xt, "packs": p1,
+                  "stack": tag}
+            c2 = {"native": True, "gates": g2, "call": ca2, "out": o2, "h0": h02, "c0": c02,
+                  "xt": s1.reshape(T * mb, H), "packs": p2, "w2pack": pw, "stack": tag}
+        nxt._stack_pending = (out1, (out2, (hT2, cT2), c2))
+        return out1, (hT1, cT1), c1
+
+    def _stack_backward(self, prev, eps, tbptt_back):
+        """Both layers' backward time loops in ONE launch (this layer's eps feeds the layer below inside the
+        kernel); this layer's weight gradients here, the layer below's gate deltas handed to its backprop."""
+        from ...ops import rnn_native
+        c2, c1 = self._cache, prev._cache
+        H = self.conf.nOut
+        mb, _, T = eps.shape
+        t_end = max(0, T - tbptt_back) if tbptt_back else 0
+        r = rnn_native.lstm2_seq_bwd(eps.permute(2, 0, 1), c1, c2, c1["packs"], c2["packs"], c2["w2pack"], H,
+                                     self.maskArray, t_end)
+        if r is None:
+            return None
+        dz1, dz2, st1, st2 = r
+        _native_weight_grads(dz2, c2, self.W("W"), H, self.PEEPHOLE, "", self.grads, False, *st2)
+        prev._stack_dz = (dz1, st1, c2["stack"])
+        # the layer below takes its gate deltas from _stack_dz: a zero-cost placeholder stands in for its epsilon
+        return self.make_gradient(), torch.zeros((), dtype=eps.dtype, device=eps.device).expand(mb, H, T)
 
     def rnnTimeStep(self, x, mask=None):
         self._check_state_mb(x)
@@ -316,6 +392,21 @@ class LSTMImpl(BaseRecurrentImpl):
             eps = eps.unsqueeze(2)
         H = self.conf.nOut
         need_dx = getattr(self, "need_input_grad", True)
+        sdz = getattr(self, "_stack_dz", None)
+        self._stack_dz = None
+        prev = getattr(self, "_stack_prev", None)
+        if sdz is not None and self._cache is not None and sdz[2] is self._cache.get("stack"):
+            # gate deltas from the stacked launch of the layer above (eps is its placeholder)
+            dx, _, _ = _native_weight_grads(sdz[0], self._cache, self.W("W"), H, self.PEEPHOLE, "", self.grads,
+                                            need_dx, *sdz[1])
+            if dx is None:
+                return self.make_gradient(), None
+            return self.make_gradient(), self.backpropDropOut(dx.to(eps.dtype))
+        if prev is not None and self._cache is not None and self._cache.get("stack") is not None and \
+                prev._cache is not None and prev._cache.get("stack") is self._cache["stack"]:
+            r = self._stack_backward(prev, eps, tbptt_back)
+            if r is not None:
+                return r
         dx, _, _ = _lstm_bwd(eps, self._cache, self.W("W"), self.W("RW"), H, self.PEEPHOLE, self.conf.activation,
                              self.conf.gateActivationFn, self.maskArray, tbptt_back, "", self.grads,
                              need_dx=need_dx)

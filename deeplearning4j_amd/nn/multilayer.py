@@ -58,6 +58,32 @@ class MultiLayerNetwork(BaseNetwork):
         for l in self.layers:
             l.need_input_grad = seen_params       # nothing trainable upstream => skip dL/dinput
             seen_params = seen_params or l.conf.numParams() > 0
+        self._plan_lstm_stacks()
+
+    def _plan_lstm_stacks(self):
+        """Consecutive LSTM / GravesLSTM layers of the same kind, with nothing between them (no preprocessor, input
+        dropout or weight noise), run as ONE pipelined two-layer launch (nn/layers/recurrent.py _stack_forward /
+        _stack_backward; the kernels decide at run time whether the shape fits)."""
+        from .conf.activations import ActivationSigmoid, ActivationTanH
+        from .layers.recurrent import LSTMImpl
+        for l in self.layers:
+            l._stack_next = l._stack_prev = None
+        i = 0
+        while i < len(self.layers) - 1:
+            a, b = self.layers[i], self.layers[i + 1]
+            ca, cb = a.conf, b.conf
+            ok = (type(a) is type(b) and isinstance(a, LSTMImpl) and type(ca) is type(cb)
+                  and ca.nOut == cb.nOut and cb.nIn == ca.nOut and (i + 1) not in self.conf.inputPreProcessors
+                  and getattr(cb, "idropout", None) is None and getattr(ca, "weightNoise", None) is None
+                  and getattr(cb, "weightNoise", None) is None
+                  and all(isinstance(c.activation, ActivationTanH) and isinstance(c.gateActivationFn,
+                                                                                  ActivationSigmoid)
+                          for c in (ca, cb)))
+            if ok:
+                a._stack_next, b._stack_prev = b, a
+                i += 2
+            else:
+                i += 1
 
     def getLayers(self):
         return self.layers

@@ -26,6 +26,9 @@ native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int
 native.register_sig("dl4j_conv_w_relayout_batched", [c_void_p, c_int, c_ll, c_void_p])
 native.register_sig("dl4j_conv_relayout_job_bytes", [])
 native.register_sig("dl4j_conv_relayout_per_block", [])
+native.register_sig("dl4j_conv_w_relayout_tiled", [c_void_p, c_int, c_ll, c_void_p])
+native.register_sig("dl4j_conv_relayout_tile_job_bytes", [])
+native.register_sig("dl4j_conv_relayout_tile_max_rs", [])
 native.register_sig("dl4j_conv_fwd", [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 + [c_void_p, c_void_p])
 native.register_sig("dl4j_conv_bwd_data_s1", [c_void_p, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
 native.register_sig("dl4j_conv_bwd_data_1x1", [c_void_p, c_void_p, c_void_p] + [c_int] * 9 + [c_void_p])
@@ -144,6 +147,9 @@ def _relayout(w, want_krsc, want_flip):
     e = _ent(w)
     v = WEIGHT_VERSION[0]
     K, C, R, S = w.shape
+    if R * S == 1 and w.is_contiguous():
+        e.krsc = w.view(K, 1, 1, C)                    # [K][C][1][1] is already [K][R][S][C]
+        want_krsc = False
     fresh = not is_managed(w.data_ptr())
     need_k = want_krsc and (fresh or e.vk != v)
     need_f = want_flip and (fresh or e.vf != v)
@@ -167,15 +173,21 @@ _plans = {}
 
 
 def relayout_all(weights, want_flip=True):
-    """Refresh the kernel-layout copies of every eligible conv weight in ONE launch (dl4j_conv_w_relayout_batched),
-    ahead of the forward pass; the per-conv lazy path then finds fresh copies. Returns the number of weights."""
+    """Refresh the kernel-layout copies of every eligible conv weight in ONE launch ahead of the forward pass; the
+    per-conv lazy path then finds fresh copies. Returns the number of weights.
+
+    The LDS-tiled kernel (dl4j_conv_w_relayout_tiled) serves every weight with at most 16 taps; a 1x1 weight's KRSC
+    layout is the weight itself (a view, never copied), only its transposed copy is refreshed."""
     ws = [w for w in weights if w.dtype in _KDT and w.is_cuda and w.dim() == 4 and w.is_contiguous()
           and w.shape[1] % 8 == 0 and w.shape[0] % 4 == 0]
     if not ws:
         return 0
+    lib = native.load()
+    if _TILED_RELAYOUT and all(w.shape[2] * w.shape[3] <= lib.dl4j_conv_relayout_tile_max_rs() and
+                               w.data_ptr() % 16 == 0 for w in ws):   # 16-byte tile loads
+        return _relayout_all_tiled(ws, want_flip, lib)
     key = (tuple((w.data_ptr(), tuple(w.shape)) for w in ws), bool(want_flip))
     plan = _plans.get(key)
-    lib = native.load()
     if plan is None:
         per_block = lib.dl4j_conv_relayout_per_block()
         assert lib.dl4j_conv_relayout_job_bytes() == 56
@@ -205,6 +217,50 @@ def relayout_all(weights, want_flip=True):
         return len(ws)                      # already fresh (e.g. several forward passes between updates)
     rc = lib.dl4j_conv_w_relayout_batched(_ptr(dev_jobs), njobs, nblk, _stream())
     native._check(rc, "conv_w_relayout_batched")
+    v = WEIGHT_VERSION[0]
+    plan[4] = v
+    for e, flip_ok in ents:
+        e.vk = v
+        if flip_ok:
+            e.vf = v
+    return len(ws)
+
+
+_TILED_RELAYOUT = os.environ.get("DL4J_AMD_RELAYOUT_TILED", "1") == "1"
+_RLT_K, _RLT_C = 64, 32
+
+
+def _relayout_all_tiled(ws, want_flip, lib):
+    key = ("tiled", tuple((w.data_ptr(), tuple(w.shape)) for w in ws), bool(want_flip))
+    plan = _plans.get(key)
+    if plan is None:
+        assert lib.dl4j_conv_relayout_tile_job_bytes() == 48
+        jt = np.dtype([("W", "<u8"), ("krsc", "<u8"), ("flip", "<u8"), ("K", "<i4"), ("C", "<i4"), ("RS", "<i4"),
+                       ("tiles_c", "<i4"), ("first", "<i8")])
+        rows, ents, nblk = [], [], 0
+        for w in ws:
+            K, C, R, S = w.shape
+            e = _ent(w)
+            if R * S == 1:
+                e.krsc = w.view(K, 1, 1, C)             # already the kernel layout
+            elif e.krsc is None:
+                e.krsc = torch.empty((K, R, S, C), dtype=w.dtype, device=w.device)
+            flip_ok = want_flip and K % 8 == 0
+            if flip_ok and e.flip is None:
+                e.flip = torch.empty((C, R, S, K), dtype=w.dtype, device=w.device)
+            tk, tc = (K + _RLT_K - 1) // _RLT_K, (C + _RLT_C - 1) // _RLT_C
+            rows.append((w.data_ptr(), 0 if R * S == 1 else e.krsc.data_ptr(), e.flip.data_ptr() if flip_ok else 0,
+                         K, C, R * S, tc, nblk))
+            nblk += tk * tc
+            ents.append((e, flip_ok))
+        arr = np.array(rows, dtype=jt)
+        dev_jobs = torch.from_numpy(arr.view(np.uint8).copy()).to(ws[0].device)
+        plan = [dev_jobs, len(rows), nblk, ents, -1]
+        _plans[key] = plan
+    dev_jobs, njobs, nblk, ents, done_v = plan
+    if done_v == WEIGHT_VERSION[0]:
+        return len(ws)
+    native._check(lib.dl4j_conv_w_relayout_tiled(_ptr(dev_jobs), njobs, nblk, _stream()), "conv_w_relayout_tiled")
     v = WEIGHT_VERSION[0]
     plan[4] = v
     for e, flip_ok in ents:

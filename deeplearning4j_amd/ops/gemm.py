@@ -50,6 +50,11 @@ def _lib():
 
 _TUNED = {}                                            # problem key -> (cfg, splits), filled by _autotune
 _TUNE = os.environ.get("DL4J_AMD_GEMM_TUNE", "1") == "1"
+# Plain products (no activation epilogue, no pre-activation / BN-statistics outputs, output in the operand dtype) also
+# time hipBLASLt (torch.mm / addmm / bmm on the same stream) as one more autotuner candidate: the fused-epilogue
+# GEMMs stay on the in-tree kernels, a library GEMM is used only where it measured faster.
+_LIB = os.environ.get("DL4J_AMD_GEMM_LIB", "1") == "1"
+LIB_CFG = (-2, 1)
 
 
 def _plan(lib, M, N, K, batch):
@@ -81,14 +86,14 @@ def _candidates(M, N, K, batch, default):
     return out
 
 
-def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True):
-    """First eager call of a problem shape: time every kernel configuration (tile shape x split-K) on a scratch
-    destination and keep the fastest (hipBLASLt-style heuristics replaced by measurement). Never runs while a HIP
-    graph is being captured; the cost-model plan is used there."""
+def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False):
+    """First eager call of a problem shape: time every kernel configuration (tile shape x split-K; plus the library
+    GEMM when ``lib``) on a scratch destination and keep the fastest. Never runs while a HIP graph is being captured;
+    the cost-model plan is used there."""
     from .timing import gpu_time
     tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
     best, best_t = default, None
-    for cand in _candidates(M, N, K, batch, default):
+    for cand in _candidates(M, N, K, batch, default) + ([LIB_CFG] if lib else []):
         if cand[1] > 1 and not splits_ok:
             continue
         if launch(cand[0], cand[1], tmp, 0.0, None) != 0:
@@ -249,7 +254,12 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     if K == 0:
         out.zero_() if beta == 0.0 else out.mul_(beta)
         return out
+    bias_in = None
     if bias is not None:
+        # the operand-dtype copy of the bias (a library GEMM's epilogue needs it): the bias itself, or the 16-bit
+        # shadow the network / SameDiff attached to an fp32 master parameter
+        bias_in = bias if bias.dtype == a.dtype else getattr(bias, "_dl4j_shadow", None)
+        bias_in = None if bias_in is None else bias_in.reshape(-1)
         bias = bias.reshape(-1)
         if bias.dtype != torch.float32 or not bias.is_contiguous():
             bias = bias.to(torch.float32).contiguous()
@@ -328,6 +338,14 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
             if c_t is not out:
                 out.copy_(c_t)
             return out
+        libmm = None if (bias is not None and bias_in is None) else \
+            _lib_gemm(a, b, c_t, swap, batched, bias_in, bias_dim, act, alpha, beta, z, out_dtype)
+        if libmm is not None:
+            key = key + ("lib", bias_in is not None, beta != 0.0)
+            kern = launch
+
+            def launch(cfg, sp, dst, bt, zz, ts=None):
+                return libmm(dst, bt) if cfg == LIB_CFG[0] else kern(cfg, sp, dst, bt, zz, ts)
         if _FORCE_CFG is not None:
             cfg = _FORCE_CFG
         else:
@@ -335,7 +353,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
             if cfg is None:
                 cfg = _plan(lib, Mx, Nx, K, batch)
                 if _TUNE and not torch.cuda.is_current_stream_capturing():
-                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg)
+                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None)
                     _TUNED[key] = cfg
         rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
     if rc == -1:
@@ -354,6 +372,32 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
     if c_t is not out:
         out.copy_(c_t)
     return out
+
+
+def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out_dtype):
+    """A launcher ``(dst, beta) -> 0`` running the product as one hipBLASLt call through torch on the current stream,
+    or None when the problem needs an in-tree epilogue (activation, pre-activation, fp32 output from 16-bit operands,
+    a row bias, alpha != 1) or its destination is not a dense matrix."""
+    if not _LIB or act not in (None, "identity") or z is not None or alpha != 1.0 or out_dtype != a.dtype or \
+            a.dtype not in (torch.bfloat16, torch.float16) or b.dtype != a.dtype:
+        return None
+    if bias is not None and (bias.dtype != a.dtype or bias_dim != 1 or swap or batched or beta != 0.0):
+        return None
+    dstv = (lambda d: d.mT) if swap else (lambda d: d)                 # noqa: E731
+    if not dstv(c_t).is_contiguous():
+        return None
+    A_, B_ = (b.mT, a.mT) if swap else (a, b)
+
+    def run(dst, bt):
+        d = dstv(dst)
+        if bias is not None:
+            torch.addmm(bias, A_, B_, out=d)
+        elif bt == 0.0:
+            (torch.bmm if batched else torch.mm)(A_, B_, out=d)
+        else:
+            (d.baddbmm_ if batched else d.addmm_)(A_, B_, beta=bt)
+        return 0
+    return run
 
 
 def linear(x, W, b=None, act=None, z=None, out_dtype=None):

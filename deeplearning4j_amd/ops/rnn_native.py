@@ -388,3 +388,133 @@ def lstm_bwd_prep(dz, out, h0, call, c0, peephole, dtype):
                                 _ptr(dpeep), R, mb, H, int(bool(peephole)), _stream())
     _check(rc, "lstm_bwd_prep")
     return dzb, hpb, db, dpeep
+
+
+# ---- pipelined two-layer stack (csrc/lstm_coop.hip lstm_fwd_stack2 / lstm_bwd_stack2)
+_P = ctypes.c_void_p
+STACK_LAUNCHES = [0, 0]        # successful stacked forward / backward launches (tests, profiling)
+
+
+class _Stack2Fwd(ctypes.Structure):
+    _fields_ = [(n, _P) for n in ("zx1", "rw1", "rw2", "w2", "b2", "peep1", "peep2", "h0_1", "c0_1", "h0_2", "c0_2",
+                                  "mask", "out1", "o16_1", "gates1", "call1", "hT1", "cT1", "out2", "o16_2",
+                                  "gates2", "call2", "hT2", "cT2", "exch", "err")] + \
+        [("Tn", c_int), ("mb", c_int), ("timeout", ctypes.c_longlong), ("tag_arg", ctypes.c_uint),
+         ("exch_words", ctypes.c_longlong)]
+
+
+class _Stack2Bwd(ctypes.Structure):
+    _fields_ = [("eps2", _P), ("eps_dt", c_int), ("pad_", c_int)] + \
+        [(n, _P) for n in ("gates1", "call1", "c0_1", "gates2", "call2", "c0_2", "rw1", "rw2", "w2", "peep1",
+                           "peep2", "mask", "dhl1", "dcl1", "dhl2", "dcl2", "dz1", "dz2", "dh0_1", "dc0_1",
+                           "dh0_2", "dc0_2", "exch", "err")] + \
+        [("Tn", c_int), ("mb", c_int), ("t_end", c_int), ("timeout", ctypes.c_longlong), ("tag_arg", ctypes.c_uint),
+         ("exch_words", ctypes.c_longlong)]
+
+
+def _stack_enabled():
+    import os
+    return os.environ.get("DL4J_AMD_LSTM_STACK", "1") == "1" and _coop_enabled()
+
+
+def stack2_supported(H, dtype, T):
+    if not _stack_enabled() or dtype != torch.bfloat16 or H != 256:
+        return False
+    lib = native.load()
+    native.register_sig("dl4j_lstm_stack2_max_t", [])
+    return 1 <= T <= lib.dl4j_lstm_stack2_max_t()
+
+
+def _p(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def lstm2_seq_fwd(zx1, packs1, packs2, w2pack, b2, H, h0s, c0s, mask, need_cache=True):
+    """Both layers of a two-layer LSTM stack in ONE pipelined launch. zx1: [T, mb, 4H] bf16 (= x·W1 + b1); packs1 /
+    packs2: RWPacks of RW1 / RW2; w2pack: RWPacks-style packing of W2 ([H, 4H]); b2: [4H] fp32. Returns
+    ([out, hT, cT, gates, call, out16] for layer 1, [...] for layer 2) or None when the stack kernel does not apply."""
+    T, mb, H4 = zx1.shape
+    if not stack2_supported(H, zx1.dtype, T) or H4 != 4 * H:
+        return None
+    lib = native.load()
+    native.register_sig("dl4j_lstm_fwd_stack2", [c_void_p, c_int, c_int, c_void_p])
+    native.register_sig("dl4j_lstm_stack2_exch_bytes", [c_int, c_int, c_int, c_int])
+    native.register_sig("dl4j_lstm_stack2_struct_bytes", [c_int])
+    lib.dl4j_lstm_stack2_exch_bytes.restype = ctypes.c_longlong
+    assert lib.dl4j_lstm_stack2_struct_bytes(0) == ctypes.sizeof(_Stack2Fwd)
+    dev = zx1.device
+    m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
+    if m is not None and m.shape[1] != T:
+        return None
+    outs = []
+    for _ in range(2):
+        outs.append([arena.empty((T, mb, H), torch.float32, dev), torch.empty(mb, H, device=dev, dtype=torch.float32),
+                     torch.empty(mb, H, device=dev, dtype=torch.float32),
+                     arena.empty((T, mb, 4 * H), torch.float32, dev) if need_cache else None,
+                     arena.empty((T, mb, H), torch.float32, dev) if need_cache else None,
+                     arena.empty((T, mb, H), zx1.dtype, dev)])
+    nbytes = lib.dl4j_lstm_stack2_exch_bytes(mb, H, T, 0)
+    b, base, reset = _coop_buf("stack_fwd", nbytes, dev, T)
+    _launch_mode(lib)
+    h = [_f32c(x) for x in h0s]
+    c = [_f32c(x) for x in c0s]
+    b2c = b2.detach().to(torch.float32).contiguous()
+    zx1 = zx1.contiguous()
+    a = _Stack2Fwd(zx1=_p(zx1), rw1=_p(packs1.fwd), rw2=_p(packs2.fwd), w2=_p(w2pack.fwd), b2=_p(b2c),
+                   peep1=_p(packs1.peep), peep2=_p(packs2.peep), h0_1=_p(h[0]), c0_1=_p(c[0]), h0_2=_p(h[1]),
+                   c0_2=_p(c[1]), mask=_p(m), out1=_p(outs[0][0]), o16_1=_p(outs[0][5]), gates1=_p(outs[0][3]),
+                   call1=_p(outs[0][4]), hT1=_p(outs[0][1]), cT1=_p(outs[0][2]), out2=_p(outs[1][0]),
+                   o16_2=_p(outs[1][5]), gates2=_p(outs[1][3]), call2=_p(outs[1][4]), hT2=_p(outs[1][1]),
+                   cT2=_p(outs[1][2]), exch=_p(b.exch), err=_p(b.err), Tn=T, mb=mb, timeout=0, tag_arg=base,
+                   exch_words=0)
+    rc = lib.dl4j_lstm_fwd_stack2(ctypes.byref(a), H, reset, c_void_p(_stream()))
+    if rc != 0:
+        b.next_tag = None
+        return None
+    _post_launch(b)
+    STACK_LAUNCHES[0] += 1
+    return outs[0], outs[1]
+
+
+def lstm2_seq_bwd(eps2_tmh, cache1, cache2, packs1, packs2, w2pack, H, mask=None, t_end=0, dh_last=(None, None),
+                  dc_last=(None, None)):
+    """Backward of a two-layer stack in ONE pipelined launch (layer 1's eps is formed inside from layer 2's gate
+    deltas). eps2_tmh: [T, mb, H] gradient of layer 2's output. Returns (dz1, dz2 [T, mb, 4H] fp32, (dh0, dc0) of
+    layer 1, (dh0, dc0) of layer 2) or None."""
+    T, mb, _ = eps2_tmh.shape
+    if not stack2_supported(H, packs1.dtype, T) or t_end >= T:
+        return None
+    lib = native.load()
+    native.register_sig("dl4j_lstm_bwd_stack2", [c_void_p, c_int, c_int, c_void_p])
+    native.register_sig("dl4j_lstm_stack2_exch_bytes", [c_int, c_int, c_int, c_int])
+    native.register_sig("dl4j_lstm_stack2_struct_bytes", [c_int])
+    lib.dl4j_lstm_stack2_exch_bytes.restype = ctypes.c_longlong
+    assert lib.dl4j_lstm_stack2_struct_bytes(1) == ctypes.sizeof(_Stack2Bwd)
+    dev = eps2_tmh.device
+    e, edt = _eps_arg(eps2_tmh)
+    m = _f32c(mask.reshape(mb, -1)) if mask is not None else None
+    dz = [arena.empty((T, mb, 4 * H), torch.float32, dev) for _ in range(2)]
+    if t_end > 0:
+        for d in dz:
+            d.zero_()
+    st = [(torch.empty(mb, H, device=dev, dtype=torch.float32), torch.empty(mb, H, device=dev, dtype=torch.float32))
+          for _ in range(2)]
+    nbytes = lib.dl4j_lstm_stack2_exch_bytes(mb, H, T, 1)
+    b, base, reset = _coop_buf("stack_bwd", nbytes, dev, T)
+    _launch_mode(lib)
+    c01, c02 = _f32c(cache1["c0"]), _f32c(cache2["c0"])
+    dl = [_f32c(x) for x in dh_last]
+    cl = [_f32c(x) for x in dc_last]
+    a = _Stack2Bwd(eps2=_p(e), eps_dt=edt, pad_=0, gates1=_p(cache1["gates"]), call1=_p(cache1["call"]), c0_1=_p(c01),
+                   gates2=_p(cache2["gates"]), call2=_p(cache2["call"]), c0_2=_p(c02), rw1=_p(packs1.bwd),
+                   rw2=_p(packs2.bwd), w2=_p(w2pack.bwd), peep1=_p(packs1.peep), peep2=_p(packs2.peep), mask=_p(m),
+                   dhl1=_p(dl[0]), dcl1=_p(cl[0]), dhl2=_p(dl[1]), dcl2=_p(cl[1]), dz1=_p(dz[0]), dz2=_p(dz[1]),
+                   dh0_1=_p(st[0][0]), dc0_1=_p(st[0][1]), dh0_2=_p(st[1][0]), dc0_2=_p(st[1][1]), exch=_p(b.exch),
+                   err=_p(b.err), Tn=T, mb=mb, t_end=int(t_end), timeout=0, tag_arg=base, exch_words=0)
+    rc = lib.dl4j_lstm_bwd_stack2(ctypes.byref(a), H, reset, c_void_p(_stream()))
+    if rc != 0:
+        b.next_tag = None
+        return None
+    _post_launch(b)
+    STACK_LAUNCHES[1] += 1
+    return dz[0], dz[1], st[0], st[1]

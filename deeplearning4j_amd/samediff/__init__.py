@@ -12,6 +12,7 @@ kernels in both directions (GEMM, conv, pooling, LayerNorm, flash attention, LST
 """
 import io
 import json
+import os
 import zipfile
 
 import torch
@@ -435,18 +436,31 @@ class SameDiff:
             self.variables[out].value = y
             self._ctx[out] = ctx
 
-    def _backward(self, seeds, wrt, targets=None, on_final=None):
+    def _backward(self, seeds, wrt, targets=None, on_final=None, sinks=None):
         """Reverse pass from ``seeds`` {variable name: upstream gradient} over the recorded ops; returns
         {name: gradient} for ``wrt`` (every op's explicit backward; no torch.autograd).
 
         ``on_final(name, grad)``: called for each ``wrt`` variable as soon as its gradient is complete, i.e. right
         after the reverse pass has processed the EARLIEST recorded op that reads it (later ops were processed
         first). Data-parallel training uses it to start each gradient bucket's all-reduce while the rest of the
-        reverse pass still runs."""
+        reverse pass still runs.
+
+        ``sinks`` {name: contiguous fp32 tensor}: destinations (views of the flat gradient buffer) for variables read
+        by exactly ONE recorded op; that op's backward writes the gradient there directly (autodiff.grad_sink)
+        instead of into a temporary the training step would then copy."""
         grads = dict(seeds)
         tg = targets if targets is not None else list(seeds)
         # the planned (fused) records only when their contexts come from a planned execution of these targets
         recs = self._plan(tg) if self._executed == tuple(tg) else self._needed(tg)
+        if sinks:
+            reads = {}
+            for _, _, refs, _ in recs:
+                for r in refs:
+                    if isinstance(r, str) and r in sinks:
+                        reads[r] = reads.get(r, 0) + 1
+            sinks = {n: t for n, t in sinks.items() if reads.get(n) == 1 and n not in grads}
+        from . import autodiff as _ad
+        dsum_for, presunk = (self._ln_bias_fusions(recs, sinks) if sinks else {}), {}
         final_at = {}
         if on_final is not None:
             want = set(wrt)
@@ -465,7 +479,15 @@ class SameDiff:
             g = grads.get(out)
             if g is not None:
                 ins = [self._val(r) for r in refs]
-                gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
+                sk = {j: sinks[r] for j, r in enumerate(refs) if isinstance(r, str) and r in sinks} if sinks else None
+                fz = dsum_for.get(i)
+                _ad.set_sinks(sk, done=presunk.get(i), dsum=None if fz is None else sinks[fz[1]])
+                try:
+                    gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
+                    if fz is not None and _ad.dsum_written():
+                        presunk[fz[0]] = {2}        # the producing linear's bias gradient is already in its sink
+                finally:
+                    _ad.set_sinks(None)
                 for r, gi in zip(refs, gins):
                     if gi is None or not isinstance(r, str):
                         continue
@@ -476,6 +498,34 @@ class SameDiff:
                     on_final(name, grads.get(name))
         self._last_grads = {k: grads.get(k) for k in wrt}
         return self._last_grads
+
+    @staticmethod
+    def _ln_bias_fusions(recs, sinks):
+        """{LayerNorm record index: (producing linear record index, bias variable)} for LayerNorms whose normalized
+        input (x or the fused residual) is the output of a bias-carrying, activation-free linear op read by nothing
+        else: LayerNorm's backward kernel emits the column sums of its input gradient, which ARE that bias gradient
+        (the CG's dense -> LayerNorm fusion, csrc/layernorm.hip dsum), so the linear skips its channel-sum pass."""
+        prod = {o: j for j, (o, _, _, _) in enumerate(recs)}
+        reads = {}
+        for _, _, refs, _ in recs:
+            for r in refs:
+                if isinstance(r, str):
+                    reads[r] = reads.get(r, 0) + 1
+        out = {}
+        for j, (_, op, refs, _) in enumerate(recs):
+            if op != "layerNorm":
+                continue
+            for pos in (0, 3):
+                y = refs[pos] if pos < len(refs) else None
+                pj = prod.get(y) if isinstance(y, str) else None
+                if pj is None or reads.get(y) != 1:
+                    continue
+                _, pop, prefs, pat = recs[pj]
+                if pop == "linear" and not pat.get("act") and len(prefs) > 2 and isinstance(prefs[2], str) and \
+                        prefs[2] in sinks:
+                    out[j] = (pj, prefs[2])
+                    break
+        return out
 
     def output(self, placeholders, *outputs):
         """Execute the recorded graph for new placeholder values; returns {name: value}."""
@@ -529,6 +579,10 @@ class SameDiff:
             if mixed:
                 shadow[off:off + k].copy_(v.value.detach().reshape(-1))
                 v.value = shadow[off:off + k].view(v.value.shape)
+                # the fp32 master next to its 16-bit shadow: ops that consume parameters in fp32 (GEMM bias, LayerNorm
+                # gamma / beta) read it instead of converting the shadow every step (autodiff.master)
+                v.value._dl4j_master = flat[off:off + k].view(v.value.shape)
+                v.value._dl4j_master._dl4j_shadow = v.value
             else:
                 v.value = flat[off:off + k].view(v.value.shape)
             segs.append(Segment(off, k, 0, off, n, cfg.updater, cfg.l1, cfg.l2, 0))   # one block: state offset 0
@@ -565,15 +619,15 @@ class SameDiff:
                               zip(cfg.dataSetLabelMapping, labs)})
                 with torch.no_grad():
                     if self._graph_ready(feeds):
-                        loss = self._graph_replay(feeds)
+                        last = self._graph_replay(feeds)
                     else:
-                        loss_t = self._train_body(feeds, sign)
-                        loss = float(loss_t)
+                        last = self._train_body(feeds, sign)
                         self._eager_steps += 1
+                # the loss stays on the device: iterations of one fit call run back to back, without a host sync
+                # between them (the A/B graph slots keep the last replay's loss valid until the call returns)
                 self.iterationCount += 1
-                last = loss
             self.epochCount += 1
-        return last
+        return None if last is None else float(last)
 
     def _train_body(self, feeds, sign):
         """One training iteration's device work: forward, reverse pass, gradient copy into the flat buffer,
@@ -593,19 +647,22 @@ class SameDiff:
             # data parallel: each variable's gradient goes into the flat buffer as soon as it is final, and a bucket's
             # all-reduce starts once all of its variables are, overlapping the rest of the reverse pass
             dp.begin()
-            self._backward(seeds, [v.name for v in vs], list(self._loss_names), on_final=dp.final)
+            self._backward(seeds, [v.name for v in vs], list(self._loss_names), on_final=dp.final,
+                           sinks=self._grad_sinks(st, vs))
             dp.finish()
         else:
-            grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names))
+            grads = self._backward(seeds, [v.name for v in vs], list(self._loss_names),
+                                   sinks=self._grad_sinks(st, vs))
             dst, src = [], []
             for v, view in zip(vs, st["views"]):
                 g = grads.get(v.name)
                 if g is None:
                     view.zero_()
-                else:
+                elif g.data_ptr() != view.data_ptr():        # gradient sinks were written in place
                     dst.append(view)
                     src.append(g.reshape(view.shape))
-            torch._foreach_copy_(dst, src)          # one multi-tensor launch for all gradients
+            if dst:
+                torch._foreach_copy_(dst, src)      # one multi-tensor launch for the remaining gradients
         fused_update(st["plan"], st["flat"], st["grad"], st["state"], self.iterationCount, self.epochCount, 1,
                      mini_batch=False, shadow=st["shadow"])
         out = None
@@ -613,6 +670,13 @@ class SameDiff:
             v = self.variables[n].value.float().reshape(())
             out = v if out is None else out + v
         return out
+
+    @staticmethod
+    def _grad_sinks(st, vs):
+        """{variable name: its fp32 flat-gradient view} (fp64 training keeps the copies: the GEMM writes fp32)."""
+        if st["grad"].dtype != torch.float32 or os.environ.get("DL4J_AMD_SD_SINKS", "1") == "0":
+            return None
+        return {v.name: view for v, view in zip(vs, st["views"])}
 
     # ------------------------------------------------------------------ HIP graphs
     def enableHipGraphs(self, enabled=True, warmup=2):
@@ -691,7 +755,7 @@ class SameDiff:
         g["graphs"][slot].replay()
         native.mark_graph_replayed(st["plan"], slot)
         g["k"] += 1
-        return float(g["loss"][slot])
+        return g["loss"][slot]
 
     def _dp_buckets(self, st):
         """The data-parallel bucket plan (one process per GPU, torch.distributed over RCCL / gloo), or None when
@@ -894,7 +958,7 @@ class _SDGradBuckets:
         view = self.view[name]
         if grad is None:
             view.zero_()
-        else:
+        elif grad.data_ptr() != view.data_ptr():          # not already written in place (gradient sink)
             view.copy_(grad.reshape(view.shape))
         self.left[b] -= 1
         if self.left[b] == 0:

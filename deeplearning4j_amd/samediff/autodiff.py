@@ -11,6 +11,7 @@ directions: ``mmul``/``linear`` -> in-tree MFMA GEMM (ops/gemm.py), ``conv2d`` -
 tensors (and fp64 gradient checks) the same ops run their torch reference math.
 """
 import math
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -18,6 +19,43 @@ import torch.nn.functional as F
 from .. import ops
 
 REGISTRY = {}
+_TLS = threading.local()
+
+
+def set_sinks(sinks, done=None, dsum=None):
+    """Gradient destinations of the op whose backward runs next: {input position: contiguous fp32 tensor shaped like
+    that input} (SameDiff._backward sets them for variables only this op reads). ``done``: input positions whose
+    sink an earlier backward already filled; ``dsum``: an fp32 sink for the column sums of this LayerNorm's input
+    gradient (the producing linear's bias gradient)."""
+    _TLS.sinks = sinks
+    _TLS.done = done
+    _TLS.dsum = dsum
+    _TLS.dsum_written = False
+
+
+def sink_done(i):
+    d = getattr(_TLS, "done", None)
+    return bool(d) and i in d
+
+
+def dsum_written():
+    return getattr(_TLS, "dsum_written", False)
+
+
+def grad_sink(i):
+    """The destination input ``i``'s gradient should be written to, or None (write a fresh tensor). A backward that
+    uses it returns that same tensor as the gradient."""
+    s = getattr(_TLS, "sinks", None)
+    return None if not s else s.get(i)
+
+
+def master(t):
+    """The fp32 master copy of a mixed-precision trainable variable (SameDiff training keeps it in the flat parameter
+    buffer, the 16-bit value is its shadow), else ``t`` itself."""
+    if t is None:
+        return None
+    m = getattr(t, "_dl4j_master", None)
+    return t if m is None else m
 
 
 class OpDef:
@@ -170,14 +208,15 @@ def _param_acc(w):
     return torch.float64 if w.dtype == torch.float64 else torch.float32
 
 
-def _colsum(g2):
-    """fp32 column sums of a [M, N] gradient (channel-sum HIP kernel on the GPU)."""
+def _colsum(g2, out=None):
+    """fp32 column sums of a [M, N] gradient (channel-sum HIP kernel on the GPU); ``out``: optional fp32 sink."""
     if g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float32) and g2.shape[1] % 8 == 0:
         from ..ops import native
-        r = native.channel_sum(g2.contiguous())
+        r = native.channel_sum(g2.contiguous(), out=None if out is None else out.view(-1))
         if r is not None:
             return r
-    return g2.to(_param_acc(g2)).sum(0)
+    r = g2.to(_param_acc(g2)).sum(0)
+    return r if out is None else out.view(-1).copy_(r)
 
 
 def _linear_fwd(ins, at):
@@ -185,7 +224,7 @@ def _linear_fwd(ins, at):
     activation in the GEMM epilogue and keeps the pre-activation for the backward."""
     x, w, b = ins
     from ..ops.gemm import mmul
-    bias = None if b is None else b.reshape(-1)
+    bias = None if b is None else master(b).reshape(-1)
     act = at.get("act")
     if act is None:
         return mmul(x, w, bias=bias), None
@@ -204,8 +243,18 @@ def _linear_bwd(ctx, g, ins, at):
     g2 = g.to(x.dtype).reshape(-1, g.shape[-1])
     x2 = x.reshape(-1, x.shape[-1])
     dx = _mm(g2, w.t()).reshape(x.shape)
-    dw = _mm(x2.t(), g2, out_dtype=None if w.dtype == torch.float64 else torch.float32)
-    db = None if b is None else _colsum(g2).reshape(b.shape)
+    sw, sb = grad_sink(1), grad_sink(2)
+    if sw is not None and x.is_cuda and w.dim() == 2:
+        from ..ops.gemm import mmul
+        dw = mmul(x2.t(), g2, out=sw)                  # straight into the flat gradient (fp32 epilogue)
+    else:
+        dw = _mm(x2.t(), g2, out_dtype=None if w.dtype == torch.float64 else torch.float32)
+    if b is None:
+        db = None
+    elif sb is not None and sink_done(2):
+        db = sb.reshape(b.shape)                      # written by the consuming LayerNorm's backward (dsum)
+    else:
+        db = _colsum(g2, sb).reshape(b.shape)
     return [dx, dw, db]
 
 
@@ -292,7 +341,8 @@ def _gather_fwd(ins, at):
 
 def _gather_bwd(ctx, g, ins, at):
     p, i = ins
-    dp = torch.zeros(p.shape, dtype=_param_acc(p), device=p.device)
+    sp = grad_sink(0)
+    dp = sp.zero_() if sp is not None else torch.zeros(p.shape, dtype=_param_acc(p), device=p.device)
     ax = at.get("axis", 0)
     if ax == 0:
         from ..ops.nn_misc import embedding_backward_
@@ -313,6 +363,7 @@ def _ln_fwd(ins, at):
     """LayerNorm over the last dim of x (+ residual: the 4th input, set by SameDiff's fusion pass for
     add -> layerNorm, summed inside the LayerNorm kernel)."""
     x, gamma, beta = ins[:3]
+    gamma, beta = master(gamma), master(beta)
     res = ins[3] if len(ins) > 3 else None
     eps = at.get("eps", 1e-5)
     N = x.shape[-1]
@@ -342,7 +393,11 @@ def _ln_bwd(ctx, g, ins, at):
     if ctx[0] == "native":
         from ..ops import transformer_native as TN
         _, x2, r2, mean, rstd = ctx
-        dx, dg, db = TN.ln_bwd(g2.to(x.dtype), x2, gamma.reshape(-1), mean, rstd, r2)
+        dsum = getattr(_TLS, "dsum", None)
+        dx, dg, db = TN.ln_bwd(g2.to(x.dtype), x2, master(gamma).reshape(-1), mean, rstd, r2,
+                               dgamma_out=grad_sink(1), dbeta_out=grad_sink(2), dsum_out=dsum)
+        if dsum is not None:
+            _TLS.dsum_written = True
         dx = dx.reshape(x.shape)
         out = [dx, dg.reshape(gamma.shape), db.reshape(beta.shape)]
         return out + ([dx.to(res.dtype)] if res is not None else [])

@@ -100,12 +100,17 @@ def test_conv_kernel_variants_agree(cuda, case):
     _close(outs[1][3], outs[0][3], 1e-5)
 
 
-def test_batched_relayout_matches_per_weight():
-    """dl4j_conv_w_relayout_batched (one launch for all weights) == the per-weight relayout kernel."""
+@pytest.mark.parametrize("tiled", [True, False])
+def test_batched_relayout_matches_per_weight(tiled):
+    """One launch refreshes every weight's kernel layouts: the LDS-tiled kernel (<= 16 taps; edge tiles in K and C,
+    K % 8 != 0 without a flipped copy, 1x1 KRSC as a view) and the element-gather kernel (a 7x7 weight in the set)
+    both equal the permuted / rotated weight exactly."""
     from deeplearning4j_amd.ops import conv_native as cn
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(0)
-    shapes = [(64, 64, 3, 3), (256, 64, 1, 1), (128, 256, 1, 1), (64, 8, 7, 7), (12, 16, 3, 3)]
+    shapes = [(64, 64, 3, 3), (256, 64, 1, 1), (128, 256, 1, 1), (12, 16, 3, 3), (200, 40, 3, 3), (72, 24, 1, 3)]
+    if not tiled:
+        shapes.append((64, 8, 7, 7))
     ws = [torch.randn(s, generator=g).to(torch.bfloat16).to(dev) for s in shapes]
     cn.bump_version()
     assert cn.relayout_all(ws) == len(ws)

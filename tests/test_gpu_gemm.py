@@ -240,3 +240,38 @@ def test_zero_padded_k_operand(K):
     g = torch.randn(M, N, device=DEV).to(torch.bfloat16)
     out2 = gemm.mmul(a.t(), g, out_dtype=torch.float32)
     _check(out2, _ref(a.t(), g), torch.bfloat16, M, f"kz^T K={K}")
+
+
+@pytest.mark.parametrize("case", ["plain", "bias_shadow", "beta", "colmajor", "batched"])
+def test_library_candidate(case, monkeypatch):
+    """The hipBLASLt candidate of the autotuner (forced here) computes the same product for every plain-GEMM form it
+    accepts: bias through the 16-bit shadow attached to an fp32 master, beta-accumulate, column-major destinations
+    (operands swapped) and 3-D batches; epilogue GEMMs (activation / fp32 output) never take it."""
+    torch.manual_seed(4)
+    M, N, K = 384, 320, 256
+    monkeypatch.setattr(gemm, "_FORCE_CFG", gemm.LIB_CFG)
+    a = _mk((M, K), torch.bfloat16)
+    b = _mk((K, N), torch.bfloat16, contig_last=False)
+    if case == "plain":
+        _check(gemm.mmul(a, b), _ref(a, b), torch.bfloat16, K, case)
+    elif case == "bias_shadow":
+        master = torch.randn(N, device=DEV)
+        master._dl4j_shadow = master.to(torch.bfloat16)
+        _check(gemm.mmul(a, b, bias=master), _ref(a, b, bias=master._dl4j_shadow), torch.bfloat16, K, case)
+    elif case == "beta":
+        c0 = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        out = c0.clone()
+        _check(gemm.mmul(a, b, out=out, beta=1.0), _ref(a, b, beta=1.0, c0=c0), torch.bfloat16, K, case)
+    elif case == "colmajor":
+        out = torch.empty(N, M, device=DEV, dtype=torch.bfloat16).t()
+        _check(gemm.mmul(a, b, out=out), _ref(a, b), torch.bfloat16, K, case)
+    else:
+        a3 = torch.randn(3, M, K, device=DEV).to(torch.bfloat16)
+        b3 = torch.randn(3, K, N, device=DEV).to(torch.bfloat16)
+        out = gemm.mmul(a3, b3)
+        ref = torch.stack([a3[i].float() @ b3[i].float() for i in range(3)])
+        assert (out.float() - ref).abs().max() <= _tol(torch.bfloat16, K) * ref.abs().max()
+    assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV, dtype=torch.bfloat16), False, False, None, 1, "gelu",
+                          1.0, 0.0, None, torch.bfloat16) is None
+    assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV), False, False, None, 1, None, 1.0, 0.0, None,
+                          torch.float32) is None

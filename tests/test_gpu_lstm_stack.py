@@ -1,0 +1,83 @@
+"""Pipelined two-layer LSTM stack (csrc/lstm_coop.hip lstm_fwd_stack2 / lstm_bwd_stack2): both layers of a
+GravesLSTM -> GravesLSTM stack in ONE launch per direction must give the same outputs, gradients and TBPTT training
+as the two single-layer launches (whose numerics tests/test_gpu_lstm.py pins to the fp64 reference). Layer 2's input
+projection runs inside the recurrence with fp32 accumulation instead of a bf16-rounded GEMM output, so the
+comparison is within bf16 tolerance, not bitwise."""
+import pytest
+import torch
+
+from deeplearning4j_amd import *  # noqa: F401,F403
+from deeplearning4j_amd.nn.conf import DataType
+from deeplearning4j_amd.ops import fallback, rnn_native
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def _net(cuda, peep=True, tbptt=None, seed=5, H=256, nIn=24, nOut=10):
+    L = GravesLSTM if peep else LSTM
+    lb = (NeuralNetConfiguration.Builder().seed(seed).updater(Adam(2e-3)).dataType(DataType.BFLOAT16).list()
+          .layer(L.Builder().nIn(nIn).nOut(H).activation(Activation.TANH).build())
+          .layer(L.Builder().nIn(H).nOut(H).activation(Activation.TANH).build())
+          .layer(RnnOutputLayer.Builder(LossFunction.MCXENT).nIn(H).nOut(nOut).activation(Activation.SOFTMAX).build()))
+    if tbptt:
+        lb.backpropType(BackpropType.TruncatedBPTT).tBPTTLength(tbptt)
+    net = MultiLayerNetwork(lb.build())
+    net.init(device=cuda)
+    return net
+
+
+def _data(cuda, mb=37, nIn=24, nOut=10, T=20, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(mb, nIn, T, generator=g).to(cuda)
+    y = torch.zeros(mb, nOut, T)
+    y[torch.arange(mb), torch.randint(0, nOut, (mb,), generator=g)] = 1
+    return x, y.to(cuda)
+
+
+@pytest.mark.parametrize("peep", [True, False])
+def test_stack_gradients_match_separate_layers(cuda, monkeypatch, peep):
+    x, y = _data(cuda)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_LSTM_STACK", flag)
+        net = _net(cuda, peep)
+        assert net.layers[0]._stack_next is net.layers[1]
+        before = list(rnn_native.STACK_LAUNCHES)
+        fallback.reset()
+        net.computeGradientAndScore(x, y)
+        torch.cuda.synchronize()
+        assert fallback.count() == 0, fallback.summary()
+        ran = [a - b for a, b in zip(rnn_native.STACK_LAUNCHES, before)]
+        assert ran == ([1, 1] if flag == "1" else [0, 0]), ran
+        rnn_native.check_coop_errors()                      # no hand-off wait timed out
+        res[flag] = (net.score(), net.flattenedGradients.clone(), net.output(x).float())
+    assert abs(res["1"][0] - res["0"][0]) < 1e-2 * abs(res["0"][0])
+    assert _rel(res["1"][2], res["0"][2]) < 2e-2
+    g1, g0 = res["1"][1], res["0"][1]
+    assert _rel(g1, g0) < 3e-2, _rel(g1, g0)
+
+
+def test_stack_tbptt_training_matches_separate_layers(cuda, monkeypatch):
+    """TBPTT (windows of 8 over 24 steps, carried h/c of both layers, truncated backward) trains like the unstacked
+    network, and the carried state lands in each layer's TBPTT map."""
+    x, y = _data(cuda, T=24)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_LSTM_STACK", flag)
+        net = _net(cuda, tbptt=8)
+        scores = []
+        for _ in range(3):
+            net.fit(x, y)
+            scores.append(net.score())
+        torch.cuda.synchronize()
+        for l in net.layers[:2]:
+            assert l.tBpttStateMap["prevAct"].shape == (x.shape[0], 256)
+        out[flag] = (scores, net.params().clone())
+    s1, s0 = out["1"][0], out["0"][0]
+    assert all(abs(a - b) < 2e-2 * abs(b) for a, b in zip(s1, s0)), (s1, s0)
+    assert _rel(out["1"][1], out["0"][1]) < 1e-2

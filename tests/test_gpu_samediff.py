@@ -116,3 +116,48 @@ def test_samediff_fit_hip_graph_matches_eager(cuda):
     (l0, p0), (l1, p1) = res
     assert all(abs(a - b) < 1e-3 * max(1.0, abs(a)) for a, b in zip(l0, l1)), (l0, l1)
     assert torch.allclose(p0, p1, atol=1e-4), (p0 - p1).abs().max()
+
+
+def test_samediff_gradient_sinks_and_master_views(cuda, monkeypatch):
+    """Training writes single-reader gradients straight into the flat gradient buffer (GEMM fp32 epilogue,
+    channel-sum, LayerNorm and embedding kernels) and reads GEMM biases / LayerNorm affine parameters from the fp32
+    master copy: same parameters as the copy-through path."""
+    from deeplearning4j_amd import Adam, DataSet
+    from deeplearning4j_amd.samediff import TrainingConfig
+    g = torch.Generator().manual_seed(2)
+    B, T, E, C = 4, 64, 128, 8
+    base = {"x": torch.randn(B, T, E, generator=g), "wqkv": torch.randn(E, 3 * E, generator=g) * E ** -0.5,
+            "bqkv": torch.randn(3 * E, generator=g) * 0.02, "wo": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bo": torch.zeros(E), "g": 1 + 0.1 * torch.randn(E, generator=g), "b": 0.1 * torch.randn(E, generator=g),
+            "wc": torch.randn(E, C, generator=g) * E ** -0.5, "wf": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bf": 0.02 * torch.randn(E, generator=g),
+            "y": torch.nn.functional.one_hot(torch.randint(0, C, (B,), generator=g), C).float()}
+    data = [DataSet(torch.randn(B, T, E, generator=g).to(cuda, torch.bfloat16),
+                    torch.nn.functional.one_hot(torch.randint(0, C, (B,), generator=g), C).to(cuda, torch.bfloat16))
+            for _ in range(3)]
+    res = []
+    for sinks in ("0", "1"):
+        monkeypatch.setenv("DL4J_AMD_SD_SINKS", sinks)
+        sd, loss = _transformer_block(cuda, torch.bfloat16, base)
+        sd.setTrainingConfig(TrainingConfig.builder().updater(Adam(1e-3)).dataSetFeatureMapping("x")
+                             .dataSetLabelMapping("y").build())
+        losses = [sd.fit(data[0])]
+        torch.cuda.synchronize()
+        st = sd._train_state
+        g1 = st["grad"].clone()                       # first step: same parameters on both paths
+        losses += [sd.fit(ds) for ds in data[1:]]
+        torch.cuda.synchronize()
+        inplace = {v.name for v, view in zip(sd.trainableVariables(), st["views"])
+                   if sd._last_grads.get(v.name) is not None and sd._last_grads[v.name].data_ptr() == view.data_ptr()}
+        if sinks == "1":
+            assert {"wqkv", "bqkv", "wo", "bo", "g", "b", "wf", "bf"} <= inplace, inplace
+            # "wo -> add -> layerNorm": the bias gradient of the out projection comes from the LayerNorm kernel
+            assert sd._ln_bias_fusions(sd._plan([loss.name]), {"bo": None}), "LN dsum fusion not planned"
+        else:
+            assert not inplace
+        assert sd.variables["bqkv"].value._dl4j_master.dtype == torch.float32
+        res.append((losses, g1, st["flat"].clone()))
+    (l0, g0, p0), (l1, g1, p1) = res
+    assert all(abs(a - b) < 1e-2 * max(1.0, abs(a)) for a, b in zip(l0, l1)), (l0, l1)
+    assert _rel(g1, g0) < 1e-2, _rel(g1, g0)          # bias sums from fp32 (LN kernel) vs bf16 (channel sum) rows
+    assert torch.allclose(p0, p1, atol=5e-3), (p0 - p1).abs().max()

@@ -1,7 +1,9 @@
 """Throughput of the in-tree MFMA GEMM (ops.gemm.mmul) vs torch.matmul (hipBLASLt) on the framework's shapes.
 
 Random uniform [-1, 1) operands (zero-filled data reads high, guide §5.4 rule 25), interleaved rounds in one
-process (rule 24), median of the rounds. Prints one line per shape: TF/s of both and the ratio.
+process (rule 24), median of the rounds. Prints one line per shape: TF/s of the in-tree kernels, of torch, their
+ratio, and of ``mmul``'s dispatch (the autotuner's pick between the in-tree configurations and the library GEMM,
+ops/gemm.py _lib_gemm) with its choice.
 Usage: python tools/gemm_bench.py [--dtype bf16|fp16] [--big]
 """
 import argparse
@@ -63,7 +65,7 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
-    print(f"{'shape':22s} {'M':>6s} {'N':>6s} {'K':>6s}   ours TF/s  torch TF/s  ratio")
+    print(f"{'shape':22s} {'M':>6s} {'N':>6s} {'K':>6s}   ours TF/s  torch TF/s  ratio  dispatch TF/s  pick")
     for name, M, N, K, la, lb in SHAPES:
         if args.only and args.only not in name:
             continue
@@ -72,14 +74,25 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=dt)
         flop = 2.0 * M * N * K
         reps = max(3, min(50, int(2e12 / flop)))
-        ours, ref = [], []
+        ours, ref, disp = [], [], []
+
+        def intree():
+            gemm._LIB = False
+            try:
+                gemm.mmul(a, b, out=out)
+            finally:
+                gemm._LIB = True
         for _ in range(args.rounds):
-            ours.append(timeit(lambda: gemm.mmul(a, b, out=out), reps))
+            ours.append(timeit(intree, reps))
             ref.append(timeit(lambda: torch.matmul(a, b, out=out), reps))
+            disp.append(timeit(lambda: gemm.mmul(a, b, out=out), reps))
         to = sorted(ours)[len(ours) // 2]
         tr = sorted(ref)[len(ref) // 2]
-        print(f"{name:22s} {M:6d} {N:6d} {K:6d}   {flop / to / 1e9:9.1f}  {flop / tr / 1e9:10.1f}  {tr / to:5.2f}",
-              flush=True)
+        td = sorted(disp)[len(disp) // 2]
+        picks = [v for k, v in gemm._TUNED.items() if k[:3] == (M, N, K) and "lib" in k]
+        pick = "lib" if picks and picks[-1] == gemm.LIB_CFG else (f"cfg{picks[-1][0]}x{picks[-1][1]}" if picks else "-")
+        print(f"{name:22s} {M:6d} {N:6d} {K:6d}   {flop / to / 1e9:9.1f}  {flop / tr / 1e9:10.1f}  {tr / to:5.2f}"
+              f"  {flop / td / 1e9:13.1f}  {pick}", flush=True)
 
 
 if __name__ == "__main__":
