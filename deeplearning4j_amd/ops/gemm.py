@@ -376,10 +376,13 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
 
 def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out_dtype):
     """A launcher ``(dst, beta) -> 0`` running the product as one hipBLASLt call through torch on the current stream,
-    or None when the problem needs an in-tree epilogue (activation, pre-activation, fp32 output from 16-bit operands,
-    a row bias, alpha != 1) or its destination is not a dense matrix."""
-    if not _LIB or act not in (None, "identity") or z is not None or alpha != 1.0 or out_dtype != a.dtype or \
+    or None when the problem needs an in-tree epilogue (activation, pre-activation, a row bias, alpha != 1, fp32
+    output combined with a bias / beta / batch) or its destination is not a dense matrix."""
+    if not _LIB or act not in (None, "identity") or z is not None or alpha != 1.0 or \
             a.dtype not in (torch.bfloat16, torch.float16) or b.dtype != a.dtype:
+        return None
+    wide = out_dtype == torch.float32                   # 16-bit operands, fp32 result (weight gradients)
+    if out_dtype != a.dtype and not (wide and bias is None and beta == 0.0 and not batched):
         return None
     if bias is not None and (bias.dtype != a.dtype or bias_dim != 1 or swap or batched or beta != 0.0):
         return None
@@ -390,7 +393,9 @@ def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out
 
     def run(dst, bt):
         d = dstv(dst)
-        if bias is not None:
+        if wide:
+            torch.mm(A_, B_, out_dtype=torch.float32, out=d)
+        elif bias is not None:
             torch.addmm(bias, A_, B_, out=d)
         elif bt == 0.0:
             (torch.bmm if batched else torch.mm)(A_, B_, out=d)

@@ -391,6 +391,7 @@ class SameDiff:
         Fusions (only where the intermediate has a single consumer and is not itself a target):
           linear -> gelu          one GEMM with the GELU in its epilogue (pre-activation kept for the backward)
           add(a, b) -> layerNorm  the residual sum done inside the LayerNorm kernel (same-shape operands)
+          lstmLayer -> lstmLayer  the two recurrences pipelined in one launch per direction (lstmStack2)
         Fused-away intermediates keep their definition-time values."""
         key = (tuple(targets) if targets is not None else None, self.fusion)
         hit = self._plans.get(key)
@@ -415,6 +416,11 @@ class SameDiff:
                 po, pop, prefs, pattrs = recs[j]
                 if op == "gelu" and pop == "linear" and "act" not in pattrs:
                     out[i] = (o, "linear", prefs, {**pattrs, "act": "gelu"})
+                    drop.add(j)
+                elif op == "lstmLayer" and pop == "lstmLayer" and refs[4:6] == [None, None] and \
+                        prefs[4:6] == [None, None] and attrs.get("peephole", False) == pattrs.get("peephole", False):
+                    # stacked LSTM layers: one pipelined launch per direction (autodiff lstmStack2)
+                    out[i] = (o, "lstmStack2", list(prefs[:4]) + list(refs[1:4]), dict(attrs))
                     drop.add(j)
                 elif op == "layerNorm" and pop == "add" and len(refs) == 3 and \
                         all(isinstance(r, str) for r in prefs):
@@ -461,6 +467,8 @@ class SameDiff:
             sinks = {n: t for n, t in sinks.items() if reads.get(n) == 1 and n not in grads}
         from . import autodiff as _ad
         dsum_for, presunk = (self._ln_bias_fusions(recs, sinks) if sinks else {}), {}
+        # inputs nobody differentiates (placeholders / constants not asked for): ops may skip their gradient
+        frozen = {n for n, k in self._kind.items() if k in ("PLACEHOLDER", "CONSTANT")} - set(wrt)
         final_at = {}
         if on_final is not None:
             want = set(wrt)
@@ -481,7 +489,8 @@ class SameDiff:
                 ins = [self._val(r) for r in refs]
                 sk = {j: sinks[r] for j, r in enumerate(refs) if isinstance(r, str) and r in sinks} if sinks else None
                 fz = dsum_for.get(i)
-                _ad.set_sinks(sk, done=presunk.get(i), dsum=None if fz is None else sinks[fz[1]])
+                _ad.set_sinks(sk, done=presunk.get(i), dsum=None if fz is None else sinks[fz[1]],
+                              nograd={j for j, r in enumerate(refs) if isinstance(r, str) and r in frozen})
                 try:
                     gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
                     if fz is not None and _ad.dsum_written():

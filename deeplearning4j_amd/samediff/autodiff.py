@@ -22,7 +22,7 @@ REGISTRY = {}
 _TLS = threading.local()
 
 
-def set_sinks(sinks, done=None, dsum=None):
+def set_sinks(sinks, done=None, dsum=None, nograd=None):
     """Gradient destinations of the op whose backward runs next: {input position: contiguous fp32 tensor shaped like
     that input} (SameDiff._backward sets them for variables only this op reads). ``done``: input positions whose
     sink an earlier backward already filled; ``dsum``: an fp32 sink for the column sums of this LayerNorm's input
@@ -31,6 +31,14 @@ def set_sinks(sinks, done=None, dsum=None):
     _TLS.done = done
     _TLS.dsum = dsum
     _TLS.dsum_written = False
+    _TLS.nograd = nograd
+
+
+def need_grad(i):
+    """False when the reverse pass will discard input ``i``'s gradient (a placeholder or constant nobody asked the
+    gradient of): the op may return None for it instead of computing it."""
+    n = getattr(_TLS, "nograd", None)
+    return not n or i not in n
 
 
 def sink_done(i):
@@ -507,6 +515,31 @@ register("maxPooling2d")(_pool("MAX"))
 register("avgPooling2d")(_pool("AVG"))
 
 
+def _lstm_native_grads(dz, xt, out, gates, call, h0, c0, x, W, RW, b, H, peephole, base, want_dx=None):
+    """[dx, dW, dRW, db] of one lstmLayer from the sequence kernel's gate deltas dz [T, mb, 4H] fp32: one glue
+    launch (bf16 dz, h_{t-1}, db, peephole sums: csrc/lstm_glue.hip) and MFMA GEMMs written straight into the
+    gradient sinks (input positions base+1..base+3); dx only when the input needs a gradient. None when the glue
+    does not take this dtype (the caller's generic path runs)."""
+    from ..ops import rnn_native
+    from ..ops.gemm import mmul
+    prep = rnn_native.lstm_bwd_prep(dz, out, h0, call, c0, peephole, W.dtype)
+    if prep is None:
+        return None
+    T, mb = dz.shape[0], dz.shape[1]
+    dzb, hpb, db, dpeep = prep
+    sw, srw, sb = grad_sink(base + 1), grad_sink(base + 2), grad_sink(base + 3)
+    dW = mmul(xt.t(), dzb, out=sw) if sw is not None else mmul(xt.t(), dzb, out_dtype=torch.float32)
+    gRW = srw if srw is not None else torch.empty(RW.shape, dtype=torch.float32, device=dz.device)
+    mmul(hpb.t(), dzb, out=gRW[:, :4 * H])
+    if peephole:
+        gRW[:, 4 * H:4 * H + 3].copy_(dpeep.t())
+    dbv = sb.view(-1).copy_(db) if sb is not None else db
+    dx = None
+    if (need_grad(base) if want_dx is None else want_dx):
+        dx = mmul(dzb, W.t()).reshape(T, mb, -1).permute(1, 2, 0).to(x.dtype)
+    return [dx, dW, gRW, dbv.reshape(b.shape)]
+
+
 def _lstm_fwd(ins, at):
     """x [mb, nIn, T] -> h [mb, H, T]; DL4J gate order [a|f|o|g], tanh/sigmoid."""
     x, W, RW, b, h0, c0 = ins
@@ -514,13 +547,19 @@ def _lstm_fwd(ins, at):
     mb, nIn, T = x.shape
     H = RW.shape[0]
     dt = W.dtype
-    xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
     from ..ops.gemm import mmul
-    zx = mmul(xt, W, bias=b.reshape(-1)).reshape(T, mb, 4 * H)
     from ..ops import rnn_native
     if x.is_cuda and rnn_native.supported(H, dt) and ops.use_native(x, "lstm"):
-        out, hT, cT, gates, call = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True)[:5]
-        return out.permute(1, 2, 0).to(x.dtype), ("native", xt, zx, out, gates, call)
+        from ..nn.layers.recurrent import _time_major_rows
+        xt = _time_major_rows(x, dt)                      # one cast/permute/pad launch, a GEMM operand in place
+        zx = mmul(xt, W, bias=master(b).reshape(-1)).reshape(T, mb, 4 * H)
+        packs = rnn_native.pack_rw(RW, H, peephole)       # both packed images in one launch, reused by backward
+        out, hT, cT, gates, call, o16 = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True, packs=packs,
+                                                                out16=x.dtype == dt)
+        y = o16.permute(1, 2, 0) if o16 is not None else out.permute(1, 2, 0).to(x.dtype)
+        return y, ("native", xt, zx, out, gates, call, packs)
+    xt = x.permute(2, 0, 1).reshape(T * mb, nIn).to(dt)
+    zx = mmul(xt, W, bias=b.reshape(-1)).reshape(T, mb, 4 * H)
     cd = torch.float64 if dt == torch.float64 else torch.float32
     h = torch.zeros(mb, H, dtype=cd, device=x.device) if h0 is None else h0.to(cd)
     c = torch.zeros(mb, H, dtype=cd, device=x.device) if c0 is None else c0.to(cd)
@@ -554,9 +593,11 @@ def _lstm_bwd(ctx, g, ins, at):
     from ..ops.gemm import mmul
     if ctx[0] == "native":
         from ..ops import rnn_native
-        _, xt, zx, out, gates, call = ctx
-        dout = g.permute(2, 0, 1).contiguous().float()
-        dz, dh0, dc0 = rnn_native.lstm_seq_bwd(dout, gates, call, c0, RW, H, peephole)
+        _, xt, zx, out, gates, call, packs = ctx
+        dz, dh0, dc0 = rnn_native.lstm_seq_bwd(g.permute(2, 0, 1), gates, call, c0, RW, H, peephole, packs=packs)
+        r = _lstm_native_grads(dz, xt, out, gates, call, h0, c0, x, W, RW, b, H, peephole, 0)
+        if r is not None:
+            return r + [None if h0 is None else dh0.to(h0.dtype), None if c0 is None else dc0.to(c0.dtype)]
         h0f = h0.float().reshape(1, mb, H) if h0 is not None else torch.zeros(1, mb, H, device=x.device)
         hprev = torch.cat([h0f, out[:-1].float()], 0).reshape(T * mb, H)
         dzf = dz.reshape(T * mb, 4 * H)
@@ -615,6 +656,68 @@ def _lstm_bwd(ctx, g, ins, at):
 
 
 register("lstmLayer")((_lstm_fwd, _lstm_bwd))
+
+
+# two stacked lstmLayer ops (SameDiff's fusion pass: the first one's output read only by the second): ONE pipelined
+# launch per direction (csrc/lstm_coop.hip lstm_fwd_stack2 / lstm_bwd_stack2, the MultiLayerNetwork stack path)
+def _lstm2_fwd(ins, at):
+    x, W1, RW1, b1, W2, RW2, b2 = ins
+    peephole = at.get("peephole", False)
+    mb, nIn, T = x.shape
+    H = RW1.shape[0]
+    dt = W1.dtype
+    from ..ops import rnn_native
+    if x.is_cuda and x.dtype == dt and ops.use_native(x, "lstm") and rnn_native.stack2_supported(H, dt, T) and \
+            RW2.shape[0] == H and tuple(W2.shape) == (H, 4 * H) and W2.dtype == dt:
+        from ..nn.layers.recurrent import _time_major_rows
+        from ..ops.gemm import mmul
+        xt = _time_major_rows(x, dt)
+        zx1 = mmul(xt, W1, bias=master(b1).reshape(-1)).reshape(T, mb, 4 * H)
+        p1, p2 = rnn_native.pack_rw(RW1, H, peephole), rnn_native.pack_rw(RW2, H, peephole)
+        pw = rnn_native.pack_rw(W2, H, False)
+        r = None
+        if p1 is not None and p2 is not None and pw is not None:
+            r = rnn_native.lstm2_seq_fwd(zx1, p1, p2, pw, master(b2).reshape(-1), H, (None, None), (None, None),
+                                         None, True)
+        if r is not None:
+            L1, L2 = r
+            return L2[5].permute(1, 2, 0), ("stack", xt, L1, L2, p1, p2, pw)
+    y1, c1 = _lstm_fwd([x, W1, RW1, b1, None, None], at)
+    y2, c2 = _lstm_fwd([y1, W2, RW2, b2, None, None], at)
+    return y2, ("pair", y1, c1, c2)
+
+
+def _lstm2_bwd(ctx, g, ins, at):
+    x, W1, RW1, b1, W2, RW2, b2 = ins
+    peephole = at.get("peephole", False)
+    H = RW1.shape[0]
+    outer = (getattr(_TLS, "sinks", None), getattr(_TLS, "nograd", None))
+    sk = outer[0] or {}
+    if ctx[0] == "pair":
+        _, y1, c1, c2 = ctx
+        try:
+            _TLS.sinks, _TLS.nograd = {k - 3: v for k, v in sk.items() if k >= 4}, None
+            g2 = _lstm_bwd(c2, g, [y1, W2, RW2, b2, None, None], at)
+            _TLS.sinks, _TLS.nograd = {k: v for k, v in sk.items() if k <= 3}, outer[1]
+            g1 = _lstm_bwd(c1, g2[0], [x, W1, RW1, b1, None, None], at)
+        finally:
+            _TLS.sinks, _TLS.nograd = outer
+        return g1[:4] + g2[1:4]
+    from ..ops import rnn_native
+    _, xt, L1, L2, p1, p2, pw = ctx
+    T, mb = L1[0].shape[0], L1[0].shape[1]
+    r = rnn_native.lstm2_seq_bwd(g.permute(2, 0, 1), {"gates": L1[3], "call": L1[4], "c0": None},
+                                 {"gates": L2[3], "call": L2[4], "c0": None}, p1, p2, pw, H)
+    if r is None:
+        raise RuntimeError("stacked LSTM forward ran but the stacked backward kernel rejected the shape")
+    dz1, dz2, _, _ = r
+    g2 = _lstm_native_grads(dz2, L1[5].reshape(T * mb, H), L2[0], L2[3], L2[4], None, None, x, W2, RW2, b2, H,
+                            peephole, 3, want_dx=False)
+    g1 = _lstm_native_grads(dz1, xt, L1[0], L1[3], L1[4], None, None, x, W1, RW1, b1, H, peephole, 0)
+    return g1 + g2[1:]
+
+
+register("lstmStack2")((_lstm2_fwd, _lstm2_bwd))
 
 
 # ----------------------------------------------------------------------------------------------- losses (scalar)

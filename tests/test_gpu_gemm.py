@@ -242,7 +242,7 @@ def test_zero_padded_k_operand(K):
     _check(out2, _ref(a.t(), g), torch.bfloat16, M, f"kz^T K={K}")
 
 
-@pytest.mark.parametrize("case", ["plain", "bias_shadow", "beta", "colmajor", "batched"])
+@pytest.mark.parametrize("case", ["plain", "bias_shadow", "beta", "colmajor", "batched", "fp32_out"])
 def test_library_candidate(case, monkeypatch):
     """The hipBLASLt candidate of the autotuner (forced here) computes the same product for every plain-GEMM form it
     accepts: bias through the 16-bit shadow attached to an fp32 master, beta-accumulate, column-major destinations
@@ -254,6 +254,9 @@ def test_library_candidate(case, monkeypatch):
     b = _mk((K, N), torch.bfloat16, contig_last=False)
     if case == "plain":
         _check(gemm.mmul(a, b), _ref(a, b), torch.bfloat16, K, case)
+    elif case == "fp32_out":                       # weight-gradient form: 16-bit operands, fp32 column-major result
+        out = torch.empty(N, M, device=DEV).t()
+        _check(gemm.mmul(a, b, out=out), _ref(a, b), torch.float32, K, case)
     elif case == "bias_shadow":
         master = torch.randn(N, device=DEV)
         master._dl4j_shadow = master.to(torch.bfloat16)
@@ -273,5 +276,5 @@ def test_library_candidate(case, monkeypatch):
         assert (out.float() - ref).abs().max() <= _tol(torch.bfloat16, K) * ref.abs().max()
     assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV, dtype=torch.bfloat16), False, False, None, 1, "gelu",
                           1.0, 0.0, None, torch.bfloat16) is None
-    assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV), False, False, None, 1, None, 1.0, 0.0, None,
-                          torch.float32) is None
+    assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV), False, False, None, 1, None, 1.0, 1.0, None,
+                          torch.float32) is None          # fp32 output with beta-accumulate stays in-tree

@@ -81,3 +81,46 @@ def test_stack_tbptt_training_matches_separate_layers(cuda, monkeypatch):
     s1, s0 = out["1"][0], out["0"][0]
     assert all(abs(a - b) < 2e-2 * abs(b) for a, b in zip(s1, s0)), (s1, s0)
     assert _rel(out["1"][1], out["0"][1]) < 1e-2
+
+
+def test_samediff_stacked_lstm_matches_pair(cuda, monkeypatch):
+    """SameDiff's lstmLayer -> lstmLayer fusion (lstmStack2) on the stacked kernels == the two single-layer ops;
+    training through TrainingConfig writes the gradients into the flat buffer (sinks)."""
+    from deeplearning4j_amd.samediff import SameDiff, TrainingConfig
+    g = torch.Generator().manual_seed(3)
+    mb, V, T, H = 32, 40, 30, 256
+    bf = torch.bfloat16
+    vals = {}
+    nin = V
+    for i in range(2):
+        vals[f"W{i}"] = torch.randn(nin, 4 * H, generator=g) * nin ** -0.5
+        vals[f"RW{i}"] = torch.randn(H, 4 * H + 3, generator=g) * H ** -0.5
+        vals[f"b{i}"] = torch.zeros(4 * H)
+        nin = H
+    vals["Wo"] = torch.randn(H, V, generator=g) * H ** -0.5
+    idx = torch.randint(0, V, (mb, T + 1), generator=g)
+    X = torch.nn.functional.one_hot(idx[:, :-1], V).permute(0, 2, 1).to(bf).to(cuda)
+    Y = torch.nn.functional.one_hot(idx[:, 1:], V).to(bf).to(cuda)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DL4J_AMD_LSTM_STACK", flag)
+        sd = SameDiff.create()
+        x = sd.placeHolder("x", X)
+        y = sd.placeHolder("y", Y)
+        h = x
+        for i in range(2):
+            h = sd.rnn().lstmLayer(f"l{i}", h, sd.var(f"W{i}", vals[f"W{i}"].to(bf).to(cuda)),
+                                   sd.var(f"RW{i}", vals[f"RW{i}"].to(bf).to(cuda)),
+                                   sd.var(f"b{i}", vals[f"b{i}"].to(bf).to(cuda)), peephole=True)
+        logits = h.permute(0, 2, 1).mmul(sd.var("Wo", vals["Wo"].to(bf).to(cuda)))
+        loss = sd.loss().softmaxCrossEntropy("loss", y, logits)
+        before = list(rnn_native.STACK_LAUNCHES)
+        gr = sd.execBackwards(loss)
+        torch.cuda.synchronize()
+        rnn_native.check_coop_errors()
+        ran = [a - b for a, b in zip(rnn_native.STACK_LAUNCHES, before)]
+        assert ran == ([1, 1] if flag == "1" else [0, 0]), ran
+        res[flag] = (float(loss.value), {k: v.float().cpu() for k, v in gr.items() if v is not None})
+    assert abs(res["1"][0] - res["0"][0]) < 1e-2 * abs(res["0"][0])
+    for k, v in res["0"][1].items():
+        assert _rel(res["1"][1][k], v) < 3e-2, (k, _rel(res["1"][1][k], v))

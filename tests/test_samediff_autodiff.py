@@ -118,6 +118,34 @@ def test_lstm_grads(peephole):
     h0, c0 = _r(mb, H, seed=5) * 0.3, _r(mb, H, seed=6) * 0.3
     _fd_check("lstmLayer", [x, W, RW, b, h0, c0], {"peephole": peephole}, [0, 1, 2, 3, 4, 5])
     _fd_check("lstmLayer", [x, W, RW, b, None, None], {"peephole": peephole}, [0, 2])
+    # two stacked layers as one fused op (the planner's lstmLayer -> lstmLayer fusion; CPU: the paired path)
+    W2 = _r(H, 4 * H, seed=7) * 0.5
+    RW2 = _r(H, 4 * H + (3 if peephole else 0), seed=8) * 0.5
+    b2 = _r(1, 4 * H, seed=9) * 0.1
+    _fd_check("lstmStack2", [x, W, RW, b, W2, RW2, b2], {"peephole": peephole}, [0, 1, 2, 3, 4, 5, 6])
+
+
+def test_lstm_stack_fusion_planned_and_equal():
+    """sd.rnn().lstmLayer twice in a row is planned as one lstmStack2 record with the same loss and gradients."""
+    from deeplearning4j_amd.samediff import SameDiff
+    mb, nIn, T, H = 2, 3, 5, 4
+    vals = {"W0": _r(nIn, 4 * H, seed=2) * 0.5, "RW0": _r(H, 4 * H + 3, seed=3) * 0.5, "b0": _r(4 * H, seed=4) * 0.1,
+            "W1": _r(H, 4 * H, seed=5) * 0.5, "RW1": _r(H, 4 * H + 3, seed=6) * 0.5, "b1": _r(4 * H, seed=7) * 0.1}
+    res = []
+    for fusion in (True, False):
+        sd = SameDiff.create()
+        sd.fusion = fusion
+        h = sd.placeHolder("x", _r(mb, nIn, T, seed=1))
+        for i in range(2):
+            h = sd.rnn().lstmLayer(f"l{i}", h, sd.var(f"W{i}", vals[f"W{i}"].clone()),
+                                   sd.var(f"RW{i}", vals[f"RW{i}"].clone()), sd.var(f"b{i}", vals[f"b{i}"].clone()),
+                                   peephole=True)
+        loss = h.mul(h).sum()
+        ops = [r[1] for r in sd._plan([loss.name])]
+        assert ("lstmStack2" in ops) == fusion and (ops.count("lstmLayer") == (0 if fusion else 2))
+        res.append(sd.execBackwards(loss))
+    for k in vals:
+        torch.testing.assert_close(res[0][k], res[1][k], rtol=1e-10, atol=1e-12)
 
 
 def test_loss_grads():
