@@ -88,6 +88,15 @@ class Evaluation(BaseEvaluation):
             self.table = np.zeros((C, C), dtype=np.int64)
             if self.labelsList is None:
                 self.labelsList = [str(i) for i in range(C)]
+        elif self.table.shape[0] < C:
+            # e.g. Evaluation(1) fed single-column binary data: two classes (reference EvalTest
+            # .testSingleClassBinaryClassification)
+            grown = np.zeros((C, C), dtype=np.int64)
+            n = self.table.shape[0]
+            grown[:n, :n] = self.table
+            self.table = grown
+            if self.labelsList is not None and len(self.labelsList) < C:
+                self.labelsList = list(self.labelsList) + [str(i) for i in range(len(self.labelsList), C)]
         if n_cols == 1:
             thr = 0.5 if self.binaryDecisionThreshold is None else self.binaryDecisionThreshold
             guess = (preds.reshape(-1) > thr).long()
@@ -367,7 +376,7 @@ class Evaluation(BaseEvaluation):
             for p in range(n):
                 c = int(self.table[a, p])
                 if c:
-                    lines.append(f"Examples labeled as {self.getClassLabel(a)} classified by model as "
+                    lines.append(f"Predictions labeled as {self.getClassLabel(a)} classified by model as "
                                  f"{self.getClassLabel(p)}: {c} times")
         warn = []
         if not suppressWarnings:
