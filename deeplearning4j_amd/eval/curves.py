@@ -79,9 +79,76 @@ class PrecisionRecallCurve(BaseCurve):
     def calculateAUPRC(self):
         return _area(self.recall, self.precision)
 
+    class Point:
+        def __init__(self, idx, threshold, precision, recall):
+            self.idx, self.threshold, self.precision, self.recall = int(idx), float(threshold), float(precision), \
+                float(recall)
+
+        def getIdx(self):
+            return self.idx
+
+        def getThreshold(self):
+            return self.threshold
+
+        def getPrecision(self):
+            return self.precision
+
+        def getRecall(self):
+            return self.recall
+
+    class Confusion:
+        def __init__(self, point, tp, fp, fn, tn):
+            self.point, self.tp, self.fp, self.fn, self.tn = point, int(tp), int(fp), int(fn), int(tn)
+
+        def getPoint(self):
+            return self.point
+
+        def getTpCount(self):
+            return self.tp
+
+        def getFpCount(self):
+            return self.fp
+
+        def getFnCount(self):
+            return self.fn
+
+        def getTnCount(self):
+            return self.tn
+
+    def _pt(self, i):
+        return PrecisionRecallCurve.Point(i, self.threshold[i], self.precision[i], self.recall[i])
+
     def getPointAtThreshold(self, t):
-        i = int(np.argmin(np.abs(self.threshold - t)))
-        return i, float(self.threshold[i]), float(self.precision[i]), float(self.recall[i])
+        """First point whose threshold is >= t (thresholds ascend), the last one when t is above all of them."""
+        # thresholds within 1e-9 count as equal (i * 0.1 vs i / 10 step arithmetic)
+        i = int(np.searchsorted(self.threshold, t - 1e-9, side="left"))
+        return self._pt(min(i, len(self.threshold) - 1))
+
+    def getPointAtPrecision(self, p):
+        """First point (lowest threshold) reaching precision p, else the last point."""
+        hit = np.nonzero(self.precision >= p)[0]
+        return self._pt(int(hit[0]) if hit.size else len(self.threshold) - 1)
+
+    def getPointAtRecall(self, r):
+        """Among the points with recall >= r: the highest-threshold one, preferring higher precision at equal
+        recall; the first point when none reaches r."""
+        found = None
+        for i in range(len(self.recall) - 1, -1, -1):
+            if self.recall[i] >= r and (found is None or (self.recall[i] == found.recall and
+                                                          self.precision[i] >= found.precision)):
+                found = self._pt(i)
+        return found if found is not None else self._pt(0)
+
+    def getConfusionMatrixAtThreshold(self, t):
+        if self.tpCount is None:
+            raise ValueError("this curve was built without confusion counts")
+        p = self.getPointAtThreshold(t)
+        i = p.idx
+        tn = self.totalCount - (self.tpCount[i] + self.fpCount[i] + self.fnCount[i])
+        return PrecisionRecallCurve.Confusion(p, self.tpCount[i], self.fpCount[i], self.fnCount[i], tn)
+
+    def getConfusionMatrixAtPoint(self, i):
+        return self.getConfusionMatrixAtThreshold(self.threshold[i])
 
     def getTitle(self):
         return f"Precision-Recall Curve (Area={self.calculateAUPRC():.4f})"

@@ -407,3 +407,76 @@ def test_regression_eval_methods_on_networks():
         re = m.evaluateRegression(ExistingDataSetIterator([ds]))
         for i in range(5):
             assert abs(re.meanSquaredError(i) - 1) < 1e-6 and abs(re.meanAbsoluteError(i) - 1) < 1e-6
+
+
+# ---- CORET:eval/ROCTest.java
+_EXP_TPR = {0: 1, 1: 1, 2: 1, 3: 1, 4: 1, 5: 1, 6: .8, 7: .6, 8: .4, 9: .2, 10: 0}
+_EXP_FPR = {0: 1, 1: .8, 2: .6, 3: .4, 4: .2, 5: 0, 6: 0, 7: 0, 8: 0, 9: 0, 10: 0}
+
+
+@pytest.mark.parametrize("single", [False, True])
+def test_roc_basic(single):
+    from deeplearning4j_amd.eval import ROC
+    p1 = torch.tensor([0.001, 0.101, 0.201, 0.301, 0.401, 0.501, 0.601, 0.701, 0.801, 0.901], dtype=torch.float64)
+    y1 = torch.tensor([0.0] * 5 + [1.0] * 5, dtype=torch.float64)
+    pred = p1.reshape(-1, 1) if single else torch.stack([1 - p1, p1], 1)
+    act = y1.reshape(-1, 1) if single else torch.stack([1 - y1, y1], 1)
+    roc = ROC(10)
+    for _ in range(2):
+        roc.eval(act, pred)
+        c = roc.getRocCurve()
+        assert c.numPoints() == 11
+        for i in range(11):
+            assert abs(c.getThreshold(i) - i / 10) < 1e-5
+            assert abs(c.getFalsePositiveRate(i) - _EXP_FPR[i]) < 1e-5
+            assert abs(c.getTruePositiveRate(i) - _EXP_TPR[i]) < 1e-5
+        assert abs(roc.calculateAUC() - 1.0) < 1e-6
+        roc.reset()
+
+
+def test_roc_known_values_and_pr_confusion():
+    from deeplearning4j_amd.eval import ROC
+    labels = torch.tensor([[0.0, 1], [0, 1], [1, 0], [1, 0], [1, 0]])
+    pred = torch.tensor([[0.199, 0.801], [0.499, 0.501], [0.399, 0.601], [0.799, 0.201], [0.899, 0.101]])
+    tpr = [1, 1, 1, 1, 1, 1, .5, .5, .5, 0, 0]
+    fpr = [1, 1, 2 / 3, 1 / 3, 1 / 3, 1 / 3, 1 / 3, 0, 0, 0, 0]
+    tps = [2, 2, 2, 2, 2, 2, 1, 1, 1, 0, 0]
+    fps = [3, 3, 2, 1, 1, 1, 1, 0, 0, 0, 0]
+    roc = ROC(10)
+    roc.eval(labels, pred)
+    c = roc.getRocCurve()
+    for i in range(11):
+        assert abs(c.getFalsePositiveRate(i) - fpr[i]) < 1e-5 and abs(c.getTruePositiveRate(i) - tpr[i]) < 1e-5
+    assert abs(roc.calculateAUC() - (0.5 / 3 + 2 / 3)) < 1e-6
+    prc = roc.getPrecisionRecallCurve()
+    for i in range(11):
+        cf = prc.getConfusionMatrixAtThreshold(i * 0.1)
+        assert (cf.getTpCount(), cf.getFpCount(), cf.getFnCount()) == (tps[i], fps[i], 2 - tps[i])
+        assert cf.getTnCount() == 5 - tps[i] - fps[i] - (2 - tps[i])
+
+
+def test_precision_recall_curve_point_methods():
+    from deeplearning4j_amd.eval.curves import PrecisionRecallCurve
+    thr = [i / 100 for i in range(101)]
+    prc = PrecisionRecallCurve(thr, thr, [1 - t for t in thr], None, None, None, -1)
+    for p in (prc.getPointAtThreshold(0.05), prc.getPointAtPrecision(0.05), prc.getPointAtRecall(1 - 0.05),
+              prc.getPointAtThreshold(0.0495), prc.getPointAtPrecision(0.0495), prc.getPointAtRecall(1 - 0.0505)):
+        assert p.getIdx() == 5 and abs(p.getThreshold() - 0.05) < 1e-6
+        assert abs(p.getPrecision() - 0.05) < 1e-6 and abs(p.getRecall() - 0.95) < 1e-6
+
+
+@pytest.mark.parametrize("remove", [True, False])
+def test_precision_recall_curve_confusion_consistent(remove):
+    from deeplearning4j_amd.eval import ROC
+    g = torch.Generator().manual_seed(11)
+    labels = (torch.rand(100, 1, generator=g) < 0.5).double()
+    probs = torch.rand(100, 1, generator=g, dtype=torch.float64)
+    r = ROC(0, remove)
+    r.eval(labels, probs)
+    prc = r.getPrecisionRecallCurve()
+    for i in range(prc.numPoints()):
+        cf = prc.getConfusionMatrixAtPoint(i)
+        p = cf.getPoint()
+        tp, fp, fn = cf.getTpCount(), cf.getFpCount(), cf.getFnCount()
+        prec = 1.0 if tp == 0 and fp == 0 else tp / (tp + fp)
+        assert abs(p.getPrecision() - prec) < 1e-8 and abs(p.getRecall() - tp / (tp + fn)) < 1e-8
