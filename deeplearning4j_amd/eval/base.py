@@ -67,7 +67,10 @@ def to_2d(labels, preds, mask=None):
         l2 = labels.permute(0, 2, 1).reshape(-1, n)
         p2 = preds.permute(0, 2, 1).reshape(-1, n)
         if mask is not None:
-            m = torch.as_tensor(mask).reshape(-1).to(l2.device) != 0
+            mk = torch.as_tensor(mask).to(l2.device)
+            if mk.dim() == 3:                         # per-output time-series mask [mb, n, T]: a 2d per-output mask
+                return l2, p2, mk.permute(0, 2, 1).reshape(-1, n)
+            m = mk.reshape(-1) != 0
             l2, p2 = l2[m], p2[m]
         return l2, p2, None
     if labels.dim() == 4:   # CNN segmentation-style output: [mb, c, h, w] -> [mb*h*w, c]

@@ -480,3 +480,66 @@ def test_precision_recall_curve_confusion_consistent(remove):
         tp, fp, fn = cf.getTpCount(), cf.getFpCount(), cf.getFnCount()
         prec = 1.0 if tp == 0 and fp == 0 else tp / (tp + fp)
         assert abs(p.getPrecision() - prec) < 1e-8 and abs(p.getRecall() - tp / (tp + fn)) < 1e-8
+
+
+# ---- CORET:eval/EvaluationBinaryTest.java
+def _bern(shape, g):
+    return (torch.rand(*shape, generator=g) < 0.5).double()
+
+
+def test_evaluation_binary_vs_evaluation_per_column():
+    from deeplearning4j_amd.eval import EvaluationBinary
+    g = torch.Generator().manual_seed(12345)
+    labels, pred = _bern((50, 4), g), torch.rand(50, 4, generator=g, dtype=torch.float64)
+    eb = EvaluationBinary()
+    eb.eval(labels, pred)
+    for i in range(4):
+        lc, pc = labels[:, i:i + 1], pred[:, i:i + 1]
+        bp = (pc > 0.5).double()
+        correct = (lc == bp)
+        e = Evaluation()
+        e.eval(lc, pc)
+        assert abs(eb.accuracy(i) - correct.double().mean().item()) < 1e-6
+        assert abs(e.accuracy() - eb.accuracy(i)) < 1e-6
+        assert abs(e.precision(1) - eb.precision(i)) < 1e-6 and abs(e.recall(1) - eb.recall(i)) < 1e-6
+        assert abs(e.f1(1) - eb.f1(i)) < 1e-6
+        assert eb.truePositives(i) == int((correct & (lc == 1)).sum()) == e.truePositives()[1]
+        assert eb.trueNegatives(i) == int((correct & (lc == 0)).sum()) == e.trueNegatives()[1]
+        assert eb.falsePositives(i) == e.falsePositives()[1] and eb.falseNegatives(i) == e.falseNegatives()[1]
+        assert eb.totalCount(i) == 50
+
+
+def test_evaluation_binary_merging_masking_time_series_roc():
+    from deeplearning4j_amd.eval import EvaluationBinary
+    g = torch.Generator().manual_seed(12345)
+    l1, l2 = _bern((30, 4), g), _bern((50, 4), g)
+    p1, p2 = torch.rand(30, 4, generator=g, dtype=torch.float64), torch.rand(50, 4, generator=g, dtype=torch.float64)
+    eb, eb1, eb2 = EvaluationBinary(), EvaluationBinary(), EvaluationBinary()
+    eb.eval(l1, p1)
+    eb.eval(l2, p2)
+    eb1.eval(l1, p1)
+    eb2.eval(l2, p2)
+    eb1.merge(eb2)
+    assert eb.stats() == eb1.stats()
+    # per-output mask
+    mask = torch.tensor([[1.0, 1, 0], [1, 0, 0], [1, 1, 0], [1, 0, 0], [1, 1, 1]])
+    labels = torch.tensor([[1.0, 1, 1], [0, 0, 0], [1, 1, 1], [0, 1, 1], [1, 0, 1]])
+    pred = torch.tensor([[0.9] * 3, [0.7] * 3, [0.6] * 3, [0.4] * 3, [0.1] * 3])
+    m = EvaluationBinary()
+    m.eval(labels, pred, mask)
+    assert [m.accuracy(i) for i in range(3)] == pytest.approx([0.6, 1.0, 0.0])
+    assert [m.truePositives(i) for i in range(3)] == [2, 2, 0]
+    assert [m.trueNegatives(i) for i in range(3)] == [1, 1, 0]
+    assert [m.falsePositives(i) for i in range(3)] == [1, 0, 0]
+    assert [m.falseNegatives(i) for i in range(3)] == [1, 0, 1]
+    # time series == step by step
+    lab, prd, msk = _bern((2, 4, 3), g), torch.rand(2, 4, 3, generator=g, dtype=torch.float64), _bern((2, 4, 3), g)
+    a, b = EvaluationBinary(), EvaluationBinary()
+    a.eval(lab, prd, msk)
+    for t in range(3):
+        b.eval(lab[:, :, t], prd[:, :, t], msk[:, :, t])
+    assert a.stats() == b.stats()
+    # with ROC attached
+    r = EvaluationBinary(4, 30)
+    r.eval(l1, p1)
+    assert r.getROCBinary() is not None and r.getROCBinary().numLabels() == 4
