@@ -676,20 +676,22 @@ __global__ void __launch_bounds__(128) lstm_fwd_stack2(Stack2Fwd a) {
   constexpr int npairs = 16 * (H / 2);
   gu64* own = exch + ((long long)role * tiles + tile) * 2 * npairs;
   gu64* ring = exch + 2LL * tiles * 2 * npairs + (long long)tile * Tn * npairs;
-  // sweep the tagged granules of one [16][H] bf16 tile into columns [coff, coff + H) of hb
+  // sweep the tagged granules of one [16][H] bf16 tile into columns [coff, coff + H) of hb; 16 loads per lane in
+  // flight (128 lanes x 16 = one [16][256] tile per round trip)
+  constexpr int SB = 16;
   auto sweep = [&](gu64* src, unsigned tag, __bf16* hb, int coff) {
     const long long deadline = wall_clock64() + a.timeout;
-    for (int base = 0; base < npairs; base += 8 * blockDim.x) {
-      unsigned long long v[8];
+    for (int base = 0; base < npairs; base += SB * blockDim.x) {
+      unsigned long long v[SB];
       for (;;) {
         bool ok = true;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < SB; ++q) {
           const int i = base + q * blockDim.x + threadIdx.x;
           v[q] = i < npairs ? __hip_atomic_load(src + i, RLX_AGENT) : ((unsigned long long)tag << 32);
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) ok &= (unsigned)(v[q] >> 32) == tag;
+        for (int q = 0; q < SB; ++q) ok &= (unsigned)(v[q] >> 32) == tag;
         if (ok) break;
         if (wall_clock64() > deadline || __hip_atomic_load(err, RLX_AGENT) != 0u) {
           __hip_atomic_store(err, 1u, RLX_AGENT);
@@ -699,7 +701,7 @@ __global__ void __launch_bounds__(128) lstm_fwd_stack2(Stack2Fwd a) {
         __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < SB; ++q) {
         const int i = base + q * blockDim.x + threadIdx.x;
         if (i < npairs) {
           const int r = i / (H / 2), k = (i - r * (H / 2)) * 2;
@@ -814,7 +816,7 @@ struct Stack2Bwd {
 template <int H, bool PEEP>
 __global__ void __launch_bounds__(128) lstm_bwd_stack2(Stack2Bwd a) {
   constexpr int U = 32, NW = 2, G = H / U, NTW = (H / 16) / NW, KL = 4 * U / 32, KSG = 4 * H / 32, LDZ = 4 * U + 8;
-  constexpr int NE = 4 * G, BATCH = NE < 16 ? NE : 16;
+  constexpr int NE = 4 * G, BATCH = NE < 32 ? NE : 32;     // all partials of a gather in one round trip
   constexpr int H4 = 4 * H;
   constexpr int RWS = (H / 16) * KL * 64;                 // fragments of one resident slice
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
