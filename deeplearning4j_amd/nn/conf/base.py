@@ -85,10 +85,11 @@ class _AutoBuilder:
         name = cls._ALIASES.get(name, name)
         if name not in cls._all_fields():
             raise AttributeError(f"{cls.__name__}.Builder has no property {name!r}")
-        if name == "weightInit" and "dist" in cls._all_fields():
+        dist_field = {"weightInit": "dist", "weightInitRecurrent": "distRecurrent"}.get(name)
+        if dist_field is not None and dist_field in cls._all_fields():
             from .weights import Distribution, WeightInit
             if isinstance(value, Distribution):       # layer.weightInit(dist) == dist(d) + WeightInit.DISTRIBUTION
-                self._kw["dist"] = value
+                self._kw[dist_field] = value
                 value = WeightInit.DISTRIBUTION
         conv = cls._CONVERTERS.get(name)
         self._kw[name] = conv(value) if conv else value
@@ -158,6 +159,12 @@ class Config:
             k = self._ALIASES.get(k, k)
             if k not in fields:
                 raise TypeError(f"{type(self).__name__} has no property {k!r}")
+            dist_field = {"weightInit": "dist", "weightInitRecurrent": "distRecurrent"}.get(k)
+            if dist_field in fields and dist_field not in kw:
+                from .weights import Distribution, WeightInit
+                if isinstance(v, Distribution):
+                    setattr(self, dist_field, v)
+                    v = WeightInit.DISTRIBUTION
             conv = self._CONVERTERS.get(k)
             setattr(self, k, conv(v) if conv and v is not None else v)
         self._post_init()

@@ -993,6 +993,7 @@ class BaseRecurrentLayer(FeedForwardLayer):
 class AbstractLSTM(BaseRecurrentLayer):
     FIELDS = {"forgetGateBiasInit": 1.0, "gateActivationFn": None}
     _CONVERTERS = dict(BaseRecurrentLayer._CONVERTERS, gateActivationFn=to_activation)
+    _ALIASES = dict(BaseRecurrentLayer._ALIASES, gateActivationFunction="gateActivationFn")
     PEEPHOLE = False
 
     def finalize_defaults(self):

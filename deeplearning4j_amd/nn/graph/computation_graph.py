@@ -39,6 +39,11 @@ def _shares_storage(a, b):
     return a0 < b1 and b0 < a1
 
 
+
+def _out_dtype(t):
+    """16-bit activations come back as fp32 (the reference's output dtype); fp32/fp64 graphs keep theirs."""
+    return t.float() if t.dtype in (torch.bfloat16, torch.float16) else t
+
 class ComputationGraph(BaseNetwork):
     _key_by_name = True
 
@@ -258,6 +263,8 @@ class ComputationGraph(BaseNetwork):
                                             f"{list(self.conf.networkInputs)}, got {len(inputs)} arrays")
         chk = self._input_check(inputs)
         idx = self._index_checked()
+        if masks is None:
+            masks = self.inputMaskArrays
         acts = {}
         amask = {}
         mb = inputs[0].shape[0]
@@ -314,12 +321,20 @@ class ComputationGraph(BaseNetwork):
         self._acts_masks = amask
         return acts
 
+    def setLayerMaskArrays(self, featureMaskArrays, labelMaskArrays):
+        """Masks used by later output/feedForward calls that pass none (reference ComputationGraph.setLayerMaskArrays)."""
+        self.inputMaskArrays = list(featureMaskArrays) if featureMaskArrays is not None else None
+        self.labelMaskArrays = list(labelMaskArrays) if labelMaskArrays is not None else None
+
+    def clearLayerMaskArrays(self):
+        self.inputMaskArrays = self.labelMaskArrays = None
+
     def output(self, *inputs, train=False, masks=None):
         if len(inputs) == 1 and isinstance(inputs[0], (list, tuple)):
             inputs = inputs[0]
         with torch.no_grad():
             acts = self.feedForward(list(inputs), train, masks)
-        outs = [acts[o].float() for o in self.outputs]
+        outs = [_out_dtype(acts[o]) for o in self.outputs]
         return outs
 
     def outputSingle(self, *inputs, train=False):
@@ -606,7 +621,7 @@ class ComputationGraph(BaseNetwork):
                         acts[name] = layer.activate(x, False)
                 else:
                     acts[name], _ = v.forward(ins, False, None)
-        return [acts[o].float() for o in self.outputs]
+        return [_out_dtype(acts[o]) for o in self.outputs]
 
     def rnnClearPreviousState(self):
         for l in self.layers_by_name.values():

@@ -75,6 +75,10 @@ class MaskZeroLayerImpl(LayerImpl):
         super().__init__(conf, index, net)
         self.inner = conf.underlying.instantiate(index=index, net=net)
 
+    def getUnderlying(self):
+        self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
+        return self.inner
+
     def activate(self, x, training=False, mask=None, **kw):
         self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
         m = (x != self.conf.maskingValue).any(dim=1).to(x.dtype)      # [mb, T]

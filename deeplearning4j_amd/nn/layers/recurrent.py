@@ -581,6 +581,10 @@ class LastTimeStepImpl(LayerImpl):
     def bind(self):
         self.inner.params, self.inner.cparams, self.inner.grads = self.params, self.cparams, self.grads
 
+    def getUnderlying(self):
+        self.bind()
+        return self.inner
+
     def activate(self, x, training=False, mask=None, **kw):
         from ..util.time_series import last_time_step
         self.bind()

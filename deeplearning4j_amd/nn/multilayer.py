@@ -163,7 +163,8 @@ class MultiLayerNetwork(BaseNetwork):
         with torch.no_grad():
             acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, featuresMask)
         out = acts[-1]
-        return out.float() if out.is_floating_point() else out
+        # 16-bit activations come back as fp32 (the reference's output dtype); fp32/fp64 networks keep theirs
+        return out.float() if out.dtype in (torch.bfloat16, torch.float16) else out
 
     def activate(self, x, train=False):
         return self.output(x, train)
@@ -366,7 +367,7 @@ class MultiLayerNetwork(BaseNetwork):
                     x = layer.rnnTimeStep(x)
                 else:
                     x = layer.activate(x, False)
-        return x.float()
+        return x.float() if x.dtype in (torch.bfloat16, torch.float16) else x
 
     def rnnClearPreviousState(self):
         for l in self.layers:
