@@ -75,12 +75,20 @@ def test_stack_tbptt_training_matches_separate_layers(cuda, monkeypatch):
             net.fit(x, y)
             scores.append(net.score())
         torch.cuda.synchronize()
+        # fit clears the carried state at the end of each sequence; one more window stores it again
+        net.rnnClearPreviousState()
+        net.feedForwardToLayer(2, x[:, :, :8], True, None, stored_state=True, store_last_for_tbptt=True)
+        states = []
         for l in net.layers[:2]:
             assert l.tBpttStateMap["prevAct"].shape == (x.shape[0], 256)
-        out[flag] = (scores, net.params().clone())
+            states += [l.tBpttStateMap["prevAct"].float(), l.tBpttStateMap["prevMem"].float()]
+        net.rnnClearPreviousState()
+        out[flag] = (scores, net.params().clone(), states)
     s1, s0 = out["1"][0], out["0"][0]
     assert all(abs(a - b) < 2e-2 * abs(b) for a, b in zip(s1, s0)), (s1, s0)
     assert _rel(out["1"][1], out["0"][1]) < 1e-2
+    for a, b in zip(out["1"][2], out["0"][2]):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
 
 
 def test_samediff_stacked_lstm_matches_pair(cuda, monkeypatch):
