@@ -200,26 +200,28 @@ class JapaneseTokenizerFactory(_SegmentingFactory):
 
 
 class ChineseTokenizerFactory(_SegmentingFactory):
-    """One token per Han character; latin words and digit runs are kept whole."""
+    """Maximum-probability word segmentation over a word dictionary (``nlp/chinese.py``; reference
+    deeplearning4j-nlp-chinese ChineseTokenizerFactory / ChineseTokenizer over ansj ToAnalysis).
+
+    dictionary: a ``chinese.CoreDictionary`` or a path to an ansj ``core.dic`` (default: ``DL4J_AMD_ZH_DICT`` when
+    set, else the small built-in closed-class dictionary). userDictionary: a ``CoreDictionary`` or userLibrary text
+    (``word TAB nature TAB freq`` lines)."""
+
+    def __init__(self, dictionary=None, userDictionary=None):
+        super().__init__()
+        from . import chinese as Z
+        if isinstance(dictionary, str):
+            dictionary = Z.CoreDictionary.from_ansj_core(dictionary)
+        if isinstance(userDictionary, str):
+            userDictionary = Z.CoreDictionary.from_user_library(userDictionary)
+        self.segmenter = Z.Segmenter(dictionary, userDictionary)
+
+    def terms(self, text):
+        """Segmented words with their natures (ansj Term)."""
+        return self.segmenter.terms(text)
 
     def segment(self, text):
-        toks, cur = [], ""
-        for ch in unicodedata.normalize("NFKC", text):
-            s = _script(ch)
-            if s == "han":
-                if cur:
-                    toks.append(cur)
-                    cur = ""
-                toks.append(ch)
-            elif s in ("latin", "digit"):
-                cur += ch
-            else:
-                if cur:
-                    toks.append(cur)
-                cur = ""
-        if cur:
-            toks.append(cur)
-        return toks
+        return self.segmenter.segment(text)
 
 
 _KO_JOSA = ("으로", "에서", "에게", "까지", "부터", "은", "는", "이", "가", "을", "를", "에", "의", "도", "로", "와", "과", "만")
