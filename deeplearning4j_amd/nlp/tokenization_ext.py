@@ -3,10 +3,10 @@ StemmingPreprocessor / PoS tokenizers, deeplearning4j-nlp-japanese (Kuromoji), -
 BERT WordPiece tokenizer for the transformer path.
 
 Japanese: the lattice / Viterbi morphological analyser of ``nlp/kuromoji.py`` (Kuromoji's algorithm; MeCab/IPADIC
-dictionaries load from their source files, a small built-in lexicon otherwise). The Chinese and Korean modules'
-dictionaries are not in this image, so those two are dictionary-free segmenters with the same TokenizerFactory API:
-* Chinese: one token per Han character (the standard dictionary-free baseline), latin/digit runs kept whole.
-* Korean: whitespace eojeol split with trailing postposition (josa) stripping.
+dictionaries load from their source files, a small built-in lexicon otherwise).
+* Chinese: maximum-probability word lattice over an ansj core dictionary (``nlp/chinese.py``; core.dic read from its
+  file, a built-in closed-class dictionary otherwise).
+* Korean: eojeol decomposition into nouns, josa, predicate stems and endings (``nlp/korean.py``).
 The Porter stemmer (English) is the algorithm behind the UIMA module's StemmingPreprocessor.
 """
 import os
@@ -224,22 +224,26 @@ class ChineseTokenizerFactory(_SegmentingFactory):
         return self.segmenter.segment(text)
 
 
-_KO_JOSA = ("으로", "에서", "에게", "까지", "부터", "은", "는", "이", "가", "을", "를", "에", "의", "도", "로", "와", "과", "만")
-
-
 class KoreanTokenizerFactory(_SegmentingFactory):
-    """Whitespace eojeol split; one trailing josa (postposition) is split off when the stem keeps >= 1 syllable."""
+    """Eojeol decomposition into nouns, josa, predicate stems and endings (``nlp/korean.py``; reference
+    deeplearning4j-nlp-korean KoreanTokenizerFactory over twitter-korean-text). dictionary: a
+    ``korean.KoreanDictionary``, a path to a noun list, or an iterable of nouns (default: ``DL4J_AMD_KO_DICT`` when
+    set, else the built-in pronoun / bound-noun set)."""
+
+    def __init__(self, dictionary=None):
+        super().__init__()
+        from . import korean as K
+        if isinstance(dictionary, str):
+            dictionary = K.KoreanDictionary.from_file(dictionary)
+        elif dictionary is not None and not isinstance(dictionary, K.KoreanDictionary):
+            dictionary = K.KoreanDictionary(dictionary)
+        self.analyzer = K.KoreanAnalyzer(dictionary)
+
+    def tokens(self, text):
+        return self.analyzer.tokenize(text)
 
     def segment(self, text):
-        out = []
-        for w in re.findall(r"\w+", unicodedata.normalize("NFC", text)):
-            for j in _KO_JOSA:
-                if w.endswith(j) and len(w) > len(j) and _script(w[0]) == "hangul":
-                    out.extend([w[:-len(j)], j])
-                    break
-            else:
-                out.append(w)
-        return out
+        return [t.text for t in self.analyzer.tokenize(text) if t.pos != "Punctuation"]
 
 
 # ------------------------------------------------------------------------------------------------ BERT WordPiece
