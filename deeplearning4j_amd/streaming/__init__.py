@@ -6,9 +6,10 @@ arrays over Kafka topics through Camel (STRM:kafka/*); ``DL4jServeRouteBuilder``
 restores a ModelSerializer zip, runs ``output`` and publishes the result (STRM:routes/DL4jServeRouteBuilder.java:
 48-92); ``CSVRecordToINDArray`` / ``CSVRecordToDataSet`` convert DataVec records (STRM:conversion/*).
 
-Kafka/Camel are not in this image, so topics are served by an in-process :class:`Broker` (thread-safe, many
-producers / consumers per topic) with the same message format (base64 of the ND4J binary array codec, so
-payloads interoperate with the reference's). :class:`ModelServer` exposes the same serve route over HTTP
+Topics are served either by an in-process :class:`Broker` (thread-safe, many producers / consumers per topic) or by
+a Kafka cluster through :class:`~deeplearning4j_amd.streaming.kafka.KafkaBroker`, which speaks the Kafka wire
+protocol itself (no client library in the image; ``streaming/kafka.py``). Either way the message format is the
+reference's: base64 of the ND4J binary array codec, so payloads interoperate. :class:`ModelServer` exposes the same serve route over HTTP
 (FastAPI) with dynamic batching through :class:`~deeplearning4j_amd.parallel.ParallelInference` on the GPU.
 """
 import base64
@@ -63,6 +64,12 @@ class Broker:
 
 
 _default_broker = Broker()
+
+
+def KafkaBroker(bootstrap, **kw):
+    """A Broker over a Kafka cluster (``"host:port[,host:port]"``); see ``streaming/kafka.py``."""
+    from .kafka import KafkaBroker as _K
+    return _K(bootstrap, **kw)
 
 
 def default_broker():
