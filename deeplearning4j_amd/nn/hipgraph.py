@@ -26,6 +26,7 @@ Eligibility: plain SGD-family optimizer, a capturable (or no) gradient accumulat
 (onForwardPass/onBackwardPass/onGradientCalculation), CUDA device, fixed shapes. Anything else falls back to the
 eager step transparently.
 """
+import collections
 import contextlib
 import gc
 import logging
@@ -89,6 +90,10 @@ def capture_gc_guard():
                 gc.enable()
 
 
+class Sig(collections.namedtuple("Sig", "shape dtype")):
+    """Shape + dtype of a tensor as the captured step will hold it (a replay key before any cast)."""
+
+
 class CapturedTrainingStep:
     def __init__(self, net, inputs, labels, fmasks=None, lmasks=None, tbptt_back=None):
         self.net = net
@@ -141,11 +146,15 @@ class CapturedTrainingStep:
         else:
             n.computeGradientAndScore(self.static_x[0], self.static_y[0], fm[0] if fm else None,
                                       lm[0] if lm else None, defer_reg=True, **kw)
+        dst, src = [], []
         for l, k, buf in self.state:               # the window's final state becomes the next replay's input
             new = l.tBpttStateMap.get(k)
             if new is not None and new is not buf:
-                buf.copy_(new)
+                dst.append(buf)
+                src.append(new)
             l.tBpttStateMap[k] = buf
+        if dst:                                    # one multi-tensor copy node instead of one per state tensor
+            torch._foreach_copy_(dst, src)
         acc = getattr(n, "gradientsAccumulator", None)
         if acc is not None:
             acc.reduce_gradients(n)                # bucketed RCCL all-reduces become graph nodes

@@ -470,24 +470,32 @@ class BaseNetwork:
         the window), each captured after ``warmup`` eager iterations of that signature."""
         if not getattr(self, "_hipgraph_enabled", False):
             return False
-        from .hipgraph import CapturedTrainingStep, carries_state, graph_eligible
-        inputs = [self._to_dev(t, self._feat_dtype()) for t in inputs]
-        labels = [self._to_dev(t, self.master_dtype) for t in labels]
+        from .hipgraph import CapturedTrainingStep, Sig, carries_state, graph_eligible
         fm = None if fmasks is None else [None if m is None else self._to_dev(m)
                                           for m in (fmasks if isinstance(fmasks, (list, tuple)) else [fmasks])]
         lm = None if lmasks is None else [None if m is None else self._to_dev(m)
                                           for m in (lmasks if isinstance(lmasks, (list, tuple)) else [lmasks])]
-        if not graph_eligible(self, inputs, labels, fm, lm, tbptt_window=tbptt_back is not None):
+        # on the device, not yet cast: a replay's copy into the static buffers does the cast in the same kernel
+        raw_in = [self._to_dev(t) for t in inputs]
+        raw_lab = [self._to_dev(t) for t in labels]
+        fdt, ldt = self._feat_dtype(), self.master_dtype
+
+        def cast_sig(ts, dt):
+            return [Sig(t.shape, dt if t.is_floating_point() else t.dtype) for t in ts]
+        sig_in, sig_lab = cast_sig(raw_in, fdt), cast_sig(raw_lab, ldt)
+        if not graph_eligible(self, raw_in, raw_lab, fm, lm, tbptt_window=tbptt_back is not None):
             return False
-        key = CapturedTrainingStep.key(inputs, labels, fm, lm, tbptt_back)
+        key = CapturedTrainingStep.key(sig_in, sig_lab, fm, lm, tbptt_back)
         if tbptt_back is not None:
             key = key + (carries_state(self),)
         graphs = self.__dict__.setdefault("_hipgraphs", {})
         cs = graphs.get(key)
         if cs is not None and cs.ok:
-            cs.step(inputs, labels, fm, lm)
+            cs.step(raw_in, raw_lab, fm, lm)
             self._hipgraph = cs
             return True
+        inputs = [t.to(fdt) if t.is_floating_point() else t for t in raw_in]
+        labels = [t.to(ldt) if t.is_floating_point() else t for t in raw_lab]
         seen = self.__dict__.setdefault("_hipgraph_seen_by", {})
         seen[key] = seen.get(key, 0) + 1
         self._hipgraph_seen = seen[key]

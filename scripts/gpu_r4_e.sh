@@ -22,6 +22,8 @@ prof() {   # prof <name> <cmd...>: kernel trace of a short run, last-step table
   rm -rf "gpurun_out/r4e_p_$name"; head -14 "gpurun_out/r4e_${name}_step.txt"
 }
 prof resnet python3 "$R/bench.py" --steps 4 --warmup 3
+step choices 300 python3 tools/conv_choices.py --batch 512
+grep -v amdgpu.ids gpurun_out/r4e_choices.log | head -80
 prof bert python3 "$R/tools/bench_bert.py" --steps 4 --warmup 3
 step bert_fp16 300 python3 tools/bench_bert.py --steps 10 --warmup 3 --dtype fp16
 step bert_sd_fp16 300 python3 tools/bench_bert_samediff.py --steps 10 --warmup 3 --dtype fp16
