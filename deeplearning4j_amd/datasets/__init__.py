@@ -4,7 +4,10 @@ from .dataset import (DataSet, DataSetIterator, ExistingDataSetIterator, Iterato
 from .iterators import (AsyncDataSetIterator, AsyncMultiDataSetIterator, BenchmarkDataSetIterator,
                         BenchmarkMultiDataSetIterator, DoublesDataSetIterator, EarlyTerminationDataSetIterator,
                         KFoldIterator, MultiDataSetIteratorAdapter, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
-                        FileDataSetIterator, ReconstructionDataSetIterator)
+                        FileDataSetIterator, ReconstructionDataSetIterator, InequalityHandling,
+                        JointParallelDataSetIterator, CombinedPreProcessor, CombinedMultiDataSetPreProcessor)
+from .normalizers import (NormalizerStandardize, NormalizerMinMaxScaler, ImagePreProcessingScaler,  # noqa: F401
+                          VGG16ImagePreProcessor, MultiNormalizerStandardize, MultiNormalizerMinMaxScaler)
 from .fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator, LFWDataSetIterator,  # noqa
                        MnistDataSetIterator, TinyImageNetDataSetIterator, UciSequenceDataSetIterator)
 from .datavec import (CSVRecordReader, CSVSequenceRecordReader, CollectionRecordReader, FileSplit,  # noqa: F401

@@ -420,3 +420,127 @@ class ReconstructionDataSetIterator(DataSetIterator):
 
     def batch(self):
         return self.base.batch()
+
+
+# ------------------------------------------------------------------------------------------------ combinators
+class InequalityHandling:
+    """What JointParallelDataSetIterator does once one source runs dry (reference enums/InequalityHandling.java)."""
+    STOP_EVERYONE = "STOP_EVERYONE"      # stop as soon as the source whose turn it is has nothing left
+    PASS_NULL = "PASS_NULL"              # an exhausted source's turns yield None; rounds run while any source has data
+    RELOCATE = "RELOCATE"                # an exhausted source's turns go to the next source that still has data
+    RESET = "RESET"                      # an exhausted source restarts, until every source has run dry once
+
+
+class JointParallelDataSetIterator(DataSetIterator):
+    """Round-robin over several source iterators, one batch per source per turn (reference
+    datasets/iterator/parallel/JointParallelDataSetIterator.java: feeds ParallelWrapper workers from several
+    sources, e.g. one per device), with the inequality policy above for sources of different lengths."""
+
+    class Builder:
+        def __init__(self, inequalityHandling=InequalityHandling.STOP_EVERYONE):
+            self._h = inequalityHandling
+            self._src = []
+            self._pp = None
+
+        def addSourceIterator(self, it):
+            self._src.append(it)
+            return self
+
+        def setPreProcessor(self, pp):
+            self._pp = pp
+            return self
+
+        def build(self):
+            j = JointParallelDataSetIterator(self._src, self._h)
+            j.preProcessor = self._pp
+            return j
+
+    def __init__(self, sources, inequalityHandling=InequalityHandling.STOP_EVERYONE):
+        if not sources:
+            raise ValueError("JointParallelDataSetIterator needs at least one source iterator")
+        self.sources = list(sources)
+        self.handling = inequalityHandling
+        self.turn = 0
+        self.dried = [False] * len(self.sources)      # ran dry at least once (RESET)
+
+    def _live(self):
+        return [i for i, s in enumerate(self.sources) if s.hasNext()]
+
+    def hasNext(self):
+        h, i = self.handling, self.turn
+        if h == InequalityHandling.STOP_EVERYONE:
+            return self.sources[i].hasNext()
+        if h == InequalityHandling.RESET:
+            if self.sources[i].hasNext():
+                return True
+            self.dried[i] = True
+            return not all(self.dried)
+        if h == InequalityHandling.PASS_NULL and i != 0:
+            return True                            # a started round is completed (with None for dry sources)
+        return bool(self._live())
+
+    def next(self, num=None):
+        if not self.hasNext():
+            raise StopIteration
+        i = self.turn
+        self.turn = (i + 1) % len(self.sources)
+        s, h = self.sources[i], self.handling
+        if s.hasNext():
+            return self._pp(s.next())
+        if h == InequalityHandling.PASS_NULL:
+            return None
+        if h == InequalityHandling.RESET:
+            self.dried[i] = True
+            s.reset()
+            return self._pp(s.next())
+        # RELOCATE: the next source (in turn order) that still has data
+        for k in range(1, len(self.sources)):
+            j = (i + k) % len(self.sources)
+            if self.sources[j].hasNext():
+                return self._pp(self.sources[j].next())
+        raise StopIteration
+
+    def reset(self):
+        for s in self.sources:
+            s.reset()
+        self.turn = 0
+        self.dried = [False] * len(self.sources)
+
+    def batch(self):
+        return self.sources[0].batch()
+
+
+class CombinedPreProcessor:
+    """Applies several DataSet pre-processors in order (reference nd4j CombinedPreProcessor; Builder.addPreProcessor
+    appends, addPreProcessor(index, p) inserts)."""
+
+    class Builder:
+        def __init__(self):
+            self._pps = []
+
+        def addPreProcessor(self, a, b=None):
+            if b is None:
+                self._pps.append(a)
+            else:
+                self._pps.insert(int(a), b)
+            return self
+
+        def build(self):
+            return CombinedPreProcessor(self._pps)
+
+    def __init__(self, preProcessors):
+        self.preProcessors = list(preProcessors)
+
+    def preProcess(self, ds):
+        for p in self.preProcessors:
+            p.preProcess(ds)
+
+    __call__ = preProcess
+
+
+class CombinedMultiDataSetPreProcessor(CombinedPreProcessor):
+    """The MultiDataSet variant (reference CombinedMultiDataSetPreProcessor)."""
+
+    class Builder(CombinedPreProcessor.Builder):
+        def build(self):
+            return CombinedMultiDataSetPreProcessor(self._pps)

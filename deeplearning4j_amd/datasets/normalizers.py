@@ -329,8 +329,9 @@ class VGG16ImagePreProcessor(DataNormalization):
         return x if which == "l" else x + self._off(x)
 
 
-class MultiNormalizerStandardize:
-    """Per-input/per-output standardization for MultiDataSet (ND4J MultiNormalizerStandardize)."""
+class _MultiNormalizer:
+    """Per-input / per-output normalization of MultiDataSets (ND4J MultiNormalizerStandardize /
+    MultiNormalizerMinMaxScaler): one single-array normalizer per feature (and, with fitLabel, label) array."""
 
     def __init__(self):
         self.fitLabels = False
@@ -340,10 +341,17 @@ class MultiNormalizerStandardize:
         self.fitLabels = bool(b)
         return self
 
+    def isFitLabel(self):
+        return self.fitLabels
+
+    def _make(self, stats):
+        raise NotImplementedError
+
     def fit(self, data):
         from .dataset import MultiDataSet
         items = [data] if isinstance(data, MultiDataSet) else list(_iter_datasets(data))
-        nf, nl = items[0].numFeatureArrays(), items[0].numLabelsArrays()
+        nf = items[0].numFeatureArrays()
+        nl = items[0].numLabelsArrays() if items[0].labels is not None else 0
         fs, ls = [_Stats() for _ in range(nf)], [_Stats() for _ in range(nl)]
         for mds in items:
             for i in range(nf):
@@ -351,8 +359,8 @@ class MultiNormalizerStandardize:
             if self.fitLabels:
                 for i in range(nl):
                     ls[i].add(mds.getLabels(i))
-        self.f = [NormalizerStandardize(s.mean(), s.std().clamp_min(EPS)) for s in fs]
-        self.l = [NormalizerStandardize(s.mean(), s.std().clamp_min(EPS)) for s in ls] if self.fitLabels else []
+        self.f = [self._make(s) for s in fs]
+        self.l = [self._make(s) for s in ls] if self.fitLabels else []
         return self
 
     def preProcess(self, mds):
@@ -368,3 +376,37 @@ class MultiNormalizerStandardize:
             mds.features[i] = n.revertFeatures(mds.features[i])
         for i, n in enumerate(self.l):
             mds.labels[i] = n.revertFeatures(mds.labels[i])
+
+    def revertFeatures(self, features):
+        return [n.revertFeatures(x) for n, x in zip(self.f, features)]
+
+    def revertLabels(self, labels):
+        return [n.revertFeatures(y) for n, y in zip(self.l, labels)]
+
+
+class MultiNormalizerStandardize(_MultiNormalizer):
+    def _make(self, st):
+        return NormalizerStandardize(st.mean(), st.std().clamp_min(EPS))
+
+    def getFeatureMean(self, i):
+        return self.f[i].getMean()
+
+    def getFeatureStd(self, i):
+        return self.f[i].getStd()
+
+
+class MultiNormalizerMinMaxScaler(_MultiNormalizer):
+    def __init__(self, minRange=0.0, maxRange=1.0):
+        super().__init__()
+        self.lo, self.hi = float(minRange), float(maxRange)
+
+    def _make(self, st):
+        n = NormalizerMinMaxScaler(self.lo, self.hi)
+        n.fMin, n.fMax = st.mn, st.mx
+        return n
+
+    def getMin(self, i):
+        return self.f[i].getMin()
+
+    def getMax(self, i):
+        return self.f[i].getMax()
