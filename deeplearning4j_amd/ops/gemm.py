@@ -86,20 +86,21 @@ def _candidates(M, N, K, batch, default):
     return out
 
 
-def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False):
+def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False, zz=None):
     """First eager call of a problem shape: time every kernel configuration (tile shape x split-K; plus the library
-    GEMM when ``lib``) on a scratch destination and keep the fastest. Never runs while a HIP graph is being captured;
-    the cost-model plan is used there."""
+    GEMM when ``lib``) on a scratch destination and keep the fastest. ``zz``: the call's pre-activation buffer, so
+    every candidate is timed with its epilogue (a forward activation rewrites it, dgelu reads it). Never runs while a
+    HIP graph is being captured; the cost-model plan is used there."""
     from .timing import gpu_time
     tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
     best, best_t = default, None
     for cand in _candidates(M, N, K, batch, default) + ([LIB_CFG] if lib else []):
         if cand[1] > 1 and not splits_ok:
             continue
-        if launch(cand[0], cand[1], tmp, 0.0, None) != 0:
+        if launch(cand[0], cand[1], tmp, 0.0, zz) != 0:
             continue
         # GPU-side time (stream parked during the enqueue): small GEMMs are shorter than the host launch path
-        t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, None), reps=3, warmup=0)
+        t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, zz), reps=3, warmup=0)
         if best_t is None or t < best_t:
             best, best_t = cand, t
     return best
@@ -341,7 +342,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         libmm = None if (bias is not None and bias_in is None) else \
             _lib_gemm(a, b, c_t, swap, batched, bias_in, bias_dim, act, alpha, beta, z, out_dtype)
         if libmm is not None:
-            key = key + ("lib", bias_in is not None, beta != 0.0)
+            key = key + ("lib", bias_in is not None, beta != 0.0, act, z is not None)
             kern = launch
 
             def launch(cfg, sp, dst, bt, zz, ts=None):
@@ -353,7 +354,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
             if cfg is None:
                 cfg = _plan(lib, Mx, Nx, K, batch)
                 if _TUNE and not torch.cuda.is_current_stream_capturing():
-                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None)
+                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None, zz=z)
                     _TUNED[key] = cfg
         rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
     if rc == -1:
@@ -375,34 +376,65 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
 
 
 def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out_dtype):
-    """A launcher ``(dst, beta) -> 0`` running the product as one hipBLASLt call through torch on the current stream,
-    or None when the problem needs an in-tree epilogue (activation, pre-activation, a row bias, alpha != 1, fp32
-    output combined with a bias / beta / batch) or its destination is not a dense matrix."""
-    if not _LIB or act not in (None, "identity") or z is not None or alpha != 1.0 or \
-            a.dtype not in (torch.bfloat16, torch.float16) or b.dtype != a.dtype:
+    """A launcher ``(dst, beta) -> 0`` running the product as one hipBLASLt call through torch on the current stream
+    (plus, for an activation epilogue, one in-tree elementwise kernel over the result), or None when the problem needs
+    an epilogue only the in-tree GEMM has (a row bias, alpha != 1, beta with an activation, fp32 output combined with
+    a bias / beta / batch) or its destination is not a dense matrix.
+    Activations: ``act(z)`` with the pre-activation kept in ``z`` when given (the library writes z, the elementwise
+    kernel reads it); ``dgelu``: out = (a @ b) * gelu'(z), applied in place on the library result."""
+    if not _LIB or alpha != 1.0 or a.dtype not in (torch.bfloat16, torch.float16) or b.dtype != a.dtype:
+        return None
+    act = None if act == "identity" else act
+    if act not in (None, "relu", "tanh", "sigmoid", "gelu", "dgelu") or (act is not None and (beta != 0.0 or batched)):
+        return None
+    if (act == "dgelu" and z is None) or (z is not None and act is None):
         return None
     wide = out_dtype == torch.float32                   # 16-bit operands, fp32 result (weight gradients)
-    if out_dtype != a.dtype and not (wide and bias is None and beta == 0.0 and not batched):
+    if out_dtype != a.dtype and not (wide and bias is None and beta == 0.0 and not batched and act is None):
         return None
     if bias is not None and (bias.dtype != a.dtype or bias_dim != 1 or swap or batched or beta != 0.0):
         return None
     dstv = (lambda d: d.mT) if swap else (lambda d: d)                 # noqa: E731
-    if not dstv(c_t).is_contiguous():
+    if not dstv(c_t).is_contiguous() or (z is not None and not dstv(z).is_contiguous()):
         return None
     A_, B_ = (b.mT, a.mT) if swap else (a, b)
+    if act is not None:
+        from . import nd4j_kernels as NK
+        if not NK.ok(c_t):
+            return None
 
     def run(dst, bt):
         d = dstv(dst)
+        pre = dstv(z) if (z is not None and act != "dgelu") else d
         if wide:
             torch.mm(A_, B_, out_dtype=torch.float32, out=d)
         elif bias is not None:
-            torch.addmm(bias, A_, B_, out=d)
+            torch.addmm(bias, A_, B_, out=pre)
         elif bt == 0.0:
-            (torch.bmm if batched else torch.mm)(A_, B_, out=d)
+            (torch.bmm if batched else torch.mm)(A_, B_, out=pre)
         else:
             (d.baddbmm_ if batched else d.addmm_)(A_, B_, beta=bt)
+        if act == "dgelu":
+            r = native_gelu_(dstv(z), d)
+            if r != 0:
+                return r
+        elif act is not None:
+            if NK.transform(pre, act, out=d) is None:
+                return -1
         return 0
     return run
+
+
+def native_gelu_(z, dy):
+    """dy *= gelu'(z) in place on the in-tree GELU kernel (csrc/activations.hip); 0 or an error code."""
+    from .native import _stream
+    from . import transformer_native as TN
+    d = _DT.get(z.dtype)
+    if d is None or not (z.is_contiguous() and dy.is_contiguous()) or dy.dtype != z.dtype:
+        return -1
+    TN.native.register_sig("dl4j_gelu", [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_longlong,
+                                         _c.c_void_p])
+    return _lib().dl4j_gelu(d, _p(z), _p(dy), _p(dy), z.numel(), _c.c_void_p(_stream()))
 
 
 def linear(x, W, b=None, act=None, z=None, out_dtype=None):

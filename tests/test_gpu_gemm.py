@@ -242,11 +242,13 @@ def test_zero_padded_k_operand(K):
     _check(out2, _ref(a.t(), g), torch.bfloat16, M, f"kz^T K={K}")
 
 
-@pytest.mark.parametrize("case", ["plain", "bias_shadow", "beta", "colmajor", "batched", "fp32_out"])
+@pytest.mark.parametrize("case", ["plain", "bias_shadow", "beta", "colmajor", "batched", "fp32_out", "gelu_z",
+                                  "relu_colmajor", "dgelu"])
 def test_library_candidate(case, monkeypatch):
-    """The hipBLASLt candidate of the autotuner (forced here) computes the same product for every plain-GEMM form it
-    accepts: bias through the 16-bit shadow attached to an fp32 master, beta-accumulate, column-major destinations
-    (operands swapped) and 3-D batches; epilogue GEMMs (activation / fp32 output) never take it."""
+    """The hipBLASLt candidate of the autotuner (forced here) computes the same product for every form it accepts:
+    bias through the 16-bit shadow attached to an fp32 master, beta-accumulate, column-major destinations (operands
+    swapped), 3-D batches, fp32 weight-gradient output, and activation epilogues run as an in-tree elementwise kernel
+    after the library product (GELU with the pre-activation kept, ReLU, the GELU-backward product)."""
     torch.manual_seed(4)
     M, N, K = 384, 320, 256
     monkeypatch.setattr(gemm, "_FORCE_CFG", gemm.LIB_CFG)
@@ -268,13 +270,30 @@ def test_library_candidate(case, monkeypatch):
     elif case == "colmajor":
         out = torch.empty(N, M, device=DEV, dtype=torch.bfloat16).t()
         _check(gemm.mmul(a, b, out=out), _ref(a, b), torch.bfloat16, K, case)
+    elif case == "gelu_z":
+        master = torch.randn(N, device=DEV)
+        master._dl4j_shadow = master.to(torch.bfloat16)
+        z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        out = gemm.mmul(a, b, bias=master, act="gelu", z=z)
+        _check(z, _ref(a, b, bias=master._dl4j_shadow), torch.bfloat16, K, "gelu pre-activation")
+        _check(out, gemm._torch_act(z.float(), "gelu"), torch.bfloat16, 8, case)
+    elif case == "relu_colmajor":
+        out = torch.empty(N, M, device=DEV, dtype=torch.bfloat16).t()
+        _check(gemm.mmul(a, b, out=out, act="relu"), _ref(a, b, act="relu"), torch.bfloat16, K, case)
+    elif case == "dgelu":
+        z = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        out = gemm.mmul(a, b, act="dgelu", z=z)
+        _check(out, _ref(a, b) * gemm._dgelu_ref(z.float()), torch.bfloat16, K, case)
     else:
         a3 = torch.randn(3, M, K, device=DEV).to(torch.bfloat16)
         b3 = torch.randn(3, K, N, device=DEV).to(torch.bfloat16)
         out = gemm.mmul(a3, b3)
         ref = torch.stack([a3[i].float() @ b3[i].float() for i in range(3)])
         assert (out.float() - ref).abs().max() <= _tol(torch.bfloat16, K) * ref.abs().max()
-    assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV, dtype=torch.bfloat16), False, False, None, 1, "gelu",
-                          1.0, 0.0, None, torch.bfloat16) is None
+    c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert gemm._lib_gemm(a, b, c16, False, False, None, 1, "gelu", 1.0, 1.0, None, torch.bfloat16) is None
+    assert gemm._lib_gemm(a, b, c16, False, False, torch.zeros(M, device=DEV, dtype=torch.bfloat16), 0, None, 1.0,
+                          0.0, None, torch.bfloat16) is None      # row bias stays in-tree
+    assert gemm._lib_gemm(a, b, c16, False, False, None, 1, "dgelu", 1.0, 0.0, None, torch.bfloat16) is None
     assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV), False, False, None, 1, None, 1.0, 1.0, None,
                           torch.float32) is None          # fp32 output with beta-accumulate stays in-tree

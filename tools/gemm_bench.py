@@ -4,7 +4,10 @@ Random uniform [-1, 1) operands (zero-filled data reads high, guide §5.4 rule 2
 process (rule 24), median of the rounds. Prints one line per shape: TF/s of the in-tree kernels, of torch, their
 ratio, and of ``mmul``'s dispatch (the autotuner's pick between the in-tree configurations and the library GEMM,
 ops/gemm.py _lib_gemm) with its choice.
-Usage: python tools/gemm_bench.py [--dtype bf16|fp16] [--big]
+A second table times the BERT layer's epilogue call sites (bias from a 16-bit shadow, bias + GELU with the
+pre-activation kept, the GELU-backward product, beta-accumulate) through ``mmul``: in-tree fused epilogue vs
+dispatch (which may pick the library product + one in-tree elementwise kernel).
+Usage: python tools/gemm_bench.py [--dtype bf16|fp16] [--rounds R] [--only NAME] [--epilogues-only]
 """
 import argparse
 import os
@@ -63,8 +66,63 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--epilogues-only", action="store_true")
     args = ap.parse_args()
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    if not args.epilogues_only:
+        plain_table(args, dt)
+    epilogue_table(args, dt)
+
+
+EPILOGUES = [
+    # (name, M, N, K, kind)
+    ("qkv fwd +bias", 4096, 2304, 768, "bias"),
+    ("o fwd +bias", 4096, 768, 768, "bias"),
+    ("ffn1 fwd +bias+gelu(z)", 4096, 3072, 768, "gelu"),
+    ("ffn2 fwd +bias", 4096, 768, 3072, "bias"),
+    ("ffn2 dX *gelu'(z)", 4096, 3072, 768, "dgelu"),
+    ("ffn1 dX +=", 4096, 768, 3072, "beta"),
+]
+
+
+def epilogue_table(args, dt):
+    print(f"{'BERT epilogue site':26s} {'M':>6s} {'N':>6s} {'K':>6s}   fused TF/s  dispatch TF/s  speedup  pick")
+    for name, M, N, K, kind in EPILOGUES:
+        if args.only and args.only not in name:
+            continue
+        a = operand(M, K, True, dt)
+        b = operand(K, N, kind not in ("dgelu", "beta"), dt)       # backward: W^T views (K contiguous)
+        out = torch.empty(M, N, device="cuda", dtype=dt)
+        z = torch.empty(M, N, device="cuda", dtype=dt) if kind in ("gelu", "dgelu") else None
+        if z is not None:
+            z.copy_(torch.randn(M, N, device="cuda"))
+        bias = None
+        if kind in ("bias", "gelu"):
+            bias = torch.randn(N, device="cuda")
+            bias._dl4j_shadow = bias.to(dt)
+        kw = dict(out=out, bias=bias, z=z, act={"gelu": "gelu", "dgelu": "dgelu"}.get(kind),
+                  beta=1.0 if kind == "beta" else 0.0)
+        flop = 2.0 * M * N * K
+        reps = max(3, min(50, int(2e12 / flop)))
+
+        def fused():
+            gemm._LIB = False
+            try:
+                gemm.mmul(a, b, **kw)
+            finally:
+                gemm._LIB = True
+        tf, td = [], []
+        for _ in range(args.rounds):
+            tf.append(timeit(fused, reps))
+            td.append(timeit(lambda: gemm.mmul(a, b, **kw), reps))
+        t1, t2 = sorted(tf)[len(tf) // 2], sorted(td)[len(td) // 2]
+        picks = [v for k, v in gemm._TUNED.items() if k[:3] == (M, N, K) and "lib" in k]
+        pick = "lib" if picks and picks[-1] == gemm.LIB_CFG else (f"cfg{picks[-1][0]}x{picks[-1][1]}" if picks else "-")
+        print(f"{name:26s} {M:6d} {N:6d} {K:6d}   {flop / t1 / 1e9:10.1f}  {flop / t2 / 1e9:13.1f}  {t1 / t2:7.2f}"
+              f"  {pick}", flush=True)
+
+
+def plain_table(args, dt):
     print(f"{'shape':22s} {'M':>6s} {'N':>6s} {'K':>6s}   ours TF/s  torch TF/s  ratio  dispatch TF/s  pick")
     for name, M, N, K, la, lb in SHAPES:
         if args.only and args.only not in name:
