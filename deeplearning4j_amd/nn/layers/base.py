@@ -162,13 +162,8 @@ class LayerImpl:
 
 def matmul(a, b, bias=None, out_dtype=None, act=None, z=None):
     """``a @ b (+ bias)`` on the in-tree MFMA GEMM (ops/gemm.py); torch reference on CPU."""
-    from ...ops.gemm import mmul
-    if bias is not None:
-        sh = getattr(bias, "_dl4j_shadow", None)
-        bias = bias.reshape(-1)
-        if sh is not None:                      # keep the 16-bit copy reachable (a library GEMM's bias operand)
-            bias._dl4j_shadow = sh.reshape(-1)
-    return mmul(a, b, bias=bias, out_dtype=out_dtype, act=act, z=z)
+    from ...ops.gemm import bias_vec, mmul
+    return mmul(a, b, bias=bias_vec(bias), out_dtype=out_dtype, act=act, z=z)
 
 
 def weight_grad_(view, a, b):

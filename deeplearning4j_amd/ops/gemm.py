@@ -437,6 +437,18 @@ def native_gelu_(z, dy):
     return _lib().dl4j_gelu(d, _p(z), _p(dy), _p(dy), z.numel(), _c.c_void_p(_stream()))
 
 
+def bias_vec(b):
+    """``b`` as a 1-D bias that keeps its 16-bit shadow (``_dl4j_shadow``, the library GEMM's bias operand) — a plain
+    ``reshape(-1)`` returns a new tensor object without the attribute."""
+    if b is None:
+        return None
+    sh = getattr(b, "_dl4j_shadow", None)
+    v = b.reshape(-1)
+    if sh is not None and v is not b:
+        v._dl4j_shadow = sh.reshape(-1)
+    return v
+
+
 def linear(x, W, b=None, act=None, z=None, out_dtype=None):
     """x [M, K] @ W [K, N] + b — DL4J preOutput (BaseLayer.java:334-336) with a fused bias / activation epilogue."""
     return mmul(x, W, bias=b, act=act, z=z, out_dtype=out_dtype)

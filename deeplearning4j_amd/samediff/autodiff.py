@@ -190,7 +190,7 @@ register("activation")((_act_fwd, _act_bwd))
 
 # ----------------------------------------------------------------------------------------------- linear algebra
 def _mm(a, b, out_dtype=None):
-    from ..ops.gemm import mmul
+    from ..ops.gemm import bias_vec, mmul
     if a.dim() <= 3 and b.dim() <= 3 and a.dim() >= 2 and b.dim() >= 2:
         return mmul(a, b, out_dtype=out_dtype)
     return torch.matmul(a, b)
@@ -231,8 +231,8 @@ def _linear_fwd(ins, at):
     """y = act(x . w + b); attr ``act`` ("gelu", set by SameDiff's fusion pass for linear -> gelu) runs the
     activation in the GEMM epilogue and keeps the pre-activation for the backward."""
     x, w, b = ins
-    from ..ops.gemm import mmul
-    bias = None if b is None else master(b).reshape(-1)
+    from ..ops.gemm import bias_vec, mmul
+    bias = None if b is None else bias_vec(master(b))
     act = at.get("act")
     if act is None:
         return mmul(x, w, bias=bias), None
@@ -521,7 +521,7 @@ def _lstm_native_grads(dz, xt, out, gates, call, h0, c0, x, W, RW, b, H, peephol
     gradient sinks (input positions base+1..base+3); dx only when the input needs a gradient. None when the glue
     does not take this dtype (the caller's generic path runs)."""
     from ..ops import rnn_native
-    from ..ops.gemm import mmul
+    from ..ops.gemm import bias_vec, mmul
     prep = rnn_native.lstm_bwd_prep(dz, out, h0, call, c0, peephole, W.dtype)
     if prep is None:
         return None
@@ -547,12 +547,12 @@ def _lstm_fwd(ins, at):
     mb, nIn, T = x.shape
     H = RW.shape[0]
     dt = W.dtype
-    from ..ops.gemm import mmul
+    from ..ops.gemm import bias_vec, mmul
     from ..ops import rnn_native
     if x.is_cuda and rnn_native.supported(H, dt) and ops.use_native(x, "lstm"):
         from ..nn.layers.recurrent import _time_major_rows
         xt = _time_major_rows(x, dt)                      # one cast/permute/pad launch, a GEMM operand in place
-        zx = mmul(xt, W, bias=master(b).reshape(-1)).reshape(T, mb, 4 * H)
+        zx = mmul(xt, W, bias=bias_vec(master(b))).reshape(T, mb, 4 * H)
         packs = rnn_native.pack_rw(RW, H, peephole)       # both packed images in one launch, reused by backward
         out, hT, cT, gates, call, o16 = rnn_native.lstm_seq_fwd(zx, RW, H, peephole, h0, c0, None, True, packs=packs,
                                                                 out16=x.dtype == dt)
@@ -590,7 +590,7 @@ def _lstm_bwd(ctx, g, ins, at):
     peephole = at.get("peephole", False)
     mb, nIn, T = x.shape
     H = RW.shape[0]
-    from ..ops.gemm import mmul
+    from ..ops.gemm import bias_vec, mmul
     if ctx[0] == "native":
         from ..ops import rnn_native
         _, xt, zx, out, gates, call, packs = ctx
@@ -670,9 +670,9 @@ def _lstm2_fwd(ins, at):
     if x.is_cuda and x.dtype == dt and ops.use_native(x, "lstm") and rnn_native.stack2_supported(H, dt, T) and \
             RW2.shape[0] == H and tuple(W2.shape) == (H, 4 * H) and W2.dtype == dt:
         from ..nn.layers.recurrent import _time_major_rows
-        from ..ops.gemm import mmul
+        from ..ops.gemm import bias_vec, mmul
         xt = _time_major_rows(x, dt)
-        zx1 = mmul(xt, W1, bias=master(b1).reshape(-1)).reshape(T, mb, 4 * H)
+        zx1 = mmul(xt, W1, bias=bias_vec(master(b1))).reshape(T, mb, 4 * H)
         p1, p2 = rnn_native.pack_rw(RW1, H, peephole), rnn_native.pack_rw(RW2, H, peephole)
         pw = rnn_native.pack_rw(W2, H, False)
         r = None
