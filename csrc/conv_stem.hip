@@ -191,7 +191,8 @@ DL4J_API int dl4j_stem_conv_fwd(const void* x, const void* wpk, void* y, float* 
 // Wave w owns k-tiles 3w..3w+2 for all 4 co-tiles (12 accumulators). Each (persistent) workgroup writes its partial
 // [64][192] sums (and the bias column sums) to a workspace; stem_wrw_reduce sums the partials in a fixed order
 // (deterministic) straight into the DL4J [64][3][7][7] fp32 gradient.
-__global__ void __launch_bounds__(256, 2) stem_conv_wrw(const u16* __restrict__ x, const u16* __restrict__ dy,
+constexpr int kWrwWgPerCu = 3;   // persistent weight-gradient workgroups per CU (LDS ~46 KB, 158 VGPRs: 3 fit)
+__global__ void __launch_bounds__(256, kWrwWgPerCu) stem_conv_wrw(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                         float* __restrict__ part, float* __restrict__ part_db, int N,
                                                         int H, int W, int OH, int OW, int RS) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -248,30 +249,28 @@ __global__ void __launch_bounds__(256, 2) stem_conv_wrw(const u16* __restrict__ 
       if (i < nchunks) *reinterpret_cast<uint2*>(xin + rr * RS + 12 + 4 * j) = pre[q];
     }
     const long long m_base = ((long long)n * OH + oh0) * OW;
-    // dy of round 0 in flight
-    uint4 g[2];
+    // dy rounds two ahead (register sets gA / gB alternate): with three workgroups per CU this keeps enough dy in
+    // flight to cover the HBM latency (one round of look-ahead with two workgroups per CU ran at ~2 TB/s)
+    auto load_dy = [&](int rnd, uint4* dst) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) g[j] = *reinterpret_cast<const uint4*>(dy + (m_base + (threadIdx.x >> 3) + 32 * j) * 64 +
-                                                                       (threadIdx.x & 7) * 8);
-    for (int rnd = 0; rnd < rounds; ++rnd) {
+      for (int j = 0; j < 2; ++j)
+        dst[j] = *reinterpret_cast<const uint4*>(dy + (m_base + rnd * 64 + (threadIdx.x >> 3) + 32 * j) * 64 +
+                                                 (threadIdx.x & 7) * 8);
+    };
+    auto round = [&](int rnd, uint4* gr) {
       u16* dt = dyt + (rnd & 1) * 64 * OUT_LD;
       // ---- transpose this round's dy tile into dyT[c][px]; bias column sums on the way
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int px = (threadIdx.x >> 3) + 32 * j, c8 = threadIdx.x & 7;
-        const u16* hv = reinterpret_cast<const u16*>(&g[j]);
+        const u16* hv = reinterpret_cast<const u16*>(&gr[j]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           dt[(c8 * 8 + i) * OUT_LD + px] = hv[i];
           dbacc[i] += bf2f(hv[i]);
         }
       }
-      if (rnd + 1 < rounds) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          g[j] = *reinterpret_cast<const uint4*>(dy + (m_base + (rnd + 1) * 64 + (threadIdx.x >> 3) + 32 * j) * 64 +
-                                                 (threadIdx.x & 7) * 8);
-      }
+      if (rnd + 2 < rounds) load_dy(rnd + 2, gr);
       __syncthreads();
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
@@ -298,6 +297,13 @@ __global__ void __launch_bounds__(256, 2) stem_conv_wrw(const u16* __restrict__ 
             acc[ct][t3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[t3], acc[ct][t3], 0, 0, 0);
         }
       }
+    };
+    uint4 gA[2], gB[2];
+    load_dy(0, gA);
+    if (rounds > 1) load_dy(1, gB);
+    for (int rnd = 0; rnd < rounds; rnd += 2) {
+      round(rnd, gA);
+      if (rnd + 1 < rounds) round(rnd + 1, gB);
     }
   }
   // ---- partial dW: lane holds C[co = ct*16 + 4*hg + j][k = (3*wave + t3)*16 + col]
@@ -360,7 +366,7 @@ DL4J_API long long dl4j_stem_wrw_workspace_floats(int N, int OH) {
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const long long G = 2LL * ncu;
+  const long long G = (long long)kWrwWgPerCu * ncu;
   return G * (64 * 192 + 64);
 }
 
@@ -381,7 +387,7 @@ DL4J_API int dl4j_stem_conv_wrw(const void* x, const void* dy, float* dW, float*
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int nblocks = N * (OH / ROWS_PER_WG);
-  const int G = nblocks < 2 * ncu ? nblocks : 2 * ncu;
+  const int G = nblocks < kWrwWgPerCu * ncu ? nblocks : kWrwWgPerCu * ncu;   // == the workspace's partial count
   float* part = ws;
   float* part_db = ws + (long long)G * 64 * 192;
   hipLaunchKernelGGL(stem_conv_wrw, dim3(G), dim3(256), lds, s, (const u16*)x, (const u16*)dy, part, part_db, N, H, W,

@@ -418,6 +418,10 @@ def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out
             r = native_gelu_(dstv(z), d)
             if r != 0:
                 return r
+        elif act == "gelu":                     # the vectorized GELU kernel (the generic transform is ~3x slower)
+            r = native_gelu_(pre, None, out=d)
+            if r != 0:
+                return r
         elif act is not None:
             if NK.transform(pre, act, out=d) is None:
                 return -1
@@ -425,16 +429,18 @@ def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out
     return run
 
 
-def native_gelu_(z, dy):
-    """dy *= gelu'(z) in place on the in-tree GELU kernel (csrc/activations.hip); 0 or an error code."""
+def native_gelu_(z, dy, out=None):
+    """On the in-tree GELU kernel (csrc/activations.hip): dy *= gelu'(z) in place, or with dy None out = gelu(z);
+    0 or an error code."""
     from .native import _stream
     from . import transformer_native as TN
     d = _DT.get(z.dtype)
-    if d is None or not (z.is_contiguous() and dy.is_contiguous()) or dy.dtype != z.dtype:
+    dst = dy if dy is not None else out
+    if d is None or not (z.is_contiguous() and dst.is_contiguous()) or dst.dtype != z.dtype:
         return -1
     TN.native.register_sig("dl4j_gelu", [_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_longlong,
                                          _c.c_void_p])
-    return _lib().dl4j_gelu(d, _p(z), _p(dy), _p(dy), z.numel(), _c.c_void_p(_stream()))
+    return _lib().dl4j_gelu(d, _p(z), _p(dy), _p(dst), z.numel(), _c.c_void_p(_stream()))
 
 
 def bias_vec(b):
