@@ -1152,20 +1152,6 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x
   T* sdy = reinterpret_cast<T*>(smem);                                        // [maxrows][OW*C]
   unsigned char* sam = smem + (size_t)maxrows * OW * C * sizeof(T);           // [maxrows][OW*C]
   const int row_elems = OW * C;
-  const int items = min(RB, H - ih0) * W * CG;
-  auto item_t = [&](int it) -> long long {
-    const int cg = it % CG, q1 = it / CG, iw = q1 % W, ih = ih0 + q1 / W;
-    return (((long long)n * H + ih) * W + iw) * CG + cg;
-  };
-  // x of this thread's first PER items is loaded before the LDS staging (it does not depend on it), so its HBM
-  // latency overlaps the staging's; later chunks load all PER items before computing any of them
-  constexpr int PER = 8;
-  RawVec8<T> xr[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int it = threadIdx.x + k * 256;
-    if (it < items) xr[k].load(x + item_t(it) * 8);
-  }
   if (nrows > 0) {
     const long long g0 = ((long long)n * OH + oh_lo) * row_elems;
     const int nv = nrows * row_elems / 8;                  // 8-element vectors
@@ -1180,6 +1166,7 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x
     }
   }
   __syncthreads();
+  const int items = min(RB, H - ih0) * W * CG;
   // a thread keeps one channel group across its items when CG divides the block size: BN factors in registers
   // (dx = A*acc - B*x - Cq, see bn_bwd_elem) instead of 40 L1 parameter loads per 8-channel item
   const bool fixed = (256 % CG) == 0;
@@ -1193,60 +1180,46 @@ __global__ __launch_bounds__(256) void bnpool_bwd_dx_lds(const T* __restrict__ x
       Cq[i] = ctx[2 * C + c] * (cdb[c] - ctx[c] * ctx[C + c] * cdg[c]);
     }
   }
-  for (int base = 0; base < items; base += PER * 256) {
-    if (base > 0) {
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int cg = it % CG, q1 = it / CG, iw = q1 % W, ih = ih0 + q1 / W;
+    const int hp = ih + pt, wp = iw + pl;
+    int oh0 = hp - kh + 1;
+    oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
+    int ow0 = wp - kw + 1;
+    ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
+    const int oh1 = min(hp / sh, OH - 1), ow1 = min(wp / sw, OW - 1);
+    const long long t = (((long long)n * H + ih) * W + iw) * CG + cg;
+    float xv[8], acc[8];
+    Vec8<T>::load(x + t * 8, xv);
 #pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int it = base + threadIdx.x + k * 256;
-        if (it < items) xr[k].load(x + item_t(it) * 8);
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh0 + a, ow = ow0 + b;
+        if (oh > oh1 || ow > ow1) continue;
+        const int o = ((oh - oh_lo) * OW + ow) * C + cg * 8;
+        float g[8];
+        Vec8<T>::load(sdy + o, g);
+        const unsigned long long pk = *reinterpret_cast<const unsigned long long*>(sam + o);
+        const unsigned me = 0x80u | (unsigned)((hp - oh * sh) * kw + (wp - ow * sw));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (((pk >> (8 * i)) & 0xff) == me) acc[i] += g[i];
       }
-    }
+    if (fixed) {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int it = base + threadIdx.x + k * 256;
-      if (it >= items) break;
-      const int cg = it % CG, q1 = it / CG, iw = q1 % W, ih = ih0 + q1 / W;
-      const int hp = ih + pt, wp = iw + pl;
-      int oh0 = hp - kh + 1;
-      oh0 = oh0 <= 0 ? 0 : (oh0 + sh - 1) / sh;
-      int ow0 = wp - kw + 1;
-      ow0 = ow0 <= 0 ? 0 : (ow0 + sw - 1) / sw;
-      const int oh1 = min(hp / sh, OH - 1), ow1 = min(wp / sw, OW - 1);
-      const long long t = (((long long)n * H + ih) * W + iw) * CG + cg;
-      float xv[8], acc[8];
+      for (int i = 0; i < 8; ++i) xv[i] = A[i] * acc[i] - B[i] * xv[i] - Cq[i];
+    } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        xv[i] = xr[k].get(i);
-        acc[i] = 0.f;
+        const int c = cg * 8 + i;
+        const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
+        xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
       }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int oh = oh0 + a, ow = ow0 + b;
-          if (oh > oh1 || ow > ow1) continue;
-          const int o = ((oh - oh_lo) * OW + ow) * C + cg * 8;
-          float g[8];
-          Vec8<T>::load(sdy + o, g);
-          const unsigned long long pk = *reinterpret_cast<const unsigned long long*>(sam + o);
-          const unsigned me = 0x80u | (unsigned)((hp - oh * sh) * kw + (wp - ow * sw));
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (((pk >> (8 * i)) & 0xff) == me) acc[i] += g[i];
-        }
-      if (fixed) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) xv[i] = A[i] * acc[i] - B[i] * xv[i] - Cq[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int c = cg * 8 + i;
-          const float xhat = (xv[i] - ctx[c]) * ctx[C + c];
-          xv[i] = ctx[2 * C + c] * (acc[i] - cdb[c] - xhat * cdg[c]);
-        }
-      }
-      Vec8<T>::store(dx + t * 8, xv);
     }
+    Vec8<T>::store(dx + t * 8, xv);
   }
 }
 

@@ -266,7 +266,9 @@ __global__ void __launch_bounds__(256, kWrwWgPerCu) stem_conv_wrw(const u16* __r
         const u16* hv = reinterpret_cast<const u16*>(&gr[j]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          dt[(c8 * 8 + i) * OUT_LD + px] = hv[i];
+          // 16-byte pixel chunks of channel row c8*8+i are XOR-swizzled by c8 (rows 8 apart are 1152 B apart, i.e.
+          // the same bank: unswizzled, the 8 channel groups of a wave's store hit one bank 8 ways)
+          dt[(c8 * 8 + i) * OUT_LD + (((px >> 3) ^ c8) << 3) + (px & 7)] = hv[i];
           dbacc[i] += bf2f(hv[i]);
         }
       }
@@ -291,7 +293,9 @@ __global__ void __launch_bounds__(256, kWrwWgPerCu) stem_conv_wrw(const u16* __r
         }
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
-          const bf16x8s_t a = *reinterpret_cast<const bf16x8s_t*>(dt + (ct * 16 + col) * OUT_LD + ch * 32 + 8 * hg);
+          const int row = ct * 16 + col;
+          const bf16x8s_t a =
+              *reinterpret_cast<const bf16x8s_t*>(dt + row * OUT_LD + (((ch * 4 + hg) ^ (row >> 3)) << 3));
 #pragma unroll
           for (int t3 = 0; t3 < 3; ++t3)
             acc[ct][t3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[t3], acc[ct][t3], 0, 0, 0);
