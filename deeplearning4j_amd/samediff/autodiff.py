@@ -234,14 +234,19 @@ def _linear_fwd(ins, at):
     from ..ops.gemm import bias_vec, mmul
     bias = None if b is None else bias_vec(master(b))
     act = at.get("act")
+    lead = x.shape[:-1]
+    if x.dim() > 2 and w.dim() == 2:
+        # [.., K] activations as one [rows, K] GEMM (not a batched one: a plain 2-D product can also take the library
+        # candidate, and one launch covers every row)
+        x = x.reshape(-1, x.shape[-1])
     if act is None:
-        return mmul(x, w, bias=bias), None
+        return mmul(x, w, bias=bias).reshape(lead + (w.shape[-1],)), None
     if x.is_cuda:
         z = torch.empty(x.shape[:-1] + (w.shape[1],), dtype=x.dtype, device=x.device)
         y = mmul(x, w, bias=bias, act=act, z=z)
-        return y, z
+        return y.reshape(lead + (w.shape[-1],)), z.reshape(lead + (w.shape[-1],))
     z = mmul(x, w, bias=bias)
-    return _gelu(z), z
+    return _gelu(z).reshape(lead + (w.shape[-1],)), z.reshape(lead + (w.shape[-1],))
 
 
 def _linear_bwd(ctx, g, ins, at):
