@@ -17,6 +17,10 @@ import zipfile
 
 import torch
 
+# reverse pass: a linear's input gradient is summed into the partial gradient other consumers already produced by the
+# GEMM itself (beta = 1), instead of a separate add (DL4J_AMD_SD_ACC=0 turns it off for A/B checks)
+_ACC_FUSE = os.environ.get("DL4J_AMD_SD_ACC", "1") == "1"
+
 from .autodiff import REGISTRY
 
 
@@ -482,6 +486,11 @@ class SameDiff:
             for name in wrt:                    # read by no op on the path to the targets: final (None) now
                 if name not in final_at:
                     on_final(name, grads.get(name))
+        produced_at = {rec[0]: k for k, rec in enumerate(recs)}
+
+        def _sp(t):
+            return t.untyped_storage().data_ptr() if torch.is_tensor(t) else None
+        seed_ptrs = {_sp(t) for t in seeds.values()}
         for i in range(len(recs) - 1, -1, -1):
             out, op, refs, attrs = recs[i]
             g = grads.get(out)
@@ -489,19 +498,34 @@ class SameDiff:
                 ins = [self._val(r) for r in refs]
                 sk = {j: sinks[r] for j, r in enumerate(refs) if isinstance(r, str) and r in sinks} if sinks else None
                 fz = dsum_for.get(i)
+                acc = None
+                if _ACC_FUSE and op == "linear" and isinstance(refs[0], str) and refs[0] not in wrt:
+                    prev = grads.get(refs[0])
+                    # in place only when no seed and no other pending gradient (a name whose producing op is still to
+                    # come, or a returned one) shares its storage
+                    if prev is not None and torch.is_tensor(prev) and _sp(prev) not in seed_ptrs and not any(
+                            n != refs[0] and produced_at.get(n, -1) < i and _sp(t) == _sp(prev)
+                            for n, t in grads.items()):
+                        acc = {0: prev}
                 _ad.set_sinks(sk, done=presunk.get(i), dsum=None if fz is None else sinks[fz[1]],
-                              nograd={j for j, r in enumerate(refs) if isinstance(r, str) and r in frozen})
+                              nograd={j for j, r in enumerate(refs) if isinstance(r, str) and r in frozen}, acc=acc)
                 try:
                     gins = REGISTRY[op].bwd(self._ctx[out], g, ins, attrs)
                     if fz is not None and _ad.dsum_written():
                         presunk[fz[0]] = {2}        # the producing linear's bias gradient is already in its sink
+                    used = set(_ad.acc_used())
                 finally:
                     _ad.set_sinks(None)
-                for r, gi in zip(refs, gins):
+                for j, (r, gi) in enumerate(zip(refs, gins)):
                     if gi is None or not isinstance(r, str):
                         continue
                     prev = grads.get(r)
-                    grads[r] = gi if prev is None else prev + gi
+                    if j in used:
+                        grads[r] = gi                # the backward already summed into prev (gi is prev)
+                    elif prev is None:
+                        grads[r] = gi
+                    else:
+                        grads[r] = prev + gi
             if on_final is not None:
                 for name in by_pos.get(i, ()):
                     on_final(name, grads.get(name))

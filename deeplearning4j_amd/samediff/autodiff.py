@@ -22,16 +22,33 @@ REGISTRY = {}
 _TLS = threading.local()
 
 
-def set_sinks(sinks, done=None, dsum=None, nograd=None):
+def set_sinks(sinks, done=None, dsum=None, nograd=None, acc=None):
     """Gradient destinations of the op whose backward runs next: {input position: contiguous fp32 tensor shaped like
     that input} (SameDiff._backward sets them for variables only this op reads). ``done``: input positions whose
     sink an earlier backward already filled; ``dsum``: an fp32 sink for the column sums of this LayerNorm's input
-    gradient (the producing linear's bias gradient)."""
+    gradient (the producing linear's bias gradient). ``acc``: {input position: the partial gradient other consumers
+    already produced} that the backward may accumulate into in place (then it reports it with ``acc_used``)."""
     _TLS.sinks = sinks
     _TLS.done = done
     _TLS.dsum = dsum
     _TLS.dsum_written = False
     _TLS.nograd = nograd
+    _TLS.acc = acc
+    _TLS.acc_used = set()
+
+
+def acc_target(i):
+    """The partial gradient of input ``i`` this backward may add its contribution into (in place), or None."""
+    a = getattr(_TLS, "acc", None)
+    return None if not a else a.get(i)
+
+
+def mark_acc_used(i):
+    _TLS.acc_used.add(i)
+
+
+def acc_used():
+    return getattr(_TLS, "acc_used", set())
 
 
 def need_grad(i):
@@ -255,7 +272,15 @@ def _linear_bwd(ctx, g, ins, at):
         g = _gelu(ctx, g.to(ctx.dtype))
     g2 = g.to(x.dtype).reshape(-1, g.shape[-1])
     x2 = x.reshape(-1, x.shape[-1])
-    dx = _mm(g2, w.t()).reshape(x.shape)
+    acc = acc_target(0)
+    if acc is not None and acc.dtype == x.dtype and acc.shape == x.shape and acc.is_contiguous() and x.is_cuda:
+        # the residual branch's gradient is already there: dx summed into it by the GEMM (beta = 1), no add launch
+        from ..ops.gemm import mmul
+        mmul(g2, w.t(), out=acc.view(-1, acc.shape[-1]), beta=1.0)
+        mark_acc_used(0)
+        dx = acc
+    else:
+        dx = _mm(g2, w.t()).reshape(x.shape)
     sw, sb = grad_sink(1), grad_sink(2)
     if sw is not None and x.is_cuda and w.dim() == 2:
         from ..ops.gemm import mmul

@@ -161,3 +161,36 @@ def test_samediff_gradient_sinks_and_master_views(cuda, monkeypatch):
     assert all(abs(a - b) < 1e-2 * max(1.0, abs(a)) for a, b in zip(l0, l1)), (l0, l1)
     assert _rel(g1, g0) < 1e-2, _rel(g1, g0)          # bias sums from fp32 (LN kernel) vs bf16 (channel sum) rows
     assert torch.allclose(p0, p1, atol=5e-3), (p0 - p1).abs().max()
+
+
+def test_samediff_residual_gradient_accumulated_in_gemm(cuda, monkeypatch):
+    """A variable read by a linear op and by a residual add: with the reverse pass summing the linear's input gradient
+    into the residual branch's partial gradient inside the GEMM (beta = 1), the gradients equal the unfused pass
+    (separate add) and the fp64 CPU reference."""
+    import deeplearning4j_amd.samediff as S
+    g = torch.Generator().manual_seed(5)
+    B, T, E = 2, 64, 128
+    base = {"x": torch.randn(B, T, E, generator=g), "w0": torch.randn(E, E, generator=g) * E ** -0.5,
+            "b0": 0.02 * torch.randn(E, generator=g), "wqkv": torch.randn(E, 3 * E, generator=g) * E ** -0.5,
+            "bqkv": 0.02 * torch.randn(3 * E, generator=g), "wo": torch.randn(E, E, generator=g) * E ** -0.5,
+            "bo": torch.zeros(E), "lg": 1 + 0.1 * torch.randn(E, generator=g), "lb": 0.1 * torch.randn(E, generator=g)}
+
+    def run(dev, dt, fuse):
+        monkeypatch.setattr(S, "_ACC_FUSE", fuse)
+        sd = SameDiff.create()
+        x = sd.placeHolder("x", base["x"].to(dev, dt))
+        v = {k: sd.var(k, base[k].to(dev, dt)) for k in base if k != "x"}
+        h0 = sd.nn().linear(x, v["w0"], v["b0"])
+        qkv = sd.nn().linear(h0, v["wqkv"], v["bqkv"])
+        a = sd.nn().fusedSelfAttention(qkv, 2)
+        h = sd.nn().layerNorm(sd.nn().linear(a, v["wo"], v["bo"]).add(h0), v["lg"], v["lb"])
+        sd.setLossVariables(h.mul(h).sum())
+        names = [k for k in base if k != "x"]
+        grads = sd.calculateGradients({}, *names)
+        return {k: grads[k].float().cpu() for k in names}
+    on = run(cuda, torch.float32, True)
+    off = run(cuda, torch.float32, False)
+    ref = run(torch.device("cpu"), torch.float64, True)
+    for k in on:
+        assert _rel(on[k], off[k]) < 1e-5, (k, _rel(on[k], off[k]))
+        assert _rel(on[k], ref[k]) < 1e-3, (k, _rel(on[k], ref[k]))
