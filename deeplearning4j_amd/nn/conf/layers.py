@@ -134,7 +134,10 @@ class Layer(Config):
                 setattr(self, k, conv(_c.deepcopy(v)) if conv else _c.deepcopy(v))
 
     def instantiate(self, **kw):
-        mod, cls = self.RUNTIME.split(":")
+        rt = self.RUNTIME
+        if not isinstance(rt, str):               # a user layer may name its runtime class directly
+            return rt(self, **kw)
+        mod, cls = rt.split(":")
         return getattr(importlib.import_module(mod), cls)(self, **kw)
 
     def getLayerName(self):
