@@ -283,7 +283,24 @@ _NET_KEYS = ("seed", "optimizationAlgo", "miniBatch", "maxNumLineSearchIteration
              "trainingWorkspaceMode", "inferenceWorkspaceMode", "cacheMode", "dataType")
 
 
-class MultiLayerConfiguration(Config):
+class _Counters:
+    """Training-progress counters kept in the configuration (reference MultiLayerConfiguration /
+    ComputationGraphConfiguration iterationCount / epochCount, serialised with it)."""
+
+    def getIterationCount(self):
+        return self.iterationCount
+
+    def setIterationCount(self, n):
+        self.iterationCount = int(n)
+
+    def getEpochCount(self):
+        return self.epochCount
+
+    def setEpochCount(self, n):
+        self.epochCount = int(n)
+
+
+class MultiLayerConfiguration(_Counters, Config):
     FIELDS = {"confs": [], "inputPreProcessors": {}, "backprop": True, "pretrain": False,
               "backpropType": BackpropType.Standard, "tbpttFwdLength": 20, "tbpttBackLength": 20,
               "globalConf": {}, "iterationCount": 0, "epochCount": 0, "inputType": None}
@@ -452,7 +469,7 @@ class GraphBuilder:
         return conf
 
 
-class ComputationGraphConfiguration(Config):
+class ComputationGraphConfiguration(_Counters, Config):
     FIELDS = {"vertices": {}, "vertexInputs": {}, "networkInputs": [], "networkOutputs": [], "backprop": True,
               "pretrain": False, "backpropType": BackpropType.Standard, "tbpttFwdLength": 20,
               "tbpttBackLength": 20, "globalConf": {}, "iterationCount": 0, "epochCount": 0, "inputTypes": None}

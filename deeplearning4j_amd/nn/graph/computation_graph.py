@@ -696,6 +696,9 @@ class ComputationGraph(BaseNetwork):
         self.labels = list(y)
 
     def setLearningRate(self, lr, layerName=None):
+        """setLearningRate(newLr), or setLearningRate(layerName, newLr) as in the reference."""
+        if isinstance(lr, str):
+            lr, layerName = layerName, lr
         self.updater.setLearningRate(lr, layerName)
 
     def save(self, path, saveUpdater=True):

@@ -420,6 +420,10 @@ class MultiLayerNetwork(BaseNetwork):
         return net
 
     def setLearningRate(self, lr, layer=None):
+        """setLearningRate(newLr) for every layer, or setLearningRate(layerNumber, newLr) as in the reference
+        (MultiLayerNetwork.java setLearningRate(int, double)); ``layer=`` may also name the layer."""
+        if layer is not None and isinstance(lr, int) and not isinstance(layer, (int, str)):
+            lr, layer = layer, lr
         name = None
         if layer is not None:
             name = self.conf.confs[layer].layerName if isinstance(layer, int) else layer
