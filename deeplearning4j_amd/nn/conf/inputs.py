@@ -30,6 +30,25 @@ class InputType(Config):
         return InputTypeConvolutionalFlat(height=int(height), width=int(width), depth=int(depth))
 
     @staticmethod
+    def inferInputType(arr):
+        """The InputType of one activation array (reference InputType.inferInputType): [mb, n] feed-forward,
+        [mb, n, T] recurrent, [mb, c, h, w] convolutional."""
+        shp = tuple(arr.shape)
+        if len(shp) == 2:
+            return InputType.feedForward(shp[1])
+        if len(shp) == 3:
+            return InputType.recurrent(shp[1], shp[2])
+        if len(shp) == 4:
+            return InputType.convolutional(shp[2], shp[3], shp[1])
+        if len(shp) == 5:
+            return InputType.convolutional3D(shp[2], shp[3], shp[4], shp[1])
+        raise ValueError(f"cannot infer an InputType for an array of rank {len(shp)}")
+
+    @staticmethod
+    def inferInputTypes(arrays):
+        return [InputType.inferInputType(a) for a in arrays]
+
+    @staticmethod
     def convolutional3D(depth, height, width, channels):
         return InputTypeConvolutional3D(depth=int(depth), height=int(height), width=int(width),
                                         channels=int(channels))

@@ -47,6 +47,48 @@ class MemoryReport:
     def getMemoryBytes(self, memoryType, minibatchSize, memoryUseMode, cacheMode=None, dataType="FLOAT"):
         raise NotImplementedError
 
+    # ---- JSON / YAML (reference MemoryReport.toJson / toYaml / fromJson / fromYaml)
+    def to_dict(self):
+        raise NotImplementedError
+
+    def toJson(self):
+        import json
+        return json.dumps(self.to_dict(), indent=2)
+
+    def toYaml(self):
+        import yaml
+        return yaml.safe_dump(self.to_dict(), sort_keys=False)
+
+    @staticmethod
+    def from_dict(d):
+        cls = {"LayerMemoryReport": LayerMemoryReport, "NetworkMemoryReport": NetworkMemoryReport}[d["@class"]]
+        return cls._from(d)
+
+    @staticmethod
+    def fromJson(s):
+        import json
+        return MemoryReport.from_dict(json.loads(s))
+
+    @staticmethod
+    def fromYaml(s):
+        import yaml
+        return MemoryReport.from_dict(yaml.safe_load(s))
+
+    def __eq__(self, other):
+        return isinstance(other, MemoryReport) and type(other) is type(self) and self.to_dict() == other.to_dict()
+
+    def __hash__(self):
+        return hash(self.toJson())
+
+
+def _it_dict(t):
+    return None if t is None else t.to_dict()
+
+
+def _it_from(d):
+    from .base import _decode
+    return None if d is None else _decode(d)
+
 
 class LayerMemoryReport(MemoryReport):
     def __init__(self, layerName, layerType, inputType, outputType, parameterSize=0, updaterStateSize=0,
@@ -64,6 +106,22 @@ class LayerMemoryReport(MemoryReport):
 
     def getName(self):
         return self.layerName
+
+    _KEYS = ("parameterSize", "updaterStateSize", "wFixInf", "wVarInf", "wFixTrain", "wVarTrain", "cacheFixed",
+             "cacheVarPerEx")
+
+    def to_dict(self):
+        d = {"@class": "LayerMemoryReport", "layerName": self.layerName, "layerType": self.layerType,
+             "inputType": _it_dict(self.inputType), "outputType": _it_dict(self.outputType)}
+        d.update({k: getattr(self, k) for k in self._KEYS})
+        return d
+
+    @classmethod
+    def _from(cls, d):
+        r = cls(d["layerName"], d["layerType"], _it_from(d["inputType"]), _it_from(d["outputType"]))
+        for k in cls._KEYS:
+            setattr(r, k, int(d[k]))
+        return r
 
     def getMemoryBytes(self, memoryType, minibatchSize, memoryUseMode, cacheMode=None, dataType="FLOAT"):
         b = bytes_per_element(dataType)
@@ -109,6 +167,20 @@ class NetworkMemoryReport(MemoryReport):
 
     def getName(self):
         return self.modelName
+
+    def to_dict(self):
+        nit = self.networkInputTypes
+        nit = [_it_dict(t) for t in nit] if isinstance(nit, (list, tuple)) else _it_dict(nit)
+        return {"@class": "NetworkMemoryReport", "modelClass": self.modelClass, "modelName": self.modelName,
+                "networkInputTypes": nit,
+                "layerAndVertexReports": [[n, r.to_dict()] for n, r in self.layerAndVertexReports.items()]}
+
+    @classmethod
+    def _from(cls, d):
+        nit = d["networkInputTypes"]
+        nit = [_it_from(t) for t in nit] if isinstance(nit, list) else _it_from(nit)
+        reps = {n: MemoryReport.from_dict(r) for n, r in d["layerAndVertexReports"]}
+        return cls(reps, d["modelClass"], d["modelName"], nit)
 
     def getTotalMemoryBytes(self, minibatchSize, memoryUseMode, cacheMode=None, dataType="FLOAT"):
         total, best = 0, (0, 0)

@@ -365,6 +365,13 @@ class GraphBuilder:
         self._fwd = 20
         self._back = 20
         self._order = []
+        self._allowDisconnected = False
+
+    def allowDisconnected(self, b=True):
+        """Permit inputs / vertices from which no network output is reachable (reference
+        GraphBuilder.allowDisconnected); otherwise build() rejects them."""
+        self._allowDisconnected = bool(b)
+        return self
 
     def addInputs(self, *names):
         self._inputs += [n for ns in names for n in (ns if isinstance(ns, (list, tuple)) else [ns])]
@@ -452,6 +459,20 @@ class GraphBuilder:
         for o in self._outputs:
             if o not in self._vertices:
                 raise ValueError(f"Output {o!r} is not a vertex")
+        if not self._allowDisconnected:
+            # every input and vertex must lead to an output (reference ComputationGraphConfiguration.validate)
+            reach, stack = set(self._outputs), list(self._outputs)
+            while stack:
+                for i in self._vertexInputs.get(stack.pop(), []):
+                    if i not in reach:
+                        reach.add(i)
+                        stack.append(i)
+            dis = [n for n in list(self._inputs) + list(self._order) if n not in reach]
+            if dis:
+                from ...exceptions import DL4JInvalidConfigException
+                raise DL4JInvalidConfigException(
+                    f"Invalid configuration: disconnected vertices found - {dis} are not connected to the network "
+                    "output; use .allowDisconnected(True) to build it anyway")
         conf = ComputationGraphConfiguration(
             vertices={k: self._vertices[k] for k in self._order}, vertexInputs=dict(self._vertexInputs),
             networkInputs=list(self._inputs), networkOutputs=list(self._outputs), backprop=self._backprop,

@@ -337,14 +337,15 @@ class KafkaBroker:
             raise KafkaError(f"list offsets {topic}[{partition}]: error {err}")
         return off
 
-    def fetch(self, topic, offset, partition=None, max_bytes=4 << 20, max_wait_ms=None):
-        """[(offset, key, value)] from ``offset`` on, and the high watermark."""
+    def fetch(self, topic, offset, partition=None, max_bytes=4 << 20, max_wait_ms=None, conn=None):
+        """[(offset, key, value)] from ``offset`` on, and the high watermark. ``conn``: a dedicated connection to the
+        partition leader (subscriptions long-poll on their own socket, so they never hold up produce requests)."""
         partition = self.partition if partition is None else partition
         mw = self.max_wait if max_wait_ms is None else max_wait_ms
         body = (_W().i32(-1).i32(mw).i32(1).i32(max_bytes).i8(0)
                 .array([topic], lambda w, t: w.string(t).array(
                     [partition], lambda w, p: w.i32(p).i64(offset).i32(max_bytes))).getvalue())
-        r = self._leader(topic, partition).request(API_FETCH, V_FETCH, body)
+        r = (conn or self._leader(topic, partition)).request(API_FETCH, V_FETCH, body)
         r.i32()                                       # throttle
         resp = r.array(lambda r: (r.string(), r.array(lambda r: (
             r.i32(), r.i16(), r.i64(), r.i64(), r.array(lambda r: (r.i64(), r.i64())), r.bytes_()))))
@@ -364,11 +365,15 @@ class KafkaBroker:
         stop = threading.Event()
         start = self.list_offset(topic)
 
+        self._leader(topic, self.partition)
+        addr = self._nodes[self._leaders[(topic, self.partition)]]
+        conn = _Conn(addr[0], addr[1], self.client_id, self.timeout)
+
         def run():
             off = start
             while not stop.is_set():
                 try:
-                    recs, _hw = self.fetch(topic, off)
+                    recs, _hw = self.fetch(topic, off, conn=conn)
                 except (KafkaError, OSError):
                     if stop.is_set():
                         break
@@ -377,6 +382,7 @@ class KafkaBroker:
                 for o, _k, v in recs:
                     q.put(v.decode("utf-8") if v is not None else None)
                     off = o + 1
+            conn.close()
         t = threading.Thread(target=run, daemon=True, name=f"kafka-fetch-{topic}")
         with self._lock:
             self._subs[id(q)] = (stop, t)
