@@ -235,7 +235,7 @@ def _param_acc(w):
 
 def _colsum(g2, out=None):
     """fp32 column sums of a [M, N] gradient (channel-sum HIP kernel on the GPU); ``out``: optional fp32 sink."""
-    if g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float32) and g2.shape[1] % 8 == 0:
+    if g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float16, torch.float32) and g2.shape[1] % 8 == 0:
         from ..ops import native
         r = native.channel_sum(g2.contiguous(), out=None if out is None else out.view(-1))
         if r is not None:
