@@ -121,8 +121,18 @@ class IUpdater(Config):
         return {}
 
     def apply_reference(self, g, state, iteration, epoch):
-        """In-place: g <- update. ``state`` is this block's flat state slice."""
-        raise NotImplementedError
+        """In-place: g <- update. ``state`` is this block's flat state slice.
+        A user updater written against the reference API (``instantiate(viewArray, initialize)`` returning a
+        GradientUpdater with ``applyUpdater(gradient, iteration, epoch)``) runs through that."""
+        inst = getattr(self, "instantiate", None)
+        if inst is None:
+            raise NotImplementedError(f"{type(self).__name__}: neither apply_reference nor instantiate is defined")
+        gu = inst(state if state.numel() else None, False)
+        gu.applyUpdater(g, iteration, epoch)
+
+    def kernel_supported(self):
+        """True when the fused HIP updater kernel implements this updater (the built-in ND4J updaters)."""
+        return type(self) in UPDATER_OPCODES
 
 
 class NoOp(IUpdater):

@@ -238,6 +238,10 @@ class BaseNetwork:
     def numParams(self, backwards=False):
         return self._numParams
 
+    def getFlattenedGradients(self):
+        """The flat gradient vector (a view; reference getFlattenedGradients)."""
+        return self.flattenedGradients
+
     def params(self):
         return self.flattenedParams.reshape(1, -1)
 

@@ -83,10 +83,16 @@ def fused_update(plan, params, grad, state, iteration, epoch, batch_size, mini_b
     reg_out: optional zeroed 1-element tensor that receives sum(l1*|p| + 0.5*l2*p^2) of the pre-update
     params (the score's regularisation term) — computed inside the same kernel pass on GPU."""
     div = float(batch_size) if mini_batch else 1.0
+    custom = [b[3] for b in plan.blocks if not b[3].kernel_supported()]
     if use_native(params, "update") and params.dtype == torch.float32:
-        from . import native
-        if native.fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update, reg_out):
-            return
+        if not custom:
+            from . import native
+            if native.fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write_update,
+                                   reg_out):
+                return
+        elif params.is_cuda:
+            from . import fallback
+            fallback.record("update", f"user updater {type(custom[0]).__name__}: per-block reference update")
     if has_gn(plan):
         pre_apply(plan, grad)
     with torch.no_grad():
