@@ -86,13 +86,16 @@ __device__ __forceinline__ float wsum16(float v) {
 }
 
 // ------------------------------------------------------------------------------------------------ forward
-template <int D, typename hb>
+// NB key blocks are staged per round (NB = 2 for D = 64: a T = 128 sequence is one round, one global round trip and
+// one barrier pair instead of two); every thread issues all of the round's K and V loads before any LDS store.
+template <int D, typename hb, int NB>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qkv, const float* __restrict__ mask,
                                                        hb* __restrict__ out, float* __restrict__ lse, int T, int H,
                                                        float scale2, int causal) {
   constexpr int KS = D / 32, DT = D / 16;
-  constexpr int LDK = D + 8, LDV = BLK + 8;
-  __shared__ __attribute__((aligned(16))) hb Ks[BLK * LDK];
+  constexpr int LDK = D + 8, LDV = NB * BLK + 8;
+  constexpr int CPR = D / 8, PER = BLK * CPR / 256;              // 16-byte chunks per row / per thread per block
+  __shared__ __attribute__((aligned(16))) hb Ks[NB * BLK * LDK];
   __shared__ __attribute__((aligned(16))) hb Vt[D * LDV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 15, hgrp = lane >> 4;
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -110,51 +113,77 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const hb* __restrict__ qk
   float m = kNegInf, l = 0.f;
   const float* mrow = mask ? mask + (long long)b * T : nullptr;
   const int nkb = causal ? min((blockIdx.x * BLK + BLK + BLK - 1) / BLK, (T + BLK - 1) / BLK) : (T + BLK - 1) / BLK;
-  for (int kb = 0; kb < nkb; ++kb) {
+  for (int kb0 = 0; kb0 < nkb; kb0 += NB) {
     __syncthreads();
-    stage_rows<D>(Ks, LDK, base + E + h * D, ld3, kb * BLK, T);
-    stage_rows_t<D>(Vt, LDV, base + 2 * E + h * D, ld3, kb * BLK, T);
+    V8<hb> kr[NB][PER], vr[NB][PER];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const int i = threadIdx.x + it * 256, r = i / CPR, c = i - r * CPR;
+        const int row = (kb0 + j) * BLK + r;
+        const bool ok = kb0 + j < nkb && row < T;
+        const hb* src = base + (long long)(ok ? row : 0) * ld3 + h * D + c * 8;
+        kr[j][it] = ok ? ld8(src + E) : V8<hb>{0, 0, 0, 0, 0, 0, 0, 0};
+        vr[j][it] = ok ? ld8(src + 2 * E) : V8<hb>{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const int i = threadIdx.x + it * 256, r = i / CPR, c = i - r * CPR;
+        *reinterpret_cast<V8<hb>*>(Ks + (j * BLK + r) * LDK + c * 8) = kr[j][it];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) Vt[(c * 8 + k) * LDV + j * BLK + r] = vr[j][it][k];
+      }
     __syncthreads();
-    f4_t s[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      s[mt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) {
+      const int kb = kb0 + j;
+      if (kb >= nkb) break;
+      const hb* Kj = Ks + j * BLK * LDK;
+      f4_t s[4];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[mt] = mma(ld8(Ks + (mt * 16 + col) * LDK + ks * 32 + 8 * hgrp), qf[ks], s[mt]);
-    }
-    float bm = kNegInf;
+      for (int mt = 0; mt < 4; ++mt) {
+        s[mt] = f4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * BLK + mt * 16 + hgrp * 4 + r;
-        bool ok = key < T && (!causal || key <= q);
-        if (ok && mrow) ok = mrow[key] != 0.f;
-        const float v = ok ? s[mt][r] * scale2 : kNegInf;
-        s[mt][r] = v;
-        bm = fmaxf(bm, v);
+        for (int ks = 0; ks < KS; ++ks) s[mt] = mma(ld8(Kj + (mt * 16 + col) * LDK + ks * 32 + 8 * hgrp), qf[ks], s[mt]);
       }
-    bm = wmax16(bm);
-    const float mn = fmaxf(m, bm);
-    const float alpha = (mn == kNegInf) ? 1.f : exp2f(m - mn);
-    float ps = 0.f;
+      float bm = kNegInf;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mn == kNegInf) ? 0.f : exp2f(s[mt][r] - mn);
-        s[mt][r] = p;
-        ps += p;
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * BLK + mt * 16 + hgrp * 4 + r;
+          bool ok = key < T && (!causal || key <= q);
+          if (ok && mrow) ok = mrow[key] != 0.f;
+          const float v = ok ? s[mt][r] * scale2 : kNegInf;
+          s[mt][r] = v;
+          bm = fmaxf(bm, v);
+        }
+      bm = wmax16(bm);
+      const float mn = fmaxf(m, bm);
+      const float alpha = (mn == kNegInf) ? 1.f : exp2f(m - mn);
+      float ps = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = (mn == kNegInf) ? 0.f : exp2f(s[mt][r] - mn);
+          s[mt][r] = p;
+          ps += p;
+        }
+      l = l * alpha + wsum16(ps);
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) acc[dt] *= alpha;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const V8<hb> pb = pack2<hb>(s[2 * k2], s[2 * k2 + 1]);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          acc[dt] = mma(ld4x2(Vt + (dt * 16 + col) * LDV + j * BLK + 32 * k2, hgrp), pb, acc[dt]);
       }
-    l = l * alpha + wsum16(ps);
-    m = mn;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) acc[dt] *= alpha;
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const V8<hb> pb = pack2<hb>(s[2 * k2], s[2 * k2 + 1]);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) acc[dt] = mma(ld4x2(Vt + (dt * 16 + col) * LDV + 32 * k2, hgrp), pb, acc[dt]);
     }
   }
   if (q < T) {
@@ -366,7 +395,8 @@ template <int D, typename hb>
 static int fwd_l(const void* qkv, const float* mask, void* out, float* lse, int B, int T, int H, float scale,
                  int causal, hipStream_t s) {
   const dim3 grid((T + BLK - 1) / BLK, B * H);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, hb>), grid, dim3(256), 0, s, (const hb*)qkv, mask, (hb*)out, lse, T, H,
+  constexpr int NB = D == 64 ? 2 : 1;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, hb, NB>), grid, dim3(256), 0, s, (const hb*)qkv, mask, (hb*)out, lse, T, H,
                      scale * kLog2e, causal);
   return (int)hipGetLastError();
 }
