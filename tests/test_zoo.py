@@ -67,3 +67,16 @@ def test_text_generation_lstm():
 def test_zoo_registry_complete():
     assert set(ZOO) == {"ResNet50", "LeNet", "SimpleCNN", "TextGenerationLSTM", "AlexNet", "VGG16", "VGG19",
                         "Darknet19", "GoogLeNet", "TinyYOLO", "YOLO2", "FaceNetNN4Small2", "InceptionResNetV1"}
+
+
+def test_lenet_cpu_bench_tool_runs():
+    """BASELINE config 1 (LeNet-MNIST on the CPU backend): the bench tool trains and prints one JSON line."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "tools/bench_lenet.py", "--steps", "2", "--warmup", "1", "--batch", "16"],
+                       capture_output=True, text=True, timeout=300,
+                       cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] > 0 and line["config"]["model"].startswith("LeNet")
