@@ -18,3 +18,5 @@ step stem 300 python3 tools/stem_bench.py
 grep -v amdgpu.ids gpurun_out/r4i_stem.log
 step b_resnet1 400 python3 bench.py --steps 30 --warmup 5
 step b_resnet2 400 python3 bench.py --steps 30 --warmup 5
+step b_bert_sd 300 python3 tools/bench_bert_samediff.py --steps 10 --warmup 3
+step b_bert 300 python3 tools/bench_bert.py --steps 10 --warmup 3
