@@ -28,15 +28,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # per-GPU batch: 512 fills the MI355X (288 GB HBM) far better than 256 (measured 22.1k vs 18.0k img/s: the conv
-    # grids of the 7x7/14x14 stages leave CUs idle at 256); weak scaling keeps it per GPU
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 512)), help="per-GPU batch")
+    # per-GPU batch, sized for 288 GB of HBM: the late 7x7 / 14x14 stages need a large batch to fill 256 CUs and
+    # the per-step serial tail (stem, BN folds, the fused update) amortizes over more images. Measured on one MI355X
+    # (profiles/r4_batch_sweep.txt): 512 -> 34.4k, 768 -> 36.5k, 1024 -> 38.2k img/s at 20.3 GiB peak,
+    # 2048 -> 40.6k at 39.9 GiB. 1024 is the default; weak scaling keeps it per GPU
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", 1024)), help="per-GPU batch")
     ap.add_argument("--variant", default=os.environ.get("BENCH_VARIANT", "dl4j"), choices=["dl4j", "canonical"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--graph", type=int, default=int(os.environ.get("BENCH_GRAPH", "0")),
                     help="capture the training step in HIP graphs (1 on, 0 off (default), -1 auto = on unless the "
-                         "collectives are not capturable, i.e. gloo). Off by default for ResNet-50 at batch 512: the "
-                         "step is not launch-bound (~520 kernels in 15 ms) and eager launches keep the conv "
+                         "collectives are not capturable, i.e. gloo). Off by default for ResNet-50: the "
+                         "step is not launch-bound (~520 kernels in 15 ms at batch 512) and eager launches keep the conv "
                          "weight-gradient stream concurrent with the data-gradient chain, which a replayed graph "
                          "does not (profiles/r4_eager_vs_graph.txt: 32.8-32.9k eager vs 31.3k graph img/s)")
     ap.add_argument("--comm-dtype", default=os.environ.get("BENCH_COMM_DTYPE", "fp32"), choices=["fp32", "bf16"],
@@ -140,7 +142,9 @@ def main():
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}", "comm": args.comm,
                        "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                        "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
-                       "final_score": final_score},
+                       "final_score": final_score,
+                       "peak_mem_gib": round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
+                       if device.type == "cuda" else None},
         }), flush=True)
     from deeplearning4j_amd.parallel.distributed import destroy
     destroy()

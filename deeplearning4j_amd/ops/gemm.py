@@ -55,6 +55,7 @@ _TUNE = os.environ.get("DL4J_AMD_GEMM_TUNE", "1") == "1"
 # GEMMs stay on the in-tree kernels, a library GEMM is used only where it measured faster.
 _LIB = os.environ.get("DL4J_AMD_GEMM_LIB", "1") == "1"
 LIB_CFG = (-2, 1)
+_F32_FORCE = None        # tests: True / False pins fp32 products to the library / the exact-fp32 kernel
 
 
 def _plan(lib, M, N, K, batch):
@@ -365,9 +366,33 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         else:
             sam, sak = A_.stride(-2), A_.stride(-1)
             sbk, sbn = B_.stride(-2), B_.stride(-1)
-        rc = lib.dl4j_gemm_simple(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), sam, sak, sA_, _p(B_), sbk, sbn,
-                                  sB_, _p(c_t), ldc, sC, float(alpha), float(beta), _p(bias), bmode, actc, _p(z),
-                                  _stream())
+
+        def simple(dst, bt):
+            return lib.dl4j_gemm_simple(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), sam, sak, sA_, _p(B_), sbk,
+                                        sbn, sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc, _p(z),
+                                        _stream())
+        run = simple
+        if in_dt == 0 and not (bias is not None and bias_in is None):
+            # fp32 operands: the exact-fp32 kernel has one 64x64 tile and no split-K, so a long-K weight gradient
+            # (LeNet conv1: K = 36864 output pixels onto a 20 x 25 tile) is one serial workgroup; the fp32 library
+            # GEMM (exact fp32, no TF32) is the second candidate, timed per shape like the 16-bit configurations
+            libmm = _lib_gemm(a, b, c_t, swap, batched, bias_in, bias_dim, act, alpha, beta, z, out_dtype)
+            if libmm is not None:
+                k32 = ("f32", Mx, Nx, K, batch, swap, sam, sak, sbk, sbn, ldc, bias_in is not None, beta != 0.0, act,
+                       z is not None)
+                use_lib = _TUNED.get(k32) if _F32_FORCE is None else _F32_FORCE
+                if use_lib is None:
+                    use_lib = False
+                    if _TUNE and not torch.cuda.is_current_stream_capturing():
+                        from .timing import gpu_time
+                        tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
+                        if simple(tmp, 0.0) == 0 and libmm(tmp, 0.0) == 0:
+                            use_lib = gpu_time(lambda: libmm(tmp, 0.0), reps=3, warmup=0) < \
+                                gpu_time(lambda: simple(tmp, 0.0), reps=3, warmup=0)
+                        _TUNED[k32] = use_lib
+                if use_lib:
+                    run = libmm
+        rc = run(c_t, float(beta))
     if rc != 0:
         raise RuntimeError(f"HIP gemm failed with code {rc} (M={M} N={N} K={K} batch={batch})")
     if c_t is not out:
@@ -382,14 +407,14 @@ def _lib_gemm(a, b, c_t, swap, batched, bias, bias_dim, act, alpha, beta, z, out
     a bias / beta / batch) or its destination is not a dense matrix.
     Activations: ``act(z)`` with the pre-activation kept in ``z`` when given (the library writes z, the elementwise
     kernel reads it); ``dgelu``: out = (a @ b) * gelu'(z), applied in place on the library result."""
-    if not _LIB or alpha != 1.0 or a.dtype not in (torch.bfloat16, torch.float16) or b.dtype != a.dtype:
+    if not _LIB or alpha != 1.0 or a.dtype not in (torch.bfloat16, torch.float16, torch.float32) or b.dtype != a.dtype:
         return None
     act = None if act == "identity" else act
     if act not in (None, "relu", "tanh", "sigmoid", "gelu", "dgelu") or (act is not None and (beta != 0.0 or batched)):
         return None
     if (act == "dgelu" and z is None) or (z is not None and act is None):
         return None
-    wide = out_dtype == torch.float32                   # 16-bit operands, fp32 result (weight gradients)
+    wide = out_dtype == torch.float32 and a.dtype != torch.float32     # 16-bit operands, fp32 result (weight grads)
     if out_dtype != a.dtype and not (wide and bias is None and beta == 0.0 and not batched and act is None):
         return None
     if bias is not None and (bias.dtype != a.dtype or bias_dim != 1 or swap or batched or beta != 0.0):

@@ -297,3 +297,41 @@ def test_library_candidate(case, monkeypatch):
     assert gemm._lib_gemm(a, b, c16, False, False, None, 1, "dgelu", 1.0, 0.0, None, torch.bfloat16) is None
     assert gemm._lib_gemm(a, b, torch.empty(M, N, device=DEV), False, False, None, 1, None, 1.0, 1.0, None,
                           torch.float32) is None          # fp32 output with beta-accumulate stays in-tree
+
+
+@pytest.mark.parametrize("case", ["long_k", "bias_relu", "colmajor", "beta", "batched"])
+@pytest.mark.parametrize("force", [True, False])
+def test_fp32_library_candidate(case, force, monkeypatch):
+    """fp32 operands: the exact-fp32 MFMA kernel and the fp32 library GEMM (the second candidate, timed per shape)
+    compute the same product to fp32 accuracy for every form; the long-K weight-gradient shape of LeNet conv1
+    (K = 36864 onto a 20 x 25 output, one 64x64 tile) is dispatched to the library by the measurement."""
+    torch.manual_seed(9)
+    monkeypatch.setattr(gemm, "_F32_FORCE", force)
+    M, N, K = (20, 25, 36864) if case == "long_k" else (300, 200, 160)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    ref = a.double() @ b.double()
+    tol = 1e-4 * ref.abs().max().item() + 1e-5 * K ** 0.5
+    if case in ("long_k", "colmajor"):
+        out = torch.empty(M, N, device=DEV) if case == "long_k" else torch.empty(N, M, device=DEV).t()
+        gemm.mmul(a, b, out=out)
+    elif case == "bias_relu":
+        bias = torch.randn(N, device=DEV)
+        out = gemm.mmul(a, b, bias=bias, act="relu")
+        ref = torch.relu(ref + bias.double())
+    elif case == "beta":
+        c0 = torch.randn(M, N, device=DEV)
+        out = c0.clone()
+        gemm.mmul(a, b, out=out, beta=1.0)
+        ref = ref + c0.double()
+    else:
+        a3, b3 = torch.randn(3, M, K, device=DEV), torch.randn(3, K, N, device=DEV)
+        out = gemm.mmul(a3, b3)
+        ref = a3.double() @ b3.double()
+    assert (out.double() - ref).abs().max().item() <= tol, case
+    if case == "long_k" and not force:
+        monkeypatch.setattr(gemm, "_F32_FORCE", None)
+        gemm._TUNED.clear()
+        gemm.mmul(a, b, out=out)
+        picked = [v for k, v in gemm._TUNED.items() if k[0] == "f32" and k[1:4] in ((M, N, K), (N, M, K))]
+        assert picked == [True], picked
