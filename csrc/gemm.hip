@@ -32,6 +32,22 @@
 
 #include "mfma_tile.h"
 
+// Diagnostic build only (tools/gemm_stamps.hip defines DL4J_GEMM_STAMPS): per-block phase timestamps of the 8-phase
+// kernel, shader clock and 100 MHz real time, written by lane 0 of wave 0 with an ordinary vector store.
+#ifdef DL4J_GEMM_STAMPS
+__device__ unsigned long long* g_gemm_stamps;
+#define GSTAMP(i)                                                                                   \
+  do {                                                                                              \
+    if (threadIdx.x == 0) {                                                                         \
+      unsigned long long* p_ = g_gemm_stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16; \
+      p_[2 * (i)] = __builtin_amdgcn_s_memtime();                                                   \
+      p_[2 * (i) + 1] = __builtin_amdgcn_s_memrealtime();                                           \
+    }                                                                                               \
+  } while (0)
+#else
+#define GSTAMP(i) do {} while (0)
+#endif
+
 namespace {
 
 template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES, bool BNB = false>
@@ -325,6 +341,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   const E* B = reinterpret_cast<const E*>(g.B) + (long long)bz * g.sB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
+  GSTAMP(0);
 
   // Per-lane DMA source: one base element offset per operand (k = kbeg) plus the lane's row/column within the
   // half-tile pattern; half h and instruction j only add wave-uniform offsets (keeps the loop free of spills).
@@ -437,6 +454,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   stage(1, 0, 0); stage(1, 1, 0); stage(1, 1, 1);
   wait_vm<6>();
   raw_barrier();
+  GSTAMP(1);
   // stagger the two wave rows by one barrier: while one group runs its MFMA cluster the other issues its reads
   const bool late = __builtin_amdgcn_readfirstlane(wr) == 1;
   if (late) raw_barrier();
@@ -482,6 +500,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   }
   if (!late) raw_barrier();
   wait_vm<0>();
+  GSTAMP(2);
 
   // epilogue (see epi_readout): pass P = wave row wr. acc[nb][mb] reg e <-> tile row wr*128 + (mb>>2)*64 +
   // (mb&3)*16 + (lane&15), tile column wc*64 + (nb>>1)*32 + (nb&1)*16 + (lane>>4)*4 + e.
@@ -522,6 +541,10 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
       }
     }
   }
+#ifdef DL4J_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  GSTAMP(3);
 }
 
 // ----------------------------------------------------------------------------------------------- simple kernel

@@ -12,9 +12,12 @@ Recurrent networks: ``tbptt_scope`` gives every truncated-BPTT window its own LO
 iteration's), and the LSTM sequence kernels' per-call buffers (outputs, gate / cell caches: the reference's LOOP_LSTM
 working memory) are carved from whichever arena is open; state carried past a scope is leveraged out of it.
 """
+import logging
 import threading
 
 import torch
+
+log = logging.getLogger("deeplearning4j_amd")
 
 _tl = threading.local()
 
@@ -163,6 +166,9 @@ class training_scope:
             leverage_states(self.net, self.ws)
             _tl.ws = None
             self.ws.notifyScopeLeft()
+            mb = getattr(self.net, "_mb", None)      # the largest minibatch the eager arena has learned from
+            if isinstance(mb, int) and mb > getattr(self.net, "_ws_learned_mb", 0):
+                self.net._ws_learned_mb = mb
         return False
 
 
@@ -182,10 +188,14 @@ def _activation_estimate(net, minibatch):
 def graph_workspace(net, minibatch, key):
     """The LOOP_FF_BP arena a captured training step owns (nn/hipgraph.py): every activation, BN / pooling buffer
     and gradient-in-flight the captured iteration allocates is carved from it, so the graph's private memory IS the
-    workspace. Sized from what the eager warmup iterations' LOOP_FF_BP arena learned (its peak, +5 %), or from the
-    memory report when that arena is not available; creation fails early, with the numbers, when the size exceeds
-    the free HBM (hipMemGetInfo). The arena is frozen: its buffer never moves while graphs hold its addresses, and an
-    allocation beyond it falls back to the graph's own pool. Returns None for networks without a training arena."""
+    workspace. Sized per capture key from what the eager warmup iterations' LOOP_FF_BP arena learned (its peak, +5 %,
+    scaled by this key's minibatch over the largest minibatch that arena saw, so a smaller tail-batch key gets a
+    proportionally smaller arena), or from the memory report when that arena is not available. When the size
+    exceeds the free HBM (hipMemGetInfo; the eager arena's buffer counts as free only when it is really released
+    here) no arena is made and None is returned: the capture then allocates from the graph's private pool (or the
+    step runs eagerly), with a warning naming the numbers. The arena is frozen: its buffer never moves while graphs
+    hold its addresses, and an allocation beyond it falls back to the graph's own pool. Returns None for networks
+    without a training arena."""
     ok = getattr(net, "_ws_ok", None)
     if ok is None:
         ok = net._ws_ok = _eligible(net)
@@ -193,19 +203,25 @@ def graph_workspace(net, minibatch, key):
         return None
     eager = getattr(net, "_loop_ws", None)
     learned = int(eager.stats()["maxPeak"]) if eager is not None else 0
+    learned_mb = int(getattr(net, "_ws_learned_mb", 0) or 0)
+    if learned > 0 and learned_mb > 0 and 0 < minibatch < learned_mb:
+        learned = int(learned * minibatch / learned_mb)
     est = _activation_estimate(net, minibatch)
     need = int(learned * 1.05) + (1 << 20) if learned > 0 else int(est)
     if need <= (1 << 20):
         return None
     free, total = torch.cuda.mem_get_info(net.device)
-    # the eager arena's buffer is released below, so it counts as free for the graph's arena
-    reusable = eager._buf.numel() if eager is not None and eager._buf is not None else 0
+    # the eager arena's buffer is released below (only when no eager step holds it open), so only then does it count
+    # as free for the graph's arena
+    releasable = eager is not None and eager._buf is not None and not eager.active
+    reusable = eager._buf.numel() if releasable else 0
     if need > free + reusable:
-        raise MemoryError(f"training step of {type(net).__name__} at minibatch {minibatch}: its workspace needs "
-                          f"{need / 2**30:.2f} GiB (learned peak {learned / 2**30:.2f} GiB, memory-report estimate "
-                          f"{est / 2**30:.2f} GiB) but only {(free + reusable) / 2**30:.2f} GiB of "
-                          f"{total / 2**30:.1f} GiB HBM are free; reduce the minibatch")
-    if eager is not None and eager._buf is not None and not eager.active:
+        log.warning("training step of %s at minibatch %d: its workspace needs %.2f GiB (learned peak %.2f GiB, "
+                    "memory-report estimate %.2f GiB) but only %.2f GiB of %.1f GiB HBM are free; capturing without "
+                    "a frozen arena", type(net).__name__, minibatch, need / 2**30, learned / 2**30, est / 2**30,
+                    (free + reusable) / 2**30, total / 2**30)
+        return None
+    if releasable:
         eager._buf = None                               # the eager arena re-learns if an eager step comes again
         eager._lib.rt_ws_set_capacity(eager._h, 0)
     from .workspace import (AllocationPolicy, LearningPolicy, MemoryWorkspace, ResetPolicy, SpillPolicy,

@@ -220,6 +220,10 @@ class Lexicon:
                                        "unknown")])
         lex = Lexicon(entries, ConnectionCosts(table, int(scale * 10)), chardef, unk)
         lex.classes = cls_id
+        # search-mode penalties are IPADIC-unit constants: express them in this lexicon's cost units (the ratio of
+        # its unknown-katakana cost to IPADIC's 9461, the unit Kuromoji's 1700-per-character penalty is set against)
+        kata = unk.get("KATAKANA")
+        lex.penalty_scale = (min(e.cost for e in kata) / 9461.0) if kata else scale / 700.0
         return lex
 
 
@@ -341,9 +345,10 @@ class LatticeTokenizer:
             return 0
         n = len(surf)
         cd = self.lex.chardef
+        k = getattr(self.lex, "penalty_scale", 1.0)        # lexicon cost units per IPADIC cost unit
         if all(cd.category(c) == "KANJI" for c in surf):
-            return (n - self.KANJI_LEN) * self.KANJI_PENALTY if n > self.KANJI_LEN else 0
-        return (n - self.OTHER_LEN) * self.OTHER_PENALTY if n > self.OTHER_LEN else 0
+            return k * (n - self.KANJI_LEN) * self.KANJI_PENALTY if n > self.KANJI_LEN else 0
+        return k * (n - self.OTHER_LEN) * self.OTHER_PENALTY if n > self.OTHER_LEN else 0
 
     def _analyze(self, text):
         N = len(text)

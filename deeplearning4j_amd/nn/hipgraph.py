@@ -262,6 +262,9 @@ def graph_eligible(net, inputs, labels, fmasks, lmasks, tbptt_window=False):
         return False                               # gloo / custom accumulators: eager steps
     if acc is not None and getattr(acc, "participants", None):
         return False                               # partial data-parallel round: its divisor is not the captured one
+    gb = getattr(acc, "global_batch", None) if acc is not None else None
+    if gb and gb != inputs[0].shape[0] * getattr(acc, "world_size", 1):
+        return False                               # unequal batches in the round: the divisor is not the captured one
     algo = net.conf.globalConf.get("optimizationAlgo")
     if algo is not None and OA.of(algo) != OA.STOCHASTIC_GRADIENT_DESCENT:
         return False

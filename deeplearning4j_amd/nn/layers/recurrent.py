@@ -375,8 +375,12 @@ class LSTMImpl(BaseRecurrentImpl):
         dz1, dz2, st1, st2 = r
         _native_weight_grads(dz2, c2, self.W("W"), H, self.PEEPHOLE, "", self.grads, False, *st2)
         prev._stack_dz = (dz1, st1, c2["stack"])
-        # the layer below takes its gate deltas from _stack_dz: a zero-cost placeholder stands in for its epsilon
-        return self.make_gradient(), torch.zeros((), dtype=eps.dtype, device=eps.device).expand(mb, H, T)
+        # the layer below takes its gate deltas from _stack_dz: a zero-cost placeholder stands in for its epsilon.
+        # It is marked, so that a layer below that does NOT find the matching _stack_dz (its cache was replaced by a
+        # re-run forward in between) raises instead of silently training on a zero gradient.
+        ph = torch.zeros((), dtype=eps.dtype, device=eps.device).expand(mb, H, T)
+        ph._dl4j_stack_placeholder = True
+        return self.make_gradient(), ph
 
     def rnnTimeStep(self, x, mask=None):
         self._check_state_mb(x)
@@ -402,6 +406,10 @@ class LSTMImpl(BaseRecurrentImpl):
             if dx is None:
                 return self.make_gradient(), None
             return self.make_gradient(), self.backpropDropOut(dx.to(eps.dtype))
+        if getattr(eps, "_dl4j_stack_placeholder", False):
+            raise RuntimeError(f"LSTM layer {self.conf.layerName!r}: received the stacked-launch epsilon placeholder "
+                               "without the matching gate deltas (the forward was re-run between the two layers' "
+                               "backprops); run forward and backward of the stack together")
         if prev is not None and self._cache is not None and self._cache.get("stack") is not None and \
                 prev._cache is not None and prev._cache.get("stack") is self._cache["stack"]:
             r = self._stack_backward(prev, eps, tbptt_back)

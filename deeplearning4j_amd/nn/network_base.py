@@ -432,6 +432,11 @@ class BaseNetwork:
             # the 1/world part); user accumulators without a world_size count as one replica
             # (a partial data-parallel round divides by the replicas that really trained: ``participants``)
             batch_size = batch_size * (getattr(acc, "participants", None) or getattr(acc, "world_size", 1))
+            if getattr(acc, "global_batch", None):
+                batch_size = acc.global_batch       # the round's total example count, identical on every replica
+        elif acc is not None and getattr(acc, "global_batch", None):
+            # averaging accumulator: gradients were already divided by the replica count
+            batch_size = acc.global_batch / (getattr(acc, "participants", None) or getattr(acc, "world_size", 1))
         reg = None
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
             reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)

@@ -40,12 +40,13 @@ def build_kernels(verbose=True, jobs=None):
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h"))
+    abi_headers = headers + glob.glob(os.path.join(CSRC, "include", "*.h"))   # only csrc/abi.hip includes these
     objs = []
     todo = []
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer(s, o, headers):
+        if _newer(s, o, abi_headers if os.path.basename(s) == "abi.hip" else headers):
             todo.append((s, o))
     flags = ["-O3", "-fPIC", f"--offload-arch={ARCH}", "-std=c++17", "-munsafe-fp-atomics", "-I", CSRC]
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
@@ -56,7 +57,9 @@ def build_kernels(verbose=True, jobs=None):
             if verbose:
                 print(f"[build] compiled {os.path.basename(futs[f])}", file=sys.stderr)
     if todo or not os.path.exists(KERNEL_LIB):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs)
+        # librccl: the C ABI's communicator entry points (csrc/abi.hip dl4j_comm_*)
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs +
+             ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
         if verbose:
             print(f"[build] linked {KERNEL_LIB}", file=sys.stderr)
     return KERNEL_LIB
@@ -74,6 +77,28 @@ def build_runtime(verbose=True):
     if verbose:
         print(f"[build] linked {RUNTIME_LIB}", file=sys.stderr)
     return RUNTIME_LIB
+
+
+ABI_DRIVER = os.path.join(ROOT, "tests", "native", "abi_driver")
+
+
+def build_abi_driver(verbose=True):
+    """The C-only driver of the public ABI (tests/native/abi_driver.c against csrc/include/dl4j_amd.h): plain gcc,
+    C99, linked with both in-tree libraries (rpath to them) and libamdhip64."""
+    src = ABI_DRIVER + ".c"
+    hdr = os.path.join(CSRC, "include", "dl4j_amd.h")
+    if not os.path.exists(src):
+        return None
+    deps = [src, hdr, KERNEL_LIB, RUNTIME_LIB]
+    if os.path.exists(ABI_DRIVER) and all(os.path.getmtime(d) <= os.path.getmtime(ABI_DRIVER) for d in deps
+                                          if os.path.exists(d)):
+        return ABI_DRIVER
+    _run(["gcc", "-std=c99", "-O2", "-Wall", "-I", os.path.join(CSRC, "include"), src, "-o", ABI_DRIVER,
+          "-L", LIBDIR, "-ldl4j_amd_kernels", "-ldl4j_amd_runtime", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib",
+          "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-lm"])
+    if verbose:
+        print(f"[build] linked {ABI_DRIVER}", file=sys.stderr)
+    return ABI_DRIVER
 
 
 SANITIZERS = ("address", "thread", "undefined")
@@ -105,6 +130,7 @@ def build_runtime_sanitized(kind, verbose=True):
 def build_all(verbose=True):
     k = build_kernels(verbose)
     r = build_runtime(verbose)
+    build_abi_driver(verbose)
     return k, r
 
 

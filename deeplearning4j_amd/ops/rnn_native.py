@@ -175,7 +175,8 @@ def check_coop_errors():
 # multi-worker trainers); while any is live, and while the conv weight-gradient overlap stream is active, the
 # cooperative kernels use the cooperative launch so that every workgroup is co-resident.
 CONCURRENT_STREAMS = [0]
-_guard = {}          # device index -> [pinned int32 snapshot, event]
+_guard = {}          # device index -> deque of (pinned int32 snapshot, event), oldest first
+_GUARD_DEPTH = 8     # snapshots allowed in flight before the host blocks on the oldest one
 USED_COOP = [False]
 
 
@@ -194,32 +195,43 @@ def _launch_mode(lib):
 
 
 def check_step_guard(device):
-    """Called once per training step after the fused update has been queued: reads the previous step's snapshot of
-    the device-wide step guard (set by a timed-out cooperative LSTM launch; the fused updater then skipped that
-    update), raises CoopTimeoutError after clearing it, and queues a snapshot of the current value."""
+    """Called once per training step after the fused update has been queued. Every step queues a snapshot of the
+    device-wide step guard (set by a timed-out cooperative LSTM launch; the fused updater then skips updates) into a
+    FIFO; every snapshot whose event has completed is checked, oldest first, and once ``_GUARD_DEPTH`` snapshots are
+    pending the host blocks on the oldest. So a timeout is reported at most ``_GUARD_DEPTH`` steps late even when the
+    host runs far ahead of the GPU (HIP-graph replay, no listener syncing): the guard is cleared and CoopTimeoutError
+    raised."""
     if not USED_COOP[0] or device is None or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
         return
+    import collections
     lib = native.load()
     native.register_sig("dl4j_lstm_step_guard", [])
     native.register_sig("dl4j_lstm_step_guard_reset", [c_void_p])
     lib.dl4j_lstm_step_guard.restype = c_void_p
-    g = _guard.get(device.index)
-    if g is not None and g[1].query() and int(g[0][0]) != 0:
+    q = _guard.get(device.index)
+    if q is None:
+        q = _guard[device.index] = collections.deque()
+    tripped = False
+    while q and (len(q) >= _GUARD_DEPTH or q[0][1].query()):
+        snap, ev = q.popleft()
+        ev.synchronize()
+        if int(snap[0]) != 0:
+            tripped = True
+    if tripped:
         lib.dl4j_lstm_step_guard_reset(c_void_p(_stream()))
-        g[0][0] = 0
+        q.clear()                      # younger snapshots may hold the same (now cleared) trip
         raise CoopTimeoutError("cooperative LSTM kernel: a cross-workgroup hand-off timed out; the fused updater "
-                               "skipped that step's update (parameters unchanged)")
-    if g is None:
-        g = _guard[device.index] = [torch.zeros(1, dtype=torch.int32, pin_memory=True), None]
+                               "skipped the update of every step since (parameters unchanged)")
     ptr = lib.dl4j_lstm_step_guard()
     if not ptr:
         return
     import ctypes as _ct
+    snap = torch.zeros(1, dtype=torch.int32, pin_memory=True)
     hip = _hip()
-    hip.hipMemcpyAsync(_ct.c_void_p(g[0].data_ptr()), _ct.c_void_p(ptr), _ct.c_size_t(4), 2, _ct.c_void_p(_stream()))
+    hip.hipMemcpyAsync(_ct.c_void_p(snap.data_ptr()), _ct.c_void_p(ptr), _ct.c_size_t(4), 2, _ct.c_void_p(_stream()))
     ev = torch.cuda.Event()
     ev.record()
-    g[1] = ev
+    q.append((snap, ev))
 
 
 _hiplib = []

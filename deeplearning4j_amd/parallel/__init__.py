@@ -9,3 +9,4 @@ from .inference import InferenceMode, ParallelInference
 from .wrapper import ParallelWrapper, TrainingMode
 from .cluster import (ParameterAveragingTrainingMaster, SharedTrainingMaster, SparkComputationGraph,  # noqa: F401
                       SparkDl4jMultiLayer, StatsUtils, TrainingMaster, TrainingStats)
+from .basic import BasicGradientsAccumulator, FancyBlockingQueue, LocalHandler  # noqa: E402,F401

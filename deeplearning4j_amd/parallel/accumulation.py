@@ -60,6 +60,9 @@ class AllReduceGradientsAccumulator:
         # replicas that trained in this round (None = all): set by the in-process wrapper for a trailing partial
         # round, where idle replicas contribute zero gradients and the divisor counts only the active ones
         self.participants = None
+        # examples summed into this round's gradient over all replicas (None = local batch x replicas): set by the
+        # in-process wrapper so that every replica divides by the same count
+        self.global_batch = None
         self._comm_streams = {}
         self._comm_forked = None
 

@@ -73,11 +73,38 @@ class EncodedGradientsAccumulator:
     network's update step with encode -> all-gather -> decode-and-apply."""
     handles_update = True
 
-    def __init__(self, threshold=1e-3, handler=None, **handler_kw):
+    def __init__(self, threshold=1e-3, handler=None, parties=1, bufferSize=100 * 1024 * 1024, queueSize=10,
+                 **handler_kw):
+        if isinstance(threshold, EncodingHandler):            # reference argument order (handler first)
+            handler, threshold = threshold, 1e-3
         self.handler = handler or EncodingHandler(threshold, **handler_kw)
         self.world_size = world_size()
         self.residual = None
         self.last_messages = None
+        # in-process message fan-out (reference receiveUpdate: every compressed message is replicated into each
+        # party's queue; a message larger than bufferSize / queueSize bytes is refused)
+        self.parties = int(parties)
+        self.bufferSize = int(bufferSize)
+        self.queueSize = int(queueSize)
+        from .basic import FancyBlockingQueue
+        self.messages = [FancyBlockingQueue() for _ in range(self.parties)]
+
+    @staticmethod
+    def getOptimalBufferSize(paramsLength, numWorkers, queueSize):
+        """Bytes of message buffer for ``numWorkers`` parties keeping ``queueSize`` messages each: a message is at most
+        paramsLength/16 ints, plus 64k ints of headroom (reference EncodedGradientsAccumulator.java:141-150)."""
+        if not isinstance(paramsLength, int):
+            paramsLength = int(paramsLength.params().numel())
+        return ((paramsLength // 16) + 65536) * int(numWorkers) * int(queueSize) * 4
+
+    def receiveUpdate(self, array):
+        """Replicate one encoded message into every party's queue (decompression stays per party)."""
+        nbytes = array.numel() * array.element_size()
+        if nbytes > self.bufferSize // max(1, self.queueSize):
+            raise MemoryError(f"Not enough memory to handle update: [{nbytes} bytes required]. Please increase "
+                              "memory amount for GradientsAccumulator")
+        for q in self.messages:
+            q.put(array.clone())
 
     # the network calls these around backward; nothing to overlap (exchange happens after the updater)
     def begin_backward(self, net):

@@ -16,8 +16,9 @@ MI355X design:
     worker i through a queue of capacity ``prefetchBuffer // N`` (>= 1); at most ``prefetchBuffer + 2N`` batches
     (queued, in training, and the round being handed out) exist at once however long the iterator is;
   * a trailing partial round of L < N batches trains on the first L workers (reference :514-578,
-    ``registerConsumers(locker)``); the other workers still run the round's collectives with a zero gradient, and the
-    update divides by the L batches that were really trained on (SHARED_GRADIENTS), so every replica stays equal;
+    ``registerConsumers(locker)``); the other workers still run the round's collectives with a zero gradient, and
+    every replica's update divides the summed gradient by the round's total example count (SHARED_GRADIENTS), so
+    every replica applies the same update even when the round's batches differ in size;
   * HIP graphs: replicas inherit the caller's ``enableHipGraphs`` mode and each worker thread captures its own
     replica's step (thread-local capture mode, per-thread capture streams and graph slots, nn/hipgraph.py);
   * no per-batch host sync: each worker records an event per step and waits only for the step ``max_inflight``
@@ -105,7 +106,16 @@ class InProcessTrainer:
         self.models = [m] + [_replica(m, d) for d in self.devices[1:]]
         from .wrapper import TrainingMode
         self.shared = wrapper.trainingMode in (TrainingMode.SHARED_GRADIENTS,)
-        if self.shared:
+        self.custom = getattr(wrapper.accumulator, "shared_in_process", False)
+        if self.custom:
+            # CUSTOM mode with a thread-shared accumulator (BasicGradientsAccumulator): every replica gets the SAME
+            # instance, which synchronises the worker threads itself (reference PW:ParallelWrapper.java:838-843)
+            if getattr(wrapper.accumulator, "parties", n) != n:
+                raise ValueError(f"accumulator built for {wrapper.accumulator.parties} parties, wrapper has {n} "
+                                 "workers")
+            for net in self.models:
+                net.setGradientsAccumulator(wrapper.accumulator)
+        elif self.shared:
             for net, c in zip(self.models, self.comms):
                 net.setGradientsAccumulator(AllReduceGradientsAccumulator(wrapper.bucket_mb, comm=c))
         self.queues = [queue.Queue(maxsize=max(1, int(wrapper.prefetchBuffer) // n)) for _ in range(n)]
@@ -131,18 +141,25 @@ class InProcessTrainer:
                 item = q.get()
                 if item is _STOP:
                     break
-                ds, rnd, active, bsz = item
+                ds, rnd, active, bsz, total = item
                 acc = getattr(net, "gradientsAccumulator", None)
-                if active < len(self.models) and acc is not None:
-                    acc.participants = active           # partial round: divide by the batches trained on
+                if acc is not None and not self.custom:
+                    # every replica divides the summed gradient by the SAME count, the round's total examples (a
+                    # short trailing batch or a partial round would otherwise give each replica its own divisor)
+                    acc.global_batch = total
+                    if active < len(self.models):
+                        acc.participants = active       # partial round: replicas that trained
                 try:
                     if ds is not None:
                         _fit_one(net, ds)               # the network moves the batch to its device
+                    elif self.custom:
+                        acc.idle_step(net)              # a zero update into the shared accumulator's barriers
                     elif self.shared:
                         net._zero_contribution_step(bsz)
                 finally:
-                    if acc is not None:
+                    if acc is not None and not self.custom:
                         acc.participants = None
+                        acc.global_batch = None
                 if ds is not None:
                     with self.cv:
                         self._live -= 1
@@ -165,6 +182,8 @@ class InProcessTrainer:
                 self.cv.notify_all()
             for c in self.comms:
                 c.abort()
+            if self.custom and hasattr(self.w.accumulator, "abort"):
+                self.w.accumulator.abort()
             while True:                     # drain so the master's puts never block forever
                 try:
                     if q.get(timeout=0.05) is _STOP:
@@ -180,6 +199,8 @@ class InProcessTrainer:
             from ..ops import rnn_native
             rnn_native.CONCURRENT_STREAMS[0] += 1      # RCCL kernels on other streams: cooperative LSTM launches
             self._concurrent = True
+        if self.custom and hasattr(self.w.accumulator, "resetParties"):
+            self.w.accumulator.resetParties()
         for i in range(len(self.models)):
             t = threading.Thread(target=self._run, args=(i,), name=f"dl4j-pw-worker-{i}", daemon=True)
             t.start()
@@ -213,11 +234,12 @@ class InProcessTrainer:
                 for batch_round in _rounds(source, n):
                     L = len(batch_round)
                     bsz = _batch_size(batch_round[0])
+                    total = sum(_batch_size(b) for b in batch_round)
                     with self.cv:
                         self._live += L             # pulled from the iterator and not yet trained on
                         self.max_live = max(self.max_live, self._live)
                     for i in range(n):
-                        self._put(i, (batch_round[i] if i < L else None, rnd, L, bsz))
+                        self._put(i, (batch_round[i] if i < L else None, rnd, L, bsz, total))
                     rnd += 1
                 self._wait_rounds(rnd)
                 for net in self.models:

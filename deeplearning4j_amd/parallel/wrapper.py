@@ -169,14 +169,17 @@ class ParallelWrapper:
         DL4J_AMD_PW_SPAWN=1) launches one child process per device instead (parallel/launcher.py: batches are
         streamed to the children over sockets; listeners do not run there). Under torchrun (a process group) every
         rank runs this method on its rank-strided share of the batches."""
-        if not is_dist() and self.workers > 1 and self.trainerContext is None and self.accumulator is None:
-            spawn = self.inProcess is False or (self.inProcess is None and
-                                                os.environ.get("DL4J_AMD_PW_SPAWN", "0") == "1")
+        shared_acc = getattr(self.accumulator, "shared_in_process", False)
+        if not is_dist() and self.workers > 1 and self.trainerContext is None and \
+                (self.accumulator is None or shared_acc):
+            spawn = not shared_acc and (self.inProcess is False or (self.inProcess is None and
+                                                                    os.environ.get("DL4J_AMD_PW_SPAWN", "0") == "1"))
             if spawn:
                 from .launcher import spawn_fit
                 return spawn_fit(self, source, numEpochs)
-            if self.trainingMode not in (TrainingMode.SHARED_GRADIENTS, TrainingMode.AVERAGING):
-                raise ValueError("in-process ParallelWrapper supports SHARED_GRADIENTS and AVERAGING; CUSTOM "
+            if self.trainingMode not in (TrainingMode.SHARED_GRADIENTS, TrainingMode.AVERAGING) and not shared_acc:
+                raise ValueError("in-process ParallelWrapper supports SHARED_GRADIENTS, AVERAGING and CUSTOM "
+                                 "accumulators shared between threads (BasicGradientsAccumulator); other CUSTOM "
                                  "accumulators / trainer contexts need one process per device (torchrun)")
             from .inprocess import InProcessTrainer
             if self._inproc is None:

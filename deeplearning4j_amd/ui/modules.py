@@ -99,7 +99,8 @@ _CSS = ("body{font-family:sans-serif;margin:0;background:#fafafa}nav{background:
         "table{border-collapse:collapse}td,th{border:1px solid #ddd;padding:2px 6px;font-size:12px}"
         ".l{cursor:pointer;color:#1f5fa8}")
 
-_JS_LINE = """function line(el,series,w,h){var xs=[],ys=[];series.forEach(function(s){s.pts.forEach(function(p){
+_JS_LINE = """function E(s){return String(s).replace(/[&<>"']/g,function(c){return '&#'+c.charCodeAt(0)+';'});}
+function line(el,series,w,h){var xs=[],ys=[];series.forEach(function(s){s.pts.forEach(function(p){
 if(p[1]!=null&&isFinite(p[1])){xs.push(p[0]);ys.push(p[1]);}})});if(!xs.length){el.innerHTML='(no data)';return;}
 var x0=Math.min.apply(null,xs),x1=Math.max.apply(null,xs),y0=Math.min.apply(null,ys),y1=Math.max.apply(null,ys);
 if(x1==x0)x1=x0+1;if(y1==y0)y1=y0+1;var svg='<svg width="'+w+'" height="'+h+'">';
@@ -316,7 +317,7 @@ class TrainModule(UIModule):
                   "line(document.getElementById('score'),[{pts:d.score}],720,220);var rs=[];for(var k in d.updateRatios)"
                   "rs.push({name:k,pts:d.updateRatios[k]});line(document.getElementById('ratio'),rs,720,220);"
                   "line(document.getElementById('perf'),[{pts:d.performance}],720,160);var h='';"
-                  f"{spec}.forEach(function(r){{h+='<tr><th>'+r[0]+'</th><td>'+d[r[1]][r[2]]+'</td></tr>';}});"
+                  f"{spec}.forEach(function(r){{h+='<tr><th>'+E(r[0])+'</th><td>'+E(d[r[1]][r[2]])+'</td></tr>';}});"
                   "document.getElementById('tabs').innerHTML=h;});}")
         return _page("train.overview.title", body, script, self.i18n)
 
@@ -403,8 +404,8 @@ class TrainModule(UIModule):
                   "var e=document.createElement('div');h.appendChild(document.createTextNode(k));h.appendChild(e);"
                   "bars(e,d.histograms[k],640,120);}});}"
                   "function load(){J('/train/model/graph').then(function(g){if(!g.vertexNames)return;var h='';"
-                  "g.vertexNames.forEach(function(n,i){h+='<div class=\"l\" onclick=\"show(\\''+n+'\\')\">'+n+' <small>'+"
-                  "g.vertexTypes[i]+'</small></div>';});document.getElementById('layers').innerHTML=h;"
+                  "window._vn=g.vertexNames;g.vertexNames.forEach(function(n,i){h+='<div class=\"l\" onclick=\"show(_vn['+i+'])\">'+"
+                  "E(n)+' <small>'+E(g.vertexTypes[i])+'</small></div>';});document.getElementById('layers').innerHTML=h;"
                   "if(cur==null&&g.layerIds.length)cur=g.layerIds[0];if(cur!=null)show(cur);});}")
         return _page("train.model.title", body, script, self.i18n)
 
@@ -493,8 +494,8 @@ class ConvolutionalListenerModule(UIModule):
 
     def page(self):
         script = ("function load(){J('/activations/data').then(function(d){var h='iteration '+d.iteration;"
-                  "for(var k in d.images)h+='<div class=\"c\"><b>'+k+'</b><br><img style=\"image-rendering:pixelated;"
-                  "width:512px\" src=\"'+d.images[k]+'?t='+Date.now()+'\"></div>';document.getElementById('acts')"
+                  "for(var k in d.images)h+='<div class=\"c\"><b>'+E(k)+'</b><br><img style=\"image-rendering:pixelated;"
+                  "width:512px\" src=\"'+E(d.images[k])+'?t='+Date.now()+'\"></div>';document.getElementById('acts')"
                   ".innerHTML=h;});}")
         return _page("activations.title", '<div id="acts"></div>', script, self.i18n)
 
@@ -550,7 +551,7 @@ class TsneModule(UIModule):
                   "if(y1==y0)y1++;var s='<svg width=\"720\" height=\"480\">';rows.forEach(function(r){var x=20+(r[0]-x0)/"
                   "(x1-x0)*680,y=460-(r[1]-y0)/(y1-y0)*440;s+='<circle cx=\"'+x.toFixed(1)+'\" cy=\"'+y.toFixed(1)+"
                   "'\" r=\"2\" fill=\"#1f77b4\"/><text x=\"'+(x+3).toFixed(1)+'\" y=\"'+y.toFixed(1)+'\" font-size=\"9\">'"
-                  "+r[2]+'</text>';});document.getElementById('plot').innerHTML=s+'</svg>';});}"
+                  "+E(r[2])+'</text>';});document.getElementById('plot').innerHTML=s+'</svg>';});}"
                   "function load(){J('/tsne/sessions').then(function(ss){var e=document.getElementById('ts');"
                   "e.innerHTML='';ss.forEach(function(x){var o=document.createElement('option');o.value=x;o.text=x;"
                   "e.appendChild(o);});e.onchange=function(){draw(e.value)};if(ss.length)draw(ss[0]);});}")

@@ -49,3 +49,31 @@ def test_step_guard_skips_update_and_raises():
     net.fit(b[3])
     torch.cuda.synchronize()
     assert not torch.equal(net.params(), p0)
+
+
+def test_step_guard_reported_without_host_sync():
+    """with the host running ahead of the GPU (no synchronize between steps) the trip must still be
+    reported within the snapshot FIFO's depth, not lost because only the newest snapshot was looked at."""
+    from deeplearning4j_amd import Adam
+    from deeplearning4j_amd.ops import rnn_native
+    rnn_native.USED_COOP[0] = True
+    rnn_native._guard.clear()
+    proto = W.make_net(Adam(0.01))
+    net = type(proto)(proto.conf)
+    net.init(proto.params().clone(), device=torch.device("cuda", 0))
+    b = W.make_batches(2, 8)
+    net.fit(b[0])
+    _set_guard(1)
+    raised = False
+    for i in range(rnn_native._GUARD_DEPTH + 3):
+        try:
+            net.fit(b[i % 2])                        # no torch.cuda.synchronize() between steps
+        except rnn_native.CoopTimeoutError:
+            raised = True
+            break
+    assert raised, "guard trip never reported"
+    torch.cuda.synchronize()
+    p0 = net.params().detach().clone()
+    net.fit(b[0])
+    torch.cuda.synchronize()
+    assert not torch.equal(net.params(), p0)         # cleared: updates apply again

@@ -110,3 +110,58 @@ def test_search_mode_decompounds(trained):
     s = K.LatticeTokenizer(trained, mode=K.Mode.SEARCH).tokenize(text)
     assert "".join(t.surface for t in s) == text
     assert max(len(t.surface) for t in s) <= max(len(t.surface) for t in n) and len(s) >= len(n)
+
+
+def _search_cases():
+    cases = []
+    with open(os.path.join(RES, "search-segmentation-tests.txt"), encoding="utf-8") as fh:
+        for line in fh.read().splitlines():
+            if not line.strip() or line.startswith("#"):
+                continue
+            text, exp = line.split("\t")
+            cases.append((text, exp.split(" ")))
+    return cases
+
+
+@need_res
+def test_search_segmentation_fixture(trained):
+    """Kuromoji's search-segmentation-tests.txt (45 decompounding cases). Its header says the expectations depend on
+    IPADIC, which is not in this image: with the corpus-estimated lexicon the dictionary words the splits need
+    (関西, 国際, ソフトウェア, ...) are unknown, so exact parity is UNPINNED. Pinned here: every case loads and
+    tokenizes in SEARCH mode back to its text; SEARCH mode's penalties are in the lexicon's own cost units, so it
+    does not break unknown katakana runs into arbitrary pieces (span F1 >= NORMAL's); and the measured span F1 does
+    not regress (0.277 at the time of writing)."""
+    cases = _search_cases()
+    assert len(cases) == 45
+    f1 = {}
+    for mode in (K.Mode.NORMAL, K.Mode.SEARCH):
+        tok = K.LatticeTokenizer(trained, mode=mode)
+        tp = fp = fn = 0
+        for text, exp in cases:
+            got = [t.surface for t in tok.tokenize(text)]
+            assert "".join(got) == text
+            a, b = _spans(got), _spans(exp)
+            tp, fp, fn = tp + len(a & b), fp + len(a - b), fn + len(b - a)
+        p, r = tp / (tp + fp), tp / (tp + fn)
+        f1[mode] = 2 * p * r / (p + r)
+    print("search-segmentation span F1:", f1)
+    assert f1[K.Mode.SEARCH] >= f1[K.Mode.NORMAL] - 1e-9
+    assert f1[K.Mode.SEARCH] >= 0.27
+
+
+def test_search_mode_heuristic_on_fixture_case():
+    """The first fixture case with the dictionary words it needs (IPADIC-like costs, penalty scale 1): NORMAL keeps
+    the cheap whole-word entry 関西国際空港, SEARCH's kanji-length penalty ((6 - 2) x 3000) splits it into
+    関西 国際 空港 exactly as the fixture expects."""
+    noun = 1
+    feats = ["名詞", "固有名詞", "組織", "*", "*", "*", "*", "*", "*"]
+    words = {"関西国際空港": 4000, "関西": 3000, "国際": 3000, "空港": 3000}
+    es = [K.Entry(w, noun, noun, c, feats) for w, c in words.items()]
+    lex = K.Lexicon(es, K.ConnectionCosts({(0, 1): 0, (1, 1): 0, (1, 0): 0}, 5000), K.CharacterDefinitions(),
+                    {cat: [K.Entry(cat, noun, noun, 20000, feats, "unknown")] for cat in K._BUILTIN_CATEGORIES})
+    normal = [t.surface for t in K.LatticeTokenizer(lex, mode=K.Mode.NORMAL).tokenize("関西国際空港")]
+    search = [t.surface for t in K.LatticeTokenizer(lex, mode=K.Mode.SEARCH).tokenize("関西国際空港")]
+    assert normal == ["関西国際空港"]
+    assert search == ["関西", "国際", "空港"]
+    if os.path.isdir(RES):
+        assert _search_cases()[0] == ("関西国際空港", search)

@@ -168,3 +168,38 @@ def test_devices_for_refuses_mixed_gpu_cpu_replicas(monkeypatch):
     class C:
         device = torch.device("cpu")
     assert inprocess.devices_for(4, C()) == [torch.device("cpu")] * 4
+
+
+def test_inprocess_short_trailing_batch_keeps_replicas_identical():
+    """a short last batch (3 examples instead of 8) in a partial round. Every replica — trained or idle —
+    divides the summed gradient by the round's total example count (8 + 3), so all replicas apply the same update
+    and equal the large-batch step over the round's 11 examples."""
+    from deeplearning4j_amd import Adam, DataSet
+    net = W.make_net(Adam(0.01))
+    batches = W.make_batches(10, 8)
+    last = batches[9]
+    batches[9] = DataSet(last.features[:3].clone(), last.labels[:3].clone())
+    pw = _pw(net, 4)
+    pw.fit(batches, 1)
+    models = pw._inproc.models
+    for m in models[1:]:
+        assert torch.equal(m.params(), models[0].params())
+    ref = W.make_net(Adam(0.01))
+    for grp in (batches[0:4], batches[4:8], batches[8:10]):
+        ref.fit(DataSet(torch.cat([b.features for b in grp]), torch.cat([b.labels for b in grp])))
+    assert torch.allclose(net.params(), ref.params(), atol=1e-5), (net.params() - ref.params()).abs().max()
+
+
+def test_inprocess_unequal_batches_in_full_round():
+    """A full round whose batches differ in size: the divisor is the round's example total on every replica."""
+    from deeplearning4j_amd import Sgd, DataSet
+    net = W.make_net(Sgd(0.1))
+    b = W.make_batches(2, 8)
+    b[1] = DataSet(b[1].features[:5].clone(), b[1].labels[:5].clone())
+    pw = _pw(net, 2)
+    pw.fit(b, 1)
+    ms = pw._inproc.models
+    assert torch.equal(ms[0].params(), ms[1].params())
+    ref = W.make_net(Sgd(0.1))
+    ref.fit(DataSet(torch.cat([x.features for x in b]), torch.cat([x.labels for x in b])))
+    assert torch.allclose(net.params(), ref.params(), atol=1e-6), (net.params() - ref.params()).abs().max()
