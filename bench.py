@@ -142,12 +142,33 @@ def main():
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}", "comm": args.comm,
                        "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                        "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
-                       "final_score": final_score,
-                       "peak_mem_gib": round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
-                       if device.type == "cuda" else None},
+                       "final_score": final_score, **memory_report(device)},
         }), flush=True)
     from deeplearning4j_amd.parallel.distributed import destroy
     destroy()
+
+
+def memory_report(device):
+    """Peak device memory of the run, counting every allocator: torch's caching allocator (parameters, gradients,
+    updater state, torch-allocated activations) PLUS the engine's own allocator (csrc/engine.hip: the LOOP_FF_BP
+    activation arena and other workspace blocks, which torch does not see), and the device-wide HBM in use at the
+    end (hipMemGetInfo: total - free, i.e. every reservation of this process incl. RCCL / runtime buffers)."""
+    if device.type != "cuda":
+        return {}
+    torch_peak = torch.cuda.max_memory_allocated(device)
+    eng_peak = eng_reserved = 0
+    try:
+        from deeplearning4j_amd.runtime import allocator
+        st = allocator(device.index).stats()
+        eng_peak, eng_reserved = int(st["peak"]), int(st["reserved"])
+    except Exception:
+        pass
+    free, total = torch.cuda.mem_get_info(device)
+    g = 2.0 ** 30
+    return {"peak_mem_gib": round((torch_peak + eng_peak) / g, 2),
+            "peak_mem_torch_gib": round(torch_peak / g, 2), "peak_mem_engine_gib": round(eng_peak / g, 2),
+            "engine_reserved_gib": round(eng_reserved / g, 2), "device_used_gib": round((total - free) / g, 2),
+            "device_total_gib": round(total / g, 1)}
 
 
 def main_inprocess(args):

@@ -29,7 +29,7 @@ struct ConvA {
   int R, S, sh, sw, ph, pw, dh, dw;
 };
 
-template <int DT, int BM, int BN, int WGM, int WGN, int STAGES, bool BNB = false>
+template <int DT, int BM, int BN, int WGM, int WGN, int STAGES, bool BNB = false, bool LEAN = false>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_glds(GemmArgs g, ConvA ca) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -157,6 +157,31 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_glds(GemmArgs g, ConvA 
     }
   }
 
+  if constexpr (LEAN) {
+    // lean epilogue (mfma_tile.h): one 16-bit image of the tile, BN statistics from it, 16-byte row stores
+    static_assert(BM * BN * 2 <= STAGES * SBYTES, "lean image exceeds the operand ring");
+    const int h = lane >> 5;
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+#pragma unroll
+    for (int a = 0; a < FN; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int lc = wn * WTN + 32 * a + 8 * q + 4 * h;
+        float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g.bias_mode == 1 && n0 + lc < g.N) bq = *reinterpret_cast<const float4*>(g.bias + n0 + lc);
+#pragma unroll
+        for (int b = 0; b < FM; ++b)
+          lean_put4<BN>(smem, wm * WTM + 32 * b + (lane & 31), lc, acc[a][b][4 * q] + bq.x, acc[a][b][4 * q + 1] + bq.y,
+                        acc[a][b][4 * q + 2] + bq.z, acc[a][b][4 * q + 3] + bq.w, g.out_dt);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (g.tstats) lean_stats<BM, BN, NW * 64>(g, smem, m0, n0, tid);
+    lean_readout<BM, BN, NW * 64>(g, reinterpret_cast<char*>(g.C), smem, m0, n0, tid);
+    return;
+  }
   // ---- epilogue through LDS (mfma_tile.h epi_readout / epi_stats)
   constexpr int PITCH = BN * 4 + 16;
   constexpr int RPP0 = (STAGES * SBYTES) / PITCH;
@@ -212,22 +237,35 @@ struct TileCfg {
 constexpr int kNumVariants = 5;
 const TileCfg kTiles[kNumVariants] = {{256, 128}, {128, 128}, {256, 64}, {128, 64}, {128, 256}};
 
-template <int DT, bool BNB>
+template <int DT, bool BNB, bool LEAN>
 int launch_conv_t(int v, const GemmArgs& g, const ConvA& ca, hipStream_t s) {
   dim3 grid(g.tiles_m * g.tiles_n);
   switch (v) {
-    case 0: hipLaunchKernelGGL((conv_glds<DT, 256, 128, 4, 2, 3, BNB>), grid, dim3(512), 0, s, g, ca); break;
-    case 1: hipLaunchKernelGGL((conv_glds<DT, 128, 128, 2, 2, 2, BNB>), grid, dim3(256), 0, s, g, ca); break;
-    case 2: hipLaunchKernelGGL((conv_glds<DT, 256, 64, 4, 1, 3, BNB>), grid, dim3(256), 0, s, g, ca); break;
-    case 3: hipLaunchKernelGGL((conv_glds<DT, 128, 64, 2, 2, 3, BNB>), grid, dim3(256), 0, s, g, ca); break;
-    default: hipLaunchKernelGGL((conv_glds<DT, 128, 256, 2, 4, 3, BNB>), grid, dim3(512), 0, s, g, ca); break;
+    case 0: hipLaunchKernelGGL((conv_glds<DT, 256, 128, 4, 2, 3, BNB, LEAN>), grid, dim3(512), 0, s, g, ca); break;
+    case 1: hipLaunchKernelGGL((conv_glds<DT, 128, 128, 2, 2, 2, BNB, LEAN>), grid, dim3(256), 0, s, g, ca); break;
+    case 2: hipLaunchKernelGGL((conv_glds<DT, 256, 64, 4, 1, 3, BNB, LEAN>), grid, dim3(256), 0, s, g, ca); break;
+    case 3: hipLaunchKernelGGL((conv_glds<DT, 128, 64, 2, 2, 3, BNB, LEAN>), grid, dim3(256), 0, s, g, ca); break;
+    default: hipLaunchKernelGGL((conv_glds<DT, 128, 256, 2, 4, 3, BNB, LEAN>), grid, dim3(512), 0, s, g, ca); break;
   }
   return (int)hipGetLastError();
 }
 
+// lean epilogue (mfma_tile.h): plain or biased 16-bit output, optional BN tile statistics; the fan-out beta
+// accumulation and the BN-backward sums keep the generic LDS epilogue
+bool conv_lean_ok(const GemmArgs& g) {
+  static const int off = [] {
+    const char* e = getenv("DL4J_AMD_GEMM_LEAN");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  if (off || g.bnb || g.beta != 0.f || g.act != 0) return false;
+  if (g.bias_mode == 1 && (reinterpret_cast<uintptr_t>(g.bias) & 15)) return false;
+  return (g.N & 7) == 0 && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0;
+}
+
 template <int DT>
 int launch_conv(int v, const GemmArgs& g, const ConvA& ca, hipStream_t s) {
-  return g.bnb ? launch_conv_t<DT, true>(v, g, ca, s) : launch_conv_t<DT, false>(v, g, ca, s);
+  if (g.bnb) return launch_conv_t<DT, true, false>(v, g, ca, s);
+  return conv_lean_ok(g) ? launch_conv_t<DT, false, true>(v, g, ca, s) : launch_conv_t<DT, false, false>(v, g, ca, s);
 }
 
 // Default tile when the host has no timing for the shape: the largest tile whose width fits the channel count and

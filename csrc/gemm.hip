@@ -50,7 +50,7 @@ __device__ unsigned long long* g_gemm_stamps;
 
 namespace {
 
-template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES, bool BNB = false>
+template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES, bool BNB = false, bool LEAN = false>
 __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_glds(GemmArgs g) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -188,6 +188,38 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_gld
     }
   }
 
+  if constexpr (LEAN) {
+    // lean epilogue (mfma_tile.h): acc[a][b] regs 4q..4q+3 <-> tile row wm*WTM + 32b + (lane&31), columns
+    // wn*WTN + 32a + 8q + 4h .. +3
+    static_assert(BM * BN * 2 <= STAGES * SBYTES, "lean image exceeds the operand ring");
+    const int h = lane >> 5;
+    char* dst = reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * 2;
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+#pragma unroll
+    for (int a = 0; a < FN; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int lc = wn * WTN + 32 * a + 8 * q + 4 * h;
+        float4 bq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g.bias_mode == 1 && n0 + lc < g.N) bq = *reinterpret_cast<const float4*>(g.bias + n0 + lc);
+#pragma unroll
+        for (int b = 0; b < FM; ++b) {
+          float v[4] = {acc[a][b][4 * q] * g.alpha + bq.x, acc[a][b][4 * q + 1] * g.alpha + bq.y,
+                        acc[a][b][4 * q + 2] * g.alpha + bq.z, acc[a][b][4 * q + 3] * g.alpha + bq.w};
+          if (g.act == 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          lean_put4<BN>(smem, wm * WTM + 32 * b + (lane & 31), lc, v[0], v[1], v[2], v[3], g.out_dt);
+        }
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (g.tstats) lean_stats<BM, BN, WGM * WGN * 64>(g, smem, m0, n0, tid);
+    lean_readout<BM, BN, WGM * WGN * 64>(g, dst, smem, m0, n0, tid);
+    return;
+  }
   // ---- epilogue through LDS (see epi_readout): acc[a][b] reg e <-> tile column wn*WTN + 32a + (e&3) + 8(e>>2) +
   // 4h, tile row wm*WTM + 32b + (lane&31); passes of RPP rows sized to the operand ring's LDS
   constexpr int PITCH = BN * 4 + 16;
@@ -318,7 +350,7 @@ template <> struct Mfma16<2> {
   }
 };
 
-template <int DT, bool AKC, bool BKC, bool BNB = false>
+template <int DT, bool AKC, bool BKC, bool BNB = false, bool LEAN = false>
 __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   typedef typename MfmaT<DT>::v8 v8;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * 16384 + 8192];   // + pad rows of the epilogue tile
@@ -504,7 +536,38 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
 
   // epilogue (see epi_readout): pass P = wave row wr. acc[nb][mb] reg e <-> tile row wr*128 + (mb>>2)*64 +
   // (mb&3)*16 + (lane&15), tile column wc*64 + (nb>>1)*32 + (nb&1)*16 + (lane>>4)*4 + e.
-  {
+  if constexpr (LEAN) {
+    char* dst = reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * 2;
+    float4 bq[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int lc = wc * 64 + (nb >> 1) * 32 + (nb & 1) * 16 + (lane >> 4) * 4;
+      bq[nb] = (g.bias_mode == 1 && n0 + lc < g.N) ? *reinterpret_cast<const float4*>(g.bias + n0 + lc)
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();                                   // every wave is done reading the operand stages
+    sfor<0, 8>([&](auto MB) {
+      constexpr int mb = decltype(MB)::value;
+      const int lr = wr * 128 + (mb >> 2) * 64 + (mb & 3) * 16 + (lane & 15);
+      sfor<0, 4>([&](auto NB) {
+        constexpr int nb = decltype(NB)::value;
+        const int lc = wc * 64 + (nb >> 1) * 32 + (nb & 1) * 16 + (lane >> 4) * 4;
+        float v[4] = {acc[nb][mb][0] * g.alpha + bq[nb].x, acc[nb][mb][1] * g.alpha + bq[nb].y,
+                      acc[nb][mb][2] * g.alpha + bq[nb].z, acc[nb][mb][3] * g.alpha + bq[nb].w};
+        if (g.act == 1)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        lean_put4<256>(smem, lr, lc, v[0], v[1], v[2], v[3], g.out_dt);
+      });
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    GSTAMP(4);
+    if (g.tstats) lean_stats<256, 256, 512>(g, smem, m0, n0, tid);
+    lean_readout<256, 256, 512>(g, dst, smem, m0, n0, tid);
+    GSTAMP(5);
+  } else {
     const bool split = g.splits > 1;
     EpiOut o;
     o.raw = split;
@@ -517,6 +580,27 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
     constexpr int PITCH = 256 * 4 + 16;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();                                   // every wave is done reading the operand stages
+#ifdef DL4J_EPI_STOREONLY
+    // diagnostic: the read-out's global stores alone (same addresses and widths, values from the accumulators)
+    {
+      const int c = tid % 32, r0 = tid / 32;
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        GSTAMP(4 + 2 * P);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + P * 128 + r0 + 16 * i;
+          uint4 pk;
+          pk.x = __float_as_uint(acc[i & 3][i][0]);
+          pk.y = __float_as_uint(acc[(i + 1) & 3][i][1]);
+          pk.z = pk.x ^ pk.y; pk.w = pk.x + pk.y;
+          if (m < g.M) *reinterpret_cast<uint4*>(o.dst + ((long long)m * o.ld + n0 + c * 8) * 2) = pk;
+        }
+        GSTAMP(5 + 2 * P);
+      }
+    }
+    if (0)
+#endif
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       if (wr == P) {
@@ -532,9 +616,11 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
+      GSTAMP(4 + 2 * P);
       if constexpr (BNB) epi_bnbwd<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
       else if (g.tstats) epi_stats<128, 256, 512>(g, smem, m0 + P * 128, n0, tid);
       epi_readout<128, 256, 512>(g, o, Zp, smem, m0 + P * 128, n0, tid);
+      GSTAMP(5 + 2 * P);
       if (P == 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         raw_barrier();
@@ -630,6 +716,15 @@ __global__ __launch_bounds__(256) void gemm_simple(GemmArgs g, SimpleArgs s) {
 }
 
 // ----------------------------------------------------------------------------------------------- dispatch
+// DL4J_AMD_GEMM_LEAN=0 forces the generic LDS epilogue everywhere (A/B experiments)
+bool lean_disabled() {
+  static const int v = [] {
+    const char* e = getenv("DL4J_AMD_GEMM_LEAN");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 struct Cfg {
   int bm, bn;
 };
@@ -642,19 +737,19 @@ struct Cfg {
 constexpr int kNumCfg = 8;
 const Cfg kCfg[kNumCfg] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}, {128, 64}, {128, 128}, {128, 128}};
 
-template <int DT, bool AKC, bool BKC>
+template <int DT, bool AKC, bool BKC, bool LEAN>
 int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
   const int tiles = g.tiles_m * g.tiles_n;
   dim3 grid(tiles, g.splits, batch);
   switch (cfg) {
-    case 0: hipLaunchKernelGGL((gemm_glds<DT, 256, 256, 2, 4, AKC, BKC, 2>), grid, dim3(512), 0, s, g); break;
-    case 1: hipLaunchKernelGGL((gemm_glds<DT, 256, 128, 4, 2, AKC, BKC, 3>), grid, dim3(512), 0, s, g); break;
-    case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 2>), grid, dim3(256), 0, s, g); break;
-    case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
-    case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 1>), grid, dim3(256), 0, s, g); break;
-    case 6: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 3>), grid, dim3(256), 0, s, g); break;
-    case 7: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 4>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC>), grid, dim3(512), 0, s, g); break;
+    case 0: hipLaunchKernelGGL((gemm_glds<DT, 256, 256, 2, 4, AKC, BKC, 2, false, LEAN>), grid, dim3(512), 0, s, g); break;
+    case 1: hipLaunchKernelGGL((gemm_glds<DT, 256, 128, 4, 2, AKC, BKC, 3, false, LEAN>), grid, dim3(512), 0, s, g); break;
+    case 2: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 2, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 3: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 3, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 1, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 6: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 3, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 7: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 4, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC, false, LEAN>), grid, dim3(512), 0, s, g); break;
   }
   return (int)hipGetLastError();
 }
@@ -675,13 +770,30 @@ int launch_fast_bnb(int cfg, const GemmArgs& g, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+template <int DT, bool LEAN>
+int launch_fast_lay(int cfg, int akc, int bkc, const GemmArgs& g, int batch, hipStream_t s) {
+  if (akc && bkc) return launch_fast<DT, true, true, LEAN>(cfg, g, batch, s);
+  if (akc) return launch_fast<DT, true, false, LEAN>(cfg, g, batch, s);
+  if (bkc) return launch_fast<DT, false, true, LEAN>(cfg, g, batch, s);
+  return launch_fast<DT, false, false, LEAN>(cfg, g, batch, s);
+}
+
 template <int DT>
-int launch_fast_l(int cfg, int akc, int bkc, const GemmArgs& g, int batch, hipStream_t s) {
+int launch_fast_l(int cfg, int akc, int bkc, const GemmArgs& g, int batch, bool lean, hipStream_t s) {
   if (g.bnb) return (akc && !bkc && batch == 1) ? launch_fast_bnb<DT>(cfg, g, s) : -3;
-  if (akc && bkc) return launch_fast<DT, true, true>(cfg, g, batch, s);
-  if (akc) return launch_fast<DT, true, false>(cfg, g, batch, s);
-  if (bkc) return launch_fast<DT, false, true>(cfg, g, batch, s);
-  return launch_fast<DT, false, false>(cfg, g, batch, s);
+  return lean ? launch_fast_lay<DT, true>(cfg, akc, bkc, g, batch, s) : launch_fast_lay<DT, false>(cfg, akc, bkc, g, batch, s);
+}
+
+// The lean epilogue's contract (mfma_tile.h): 16-bit output, alpha + optional per-column bias + none / relu, no
+// beta, no pre-activation, no split-K slabs, 16-byte addressable rows; BN tile statistics from the 16-bit image.
+bool lean_ok(const GemmArgs& g, int batch) {
+  if (g.splits > 1 || g.bnb || g.out_dt == 0 || g.beta != 0.f || g.Z) return false;
+  if (g.tstats && g.act != 0) return false;        // statistics are of the stored pre-activation output
+  if (g.act != 0 && g.act != 1) return false;
+  if (g.bias_mode == 2 || (g.bias_mode == 1 && (reinterpret_cast<uintptr_t>(g.bias) & 15))) return false;
+  if ((g.N & 7) || (g.ldc & 7) || (reinterpret_cast<uintptr_t>(g.C) & 15)) return false;
+  if (batch > 1 && (g.sC & 7)) return false;
+  return !lean_disabled();
 }
 
 // Choose tile config + split-K. The 8-phase 256x256 kernel when it can fill >= half the chip (split-K over >= 8
@@ -812,7 +924,9 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   }
   g.tiles_m = (M + kCfg[cfg].bm - 1) / kCfg[cfg].bm;
   g.tiles_n = (N + kCfg[cfg].bn - 1) / kCfg[cfg].bn;
-  const int e = in_dt == 1 ? launch_fast_l<1>(cfg, akc, bkc, g, batch, s) : launch_fast_l<2>(cfg, akc, bkc, g, batch, s);
+  const bool lean = lean_ok(g, batch);
+  const int e = in_dt == 1 ? launch_fast_l<1>(cfg, akc, bkc, g, batch, lean, s)
+                           : launch_fast_l<2>(cfg, akc, bkc, g, batch, lean, s);
   if (e || splits <= 1) return e;
   const long long total = (long long)M * ((N + 3) / 4);
   long long blocks = (total + 255) / 256;

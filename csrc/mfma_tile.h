@@ -191,6 +191,121 @@ __device__ __forceinline__ void store4(const GemmArgs& g, void* C, void* Z, int 
   }
 }
 
+// ----------------------------------------------------------------------------------------------- lean epilogue
+// The common output case — 16-bit C = act(alpha * acc + bias[col]), act none / relu, no beta, no pre-activation, no
+// statistics, no split-K — leaves the block through ONE 16-bit LDS image of the whole tile ([BM][BN] x 2 bytes, row
+// pitch BN*2, 16-byte chunks XOR-swizzled by row): every wave converts its accumulators in registers and writes
+// 4-column (8-byte) pieces, one barrier, then every thread stores 16-byte row chunks. Half the LDS bytes of the fp32
+// image, one pass instead of two, and little epilogue state: the generic path (epi_readout) kept so many kernel
+// arguments live that the 8-phase kernel spilled 76 SGPRs / 4 VGPRs inside its main loop (measured 37.1k vs 26.9k
+// loop cycles at K = 768 with a minimal epilogue, tools/native/gemm_stamps.hip).
+// Host contract (lean_ok in csrc/gemm.hip): out_dt 1/2, N % 8 == 0, ldc % 8 == 0, 16-byte aligned C, bias 16-byte
+// aligned (or absent), batch strides multiples of 8.
+template <int BN>
+__device__ __forceinline__ int lean_off(int r, int c) {          // byte offset of column c (multiple of 4) of row r
+  return r * (BN * 2) + ((((c >> 3) ^ (r & 7))) << 4) + (c & 7) * 2;
+}
+
+template <int BN>
+__device__ __forceinline__ void lean_put4(char* T, int r, int c, float v0, float v1, float v2, float v3, int dt) {
+  uint2 pk;
+  pk.x = (unsigned)to16(v0, dt) | ((unsigned)to16(v1, dt) << 16);
+  pk.y = (unsigned)to16(v2, dt) | ((unsigned)to16(v3, dt) << 16);
+  *reinterpret_cast<uint2*>(T + lean_off<BN>(r, c)) = pk;
+}
+
+// alpha, per-column bias (4 columns from column n), activation (0 / 1 = relu) on 4 consecutive values
+__device__ __forceinline__ void lean_math4(const GemmArgs& g, int n, float* v) {
+  float b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.bias_mode == 1 && n < g.N) {
+    const float4 q = *reinterpret_cast<const float4*>(g.bias + n);
+    b[0] = q.x; b[1] = q.y; b[2] = q.z; b[3] = q.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = v[j] * g.alpha + b[j];
+    if (g.act == 1) v[j] = fmaxf(v[j], 0.f);
+  }
+}
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void lean_readout(const GemmArgs& g, char* dst, const char* T, int m0, int n0, int tid) {
+  constexpr int CPR = BN / 8;
+  constexpr int RSTEP = NT / CPR;
+  static_assert(NT % CPR == 0 && BM % RSTEP == 0, "lean read-out geometry");
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  if (n >= g.N) return;
+#pragma unroll 4
+  for (int r = r0; r < BM; r += RSTEP) {
+    const int m = m0 + r;
+    const uint4 q = *reinterpret_cast<const uint4*>(T + r * (BN * 2) + ((c ^ (r & 7)) << 4));
+    if (m < g.M) *reinterpret_cast<uint4*>(dst + ((long long)m * g.ldc + n) * 2) = q;
+  }
+}
+
+// BatchNorm tile statistics from the lean 16-bit image (the values exactly as stored): same work split, sums and
+// output planes as epi_stats_wave (below) — one wave per (64-row partial, 64-column slab), lane 16q + c takes
+// columns 4c..4c+3 of rows 16q..16q+15 (8-byte LDS reads), row quarters combined by two xor-shuffles.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void lean_stats(const GemmArgs& g, const char* T, int m0, int n0, int tid) {
+  static_assert(BN % 64 == 0 && BM % 64 == 0, "lean statistics need 64-row / 64-column tiles");
+  constexpr int PARTS = BM / 64, SLABS = BN / 64, NW = NT / 64;
+  const int lane = tid & 63, w = tid >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  const int dt = g.out_dt;
+  auto val = [&](unsigned wv, int j) {
+    const u16 u = (u16)(wv >> (16 * (j & 1)));
+    return dt == 1 ? bf2f(u) : __half2float(__ushort_as_half(u));
+  };
+  for (int item = w; item < PARTS * SLABS; item += NW) {
+    const int part = item / SLABS, slab = item - (item / SLABS) * SLABS;
+    const int rbeg = m0 + part * 64;
+    const long long pidx = rbeg / 64;
+    if (pidx >= g.stats_P) continue;
+    const int rows = min(64, g.M - rbeg);
+    const int col = slab * 64 + 4 * c;
+    const int n = n0 + col;
+    float sh[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    if (rows > 0) {
+      const uint2 y0 = *reinterpret_cast<const uint2*>(T + lean_off<BN>(part * 64, col));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sh[j] = val(j < 2 ? y0.x : y0.y, j);
+      const int r0 = 16 * q;
+      const int rn = rows - r0 < 16 ? (rows - r0 > 0 ? rows - r0 : 0) : 16;
+      uint2 v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        v[r] = *reinterpret_cast<const uint2*>(T + lean_off<BN>(part * 64 + r0 + r, col));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r >= rn) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = val(j < 2 ? v[r].x : v[r].y, j) - sh[j];
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16);
+      s2[j] += __shfl_xor(s2[j], 16);
+      s1[j] += __shfl_xor(s1[j], 32);
+      s2[j] += __shfl_xor(s2[j], 32);
+    }
+    if (q == 0 && n < g.N) {
+      float* p1 = g.tstats + pidx * g.N + n;
+      float* p2 = g.tstats + ((long long)g.stats_P + pidx) * g.N + n;
+      float* p3 = g.tstats + (2LL * g.stats_P + pidx) * g.N + n;
+      *reinterpret_cast<float4*>(p1) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+      *reinterpret_cast<float4*>(p2) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+      *reinterpret_cast<float4*>(p3) = make_float4(sh[0], sh[1], sh[2], sh[3]);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------------------------- LDS epilogue
 // Finished fp32 accumulators leave a block through LDS: pass P, the waves owning tile rows [P*RPP, (P+1)*RPP)
 // store their raw accumulators into an fp32 [RPP][BN] image (row pitch BN*4 + 16 bytes), then every thread takes
@@ -379,6 +494,11 @@ __device__ __forceinline__ void epi_sweep(const GemmArgs& g, const EpiOut& o, vo
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= dgelu(z[j]);
       }
+#ifdef DL4J_EPI_NOSTORE
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(v[j]));
+      continue;
+#endif
       if (storez) store8(reinterpret_cast<char*>(Zp) + off, v);
       if (act == 1) {
 #pragma unroll

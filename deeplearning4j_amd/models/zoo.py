@@ -76,10 +76,14 @@ class _ZooBuilder:
 class ResNet50(ZooModel):
     """variant: "dl4j" (reference zoo graph, default) or "canonical"."""
 
-    def __init__(self, numLabels=1000, seed=123, inputShape=None, variant="dl4j", updater=None, **kw):
+    def __init__(self, numLabels=1000, seed=123, inputShape=None, variant="dl4j", updater=None, weightInit=None,
+                 **kw):
         super().__init__(numLabels, seed, inputShape, **kw)
         self.variant = variant
         self.updater = updater
+        # the reference zoo initialises from N(0, 0.5) (ZOO:model/ResNet50.java), which saturates the random-init
+        # softmax; numerics checks pass e.g. WeightInit.RELU instead
+        self.weightInit = weightInit
 
     def _identity(self, g, k, filters, stage, block, inp):
         conv, bn, act, sc = (f"res{stage}{block}_branch", f"bn{stage}{block}_branch", f"act{stage}{block}_branch",
@@ -118,7 +122,8 @@ class ResNet50(ZooModel):
         upd = self.updater if self.updater is not None else RmsProp(0.1, 0.96, 0.001)
         g = (self._builder().activation(Activation.IDENTITY)
              .optimizationAlgo(OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT)
-             .updater(upd).weightInit(NormalDistribution(0.0, 0.5)).l1(1e-7).l2(5e-5).miniBatch(True)
+             .updater(upd).weightInit(self.weightInit if self.weightInit is not None else NormalDistribution(0.0, 0.5))
+             .l1(1e-7).l2(5e-5).miniBatch(True)
              .convolutionMode(ConvolutionMode.Truncate).graphBuilder())
         g.addInputs("input").setInputTypes(InputType.convolutional(h, w, c))
         g.addLayer("stem-zero", ZeroPaddingLayer.Builder(3, 3).build(), "input")

@@ -21,6 +21,23 @@ KERNEL_LIB = os.path.join(LIBDIR, "libdl4j_amd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libdl4j_amd_runtime.so")
 
 
+def _local_includes(src, seen=None):
+    """Headers a source pulls in with #include "..." (recursively, resolved next to the including file): a
+    source is rebuilt only when one of ITS headers changed."""
+    import re
+    seen = set() if seen is None else seen
+    try:
+        text = open(src).read()
+    except OSError:
+        return seen
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        h = os.path.normpath(os.path.join(os.path.dirname(src), name))
+        if h not in seen and os.path.exists(h):
+            seen.add(h)
+            _local_includes(h, seen)
+    return seen
+
+
 def _newer(src, obj, headers):
     if not os.path.exists(obj):
         return True
@@ -39,14 +56,12 @@ def build_kernels(verbose=True, jobs=None):
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
-    abi_headers = headers + glob.glob(os.path.join(CSRC, "include", "*.h"))   # only csrc/abi.hip includes these
     objs = []
     todo = []
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer(s, o, abi_headers if os.path.basename(s) == "abi.hip" else headers):
+        if _newer(s, o, sorted(_local_includes(s))):
             todo.append((s, o))
     flags = ["-O3", "-fPIC", f"--offload-arch={ARCH}", "-std=c++17", "-munsafe-fp-atomics", "-I", CSRC]
     jobs = jobs or min(8, os.cpu_count() or 4, 16)

@@ -72,6 +72,20 @@ int main(int argc, char** argv) {
          cfg, pro.size(), ms * 1000.f, (rt_max - rt_min) / 100.0, smax / 100.0);
   printf("  cycles  median / max: prologue %.0f / %.0f   loop %.0f / %.0f   epilogue %.0f / %.0f   total %.0f / %.0f\n",
          med(pro), mx(pro), med(loop), mx(loop), med(epi), mx(epi), med(tot), mx(tot));
+  {
+    std::vector<double> w0, r0, w1, r1, drain;
+    for (int b = 0; b < tiles; ++b) {
+      const unsigned long long* p = &h[(size_t)b * 16];
+      if (!p[0]) continue;
+      w0.push_back((double)(p[8] - p[4]));     // pass 0: LDS image write + barrier
+      r0.push_back((double)(p[10] - p[8]));    // pass 0: read-out + stores issued
+      w1.push_back((double)(p[12] - p[10]));   // pass 1: barrier + LDS image write + barrier
+      r1.push_back((double)(p[14] - p[12]));   // pass 1: read-out
+      drain.push_back((double)(p[6] - p[14])); // store drain (vmcnt(0))
+    }
+    printf("  epilogue medians: pass0 lds-write %.0f readout %.0f | pass1 lds-write %.0f readout %.0f | drain %.0f\n",
+           med(w0), med(r0), med(w1), med(r1), med(drain));
+  }
   printf("  implied clock %.2f GHz (median total cycles / median block real time)\n",
          med(tot) / 1e3 / ((rt_max - rt_min) / 100.0));
   return 0;
