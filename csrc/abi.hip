@@ -70,9 +70,18 @@ DL4J_API int dl4j_matmul(const dl4j_tensor_t* A, const dl4j_tensor_t* B, dl4j_te
     if (rc == 0) return 0;
     // any layout the 16-byte DMA kernel cannot address falls through to the exact-fp32 kernel
   }
-  return dl4j_gemm_simple(A->dtype, C->dtype, (int)M, (int)N, (int)K, (int)batch, A->data, A->strides[r], A->strides[c],
-                          sA, B->data, B->strides[r], B->strides[c], sB, C->data, C->strides[r], sC, alpha, beta,
-                          nullptr, 0, 0, nullptr, s) == 0 ? 0 : DL4J_ERR_LAUNCH;
+  int tile = 0, splits = 1;
+  const long long wsb = dl4j_gemm_f32_plan((int)M, (int)N, (int)K, (int)batch, &tile, &splits);
+  float* ws = nullptr;
+  if (wsb > 0 && hipMallocAsync(reinterpret_cast<void**>(&ws), (size_t)wsb, s) != hipSuccess) {
+    ws = nullptr;
+    splits = 1;
+  }
+  const int rc = dl4j_gemm_f32(A->dtype, C->dtype, (int)M, (int)N, (int)K, (int)batch, A->data, A->strides[r],
+                               A->strides[c], sA, B->data, B->strides[r], B->strides[c], sB, C->data, C->strides[r], sC,
+                               alpha, beta, nullptr, 0, 0, nullptr, tile, splits, ws, s);
+  if (ws) (void)hipFreeAsync(ws, s);
+  return rc == 0 ? 0 : DL4J_ERR_LAUNCH;
 }
 
 // ---------------------------------------------------------------------------------------------------- updater

@@ -208,16 +208,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_gld
         for (int b = 0; b < FM; ++b) {
           float v[4] = {acc[a][b][4 * q] * g.alpha + bq.x, acc[a][b][4 * q + 1] * g.alpha + bq.y,
                         acc[a][b][4 * q + 2] * g.alpha + bq.z, acc[a][b][4 * q + 3] * g.alpha + bq.w};
-          if (g.act == 1)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          lean_act4(g, v);
           lean_put4<BN>(smem, wm * WTM + 32 * b + (lane & 31), lc, v[0], v[1], v[2], v[3], g.out_dt);
         }
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
     if (g.tstats) lean_stats<BM, BN, WGM * WGN * 64>(g, smem, m0, n0, tid);
-    lean_readout<BM, BN, WGM * WGN * 64>(g, dst, smem, m0, n0, tid);
+    lean_readout<BM, BN, WGM * WGN * 64>(g, dst, smem, m0, n0, tid,
+                                         g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * 2 : nullptr);
     return;
   }
   // ---- epilogue through LDS (see epi_readout): acc[a][b] reg e <-> tile column wn*WTN + 32a + (e&3) + 8(e>>2) +
@@ -555,9 +554,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
         const int lc = wc * 64 + (nb >> 1) * 32 + (nb & 1) * 16 + (lane >> 4) * 4;
         float v[4] = {acc[nb][mb][0] * g.alpha + bq[nb].x, acc[nb][mb][1] * g.alpha + bq[nb].y,
                       acc[nb][mb][2] * g.alpha + bq[nb].z, acc[nb][mb][3] * g.alpha + bq[nb].w};
-        if (g.act == 1)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        lean_act4(g, v);
         lean_put4<256>(smem, lr, lc, v[0], v[1], v[2], v[3], g.out_dt);
       });
     });
@@ -565,7 +562,8 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
     raw_barrier();
     GSTAMP(4);
     if (g.tstats) lean_stats<256, 256, 512>(g, smem, m0, n0, tid);
-    lean_readout<256, 256, 512>(g, dst, smem, m0, n0, tid);
+    lean_readout<256, 256, 512>(g, dst, smem, m0, n0, tid,
+                                g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * g.sC * 2 : nullptr);
     GSTAMP(5);
   } else {
     const bool split = g.splits > 1;
@@ -715,6 +713,151 @@ __global__ __launch_bounds__(256) void gemm_simple(GemmArgs g, SimpleArgs s) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------- exact fp32, tiled
+// BM x BN x 16 tiles (4 waves as 2 x 2, each (BM/2) x (BN/2) of v_mfma_f32_32x32x2_f32 accumulators: exact fp32
+// products), operands of any dtype / strides converted to fp32 while staging to LDS (two buffers: the next K-step's
+// global loads are issued before the current step's MFMAs), and split-K over grid.y: each split writes its raw fp32
+// tile to a slab and gemm_splitk_reduce applies the epilogue in a fixed order. The one-tile gemm_simple above is the
+// fallback for the smallest problems.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_f32t(GemmArgs g, SimpleArgs s) {
+  constexpr int FM = BM / 64, FN = BN / 64;          // 32x32 accumulators per wave along M / N
+  constexpr int LA = BM * 16 / 256, LB = BN * 16 / 256;   // elements staged per thread per operand
+  __shared__ float As[2][16][BM + 4];
+  __shared__ float Bs[2][16][BN + 4];
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int z = blockIdx.y, bz = blockIdx.z;
+  const int kbeg = z * g.kps, kend = min(g.K, kbeg + g.kps);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const long long aoff = (long long)bz * s.bA, boff = (long long)bz * s.bB;
+  const bool a_mfast = s.sam == 1, b_nfast = s.sbn == 1;
+  f32x16_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  float ra[LA], rb[LB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int e = tid + 256 * u;
+      int kk, r;
+      if (a_mfast) { kk = e / BM; r = e % BM; } else { r = e >> 4; kk = e & 15; }
+      const int m = m0 + r, k = k0 + kk;
+      ra[u] = (m < g.M && k < kend) ? ld_in(s.A, s.in_dt, aoff + m * s.sam + k * s.sak) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = tid + 256 * u;
+      int kk, r;
+      if (b_nfast) { kk = e / BN; r = e % BN; } else { r = e >> 4; kk = e & 15; }
+      const int n = n0 + r, k = k0 + kk;
+      rb[u] = (n < g.N && k < kend) ? ld_in(s.B, s.in_dt, boff + k * s.sbk + n * s.sbn) : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int e = tid + 256 * u;
+      int kk, r;
+      if (a_mfast) { kk = e / BM; r = e % BM; } else { r = e >> 4; kk = e & 15; }
+      As[buf][kk][r] = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int e = tid + 256 * u;
+      int kk, r;
+      if (b_nfast) { kk = e / BN; r = e % BN; } else { r = e >> 4; kk = e & 15; }
+      Bs[buf][kk][r] = rb[u];
+    }
+  };
+  int buf = 0;
+  if (kbeg < kend) {
+    gload(kbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
+    const bool more = k0 + 16 < kend;
+    if (more) gload(k0 + 16);                        // in flight during this step's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < 16; kk += 2) {
+      float a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = As[buf][kk + (lane >> 5)][wm * (BM / 2) + 32 * i + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = Bs[buf][kk + (lane >> 5)][wn * (BN / 2) + 32 * j + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // C/D map of each accumulator: row (m) = (e&3) + 8(e>>2) + 4h, col (n) = lane&31
+  const int h = lane >> 5;
+  const bool split = g.splits > 1;
+  void* C = reinterpret_cast<char*>(g.C) + (long long)bz * s.bC * (g.out_dt == 0 ? 4 : 2);
+  void* Zp = g.Z ? reinterpret_cast<char*>(g.Z) + (long long)bz * s.bC * (g.out_dt == 0 ? 4 : 2) : nullptr;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
+    if (n >= g.N) continue;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        float x = acc[i][j][e];
+        if (split) {
+          g.ws[(long long)z * g.M * g.N + (long long)m * g.N + n] = x;
+          continue;
+        }
+        x *= g.alpha;
+        if (g.bias_mode == 1) x += g.bias[n];
+        else if (g.bias_mode == 2) x += g.bias[m];
+        const long long o = (long long)m * g.ldc + n;
+        if (g.beta != 0.f) x += g.beta * ld_out(C, g.out_dt, o);
+        if (g.act == kActDGelu) {
+          if (Zp) x *= dgelu(ld_out(Zp, g.out_dt, o));
+        } else {
+          if (Zp) {
+            if (g.out_dt == 0) reinterpret_cast<float*>(Zp)[o] = x;
+            else reinterpret_cast<u16*>(Zp)[o] = to16(x, g.out_dt);
+          }
+          x = apply_act(x, g.act);
+        }
+        if (g.out_dt == 0) reinterpret_cast<float*>(C)[o] = x;
+        else reinterpret_cast<u16*>(C)[o] = to16(x, g.out_dt);
+      }
+  }
+}
+
+// tile (64 or 128) and split count for the tiled exact-fp32 kernel: fill the 256 CUs with >= 256-deep K slices
+void plan_f32(int M, int N, int K, int batch, int* tile, int* splits) {
+  const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64) * batch;
+  *tile = (t128 >= 128) ? 128 : 64;
+  const long long t = *tile == 128 ? t128 : t64;
+  int sp = 1;
+  if (batch == 1 && t < 256) {
+    sp = (int)((256 + t - 1) / t);
+    const int maxs = K / 256;
+    if (sp > maxs) sp = maxs;
+    if (sp > 256) sp = 256;
+    if (sp < 1) sp = 1;
+  }
+  *splits = sp;
+}
+
 // ----------------------------------------------------------------------------------------------- dispatch
 // DL4J_AMD_GEMM_LEAN=0 forces the generic LDS epilogue everywhere (A/B experiments)
 bool lean_disabled() {
@@ -784,12 +927,15 @@ int launch_fast_l(int cfg, int akc, int bkc, const GemmArgs& g, int batch, bool 
   return lean ? launch_fast_lay<DT, true>(cfg, akc, bkc, g, batch, s) : launch_fast_lay<DT, false>(cfg, akc, bkc, g, batch, s);
 }
 
-// The lean epilogue's contract (mfma_tile.h): 16-bit output, alpha + optional per-column bias + none / relu, no
-// beta, no pre-activation, no split-K slabs, 16-byte addressable rows; BN tile statistics from the 16-bit image.
+// The lean epilogue's contract (mfma_tile.h): 16-bit output, alpha + optional per-column bias + none / relu / gelu
+// (pre-activation kept in Z or not) / gelu-backward from Z, no beta, no split-K slabs, 16-byte addressable rows; BN
+// tile statistics from the 16-bit image.
 bool lean_ok(const GemmArgs& g, int batch) {
-  if (g.splits > 1 || g.bnb || g.out_dt == 0 || g.beta != 0.f || g.Z) return false;
+  if (g.splits > 1 || g.bnb || g.out_dt == 0 || g.beta != 0.f) return false;
   if (g.tstats && g.act != 0) return false;        // statistics are of the stored pre-activation output
-  if (g.act != 0 && g.act != 1) return false;
+  if (g.act != 0 && g.act != 1 && g.act != 4 && g.act != kActDGelu) return false;
+  if (g.act == kActDGelu && !g.Z) return false;
+  if (g.Z && ((g.act != 4 && g.act != kActDGelu) || (reinterpret_cast<uintptr_t>(g.Z) & 15))) return false;
   if (g.bias_mode == 2 || (g.bias_mode == 1 && (reinterpret_cast<uintptr_t>(g.bias) & 15))) return false;
   if ((g.N & 7) || (g.ldc & 7) || (reinterpret_cast<uintptr_t>(g.C) & 15)) return false;
   if (batch > 1 && (g.sC & 7)) return false;
@@ -927,6 +1073,52 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   const bool lean = lean_ok(g, batch);
   const int e = in_dt == 1 ? launch_fast_l<1>(cfg, akc, bkc, g, batch, lean, s)
                            : launch_fast_l<2>(cfg, akc, bkc, g, batch, lean, s);
+  if (e || splits <= 1) return e;
+  const long long total = (long long)M * ((N + 3) / 4);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g);
+  return (int)hipGetLastError();
+}
+
+// Tiled exact-fp32 path (gemm_f32t): workspace bytes for the split-K slabs of (M, N, K, batch); *tile, *splits out.
+DL4J_API long long dl4j_gemm_f32_plan(int M, int N, int K, int batch, int* tile, int* splits) {
+  plan_f32(M, N, K, batch, tile, splits);
+  if (*splits <= 1) return 0;
+  int kps = (K + *splits - 1) / *splits;
+  kps = (kps + 15) / 16 * 16;
+  *splits = (K + kps - 1) / kps;
+  return *splits > 1 ? (long long)(*splits) * M * N * 4 : 0;
+}
+
+// Any dtype (0 f32 / 1 bf16 / 2 f16 input), any element strides, exact fp32 MFMA products, BM x BN tiles + split-K.
+// tile: 64 or 128 (<= 0: planned); splits > 1 needs ws (dl4j_gemm_f32_plan bytes).
+DL4J_API int dl4j_gemm_f32(int in_dt, int out_dt, int M, int N, int K, int batch, const void* A, long long sam,
+                           long long sak, long long sA, const void* B, long long sbk, long long sbn, long long sB,
+                           void* C, long long ldc, long long sC, float alpha, float beta, const float* bias,
+                           int bias_mode, int act, void* Z, int tile, int splits, float* ws, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (tile <= 0) plan_f32(M, N, K, batch, &tile, &splits);
+  if (batch > 1 || splits < 1) splits = 1;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + 15) / 16 * 16;
+  if (kps < 16) kps = 16;
+  splits = (K + kps - 1) / kps;
+  if (splits < 1) splits = 1;
+  if (splits > 1 && !ws) return -2;
+  GemmArgs g = {};
+  g.C = C; g.Z = Z; g.bias = bias; g.ldc = ldc; g.M = M; g.N = N; g.K = K; g.ws = ws;
+  g.kps = splits > 1 ? kps : (K > 0 ? K : 16);
+  g.splits = splits;
+  g.alpha = alpha; g.beta = beta; g.bias_mode = bias ? bias_mode : 0; g.act = act; g.out_dt = out_dt;
+  SimpleArgs sa;
+  sa.A = A; sa.B = B; sa.sam = sam; sa.sak = sak; sa.sbk = sbk; sa.sbn = sbn;
+  sa.bA = sA; sa.bB = sB; sa.bC = sC; sa.in_dt = in_dt;
+  const int tiles = tile == 128 ? ((M + 127) / 128) * ((N + 127) / 128) : ((M + 63) / 64) * ((N + 63) / 64);
+  dim3 grid(tiles, splits, batch);
+  if (tile == 128) hipLaunchKernelGGL((gemm_f32t<128, 128>), grid, dim3(256), 0, s, g, sa);
+  else hipLaunchKernelGGL((gemm_f32t<64, 64>), grid, dim3(256), 0, s, g, sa);
+  int e = (int)hipGetLastError();
   if (e || splits <= 1) return e;
   const long long total = (long long)M * ((N + 3) / 4);
   long long blocks = (total + 255) / 256;

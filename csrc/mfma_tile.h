@@ -214,6 +214,17 @@ __device__ __forceinline__ void lean_put4(char* T, int r, int c, float v0, float
   *reinterpret_cast<uint2*>(T + lean_off<BN>(r, c)) = pk;
 }
 
+// activation applied by the lean writer: relu, or GELU when no pre-activation is kept (with Z the read-out applies it)
+__device__ __forceinline__ void lean_act4(const GemmArgs& g, float* v) {
+  if (g.act == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+  } else if (g.act == 4 && g.Z == nullptr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+  }
+}
+
 // alpha, per-column bias (4 columns from column n), activation (0 / 1 = relu) on 4 consecutive values
 __device__ __forceinline__ void lean_math4(const GemmArgs& g, int n, float* v) {
   float b[4] = {0.f, 0.f, 0.f, 0.f};
@@ -228,19 +239,78 @@ __device__ __forceinline__ void lean_math4(const GemmArgs& g, int n, float* v) {
   }
 }
 
+// Read-out of the lean image: 16-byte row chunks to C. With a pre-activation buffer Z: act GELU stores the image (the
+// rounded pre-activation) to Z and gelu(Z) to C; act DGELU multiplies the image by gelu'(Z) read from Z (loads for 4
+// rows issued before their stores). Both match the library-product + elementwise-kernel numerics (the elementwise
+// pass reads the rounded product).
 template <int BM, int BN, int NT>
-__device__ __forceinline__ void lean_readout(const GemmArgs& g, char* dst, const char* T, int m0, int n0, int tid) {
+__device__ __forceinline__ void lean_readout(const GemmArgs& g, char* dst, const char* T, int m0, int n0, int tid,
+                                             char* zdst = nullptr) {
   constexpr int CPR = BN / 8;
   constexpr int RSTEP = NT / CPR;
-  static_assert(NT % CPR == 0 && BM % RSTEP == 0, "lean read-out geometry");
+  constexpr int ITER = BM / RSTEP;
+  constexpr int GROUP = ITER < 4 ? ITER : 4;
+  static_assert(NT % CPR == 0 && BM % RSTEP == 0 && ITER % GROUP == 0, "lean read-out geometry");
   const int c = tid % CPR, r0 = tid / CPR;
   const int n = n0 + c * 8;
   if (n >= g.N) return;
+  const int dt = g.out_dt;
+  const int zmode = zdst == nullptr ? 0 : (g.act == kActDGelu ? 2 : 1);
+  auto unpack = [&](const uint4& q, float* v) {
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u16 u = (u16)(w[j >> 1] >> (16 * (j & 1)));
+      v[j] = dt == 1 ? bf2f(u) : __half2float(__ushort_as_half(u));
+    }
+  };
+  auto pack = [&](const float* v) {
+    uint4 q;
+    q.x = (unsigned)to16(v[0], dt) | ((unsigned)to16(v[1], dt) << 16);
+    q.y = (unsigned)to16(v[2], dt) | ((unsigned)to16(v[3], dt) << 16);
+    q.z = (unsigned)to16(v[4], dt) | ((unsigned)to16(v[5], dt) << 16);
+    q.w = (unsigned)to16(v[6], dt) | ((unsigned)to16(v[7], dt) << 16);
+    return q;
+  };
+  if (zmode == 0) {
 #pragma unroll 4
-  for (int r = r0; r < BM; r += RSTEP) {
-    const int m = m0 + r;
-    const uint4 q = *reinterpret_cast<const uint4*>(T + r * (BN * 2) + ((c ^ (r & 7)) << 4));
-    if (m < g.M) *reinterpret_cast<uint4*>(dst + ((long long)m * g.ldc + n) * 2) = q;
+    for (int r = r0; r < BM; r += RSTEP) {
+      const int m = m0 + r;
+      const uint4 q = *reinterpret_cast<const uint4*>(T + r * (BN * 2) + ((c ^ (r & 7)) << 4));
+      if (m < g.M) *reinterpret_cast<uint4*>(dst + ((long long)m * g.ldc + n) * 2) = q;
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int G = 0; G < ITER; G += GROUP) {
+    uint4 zq[GROUP];
+#pragma unroll
+    for (int i = 0; i < GROUP; ++i) {
+      const int m = m0 + r0 + (G + i) * RSTEP;
+      zq[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (zmode == 2 && m < g.M) zq[i] = *reinterpret_cast<const uint4*>(zdst + ((long long)m * g.ldc + n) * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < GROUP; ++i) {
+      const int r = r0 + (G + i) * RSTEP;
+      const int m = m0 + r;
+      const uint4 q = *reinterpret_cast<const uint4*>(T + r * (BN * 2) + ((c ^ (r & 7)) << 4));
+      if (m >= g.M) continue;
+      const long long off = ((long long)m * g.ldc + n) * 2;
+      float v[8];
+      unpack(q, v);
+      if (zmode == 1) {
+        *reinterpret_cast<uint4*>(zdst + off) = q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+      } else {
+        float z[8];
+        unpack(zq[i], z);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= dgelu(z[j]);
+      }
+      *reinterpret_cast<uint4*>(dst + off) = pack(v);
+    }
   }
 }
 

@@ -44,16 +44,22 @@ def _lib():
         lib.dl4j_gemm.restype = I
         lib.dl4j_gemm_simple.argtypes = [I, I, I, I, I, I, V, LL, LL, LL, V, LL, LL, LL, V, LL, LL, F, F, V, I, I, V, V]
         lib.dl4j_gemm_simple.restype = I
+        lib.dl4j_gemm_f32_plan.argtypes = [I, I, I, I, _c.POINTER(I), _c.POINTER(I)]
+        lib.dl4j_gemm_f32_plan.restype = LL
+        lib.dl4j_gemm_f32.argtypes = [I, I, I, I, I, I, V, LL, LL, LL, V, LL, LL, LL, V, LL, LL, F, F, V, I, I, V, I, I,
+                                      V, V]
+        lib.dl4j_gemm_f32.restype = I
         _sig_done[0] = True
     return lib
 
 
 _TUNED = {}                                            # problem key -> (cfg, splits), filled by _autotune
 _TUNE = os.environ.get("DL4J_AMD_GEMM_TUNE", "1") == "1"
-# Plain products (no activation epilogue, no pre-activation / BN-statistics outputs, output in the operand dtype) also
-# time hipBLASLt (torch.mm / addmm / bmm on the same stream) as one more autotuner candidate: the fused-epilogue
-# GEMMs stay on the in-tree kernels, a library GEMM is used only where it measured faster.
-_LIB = os.environ.get("DL4J_AMD_GEMM_LIB", "1") == "1"
+# Opt-in (DL4J_AMD_GEMM_LIB=1): hipBLASLt (torch.mm / addmm / bmm on the same stream, plus an in-tree elementwise
+# kernel for an activation epilogue) as one more autotuner candidate, used where it measured faster. Off by default:
+# every product runs on the in-tree MFMA kernels, and a library pick is counted as a helper fallback
+# (ops/fallback.py, helperCountFail()).
+_LIB = os.environ.get("DL4J_AMD_GEMM_LIB", "0") == "1"
 LIB_CFG = (-2, 1)
 _F32_FORCE = None        # tests: True / False pins fp32 products to the library / the exact-fp32 kernel
 
@@ -357,6 +363,8 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
                 if _TUNE and not torch.cuda.is_current_stream_capturing():
                     cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None, zz=z)
                     _TUNED[key] = cfg
+        if cfg == LIB_CFG:
+            fallback.record("gemm", "library GEMM (hipBLASLt) picked by the autotuner (DL4J_AMD_GEMM_LIB=1)")
         rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
     if rc == -1:
         # exact-fp32 MFMA kernel: any dtype / strides
@@ -367,15 +375,19 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
             sam, sak = A_.stride(-2), A_.stride(-1)
             sbk, sbn = B_.stride(-2), B_.stride(-1)
 
+        # tiled split-K exact-fp32 kernel (64/128 tiles, slabs from torch's allocator; reduce applies the epilogue)
+        tile, nsp = _c.c_int(0), _c.c_int(1)
+        wsb = lib.dl4j_gemm_f32_plan(Mx, Nx, K, batch, _c.byref(tile), _c.byref(nsp))
+        ws32 = torch.empty(wsb // 4, dtype=torch.float32, device=c_t.device) if wsb > 0 else None
+
         def simple(dst, bt):
-            return lib.dl4j_gemm_simple(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), sam, sak, sA_, _p(B_), sbk,
-                                        sbn, sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc, _p(z),
-                                        _stream())
+            return lib.dl4j_gemm_f32(in_dt, _DT[out_dtype], Mx, Nx, K, batch, _p(A_), sam, sak, sA_, _p(B_), sbk,
+                                     sbn, sB_, _p(dst), ldc, sC, float(alpha), bt, _p(bias), bmode, actc, _p(z),
+                                     tile.value, nsp.value, _p(ws32), _stream())
         run = simple
         if in_dt == 0 and not (bias is not None and bias_in is None):
-            # fp32 operands: the exact-fp32 kernel has one 64x64 tile and no split-K, so a long-K weight gradient
-            # (LeNet conv1: K = 36864 output pixels onto a 20 x 25 tile) is one serial workgroup; the fp32 library
-            # GEMM (exact fp32, no TF32) is the second candidate, timed per shape like the 16-bit configurations
+            # fp32 operands with DL4J_AMD_GEMM_LIB=1: the fp32 library GEMM (exact fp32, no TF32) is a second
+            # candidate, timed per shape like the 16-bit configurations (counted as a fallback when picked)
             libmm = _lib_gemm(a, b, c_t, swap, batched, bias_in, bias_dim, act, alpha, beta, z, out_dtype)
             if libmm is not None:
                 k32 = ("f32", Mx, Nx, K, batch, swap, sam, sak, sbk, sbn, ldc, bias_in is not None, beta != 0.0, act,
@@ -392,6 +404,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
                         _TUNED[k32] = use_lib
                 if use_lib:
                     run = libmm
+                    fallback.record("gemm", "fp32 library GEMM (hipBLASLt) picked by the autotuner")
         rc = run(c_t, float(beta))
     if rc != 0:
         raise RuntimeError(f"HIP gemm failed with code {rc} (M={M} N={N} K={K} batch={batch})")

@@ -251,7 +251,10 @@ def test_library_candidate(case, monkeypatch):
     after the library product (GELU with the pre-activation kept, ReLU, the GELU-backward product)."""
     torch.manual_seed(4)
     M, N, K = 384, 320, 256
+    monkeypatch.setattr(gemm, "_LIB", True)                  # opt-in (DL4J_AMD_GEMM_LIB=1)
     monkeypatch.setattr(gemm, "_FORCE_CFG", gemm.LIB_CFG)
+    from deeplearning4j_amd.ops import fallback
+    n0 = fallback.count("gemm")
     a = _mk((M, K), torch.bfloat16)
     b = _mk((K, N), torch.bfloat16, contig_last=False)
     if case == "plain":
@@ -290,6 +293,7 @@ def test_library_candidate(case, monkeypatch):
         out = gemm.mmul(a3, b3)
         ref = torch.stack([a3[i].float() @ b3[i].float() for i in range(3)])
         assert (out.float() - ref).abs().max() <= _tol(torch.bfloat16, K) * ref.abs().max()
+    assert fallback.count("gemm") > n0, "a library pick must be counted as a helper fallback"
     c16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     assert gemm._lib_gemm(a, b, c16, False, False, None, 1, "gelu", 1.0, 1.0, None, torch.bfloat16) is None
     assert gemm._lib_gemm(a, b, c16, False, False, torch.zeros(M, device=DEV, dtype=torch.bfloat16), 0, None, 1.0,
@@ -306,6 +310,7 @@ def test_fp32_library_candidate(case, force, monkeypatch):
     compute the same product to fp32 accuracy for every form; the long-K weight-gradient shape of LeNet conv1
     (K = 36864 onto a 20 x 25 output, one 64x64 tile) is dispatched to the library by the measurement."""
     torch.manual_seed(9)
+    monkeypatch.setattr(gemm, "_LIB", True)                  # opt-in (DL4J_AMD_GEMM_LIB=1)
     monkeypatch.setattr(gemm, "_F32_FORCE", force)
     M, N, K = (20, 25, 36864) if case == "long_k" else (300, 200, 160)
     a = torch.randn(M, K, device=DEV)
@@ -329,9 +334,25 @@ def test_fp32_library_candidate(case, force, monkeypatch):
         out = gemm.mmul(a3, b3)
         ref = a3.double() @ b3.double()
     assert (out.double() - ref).abs().max().item() <= tol, case
-    if case == "long_k" and not force:
-        monkeypatch.setattr(gemm, "_F32_FORCE", None)
-        gemm._TUNED.clear()
-        gemm.mmul(a, b, out=out)
-        picked = [v for k, v in gemm._TUNED.items() if k[0] == "f32" and k[1:4] in ((M, N, K), (N, M, K))]
-        assert picked == [True], picked
+
+
+@pytest.mark.parametrize("shape", [(20, 25, 36864), (300, 200, 160), (512, 1000, 2048), (2048, 1000, 512),
+                                   (64, 64, 16), (1, 7, 3)])
+def test_fp32_tiled_split_k_kernel(shape):
+    """The in-tree exact-fp32 path (gemm_f32t: 64/128 tiles, split-K slabs + fixed-order reduce) against fp64 on the
+    shapes that used to need the library: LeNet conv1's weight gradient (K = 36864 onto 20 x 25), the ResNet FC
+    products, and tiny / ragged edges; the library candidate is off (default), so no fallback is counted."""
+    from deeplearning4j_amd.ops import fallback
+    torch.manual_seed(2)
+    M, N, K = shape
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    n0 = fallback.count()
+    out = gemm.mmul(a, b)
+    ref = a.double() @ b.double()
+    tol = 1e-4 * ref.abs().max().item() + 1e-5 * K ** 0.5
+    assert (out.double() - ref).abs().max().item() <= tol
+    bias = torch.randn(N, device=DEV)
+    out2 = gemm.mmul(a.t().contiguous().t(), b, bias=bias, act="relu")
+    assert (out2.double() - torch.relu(ref + bias.double())).abs().max().item() <= tol
+    assert fallback.count() == n0
