@@ -12,7 +12,8 @@ one-hot labels (BenchmarkDataSetIterator semantics: one fixed random batch, re-f
 iteration: forward, backward, (DP) gradient all-reduce, fused RmsProp update of all 25.6M params.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU, RCCL).
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU, RCCL), or
+plain ``python bench.py --gpus N`` for the in-process ParallelWrapper (one host thread per GPU, ncclCommInitAll).
 """
 import argparse
 import json
@@ -46,12 +47,15 @@ def main():
     ap.add_argument("--comm", default=os.environ.get("BENCH_COMM", "torch"), choices=["torch", "rccl"],
                     help="N > 1 transport: torch.distributed's RCCL process group, or the framework's own RCCL "
                          "communicator (parallel/rccl.py, ncclCommInitRank with the id exchanged through the store)")
-    ap.add_argument("--inprocess", action="store_true",
+    ap.add_argument("--inprocess", type=int, default=-1,
                     help="one process, one host thread per GPU (ParallelWrapper.inProcess: replicas on GPUs 0..N-1, "
-                         "RCCL communicators from ncclCommInitAll, graph-captured steps per worker); ignored under "
-                         "torchrun")
+                         "RCCL communicators from ncclCommInitAll, graph-captured steps per worker). Default (-1): on "
+                         "whenever --gpus N > 1 is run WITHOUT torchrun (the reference's ParallelWrapper design); "
+                         "1 forces it (also at N = 1), 0 disables it. Ignored under torchrun (WORLD_SIZE set), which "
+                         "runs one process per GPU over torch.distributed's RCCL group")
     args = ap.parse_args()
-    if args.inprocess and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+    under_torchrun = "WORLD_SIZE" in os.environ
+    if not under_torchrun and (args.inprocess == 1 or (args.inprocess < 0 and args.gpus > 1)):
         return main_inprocess(args)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -227,7 +231,7 @@ def main_inprocess(args):
                    "comm": "rccl (ncclCommInitAll)",
                    "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                    "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
-                   "final_score": net.score()},
+                   "final_score": net.score(), **memory_report(dev0)},
     }), flush=True)
 
 

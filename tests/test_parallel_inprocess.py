@@ -203,3 +203,27 @@ def test_inprocess_unequal_batches_in_full_round():
     ref = W.make_net(Sgd(0.1))
     ref.fit(DataSet(torch.cat([x.features for x in b]), torch.cat([x.labels for x in b])))
     assert torch.allclose(net.params(), ref.params(), atol=1e-6), (net.params() - ref.params()).abs().max()
+
+
+def test_inprocess_eight_workers_bucketed_equals_large_batch():
+    """8 worker threads (the 8-GPU node's thread-per-device layout) through the real in-process code path: round-robin
+    feed, per-worker replicas, the bucketed all-reduce accumulator with a small bucket size (several buckets issued
+    during backward) over the host loopback communicator. Every round equals one large-batch step over the round's 8
+    batches, and all 8 replicas end bit-identical."""
+    from deeplearning4j_amd import Adam, DataSet
+    from deeplearning4j_amd.parallel import ParallelWrapper
+    net = W.make_net(Adam(0.01))
+    batches = W.make_batches(16, 4)
+    pw = ParallelWrapper.Builder(net).workers(8).inProcess(True).bucketSizeMB(1e-4).build()
+    pw.fit(batches, 1)
+    ms = pw._inproc.models
+    assert len(ms) == 8
+    for m in ms[1:]:
+        assert torch.equal(m.params(), ms[0].params())
+    acc = ms[0].gradientsAccumulator
+    assert acc._buckets is not None and len(acc._buckets) > 1, "expected several gradient buckets"
+    ref = W.make_net(Adam(0.01))
+    for i in range(0, 16, 8):
+        grp = batches[i:i + 8]
+        ref.fit(DataSet(torch.cat([b.features for b in grp]), torch.cat([b.labels for b in grp])))
+    assert torch.allclose(net.params(), ref.params(), atol=1e-5), (net.params() - ref.params()).abs().max()
