@@ -326,6 +326,7 @@ DL4J_API int dl4j_conv_fwd_v3(int dt, const void* X, const void* Wkrsc, const fl
   g.tiles_m = (int)((M + kTiles[variant].bm - 1) / kTiles[variant].bm);
   g.tiles_n = (K + kTiles[variant].bn - 1) / kTiles[variant].bn;
   g.coalesce = 1;                                   // K % 8 == 0 and a 16-byte aligned Y: 16-byte row stores
+  g.store_nt = store_nt_for(M * K * 2);
   g.tstats = tstats;
   g.stats_P = tstats ? (int)((M + 63) / 64) : 0;
   if (tstats && bnb_armed().mode) {                 // BN-backward sums of dX (stride-1 bwd-data as a transposed conv)

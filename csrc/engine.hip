@@ -261,6 +261,42 @@ RT_API int dl4j_rt_stream_create(int dev, int high_priority, void** out) {
   *out = (void*)s;
   return rc(e);
 }
+// Stream restricted to `ncu` of the device's CUs (hardware queue CU mask), spread evenly over the CU index range so
+// every XCD / shader engine keeps the same share whichever way the mask bits map onto them. Used for the
+// weight-gradient side stream: its long-running blocks then never occupy the remaining CUs, so the short, latency-
+// critical kernels of the main chain (BatchNorm folds, elementwise passes) start at once instead of queueing behind
+// them. ncu <= 0 or >= the CU count: an unmasked stream.
+RT_API int dl4j_rt_stream_create_cumask(int dev, int ncu, void** out) {
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return -1;
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) return -1;
+  hipDeviceProp_t p;
+  hipError_t e = hipGetDeviceProperties(&p, dev);
+  hipStream_t s = nullptr;
+  if (e == hipSuccess) {
+    const int n = p.multiProcessorCount;
+    if (ncu <= 0 || ncu >= n) {
+      e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    } else {
+      uint32_t mask[64] = {0};
+      const int words = (n + 31) / 32 < 64 ? (n + 31) / 32 : 64;
+      for (int i = 0; i < n && i < 64 * 32; ++i)
+        if ((long long)(i + 1) * ncu / n > (long long)i * ncu / n) mask[i >> 5] |= 1u << (i & 31);
+      e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+    }
+  }
+  if (cur != dev) (void)hipSetDevice(cur);
+  *out = (void*)s;
+  return rc(e);
+}
+// number of CUs enabled in a stream's mask (the whole device for an unmasked stream)
+RT_API int dl4j_rt_stream_cu_count(void* s) {
+  uint32_t mask[64] = {0};
+  if (hipExtStreamGetCUMask((hipStream_t)s, 64, mask) != hipSuccess) return -1;
+  int c = 0;
+  for (int i = 0; i < 64; ++i) c += __builtin_popcount(mask[i]);
+  return c;
+}
 RT_API int dl4j_rt_stream_destroy(void* s) { return rc(hipStreamDestroy((hipStream_t)s)); }
 RT_API int dl4j_rt_stream_sync(void* s) { return rc(hipStreamSynchronize((hipStream_t)s)); }
 RT_API int dl4j_rt_stream_query(void* s) {

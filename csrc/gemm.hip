@@ -50,16 +50,24 @@ __device__ unsigned long long* g_gemm_stamps;
 
 namespace {
 
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+// LDS bytes of a gemm_glds instantiation: the operand ring, grown where a single-stage wide tile's epilogue image
+// (lean: [BM][BN] 16-bit; generic: >= 64 rows of fp32 at pitch BN*4+16) is larger than the ring
+constexpr int glds_smem(int BM, int BN, int STAGES) {
+  return cmax(STAGES * (BM + BN) * 128, cmax(BM * BN * 2, 64 * (BN * 4 + 16)));
+}
+
 template <int DT, int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int STAGES, bool BNB = false, bool LEAN = false>
-__global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_glds(GemmArgs g) {
+__global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 && WGM * WGN == 4 ? 4 : 2)) void gemm_glds(GemmArgs g) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int FM = WTM / 32, FN = WTN / 32;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128, SBYTES = ABYTES + BBYTES;
+  constexpr int SMEM = glds_smem(BM, BN, STAGES);
   constexpr int NIA = BM / 8 / NW, NIB = BN / 8 / NW;     // 1-KB DMA instructions per wave per stage
   static_assert(NIA * NW * 8 == BM && NIB * NW * 8 == BN, "tile / wave count mismatch");
   typedef typename MfmaT<DT>::v8 v8;
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * SBYTES];
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int per_group = 8 * g.tiles_n;
   const int bid = xcd_remap_g(blockIdx.x, gridDim.x);
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_gld
   if constexpr (LEAN) {
     // lean epilogue (mfma_tile.h): acc[a][b] regs 4q..4q+3 <-> tile row wm*WTM + 32b + (lane&31), columns
     // wn*WTN + 32a + 8q + 4h .. +3
-    static_assert(BM * BN * 2 <= STAGES * SBYTES, "lean image exceeds the operand ring");
+    static_assert(BM * BN * 2 <= SMEM, "lean image exceeds the block's LDS");
     const int h = lane >> 5;
     char* dst = reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * 2;
     wait_vm<0>();
@@ -222,7 +230,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 ? 4 : 2)) void gemm_gld
   // ---- epilogue through LDS (see epi_readout): acc[a][b] reg e <-> tile column wn*WTN + 32a + (e&3) + 8(e>>2) +
   // 4h, tile row wm*WTM + 32b + (lane&31); passes of RPP rows sized to the operand ring's LDS
   constexpr int PITCH = BN * 4 + 16;
-  constexpr int RPP0 = (STAGES * SBYTES) / PITCH;
+  constexpr int RPP0 = SMEM / PITCH;
   constexpr int RPP = RPP0 >= BM ? BM : (RPP0 >= BM / 2 ? BM / 2 : (RPP0 >= BM / 4 ? BM / 4 : 64));
   static_assert(RPP >= 64 && RPP % 64 == 0, "epilogue pass too small");
   const int h = lane >> 5;
@@ -860,6 +868,7 @@ void plan_f32(int M, int N, int K, int batch, int* tile, int* splits) {
 
 // ----------------------------------------------------------------------------------------------- dispatch
 // DL4J_AMD_GEMM_LEAN=0 forces the generic LDS epilogue everywhere (A/B experiments)
+
 bool lean_disabled() {
   static const int v = [] {
     const char* e = getenv("DL4J_AMD_GEMM_LEAN");
@@ -877,8 +886,12 @@ struct Cfg {
 //          5 = 128x64 single-buffered (24 KB LDS, up to 4 blocks/CU: memory-bound skinny / small-K shapes)
 //          6 = 128x128 3 stages (96 KB, 1 block/CU: two K-tiles in flight across each barrier instead of one)
 //          7 = 128x128 4 stages (128 KB: three K-tiles in flight) — latency-bound small-grid / split-K shapes
-constexpr int kNumCfg = 8;
-const Cfg kCfg[kNumCfg] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256}, {128, 64}, {128, 128}, {128, 128}};
+//          8 = 128x128 single-buffered (32 KB, 4 blocks/CU), 9 = 128x256 single-buffered (8 waves, 64 KB, 2 blocks/CU):
+//              short-K, output-heavy products (the expanding 1x1 convolutions: K = 64..256, N = 256..1024), where
+//              a wide tile loads each A row panel once for more output columns and halves the blocks per output
+constexpr int kNumCfg = 10;
+const Cfg kCfg[kNumCfg] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256},
+                           {128, 64},  {128, 128}, {128, 128}, {128, 128}, {128, 256}};
 
 template <int DT, bool AKC, bool BKC, bool LEAN>
 int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
@@ -892,6 +905,8 @@ int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
     case 5: hipLaunchKernelGGL((gemm_glds<DT, 128, 64, 2, 2, AKC, BKC, 1, false, LEAN>), grid, dim3(256), 0, s, g); break;
     case 6: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 3, false, LEAN>), grid, dim3(256), 0, s, g); break;
     case 7: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 4, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 8: hipLaunchKernelGGL((gemm_glds<DT, 128, 128, 2, 2, AKC, BKC, 1, false, LEAN>), grid, dim3(256), 0, s, g); break;
+    case 9: hipLaunchKernelGGL((gemm_glds<DT, 128, 256, 2, 4, AKC, BKC, 1, false, LEAN>), grid, dim3(512), 0, s, g); break;
     default: hipLaunchKernelGGL((gemm_8ph<DT, AKC, BKC, false, LEAN>), grid, dim3(512), 0, s, g); break;
   }
   return (int)hipGetLastError();
@@ -1051,6 +1066,7 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   g.tstats = nullptr;
   g.stats_P = 0;
   g.bnx = nullptr; g.bnctx = nullptr; g.bnmask = nullptr; g.bnb = 0;
+  g.store_nt = store_nt_for((long long)M * N * batch * (out_dt == 0 ? 4 : 2));
   if (tstats) {                                   // statistics only from the 8-phase epilogue without split-K
     if (splits > 1 || batch > 1) return -3;
     g.tstats = tstats;

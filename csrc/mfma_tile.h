@@ -64,7 +64,20 @@ struct GemmArgs {
   const float* bnctx;
   const unsigned char* bnmask;   // bnb 3: the forward's ReLU bitmask (1 byte per 8 channels, residual BN layers)
   int bnb;
+  int store_nt;                  // lean read-out: 1 = non-temporal (streaming) output stores (DL4J_AMD_GEMM_STORE_NT)
 };
+
+// Non-temporal (streaming) output stores in the lean read-out for outputs of >= 32 MB, which no L2 keeps for the
+// next kernel anyway: the write-heavy expanding 1x1 convolutions (K = 64..128, N = 256..512) measured 299 -> 271 us
+// and 153 -> 115 us, the ResNet-50 step +0.8 % (tools/gemm_conv1x1_bench.py, profiles/r5_conv1x1_gemm.txt).
+// DL4J_AMD_GEMM_STORE_NT=0 / 1 forces them off / on for every size.
+inline int store_nt_for(long long out_bytes) {
+  static const int v = [] {
+    const char* e = getenv("DL4J_AMD_GEMM_STORE_NT");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  return v >= 0 ? v : (out_bytes >= (32LL << 20) ? 1 : 0);
+}
 
 // The BN-backward epilogue request armed by dl4j_bnb_arm (csrc/gemm.hip) for the next GEMM / conv launches of this
 // host thread (read into GemmArgs at launch time, so HIP-graph capture records it by value).
@@ -106,23 +119,41 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 
 // ----------------------------------------------------------------------------------------------- epilogue
+// erf for the GELU epilogues: Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below the 16-bit output's rounding),
+// one hardware reciprocal, one exp2 and five FMAs, returning exp(-x^2) as well so gelu' reuses it. A 256x256 tile's
+// GELU read-out runs 128 values per lane on two waves per SIMD after the main loop, i.e. it is VALU-bound: the
+// library erff (two polynomial branches, both evaluated by the wave) cost ~19 us of a 52 us BERT FFN1 GEMM.
+__device__ __forceinline__ float erf_as(float x, float& ex2) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                           0.254829592f);
+  ex2 = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+  return copysignf(fmaf(-p, ex2, 1.f), x);
+}
+__device__ __forceinline__ float gelu_f(float v) {
+  float e;
+  return 0.5f * v * (1.f + erf_as(v * 0.70710678118654752f, e));
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
     case 1: return fmaxf(v, 0.f);
     case 2: return tanhf(v);
     case 3: return 1.f / (1.f + __expf(-v));
-    case 4: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case 4: return gelu_f(v);
     default: return v;
   }
 }
 
 // act 5 (DGELU, backward of exact GELU): v *= gelu'(z) with z READ from the pre-activation buffer Z (same layout as C),
 // so dz = (dy·Wᵀ) * gelu'(z) is one GEMM instead of a GEMM plus an elementwise pass.
+// gelu'(z) = Phi(z) + z phi(z), phi(z) = exp(-z^2/2) / sqrt(2 pi) = the erf's exp(-(z/sqrt2)^2) term.
 constexpr int kActDGelu = 5;
 __device__ __forceinline__ float dgelu(float z) {
-  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-  const float pdf = __expf(-0.5f * z * z) * 0.39894228040143268f;
-  return cdf + z * pdf;
+  float e;
+  const float cdf = 0.5f * (1.f + erf_as(z * 0.70710678118654752f, e));
+  return fmaf(z * 0.39894228040143268f, e, cdf);
 }
 
 __device__ __forceinline__ float ld_out(const void* C, int dt, long long i) {
@@ -221,7 +252,7 @@ __device__ __forceinline__ void lean_act4(const GemmArgs& g, float* v) {
     for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
   } else if (g.act == 4 && g.Z == nullptr) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+    for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j]);
   }
 }
 
@@ -277,7 +308,16 @@ __device__ __forceinline__ void lean_readout(const GemmArgs& g, char* dst, const
     for (int r = r0; r < BM; r += RSTEP) {
       const int m = m0 + r;
       const uint4 q = *reinterpret_cast<const uint4*>(T + r * (BN * 2) + ((c ^ (r & 7)) << 4));
-      if (m < g.M) *reinterpret_cast<uint4*>(dst + ((long long)m * g.ldc + n) * 2) = q;
+      if (m < g.M) {
+        char* p = dst + ((long long)m * g.ldc + n) * 2;
+        if (g.store_nt) {
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          const u32x4_t v = {q.x, q.y, q.z, q.w};
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+        } else {
+          *reinterpret_cast<uint4*>(p) = q;
+        }
+      }
     }
     return;
   }
@@ -302,7 +342,7 @@ __device__ __forceinline__ void lean_readout(const GemmArgs& g, char* dst, const
       if (zmode == 1) {
         *reinterpret_cast<uint4*>(zdst + off) = q;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+        for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
       } else {
         float z[8];
         unpack(zq[i], z);
@@ -575,7 +615,7 @@ __device__ __forceinline__ void epi_sweep(const GemmArgs& g, const EpiOut& o, vo
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
       } else if (act == 4) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+        for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
       }
       store8(o.dst + off, v);
     }

@@ -55,6 +55,7 @@ def _lib():
 
 _TUNED = {}                                            # problem key -> (cfg, splits), filled by _autotune
 _TUNE = os.environ.get("DL4J_AMD_GEMM_TUNE", "1") == "1"
+_TUNE_LOG = os.environ.get("DL4J_AMD_GEMM_TUNE_LOG", "0") == "1"   # print every autotuned shape's candidate times
 # Opt-in (DL4J_AMD_GEMM_LIB=1): hipBLASLt (torch.mm / addmm / bmm on the same stream, plus an in-tree elementwise
 # kernel for an activation epilogue) as one more autotuner candidate, used where it measured faster. Off by default:
 # every product runs on the in-tree MFMA kernels, and a library pick is counted as a helper fallback
@@ -77,7 +78,7 @@ def _candidates(M, N, K, batch, default):
     splits = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     if K % 64 == 0:
         c += [(4, s) for s in splits if s == 1 or (batch == 1 and K // s >= 512 and t256 * s <= 1024)]
-    c += [(x, 1) for x in (0, 1, 2, 3, 5, 6, 7)]
+    c += [(x, 1) for x in (0, 1, 2, 3, 5, 6, 7, 8, 9)]
     if batch == 1:
         # small output grids (e.g. the LSTM's [256 x 1024] weight gradients over K = T*mb = 1600) need deep split-K
         # to fill the CUs: down to 128-deep K slices when the tile grid is under a quarter of the chip
@@ -101,6 +102,7 @@ def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False, z
     from .timing import gpu_time
     tmp = torch.empty_strided(c_t.size(), c_t.stride(), dtype=c_t.dtype, device=c_t.device)
     best, best_t = default, None
+    log = [] if _TUNE_LOG else None
     for cand in _candidates(M, N, K, batch, default) + ([LIB_CFG] if lib else []):
         if cand[1] > 1 and not splits_ok:
             continue
@@ -108,8 +110,14 @@ def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False, z
             continue
         # GPU-side time (stream parked during the enqueue): small GEMMs are shorter than the host launch path
         t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, zz), reps=3, warmup=0)
+        if log is not None:
+            log.append((t, cand))
         if best_t is None or t < best_t:
             best, best_t = cand, t
+    if log:
+        log.sort()
+        print(f"[gemm-tune] M={M} N={N} K={K} batch={batch} out={c_t.dtype} zz={zz is not None} best={best} " +
+              " ".join(f"{c[0]}/{c[1]}:{t * 1e3:.1f}" for t, c in log[:8]), flush=True)
     return best
 
 

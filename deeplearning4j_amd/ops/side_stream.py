@@ -29,13 +29,31 @@ def enabled():
     return os.environ.get("DL4J_AMD_WRW_STREAM", "1") == "1"
 
 
+def side_cus():
+    """CUs the weight-gradient stream may use (``DL4J_AMD_WRW_CUS``; 0 = all). A CU-masked side stream leaves the
+    rest of the chip to the main chain, whose short BatchNorm / elementwise kernels would otherwise wait for the
+    long-running weight-gradient blocks to retire before they get a CU."""
+    try:
+        return int(os.environ.get("DL4J_AMD_WRW_CUS", "0"))
+    except ValueError:
+        return 0
+
+
 def _side(dev):
     # one side stream per (host thread, device): a stream shared by two threads would join one thread's HIP-graph
     # capture and pull the other thread's weight-gradient launches into it (in-process ParallelWrapper workers)
     streams = _tl.__dict__.setdefault("streams", {})
     s = streams.get(dev.index)
     if s is None:
-        s = streams[dev.index] = torch.cuda.Stream(dev)
+        cus = side_cus()
+        if cus > 0:
+            from .. import runtime as rt
+            native = rt.Stream(dev.index, cus=cus)
+            s = native.torch_stream()
+            s._dl4j_native = native          # keeps the HIP stream alive as long as the torch wrapper
+        else:
+            s = torch.cuda.Stream(dev)
+        streams[dev.index] = s
     return s
 
 

@@ -119,14 +119,24 @@ class Stream:
     """A native HIP stream (non-blocking; ``high_priority`` for latency-critical work such as gradient
     communication). ``torch_stream()`` wraps it for torch so framework kernels can be enqueued on it."""
 
-    def __init__(self, device=0, high_priority=False, handle=None):
+    def __init__(self, device=0, high_priority=False, handle=None, cus=0):
+        """``cus`` > 0: restrict the stream's kernels to that many CUs (hardware queue CU mask, spread evenly)."""
         self.device = device
         self._own = handle is None
         if handle is None:
             h = c_void_p()
-            _ok(lib().dl4j_rt_stream_create(device, 1 if high_priority else 0, ctypes.byref(h)), "stream_create")
+            if cus > 0:
+                _ok(lib().dl4j_rt_stream_create_cumask(device, int(cus), ctypes.byref(h)), "stream_create_cumask")
+            else:
+                _ok(lib().dl4j_rt_stream_create(device, 1 if high_priority else 0, ctypes.byref(h)), "stream_create")
             handle = h.value
         self.handle = handle
+
+    def cu_count(self):
+        r = lib().dl4j_rt_stream_cu_count(self.ptr)
+        if r < 0:
+            raise EngineError(f"stream_cu_count {r}")
+        return r
 
     @property
     def ptr(self):
