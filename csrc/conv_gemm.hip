@@ -189,6 +189,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_glds(GemmArgs g, ConvA 
   static_assert(RPP >= 64 && RPP % 64 == 0, "epilogue pass too small");
   const int h = lane >> 5;
   EpiOut o;
+  o.coh = false;
   o.raw = false;
   o.dt = g.out_dt;
   o.dst = reinterpret_cast<char*>(g.C);
@@ -577,6 +578,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void conv_wrw_glds(GemmArgs g, Wr
   static_assert(RPP >= 32, "epilogue pass too small");
   const int h = lane >> 5;
   EpiOut o;
+  o.coh = false;
   o.raw = true;
   o.dt = 0;
   o.dst = reinterpret_cast<char*>(g.ws + (long long)split * g.M * g.N);

@@ -50,6 +50,56 @@ __device__ unsigned long long* g_gemm_stamps;
 
 namespace {
 
+// In-kernel split-K fixup (gemm_glds with GemmArgs::sk_ticket): every split block writes its fp32 slab with sc1
+// stores (written through the XCD-local L2), drains them, and bumps the tile's arrival counter; the block that arrives
+// last sums the tile's slabs in split order — exactly the fixed order of gemm_splitk_reduce, so the result is
+// bitwise the same — and applies the epilogue, instead of the separate reduce launch (BERT-base: 63 reduce launches,
+// 0.51 ms of an 8.2 ms step). Slab reads are agent-scope atomic loads (sc1), so the last block never invalidates its
+// L2. Opt-in: measured slower than the reduce launch (splitk_fixup_mode below).
+typedef __attribute__((address_space(1))) unsigned gq32_t;
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void splitk_fixup(const GemmArgs& g, int m0, int n0, int tid) {
+  constexpr int C4 = BN / 4;
+  constexpr int PER = BM * C4 / NT;
+  static_assert((BM * C4) % NT == 0, "split-K fixup geometry");
+  const long long MN = (long long)g.M * g.N;
+  const bool vec = (g.N & 3) == 0;
+  float v[PER][4];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
+  for (int z = 0; z < g.splits; ++z) {
+    const float* slab = g.ws + z * MN;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * NT;
+      const int r = idx / C4, c = idx - (idx / C4) * C4;
+      const int m = m0 + r, n = n0 + 4 * c;
+      if (m >= g.M || n >= g.N) continue;
+      const float* p = slab + (long long)m * g.N + n;
+      typedef __attribute__((address_space(1))) unsigned long long gq64;
+      if (vec) {
+        const unsigned long long lo = __hip_atomic_load((gq64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load((gq64*)(p + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[i][0] += __uint_as_float((unsigned)lo);
+        v[i][1] += __uint_as_float((unsigned)(lo >> 32));
+        v[i][2] += __uint_as_float((unsigned)hi);
+        v[i][3] += __uint_as_float((unsigned)(hi >> 32));
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (n + j < g.N)
+            v[i][j] += __uint_as_float(__hip_atomic_load((gq32_t*)(p + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = tid + i * NT;
+    const int r = idx / C4, c = idx - (idx / C4) * C4;
+    const int m = m0 + r, n = n0 + 4 * c;
+    if (m < g.M && n < g.N) store4(g, g.C, g.Z, m, n, v[i]);
+  }
+}
+
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 // LDS bytes of a gemm_glds instantiation: the operand ring, grown where a single-stage wide tile's epilogue image
 // (lean: [BM][BN] 16-bit; generic: >= 64 rows of fp32 at pitch BN*4+16) is larger than the ring
@@ -236,7 +286,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 && WGM * WGN == 4 ? 4 :
   const int h = lane >> 5;
   const bool split = g.splits > 1;
   EpiOut o;
+  o.coh = false;
   o.raw = split;
+  o.coh = split && g.sk_ticket != nullptr;
   o.dt = split ? 0 : g.out_dt;
   o.dst = split ? reinterpret_cast<char*>(g.ws + (long long)z * g.M * g.N)
                 : reinterpret_cast<char*>(g.C) + (long long)bz * g.sC * (g.out_dt == 0 ? 4 : 2);
@@ -272,6 +324,23 @@ __global__ __launch_bounds__(WGM* WGN * 64, (STAGES == 1 && WGM * WGN == 4 ? 4 :
     if (P + 1 < BM / RPP) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
+    }
+  }
+  if constexpr (!BNB) {
+    if (o.coh) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's slab stores are in memory
+      __syncthreads();                                               // ... and every other wave's; image reads done
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((gq32_t*)&g.sk_ticket[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(g.splits - 1);
+        if (last) __hip_atomic_store((gq32_t*)&g.sk_ticket[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
+      __syncthreads();
+      if (*flag == 0) return;
+      splitk_fixup<BM, BN, WGM * WGN * 64>(g, m0, n0, tid);
     }
   }
 }
@@ -576,6 +645,7 @@ __global__ __launch_bounds__(512) void gemm_8ph(GemmArgs g) {
   } else {
     const bool split = g.splits > 1;
     EpiOut o;
+    o.coh = false;
     o.raw = split;
     o.dt = split ? 0 : g.out_dt;
     o.dst = split ? reinterpret_cast<char*>(g.ws + (long long)z * g.M * g.N)
@@ -869,6 +939,36 @@ void plan_f32(int M, int N, int K, int batch, int* tile, int* splits) {
 // ----------------------------------------------------------------------------------------------- dispatch
 // DL4J_AMD_GEMM_LEAN=0 forces the generic LDS epilogue everywhere (A/B experiments)
 
+// Arrival counters of the in-kernel split-K fixup: 512 launches in flight x 2048 tiles, zero-initialised, each
+// counter reset by its tile's last block (so no per-launch memset; a graph replay finds them at zero again).
+constexpr int kSkSlots = 512, kSkTiles = 2048;
+__device__ unsigned g_sk_ticket[kSkSlots * kSkTiles];
+
+// Off by default (DL4J_AMD_GEMM_SPLITK_FIXUP=1 turns it on): measured slower on BERT-base, 447k vs 529k tok/s
+// (profiles/r5_splitk_fixup.txt) — the write-through slab stores and the tile's serial last-block pass cost more than
+// the reduce launch they replace, and the autotuner then moves shapes to other configurations.
+int& splitk_fixup_mode() {
+  static int v = [] {
+    const char* e = getenv("DL4J_AMD_GEMM_SPLITK_FIXUP");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
+unsigned* sk_ticket_slot() {
+  static unsigned* base[64] = {nullptr};
+  static unsigned next = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_sk_ticket)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  const unsigned k = __atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % (unsigned)kSkSlots;
+  return base[dev] + (long long)kSkTiles * k;
+}
+
 bool lean_disabled() {
   static const int v = [] {
     const char* e = getenv("DL4J_AMD_GEMM_LEAN");
@@ -993,6 +1093,14 @@ void plan(int M, int N, int K, int batch, int* cfg, int* splits) {
 
 }  // namespace
 
+// 1: split-K products of the gemm_glds tiles sum their slabs in the kernel; 0 (default): separate reduce launch.
+// Returns the previous mode.
+DL4J_API int dl4j_gemm_set_splitk_fixup(int on) {
+  const int old = splitk_fixup_mode();
+  splitk_fixup_mode() = on ? 1 : 0;
+  return old;
+}
+
 // Returns the workspace bytes the fast path needs for (M, N, K, batch) with config (cfg, splits) chosen by plan().
 DL4J_API long long dl4j_gemm_plan(int M, int N, int K, int batch, int* cfg, int* splits) {
   plan(M, N, K, batch, cfg, splits);
@@ -1054,6 +1162,7 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   }
   if (batch > 1) splits = 1;
   GemmArgs g;
+  g.sk_ticket = nullptr;
   g.A = A; g.B = B; g.C = C; g.Z = Z; g.bias = bias; g.ws = ws;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.sA = sA; g.sB = sB; g.sC = sC;
   g.M = M; g.N = N; g.K = K;
@@ -1087,9 +1196,12 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   g.tiles_m = (M + kCfg[cfg].bm - 1) / kCfg[cfg].bm;
   g.tiles_n = (N + kCfg[cfg].bn - 1) / kCfg[cfg].bn;
   const bool lean = lean_ok(g, batch);
+  if (splits > 1 && cfg != 4 && batch == 1 && !g.bnb && splitk_fixup_mode() &&
+      (long long)g.tiles_m * g.tiles_n <= kSkTiles)
+    g.sk_ticket = sk_ticket_slot();            // gemm_glds sums the slabs itself: no reduce launch
   const int e = in_dt == 1 ? launch_fast_l<1>(cfg, akc, bkc, g, batch, lean, s)
                            : launch_fast_l<2>(cfg, akc, bkc, g, batch, lean, s);
-  if (e || splits <= 1) return e;
+  if (e || splits <= 1 || g.sk_ticket) return e;
   const long long total = (long long)M * ((N + 3) / 4);
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;

@@ -65,6 +65,7 @@ struct GemmArgs {
   const unsigned char* bnmask;   // bnb 3: the forward's ReLU bitmask (1 byte per 8 channels, residual BN layers)
   int bnb;
   int store_nt;                  // lean read-out: 1 = non-temporal (streaming) output stores (DL4J_AMD_GEMM_STORE_NT)
+  unsigned* sk_ticket;           // split-K fixup in the kernel (gemm_glds): per-tile arrival counters, else null
 };
 
 // Non-temporal (streaming) output stores in the lean read-out for outputs of >= 32 MB, which no L2 keeps for the
@@ -428,7 +429,19 @@ struct EpiOut {
   int dt;             // destination dtype (0 f32, 1 bf16, 2 f16)
   bool raw;           // split-K slab: no epilogue math
   bool vec;           // 16-byte aligned rows (ld and base) for vector stores
+  bool coh;           // slab stores coherent at agent scope (sc1 write-through): read by another block's fixup
 };
+
+// 16-byte / 4-byte stores visible to every XCD once the storing wave's vmcnt drains (sc1: written through the
+// XCD-local L2), for split-K slabs that the tile's last-arriving block sums (gemm_glds fixup)
+__device__ __forceinline__ void st_coh16(void* p, float a, float b, float c, float d) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const f32x4v v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_coh4(float* p, float a) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, void* Zp, int m, int n, float* v) {
   if (!o.raw) {
@@ -480,6 +493,11 @@ __device__ __forceinline__ void epi_chunk8(const GemmArgs& g, const EpiOut& o, v
     }
   }
   char* p = o.dst + ((long long)m * o.ld + n) * (o.dt == 0 ? 4 : 2);
+  if (o.coh) {
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N) st_coh4(reinterpret_cast<float*>(p) + j, v[j]);
+    return;
+  }
   if (o.vec && n + 8 <= g.N) {
     if (o.dt == 0) {
       reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -545,10 +563,16 @@ __device__ __forceinline__ void epi_sweep(const GemmArgs& g, const EpiOut& o, vo
       }
     }
   };
+  const bool coh = o.coh;
   auto store8 = [&](char* p, const float* w) {
     if constexpr (F32) {
-      reinterpret_cast<float4*>(p)[0] = make_float4(w[0], w[1], w[2], w[3]);
-      reinterpret_cast<float4*>(p)[1] = make_float4(w[4], w[5], w[6], w[7]);
+      if (coh) {
+        st_coh16(p, w[0], w[1], w[2], w[3]);
+        st_coh16(p + 16, w[4], w[5], w[6], w[7]);
+      } else {
+        reinterpret_cast<float4*>(p)[0] = make_float4(w[0], w[1], w[2], w[3]);
+        reinterpret_cast<float4*>(p)[1] = make_float4(w[4], w[5], w[6], w[7]);
+      }
     } else {
       uint4 pk;
       pk.x = (unsigned)to16(w[0], dt) | ((unsigned)to16(w[1], dt) << 16);

@@ -129,6 +129,57 @@ def test_split_k_deterministic():
     _check(o1, _ref(a, b), torch.bfloat16, 8192, "split-K")
 
 
+@pytest.mark.parametrize("case", ["fp32_dw", "bf16_bias_gelu", "ragged_beta", "dgelu"])
+def test_split_k_in_kernel_fixup_matches_reduce(case, monkeypatch):
+    """Split-K on the gemm_glds tiles: the tile's last-arriving block sums the slabs in split order inside the kernel
+    (dl4j_gemm_set_splitk_fixup(1), opt-in) — bitwise equal to the separate reduce launch, and to the reference."""
+    import ctypes
+    from deeplearning4j_amd.ops import native
+    lib = native.load()
+    lib.dl4j_gemm_set_splitk_fixup.argtypes = [ctypes.c_int]
+    torch.manual_seed(11)
+    kw, z = {}, None
+    if case == "fp32_dw":
+        M, N, K, dt, cfg = 768, 3072, 4096, torch.float32, (3, 3)
+    elif case == "bf16_bias_gelu":
+        M, N, K, dt, cfg = 1000, 768, 3072, torch.bfloat16, (2, 4)
+        kw = dict(bias=torch.randn(N, device=DEV), act="gelu")
+    elif case == "ragged_beta":
+        M, N, K, dt, cfg = 333, 250, 2048, torch.float32, (5, 3)
+        kw = dict(beta=1.0)
+    else:
+        M, N, K, dt, cfg = 512, 1024, 1536, torch.bfloat16, (7, 2)
+        z = torch.randn(M, N, device=DEV).bfloat16()
+        kw = dict(act="dgelu", z=z)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16() * 0.05
+    c0 = torch.randn(M, N, device=DEV).to(dt)
+    monkeypatch.setattr(gemm, "_FORCE_CFG", cfg)
+    outs = []
+    old = lib.dl4j_gemm_set_splitk_fixup(1)
+    try:
+        for mode in (1, 0):
+            lib.dl4j_gemm_set_splitk_fixup(mode)
+            out = c0.clone()
+            gemm.mmul(a, b, out=out, **kw)
+            outs.append(out)
+        torch.cuda.synchronize()
+    finally:
+        lib.dl4j_gemm_set_splitk_fixup(old)
+    assert torch.equal(outs[0], outs[1]), f"{case}: in-kernel fixup differs from the reduce kernel"
+    r = a.float() @ b.float()
+    if "bias" in kw:
+        r = r + kw["bias"].reshape(1, -1)
+    if kw.get("beta"):
+        r = r + c0.float()
+    if kw.get("act") == "gelu":
+        r = torch.nn.functional.gelu(r)
+    elif kw.get("act") == "dgelu":
+        zf = z.float()
+        r = r * (0.5 * (1 + torch.erf(zf / 2 ** 0.5)) + zf * torch.exp(-0.5 * zf * zf) / (2 * 3.141592653589793) ** 0.5)
+    _check(outs[0], r, torch.bfloat16, K, case)
+
+
 def test_identity_asymmetric():
     """A = I, asymmetric B: a transposed C-write would show."""
     n = 256
@@ -161,7 +212,8 @@ def test_graph_capture():
     _check(out, _ref(a, b), torch.bfloat16, 2048, "graph replay")
 
 
-@pytest.mark.parametrize("cfg", [(0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (4, 3), (2, 2), (5, 1)])
+@pytest.mark.parametrize("cfg", [(0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (4, 3), (2, 2), (5, 1), (8, 1), (9, 1),
+                                 (3, 3), (7, 2)])
 @pytest.mark.parametrize("a_kc", [True, False])
 @pytest.mark.parametrize("b_kc", [True, False])
 def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
@@ -175,7 +227,7 @@ def test_every_tile_config(cfg, a_kc, b_kc, monkeypatch):
     _check(out, _ref(a, b), torch.bfloat16, K, f"cfg {cfg} a_kc={a_kc} b_kc={b_kc}")
 
 
-@pytest.mark.parametrize("cfg", [None, (0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (5, 1)])
+@pytest.mark.parametrize("cfg", [None, (0, 1), (1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (8, 1), (9, 1)])
 def test_bn_stats_epilogue(cfg, monkeypatch):
     """Per-64-row BatchNorm partial statistics from the GEMM epilogue (conv -> BN fusion) match the stored output."""
     torch.manual_seed(10)
