@@ -79,6 +79,38 @@ class DataSet:
     def batchBy(self, n):
         return [self._sub(torch.arange(i, min(i + n, self.numExamples()))) for i in range(0, self.numExamples(), n)]
 
+    # ND4J DataSet feature transforms (in place), used by the reference's tests on Iris / MNIST batches
+    def normalizeZeroMeanZeroUnitVariance(self):
+        """Per-column (per-feature) standardisation over the examples: (x - mean) / std, std of a constant column
+        treated as 1 so it stays 0."""
+        f = self.features.double()
+        mu = f.mean(0, keepdim=True)
+        sd = f.std(0, unbiased=True, keepdim=True)
+        sd = torch.where(sd > 0, sd, torch.ones_like(sd))
+        self.features = ((f - mu) / sd).to(self.features.dtype)
+
+    def scaleMinAndMax(self, lo, hi):
+        """Per-column linear rescale of the features to [lo, hi]."""
+        f = self.features.double()
+        mn, mx = f.amin(0, keepdim=True), f.amax(0, keepdim=True)
+        rng = torch.where(mx > mn, mx - mn, torch.ones_like(mx))
+        self.features = (lo + (f - mn) / rng * (hi - lo)).to(self.features.dtype)
+
+    def binarize(self, cutoff=0.0):
+        """Features > cutoff -> 1, else 0."""
+        self.features = (self.features > cutoff).to(self.features.dtype)
+
+    def labelCounts(self):
+        """{class index: number of examples} of a one-hot / probability label matrix."""
+        idx = self.labels.reshape(self.labels.shape[0], -1).argmax(1)
+        u, c = torch.unique(idx, return_counts=True)
+        return {int(a): int(b) for a, b in zip(u, c)}
+
+    def get(self, i):
+        """Example(s) ``i`` (an int or an index list) as a new DataSet."""
+        idx = torch.as_tensor([i] if isinstance(i, int) else list(i), dtype=torch.long)
+        return self._sub(idx)
+
     def asList(self):
         return self.batchBy(1)
 

@@ -114,6 +114,16 @@ class BackTrackLineSearch:
 
 
 # ------------------------------------------------------------------------------------------ optimizers
+def _batch_size(x):
+    """Minibatch size of an input (array, or list of arrays for a graph); 1 for a model with no input — a cost
+    function optimized directly (the reference's Model.computeGradientAndScore() with no DataSet)."""
+    if hasattr(x, "shape"):
+        return x.shape[0]
+    if isinstance(x, (list, tuple)) and x and hasattr(x[0], "shape"):
+        return x[0].shape[0]
+    return 1
+
+
 class BaseOptimizer:
     def __init__(self, model, stepFunction=None, terminationConditions=None, maxLineSearchIterations=None):
         self.model = model
@@ -141,8 +151,7 @@ class BaseOptimizer:
         self.score = float(m.score())
         p = m.flattenedParams
         keep = p.clone()
-        m.updater.update(p, m.flattenedGradients, m.conf.iterationCount, m.conf.epochCount, x.shape[0] if
-                         hasattr(x, "shape") else x[0].shape[0], None)
+        m.updater.update(p, m.flattenedGradients, m.conf.iterationCount, m.conf.epochCount, _batch_size(x), None)
         p.copy_(keep)
         m._params_changed()
         return m.flattenedGradients.clone(), self.score

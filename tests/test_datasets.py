@@ -147,3 +147,30 @@ def test_dataset_save_load_file_iterator_and_splitter(tmp_path):
     rec = ReconstructionDataSetIterator(ListDataSetIterator([d]))
     x = rec.next()
     assert torch.equal(x.features, x.labels)
+
+
+def test_dataset_feature_transforms():
+    """ND4J DataSet transforms used by the reference tests: per-column standardisation (a constant column stays 0),
+    min/max rescale, binarize, label counts and example selection."""
+    from deeplearning4j_amd.datasets.dataset import DataSet
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(50, 4, generator=g) * 7 + 3
+    x[:, 2] = 5.0
+    y = torch.nn.functional.one_hot(torch.arange(50) % 3, 3).float()
+    ds = DataSet(x.clone(), y)
+    ds.normalizeZeroMeanZeroUnitVariance()
+    f = ds.getFeatures()
+    assert torch.allclose(f.mean(0), torch.zeros(4), atol=1e-5)
+    assert torch.allclose(f[:, [0, 1, 3]].std(0), torch.ones(3), atol=1e-5)
+    assert torch.all(f[:, 2] == 0)
+    ds2 = DataSet(x.clone(), y)
+    ds2.scaleMinAndMax(-1.0, 1.0)
+    f2 = ds2.getFeatures()
+    assert torch.allclose(f2[:, [0, 1, 3]].amin(0), -torch.ones(3)) and torch.allclose(f2[:, [0, 1, 3]].amax(0), torch.ones(3))
+    ds3 = DataSet(x.clone(), y)
+    ds3.binarize(6.5)
+    assert set(ds3.getFeatures().unique().tolist()) <= {0.0, 1.0}
+    assert ds.labelCounts() == {0: 17, 1: 17, 2: 16}
+    one = ds.get(4)
+    assert one.numExamples() == 1 and torch.equal(one.getLabels()[0], y[4])
+    assert ds.get([1, 2, 3]).numExamples() == 3
