@@ -19,7 +19,7 @@ import torch
 
 from ..memory import arena
 
-from . import native, side_stream
+from . import native, side_stream, tunedb
 from .native import _ptr, _stream, c_int, c_ll, c_void_p
 
 native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
@@ -393,6 +393,10 @@ def _v3_pick(key, launch, out, make_ts, allow_r2=True):
     v = _V3_CHOICE.get(key)
     if v is not None:
         return v
+    v = tunedb.lookup("conv_v3", key)
+    if v is not None:
+        _V3_CHOICE[key] = v
+        return v
     lib = native.load()
     geom = key[1]
     M, K = geom[0] * geom[13] * geom[14], geom[4]
@@ -410,10 +414,11 @@ def _v3_pick(key, launch, out, make_ts, allow_r2=True):
             ts = make_ts(var)
             if launch(var, scratch, ts) not in (0, 1):
                 continue
-            t = _timed(lambda: launch(var, scratch, ts), reps=3)
+            t = _timed(lambda: launch(var, scratch, ts), reps=tunedb.reps(3))
             if bt is None or t < bt:
                 best, bt = var, t
     v = _V3_CHOICE[key] = best if best is not None else -1
+    tunedb.record("conv_v3", key, v)
     return v
 
 
@@ -715,6 +720,10 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
     v = _WRW_CHOICE.get(key)
     if v is not None:
         return v
+    v = tunedb.lookup("conv_wrw", key)
+    if v is not None:
+        _WRW_CHOICE[key] = v
+        return v
     lib = native.load()
     halo = _halo_candidates(geom)
     if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
@@ -736,10 +745,11 @@ def _wrw_pick(geom, x, dy, dWt, need_db, grads_zeroed):
                                           need_db, scratch, sdb, False, scratch, True) and 0
             if (run() or 0) != 0:
                 continue
-            t = _timed(run, reps=3)
+            t = _timed(run, reps=tunedb.reps(3))
             if bt is None or t < bt:
                 best, bt = c, t
     v = _WRW_CHOICE[key] = best if best is not None else (("r2",) if x.dtype == torch.bfloat16 else ("v3", 0))
+    tunedb.record("conv_wrw", key, v)
     return v
 
 
@@ -849,13 +859,18 @@ def _choose(key, run_gemm, run_old):
     if c is None:
         if not GEMM_1X1:
             return False
+        c = tunedb.lookup("conv_1x1", key)
+        if c is not None:
+            _CHOICE[key] = c
+            return c
         if torch.cuda.is_current_stream_capturing() or os.environ.get("DL4J_AMD_CONV_TUNE", "1") != "1":
             return True
         # candidates run inline on this stream: on the overlap stream they would still be writing their scratch
         # outputs after those are freed, and the main-stream timing events would not cover them
         with side_stream.suspended():
-            tg, to = _timed(run_gemm), _timed(run_old)
+            tg, to = _timed(run_gemm, reps=tunedb.reps(2)), _timed(run_old, reps=tunedb.reps(2))
         c = _CHOICE[key] = tg <= to
+        tunedb.record("conv_1x1", key, c)
     return c
 
 

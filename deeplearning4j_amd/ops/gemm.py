@@ -20,7 +20,7 @@ import os
 
 import torch
 
-from . import fallback
+from . import fallback, tunedb
 from .dispatch import use_native
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -109,7 +109,7 @@ def _autotune(launch, c_t, M, N, K, batch, default, splits_ok=True, lib=False, z
         if launch(cand[0], cand[1], tmp, 0.0, zz) != 0:
             continue
         # GPU-side time (stream parked during the enqueue): small GEMMs are shorter than the host launch path
-        t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, zz), reps=3, warmup=0)
+        t = gpu_time(lambda: launch(cand[0], cand[1], tmp, 0.0, zz), reps=tunedb.reps(3), warmup=0)
         if log is not None:
             log.append((t, cand))
         if best_t is None or t < best_t:
@@ -343,11 +343,16 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
             kst = key + ("stats", stats_tag)
             cfg = (_FORCE_CFG[0], 1) if _FORCE_CFG is not None else _TUNED.get(kst)
             if cfg is None:
-                cfg = (4, 1) if K % 64 == 0 else (2, 1)
-                if _TUNE and not torch.cuda.is_current_stream_capturing():
-                    cfg = _autotune(lambda c_, s_, d_, bt_, zz_: launch(c_, s_, d_, bt_, zz_, stats), c_t, Mx, Nx, K,
-                                    batch, cfg, splits_ok=False)
+                cfg = tunedb.lookup("gemm", kst)
+                if cfg is not None:
                     _TUNED[kst] = cfg
+                else:
+                    cfg = (4, 1) if K % 64 == 0 else (2, 1)
+                    if _TUNE and not torch.cuda.is_current_stream_capturing():
+                        cfg = _autotune(lambda c_, s_, d_, bt_, zz_: launch(c_, s_, d_, bt_, zz_, stats), c_t, Mx, Nx,
+                                        K, batch, cfg, splits_ok=False)
+                        _TUNED[kst] = cfg
+                        tunedb.record("gemm", kst, cfg)
             rc = launch(cfg[0], 1, c_t, float(beta), z, stats)
             if rc != 0:
                 raise RuntimeError(f"HIP gemm (stats) failed with code {rc}")
@@ -367,10 +372,15 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         else:
             cfg = _TUNED.get(key)
             if cfg is None:
-                cfg = _plan(lib, Mx, Nx, K, batch)
-                if _TUNE and not torch.cuda.is_current_stream_capturing():
-                    cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None, zz=z)
+                cfg = tunedb.lookup("gemm", key)
+                if cfg is not None:
                     _TUNED[key] = cfg
+                else:
+                    cfg = _plan(lib, Mx, Nx, K, batch)
+                    if _TUNE and not torch.cuda.is_current_stream_capturing():
+                        cfg = _autotune(launch, c_t, Mx, Nx, K, batch, cfg, lib=libmm is not None, zz=z)
+                        _TUNED[key] = cfg
+                        tunedb.record("gemm", key, cfg)
         if cfg == LIB_CFG:
             fallback.record("gemm", "library GEMM (hipBLASLt) picked by the autotuner (DL4J_AMD_GEMM_LIB=1)")
         rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
