@@ -300,13 +300,46 @@ class _Counters:
         self.epochCount = int(n)
 
 
+class LayerConfiguration:
+    """The per-layer NeuralNetConfiguration view returned by ``MultiLayerConfiguration.getConf(i)``
+    (reference NeuralNetConfiguration.getLayer / getVariables); attributes resolve on the wrapped layer config."""
+
+    __slots__ = ("_layer",)
+
+    def __init__(self, layer):
+        object.__setattr__(self, "_layer", layer)
+
+    def getLayer(self):
+        return self._layer
+
+    def setLayer(self, layer):
+        object.__setattr__(self, "_layer", layer)
+
+    def getVariables(self):
+        return [s.key for s in self._layer.param_specs()] if hasattr(self._layer, "param_specs") else []
+
+    def __getattr__(self, name):
+        return getattr(self._layer, name)
+
+    def __setattr__(self, name, value):
+        setattr(self._layer, name, value)
+
+    def __eq__(self, other):
+        return self._layer == (other._layer if isinstance(other, LayerConfiguration) else other)
+
+    def __repr__(self):
+        return f"LayerConfiguration({self._layer!r})"
+
+
 class MultiLayerConfiguration(_Counters, Config):
     FIELDS = {"confs": [], "inputPreProcessors": {}, "backprop": True, "pretrain": False,
               "backpropType": BackpropType.Standard, "tbpttFwdLength": 20, "tbpttBackLength": 20,
               "globalConf": {}, "iterationCount": 0, "epochCount": 0, "inputType": None}
 
     def getConf(self, i):
-        return self.confs[i]
+        """Layer i's configuration as the reference's per-layer NeuralNetConfiguration: ``getLayer()`` is the layer
+        config; every other attribute reads through to it (this framework keeps one object per layer)."""
+        return LayerConfiguration(self.confs[i])
 
     def getMemoryReport(self, inputType=None):
         """Per-layer memory estimates (reference MultiLayerConfiguration.getMemoryReport)."""

@@ -77,7 +77,7 @@ def test_frozen_layer_with_backprop():
     net = build(FrozenLayerWithBackprop)
     from deeplearning4j_amd import MultiLayerConfiguration
     c2 = MultiLayerConfiguration.fromJson(net.getLayerWiseConfigurations().toJson())
-    assert type(c2.getConf(1)).__name__ == "FrozenLayerWithBackprop"
+    assert type(c2.getConf(1).getLayer()).__name__ == "FrozenLayerWithBackprop"
 
 
 def test_multidataset_iterator_adapter():
