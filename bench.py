@@ -24,6 +24,13 @@ import time
 import torch
 
 
+def _kernel_db():
+    """Which kernel-choice database the autotuners consulted (ops/tunedb.py), for the JSON provenance."""
+    from deeplearning4j_amd.ops import tunedb
+    p = tunedb.loaded_from()
+    return os.path.relpath(p, os.path.dirname(os.path.abspath(__file__))) if p else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +153,7 @@ def main():
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}", "comm": args.comm,
                        "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                        "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
+                       "kernel_db": _kernel_db(),
                        "final_score": final_score, **memory_report(device)},
         }), flush=True)
     from deeplearning4j_amd.parallel.distributed import destroy
@@ -231,6 +239,7 @@ def main_inprocess(args):
                    "comm": "rccl (ncclCommInitAll)",
                    "updater": "RmsProp(0.1,0.96,1e-3) + l1 1e-7 + l2 5e-5 (fused HIP updater)",
                    "hip_graph": bool(use_graph and getattr(net, "_hipgraph", None) is not None),
+                   "kernel_db": _kernel_db(),
                    "final_score": net.score(), **memory_report(dev0)},
     }), flush=True)
 
