@@ -160,8 +160,10 @@ class MultiLayerNetwork(BaseNetwork):
     def output(self, x, train=False, featuresMask=None, labelsMask=None):
         if isinstance(x, DataSetIterator):
             return [self.output(ds.features, train, ds.featuresMask) for ds in x]
+        if featuresMask is None:
+            featuresMask = self.mask            # masks set with setLayerMaskArrays apply (reference output(INDArray))
         with torch.no_grad():
-            acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, featuresMask)
+            acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, self._to_dev(featuresMask))
         out = acts[-1]
         # 16-bit activations come back as fp32 (the reference's output dtype); fp32/fp64 networks keep theirs
         return out.float() if out.dtype in (torch.bfloat16, torch.float16) else out
