@@ -70,6 +70,11 @@ class ILossFunction(Config):
         w = self._w(g)
         if w is not None:
             g = g * w
+        if mask is not None and tuple(mask.shape) == tuple(g.shape):
+            # per-output masking: dL/da is masked BEFORE the activation backprop as well — for softmax dL/dz_i
+            # depends on every dL/da_j, so a masked label would otherwise still steer the unmasked outputs
+            # (the ND4J loss functions' per-output masking rule)
+            g = _apply_mask(g, mask)
         g = act.backprop(z, g)
         g = _apply_mask(g, mask)
         return g.to(preOutput.dtype)

@@ -422,6 +422,10 @@ class ComputationGraph(BaseNetwork):
 
     def computeGradientAndScore(self, inputs=None, labels=None, fmasks=None, lmasks=None, stored_state=False,
                                 store_last_for_tbptt=False, tbptt_back=None, defer_reg=False):
+        if inputs is None:
+            # the setInputs / setLabels / setLayerMaskArrays path (reference computeGradientAndScore())
+            fmasks = getattr(self, "inputMaskArrays", None) if fmasks is None else fmasks
+            lmasks = getattr(self, "labelMaskArrays", None) if lmasks is None else lmasks
         inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
         labels = self.labels if labels is None else labels
         if torch.is_tensor(labels):

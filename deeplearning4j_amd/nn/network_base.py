@@ -97,7 +97,9 @@ class BaseNetwork:
             if p.numel() != total:
                 raise ValueError(f"Invalid parameters: expected {total} params, got {p.numel()}")
             flat = p.to(self.device, self.master_dtype)
-            flat = flat.clone() if (clone or flat.data_ptr() == p.data_ptr()) else flat
+            # cloneParametersArray=False adopts the caller's vector (the layers' parameters become views of it,
+            # reference MultiLayerNetwork.init(INDArray, boolean)); a device / dtype change copies anyway
+            flat = flat.clone() if clone else flat
             init = False
         else:
             flat = torch.zeros(total, dtype=self.master_dtype, device=self.device)
@@ -157,8 +159,18 @@ class BaseNetwork:
         self.sync_shadow()
 
     def _fit_batch(self, x, y, fmask=None, lmask=None):
-        """One optimizer iteration on a minibatch: the fused SGD-family step, or a line-search optimizer
-        (LBFGS / CG / line GD) when the configuration asks for one (reference Solver.java:50-84)."""
+        """One optimizer iteration on a minibatch; afterwards no layer keeps the iteration's mask arrays
+        (reference MultiLayerNetwork.fit -> clearLayerMaskArrays)."""
+        try:
+            return self._fit_batch_step(x, y, fmask, lmask)
+        finally:
+            if fmask is not None or lmask is not None:
+                for _, _, impl, _ in self._layer_offsets:
+                    impl.maskArray = None
+
+    def _fit_batch_step(self, x, y, fmask=None, lmask=None):
+        """The fused SGD-family step, or a line-search optimizer (LBFGS / CG / line GD) when the configuration
+        asks for one (reference Solver.java:50-84)."""
         from .conf.enums import OptimizationAlgorithm as OA
         algo = self.conf.globalConf.get("optimizationAlgo") if hasattr(self.conf, "globalConf") else None
         if algo is None or OA.of(algo) == OA.STOCHASTIC_GRADIENT_DESCENT:
