@@ -604,6 +604,7 @@ class ComputationGraph(BaseNetwork):
     # ------------------------------------------------------------------------------ rnn
     def rnnTimeStep(self, *inputs):
         inputs = self._prep_inputs(list(inputs))
+        mb = inputs[0].shape[0]          # a FF->RNN preprocessor reshapes [mb*T, n] rows back by the INPUT minibatch
         acts = {n: inputs[i] for i, n in enumerate(self.conf.networkInputs)}
         with torch.no_grad():
             for name in self.topo:
@@ -615,7 +616,7 @@ class ComputationGraph(BaseNetwork):
                 if isinstance(v, LayerVertex):
                     x = ins[0] if len(ins) == 1 else torch.cat(ins, 1)
                     if v.preProcessor is not None:
-                        x = v.preProcessor.preProcess(x, x.shape[0], False)
+                        x = v.preProcessor.preProcess(x, mb, False)
                     layer = self.layers_by_name[name]
                     if name in self._residual_of:
                         layer.residual = acts[self._residual_of[name]]
