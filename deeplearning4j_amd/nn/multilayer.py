@@ -149,6 +149,22 @@ class MultiLayerNetwork(BaseNetwork):
             self._validated = chk
         return acts
 
+    def rnnActivateUsingStoredState(self, x, training=False, storeLastForTBPTT=False):
+        """Forward pass whose recurrent layers start from their stored rnnTimeStep state (zeros when none) without
+        changing it; with ``storeLastForTBPTT`` each layer's final state is kept as its TBPTT state
+        (rnnGetTBPTTState). Reference MultiLayerNetwork.rnnActivateUsingStoredState."""
+        rec = [l for l in self.layers if hasattr(l, "tBpttStateMap") and hasattr(l, "stateMap")]
+        saved = [dict(l.tBpttStateMap) for l in rec]
+        for l in rec:
+            l.tBpttStateMap = dict(l.stateMap)
+        try:
+            with torch.no_grad():
+                return self.feedForwardToLayer(len(self.layers) - 1, x, training, None, True, storeLastForTBPTT)
+        finally:
+            if not storeLastForTBPTT:
+                for l, s in zip(rec, saved):
+                    l.tBpttStateMap = s
+
     def feedForward(self, x=None, train=False, fmask=None):
         x = self.input if x is None else x
         acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, fmask)
