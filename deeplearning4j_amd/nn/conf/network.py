@@ -479,6 +479,24 @@ class GraphBuilder:
         self._back = int(n)
         return self
 
+    # vertices that consume exactly one activation: given several inputs they get a MergeVertex "<name>-merge" in
+    # front of them (reference GraphBuilder.build, TestComputationGraphNetwork.testMergeVertexAddition)
+    _SINGLE_INPUT = ("LayerVertex", "L2NormalizeVertex", "ScaleVertex", "ShiftVertex", "ReshapeVertex", "SubsetVertex",
+                     "PreprocessorVertex", "PoolHelperVertex", "UnstackVertex", "DuplicateToTimeSeriesVertex",
+                     "LastTimeStepVertex")
+
+    def _add_merge_vertices(self):
+        from .graph import MergeVertex
+        for name in list(self._order):
+            ins = self._vertexInputs.get(name, [])
+            if len(ins) < 2 or type(self._vertices[name]).__name__ not in self._SINGLE_INPUT:
+                continue
+            mname = f"{name}-merge"
+            self._vertices[mname] = MergeVertex()
+            self._vertexInputs[mname] = list(ins)
+            self._vertexInputs[name] = [mname]
+            self._order.insert(self._order.index(name), mname)
+
     def build(self):
         if not self._inputs:
             raise ValueError("ComputationGraph must have at least one input (addInputs)")
@@ -506,6 +524,7 @@ class GraphBuilder:
                 raise DL4JInvalidConfigException(
                     f"Invalid configuration: disconnected vertices found - {dis} are not connected to the network "
                     "output; use .allowDisconnected(True) to build it anyway")
+        self._add_merge_vertices()
         conf = ComputationGraphConfiguration(
             vertices={k: self._vertices[k] for k in self._order}, vertexInputs=dict(self._vertexInputs),
             networkInputs=list(self._inputs), networkOutputs=list(self._outputs), backprop=self._backprop,
@@ -542,6 +561,19 @@ class ComputationGraphConfiguration(_Counters, Config):
     def getMemoryReport(self, *inputTypes):
         from .memory import cg_memory_report
         return cg_memory_report(self, list(inputTypes) or None)
+
+    # reference ComputationGraphConfiguration getters
+    def getVertices(self):
+        return self.vertices
+
+    def getVertexInputs(self):
+        return self.vertexInputs
+
+    def getNetworkInputs(self):
+        return list(self.networkInputs)
+
+    def getNetworkOutputs(self):
+        return list(self.networkOutputs)
 
     def topologicalOrder(self):
         """Kahn's algorithm, ties broken by insertion order (reference ComputationGraph.java:1216-1318)."""

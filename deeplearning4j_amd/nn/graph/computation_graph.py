@@ -439,7 +439,12 @@ class ComputationGraph(BaseNetwork):
                 l.onForwardPass(self, acts)
         mb_in = self._prep_mb if getattr(self, "_prep_mb", None) else None
         for i, o in enumerate(self.outputs):
-            layer = self.layers_by_name[o]
+            layer = self.layers_by_name.get(o)
+            if layer is None or not hasattr(layer, "setLabels"):
+                from ...exceptions import DL4JException
+                kind = type(layer.conf).__name__ if layer is not None else type(self.conf.vertices[o]).__name__
+                raise DL4JException(f"Cannot calculate gradient and score: network output \"{o}\" is not an output "
+                                    f"layer ({kind}); end the graph in an OutputLayer / RnnOutputLayer / LossLayer")
             layer.setLabels(self._to_dev(labels[i], self.master_dtype))
             layer.inputMiniBatchSize = mb_in
             lm = lmasks[i] if lmasks is not None and i < len(lmasks) else None
