@@ -6,7 +6,9 @@ ops + RCCL over xGMI for data parallelism. See SURVEY.md for the component map.
 __version__ = "0.1.0"
 
 from .datasets import *  # noqa: F401,F403
-from .exceptions import DL4JException, DL4JInvalidConfigException, DL4JInvalidInputException  # noqa: F401
+from .exceptions import (DL4JException, DL4JInvalidConfigException, DL4JInvalidInputException,  # noqa: F401
+                         InvalidInputTypeException)
 from .nn.conf import *  # noqa: F401,F403
 from .nn.graph import ComputationGraph
 from .nn.multilayer import MultiLayerNetwork
+from .nn.transferlearning import FineTuneConfiguration, TransferLearning, TransferLearningHelper  # noqa: F401

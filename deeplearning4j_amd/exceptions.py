@@ -16,3 +16,8 @@ class DL4JInvalidConfigException(DL4JException, ValueError):
 class DL4JInvalidInputException(DL4JException, ValueError):
     """Data that does not match the network (feature count vs nIn, rank of a CNN / RNN input, label width vs nOut,
     embedding indices outside [0, nIn))."""
+
+
+class InvalidInputTypeException(DL4JInvalidConfigException):
+    """An InputType that a layer cannot take, found while shapes are inferred at build time (reference
+    nn/conf/inputs/InvalidInputTypeException.java), e.g. a convolution kernel larger than the padded input."""

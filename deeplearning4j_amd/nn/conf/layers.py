@@ -24,7 +24,7 @@ from .losses import to_loss
 from .regularization import to_dropout
 from .updaters import to_updater
 from .validation import validate_kernel_geometry
-from ...exceptions import DL4JInvalidConfigException
+from ...exceptions import DL4JInvalidConfigException, InvalidInputTypeException
 from .weights import to_weight_init
 
 
@@ -142,6 +142,10 @@ class Layer(Config):
 
     def getLayerName(self):
         return self.layerName
+
+    def getActivationFn(self):
+        """The layer's activation function object (inherited from the global config when not set on the layer)."""
+        return getattr(self, "activation", None)
 
 
 class NoParamLayer(Layer):
@@ -344,8 +348,15 @@ class RnnOutputLayer(BaseOutputLayer):
 class RnnLossLayer(LossLayer):
     RUNTIME = "deeplearning4j_amd.nn.layers.output:RnnLossLayerImpl"
 
+    def getOutputType(self, layerIndex, inputType):
+        if isinstance(inputType, InputTypeFeedForward):
+            return InputType.recurrent(inputType.size)
+        return inputType
+
     def getPreProcessorForInputType(self, inputType):
-        return None
+        # feed-forward / CNN activations are reshaped back to time series first, as for the RNN layers (reference
+        # RnnLossLayer.getPreProcessorForInputType -> InputTypeUtil.getPreprocessorForInputTypeRnnLayers)
+        return RnnOutputLayer.getPreProcessorForInputType(self, inputType)
 
 
 class CnnLossLayer(LossLayer):
@@ -368,7 +379,7 @@ def conv_out_size(in_size, k, s, p, d, mode):
         return int(math.ceil(in_size / s))
     num = in_size - k_eff + 2 * p
     if num < 0:
-        raise DL4JInvalidConfigException(f"Invalid input size {in_size} for kernel {k_eff}, padding {p}: the "
+        raise InvalidInputTypeException(f"Invalid input size {in_size} for kernel {k_eff}, padding {p}: the "
                                          f"kernel is larger than the padded input")
     if mode == ConvolutionMode.Strict and num % s != 0:
         raise DL4JInvalidConfigException(
@@ -1092,6 +1103,10 @@ class Bidirectional(BaseWrapperLayer):
     FIELDS = {"mode": "CONCAT"}
     RUNTIME = "deeplearning4j_amd.nn.layers.recurrent:BidirectionalImpl"
 
+    class Mode:
+        """Bidirectional.Mode.CONCAT / ADD / MUL / AVERAGE (reference Bidirectional.Mode)."""
+        CONCAT, ADD, MUL, AVERAGE = "CONCAT", "ADD", "MUL", "AVERAGE"
+
     @classmethod
     def _builder_positional(cls, kw, *args):
         if len(args) == 1:
@@ -1149,6 +1164,7 @@ class LastTimeStep(BaseWrapperLayer):
 class FrozenLayer(BaseWrapperLayer):
     """Wraps a layer and blocks all updates to its params (reference FrozenLayer.java:77)."""
     RUNTIME = "deeplearning4j_amd.nn.layers.misc:FrozenLayerImpl"
+    _ALIASES = dict(Layer._ALIASES, layer="underlying")     # FrozenLayer.Builder().layer(l)
 
     def __init__(self, layer=None, **kw):
         if layer is not None:

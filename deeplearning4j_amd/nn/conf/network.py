@@ -495,7 +495,8 @@ class GraphBuilder:
             self._vertices[mname] = MergeVertex()
             self._vertexInputs[mname] = list(ins)
             self._vertexInputs[name] = [mname]
-            self._order.insert(self._order.index(name), mname)
+            # right after its consumer, as the reference's builder adds it (vertex indices follow this order)
+            self._order.insert(self._order.index(name) + 1, mname)
 
     def build(self):
         if not self._inputs:

@@ -97,6 +97,12 @@ class FeedForwardToRnnPreProcessor(InputPreProcessor):
         mb, size, T = eps.shape
         return eps.permute(2, 0, 1).reshape(T * mb, size)
 
+    def feedForwardMaskArray(self, mask, currentMaskState, miniBatchSize):
+        """[T*mb, 1] per-row mask (time-major, as RnnToFeedForward produced it) back to [mb, T]."""
+        if mask is None or mask.dim() != 2 or mask.shape[1] != 1 or mask.shape[0] == miniBatchSize:
+            return mask, currentMaskState
+        return mask.reshape(-1, miniBatchSize).t(), currentMaskState
+
     def getOutputType(self, inputType):
         if isinstance(inputType, InputTypeFeedForward):
             return InputType.recurrent(inputType.size)

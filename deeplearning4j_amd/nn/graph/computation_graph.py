@@ -257,6 +257,8 @@ class ComputationGraph(BaseNetwork):
 
     def feedForward(self, inputs=None, train=False, masks=None, stored_state=False, store_last_for_tbptt=False,
                     layerTillIndex=None):
+        if isinstance(inputs, bool):            # reference feedForward(boolean train) on the set inputs
+            inputs, train = None, inputs
         inputs = self._prep_inputs(self.inputs if inputs is None else inputs)
         if len(inputs) != len(self.conf.networkInputs):
             raise DL4JInvalidInputException(f"ComputationGraph has {len(self.conf.networkInputs)} inputs "
@@ -267,16 +269,19 @@ class ComputationGraph(BaseNetwork):
             masks = self.inputMaskArrays
         acts = {}
         amask = {}
+        active = {}                 # feature-mask state per vertex: False once an LSTM passed the mask through
         mb = inputs[0].shape[0]
         self._prep_mb = mb
         for i, n in enumerate(self.conf.networkInputs):
             acts[n] = inputs[i]
             amask[n] = masks[i] if masks is not None and i < len(masks) else None
+            active[n] = True
         self._ctx = {}
         for name in self.topo:
             v = self.conf.vertices[name]
             ins = [acts[i] for i in self.vertex_inputs[name]]
             ms = [amask.get(i) for i in self.vertex_inputs[name]]
+            active[name] = any(active.get(i, True) for i in self.vertex_inputs[name])
             if isinstance(v, LayerVertex):
                 x = ins[0] if len(ins) == 1 else torch.cat(ins, dim=1)
                 if len(ins) > 1:
@@ -297,6 +302,8 @@ class ComputationGraph(BaseNetwork):
                 if name in self._residual_of:
                     layer.residual = acts[self._residual_of[name]]
                 tok = _prof.layer_begin("fwd", name, layer) if _prof.ACTIVE else None
+                if not active[name] and hasattr(layer, "setLabels"):
+                    mask = None             # a passed-through feature mask does not mask an output layer
                 if stored_state and hasattr(layer, "tBpttStateMap"):
                     out = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
                 else:
@@ -305,6 +312,8 @@ class ComputationGraph(BaseNetwork):
                     _prof.layer_end(tok, "fwd", name, layer, out)
                 acts[name] = out
                 amask[name], _ = layer.feedForwardMaskArray(mask, None, mb)
+                if getattr(layer, "MASK_PASSTHROUGH", False):
+                    active[name] = False
             elif name in self._passthrough:
                 acts[name] = acts[self._passthrough[name]]
                 amask[name] = ms[0] if ms else None
@@ -335,6 +344,11 @@ class ComputationGraph(BaseNetwork):
         with torch.no_grad():
             acts = self.feedForward(list(inputs), train, masks)
         outs = [_out_dtype(acts[o]) for o in self.outputs]
+        lm = self.labelMaskArrays
+        if lm is not None:                      # label masks set with setLayerMaskArrays zero those outputs
+            from ..network_base import _apply_output_mask
+            outs = [_apply_output_mask(t, lm[i]) if i < len(lm) and hasattr(self.layers_by_name.get(o), "setLabels")
+                    else t for i, (o, t) in enumerate(zip(self.outputs, outs))]
         return outs
 
     def outputSingle(self, *inputs, train=False):
@@ -704,6 +718,40 @@ class ComputationGraph(BaseNetwork):
 
     def setLabels(self, *y):
         self.labels = list(y)
+
+    def setInput(self, i, x):
+        """Set network input i (reference ComputationGraph.setInput(int, INDArray))."""
+        n = len(self.conf.networkInputs)
+        cur = list(self.inputs) if self.inputs is not None else []
+        cur += [None] * (n - len(cur))
+        cur[i] = x
+        self.inputs = cur
+
+    def setLabel(self, i, y):
+        """Set the labels of output i (reference ComputationGraph.setLabel(int, INDArray))."""
+        cur = list(self.labels) if self.labels is not None else []
+        cur += [None] * (len(self.outputs) - len(cur))
+        cur[i] = y
+        self.labels = cur
+
+    def getInput(self, i):
+        return self.inputs[i]
+
+    def getNumInputArrays(self):
+        return len(self.conf.networkInputs)
+
+    def getNumOutputArrays(self):
+        return len(self.conf.networkOutputs)
+
+    def topologicalSortOrder(self):
+        """Topological order as vertex indices: inputs first, then vertices in the order they were added
+        (reference ComputationGraph.topologicalSortOrder / calcTopologicalSortOrder :1216-1318)."""
+        idx = {n: i for i, n in enumerate(list(self.conf.networkInputs) + list(self.conf.vertices))}
+        return [idx[n] for n in self.conf.topologicalOrder()]
+
+    def gradientAndScore(self):
+        """(gradient, score) of the last computeGradientAndScore (reference Model.gradientAndScore)."""
+        return self.gradient(), self.score()
 
     def setLearningRate(self, lr, layerName=None):
         """setLearningRate(newLr), or setLearningRate(layerName, newLr) as in the reference."""

@@ -287,6 +287,9 @@ class BaseRecurrentImpl(LayerImpl):
 
 class LSTMImpl(BaseRecurrentImpl):
     PEEPHOLE = False
+    # the feature mask leaves an LSTM in the Passthrough state: layers above still see it, but an output layer no
+    # longer masks its score with it (reference GravesLSTM/LSTM.feedForwardMaskArray, RnnOutputLayer:204-216)
+    MASK_PASSTHROUGH = True
     GRADS_OVERWRITE = True        # W / RW / b gradient views are written whole every backward (no accumulation)
 
     def _run(self, x, training, h0, c0, need_cache, mask):
@@ -431,6 +434,7 @@ class GravesBidirectionalLSTMImpl(BaseRecurrentImpl):
     def activate(self, x, training=False, mask=None, **kw):
         from ..util.time_series import reverse_time_series
         self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
         self.input = x
         self.maskArray = mask
         H = self.conf.nOut
@@ -453,7 +457,8 @@ class GravesBidirectionalLSTMImpl(BaseRecurrentImpl):
         er = reverse_time_series(eps, self.maskArray)
         dxb, _, _ = _lstm_bwd(er, self._cb, self.W("WB"), self.W("RWB"), H, True, a, ga, self._mr, tbptt_back, "",
                               {"W": self.grads["WB"], "RW": self.grads["RWB"], "b": self.grads["bB"]})
-        return self.make_gradient(), (dxf + reverse_time_series(dxb, self.maskArray)).to(eps.dtype)
+        return self.make_gradient(), self.backpropDropOut((dxf + reverse_time_series(dxb, self.maskArray))
+                                                          .to(eps.dtype))
 
     def rnnTimeStep(self, x, mask=None):
         raise NotImplementedError("GravesBidirectionalLSTM does not support rnnTimeStep (needs the full sequence)")
@@ -484,6 +489,8 @@ class SimpleRnnImpl(BaseRecurrentImpl):
     def activate(self, x, training=False, mask=None, stored_state=False, store_last_for_tbptt=False):
         if x.dim() == 2:
             x = x.unsqueeze(2)
+        self.training = training
+        x = self.applyDropOutIfNecessary(x, training)
         self.input = x
         self.maskArray = mask
         h0 = self.tBpttStateMap.get("prevAct") if stored_state else None
@@ -521,7 +528,7 @@ class SimpleRnnImpl(BaseRecurrentImpl):
         weight_grad_(self.grads["RW"], torch.stack(c["hprev"], 0).reshape(T * mb, H).t(), dzf)
         copy_grad_(self.grads["b"], dzf.sum(0))
         dx = matmul(dzf.to(self.W("W").dtype), self.W("W").t()).reshape(T, mb, -1).permute(1, 2, 0)
-        return self.make_gradient(), dx.to(eps.dtype)
+        return self.make_gradient(), self.backpropDropOut(dx.to(eps.dtype))
 
 
 class _SubView(LayerImpl):

@@ -124,6 +124,7 @@ class MultiLayerNetwork(BaseNetwork):
         mb = x.shape[0]
         acts = [x]
         mask = fmask
+        active = True                     # feature-mask state: False once an LSTM has passed it through
         chk = self._input_check([x])
         idx = self._index_checked()
         for i in range(layerNum + 1):
@@ -137,14 +138,17 @@ class MultiLayerNetwork(BaseNetwork):
                 continue
             layer.iteration, layer.epoch = self.conf.iterationCount, self.conf.epochCount
             tok = _prof.layer_begin("fwd", i, layer) if _prof.ACTIVE else None
+            lmask = mask if active or not hasattr(layer, "setLabels") else None
             if stored_state and hasattr(layer, "tBpttStateMap"):
-                x = layer.activate(x, train, mask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
+                x = layer.activate(x, train, lmask, stored_state=True, store_last_for_tbptt=store_last_for_tbptt)
             else:
-                x = layer.activate(x, train, mask)
+                x = layer.activate(x, train, lmask)
             if tok is not None:
                 _prof.layer_end(tok, "fwd", i, layer, x)
-            mask, _ = layer.feedForwardMaskArray(mask, None, mb)
+            mask, _ = layer.feedForwardMaskArray(lmask, None, mb)
+            active = active and not getattr(layer, "MASK_PASSTHROUGH", False)
             acts.append(x)
+        self._fmask_active = active
         if chk is not None and layerNum == len(self.layers) - 1:
             self._validated = chk
         return acts
@@ -178,14 +182,29 @@ class MultiLayerNetwork(BaseNetwork):
             return [self.output(ds.features, train, ds.featuresMask) for ds in x]
         if featuresMask is None:
             featuresMask = self.mask            # masks set with setLayerMaskArrays apply (reference output(INDArray))
+        if labelsMask is None:
+            labelsMask = self.labelsMask
         with torch.no_grad():
             acts = self.feedForwardToLayer(len(self.layers) - 1, x, train, self._to_dev(featuresMask))
         out = acts[-1]
+        if labelsMask is not None and hasattr(self.layers[-1], "setLabels"):
+            from .network_base import _apply_output_mask
+            out = _apply_output_mask(out, labelsMask)
         # 16-bit activations come back as fp32 (the reference's output dtype); fp32/fp64 networks keep theirs
         return out.float() if out.dtype in (torch.bfloat16, torch.float16) else out
 
     def activate(self, x, train=False):
         return self.output(x, train)
+
+    def preOutput(self, x, train=False):
+        """The output layer's pre-activation (z = x W + b) for input x, in the layout of its output (reference
+        MultiLayerNetwork.preOutput)."""
+        out = self.layers[-1]
+        with torch.no_grad():
+            self.feedForwardToLayer(len(self.layers) - 1, x, train)
+        if getattr(out, "_z", None) is None:
+            raise NotImplementedError(f"preOutput: {type(out).__name__} is not an output layer")
+        return out._out_from2d(out._z)
 
     def predict(self, x):
         return torch.argmax(self.output(x), dim=1)
@@ -255,7 +274,8 @@ class MultiLayerNetwork(BaseNetwork):
         out.inputMiniBatchSize = self._mb
         if lmask is not None:
             out.maskArray = self._to_dev(lmask)
-        elif fmask is not None and out.maskArray is None and out.input is not None and out.input.dim() == 3:
+        elif (fmask is not None and out.maskArray is None and out.input is not None and out.input.dim() == 3
+              and getattr(self, "_fmask_active", True)):
             # the feature mask doubles as the label mask of a time-series output; a layer that consumed the mask
             # on the way (LastTimeStep, global pooling) left a 2-D output that has none
             out.maskArray = self._to_dev(fmask)

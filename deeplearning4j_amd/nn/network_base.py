@@ -65,6 +65,22 @@ def init_param_(view, spec, conf, gen):
         raise ValueError(kind)
 
 
+def _apply_output_mask(out, m):
+    """Zero the label-masked entries of an output layer's activations (reference RnnOutputLayer.output :131-155 and
+    BaseOutputLayer.applyMask :427-435): [mb, T] per-step masks on [mb, n, T] outputs, per-output masks of the
+    output's own shape, [mb] / [mb, 1] per-example masks on 2-D outputs."""
+    if m is None:
+        return out
+    m = m.to(device=out.device, dtype=out.dtype)
+    if m.shape == out.shape:
+        return out * m
+    if out.dim() == 3 and m.dim() == 2:
+        return out * m.unsqueeze(1)
+    if out.dim() == 2 and m.numel() == out.shape[0]:
+        return out * m.reshape(-1, 1)
+    raise ValueError(f"label mask of shape {tuple(m.shape)} does not fit output {tuple(out.shape)}")
+
+
 class BaseNetwork:
     def __init__(self, conf):
         self.conf = conf

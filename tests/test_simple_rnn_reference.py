@@ -1,0 +1,115 @@
+"""SimpleRnn recurrence and recurrent-layer dropout, after the reference's TestSimpleRnn
+(deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/recurrent/TestSimpleRnn.java:25-70) and
+TestRnnLayers.testDropoutRecurrentLayers (TestRnnLayers.java:28-110): SimpleRnn's output at step t is
+tanh(x_t W + h_{t-1} RW + b), checked step by step against a hand recurrence, and it survives ModelSerializer; for
+GravesLSTM / LSTM / SimpleRnn, input dropout changes neither the initial parameters nor inference output, but does
+change the training-mode output and the parameters after one fit. fp64, CPU."""
+import io
+
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+
+
+def test_simple_rnn_matches_hand_recurrence():
+    m, nIn, n, T = 3, 5, 6, 7
+    x = torch.rand(m, nIn, T, generator=torch.Generator().manual_seed(12345), dtype=torch.float64)
+    conf = (D.NeuralNetConfiguration.Builder().updater(D.NoOp()).weightInit(D.WeightInit.XAVIER)
+            .activation(D.Activation.TANH).dataType(D.DataType.DOUBLE).list()
+            .layer(D.SimpleRnn.Builder().nIn(nIn).nOut(n).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    out = net.output(x)
+    w, rw, b = net.getParam("0_W"), net.getParam("0_RW"), net.getParam("0_b").reshape(1, -1)
+    last = None
+    for t in range(T):
+        z = x[:, :, t] @ w + b
+        if last is not None:
+            z = z + last @ rw
+        exp = torch.tanh(z)
+        assert torch.allclose(out[:, :, t], exp, atol=1e-12), t
+        last = exp
+    from deeplearning4j_amd.utils.model_serializer import ModelSerializer
+    buf = io.BytesIO()
+    ModelSerializer.writeModel(net, buf, True)
+    buf.seek(0)
+    back = ModelSerializer.restoreMultiLayerNetwork(buf, True)
+    assert torch.equal(back.output(x), out)
+
+
+def _rnn_layer(kind, dropout):
+    cls = {"graves": D.GravesLSTM, "lstm": D.LSTM, "simple": D.SimpleRnn}[kind]
+    b = cls.Builder().activation(D.Activation.TANH).nIn(10).nOut(10)
+    if dropout is not None:
+        b = b.dropOut(dropout)
+    return b.build()
+
+
+def _net(kind, dropout):
+    conf = (D.NeuralNetConfiguration.Builder().seed(12345).dataType(D.DataType.DOUBLE).list()
+            .layer(_rnn_layer(kind, dropout))
+            .layer(D.RnnOutputLayer.Builder().activation(D.Activation.TANH).nIn(10).nOut(10).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    return net
+
+
+@pytest.mark.parametrize("kind", ["graves", "lstm", "simple"])
+def test_dropout_recurrent_layers(kind):
+    torch.manual_seed(12345)
+    net, netD = _net(kind, None), _net(kind, 0.5)
+    assert torch.equal(net.params(), netD.params())
+    f = torch.rand(3, 10, 10, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    assert torch.equal(net.output(f), netD.output(f))                 # inference: no dropout
+    assert not torch.allclose(net.output(f, True), netD.output(f, True))  # training mode: dropout applied
+    lab = torch.zeros(3, 10, 10, dtype=torch.float64)
+    g = torch.Generator().manual_seed(12345)
+    for i in range(3):
+        for t in range(10):
+            lab[i, int(torch.randint(10, (1,), generator=g)), t] = 1.0
+    net.fit(f.clone(), lab)
+    netD.fit(f.clone(), lab)
+    assert not torch.allclose(net.params(), netD.params())
+
+
+def _rev(t):
+    return torch.flip(t, dims=[2])
+
+
+@pytest.mark.parametrize("mode", ["CONCAT", "ADD", "AVERAGE", "MUL"])
+def test_bidirectional_simple_rnn_matches_two_directions(mode):
+    """BidirectionalTest.testSimpleBidirectional (BidirectionalTest.java:358-478): Bidirectional(mode, SimpleRnn)
+    equals a forward SimpleRnn merged with a SimpleRnn run over the reversed series (its output reversed back); for
+    ADD / CONCAT the per-direction parameter gradients equal those of the two single-direction layers."""
+    x = torch.rand(3, 10, 6, generator=torch.Generator().manual_seed(12345), dtype=torch.float64)
+
+    def base():
+        return (D.NeuralNetConfiguration.Builder().activation(D.Activation.TANH).weightInit(D.WeightInit.XAVIER)
+                .updater(D.Adam()).dataType(D.DataType.DOUBLE).list())
+    n1 = D.MultiLayerNetwork(base().layer(D.Bidirectional(getattr(D.Bidirectional.Mode, mode),
+                                                          D.SimpleRnn.Builder().nIn(10).nOut(10).build())).build())
+    n1.init()
+    n2 = D.MultiLayerNetwork(base().layer(D.SimpleRnn.Builder().nIn(10).nOut(10).build()).build())
+    n2.init()
+    n3 = D.MultiLayerNetwork(base().layer(D.SimpleRnn.Builder().nIn(10).nOut(10).build()).build())
+    n3.init()
+    for k in ("W", "RW", "b"):
+        n2.setParam(f"0_{k}", n1.getParam(f"0_f{k}"))
+        n3.setParam(f"0_{k}", n1.getParam(f"0_b{k}"))
+    o1, o2, o3 = n1.output(x), n2.output(x), _rev(n3.output(_rev(x)))
+    exp = {"ADD": o2 + o3, "MUL": o2 * o3, "AVERAGE": (o2 + o3) * 0.5, "CONCAT": torch.cat([o2, o3], 1)}[mode]
+    assert torch.allclose(o1, exp, atol=1e-12)
+    if mode in ("ADD", "CONCAT"):
+        eps = torch.rand(3, 10, 6, generator=torch.Generator().manual_seed(7), dtype=torch.float64)
+        eps1 = torch.cat([eps, eps], 1) if mode == "CONCAT" else eps
+        l1, l2, l3 = n1.getLayer(0), n2.getLayer(0), n3.getLayer(0)
+        l1.activate(x, True)
+        l2.activate(x, True)
+        l3.activate(_rev(x), True)
+        g1 = {k: v.clone() for k, v in l1.backpropGradient(eps1)[0].gradientForVariable().items()}
+        g2 = {k: v.clone() for k, v in l2.backpropGradient(eps)[0].gradientForVariable().items()}
+        g3 = {k: v.clone() for k, v in l3.backpropGradient(_rev(eps))[0].gradientForVariable().items()}
+        for k in ("W", "RW", "b"):
+            assert torch.allclose(g1["f" + k], g2[k], atol=1e-12), k
+            assert torch.allclose(g1["b" + k], g3[k], atol=1e-12), k
