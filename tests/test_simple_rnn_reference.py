@@ -113,3 +113,37 @@ def test_bidirectional_simple_rnn_matches_two_directions(mode):
         for k in ("W", "RW", "b"):
             assert torch.allclose(g1["f" + k], g2[k], atol=1e-12), k
             assert torch.allclose(g1["b" + k], g3[k], atol=1e-12), k
+
+
+def test_graves_bidirectional_lstm_is_forward_plus_reversed_graves_lstm():
+    """GravesBidirectionalLSTMTest.testSimpleForwardsAndBackwardsActivation (GravesBidirectionalLSTMTest.java:246-430):
+    with its forward parameters copied into one GravesLSTM and its backward parameters into another run over the
+    reversed series, the bidirectional layer's activation is the sum of the two, and its per-direction gradients are
+    theirs."""
+    nIn, n, mb, T = 2, 3, 1, 5
+
+    def net(layer):
+        m = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().seed(12345).updater(D.NoOp())
+                                .dataType(D.DataType.DOUBLE).list().layer(layer).build())
+        m.init()
+        return m
+    bi = net(D.GravesBidirectionalLSTM.Builder().nIn(nIn).nOut(n).weightInit(D.WeightInit.DISTRIBUTION)
+             .dist(D.UniformDistribution(-0.1, 0.1)).activation(D.Activation.TANH).build())
+    fw = net(D.GravesLSTM.Builder().nIn(nIn).nOut(n).activation(D.Activation.TANH).build())
+    bw = net(D.GravesLSTM.Builder().nIn(nIn).nOut(n).activation(D.Activation.TANH).build())
+    for k, kf, kb in (("W", "WF", "WB"), ("RW", "RWF", "RWB"), ("b", "bF", "bB")):
+        assert tuple(fw.getParam(f"0_{k}").shape) == tuple(bi.getParam(f"0_{kf}").shape)
+        fw.setParam(f"0_{k}", bi.getParam(f"0_{kf}"))
+        bw.setParam(f"0_{k}", bi.getParam(f"0_{kb}"))
+    x = torch.rand(mb, nIn, T, generator=torch.Generator().manual_seed(12345), dtype=torch.float64)
+    lb, lf, lr = bi.getLayer(0), fw.getLayer(0), bw.getLayer(0)
+    out = lb.activate(x, True)
+    exp = lf.activate(x, True) + _rev(lr.activate(_rev(x), True))
+    assert torch.allclose(out, exp, atol=1e-12)
+    eps = torch.rand(mb, n, T, generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    gb = {k: v.clone() for k, v in lb.backpropGradient(eps)[0].gradientForVariable().items()}
+    gf = {k: v.clone() for k, v in lf.backpropGradient(eps)[0].gradientForVariable().items()}
+    gr = {k: v.clone() for k, v in lr.backpropGradient(_rev(eps))[0].gradientForVariable().items()}
+    for k, kf, kb in (("W", "WF", "WB"), ("RW", "RWF", "RWB"), ("b", "bF", "bB")):
+        assert torch.allclose(gb[kf], gf[k], atol=1e-12), k
+        assert torch.allclose(gb[kb], gr[k], atol=1e-12), k
