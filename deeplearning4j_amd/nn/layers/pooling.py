@@ -19,6 +19,20 @@ class GlobalPoolingLayerImpl(LayerImpl):
         return (x.dim() == 4 and mask is None and dims == (2, 3) and pt in (PoolingType.AVG, PoolingType.SUM)
                 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous())
 
+    @staticmethod
+    def _cnn_mask(mask, x):
+        """A [mb, H] or [mb, W] mask over CNN activations whose other spatial size is 1 (reference
+        MaskedReductionUtil.maskedPoolingConvolution), or a [mb, 1, H, W] mask, as [mb, 1, H, W]."""
+        n, _, h, w = x.shape
+        if mask.dim() == 4:
+            return mask.expand(n, 1, h, w)
+        if mask.dim() == 2 and mask.shape[1] == w and (h == 1 or mask.shape[1] != h):
+            return mask.reshape(n, 1, 1, w).expand(n, 1, h, w)
+        if mask.dim() == 2 and mask.shape[1] == h:
+            return mask.reshape(n, 1, h, 1).expand(n, 1, h, w)
+        raise ValueError(f"GlobalPooling: a mask of shape {tuple(mask.shape)} does not fit CNN activations "
+                         f"{tuple(x.shape)}; use [mb, H] with W == 1 or [mb, W] with H == 1")
+
     def activate(self, x, training=False, mask=None):
         self.input = x
         dims = self._dims(x)
@@ -41,6 +55,8 @@ class GlobalPoolingLayerImpl(LayerImpl):
         m = None
         if mask is not None and x.dim() == 3:
             m = _acc(mask).unsqueeze(1)                                  # [mb,1,T]
+        elif mask is not None and x.dim() == 4:
+            m = self._cnn_mask(_acc(mask), x)                           # [mb,1,H,W]
         self._mask = m
         if pt == PoolingType.MAX:
             xm = xf if m is None else xf.masked_fill(m == 0, float("-inf"))

@@ -1,0 +1,84 @@
+"""LocalResponseNormalization against the reference's numeric fixture, after LocalResponseTest
+(deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/normalization/LocalResponseTest.java:35-200): the
+input, expected activations, epsilon and expected input-epsilon arrays ([2, 7, 3, 2], k=2, n=5, alpha=1e-4,
+beta=0.75) are read from the reference test's own source text; plus the hand-computed cross-channel formula
+(testLrnManual) with the default k=2, n=5 window and an LRN inside a small CNN that fits. fp64, CPU."""
+import os
+import re
+
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+
+SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/normalization/"
+       "LocalResponseTest.java")
+
+
+def _fixture(name):
+    text = open(SRC).read()
+    m = re.search(name + r"\s*=\s*Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}", text)
+    vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
+    shape = [int(v) for v in m.group(2).split(",")]
+    return torch.tensor(vals, dtype=torch.float64).reshape(shape)
+
+
+def _layer(**kw):
+    b = D.LocalResponseNormalization.Builder()
+    for k, v in kw.items():
+        b = getattr(b, k)(v)
+    conf = (D.NeuralNetConfiguration.Builder().seed(123).dataType(D.DataType.DOUBLE).list().layer(b.build())
+            .layer(D.CnnLossLayer.Builder(D.LossFunction.MSE).activation(D.Activation.IDENTITY).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    return net.getLayer(0)
+
+
+@pytest.mark.skipif(not os.path.exists(SRC), reason="reference LocalResponseTest.java not present")
+def test_lrn_matches_reference_fixture():
+    x = _fixture("x")
+    layer = _layer(k=2, n=5, alpha=1e-4, beta=0.75)
+    act = layer.activate(x, True)
+    assert tuple(act.shape) == (2, 7, 3, 2)
+    # the reference's own expected values were generated in numpy to ~1e-8 precision
+    assert torch.allclose(act, _fixture("activationsExpected"), atol=1e-6)
+    g, eps_in = layer.backpropGradient(_fixture("epsilon"))
+    exp = _fixture("newEpsilonExpected")
+    assert tuple(eps_in.shape) == tuple(exp.shape)
+    flat, eflat = eps_in.reshape(-1), exp.reshape(-1)
+    for i in (8, 20):                           # the indices the reference checks, to 1e-4
+        assert abs(float(flat[i]) - float(eflat[i])) < 1e-4, i
+    assert torch.allclose(eps_in, exp, atol=1e-4)
+    assert g.getGradientFor("W") is None
+
+
+def test_lrn_manual_formula():
+    wh, depth, mb, n, k, alpha, beta = 5, 6, 3, 5, 2.0, 1e-4, 0.75
+    x = torch.rand(mb, depth, wh, wh, generator=torch.Generator().manual_seed(12345), dtype=torch.float64)
+    exp = torch.zeros_like(x)
+    for i in range(depth):
+        lo, hi = max(0, i - n // 2), min(depth - 1, i + n // 2)
+        s = (x[:, lo:hi + 1] ** 2).sum(1)
+        exp[:, i] = x[:, i] / (k + alpha * s) ** beta
+    out = _layer().activate(x, True)                  # defaults k=2, n=5, alpha=1e-4, beta=0.75
+    assert torch.allclose(out, exp, atol=1e-12)
+
+
+def test_lrn_in_cnn_fits():
+    conf = (D.NeuralNetConfiguration.Builder().seed(123).list()
+            .layer(0, D.ConvolutionLayer.Builder().nIn(1).nOut(6).weightInit(D.WeightInit.XAVIER)
+                   .activation(D.Activation.RELU).build())
+            .layer(1, D.LocalResponseNormalization.Builder().build())
+            .layer(2, D.DenseLayer.Builder().nOut(2).build())
+            .layer(3, D.OutputLayer.Builder(D.LossFunction.MCXENT).weightInit(D.WeightInit.XAVIER)
+                   .activation(D.Activation.SOFTMAX).nIn(2).nOut(10).build())
+            .setInputType(D.InputType.convolutionalFlat(28, 28, 1)).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    x = torch.rand(2, 784, generator=torch.Generator().manual_seed(1))
+    y = torch.zeros(2, 10)
+    y[0, 1] = y[1, 7] = 1
+    before = net.params().clone()
+    net.fit(D.DataSet(x, y))
+    assert not torch.equal(before, net.params())
+    assert torch.isfinite(net.params()).all()
