@@ -75,6 +75,15 @@ class Layer(Config):
             kw["constraints"].append(c)
 
     @staticmethod
+    def _builder_hook_constrainRecurrent(kw, v):
+        # recurrent weights of LSTM / GravesLSTM / SimpleRnn (reference BaseRecurrentLayer.Builder.constrainRecurrent)
+        kw.setdefault("constraints", [])
+        for c in (v if isinstance(v, list) else [v]):
+            c = c.clone()
+            c.params = ["RW"]
+            kw["constraints"].append(c)
+
+    @staticmethod
     def _builder_hook_constrainAllParameters(kw, v):
         kw.setdefault("constraints", [])
         for c in (v if isinstance(v, list) else [v]):

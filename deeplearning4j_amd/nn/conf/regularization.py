@@ -223,9 +223,9 @@ class MaxNormConstraint(LayerConstraint):
         super().__init__(maxNorm=maxNorm, **kw)
 
     def apply_(self, key, p):
-        # reference MaxNormConstraint: norm over the input dimension(s) = all dims except the output one
-        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
-        n = p.norm(dim=dims, keepdim=True)
+        # reference MaxNormConstraint: norms along the configured dimensions (1 for [nIn, nOut] dense / RNN weights,
+        # [1, 2, 3] for [out, in, kH, kW] conv weights)
+        n = p.norm(dim=self._norm_dims(p), keepdim=True)
         scale = torch.clamp(self.maxNorm / (n + 1e-6), max=1.0)
         p.mul_(scale)
 
@@ -233,9 +233,13 @@ class MaxNormConstraint(LayerConstraint):
 class MinMaxNormConstraint(LayerConstraint):
     FIELDS = {"min": 0.0, "max": 1.0, "rate": 1.0}
 
+    def __init__(self, min=0.0, max=1.0, rate=1.0, *dims, **kw):
+        if dims:
+            kw["dimensions"] = list(dims)
+        super().__init__(min=min, max=max, rate=rate, **kw)
+
     def apply_(self, key, p):
-        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
-        n = p.norm(dim=dims, keepdim=True)
+        n = p.norm(dim=self._norm_dims(p), keepdim=True)
         clipped = torch.clamp(n, self.min, self.max)
         target = self.rate * clipped + (1 - self.rate) * n
         p.mul_(target / (n + 1e-6))
@@ -247,9 +251,13 @@ class NonNegativeConstraint(LayerConstraint):
 
 
 class UnitNormConstraint(LayerConstraint):
+    def __init__(self, *dims, **kw):
+        if dims:
+            kw["dimensions"] = list(dims)
+        super().__init__(**kw)
+
     def apply_(self, key, p):
-        dims = [0] if p.dim() == 2 else list(range(1, p.dim()))
-        p.div_(p.norm(dim=dims, keepdim=True) + 1e-6)
+        p.div_(p.norm(dim=self._norm_dims(p), keepdim=True) + 1e-6)
 
 
 _ = Distribution  # re-export convenience
