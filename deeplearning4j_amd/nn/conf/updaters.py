@@ -28,6 +28,16 @@ class ScheduleType(Enum):
 
 class ISchedule(Config):
     FIELDS = {"scheduleType": ScheduleType.ITERATION}
+    _POSITIONAL = None      # reference constructor order; default (scheduleType, *this class's FIELDS)
+
+    def __init__(self, *args, **kw):
+        if args:
+            names = self._POSITIONAL or ("scheduleType",) + tuple(type(self).__dict__.get("FIELDS", {}))
+            if len(args) > len(names):
+                raise TypeError(f"{type(self).__name__} takes at most {len(names)} positional arguments {names}")
+            for n, a in zip(names, args):
+                kw[n] = a
+        super().__init__(**kw)
 
     def _t(self, iteration, epoch):
         return iteration if self.scheduleType == ScheduleType.ITERATION else epoch
@@ -38,6 +48,7 @@ class ISchedule(Config):
 
 class FixedSchedule(ISchedule):
     FIELDS = {"value": 0.0}
+    _POSITIONAL = ("value",)
 
     def valueAt(self, iteration, epoch):
         return self.value
