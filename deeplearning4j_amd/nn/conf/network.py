@@ -248,6 +248,26 @@ class ListBuilder:
         self._g["cacheMode"] = CacheMode.of(m)
         return self
 
+    @staticmethod
+    def _infer_input_type(confs, pps):
+        """No setInputType: a first recurrent layer with nIn implies recurrent input, a first Dense / Embedding /
+        Output layer with nIn implies feed-forward input (convolutional input cannot be guessed), so the FF<->RNN
+        preprocessors still get added (reference MultiLayerConfiguration.Builder.build)."""
+        from .layers import DenseLayer, EmbeddingLayer, OutputLayer
+        if not confs or 0 in pps:
+            return None
+        first = confs[0]
+        n_in = getattr(first, "nIn", 0) or 0
+        if n_in <= 0:
+            return None
+        from .layers import Bidirectional, GravesBidirectionalLSTM, GravesLSTM, LSTM, SimpleRnn
+        if isinstance(first, (LSTM, GravesLSTM, GravesBidirectionalLSTM, SimpleRnn)) and \
+                not isinstance(first, Bidirectional):
+            return InputType.recurrent(n_in)
+        if type(first) in (DenseLayer, EmbeddingLayer, OutputLayer):
+            return InputType.feedForward(n_in)
+        return None
+
     def build(self):
         n = len(self._layers)
         if sorted(self._layers) != list(range(n)):
@@ -257,8 +277,8 @@ class ListBuilder:
         for c in confs:
             c.applyGlobal(g)
         pps = dict(self._pp)
-        if self._inputType is not None:
-            t = self._inputType
+        t = self._inputType if self._inputType is not None else self._infer_input_type(confs, pps)
+        if t is not None:
             for i, c in enumerate(confs):
                 if i not in pps:
                     pp = c.getPreProcessorForInputType(t)
