@@ -182,26 +182,90 @@ def _to_device(ds, device, pin=False):
     return DataSet(mv(ds.features), mv(ds.labels), mv(ds.featuresMask), mv(ds.labelsMask))
 
 
-class MultipleEpochsIterator(DataSetIterator):
-    def __init__(self, numEpochs, base):
-        self.n = numEpochs
-        self.base = base
-        self.epoch = 0
+class _DataSetSource:
+    """A single in-memory DataSet seen as an iterator: next(num) hands out the next num examples (all remaining when
+    num is None)."""
+
+    def __init__(self, ds):
+        self.ds = ds
+        self.pos = 0
 
     def hasNext(self):
+        return self.pos < self.ds.numExamples()
+
+    def next(self, num=None):
+        n = self.ds.numExamples()
+        end = n if num is None else min(n, self.pos + num)
+        out = self.ds if (self.pos == 0 and end == n) else self.ds.get(list(range(self.pos, end)))
+        self.pos = end
+        return out
+
+    def reset(self):
+        self.pos = 0
+
+    def batch(self):
+        return self.ds.numExamples()
+
+
+class MultipleEpochsIterator(DataSetIterator):
+    """Replays an iterator (or one DataSet) for ``numEpochs`` epochs, or for ``totalIterations`` minibatches
+    (reference datasets/iterator/MultipleEpochsIterator.java). Constructors as in the reference:
+    (numEpochs, iterator[, queueSize]), (iterator, queueSize, totalIterations), (numEpochs, DataSet). ``epochs``
+    counts completed passes."""
+
+    def __init__(self, *args):
+        from .dataset import DataSet
+        self.numEpochs, self.totalIterations = 1, None
+        if isinstance(args[0], int):
+            self.numEpochs = args[0]
+            src = args[1]
+        else:
+            src = args[0]
+            if len(args) >= 3:
+                self.totalIterations = int(args[2])
+                self.numEpochs = 2 ** 62
+        self.base = _DataSetSource(src) if isinstance(src, DataSet) else src
+        self.epochs = 0
+        self.iterations = 0
+        self._counted = False
+
+    @property
+    def n(self):
+        return self.numEpochs
+
+    @property
+    def epoch(self):
+        return self.epochs
+
+    def hasNext(self):
+        if self.totalIterations is not None:
+            if self.iterations >= self.totalIterations:
+                return False
+            if not self.base.hasNext():
+                self.epochs += 1
+                self.base.reset()
+            return self.base.hasNext()
         if self.base.hasNext():
             return True
-        if self.epoch + 1 < self.n:
-            self.epoch += 1
+        if not self._counted:                  # the underlying pass just ended
+            self.epochs += 1
+            self._counted = True
+        if self.epochs < self.numEpochs:
             self.base.reset()
+            self._counted = False
             return self.base.hasNext()
         return False
 
     def next(self, num=None):
-        return self.base.next()
+        if not self.hasNext():
+            raise StopIteration("MultipleEpochsIterator: no more minibatches")
+        self.iterations += 1
+        return self.base.next(num) if num is not None else self.base.next()
 
     def reset(self):
-        self.epoch = 0
+        self.epochs = 0
+        self.iterations = 0
+        self._counted = False
         self.base.reset()
 
     def batch(self):
@@ -209,7 +273,12 @@ class MultipleEpochsIterator(DataSetIterator):
 
 
 class EarlyTerminationDataSetIterator(DataSetIterator):
+    """At most ``terminationPoint`` minibatches per pass; asking for more is an error (reference
+    datasets/iterator/EarlyTerminationDataSetIterator.java)."""
+
     def __init__(self, base, terminationPoint):
+        if terminationPoint <= 0:
+            raise ValueError("Termination point (the number of calls to .next() or .fit()) must be > 0")
         self.base = base
         self.limit = terminationPoint
         self.i = 0
@@ -218,8 +287,10 @@ class EarlyTerminationDataSetIterator(DataSetIterator):
         return self.i < self.limit and self.base.hasNext()
 
     def next(self, num=None):
+        if self.i >= self.limit:
+            raise RuntimeError("Calls to next have exceeded the allotted number of minibatches.")
         self.i += 1
-        return self.base.next()
+        return self.base.next(num) if num is not None else self.base.next()
 
     def reset(self):
         self.i = 0
