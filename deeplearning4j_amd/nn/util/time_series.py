@@ -29,3 +29,42 @@ def last_time_step(x, mask=None):
         return x[:, :, -1]
     lengths = mask.reshape(mask.shape[0], -1).sum(dim=1).long().clamp(min=1)
     return x[torch.arange(x.shape[0], device=x.device), :, lengths - 1]
+
+
+class TimeSeriesUtils:
+    """Static helpers with the reference's names (nn/util/TimeSeriesUtils.java). 2-D forms of [mb, n, T] series are
+    time-major (row t*mb + i is example i at step t), the layout RnnToFeedForwardPreProcessor produces."""
+
+    @staticmethod
+    def movingAverage(x, n):
+        """Mean of every window of n consecutive values of a vector (len(x) - n + 1 values)."""
+        x = torch.as_tensor(x).reshape(-1).double()
+        c = torch.cumsum(x, 0)
+        c[n:] = c[n:] - c[:-n].clone()
+        return c[n - 1:] / n
+
+    @staticmethod
+    def reverseTimeSeries(x, mask=None):
+        return reverse_time_series(x, mask)
+
+    @staticmethod
+    def reshape3dTo2d(x):
+        mb, n, T = x.shape
+        return x.permute(2, 0, 1).reshape(T * mb, n)
+
+    @staticmethod
+    def reshape2dTo3d(x, miniBatchSize):
+        rows, n = x.shape
+        return x.reshape(rows // miniBatchSize, miniBatchSize, n).permute(1, 2, 0)
+
+    @staticmethod
+    def reshapeTimeSeriesMaskToVector(mask):
+        return mask.t().reshape(-1, 1)
+
+    @staticmethod
+    def reshapeVectorToTimeSeriesMask(v, miniBatchSize):
+        return v.reshape(-1, miniBatchSize).t()
+
+    @staticmethod
+    def pullLastTimeSteps(x, mask=None):
+        return last_time_step(x, mask)
