@@ -172,6 +172,29 @@ class Config:
     def _post_init(self):
         pass
 
+    _GETTER_ALIASES = {"IUpdater": "updater", "ActivationFn": "activation", "LossFn": "lossFn",
+                       "LossFunction": "lossFn", "Dist": "dist"}
+
+    def __getattr__(self, name):
+        """Java-style getters for every field (``getL2()``, ``getIUpdater()``, ``getMomentum()``, ``isX()``), as the
+        reference's Lombok-generated accessors. Only reached when normal attribute lookup fails."""
+        if name.startswith("_") or not (name.startswith("get") or name.startswith("is")) or len(name) < 3:
+            raise AttributeError(name)
+        stem = name[3:] if name.startswith("get") else name[2:]
+        if not stem:
+            raise AttributeError(name)
+        fields = type(self)._all_fields()
+        field = self._GETTER_ALIASES.get(stem)
+        if field is None:
+            for cand in (stem[0].lower() + stem[1:], stem, stem.lower()):
+                cand = self._ALIASES.get(cand, cand)
+                if cand in fields:
+                    field = cand
+                    break
+        if field is None or field not in fields:
+            raise AttributeError(f"{type(self).__name__} has no attribute {name!r}")
+        return lambda: self.__dict__.get(field)
+
     # --- serde -------------------------------------------------------------------------------
     def to_dict(self):
         d = {"@class": type(self).__name__}

@@ -182,6 +182,9 @@ class BaseLayer(Layer):
             self.activation = ActivationSigmoid()
         if self.weightInit is None:
             self.weightInit = WeightInit.XAVIER
+        if self.weightInit == WeightInit.DISTRIBUTION and self.dist is None:
+            from .weights import NormalDistribution
+            self.dist = NormalDistribution(0, 1)      # the reference builder's default distribution
         if self.biasInit is None:
             self.biasInit = 0.0
         for k in ("l1", "l2", "l1Bias", "l2Bias"):
