@@ -13,13 +13,14 @@ from .weights import Distribution, NormalDistribution
 
 
 class IDropout(Config):
-    """applyDropout(x, iteration, epoch, training) -> x'; backprop(grad) uses the saved mask.
+    """applyDropout(x, iteration, epoch, inPlace) -> x'; backprop(grad) uses the saved mask. As in the reference it is
+    called only for training passes; ``inPlace`` is accepted for signature parity (the input is never overwritten).
 
     On the GPU the whole family runs on one counter-based Philox kernel (csrc/nn_misc.hip): no mask is stored, the
     backward regenerates it from the layer's (seed, device counter), and the counter advance is a device op, so
     captured HIP-graph steps draw a fresh mask every replay. CPU tensors use torch's generator and a saved mask."""
 
-    def applyDropout(self, x, iteration=0, epoch=0, training=True):
+    def applyDropout(self, x, iteration=0, epoch=0, inPlace=False):
         raise NotImplementedError
 
     def backprop(self, grad):
@@ -64,9 +65,7 @@ class Dropout(IDropout):
     def __init__(self, p=0.5, **kw):
         super().__init__(p=p, **kw)
 
-    def applyDropout(self, x, iteration=0, epoch=0, training=True):
-        if not training:
-            return x
+    def applyDropout(self, x, iteration=0, epoch=0, inPlace=False):
         p = _pval(self.p, iteration, epoch)
         if p >= 1.0:
             self._mask = self._native = None
@@ -94,13 +93,17 @@ class AlphaDropout(IDropout):
     def __init__(self, p=0.5, **kw):
         super().__init__(p=p, **kw)
 
-    def applyDropout(self, x, iteration=0, epoch=0, training=True):
-        if not training:
-            return x
+    def a(self, p):
+        alpha_p = -self.LAMBDA * self.ALPHA
+        return 1.0 / math.sqrt(p + alpha_p * alpha_p * p * (1 - p))
+
+    def b(self, p):
+        return -self.a(p) * (1 - p) * (-self.LAMBDA * self.ALPHA)
+
+    def applyDropout(self, x, iteration=0, epoch=0, inPlace=False):
         p = _pval(self.p, iteration, epoch)
         alpha_p = -self.LAMBDA * self.ALPHA
-        a = 1.0 / math.sqrt(p + alpha_p * alpha_p * p * (1 - p))
-        b = -a * alpha_p * (1 - p)
+        a, b = self.a(p), self.b(p)
         y = self._gpu(x, "alpha", p=p, a=a, b=b, alpha_p=alpha_p)
         if y is not None:
             return y
@@ -120,9 +123,7 @@ class GaussianDropout(IDropout):
     def __init__(self, rate=0.5, **kw):
         super().__init__(rate=rate, **kw)
 
-    def applyDropout(self, x, iteration=0, epoch=0, training=True):
-        if not training:
-            return x
+    def applyDropout(self, x, iteration=0, epoch=0, inPlace=False):
         r = _pval(self.rate, iteration, epoch)
         std = math.sqrt(r / (1 - r))
         y = self._gpu(x, "gaussian_dropout", sd=std)
@@ -143,9 +144,7 @@ class GaussianNoise(IDropout):
     def __init__(self, stddev=0.1, **kw):
         super().__init__(stddev=stddev, **kw)
 
-    def applyDropout(self, x, iteration=0, epoch=0, training=True):
-        if not training:
-            return x
+    def applyDropout(self, x, iteration=0, epoch=0, inPlace=False):
         s = _pval(self.stddev, iteration, epoch)
         y = self._gpu(x, "gaussian_noise", sd=s)
         return y if y is not None else x + torch.randn_like(x) * s

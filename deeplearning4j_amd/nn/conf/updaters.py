@@ -92,6 +92,21 @@ class StepSchedule(ISchedule):
 class MapSchedule(ISchedule):
     FIELDS = {"values": None}
 
+    class Builder:
+        """MapSchedule.Builder(ScheduleType).add(i, v)...build() (reference MapSchedule.Builder)."""
+
+        def __init__(self, scheduleType):
+            self._t, self._v = scheduleType, {}
+
+        def add(self, position, value):
+            self._v[int(position)] = value
+            return self
+
+        def build(self):
+            if 0 not in self._v:
+                raise ValueError("MapSchedule needs a value for position 0")
+            return MapSchedule(self._t, dict(self._v))
+
     def valueAt(self, iteration, epoch):
         t = self._t(iteration, epoch)
         keys = sorted(int(k) for k in self.values)

@@ -80,7 +80,7 @@ class LayerImpl:
         d = getattr(self.conf, "idropout", None)
         if training and d is not None:
             self.dropoutApplied = True
-            return d.applyDropout(x, self.iteration, self.epoch, True)
+            return d.applyDropout(x, self.iteration, self.epoch, False)
         self.dropoutApplied = False
         return x
 
