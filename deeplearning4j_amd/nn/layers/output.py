@@ -246,13 +246,20 @@ class CnnLossLayerImpl(BaseOutputLayerImpl):
 class CenterLossOutputLayerImpl(BaseOutputLayerImpl):
     """Adds lambda/2 * ||x - c_y||^2 to the score; centers move toward class means with rate alpha."""
 
+    def activate(self, x, training=False, mask=None):
+        self._center_sq = None
+        return super().activate(x, training, mask)
+
     def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
         base = super().computeScore(fullNetworkL1, fullNetworkL2, training)
-        c = self.params["cL"]
-        y = _acc(self.labels)
-        centers = y @ _acc(c)
-        d = _acc(self._x2) - centers
-        return base + 0.5 * self.conf.lambda_ * (d * d).sum() / self._score_mb()
+        sq = getattr(self, "_center_sq", None)
+        if sq is None:
+            c = self.params["cL"]
+            d = _acc(self._x2) - _acc(self.labels) @ _acc(c)
+            sq = (d * d).sum()
+        # with the centers as they were for this forward pass: backprop moves them afterwards, the reference moves
+        # them in the update that follows the score (CenterLossOutputLayer.computeScore)
+        return base + 0.5 * self.conf.lambda_ * sq / self._score_mb()
 
     def backpropGradient(self, eps=None):
         g, eps_prev = super().backpropGradient(eps)
@@ -260,6 +267,7 @@ class CenterLossOutputLayerImpl(BaseOutputLayerImpl):
         y = _acc(self.labels)
         x = _acc(self._x2)
         d = x - y @ _acc(c)
+        self._center_sq = (d * d).sum()
         eps_prev = eps_prev + (self.conf.lambda_ * d).to(eps_prev.dtype)
         if self.conf.gradientCheck:
             # the exact gradient of the center term w.r.t. the centers; the centers themselves stay put
