@@ -12,3 +12,5 @@ from .nn.conf import *  # noqa: F401,F403
 from .nn.graph import ComputationGraph
 from .nn.multilayer import MultiLayerNetwork
 from .nn.transferlearning import FineTuneConfiguration, TransferLearning, TransferLearningHelper  # noqa: F401
+from .eval import (Evaluation, EvaluationBinary, EvaluationCalibration, RegressionEvaluation,  # noqa: F401
+                   ROC, ROCBinary, ROCMultiClass)
