@@ -1,0 +1,78 @@
+"""SubsamplingLayer against the reference's numeric fixtures, after SubsamplingLayerTest
+(deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/SubsamplingLayerTest.java:48-180): 2x2
+MAX and AVG pooling (stride 2) of the fixed [1, 2, 4, 4] input give the expected [1, 2, 2, 2] outputs, and their
+backward passes route / spread the given epsilons to the expected [1, 2, 4, 4] input gradients; no "W" gradient; a
+kernel larger than the input is rejected. The arrays are read from the reference test's source text. fp64, CPU."""
+import os
+import re
+
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+
+SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/"
+       "SubsamplingLayerTest.java")
+pytestmark = pytest.mark.skipif(not os.path.exists(SRC), reason="reference SubsamplingLayerTest.java not present")
+
+
+def _arrays(after):
+    """Every Nd4j.create(new double[]{...}, new int[]{...}) literal after the first occurrence of ``after``."""
+    text = open(SRC).read()
+    text = text[text.index(after):]
+    out = []
+    for m in re.finditer(r"Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}\)", text):
+        vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
+        out.append(torch.tensor(vals, dtype=torch.float64).reshape([int(v) for v in m.group(2).split(",")]))
+    return out
+
+
+def _contained():
+    return _arrays("public INDArray getContainedData")[0]
+
+
+def _layer(pt):
+    conf = (D.NeuralNetConfiguration.Builder().seed(123).dataType(D.DataType.DOUBLE).list()
+            .layer(D.SubsamplingLayer.Builder(pt, [2, 2]).build())
+            .layer(D.CnnLossLayer.Builder(D.LossFunction.MSE).activation(D.Activation.IDENTITY).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    return net.getLayer(0)
+
+
+@pytest.mark.parametrize("pt,method", [(D.PoolingType.MAX, "testSubSampleMaxActivate"),
+                                       (D.PoolingType.AVG, "testSubSampleMeanActivate")])
+def test_pooling_forward_fixture(pt, method):
+    exp = _arrays("public void " + method)[0]
+    out = _layer(pt).activate(_contained(), False)
+    assert tuple(out.shape) == (1, 2, 2, 2)
+    assert torch.allclose(out, exp, atol=1e-12)
+
+
+@pytest.mark.parametrize("pt,method", [(D.PoolingType.MAX, "testSubSampleLayerMaxBackprop"),
+                                       (D.PoolingType.AVG, "testSubSampleLayerAvgBackprop")])
+def test_pooling_backward_fixture(pt, method):
+    eps_in, exp = _arrays("public void " + method)[:2]
+    layer = _layer(pt)
+    layer.activate(_contained(), True)
+    g, eps = layer.backpropGradient(eps_in)
+    assert tuple(eps.shape) == (1, 2, 4, 4)
+    assert torch.allclose(eps, exp, atol=1e-12)
+    assert g.getGradientFor("W") is None
+
+
+def test_kernel_larger_than_input_rejected():
+    """testSubTooLargeKernel: a 3x3 conv leaves height 18 of a 20x23 image; a pooling kernel of height 19 does not
+    fit (18 would)."""
+    def build(kh):
+        return (D.NeuralNetConfiguration.Builder().seed(123).list()
+                .layer(0, D.ConvolutionLayer.Builder(3, 3).stride(1, 1).nOut(2).activation(D.Activation.RELU)
+                       .weightInit(D.WeightInit.XAVIER).build())
+                .layer(1, D.SubsamplingLayer.Builder().poolingType(D.PoolingType.MAX).kernelSize(kh, 1).stride(1, 1)
+                       .build())
+                .layer(2, D.OutputLayer.Builder().nOut(2).weightInit(D.WeightInit.XAVIER)
+                       .activation(D.Activation.SOFTMAX).build())
+                .setInputType(D.InputType.convolutional(20, 23, 1)).build())
+    build(20 - 3 + 1)
+    with pytest.raises(Exception):
+        build(20 - 3 + 2)
