@@ -34,16 +34,19 @@ def _out(nin=None, nout=10):
 
 
 # ------------------------------------------------------------------------------------------------ configurations
-@pytest.mark.parametrize("case", ["dense_nin0", "dense_nout0", "output_nin0", "rnnout_nin0", "lstm_nin0",
+@pytest.mark.parametrize("case", ["dense_nin0", "dense_nout0", "output_nout0", "rnnout_nout0", "lstm_nin0",
                                   "lstm_nout0", "conv_nin0", "conv_nout0"])
 def test_zero_sizes(case):
+    # the reference's testOutputLayerNin0 / testRnnOutputLayerNin0 build getDensePlusOutput(10, 0) /
+    # getLSTMPlusRnnOutput(10, 0): an output layer with nOut 0 (an output layer's nIn of 0 is simply inferred from
+    # the layer below, TestInvalidConfigurations.java:22-111)
     layers = {
         "dense_nin0": [DenseLayer.Builder().nIn(0).nOut(10).build(), _out(10)],
         "dense_nout0": [DenseLayer.Builder().nIn(10).nOut(0).build(), _out(10)],
-        "output_nin0": [DenseLayer.Builder().nIn(10).nOut(10).build(),
-                        OutputLayer.Builder().nIn(0).nOut(10).build()],
-        "rnnout_nin0": [GravesLSTM.Builder().nIn(10).nOut(10).build(),
-                        RnnOutputLayer.Builder().nIn(0).nOut(10).build()],
+        "output_nout0": [DenseLayer.Builder().nIn(10).nOut(10).build(),
+                         OutputLayer.Builder().nIn(10).nOut(0).build()],
+        "rnnout_nout0": [GravesLSTM.Builder().nIn(10).nOut(10).build(),
+                         RnnOutputLayer.Builder().nIn(10).nOut(0).build()],
         "lstm_nin0": [GravesLSTM.Builder().nIn(0).nOut(10).build(), RnnOutputLayer.Builder().nIn(10).nOut(10).build()],
         "lstm_nout0": [GravesLSTM.Builder().nIn(10).nOut(0).build(), RnnOutputLayer.Builder().nIn(10).nOut(10).build()],
         "conv_nin0": [ConvolutionLayer.Builder().nIn(0).nOut(5).build(), _out(5 * 6 * 6)],
