@@ -1,0 +1,62 @@
+"""ConvolutionLayer against the reference's contained fixture, after ConvolutionLayerTest
+(deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/ConvolutionLayerTest.java:120-360): a 2x2
+stride-2 sigmoid convolution with all weights 0.5 and biases 1 over the fixed [1, 1, 8, 8] input gives the expected
+[1, 2, 4, 4] activations (arrays read from the reference test's source); the bias initialises from biasInit; a kernel
+larger than the input, a zero stride and a zero kernel size are rejected at build time. fp64, CPU."""
+import os
+import re
+
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+
+SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/"
+       "ConvolutionLayerTest.java")
+
+
+def _array(after):
+    text = open(SRC).read()
+    text = text[text.index(after):]
+    m = re.search(r"Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}\)", text)
+    vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
+    return torch.tensor(vals, dtype=torch.float64).reshape([int(v) for v in m.group(2).split(",")])
+
+
+def _conv_net(n_in, n_out, k, s, p, bias_init=None, act=D.Activation.SIGMOID):
+    b = D.ConvolutionLayer.Builder(k, s, p).nIn(n_in).nOut(n_out).activation(act)
+    if bias_init is not None:
+        b = b.biasInit(bias_init)
+    conf = (D.NeuralNetConfiguration.Builder().dataType(D.DataType.DOUBLE).list().layer(b.build())
+            .layer(D.CnnLossLayer.Builder(D.LossFunction.MSE).activation(D.Activation.IDENTITY).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    return net
+
+
+@pytest.mark.skipif(not os.path.exists(SRC), reason="reference ConvolutionLayerTest.java not present")
+def test_activate_results_contained():
+    net = _conv_net(1, 2, [2, 2], [2, 2], [0, 0])
+    layer = net.getLayer(0)
+    layer.setParam("W", torch.full((2, 1, 2, 2), 0.5, dtype=torch.float64))
+    layer.setParam("b", torch.ones(2, dtype=torch.float64))
+    x = _array("public INDArray getContainedData")
+    exp = _array("public void testActivateResultsContained")
+    out = layer.activate(x, False)
+    assert tuple(out.shape) == (1, 2, 4, 4)
+    assert torch.allclose(out, exp, atol=1e-8)
+
+
+def test_cnn_bias_init():
+    b = _conv_net(1, 3, [2, 2], [1, 1], [0, 0], bias_init=1.0).getLayer(0).getParam("b")
+    assert b.reshape(-1).numel() == 3 and torch.allclose(b, torch.ones_like(b))
+
+
+@pytest.mark.parametrize("case", ["too_large", "zero_stride", "zero_kernel"])
+def test_invalid_conv_configs(case):
+    k, s = {"too_large": ([10, 10], [1, 1]), "zero_stride": ([2, 2], [0, 0]), "zero_kernel": ([0, 0], [1, 1])}[case]
+    with pytest.raises(Exception):
+        (D.NeuralNetConfiguration.Builder().list()
+         .layer(0, D.ConvolutionLayer.Builder(k, s, [0, 0]).nIn(1).nOut(2).build())
+         .layer(1, D.OutputLayer.Builder().nOut(2).build())
+         .setInputType(D.InputType.convolutional(6, 6, 1)).build())
