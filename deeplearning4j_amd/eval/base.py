@@ -88,6 +88,8 @@ def to_2d(labels, preds, mask=None):
 
 
 def _enc(v):
+    if hasattr(v, "to_state") and hasattr(type(v), "from_state"):      # per-label ROC accumulators
+        return {"@roc": v.to_state()}
     if isinstance(v, np.ndarray):
         return {"@nd": v.tolist(), "dtype": str(v.dtype)}
     if torch.is_tensor(v):
@@ -105,6 +107,9 @@ def _enc(v):
 
 def _dec(v):
     if isinstance(v, dict):
+        if "@roc" in v:
+            from .roc import _BinaryROCState
+            return _BinaryROCState.from_state(v["@roc"])
         if "@nd" in v:
             return np.asarray(v["@nd"], dtype=v["dtype"])
         if "@map" in v:
@@ -156,6 +161,8 @@ class BaseEvaluation:
     def fromJson(cls, s):
         obj = json.loads(s)
         k = BaseEvaluation._REG[obj["@class"]]
+        if "fields" not in obj and k.fromJson.__func__ is not BaseEvaluation.fromJson.__func__:
+            return k.fromJson(s)                  # a class with its own JSON layout (ROC)
         inst = k.__new__(k)
         for f, v in obj["fields"].items():
             setattr(inst, f, _dec(v))
