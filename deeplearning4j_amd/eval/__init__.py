@@ -15,3 +15,4 @@ from .roc import ROC, ROCBinary, ROCMultiClass
 __all__ = ["BaseEvaluation", "EvaluationAveraging", "EvaluationUtils", "Evaluation", "EvaluationBinary",
            "EvaluationCalibration", "ConfusionMatrix", "RegressionEvaluation", "ROC", "ROCBinary", "ROCMultiClass",
            "RocCurve", "PrecisionRecallCurve", "Histogram", "ReliabilityDiagram", "Prediction"]
+from .tools import EvaluationTools  # noqa: F401

@@ -1,0 +1,84 @@
+"""EvaluationTools HTML reports, after the reference's EvaluationToolsTests
+(deeplearning4j-core/src/test/java/org/deeplearning4j/evaluation/EvaluationToolsTests.java:30-130): an Iris MLP's
+binary ROC (setosa+versicolor vs virginica) and three-class ROCMultiClass (with class names), for 20 threshold steps
+and exact mode, and an EvaluationCalibration over random softmax outputs each render to a self-contained HTML page
+(inline SVG, names HTML-escaped) that can be written to a file. CPU."""
+import os
+import random
+
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+from deeplearning4j_amd.eval import EvaluationTools
+
+IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+
+
+def _iris_net(n_out):
+    conf = (D.NeuralNetConfiguration.Builder().weightInit(D.WeightInit.XAVIER).seed(12345).list()
+            .layer(0, D.DenseLayer.Builder().nIn(4).nOut(4).activation(D.Activation.TANH).build())
+            .layer(1, D.OutputLayer.Builder().nIn(4).nOut(n_out).activation(D.Activation.SOFTMAX)
+                   .lossFunction(D.LossFunction.MCXENT).build()).build())
+    net = D.MultiLayerNetwork(conf)
+    net.init()
+    return net
+
+
+def _iris():
+    ds = D.IrisDataSetIterator(150, 150, path=IRIS).next()
+    f = ds.getFeatures()
+    f = (f - f.mean(0)) / f.std(0)
+    return f, ds.getLabels()
+
+
+@pytest.mark.skipif(not os.path.exists(IRIS), reason="reference iris.dat not present")
+@pytest.mark.parametrize("steps", [20, 0])
+def test_roc_html(steps, tmp_path):
+    f, lab = _iris()
+    lab2 = torch.stack([lab[:, 0] + lab[:, 1], lab[:, 2]], 1)
+    net = _iris_net(2)
+    for _ in range(30):
+        net.fit(D.DataSet(f, lab2))
+    roc = D.ROC(steps)
+    roc.eval(lab2, net.output(f))
+    page = EvaluationTools.rocChartToHtml(roc)
+    assert page.startswith("<!DOCTYPE html>") and page.count("<svg") == 2 and "<script" not in page
+    assert "AUC=" in page
+    out = tmp_path / "roc.html"
+    EvaluationTools.exportRocChartsToHtmlFile(roc, str(out))
+    assert out.read_text(encoding="utf-8") == page
+
+
+@pytest.mark.skipif(not os.path.exists(IRIS), reason="reference iris.dat not present")
+@pytest.mark.parametrize("steps", [20, 0])
+def test_roc_multi_html(steps):
+    f, lab = _iris()
+    net = _iris_net(3)
+    for _ in range(30):
+        net.fit(D.DataSet(f, lab))
+    roc = D.ROCMultiClass(steps)
+    roc.eval(lab, net.output(f))
+    page = EvaluationTools.rocChartToHtml(roc, ["setosa", "versicolor", "<virginica>"])
+    assert page.count("<svg") == 6
+    assert "setosa" in page and "&lt;virginica&gt;" in page and "<virginica>" not in page
+    with pytest.raises(ValueError):
+        EvaluationTools.rocChartToHtml(roc, ["only-one"])
+
+
+def test_evaluation_calibration_html(tmp_path):
+    g = torch.Generator().manual_seed(12345)
+    p = torch.rand(1000, 3, generator=g)
+    p = p / p.sum(1, keepdim=True)
+    lab = torch.zeros(1000, 3)
+    r = random.Random(12345)
+    for i in range(1000):
+        lab[i, r.randrange(3)] = 1
+    ec = D.EvaluationCalibration()
+    ec.eval(lab, p)
+    page = EvaluationTools.evaluationCalibrationToHtml(ec)
+    # reliability diagram + (1 + 3) residual histograms + (1 + 3) probability histograms
+    assert page.count("<svg") == 9 and "Reliability" in page
+    out = tmp_path / "cal.html"
+    EvaluationTools.exportevaluationCalibrationToHtmlFile(ec, str(out))
+    assert out.read_text(encoding="utf-8") == page
