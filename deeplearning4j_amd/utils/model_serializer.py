@@ -146,34 +146,65 @@ class ModelSerializer:
         return model.conf.toJson(), model.params().detach().cpu().clone()
 
 
-def guess_model_type(path):
-    """ModelGuesser (reference CORE:util/ModelGuesser.java:20): DL4J zip vs config JSON vs Keras h5."""
-    with open(path, "rb") as fh:
-        head = fh.read(8)
+def _guess_bytes(head):
     if head[:2] == b"PK":
         return "dl4j"
     if head[:8] == b"\x89HDF\r\n\x1a\n":
         return "keras"
-    if head[:1] in (b"{", b"["):
+    if head.lstrip()[:1] in (b"{", b"["):
         return "json"
     return "unknown"
 
 
+def guess_model_type(path):
+    """ModelGuesser (reference CORE:util/ModelGuesser.java:20): DL4J zip vs config JSON vs Keras h5."""
+    with open(path, "rb") as fh:
+        head = fh.read(8)
+    return _guess_bytes(head)
+
+
+def _source_bytes(src):
+    """(bytes, path-or-None) of a path or a readable binary stream."""
+    if isinstance(src, (str, os.PathLike)):
+        with open(src, "rb") as fh:
+            return fh.read(), str(src)
+    return src.read(), None
+
+
 class ModelGuesser:
-    @staticmethod
-    def loadModelGuess(path):
-        t = guess_model_type(path)
-        if t == "dl4j":
-            return ModelSerializer.restoreModel(path)
-        if t == "keras":
-            from ..modelimport.keras import KerasModelImport
-            return KerasModelImport.importKerasModelAndWeights(path)
-        raise ValueError(f"Unable to guess model type of {path}")
+    """Load a model, configuration or normalizer without knowing its format (reference util/ModelGuesser.java):
+    DL4J model zips, Keras HDF5 files and configuration JSON, from a path or an input stream."""
 
     @staticmethod
-    def loadConfigGuess(path):
-        with open(path) as fh:
-            return _config_from_json(fh.read())
+    def loadModelGuess(src):
+        data, path = _source_bytes(src)
+        t = _guess_bytes(data[:8])
+        if t == "dl4j":
+            return ModelSerializer.restoreModel(io.BytesIO(data))
+        if t == "keras":
+            from ..modelimport.keras import KerasModelImport
+            if path is None:
+                import tempfile
+                with tempfile.NamedTemporaryFile(suffix=".h5", delete=False) as tf:
+                    tf.write(data)
+                    path = tf.name
+                try:
+                    return KerasModelImport.importKerasModelAndWeights(path)
+                finally:
+                    os.unlink(path)
+            return KerasModelImport.importKerasModelAndWeights(path)
+        raise ValueError(f"Unable to guess model type of {path or 'the stream'}")
+
+    @staticmethod
+    def loadConfigGuess(src):
+        data, _ = _source_bytes(src)
+        return _config_from_json(data.decode("utf-8"))
+
+    @staticmethod
+    def loadNormalizer(src):
+        """The normalizer stored inside a DL4J model zip (None when it has none)."""
+        data, _ = _source_bytes(src)
+        return ModelSerializer.restoreNormalizerFromFile(io.BytesIO(data))
 
 
 _ = torch
