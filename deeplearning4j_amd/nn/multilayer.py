@@ -196,6 +196,27 @@ class MultiLayerNetwork(BaseNetwork):
     def activate(self, x, train=False):
         return self.output(x, train)
 
+    def computeZ(self, x, training=False):
+        """[input, z_0, z_1, ...]: every layer's pre-activation on the way forward (reference
+        MultiLayerNetwork.computeZ); layers without one (pooling, activation) contribute their output."""
+        x = x.toTensor() if hasattr(x, "toTensor") else x
+        x = self._to_dev(x, self._feat_dtype()) if x.is_floating_point() else self._to_dev(x)
+        mb = x.shape[0]
+        out = [x]
+        with torch.no_grad():
+            for i, layer in enumerate(self.layers):
+                x = self._pp(i, x, mb, training)
+                if hasattr(layer, "preOutput2d"):
+                    z = layer._out_from2d(layer.preOutput2d(layer._in2d(x)))
+                else:
+                    try:
+                        z = layer.preOutput(x, training)
+                    except NotImplementedError:
+                        z = None
+                x = layer.activate(x, training)
+                out.append(x if z is None else z)
+        return out
+
     def preOutput(self, x, train=False):
         """The output layer's pre-activation (z = x W + b) for input x, in the layout of its output (reference
         MultiLayerNetwork.preOutput)."""
@@ -259,6 +280,11 @@ class MultiLayerNetwork(BaseNetwork):
         self._mb = x.shape[0]
         self._prepare_conv_weights()
         out_l = self.layers[-1]
+        if not hasattr(out_l, "setLabels"):
+            from ..exceptions import DL4JException
+            raise DL4JException(f"Cannot calculate gradient and score: the last layer ({type(out_l.conf).__name__}) "
+                                f"is not an output layer; end the network in an OutputLayer / RnnOutputLayer / "
+                                f"LossLayer (reference MultiLayerNetwork.computeGradientAndScore)")
         # nobody reads the output activation of a training forward unless a listener asks for the activations
         out_l._skip_train_output = not any(hasattr(l, "onForwardPass") for l in self.listeners)
         try:

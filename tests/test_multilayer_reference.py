@@ -1,0 +1,101 @@
+"""MultiLayerNetwork behaviours, after the reference's MultiLayerTest
+(deeplearning4j-core/src/test/java/org/deeplearning4j/nn/multilayer/MultiLayerTest.java:462-1000): scoreExamples
+with and without the regularisation term equals per-example score() of the regularised / unregularised network (and
+regularisation raises it); bias L1 / L2 are configured per layer, contribute nothing while biases are zero and
+something after training; computeZ returns the input and every layer's pre-activation; computing a score without an
+output layer is an error. fp64, CPU."""
+import pytest
+import torch
+
+import deeplearning4j_amd as D
+from deeplearning4j_amd.exceptions import DL4JException
+
+
+def _mlp(reg):
+    b = D.NeuralNetConfiguration.Builder().seed(12345).updater(D.Sgd(0.1)).activation(D.Activation.TANH) \
+        .weightInit(D.WeightInit.XAVIER).dataType(D.DataType.DOUBLE)
+    if reg:
+        b = b.l1(0.01).l2(0.01)
+    net = D.MultiLayerNetwork(b.list().layer(0, D.DenseLayer.Builder().nIn(5).nOut(20).build())
+                              .layer(1, D.DenseLayer.Builder().nIn(20).nOut(30).build())
+                              .layer(2, D.OutputLayer.Builder().lossFunction(D.LossFunction.MSE).nIn(30).nOut(6)
+                                     .build()).build())
+    net.init()
+    return net
+
+
+def test_score_examples():
+    net, noreg = _mlp(True), _mlp(False)
+    noreg.setParameters(net.params().clone())
+    g = torch.Generator().manual_seed(12345)
+    x, y = torch.rand(3, 5, generator=g, dtype=torch.float64), torch.rand(3, 6, generator=g, dtype=torch.float64)
+    ds = D.DataSet(x, y)
+    with_reg = net.scoreExamples(ds, True).reshape(-1)
+    without = net.scoreExamples(ds, False).reshape(-1)
+    assert with_reg.numel() == 3 and without.numel() == 3
+    for i in range(3):
+        single = D.DataSet(x[i:i + 1], y[i:i + 1])
+        assert abs(float(net.score(single)) - float(with_reg[i])) < 1e-4
+        assert abs(float(noreg.score(single)) - float(without[i])) < 1e-4
+        assert float(with_reg[i]) > float(without[i])
+
+
+def _bias_net(bias_reg):
+    b = (D.NeuralNetConfiguration.Builder().weightInit(D.WeightInit.XAVIER).activation(D.Activation.TANH).seed(123)
+         .dataType(D.DataType.DOUBLE))
+    if bias_reg:
+        b = b.l1Bias(0.1).l2Bias(0.2)
+    net = D.MultiLayerNetwork(b.list().layer(0, D.DenseLayer.Builder().nIn(10).nOut(10).build())
+                              .layer(1, D.OutputLayer.Builder(D.LossFunction.MSE).activation(D.Activation.IDENTITY)
+                                     .nIn(10).nOut(10).build()).build())
+    net.init()
+    return net
+
+
+def test_bias_l1_l2():
+    n1, n2 = _bias_net(False), _bias_net(True)
+    assert n2.getLayer(0).conf.getL1Bias() == pytest.approx(0.1)
+    assert n2.getLayer(0).conf.getL2Bias() == pytest.approx(0.2)
+    g = torch.Generator().manual_seed(123)
+    x, y = torch.rand(10, 10, generator=g, dtype=torch.float64), torch.rand(10, 10, generator=g, dtype=torch.float64)
+    n2.setParams(n1.params().clone())
+    for n in (n1, n2):
+        n.setInput(x)
+        n.setLabels(y)
+        n.computeGradientAndScore()
+    for n in (n1, n2):
+        assert float(n.calcL1(True)) == 0.0 and float(n.calcL2(True)) == 0.0   # biases start at zero
+    assert abs(float(n1.score()) - float(n2.score())) < 1e-8
+    for _ in range(10):
+        n1.fit(x, y)
+    n2.setParams(n1.params().clone())
+    for n in (n1, n2):
+        n.computeGradientAndScore()
+    assert float(n1.calcL1(True)) == 0.0 and float(n1.calcL2(True)) == 0.0
+    assert float(n2.calcL1(True)) > 0.0 and float(n2.calcL2(True)) > 0.0
+    assert float(n2.score()) > float(n1.score())
+
+
+def test_compute_z():
+    net = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().weightInit(D.WeightInit.XAVIER)
+                              .activation(D.Activation.TANH).dataType(D.DataType.DOUBLE).list()
+                              .layer(0, D.DenseLayer.Builder().nIn(10).nOut(10).build())
+                              .layer(1, D.DenseLayer.Builder().nIn(10).nOut(10).build()).build())
+    net.init()
+    x = torch.rand(10, 10, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    zs = net.computeZ(x, False)
+    assert len(zs) == 3 and torch.equal(zs[0], x)
+    W0, b0 = net.getParam("0_W"), net.getParam("0_b").reshape(1, -1)
+    W1, b1 = net.getParam("1_W"), net.getParam("1_b").reshape(1, -1)
+    assert torch.allclose(zs[1], x @ W0 + b0, atol=1e-12)
+    assert torch.allclose(zs[2], torch.tanh(x @ W0 + b0) @ W1 + b1, atol=1e-12)
+
+
+def test_error_no_output_layer():
+    net = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().list()
+                              .layer(0, D.DenseLayer.Builder().nIn(10).nOut(10).build()).build())
+    net.init()
+    net.setInput(torch.zeros(1, 10))
+    net.setLabels(torch.zeros(1, 10))
+    with pytest.raises(DL4JException):
+        net.computeGradientAndScore()
