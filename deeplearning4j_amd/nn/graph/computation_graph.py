@@ -737,6 +737,12 @@ class ComputationGraph(BaseNetwork):
     def getInput(self, i):
         return self.inputs[i]
 
+    def layerSize(self, name):
+        """nOut of layer ``name`` (0 for layers without one) (reference ComputationGraph.layerSize)."""
+        if name not in self.layers_by_name:
+            raise ValueError(f"No layer named {name!r}")
+        return int(getattr(self.layers_by_name[name].conf, "nOut", 0) or 0)
+
     def getNumInputArrays(self):
         return len(self.conf.networkInputs)
 

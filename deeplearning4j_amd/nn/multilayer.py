@@ -196,6 +196,12 @@ class MultiLayerNetwork(BaseNetwork):
     def activate(self, x, train=False):
         return self.output(x, train)
 
+    def layerSize(self, layer):
+        """nOut of layer ``layer`` (0 for layers without one, e.g. pooling) (reference MultiLayerNetwork.layerSize)."""
+        if not 0 <= layer < len(self.layers):
+            raise ValueError(f"Invalid layer index {layer}: the network has {len(self.layers)} layers")
+        return int(getattr(self.layers[layer].conf, "nOut", 0) or 0)
+
     def computeZ(self, x, training=False):
         """[input, z_0, z_1, ...]: every layer's pre-activation on the way forward (reference
         MultiLayerNetwork.computeZ); layers without one (pooling, activation) contribute their output."""

@@ -99,3 +99,34 @@ def test_error_no_output_layer():
     net.setLabels(torch.zeros(1, 10))
     with pytest.raises(DL4JException):
         net.computeGradientAndScore()
+
+
+def test_layer_size():
+    net = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().list()
+                              .layer(D.ConvolutionLayer.Builder().kernelSize(2, 2).nOut(6).build())
+                              .layer(D.SubsamplingLayer.Builder().kernelSize(2, 2).build())
+                              .layer(D.DenseLayer.Builder().nOut(30).build())
+                              .layer(D.OutputLayer.Builder().nOut(13).build())
+                              .setInputType(D.InputType.convolutional(28, 28, 3)).build())
+    net.init()
+    assert [net.layerSize(i) for i in range(4)] == [6, 0, 30, 13]
+
+
+def test_zero_param_net_fits_and_serialises():
+    import io
+    from deeplearning4j_amd.utils.model_serializer import ModelSerializer
+    net = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().list()
+                              .layer(D.SubsamplingLayer.Builder().kernelSize(2, 2).stride(2, 2).build())
+                              .layer(D.LossLayer.Builder().activation(D.Activation.SIGMOID)
+                                     .lossFunction(D.LossFunction.MSE).build())
+                              .setInputType(D.InputType.convolutionalFlat(28, 28, 1)).build())
+    net.init()
+    assert net.numParams() == 0
+    x = torch.rand(16, 784, generator=torch.Generator().manual_seed(12345))
+    out = net.output(x)
+    net.fit(D.DataSet(x, torch.zeros(out.shape)))
+    buf = io.BytesIO()
+    ModelSerializer.writeModel(net, buf, True)
+    buf.seek(0)
+    net2 = ModelSerializer.restoreMultiLayerNetwork(buf, True)
+    assert torch.equal(net2.output(x), out)
