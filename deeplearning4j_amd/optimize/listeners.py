@@ -209,6 +209,37 @@ class ParamAndGradientIterationListener(TrainingListener):
         self.rows = []
         self._wrote_header = False
 
+    class _Builder:
+        def __init__(self):
+            self._kw = {}
+
+        def __getattr__(self, name):
+            if name.startswith("_"):
+                raise AttributeError(name)
+
+            def setter(v=True):
+                self._kw[name] = v
+                return self
+            return setter
+
+        def build(self):
+            return ParamAndGradientIterationListener(**self._kw)
+
+    @classmethod
+    def builder(cls):
+        """Fluent builder with the reference's property names (ParamAndGradientIterationListener.builder())."""
+        return cls._Builder()
+
+    def _stat_names(self):
+        names = []
+        if self.printMean:
+            names.append("mean")
+        if self.printMinMax:
+            names += ["min", "max"]
+        if self.printMeanAbsValue:
+            names.append("meanAbsValue")
+        return names
+
     def _stats(self, t):
         import torch
         t = t.detach().float().reshape(-1)
@@ -230,12 +261,15 @@ class ParamAndGradientIterationListener(TrainingListener):
         grads = model.gradient().gradientForVariable() if hasattr(model, "gradient") else {}
         row = [iteration, model.score()]
         header = ["n", "score"]
+        stat_names = self._stat_names()
         for k, p in params.items():
-            header.append(f"param_{k}")
+            if p.numel() == 0:
+                continue
+            header += [f"param_{k}_{n}" for n in stat_names]
             row += self._stats(p)
             g = grads.get(k)
-            if g is not None:
-                header.append(f"grad_{k}")
+            if g is not None and g.numel() > 0:
+                header += [f"grad_{k}_{n}" for n in stat_names]
                 row += self._stats(g)
         self.rows.append(row)
         line = self.delimiter.join(str(x) for x in row)

@@ -1,0 +1,41 @@
+"""ParamAndGradientIterationListener, after the reference's TestParamAndGradientIterationListener
+(deeplearning4j-core/src/test/java/org/deeplearning4j/optimize/listener/TestParamAndGradientIterationListener.java):
+built through builder() with the reference's options, it writes a tab-delimited header plus one row every
+``iterations`` iterations for an Iris MLP trained for two epochs, with one column per parameter / gradient statistic.
+CPU."""
+import os
+
+import pytest
+
+import deeplearning4j_amd as D
+from deeplearning4j_amd.optimize.listeners import ParamAndGradientIterationListener
+
+IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+
+
+@pytest.mark.skipif(not os.path.exists(IRIS), reason="reference iris.dat not present")
+def test_param_and_gradient_listener_file(tmp_path):
+    it = D.IrisDataSetIterator(30, 150, path=IRIS)
+    net = D.MultiLayerNetwork(D.NeuralNetConfiguration.Builder().updater(D.Sgd(1e-5)).list()
+                              .layer(0, D.DenseLayer.Builder().nIn(4).nOut(20).build())
+                              .layer(1, D.DenseLayer.Builder().nIn(20).nOut(30).build())
+                              .layer(2, D.OutputLayer.Builder(D.LossFunction.MCXENT).activation(D.Activation.SOFTMAX)
+                                     .nIn(30).nOut(3).build()).build())
+    net.init()
+    path = tmp_path / "paramAndGradTest.txt"
+    listener = (ParamAndGradientIterationListener.builder().outputToFile(True).file(str(path)).outputToConsole(False)
+                .outputToLogger(False).iterations(2).printHeader(True).printMean(False).printMinMax(False)
+                .printMeanAbsValue(True).delimiter("\t").build())
+    net.setListeners(listener)
+    for _ in range(2):
+        it.reset()
+        net.fit(it)
+    lines = path.read_text().strip().split("\n")
+    header = lines[0].split("\t")
+    assert header[:2] == ["n", "score"]
+    # 3 layers x (W, b) x (param, grad) x one statistic (meanAbsValue)
+    assert len(header) == 2 + 3 * 2 * 2
+    assert all(h.endswith("_meanAbsValue") for h in header[2:])
+    rows = [l.split("\t") for l in lines[1:]]
+    assert len(rows) == 5                       # iterations 0, 2, 4, 6, 8 of 10
+    assert all(len(r) == len(header) for r in rows)
