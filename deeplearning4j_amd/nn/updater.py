@@ -128,7 +128,19 @@ class NetworkUpdater:
 
     def update(self, params, grad, iteration, epoch, batch_size, shadow=None, reg_out=None):
         """Apply the whole update (preApply -> updater -> l1/l2 -> /batch -> params -= u) in place; the gradient
-        normalization runs inside fused_update (kernel pass on the GPU, ``pre_apply`` on the host path)."""
+        normalization runs inside fused_update (kernel pass on the GPU, ``pre_apply`` on the host path).
+
+        Called as ``update(model, gradient, iteration, epoch, batchSize)`` (the reference's Updater.update), the
+        Gradient is turned into the update in place instead -- the parameters stay as they are and the updater state
+        advances -- so a gradient computed by one network can be applied to another (params -= gradient)."""
+        if hasattr(grad, "gradient") and callable(getattr(params, "params", None)):
+            flat_g = grad.gradient().reshape(-1)
+            p = params.params().reshape(-1).detach().clone()
+            before = p.clone()
+            fused_update(self.plan, p, flat_g.detach().clone(), self.state, iteration, epoch, batch_size,
+                         self.net.conf.globalConf.get("miniBatch", True), None)
+            flat_g.copy_((before - p).to(flat_g.dtype))
+            return
         fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
                      self.net.conf.globalConf.get("miniBatch", True), shadow, reg_out=reg_out)
 
