@@ -420,32 +420,53 @@ class INDArrayDataSetIterator(DoublesDataSetIterator):
 
 
 class DataSetIteratorSplitter:
-    """Splits one iterator into train / test sub-iterators by batch count (DataSetIteratorSplitter.java):
-    the first ``ratio * totalBatches`` batches feed getTrainIterator(), the rest getTestIterator()."""
+    """Splits one iterator into train / test views by batch count (DataSetIteratorSplitter.java): the first
+    ``ratio * totalBatches`` batches of each pass feed getTrainIterator(), the following ones getTestIterator().
+    Streaming: nothing is cached, the views share the underlying iterator's position. A test pass that starts before
+    the train part of the current pass was consumed skips it; resetting either view restarts the underlying pass."""
 
     def __init__(self, base, totalBatches, ratio):
         if not 0.0 < ratio < 1.0:
             raise ValueError("ratio must be in (0, 1)")
         self.base, self.total = base, int(totalBatches)
         self.ntrain = int(self.total * ratio)
-        self._cache = None
+        self.pos = 0                          # batches of the current underlying pass handed out (or skipped)
 
-    def _batches(self):
-        if self._cache is None:
-            self.base.reset()
-            out = []
-            while self.base.hasNext() and len(out) < self.total:
-                out.append(self.base.next())
-            self._cache = out
-        return self._cache
+    def _restart(self):
+        self.base.reset()
+        self.pos = 0
 
     def getTrainIterator(self):
-        from .dataset import ListDataSetIterator
-        return ListDataSetIterator(self._batches()[:self.ntrain])
+        return _SplitView(self, 0, self.ntrain)
 
     def getTestIterator(self):
-        from .dataset import ListDataSetIterator
-        return ListDataSetIterator(self._batches()[self.ntrain:])
+        return _SplitView(self, self.ntrain, self.total)
+
+
+class _SplitView(DataSetIterator):
+    def __init__(self, sp, lo, hi):
+        self.sp, self.lo, self.hi = sp, lo, hi
+
+    def hasNext(self):
+        sp = self.sp
+        if sp.pos > self.hi or (self.lo == 0 and sp.pos >= self.hi):
+            return False
+        while sp.pos < self.lo and sp.base.hasNext():      # test view: skip the train part of this pass
+            sp.base.next()
+            sp.pos += 1
+        return sp.pos < self.hi and sp.base.hasNext()
+
+    def next(self, num=None):
+        if not self.hasNext():
+            raise StopIteration("DataSetIteratorSplitter: this part of the pass is exhausted (reset first)")
+        self.sp.pos += 1
+        return self._pp(self.sp.base.next())
+
+    def reset(self):
+        self.sp._restart()
+
+    def batch(self):
+        return self.sp.base.batch()
 
 
 MultiDataSetIteratorSplitter = DataSetIteratorSplitter
