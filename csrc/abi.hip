@@ -45,7 +45,10 @@ DL4J_API int dl4j_matmul(const dl4j_tensor_t* A, const dl4j_tensor_t* B, dl4j_te
   if (B->shape[r] != K || C->shape[r] != M || C->shape[c] != N) return DL4J_ERR_SHAPE;
   const long long batch = nd == 3 ? A->shape[0] : 1;
   if (nd == 3 && (B->shape[0] != batch || C->shape[0] != batch)) return DL4J_ERR_SHAPE;
-  if (A->dtype != B->dtype) return DL4J_ERR_DTYPE;
+  // every kernel behind this entry point reads / writes F32, BF16 or F16 only (an I32 or unknown code would be
+  // reinterpreted as fp16 by the fp32 kernel's loader, and any non-F32 C code gets 16-bit stores)
+  auto float_code = [](int dt) { return dt == DL4J_F32 || dt == DL4J_BF16 || dt == DL4J_F16; };
+  if (A->dtype != B->dtype || !float_code(A->dtype) || !float_code(C->dtype)) return DL4J_ERR_DTYPE;
   if (C->strides[c] != 1) return DL4J_ERR_LAYOUT;                     // row-major destination rows
   const long long sA = nd == 3 ? A->strides[0] : 0, sB = nd == 3 ? B->strides[0] : 0, sC = nd == 3 ? C->strides[0] : 0;
   if (M > 0x7fffffffLL || N > 0x7fffffffLL || K > 0x7fffffffLL || batch > 65535) return DL4J_ERR_SHAPE;

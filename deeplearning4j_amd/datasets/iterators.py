@@ -423,14 +423,34 @@ class DataSetIteratorSplitter:
     """Splits one iterator into train / test views by batch count (DataSetIteratorSplitter.java): the first
     ``ratio * totalBatches`` batches of each pass feed getTrainIterator(), the following ones getTestIterator().
     Streaming: nothing is cached, the views share the underlying iterator's position. A test pass that starts before
-    the train part of the current pass was consumed skips it; resetting either view restarts the underlying pass."""
+    the train part of the current pass was consumed skips it; resetting either view restarts the underlying pass.
+
+    Cost: the test view of a fresh pass replays (reads and discards) the ``ntrain`` train batches of that pass first,
+    so a test-only evaluation after ``reset()`` costs a full pass of the underlying iterator.
+    As in the reference (DataSetIteratorSplitter.java:158-166), the first train batch of the first pass is kept and
+    compared with the first train batch of every later pass: a shuffling underlying iterator would silently move
+    examples between the train and test parts, so that raises instead. ``next(num)`` is unsupported (the reference
+    throws UnsupportedOperationException)."""
 
     def __init__(self, base, totalBatches, ratio):
         if not 0.0 < ratio < 1.0:
             raise ValueError("ratio must be in (0, 1)")
+        if int(totalBatches) <= 0:
+            raise ValueError("totalBatches should be a positive value")
         self.base, self.total = base, int(totalBatches)
         self.ntrain = int(self.total * ratio)
         self.pos = 0                          # batches of the current underlying pass handed out (or skipped)
+        self.first_train = None               # features of the first train batch of the first pass
+
+    def _check_first(self, ds):
+        f = ds.getFeatures() if hasattr(ds, "getFeatures") else getattr(ds, "features", None)
+        if f is None:
+            return
+        f = f.detach().to("cpu", torch.float32)
+        if self.first_train is None:
+            self.first_train = f.clone()
+        elif f.shape != self.first_train.shape or not torch.allclose(f, self.first_train, atol=1e-5, rtol=0):
+            raise RuntimeError("DataSetIteratorSplitter: first examples do not match. Randomization was used?")
 
     def _restart(self):
         self.base.reset()
@@ -457,10 +477,16 @@ class _SplitView(DataSetIterator):
         return sp.pos < self.hi and sp.base.hasNext()
 
     def next(self, num=None):
+        if num is not None:
+            raise NotImplementedError("DataSetIteratorSplitter views do not support next(num)")
         if not self.hasNext():
             raise StopIteration("DataSetIteratorSplitter: this part of the pass is exhausted (reset first)")
+        first = self.sp.pos == 0
         self.sp.pos += 1
-        return self._pp(self.sp.base.next())
+        ds = self.sp.base.next()
+        if first:
+            self.sp._check_first(ds)
+        return self._pp(ds)
 
     def reset(self):
         self.sp._restart()

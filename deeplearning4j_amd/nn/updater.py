@@ -134,15 +134,46 @@ class NetworkUpdater:
         Gradient is turned into the update in place instead -- the parameters stay as they are and the updater state
         advances -- so a gradient computed by one network can be applied to another (params -= gradient)."""
         if hasattr(grad, "gradient") and callable(getattr(params, "params", None)):
-            flat_g = grad.gradient().reshape(-1)
-            p = params.params().reshape(-1).detach().clone()
+            flat_g = grad.gradient()
+            gmap = keys = None
+            pflat = params.params().reshape(-1)
+            if flat_g is None:
+                # same element layout as the flat parameter vector: each variable lands where its parameter view
+                # sits in it (f-order weight views included)
+                gmap, keys = self._map_keys(params, grad)
+                table = params.paramTable()
+                flat_g = torch.zeros_like(pflat)
+                base = pflat.storage_offset()
+                views = {k: flat_g.as_strided(table[k].shape, table[k].stride(), table[k].storage_offset() - base)
+                         for k in keys}
+                for k in keys:
+                    views[k].copy_(gmap[k].reshape(table[k].shape))
+            flat_g = flat_g.reshape(-1)
+            p = pflat.detach().clone()
             before = p.clone()
-            fused_update(self.plan, p, flat_g.detach().clone(), self.state, iteration, epoch, batch_size,
-                         self.net.conf.globalConf.get("miniBatch", True), None)
-            flat_g.copy_((before - p).to(flat_g.dtype))
+            fused_update(self.plan, p, flat_g.detach().clone().to(p.dtype), self.state, iteration, epoch,
+                         batch_size, self.net.conf.globalConf.get("miniBatch", True), None)
+            upd = before - p
+            if gmap is None:
+                flat_g.copy_(upd.to(flat_g.dtype))
+            else:
+                flat_g.copy_(upd.to(flat_g.dtype))
+                for k in keys:
+                    gmap[k].copy_(views[k].reshape(gmap[k].shape))
             return
         fused_update(self.plan, params, grad, self.state, iteration, epoch, batch_size,
                      self.net.conf.globalConf.get("miniBatch", True), shadow, reg_out=reg_out)
+
+    @staticmethod
+    def _map_keys(model, grad):
+        """Parameter keys of a Gradient built only with setGradientFor (no flattened view), in the model's flat
+        parameter order (paramTable), or a ValueError naming what is missing."""
+        gmap = grad.gradientForVariable() if hasattr(grad, "gradientForVariable") else {}
+        keys = list(model.paramTable().keys())
+        missing = [k for k in keys if k not in gmap]
+        if missing:
+            raise ValueError(f"Gradient has no flattened view and no entry for parameter(s) {missing[:4]}")
+        return gmap, keys
 
     def update_range(self, params, grad, iteration, epoch, batch_size, lo, hi):
         """Update only the parameters in the flat range [lo, hi) (layer-wise pretraining): the fused update

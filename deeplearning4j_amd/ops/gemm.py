@@ -342,10 +342,12 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
                 raise ValueError("GEMM BatchNorm statistics need a row-major, unbatched destination")
             kst = key + ("stats", stats_tag)
             cfg = (_FORCE_CFG[0], 1) if _FORCE_CFG is not None else _TUNED.get(kst)
+            from_db = False
             if cfg is None:
                 cfg = tunedb.lookup("gemm", kst)
                 if cfg is not None:
                     _TUNED[kst] = cfg
+                    from_db = True
                 else:
                     cfg = (4, 1) if K % 64 == 0 else (2, 1)
                     if _TUNE and not torch.cuda.is_current_stream_capturing():
@@ -354,6 +356,12 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
                         _TUNED[kst] = cfg
                         tunedb.record("gemm", kst, cfg)
             rc = launch(cfg[0], 1, c_t, float(beta), z, stats)
+            if rc != 0 and from_db:
+                # a recorded choice this build refuses: drop it and take the planner's default configuration
+                tunedb.forget("gemm", kst)
+                cfg = (4, 1) if K % 64 == 0 else (2, 1)
+                _TUNED[kst] = cfg
+                rc = launch(cfg[0], 1, c_t, float(beta), z, stats)
             if rc != 0:
                 raise RuntimeError(f"HIP gemm (stats) failed with code {rc}")
             if c_t is not out:
@@ -367,6 +375,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
 
             def launch(cfg, sp, dst, bt, zz, ts=None):
                 return libmm(dst, bt) if cfg == LIB_CFG[0] else kern(cfg, sp, dst, bt, zz, ts)
+        from_db = False
         if _FORCE_CFG is not None:
             cfg = _FORCE_CFG
         else:
@@ -375,6 +384,7 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
                 cfg = tunedb.lookup("gemm", key)
                 if cfg is not None:
                     _TUNED[key] = cfg
+                    from_db = True
                 else:
                     cfg = _plan(lib, Mx, Nx, K, batch)
                     if _TUNE and not torch.cuda.is_current_stream_capturing():
@@ -384,6 +394,12 @@ def mmul(a, b, out=None, bias=None, bias_dim=1, act=None, alpha=1.0, beta=0.0, o
         if cfg == LIB_CFG:
             fallback.record("gemm", "library GEMM (hipBLASLt) picked by the autotuner (DL4J_AMD_GEMM_LIB=1)")
         rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
+        if rc != 0 and from_db:
+            # a recorded choice this build / device refuses: drop it, re-plan (the autotuner re-times next call)
+            tunedb.forget("gemm", key)
+            _TUNED.pop(key, None)
+            cfg = _plan(lib, Mx, Nx, K, batch)
+            rc = launch(cfg[0], cfg[1], c_t, float(beta), z)
     if rc == -1:
         # exact-fp32 MFMA kernel: any dtype / strides
         if swap:

@@ -10,6 +10,10 @@ key) for one GPU architecture.
 * Record: with ``DL4J_AMD_TUNE_RECORD=<file>`` every decision the autotuners make is added to that file at exit
   (merged with what it already holds); ``DL4J_AMD_TUNE_REPS`` raises the timing repetitions for such a run.
 * Entries carry the schema version below; a file with another version is ignored (tile configuration ids changed).
+* The file also records the compute-unit count of the device it was timed on; on a device of the same architecture
+  with another CU count (a partitioned or binned part) the decisions are ignored and the autotuners re-time.
+* A recorded choice a kernel refuses at launch (non-zero return code) is dropped with ``forget`` and the caller
+  falls back to its planner / autotuner instead of failing.
 """
 import atexit
 import json
@@ -34,6 +38,15 @@ def _arch():
         return None
 
 
+def _cus():
+    try:
+        if not torch.cuda.is_available():
+            return None
+        return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    except Exception:       # noqa: BLE001
+        return None
+
+
 def default_path(arch=None):
     arch = arch or _arch()
     return None if arch is None else os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunedb",
@@ -55,7 +68,8 @@ def _load():
                 try:
                     with open(p) as fh:
                         data = json.load(fh)
-                    if data.get("version") == VERSION:
+                    cus, want = data.get("cus"), _cus()
+                    if data.get("version") == VERSION and (cus is None or want is None or cus == want):
                         db = data.get("tables", {})
                         _path_used = p
                 except (OSError, ValueError):
@@ -78,6 +92,13 @@ def lookup(table, key):
     return None if v is None else _native(v)
 
 
+def forget(table, key):
+    """Drop a loaded decision (a kernel refused it at launch), so the next call re-plans or re-times."""
+    with _lock:
+        _load().get(table, {}).pop(repr(key), None)
+        _recorded.get(table, {}).pop(repr(key), None)
+
+
 def record(table, key, value):
     """Remember an autotuner decision (kept in memory; written at exit when DL4J_AMD_TUNE_RECORD is set)."""
     with _lock:
@@ -93,7 +114,7 @@ def reps(default):
 
 def save(path, arch=None):
     """Merge the decisions of this process into ``path`` (same-version entries already there are kept)."""
-    data = {"version": VERSION, "arch": arch or _arch(), "tables": {}}
+    data = {"version": VERSION, "arch": arch or _arch(), "cus": _cus(), "tables": {}}
     if os.path.exists(path):
         try:
             with open(path) as fh:

@@ -133,6 +133,26 @@ static void test_matmul_f32(void) {
   free(a); free(b); free(c); free(c0);
 }
 
+/* dtype validation: int32 operands or an int32 / unknown destination code are refused, nothing is launched */
+static void test_matmul_dtype_rejects(void) {
+  int32_t dummy[4] = {0, 0, 0, 0};
+  dl4j_tensor_t A, B, C;
+  set2(&A, dummy, DL4J_I32, 2, 2, 2, 1);
+  set2(&B, dummy, DL4J_I32, 2, 2, 2, 1);
+  set2(&C, dummy, DL4J_F32, 2, 2, 2, 1);
+  int rc = dl4j_matmul(&A, &B, &C, 1.0f, 0.0f, 0);
+  CHECK(rc == DL4J_ERR_DTYPE, "dl4j_matmul I32 operands rc=%d", rc);
+  set2(&A, dummy, DL4J_F32, 2, 2, 2, 1);
+  set2(&B, dummy, DL4J_F32, 2, 2, 2, 1);
+  set2(&C, dummy, DL4J_I32, 2, 2, 2, 1);
+  rc = dl4j_matmul(&A, &B, &C, 1.0f, 0.0f, 0);
+  CHECK(rc == DL4J_ERR_DTYPE, "dl4j_matmul I32 destination rc=%d", rc);
+  C.dtype = 77;
+  rc = dl4j_matmul(&A, &B, &C, 1.0f, 0.0f, 0);
+  CHECK(rc == DL4J_ERR_DTYPE, "dl4j_matmul unknown destination code rc=%d", rc);
+  printf("matmul dtype rejects: ok\n");
+}
+
 /* 3x3 convolution, NHWC activations, KRSC weights, bf16 in / bf16 out, + bias */
 static void test_conv(void) {
   const int N = 2, H = 8, W = 8, C = 64, K = 64, R = 3, S = 3, OH = 8, OW = 8;
@@ -265,6 +285,7 @@ int main(void) {
   } else {
     test_matmul_bf16();
     test_matmul_f32();
+    test_matmul_dtype_rejects();
     test_conv();
     test_update_adam();
     test_comm();

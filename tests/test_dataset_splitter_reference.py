@@ -66,3 +66,25 @@ def test_test_view_every_second_epoch():
                 total += 1
         train.reset()
     assert total == 700 * 4 + 300 * 2
+
+
+def test_shuffled_base_raises_and_next_num_refused():
+    """Reference DataSetIteratorSplitter.java:158-166: the first train batch of later passes must equal the first
+    pass's, or the split moved examples between train and test; next(num) is unsupported."""
+    import pytest
+
+    class Shuffling(_Numbered):
+        def next(self, num=None):
+            d = D.DataSet(torch.full((4, 3), float((self.i + self.resets) % self.n)), torch.zeros(4, 2))
+            self.i += 1
+            return d
+
+    sp = D.DataSetIteratorSplitter(Shuffling(10), 10, 0.7)
+    tr = sp.getTrainIterator()
+    with pytest.raises(NotImplementedError):
+        tr.next(4)
+    while tr.hasNext():
+        tr.next()
+    tr.reset()
+    with pytest.raises(RuntimeError, match="Randomization"):
+        tr.next()

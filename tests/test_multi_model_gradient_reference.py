@@ -55,3 +55,31 @@ def test_gradient_apply_multilayer(upd, reg):
         n1.fit(f, lab)
         n2.fit(f, lab)
         assert torch.allclose(n1.params(), n2.params(), atol=1e-10)
+
+
+def test_gradient_apply_from_variable_map_only():
+    """A Gradient built only with setGradientFor (no flattened view): the update is computed over the variables in the
+    model's parameter order and written back into each per-variable array (the flattened path gives the same)."""
+    n1, n2 = D.MultiLayerNetwork(_conf(D.Sgd(0.1), True)), D.MultiLayerNetwork(_conf(D.Sgd(0.1), True))
+    n1.init()
+    n2.init()
+    mb = 5
+    f = torch.rand(mb, 10, generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    lab = torch.eye(10, dtype=torch.float64)[:mb]
+    n1.setInput(f)
+    n1.setLabels(lab)
+    n1.computeGradientAndScore()
+    flat = n1.gradient()
+    from deeplearning4j_amd.nn.gradient import Gradient
+    gm = Gradient()
+    for k, v in flat.gradientForVariable().items():
+        gm.setGradientFor(k, v.detach().clone())
+    n2.getUpdater().update(n2, flat, 0, 0, mb)
+    n1b = D.MultiLayerNetwork(_conf(D.Sgd(0.1), True))
+    n1b.init()
+    n1b.getUpdater().update(n1b, gm, 0, 0, mb)
+    for k, v in flat.gradientForVariable().items():
+        assert torch.allclose(gm.getGradientFor(k), v, atol=1e-12), k
+    empty = Gradient()
+    with pytest.raises(ValueError, match="no flattened view"):
+        n1b.getUpdater().update(n1b, empty, 0, 0, mb)

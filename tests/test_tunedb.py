@@ -67,3 +67,21 @@ def test_off_switch_and_reps(tmp_path, fresh):
     assert tunedb.reps(3) == 9
     fresh.setenv("DL4J_AMD_TUNE_REPS", "1")
     assert tunedb.reps(3) == 3
+
+
+def test_cu_count_mismatch_ignores_file_and_forget(tmp_path, fresh):
+    """A file timed on a device with another compute-unit count is ignored; a refused entry is dropped by forget()."""
+    p = tmp_path / "gfx950.json"
+    p.write_text(json.dumps({"version": tunedb.VERSION, "arch": "gfx950", "cus": 256,
+                             "tables": {"gemm": {repr((1, 2, 3)): [3, 2]}}}))
+    fresh.setenv("DL4J_AMD_TUNE_DB", str(p))
+    fresh.setattr(tunedb, "_cus", lambda: 304)
+    assert tunedb.lookup("gemm", (1, 2, 3)) is None
+    fresh.setattr(tunedb, "_db", None)
+    fresh.setattr(tunedb, "_cus", lambda: 256)
+    assert tunedb.lookup("gemm", (1, 2, 3)) == (3, 2)
+    tunedb.forget("gemm", (1, 2, 3))
+    assert tunedb.lookup("gemm", (1, 2, 3)) is None
+    fresh.setattr(tunedb, "_db", None)
+    fresh.setattr(tunedb, "_cus", lambda: None)       # no device (CPU): the file is used as is
+    assert tunedb.lookup("gemm", (1, 2, 3)) == (3, 2)
