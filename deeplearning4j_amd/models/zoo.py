@@ -42,19 +42,145 @@ class ZooModel:
     def setInputShape(self, shape):
         self.inputShape = shape[0] if isinstance(shape[0], (list, tuple)) else shape
 
-    def pretrainedAvailable(self, t=None):
-        return False
+    # pretrained weight files of the reference zoo: {PretrainedType: (url, Adler-32)} per model class name
+    # (ZOO:model/*.java pretrainedUrl / pretrainedChecksum); checked against any local copy before restoring
+    def pretrainedUrl(self, pretrainedType=None):
+        e = _PRETRAINED.get(self._pretrained_key(), {}).get(pretrainedType or PretrainedType.IMAGENET)
+        return None if e is None else e[0]
 
-    def initPretrained(self, path=None):
+    def pretrainedChecksum(self, pretrainedType=None):
+        e = _PRETRAINED.get(self._pretrained_key(), {}).get(pretrainedType or PretrainedType.IMAGENET)
+        return 0 if e is None else e[1]
+
+    def _pretrained_key(self):
+        return type(self).__name__
+
+    def pretrainedAvailable(self, pretrainedType=None):
+        return self.pretrainedUrl(pretrainedType) is not None
+
+    def zooType(self):
+        return ZooType.of_model(type(self).__name__)
+
+    def modelType(self):
+        return ComputationGraph if hasattr(self, "graphBuilder") else MultiLayerNetwork
+
+    def metaDataFull(self):
+        return ModelMetaData([list(self.inputShape)], 1, self.zooType())
+
+    def initPretrained(self, pretrainedType=None, path=None, verify=True):
+        """Restore pretrained weights (ZOO:ZooModel.java:51-93). No download is possible here: the weight file is
+        ``path`` (a ModelSerializer zip) or the file the reference would have cached under
+        ``~/.deeplearning4j/models/<name of the url>``. When the model has a known Adler-32 checksum for
+        ``pretrainedType`` the file is verified first and a mismatch raises (a mismatching cached file is deleted,
+        as the reference does; a file passed by path is left alone). ``initPretrained("<path>")`` also works."""
+        import os
+        if isinstance(pretrainedType, str) and not hasattr(PretrainedType, pretrainedType):
+            pretrainedType, path = None, pretrainedType
+        pretrainedType = PretrainedType.of(pretrainedType) if pretrainedType is not None else None
+        url = self.pretrainedUrl(pretrainedType)
+        cached = False
         if path is None:
-            raise RuntimeError("Pretrained weights cannot be downloaded in this environment; pass a local "
-                               "ModelSerializer zip path")
+            if url is None:
+                raise NotImplementedError(f"Pretrained {pretrainedType or PretrainedType.IMAGENET} weights are not "
+                                          f"available for this model.")
+            path = os.path.join(ROOT_CACHE_DIR, os.path.basename(url))
+            cached = True
+            if not os.path.exists(path):
+                raise RuntimeError(f"Pretrained weights cannot be downloaded in this environment: place {url} at "
+                                   f"{path} or pass a local ModelSerializer zip path")
+        expected = self.pretrainedChecksum(pretrainedType) if (url is not None and verify) else 0
+        if expected:
+            from .labels import adler32_file
+            local = adler32_file(path)
+            if local != expected:
+                if cached:
+                    os.remove(path)
+                raise RuntimeError(f"Pretrained model file failed checksum (Adler-32 {local}, expecting {expected})")
         from ..utils.model_serializer import ModelSerializer
         return ModelSerializer.restoreModel(path)
 
     def _builder(self):
         return NeuralNetConfiguration.Builder().seed(self.seed).dataType(self.dataType) \
             .trainingWorkspaceMode(self.workspaceMode).inferenceWorkspaceMode(self.workspaceMode)
+
+
+import enum as _enum
+import os as _os
+
+ROOT_CACHE_DIR = _os.path.join(_os.path.expanduser("~"), ".deeplearning4j", "models")
+
+
+class PretrainedType(_enum.Enum):
+    """Datasets pretrained weights exist for (ZOO:PretrainedType.java)."""
+    IMAGENET = "IMAGENET"
+    MNIST = "MNIST"
+    CIFAR10 = "CIFAR10"
+    VGGFACE = "VGGFACE"
+
+    @classmethod
+    def of(cls, v):
+        return v if isinstance(v, cls) else cls[str(v).upper()]
+
+
+class ZooType(_enum.Enum):
+    """Model selectors (ZOO:ZooType.java): single models plus the ALL / CNN / RNN groups."""
+    ALL = "ALL"
+    CNN = "CNN"
+    SIMPLECNN = "SIMPLECNN"
+    ALEXNET = "ALEXNET"
+    LENET = "LENET"
+    GOOGLENET = "GOOGLENET"
+    VGG16 = "VGG16"
+    VGG19 = "VGG19"
+    RESNET50 = "RESNET50"
+    INCEPTIONRESNETV1 = "INCEPTIONRESNETV1"
+    FACENETNN4SMALL2 = "FACENETNN4SMALL2"
+    RNN = "RNN"
+    TEXTGENLSTM = "TEXTGENLSTM"
+    DARKNET19 = "DARKNET19"
+    TINYYOLO = "TINYYOLO"
+    YOLO2 = "YOLO2"
+
+    @classmethod
+    def of_model(cls, class_name):
+        m = {"TextGenerationLSTM": "TEXTGENLSTM"}
+        return cls[m.get(class_name, class_name.upper())] if m.get(class_name, class_name.upper()) in cls.__members__ \
+            else None
+
+
+class ModelMetaData:
+    """Input shapes / output count / zoo type of a model (ZOO:ModelMetaData.java)."""
+
+    def __init__(self, inputShape, numOutputs, zooType):
+        self.inputShape, self.numOutputs, self.zooType = inputShape, numOutputs, zooType
+
+    def getInputShape(self):
+        return self.inputShape
+
+    def getNumOutputs(self):
+        return self.numOutputs
+
+    def getZooType(self):
+        return self.zooType
+
+    def useMDS(self):
+        return len(self.inputShape) > 1
+
+
+_BLOB = "http://blob.deeplearning4j.org/models/"
+_PRETRAINED = {
+    "ResNet50": {PretrainedType.IMAGENET: (_BLOB + "resnet50_dl4j_inference.zip", 1982516793)},
+    "LeNet": {PretrainedType.MNIST: (_BLOB + "lenet_dl4j_mnist_inference.zip", 1906861161)},
+    "GoogLeNet": {PretrainedType.IMAGENET: (_BLOB + "googlenet_dl4j_inference.zip", 3337733202)},
+    "VGG16": {PretrainedType.IMAGENET: (_BLOB + "vgg16_dl4j_inference.zip", 3501732770),
+              PretrainedType.CIFAR10: (_BLOB + "vgg16_dl4j_cifar10_inference.v1.zip", 2192260131),
+              PretrainedType.VGGFACE: (_BLOB + "vgg16_dl4j_vggface_inference.v1.zip", 2706403553)},
+    "VGG19": {PretrainedType.IMAGENET: (_BLOB + "vgg19_dl4j_inference.zip", 2782932419)},
+    "TinyYOLO": {PretrainedType.IMAGENET: (_BLOB + "tiny-yolo-voc_dl4j_inference.v1.zip", 2004171617)},
+    "YOLO2": {PretrainedType.IMAGENET: (_BLOB + "yolo2_dl4j_inference.v1.zip", 1357637732)},
+    "Darknet19": {PretrainedType.IMAGENET: (_BLOB + "darknet19_dl4j_inference.v1.zip", 3952910425)},
+    "Darknet19@448": {PretrainedType.IMAGENET: (_BLOB + "darknet19_448_dl4j_inference.v1.zip", 870575230)},
+}
 
 
 class _ZooBuilder:
@@ -322,6 +448,10 @@ class VGG19(VGG16):
 # --------------------------------------------------------------------------------------------- Darknet19
 class Darknet19(ZooModel):
     """Darknet-19 (reference ZOO:model/Darknet19.java): conv-BN-leakyReLU stacks + global avg pool."""
+
+    def _pretrained_key(self):
+        # the 448x448 ImageNet weights are a separate file (ZOO:model/Darknet19.java:62-81)
+        return "Darknet19@448" if list(self.inputShape[1:]) == [448, 448] else "Darknet19"
 
     def _cbl(self, g, name, k, n, inp):
         g.addLayer(f"conv{name}", ConvolutionLayer.Builder([k, k]).nOut(n).hasBias(False)
@@ -703,6 +833,46 @@ class InceptionResNetV1(ZooModel):
         net = ComputationGraph(self.conf())
         net.init(device=device)
         return net
+
+
+class ModelSelector:
+    """Instantiate zoo models by ZooType (ZOO:ModelSelector.java:16-140): a single type, a group (CNN: SimpleCNN,
+    AlexNet, LeNet, GoogLeNet, ResNet50, VGG16, VGG19, Darknet19, TinyYOLO, YOLO2; RNN: TextGenerationLSTM; ALL: both)
+    or several types, as {ZooType: ZooModel}. Defaults as the reference: numLabels 1 for select(type), 0 for
+    select(*types), seed 123. Unlike the reference's GOOGLENET case (which files GoogLeNet under LENET) every model is
+    keyed by its own type."""
+    _CNN = ("SIMPLECNN", "ALEXNET", "LENET", "GOOGLENET", "RESNET50", "VGG16", "VGG19", "DARKNET19", "TINYYOLO",
+            "YOLO2")
+    _SINGLE = {"TEXTGENLSTM": "TextGenerationLSTM", "SIMPLECNN": "SimpleCNN", "ALEXNET": "AlexNet", "LENET": "LeNet",
+               "INCEPTIONRESNETV1": "InceptionResNetV1", "FACENETNN4SMALL2": "FaceNetNN4Small2",
+               "GOOGLENET": "GoogLeNet", "RESNET50": "ResNet50", "VGG16": "VGG16", "VGG19": "VGG19",
+               "DARKNET19": "Darknet19", "TINYYOLO": "TinyYOLO", "YOLO2": "YOLO2"}
+
+    @classmethod
+    def select(cls, *zooTypes, numLabels=None, seed=123, workspaceMode=WorkspaceMode.ENABLED):
+        if not zooTypes:
+            raise ValueError("no ZooType given")
+        if numLabels is None:
+            numLabels = 1 if len(zooTypes) == 1 else 0
+        out = {}
+        for t in zooTypes:
+            cls._add(out, ZooType[t] if isinstance(t, str) else t, numLabels, seed, workspaceMode)
+        if not out:
+            raise ValueError("Zero models have been selected for benchmarking.")
+        return out
+
+    @classmethod
+    def _add(cls, out, t, numLabels, seed, ws):
+        if t == ZooType.ALL:
+            cls._add(out, ZooType.CNN, numLabels, seed, ws)
+            cls._add(out, ZooType.RNN, numLabels, seed, ws)
+        elif t == ZooType.CNN:
+            for n in cls._CNN:
+                cls._add(out, ZooType[n], numLabels, seed, ws)
+        elif t == ZooType.RNN:
+            cls._add(out, ZooType.TEXTGENLSTM, numLabels, seed, ws)
+        elif t.name in cls._SINGLE:
+            out[t] = ZOO[cls._SINGLE[t.name]](numLabels=numLabels, seed=seed, workspaceMode=ws)
 
 
 ZOO = {"ResNet50": ResNet50, "LeNet": LeNet, "SimpleCNN": SimpleCNN, "TextGenerationLSTM": TextGenerationLSTM,
