@@ -138,7 +138,19 @@ class SequenceVectors(WordVectorsImpl):
 
     # ------------------------------------------------------------------ data
     def _load_sequences(self):
-        """Subclasses fill self.sequences / self.seq_labels (lists of label lists)."""
+        """Subclasses fill self.sequences / self.seq_labels (lists of label lists); the base class reads the
+        Builder's source of ``Sequence`` objects (elements, optional sequence labels)."""
+        src = getattr(self, "_source", None)
+        if self.sequences is None and src is not None:
+            seqs, labs, any_label = [], [], False
+            for sq in src:
+                els = sq.getElements() if hasattr(sq, "getElements") else list(sq)
+                seqs.append([str(e) for e in els])
+                ls = sq.getSequenceLabels() if hasattr(sq, "getSequenceLabels") else None
+                labs.append([str(x) for x in (ls or [])])
+                any_label |= bool(ls)
+            self.sequences = seqs
+            self.seq_labels = labs if (any_label and self.conf.sequenceLearningAlgorithm) else None
         if self.sequences is None:
             raise ValueError("no training sequences configured")
 
@@ -294,6 +306,21 @@ class _BaseBuilder:
         m.useUnknown = self.c.useUnknown
         m.UNK = self.c.UNK
         return m
+
+
+class _SequenceVectorsBuilder(_BaseBuilder):
+    """SequenceVectors.Builder (NLP:models/sequencevectors/SequenceVectors.java Builder): trains on any iterable of
+    ``Sequence`` objects (elements = labels, optional sequence labels) — e.g. a graph/walkers.GraphTransformer, the
+    reference's route for graph embeddings (walkers -> GraphTransformer -> AbstractSequenceIterator ->
+    SequenceVectors). Sequence labels are learned with ``sequenceLearningAlgorithm`` (DBOW / DM) when set."""
+
+    def build(self):
+        m = SequenceVectors(self.c)
+        m._source = self._iter
+        return self._finish(m)
+
+
+SequenceVectors.Builder = _SequenceVectorsBuilder
 
 
 class Word2Vec(SequenceVectors):
