@@ -32,6 +32,11 @@
 
 #include "mfma_tile.h"
 
+// csrc/gemm_stream.hip: the persistent streaming kernel behind configuration 10 (-4 when the shape is not its own)
+DL4J_API int dl4j_gemm_stream(int in_dt, const void* A, long long lda, const void* B, long long ldb, void* C,
+                              long long ldc, int M, int N, int K, float alpha, const float* bias, int bias_mode,
+                              int act, int out_dt, float* tstats, int stats_P, int store_nt, hipStream_t s);
+
 // Diagnostic build only (tools/gemm_stamps.hip defines DL4J_GEMM_STAMPS): per-block phase timestamps of the 8-phase
 // kernel, shader clock and 100 MHz real time, written by lane 0 of wave 0 with an ordinary vector store.
 #ifdef DL4J_GEMM_STAMPS
@@ -936,6 +941,7 @@ void plan_f32(int M, int N, int K, int batch, int* tile, int* splits) {
   *splits = sp;
 }
 
+
 // ----------------------------------------------------------------------------------------------- dispatch
 // DL4J_AMD_GEMM_LEAN=0 forces the generic LDS epilogue everywhere (A/B experiments)
 
@@ -989,9 +995,10 @@ struct Cfg {
 //          8 = 128x128 single-buffered (32 KB, 4 blocks/CU), 9 = 128x256 single-buffered (8 waves, 64 KB, 2 blocks/CU):
 //              short-K, output-heavy products (the expanding 1x1 convolutions: K = 64..256, N = 256..1024), where
 //              a wide tile loads each A row panel once for more output columns and halves the blocks per output
-constexpr int kNumCfg = 10;
+//          10 = gemm_stream (persistent, loader wave + resident B panel; tall short-K products, M % 128 == 0)
+constexpr int kNumCfg = 11;
 const Cfg kCfg[kNumCfg] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {256, 256},
-                           {128, 64},  {128, 128}, {128, 128}, {128, 128}, {128, 256}};
+                           {128, 64},  {128, 128}, {128, 128}, {128, 128}, {128, 256}, {128, 128}};
 
 template <int DT, bool AKC, bool BKC, bool LEAN>
 int launch_fast(int cfg, const GemmArgs& g, int batch, hipStream_t s) {
@@ -1196,6 +1203,11 @@ DL4J_API int dl4j_gemm(int in_dt, int out_dt, int M, int N, int K, int batch, co
   g.tiles_m = (M + kCfg[cfg].bm - 1) / kCfg[cfg].bm;
   g.tiles_n = (N + kCfg[cfg].bn - 1) / kCfg[cfg].bn;
   const bool lean = lean_ok(g, batch);
+  if (cfg == 10) {                                // streaming kernel: its contract, else refused (-4)
+    if (!akc || !bkc || batch != 1 || splits != 1 || !lean || g.bnb || g.Z || (M % 128)) return -4;
+    return dl4j_gemm_stream(in_dt, A, lda, B, ldb, C, ldc, M, N, K, alpha, g.bias, g.bias_mode, act, out_dt, tstats,
+                            stats_P, g.store_nt, s);
+  }
   if (splits > 1 && cfg != 4 && batch == 1 && !g.bnb && splitk_fixup_mode() &&
       (long long)g.tiles_m * g.tiles_n <= kSkTiles)
     g.sk_ticket = sk_ticket_slot();            // gemm_glds sums the slabs itself: no reduce launch

@@ -5,7 +5,8 @@ from .iterators import (AsyncDataSetIterator, AsyncMultiDataSetIterator, Benchma
                         BenchmarkMultiDataSetIterator, DoublesDataSetIterator, EarlyTerminationDataSetIterator,
                         KFoldIterator, MultiDataSetIteratorAdapter, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
                         FileDataSetIterator, ReconstructionDataSetIterator, InequalityHandling,
-                        JointParallelDataSetIterator, CombinedPreProcessor, CombinedMultiDataSetPreProcessor)
+                        JointParallelDataSetIterator, CombinedPreProcessor, CombinedMultiDataSetPreProcessor,
+                        BaseParallelDataSetIterator, FileSplitDataSetIterator, FileSplitParallelDataSetIterator)
 from .normalizers import (NormalizerStandardize, NormalizerMinMaxScaler, ImagePreProcessingScaler,  # noqa: F401
                           VGG16ImagePreProcessor, MultiNormalizerStandardize, MultiNormalizerMinMaxScaler)
 from .fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator, LFWDataSetIterator,  # noqa

@@ -628,6 +628,178 @@ class JointParallelDataSetIterator(DataSetIterator):
         return self.sources[0].batch()
 
 
+class FileSplitDataSetIterator(DataSetIterator):
+    """DataSets from an explicit list of files through a callback (reference iterator/FileSplitDataSetIterator.java +
+    callbacks/FileCallback): ``callback(path) -> DataSet``; the default callback is ``DataSet.load``."""
+
+    def __init__(self, files, callback=None):
+        from .dataset import DataSet
+        self.files = list(files)
+        self.callback = callback or DataSet.load
+        self.i = 0
+
+    def hasNext(self):
+        return self.i < len(self.files)
+
+    def next(self, num=None):
+        if num is not None:
+            raise NotImplementedError("FileSplitDataSetIterator does not support next(num)")
+        f = self.files[self.i]
+        self.i += 1
+        cb = self.callback
+        return self._pp(cb.call(f) if hasattr(cb, "call") else cb(f))
+
+    def reset(self):
+        self.i = 0
+
+
+class BaseParallelDataSetIterator(DataSetIterator):
+    """One iterator over N producers (reference iterator/parallel/BaseParallelDataSetIterator.java:20-126): ``next()``
+    takes the producers round-robin with the InequalityHandling policy once one runs dry, and a ParallelWrapper
+    worker thread bound to producer k (``attachThread(k)``) pulls only its own producer with ``hasNextFor()`` /
+    ``nextFor()`` — the per-device feeding of ParallelWrapper. Subclasses implement ``hasNextFor(k)``,
+    ``nextFor(k)`` and ``resetProducer(k)``."""
+
+    def __init__(self, numProducers, inequalityHandling=InequalityHandling.STOP_EVERYONE):
+        self.numProducers = int(numProducers)
+        self.inequalityHandling = inequalityHandling
+        self.counter = 0
+        self.states = [True] * self.numProducers          # producer still has data
+        self.resetTracker = [False] * self.numProducers   # producer ran dry at least once (RESET)
+        self.allDepleted = False
+        self._affinity = threading.local()
+
+    # ---- per-producer API
+    def hasNextFor(self, consumer=None):
+        raise NotImplementedError
+
+    def nextFor(self, consumer=None):
+        raise NotImplementedError
+
+    def resetProducer(self, consumer):
+        raise NotImplementedError
+
+    def attachThread(self, producer):
+        if not 0 <= int(producer) < self.numProducers:
+            raise ValueError(f"Non-existent producer {producer}")
+        self._affinity.producer = int(producer)
+
+    def _attached(self):
+        k = getattr(self._affinity, "producer", None)
+        if k is None:
+            raise RuntimeError("attachThread(int) should be called prior to this call")
+        return k
+
+    # ---- round-robin view
+    def _cur(self):
+        return self.counter % self.numProducers
+
+    def hasNext(self):
+        if self.allDepleted or not any(self.states):
+            return False
+        cur = self._cur()
+        if self.hasNextFor(cur):
+            return True
+        self.states[cur] = False
+        if not any(self.states):
+            return False
+        h = self.inequalityHandling
+        if h == InequalityHandling.RESET:
+            self.resetTracker[cur] = True
+            if all(self.resetTracker):
+                self.allDepleted = True
+                return False
+            self.resetProducer(cur)
+            self.states[cur] = True
+            return True
+        if h == InequalityHandling.RELOCATE:
+            while True:
+                self.counter += 1
+                k = self._cur()
+                self.states[k] = bool(self.hasNextFor(k))
+                if self.states[k]:
+                    return True
+                if not any(self.states):
+                    return False
+        if h == InequalityHandling.PASS_NULL:
+            return True
+        return all(self.states)                            # STOP_EVERYONE
+
+    def next(self, num=None):
+        if num is not None:
+            raise NotImplementedError("parallel iterators do not support next(num)")
+        cur = self._cur()
+        ds = self.nextFor(cur) if self.hasNextFor(cur) else None   # PASS_NULL: a dry producer's turn yields None
+        self.counter += 1
+        return None if ds is None else self._pp(ds)
+
+    def reset(self):
+        for k in range(self.numProducers):
+            self.resetProducer(k)
+            self.states[k] = True
+            self.resetTracker[k] = False
+        self.allDepleted = False
+        self.counter = 0
+
+    def resetSupported(self):
+        return True
+
+    def asyncSupported(self):
+        return False
+
+
+class FileSplitParallelDataSetIterator(BaseParallelDataSetIterator):
+    """Per-device producers over a folder of DataSet files (reference iterator/parallel/
+    FileSplitParallelDataSetIterator.java): the files matching ``pattern`` (``%d`` = any index, default
+    "dataset-%d.bin") are split into ``numThreads`` contiguous parts, each read by its own AsyncDataSetIterator
+    (``bufferPerThread`` batches prefetched; on a GPU build each part is staged onto device ``k % numDevices``).
+    Unlike the reference's Lists.partition split, which drops the last ``files % numThreads`` files, the parts here
+    differ in size by at most one file."""
+    DEFAULT_PATTERN = "dataset-%d.bin"
+
+    def __init__(self, rootFolder, pattern=DEFAULT_PATTERN, callback=None, numThreads=None, bufferPerThread=2,
+                 inequalityHandling=InequalityHandling.STOP_EVERYONE, devices=None):
+        import os
+        import re
+        if not os.path.isdir(rootFolder):
+            raise ValueError("Root folder should point to existing folder")
+        if numThreads is None:
+            numThreads = max(1, torch.cuda.device_count())
+        super().__init__(numThreads, inequalityHandling)
+        rx = re.compile("^" + ".*".join(re.escape(x) for x in pattern.split("%d")) + "$")
+        key = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]      # noqa: E731
+        files = sorted((f for f in os.listdir(rootFolder) if rx.match(f)), key=key)
+        if not files:
+            raise ValueError("No suitable files were found")
+        if devices is None:
+            devices = [torch.device("cuda", k) for k in range(torch.cuda.device_count())] or [None]
+        n, T = len(files), self.numProducers
+        bounds = [(k * n) // T for k in range(T + 1)]
+        self.parts = [[os.path.join(rootFolder, f) for f in files[bounds[k]:bounds[k + 1]]] for k in range(T)]
+        self.asyncIterators = [AsyncDataSetIterator(FileSplitDataSetIterator(part, callback), bufferPerThread,
+                                                    devices[k % len(devices)])
+                               for k, part in enumerate(self.parts)]
+
+    def _check(self, k):
+        if not 0 <= k < self.numProducers:
+            raise ValueError("Non-existent consumer was requested")
+        return self.asyncIterators[k]
+
+    def hasNextFor(self, consumer=None):
+        return self._check(self._attached() if consumer is None else consumer).hasNext()
+
+    def nextFor(self, consumer=None):
+        return self._check(self._attached() if consumer is None else consumer).next()
+
+    def resetProducer(self, consumer):
+        self._check(consumer).reset()
+
+    def shutdown(self):
+        for it in self.asyncIterators:
+            if hasattr(it, "shutdown"):
+                it.shutdown()
+
+
 class CombinedPreProcessor:
     """Applies several DataSet pre-processors in order (reference nd4j CombinedPreProcessor; Builder.addPreProcessor
     appends, addPreProcessor(index, p) inserts)."""

@@ -62,6 +62,7 @@ _TUNE_LOG = os.environ.get("DL4J_AMD_GEMM_TUNE_LOG", "0") == "1"   # print every
 # (ops/fallback.py, helperCountFail()).
 _LIB = os.environ.get("DL4J_AMD_GEMM_LIB", "0") == "1"
 LIB_CFG = (-2, 1)
+STREAM_CFG = (10, 1)     # csrc/gemm_stream.hip: persistent loader-wave kernel for tall short-K (1x1-conv) products
 _F32_FORCE = None        # tests: True / False pins fp32 products to the library / the exact-fp32 kernel
 
 
@@ -79,6 +80,8 @@ def _candidates(M, N, K, batch, default):
     if K % 64 == 0:
         c += [(4, s) for s in splits if s == 1 or (batch == 1 and K // s >= 512 and t256 * s <= 1024)]
     c += [(x, 1) for x in (0, 1, 2, 3, 5, 6, 7, 8, 9)]
+    if batch == 1 and M % 128 == 0 and N % 64 == 0 and K % 64 == 0 and K // 64 in (1, 2, 4, 8):
+        c.append(STREAM_CFG)      # persistent streaming kernel (refuses, -4, layouts / epilogues it lacks)
     if batch == 1:
         # small output grids (e.g. the LSTM's [256 x 1024] weight gradients over K = T*mb = 1600) need deep split-K
         # to fill the CUs: down to 128-deep K slices when the tile grid is under a quarter of the chip

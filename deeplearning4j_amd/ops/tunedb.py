@@ -6,7 +6,8 @@ key) for one GPU architecture.
 * Lookup: ``deeplearning4j_amd/ops/tunedb/<arch>.json`` (or ``DL4J_AMD_TUNE_DB``) is read once; a shape found there
   is not re-timed, so a fresh process takes the recorded choice at its first call (no tuning pass in the first
   step, and the same kernels run from one process to the next instead of whatever won a 3-repetition timing on that
-  run). ``DL4J_AMD_TUNE_DB=off`` disables the database.
+  run). ``DL4J_AMD_TUNE_DB=off`` disables the database,
+  ``DL4J_AMD_TUNE_DB_SKIP=gemm`` only the named tables.
 * Record: with ``DL4J_AMD_TUNE_RECORD=<file>`` every decision the autotuners make is added to that file at exit
   (merged with what it already holds); ``DL4J_AMD_TUNE_REPS`` raises the timing repetitions for such a run.
 * Entries carry the schema version below; a file with another version is ignored (tile configuration ids changed).
@@ -86,8 +87,15 @@ def _native(v):
     return tuple(_native(x) for x in v) if isinstance(v, list) else v
 
 
+def _skipped():
+    return {t for t in os.environ.get("DL4J_AMD_TUNE_DB_SKIP", "").split(",") if t}
+
+
 def lookup(table, key):
-    """The recorded choice for ``key`` (tuples come back as tuples), or None."""
+    """The recorded choice for ``key`` (tuples come back as tuples), or None. Tables named in
+    ``DL4J_AMD_TUNE_DB_SKIP`` (comma-separated) are re-timed instead (re-recording one table after a kernel change)."""
+    if table in _skipped():
+        return None
     v = _load().get(table, {}).get(repr(key))
     return None if v is None else _native(v)
 
