@@ -181,10 +181,13 @@ __global__ __launch_bounds__(256) void bn_finalize(const float* __restrict__ par
 
 // mask (optional, RES only): one byte per 8-channel vector, bit i = ReLU active for channel 8*(v % (C/8)) + i, so
 // the backward pass reads 1/16 of the residual's bytes instead of re-reading the residual.
-template <typename T, bool RELU, bool RES>
+// RBN (residual BatchNorm folded in): the residual is the RAW output of the shortcut branch's conv and that branch's
+// own training BN (context rctx, statistics already folded) is applied here: y = relu(bn(x) + bn_r(res)). The
+// shortcut BN layer then never materialises its output (ResNet convBlock: conv -> BN -> add); see bn_bwd_* RBN.
+template <typename T, bool RELU, bool RES, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
                                                 long long M, int C, const float* __restrict__ ctx,
-                                                unsigned char* __restrict__ mask) {
+                                                unsigned char* __restrict__ mask, const float* __restrict__ rctx) {
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
   const float* scale = ctx + 2 * C;
@@ -195,9 +198,13 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
     // every grid-stride step keeps this thread on the same 8 channels: per-channel factors live in registers and
     // two independent vectors are in flight per iteration (instead of 16 L1 parameter loads per 16-byte vector)
     const int c0 = idx_mod(v0, T8) * 8;
-    float sc[8], sf[8];
+    float sc[8], sf[8], rsc[8], rsf[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i];
+      rsc[i] = RBN ? rctx[2 * C + c0 + i] : 1.f;
+      rsf[i] = RBN ? rctx[3 * C + c0 + i] : 0.f;
+    }
     long long v = v0;
     for (; v + stride < nvec; v += 2 * stride) {
       float a[2][8], r[2][8];
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float t = a[u][i] * sc[i] + sf[i];
-          if (RES) t += r[u][i];
+          if (RES) t += RBN ? fmaf(r[u][i], rsc[i], rsf[i]) : r[u][i];
           bits |= (t > 0.f ? 1u : 0u) << i;
           a[u][i] = RELU ? fmaxf(t, 0.f) : t;
         }
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float t = a[i] * sc[i] + sf[i];
-        if (RES) t += r[i];
+        if (RES) t += RBN ? fmaf(r[i], rsc[i], rsf[i]) : r[i];
         bits |= (t > 0.f ? 1u : 0u) << i;
         a[i] = RELU ? fmaxf(t, 0.f) : t;
       }
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float t = a[i] * scale[c0 + i] + shift[c0 + i];
-      if (RES) t += r[i];
+      if (RES) t += RBN ? fmaf(r[i], rctx[2 * C + c0 + i], rctx[3 * C + c0 + i]) : r[i];
       bits |= (t > 0.f ? 1u : 0u) << i;
       a[i] = RELU ? fmaxf(t, 0.f) : t;
     }
@@ -256,21 +263,26 @@ __global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T
 }
 
 // -------------------------------------------------------------------------------------------- backward
-template <typename T, bool RELU, bool RES>
+// RBN: the residual is the raw shortcut-conv output and its BN (rctx) was applied inside bn_apply: the same masked
+// d also feeds that BN's backward, so its sums sum(d) (= db) and sum(d * xhat_r) (part_dg2) come from this pass too.
+template <typename T, bool RELU, bool RES, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, const T* __restrict__ res,
                                                       const T* __restrict__ dy, long long M, int C,
                                                       long long rows_per_blk, const float* __restrict__ ctx,
                                                       float* __restrict__ part_db, float* __restrict__ part_dg,
-                                                      const unsigned char* __restrict__ mask) {
+                                                      const unsigned char* __restrict__ mask,
+                                                      const float* __restrict__ rctx, float* __restrict__ part_dg2) {
   const int T8 = C >> 3;
   const int R = 256 / T8;
   const int cg = threadIdx.x % T8, r0 = threadIdx.x / T8;
-  float db[8], dg[8], mu[8], is[8], sc[8], sf[8];
+  float db[8], dg[8], mu[8], is[8], sc[8], sf[8], dg2[8], mu2[8], is2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    db[i] = 0.f; dg[i] = 0.f;
+    db[i] = 0.f; dg[i] = 0.f; dg2[i] = 0.f;
     mu[i] = ctx[cg * 8 + i]; is[i] = ctx[C + cg * 8 + i];
     sc[i] = ctx[2 * C + cg * 8 + i]; sf[i] = ctx[3 * C + cg * 8 + i];
+    mu2[i] = RBN ? rctx[cg * 8 + i] : 0.f;
+    is2[i] = RBN ? rctx[C + cg * 8 + i] : 0.f;
   }
   const long long rbeg = (long long)blockIdx.x * rows_per_blk;
   long long rend = rbeg + rows_per_blk;
@@ -292,7 +304,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
         b.gv[u].load(dy + o);
         if (RES) {
           if (mask) b.mb[u] = mask[rr * T8 + cg];
-          else b.rv[RES ? u : 0].load(res + o);
+          if (!mask || RBN) b.rv[RES ? u : 0].load(res + o);
         }
       }
     };
@@ -308,11 +320,13 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
             d = (b.mb[u] >> i) & 1u ? d : 0.f;
           } else if (RELU) {
             float t = xf * sc[i] + sf[i];
-            if (RES) t += b.rv[RES ? u : 0].get(i);
+            if (RES) t += RBN ? fmaf(b.rv[RES ? u : 0].get(i), rctx[2 * C + cg * 8 + i], rctx[3 * C + cg * 8 + i])
+                              : b.rv[RES ? u : 0].get(i);
             d = t > 0.f ? d : 0.f;
           }
           db[i] += d;
           dg[i] += d * (xf - mu[i]) * is[i];
+          if (RBN) dg2[i] += d * (b.rv[RES ? u : 0].get(i) - mu2[i]) * is2[i];
         }
       }
     };
@@ -332,18 +346,25 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const T* __restrict__ x, c
   }
   __shared__ float red1[256 * 9];   // row pitch 9 floats: conflict-free 8-float stores
   __shared__ float red2[256 * 9];
+  __shared__ float red3[RBN ? 256 * 9 : 1];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     red1[threadIdx.x * 9 + i] = (r0 < R) ? db[i] : 0.f;
     red2[threadIdx.x * 9 + i] = (r0 < R) ? dg[i] : 0.f;
+    if (RBN) red3[threadIdx.x * 9 + i] = (r0 < R) ? dg2[i] : 0.f;
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c >> 3, k = c & 7;
-    float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < R; ++rr) { a += red1[(rr * T8 + g) * 9 + k]; b += red2[(rr * T8 + g) * 9 + k]; }
+    float a = 0.f, b = 0.f, e = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      a += red1[(rr * T8 + g) * 9 + k];
+      b += red2[(rr * T8 + g) * 9 + k];
+      if (RBN) e += red3[(rr * T8 + g) * 9 + k];
+    }
     part_db[(long long)blockIdx.x * C + c] = a;
     part_dg[(long long)blockIdx.x * C + c] = b;
+    if (RBN) part_dg2[(long long)blockIdx.x * C + c] = e;
   }
 }
 
@@ -641,12 +662,15 @@ __device__ __forceinline__ void bn_bwd_elem(float& xv, float& gv, float& rv, flo
   xv = A * d - B * xv - Cq;
 }
 
-template <typename T, bool RELU, bool RES>
+// RBN: dres receives the gradient w.r.t. the shortcut BN's INPUT (that BN's backward of the masked d, with its
+// context rctx and its mean(d * xhat_r) cdg2; mean(d) is cdb, shared), so that layer needs no pass of its own.
+template <typename T, bool RELU, bool RES, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                     const T* __restrict__ dy, T* __restrict__ dx, T* __restrict__ dres,
                                                     long long M, int C, const float* __restrict__ ctx,
                                                     const float* __restrict__ cdb, const float* __restrict__ cdg,
-                                                    const unsigned char* __restrict__ mask) {
+                                                    const unsigned char* __restrict__ mask,
+                                                    const float* __restrict__ rctx, const float* __restrict__ cdg2) {
   const bool use_mask = RES && mask != nullptr;
   const long long nvec = M * (C >> 3);
   const int T8 = C >> 3;
@@ -654,9 +678,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
   const long long stride = (long long)gridDim.x * blockDim.x;
   const long long v0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool fixed = stride % T8 == 0;   // the thread's channel group never changes: factors in registers
-  float A[8], B[8], Cq[8], sf[8];
-  if (fixed) {
-    const int c0 = idx_mod(v0, T8) * 8;
+  float A[8], B[8], Cq[8], sf[8], A2[8], B2[8], Cq2[8];
+  auto factors = [&](int c0) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int c = c0 + i;
@@ -664,8 +687,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
       B[i] = scale[c] * invstd[c] * cdg[c];
       Cq[i] = scale[c] * (cdb[c] - mean[c] * invstd[c] * cdg[c]);
       sf[i] = shift[c];
+      if (RBN) {
+        const float s2 = rctx[2 * C + c], i2 = rctx[C + c];
+        A2[i] = s2;
+        B2[i] = s2 * i2 * cdg2[c];
+        Cq2[i] = s2 * (cdb[c] - rctx[c] * i2 * cdg2[c]);
+      }
     }
-  }
+  };
+  if (fixed) factors(idx_mod(v0, T8) * 8);
   long long v = v0;
   if (fixed) {
     // four independent vectors in flight, kept packed until used (RawVec8: half the registers of unpacked floats)
@@ -679,7 +709,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
         gr[u].load(dy + (v + u * stride) * 8);
         mb[u] = 0u;
         if (use_mask) mb[u] = mask[v + u * stride];
-        else if (RES) rr[RES ? u : 0].load(res + (v + u * stride) * 8);
+        if (RES && (!use_mask || RBN)) rr[RES ? u : 0].load(res + (v + u * stride) * 8);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -688,9 +718,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
         for (int i = 0; i < 8; ++i) {
           xv[i] = xr[u].get(i);
           gv[i] = gr[u].get(i);
-          rv[i] = (RES && !use_mask) ? rr[RES ? u : 0].get(i) : 0.f;
+          rv[i] = (RES && (!use_mask || RBN)) ? rr[RES ? u : 0].get(i) : 0.f;
+          const float r_in = rv[i];
+          if (RBN && !use_mask) rv[i] = fmaf(r_in, A2[i], rctx[3 * C + idx_mod(v + u * stride, T8) * 8 + i]);
           bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i],
                                  use_mask ? (int)((mb[u] >> i) & 1u) : -1);
+          if (RBN) rv[i] = A2[i] * rv[i] - B2[i] * r_in - Cq2[i];
         }
         Vec8<T>::store(dx + (v + u * stride) * 8, xv);
         if (RES) Vec8<T>::store(dres + (v + u * stride) * 8, rv);
@@ -698,26 +731,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ x, con
     }
   }
   for (; v < nvec; v += stride) {
-    if (!fixed) {
-      const int c0 = idx_mod(v, T8) * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int c = c0 + i;
-        A[i] = scale[c];
-        B[i] = scale[c] * invstd[c] * cdg[c];
-        Cq[i] = scale[c] * (cdb[c] - mean[c] * invstd[c] * cdg[c]);
-        sf[i] = shift[c];
-      }
-    }
+    if (!fixed) factors(idx_mod(v, T8) * 8);
     float xv[8], gv[8], rv[8];
     unsigned mb = 0u;
     Vec8<T>::load(x + v * 8, xv);
     Vec8<T>::load(dy + v * 8, gv);
     if (use_mask) mb = mask[v];
-    else if (RES) Vec8<T>::load(res + v * 8, rv);
+    if (RES && (!use_mask || RBN)) Vec8<T>::load(res + v * 8, rv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const float r_in = rv[i];
+      if (RBN && !use_mask) rv[i] = fmaf(r_in, A2[i], rctx[3 * C + idx_mod(v, T8) * 8 + i]);
       bn_bwd_elem<RELU, RES>(xv[i], gv[i], rv[i], A[i], B[i], Cq[i], sf[i], use_mask ? (int)((mb >> i) & 1u) : -1);
+      if (RBN) rv[i] = A2[i] * rv[i] - B2[i] * r_in - Cq2[i];
+    }
     Vec8<T>::store(dx + v * 8, xv);
     if (RES) Vec8<T>::store(dres + v * 8, rv);
   }
@@ -787,7 +814,8 @@ static inline void bn_reduce_stage(float*& p1, float*& p2, int& nblk, int C, flo
 template <typename T>
 static int bn_fwd_impl(const T* x, const T* res, T* y, long long M, int C, const float* gamma, const float* beta,
                        float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
-                       int training, int relu, float* ws, float* ctx_out, unsigned char* mask, hipStream_t s) {
+                       int training, int relu, float* ws, float* ctx_out, unsigned char* mask, hipStream_t s,
+                       const float* rctx = nullptr) {
   int nblk; long long rpb;
   bn_grid(M, C, &nblk, &rpb);
   float* p1 = ws;
@@ -803,8 +831,13 @@ static int bn_fwd_impl(const T* x, const T* res, T* y, long long M, int C, const
     hipLaunchKernelGGL(bn_finalize<T>, dim3((C + 63) / 64), dim3(256), 0, s, p1, p2, nblk, C, M, x, gamma, beta,
                        gconst, bconst, run_mean, run_var, decay, eps, training, ctx_out);
   }
-  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C, ctx_out,
-               mask);
+  if (!y) return (int)hipGetLastError();              // statistics only (a shortcut BN folded into its consumer)
+  if (rctx && res)
+    hipLaunchKernelGGL((bn_apply<T, true, true, true>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C,
+                       ctx_out, mask, rctx);
+  else
+    BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, y, M, C, ctx_out, mask,
+                 (const float*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -835,7 +868,7 @@ template <typename T>
 static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C, const float* tstats, long long P,
                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
                              float* run_var, float decay, float eps, int relu, float* ws, float* ctx_out,
-                             unsigned char* mask, hipStream_t s) {
+                             unsigned char* mask, hipStream_t s, const float* rctx = nullptr) {
   const long long S = (P + 31) / 32;
   BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
           nullptr, nullptr, nullptr, nullptr, nullptr, 64};
@@ -851,8 +884,13 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
     rc = bn_fold_launch<T, 0, 0>(p1, p2, S, C, p2 + S * C, f, s);
   }
   if (rc) return rc;
-  BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C, ctx_out,
-               mask);
+  if (!y) return (int)hipGetLastError();              // statistics only (a shortcut BN folded into its consumer)
+  if (rctx && res)
+    hipLaunchKernelGGL((bn_apply<T, true, true, true>), dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C,
+                       ctx_out, mask, rctx);
+  else
+    BN_DISPATCH3(bn_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, xb, res, y, M, C, ctx_out,
+                 mask, (const float*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -881,14 +919,86 @@ static int bn_bwd_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, lo
   float* q = p2 + (long long)nblk * C;
   float* cdb = q + 2LL * ((nblk + 31) / 32) * C;
   float* cdg = cdb + C;
-  BN_DISPATCH3(bn_bwd_partial, T, relu, res, dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1, p2, mask);
+  BN_DISPATCH3(bn_bwd_partial, T, relu, res, dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1, p2, mask,
+               (const float*)nullptr, (float*)nullptr);
   BnFin f{M, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0.f, 0.f, nullptr, dbeta, dgamma, cdb, cdg,
           nullptr, 0};
   const int rc = bn_fold_launch<T, 0, 1>(p1, p2, nblk, C, q, f, s);
   if (rc) return rc;
   BN_DISPATCH3(bn_bwd_apply, T, relu, res, dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, dy, dx, dres, M, C, ctx,
-               cdb, cdg, mask);
+               cdb, cdg, mask, (const float*)nullptr, (const float*)nullptr);
   return (int)hipGetLastError();
+}
+
+// Residual layer whose shortcut BN is folded in (RBN): one partial pass gives both layers' sums, two folds, one apply
+// writing dx and the gradient w.r.t. the shortcut BN's input (dres). Workspace: dl4j_bn_bwd_rbn_workspace_floats.
+DL4J_API long long dl4j_bn_bwd_rbn_workspace_floats(long long M, int C) {
+  int nblk; long long rpb;
+  bn_bwd_grid(M, C, &nblk, &rpb);
+  return 3LL * nblk * C + 4LL * ((nblk + 31) / 32) * C + 4LL * C;
+}
+
+template <typename T>
+static int bn_bwd_rbn_impl(const T* x, const T* res, const T* dy, T* dx, T* dres, long long M, int C, const float* ctx,
+                           float* dgamma, float* dbeta, const float* rctx, float* dgamma2, float* dbeta2, float* ws,
+                           const unsigned char* mask, hipStream_t s) {
+  int nblk; long long rpb;
+  bn_bwd_grid(M, C, &nblk, &rpb);
+  const long long S = (nblk + 31) / 32;
+  float* p1 = ws;
+  float* p2 = p1 + (long long)nblk * C;
+  float* p3 = p2 + (long long)nblk * C;
+  float* q = p3 + (long long)nblk * C;
+  float* q2 = q + 2 * S * C;
+  float* cdb = q2 + 2 * S * C;
+  float* cdg = cdb + C;
+  float* cdb2 = cdg + C;
+  float* cdg2 = cdb2 + C;
+  hipLaunchKernelGGL((bn_bwd_partial<T, true, true, true>), dim3(nblk), dim3(256), 0, s, x, res, dy, M, C, rpb, ctx, p1,
+                     p2, mask, rctx, p3);
+  BnFin f{M, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0.f, 0.f, nullptr, dbeta, dgamma, cdb, cdg,
+          nullptr, 0};
+  int rc = bn_fold_launch<T, 0, 1>(p1, p2, nblk, C, q, f, s);
+  if (rc) return rc;
+  BnFin f2{M, nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0.f, 0.f, nullptr, dbeta2, dgamma2, cdb2, cdg2,
+           nullptr, 0};
+  rc = bn_fold_launch<T, 0, 1>(p1, p3, nblk, C, q2, f2, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL((bn_bwd_apply<T, true, true, true>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, res, dy, dx, dres,
+                     M, C, ctx, cdb, cdg, mask, rctx, cdg2);
+  return (int)hipGetLastError();
+}
+
+DL4J_API int dl4j_bn_bwd_rbn(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres,
+                             long long M, int C, const float* ctx, float* dgamma, float* dbeta, const float* rctx,
+                             float* dgamma2, float* dbeta2, float* ws, const unsigned char* mask, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || !res || !dres || !rctx || (dtype != 1 && dtype != 2)) return -1;
+  if (dtype == 2)
+    return bn_bwd_rbn_impl<f16>((const f16*)x, (const f16*)res, (const f16*)dy, (f16*)dx, (f16*)dres, M, C, ctx, dgamma,
+                                dbeta, rctx, dgamma2, dbeta2, ws, mask, s);
+  return bn_bwd_rbn_impl<bf16>((const bf16*)x, (const bf16*)res, (const bf16*)dy, (bf16*)dx, (bf16*)dres, M, C, ctx,
+                               dgamma, dbeta, rctx, dgamma2, dbeta2, ws, mask, s);
+}
+
+// Residual forward with the shortcut BN folded in: y = relu(bn(x) + bn_r(res)), rctx the shortcut BN's finalized
+// context (its statistics-only forward). tstats / P: the producing conv's tile statistics (or null: full pass).
+DL4J_API int dl4j_bn_fwd_rbn(int dtype, const void* x, const void* res, const float* rctx, void* y, long long M, int C,
+                             const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
+                             float* run_var, float decay, float eps, float* ws, float* ctx_out, unsigned char* mask,
+                             const float* tstats, long long P, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || !res || !rctx || !y || (dtype != 1 && dtype != 2)) return -1;
+  if (tstats) {
+    if (dtype == 2)
+      return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, gamma, beta, gconst,
+                                    bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
+    return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, gamma, beta, gconst,
+                                   bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
+  }
+  if (dtype == 2)
+    return bn_fwd_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, gamma, beta, gconst, bconst, run_mean,
+                            run_var, decay, eps, 1, 1, ws, ctx_out, mask, s, rctx);
+  return bn_fwd_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, gamma, beta, gconst, bconst, run_mean,
+                           run_var, decay, eps, 1, 1, ws, ctx_out, mask, s, rctx);
 }
 
 DL4J_API int dl4j_bn_bwd(int dtype, const void* x, const void* res, const void* dy, void* dx, void* dres, long long M,
@@ -926,13 +1036,13 @@ static int bn_bwd_planes_impl(const T* x, const T* dy, T* dx, T* dres, const uns
   if (rc) return rc;
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply<T, true, true>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
-                       dres, M, C, ctx, cdb, cdg, mask);
+                       dres, M, C, ctx, cdb, cdg, mask, nullptr, nullptr);
   else if (relu)
     hipLaunchKernelGGL((bn_bwd_apply<T, true, false>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
-                       nullptr, M, C, ctx, cdb, cdg, nullptr);
+                       nullptr, M, C, ctx, cdb, cdg, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL((bn_bwd_apply<T, false, false>), dim3(apply_grid(M, C)), dim3(256), 0, s, x, nullptr, dy, dx,
-                       nullptr, M, C, ctx, cdb, cdg, nullptr);
+                       nullptr, M, C, ctx, cdb, cdg, nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

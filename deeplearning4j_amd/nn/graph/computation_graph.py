@@ -143,6 +143,17 @@ class ComputationGraph(BaseNetwork):
                     self._residual_of[name] = other
                     self._passthrough[nxt_name] = name
                     self._passthrough[relu_name] = nxt_name
+                    # the shortcut branch ends in its own BN (ResNet convBlock: conv -> BN -> add): in training that BN
+                    # only folds its statistics and this layer applies both normalisations in one pass (forward) and
+                    # runs both backwards from one partial-sum pass (csrc/batchnorm.hip RBN kernels)
+                    ov = self.conf.vertices.get(other)
+                    if isinstance(ov, LayerVertex) and isinstance(ov.layerConf, BatchNormalization) and \
+                            ov.layerConf.idropout is None and ov.preProcessor is None and \
+                            self.consumers.get(other) == [nxt_name] and other not in self.outputs and \
+                            not getattr(ov.layerConf, "useLogStd", False) and \
+                            os.environ.get("DL4J_AMD_FUSE_RES_BN", "1") == "1":
+                        self.layers_by_name[name].residual_bn = self.layers_by_name[other]
+                        self.layers_by_name[other].defer_apply = True
                     continue
             if is_relu_layer(nxt_name) and nxt_name not in self.outputs:
                 self.layers_by_name[name].fuse_relu = True
@@ -447,7 +458,19 @@ class ComputationGraph(BaseNetwork):
         self._mb = inputs[0].shape[0]
         self._prepare_conv_weights()
         fm = [self._to_dev(m) for m in fmasks] if fmasks else None
-        acts = self.feedForward(inputs, True, fm, stored_state, store_last_for_tbptt)
+        # the output activation of a training forward is not read (the fused loss recomputes the softmax from the
+        # pre-activation) unless a listener asks for the activations or another vertex consumes that output
+        skip = not any(hasattr(l, "onForwardPass") for l in self.listeners)
+        outs = [self.layers_by_name.get(o) for o in self.outputs]
+        for o, l in zip(self.outputs, outs):
+            if l is not None and skip and not self.consumers.get(o):
+                l._skip_train_output = True
+        try:
+            acts = self.feedForward(inputs, True, fm, stored_state, store_last_for_tbptt)
+        finally:
+            for l in outs:
+                if l is not None:
+                    l._skip_train_output = False
         for l in self.listeners:
             if hasattr(l, "onForwardPass"):
                 l.onForwardPass(self, acts)

@@ -47,10 +47,31 @@ class BatchNormalizationImpl(LayerImpl):
             self._track_deferred_bias(training)
             return y
         self._pool_fused = False
+        self._apply_deferred = False
+        if getattr(self, "defer_apply", False) and training:
+            # shortcut BN folded into its residual consumer (planner): statistics only, the raw input flows on and
+            # the consumer applies this layer's normalisation (and runs its backward)
+            r = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
+                               stats_only=True)
+            if r is not None:
+                self._apply_deferred = True
+                y, self._ctx = r
+                self._track_deferred_bias(training)
+                return y
         # the reference BN layer applies no activation function of its own (BatchNormalization.java:225,398)
         res = getattr(self, "residual", None)
-        y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
-                                      relu=self.fuse_relu, residual=res)
+        rbn = getattr(self, "residual_bn", None)
+        self._rbn_active = None
+        if res is not None and rbn is not None and getattr(rbn, "_apply_deferred", False):
+            r = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
+                               relu=True, residual=res, rctx=rbn._ctx[2])
+            if r is None:
+                raise RuntimeError(f"{self.layerId()}: fused shortcut BatchNormalization could not run")
+            y, self._ctx = r
+            self._rbn_active = rbn
+        else:
+            y, self._ctx = ops.bn_forward(x, g, b, self.params["mean"], self.params["var"], training, c.decay, c.eps,
+                                          relu=self.fuse_relu, residual=res)
         self.residual = None
         self._track_deferred_bias(training)
         return y
@@ -67,9 +88,20 @@ class BatchNormalizationImpl(LayerImpl):
 
     def backpropGradient(self, eps):
         gg, gb = self.grads.get("gamma"), self.grads.get("beta")
+        if getattr(self, "_apply_deferred", False):
+            # the residual consumer already wrote this layer's gamma / beta gradients and hands back the gradient
+            # w.r.t. this layer's input
+            self._apply_deferred = False
+            self._zero_stat_grads()
+            return self.make_gradient(), self.backpropDropOut(eps)
         if getattr(self, "_pool_fused", False):
             dx, dgamma, dbeta = ops.bn_pool_backward(eps, self._ctx, gg, gb)
             self.dresidual = None
+        elif getattr(self, "_rbn_active", None) is not None:
+            rbn = self._rbn_active
+            self._rbn_active = None
+            dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx, gg, gb,
+                                                                rgrads=(rbn.grads.get("gamma"), rbn.grads.get("beta")))
         else:
             dx, dgamma, dbeta, self.dresidual = ops.bn_backward(eps, self._ctx, gg, gb)
         if gg is not None:
@@ -77,12 +109,15 @@ class BatchNormalizationImpl(LayerImpl):
                 copy_grad_(gg, dgamma)
             if dbeta is not gb:
                 copy_grad_(gb, dbeta)
+        self._zero_stat_grads()
+        return self.make_gradient(), self.backpropDropOut(dx)
+
+    def _zero_stat_grads(self):
         if not getattr(self, "_stat_grads_zero", False):
             # running-stat "gradients" are zero (reference :164-167,205-208); their NoOp update keeps them so
             self.grads["mean"].zero_()
             self.grads["var"].zero_()
             self._stat_grads_zero = True
-        return self.make_gradient(), self.backpropDropOut(dx)
 
 
 def _is_identity(a):

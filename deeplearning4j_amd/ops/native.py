@@ -308,7 +308,11 @@ def _rows_like(t, ref):
     return t.to(ref.dtype)
 
 
-def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual=None):
+def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual=None, rctx=None,
+           stats_only=False):
+    """``stats_only``: training statistics + running-stat update + context, no output (a shortcut BN whose apply
+    the residual consumer does: returns (x, ctx)). ``rctx``: that shortcut BN's context — ``residual`` is then its
+    raw input and the apply computes relu(bn(x) + bn_r(residual))."""
     dt = _dt16(x)
     xr = _as_rows_nhwc(x) if dt is not None else None
     if xr is None:
@@ -316,8 +320,12 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     M, C = xr.shape
     if C % 8 != 0 or C // 8 > 256 or run_mean.dtype != torch.float32:
         return None
+    if (stats_only or rctx is not None) and not (training and dt in (1, 2)):
+        return None
     lib = load()
-    y = _like_rows(x)
+    if rctx is not None:
+        return _bn_fwd_rbn(lib, x, xr, dt, M, C, gamma, beta, run_mean, run_var, decay, eps, residual, rctx)
+    y = None if stats_only else _like_rows(x)
     ws = _ae((lib.dl4j_bn_workspace_floats(M, C),), torch.float32, x.device)
     ctx = _ae((4 * C,), torch.float32, x.device)
     g = gamma if torch.is_tensor(gamma) else None
@@ -341,6 +349,8 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
                                    _ptr(wst), _ptr(ctx), _ptr(mask), _stream())
         _check(rc, "bn_fwd_tiles")
+        if stats_only:
+            return x, ("NATIVE_STATS", x, ctx, False, M, C, None, None)
         _bnb_request(y, xr, ctx, relu, res, mask, training, dt)
         return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
     rc = lib.dl4j_bn_fwd(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(g), _ptr(b),
@@ -348,8 +358,37 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
                          _ptr(run_var), float(decay), float(eps), 1 if training else 0, 1 if relu else 0, _ptr(ws),
                          _ptr(ctx), _ptr(mask), _stream())
     _check(rc, "bn_fwd")
+    if stats_only:
+        return x, ("NATIVE_STATS", x, ctx, False, M, C, None, None)
     _bnb_request(y, xr, ctx, relu, res, mask, training, dt)
     return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
+
+
+def _bn_fwd_rbn(lib, x, xr, dt, M, C, gamma, beta, run_mean, run_var, decay, eps, residual, rctx):
+    """Residual BN apply with the shortcut BN folded in (csrc/batchnorm.hip dl4j_bn_fwd_rbn)."""
+    y = _like_rows(x)
+    ctx = _ae((4 * C,), torch.float32, x.device)
+    g = gamma if torch.is_tensor(gamma) else None
+    b = beta if torch.is_tensor(beta) else None
+    res = _rows_like(residual, x)
+    mask = _ae((M * C // 8,), torch.uint8, x.device)
+    ts = getattr(x, "_bn_tile_stats", None)
+    tiles = ts is not None and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and (len(ts) < 3 or ts[2] == 64)
+    register_sig("dl4j_bn_fwd_rbn", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
+                                     c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_ll, c_void_p])
+    if tiles:
+        register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
+        lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
+        ws = _ae((lib.dl4j_bn_tiles_workspace_floats(ts[1], C),), torch.float32, x.device)
+    else:
+        ws = _ae((lib.dl4j_bn_workspace_floats(M, C),), torch.float32, x.device)
+    rc = lib.dl4j_bn_fwd_rbn(dt, _ptr(xr), _ptr(res), _ptr(rctx), _ptr(y), M, C, _ptr(g), _ptr(b),
+                             float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
+                             _ptr(run_var), float(decay), float(eps), _ptr(ws), _ptr(ctx), _ptr(mask),
+                             _ptr(ts[0]) if tiles else None, ts[1] if tiles else 0, _stream())
+    _check(rc, "bn_fwd_rbn")
+    return y, ("NATIVE", x, ctx, True, M, C, res, mask, rctx)
 
 
 # ------------------------------------------------------------------ BN backward sums from the producer's epilogue
@@ -408,9 +447,12 @@ def _bnb_planes(dy, c, res, M, C, mask=None):
     return planes
 
 
-def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
-    _, x, c, relu, M, C, res, mask = ctx
-    planes = _bnb_planes(dy, c, res, M, C, mask)
+def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None, rgrads=None):
+    """``rgrads``: (dgamma, dbeta) outputs of the folded-in shortcut BN (ctx from _bn_fwd_rbn); dres is then the
+    gradient w.r.t. that BN's input. Returns (dx, dgamma, dbeta, dres) and, with rgrads, fills them."""
+    _, x, c, relu, M, C, res, mask = ctx[:8]
+    rctx = ctx[8] if len(ctx) > 8 else None
+    planes = _bnb_planes(dy, c, res, M, C, mask) if rctx is None else None
     dy = _rows_like(dy, x)
     lib = load()
     dx = _like_rows(x)
@@ -418,6 +460,25 @@ def bn_bwd(dy, ctx, dgamma_out=None, dbeta_out=None):
     ok = lambda t: t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == C  # noqa
     dgamma = dgamma_out if ok(dgamma_out) else _ae((C,), torch.float32, x.device)
     dbeta = dbeta_out if ok(dbeta_out) else _ae((C,), torch.float32, x.device)
+    if rctx is not None:
+        rg = rgrads if rgrads is not None else (None, None)
+        dg2 = rg[0] if ok(rg[0]) else _ae((C,), torch.float32, x.device)
+        db2 = rg[1] if ok(rg[1]) else _ae((C,), torch.float32, x.device)
+        register_sig("dl4j_bn_bwd_rbn_workspace_floats", [c_ll, c_int])
+        lib.dl4j_bn_bwd_rbn_workspace_floats.restype = c_ll
+        register_sig("dl4j_bn_bwd_rbn", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p])
+        ws = _ae((lib.dl4j_bn_bwd_rbn_workspace_floats(M, C),), torch.float32, x.device)
+        rc = lib.dl4j_bn_bwd_rbn(_dt16(x), _ptr(x), _ptr(res), _ptr(dy), _ptr(dx), _ptr(dres), M, C, _ptr(c),
+                                 _ptr(dgamma), _ptr(dbeta), _ptr(rctx), _ptr(dg2), _ptr(db2), _ptr(ws), _ptr(mask),
+                                 _stream())
+        _check(rc, "bn_bwd_rbn")
+        if rgrads is not None:
+            for dst, src in zip(rgrads, (dg2, db2)):
+                if dst is not None and dst is not src:
+                    dst.copy_(src.reshape(dst.shape))
+        return dx, dgamma, dbeta, dres
     if planes is not None:
         register_sig("dl4j_bn_bwd_planes_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_bwd_planes_workspace_floats.restype = c_ll

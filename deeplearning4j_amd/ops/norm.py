@@ -22,11 +22,21 @@ def _bshape(x):
     return (1, -1) if x.dim() == 2 else (1, -1, 1, 1)
 
 
-def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=False, residual=None):
+def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=False, residual=None, rctx=None,
+               stats_only=False):
     """Returns (y, ctx). gamma/beta may be python floats (lockGammaBeta). Running stats updated in place
-    when training. ``residual``: fused shortcut, y = relu(bn(x) + residual) (relu implied)."""
+    when training. ``residual``: fused shortcut, y = relu(bn(x) + residual) (relu implied).
+    HIP-only fusions (None when the kernel path cannot take them; the caller then runs the unfused layers):
+    ``stats_only`` returns (x, ctx) after the statistics / running-stat update (the apply is done by the residual
+    consumer), ``rctx`` (a stats_only context) applies that shortcut BN to the raw ``residual`` inside this pass."""
     if residual is not None:
         relu = True
+    if stats_only or rctx is not None:
+        if not (use_native(x, "bn") and x.dim() in (2, 4) and torch.is_tensor(gamma)):
+            return None
+        from . import native
+        return native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual, rctx=rctx,
+                             stats_only=stats_only)
     if use_native(x, "bn") and x.dim() in (2, 4) and torch.is_tensor(gamma):
         from . import native
         r = native.bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residual)
@@ -61,13 +71,14 @@ def bn_forward(x, gamma, beta, run_mean, run_var, training, decay, eps, relu=Fal
     return y, ("REF", x, mean, invstd, g, b, relu, y if relu else None, residual is not None)
 
 
-def bn_backward(dy, ctx, dgamma_out=None, dbeta_out=None):
+def bn_backward(dy, ctx, dgamma_out=None, dbeta_out=None, rgrads=None):
     """Returns (dx, dgamma, dbeta, dresidual) — dgamma/dbeta are sums over the batch (not averaged);
     dresidual is None unless the forward fused a residual. The native kernel writes dgamma/dbeta straight
-    into ``dgamma_out``/``dbeta_out`` (the layer's fp32 gradient views) when given."""
+    into ``dgamma_out``/``dbeta_out`` (the layer's fp32 gradient views) when given. With a folded-in shortcut BN
+    (forward ``rctx``) dresidual is the gradient w.r.t. that BN's input and ``rgrads`` = its (dgamma, dbeta) views."""
     if ctx[0] == "NATIVE":
         from . import native
-        return native.bn_bwd(dy, ctx, dgamma_out, dbeta_out)
+        return native.bn_bwd(dy, ctx, dgamma_out, dbeta_out, rgrads=rgrads)
     _, x, mean, invstd, g, b, relu, y, has_res = ctx
     dims = _dims(x)
     bs = _bshape(x)
