@@ -399,3 +399,30 @@ DL4J_API int dl4j_stem_conv_wrw(const void* x, const void* dy, float* dW, float*
   hipLaunchKernelGGL(stem_wrw_reduce, dim3((64 * 147 + 64 + 15) / 16), dim3(256), 0, s, part, part_db, G, dW, db);
   return (int)hipGetLastError();
 }
+
+// Fragment-packed stem weights for stem_conv_fwd, rebuilt whenever the weights change (every training step): pk is
+// bf16 [4][6][64][8]; element (i, j, m, n) holds tap row = j*32 + (m/16)*8 + n of a [192][64] image whose row
+// r*24 + s*3 + c carries W[k][c][r][s] for k = i*16 + m%16 (rows with (row % 24) >= 21 are zero padding).
+// W is read through element strides (k, c, r, s), so any view of the [64][3][7][7] weights works. One launch
+// instead of the permute / index-copy / reshape sequence on the host side.
+__global__ __launch_bounds__(256) void stem_pack_weights(const u16* __restrict__ w, u16* __restrict__ pk,
+                                                         long long sk, long long sc, long long sr, long long ss) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 4 * 6 * 64 * 8) return;
+  const int n = e & 7, m = (e >> 3) & 63, j = (e >> 9) % 6, i = e / (6 * 512);
+  const int row = j * 32 + (m >> 4) * 8 + n, k = i * 16 + (m & 15);
+  const int r = row / 24, rem = row - r * 24;
+  u16 v = 0;
+  if (rem < 21) {
+    const int s_ = rem / 3, c = rem - s_ * 3;
+    v = w[k * sk + c * sc + r * sr + s_ * ss];
+  }
+  pk[e] = v;
+}
+
+DL4J_API int dl4j_stem_pack_weights(const void* w, void* pk, long long sk, long long sc, long long sr, long long ss,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(stem_pack_weights, dim3((4 * 6 * 64 * 8 + 255) / 256), dim3(256), 0, s, (const u16*)w, (u16*)pk,
+                     sk, sc, sr, ss);
+  return (int)hipGetLastError();
+}

@@ -709,3 +709,34 @@ DL4J_API int dl4j_col2im(int dt, const void* cols, void* x, int N, int C, int Hp
 #undef L
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------ fill
+// out[0 .. nbytes) = a repeated 4-byte pattern (fp32 value, or two copies of a 16-bit value): the zero fills of the
+// training step (flat gradient before backward, the gaps of strided backward-data outputs) without a library kernel.
+// 16-byte stores, grid-stride; a ragged head / tail (unaligned base or size) in 4-byte (2-byte) pieces.
+__global__ __launch_bounds__(256) void fill_pattern(char* __restrict__ out, long long nbytes, unsigned pat) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(out);
+  const long long head = (long long)((16 - (base & 15)) & 15) > nbytes ? nbytes : (long long)((16 - (base & 15)) & 15);
+  const long long nvec = (nbytes - head) / 16;
+  uint4* v = reinterpret_cast<uint4*>(out + head);
+  const uint4 q = make_uint4(pat, pat, pat, pat);
+  for (long long i = tid; i < nvec; i += stride) v[i] = q;
+  if (tid == 0) {
+    // head and tail bytes: the pattern is 4-byte periodic from the base (2-byte fills are 2-byte aligned)
+    for (long long b = 0; b < head; b += 2)
+      *reinterpret_cast<unsigned short*>(out + b) = (unsigned short)(pat >> (8 * ((base + b) & 3)));
+    for (long long b = head + nvec * 16; b < nbytes; b += 2)
+      *reinterpret_cast<unsigned short*>(out + b) = (unsigned short)(pat >> (8 * ((base + b) & 3)));
+  }
+}
+
+// elem_bytes 4 (pattern = the fp32 bits) or 2 (pattern = the 16-bit value in both halves); nbytes a multiple of 2.
+DL4J_API int dl4j_fill(void* out, long long nbytes, unsigned pattern, hipStream_t s) {
+  if (nbytes <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(out) & 1) || (nbytes & 1)) return -1;
+  hipLaunchKernelGGL(fill_pattern, dim3(grid1((nbytes + 15) / 16)), dim3(256), 0, s, reinterpret_cast<char*>(out),
+                     nbytes, pattern);
+  return (int)hipGetLastError();
+}

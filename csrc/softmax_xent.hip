@@ -122,3 +122,31 @@ DL4J_API int dl4j_softmax_xent_masked(int dtype, const void* z, const float* y, 
   if (!rmask) return -1;
   return softmax_xent_launch(dtype, z, y, B, V, grad, score, nullptr, clip_eps, rmask, s);
 }
+
+// ------------------------------------------------------------------------------------------------ score scalar
+// out[0] = (sum_{i<n} s[i] + add) * scale + (reg ? reg[0] * reg_scale : 0), one 256-thread block, fixed summation
+// order (bitwise reproducible). The training score on the device without library reduce / elementwise kernels:
+// per-example losses -> minibatch score (BaseOutputLayer.computeScore: (sum + l1 + l2) / minibatch), and the
+// updater's per-block regularisation partials folded into it. out may alias reg.
+__global__ __launch_bounds__(256) void score_reduce(const float* __restrict__ s, long long n, float add, float scale,
+                                                    const float* reg, float reg_scale, float* out) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 256) acc += s[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float r = reg ? reg[0] * reg_scale : 0.f;
+    out[0] = (red[0] + add) * scale + r;
+  }
+}
+
+DL4J_API int dl4j_score_reduce(const float* s, long long n, float add, float scale, const float* reg, float reg_scale,
+                               float* out, hipStream_t st) {
+  hipLaunchKernelGGL(score_reduce, dim3(1), dim3(256), 0, st, s, n, add, scale, reg, reg_scale, out);
+  return (int)hipGetLastError();
+}

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
                                                            TS* __restrict__ shadow, float inv_div, int write_update,
                                                            float* __restrict__ reg_out,
                                                            const float* __restrict__ gn_partial,
-                                                           const unsigned* __restrict__ guard) {
+                                                           const unsigned* __restrict__ guard, int reg_partials) {
   // a cooperative LSTM launch of this step timed out (csrc/lstm_coop.hip step guard): its outputs are invalid, so
   // parameters, updater state and shadow stay as they were; the host reports the failure
   if (guard && __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -166,7 +166,12 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
   if (reg_out != nullptr && (s.l1 > 0.f || s.l2 > 0.f)) {
     __shared__ float red[4];
     reg = block_reduce<false>(reg, red);
-    if (threadIdx.x == 0) atomicAdd(reg_out, reg);
+    if (threadIdx.x == 0) {
+      if (reg_partials) reg_out[blockIdx.x] = reg;        // fixed-order sum later (dl4j_score_reduce): deterministic
+      else atomicAdd(reg_out, reg);
+    }
+  } else if (reg_out != nullptr && reg_partials && threadIdx.x == 0) {
+    reg_out[blockIdx.x] = 0.f;
   }
 }
 
@@ -176,9 +181,30 @@ __global__ __launch_bounds__(256) void fused_update_kernel(const SegDesc* __rest
 // writes it), else null.
 unsigned* lstm_step_guard_ptr();      // csrc/lstm_coop.hip
 
+static int fused_update_launch(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
+                               void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
+                               float* gn_partial, hipStream_t stream, int reg_partials);
+
 DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
                                void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
                                float* gn_partial, hipStream_t stream) {
+  return fused_update_launch(segs, btab, nblocks, p, g, st, shadow, shadow_kind, inv_div, write_update, reg_out,
+                             gn_partial, stream, 0);
+}
+
+// Same, with the regularisation term written as one partial per block (reg_part: nblocks floats, every block writes
+// its slot) instead of a float atomicAdd into one word: the score is then reduced in a fixed order (dl4j_score_reduce)
+// and is bitwise reproducible run to run.
+DL4J_API int dl4j_fused_update_regpart(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
+                                       void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_part,
+                                       float* gn_partial, hipStream_t stream) {
+  return fused_update_launch(segs, btab, nblocks, p, g, st, shadow, shadow_kind, inv_div, write_update, reg_part,
+                             gn_partial, stream, 1);
+}
+
+static int fused_update_launch(const void* segs, const void* btab, int nblocks, float* p, float* g, float* st,
+                               void* shadow, int shadow_kind, float inv_div, int write_update, float* reg_out,
+                               float* gn_partial, hipStream_t stream, int reg_partials) {
   if (nblocks <= 0) return 0;
   const unsigned* guard = lstm_step_guard_ptr();
   if (gn_partial)
@@ -187,15 +213,15 @@ DL4J_API int dl4j_fused_update(const void* segs, const void* btab, int nblocks, 
   if (shadow_kind == 1)
     hipLaunchKernelGGL(fused_update_kernel<bf16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (bf16*)shadow, inv_div, write_update, reg_out,
-                       (const float*)gn_partial, guard);
+                       (const float*)gn_partial, guard, reg_partials);
   else if (shadow_kind == 2)
     hipLaunchKernelGGL(fused_update_kernel<f16>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (f16*)shadow, inv_div, write_update, reg_out,
-                       (const float*)gn_partial, guard);
+                       (const float*)gn_partial, guard, reg_partials);
   else
     hipLaunchKernelGGL(fused_update_kernel<float>, dim3(nblocks), dim3(256), 0, stream, (const SegDesc*)segs,
                        (const int2*)btab, p, g, st, (float*)nullptr, inv_div, write_update, reg_out,
-                       (const float*)gn_partial, guard);
+                       (const float*)gn_partial, guard, reg_partials);
   return (int)hipGetLastError();
 }
 

@@ -144,6 +144,12 @@ class BaseOutputLayerImpl(LayerImpl):
 
     def computeScore(self, fullNetworkL1=0.0, fullNetworkL2=0.0, training=True):
         s, _ = self._loss_and_grad()
+        if s.is_cuda and s.dtype == torch.float32 and s.is_contiguous() and \
+                not torch.is_tensor(fullNetworkL1) and not torch.is_tensor(fullNetworkL2):
+            from ...ops import native
+            if native.load() is not None:
+                # (sum + l1 + l2) / minibatch in one in-tree block (fixed order)
+                return native.score_reduce(s, float(fullNetworkL1) + float(fullNetworkL2), 1.0 / self._score_mb())
         return (s.sum() + fullNetworkL1 + fullNetworkL2) / self._score_mb()
 
     def computeScoreForExamples(self, fullNetworkL1=0.0, fullNetworkL2=0.0):

@@ -381,7 +381,8 @@ class BaseNetwork:
         self._grads_zeroed = self.flattenedGradients is not None and self.flattenedGradients.is_cuda and \
             self._grad_zero_needed()
         if self._grads_zeroed:
-            self.flattenedGradients.zero_()
+            from ..ops.nd4j_kernels import zero_
+            zero_(self.flattenedGradients)
         acc = getattr(self, "gradientsAccumulator", None)
         if acc is not None and hasattr(acc, "begin_backward"):
             acc.begin_backward(self)
@@ -467,10 +468,19 @@ class BaseNetwork:
             batch_size = acc.global_batch / (getattr(acc, "participants", None) or getattr(acc, "world_size", 1))
         reg = None
         if any(sg.l1 > 0 or sg.l2 > 0 for sg in self.updater.plan.segments):
-            reg = torch.zeros(1, dtype=self.master_dtype, device=self.device)
+            # the HIP updater writes (not accumulates) it; the host path expects zeros
+            reg = torch.empty(1, dtype=self.master_dtype, device=self.device) if self.device.type == "cuda" and \
+                self.master_dtype == torch.float32 else torch.zeros(1, dtype=self.master_dtype, device=self.device)
         self.updater.update(self.flattenedParams, self.flattenedGradients, it, ep, batch_size, self.shadow, reg)
-        if getattr(self, "_loss_part", None) is not None:
-            self._score_t = self._loss_part + (reg[0] / mb_local if reg is not None else 0.0)
+        lp = getattr(self, "_loss_part", None)
+        if lp is not None:
+            from ..ops import native as _native
+            if reg is not None and _native.score_reduce_ok(reg, lp if torch.is_tensor(lp) else None) and \
+                    torch.is_tensor(lp) and lp.numel() == 1:
+                # score = loss + reg / minibatch on one in-tree block (no library elementwise kernels)
+                self._score_t = _native.score_reduce(reg, 0.0, 1.0 / mb_local, reg=lp.reshape(1), reg_scale=1.0)
+            else:
+                self._score_t = lp + (reg[0] / mb_local if reg is not None else 0.0)
             self._loss_part = None
             self._score_val = None
         for _, _, impl, _ in self._layer_offsets:

@@ -602,7 +602,8 @@ def _bwd_data_phases(dy, w, plan, N, H, W, C, K, OH, OW, stride, dx_accum, adt):
     else:
         dx = arena.empty((N, C, H, W), adt, dy.device, channels_last=True)
         if zero_taps or len(plan) < sh * sw:
-            dx.zero_()
+            from .nd4j_kernels import zero_
+            zero_(dx)
     for (i0h, i0w, Rf, Sf, Hf, Wf, u0h, u0w, pth, ptw) in plan:
         if Rf == 0 or Sf == 0:
             continue

@@ -29,17 +29,23 @@ def pack_weights(w):
     key = (w.data_ptr(), str(w.device))
     ent = _packed.get(key)
     if ent is None:
-        k = torch.arange(147, device=w.device)
-        r, rem = k // 21, k % 21                                    # rem = s*3 + c
-        ent = _packed[key] = {"idx": r * 24 + rem, "full": torch.zeros(192, 64, dtype=torch.bfloat16,
-                                                                       device=w.device),
-                              "pk": torch.empty(4, 6, 64, 8, dtype=torch.bfloat16, device=w.device), "v": -1}
+        ent = _packed[key] = {"pk": torch.empty(4, 6, 64, 8, dtype=torch.bfloat16, device=w.device), "v": -1}
     if ent["v"] != WEIGHT_VERSION[0] or not is_managed(w.data_ptr()):
-        src = w.permute(2, 3, 1, 0).reshape(147, 64)               # rows (r, s, c)
-        ent["full"].index_copy_(0, ent["idx"], src)
-        ent["pk"].copy_(ent["full"].view(6, 4, 8, 4, 16).permute(3, 0, 1, 4, 2).reshape(4, 6, 64, 8))
+        lib = native.load()
+        native.register_sig("dl4j_stem_pack_weights", [c_void_p, c_void_p] + [ctypes.c_longlong] * 4 + [c_void_p])
+        rc = lib.dl4j_stem_pack_weights(_ptr(w), _ptr(ent["pk"]), *[int(t) for t in w.stride()], c_void_p(_stream()))
+        native._check(rc, "stem_pack_weights")
         ent["v"] = WEIGHT_VERSION[0]
     return ent["pk"]
+
+
+def pack_weights_reference(w):
+    """The packing as torch ops (tests compare the kernel against it)."""
+    k = torch.arange(147, device=w.device)
+    r, rem = k // 21, k % 21
+    full = torch.zeros(192, 64, dtype=w.dtype, device=w.device)
+    full.index_copy_(0, r * 24 + rem, w.permute(2, 3, 1, 0).reshape(147, 64))
+    return full.view(6, 4, 8, 4, 16).permute(3, 0, 1, 4, 2).reshape(4, 6, 64, 8).contiguous()
 
 
 def forward(x, w, want_stats=False):

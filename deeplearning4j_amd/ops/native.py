@@ -289,13 +289,46 @@ def fused_update(plan, params, grad, state, iteration, epoch, div, shadow, write
         if gn_part is None or gn_part.numel() < cache.nblocks or gn_part.device != params.device:
             gn_part = cache.gn_partial = torch.empty(max(cache.nblocks, 1), dtype=torch.float32,
                                                      device=params.device)
-    rc = lib.dl4j_fused_update(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
-                               _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, _ptr(reg_out),
-                               _ptr(gn_part), _stream())
-    _check(rc, "fused_update")
+    reg_part = None
+    if reg_out is not None:
+        # per-block regularisation partials, summed in a fixed order below: a reproducible score (no float atomics)
+        reg_part = getattr(cache, "reg_partial", None)
+        if reg_part is None or reg_part.numel() < cache.nblocks or reg_part.device != params.device:
+            reg_part = cache.reg_partial = torch.empty(max(cache.nblocks, 1), dtype=torch.float32,
+                                                       device=params.device)
+        register_sig("dl4j_fused_update_regpart", [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                   c_int, c_float, c_int, c_void_p, c_void_p, c_void_p])
+        rc = lib.dl4j_fused_update_regpart(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
+                                           _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0,
+                                           _ptr(reg_part), _ptr(gn_part), _stream())
+        _check(rc, "fused_update")
+        score_reduce(reg_part[:cache.nblocks], 0.0, 1.0, out=reg_out.reshape(-1)[:1])
+    else:
+        rc = lib.dl4j_fused_update(_ptr(st.dev), _ptr(cache.btab), cache.nblocks, _ptr(params), _ptr(grad),
+                                   _ptr(state), _ptr(shadow), sk, 1.0 / div, 1 if write_update else 0, None,
+                                   _ptr(gn_part), _stream())
+        _check(rc, "fused_update")
     from . import rnn_native
     rnn_native.check_step_guard(params.device)     # a timed-out cooperative LSTM launch skips the update: report it
     return True
+
+
+def score_reduce(s, add, scale, reg=None, reg_scale=0.0, out=None):
+    """out[0] = (sum(s) + add) * scale + reg[0] * reg_scale on one HIP block (fixed order; csrc/softmax_xent.hip).
+    s: contiguous fp32 CUDA tensor; returns ``out`` (a fresh 0-d tensor when not given)."""
+    lib = load()
+    register_sig("dl4j_score_reduce", [c_void_p, c_ll, c_float, c_float, c_void_p, c_float, c_void_p, c_void_p])
+    if out is None:
+        out = torch.empty((), dtype=torch.float32, device=s.device)
+    rc = lib.dl4j_score_reduce(_ptr(s), s.numel(), float(add), float(scale), _ptr(reg), float(reg_scale), _ptr(out),
+                               _stream())
+    _check(rc, "score_reduce")
+    return out
+
+
+def score_reduce_ok(*ts):
+    return all(t is None or (torch.is_tensor(t) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous())
+               for t in ts) and load() is not None
 
 
 # ------------------------------------------------------------------------------------------ batch norm

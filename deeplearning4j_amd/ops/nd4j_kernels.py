@@ -31,6 +31,7 @@ native.register_sig("dl4j_strided_copy2", [c_int, c_int, c_void_p, c_void_p, c_i
 native.register_sig("dl4j_col2im", [c_int, c_void_p, c_void_p] + [c_int] * 12 + [c_void_p])
 native.register_sig("dl4j_mergemax", [c_int, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_void_p])
 native.register_sig("dl4j_mergemax_bp", [c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p])
+native.register_sig("dl4j_fill", [c_void_p, c_ll, ctypes.c_uint, c_void_p])
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 CALLS = __import__("collections").Counter()     # kernel launches per entry point (tests check the GPU path ran)
@@ -406,3 +407,24 @@ def col2im(cols, N, C, Hp, Wp, R, S, stride, dilation, OH, OW):
     _check(native.load().dl4j_col2im(DT[cols.dtype], _ptr(cols), _ptr(x), N, C, Hp, Wp, R, S, stride[0], stride[1],
                                      dilation[0], dilation[1], OH, OW, _stream()), "col2im")
     return x
+
+
+def fill_(t, value=0.0):
+    """In-place fill of a contiguous (any memory format, dense storage) CUDA tensor with the in-tree fill kernel;
+    torch's fill elsewhere (CPU tensors, non-dense views). Returns t."""
+    import struct
+    if not (t.is_cuda and t.numel() and t.dtype in DT and enabled() and
+            (t.is_contiguous() or t.is_contiguous(memory_format=torch.channels_last))):
+        return t.fill_(value)
+    if t.dtype == torch.float32:
+        pat = struct.unpack("<I", struct.pack("<f", float(value)))[0]
+    else:
+        h = torch.tensor([float(value)], dtype=t.dtype).view(torch.int16).item() & 0xFFFF
+        pat = h | (h << 16)
+    native._check(native.load().dl4j_fill(_ptr(t), t.numel() * t.element_size(), pat, _stream()), "fill")
+    CALLS["fill"] += 1
+    return t
+
+
+def zero_(t):
+    return fill_(t, 0.0)

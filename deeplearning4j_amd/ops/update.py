@@ -80,7 +80,7 @@ class UpdatePlan:
 def fused_update(plan, params, grad, state, iteration, epoch, batch_size, mini_batch=True, shadow=None,
                  write_update=True, reg_out=None):
     """params/grad/state: flat 1-D fp32 (or fp64) tensors. shadow: optional bf16 flat copy of params.
-    reg_out: optional zeroed 1-element tensor that receives sum(l1*|p| + 0.5*l2*p^2) of the pre-update
+    reg_out: optional 1-element tensor overwritten with sum(l1*|p| + 0.5*l2*p^2) of the pre-update
     params (the score's regularisation term) — computed inside the same kernel pass on GPU."""
     div = float(batch_size) if mini_batch else 1.0
     custom = [b[3] for b in plan.blocks if not b[3].kernel_supported()]
