@@ -384,18 +384,30 @@ __device__ __forceinline__ void lean_stats(const GemmArgs& g, const char* T, int
       for (int j = 0; j < 4; ++j) sh[j] = val(j < 2 ? y0.x : y0.y, j);
       const int r0 = 16 * q;
       const int rn = rows - r0 < 16 ? (rows - r0 > 0 ? rows - r0 : 0) : 16;
-      uint2 v[16];
+      if (rn == 16) {
+        // whole 16-row quarter: 16 independent LDS reads, statically indexed (the earlier loop with a data-dependent
+        // break put this array in scratch memory, whose loads then drained every outstanding store with vmcnt(0))
+        uint2 v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        v[r] = *reinterpret_cast<const uint2*>(T + lean_off<BN>(part * 64 + r0 + r, col));
+        for (int r = 0; r < 16; ++r)
+          v[r] = *reinterpret_cast<const uint2*>(T + lean_off<BN>(part * 64 + r0 + r, col));
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (r >= rn) break;
+        for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = val(j < 2 ? v[r].x : v[r].y, j) - sh[j];
-          s1[j] += d;
-          s2[j] = fmaf(d, d, s2[j]);
+          for (int j = 0; j < 4; ++j) {
+            const float d = val(j < 2 ? v[r].x : v[r].y, j) - sh[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+      } else {
+        for (int r = 0; r < rn; ++r) {
+          const uint2 w = *reinterpret_cast<const uint2*>(T + lean_off<BN>(part * 64 + r0 + r, col));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = val(j < 2 ? w.x : w.y, j) - sh[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
         }
       }
     }

@@ -371,10 +371,19 @@ def _stats_buf(variant, M, K, device):
     return torch.empty((3, P, K), dtype=torch.float32, device=device)
 
 
+STREAM_VAR = 100     # persistent loader/consumer conv kernel (csrc/gemm_stream.hip conv_stream), a tuner candidate
+
+
 def _fwd_launch(variant, x, wk, bias, y, geom, beta, ts):
     """One conv launch on the chosen kernel. Returns 1 when BN tile statistics were written to ts, 0 when not, a
     negative code / HIP error otherwise."""
     lib = native.load()
+    if variant == STREAM_VAR:
+        native.register_sig("dl4j_conv_stream", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 +
+                            [ctypes.c_float, c_void_p, c_void_p])
+        rc = lib.dl4j_conv_stream(_dtc(x), _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts),
+                                  _stream())
+        return 1 if (rc == 0 and ts is not None) else rc
     if variant >= 0:
         rc = lib.dl4j_conv_fwd_v3(_dtc(x), _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts),
                                   variant, _stream())
@@ -404,7 +413,8 @@ def _v3_pick(key, launch, out, make_ts, allow_r2=True):
         return lib.dl4j_conv_v3_default_variant(M, K)
     # allow_r2=False: the round-2 kernel lacks an epilogue the caller needs (BN-backward sums), so its lower kernel
     # time would not be the lower step time
-    cands = list(range(lib.dl4j_conv_v3_num_variants())) + ([-1] if out.dtype == torch.bfloat16 and allow_r2 else [])
+    cands = list(range(lib.dl4j_conv_v3_num_variants())) + [STREAM_VAR] + \
+        ([-1] if out.dtype == torch.bfloat16 and allow_r2 else [])
     scratch = torch.empty_like(out)
     if key[0] == "bwd_acc":
         scratch.copy_(out)

@@ -11,6 +11,7 @@ timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thre
 tail -1 gpurun_out/r6b_gemm_tests.log
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_res_bn_fusion.py > gpurun_out/r6b_rbn_tests.log 2>&1 || { tail -30 gpurun_out/r6b_rbn_tests.log; exit 1; }
 tail -1 gpurun_out/r6b_rbn_tests.log
+timeout -k 10 300 python3 -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_gpu_step_kernels.py > gpurun_out/r6b_step_kernels.log 2>&1; echo "step-kernels rc=$?"; grep -E "torch:|kernels,|passed|failed" gpurun_out/r6b_step_kernels.log | head -30
 DL4J_AMD_TUNE_DB_SKIP=gemm DL4J_AMD_TUNE_RECORD=$R/gpurun_out/r6b_tune_zoo.json DL4J_AMD_TUNE_REPS=6 timeout -k 10 300 python3 -u bench.py > gpurun_out/r6b_bench_retune.log 2>&1 || { tail -20 gpurun_out/r6b_bench_retune.log; exit 1; }
 tail -1 gpurun_out/r6b_bench_retune.log | cut -c1-200
 timeout -k 10 300 python3 -u bench.py > gpurun_out/r6b_bench_db.log 2>&1 || { tail -20 gpurun_out/r6b_bench_db.log; exit 1; }

@@ -81,3 +81,43 @@ def test_refuses_outside_contract():
             gemm.mmul(a, w.t(), out_dtype=torch.bfloat16)
     finally:
         gemm._FORCE_CFG = old
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, C, K, R, S, stride, pad
+    (16, 28, 28, 64, 64, 3, 3, 1, 1),
+    (32, 14, 14, 128, 128, 3, 3, 1, 1),
+    (8, 28, 28, 64, 256, 1, 1, 1, 0),
+    (128, 14, 14, 256, 128, 3, 3, 2, 1),     # strided, ragged taps at the border
+    (128, 7, 7, 512, 512, 3, 3, 1, 1),
+])
+@pytest.mark.parametrize("stats", [False, True])
+def test_conv_stream(case, stats):
+    """Persistent implicit-GEMM conv (conv_stream, conv variant 100) vs fp32 torch conv2d, with bias and the BN
+    tile-statistics epilogue."""
+    from deeplearning4j_amd.ops import conv_native
+    N, H, W, C, K, R, S, st, pd = case
+    torch.manual_seed(11)
+    x = (torch.randn(N, C, H, W, device=DEV) * 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, S, device=DEV) * 0.1).to(torch.bfloat16)
+    b = torch.randn(K, device=DEV)
+    OH, OW = (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1
+    M = N * OH * OW
+    if M % 128:
+        pytest.skip("conv_stream needs N*OH*OW % 128 == 0")
+    wk = w.permute(0, 2, 3, 1).contiguous()                       # [K][R][S][C]
+    y = torch.empty(N, K, OH, OW, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ts = torch.full((3, M // 64, K), float("nan"), device=DEV) if stats else None
+    geom = (N, H, W, C, K, R, S, st, st, pd, pd, 1, 1, OH, OW)
+    rc = conv_native._fwd_launch(conv_native.STREAM_VAR, x, wk, b, y, geom, 0.0, ts)
+    assert rc == (1 if stats else 0), rc
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), b, stride=st, padding=pd)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 3e-2 * max(1.0, ref.abs().max().item() / 4) * (R * S * C / 64) ** 0.5 / 3, err
+    if stats:
+        yr = y.permute(0, 2, 3, 1).reshape(M, K).float().reshape(M // 64, 64, K)
+        sh = yr[:, 0]
+        assert torch.equal(ts[2], sh)
+        d = yr - sh[:, None]
+        assert torch.allclose(ts[0], d.sum(1), atol=2e-2, rtol=1e-4)

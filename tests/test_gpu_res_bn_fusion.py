@@ -17,7 +17,7 @@ def _net(fuse, monkeypatch):
     monkeypatch.setenv("DL4J_AMD_FUSE_RES_BN", "1" if fuse else "0")
     torch.manual_seed(3)
     return ResNet50(numLabels=100, dataType=DataType.BFLOAT16, updater=Sgd(0.01), weightInit=WeightInit.RELU,
-                    inputShape=[3, 96, 96]).init(torch.device("cuda", 0))
+                    inputShape=[3, 224, 224]).init(torch.device("cuda", 0))
 
 
 def test_shortcut_bn_folding_matches_unfused(monkeypatch):
@@ -28,9 +28,9 @@ def test_shortcut_bn_folding_matches_unfused(monkeypatch):
     assert len(deferred) == 4, deferred
     assert not any(getattr(l, "defer_apply", False) for l in plain.layers_by_name.values())
     g = torch.Generator(device="cpu").manual_seed(5)
-    x = torch.rand(64, 3, 96, 96, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y = torch.zeros(64, 100, device="cuda")
-    y[torch.arange(64), torch.randint(0, 100, (64,), generator=g).cuda()] = 1.0
+    x = torch.rand(16, 3, 224, 224, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.zeros(16, 100, device="cuda")
+    y[torch.arange(16), torch.randint(0, 100, (16,), generator=g).cuda()] = 1.0
     p0 = fused.params().detach().clone()
     fused.fit([x], [y])
     ran = [n for n in deferred if fused.layers_by_name[n]._ctx[0] == "NATIVE_STATS"]

@@ -46,11 +46,11 @@ def test_fill_kernel():
 def test_resnet50_step_launches_no_torch_compute_kernels():
     from deeplearning4j_amd.models import ResNet50
     from deeplearning4j_amd.nn.conf import DataType
-    net = ResNet50(numLabels=100, dataType=DataType.BFLOAT16, inputShape=[3, 96, 96]).init(torch.device("cuda", 0))
+    net = ResNet50(numLabels=100, dataType=DataType.BFLOAT16, inputShape=[3, 224, 224]).init(torch.device("cuda", 0))
     g = torch.Generator(device="cpu").manual_seed(1)
-    x = torch.rand(32, 3, 96, 96, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y = torch.zeros(32, 100, device="cuda")
-    y[torch.arange(32), torch.randint(0, 100, (32,), generator=g).cuda()] = 1.0
+    x = torch.rand(16, 3, 224, 224, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.zeros(16, 100, device="cuda")
+    y[torch.arange(16), torch.randint(0, 100, (16,), generator=g).cuda()] = 1.0
     ks = _step_kernels(net, x, y)
     assert len(ks) > 100
     torch_ks = sorted({n for n, _ in ks if _is_torch_kernel(n)})
