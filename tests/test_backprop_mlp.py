@@ -10,8 +10,9 @@ import pytest
 import torch
 
 import deeplearning4j_amd as D
+from _ref_fixtures import path as _ref_path
 
-IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+IRIS = _ref_path("deeplearning4j-core/src/main/resources/iris.dat")
 pytestmark = pytest.mark.skipif(not os.path.exists(IRIS), reason="reference iris.dat not present")
 
 

@@ -12,8 +12,9 @@ import torch
 
 import deeplearning4j_amd as D
 from deeplearning4j_amd.exceptions import DL4JException
+from _ref_fixtures import path as _ref_path
 
-IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+IRIS = _ref_path("deeplearning4j-core/src/main/resources/iris.dat")
 
 
 def test_set_outputs_multiple_calls_replace():

@@ -8,8 +8,9 @@ import pytest
 
 from deeplearning4j_amd.nlp import chinese as Z
 from deeplearning4j_amd.nlp.tokenization_ext import ChineseTokenizerFactory
+from _ref_fixtures import path as _ref_path
 
-CORE = ("/root/reference/deeplearning4j-nlp-parent/deeplearning4j-nlp-chinese/src/main/resources/core.dic")
+CORE = _ref_path("deeplearning4j-nlp-parent/deeplearning4j-nlp-chinese/src/main/resources/core.dic")
 need_core = pytest.mark.skipif(not os.path.exists(CORE), reason="reference core.dic not present")
 
 

@@ -3,24 +3,17 @@
 stride-2 sigmoid convolution with all weights 0.5 and biases 1 over the fixed [1, 1, 8, 8] input gives the expected
 [1, 2, 4, 4] activations (arrays read from the reference test's source); the bias initialises from biasInit; a kernel
 larger than the input, a zero stride and a zero kernel size are rejected at build time. fp64, CPU."""
-import os
-import re
 
 import pytest
 import torch
 
 import deeplearning4j_amd as D
 
-SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/"
-       "ConvolutionLayerTest.java")
+from _ref_fixtures import java_arrays
 
 
 def _array(after):
-    text = open(SRC).read()
-    text = text[text.index(after):]
-    m = re.search(r"Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}\)", text)
-    vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
-    return torch.tensor(vals, dtype=torch.float64).reshape([int(v) for v in m.group(2).split(",")])
+    return java_arrays("ConvolutionLayerTest", after)[0]
 
 
 def _conv_net(n_in, n_out, k, s, p, bias_init=None, act=D.Activation.SIGMOID):
@@ -34,7 +27,6 @@ def _conv_net(n_in, n_out, k, s, p, bias_init=None, act=D.Activation.SIGMOID):
     return net
 
 
-@pytest.mark.skipif(not os.path.exists(SRC), reason="reference ConvolutionLayerTest.java not present")
 def test_activate_results_contained():
     net = _conv_net(1, 2, [2, 2], [2, 2], [0, 0])
     layer = net.getLayer(0)

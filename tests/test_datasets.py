@@ -15,8 +15,9 @@ from deeplearning4j_amd.datasets.datavec import (AlignmentMode, CollectionRecord
 from deeplearning4j_amd.datasets.fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator,
                                                   LFWDataSetIterator, MnistDataSetIterator, UciSequenceDataSetIterator,
                                                   write_idx)
+from _ref_fixtures import path as _ref_path
 
-IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+IRIS = _ref_path("deeplearning4j-core/src/main/resources/iris.dat")
 
 
 def test_mnist_idx(tmp_path):

@@ -11,8 +11,9 @@ import torch
 
 import deeplearning4j_amd as D
 from deeplearning4j_amd.eval import EvaluationTools
+from _ref_fixtures import path as _ref_path
 
-IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+IRIS = _ref_path("deeplearning4j-core/src/main/resources/iris.dat")
 
 
 def _iris_net(n_out):

@@ -9,8 +9,9 @@ import pytest
 
 from deeplearning4j_amd.nlp import kuromoji as K
 from deeplearning4j_amd.nlp.tokenization_ext import JapaneseTokenizerFactory
+from _ref_fixtures import path as _ref_path
 
-RES = "/root/reference/deeplearning4j-nlp-parent/deeplearning4j-nlp-japanese/src/test/resources"
+RES = _ref_path("deeplearning4j-nlp-parent/deeplearning4j-nlp-japanese/src/test/resources")
 need_res = pytest.mark.skipif(not os.path.isdir(RES), reason="reference Kuromoji test resources not present")
 
 

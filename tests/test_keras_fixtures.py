@@ -19,8 +19,9 @@ from deeplearning4j_amd.modelimport import hdf5
 from deeplearning4j_amd.modelimport.keras import KerasLayer, KerasModelImport, space_to_depth_mapper
 from deeplearning4j_amd.nn.conf.inputs import (InputTypeConvolutional, InputTypeConvolutionalFlat,
                                                InputTypeFeedForward, InputTypeRecurrent)
+from _ref_fixtures import path as _ref_path
 
-R = "/root/reference/deeplearning4j-modelimport/src/test/resources/"
+R = _ref_path("deeplearning4j-modelimport/src/test/resources") + "/"
 pytestmark = pytest.mark.skipif(not os.path.isdir(R), reason="reference fixtures not present")
 CPU = torch.device("cpu")
 CONFIGS = sorted(glob.glob(R + "configs/keras1/*.json") + glob.glob(R + "configs/keras2/*.json"))

@@ -16,8 +16,9 @@ import torch
 from deeplearning4j_amd.modelimport import hdf5
 from deeplearning4j_amd.modelimport.keras import (KerasLayer, KerasModelImport, UnsupportedKerasConfigurationException,
                                                    space_to_depth_mapper)
+from _ref_fixtures import path as _ref_path
 
-R = "/root/reference/deeplearning4j-modelimport/src/test/resources/weights/"
+R = _ref_path("deeplearning4j-modelimport/src/test/resources/weights") + "/"
 pytestmark = pytest.mark.skipif(not os.path.isdir(R), reason="reference fixtures not present")
 CPU = torch.device("cpu")
 

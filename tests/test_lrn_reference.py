@@ -3,24 +3,17 @@
 input, expected activations, epsilon and expected input-epsilon arrays ([2, 7, 3, 2], k=2, n=5, alpha=1e-4,
 beta=0.75) are read from the reference test's own source text; plus the hand-computed cross-channel formula
 (testLrnManual) with the default k=2, n=5 window and an LRN inside a small CNN that fits. fp64, CPU."""
-import os
-import re
 
 import pytest
 import torch
 
 import deeplearning4j_amd as D
 
-SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/normalization/"
-       "LocalResponseTest.java")
+from _ref_fixtures import java_named
 
 
 def _fixture(name):
-    text = open(SRC).read()
-    m = re.search(name + r"\s*=\s*Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}", text)
-    vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
-    shape = [int(v) for v in m.group(2).split(",")]
-    return torch.tensor(vals, dtype=torch.float64).reshape(shape)
+    return java_named("LocalResponseTest", name)
 
 
 def _layer(**kw):
@@ -34,7 +27,6 @@ def _layer(**kw):
     return net.getLayer(0)
 
 
-@pytest.mark.skipif(not os.path.exists(SRC), reason="reference LocalResponseTest.java not present")
 def test_lrn_matches_reference_fixture():
     x = _fixture("x")
     layer = _layer(k=2, n=5, alpha=1e-4, beta=0.75)

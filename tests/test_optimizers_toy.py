@@ -17,6 +17,7 @@ import torch
 
 from deeplearning4j_amd.optimize.solvers import (ConjugateGradient, LBFGS, LineGradientDescent,
                                                  NegativeDefaultStepFunction, StochasticGradientDescent)
+from _ref_fixtures import path as _ref_path
 
 ALGOS = {"sgd": StochasticGradientDescent, "line": LineGradientDescent, "cg": ConjugateGradient, "lbfgs": LBFGS}
 
@@ -199,7 +200,7 @@ def test_rosenbrock_gradient_is_exact():
     assert torch.allclose(Rastrigin(x2.detach()).grad(x2.detach()), x2.grad)
 
 
-IRIS = "/root/reference/deeplearning4j-core/src/main/resources/iris.dat"
+IRIS = _ref_path("deeplearning4j-core/src/main/resources/iris.dat")
 
 
 @pytest.mark.skipif(not os.path.exists(IRIS), reason="reference iris.dat not present")

@@ -2,29 +2,18 @@
 (deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/SubsamplingLayerTest.java:48-180): 2x2
 MAX and AVG pooling (stride 2) of the fixed [1, 2, 4, 4] input give the expected [1, 2, 2, 2] outputs, and their
 backward passes route / spread the given epsilons to the expected [1, 2, 4, 4] input gradients; no "W" gradient; a
-kernel larger than the input is rejected. The arrays are read from the reference test's source text. fp64, CPU."""
-import os
-import re
-
+kernel larger than the input is rejected. The arrays are the reference test's literals, vendored as JSON (tests/fixtures/java). fp64, CPU."""
 import pytest
 import torch
 
 import deeplearning4j_amd as D
 
-SRC = ("/root/reference/deeplearning4j-core/src/test/java/org/deeplearning4j/nn/layers/convolution/"
-       "SubsamplingLayerTest.java")
-pytestmark = pytest.mark.skipif(not os.path.exists(SRC), reason="reference SubsamplingLayerTest.java not present")
+from _ref_fixtures import java_arrays
 
 
 def _arrays(after):
-    """Every Nd4j.create(new double[]{...}, new int[]{...}) literal after the first occurrence of ``after``."""
-    text = open(SRC).read()
-    text = text[text.index(after):]
-    out = []
-    for m in re.finditer(r"Nd4j\.create\(new double\[\]\s*\{([^}]*)\}\s*,\s*new int\[\]\s*\{([^}]*)\}\)", text):
-        vals = [float(v) for v in m.group(1).replace("\n", " ").split(",")]
-        out.append(torch.tensor(vals, dtype=torch.float64).reshape([int(v) for v in m.group(2).split(",")]))
-    return out
+    """Every Nd4j.create(new double[]{...}, new int[]{...}) literal after the declaration ``after``."""
+    return java_arrays("SubsamplingLayerTest", after)
 
 
 def _contained():
