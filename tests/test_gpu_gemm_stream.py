@@ -114,7 +114,8 @@ def test_conv_stream(case, stats):
     torch.cuda.synchronize()
     ref = torch.nn.functional.conv2d(x.float(), w.float(), b, stride=st, padding=pd)
     err = (y.float() - ref).abs().max().item()
-    assert err <= 3e-2 * max(1.0, ref.abs().max().item() / 4) * (R * S * C / 64) ** 0.5 / 3, err
+    # bf16 output rounding (2^-8 relative) + accumulation of bf16 products over R*S*C terms
+    assert err <= 8e-3 * ref.abs().max().item() + 1e-2 * (R * S * C / 64) ** 0.5, err
     if stats:
         yr = y.permute(0, 2, 3, 1).reshape(M, K).float().reshape(M // 64, 64, K)
         sh = yr[:, 0]
