@@ -188,3 +188,30 @@ def to_weight_init(w):
     if w is None or isinstance(w, WeightInit):
         return w
     return WeightInit[str(w).upper()]
+
+
+class WeightInitUtil:
+    """Reference nn/weights/WeightInitUtil.java: ``initWeights(fanIn, fanOut, shape, WeightInit, Distribution,
+    params[, order])`` fills the given array (a view, e.g. into the flat parameter vector) in place and returns it
+    reshaped to ``shape``. The random stream is the framework's generator (``Nd4j.getRandom()`` seeds it), so the same
+    seed gives the same weights as an explicit sample of the scheme's distribution with that seed."""
+
+    DEFAULT_WEIGHT_INIT_ORDER = "f"
+
+    @staticmethod
+    def initWeights(fanIn, fanOut, shape, initScheme, dist, params, order="f"):
+        shape = [int(v) for v in shape]
+        if params.numel() != int(math.prod(shape)):
+            raise ValueError(f"params length {params.numel()} does not match shape {shape}")
+        gen = _default_generator()
+        flat = params.reshape(-1)
+        init_weights_(flat, fanIn, fanOut, shape, initScheme, dist, gen)
+        if order == "f":
+            return flat.reshape(list(reversed(shape))).permute(*reversed(range(len(shape))))
+        return flat.reshape(shape)
+
+
+def _default_generator():
+    """The ND4J facade's process-wide generator (``Nd4j.getRandom().setSeed`` seeds it)."""
+    from ...nd4j.factory import _Random
+    return _Random.gen()
