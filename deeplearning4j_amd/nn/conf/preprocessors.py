@@ -10,6 +10,18 @@ from .inputs import InputType, InputTypeConvolutional, InputTypeFeedForward, Inp
 
 
 class InputPreProcessor(Config):
+    def __init__(self, *args, **kw):
+        # the reference's positional constructors, e.g. CnnToFeedForwardPreProcessor(inputHeight, inputWidth,
+        # numChannels): positional arguments fill the fields in declaration order
+        names = tuple(type(self)._all_fields())
+        if len(args) > len(names):
+            raise TypeError(f"{type(self).__name__} takes at most {len(names)} positional arguments")
+        for n, a in zip(names, args):
+            if n in kw:
+                raise TypeError(f"{type(self).__name__}: {n} given twice")
+            kw[n] = a
+        super().__init__(**kw)
+
     def preProcess(self, x, miniBatchSize, training=False):
         raise NotImplementedError
 

@@ -58,7 +58,7 @@ def main():
               f"  {best}", flush=True)
         del x, y, ts
         torch.cuda.empty_cache()
-    print("count-weighted us: best of round-3 variants %.1f, best incl. conv_stream %.1f" %
+    print("count-weighted ns: best of round-3 variants %.1f, best incl. conv_stream %.1f" %
           (tot["best_old"], tot["best_all"]))
 
 
