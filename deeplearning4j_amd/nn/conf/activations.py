@@ -42,6 +42,13 @@ class IActivation(Config):
     def __call__(self, x, training=False):
         return self.getActivation(x, training)
 
+    def __str__(self):
+        """The ND4J toString form: the lower-case activation name, with parameters when it has any
+        (``sigmoid``, ``hardsigmoid``, ``leakyrelu(alpha=0.01)``)."""
+        name = next((e.value.lower() for e, c in _ACT_MAP.items() if c is type(self)), type(self).__name__)
+        f = self._all_fields()
+        return name + ("(" + ", ".join(f"{k}={getattr(self, k)}" for k in f) + ")" if f else "")
+
 
 class ActivationIdentity(IActivation):
     def getActivation(self, x, training=False):

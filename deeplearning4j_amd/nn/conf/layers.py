@@ -152,6 +152,12 @@ class Layer(Config):
     def getLayerName(self):
         return self.layerName
 
+    def __call__(self):
+        """``layer.conf()`` as in the reference (a runtime layer's conf() is its per-layer NeuralNetConfiguration,
+        whose getLayer() is this config): runtime layers keep the config itself in ``.conf``."""
+        from .network import LayerConfiguration
+        return LayerConfiguration(self)
+
     def getActivationFn(self):
         """The layer's activation function object (inherited from the global config when not set on the layer)."""
         return getattr(self, "activation", None)

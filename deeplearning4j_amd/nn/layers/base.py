@@ -49,6 +49,17 @@ class LayerImpl:
         for k, v in table.items():
             self.setParam(k, v)
 
+    def update(self, gradient, paramType=None):
+        """Add a gradient (an already-computed update) to the parameters, reference BaseLayer.update(Gradient) /
+        update(INDArray, String) (nn/layers/BaseLayer.java:167-176: ``param.addi(gradient)``)."""
+        if paramType is None:
+            for k, g in gradient.gradientForVariable().items():
+                self.update(g, k)
+            return
+        with torch.no_grad():
+            p = self.params[paramType]
+            self.setParam(paramType, p + gradient.reshape(p.shape).to(p.dtype))
+
     def W(self, key="W"):
         """Compute-dtype view of parameter ``key`` (with weight noise / DropConnect applied when training)."""
         p = self.cparams.get(key, self.params.get(key))
