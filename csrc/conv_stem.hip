@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256) void stem_pack_weights(const u16* __restrict__
   const int row = j * 32 + (m >> 4) * 8 + n, k = i * 16 + (m & 15);
   const int r = row / 24, rem = row - r * 24;
   u16 v = 0;
-  if (rem < 21) {
+  if (r < 7 && rem < 21) {                     // rows 168..191 (r == 7) are padding too
     const int s_ = rem / 3, c = rem - s_ * 3;
     v = w[k * sk + c * sc + r * sr + s_ * ss];
   }

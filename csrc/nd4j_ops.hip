@@ -740,3 +740,23 @@ DL4J_API int dl4j_fill(void* out, long long nbytes, unsigned pattern, hipStream_
                      nbytes, pattern);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------ axpy
+// y[i] += alpha * x[i] for an fp32 y and an x of dtype dt: the running-mean correction of a BatchNormalization whose
+// producing convolution deferred its bias (the bias cancels in the batch statistics; the running mean must still
+// track E[conv + bias]). A handful of channels per call: one grid-stride pass.
+template <typename T>
+__global__ __launch_bounds__(256) void axpy_kernel(const T* __restrict__ x, float* __restrict__ y, long long n,
+                                                   float alpha) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] += alpha * ldf(x, i);
+}
+
+DL4J_API int dl4j_axpy(int dt, const void* x, float* y, long long n, float alpha, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int g = grid1(n);
+#define L(T) hipLaunchKernelGGL((axpy_kernel<T>), dim3(g), dim3(256), 0, s, (const T*)x, y, n, alpha)
+  DT_DISPATCH(dt, L);
+#undef L
+  return (int)hipGetLastError();
+}

@@ -82,9 +82,9 @@ class BatchNormalizationImpl(LayerImpl):
         if training and db is not None:
             # the producing conv skipped its bias (it cancels in the batch statistics): the running mean must
             # still track E[conv + bias]
+            from ...ops.nd4j_kernels import axpy_
             with torch.no_grad():
-                rm = self.params["mean"]
-                rm.add_(db.params["b"].reshape(rm.shape).to(rm.dtype), alpha=1.0 - c.decay)
+                axpy_(self.params["mean"], db.params["b"], 1.0 - c.decay)
 
     def backpropGradient(self, eps):
         gg, gb = self.grads.get("gamma"), self.grads.get("beta")

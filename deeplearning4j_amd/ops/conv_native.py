@@ -19,7 +19,7 @@ import torch
 
 from ..memory import arena
 
-from . import native, side_stream, tunedb
+from . import native, nd4j_kernels, side_stream, tunedb
 from .native import _ptr, _stream, c_int, c_ll, c_void_p
 
 native.register_sig("dl4j_conv_w_relayout", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
@@ -516,8 +516,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             if acc:
                 dx = dx_accum                                # only the strided rows are touched (+=)
             else:
-                dx = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
-                                 memory_format=torch.channels_last).zero_()
+                dx = nd4j_kernels.zero_(torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device,
+                                                    memory_format=torch.channels_last))
             rc = lib.dl4j_conv_bwd_data_1x1(_ptr(dy), _ptr(flip), _ptr(dx), N, H, W, C, K, stride[0], OH, OW,
                                             int(acc), _stream())
             native._check(rc, "conv_bwd_data_1x1")
@@ -532,8 +532,8 @@ def _conv2d_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db, gW=
             sh, sw = stride
             eh = H - ((OH - 1) * sh + R - pad4[0] - pad4[1])
             ew = W - ((OW - 1) * sw + S - pad4[2] - pad4[3])
-            dyz = torch.empty((N, K, (OH - 1) * sh + 1 + eh, (OW - 1) * sw + 1 + ew), dtype=adt,
-                              device=x.device, memory_format=torch.channels_last).zero_()
+            dyz = nd4j_kernels.zero_(torch.empty((N, K, (OH - 1) * sh + 1 + eh, (OW - 1) * sw + 1 + ew), dtype=adt,
+                                                 device=x.device, memory_format=torch.channels_last))
             dyz[:, :, :(OH - 1) * sh + 1:sh, :(OW - 1) * sw + 1:sw] = dy
             dx = _conv2d_bwd(x, w, dyz, (1, 1), pad4, dilation, True, False, False, dx_accum=dx_accum)[0]
         else:
@@ -791,7 +791,7 @@ def _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, n
     if R == 1 and S == 1:
         ws = dWt
         if not (direct and grads_zeroed):
-            ws.zero_()
+            nd4j_kernels.zero_(ws)
     else:
         ws = _zeroed_wrw_ws(K, R, S, C, x.device)
     dbt = None
@@ -799,7 +799,7 @@ def _conv2d_wrw_r2(x, dy, N, H, W, C, K, R, S, OH, OW, stride, pad4, dilation, n
         directb = gb is not None and gb.dtype == torch.float32 and gb.is_contiguous()
         dbt = gb.reshape(-1) if directb else torch.empty(K, dtype=torch.float32, device=x.device)
         if not (directb and grads_zeroed):
-            dbt.zero_()
+            nd4j_kernels.zero_(dbt)
     splits = _wrw_splits(lib, x, dy, ws, dbt, N, H, W, C, K, R, S, stride, pad4, dilation, OH, OW)
     rc = lib.dl4j_conv_wrw(_ptr(x), _ptr(dy), _ptr(ws), _ptr(dbt), N, H, W, C, K, R, S, stride[0], stride[1],
                            pad4[0], pad4[2], dilation[0], dilation[1], OH, OW, splits, _stream())
@@ -892,8 +892,8 @@ def _pad_ch(t, n, dim=1, cl=False):
         return t
     shp = list(t.shape)
     shp[dim] = n
-    out = torch.empty(shp, dtype=t.dtype, device=t.device,
-                      memory_format=torch.channels_last if cl else torch.contiguous_format).zero_()
+    out = nd4j_kernels.zero_(torch.empty(shp, dtype=t.dtype, device=t.device,
+                                         memory_format=torch.channels_last if cl else torch.contiguous_format))
     out.narrow(dim, 0, t.shape[dim]).copy_(t)
     return out
 

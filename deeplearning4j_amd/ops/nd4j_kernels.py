@@ -32,6 +32,7 @@ native.register_sig("dl4j_col2im", [c_int, c_void_p, c_void_p] + [c_int] * 12 + 
 native.register_sig("dl4j_mergemax", [c_int, c_void_p, c_int, c_void_p, c_void_p, c_ll, c_void_p])
 native.register_sig("dl4j_mergemax_bp", [c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p])
 native.register_sig("dl4j_fill", [c_void_p, c_ll, ctypes.c_uint, c_void_p])
+native.register_sig("dl4j_axpy", [c_int, c_void_p, c_void_p, c_ll, ctypes.c_float, c_void_p])
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 CALLS = __import__("collections").Counter()     # kernel launches per entry point (tests check the GPU path ran)
@@ -428,3 +429,14 @@ def fill_(t, value=0.0):
 
 def zero_(t):
     return fill_(t, 0.0)
+
+
+def axpy_(y, x, alpha):
+    """y += alpha * x for a dense fp32 CUDA ``y`` and an ``x`` of y's element count (fp32 / bf16 / fp16) with the
+    in-tree kernel; torch elsewhere. Returns y."""
+    if not (y.is_cuda and y.dtype == torch.float32 and x.dtype in DT and enabled() and y.is_contiguous() and
+            x.is_contiguous() and x.numel() == y.numel()):
+        return y.add_(x.reshape(y.shape).to(y.dtype), alpha=alpha)
+    native._check(native.load().dl4j_axpy(DT[x.dtype], _ptr(x), _ptr(y), y.numel(), float(alpha), _stream()), "axpy")
+    CALLS["axpy"] += 1
+    return y
