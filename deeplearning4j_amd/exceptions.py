@@ -21,3 +21,7 @@ class DL4JInvalidInputException(DL4JException, ValueError):
 class InvalidInputTypeException(DL4JInvalidConfigException):
     """An InputType that a layer cannot take, found while shapes are inferred at build time (reference
     nn/conf/inputs/InvalidInputTypeException.java), e.g. a convolution kernel larger than the padded input."""
+
+
+class UnsupportedOperationException(DL4JException, NotImplementedError):
+    """java.lang.UnsupportedOperationException: a configured feature the engine refuses (e.g. HESSIAN_FREE)."""

@@ -62,6 +62,7 @@ class OptimizationAlgorithm(_StrEnum):
     STOCHASTIC_GRADIENT_DESCENT = "STOCHASTIC_GRADIENT_DESCENT"
     LINE_GRADIENT_DESCENT = "LINE_GRADIENT_DESCENT"
     CONJUGATE_GRADIENT = "CONJUGATE_GRADIENT"
+    HESSIAN_FREE = "HESSIAN_FREE"          # deprecated in the reference; configurable, refused at fit time
     LBFGS = "LBFGS"
 
 

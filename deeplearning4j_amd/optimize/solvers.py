@@ -15,6 +15,8 @@ import logging
 
 import torch
 
+from ..exceptions import UnsupportedOperationException
+
 log = logging.getLogger("deeplearning4j_amd")
 
 
@@ -79,18 +81,49 @@ class ZeroDirection(TerminationCondition):
 
 # ------------------------------------------------------------------------------------------ line search
 class BackTrackLineSearch:
-    """Backtracking line search with the Armijo sufficient-decrease test (BackTrackLineSearch.java): start at
-    step 1, halve (with a quadratic-interpolation guess when it is inside [0.1, 0.5] x step) until
-    f(x - s*d) <= f(x) - c * s * <g, d>, at most ``maxIterations`` evaluations."""
+    """Backtracking line search with the Armijo test (BackTrackLineSearch.java:62-340): start at step 1 and shrink
+    (quadratic-interpolation guess clamped to [0.1, 0.5] x step) until the sufficient-decrease condition
+    f(x - s*d) <= f(x) - c * s * <g, d> holds, at most ``maxIterations`` evaluations; the best step seen is returned
+    otherwise (0.0 when no step improved). A step function that ADDS the direction (DefaultStepFunction /
+    GradientStepFunction) makes it a maximisation, as in the reference: sufficient increase
+    f(x + s*d) >= f(x) - c * s * <g, d>.
 
-    def __init__(self, model, score_fn, stepFunction=None, maxIterations=5, c1=1e-4):
-        self.model, self.score_fn = model, score_fn
+    Constructors as the reference: ``BackTrackLineSearch(model, optimizer)``, ``(model, stepFunction, optimizer)``,
+    or ``(model, score_fn, stepFunction, maxIterations)`` (score_fn: the objective at the model's current
+    parameters; by default the model's score on its current input / labels)."""
+
+    def __init__(self, model, score_fn=None, stepFunction=None, maxIterations=None, c1=1e-4):
+        optimizer = None
+        if isinstance(score_fn, StepFunction):
+            score_fn, stepFunction, optimizer = None, score_fn, stepFunction
+        elif isinstance(score_fn, BaseOptimizer):
+            score_fn, optimizer = None, score_fn
+        if isinstance(stepFunction, BaseOptimizer):
+            optimizer, stepFunction = stepFunction, None
+        self.model = model
+        self.score_fn = score_fn or self._model_score
+        self.optimizer = optimizer
         self.stepFunction = stepFunction or NegativeDefaultStepFunction()
+        if maxIterations is None:
+            g = getattr(getattr(model, "conf", None), "globalConf", None) or {}
+            maxIterations = g.get("maxNumLineSearchIterations", 5)
         self.maxIterations, self.c1 = max(1, int(maxIterations)), c1
 
-    def optimize(self, params, gradient, direction, f0):
+    def _model_score(self):
+        m = self.model
+        if self.optimizer is not None and self.optimizer._batch is not None:
+            return self.optimizer._score_only()
+        return float(m._score_batch(m.input, m.labels, getattr(m, "mask", None), getattr(m, "labelsMask", None)))
+
+    def minimizes(self):
+        return isinstance(self.stepFunction, (NegativeDefaultStepFunction, NegativeGradientStepFunction))
+
+    def optimize(self, params, gradient, direction, f0=None):
+        if f0 is None:
+            f0 = float(self.model.score())
+        minimize = self.minimizes()
         slope = float(torch.dot(gradient.reshape(-1).double(), direction.reshape(-1).double()))
-        if slope <= 0:
+        if minimize and slope <= 0:
             return 0.0
         x0 = params.clone()
         step = 1.0
@@ -100,13 +133,17 @@ class BackTrackLineSearch:
             self.stepFunction.step(params, direction, step)
             self.model._params_changed()
             f = self.score_fn()
-            if f < best_f:
+            if (f < best_f) if minimize else (f > best_f):
                 best_step, best_f = step, f
-            if f <= f0 - self.c1 * step * slope:
+            if minimize and f <= f0 - self.c1 * step * slope:
                 break
-            # quadratic model through f0, slope, f(step)
-            denom = 2.0 * (f - f0 + slope * step)
-            nxt = slope * step * step / denom if denom > 0 else step * 0.5
+            if not minimize and f >= f0 - self.c1 * step * abs(slope):
+                best_step = step
+                break
+            # quadratic model through f0, slope, f(step) (of -f when maximising)
+            df = (f - f0) if minimize else (f0 - f)
+            denom = 2.0 * (df + abs(slope) * step)
+            nxt = abs(slope) * step * step / denom if denom > 0 else step * 0.5
             step = min(max(nxt, 0.1 * step), 0.5 * step)
         params.copy_(x0)
         self.model._params_changed()
@@ -286,6 +323,10 @@ class Solver:
             algo = OA.of(self.model.conf.globalConf.get("optimizationAlgo", OA.STOCHASTIC_GRADIENT_DESCENT))
             sf = self.model.conf.globalConf.get("stepFunction")
             kw = {"stepFunction": _step_function(sf)} if sf is not None else {}
+            if algo == OA.HESSIAN_FREE:
+                raise UnsupportedOperationException(
+                    "HESSIAN_FREE optimisation is deprecated in the reference and has no solver "
+                    "(OptimizationAlgorithm.java:27); use LBFGS or CONJUGATE_GRADIENT")
             cls = {OA.STOCHASTIC_GRADIENT_DESCENT: StochasticGradientDescent,
                    OA.LINE_GRADIENT_DESCENT: LineGradientDescent, OA.CONJUGATE_GRADIENT: ConjugateGradient,
                    OA.LBFGS: LBFGS}[algo]
