@@ -242,7 +242,28 @@ class ComputationGraph(BaseNetwork):
         return self.layers_by_name[name]
 
     def getVertex(self, name):
-        return self.conf.vertices[name]
+        """The runtime vertex (reference nn/graph/vertex/GraphVertex): name / index / layer accessors and
+        setLayerAsFrozen(); configuration attributes read through to the vertex configuration."""
+        return _RuntimeVertex(self, name)
+
+    def getVertices(self):
+        """Runtime vertices in the index space of topologicalSortOrder(): network inputs first, then the vertices
+        in the order they were added."""
+        return [_RuntimeVertex(self, n) for n in list(self.conf.networkInputs) + list(self.conf.vertices)]
+
+    def _replace_impl(self, idx, name, old, new):
+        self.layers_by_name[name] = new
+
+    def _summary_types(self, inputTypes):
+        import copy
+        c = copy.deepcopy(self.conf)
+        c.inputTypes = list(inputTypes)
+        types = c.addPreProcessorsAndInferNIn()
+        out = {}
+        for name in self.layers_by_name:
+            ins = [types[i] for i in c.vertexInputs[name]]
+            out[name] = (ins[0] if len(ins) == 1 else ins, types[name])
+        return out
 
     def getNumLayers(self):
         return len(self.layers_by_name)
@@ -800,3 +821,41 @@ class ComputationGraph(BaseNetwork):
     def clear(self):
         for l in self.layers_by_name.values():
             l.clear()
+
+
+class _RuntimeVertex:
+    """A live graph vertex (reference GraphVertex): getVertexName / getVertexIndex / hasLayer / getLayer /
+    getInputVertices / setLayerAsFrozen; any other attribute is the vertex configuration's."""
+
+    def __init__(self, graph, name):
+        object.__setattr__(self, "_g", graph)
+        object.__setattr__(self, "_name", name)
+
+    def getVertexName(self):
+        return self._name
+
+    def getVertexIndex(self):
+        return (list(self._g.conf.networkInputs) + list(self._g.conf.vertices)).index(self._name)
+
+    def isInputVertex(self):
+        return self._name in self._g.conf.networkInputs
+
+    def hasLayer(self):
+        return self._name in self._g.layers_by_name
+
+    def getLayer(self):
+        return self._g.layers_by_name.get(self._name)
+
+    def getInputVertices(self):
+        return list(self._g.conf.vertexInputs.get(self._name, []))
+
+    def setLayerAsFrozen(self):
+        if not self.hasLayer():
+            raise ValueError(f"vertex {self._name!r} has no layer to freeze")
+        self._g._freeze_layer_in_place(self._name)
+
+    def __getattr__(self, item):
+        return getattr(self._g.conf.vertices[self._name], item)
+
+    def __repr__(self):
+        return f"GraphVertex({self._name!r})"

@@ -11,12 +11,25 @@ from ..gradient import Gradient
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
+class ParamTable(dict):
+    """Parameter (or gradient) views by key. Calling it returns the layer's flat segment of the network's parameter
+    vector, as the reference's ``Layer.params()`` (a view when the network laid the layer out, else a copy)."""
+    flat = None
+
+    def __call__(self):
+        if self.flat is not None:
+            return self.flat
+        if not self:
+            return torch.zeros(0)
+        return torch.cat([v.reshape(-1) for v in self.values()])
+
+
 class LayerImpl:
     def __init__(self, conf, index=0, net=None):
         self.conf = conf
         self.index = index
         self.net = net
-        self.params = {}      # key -> master view (fp32/fp64)
+        self.params = ParamTable()   # key -> master view (fp32/fp64); params() -> flat segment
         self.cparams = {}     # key -> compute-dtype view (shadow) ; == params when no shadow
         self.grads = {}       # key -> gradient view
         self.input = None
@@ -48,6 +61,26 @@ class LayerImpl:
     def setParamTable(self, table):
         for k, v in table.items():
             self.setParam(k, v)
+
+    def setParams(self, flat):
+        """Overwrite all of this layer's parameters from one flat vector (reference Layer.setParams)."""
+        flat = flat.reshape(-1)
+        if flat.numel() != self.numParams():
+            raise ValueError(f"{self.numParams()} parameters expected, got {flat.numel()}")
+        with torch.no_grad():
+            if self.params.flat is not None:
+                self.params.flat.copy_(flat.to(self.params.flat.dtype))
+            else:
+                o = 0
+                for k, v in self.params.items():
+                    v.copy_(flat[o:o + v.numel()].reshape(v.shape).to(v.dtype))
+                    o += v.numel()
+        if self.net is not None:
+            self.net._params_changed()
+        else:
+            for k in self.params:
+                if self.cparams.get(k) is not None and self.cparams[k] is not self.params[k]:
+                    self.cparams[k].copy_(self.params[k])
 
     def update(self, gradient, paramType=None):
         """Add a gradient (an already-computed update) to the parameters, reference BaseLayer.update(Gradient) /

@@ -503,6 +503,20 @@ class MultiLayerNetwork(BaseNetwork):
         u = self.conf.confs[layer].updater
         return u.getLearningRate(self.conf.iterationCount, self.conf.epochCount) if u is not None else None
 
+    def _replace_impl(self, idx, name, old, new):
+        self.layers[idx] = new
+
+    def _summary_types(self, inputTypes):
+        t = inputTypes[0]
+        out = {}
+        for idx, name, impl, _ in self._layer_offsets:
+            lc = impl.conf
+            pp = self.conf.inputPreProcessors.get(idx) or lc.getPreProcessorForInputType(t)
+            t_in = pp.getOutputType(t) if pp is not None else t
+            t = lc.getOutputType(idx, t_in)
+            out[name] = (t_in, t)
+        return out
+
     def setInput(self, x):
         self.input = x
 

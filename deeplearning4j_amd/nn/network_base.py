@@ -16,6 +16,7 @@ import torch
 from .conf.enums import DataType
 from .conf.weights import WeightInit, init_weights_
 from .updater import NetworkUpdater, build_entries
+from .layers.base import ParamTable
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 from .. import profiling as _prof
 
@@ -136,7 +137,7 @@ class BaseNetwork:
             self._offset_of[idx] = off
             self._offset_of[name] = off
             o = off
-            impl.params, impl.grads, impl.cparams = {}, {}, {}
+            impl.params, impl.grads, impl.cparams = ParamTable(), ParamTable(), ParamTable()
             for spec in impl.conf.param_specs():
                 v = make_view(flat, o, spec)
                 if init:
@@ -156,6 +157,8 @@ class BaseNetwork:
                 else:
                     impl.cparams[spec.key] = v
                 o += spec.numel
+            impl.params.flat = flat[off:o]
+            impl.grads.flat = self.flattenedGradients[off:o]
             off = o
         if self.shadow is not None:
             with torch.no_grad():
@@ -168,6 +171,33 @@ class BaseNetwork:
         self.updater = NetworkUpdater(self, build_entries(self._layer_offsets))
         self.updater.init_state(self.device, self.master_dtype)
         self.initCalled = True
+
+    def _freeze_layer_in_place(self, key):
+        """Wrap a live layer in a FrozenLayer (reference GraphVertex.setLayerAsFrozen / FrozenLayer(layer)): the
+        wrapper shares the layer's parameter and gradient views, so nothing moves in the flat vectors; the updater is
+        rebuilt so the layer's segment gets the NoOp update (its previous updater state is dropped). The network
+        configuration is left as it was, as in the reference (only the runtime layer changes)."""
+        from .conf.layers import FrozenLayer
+        from .updater import NetworkUpdater, build_entries
+        for i, (idx, name, impl, off) in enumerate(self._layer_offsets):
+            if key not in (idx, name):
+                continue
+            if isinstance(impl.conf, FrozenLayer):
+                return impl
+            conf = FrozenLayer(layer=impl.conf, layerName=getattr(impl.conf, "layerName", None))
+            fz = conf.instantiate(index=impl.index, net=self)
+            fz.inner = impl
+            fz.params, fz.grads, fz.cparams = impl.params, impl.grads, impl.cparams
+            fz.bind()
+            self._layer_offsets[i] = (idx, name, fz, off)
+            self._replace_impl(idx, name, impl, fz)
+            self.updater = NetworkUpdater(self, build_entries(self._layer_offsets))
+            self.updater.init_state(self.device, self.master_dtype)
+            return fz
+        raise ValueError(f"No layer {key!r}")
+
+    def _replace_impl(self, idx, name, old, new):
+        raise NotImplementedError
 
     def _params_changed(self):
         """Parameters were modified outside the fused updater (line search, setParams): refresh the bf16 compute
@@ -599,16 +629,28 @@ class BaseNetwork:
             self._idx_layers = {k for k, c in items if isinstance(c, EmbeddingLayer)}
         return self._idx_layers
 
-    def summary(self):
-        lines = [f"{'idx':>4} {'name':<28} {'type':<32} {'nParams':>12}"]
+    def summary(self, *inputTypes):
+        """Per-layer table (index, name, type, parameter count); with the network's input type(s) — as the
+        reference's summary(InputType...) — also each layer's input and output activation types."""
+        io = self._summary_types(inputTypes) if inputTypes else {}
+        head = f"{'idx':>4} {'name':<28} {'type':<32} {'nParams':>12}"
+        if io:
+            head += f"  {'input type':<40} {'output type'}"
+        lines = [head]
         total = 0
         for idx, name, impl, _ in self._layer_offsets:
             n = impl.conf.numParams()
             total += n
-            lines.append(f"{idx:>4} {str(name):<28} {type(impl.conf).__name__:<32} {n:>12,}")
+            row = f"{idx:>4} {str(name):<28} {type(impl.conf).__name__:<32} {n:>12,}"
+            if io and name in io:
+                row += f"  {str(io[name][0]):<40} {io[name][1]}"
+            lines.append(row)
         lines.append(f"Total Parameters: {total:,}")
         lines.append(f"Compute dtype: {self.compute_dtype}, device: {self.device}")
         return "\n".join(lines)
+
+    def _summary_types(self, inputTypes):
+        return {}
 
     def memoryReport(self, minibatch=1):
         from .conf.memory import network_memory_report

@@ -23,7 +23,8 @@ _FT_GLOBAL_KEYS = ("seed", "optimizationAlgo", "miniBatch", "maxNumLineSearchIte
 
 
 class FineTuneConfiguration:
-    """Hyperparameter overrides applied to every (non-frozen) layer of the new network."""
+    """Hyperparameter overrides applied to every layer of the new network, frozen ones included (their parameters
+    do not move, but their configuration reads as the reference's: TransferLearning.java:359-365, 474-487)."""
 
     def __init__(self, **kw):
         self.overrides = kw
@@ -182,7 +183,7 @@ class TransferLearning:
             confs = []
             for i, c in enumerate(self.confs):
                 c = _base(c)
-                if self.ft is not None and i > self.frozenTill:
+                if self.ft is not None:
                     self.ft.applyToLayer(c)
                 if c.layerName is None:
                     c.layerName = f"layer{i}"
@@ -313,7 +314,7 @@ class TransferLearning:
             for k, v in self.vertices.items():
                 if hasattr(v, "layerConf"):
                     lc = _base(v.layerConf)
-                    if self.ft is not None and k not in self.frozen:
+                    if self.ft is not None:
                         self.ft.applyToLayer(lc)
                     v.layerConf = FrozenLayer(layer=lc, layerName=lc.layerName) if k in self.frozen else lc
                 verts[k] = v
