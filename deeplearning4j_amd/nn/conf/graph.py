@@ -417,6 +417,12 @@ class LayerVertex(GraphVertex):
     def numParams(self):
         return self.layerConf.numParams()
 
+    def getLayerConf(self):
+        """The reference's per-layer NeuralNetConfiguration view: ``getLayerConf().getLayer()`` is the layer
+        configuration (a FrozenLayer wrapper stays a FrozenLayer)."""
+        from .network import LayerConfiguration
+        return LayerConfiguration(self.layerConf)
+
     def getOutputType(self, layerIndex, *inputTypes):
         t = inputTypes[0]
         if self.preProcessor is not None:

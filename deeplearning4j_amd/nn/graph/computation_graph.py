@@ -384,6 +384,9 @@ class ComputationGraph(BaseNetwork):
         return outs
 
     def outputSingle(self, *inputs, train=False):
+        """outputSingle(x...) or, as the reference, outputSingle(train, x...)."""
+        if inputs and isinstance(inputs[0], bool):
+            train, inputs = inputs[0], inputs[1:]
         return self.output(*inputs, train=train)[0]
 
     # ------------------------------------------------------------------------------ backward
