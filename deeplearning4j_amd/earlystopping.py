@@ -561,6 +561,12 @@ class EarlyStoppingParallelTrainer(EarlyStoppingTrainer):
 
     def __init__(self, esConfig, net, train, trainMulti=None, listener=None, workers=None, prefetchBuffer=16,
                  averagingFrequency=1, reportScoreAfterAveraging=True, useLegacyAveraging=True, trainingMode=None):
+        if isinstance(listener, int) and not isinstance(listener, bool):
+            # the reference's positional order (esConf, model, train, trainMulti, workers, prefetchBuffer,
+            # averagingFrequency[, reportScoreAfterAveraging, useLegacyAveraging])
+            listener, workers, prefetchBuffer, averagingFrequency = None, listener, \
+                (workers if workers is not None else prefetchBuffer), \
+                (prefetchBuffer if workers is not None else averagingFrequency)
         from .parallel.wrapper import ParallelWrapper, TrainingMode
         super().__init__(esConfig, net, train if train is not None else trainMulti, listener)
         mode = trainingMode if trainingMode is not None else TrainingMode.SHARED_GRADIENTS
@@ -597,4 +603,8 @@ class EarlyStoppingParallelTrainer(EarlyStoppingTrainer):
         res = super().fit()
         from .parallel.distributed import barrier
         barrier()
+        if res.bestModel is None and res.terminationReason == TerminationReason.IterationTerminationCondition:
+            # stopped inside the first epoch, before any score was saved: the current model is the result
+            # (EarlyStoppingParallelTrainer.java:186-196)
+            res.bestModel = self.model
         return res

@@ -17,9 +17,14 @@ log = logging.getLogger("deeplearning4j_amd")
 
 
 def _factory(spec):
+    """``module:callable`` returning an iterator, or ``module:Class`` of a provider factory whose create() returns
+    one (the reference's DataSetIteratorProviderFactory / MultiDataSetProviderFactory classes)."""
     mod, _, fn = spec.partition(":")
     obj = getattr(importlib.import_module(mod), fn or "create")
-    return obj() if callable(obj) else obj
+    obj = obj() if callable(obj) else obj
+    if hasattr(obj, "create") and not hasattr(obj, "__iter__") and not hasattr(obj, "next"):
+        obj = obj.create()
+    return obj
 
 
 def main(argv=None):
