@@ -30,6 +30,94 @@ class _Request:
         self.x, self.future, self.n = x, fut, x.shape[0]
 
 
+class Pair(tuple):
+    """(first, second) with the reference's getters (org.nd4j.linalg.primitives.Pair)."""
+
+    def __new__(cls, first, second):
+        return super().__new__(cls, (first, second))
+
+    def getFirst(self):
+        return self[0]
+
+    def getSecond(self):
+        return self[1]
+
+
+def _rows(a):
+    a = torch.as_tensor(a)
+    return a.reshape(1, -1) if a.dim() <= 1 else a
+
+
+class BatchedInferenceObservable:
+    """Request batcher of the BATCHED mode as a standalone object (reference PW:inference/observers/
+    BatchedInferenceObservable.java): ``addInput(arrays, masks)`` queues one request (rank-1 arrays are single rows);
+    ``getInputBatches()`` stacks consecutive requests along dimension 0 into as few batches as possible — a new batch
+    starts when an array's trailing shape, the mask layout or the example limit changes — and remembers each batch's
+    request range; after the forward passes, ``setOutputBatches([...])`` + ``getOutputs()`` split every batched
+    output back into one array list per request, in request order."""
+
+    def __init__(self, batchLimit=None):
+        self.batchLimit = batchLimit
+        self.inputs = []                      # per request: (list of arrays, list of masks or None)
+        self.outputBatchInputArrays = []      # per batch: [first request, last request]
+        self.outputBatches = None
+        self.counter = 0
+
+    def addInput(self, inputs, masks=None):
+        self.inputs.append(([_rows(a) for a in inputs], None if masks is None else [
+            None if m is None else _rows(m) for m in masks]))
+        self.counter += 1
+
+    def getCounter(self):
+        return self.counter
+
+    def setCounter(self, n):
+        self.counter = int(n)
+
+    @staticmethod
+    def _key(req):
+        arrays, masks = req
+        return (tuple(tuple(a.shape[1:]) for a in arrays),
+                None if masks is None else tuple(None if m is None else tuple(m.shape[1:]) for m in masks))
+
+    def getInputBatches(self):
+        out, self.outputBatchInputArrays = [], []
+        start = 0
+        while start < len(self.inputs):
+            key, n, end = self._key(self.inputs[start]), self.inputs[start][0][0].shape[0], start + 1
+            while end < len(self.inputs) and self._key(self.inputs[end]) == key:
+                m = self.inputs[end][0][0].shape[0]
+                if self.batchLimit is not None and n + m > self.batchLimit:
+                    break
+                n += m
+                end += 1
+            reqs = self.inputs[start:end]
+            feats = [torch.cat([r[0][j] for r in reqs], 0) for j in range(len(reqs[0][0]))]
+            masks = None
+            if reqs[0][1] is not None:
+                masks = [None if reqs[0][1][j] is None else torch.cat([r[1][j] for r in reqs], 0)
+                         for j in range(len(reqs[0][1]))]
+            out.append(Pair(feats, masks))
+            self.outputBatchInputArrays.append([start, end - 1])
+            start = end
+        return out
+
+    def setOutputBatches(self, batches):
+        self.outputBatches = [list(b) for b in batches]
+
+    def getOutputs(self):
+        if self.outputBatches is None or len(self.outputBatches) != len(self.outputBatchInputArrays):
+            raise RuntimeError("output batches do not match the input batches")
+        res = []
+        for outs, (a, b) in zip(self.outputBatches, self.outputBatchInputArrays):
+            off = 0
+            for r in range(a, b + 1):
+                n = self.inputs[r][0][0].shape[0]
+                res.append([o[off:off + n] for o in outs])
+                off += n
+        return res[:self.counter] if self.counter else res
+
+
 class ParallelInference:
     InferenceMode = InferenceMode
 
@@ -161,18 +249,24 @@ class ParallelInference:
             if batch is None:
                 break
             try:
-                x = torch.cat([r.x for r in batch], 0)
-                if dev.type == "cuda":
-                    with torch.cuda.device(dev), torch.cuda.stream(stream):
-                        xd = x.pin_memory().to(dev, non_blocking=True) if not x.is_cuda else x.to(dev)
-                        out = self._replicas[i].output(xd)
-                        out = out.to("cpu", non_blocking=False)
-                else:
-                    out = self._replicas[i].output(x)
-                off = 0
+                # requests of differing feature shapes go through separate forward passes
+                ob = BatchedInferenceObservable()
                 for r in batch:
-                    r.future.set_result(out[off:off + r.n])
-                    off += r.n
+                    ob.addInput([r.x])
+                outs = []
+                for b in ob.getInputBatches():
+                    x = b.getFirst()[0]
+                    if dev.type == "cuda":
+                        with torch.cuda.device(dev), torch.cuda.stream(stream):
+                            xd = x.pin_memory().to(dev, non_blocking=True) if not x.is_cuda else x.to(dev)
+                            out = self._replicas[i].output(xd)
+                            out = out.to("cpu", non_blocking=False)
+                    else:
+                        out = self._replicas[i].output(x)
+                    outs.append([out])
+                ob.setOutputBatches(outs)
+                for r, o in zip(batch, ob.getOutputs()):
+                    r.future.set_result(o[0])
             except Exception as e:      # deliver the failure to every waiting caller
                 for r in batch:
                     if not r.future.done():
