@@ -185,6 +185,19 @@ class KerasLayer:
     def clearCustomLayers():
         _CUSTOM.clear()
 
+    @staticmethod
+    def fromConfig(layerConfig, previousLayer=None, kerasMajorVersion=None):
+        """One Keras layer config map ({class_name, config[, keras_version]}) -> the DL4J layer configuration (or
+        graph vertex), as the reference's per-class Keras layer objects (KerasDense(layerConfig).getDenseLayer(),
+        ...). ``previousLayer``: the config map of the layer feeding it (a mask_zero Embedding wraps a recurrent
+        layer in MaskZeroLayer)."""
+        v = kerasMajorVersion or int(layerConfig.get("keras_version", 2))
+        ctx = _Ctx(v, False)
+        m = _map_layer(layerConfig, ctx)
+        if previousLayer is not None and _masks_zero(_map_layer(previousLayer, ctx)):
+            _mask_zero_wrap(m)
+        return m.obj
+
 
 def space_to_depth_mapper(block_size=2):
     """Mapper for the reference's KerasSpaceToDepth custom Lambda (space_to_depth with block 2)."""
@@ -299,7 +312,148 @@ class _Ctx:
         self.theano = backend == "theano"
 
 
+# --------------------------------------------------------------------------------------- common layer fields
+# Keras initializer names -> DL4J WeightInit (KER:utils/KerasInitilizationUtils.java:56-175); distributions below
+_INIT = {"glorot_normal": "XAVIER", "glorot_uniform": "XAVIER_UNIFORM", "lecun_normal": "LECUN_NORMAL",
+         "lecun_uniform": "LECUN_UNIFORM", "he_normal": "RELU", "he_uniform": "RELU_UNIFORM", "one": "ONES",
+         "ones": "ONES", "zero": "ZERO", "zeros": "ZERO", "identity": "IDENTITY"}
+
+
+def _init(spec):
+    """(WeightInit, Distribution or None) of a Keras 1 initializer name or a Keras 2 {class_name, config}; None when
+    the layer config has none."""
+    from ..nn.conf import weights as Wt
+    if spec is None:
+        return None
+    if isinstance(spec, dict):
+        name, icfg = spec.get("class_name"), spec.get("config") or {}
+    else:
+        name, icfg = spec, {}
+    key = {"RandomUniform": "random_uniform", "RandomNormal": "random_normal", "Ones": "ones", "Zeros": "zeros",
+           "Constant": "constant", "Orthogonal": "orthogonal", "TruncatedNormal": "truncated_normal",
+           "Identity": "identity", "GlorotNormal": "glorot_normal", "GlorotUniform": "glorot_uniform",
+           "HeNormal": "he_normal", "HeUniform": "he_uniform", "LecunNormal": "lecun_normal",
+           "LecunUniform": "lecun_uniform"}.get(name, name)
+    if key in _INIT:
+        return Wt.WeightInit[_INIT[key]], None
+    if key in ("uniform", "random_uniform"):
+        if "minval" in icfg:
+            return Wt.WeightInit.DISTRIBUTION, Wt.UniformDistribution(float(icfg["minval"]), float(icfg["maxval"]))
+        sc = float(icfg.get("scale", 0.05))
+        return Wt.WeightInit.DISTRIBUTION, Wt.UniformDistribution(-sc, sc)
+    if key in ("normal", "random_normal"):
+        if "stddev" in icfg:
+            return Wt.WeightInit.DISTRIBUTION, Wt.NormalDistribution(float(icfg.get("mean", 0.0)),
+                                                                     float(icfg["stddev"]))
+        return Wt.WeightInit.DISTRIBUTION, Wt.NormalDistribution(0.0, float(icfg.get("scale", 0.05)))
+    if key == "constant":
+        return Wt.WeightInit.DISTRIBUTION, Wt.ConstantDistribution(float(icfg.get("value", 0.0)))
+    if key == "orthogonal":
+        return Wt.WeightInit.DISTRIBUTION, Wt.OrthogonalDistribution(float(icfg.get("gain", icfg.get("scale", 1.0))))
+    if key == "truncated_normal":
+        return Wt.WeightInit.DISTRIBUTION, Wt.TruncatedNormalDistribution(float(icfg.get("mean", 0.0)),
+                                                                          float(icfg.get("stddev", 0.05)))
+    if key == "VarianceScaling":
+        mode = {"fan_in": "FAN_IN", "fan_out": "FAN_OUT", "fan_avg": "FAN_AVG"}.get(icfg.get("mode"))
+        if mode is None:
+            raise InvalidKerasConfigurationException("VarianceScaling 'mode' must be fan_in, fan_out or fan_avg")
+        dist = "NORMAL" if icfg.get("distribution", "normal") in ("normal", "truncated_normal") else "UNIFORM"
+        return Wt.WeightInit[f"VAR_SCALING_{dist}_{mode}"], None
+    raise UnsupportedKerasConfigurationException(f"Unsupported Keras weight initializer {name!r}")
+
+
+def _reg(cfg, *fields):
+    """(l1, l2) of the first present regularizer field: {l1, l2} or {class_name: L1L2, config: {l1, l2}}
+    (KER:utils/KerasRegularizerUtils.java:20-60)."""
+    for f in fields:
+        r = cfg.get(f)
+        if isinstance(r, dict):
+            inner = r.get("config") if r.get("class_name") == "L1L2" else r
+            inner = inner or {}
+            return float(inner.get("l1", 0.0) or 0.0), float(inner.get("l2", 0.0) or 0.0)
+    return 0.0, 0.0
+
+
+def _apply_common(k, ctx):
+    """The fields every DL4J layer built from Keras gets (KER:KerasLayer.java, KerasLayerUtils): the layer name,
+    weight initialisation, L1 / L2 weight and bias regularisation, the generic ``dropout`` fraction (retain
+    probability 1 - p), and for LSTMs the recurrent initialisation and the forget-gate bias."""
+    cfg, obj = k.cfg or {}, k.obj
+    if k.kind not in ("layer", "timedistributed") or not isinstance(obj, L.Layer):
+        return k
+    from ..nn.conf.regularization import Dropout
+    target = obj
+    while isinstance(target, (L.LastTimeStep,)) and getattr(target, "underlying", None) is not None:
+        target = target.underlying
+    for o in {id(obj): obj, id(target): target}.values():
+        if k.name is not None and "layerName" in o._all_fields():
+            o.layerName = k.name
+    fields = target._all_fields()
+    emb = k.keras_class == "Embedding"
+    init = _init(cfg.get("embeddings_initializer") if emb and "embeddings_initializer" in cfg else
+                 cfg.get("kernel_initializer", cfg.get("init", cfg.get("depthwise_initializer"))))
+    if init is not None and "weightInit" in fields:
+        target.weightInit, dist = init
+        if dist is not None:
+            target.dist = dist
+    if "weightInitRecurrent" in fields:
+        rinit = _init(cfg.get("recurrent_initializer", cfg.get("inner_init")))
+        if rinit is not None:
+            target.weightInitRecurrent = rinit[0]
+            if rinit[1] is not None:
+                target.distRecurrent = rinit[1]
+    if "l1" in fields:
+        l1, l2 = _reg(cfg, "embeddings_regularizer", "kernel_regularizer", "W_regularizer") if emb else \
+            _reg(cfg, "kernel_regularizer", "W_regularizer", "depthwise_regularizer")
+        if l1:
+            target.l1 = l1
+        if l2:
+            target.l2 = l2
+        b1, b2 = _reg(cfg, "bias_regularizer", "b_regularizer")
+        if b1:
+            target.l1Bias = b1
+        if b2:
+            target.l2Bias = b2
+    p = cfg.get("dropout", cfg.get("dropout_W"))
+    if isinstance(p, (int, float)) and not isinstance(p, bool) and p > 0 and "idropout" in fields and \
+            k.keras_class not in ("Dropout", "SpatialDropout1D", "SpatialDropout2D", "AlphaDropout",
+                                  "GaussianDropout", "GaussianNoise"):
+        target.idropout = Dropout(1.0 - float(p))
+    if "forgetGateBiasInit" in fields:
+        if "unit_forget_bias" in cfg:
+            target.forgetGateBiasInit = 1.0 if cfg["unit_forget_bias"] else 0.0
+        elif "forget_bias_init" in cfg:
+            fb = cfg["forget_bias_init"]
+            if isinstance(fb, str):
+                if fb not in ("one", "ones", "zero", "zeros"):
+                    raise UnsupportedKerasConfigurationException(f"LSTM forget_bias_init {fb!r}")
+                target.forgetGateBiasInit = 1.0 if fb.startswith("one") else 0.0
+            else:
+                target.forgetGateBiasInit = float(fb)
+    return k
+
+
 def _map_layer(kl, ctx):
+    return _apply_common(_map_layer_core(kl, ctx), ctx)
+
+
+def _masks_zero(k):
+    return k is not None and k.keras_class == "Embedding" and bool((k.cfg or {}).get("mask_zero", False))
+
+
+def _mask_zero_wrap(m):
+    """A recurrent layer fed by a mask_zero Embedding: MaskZeroLayer(layer) (inside the LastTimeStep wrapper when
+    return_sequences is false), as KER:layers/recurrent/KerasLstm.java / KerasSimpleRnn.java."""
+    if m.keras_class not in ("LSTM", "SimpleRNN", "Bidirectional"):
+        return m
+    if isinstance(m.obj, L.LastTimeStep):
+        m.obj.underlying = L.MaskZeroLayer(underlying=m.obj.underlying, maskingValue=0.0)
+    else:
+        m.obj = L.MaskZeroLayer(underlying=m.obj, maskingValue=0.0)
+    return m
+
+
+def _map_layer_core(kl, ctx):
     cls = kl["class_name"]
     cfg = kl.get("config", {}) or {}
     name = cfg.get("name") or kl.get("name")
@@ -331,11 +485,11 @@ def _map_layer(kl, ctx):
     if cls in ("AlphaDropout", "GaussianDropout", "GaussianNoise"):
         from ..nn.conf import regularization as R
         if cls == "AlphaDropout":
-            d = R.AlphaDropout(1.0 - float(cfg.get("rate", 0.0)))
+            d = R.AlphaDropout(1.0 - float(cfg.get("rate", cfg.get("p", 0.0))))
         elif cls == "GaussianDropout":
-            d = R.GaussianDropout(float(cfg.get("rate", 0.0)))
+            d = R.GaussianDropout(float(cfg.get("rate", cfg.get("p", 0.0))))
         else:
-            d = R.GaussianNoise(float(cfg.get("stddev", 0.0)))
+            d = R.GaussianNoise(float(cfg.get("stddev", cfg.get("sigma", 0.0))))
         return _KLayer(name, "layer", L.DropoutLayer(idropout=d), keras_class=cls, cfg=cfg)
     if cls == "Flatten":
         return _KLayer(name, "flatten", keras_class=cls, cfg=cfg)
@@ -466,7 +620,15 @@ def _map_layer(kl, ctx):
         lay = L.EmbeddingSequenceLayer(nIn=int(cfg["input_dim"]), nOut=int(cfg["output_dim"]),
                                        inputLength=int(il) if il is not None else -1, hasBias=False,
                                        activation=Activation.IDENTITY)
-        return _KLayer(name, "layer", lay, setter=_embedding_setter, keras_class=cls, cfg=cfg)
+        setter = _embedding_setter
+        if cfg.get("mask_zero", False):
+            # index 0 is Keras' padding token: its embedding row is zero, and the next recurrent layer masks the
+            # all-zero time steps (KER:layers/embeddings/KerasEmbedding.java setWeights / hasZeroMasking)
+            def setter(p, kw):
+                _embedding_setter(p, kw)
+                with torch.no_grad():
+                    p["W"][0].zero_()
+        return _KLayer(name, "layer", lay, setter=setter, keras_class=cls, cfg=cfg)
     if cls == "ZeroPadding2D":
         pd = cfg.get("padding", [1, 1])
         if isinstance(pd, int):
@@ -625,7 +787,8 @@ class KerasModel:
             if kl["class_name"] == "InputLayer":
                 shape = kl["config"]["batch_input_shape"]
                 continue
-            mapped.append(_map_layer(kl, self.ctx))
+            m = _map_layer(kl, self.ctx)
+            mapped.append(_mask_zero_wrap(m) if mapped and _masks_zero(mapped[-1]) else m)
         if mapped and mapped[0].keras_class == "Embedding":
             # index input [mb, T]: T may be null (variable length)
             T = shape[1] if len(shape) > 1 else None
@@ -742,6 +905,7 @@ class KerasModel:
         gb.setInputTypes(*[types[n] for n in inputs])
         setters = []
         rename = {}
+        by_name = {}
         for kl in c["layers"]:
             if kl["class_name"] == "InputLayer":
                 continue
@@ -749,6 +913,9 @@ class KerasModel:
             nodes = kl.get("inbound_nodes") or []
             inb = [rename.get(x[0], x[0]) for x in (nodes[0] if nodes else [])]
             m = _map_layer(kl, self.ctx)
+            by_name[name] = m
+            if len(inb) == 1 and _masks_zero(by_name.get(inb[0])):
+                _mask_zero_wrap(m)
             cl = cl_of.get(inb[0], True) if inb else True
             cl = _channels_last(kl.get("config", {}), cl)
             if m.kind == "skip":

@@ -89,6 +89,9 @@ class ActivationReLU6(IActivation):
 class ActivationLReLU(IActivation):
     FIELDS = {"alpha": 0.01}
 
+    def __str__(self):
+        return f"leakyrelu(a={self.alpha})"          # ND4J ActivationLReLU.toString
+
     def getActivation(self, x, training=False):
         r = _kf(x, "leakyrelu", self.alpha)
         if r is not None:
