@@ -866,12 +866,12 @@ DL4J_API long long dl4j_bn_tiles_workspace_floats(long long P, int C) {
 
 template <typename T>
 static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C, const float* tstats, long long P,
-                             const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
-                             float* run_var, float decay, float eps, int relu, float* ws, float* ctx_out,
-                             unsigned char* mask, hipStream_t s, const float* rctx = nullptr) {
+                             int rpp, const float* gamma, const float* beta, float gconst, float bconst,
+                             float* run_mean, float* run_var, float decay, float eps, int relu, float* ws,
+                             float* ctx_out, unsigned char* mask, hipStream_t s, const float* rctx = nullptr) {
   const long long S = (P + 31) / 32;
   BnFin f{M, xb, gamma, beta, gconst, bconst, run_mean, run_var, decay, eps, ctx_out,
-          nullptr, nullptr, nullptr, nullptr, nullptr, 64};
+          nullptr, nullptr, nullptr, nullptr, nullptr, rpp};
   int rc;
   if (bn_fold_enabled()) {
     // one launch: tile re-centring + fold + finalize
@@ -880,7 +880,7 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
     float* p1 = ws;
     float* p2 = ws + S * C;
     hipLaunchKernelGGL(bn_tiles_reduce<T>, dim3((C + 63) / 64, (unsigned)S), dim3(256), 0, s, tstats, P, C, M, xb, p1,
-                       p2, 64);
+                       p2, rpp);
     rc = bn_fold_launch<T, 0, 0>(p1, p2, S, C, p2 + S * C, f, s);
   }
   if (rc) return rc;
@@ -894,18 +894,21 @@ static int bn_fwd_tiles_impl(const T* xb, const T* res, T* y, long long M, int C
   return (int)hipGetLastError();
 }
 
+// rpp: rows per partial (64 for the implicit-GEMM / GEMM epilogues, the chunk's pixel count for dl4j_conv_halo);
+// partial p covers rows [rpp*p, rpp*p + rpp).
 DL4J_API int dl4j_bn_fwd_tiles(int dtype, const void* x, const void* res, void* y, long long M, int C,
-                               const float* tstats, long long P, const float* gamma, const float* beta, float gconst,
-                               float bconst, float* run_mean, float* run_var, float decay, float eps, int relu,
-                               float* ws, float* ctx_out, unsigned char* mask, hipStream_t s) {
-  if (C % 8 != 0 || C / 8 > 256 || (dtype != 1 && dtype != 2) || P < 1) return -1;
+                               const float* tstats, long long P, int rpp, const float* gamma, const float* beta,
+                               float gconst, float bconst, float* run_mean, float* run_var, float decay, float eps,
+                               int relu, float* ws, float* ctx_out, unsigned char* mask, hipStream_t s) {
+  if (C % 8 != 0 || C / 8 > 256 || (dtype != 1 && dtype != 2) || P < 1 || rpp < 1 || P * (long long)rpp < M)
+    return -1;
   if (res) relu = 1;
   else mask = nullptr;
   if (dtype == 2)
-    return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, gamma, beta, gconst,
+    return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, rpp, gamma, beta, gconst,
                                   bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, mask, s);
-  return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, gamma, beta, gconst,
-                                 bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, mask, s);
+  return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, rpp, gamma, beta,
+                                 gconst, bconst, run_mean, run_var, decay, eps, relu, ws, ctx_out, mask, s);
 }
 
 // dres: gradient w.r.t. the fused residual input (required when res != nullptr).
@@ -985,14 +988,15 @@ DL4J_API int dl4j_bn_bwd_rbn(int dtype, const void* x, const void* res, const vo
 DL4J_API int dl4j_bn_fwd_rbn(int dtype, const void* x, const void* res, const float* rctx, void* y, long long M, int C,
                              const float* gamma, const float* beta, float gconst, float bconst, float* run_mean,
                              float* run_var, float decay, float eps, float* ws, float* ctx_out, unsigned char* mask,
-                             const float* tstats, long long P, hipStream_t s) {
+                             const float* tstats, long long P, int rpp, hipStream_t s) {
   if (C % 8 != 0 || C / 8 > 256 || !res || !rctx || !y || (dtype != 1 && dtype != 2)) return -1;
   if (tstats) {
+    if (rpp < 1) return -1;
     if (dtype == 2)
-      return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, gamma, beta, gconst,
-                                    bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
-    return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, gamma, beta, gconst,
-                                   bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
+      return bn_fwd_tiles_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, tstats, P, rpp, gamma, beta,
+                                    gconst, bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
+    return bn_fwd_tiles_impl<bf16>((const bf16*)x, (const bf16*)res, (bf16*)y, M, C, tstats, P, rpp, gamma, beta,
+                                   gconst, bconst, run_mean, run_var, decay, eps, 1, ws, ctx_out, mask, s, rctx);
   }
   if (dtype == 2)
     return bn_fwd_impl<f16>((const f16*)x, (const f16*)res, (f16*)y, M, C, gamma, beta, gconst, bconst, run_mean,

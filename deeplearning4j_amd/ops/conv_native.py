@@ -346,11 +346,11 @@ def _conv2d_fwd(x, w, b, stride, pad4, dilation, want_stats=False, use_gemm=True
     if _v3_ok(C, K, R, S):
         key = ("fwd", geom, bias is not None, stats, x.dtype)
         v = _v3_pick(key, lambda var, out, t: _fwd_launch(var, x, krsc, bias, out, geom, 0.0, t),
-                     y, lambda var: _stats_buf(var, N * OH * OW, K, x.device) if stats else None)
-    ts = _stats_buf(v, N * OH * OW, K, x.device) if stats else None
+                     y, lambda var: _stats_buf(var, N * OH * OW, K, x.device, geom) if stats else None)
+    ts = _stats_buf(v, N * OH * OW, K, x.device, geom) if stats else None
     rc = _fwd_launch(v, x, krsc, bias, y, geom, 0.0, ts)
     if rc == 1:
-        y._bn_tile_stats = (ts, ts.shape[1])
+        _attach_tile_stats(y, ts, v, geom)
         rc = 0
     native._check(rc, "conv_fwd")
     return y
@@ -365,19 +365,54 @@ def _v3_ok(C, K, R, S):
     return V3 and C % 64 == 0 and K % 8 == 0 and R * S <= 64
 
 
-def _stats_buf(variant, M, K, device):
-    # BatchNorm tile partials, 64-row partials: the round-2 kernel pads to whole 128-row tiles
-    P = (M + 63) // 64 if variant >= 0 else 2 * ((M + 127) // 128)
+def _stats_buf(variant, M, K, device, geom=None):
+    # BatchNorm tile partials, 64-row partials: the round-2 kernel pads to whole 128-row tiles; the halo kernel writes
+    # one partial per pixel chunk
+    if variant == HALO_VAR:
+        P, _ = _halo_plan(geom)
+        if not P:
+            return None
+    else:
+        P = (M + 63) // 64 if variant >= 0 else 2 * ((M + 127) // 128)
     return torch.empty((3, P, K), dtype=torch.float32, device=device)
 
 
 STREAM_VAR = 100     # persistent loader/consumer conv kernel (csrc/gemm_stream.hip conv_stream), a tuner candidate
+HALO_VAR = 101       # halo-staged 3x3 / 64-channel kernel (csrc/conv_halo.hip), a tuner candidate
+native.register_sig("dl4j_conv_halo_plan", [c_int] * 15 + [ctypes.POINTER(c_int)], restype=c_ll)
+native.register_sig("dl4j_conv_halo", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 +
+                    [ctypes.c_float, c_void_p, c_void_p])
+_HALO_PLANS = {}
+
+
+def _halo_plan(geom):
+    """(chunks, pixels per chunk) of dl4j_conv_halo for a geometry, (0, 0) when it is not that kernel's."""
+    r = _HALO_PLANS.get(geom)
+    if r is None:
+        pc = ctypes.c_int(0)
+        n = native.load().dl4j_conv_halo_plan(*geom, ctypes.byref(pc))
+        r = _HALO_PLANS[geom] = (int(n), int(pc.value)) if n > 0 else (0, 0)
+    return r
+
+
+def _attach_tile_stats(y, ts, variant, geom):
+    """The producer's BN tile statistics for a consuming training BN layer (ops/native.py _tile_rpp)."""
+    if variant == HALO_VAR:
+        y._bn_tile_stats = (ts, ts.shape[1], _halo_plan(geom)[1])
+    else:
+        y._bn_tile_stats = (ts, ts.shape[1])
 
 
 def _fwd_launch(variant, x, wk, bias, y, geom, beta, ts):
     """One conv launch on the chosen kernel. Returns 1 when BN tile statistics were written to ts, 0 when not, a
     negative code / HIP error otherwise."""
     lib = native.load()
+    if variant == HALO_VAR:
+        if ts is not None and ts.shape[1] != _halo_plan(geom)[0]:
+            return -1
+        rc = lib.dl4j_conv_halo(_dtc(x), _ptr(x), _ptr(wk), _ptr(bias), _ptr(y), *geom, float(beta), _ptr(ts),
+                                _stream())
+        return 1 if (rc == 0 and ts is not None) else rc
     if variant == STREAM_VAR:
         native.register_sig("dl4j_conv_stream", [c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 15 +
                             [ctypes.c_float, c_void_p, c_void_p])
@@ -413,7 +448,7 @@ def _v3_pick(key, launch, out, make_ts, allow_r2=True):
         return lib.dl4j_conv_v3_default_variant(M, K)
     # allow_r2=False: the round-2 kernel lacks an epilogue the caller needs (BN-backward sums), so its lower kernel
     # time would not be the lower step time
-    cands = list(range(lib.dl4j_conv_v3_num_variants())) + [STREAM_VAR] + \
+    cands = list(range(lib.dl4j_conv_v3_num_variants())) + [STREAM_VAR, HALO_VAR] + \
         ([-1] if out.dtype == torch.bfloat16 and allow_r2 else [])
     scratch = torch.empty_like(out)
     if key[0] == "bwd_acc":

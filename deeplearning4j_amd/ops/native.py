@@ -368,16 +368,16 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     # never re-reads the residual
     mask = _ae((M * C // 8,), torch.uint8, x.device) if res is not None and training else None
     ts = getattr(x, "_bn_tile_stats", None)
-    if training and ts is not None and dt in (1, 2) and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and \
-            (len(ts) < 3 or ts[2] == 64):
+    rpp = _tile_rpp(ts, M, C) if training and dt in (1, 2) else None
+    if rpp is not None:
         # statistics already reduced per tile by the producing conv kernel's epilogue
-        register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_void_p,
-                                           c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_int,
-                                           c_void_p, c_void_p, c_void_p, c_void_p])
+        register_sig("dl4j_bn_fwd_tiles", [c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int,
+                                           c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_float, c_float,
+                                           c_int, c_void_p, c_void_p, c_void_p, c_void_p])
         register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
         wst = _ae((lib.dl4j_bn_tiles_workspace_floats(ts[1], C),), torch.float32, x.device)
-        rc = lib.dl4j_bn_fwd_tiles(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(ts[0]), ts[1], _ptr(g), _ptr(b),
+        rc = lib.dl4j_bn_fwd_tiles(dt, _ptr(xr), _ptr(res), _ptr(y), M, C, _ptr(ts[0]), ts[1], rpp, _ptr(g), _ptr(b),
                                    float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0,
                                    _ptr(run_mean), _ptr(run_var), float(decay), float(eps), 1 if relu else 0,
                                    _ptr(wst), _ptr(ctx), _ptr(mask), _stream())
@@ -397,6 +397,18 @@ def bn_fwd(x, gamma, beta, run_mean, run_var, training, decay, eps, relu, residu
     return y, ("NATIVE", x, ctx, relu, M, C, res, mask)
 
 
+def _tile_rpp(ts, M, C):
+    """Rows per partial of a producer's BN tile statistics ``(planes [3, P, C], P[, rpp])`` that cover the M rows of
+    this BN input, else None: 64-row partials (the implicit-GEMM / GEMM epilogues, P = 2 * ceil(M / 128)) or one
+    partial per chunk of rpp rows (dl4j_conv_halo, P = ceil(M / rpp))."""
+    if ts is None or ts[0].shape[2] != C:
+        return None
+    rpp = ts[2] if len(ts) > 2 else 64
+    if rpp == 64:
+        return 64 if ts[1] == 2 * ((M + 127) // 128) else None
+    return rpp if ts[1] == (M + rpp - 1) // rpp else None
+
+
 def _bn_fwd_rbn(lib, x, xr, dt, M, C, gamma, beta, run_mean, run_var, decay, eps, residual, rctx):
     """Residual BN apply with the shortcut BN folded in (csrc/batchnorm.hip dl4j_bn_fwd_rbn)."""
     y = _like_rows(x)
@@ -406,10 +418,11 @@ def _bn_fwd_rbn(lib, x, xr, dt, M, C, gamma, beta, run_mean, run_var, decay, eps
     res = _rows_like(residual, x)
     mask = _ae((M * C // 8,), torch.uint8, x.device)
     ts = getattr(x, "_bn_tile_stats", None)
-    tiles = ts is not None and ts[0].shape[2] == C and ts[1] == 2 * ((M + 127) // 128) and (len(ts) < 3 or ts[2] == 64)
+    rpp = _tile_rpp(ts, M, C)
+    tiles = rpp is not None
     register_sig("dl4j_bn_fwd_rbn", [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p,
                                      c_float, c_float, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_ll, c_void_p])
+                                     c_void_p, c_void_p, c_ll, c_int, c_void_p])
     if tiles:
         register_sig("dl4j_bn_tiles_workspace_floats", [c_ll, c_int])
         lib.dl4j_bn_tiles_workspace_floats.restype = c_ll
@@ -419,7 +432,7 @@ def _bn_fwd_rbn(lib, x, xr, dt, M, C, gamma, beta, run_mean, run_var, decay, eps
     rc = lib.dl4j_bn_fwd_rbn(dt, _ptr(xr), _ptr(res), _ptr(rctx), _ptr(y), M, C, _ptr(g), _ptr(b),
                              float(gamma) if g is None else 1.0, float(beta) if b is None else 0.0, _ptr(run_mean),
                              _ptr(run_var), float(decay), float(eps), _ptr(ws), _ptr(ctx), _ptr(mask),
-                             _ptr(ts[0]) if tiles else None, ts[1] if tiles else 0, _stream())
+                             _ptr(ts[0]) if tiles else None, ts[1] if tiles else 0, rpp if tiles else 0, _stream())
     _check(rc, "bn_fwd_rbn")
     return y, ("NATIVE", x, ctx, True, M, C, res, mask, rctx)
 
