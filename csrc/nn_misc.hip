@@ -1,5 +1,6 @@
 // Less common NN layers on gfx950: cross-channel LRN, counter-based (Philox-4x32-10) dropout family, embedding
-// gather / scatter-add, depthwise convolution (fwd, bwd-data, bwd-weight).
+// gather / scatter-add, the BERT input-embedding sum and its position / type gradients, depthwise convolution (fwd,
+// bwd-data, bwd-weight).
 //
 // Reference semantics:
 //   LRN            deeplearning4j-cuda CudnnLocalResponseNormalizationHelper.java:160,199 and
@@ -186,6 +187,66 @@ __global__ __launch_bounds__(256) void emb_scatter_kernel(const T* __restrict__ 
   }
 }
 
+// BERT input embedding: e[r, :] = Wword[idx[r], :] + Wpos[r % T, :] + Wtype[0, :] for r = b*T + t, summed in fp32
+// and rounded once (three gathers and two adds of the imported graph in one pass). Rows are 16-byte vectors.
+template <typename T>
+__global__ __launch_bounds__(256) void bert_embed_fwd_kernel(const T* __restrict__ Ww, const T* __restrict__ Wp,
+                                                             const T* __restrict__ Wt,
+                                                             const long long* __restrict__ idx, T* __restrict__ out,
+                                                             int rows, int Tn, int E, long long sw, long long sp,
+                                                             int V) {
+  const int lane = threadIdx.x & 63;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += gridDim.x * 4) {
+    const long long k = idx[r];
+    const bool ok = k >= 0 && k < V;
+    const T* a = Ww + (ok ? k : 0) * sw;
+    const T* p = Wp + (long long)(r % Tn) * sp;
+    T* dst = out + (long long)r * E;
+    for (int c = lane * 8; c < E; c += 512) {
+      float va[8], vp[8], vt[8];
+      Vec8<T>::load(a + c, va);
+      Vec8<T>::load(p + c, vp);
+      Vec8<T>::load(Wt + c, vt);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) va[e] = (ok ? va[e] : 0.f) + vp[e] + vt[e];
+      Vec8<T>::store(dst + c, va);
+    }
+  }
+}
+
+// Position / token-type gradients of that sum, deterministic (no atomics):
+//   gpos[t, c] = sum_b de[b*T + t, c] for t < T, 0 for T <= t < Tmax      (one thread per (t, c), c fastest)
+template <typename T>
+__global__ __launch_bounds__(256) void bert_embed_bwd_pos_kernel(const T* __restrict__ de, float* __restrict__ gpos,
+                                                                 int B, int Tn, int Tmax, int E, long long sgr,
+                                                                 long long sgc) {
+  const long long total = (long long)Tmax * E;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / E), c = (int)(i - (long long)t * E);
+    float s = 0.f;
+    if (t < Tn)
+      for (int b = 0; b < B; ++b) s += ld1<T>(de + ((long long)b * Tn + t) * E + c);
+    gpos[t * sgr + c * sgc] = s;
+  }
+}
+
+//   gtype[0, c] = sum_{t < T} gpos[t, c], gtype[j > 0, c] = 0                (after the kernel above)
+__global__ __launch_bounds__(256) void bert_embed_bwd_type_kernel(const float* __restrict__ gpos,
+                                                                  float* __restrict__ gtype, int Tn, int ntype, int E,
+                                                                  long long sgr, long long sgc, long long str,
+                                                                  long long stc) {
+  const long long total = (long long)ntype * E;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i / E), c = (int)(i - (long long)j * E);
+    float s = 0.f;
+    if (j == 0)
+      for (int t = 0; t < Tn; ++t) s += gpos[t * sgr + c * sgc];
+    gtype[j * str + c * stc] = s;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ depthwise conv
 // Channels-last activations: x [N, H, W, C], y [N, OH, OW, OC], OC = C*dm, oc = c*dm + m.
 // Weights re-laid out by the host as wr [KH*KW, OC] (fp32).
@@ -335,6 +396,32 @@ DL4J_API int dl4j_emb_scatter_add(int dt, const void* g, const long long* idx, f
   if (rows <= 0) return 0;
   DISPATCH_T(dt, hipLaunchKernelGGL(emb_scatter_kernel<T>, dim3(grid_for(rows, 4)), dim3(256), 0, s, (const T*)g, idx,
                                     dW, rows, D, sdr, sdc, V));
+  return (int)HIP_LAUNCH_CHECK();
+}
+
+// Wword / Wpos: row strides sw / sp with unit column stride; Wtype row 0 contiguous; E % 8 == 0, 16-byte aligned.
+DL4J_API int dl4j_bert_embed_fwd(int dt, const void* Ww, const void* Wp, const void* Wt, const long long* idx,
+                                 void* out, int rows, int Tn, int E, long long sw, long long sp, int V,
+                                 hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (Tn <= 0 || E % 8 || sw % 8 || sp % 8) return -1;
+  for (const void* q : {Ww, Wp, Wt, (const void*)out})
+    if (reinterpret_cast<uintptr_t>(q) & 15) return -1;
+  DISPATCH_T(dt, hipLaunchKernelGGL(bert_embed_fwd_kernel<T>, dim3(grid_for(rows, 4)), dim3(256), 0, s, (const T*)Ww,
+                                    (const T*)Wp, (const T*)Wt, idx, (T*)out, rows, Tn, E, sw, sp, V));
+  return (int)HIP_LAUNCH_CHECK();
+}
+
+// de [B*T, E] contiguous; gpos [Tmax, E] and gtype [ntype, E] fp32 views with element strides (row, col).
+DL4J_API int dl4j_bert_embed_bwd_pt(int dt, const void* de, float* gpos, float* gtype, int B, int Tn, int Tmax, int E,
+                                    long long sgr, long long sgc, int ntype, long long str, long long stc,
+                                    hipStream_t s) {
+  if (B <= 0 || Tn <= 0 || Tn > Tmax || E <= 0) return -1;
+  DISPATCH_T(dt, hipLaunchKernelGGL(bert_embed_bwd_pos_kernel<T>, dim3(grid_for((long long)Tmax * E)), dim3(256), 0,
+                                    s, (const T*)de, gpos, B, Tn, Tmax, E, sgr, sgc));
+  if (gtype && ntype > 0)
+    hipLaunchKernelGGL(bert_embed_bwd_type_kernel, dim3(grid_for((long long)ntype * E)), dim3(256), 0, s, gpos, gtype,
+                       Tn, ntype, E, sgr, sgc, str, stc);
   return (int)HIP_LAUNCH_CHECK();
 }
 

@@ -381,7 +381,8 @@ class LSTMImpl(BaseRecurrentImpl):
         # the layer below takes its gate deltas from _stack_dz: a zero-cost placeholder stands in for its epsilon.
         # It is marked, so that a layer below that does NOT find the matching _stack_dz (its cache was replaced by a
         # re-run forward in between) raises instead of silently training on a zero gradient.
-        ph = torch.zeros((), dtype=eps.dtype, device=eps.device).expand(mb, H, T)
+        from ...ops import nd4j_kernels as NK
+        ph = NK.zero_(torch.empty((), dtype=eps.dtype, device=eps.device)).expand(mb, H, T)
         ph._dl4j_stack_placeholder = True
         return self.make_gradient(), ph
 

@@ -207,10 +207,14 @@ class BertEmbeddingLayerImpl(LayerImpl):
         idx = x.long()
         B, T = idx.shape
         dt = self.W("Wword").dtype
-        e = self.W("Wword")[idx.reshape(-1)] + self.W("Wpos")[:T].repeat(B, 1) + self.W("Wtype")[0].reshape(1, -1)
-        y, ln = _ln_fwd(e.to(dt).contiguous(), None, self.params["lng"], self.params["lnb"], c.layerNormEps)
+        from ...ops import nn_misc
+        e = nn_misc.bert_embed_forward(self.W("Wword"), self.W("Wpos"), self.W("Wtype"), idx) if idx.is_cuda else None
+        if e is None:
+            e = self.W("Wword")[idx.reshape(-1)] + self.W("Wpos")[:T].repeat(B, 1) + self.W("Wtype")[0].reshape(1, -1)
+            e = e.to(dt).contiguous()
+        y, ln = _ln_fwd(e, None, self.params["lng"], self.params["lnb"], c.layerNormEps)
         if training:
-            self._c = (idx, e.to(dt).contiguous(), ln, B, T)
+            self._c = (idx, e, ln, B, T)
         return y.reshape(B, T, -1).permute(0, 2, 1)
 
     def backpropGradient(self, eps, **kw):
@@ -219,6 +223,19 @@ class BertEmbeddingLayerImpl(LayerImpl):
         dy = _token_major(eps).to(e.dtype)
         g = self.grads
         de = _ln_bwd(dy, e, None, self.params["lng"], ln, g["lng"], g["lnb"])
+        from ...ops import nd4j_kernels as NK
+        from ...ops import nn_misc
+        if de.is_cuda and g["Wword"].dtype == torch.float32:
+            # word rows: scatter-add of the 16-bit row gradients into the fp32 view (in-tree kernel, no fp32 copy
+            # of de); position / type rows: deterministic column sums written in place
+            if getattr(self.net, "_grads_zeroed", False):
+                nn_misc.embedding_backward_(g["Wword"], idx, de)     # flat gradient already cleared this step
+            else:
+                gw = NK.zero_(torch.empty_like(g["Wword"]))
+                nn_misc.embedding_backward_(gw, idx, de)
+                copy_grad_(g["Wword"], gw)
+            if nn_misc.bert_embed_backward_pt(de.contiguous(), g["Wpos"], g["Wtype"], B, T):
+                return self.make_gradient(), None
         de = de.to(g["Wword"].dtype)
         if getattr(self.net, "_grads_zeroed", False) and g["Wword"].is_contiguous():
             g["Wword"].index_add_(0, idx.reshape(-1), de)          # flat gradient already cleared this step
@@ -241,19 +258,41 @@ class BertEmbeddingLayerImpl(LayerImpl):
 
 class BertPoolerLayerImpl(LayerImpl):
     def activate(self, x, training=False, mask=None, **kw):
+        from ...ops import nd4j_kernels as NK
         self.input = x
         x0 = x[:, :, 0].to(self.W("W").dtype)
-        y = matmul(x0, self.W("W"), bias=self.Wbias("b"), act="tanh")
+        if training and x0.is_cuda:
+            # keep the pre-activation: backward is eps * tanh'(z) on the in-tree derivative kernel (the GEMM
+            # epilogue stores a pre-activation for GELU only)
+            z = matmul(x0, self.W("W"), bias=self.Wbias("b"))
+            y = NK.transform(z, "tanh")
+            if y is not None:
+                self._c = (x0, z, None, x.shape)
+                return y
+            y = torch.tanh(z)
+        else:
+            y = matmul(x0, self.W("W"), bias=self.Wbias("b"), act="tanh")
         if training:
-            self._c = (x0, y, x.shape)
+            self._c = (x0, None, y, x.shape)
         return y
 
     def backpropGradient(self, eps, **kw):
-        x0, y, shape = self._c
+        from ...ops import nd4j_kernels as NK
+        x0, z, y, shape = self._c
         self._c = None
-        dz = (eps.to(y.dtype) * (1 - y * y))
+        dz = NK.transform_bp(z, eps.to(z.dtype), "tanh") if z is not None else None
+        if dz is None:
+            y = torch.tanh(z) if y is None else y
+            dz = eps.to(y.dtype) * (1 - y * y)
         _wgrad(self.grads["W"], x0, dz)
         _bsum(self.grads["b"], dz)
+        B, E, T = shape
+        if x0.is_cuda:
+            # token-major [B, T, E] storage returned as a [B, E, T] view, so the encoder below reads it without a
+            # transposing copy; only token 0 receives a gradient
+            dxt = NK.zero_(torch.empty((B, T, E), dtype=x0.dtype, device=x0.device))
+            mmul(dz, self.W("W").t(), out=dxt[:, 0, :])
+            return self.make_gradient(), dxt.permute(0, 2, 1)
         dx = torch.zeros(shape, dtype=x0.dtype, device=x0.device)
         dx[:, :, 0] = matmul(dz, self.W("W").t())
         return self.make_gradient(), dx

@@ -509,8 +509,10 @@ class BaseNetwork:
                     torch.is_tensor(lp) and lp.numel() == 1:
                 # score = loss + reg / minibatch on one in-tree block (no library elementwise kernels)
                 self._score_t = _native.score_reduce(reg, 0.0, 1.0 / mb_local, reg=lp.reshape(1), reg_scale=1.0)
+            elif reg is None:
+                self._score_t = lp                  # no regularisation term: the loss part is the score
             else:
-                self._score_t = lp + (reg[0] / mb_local if reg is not None else 0.0)
+                self._score_t = lp + reg[0] / mb_local
             self._loss_part = None
             self._score_val = None
         for _, _, impl, _ in self._layer_offsets:
@@ -601,6 +603,13 @@ class BaseNetwork:
             import numpy as np
             t = torch.from_numpy(np.asarray(t))
         t = t.to(self.device, non_blocking=True)
+        if dtype is not None and t.is_floating_point() and t.dtype != dtype and t.is_cuda:
+            # cast (and, for images, NCHW -> channels-last) in one in-tree strided-copy launch
+            from ..ops import nd4j_kernels as NK
+            src = t.permute(0, 2, 3, 1) if t.dim() == 4 else t
+            c = NK.cast_pad_last(src, dtype, src.shape[-1]) if t.dim() > 0 and t.numel() else None
+            if c is not None:
+                t = c.permute(0, 3, 1, 2) if t.dim() == 4 else c
         if dtype is not None and t.is_floating_point():
             t = t.to(dtype)
         if t.dim() == 4 and t.is_cuda:

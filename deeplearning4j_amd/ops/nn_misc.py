@@ -27,6 +27,10 @@ _SIGS = {
                      c_float, c_float, c_void_p],
     "dl4j_emb_gather": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_ll, c_ll, c_int, c_void_p],
     "dl4j_emb_scatter_add": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_ll, c_ll, c_int, c_void_p],
+    "dl4j_bert_embed_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_ll,
+                            c_int, c_void_p],
+    "dl4j_bert_embed_bwd_pt": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_ll, c_ll, c_int, c_ll,
+                               c_ll, c_void_p],
     "dl4j_dwconv_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "dl4j_dwconv_bwd_data": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "dl4j_dwconv_bwd_weight": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -182,6 +186,35 @@ def embedding_backward_(dW, idx, g):
     note(g, "embedding", f"scatter {g.dtype}")
     dW.index_add_(0, flat.long(), g2.to(dW.dtype))
     return dW
+
+
+def bert_embed_forward(Ww, Wp, Wt, idx):
+    """[B*T, E] = Wword[idx] + Wpos[t] + Wtype[0] for token ids ``idx`` [B, T] in one HIP pass (fp32 sum, one rounding);
+    None when the kernel does not take these operands (the caller sums with torch)."""
+    B, T = idx.shape
+    E = Ww.shape[1]
+    if not (use_native(Ww, "embedding") and _dt(Ww) is not None and Ww.dtype == Wp.dtype == Wt.dtype and
+            Ww.dim() == Wp.dim() == Wt.dim() == 2 and Ww.stride(1) == Wp.stride(1) == Wt.stride(1) == 1 and
+            Wp.shape[0] >= T and Wp.shape[1] == Wt.shape[1] == E):
+        return None
+    fi = idx.reshape(-1).to(torch.int64).contiguous()
+    out = torch.empty((B * T, E), dtype=Ww.dtype, device=Ww.device)
+    rc = _lib().dl4j_bert_embed_fwd(_dt(Ww), _p(Ww), _p(Wp), _p(Wt), _p(fi), _p(out), B * T, T, E, Ww.stride(0),
+                                    Wp.stride(0), Ww.shape[0], _s())
+    return out if rc == 0 else None
+
+
+def bert_embed_backward_pt(de, gpos, gtype, B, T):
+    """Position gradient gpos [Tmax, E] (rows >= T zeroed) and token-type gradient gtype [ntype, E] (row 0 = sum of
+    every row of de [B*T, E], other rows zeroed), written into fp32 gradient views; False when not taken."""
+    if not (use_native(de, "embedding") and _dt(de) is not None and de.is_contiguous() and
+            gpos.dtype == gtype.dtype == torch.float32 and gpos.dim() == gtype.dim() == 2 and
+            gpos.shape[1] == gtype.shape[1] == de.shape[1] and gpos.shape[0] >= T):
+        return False
+    rc = _lib().dl4j_bert_embed_bwd_pt(_dt(de), _p(de), _p(gpos), _p(gtype), B, T, gpos.shape[0], de.shape[1],
+                                       gpos.stride(0), gpos.stride(1), gtype.shape[0], gtype.stride(0),
+                                       gtype.stride(1), _s())
+    return rc == 0
 
 
 # ------------------------------------------------------------------------------------------------ depthwise conv

@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-from . import native
+from . import native, nd4j_kernels
 from ..memory import arena
 from .native import _check, _ptr, _stream, c_int, c_void_p
 
@@ -392,7 +392,7 @@ def lstm_bwd_prep(dz, out, h0, call, c0, peephole, dtype):
     native.register_sig("dl4j_lstm_bwd_prep", [c_int] + [c_void_p] * 9 + [c_int, c_int, c_int, c_int, c_void_p])
     dzb = torch.empty(R, G, dtype=dtype, device=dz.device)
     hpb = torch.empty(R, H, dtype=dtype, device=dz.device)
-    acc = torch.zeros(G + 3 * H, dtype=torch.float32, device=dz.device)   # one fill for both atomic accumulators
+    acc = nd4j_kernels.zero_(torch.empty(G + 3 * H, dtype=torch.float32, device=dz.device))   # both accumulators
     db, dpeep = acc[:G], acc[G:].view(3, H)
     dzc, oc, cc = dz.contiguous(), out.contiguous(), call.contiguous()
     h0f, c0f = _f32c(h0), _f32c(c0)

@@ -8,14 +8,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _step_kernels(net, x, y, steps=1):
+def _step_kernels(net, x, y, steps=1, step=None):
     from torch.profiler import ProfilerActivity, profile
-    net.fit([x], [y])                      # warm-up: autotuners / kernel-choice database, arena sizing
-    net.fit([x], [y])
+    step = step or (lambda: net.fit([x], [y]))
+    step()                                 # warm-up: autotuners / kernel-choice database, arena sizing
+    step()
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         for _ in range(steps):
-            net.fit([x], [y])
+            step()
         torch.cuda.synchronize()
     out = []
     for e in prof.events():
@@ -41,6 +42,43 @@ def test_fill_kernel():
     x = torch.ones(4, 8, 5, 5, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     NK.zero_(x)
     assert torch.count_nonzero(x) == 0
+
+
+def _audit(ks, what):
+    assert len(ks) > 20, what
+    torch_ks = sorted({n for n, _ in ks if _is_torch_kernel(n)})
+    t_all = sum(t for _, t in ks)
+    t_torch = sum(t for n, t in ks if _is_torch_kernel(n))
+    print(f"{what}: {len(ks)} kernels, {len(torch_ks)} distinct torch kernels, {100 * t_torch / max(t_all, 1):.2f} % "
+          f"of time")
+    for n in torch_ks:
+        print("  torch:", n[:140])
+    assert not torch_ks, f"torch compute kernels in the {what} step: {torch_ks[:6]}"
+
+
+def test_bert_step_launches_no_torch_compute_kernels():
+    """BertBase fine-tuning step (tools/bench_bert.py's model; 2 encoder layers, seq 128, bf16)."""
+    from deeplearning4j_amd.models import BertBase
+    from deeplearning4j_amd.nn.conf import DataType
+    net = BertBase(numLabels=2, inputShape=[128], layers=2, dataType=DataType.BFLOAT16).init(device=torch.device("cuda", 0))
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randint(0, 30522, (8, 128), generator=g).cuda()
+    y = torch.nn.functional.one_hot(torch.randint(0, 2, (8,), generator=g), 2).float().cuda()
+    _audit(_step_kernels(net, x, y), "BERT")
+
+
+def test_lstm_char_lm_step_launches_no_torch_compute_kernels():
+    """TextGenerationLSTM (tools/bench_lstm.py's model, 2x GravesLSTM-256, TBPTT 50, bf16), eager so the profiler sees
+    every launch: one fit over two TBPTT windows."""
+    from deeplearning4j_amd.models import TextGenerationLSTM
+    from deeplearning4j_amd.nn.conf import DataType
+    net = TextGenerationLSTM(numLabels=77, inputShape=[1, 77], hidden=256,
+                             dataType=DataType.BFLOAT16).init(device=torch.device("cuda", 0))
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randint(0, 77, (8, 101), generator=g)
+    x = torch.nn.functional.one_hot(idx[:, :-1], 77).permute(0, 2, 1).float().cuda()
+    y = torch.nn.functional.one_hot(idx[:, 1:], 77).permute(0, 2, 1).float().cuda()
+    _audit(_step_kernels(net, x, y, step=lambda: net.fit(x, y)), "LSTM char-LM")
 
 
 def test_resnet50_step_launches_no_torch_compute_kernels():
