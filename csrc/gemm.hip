@@ -372,6 +372,49 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g) {
   }
 }
 
+// Deep split-K reduce: few outputs, many slabs (long-K weight gradients of small layers, e.g. 20 x 25 over 50k
+// pixels in 242 slabs, where one thread per output quad serialised 242 loads: 92 us). A block owns 16 output quads;
+// its 16 slab groups sum slabs grp, grp+16, ... with eight loads in flight, then combine through LDS in group order
+// (fixed order: bitwise reproducible).
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_deep(GemmArgs g) {
+  const long long MN = (long long)g.M * g.N;
+  const int nq = (g.N + 3) / 4;
+  const long long total = (long long)g.M * nq;
+  const int ql = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long long q = (long long)blockIdx.x * 16 + ql;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  int m = 0, n = 0;
+  if (q < total) {
+    m = (int)(q / nq);
+    n = (int)(q - (long long)m * nq) * 4;
+    const float* base = g.ws + (long long)m * g.N + n;
+    for (int z0 = grp; z0 < g.splits; z0 += 16 * 8) {
+      float t[8][4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int z = z0 + 16 * u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[u][j] = (z < g.splits && n + j < g.N) ? base[(long long)z * MN + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += t[u][j];
+    }
+  }
+  __shared__ float red[16][16][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[grp][ql][j] = v[j];
+  __syncthreads();
+  if (grp == 0 && q < total) {
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += red[k][ql][j];
+    store4(g, g.C, g.Z, m, n, o);
+  }
+}
+
 // ----------------------------------------------------------------------------------------------- 8-phase kernel
 // 256 x 256 x 64 tile, 8 waves (2 along M x 4 along N, 128 x 64 outputs each), v_mfma_f32_16x16x32, LDS-DMA staging
 // in half-tiles with loads kept in flight across barriers (guide §5 "The 256² 8-phase template", T2-T5).
@@ -925,15 +968,20 @@ __global__ __launch_bounds__(256) void gemm_f32t(GemmArgs g, SimpleArgs s) {
 }
 
 // tile (64 or 128) and split count for the tiled exact-fp32 kernel: fill the 256 CUs with >= 256-deep K slices
+// Tile and split-K count of the exact-fp32 kernel. Each K-step of a block waits on its own global loads, so the
+// kernel needs several blocks per CU to hide load latency: split K until ~768 blocks are in flight, keeping >= 48
+// K-elements per slab (tools/f32_gemm_probe.py on the LeNet shapes: conv2 forward 77 -> 39 us with 4 splits, its
+// weight gradient 77 -> 39-51 us with 96-128, dense forward / data gradient 2-3x faster). 128-wide tiles only for
+// large problems (they lost on every LeNet shape).
 void plan_f32(int M, int N, int K, int batch, int* tile, int* splits) {
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64) * batch;
-  *tile = (t128 >= 128) ? 128 : 64;
+  *tile = (t128 >= 512) ? 128 : 64;
   const long long t = *tile == 128 ? t128 : t64;
   int sp = 1;
-  if (batch == 1 && t < 256) {
-    sp = (int)((256 + t - 1) / t);
-    const int maxs = K / 256;
+  if (batch == 1 && t < 768) {
+    sp = (int)((768 + t - 1) / t);
+    const int maxs = K / 48;
     if (sp > maxs) sp = maxs;
     if (sp > 256) sp = 256;
     if (sp < 1) sp = 1;
@@ -1261,6 +1309,10 @@ DL4J_API int dl4j_gemm_f32(int in_dt, int out_dt, int M, int N, int K, int batch
   int e = (int)hipGetLastError();
   if (e || splits <= 1) return e;
   const long long total = (long long)M * ((N + 3) / 4);
+  if (splits >= 16) {
+    hipLaunchKernelGGL(gemm_splitk_reduce_deep, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, s, g);
+    return (int)hipGetLastError();
+  }
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g);

@@ -13,6 +13,8 @@
 //   strided_copy  out (contiguous, rank <= 8) = x at arbitrary (incl. 0 / negative) strides, optional zero padding
 //                 per dim: reverse, permute materialisation, space<->depth, space<->batch, nearest upsampling
 //   mergemax      elementwise max over up to 8 inputs + argmax bytes; mergemax_bp routes eps to the argmax input
+//   im2col_rows / col2im_rows   row-per-output-pixel im2col (padding in the same pass) and its gather-form adjoint
+//                 onto a channels-last image: the exact-fp32 conv as three single GEMMs (ops/conv.py)
 // dtype codes: 0 fp32, 1 bf16, 2 fp16 (fp32 math everywhere).
 #include "common.h"
 
@@ -491,6 +493,67 @@ __global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ cols,
   }
 }
 
+// ------------------------------------------------------------------------------------------------ im2col rows
+// Row-per-output-pixel im2col for the exact-fp32 conv (one GEMM over all images instead of one per image):
+//   cols[(n*OH + oh)*OW + ow][(c*R + r)*S + q] = x[n][c][oh*sh + r*dh - pt][ow*sw + q*dw - pl]   (0 outside)
+// x at element strides (sN, sC, sH, sW): NCHW or channels-last; the column order (c, r, q) matches the weight
+// [K][C][R][S] reshaped to [K][C*R*S], so no weight copy is needed.
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_rows_kernel(const T* __restrict__ x, T* __restrict__ cols, int N, int C,
+                                                          int H, int W, long long sN, long long sC, long long sH,
+                                                          long long sW, int R, int S, int sh, int sw, int pt, int pl,
+                                                          int dh, int dw, int OH, int OW) {
+  const long long CRS = (long long)C * R * S;
+  const long long total = (long long)N * OH * OW * CRS;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long long row = i / CRS;
+    const int col = (int)(i - row * CRS);
+    const int q = col % S, r = (col / S) % R, c = col / (R * S);
+    const int ow = (int)(row % OW);
+    const long long t = row / OW;
+    const int oh = (int)(t % OH);
+    const long long n = t / OH;
+    const int h = oh * sh + r * dh - pt, w = ow * sw + q * dw - pl;
+    const bool in = h >= 0 && h < H && w >= 0 && w < W;
+    stf(cols, i, in ? ldf(x, n * sN + c * sC + h * sH + w * sW) : 0.f);
+  }
+}
+
+// Adjoint of im2col_rows onto the UNPADDED image, written channels-last: dx[n][h][w][c] = sum of the dcols entries
+// whose window tap lands on (h, w). Gather form (no atomics, deterministic), channel index fastest.
+template <typename T>
+__global__ __launch_bounds__(256) void col2im_rows_kernel(const T* __restrict__ cols, T* __restrict__ dx, int N, int C,
+                                                          int H, int W, int R, int S, int sh, int sw, int pt, int pl,
+                                                          int dh, int dw, int OH, int OW) {
+  const long long CRS = (long long)C * R * S;
+  const long long total = (long long)N * H * W * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const long long n = t / H;
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const int ohn = h + pt - r * dh;
+      if (ohn < 0 || ohn % sh) continue;
+      const int oh = ohn / sh;
+      if (oh >= OH) continue;
+      for (int q = 0; q < S; ++q) {
+        const int own = w + pl - q * dw;
+        if (own < 0 || own % sw) continue;
+        const int ow = own / sw;
+        if (ow >= OW) continue;
+        acc += ldf(cols, ((n * OH + oh) * OW + ow) * CRS + ((long long)c * R + r) * S + q);
+      }
+    }
+    stf(dx, i, acc);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ mergemax
 struct PtrList {
   const void* p[8];
@@ -705,6 +768,34 @@ DL4J_API int dl4j_col2im(int dt, const void* cols, void* x, int N, int C, int Hp
   const int g = grid1((long long)N * C * Hp * Wp);
 #define L(T) hipLaunchKernelGGL((col2im_kernel<T>), dim3(g), dim3(256), 0, s, (const T*)cols, (T*)x, N, C, Hp, Wp, R, S, \
                                 sh, sw, dh, dw, OH, OW)
+  DT_DISPATCH(dt, L);
+#undef L
+  return (int)hipGetLastError();
+}
+
+// cols [N*OH*OW][C*R*S] <- x [N][C][H][W] at element strides st[4] = (sN, sC, sH, sW); geometry g[12] =
+// {R, S, sh, sw, pt, pl, dh, dw, OH, OW, H, W}.
+DL4J_API int dl4j_im2col_rows(int dt, const void* x, void* cols, int N, int C, const long long* st, const int* g,
+                              hipStream_t s) {
+  const int R = g[0], S = g[1], sh = g[2], sw = g[3], pt = g[4], pl = g[5], dh = g[6], dw = g[7], OH = g[8],
+            OW = g[9], H = g[10], W = g[11];
+  if (sh < 1 || sw < 1 || dh < 1 || dw < 1 || R < 1 || S < 1 || OH < 1 || OW < 1) return -1;
+  const int gr = grid1((long long)N * OH * OW * C * R * S);
+#define L(T) hipLaunchKernelGGL((im2col_rows_kernel<T>), dim3(gr), dim3(256), 0, s, (const T*)x, (T*)cols, N, C, H, W, \
+                                st[0], st[1], st[2], st[3], R, S, sh, sw, pt, pl, dh, dw, OH, OW)
+  DT_DISPATCH(dt, L);
+#undef L
+  return (int)hipGetLastError();
+}
+
+// dx [N][H][W][C] (channels-last, unpadded) <- dcols [N*OH*OW][C*R*S]; same geometry array as dl4j_im2col_rows.
+DL4J_API int dl4j_col2im_rows(int dt, const void* cols, void* dx, int N, int C, const int* g, hipStream_t s) {
+  const int R = g[0], S = g[1], sh = g[2], sw = g[3], pt = g[4], pl = g[5], dh = g[6], dw = g[7], OH = g[8],
+            OW = g[9], H = g[10], W = g[11];
+  if (sh < 1 || sw < 1 || dh < 1 || dw < 1 || R < 1 || S < 1) return -1;
+  const int gr = grid1((long long)N * H * W * C);
+#define L(T) hipLaunchKernelGGL((col2im_rows_kernel<T>), dim3(gr), dim3(256), 0, s, (const T*)cols, (T*)dx, N, C, H, W, \
+                                R, S, sh, sw, pt, pl, dh, dw, OH, OW)
   DT_DISPATCH(dt, L);
 #undef L
   return (int)hipGetLastError();

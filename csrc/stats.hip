@@ -146,8 +146,9 @@ DL4J_API int dl4j_segment_stats(int dtype, const void* x, const long long* off, 
 // channels-last is exactly such a matrix). Each thread owns 8 consecutive channels (one 16-byte load for bf16) of a
 // row; a block sweeps rows in a grid-stride loop and reduces through LDS into its own partial row part[block][C]
 // (plain stores); channel_sum_reduce then sums the partial rows in block order. No float atomics: bitwise
-// reproducible (DL4J_AMD_DETERMINISTIC data-parallel equivalence). Requires C % 8 == 0; channels beyond 2048 are
-// split over blockIdx.y chunks of 2048 (transformer bias gradients: 768 / 2304 / 3072 columns).
+// reproducible (DL4J_AMD_DETERMINISTIC data-parallel equivalence). C % 8 == 0: channels beyond 2048 are split over
+// blockIdx.y chunks of 2048 (transformer bias gradients: 768 / 2304 / 3072 columns); other widths take the
+// one-column-per-thread kernel below.
 // ------------------------------------------------------------------------------------------------------
 namespace {
 template <typename T>
@@ -219,9 +220,43 @@ __global__ __launch_bounds__(256) void channel_sum_reduce(const float* __restric
   if (grp == 0 && c < C) out[c] = (red[threadIdx.x] + red[threadIdx.x + 64]) + (red[threadIdx.x + 128] + red[threadIdx.x + 192]);
 }
 
+// C % 8 != 0 (LeNet's 20 / 50 / 500-wide bias gradients): one thread per column of a 256-column chunk
+// (blockIdx.y), 256 / min(C, 256) rows per block iteration, eight independent loads in flight; same partial rows.
+template <typename T>
+__global__ __launch_bounds__(256) void channel_sum_scalar_kernel(const T* __restrict__ x, long long M, int ld,
+                                                                 float* __restrict__ part) {
+  extern __shared__ float red[];
+  const int c0 = blockIdx.y * 256;
+  const int Cc = min(256, ld - c0);
+  const int Cw = min(ld, 256);                           // LDS row pitch: rows_per_iter * Cw <= 256 floats
+  const int rows_per_iter = 256 / Cw;
+  const int c = threadIdx.x % Cw, r0 = threadIdx.x / Cw;
+  float acc = 0.f;
+  if (r0 < rows_per_iter && c < Cc) {
+    long long r = (long long)blockIdx.x * rows_per_iter + r0;
+    const long long step = (long long)gridDim.x * rows_per_iter;
+    constexpr int U = 8;
+    for (; r + (U - 1) * step < M; r += U * step) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld1<T>(x + (r + u * step) * ld + c0 + c);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    for (; r < M; r += step) acc += ld1<T>(x + r * ld + c0 + c);
+  }
+  if (r0 < rows_per_iter) red[r0 * Cw + c] = acc;
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < Cc; cc += 256) {
+    float sum = 0.f;
+    for (int k = 0; k < rows_per_iter; ++k) sum += red[k * Cw + cc];
+    part[(long long)blockIdx.x * ld + c0 + cc] = sum;
+  }
+}
+
 int channel_sum_blocks(long long M, int C) {
   const int Cc = C < 2048 ? C : 2048;                    // widest chunk; the last chunk may be narrower
-  const int rows_per_iter = 256 / (Cc / 8);
+  const int rows_per_iter = C % 8 ? 256 / (C < 256 ? C : 256) : 256 / (Cc / 8);
   long long blocks = (M + rows_per_iter * 32 - 1) / (rows_per_iter * 32);
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
@@ -234,9 +269,20 @@ DL4J_API long long dl4j_channel_sum_ws_floats(long long M, int C) { return (long
 
 // ws: >= dl4j_channel_sum_ws_floats(M, C) fp32 scratch.
 DL4J_API int dl4j_channel_sum(int dtype, const void* x, long long M, int C, float* out, float* ws, hipStream_t stream) {
-  if (C % 8 != 0 || M <= 0 || !ws) return -1;
+  if (C <= 0 || M <= 0 || !ws) return -1;
   const int blocks = channel_sum_blocks(M, C);
   const size_t lds = sizeof(float) * 256 * 8;             // >= rows_per_iter * chunk width for every chunk
+  if (C % 8) {
+    const dim3 gs((unsigned)blocks, (C + 255) / 256);
+    if (dtype == 1)
+      hipLaunchKernelGGL(channel_sum_scalar_kernel<bf16>, gs, dim3(256), lds, stream, (const bf16*)x, M, C, ws);
+    else if (dtype == 2)
+      hipLaunchKernelGGL(channel_sum_scalar_kernel<f16>, gs, dim3(256), lds, stream, (const f16*)x, M, C, ws);
+    else
+      hipLaunchKernelGGL(channel_sum_scalar_kernel<float>, gs, dim3(256), lds, stream, (const float*)x, M, C, ws);
+    hipLaunchKernelGGL(channel_sum_reduce, dim3((C + 63) / 64), dim3(256), 0, stream, ws, blocks, C, out);
+    return (int)hipGetLastError();
+  }
   const dim3 grid((unsigned)blocks, (C + 2047) / 2048);
   if (dtype == 1)
     hipLaunchKernelGGL(channel_sum_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)x, M, C, ws);

@@ -42,6 +42,12 @@ class CnnToFeedForwardPreProcessor(InputPreProcessor):
         if x.dim() == 2:
             return x
         self._shape = x.shape
+        if x.is_cuda and not x.is_contiguous():
+            # NCHW flatten order (the reference's c-order reshape) of a channels-last activation: one in-tree copy
+            from ...ops import nd4j_kernels as NK
+            y = NK.materialize(x)
+            if y is not None:
+                return y.reshape(x.shape[0], -1)
         return x.reshape(x.shape[0], -1)
 
     def backprop(self, eps, miniBatchSize):

@@ -233,7 +233,7 @@ def bias_grad_(view, delta):
             return
     if delta.is_cuda and delta.dim() == 2 and delta.dtype in (torch.float32, torch.bfloat16, torch.float16) \
             and delta.is_contiguous() \
-            and view.dtype == torch.float32 and view.is_contiguous() and delta.shape[1] % 8 == 0:
+            and view.dtype == torch.float32 and view.is_contiguous():
         from ...ops import native
         if native.channel_sum(delta, out=view.reshape(-1)) is not None:
             return

@@ -18,7 +18,11 @@ from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 def _cl(x):
     if x.is_cuda and x.dim() == 4:
-        return x.contiguous(memory_format=torch.channels_last)
+        if x.is_contiguous(memory_format=torch.channels_last):
+            return x
+        from ...ops import nd4j_kernels as NK
+        y = NK.channels_last_copy(x)                              # in-tree strided copy, no library kernel
+        return y if y is not None else x.contiguous(memory_format=torch.channels_last)
     return x
 
 

@@ -6,8 +6,8 @@ CudnnConvolutionHelper contract, CUDA:convolution/CudnnConvolutionHelper.java:29
 asymmetric padding is exact.
 
 GPU: bf16 / fp16 implicit-GEMM HIP kernels on MFMA (``csrc/conv_gemm.hip``, ``conv_igemm.hip``, ``conv_wrw.hip``)
-when the shape is supported; fp32 convs as im2col / col2im on the in-tree strided-copy and gather kernels
-(``csrc/nd4j_ops.hip``) + the in-tree exact-fp32 MFMA GEMM; anything else takes the library path and is counted
+when the shape is supported; fp32 convs as row-per-pixel im2col / col2im kernels (``csrc/nd4j_ops.hip``) + one
+in-tree exact-fp32 MFMA GEMM per product; anything else takes the library path and is counted
 (ops/fallback.py).
 CPU: torch reference (fp32/fp64).
 """
@@ -26,51 +26,65 @@ def _fp32_gemm_ok(x, groups):
     return x.is_cuda and x.dtype == torch.float32 and groups == 1 and x.dim() == 4 and use_native(x, "conv")
 
 
-def _fp32_conv_fwd(x, w, b, stride, pad4, dilation):
-    """fp32 conv on the GPU without the library: im2col (zero-pad + strided-copy kernels, ops/nd4j_kernels.py) + the
-    in-tree exact-fp32 MFMA GEMM (ops/gemm.py) + the broadcast-add kernel for the bias."""
-    from . import nd4j_kernels as K
-    from .gemm import mmul
-    Kc, _, R, S = w.shape
-    cols = K.im2col(x, R, S, stride, pad4, dilation)
-    if cols is None:
-        return None
-    N = x.shape[0]
+def _out_hw(x, R, S, stride, pad4, dilation):
     pt, pb, pl, pr = pad4
     OH = (x.shape[2] + pt + pb - dilation[0] * (R - 1) - 1) // stride[0] + 1
     OW = (x.shape[3] + pl + pr - dilation[1] * (S - 1) - 1) // stride[1] + 1
-    y = mmul(w.reshape(Kc, -1).to(torch.float32), cols)                                          # [N, K, L]
-    y = y.reshape(N, Kc, OH, OW)
-    if b is not None:
-        yb = K.binary(y, b.reshape(1, -1, 1, 1).to(y.dtype).contiguous(), "add")
-        y = yb if yb is not None else y + b.reshape(1, -1, 1, 1).to(y.dtype)
-    return y
+    return OH, OW
+
+
+def _fp32_conv_fwd(x, w, b, stride, pad4, dilation):
+    """fp32 conv on the GPU without the library: row-per-pixel im2col (one in-tree kernel, padding included) and ONE
+    exact-fp32 MFMA GEMM over every image, ``[N*OH*OW, C*R*S] x [C*R*S, K]`` with the bias in its epilogue; the
+    output is that product viewed channels-last (no layout copy). Reference: ConvolutionLayer.java:290-428 (im2col +
+    gemm, one GEMM per minibatch)."""
+    from . import nd4j_kernels as K
+    from .gemm import mmul
+    Kc, C, R, S = w.shape
+    N = x.shape[0]
+    OH, OW = _out_hw(x, R, S, stride, pad4, dilation)
+    if OH < 1 or OW < 1:
+        return None
+    cols = K.im2col_rows(x, R, S, stride, pad4, dilation, OH, OW)
+    if cols is None:
+        return None
+    y = mmul(cols, w.reshape(Kc, -1).to(torch.float32).t(),
+             bias=None if b is None else b.reshape(-1).to(torch.float32))                     # [N*OH*OW, K]
+    return y.reshape(N, OH, OW, Kc).permute(0, 3, 1, 2)
 
 
 def _fp32_conv_bwd(x, w, dy, stride, pad4, dilation, need_dx, need_dw, need_db):
+    """Backward of ``_fp32_conv_fwd``: dX = col2im_rows(dY · W) (gather form, channels-last, no atomics),
+    dW = dYᵀ · im2col_rows(X) (one GEMM, the pixel dimension is its K), db = column sums of dY."""
     from . import nd4j_kernels as K
     from .gemm import mmul
-    pt, pb, pl, pr = pad4
     N, C, H, W = x.shape
-    Hp, Wp = H + pt + pb, W + pl + pr
     Kc, _, R, S = w.shape
     OH, OW = dy.shape[2], dy.shape[3]
-    L = OH * OW
-    dy3 = dy.reshape(N, Kc, L).to(torch.float32).contiguous()
+    if dy.dtype != torch.float32:
+        return None
+    dyr = dy.permute(0, 2, 3, 1)
+    if not dyr.is_contiguous():
+        dyr = K.materialize(dyr)
+        if dyr is None:
+            return None
+    dy2 = dyr.reshape(N * OH * OW, Kc)
+    w2 = w.reshape(Kc, -1).to(torch.float32)
     dx = dw = db = None
     if need_dx:
-        dcols = mmul(w.reshape(Kc, -1).t().to(torch.float32), dy3)                              # [N, CRS, L]
-        dxp = K.col2im(dcols, N, C, Hp, Wp, R, S, stride, dilation, OH, OW)
-        if dxp is None:
+        dx = K.col2im_rows(mmul(dy2, w2), N, C, H, W, R, S, stride, pad4, dilation, OH, OW)
+        if dx is None:
             return None
-        dx = K.materialize(dxp[:, :, pt:pt + H, pl:pl + W]) if any(pad4) else dxp
     if need_dw:
-        cols = K.im2col(x, R, S, stride, pad4, dilation)
+        cols = K.im2col_rows(x, R, S, stride, pad4, dilation, OH, OW)
         if cols is None:
             return None
-        dw = mmul(dy3.permute(1, 0, 2).reshape(Kc, N * L), cols.permute(0, 2, 1).reshape(N * L, -1)).reshape(w.shape)
+        dw = mmul(dy2.t(), cols).reshape(w.shape)
     if need_db:
-        db = K.reduce(dy3, "sum", [0, 2])
+        from . import native
+        db = native.channel_sum(dy2)
+        if db is None:
+            db = K.reduce(dy2, "sum", [0])
     return dx, dw, db
 
 

@@ -925,6 +925,10 @@ def _pad_ch(t, n, dim=1, cl=False):
     up to ``n``."""
     if t.shape[dim] == n:
         return t
+    if cl and dim == 1 and t.dim() == 4 and t.is_cuda:
+        y = nd4j_kernels.channels_last_copy(t, n)                   # pad + layout in one in-tree launch
+        if y is not None:
+            return y
     shp = list(t.shape)
     shp[dim] = n
     out = nd4j_kernels.zero_(torch.empty(shp, dtype=t.dtype, device=t.device,

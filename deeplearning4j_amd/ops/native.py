@@ -740,7 +740,7 @@ def channel_sum(rows, out=None):
     """fp32 column sums of a contiguous [M, C] fp32/bf16 CUDA matrix (dl4j_channel_sum); None if unsupported.
     ``out``: optional contiguous fp32 [C] destination (e.g. a flat-gradient view)."""
     dt = _dt16(rows)
-    if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] % 8:
+    if dt is None or rows.dim() != 2 or not rows.is_contiguous() or rows.shape[1] == 0:
         return None
     lib = load()
     register_sig("dl4j_channel_sum", [c_int, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p])

@@ -33,6 +33,8 @@ native.register_sig("dl4j_mergemax", [c_int, c_void_p, c_int, c_void_p, c_void_p
 native.register_sig("dl4j_mergemax_bp", [c_int, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p])
 native.register_sig("dl4j_fill", [c_void_p, c_ll, ctypes.c_uint, c_void_p])
 native.register_sig("dl4j_axpy", [c_int, c_void_p, c_void_p, c_ll, ctypes.c_float, c_void_p])
+native.register_sig("dl4j_im2col_rows", [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p])
+native.register_sig("dl4j_col2im_rows", [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p])
 
 DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 CALLS = __import__("collections").Counter()     # kernel launches per entry point (tests check the GPU path ran)
@@ -263,6 +265,18 @@ def cast_pad_last(v, dtype, K8, out=None):
     return y
 
 
+def channels_last_copy(x, C=None):
+    """Channels-last copy of the 4-D ``x`` (any strides) with its channel dimension zero-padded (C > channels) or
+    truncated (C < channels) to ``C``, in one strided-copy launch; None when the kernel does not take x."""
+    if not ok(x) or x.dim() != 4:
+        return None
+    c = x.shape[1]
+    C = c if C is None else int(C)
+    src = x[:, :C] if C < c else x
+    y = cast_pad_last(src.permute(0, 2, 3, 1), x.dtype, C)
+    return None if y is None else y.permute(0, 3, 1, 2)
+
+
 def pad2d(x, pads):
     """Zero padding of the last two dims of an NCHW tensor: pads = (top, bottom, left, right)."""
     if not ok(x) or x.dim() != 4:
@@ -408,6 +422,35 @@ def col2im(cols, N, C, Hp, Wp, R, S, stride, dilation, OH, OW):
     _check(native.load().dl4j_col2im(DT[cols.dtype], _ptr(cols), _ptr(x), N, C, Hp, Wp, R, S, stride[0], stride[1],
                                      dilation[0], dilation[1], OH, OW, _stream()), "col2im")
     return x
+
+
+def _rows_geom(H, W, R, S, stride, pad_tl, dilation, OH, OW):
+    return (ctypes.c_int * 12)(R, S, stride[0], stride[1], pad_tl[0], pad_tl[1], dilation[0], dilation[1], OH, OW, H,
+                               W)
+
+
+def im2col_rows(x, R, S, stride, pad4, dilation, OH, OW):
+    """[N*OH*OW, C*R*S] im2col rows (column order c, r, s) of the NCHW-logical ``x`` at any strides, zero padding in
+    the same launch; None when the kernel does not take x."""
+    if not ok(x) or x.dim() != 4:
+        return None
+    N, C, H, W = x.shape
+    cols = torch.empty((N * OH * OW, C * R * S), dtype=x.dtype, device=x.device)
+    g = _rows_geom(H, W, R, S, stride, (pad4[0], pad4[2]), dilation, OH, OW)
+    _check(native.load().dl4j_im2col_rows(DT[x.dtype], _ptr(x), _ptr(cols), N, C, _arr(x.stride()), g, _stream()),
+           "im2col_rows")
+    return cols
+
+
+def col2im_rows(dcols, N, C, H, W, R, S, stride, pad4, dilation, OH, OW):
+    """Adjoint of ``im2col_rows``: the [N, C, H, W] image gradient, channels-last, overlapping taps summed."""
+    if not ok(dcols):
+        return None
+    dcols = dcols.contiguous()
+    dx = torch.empty((N, H, W, C), dtype=dcols.dtype, device=dcols.device)
+    g = _rows_geom(H, W, R, S, stride, (pad4[0], pad4[2]), dilation, OH, OW)
+    _check(native.load().dl4j_col2im_rows(DT[dcols.dtype], _ptr(dcols), _ptr(dx), N, C, g, _stream()), "col2im_rows")
+    return dx.permute(0, 3, 1, 2)
 
 
 def fill_(t, value=0.0):

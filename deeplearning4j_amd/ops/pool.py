@@ -10,6 +10,13 @@ from .dispatch import use_native
 from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
+def _cl_channels(t, C):
+    """The first C channels of the 4-D ``t`` as a channels-last tensor (one in-tree strided copy on the GPU)."""
+    from . import nd4j_kernels as NK
+    y = NK.channels_last_copy(t, C)
+    return y if y is not None else t[:, :C].contiguous(memory_format=torch.channels_last)
+
+
 def pool2d_forward(x, ptype, kernel, stride, pad4, dilation=(1, 1), pnorm=2, eps=1e-8):
     """Returns (y, ctx). ptype in {'MAX','AVG','SUM','PNORM'}."""
     pt, pb, pl, pr = pad4
@@ -19,11 +26,10 @@ def pool2d_forward(x, ptype, kernel, stride, pad4, dilation=(1, 1), pnorm=2, eps
         if x.dim() == 4 and C % 8:
             # channel counts off the 8-wide vector (LeNet's 20 / 50): zero-padded channels through the same kernel
             from .conv_native import _pad_ch, _r8
-            r = native.pool2d_fwd(_pad_ch(x.contiguous(memory_format=torch.channels_last), _r8(C), cl=True),
-                                  ptype, kernel, stride, pad4)
+            r = native.pool2d_fwd(_pad_ch(x, _r8(C), cl=True), ptype, kernel, stride, pad4)
             if r is not None:
                 y, ctx = r
-                return y[:, :C].contiguous(memory_format=torch.channels_last), ("PADC", C, ctx)
+                return _cl_channels(y, C), ("PADC", C, ctx)
         r = native.pool2d_fwd(x, ptype, kernel, stride, pad4)
         if r is not None:
             return r
@@ -52,8 +58,8 @@ def pool2d_backward(dy, ctx):
     if kind == "PADC":
         from .conv_native import _pad_ch, _r8
         C, inner = ctx[1], ctx[2]
-        dx = pool2d_backward(_pad_ch(dy.contiguous(memory_format=torch.channels_last), _r8(C), cl=True), inner)
-        return dx[:, :C].contiguous(memory_format=torch.channels_last)
+        dx = pool2d_backward(_pad_ch(dy, _r8(C), cl=True), inner)
+        return _cl_channels(dx, C)
     if kind == "NATIVE":
         from . import native
         return native.pool2d_bwd(dy, ctx)

@@ -218,14 +218,19 @@ def test_shape_layers_and_max_vertex_on_gpu(cuda):
 
 @pytest.mark.parametrize("case", [((2, 3, 9, 11), (4, 3, 3, 3), (1, 1), (1, 1, 1, 1), (1, 1)),
                                   ((2, 5, 12, 10), (6, 5, 5, 3), (2, 1), (2, 1, 0, 2), (1, 2)),
-                                  ((1, 4, 8, 8), (3, 4, 1, 1), (2, 2), (0, 0, 0, 0), (1, 1))])
-def test_fp32_conv_im2col_col2im_kernels(cuda, case):
-    """fp32 conv forward / backward on the in-tree im2col (pad + strided copy) and gather col2im kernels + the fp32
-    MFMA GEMM, against torch's fp32 conv, with the kernels' launch counters advancing (no ATen unfold / fold)."""
+                                  ((1, 4, 8, 8), (3, 4, 1, 1), (2, 2), (0, 0, 0, 0), (1, 1)),
+                                  ((64, 20, 12, 12), (50, 20, 5, 5), (1, 1), (0, 0, 0, 0), (1, 1))])
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_fp32_conv_im2col_col2im_kernels(cuda, case, channels_last):
+    """fp32 conv forward / backward on the in-tree row-per-pixel im2col (padding in the same launch) and gather
+    col2im kernels + one fp32 MFMA GEMM per product, against torch's fp32 conv, with the kernels' launch counters
+    advancing (no ATen unfold / fold). The last case is LeNet's second conv at batch 64."""
     from deeplearning4j_amd.ops import conv as C
     xs, ws, st, pad4, dil = case
     g = torch.Generator().manual_seed(9)
     x = torch.randn(xs, generator=g).to(cuda)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
     w = torch.randn(ws, generator=g).to(cuda) * 0.2
     b = torch.randn(ws[0], generator=g).to(cuda)
     K.CALLS.clear()
@@ -237,9 +242,11 @@ def test_fp32_conv_im2col_col2im_kernels(cuda, case):
     assert torch.allclose(y, yr, atol=1e-4, rtol=1e-4)
     dy = torch.randn(yr.shape, generator=g).to(cuda)
     yr.backward(dy)
+    if channels_last:
+        dy = dy.contiguous(memory_format=torch.channels_last)
     dx, dw, db = C._fp32_conv_bwd(x, w, dy, st, pad4, dil, True, True, True)
     H, W = xs[2], xs[3]
     assert torch.allclose(dx, xr.grad[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W], atol=1e-4, rtol=1e-4)
     assert torch.allclose(dw, wr.grad, atol=1e-3, rtol=1e-4)
     assert torch.allclose(db, br.grad, atol=1e-4, rtol=1e-4)
-    assert K.CALLS["strided_copy"] >= 2 and K.CALLS["col2im"] == 1
+    assert K.CALLS["im2col_rows"] == 2 and K.CALLS["col2im_rows"] == 1

@@ -81,6 +81,17 @@ def test_lstm_char_lm_step_launches_no_torch_compute_kernels():
     _audit(_step_kernels(net, x, y, step=lambda: net.fit(x, y)), "LSTM char-LM")
 
 
+def test_lenet_fp32_step_launches_no_torch_compute_kernels():
+    """The exact-fp32 LeNet step (tools/bench_lenet.py's model: BASELINE config 1): convs as row-im2col + one fp32 GEMM
+    per product, channel-padded pooling, NCHW flatten — all on in-tree kernels."""
+    from deeplearning4j_amd.models import LeNet
+    net = LeNet(numLabels=10).init(device=torch.device("cuda", 0))
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(64, 784, generator=g).cuda()
+    y = torch.nn.functional.one_hot(torch.randint(0, 10, (64,), generator=g), 10).float().cuda()
+    _audit(_step_kernels(net, x, y, step=lambda: net.fit(x, y)), "LeNet fp32")
+
+
 def test_resnet50_step_launches_no_torch_compute_kernels():
     from deeplearning4j_amd.models import ResNet50
     from deeplearning4j_amd.nn.conf import DataType

@@ -2,7 +2,7 @@
 the LSTM char-LM or ResNet-50 with Python stacks and prints every aten op that launched a device kernel, with the
 framework frames that called it. Diagnostic companion to tests/test_gpu_step_kernels.py.
 
-Usage: python tools/step_torch_ops.py [bert|lstm|resnet]"""
+Usage: python tools/step_torch_ops.py [bert|lstm|resnet|lenet]"""
 import os
 import sys
 
@@ -27,6 +27,12 @@ def build(which):
         idx = torch.randint(0, 77, (8, 101), generator=g)
         x = torch.nn.functional.one_hot(idx[:, :-1], 77).permute(0, 2, 1).float().to(dev)
         y = torch.nn.functional.one_hot(idx[:, 1:], 77).permute(0, 2, 1).float().to(dev)
+        return lambda: net.fit(x, y)
+    if which == "lenet":
+        from deeplearning4j_amd.models import LeNet
+        net = LeNet(numLabels=10).init(device=dev)                  # tools/bench_lenet.py's model and input
+        x = torch.rand(64, 784, generator=g).to(dev)
+        y = torch.nn.functional.one_hot(torch.randint(0, 10, (64,), generator=g), 10).float().to(dev)
         return lambda: net.fit(x, y)
     from deeplearning4j_amd.models import ResNet50
     net = ResNet50(numLabels=100, dataType=DataType.BFLOAT16, inputShape=[3, 224, 224]).init(dev)
