@@ -54,4 +54,5 @@ def use_native(t, op=None):
 
 
 def stream_ptr():
-    return torch.cuda.current_stream().cuda_stream
+    from .native import _stream
+    return _stream()

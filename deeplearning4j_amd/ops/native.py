@@ -68,7 +68,15 @@ def register_sig(name, args, restype=c_int):
         f.restype = restype
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_dev = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream():
+    """Handle of the current HIP stream (the one torch.cuda.current_stream() names, incl. stream contexts and graph
+    capture): two C calls instead of the Python stream object — kernel launches pay this on every call."""
+    if _raw_stream is not None and _cur_dev is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 

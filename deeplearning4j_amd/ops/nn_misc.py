@@ -54,7 +54,8 @@ def _p(t):
 
 
 def _s():
-    return c_void_p(torch.cuda.current_stream().cuda_stream)
+    from .native import _stream
+    return c_void_p(_stream())
 
 
 def _check(rc, what):

@@ -235,18 +235,21 @@ def test_fp32_conv_im2col_col2im_kernels(cuda, case, channels_last):
     b = torch.randn(ws[0], generator=g).to(cuda)
     K.CALLS.clear()
     y = C._fp32_conv_fwd(x, w, b, st, pad4, dil)
-    xr = torch.nn.functional.pad(x, (pad4[2], pad4[3], pad4[0], pad4[1])).requires_grad_(True)
-    wr = w.clone().requires_grad_(True)
-    br = b.clone().requires_grad_(True)
+    # fp64 reference on the CPU (no library conv on the GPU in this test)
+    xr = torch.nn.functional.pad(x.cpu().double(), (pad4[2], pad4[3], pad4[0], pad4[1])).requires_grad_(True)
+    wr = w.cpu().double().requires_grad_(True)
+    br = b.cpu().double().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, br, st, 0, dil)
-    assert torch.allclose(y, yr, atol=1e-4, rtol=1e-4)
-    dy = torch.randn(yr.shape, generator=g).to(cuda)
-    yr.backward(dy)
+    assert torch.allclose(y.cpu().double(), yr.detach(), atol=1e-4, rtol=1e-4)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy.double())
+    dy = dy.to(cuda)
     if channels_last:
         dy = dy.contiguous(memory_format=torch.channels_last)
     dx, dw, db = C._fp32_conv_bwd(x, w, dy, st, pad4, dil, True, True, True)
     H, W = xs[2], xs[3]
-    assert torch.allclose(dx, xr.grad[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W], atol=1e-4, rtol=1e-4)
-    assert torch.allclose(dw, wr.grad, atol=1e-3, rtol=1e-4)
-    assert torch.allclose(db, br.grad, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dx.cpu().double(), xr.grad[:, :, pad4[0]:pad4[0] + H, pad4[2]:pad4[2] + W], atol=1e-4,
+                          rtol=1e-4)
+    assert torch.allclose(dw.cpu().double(), wr.grad, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(db.cpu().double(), br.grad, atol=1e-4, rtol=1e-4)
     assert K.CALLS["im2col_rows"] == 2 and K.CALLS["col2im_rows"] == 1
