@@ -16,7 +16,8 @@ from deeplearning4j_amd.nn.util.dtypes import acc as _acc  # noqa: E402
 
 
 class GraphVertex(Config):
-    def numParams(self):
+    def numParams(self, backprop=True):
+        """Parameter count (the reference's numParams(boolean backprop); the flag does not change it here)."""
         return 0
 
     def getOutputType(self, layerIndex, *inputTypes):
@@ -414,7 +415,7 @@ class LayerVertex(GraphVertex):
     """Graph node holding a layer config (+ optional preprocessor)."""
     FIELDS = {"layerConf": None, "preProcessor": None}
 
-    def numParams(self):
+    def numParams(self, backprop=True):
         return self.layerConf.numParams()
 
     def getLayerConf(self):

@@ -41,6 +41,13 @@ class CnnToFeedForwardPreProcessor(InputPreProcessor):
     def preProcess(self, x, miniBatchSize, training=False):
         if x.dim() == 2:
             return x
+        exp = (self.numChannels, self.inputHeight, self.inputWidth)
+        if x.dim() == 4 and all(v > 0 for v in exp) and tuple(x.shape[1:]) != tuple(exp):
+            # the flattened size can agree while the layout does not (reference CnnToFeedForwardPreProcessor:84-89)
+            from ...exceptions import IllegalStateException
+            raise IllegalStateException(
+                f"Invalid input array: expected shape [minibatch, channels, height, width] = [minibatch, {exp[0]}, "
+                f"{exp[1]}, {exp[2]}] - got {list(x.shape)}")
         self._shape = x.shape
         if x.is_cuda and not x.is_contiguous():
             # NCHW flatten order (the reference's c-order reshape) of a channels-last activation: one in-tree copy

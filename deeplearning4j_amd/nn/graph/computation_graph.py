@@ -371,6 +371,9 @@ class ComputationGraph(BaseNetwork):
         self.inputMaskArrays = self.labelMaskArrays = None
 
     def output(self, *inputs, train=False, masks=None):
+        """output(x...), output([x...]) or, as the reference, output(train, x...)."""
+        if inputs and isinstance(inputs[0], bool):
+            train, inputs = inputs[0], inputs[1:]
         if len(inputs) == 1 and isinstance(inputs[0], (list, tuple)):
             inputs = inputs[0]
         with torch.no_grad():
