@@ -55,6 +55,9 @@ class Layer(Config):
     FIELDS = {"layerName": None, "idropout": None, "constraints": None}
     _ALIASES = {"name": "layerName", "dropOut": "idropout", "dropout": "idropout"}
     _CONVERTERS = {"idropout": to_dropout}
+
+    def getIDropout(self):
+        return self.idropout
     RUNTIME = None      # "module:Class" of the runtime implementation
 
     # ---- builder hooks ---------------------------------------------------------------------

@@ -190,6 +190,11 @@ class Sgd(IUpdater):
 class Nesterovs(IUpdater):
     FIELDS = {"learningRate": 0.1, "learningRateSchedule": None, "momentum": 0.9, "momentumSchedule": None}
     STATE_MULT = 1
+    DEFAULT_NESTEROV_MOMENTUM = 0.9
+    DEFAULT_NESTEROV_LEARNING_RATE = 0.1
+
+    def getMomentumISchedule(self):
+        return self.momentumSchedule
 
     def __init__(self, learningRate=0.1, momentum=0.9, **kw):
         if isinstance(learningRate, ISchedule):
@@ -215,6 +220,8 @@ class Adam(IUpdater):
     FIELDS = {"learningRate": 1e-3, "learningRateSchedule": None, "beta1": 0.9, "beta2": 0.999,
               "epsilon": 1e-8}
     STATE_MULT = 2
+    DEFAULT_ADAM_LEARNING_RATE, DEFAULT_ADAM_BETA1_MEAN_DECAY = 1e-3, 0.9
+    DEFAULT_ADAM_BETA2_VAR_DECAY, DEFAULT_ADAM_EPSILON = 0.999, 1e-8
 
     def __init__(self, learningRate=1e-3, beta1=0.9, beta2=0.999, epsilon=1e-8, **kw):
         if isinstance(learningRate, ISchedule):
@@ -284,6 +291,7 @@ class AdaDelta(IUpdater):
     FIELDS = {"rho": 0.95, "epsilon": 1e-6}
     STATE_MULT = 2
     HAS_LR = False
+    DEFAULT_ADADELTA_RHO, DEFAULT_ADADELTA_EPSILON = 0.95, 1e-6
 
     def __init__(self, rho=0.95, epsilon=1e-6, **kw):
         super().__init__(rho=rho, epsilon=epsilon, **kw)
@@ -300,6 +308,7 @@ class AdaDelta(IUpdater):
 class RmsProp(IUpdater):
     FIELDS = {"learningRate": 1e-1, "learningRateSchedule": None, "rmsDecay": 0.95, "epsilon": 1e-8}
     STATE_MULT = 1
+    DEFAULT_RMSPROP_LEARNING_RATE, DEFAULT_RMSPROP_RMSDECAY, DEFAULT_RMSPROP_EPSILON = 1e-1, 0.95, 1e-8
 
     def __init__(self, learningRate=1e-1, rmsDecay=0.95, epsilon=1e-8, **kw):
         if isinstance(learningRate, ISchedule):

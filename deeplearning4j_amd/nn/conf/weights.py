@@ -12,9 +12,30 @@ import torch
 from .base import Config, register_enum
 
 
+def _jdouble(v):
+    """Java's Double.toString of v (0.0, 1.0, 0.5, 1.0E-8)."""
+    v = float(v)
+    if v == int(v) and abs(v) < 1e7:
+        return f"{v:.1f}"
+    if 1e-3 <= abs(v) < 1e7:
+        return repr(v)
+    m, e = f"{v:.16e}".split("e")
+    m = m.rstrip("0")
+    m = m + "0" if m.endswith(".") else m
+    return f"{m}E{int(e)}"
+
+
 class Distribution(Config):
     def sample_(self, t, gen=None):
         raise NotImplementedError
+
+    def __str__(self):
+        """The reference's toString: ``NormalDistribution{mean=0.0, std=1.0}`` (nn/conf/distribution/*.java)."""
+        parts = []
+        for k, d in self.FIELDS.items():
+            v = getattr(self, k)
+            parts.append(f"{k}={_jdouble(v) if isinstance(d, float) else v}")
+        return f"{type(self).__name__}{{{', '.join(parts)}}}"
 
 
 class NormalDistribution(Distribution):
