@@ -27,6 +27,6 @@ class UnsupportedOperationException(DL4JException, NotImplementedError):
     """java.lang.UnsupportedOperationException: a configured feature the engine refuses (e.g. HESSIAN_FREE)."""
 
 
-class IllegalStateException(DL4JException):
+class IllegalStateException(DL4JException, ValueError):
     """java.lang.IllegalStateException: an array whose shape contradicts the state a component was configured with
     (e.g. a CNN-to-feed-forward preprocessor fed [mb, C, W, H] instead of [mb, C, H, W])."""

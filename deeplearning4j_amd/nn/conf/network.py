@@ -9,6 +9,7 @@ counts so learning-rate schedules resume (MultiLayerConfiguration.java:80-83).
 import copy
 import json
 
+from ...exceptions import IllegalStateException
 from .base import Config, _decode
 from .enums import BackpropType, CacheMode, ConvolutionMode, DataType, OptimizationAlgorithm, WorkspaceMode
 from .graph import GraphVertex, LayerVertex
@@ -533,14 +534,14 @@ class GraphBuilder:
 
     def build(self):
         if not self._inputs:
-            raise ValueError("ComputationGraph must have at least one input (addInputs)")
+            raise IllegalStateException("ComputationGraph must have at least one input (addInputs)")
         if not self._outputs:
-            raise ValueError("ComputationGraph must have at least one output (setOutputs)")
+            raise IllegalStateException("ComputationGraph must have at least one output (setOutputs)")
         names = set(self._vertices) | set(self._inputs)
         for v, ins in self._vertexInputs.items():
             for i in ins:
                 if i not in names:
-                    raise ValueError(f"Vertex {v!r} has unknown input {i!r}")
+                    raise IllegalStateException(f"Vertex {v!r} has unknown input {i!r}")
         for o in self._outputs:
             if o not in self._vertices:
                 raise ValueError(f"Output {o!r} is not a vertex")
@@ -628,7 +629,7 @@ class ComputationGraphConfiguration(_Counters, Config):
                 if indeg[m] == 0:
                     queue.append(m)
         if len(order) != len(all_names):
-            raise ValueError("Invalid ComputationGraph configuration: graph contains a cycle")
+            raise IllegalStateException("Invalid ComputationGraph configuration: graph contains a cycle")
         return order
 
     def addPreProcessorsAndInferNIn(self):
