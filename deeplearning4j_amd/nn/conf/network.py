@@ -538,13 +538,17 @@ class GraphBuilder:
         if not self._outputs:
             raise IllegalStateException("ComputationGraph must have at least one output (setOutputs)")
         names = set(self._vertices) | set(self._inputs)
+        for v in self._vertices:
+            if not self._vertexInputs.get(v):
+                # reference ComputationGraphConfiguration.validate:299, checked before the disconnected vertices
+                raise IllegalStateException(f"Invalid configuration: vertex {v!r} has no inputs")
         for v, ins in self._vertexInputs.items():
             for i in ins:
                 if i not in names:
                     raise IllegalStateException(f"Vertex {v!r} has unknown input {i!r}")
         for o in self._outputs:
             if o not in self._vertices:
-                raise ValueError(f"Output {o!r} is not a vertex")
+                raise IllegalStateException(f"Output {o!r} is not a vertex")
         if not self._allowDisconnected:
             # every input and vertex must lead to an output (reference ComputationGraphConfiguration.validate)
             reach, stack = set(self._outputs), list(self._outputs)
