@@ -125,6 +125,11 @@ class Layer(Config):
             return self.biasUpdater
         return getattr(self, "updater", None)
 
+    def getUpdaterByParam(self, key):
+        """The updater of parameter ``key``: the bias updater for bias parameters when one is set (reference
+        BaseLayer.getUpdaterByParam)."""
+        return self.updaterFor(key)
+
     def l1For(self, key):
         if self.is_bias(key):
             return getattr(self, "l1Bias", 0.0) or 0.0

@@ -271,8 +271,11 @@ class ListBuilder:
 
     def build(self):
         n = len(self._layers)
+        if n == 0:
+            raise IllegalStateException("Invalid configuration: no layers defined")
         if sorted(self._layers) != list(range(n)):
-            raise ValueError(f"Layer indices must be contiguous from 0: got {sorted(self._layers)}")
+            raise IllegalStateException(f"Invalid configuration: layer indices must be contiguous from 0: got "
+                                        f"{sorted(self._layers)}")
         confs = [copy.deepcopy(self._layers[i]) for i in range(n)]
         g = self._g
         for c in confs:

@@ -42,6 +42,17 @@ class LayerImpl:
         self.helperCountFail = 0
         self.dropoutApplied = False
 
+    # -------------------------------------------------------------------------- listeners
+    def getListeners(self):
+        """The layer's training listeners: its own, else those of the network that owns it (the reference sets the
+        network's listeners on every layer, whether they are set before or after init)."""
+        if self.listeners:
+            return self.listeners
+        return list(getattr(self.net, "listeners", None) or [])
+
+    def setListeners(self, *ls):
+        self.listeners = [x for l in ls for x in (l if isinstance(l, (list, tuple)) else [l])]
+
     # -------------------------------------------------------------------------- params
     def numParams(self):
         return self.conf.numParams()
