@@ -125,6 +125,12 @@ class Layer(Config):
             return self.biasUpdater
         return getattr(self, "updater", None)
 
+    def getL1ByParam(self, key):
+        return self.l1For(key)
+
+    def getL2ByParam(self, key):
+        return self.l2For(key)
+
     def getUpdaterByParam(self, key):
         """The updater of parameter ``key``: the bias updater for bias parameters when one is set (reference
         BaseLayer.getUpdaterByParam)."""
@@ -787,10 +793,11 @@ class BatchNormalization(FeedForwardLayer):
         return super().updaterFor(key)
 
     def l1For(self, key):
-        return 0.0 if key in ("mean", "var") else super().l1For(key)
+        # no BatchNormalization parameter is regularised (reference BatchNormalization.getL1ByParam :132-135)
+        return 0.0
 
     def l2For(self, key):
-        return 0.0 if key in ("mean", "var") else super().l2For(key)
+        return 0.0
 
 
 class LocalResponseNormalization(Layer):
@@ -1254,9 +1261,20 @@ class AutoEncoder(FeedForwardLayer):
 class VariationalAutoencoder(FeedForwardLayer):
     """VAE layer (Kingma & Welling), reference nn/layers/variational/VariationalAutoencoder.java:51."""
     FIELDS = {"encoderLayerSizes": [100], "decoderLayerSizes": [100], "outputDistribution": None,
-              "pzxActivationFn": None, "numSamples": 1}
+              "pzxActivationFn": None, "numSamples": 1, "lossFunction": None}
     _CONVERTERS = dict(FeedForwardLayer._CONVERTERS, pzxActivationFn=to_activation)
     RUNTIME = "deeplearning4j_amd.nn.layers.variational:VariationalAutoencoderImpl"
+
+    @staticmethod
+    def _builder_hook_lossFunction(kw, v):
+        """lossFunction(activation, loss): an ordinary loss as the reconstruction distribution (reference
+        VariationalAutoencoder.Builder.lossFunction -> LossFunctionWrapper); lossFunction(loss): the pretrain-layer
+        loss field inherited from BasePretrainNetwork.Builder (not used by the VAE's own objective)."""
+        if isinstance(v, list) and len(v) == 2:
+            from .variational import LossFunctionWrapper
+            kw["outputDistribution"] = LossFunctionWrapper(v[0], v[1])
+        else:
+            kw["lossFunction"] = v
 
     def _dist_size(self):
         d = self.outputDistribution

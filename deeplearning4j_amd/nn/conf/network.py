@@ -34,11 +34,28 @@ _GLOBAL_DEFAULTS = {
 
 
 class NeuralNetConfiguration:
-    """Namespace holding the global ``Builder`` (reference class of the same name)."""
+    """Namespace holding the global ``Builder`` (reference class of the same name). ``Builder().layer(l).build()``
+    gives the reference's single-layer configuration (``SingleLayerConfiguration``)."""
+
+    @staticmethod
+    def fromJson(s):
+        return SingleLayerConfiguration.fromJson(s)
+
+    @staticmethod
+    def fromYaml(s):
+        return SingleLayerConfiguration.fromYaml(s)
 
     class Builder:
         def __init__(self):
             self._g = dict(_GLOBAL_DEFAULTS)
+            self._layer = None
+
+        def layer(self, layer):
+            """The single layer of a NeuralNetConfiguration (reference Builder.layer(Layer))."""
+            if hasattr(layer, "build") and not isinstance(layer, Layer):
+                layer = layer.build()
+            self._layer = layer
+            return self
 
         def _set(self, k, v):
             self._g[k] = v
@@ -182,7 +199,91 @@ class NeuralNetConfiguration:
             return GraphBuilder(self._g)
 
         def build(self):
+            if self._layer is not None:
+                return SingleLayerConfiguration.of(self._g, self._layer)
             return dict(self._g)
+
+
+class SingleLayerConfiguration(Config):
+    """The reference's single-layer NeuralNetConfiguration (nn/conf/NeuralNetConfiguration.java: one ``layer`` plus
+    the settings that travel with it: seed, optimisation algorithm, minibatch / minimize flags, line-search
+    iterations, step function, pretrain flag). The builder's inheritable properties are applied to the layer."""
+    FIELDS = {"layer": None, "seed": 12345, "optimizationAlgo": OptimizationAlgorithm.STOCHASTIC_GRADIENT_DESCENT,
+              "miniBatch": True, "minimize": True, "maxNumLineSearchIterations": 5, "stepFunction": None,
+              "pretrain": False, "dataType": DataType.FLOAT}
+
+    @classmethod
+    def of(cls, g, layer):
+        layer = copy.deepcopy(layer)
+        if hasattr(layer, "applyGlobal"):
+            layer.applyGlobal(g)
+        if hasattr(layer, "finalize_defaults"):
+            layer.finalize_defaults()
+        return cls(layer=layer, **{k: g[k] for k in ("seed", "optimizationAlgo", "miniBatch", "minimize",
+                                                      "maxNumLineSearchIterations", "stepFunction", "dataType")
+                                   if k in g})
+
+    def to_dict(self):
+        d = super().to_dict()
+        if self.stepFunction is not None and not isinstance(self.stepFunction, Config):
+            d["stepFunction"] = {"@stepFunction": type(self.stepFunction).__name__}
+        return d
+
+    @classmethod
+    def from_dict(cls, d):
+        sf = d.get("stepFunction")
+        if isinstance(sf, dict) and "@stepFunction" in sf:
+            from ...optimize import solvers
+            d = dict(d)
+            d["stepFunction"] = None
+            obj = super().from_dict(d)
+            obj.stepFunction = getattr(solvers, sf["@stepFunction"])()
+            return obj
+        return super().from_dict(d)
+
+    def __eq__(self, other):
+        if type(self) is not type(other):
+            return False
+        a, b = self.to_dict(), other.to_dict()
+        return a == b
+
+    __hash__ = Config.__hash__
+
+    def getLayer(self):
+        return self.layer
+
+    def setLayer(self, layer):
+        self.layer = layer
+
+    def isPretrain(self):
+        return bool(self.pretrain)
+
+    def setPretrain(self, b):
+        self.pretrain = bool(b)
+
+    def getStepFunction(self):
+        return self.stepFunction
+
+    def setStepFunction(self, f):
+        self.stepFunction = f
+
+    def getL1ByParam(self, key):
+        return self.layer.l1For(key)
+
+    def getL2ByParam(self, key):
+        return self.layer.l2For(key)
+
+    def getVariables(self):
+        return [s.key for s in self.layer.param_specs()] if hasattr(self.layer, "param_specs") else []
+
+    def toYaml(self):
+        import yaml
+        return yaml.safe_dump(json.loads(self.toJson()), sort_keys=True)
+
+    @classmethod
+    def fromYaml(cls, s):
+        import yaml
+        return _decode(yaml.safe_load(s))
 
 
 class ListBuilder:
