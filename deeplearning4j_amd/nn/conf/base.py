@@ -178,9 +178,11 @@ class Config:
     def __getattr__(self, name):
         """Java-style getters for every field (``getL2()``, ``getIUpdater()``, ``getMomentum()``, ``isX()``), as the
         reference's Lombok-generated accessors. Only reached when normal attribute lookup fails."""
-        if name.startswith("_") or not (name.startswith("get") or name.startswith("is")) or len(name) < 3:
+        if name.startswith("_") or not (name.startswith("get") or name.startswith("is") or name.startswith("set")) \
+                or len(name) < 3:
             raise AttributeError(name)
-        stem = name[3:] if name.startswith("get") else name[2:]
+        setter = name.startswith("set")
+        stem = name[3:] if name.startswith(("get", "set")) else name[2:]
         if not stem:
             raise AttributeError(name)
         fields = type(self)._all_fields()
@@ -193,6 +195,12 @@ class Config:
                     break
         if field is None or field not in fields:
             raise AttributeError(f"{type(self).__name__} has no attribute {name!r}")
+        if setter:
+            conv = self._CONVERTERS.get(field)
+
+            def _set(v):
+                setattr(self, field, conv(v) if conv and v is not None else v)
+            return _set
         return lambda: self.__dict__.get(field)
 
     # --- serde -------------------------------------------------------------------------------
