@@ -32,6 +32,47 @@ class FineTuneConfiguration:
         self.tbpttFwdLength = kw.pop("tbpttFwdLength", None)
         self.tbpttBackLength = kw.pop("tbpttBackLength", None)
 
+    # ---- serde (reference FineTuneConfiguration.toJson / toYaml / fromJson / fromYaml) -------------------------
+    def _as_dict(self):
+        from .conf.base import _encode
+        d = {"@class": "FineTuneConfiguration", "overrides": {k: _encode(v) for k, v in sorted(self.overrides.items())}}
+        for k in ("backpropType", "tbpttFwdLength", "tbpttBackLength"):
+            d[k] = _encode(getattr(self, k))
+        return d
+
+    @classmethod
+    def _from_dict(cls, d):
+        from .conf.base import _decode
+        obj = cls()
+        obj.overrides = {k: _decode(v) for k, v in d.get("overrides", {}).items()}
+        for k in ("backpropType", "tbpttFwdLength", "tbpttBackLength"):
+            setattr(obj, k, _decode(d.get(k)))
+        return obj
+
+    def toJson(self):
+        import json
+        return json.dumps(self._as_dict(), indent=2, sort_keys=True)
+
+    @classmethod
+    def fromJson(cls, s):
+        import json
+        return cls._from_dict(json.loads(s))
+
+    def toYaml(self):
+        import yaml
+        return yaml.safe_dump(self._as_dict(), sort_keys=True)
+
+    @classmethod
+    def fromYaml(cls, s):
+        import yaml
+        return cls._from_dict(yaml.safe_load(s))
+
+    def __eq__(self, other):
+        return isinstance(other, FineTuneConfiguration) and self._as_dict() == other._as_dict()
+
+    def __hash__(self):
+        return hash(self.toJson())
+
     class Builder:
         def __init__(self):
             self._kw = {}
