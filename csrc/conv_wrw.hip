@@ -14,7 +14,8 @@
 // 16-byte chunks so the 4 rows x 64 B a half-wave reads hit 16 distinct bank slots.
 // Each (split, tile) writes its fp32 block into a slab part[split][K][RS*C] (no atomics); wrw_halo_reduce sums the
 // slabs in a fixed order and writes the DL4J [K][C][R][S] layout (+ the conv-bias gradient from per-split column
-// sums of the staged dY rows): bitwise deterministic.
+// sums of the staged dY rows): bitwise deterministic. Opt-in alternative (DL4J_AMD_WRW_TREE): the slabs summed
+// inside wrw_halo by a last-arrival reduction tree (tree_reduce below), measured slower (profiles/r6_wrw_tree.txt).
 // 1x1 convolutions (any stride, no padding) use the same engine with a "gather" X image (row p = X pixel of p).
 // Reference semantics: ConvolutionLayer.backpropGradient (deeplearning4j-nn/.../layers/convolution/
 // ConvolutionLayer.java:131-265), cuDNN's backward-filter in CudnnConvolutionHelper.java:179-246.
@@ -44,6 +45,12 @@ struct HaloArgs {
   int tiles_k, tiles_c;
   int M;                 // N*OH*OW (gather mode)
   FDv fHW, fHRHW, fOW, fTHOW, fOHOW;
+  // in-kernel slab reduction (null ticket = separate wrw_halo_reduce launch): arrival counters of this launch,
+  // tkpt per tile; fan-in of the reduction tree; the final outputs
+  unsigned* ticket;
+  int tkpt, fan, splits;
+  float* dW;
+  float* db;
 };
 
 template <int CPR>
@@ -112,6 +119,100 @@ template <int N> __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N <= 63, "vmcnt is a 6-bit counter");
   // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] (15 = no wait) | vmcnt[5:4] at [15:14]
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// In-kernel fixed-order slab reduction (replaces the wrw_halo_reduce launch when HaloArgs::ticket is set).
+// The splits of one tile form a tree with fan-in F: slab s is leaf s; the block that arrives last at a node (agent-
+// scope arrival counter, reset by that block) sums the node's children in index order and stores the sum in place
+// over its first child's slab, then climbs; at the root the sum goes to dW (DL4J [K][C][R][S] layout) and db. Every
+// reader is the only block touching those slabs at that moment, slab stores are sc1 write-through and slab reads are
+// agent-scope atomic loads, so no L2 invalidate is needed; the summation order depends only on the split count:
+// bitwise deterministic. The serial tail per level is F slabs of one tile, against a whole-GPU reduce launch.
+typedef __attribute__((address_space(1))) unsigned gq32_w;
+typedef __attribute__((address_space(1))) unsigned long long gq64_w;
+__device__ __forceinline__ float4 ld_coh16(const float* p) {
+  const unsigned long long lo = __hip_atomic_load((gq64_w*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long hi = __hip_atomic_load((gq64_w*)(p + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float4(__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
+                     __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32)));
+}
+__device__ __forceinline__ float ld_coh4(const float* p) {
+  return __uint_as_float(__hip_atomic_load((gq32_w*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int BK, int BC, int T>
+__device__ __forceinline__ void tree_reduce(const HaloArgs& a, int split, int tile, int k0, int c0, bool do_bias, int tid,
+                                         int* flag) {
+  constexpr int C4 = BC / 4, ITEMS = BK * T * C4, PB = 8;
+  const int RSC = T * a.C, F = a.fan;
+  const long long slab_sz = (long long)a.K * RSC;
+  unsigned* cnt = a.ticket + (long long)tile * a.tkpt;
+  int node = split, n = a.splits, off = 0;
+  long long stride = 1;                                  // leaves between consecutive nodes of this level
+  for (;;) {
+    const int parent = node / F, first = parent * F, nch = min(F, n - first), np = (n + F - 1) / F;
+    if (n > 1) {
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((gq32_w*)&cnt[off + parent], 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(nch - 1);
+        if (last) __hip_atomic_store((gq32_w*)&cnt[off + parent], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
+      __syncthreads();
+      const int last = *flag;
+      __syncthreads();
+      if (!last) return;
+    }
+    const bool root = np == 1;
+    float* dst = a.part + (long long)first * stride * slab_sz;
+    // passes of PB float4 per thread (bounded registers; the block's main-loop accumulators are dead here)
+#pragma unroll 1
+    for (int p0 = 0; p0 < ITEMS; p0 += 256 * PB) {
+      float4 v[PB];
+      int o[PB];
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int it = p0 + tid + i * 256;
+        const int k = k0 + it / (T * C4), rem = it % (T * C4), t = rem / C4, c = c0 + 4 * (rem % C4);
+        o[i] = (it < ITEMS && k < a.K && c < a.C) ? k * RSC + t * a.C + c : -1;
+      }
+      for (int ch = 0; ch < nch; ++ch) {
+        const float* src = a.part + (long long)(first + ch) * stride * slab_sz;
+#pragma unroll
+        for (int i = 0; i < PB; ++i)
+          if (o[i] >= 0) {
+            const float4 w = ld_coh16(src + o[i]);
+            v[i].x += w.x; v[i].y += w.y; v[i].z += w.z; v[i].w += w.w;
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        if (o[i] < 0) continue;
+        if (root) {
+          const int k = o[i] / RSC, rem = o[i] - k * RSC, t = rem / a.C, c = rem - t * a.C;
+          float* q = a.dW + ((long long)k * a.C + c) * T + t;
+          q[0] = v[i].x; q[T] = v[i].y; q[2 * T] = v[i].z; q[3 * T] = v[i].w;
+        } else {
+          st_coh16(dst + o[i], v[i].x, v[i].y, v[i].z, v[i].w);
+        }
+      }
+    }
+    if (do_bias && tid < BK && k0 + tid < a.K) {
+      float sb = 0.f;
+      for (int ch = 0; ch < nch; ++ch) sb += ld_coh4(a.partb + (long long)(first + ch) * stride * a.K + k0 + tid);
+      if (root) a.db[k0 + tid] = sb;
+      else st_coh4(a.partb + (long long)first * stride * a.K + k0 + tid, sb);
+    }
+    if (root) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    off += np;
+    node = parent;
+    n = np;
+    stride *= F;
+  }
 }
 
 // Compile-time stage geometry of one instantiation (shared with the host planner).
@@ -421,10 +522,15 @@ __global__ __launch_bounds__(WK* WC* TG * 64, 1) void wrw_halo(HaloArgs a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int c = c0 + (wc * FC + j) * 32 + 8 * q + 4 * h;
-            if (c < a.C)
-              *reinterpret_cast<float4*>(slab + (long long)k * RSC + (t0 + ti) * a.C + c) =
-                  make_float4(acc[ti][i][j][4 * q], acc[ti][i][j][4 * q + 1], acc[ti][i][j][4 * q + 2],
-                              acc[ti][i][j][4 * q + 3]);
+            if (c < a.C) {
+              float* dst = slab + (long long)k * RSC + (t0 + ti) * a.C + c;
+              if (a.ticket)     // read back by another block's tree step: written through the XCD-local L2
+                st_coh16(dst, acc[ti][i][j][4 * q], acc[ti][i][j][4 * q + 1], acc[ti][i][j][4 * q + 2],
+                         acc[ti][i][j][4 * q + 3]);
+              else
+                *reinterpret_cast<float4*>(dst) = make_float4(acc[ti][i][j][4 * q], acc[ti][i][j][4 * q + 1],
+                                                              acc[ti][i][j][4 * q + 2], acc[ti][i][j][4 * q + 3]);
+            }
           }
     }
   };
@@ -444,8 +550,14 @@ __global__ __launch_bounds__(WK* WC* TG * 64, 1) void wrw_halo(HaloArgs a) {
     if (tid < BK && k0 + tid < a.K) {
       float sum = 0.f;
       for (int r = 0; r < BRG; ++r) sum += red[r * BK + tid];
-      a.partb[(long long)split * a.K + k0 + tid] = sum;
+      if (a.ticket) st_coh4(a.partb + (long long)split * a.K + k0 + tid, sum);
+      else a.partb[(long long)split * a.K + k0 + tid] = sum;
     }
+  }
+  if (a.ticket) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's slab stores are in memory
+    __syncthreads();                                               // ... and every wave's; LDS reads done
+    tree_reduce<BK, BC, T>(a, split, tile, k0, c0, do_bias, tid, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -630,7 +742,56 @@ int launch_halo(const Plan& P, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Arrival counters of the in-kernel slab reduction: 256 launches in flight x kWrwTickets, zero-initialised; every
+// counter is reset by the block that completes it, so a graph replay finds them at zero again.
+constexpr int kWrwSlots = 256, kWrwTickets = 4096;
+__device__ unsigned g_wrw_ticket[kWrwSlots * kWrwTickets];
+
+unsigned* wrw_ticket_slot() {
+  static unsigned* base[64] = {nullptr};
+  static unsigned next = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wrw_ticket)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  const unsigned k = __atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED) % (unsigned)kWrwSlots;
+  return base[dev] + (long long)kWrwTickets * k;
+}
+
+// Fan-in of the in-kernel reduction tree; 0 or 1 = the separate wrw_halo_reduce launch (DL4J_AMD_WRW_TREE).
+// Off by default: measured slower on the zoo ResNet-50 at batch 1024 (profiles/r6_wrw_tree.txt: fan 8 39.5k vs
+// 41.5k images/s; limited to <= 16 splits still -1.2 %) — the write-through slab stores and the serial per-tile
+// tail of the last levels cost more than the reduce launch they replace, which overlaps the data-gradient chain on
+// the weight-gradient stream anyway.
+int& wrw_tree_fan() {
+  static int v = [] {
+    const char* e = getenv("DL4J_AMD_WRW_TREE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// Largest split count that takes the in-kernel tree (DL4J_AMD_WRW_TREE_MAX): above it the serial tail of the
+// tree's last levels (fan-in slabs of one tile per level) outlasts the separate reduce launch.
+int wrw_tree_max_splits() {
+  static const int v = [] {
+    const char* e = getenv("DL4J_AMD_WRW_TREE_MAX");
+    return e ? atoi(e) : 1 << 30;
+  }();
+  return v;
+}
+
 }  // namespace
+
+// Sets the fan-in of the weight-gradient slab reduction tree (<= 1: separate reduce launch); returns the old value.
+DL4J_API int dl4j_conv_wrw_set_tree(int fan) {
+  const int old = wrw_tree_fan();
+  wrw_tree_fan() = fan;
+  return old;
+}
 
 // Workspace floats for dl4j_conv_wrw_halo (slabs + bias partials); 0 when the shape / variant is not supported.
 // variant 0 = automatic. Writes the split count used to *splits_out.
@@ -658,8 +819,22 @@ DL4J_API int dl4j_conv_wrw_halo(int dt, const void* X, const void* dY, float* dW
   P.a.part = ws;
   const long long RSC = (long long)R * S * C;
   P.a.partb = db ? ws + (long long)P.splits * K * RSC : nullptr;
+  P.a.splits = P.splits;
+  P.a.dW = dW;
+  P.a.db = db;
+  P.a.fan = wrw_tree_fan();
+  P.a.ticket = nullptr;
+  if (P.a.fan > 1 && P.splits <= wrw_tree_max_splits()) {
+    int tkpt = 0;
+    for (int n = P.splits; n > 1;) {
+      n = (n + P.a.fan - 1) / P.a.fan;
+      tkpt += n;
+    }
+    P.a.tkpt = tkpt;
+    if ((long long)P.a.tiles_k * P.a.tiles_c * tkpt <= kWrwTickets) P.a.ticket = wrw_ticket_slot();
+  }
   int e = dt == 1 ? launch_halo<1>(P, s) : launch_halo<2>(P, s);
-  if (e) return e;
+  if (e || P.a.ticket) return e;
   const long long total = (long long)K * RSC;
   const unsigned nb = (unsigned)((total + 63) / 64) + (db ? (unsigned)((K + 63) / 64) : 0u);
   hipLaunchKernelGGL(wrw_halo_reduce, dim3(nb), dim3(256), 0, s, ws, dW, P.splits, K, C, R * S, P.a.partb, db);

@@ -197,6 +197,49 @@ def test_halo_weight_gradient(cuda, case):
         assert torch.equal(again, dW), c
 
 
+@pytest.mark.parametrize("case,splits", [(HALO_CASES[0], 1), (HALO_CASES[0], 9), (HALO_CASES[0], 64),
+                                         (HALO_CASES[5], 7), (HALO_CASES[6], 100), (HALO_CASES[9], 13)])
+def test_halo_in_kernel_tree_reduce(cuda, case, splits):
+    """csrc/conv_wrw.hip tree_reduce: the split slabs summed inside wrw_halo by the last-arriving block of each tree
+    node (fan-in 8 default, 2 = deepest tree, 64 = one level) against the separate wrw_halo_reduce launch (fan 0) and
+    the fp32 torch weight gradient; weight and bias gradients bitwise reproducible for every fan-in, including single
+    split, partial last groups and partial k / c tiles."""
+    import ctypes
+    lib = native.load()
+    lib.dl4j_conv_wrw_set_tree.argtypes = [ctypes.c_int]
+    N, C, H, W, K, R, S, stride, pad4, dil = case
+    x, w, _ = _data(case)
+    wr = w.float().requires_grad_(True)
+    yr = _ref(x, wr, None, stride, pad4, dil)
+    g = torch.Generator().manual_seed(9)
+    dy = torch.randn(yr.shape, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    geom = (N, H, W, C, K, R, S, stride[0], stride[1], pad4[0], pad4[2], dil[0], dil[1], dy.shape[2], dy.shape[3])
+    var = conv_native._halo_candidates(geom)[0][1]
+    db_ref = dy.float().sum(dim=(0, 2, 3))
+    old = lib.dl4j_conv_wrw_set_tree(8)
+    res = {}
+    try:
+        for fan in (0, 8, 2, 64):
+            lib.dl4j_conv_wrw_set_tree(fan)
+            outs = []
+            for _ in range(2):
+                dW = torch.full((K, C, R, S), 3.0, device=cuda)
+                db = torch.full((K,), 3.0, device=cuda)
+                assert conv_native._wrw_launch(("halo", var, splits), x, dy, dW, geom, db) == 0
+                torch.cuda.synchronize()
+                outs.append((dW, db))
+            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), fan
+            _close(outs[0][0], wr.grad, 1e-2)
+            _close(outs[0][1], db_ref, 1e-3)
+            res[fan] = outs[0]
+    finally:
+        lib.dl4j_conv_wrw_set_tree(old)
+    for fan in (8, 2, 64):
+        torch.testing.assert_close(res[fan][0], res[0][0], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(res[fan][1], res[0][1], rtol=1e-5, atol=1e-4)
+
+
 def test_halo_rejects_unsupported_shapes():
     lib = native.load()
     import ctypes
