@@ -12,5 +12,7 @@ from .nn.conf import *  # noqa: F401,F403
 from .nn.graph import ComputationGraph
 from .nn.multilayer import MultiLayerNetwork
 from .nn.transferlearning import FineTuneConfiguration, TransferLearning, TransferLearningHelper  # noqa: F401
+from .nn.simple import RankClassificationResult  # noqa: F401
+from .utils.misc_util import FeatureUtil, SerializationUtils  # noqa: F401
 from .eval import (Evaluation, EvaluationBinary, EvaluationCalibration, RegressionEvaluation,  # noqa: F401
                    ROC, ROCBinary, ROCMultiClass)

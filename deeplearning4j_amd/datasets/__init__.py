@@ -6,7 +6,9 @@ from .iterators import (AsyncDataSetIterator, AsyncMultiDataSetIterator, Benchma
                         KFoldIterator, MultiDataSetIteratorAdapter, MultipleEpochsIterator, SamplingDataSetIterator, DataSetIteratorSplitter,
                         FileDataSetIterator, ReconstructionDataSetIterator, InequalityHandling,
                         JointParallelDataSetIterator, CombinedPreProcessor, CombinedMultiDataSetPreProcessor,
-                        BaseParallelDataSetIterator, FileSplitDataSetIterator, FileSplitParallelDataSetIterator)
+                        BaseParallelDataSetIterator, FileSplitDataSetIterator, FileSplitParallelDataSetIterator,
+                        EarlyTerminationMultiDataSetIterator, FloatsDataSetIterator, INDArrayDataSetIterator,
+                        MultiDataSetIteratorSplitter)
 from .normalizers import (NormalizerStandardize, NormalizerMinMaxScaler, ImagePreProcessingScaler,  # noqa: F401
                           VGG16ImagePreProcessor, MultiNormalizerStandardize, MultiNormalizerMinMaxScaler)
 from .fetchers import (CifarDataSetIterator, EmnistDataSetIterator, IrisDataSetIterator, LFWDataSetIterator,  # noqa

@@ -300,6 +300,12 @@ class EarlyTerminationDataSetIterator(DataSetIterator):
         return self.base.batch()
 
 
+class EarlyTerminationMultiDataSetIterator(EarlyTerminationDataSetIterator):
+    """EarlyTerminationDataSetIterator over a MultiDataSetIterator (reference
+    datasets/iterator/EarlyTerminationMultiDataSetIterator.java): at most ``terminationPoint`` MultiDataSets per pass,
+    the same ones again after reset, and a further next() is an error."""
+
+
 class MultiDataSetIteratorAdapter:
     """Presents a DataSetIterator as a MultiDataSetIterator (reference
     datasets/iterator/impl/MultiDataSetIteratorAdapter.java:13-61): each DataSet becomes a single-input,
@@ -415,8 +421,56 @@ class DoublesDataSetIterator(DataSetIterator):
         return self.bs
 
 
-class INDArrayDataSetIterator(DoublesDataSetIterator):
-    pass
+class FloatsDataSetIterator(DoublesDataSetIterator):
+    """(float[] features, float[] labels) pairs in float32 minibatches (reference
+    datasets/iterator/FloatsDataSetIterator.java over AbstractDataSetIterator): the iterable is drained lazily, one
+    minibatch at a time, and re-iterated on reset, so a generator-backed iterable need not fit in memory."""
+
+    def __init__(self, iterable, batchSize):
+        self.source = iterable
+        self.bs = batchSize
+        self._it = iter(iterable)
+        self._peek = None
+
+    def _fill(self):
+        if self._peek is None:
+            self._peek = next(self._it, None)
+        return self._peek
+
+    def hasNext(self):
+        return self._fill() is not None
+
+    def next(self, num=None):
+        n = num or self.bs
+        chunk = []
+        while len(chunk) < n and self._fill() is not None:
+            chunk.append(self._peek)
+            self._peek = None
+        if not chunk:
+            raise StopIteration("FloatsDataSetIterator: no more pairs (reset first)")
+        f = torch.tensor([list(p[0]) for p in chunk], dtype=torch.float32)
+        l = torch.tensor([list(p[1]) for p in chunk], dtype=torch.float32)
+        return self._pp(DataSet(f, l))
+
+    def reset(self):
+        self._it = iter(self.source)
+        self._peek = None
+
+
+class INDArrayDataSetIterator(FloatsDataSetIterator):
+    """(INDArray features, INDArray labels) pairs (reference datasets/iterator/INDArrayDataSetIterator.java): rows
+    are stacked into minibatches as given (any float dtype is kept as float32)."""
+
+    def next(self, num=None):
+        n = num or self.bs
+        chunk = []
+        while len(chunk) < n and self._fill() is not None:
+            chunk.append(self._peek)
+            self._peek = None
+        if not chunk:
+            raise StopIteration("INDArrayDataSetIterator: no more pairs (reset first)")
+        t = lambda a: torch.as_tensor(getattr(a, "tensor", a)).reshape(-1).float()  # noqa: E731
+        return self._pp(DataSet(torch.stack([t(p[0]) for p in chunk]), torch.stack([t(p[1]) for p in chunk])))
 
 
 class DataSetIteratorSplitter:
@@ -446,6 +500,8 @@ class DataSetIteratorSplitter:
         f = ds.getFeatures() if hasattr(ds, "getFeatures") else getattr(ds, "features", None)
         if f is None:
             return
+        if isinstance(f, (list, tuple)):            # MultiDataSet: every feature array, flattened in order
+            f = torch.cat([a.detach().reshape(-1).to("cpu", torch.float32) for a in f])
         f = f.detach().to("cpu", torch.float32)
         if self.first_train is None:
             self.first_train = f.clone()

@@ -63,6 +63,10 @@ class BaseOutputLayerImpl(LayerImpl):
         return x
 
     def _lab2d(self, y):
+        # 3d time-series labels after an RNN->FF preprocessor (e.g. TBPTT windows): [mb, n, T] -> [mb*T, n], the row
+        # order RnnToFeedForwardPreProcessor gives the activations (reference BaseOutputLayer.getLabels2d)
+        if y is not None and y.dim() == 3:
+            return y.permute(0, 2, 1).reshape(-1, y.shape[1])
         return y
 
     def _mask2d(self, m):
