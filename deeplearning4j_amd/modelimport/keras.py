@@ -198,6 +198,20 @@ class KerasLayer:
             _mask_zero_wrap(m)
         return m.obj
 
+    @staticmethod
+    def getInputPreprocessor(layerConfig, inputType, kerasMajorVersion=None):
+        """The preprocessor a shape-only Keras layer (Reshape) puts in front of its consumer, for the given input
+        type (reference KerasReshape.getInputPreprocessor(InputType...)): None for layers that carry a DL4J layer."""
+        v = kerasMajorVersion or int(layerConfig.get("keras_version", 2))
+        m = _map_layer(layerConfig, _Ctx(v, False))
+        if m.kind != "reshape":
+            return None
+        cl = _channels_last(m.cfg)
+        pp = KerasReshapePreprocessor(targetShape=list(m.cfg["target_shape"]), channelsLast=cl)
+        if inputType is not None:
+            pp.getOutputType(inputType)
+        return pp
+
 
 def space_to_depth_mapper(block_size=2):
     """Mapper for the reference's KerasSpaceToDepth custom Lambda (space_to_depth with block 2)."""
@@ -319,16 +333,17 @@ _INIT = {"glorot_normal": "XAVIER", "glorot_uniform": "XAVIER_UNIFORM", "lecun_n
          "ones": "ONES", "zero": "ZERO", "zeros": "ZERO", "identity": "IDENTITY"}
 
 
-def _init(spec):
+def _init(spec, layer_cfg=None):
     """(WeightInit, Distribution or None) of a Keras 1 initializer name or a Keras 2 {class_name, config}; None when
-    the layer config has none."""
+    the layer config has none. Keras 1 keeps the initializer parameters (mean / stddev / scale / minval / maxval /
+    value / gain) in the layer config itself (KER:utils/KerasInitilizationUtils.java getWeightInitFromConfig)."""
     from ..nn.conf import weights as Wt
     if spec is None:
         return None
     if isinstance(spec, dict):
         name, icfg = spec.get("class_name"), spec.get("config") or {}
     else:
-        name, icfg = spec, {}
+        name, icfg = spec, dict(layer_cfg or {})
     key = {"RandomUniform": "random_uniform", "RandomNormal": "random_normal", "Ones": "ones", "Zeros": "zeros",
            "Constant": "constant", "Orthogonal": "orthogonal", "TruncatedNormal": "truncated_normal",
            "Identity": "identity", "GlorotNormal": "glorot_normal", "GlorotUniform": "glorot_uniform",
@@ -391,7 +406,7 @@ def _apply_common(k, ctx):
     fields = target._all_fields()
     emb = k.keras_class == "Embedding"
     init = _init(cfg.get("embeddings_initializer") if emb and "embeddings_initializer" in cfg else
-                 cfg.get("kernel_initializer", cfg.get("init", cfg.get("depthwise_initializer"))))
+                 cfg.get("kernel_initializer", cfg.get("init", cfg.get("depthwise_initializer"))), cfg)
     if init is not None and "weightInit" in fields:
         target.weightInit, dist = init
         if dist is not None:
