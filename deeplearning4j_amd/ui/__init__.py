@@ -6,3 +6,5 @@ from .storage import (CollectionStatsStorageRouter, FileStatsStorage, InMemorySt
 from .stats import (StatsInitializationConfiguration, StatsListener, StatsType, StatsUpdateConfiguration,  # noqa
                     SummaryType, summarize)
 from .server import UIServer  # noqa: F401
+from .histogram import HistogramBin  # noqa: F401
+from .storage import SbeStorageMetaData, StorageMetaData  # noqa: F401

@@ -60,9 +60,44 @@ class Persistable:
 
 
 class StorageMetaData(Persistable):
-    def __init__(self, sessionID, typeID, workerID="", initTypeClass=None, updateTypeClass=None, timeStamp=None):
-        super().__init__(sessionID, typeID, workerID, timeStamp,
-                         {"initTypeClass": initTypeClass, "updateTypeClass": updateTypeClass}, "meta")
+    """Session metadata: the record classes used for initialisation / updates plus optional extra metadata (a JSON
+    value here; the reference's SbeStorageMetaData carries a Java-serialised object)."""
+
+    def __init__(self, sessionID=None, typeID=None, workerID="", initTypeClass=None, updateTypeClass=None,
+                 timeStamp=None, extraMeta=None):
+        super().__init__(sessionID, typeID, workerID, 0 if timeStamp is None and sessionID is None else timeStamp,
+                         {"initTypeClass": initTypeClass, "updateTypeClass": updateTypeClass,
+                          "extraMeta": extraMeta}, "meta")
+
+    def getInitTypeClass(self):
+        return self.data.get("initTypeClass")
+
+    def getUpdateTypeClass(self):
+        return self.data.get("updateTypeClass")
+
+    def getExtraMetaData(self):
+        return self.data.get("extraMeta")
+
+    def decode(self, b):
+        """In place, as the reference's ``m2.decode(bytes)``; also returns self."""
+        d = json.loads(b.decode("utf-8") if isinstance(b, (bytes, bytearray)) else b)
+        self.sessionID, self.typeID, self.workerID = d["sessionID"], d["typeID"], d["workerID"]
+        self.timeStamp, self.data, self.kind = d["timeStamp"], dict(d["data"]), d.get("kind", "meta")
+        return self
+
+    def __eq__(self, other):
+        return isinstance(other, StorageMetaData) and self.to_dict() == other.to_dict()
+
+    def __hash__(self):
+        return hash((self.sessionID, self.typeID, self.workerID, self.timeStamp))
+
+
+class SbeStorageMetaData(StorageMetaData):
+    """The reference's constructor order: (timeStamp, sessionID, typeID, workerID, initType, updateType[, extra])."""
+
+    def __init__(self, timeStamp=0, sessionID=None, typeID=None, workerID=None, initTypeClass=None,
+                 updateTypeClass=None, extraMeta=None):
+        super().__init__(sessionID, typeID, workerID, initTypeClass, updateTypeClass, timeStamp, extraMeta)
 
 
 class StatsStorageEvent:
