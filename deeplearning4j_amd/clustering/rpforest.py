@@ -12,6 +12,27 @@ from .distances import SIMILARITIES, pairwise
 
 class RPUtils:
     @staticmethod
+    def computeDistance(function, x, y, result=None):
+        """One distance (RPUtils.computeDistance): euclidean / manhattan / cosinedistance / cosinesimilarity / dot /
+        jaccard / hamming between two vectors."""
+        xv = torch.as_tensor(getattr(x, "tensor", x), dtype=torch.float64).reshape(1, -1)
+        yv = torch.as_tensor(getattr(y, "tensor", y), dtype=torch.float64).reshape(1, -1)
+        return float(pairwise(xv, yv, function)[0, 0])
+
+    @staticmethod
+    def computeDistanceMulti(function, x, y, result=None):
+        """Distances from vector x to every row of y (RPUtils.computeDistanceMulti); written into ``result`` when
+        given, and returned."""
+        xv = torch.as_tensor(getattr(x, "tensor", x), dtype=torch.float64).reshape(1, -1)
+        ym = torch.as_tensor(getattr(y, "tensor", y), dtype=torch.float64).reshape(-1, xv.shape[1])
+        d = pairwise(xv, ym, function)[0]
+        if result is not None:
+            r = getattr(result, "tensor", result)
+            r.reshape(-1).copy_(d.to(r.dtype))
+            return result
+        return d
+
+    @staticmethod
     def getAllCandidates(x, trees):
         cand = set()
         for t in trees:

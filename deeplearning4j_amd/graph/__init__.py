@@ -41,6 +41,12 @@ class Vertex:
     def __repr__(self):
         return f"Vertex({self.idx}, {self.value!r})"
 
+    def __eq__(self, o):
+        return isinstance(o, Vertex) and (self.idx, self.value) == (o.idx, o.value)
+
+    def __hash__(self):
+        return hash(self.idx)
+
 
 class Edge:
     def __init__(self, frm, to, value=None, directed=False):
@@ -61,6 +67,13 @@ class Edge:
     def __repr__(self):
         return f"Edge({self.frm}{'->' if self.directed else '--'}{self.to}, {self.value!r})"
 
+    def __eq__(self, o):
+        return isinstance(o, Edge) and (self.frm, self.to, self.value, self.directed) == \
+            (o.frm, o.to, o.value, o.directed)
+
+    def __hash__(self):
+        return hash((self.frm, self.to))
+
 
 class NoEdgeHandling:
     SELF_LOOP_ON_DISCONNECTED = "SELF_LOOP_ON_DISCONNECTED"
@@ -77,6 +90,11 @@ class Graph:
         self.allowMultiple = allowMultipleEdges
         self.edges = [[] for _ in self.vertices]
         self._csr = None
+
+    def __eq__(self, o):
+        return isinstance(o, Graph) and self.vertices == o.vertices and self.edges == o.edges
+
+    __hash__ = None
 
     def numVertices(self):
         return len(self.vertices)
@@ -148,16 +166,28 @@ class GraphLoader:
     @staticmethod
     def loadWeightedEdgeListFile(path, numVertices, delim=",", directed=False, allowMultipleEdges=False,
                                  ignoreLinesStartingWith=("//",)):
+        if isinstance(allowMultipleEdges, (list, tuple, str)):   # reference overload (path, n, delim, directed, ignore)
+            allowMultipleEdges, ignoreLinesStartingWith = False, allowMultipleEdges
         if isinstance(ignoreLinesStartingWith, str):
             ignoreLinesStartingWith = (ignoreLinesStartingWith,)
-        g = Graph(numVertices, allowMultipleEdges)
+        g = Graph([StringVertexFactory().create(i) for i in range(numVertices)], allowMultipleEdges)
         for ln in GraphLoader._lines(path, ignoreLinesStartingWith):
             a, b, w = ln.split(delim)[:3]
             g.addEdge(int(a), int(b), float(w), directed)
         return g
 
     @staticmethod
-    def loadGraph(vertexFile, edgeFile, delim=",", directed=False):
+    def loadGraph(vertexFile, edgeFile, delim=",", directed=False, allowMultipleEdges=False):
+        if isinstance(edgeFile, EdgeLineProcessor):
+            # reference overload loadGraph(path, EdgeLineProcessor, VertexFactory, numVertices, allowMultipleEdges)
+            proc, factory, n = edgeFile, delim, directed
+            g = Graph([factory.create(i) for i in range(int(n))], bool(allowMultipleEdges))
+            with open(vertexFile, encoding="utf-8") as fh:
+                for ln in fh:
+                    e = proc.processLine(ln.rstrip("\n"))
+                    if e is not None:
+                        g.addEdge(e.getFrom(), e.getTo(), e.getValue(), e.isDirected())
+            return g
         verts = []
         for ln in GraphLoader._lines(vertexFile):
             i, v = ln.split(delim, 1)
@@ -168,6 +198,55 @@ class GraphLoader:
             a, b = ln.split(delim)[:2]
             g.addEdge(int(a), int(b), None, directed)
         return g
+
+
+class EdgeLineProcessor:
+    """Turns one line of an edge-list file into an Edge, or None for comment / blank lines."""
+
+    def processLine(self, line):
+        raise NotImplementedError
+
+
+class WeightedEdgeLineProcessor(EdgeLineProcessor):
+    """"from<delim>to<delim>weight" lines (reference graph/data/impl/WeightedEdgeLineProcessor.java)."""
+
+    def __init__(self, delim=",", directed=False, ignoreLinesStartingWith=("//",)):
+        self.delim, self.directed = delim, bool(directed)
+        self.ignore = (ignoreLinesStartingWith,) if isinstance(ignoreLinesStartingWith, str) else \
+            tuple(ignoreLinesStartingWith or ())
+
+    def processLine(self, line):
+        ln = line.strip()
+        if not ln or any(ln.startswith(p) for p in self.ignore):
+            return None
+        a, b, w = ln.split(self.delim)[:3]
+        return Edge(int(a), int(b), float(w), self.directed)
+
+
+class DelimitedEdgeLineProcessor(EdgeLineProcessor):
+    """Unweighted "from<delim>to" lines (reference DelimitedEdgeLineProcessor.java)."""
+
+    def __init__(self, delim=",", directed=False, ignoreLinesStartingWith=("//",)):
+        self.delim, self.directed = delim, bool(directed)
+        self.ignore = (ignoreLinesStartingWith,) if isinstance(ignoreLinesStartingWith, str) else \
+            tuple(ignoreLinesStartingWith or ())
+
+    def processLine(self, line):
+        ln = line.strip()
+        if not ln or any(ln.startswith(p) for p in self.ignore):
+            return None
+        a, b = ln.split(self.delim)[:2]
+        return Edge(int(a), int(b), None, self.directed)
+
+
+class StringVertexFactory:
+    """Vertex i carries the string form of i (reference graph/vertexfactory/StringVertexFactory.java)."""
+
+    def __init__(self, fmt=None):
+        self.fmt = fmt
+
+    def create(self, idx):
+        return Vertex(idx, (self.fmt % idx) if self.fmt else str(idx))
 
 
 class VertexSequence:

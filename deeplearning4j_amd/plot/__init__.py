@@ -66,6 +66,7 @@ class _TsneBase:
         self.realMin = 1e-12
         self.initialMomentum = 0.5
         self.finalMomentum = 0.8
+        self.momentum = 0.5             # current momentum (the schedule moves it initial -> final at the switch)
         self.minGain = 1e-2
         self.switchMomentumIteration = 100
         self.normalize = True
@@ -101,7 +102,7 @@ class _TsneBase:
         def setRealMin(self, v): return self._s("realMin", float(v))  # noqa: E704
         def setInitialMomentum(self, v): return self._s("initialMomentum", float(v))  # noqa: E704
         def setFinalMomentum(self, v): return self._s("finalMomentum", float(v))  # noqa: E704
-        def setMomentum(self, v): return self._s("initialMomentum", float(v))  # noqa: E704
+        def setMomentum(self, v): return self._s("momentum", float(v))  # noqa: E704
         def setSwitchMomentumIteration(self, v): return self._s("switchMomentumIteration", int(v))  # noqa: E704
         def normalize(self, v): return self._s("normalize", bool(v))  # noqa: E704
         def usePca(self, v): return self._s("usePca", bool(v))  # noqa: E704
@@ -122,6 +123,20 @@ class _TsneBase:
 
         def build(self):
             return self.TARGET(**self.kw)
+
+    def getTheta(self):
+        return self.theta
+
+    def isInvert(self):
+        return self.invert
+
+    def getSimiarlityFunction(self):        # the reference's spelling
+        return self.similarityFunction
+
+    getSimilarityFunction = getSimiarlityFunction
+
+    def getPerplexity(self):
+        return self.perplexity
 
     def setListeners(self, *ls):
         self.listeners = list(ls[0] if len(ls) == 1 and isinstance(ls[0], (list, tuple)) else ls)
