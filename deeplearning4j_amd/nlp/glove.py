@@ -35,6 +35,23 @@ COOC_DTYPE = np.dtype([("i", "<i4"), ("j", "<i4"), ("x", "<f4")])
 _BYTES_PER_ENTRY = 64          # hash-map footprint per counted pair (key, value, bucket, node) for the memory cap
 
 
+class RoundCount:
+    """Cyclic counter 0..limit (reference models/glove/count/RoundCount.java): the shadow-copy thread of the
+    co-occurrence counter alternates spill files by round; previous() is the round before the current one."""
+
+    def __init__(self, limit):
+        self.limit, self.current = int(limit), 0
+
+    def previous(self):
+        return self.limit if self.current == 0 else self.current - 1
+
+    def get(self):
+        return self.current
+
+    def tick(self):
+        self.current = 0 if self.current == self.limit else self.current + 1
+
+
 class CoOccurrenceCounter:
     """Co-occurrence counting with bounded memory (reference NLP:models/glove/AbstractCoOccurrences.java:55-104,
     185-266, 387-520: its maxMemory-triggered shadow copies to temp files). Sequences are fed in chunks

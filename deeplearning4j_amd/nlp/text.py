@@ -309,6 +309,28 @@ class AggregatingSentenceIterator(SentenceIterator):
         self.hasNext()
         return self._pp(self.its[self._k].nextSentence())
 
+    class Builder:
+        """Reference AggregatingSentenceIterator.Builder: addSentenceIterator(...) / addSentenceIterators(list) /
+        addSentencePreProcessor(p).build()."""
+
+        def __init__(self):
+            self._its, self._pp_ = [], None
+
+        def addSentenceIterator(self, it):
+            self._its.append(it)
+            return self
+
+        def addSentenceIterators(self, its):
+            self._its.extend(its)
+            return self
+
+        def addSentencePreProcessor(self, p):
+            self._pp_ = p
+            return self
+
+        def build(self):
+            return AggregatingSentenceIterator(self._its, self._pp_)
+
 
 class MutipleEpochsSentenceIterator(SentenceIterator):
     def __init__(self, base, epochs):

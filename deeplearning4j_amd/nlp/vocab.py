@@ -95,7 +95,10 @@ class AbstractCache:
         self.totalWordCount += by
 
     def addWordToIndex(self, index, label):
-        e = self._by_label[label]
+        e = self._by_label.get(label)
+        if e is None:               # unseen word: added with frequency 1 (reference InMemoryLookupCache)
+            e = VocabWord(label, 1.0)
+            self._by_label[label] = e
         e.index = index
         while len(self._by_index) <= index:
             self._by_index.append(None)

@@ -1,0 +1,90 @@
+"""Small NLP ports, after the reference's EndingPreProcessorTest, RoundCountTest, MutipleEpochsSentenceIteratorTest
+and AggregatingSentenceIteratorTest (deeplearning4j-nlp-parent/deeplearning4j-nlp/src/test/java/org/deeplearning4j/
+text/tokenization/tokenizer/tokenprepreprocessor/EndingPreProcessorTest.java, models/glove/count/RoundCountTest.java,
+text/sentenceiterator/MutipleEpochsSentenceIteratorTest.java, AggregatingSentenceIteratorTest.java). The reference's
+big/raw_sentences.txt (97,162 lines) is not in this tree: a generated file of 971 lines stands in and the expected
+counts scale with it. CPU."""
+import deeplearning4j_amd.nlp as N
+from deeplearning4j_amd.nlp.glove import RoundCount
+
+LINES = 971
+
+
+def _file(tmp_path):
+    f = tmp_path / "raw_sentences.txt"
+    f.write_text("".join(f"sentence number {i} of the stand-in corpus\n" for i in range(LINES)))
+    return str(f)
+
+
+def test_ending_preprocessor():
+    assert N.EndingPreProcessor().preProcess("ending") == "end"
+
+
+def test_round_count_get():
+    c = RoundCount(1)
+    assert c.get() == 0
+    c.tick()
+    assert c.get() == 1
+    c.tick()
+    assert c.get() == 0
+    c = RoundCount(3)
+    for expect in (0, 1, 2, 3, 0):
+        assert c.get() == expect
+        c.tick()
+
+
+def test_round_count_previous():
+    c = RoundCount(3)
+    for cur, prev in ((0, 3), (1, 0), (2, 1), (3, 2), (0, 3)):
+        assert c.get() == cur and c.previous() == prev
+        c.tick()
+
+
+def test_multiple_epochs_sentence_iterator(tmp_path):
+    it = N.MutipleEpochsSentenceIterator(N.BasicLineIterator(_file(tmp_path)), 100)
+    cnt = 0
+    while it.hasNext():
+        it.nextSentence()
+        cnt += 1
+    assert cnt == LINES * 100
+
+
+def test_aggregating_sentence_iterator(tmp_path):
+    f = _file(tmp_path)
+    aggr = N.AggregatingSentenceIterator.Builder().addSentenceIterator(N.BasicLineIterator(f)) \
+        .addSentenceIterator(N.BasicLineIterator(f)).build()
+    cnt = 0
+    while aggr.hasNext():
+        aggr.nextSentence()
+        cnt += 1
+    assert cnt == LINES * 2
+    aggr.reset()
+    while aggr.hasNext():
+        aggr.nextSentence()
+        cnt += 1
+    assert cnt == LINES * 4
+
+
+# ---- NGramTokenizerTest (.../text/tokenization/tokenizer/NGramTokenizerTest.java)
+def test_ngram_tokenizer():
+    text = "Mary had a little lamb."
+    factory = N.NGramTokenizerFactory(N.DefaultTokenizerFactory(), 1, 2)
+    t1, t2 = factory.create(text), factory.create(text)
+    while t1.hasMoreTokens():
+        assert t1.nextToken() == t2.nextToken()
+    assert factory.create(text).countTokens() == 9
+    tokens = factory.create(text).getTokens()
+    for w in ("Mary", "had", "a", "little", "lamb.", "Mary had", "had a", "a little", "little lamb."):
+        assert w in tokens
+    tokens = N.NGramTokenizerFactory(N.DefaultTokenizerFactory(), 2, 2).create(text).getTokens()
+    assert sorted(tokens) == sorted(["Mary had", "had a", "a little", "little lamb."])
+
+
+# ---- InMemoryVocabStoreTests (.../wordstore/InMemoryVocabStoreTests.java)
+def test_vocab_store_put():
+    cache = N.InMemoryLookupCache()
+    assert not cache.containsWord("hello")
+    cache.addWordToIndex(0, "hello")
+    assert cache.containsWord("hello")
+    assert cache.numWords() == 1
+    assert cache.wordAtIndex(0) == "hello"
