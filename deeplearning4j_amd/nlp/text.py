@@ -424,7 +424,8 @@ class LabelsSource:
 
     def nextLabel(self):
         if self.template is not None:
-            lab = self.template % self.counter
+            # "%d" templates are formatted; any other string gets the counter appended (reference LabelsSource)
+            lab = self.template % self.counter if "%d" in self.template else f"{self.template}{self.counter}"
             self.counter += 1
             self.storeLabel(lab)
             return lab

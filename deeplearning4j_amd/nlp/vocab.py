@@ -12,6 +12,8 @@ MAX_CODE_LENGTH = 40
 
 class SequenceElement:
     def __init__(self, label, frequency=1.0, special=False):
+        if isinstance(frequency, str) and not isinstance(label, str):   # reference order VocabWord(frequency, word)
+            label, frequency = frequency, label
         self.label = label
         self.elementFrequency = float(frequency)
         self.sequencesCount = 0
@@ -63,13 +65,63 @@ class SequenceElement:
     def __repr__(self):
         return f"{type(self).__name__}({self.label!r}, freq={self.elementFrequency}, idx={self.index})"
 
+    def __eq__(self, other):
+        # same element = same class and label (reference SequenceElement.equals)
+        return type(other) is type(self) and other.label == self.label
+
+    def __hash__(self):
+        return hash(self.label)
+
+    def toJSON(self):
+        import json
+        return json.dumps({"@class": type(self).__name__, "label": self.label,
+                           "elementFrequency": self.elementFrequency, "sequencesCount": self.sequencesCount,
+                           "index": self.index, "codes": list(self.codes), "points": list(self.points),
+                           "special": bool(self.special)})
+
+    @classmethod
+    def fromJSON(cls, s):
+        import json
+        d = json.loads(s)
+        e = cls(d["label"], d.get("elementFrequency", 1.0), d.get("special", False))
+        e.sequencesCount, e.index = d.get("sequencesCount", 0), d.get("index", -1)
+        e.codes, e.points = list(d.get("codes", [])), list(d.get("points", []))
+        return e
+
 
 class VocabWord(SequenceElement):
     pass
 
 
+class AbstractElementFactory:
+    """JSON (de)serialiser for one element class (reference models/sequencevectors/serialization/
+    AbstractElementFactory.java), used by the vocabulary writers."""
+
+    def __init__(self, cls):
+        self.cls = cls
+
+    def serialize(self, element):
+        return element.toJSON()
+
+    def deserialize(self, s):
+        return self.cls.fromJSON(s)
+
+
 class AbstractCache:
     """In-memory VocabCache: label <-> element <-> index, counts, document frequencies."""
+
+    class Builder:
+        def __init__(self):
+            pass
+
+        def hugeModelExpected(self, b):
+            return self
+
+        def minElementFrequency(self, f):
+            return self
+
+        def build(self):
+            return AbstractCache()
 
     def __init__(self):
         self._by_label = {}
@@ -79,6 +131,8 @@ class AbstractCache:
 
     # --- building
     def addToken(self, element):
+        if not element.special:
+            self.totalWordCount += element.elementFrequency
         if element.label in self._by_label:
             e = self._by_label[element.label]
             e.increaseElementFrequency(element.elementFrequency)
@@ -110,6 +164,8 @@ class AbstractCache:
 
     def removeElement(self, label):
         e = self._by_label.pop(label, None)
+        if e is not None and not e.special:
+            self.totalWordCount -= e.elementFrequency
         if e is not None and 0 <= e.index < len(self._by_index) and self._by_index[e.index] is e:
             self._by_index[e.index] = None
 
@@ -309,6 +365,11 @@ class Huffman:
         for i, e in enumerate(self.elements):
             e.codes = self.codes[i]
             e.points = self.points[i]
+        if not any(x is not None for x in cache._by_index):
+            # an unindexed cache takes the Huffman order: most frequent element first (reference Huffman.applyIndexes)
+            order = sorted(range(len(self.elements)), key=lambda i: -self.elements[i].elementFrequency)
+            for rank, i in enumerate(order):
+                cache.addWordToIndex(rank, self.elements[i].label)
         return cache
 
 
