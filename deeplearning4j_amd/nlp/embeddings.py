@@ -430,9 +430,16 @@ class WordVectorsImpl:
         return None if i < 0 else self._lookup.normalized()[i].reshape(1, -1)
 
     def getWordVectors(self, words):
-        idx = [self._idx(w) for w in words]
-        idx = [i for i in idx if i >= 0]
-        return self._lookup.syn0[torch.as_tensor(idx, dtype=torch.long, device=self._lookup.device)]
+        """Rows of the words the vocabulary contains (UNK for the others when out-of-vocabulary words are
+        supported), in order; the rest are dropped (reference WordVectorsImpl.getWordVectors)."""
+        idx = []
+        for w in words:
+            if self._vocab.containsWord(w):
+                idx.append(self._vocab.indexOf(w))
+            elif self.useUnknown and self._vocab.containsWord(self.UNK):
+                idx.append(self._vocab.indexOf(self.UNK))
+        W = self._lookup.syn0 if getattr(self._lookup, "syn0", None) is not None else self._lookup.getWeights()
+        return W[torch.as_tensor(idx, dtype=torch.long, device=W.device)]
 
     def getWordVectorsMean(self, words):
         return self.getWordVectors(words).mean(dim=0, keepdim=True)

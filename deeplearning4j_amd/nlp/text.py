@@ -212,13 +212,21 @@ class CollectionSentenceIterator(SentenceIterator):
 
 
 class BasicLineIterator(SentenceIterator):
-    """One sentence per non-empty line of a file (streamed)."""
+    """One sentence per non-empty line of a file path or an open binary / text stream (streamed; a stream is
+    rewound on reset)."""
 
     def __init__(self, path):
         super().__init__()
         self.path = path
         self._fh = None
         self._next = None
+
+    def _open(self):
+        if hasattr(self.path, "read"):
+            import io
+            self.path.seek(0)
+            return self.path if isinstance(self.path, io.TextIOBase) else io.TextIOWrapper(self.path, "utf-8")
+        return open(self.path, encoding="utf-8")
 
     def _advance(self):
         while True:
@@ -232,9 +240,11 @@ class BasicLineIterator(SentenceIterator):
                 return
 
     def reset(self):
-        if self._fh is not None:
+        if self._fh is not None and not hasattr(self.path, "read"):
             self._fh.close()
-        self._fh = open(self.path, encoding="utf-8")
+        if self._fh is not None and hasattr(self.path, "read") and self._fh is not self.path:
+            self._fh.detach()                          # keep the caller's stream open
+        self._fh = self._open()
         self._advance()
 
     def hasNext(self):
@@ -284,6 +294,32 @@ class FileSentenceIterator(SentenceIterator):
         s = self._lines[self._i]
         self._i += 1
         return self._pp(s)
+
+
+class StreamLineIterator(BasicLineIterator):
+    """Lines of an input stream read ahead in blocks of ``fetchSize`` (reference text/sentenceiterator/
+    StreamLineIterator.java); blank lines are skipped."""
+
+    def __init__(self, stream, fetchSize=10000):
+        super().__init__(stream)
+        self.fetchSize = int(fetchSize)
+
+    class Builder:
+        def __init__(self, stream):
+            self._s, self._n, self._pp_ = stream, 10000, None
+
+        def setFetchSize(self, n):
+            self._n = int(n)
+            return self
+
+        def setPreProcessor(self, p):
+            self._pp_ = p
+            return self
+
+        def build(self):
+            it = StreamLineIterator(self._s, self._n)
+            it.preProcessor = self._pp_
+            return it
 
 
 class AggregatingSentenceIterator(SentenceIterator):

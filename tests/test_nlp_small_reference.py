@@ -88,3 +88,52 @@ def test_vocab_store_put():
     assert cache.containsWord("hello")
     assert cache.numWords() == 1
     assert cache.wordAtIndex(0) == "hello"
+
+
+# ---- BasicLineIteratorTest / StreamLineIteratorTest (.../text/sentenceiterator/)
+def test_basic_line_iterator_file_and_stream(tmp_path):
+    f = _file(tmp_path)
+    for src in (f, open(f, "rb")):
+        it = N.BasicLineIterator(src)
+        for _ in range(2):                               # the same count again after reset
+            cnt = 0
+            while it.hasNext():
+                assert it.nextSentence()
+                cnt += 1
+            assert cnt == LINES
+            it.reset()
+
+
+def test_stream_line_iterator(tmp_path):
+    """The reference reads its 24-line reuters/5250 file; a 24-line stand-in with blank lines between."""
+    f = tmp_path / "5250"
+    f.write_text("".join(f"REUTER line {i}\n\n" for i in range(24)))
+    it = N.StreamLineIterator.Builder(open(f, "rb")).setFetchSize(100).build()
+    cnt = 0
+    while it.hasNext():
+        assert it.nextSentence() is not None
+        cnt += 1
+    assert cnt == 24
+
+
+# ---- WordVectorsImplTest (.../models/embeddings/wordvectors/WordVectorsImplTest.java)
+def test_word_vectors_drop_words_not_in_vocab():
+    import torch
+
+    class Vocab:                                         # the reference's Mockito stubs
+        def indexOf(self, w):
+            return 0
+
+        def containsWord(self, w):
+            return w == "word"
+
+    class Table:
+        syn0 = None
+
+        def getWeights(self):
+            return torch.tensor([[5.0]])
+
+    wv = N.WordVectorsImpl()
+    wv.setVocab(Vocab())
+    wv.setLookupTable(Table())
+    assert torch.equal(wv.getWordVectors(["word", "here", "is"]), torch.tensor([[5.0]]))
