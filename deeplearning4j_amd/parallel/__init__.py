@@ -10,3 +10,5 @@ from .wrapper import ParallelWrapper, TrainingMode
 from .cluster import (ParameterAveragingTrainingMaster, SharedTrainingMaster, SparkComputationGraph,  # noqa: F401
                       SparkDl4jMultiLayer, StatsUtils, TrainingMaster, TrainingStats)
 from .basic import BasicGradientsAccumulator, FancyBlockingQueue, LocalHandler  # noqa: E402,F401
+
+from .concurrency import AsyncIterator, MultiBoolean  # noqa: F401,E402
