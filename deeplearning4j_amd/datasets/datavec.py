@@ -19,6 +19,15 @@ from .dataset import DataSet, DataSetIterator, MultiDataSet
 
 
 # ------------------------------------------------------------------------------------------------ input splits
+
+def _check_classes(classes, n):
+    """A class index outside [0, numPossibleLabels) is a data error, reported as the reference does (its message
+    says the value could not be converted "to one-hot")."""
+    for c in classes:
+        if not 0 <= c < n:
+            raise ValueError(f"Invalid classification data: can't convert class index {c} to one-hot "
+                             f"representation with {n} possible labels (valid indices 0..{n - 1})")
+
 class FileSplit:
     def __init__(self, path, allowFormat=None, recursive=True):
         if os.path.isdir(path):
@@ -286,8 +295,10 @@ class RecordReaderDataSetIterator(DataSetIterator):
         elif self.reg:
             y = torch.tensor([[float(v) for v in l] for l in labs], dtype=torch.float32)
         else:
+            cls = [int(float(l[0])) for l in labs]
+            _check_classes(cls, self.n)
             y = torch.zeros(len(labs), self.n)
-            y[torch.arange(len(labs)), torch.tensor([int(float(l[0])) for l in labs])] = 1.0
+            y[torch.arange(len(labs)), torch.tensor(cls)] = 1.0
         return self._pp(DataSet(x, y))
 
     def reset(self):
@@ -345,6 +356,7 @@ class SequenceRecordReaderDataSetIterator(DataSetIterator):
         if self.reg:
             return s
         oh = np.zeros((s.shape[0], self.n), np.float32)
+        _check_classes(s[:, 0].astype(np.int64).tolist(), self.n)
         oh[np.arange(s.shape[0]), s[:, 0].astype(np.int64)] = 1.0
         return oh
 
