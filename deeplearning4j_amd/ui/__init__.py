@@ -8,3 +8,4 @@ from .stats import (StatsInitializationConfiguration, StatsListener, StatsType, 
 from .server import UIServer  # noqa: F401
 from .histogram import HistogramBin  # noqa: F401
 from .storage import SbeStorageMetaData, StorageMetaData  # noqa: F401
+from .connection import UiConnectionInfo  # noqa: F401,E402
