@@ -8,3 +8,4 @@ from .word2vec import (CBOW, DBOW, DM, ParagraphVectors, ScoreListener, Sequence
 from .tokenization_ext import (BertWordPieceTokenizerFactory, ChineseTokenizerFactory,  # noqa: F401
                                JapaneseTokenizerFactory, KoreanTokenizerFactory, PorterStemmer, StemmingPreprocessor)
 from .distributed import DistributedWord2Vec, SparkWord2Vec  # noqa: F401
+from .text import ContextLabelRetriever  # noqa: F401,E402

@@ -620,3 +620,36 @@ class FilenamesLabelAwareIterator(FileLabelAwareIterator):
                     self.files.append((os.path.join(dp, f), f))
         self.labelsSource = LabelsSource([l for _, l in self.files])
         self._i = 0
+
+
+class ContextLabelRetriever:
+    """Inline span labels (reference deeplearning4j-nlp-uima/.../util/ContextLabelRetriever.java): in
+    "<POS> great film </POS> overall" the tokens between <LABEL> and </LABEL> carry LABEL and every other run of
+    tokens carries "none"; returns (the sentence without the tags, {(firstToken, endToken): label})."""
+
+    @staticmethod
+    def stringWithLabels(sentence, tokenizerFactory):
+        import re
+        tokens = tokenizerFactory.create(sentence).getTokens()
+        words, spans = [], {}
+        label, start = None, 0
+
+        def close(lab):
+            if len(words) > start:
+                spans[(start, len(words))] = lab
+        for t in tokens:
+            m = re.fullmatch(r"<(/?)([^<>/\s]+)>", t)
+            if m and not m.group(1):                  # opening tag: close the running "none" span
+                close("none")
+                label, start = m.group(2), len(words)
+            elif m and m.group(1):                    # closing tag
+                if label != m.group(2):
+                    raise ValueError(f"closing tag </{m.group(2)}> does not match <{label}>")
+                close(label)
+                label, start = None, len(words)
+            else:
+                words.append(t)
+        if label is not None:
+            raise ValueError(f"unclosed label <{label}>")
+        close("none")
+        return " ".join(words), spans

@@ -137,3 +137,13 @@ def test_word_vectors_drop_words_not_in_vocab():
     wv.setVocab(Vocab())
     wv.setLookupTable(Table())
     assert torch.equal(wv.getWordVectors(["word", "here", "is"]), torch.tensor([[5.0]]))
+
+
+# ---- ContextLabelTest (deeplearning4j-nlp-uima/src/test/java/org/deeplearning4j/util/ContextLabelTest.java); the
+# reference tokenizes with its UIMA factory, which is not available here: the whitespace tokenizer stands in
+def test_context_label_basic():
+    text, spans = N.ContextLabelRetriever.stringWithLabels("<NEGATIVE> This sucks really bad </NEGATIVE> .",
+                                                         N.DefaultTokenizerFactory())
+    assert len(spans) == 2
+    assert "NEGATIVE" in spans.values() and "none" in spans.values()
+    assert text == "This sucks really bad ."
